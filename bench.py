@@ -1,0 +1,172 @@
+"""Headline benchmark: agent-env-steps/s (+ learner updates/s) at 4096 envs x 8 agents per GPU.
+
+Workload (BASELINE.json configs[1]): QMIX 8-agent gridworld, 4096 envs per GPU, agent
+Q-net GRU-64 (F1 = G = H = 64), chunk 10, device PER. One "step" = one lockstep
+rollout step of every env on every rank: behavior Q forward + eps-greedy, env step,
+target Q forward on the next obs, TD error + transition store, and every 10th step
+the chunk insert into the prioritized replay. Synthetic data = the build's own
+gridworld (the reference's ma_gym env is absent); random-init weights.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
+torch.distributed.run (one process per GPU, RCCL). Envs shard across ranks with no
+data-path collective (weak scaling); rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "mini-marl_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (vector = f32 MFMA), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def qnet_flops_per_agent_step(D, F1, G, H, A):
+    return 2 * (D * F1 + F1 * G + 3 * G * H + 3 * H * H + H * A)
+
+
+def cpu_baseline(E, N, F1, G, H, budget_s=12.0):
+    """Oracle (CPU port) of the same rollout step on the host cores: numpy env + torch-CPU nets."""
+    import numpy as np
+    from oracle import nets
+    from oracle.env import EnvSpec, VecEnvOracle
+    torch.manual_seed(0)
+    spec = EnvSpec(N, 100)
+    D = spec.obs_dim
+    P = {"W1": torch.randn(N, F1, D) * 0.1, "b1": torch.zeros(N, F1), "W2": torch.randn(N, G, F1) * 0.1,
+         "b2": torch.zeros(N, G), "Wih": torch.randn(N, 3 * H, G) * 0.1, "Whh": torch.randn(N, 3 * H, H) * 0.1,
+         "bih": torch.zeros(N, 3 * H), "bhh": torch.zeros(N, 3 * H), "Wq": torch.randn(N, 5, H) * 0.1,
+         "bq": torch.zeros(N, 5)}
+    env = VecEnvOracle(spec, E)
+    obs = torch.tensor(env.observe())
+    h = torch.zeros(E, N, H)
+    ht = torch.zeros(E, N, H)
+    rng = np.random.default_rng(0)
+    steps = 0
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        while True:
+            q, h = nets.agent_forward(P, obs, h)
+            act = q.argmax(2).numpy()
+            rnd = rng.random(E) < 0.1
+            act[rnd] = rng.integers(0, 5, (int(rnd.sum()), N))
+            nxt, rew, done = env.step(act)
+            tq, ht = nets.agent_forward(P, torch.tensor(nxt), ht)
+            qs = q.gather(2, torch.tensor(act).long().unsqueeze(-1)).squeeze(-1)
+            _td = (torch.tensor(rew).sum(1) + (1 - torch.tensor(done).float()) * 0.99 * tq.max(2)[0].sum(1)
+                   - qs.sum(1)).abs()
+            env.reset_envs(done)
+            keep = torch.tensor(~done).float().view(E, 1, 1)
+            h, ht = h * keep, ht * keep
+            obs = torch.tensor(env.observe())
+            steps += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": steps * E * N / dt, "unit": "agent-env-steps/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle rollout step (numpy env + torch-CPU GRU-{H} nets, behavior+target, TD) at "
+                      f"{E} envs x {N} agents, {steps} steps in {dt:.1f}s"}
+
+
+def time_kernel(fn, iters=50):
+    """Average device time of fn() via events on torch's current stream (our launch stream)."""
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    start.record()
+    for _ in range(iters):
+        fn()
+    end.record()
+    torch.cuda.synchronize()
+    return start.elapsed_time(end) / iters / 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--hidden", type=int, default=64)
+    ap.add_argument("--epsilon", type=float, default=0.1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from minimarl.engine import RolloutEngine
+    E, N, Hh = args.envs, args.agents, args.hidden
+    F1, G = 64, Hh
+    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=16 * E, seed=1234 + rank, device=dev)
+    D = eng.D
+    for _ in range(args.warmup):
+        eng.step(args.epsilon)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step(args.epsilon)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = args.steps * E * N * world / elapsed
+
+    # roofline of the dominant kernel: the fused agent Q forward (behavior launch of a step)
+    fwd = lambda: eng.behavior.forward_io(E, eng.io_b)  # noqa: E731
+    t_fwd = time_kernel(fwd)
+    flops = qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
+    achieved = flops / t_fwd / 1e12
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                "kernel": "agent_q_fwd_kernel<64,64,64,1>", "kernel_us": round(t_fwd * 1e6, 2),
+                "flop_per_launch": flops}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(E, N, F1, G, Hh)
+
+    if rank == 0:
+        line = {
+            "metric": "agent-env-steps/sec (4096 envs x 8 agents per GPU, QMIX GRU-64 rollout step)",
+            "value": round(value, 1), "unit": "agent-env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (build's gridworld, random init)",
+            "config": {"workload": "QMIX 8-agent gridworld rollout, 4096 envs/GPU, GRU-64 agents, chunk 10, PER",
+                       "envs_per_gpu": E, "agents": N, "obs_dim": D, "f1": F1, "gru": Hh, "chunk": 10,
+                       "parallelism": f"env-shard x{world}"},
+            "learner_updates_per_s": None,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

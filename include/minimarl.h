@@ -1,0 +1,136 @@
+/*
+ * minimarl — MI355X-native C ABI for the QMIX / VDN rollout-and-learn hot path.
+ *
+ * Plain C: raw device pointers, sizes, strides and a hipStream_t passed as
+ * void*. Every call enqueues work on that stream and returns immediately (no
+ * host synchronisation) unless documented otherwise. Return value: 0 on
+ * success, a negative errno-style code otherwise; mm_last_error() gives the
+ * message (thread-local). Handles are opaque, created/destroyed in pairs,
+ * stream-ordered and not thread-safe per handle.
+ *
+ * Which reference interface each entry point replaces (reference @ /root/reference):
+ *   mm_env_*             gym.make("ma_gym:Checkers-v0") reset/step   vdn/main.py:61-64,83,93,143; qmix/main.py:66-71,189
+ *   mm_agent_q_fwd       Q_Net.forward / sample_action               qmix/_network.py:44-74; vdn/_network.py:52-58,71-88
+ *   mm_qnet_*            Q_Net parameters (per-agent Linear/GRUCell)  qmix/_network.py:15-42; vdn/_network.py:32-42,61-69
+ *   mm_td_chunk_step     cal_td_error + chunk assembly               vdn/_utils.py:44-52; vdn/main.py:140-167
+ *   mm_per_*             Prioritized_Experience_Replay + SumTree     vdn/replay_buffer/{buffer,sumtree}.py; qmix/replay_buffer/{per,sumtree}.py
+ *   mm_mixer_fwd         Mix_Net.forward                             qmix/_network.py:199-217
+ */
+#ifndef MINIMARL_H
+#define MINIMARL_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* mm_stream_t; /* hipStream_t */
+
+const char* mm_last_error(void);
+int mm_version(void);
+
+/* ------------------------------------------------------------------ Q-network */
+/* Per-agent (non-shared) Q_Net: Linear(D,F1)+ReLU, Linear(F1,G)+ReLU, GRUCell(G,H), Linear(H,A).
+ * Reference sizes: F1=64, G=H=32 (qmix/_network.py:11-13). Supported (F1,G,H):
+ * (64,32,32) (64,64,64) (128,32,32) (64,32,64); A <= 64; any D >= 1. */
+typedef struct mm_qnet_dims {
+  int32_t n_agents, obs_dim, f1, g, h, n_actions;
+} mm_qnet_dims;
+
+/* Canonical flat parameter layout (float32): the 10 tensors
+ *   W1[N,F1,D] b1[N,F1] W2[N,G,F1] b2[N,G] Wih[N,3H,G] Whh[N,3H,H] bih[N,3H] bhh[N,3H] Wq[N,A,H] bq[N,A]
+ * concatenated in that order. offs[0..9] = element offsets, offs[10] = total. */
+int mm_qnet_param_offsets(const mm_qnet_dims* d, int64_t offs[11]);
+/* Size (floats) of the MFMA-fragment-packed weight image used by mm_agent_q_fwd. */
+int64_t mm_qnet_packed_count(const mm_qnet_dims* d);
+/* Repack flat params into the fragment image (call after every optimizer step). */
+int mm_qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s);
+
+enum { MM_Q_NONE = 0, MM_Q_ACT = 1, MM_Q_MAX = 2, MM_Q_GATHER = 3 };
+
+typedef struct mm_qfwd_io {
+  /* obs(e, agent, f) = obs[r(e)*obs_se + obs_off + agent*obs_sa + f] with r(e) = e, or r(e) = obs_row[e]
+   * when obs_row != NULL (a gather); obs_row[e] < 0 selects reset_obs[agent*obs_sa + f] instead. */
+  const float* obs; int64_t obs_se, obs_sa, obs_off;
+  const int64_t* obs_row; const float* reset_obs;
+  /* hidden in/out: h(e, agent, f) = h[e*se + agent*sa + f*sf]; reset[e] != 0 => h_in treated as 0 */
+  const float* h_in; int64_t hin_se, hin_sa, hin_sf;
+  float* h_out; int64_t hout_se, hout_sa, hout_sf;
+  const uint8_t* reset;
+  float* q_out; int64_t q_se, q_sa;                 /* optional Q values [.., A] (unit stride) */
+  int32_t mode;                                       /* MM_Q_* */
+  /* MM_Q_ACT: epsilon-greedy, one uniform per env row (vdn/_network.py:53). Injected draws if
+   * u != NULL (u[E], rand_act[E*N]) else counter RNG(seed, counter, env[, agent]). */
+  float epsilon; const float* u; const int32_t* rand_act; uint64_t seed; uint64_t counter;
+  int32_t* act_out;                                   /* [E,N] chosen actions (ACT) */
+  const int32_t* act_in; int64_t act_se;              /* GATHER: act_in[e*act_se + agent] */
+  float* qsel_out;                                    /* [E,N]: Q(a_chosen) (ACT/GATHER) or max_a Q (MAX) */
+} mm_qfwd_io;
+
+int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,
+                   mm_stream_t s);
+
+/* Survey-style convenience entry: contiguous obs [E,N,D], hidden [E,N,H] -> q [E,N,A], h_out [E,N,H]. */
+int mm_agent_q_fwd_simple(const mm_qnet_dims* d, const float* packed, const float* obs, const float* h,
+                          float* q, float* h_out, int64_t n_envs, mm_stream_t s);
+
+/* ------------------------------------------------------------------ environment */
+typedef struct mm_env_cfg {
+  int32_t n_agents, max_steps, full_observable, cols;
+  float step_cost;
+} mm_env_cfg;
+typedef struct mm_env mm_env;
+
+int mm_env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out);
+void mm_env_destroy(mm_env* env);
+int mm_env_obs_dim(const mm_env* env);
+/* Reset every env; writes obs [E,N,D]. */
+int mm_env_reset(mm_env* env, float* obs, mm_stream_t s);
+/* Step every env with act [E,N] (int32): writes the (terminal) next obs [E,N,D], rew [E,N],
+ * done [E] (env-level, 1 byte). If obs_cur != NULL the env also auto-resets done envs and writes
+ * the next CURRENT obs (reset obs where done) into obs_cur; otherwise done envs stay terminal. */
+int mm_env_step(mm_env* env, const int32_t* act, float* next_obs, float* obs_cur, float* rew,
+                uint8_t* done, mm_stream_t s);
+/* Copy out the integer state (for parity tests): pos [E,N,2] int32, grid [E,R,C] int8, steps [E],
+ * apples [E]; host pointers, synchronous. */
+int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples);
+int mm_env_grid_shape(const mm_env* env, int32_t* rows, int32_t* cols);
+
+/* ------------------------------------------------------------------ TD error + chunk store */
+/* One rollout step for E envs: td = |sum_i r_i + (1-done)*gamma*sum_i maxq'_i - sum_i q_taken_i|
+ * (vdn/_utils.py:44-52), accumulated into chunk_td[E]; and the transition is written into the
+ * device chunk store at slot t = step_in_chunk of chunk row chunk_base+e:
+ *   act8[row, t, N] (uint8), rew[row, t, N] (f32), done[row, t] (uint8)
+ * obs are written by the env kernel directly into the store. */
+int mm_td_chunk_step(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                     const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
+                     int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
+                     uint8_t* store_done, int64_t store_row0, mm_stream_t s);
+
+/* ------------------------------------------------------------------ prioritized replay */
+enum { MM_PER_VDN = 0, MM_PER_QMIX = 1 };
+typedef struct mm_per mm_per;
+int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, double eps, double step_weight,
+                  int32_t use_step_weight, double alpha_inc, double beta_inc, mm_per** out);
+void mm_per_destroy(mm_per* per);
+/* Insert K chunks with rollout td sums td[K] (device f32): free slots first, then the K lowest
+ * leaves are replaced; slots_out[K] (device int64) receives the data slot of each insert. */
+int mm_per_add_batch(mm_per* per, const float* td, int64_t k, int64_t* slots_out, mm_stream_t s);
+/* Stratified sample of B leaves with injected fractions fracs[B] (device f64, in [0,1)):
+ * nodes_out / slots_out (device int64), is_w (device f32). Anneals alpha/beta first. */
+int mm_per_sample(mm_per* per, int32_t batch, const double* fracs, int64_t* nodes_out, int64_t* slots_out,
+                  float* is_w, mm_stream_t s);
+/* Same with device-generated fractions from a counter RNG. */
+int mm_per_sample_rng(mm_per* per, int32_t batch, uint64_t seed, uint64_t counter, int64_t* nodes_out,
+                      int64_t* slots_out, float* is_w, mm_stream_t s);
+/* Priority update leaf(nodes[b]) = (td[b]+eps)^alpha; duplicate nodes: last sample index wins. */
+int mm_per_update(mm_per* per, const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s);
+double* mm_per_tree_ptr(mm_per* per);               /* device f64 [2*cap-1] */
+int64_t mm_per_size(const mm_per* per);
+double mm_per_alpha(const mm_per* per);
+double mm_per_beta(const mm_per* per);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,334 @@
+// Fused per-agent Q-network forward for E lockstep envs x N agents (gfx950).
+//
+// Replaces Q_Net.forward + sample_action (qmix/_network.py:44-74,
+// vdn/_network.py:52-58,71-88): per agent i (own weights)
+//   x1 = ReLU(W1 o + b1) (D->F1), x2 = ReLU(W2 x1 + b2) (F1->G),
+//   h' = GRUCell(x2, h) (torch gate order r, z, n; h' = n + z*(h-n)),
+//   q  = Wq h' + bq, then epsilon-greedy / max / gather epilogue.
+//
+// Mapping: one wave = 32 envs of one agent; features on MFMA rows, envs on
+// columns, so every layer's D registers are directly the next layer's B
+// operand (see common.h kperm) — no LDS, no transposes. Weights are the A
+// operand, read as 16-float contiguous per-lane fragments from the packed image
+// (4 x dwordx4 per 16 MFMAs), L2/L1-resident: block b serves agent b % N, so
+// with N = 8 each XCD's L2 only ever holds one agent's weights.
+// Arithmetic: exact-f32 MFMA v_mfma_f32_32x32x2_f32 (fp32 in, fp32 accumulate).
+#include "common.h"
+#include "minimarl.h"
+#include "qnet_geo.h"
+
+namespace mm {
+
+struct QFwdParams {
+  mm_qfwd_io io;
+  QnetGeo g;
+  const float* packed;
+  int E, N, D, A;
+};
+
+__device__ __forceinline__ void load_frag(const float* base, int lane, float (&a)[16]) {
+  const float4* p = reinterpret_cast<const float4*>(base + lane * 16);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 v = p[q];
+    a[4 * q + 0] = v.x;
+    a[4 * q + 1] = v.y;
+    a[4 * q + 2] = v.z;
+    a[4 * q + 3] = v.w;
+  }
+}
+
+__device__ __forceinline__ f32x16 load_bias(const float* base, int hh) {
+  const float4* p = reinterpret_cast<const float4*>(base + hh * 16);
+  f32x16 r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 v = p[q];
+    r[4 * q + 0] = v.x;
+    r[4 * q + 1] = v.y;
+    r[4 * q + 2] = v.z;
+    r[4 * q + 3] = v.w;
+  }
+  return r;
+}
+
+// acc += W[rb-block] * X, X given as KB k-blocks of D-layout registers.
+template <int KB>
+__device__ __forceinline__ void mma_layer_block(const float* wl, int rb, const f32x16 (&x)[KB], int lane, f32x16& acc) {
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    float a[16];
+    load_frag(wl + (int64_t)(rb * KB + kb) * 1024, lane, a);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = mfma32(a[s], x[kb][s], acc);
+  }
+}
+
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(256) void agent_q_fwd_kernel(QFwdParams p) {
+  constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 31, hh = lane >> 5;
+  const int agent = blockIdx.x % p.N;
+  const int tile = blockIdx.x / p.N;
+  const int e = tile * 128 + (threadIdx.x >> 6) * 32 + j;
+  const bool valid = e < p.E;
+  const mm_qfwd_io& io = p.io;
+  const float* W = p.packed + (int64_t)agent * p.g.agent_stride;
+
+  // ---- layer 1: x1 = ReLU(W1 o + b1), K = D streamed in 32-wide k-blocks
+  const float* orow = nullptr;
+  if (valid) {
+    const int64_t r = io.obs_row ? io.obs_row[e] : (int64_t)e;
+    orow = (r >= 0) ? io.obs + r * io.obs_se + io.obs_off + (int64_t)agent * io.obs_sa
+                    : io.reset_obs + (int64_t)agent * io.obs_sa;
+  }
+  f32x16 x1[RB1];
+#pragma unroll
+  for (int rb = 0; rb < RB1; ++rb) x1[rb] = load_bias(W + p.g.off_b1 + rb * 32, hh);
+  for (int kb = 0; kb < p.g.KD; ++kb) {
+    float xb[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = kb * 32 + kperm(s, hh);
+      xb[s] = (valid && k < p.D) ? orow[k] : 0.0f;
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB1; ++rb) {
+      float a[16];
+      load_frag(W + p.g.off_l1 + (int64_t)(rb * p.g.KD + kb) * 1024, lane, a);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) x1[rb] = mfma32(a[s], xb[s], x1[rb]);
+    }
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB1; ++rb)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) x1[rb][s] = fmaxf(x1[rb][s], 0.0f);
+
+  // ---- layer 2: x2 = ReLU(W2 x1 + b2)
+  f32x16 x2[RB2];
+#pragma unroll
+  for (int rb = 0; rb < RB2; ++rb) {
+    x2[rb] = load_bias(W + p.g.off_b2 + rb * 32, hh);
+    mma_layer_block<RB1>(W + p.g.off_l2, rb, x1, lane, x2[rb]);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) x2[rb][s] = fmaxf(x2[rb][s], 0.0f);
+  }
+
+  // ---- GRU cell
+  const bool zero_h = !valid || (io.reset && io.reset[e]);
+  f32x16 h0[HB];
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int f = hb * 32 + kperm(s, hh);
+      h0[hb][s] = zero_h ? 0.0f
+                         : io.h_in[(int64_t)e * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)f * io.hin_sf];
+    }
+  }
+  f32x16 h1[HB];
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb) {
+    f32x16 ar = load_bias(W + p.g.off_brz + hb * 32, hh);
+    f32x16 az = load_bias(W + p.g.off_brz + (HB + hb) * 32, hh);
+    f32x16 anx = load_bias(W + p.g.off_bin + hb * 32, hh);
+    f32x16 anh = load_bias(W + p.g.off_bhn + hb * 32, hh);
+    mma_layer_block<RB2>(W + p.g.off_ih, hb, x2, lane, ar);
+    mma_layer_block<RB2>(W + p.g.off_ih, HB + hb, x2, lane, az);
+    mma_layer_block<RB2>(W + p.g.off_ih, 2 * HB + hb, x2, lane, anx);
+    mma_layer_block<HB>(W + p.g.off_hh, hb, h0, lane, ar);
+    mma_layer_block<HB>(W + p.g.off_hh, HB + hb, h0, lane, az);
+    mma_layer_block<HB>(W + p.g.off_hh, 2 * HB + hb, h0, lane, anh);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float r = sigmoidf_(ar[s]);
+      const float z = sigmoidf_(az[s]);
+      const float n = tanhf(anx[s] + r * anh[s]);
+      h1[hb][s] = n + z * (h0[hb][s] - n);
+    }
+  }
+  if (valid && io.h_out) {
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int f = hb * 32 + kperm(s, hh);
+        io.h_out[(int64_t)e * io.hout_se + (int64_t)agent * io.hout_sa + (int64_t)f * io.hout_sf] = h1[hb][s];
+      }
+  }
+
+  // ---- Q head
+  f32x16 qa[AB];
+#pragma unroll
+  for (int ab = 0; ab < AB; ++ab) {
+    qa[ab] = load_bias(W + p.g.off_bq + ab * 32, hh);
+    mma_layer_block<HB>(W + p.g.off_q, ab, h1, lane, qa[ab]);
+  }
+  if (valid && io.q_out) {
+    float* qrow = io.q_out + (int64_t)e * io.q_se + (int64_t)agent * io.q_sa;
+#pragma unroll
+    for (int ab = 0; ab < AB; ++ab)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int row = ab * 32 + kperm(s, hh);
+        if (row < p.A) qrow[row] = qa[ab][s];
+      }
+  }
+  if (io.mode == MM_Q_NONE) return;
+
+  // ---- epilogue: first-index argmax over A rows spread across the two lane halves
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int ab = 0; ab < AB; ++ab)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int row = ab * 32 + kperm(s, hh);
+      const float v = qa[ab][s];
+      if (row < p.A && (v > best || (v == best && row < bi))) {
+        best = v;
+        bi = row;
+      }
+    }
+  const float ob = __shfl_xor(best, 32);
+  const int oi = __shfl_xor(bi, 32);
+  if (ob > best || (ob == best && oi < bi)) {
+    best = ob;
+    bi = oi;
+  }
+  int act = bi;
+  if (io.mode == MM_Q_ACT) {
+    float u;
+    if (io.u) {
+      u = valid ? io.u[e] : 1.0f;
+    } else {
+      u = rng_uniform(rng_draw(io.seed, io.counter, (uint64_t)e, 0xFFFFFFFFull));
+    }
+    if (u <= io.epsilon) {
+      if (io.rand_act) {
+        act = valid ? io.rand_act[(int64_t)e * p.N + agent] : 0;
+      } else {
+        act = (int)(rng_draw(io.seed ^ 0x5bd1e995ull, io.counter, (uint64_t)e, (uint64_t)agent) % (uint64_t)p.A);
+      }
+    }
+  } else if (io.mode == MM_Q_GATHER) {
+    act = valid ? io.act_in[(int64_t)e * io.act_se + agent] : 0;
+  }
+  float mine = 0.0f;
+#pragma unroll
+  for (int ab = 0; ab < AB; ++ab)
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      if (ab * 32 + kperm(s, hh) == act) mine = qa[ab][s];
+  const float qsel = (io.mode == MM_Q_MAX) ? best : mine + __shfl_xor(mine, 32);
+  if (valid && hh == 0) {
+    const int64_t o = (int64_t)e * p.N + agent;
+    if (io.act_out && io.mode == MM_Q_ACT) io.act_out[o] = act;
+    if (io.qsel_out) io.qsel_out[o] = qsel;
+  }
+}
+
+// ---------------------------------------------------------------- packing
+// One thread per packed element: gathers the canonical flat parameters into
+// the per-lane MFMA fragment image (zero padding outside the real shape).
+__global__ void qnet_pack_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
+                                 int D, int F1, int G, int H, int A, QnetOffsets o) {
+  const int64_t per_agent = g.agent_stride;
+  const int64_t total = per_agent * N;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int agent = (int)(idx / per_agent);
+    int64_t r = idx % per_agent;
+    float v = 0.0f;
+    // weight images: [rb][kb][lane][s]
+    auto wimg = [&](int64_t off, int KB, int rows, int cols, int64_t src, int64_t& rr, bool& hit) {
+      const int64_t sz = (int64_t)((rows + 31) / 32) * KB * 1024;
+      if (rr >= off && rr < off + sz) {
+        const int64_t t = rr - off;
+        const int s = (int)(t & 15), lane = (int)((t >> 4) & 63);
+        const int64_t blk = t >> 10;
+        const int kb = (int)(blk % KB), rb = (int)(blk / KB);
+        const int row = rb * 32 + (lane & 31), col = kb * 32 + kperm(s, lane >> 5);
+        if (row < rows && col < cols) v = params[src + (int64_t)row * cols + col];
+        hit = true;
+      }
+    };
+    // bias images: [rb][h][s] -> b[32 rb + kperm(s, h)]
+    auto bimg = [&](int64_t off, int rows, int64_t src, int64_t src2, int64_t& rr, bool& hit) {
+      const int64_t sz = (int64_t)((rows + 31) / 32) * 32;
+      if (rr >= off && rr < off + sz) {
+        const int64_t t = rr - off;
+        const int s = (int)(t & 15), h = (int)((t >> 4) & 1), rb = (int)(t >> 5);
+        const int row = rb * 32 + kperm(s, h);
+        if (row < rows) v = params[src + row] + (src2 >= 0 ? params[src2 + row] : 0.0f);
+        hit = true;
+      }
+    };
+    bool hit = false;
+    wimg(g.off_l1, g.KD, F1, D, o.W1 + (int64_t)agent * F1 * D, r, hit);
+    if (!hit) wimg(g.off_l2, F1 / 32, G, F1, o.W2 + (int64_t)agent * G * F1, r, hit);
+    if (!hit) wimg(g.off_ih, G / 32, 3 * H, G, o.Wih + (int64_t)agent * 3 * H * G, r, hit);
+    if (!hit) wimg(g.off_hh, H / 32, 3 * H, H, o.Whh + (int64_t)agent * 3 * H * H, r, hit);
+    if (!hit) wimg(g.off_q, H / 32, A, H, o.Wq + (int64_t)agent * A * H, r, hit);
+    if (!hit) bimg(g.off_b1, F1, o.b1 + (int64_t)agent * F1, -1, r, hit);
+    if (!hit) bimg(g.off_b2, G, o.b2 + (int64_t)agent * G, -1, r, hit);
+    if (!hit) bimg(g.off_brz, 2 * H, o.bih + (int64_t)agent * 3 * H, o.bhh + (int64_t)agent * 3 * H, r, hit);
+    if (!hit) bimg(g.off_bin, H, o.bih + (int64_t)agent * 3 * H + 2 * H, -1, r, hit);
+    if (!hit) bimg(g.off_bhn, H, o.bhh + (int64_t)agent * 3 * H + 2 * H, -1, r, hit);
+    if (!hit) bimg(g.off_bq, A, o.bq + (int64_t)agent * A, -1, r, hit);
+    packed[idx] = v;
+  }
+}
+
+int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s) {
+  QnetGeo g;
+  QnetOffsets o;
+  int rc = qnet_geometry(d, &g, &o);
+  if (rc) return rc;
+  const int64_t total = g.agent_stride * d->n_agents;
+  const int threads = 256;
+  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 4096);
+  hipLaunchKernelGGL(qnet_pack_kernel, dim3(blocks), dim3(threads), 0, s, params, packed, g, d->n_agents,
+                     d->obs_dim, d->f1, d->g, d->h, d->n_actions, o);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+template <int F1, int G, int H, int AB>
+static int launch_fwd(const QFwdParams& p, hipStream_t s) {
+  const int tiles = (p.E + 127) / 128;
+  hipLaunchKernelGGL((agent_q_fwd_kernel<F1, G, H, AB>), dim3(tiles * p.N), dim3(256), 0, s, p);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs, hipStream_t s) {
+  MM_REQUIRE(d && packed && io, "agent_q_fwd: null argument");
+  MM_REQUIRE(n_envs >= 0 && n_envs < (1ll << 31), "agent_q_fwd: bad n_envs %lld", (long long)n_envs);
+  if (n_envs == 0) return MM_OK;
+  QFwdParams p;
+  p.io = *io;
+  QnetOffsets o;
+  int rc = qnet_geometry(d, &p.g, &o);
+  if (rc) return rc;
+  p.packed = packed;
+  p.E = (int)n_envs;
+  p.N = d->n_agents;
+  p.D = d->obs_dim;
+  p.A = d->n_actions;
+  MM_REQUIRE(io->obs && (io->h_in || true), "agent_q_fwd: obs required");
+  MM_REQUIRE(io->h_in || io->reset == nullptr, "agent_q_fwd: h_in required");
+  MM_REQUIRE(io->mode != MM_Q_GATHER || io->act_in, "agent_q_fwd: GATHER needs act_in");
+  MM_REQUIRE(io->obs_row == nullptr || io->reset_obs, "agent_q_fwd: obs_row needs reset_obs");
+  const int AB = (d->n_actions + 31) / 32;
+  if (d->f1 == 64 && d->g == 32 && d->h == 32) return AB == 1 ? launch_fwd<64, 32, 32, 1>(p, s) : launch_fwd<64, 32, 32, 2>(p, s);
+  if (d->f1 == 64 && d->g == 64 && d->h == 64) return AB == 1 ? launch_fwd<64, 64, 64, 1>(p, s) : launch_fwd<64, 64, 64, 2>(p, s);
+  if (d->f1 == 128 && d->g == 32 && d->h == 32) return AB == 1 ? launch_fwd<128, 32, 32, 1>(p, s) : launch_fwd<128, 32, 32, 2>(p, s);
+  if (d->f1 == 64 && d->g == 32 && d->h == 64) return AB == 1 ? launch_fwd<64, 32, 64, 1>(p, s) : launch_fwd<64, 32, 64, 2>(p, s);
+  set_error("agent_q_fwd: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
+  return MM_EINVAL;
+}
+
+}  // namespace mm

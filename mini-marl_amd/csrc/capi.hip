@@ -1,0 +1,75 @@
+// extern "C" surface of libminimarl (see include/minimarl.h) + error plumbing.
+#include <cstdarg>
+#include <cstdio>
+
+#include "common.h"
+#include "minimarl.h"
+#include "qnet_geo.h"
+
+namespace mm {
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s);
+int agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs, hipStream_t s);
+}  // namespace mm
+
+extern "C" {
+
+const char* mm_last_error(void) { return mm::g_err; }
+int mm_version(void) { return 100; }
+
+int mm_qnet_param_offsets(const mm_qnet_dims* d, int64_t offs[11]) {
+  mm::QnetOffsets o;
+  int rc = mm::qnet_offsets(d, &o);
+  if (rc) return rc;
+  const int64_t v[11] = {o.W1, o.b1, o.W2, o.b2, o.Wih, o.Whh, o.bih, o.bhh, o.Wq, o.bq, o.total};
+  for (int i = 0; i < 11; ++i) offs[i] = v[i];
+  return MM_OK;
+}
+
+int64_t mm_qnet_packed_count(const mm_qnet_dims* d) {
+  mm::QnetGeo g;
+  mm::QnetOffsets o;
+  if (mm::qnet_geometry(d, &g, &o)) return -1;
+  return g.agent_stride * d->n_agents;
+}
+
+int mm_qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s) {
+  MM_REQUIRE(params && packed, "qnet_pack: null pointer");
+  return mm::qnet_pack(d, params, packed, (hipStream_t)s);
+}
+
+int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,
+                   mm_stream_t s) {
+  return mm::agent_q_fwd(d, packed, io, n_envs, (hipStream_t)s);
+}
+
+int mm_agent_q_fwd_simple(const mm_qnet_dims* d, const float* packed, const float* obs, const float* h, float* q,
+                          float* h_out, int64_t n_envs, mm_stream_t s) {
+  MM_REQUIRE(d, "agent_q_fwd_simple: null dims");
+  mm_qfwd_io io = {};
+  io.obs = obs;
+  io.obs_se = (int64_t)d->n_agents * d->obs_dim;
+  io.obs_sa = d->obs_dim;
+  io.h_in = h;
+  io.hin_se = (int64_t)d->n_agents * d->h;
+  io.hin_sa = d->h;
+  io.hin_sf = 1;
+  io.h_out = h_out;
+  io.hout_se = io.hin_se;
+  io.hout_sa = io.hin_sa;
+  io.hout_sf = 1;
+  io.q_out = q;
+  io.q_se = (int64_t)d->n_agents * d->n_actions;
+  io.q_sa = d->n_actions;
+  io.mode = MM_Q_NONE;
+  return mm::agent_q_fwd(d, packed, &io, n_envs, (hipStream_t)s);
+}
+}

@@ -1,0 +1,63 @@
+// Shared helpers for the minimarl HIP/CDNA4 kernels (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MM_OK 0
+#define MM_EINVAL (-22)
+#define MM_EHIP (-5)
+#define MM_ENOMEM (-12)
+
+namespace mm {
+
+void set_error(const char* fmt, ...);
+
+// A wave (64 lanes) computes a 32-env x (feature rows) tile with the exact-f32
+// MFMA v_mfma_f32_32x32x2_f32. Fragment maps (gfx950):
+//   A[i = lane&31][k = lane>>5], B[k = lane>>5][j = lane&31],
+//   D reg r of lane (j, h=lane>>5): row (r&3) + 8*(r>>2) + 4*h, col j.
+// Chaining layers through registers: k-step s of a 32-deep k-block uses, in
+// lane half h, the input feature kperm(s, h) = (s&3) + 8*(s>>2) + 4*h, i.e.
+// exactly D register s of the producing layer. Weights are pre-packed so that
+// lane (i, h) of k-step s reads W[32*rb + i][32*kb + kperm(s, h)].
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__host__ __device__ __forceinline__ int kperm(int s, int h) { return (s & 3) + 8 * (s >> 2) + 4 * h; }
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// splitmix64-based counter RNG (stateless; one draw per (seed, counter, a, b)).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t rng_draw(uint64_t seed, uint64_t counter, uint64_t a, uint64_t b) {
+  return mix64(seed ^ mix64(counter * 0xD1B54A32D192ED03ull ^ mix64(a * 0x8CB92BA72F3D8DD7ull + b)));
+}
+__device__ __forceinline__ float rng_uniform(uint64_t r) { return (float)(r >> 40) * (1.0f / 16777216.0f); }
+
+}  // namespace mm
+
+#define MM_HIP_CHECK(expr)                                                     \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      mm::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),     \
+                    __FILE__, __LINE__);                                       \
+      return MM_EHIP;                                                          \
+    }                                                                          \
+  } while (0)
+
+#define MM_REQUIRE(cond, ...)        \
+  do {                               \
+    if (!(cond)) {                   \
+      mm::set_error(__VA_ARGS__);    \
+      return MM_EINVAL;              \
+    }                                \
+  } while (0)

@@ -1,0 +1,312 @@
+// Lockstep "checkers" gridworld: E envs x N agents stepped by one kernel (gfx950).
+//
+// Replaces the per-step gym env call (vdn/main.py:93,143; qmix/main.py:115,189;
+// mappo/runner/shared/magym_runner.py:53-57). ma_gym itself is absent, so the
+// dynamics are the build's own spec, defined in oracle/env.py (parity with
+// ma_gym: UNPINNED; parity with oracle/env.py: bit-exact, integer state).
+//
+// Block = 256 threads, EB = 64 envs. Phase 0 stages the block's grids (bytes,
+// [E][R*C] so the copy is one contiguous coalesced run) and positions in LDS;
+// phase 1 runs the sequential-in-agent-order dynamics one thread per env;
+// phase 2 generates obs [env, agent, feat] with consecutive threads on
+// consecutive floats (coalesced stores); phase 3 writes state back (or the
+// initial state for envs that auto-reset).
+#include <vector>
+
+#include "common.h"
+#include "minimarl.h"
+
+namespace mm {
+static constexpr int OBS_LOCAL = 47;
+static constexpr int EB = 64;
+
+struct EnvDev {
+  int E, N, R, C, D, max_steps, full_obs, init_apples;
+  float step_cost, inv_r, inv_c;
+  int32_t* pos;     // [E][N] r*256 + c
+  int8_t* grid;     // [E][R*C] 0 empty, 1 lemon, 2 apple
+  int32_t* steps;   // [E]
+  int32_t* apples;  // [E]
+  const int8_t* init_grid;  // [R*C]
+  const int32_t* init_pos;  // [N]
+  float* reset_obs;         // [N][D]
+};
+}  // namespace mm
+
+struct mm_env {
+  mm::EnvDev d;
+  void* alloc;
+};
+
+namespace mm {
+
+__device__ __forceinline__ float obs_value(const EnvDev& d, const int32_t* pos, const int8_t* grid, int k, int f) {
+  // f in [0, 47): local obs feature of agent k
+  const int p = pos[k];
+  const int r = p >> 8, c = p & 255;
+  if (f == 0) return (float)r * d.inv_r;
+  if (f == 1) return (float)c * d.inv_c;
+  const int cell = (f - 2) / 5, ch = (f - 2) % 5;
+  const int rr = r + cell / 3 - 1, cc = c + cell % 3 - 1;
+  const bool inside = rr >= 0 && rr < d.R && cc >= 0 && cc < d.C;
+  if (!inside) return ch == 4 ? 1.0f : 0.0f;
+  if (ch == 4) return 0.0f;
+  const int item = grid[rr * d.C + cc];
+  if (ch == 0) return item == 1 ? 1.0f : 0.0f;
+  if (ch == 1) return item == 2 ? 1.0f : 0.0f;
+  if (item != 0) return 0.0f;
+  const int key = (rr << 8) | cc;
+  for (int j = 0; j < d.N; ++j)
+    if (pos[j] == key) return ((j & 1) == (ch - 2)) ? 1.0f : 0.0f;
+  return 0.0f;
+}
+
+// Writes obs of one env (N x D) from the given state into out (+ optional 2nd copy).
+__device__ __forceinline__ float obs_elem(const EnvDev& d, const int32_t* pos, const int8_t* grid, int k, int f) {
+  if (d.full_obs) return obs_value(d, pos, grid, f / OBS_LOCAL, f % OBS_LOCAL);
+  (void)k;
+  return obs_value(d, pos, grid, k, f);
+}
+
+__global__ __launch_bounds__(256) void env_reset_kernel(EnvDev d, float* obs, int write_table) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int32_t* spos = reinterpret_cast<int32_t*>(smem);
+  int8_t* sgrid = reinterpret_cast<int8_t*>(smem + ((d.N * 4 + 15) & ~15));
+  const int RC = d.R * d.C;
+  for (int i = threadIdx.x; i < d.N; i += blockDim.x) spos[i] = d.init_pos[i];
+  for (int i = threadIdx.x; i < RC; i += blockDim.x) sgrid[i] = d.init_grid[i];
+  __syncthreads();
+  if (write_table && blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < d.N * d.D; i += blockDim.x)
+      d.reset_obs[i] = obs_elem(d, spos, sgrid, i / d.D, i % d.D);
+  }
+  const int e0 = blockIdx.x * EB;
+  const int ne = min(EB, d.E - e0);
+  for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) d.grid[(int64_t)e0 * RC + i] = sgrid[i % RC];
+  for (int i = threadIdx.x; i < ne * d.N; i += blockDim.x) d.pos[(int64_t)e0 * d.N + i] = spos[i % d.N];
+  for (int i = threadIdx.x; i < ne; i += blockDim.x) {
+    d.steps[e0 + i] = 0;
+    d.apples[e0 + i] = d.init_apples;
+  }
+  if (obs) {
+    const int ND = d.N * d.D;
+    for (int i = threadIdx.x; i < ne * ND; i += blockDim.x) {
+      const int k = (i % ND) / d.D, f = i % d.D;
+      obs[(int64_t)e0 * ND + i] = obs_elem(d, spos, sgrid, k, f);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* __restrict__ act,
+                                                       float* __restrict__ next_obs, int64_t next_se,
+                                                       const int64_t* __restrict__ next_row,
+                                                       float* __restrict__ obs_cur, float* __restrict__ rew,
+                                                       uint8_t* __restrict__ done_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int RC = d.R * d.C;
+  const int N = d.N;
+  int32_t* spos = reinterpret_cast<int32_t*>(smem);                        // [EB][N]
+  uint8_t* sdone = reinterpret_cast<uint8_t*>(smem + EB * N * 4);          // [EB]
+  int8_t* sgrid = reinterpret_cast<int8_t*>(smem + EB * N * 4 + EB);       // [EB][RC]
+  const int e0 = blockIdx.x * EB;
+  const int ne = min(EB, d.E - e0);
+
+  // phase 0: stage grids and positions (contiguous runs)
+  for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) sgrid[i] = d.grid[(int64_t)e0 * RC + i];
+  for (int i = threadIdx.x; i < ne * N; i += blockDim.x) spos[i] = d.pos[(int64_t)e0 * N + i];
+  __syncthreads();
+
+  // phase 1: dynamics, one thread per env, agents in id order (oracle/env.py VecEnvOracle.step)
+  if (threadIdx.x < ne) {
+    const int le = threadIdx.x, e = e0 + le;
+    int32_t* p = spos + le * N;
+    int8_t* g = sgrid + le * RC;
+    int apples = d.apples[e];
+    const int steps = d.steps[e] + 1;
+    for (int k = 0; k < N; ++k) {
+      const int a = act[(int64_t)e * N + k];
+      const int r = p[k] >> 8, c = p[k] & 255;
+      const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
+      const int nc = c + (a == 1 ? -1 : (a == 3 ? 1 : 0));
+      bool ok = nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
+      const int key = (nr << 8) | nc;
+      for (int j = 0; j < N; ++j) ok = ok && (j == k || p[j] != key);
+      if (ok) p[k] = key;
+      const int cell = (p[k] >> 8) * d.C + (p[k] & 255);
+      const int item = g[cell];
+      float rk = d.step_cost;
+      const bool big = (k & 1) == 0;
+      rk += item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f);
+      apples -= item == 2 ? 1 : 0;
+      g[cell] = 0;
+      rew[(int64_t)e * N + k] = rk;
+    }
+    const bool dn = steps >= d.max_steps || apples == 0;
+    sdone[le] = dn ? 1 : 0;
+    done_out[e] = dn ? 1 : 0;
+    d.steps[e] = dn && obs_cur ? 0 : steps;
+    d.apples[e] = dn && obs_cur ? d.init_apples : apples;
+  }
+  __syncthreads();
+
+  // phase 2: obs (terminal next obs), consecutive threads -> consecutive floats of an env's [N][D] block
+  const int ND = N * d.D;
+  for (int i = threadIdx.x; i < ne * ND; i += blockDim.x) {
+    const int le = i / ND, r = i % ND;
+    const int k = r / d.D, f = r % d.D;
+    const float v = obs_elem(d, spos + le * N, sgrid + le * RC, k, f);
+    const int64_t row = next_row ? next_row[e0 + le] : (int64_t)(e0 + le);
+    next_obs[row * next_se + r] = v;
+    if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? d.reset_obs[r] : v;
+  }
+
+  // phase 3: state write-back (initial state for auto-reset envs)
+  for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) {
+    const int le = i / RC;
+    d.grid[(int64_t)e0 * RC + i] = (obs_cur && sdone[le]) ? d.init_grid[i % RC] : sgrid[i];
+  }
+  for (int i = threadIdx.x; i < ne * N; i += blockDim.x) {
+    const int le = i / N;
+    d.pos[(int64_t)e0 * N + i] = (obs_cur && sdone[le]) ? d.init_pos[i % N] : spos[i];
+  }
+}
+
+static size_t step_smem(const EnvDev& d) { return (size_t)EB * d.N * 4 + EB + (size_t)EB * d.R * d.C; }
+
+int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out) {
+  (void)seed;  // the layout is deterministic (ma_gym Checkers resets to a fixed layout)
+  MM_REQUIRE(cfg && out, "env_create: null argument");
+  MM_REQUIRE(n_envs >= 1 && n_envs < (1ll << 31), "env_create: bad n_envs");
+  MM_REQUIRE(cfg->n_agents >= 1 && cfg->n_agents <= 64, "env_create: n_agents must be in [1,64]");
+  const int cols = cfg->cols > 0 ? cfg->cols : 8;
+  MM_REQUIRE(cols >= 3 && cols <= 255, "env_create: cols must be in [3,255]");
+  EnvDev d;
+  d.E = (int)n_envs;
+  d.N = cfg->n_agents;
+  d.R = 3 * ((d.N + 1) / 2);
+  d.C = cols;
+  MM_REQUIRE(d.R <= 255, "env_create: too many agents for the grid");
+  d.full_obs = cfg->full_observable ? 1 : 0;
+  d.D = OBS_LOCAL * (d.full_obs ? d.N : 1);
+  d.max_steps = cfg->max_steps;
+  d.step_cost = cfg->step_cost;
+  d.inv_r = 1.0f / (float)(d.R > 1 ? d.R - 1 : 1);
+  d.inv_c = 1.0f / (float)(d.C > 1 ? d.C - 1 : 1);
+  const int RC = d.R * d.C;
+  std::vector<int8_t> grid(RC, 0);
+  int apples = 0;
+  for (int r = 0; r < d.R; ++r)
+    for (int c = 0; c < d.C - 2; ++c) {
+      grid[r * d.C + c] = ((r + c) % 2 == 0) ? 2 : 1;
+      apples += ((r + c) % 2 == 0);
+    }
+  d.init_apples = apples;
+  std::vector<int32_t> pos(d.N);
+  for (int k = 0; k < d.N; ++k) pos[k] = ((3 * (k / 2) + 2 * (k % 2)) << 8) | (d.C - 2);
+  MM_REQUIRE(step_smem(d) <= 64 * 1024, "env_create: grid too large for LDS staging");
+
+  const size_t E = (size_t)d.E;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  const size_t o_pos = take(E * d.N * 4), o_grid = take(E * RC), o_steps = take(E * 4), o_apples = take(E * 4),
+               o_igrid = take(RC), o_ipos = take(d.N * 4), o_robs = take((size_t)d.N * d.D * 4);
+  void* base = nullptr;
+  MM_HIP_CHECK(hipMalloc(&base, off));
+  char* b = static_cast<char*>(base);
+  d.pos = reinterpret_cast<int32_t*>(b + o_pos);
+  d.grid = reinterpret_cast<int8_t*>(b + o_grid);
+  d.steps = reinterpret_cast<int32_t*>(b + o_steps);
+  d.apples = reinterpret_cast<int32_t*>(b + o_apples);
+  d.init_grid = reinterpret_cast<int8_t*>(b + o_igrid);
+  d.init_pos = reinterpret_cast<int32_t*>(b + o_ipos);
+  d.reset_obs = reinterpret_cast<float*>(b + o_robs);
+  MM_HIP_CHECK(hipMemcpy(b + o_igrid, grid.data(), RC, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(b + o_ipos, pos.data(), d.N * 4, hipMemcpyHostToDevice));
+  mm_env* env = new mm_env;
+  env->d = d;
+  env->alloc = base;
+  const int blocks = (d.E + EB - 1) / EB;
+  const size_t sm = ((d.N * 4 + 15) & ~15) + RC;
+  hipLaunchKernelGGL(env_reset_kernel, dim3(blocks), dim3(256), sm, 0, d, (float*)nullptr, 1);
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    set_error("env_create: reset failed: %s", hipGetErrorString(e));
+    (void)hipFree(base);
+    delete env;
+    return MM_EHIP;
+  }
+  *out = env;
+  return MM_OK;
+}
+
+int env_reset(mm_env* env, float* obs, hipStream_t s) {
+  MM_REQUIRE(env, "env_reset: null env");
+  const EnvDev& d = env->d;
+  const int blocks = (d.E + EB - 1) / EB;
+  const size_t sm = ((d.N * 4 + 15) & ~15) + d.R * d.C;
+  hipLaunchKernelGGL(env_reset_kernel, dim3(blocks), dim3(256), sm, s, d, obs, 0);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int env_step(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
+             float* obs_cur, float* rew, uint8_t* done, hipStream_t s) {
+  MM_REQUIRE(env && act && next_obs && rew && done, "env_step: null argument");
+  const EnvDev& d = env->d;
+  const int blocks = (d.E + EB - 1) / EB;
+  hipLaunchKernelGGL(env_step_kernel, dim3(blocks), dim3(256), step_smem(d), s, d, act, next_obs,
+                     next_se > 0 ? next_se : (int64_t)d.N * d.D, next_row, obs_cur, rew, done);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+const float* env_reset_obs(const mm_env* env) { return env->d.reset_obs; }
+
+}  // namespace mm
+
+extern "C" {
+int mm_env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out) {
+  return mm::env_create(cfg, n_envs, seed, out);
+}
+void mm_env_destroy(mm_env* env) {
+  if (!env) return;
+  (void)hipFree(env->alloc);
+  delete env;
+}
+int mm_env_obs_dim(const mm_env* env) { return env ? env->d.D : -1; }
+int mm_env_grid_shape(const mm_env* env, int32_t* rows, int32_t* cols) {
+  if (!env) return MM_EINVAL;
+  *rows = env->d.R;
+  *cols = env->d.C;
+  return MM_OK;
+}
+int mm_env_reset(mm_env* env, float* obs, mm_stream_t s) { return mm::env_reset(env, obs, (hipStream_t)s); }
+int mm_env_step(mm_env* env, const int32_t* act, float* next_obs, float* obs_cur, float* rew, uint8_t* done,
+                mm_stream_t s) {
+  return mm::env_step(env, act, next_obs, 0, nullptr, obs_cur, rew, done, (hipStream_t)s);
+}
+int mm_env_step_rows(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
+                     float* obs_cur, float* rew, uint8_t* done, mm_stream_t s) {
+  return mm::env_step(env, act, next_obs, next_se, next_row, obs_cur, rew, done, (hipStream_t)s);
+}
+const float* mm_env_reset_obs(const mm_env* env) { return env ? env->d.reset_obs : nullptr; }
+int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples) {
+  if (!env) return MM_EINVAL;
+  const mm::EnvDev& d = env->d;
+  if (hipDeviceSynchronize() != hipSuccess) return MM_EHIP;
+  std::vector<int32_t> p((size_t)d.E * d.N);
+  if (hipMemcpy(p.data(), d.pos, p.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
+  for (size_t i = 0; i < p.size(); ++i) {
+    pos[2 * i] = p[i] >> 8;
+    pos[2 * i + 1] = p[i] & 255;
+  }
+  if (grid && hipMemcpy(grid, d.grid, (size_t)d.E * d.R * d.C, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
+  if (steps && hipMemcpy(steps, d.steps, (size_t)d.E * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
+  if (apples && hipMemcpy(apples, d.apples, (size_t)d.E * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
+  return MM_OK;
+}
+}

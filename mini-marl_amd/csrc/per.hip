@@ -1,0 +1,341 @@
+// Device-resident chunk-level prioritized replay (sum tree) for gfx950.
+//
+// Replaces Prioritized_Experience_Replay + SumTree (vdn/replay_buffer/buffer.py:10-90,
+// vdn/replay_buffer/sumtree.py:8-66; qmix/replay_buffer/per.py:10-81,
+// qmix/replay_buffer/sumtree.py:8-72). Same heap layout (2*cap-1 f64 nodes,
+// leaves at [cap-1, 2cap-2], children 2i+1/2i+2, "s <= left -> go left"),
+// same priority (td+eps)^alpha, same stratified sampling and IS weights, VDN's
+// whole-tree step-weight decay after every sample. The tree never leaves HBM.
+//
+// Batched insert (K chunks from K envs at once — the reference inserts one
+// chunk per call): free slots first in order; the remaining inserts replace the
+// K' smallest existing leaves (ties -> lower slot), assigned in ascending slot
+// order. Equal to the reference's sequential min-eviction whenever no new chunk
+// would itself be evicted within the batch (oracle/sumtree.py add_batch).
+//
+// Every op is ONE single-workgroup launch (1024 threads): K-smallest selection
+// by an 8-pass radix select on the f64 bit patterns with LDS histograms, slot
+// compaction by block prefix sums, then a level-by-level rebuild of the internal
+// nodes. Row indirection: slot_row[slot] is the chunk-store row holding that
+// slot's data; an insert swaps the staging row in and hands the freed row back,
+// so chunk data is never copied.
+#pragma clang fp contract(off)
+#include <vector>
+
+#include "common.h"
+#include "minimarl.h"
+
+struct mm_per {
+  int64_t cap;
+  int32_t flavor;
+  double alpha, beta, eps, step_weight, alpha_inc, beta_inc;
+  int32_t use_step_weight;
+  int64_t n_data;
+  double* tree;       // [2cap-1]
+  int64_t* slot_row;  // [cap]
+  void* alloc;
+};
+
+namespace mm {
+static constexpr int PT = 1024;
+
+__device__ void rebuild_tree(double* tree, int64_t cap) {
+  // internal nodes [0, cap-2]; depth(i) = floor(log2(i+1)); deepest internal level first
+  if (cap <= 1) return;
+  int maxd = 63 - __clzll((unsigned long long)(cap - 1));  // depth of node cap-2
+  for (int dpt = maxd; dpt >= 0; --dpt) {
+    const int64_t lo = (1ll << dpt) - 1, hi = min((1ll << (dpt + 1)) - 2, cap - 2);
+    for (int64_t i = lo + threadIdx.x; i <= hi; i += PT) tree[i] = tree[2 * i + 1] + tree[2 * i + 2];
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+  // exclusive scan of one value per thread over PT threads (Hillis-Steele in LDS)
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int off = 1; off < PT; off <<= 1) {
+    uint32_t t = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  uint32_t incl = sh[threadIdx.x];
+  *total = sh[PT - 1];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ __launch_bounds__(PT) void per_add_kernel(double* tree, int64_t* slot_row, int64_t cap, int64_t n_data,
+                                                     const float* td, int64_t K, double alpha, double eps,
+                                                     int64_t* rows_inout, int64_t* slots_out, int64_t* scratch) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t scan_sh[PT];
+  __shared__ uint64_t s_prefix;
+  __shared__ int64_t s_need;
+  __shared__ uint32_t s_tot;
+  double* leaves = tree + (cap - 1);
+  const int64_t free_n = min(K, cap - n_data);
+  const int64_t rest = K - free_n;
+  int64_t* victims = scratch;  // [rest]
+  if (rest > 0) {
+    // candidates: leaves [0, n_data) (slots filled in this batch are never victims)
+    const int64_t M = n_data;
+    if (threadIdx.x == 0) {
+      s_prefix = 0;
+      s_need = rest;
+    }
+    __syncthreads();
+    // radix select (MSB first, 8 bits per pass) of the rest-th smallest key
+    for (int pass = 7; pass >= 0; --pass) {
+      for (int i = threadIdx.x; i < 256; i += PT) hist[i] = 0;
+      __syncthreads();
+      const int shift = pass * 8;
+      const uint64_t hi_mask = (pass == 7) ? 0ull : (~0ull << (shift + 8));
+      for (int64_t i = threadIdx.x; i < M; i += PT) {
+        const uint64_t key = (uint64_t)__double_as_longlong(leaves[i]);
+        if ((key & hi_mask) == (s_prefix & hi_mask)) atomicAdd(&hist[(key >> shift) & 255], 1u);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int64_t need = s_need;
+        int b = 0;
+        for (; b < 256; ++b) {
+          if ((int64_t)hist[b] >= need) break;
+          need -= hist[b];
+        }
+        s_prefix |= ((uint64_t)b << shift);
+        s_need = need;  // how many with key == threshold are taken (after all passes)
+      }
+      __syncthreads();
+    }
+    const uint64_t T = s_prefix;
+    const int64_t take_eq = s_need;
+    // compaction in ascending slot order: key < T, plus the first take_eq slots with key == T
+    int64_t base_lt = 0, base_eq = 0;
+    for (int64_t c0 = 0; c0 < M; c0 += PT) {
+      const int64_t i = c0 + threadIdx.x;
+      uint64_t key = i < M ? (uint64_t)__double_as_longlong(leaves[i]) : ~0ull;
+      const uint32_t lt = (i < M && key < T) ? 1u : 0u;
+      const uint32_t eq = (i < M && key == T) ? 1u : 0u;
+      uint32_t tot_lt, tot_eq;
+      const uint64_t pre_lt = block_excl_scan(lt, scan_sh, &tot_lt);
+      const uint64_t pre_eq = block_excl_scan(eq, scan_sh, &tot_eq);
+      // the final victim list is sorted by slot: position = (#lt before) + (#eq taken before)
+      const int64_t eq_rank = base_eq + (int64_t)pre_eq;
+      const int64_t lt_rank = base_lt + (int64_t)pre_lt;
+      if (lt || (eq && eq_rank < take_eq)) {
+        const int64_t pos = lt_rank + min(eq_rank, take_eq);
+        victims[pos] = i;
+      }
+      base_lt += tot_lt;
+      base_eq += tot_eq;
+    }
+    (void)s_tot;
+    __syncthreads();
+  }
+  // write priorities, slot assignment, row swap
+  for (int64_t j = threadIdx.x; j < K; j += PT) {
+    const int64_t slot = j < free_n ? n_data + j : victims[j - free_n];
+    const double p = pow((double)td[j] + eps, alpha);
+    leaves[slot] = p;
+    if (slots_out) slots_out[j] = slot;
+    if (rows_inout) {
+      const int64_t old = slot_row[slot];
+      slot_row[slot] = rows_inout[j];
+      rows_inout[j] = old;
+    }
+  }
+  __syncthreads();
+  rebuild_tree(tree, cap);
+}
+
+__global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t cap, int B, const double* fracs,
+                                                        uint64_t seed, uint64_t counter, double beta, double decay,
+                                                        int64_t* nodes_out, int64_t* slots_out, float* is_w) {
+  __shared__ double s_w[PT];
+  __shared__ double s_p[PT];
+  const int64_t n_nodes = 2 * cap - 1;
+  const double total = tree[0];
+  const double seg = total / (double)B;
+  for (int k = threadIdx.x; k < B; k += PT) {
+    double f = fracs ? fracs[k] : (double)(rng_draw(seed, counter, (uint64_t)k, 77) >> 11) * (1.0 / 9007199254740992.0);
+    const double a = seg * (double)k;
+    const double b = seg * (double)(k + 1);
+    double s = a + (b - a) * f;
+    int64_t idx = 0;
+    while (true) {
+      const int64_t left = 2 * idx + 1;
+      if (left >= n_nodes) break;
+      const double lv = tree[left];
+      if (s <= lv) {
+        idx = left;
+      } else {
+        s = s - lv;
+        idx = left + 1;
+      }
+    }
+    nodes_out[k] = idx;
+    if (slots_out) slots_out[k] = idx - (cap - 1);
+    s_p[k] = tree[idx];
+  }
+  __syncthreads();
+  // VDN: whole tree x step_weight after sampling (buffer.py:72-73)
+  if (decay != 1.0) {
+    for (int64_t i = threadIdx.x; i < n_nodes; i += PT) tree[i] = decay * tree[i];
+    __syncthreads();
+  }
+  const double total2 = tree[0];
+  double mx = 0.0;
+  for (int k = threadIdx.x; k < B; k += PT) {
+    const double w = pow((double)cap * (s_p[k] / total2), -beta);
+    s_w[k] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < B; ++k) mx = fmax(mx, s_w[k]);
+    s_p[0] = mx;  // broadcast (priorities no longer needed)
+  }
+  __syncthreads();
+  mx = s_p[0];
+  for (int k = threadIdx.x; k < B; k += PT) is_w[k] = (float)(s_w[k] / mx);
+}
+
+__global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t cap, const int64_t* nodes, const float* td,
+                                                        int B, float alpha, float eps) {
+  for (int k = threadIdx.x; k < B; k += PT) {
+    const int64_t nd = nodes[k];
+    bool last = true;
+    for (int k2 = k + 1; k2 < B; ++k2) last = last && (nodes[k2] != nd);
+    // the reference computes (td + eps) ** alpha on a float32 tensor (vdn/_train.py:230-233)
+    if (last && nd >= cap - 1 && nd < 2 * cap - 1) tree[nd] = (double)powf(td[k] + eps, alpha);
+  }
+  __syncthreads();
+  rebuild_tree(tree, cap);
+}
+
+}  // namespace mm
+
+extern "C" {
+
+int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, double eps, double step_weight,
+                  int32_t use_step_weight, double alpha_inc, double beta_inc, mm_per** out) {
+  MM_REQUIRE(out && capacity >= 1 && capacity < (1ll << 30), "per_create: bad capacity");
+  mm_per* p = new mm_per;
+  p->cap = capacity;
+  p->flavor = flavor;
+  p->alpha = alpha;
+  p->beta = beta;
+  p->eps = eps;
+  p->step_weight = step_weight;
+  p->use_step_weight = use_step_weight && flavor == MM_PER_VDN;
+  p->alpha_inc = alpha_inc;
+  p->beta_inc = beta_inc;
+  p->n_data = 0;
+  const size_t tree_b = ((size_t)(2 * capacity - 1) * 8 + 255) & ~size_t(255);
+  const size_t row_b = ((size_t)capacity * 8 + 255) & ~size_t(255);
+  const size_t scr_b = (size_t)capacity * 8;
+  void* base = nullptr;
+  if (hipMalloc(&base, tree_b + row_b + scr_b) != hipSuccess) {
+    delete p;
+    mm::set_error("per_create: hipMalloc failed");
+    return MM_ENOMEM;
+  }
+  p->alloc = base;
+  p->tree = static_cast<double*>(base);
+  p->slot_row = reinterpret_cast<int64_t*>(static_cast<char*>(base) + tree_b);
+  std::vector<int64_t> rows(capacity);
+  for (int64_t i = 0; i < capacity; ++i) rows[i] = i;  // slot s reserves row s until first filled
+  if (hipMemset(p->tree, 0, tree_b) != hipSuccess ||
+      hipMemcpy(p->slot_row, rows.data(), capacity * 8, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(base);
+    delete p;
+    mm::set_error("per_create: init failed");
+    return MM_EHIP;
+  }
+  *out = p;
+  return MM_OK;
+}
+
+void mm_per_destroy(mm_per* per) {
+  if (!per) return;
+  (void)hipFree(per->alloc);
+  delete per;
+}
+
+static int64_t* per_scratch(mm_per* p) {
+  const size_t tree_b = ((size_t)(2 * p->cap - 1) * 8 + 255) & ~size_t(255);
+  const size_t row_b = ((size_t)p->cap * 8 + 255) & ~size_t(255);
+  return reinterpret_cast<int64_t*>(static_cast<char*>(p->alloc) + tree_b + row_b);
+}
+
+int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s) {
+  MM_REQUIRE(per && (td || k == 0), "per_add: null argument");
+  MM_REQUIRE(k >= 0 && k <= per->cap, "per_add: batch %lld larger than capacity", (long long)k);
+  if (k == 0) return MM_OK;
+  hipLaunchKernelGGL(mm::per_add_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->slot_row, per->cap,
+                     per->n_data, td, k, per->alpha, per->eps, rows_inout, slots_out, per_scratch(per));
+  MM_HIP_CHECK(hipGetLastError());
+  per->n_data = std::min(per->cap, per->n_data + k);
+  return MM_OK;
+}
+
+int mm_per_add_batch(mm_per* per, const float* td, int64_t k, int64_t* slots_out, mm_stream_t s) {
+  return mm_per_insert(per, td, k, nullptr, slots_out, s);
+}
+
+static int per_sample_impl(mm_per* per, int32_t batch, const double* fracs, uint64_t seed, uint64_t counter,
+                           int64_t* nodes_out, int64_t* slots_out, float* is_w, mm_stream_t s) {
+  MM_REQUIRE(per && nodes_out && is_w, "per_sample: null argument");
+  MM_REQUIRE(batch >= 1 && batch <= mm::PT, "per_sample: batch must be in [1, %d]", mm::PT);
+  MM_REQUIRE(per->n_data > 0, "per_sample: empty buffer");
+  // anneal before the draws (buffer.py:53-56)
+  per->alpha = std::min(1.0, per->alpha + per->alpha_inc);
+  per->beta = std::min(1.0, per->beta + per->beta_inc);
+  const double decay = per->use_step_weight ? per->step_weight : 1.0;
+  hipLaunchKernelGGL(mm::per_sample_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->cap, batch,
+                     fracs, seed, counter, per->beta, decay, nodes_out, slots_out, is_w);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_per_sample(mm_per* per, int32_t batch, const double* fracs, int64_t* nodes_out, int64_t* slots_out,
+                  float* is_w, mm_stream_t s) {
+  MM_REQUIRE(fracs, "per_sample: fracs required");
+  return per_sample_impl(per, batch, fracs, 0, 0, nodes_out, slots_out, is_w, s);
+}
+
+int mm_per_sample_rng(mm_per* per, int32_t batch, uint64_t seed, uint64_t counter, int64_t* nodes_out,
+                      int64_t* slots_out, float* is_w, mm_stream_t s) {
+  return per_sample_impl(per, batch, nullptr, seed, counter, nodes_out, slots_out, is_w, s);
+}
+
+int mm_per_update(mm_per* per, const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s) {
+  MM_REQUIRE(per && nodes && td, "per_update: null argument");
+  MM_REQUIRE(batch >= 1 && batch <= 65536, "per_update: bad batch");
+  hipLaunchKernelGGL(mm::per_update_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->cap, nodes, td,
+                     batch, (float)per->alpha, (float)per->eps);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+double* mm_per_tree_ptr(mm_per* per) { return per ? per->tree : nullptr; }
+int64_t* mm_per_slot_rows(mm_per* per) { return per ? per->slot_row : nullptr; }
+int64_t mm_per_size(const mm_per* per) { return per ? per->n_data : -1; }
+int64_t mm_per_capacity(const mm_per* per) { return per ? per->cap : -1; }
+double mm_per_alpha(const mm_per* per) { return per ? per->alpha : 0.0; }
+double mm_per_beta(const mm_per* per) { return per ? per->beta : 0.0; }
+void mm_per_set_size(mm_per* per, int64_t n) {
+  if (per) per->n_data = n;
+}
+int mm_per_copy_tree(mm_per* per, double* dst, mm_stream_t s) {
+  MM_REQUIRE(per && dst, "per_copy_tree: null argument");
+  MM_HIP_CHECK(hipMemcpyAsync(dst, per->tree, (size_t)(2 * per->cap - 1) * 8, hipMemcpyDeviceToDevice, (hipStream_t)s));
+  return MM_OK;
+}
+int mm_per_copy_slot_rows(mm_per* per, int64_t* dst, mm_stream_t s) {
+  MM_REQUIRE(per && dst, "per_copy_slot_rows: null argument");
+  MM_HIP_CHECK(hipMemcpyAsync(dst, per->slot_row, (size_t)per->cap * 8, hipMemcpyDeviceToDevice, (hipStream_t)s));
+  return MM_OK;
+}
+}

@@ -1,0 +1,94 @@
+// Rollout bookkeeping kernels: per-step TD error into the chunk priority and the
+// transition store, plus the chunk-begin obs copy (gfx950).
+//
+// Replaces cal_td_error + the python chunk lists (vdn/_utils.py:44-52,
+// vdn/main.py:140-167, qmix/main.py:183-233): per env e at rollout step t
+//   td = |sum_i r_i + (1-d)*gamma*sum_i max_a Q'_i - sum_i Q_{i,a_i}|   (no xN here)
+//   chunk_td[e] += td; store act/rew/done at slot t of the env's staging row.
+// Chunks span episode boundaries exactly like the reference's global count_step.
+// HBM-bound, one thread per env; sums over agents in registers.
+#include "common.h"
+#include "minimarl.h"
+
+namespace mm {
+
+__global__ __launch_bounds__(256) void td_chunk_kernel(int E, int N, float gamma, const float* __restrict__ rew,
+                                                       const uint8_t* __restrict__ done,
+                                                       const float* __restrict__ q_taken,
+                                                       const float* __restrict__ maxq_next,
+                                                       const int32_t* __restrict__ act, float* __restrict__ chunk_td,
+                                                       int t, int C, uint8_t* __restrict__ s_act,
+                                                       float* __restrict__ s_rew, uint8_t* __restrict__ s_done,
+                                                       const int64_t* __restrict__ rows) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  float sr = 0.f, sq = 0.f, st = 0.f;
+  const int64_t row = rows ? rows[e] : (int64_t)e;
+  for (int k = 0; k < N; ++k) {
+    const int64_t o = (int64_t)e * N + k;
+    const float r = rew[o];
+    sr += r;
+    sq += q_taken[o];
+    st += maxq_next[o];
+    if (s_act) s_act[(row * C + t) * N + k] = (uint8_t)act[o];
+    if (s_rew) s_rew[(row * C + t) * N + k] = r;
+  }
+  const float d = done[e] ? 1.0f : 0.0f;
+  const float td = fabsf(sr + (1.0f - d) * gamma * st - sq);
+  chunk_td[e] = (t == 0 ? 0.0f : chunk_td[e]) + td;
+  if (s_done) s_done[row * C + t] = done[e];
+}
+
+// chunk begin: obs_cur [E][ND] -> store slot 0 of each env's staging row
+__global__ __launch_bounds__(256) void chunk_begin_kernel(int E, int ND, const float* __restrict__ obs_cur,
+                                                          float* __restrict__ s_obs, int64_t row_stride,
+                                                          const int64_t* __restrict__ rows) {
+  const int64_t total = (int64_t)E * ND;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i / ND, r = i % ND;
+    const int64_t row = rows ? rows[e] : e;
+    s_obs[row * row_stride + r] = obs_cur[i];
+  }
+}
+
+}  // namespace mm
+
+extern "C" {
+int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                          const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
+                          int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
+                          uint8_t* store_done, const int64_t* rows, mm_stream_t s) {
+  MM_REQUIRE(rew && done && q_taken && max_q_next && act && chunk_td, "td_chunk_step: null argument");
+  MM_REQUIRE(step_in_chunk >= 0 && step_in_chunk < chunk_len, "td_chunk_step: bad step");
+  if (n_envs <= 0) return MM_OK;
+  const int threads = 256;
+  const int blocks = (int)((n_envs + threads - 1) / threads);
+  hipLaunchKernelGGL(mm::td_chunk_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)s, (int)n_envs, n_agents,
+                     gamma, rew, done, q_taken, max_q_next, act, chunk_td, step_in_chunk, chunk_len, store_act,
+                     store_rew, store_done, rows);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_td_chunk_step(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                     const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
+                     int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
+                     uint8_t* store_done, int64_t store_row0, mm_stream_t s) {
+  (void)store_row0;
+  return mm_td_chunk_step_rows(n_envs, n_agents, gamma, rew, done, q_taken, max_q_next, act, chunk_td,
+                               step_in_chunk, chunk_len, store_act, store_rew, store_done, nullptr, s);
+}
+
+int mm_chunk_begin(int64_t n_envs, int32_t nd, const float* obs_cur, float* store_obs, int64_t row_stride,
+                   const int64_t* rows, mm_stream_t s) {
+  MM_REQUIRE(obs_cur && store_obs, "chunk_begin: null argument");
+  if (n_envs <= 0) return MM_OK;
+  const int threads = 256;
+  const int64_t total = n_envs * nd;
+  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 8192);
+  hipLaunchKernelGGL(mm::chunk_begin_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)s, (int)n_envs, nd,
+                     obs_cur, store_obs, row_stride, rows);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+}

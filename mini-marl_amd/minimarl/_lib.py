@@ -1,0 +1,117 @@
+"""ctypes binding of libminimarl.so (the C ABI declared in include/minimarl.h).
+
+This is the product path: it loads the in-tree HIP library and fails loudly if it
+is missing — there is no CPU fallback anywhere in ``minimarl``.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libminimarl.so")
+
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
+c_vp = ctypes.c_void_p
+
+MM_Q_NONE, MM_Q_ACT, MM_Q_MAX, MM_Q_GATHER = 0, 1, 2, 3
+MM_PER_VDN, MM_PER_QMIX = 0, 1
+
+
+class QnetDims(ctypes.Structure):
+    _fields_ = [("n_agents", c_i32), ("obs_dim", c_i32), ("f1", c_i32), ("g", c_i32), ("h", c_i32),
+                ("n_actions", c_i32)]
+
+
+class QFwdIO(ctypes.Structure):
+    _fields_ = [
+        ("obs", c_vp), ("obs_se", c_i64), ("obs_sa", c_i64), ("obs_off", c_i64),
+        ("obs_row", c_vp), ("reset_obs", c_vp),
+        ("h_in", c_vp), ("hin_se", c_i64), ("hin_sa", c_i64), ("hin_sf", c_i64),
+        ("h_out", c_vp), ("hout_se", c_i64), ("hout_sa", c_i64), ("hout_sf", c_i64),
+        ("reset", c_vp),
+        ("q_out", c_vp), ("q_se", c_i64), ("q_sa", c_i64),
+        ("mode", c_i32),
+        ("epsilon", c_f32), ("u", c_vp), ("rand_act", c_vp), ("seed", c_u64), ("counter", c_u64),
+        ("act_out", c_vp),
+        ("act_in", c_vp), ("act_se", c_i64),
+        ("qsel_out", c_vp),
+    ]
+
+
+class EnvCfg(ctypes.Structure):
+    _fields_ = [("n_agents", c_i32), ("max_steps", c_i32), ("full_observable", c_i32), ("cols", c_i32),
+                ("step_cost", c_f32)]
+
+
+# (name, restype, argtypes) for every entry point of include/minimarl.h (+ extended ones)
+_SIGS = [
+    ("mm_last_error", ctypes.c_char_p, []),
+    ("mm_version", c_i32, []),
+    ("mm_qnet_param_offsets", c_i32, [ctypes.POINTER(QnetDims), ctypes.POINTER(c_i64)]),
+    ("mm_qnet_packed_count", c_i64, [ctypes.POINTER(QnetDims)]),
+    ("mm_qnet_pack", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_vp, c_vp]),
+    ("mm_agent_q_fwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp]),
+    ("mm_agent_q_fwd_simple", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    ("mm_env_create", c_i32, [ctypes.POINTER(EnvCfg), c_i64, c_u64, ctypes.POINTER(c_vp)]),
+    ("mm_env_destroy", None, [c_vp]),
+    ("mm_env_obs_dim", c_i32, [c_vp]),
+    ("mm_env_reset", c_i32, [c_vp, c_vp, c_vp]),
+    ("mm_env_step", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_step_rows", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_reset_obs", c_vp, [c_vp]),
+    ("mm_env_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_grid_shape", c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
+    ("mm_td_chunk_step", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
+                                 c_vp, c_vp, c_i64, c_vp]),
+    ("mm_td_chunk_step_rows", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_chunk_begin", c_i32, [c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    ("mm_per_create", c_i32, [c_i64, c_i32, c_f64, c_f64, c_f64, c_f64, c_i32, c_f64, c_f64,
+                              ctypes.POINTER(c_vp)]),
+    ("mm_per_destroy", None, [c_vp]),
+    ("mm_per_add_batch", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    ("mm_per_insert", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ("mm_per_sample", c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_per_sample_rng", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_per_update", c_i32, [c_vp, c_vp, c_vp, c_i32, c_vp]),
+    ("mm_per_tree_ptr", c_vp, [c_vp]),
+    ("mm_per_slot_rows", c_vp, [c_vp]),
+    ("mm_per_size", c_i64, [c_vp]),
+    ("mm_per_capacity", c_i64, [c_vp]),
+    ("mm_per_alpha", c_f64, [c_vp]),
+    ("mm_per_beta", c_f64, [c_vp]),
+    ("mm_per_set_size", None, [c_vp, c_i64]),
+    ("mm_per_copy_tree", c_i32, [c_vp, c_vp, c_vp]),
+    ("mm_per_copy_slot_rows", c_i32, [c_vp, c_vp, c_vp]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the HIP library. Raises if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"minimarl: HIP library not built ({LIB_PATH}); run `make -C mini-marl_amd` "
+                              "or __graft_entry__.build() — there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in _SIGS:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def symbols():
+    return [s[0] for s in _SIGS]
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().mm_last_error().decode(errors="replace")
+        raise RuntimeError(f"minimarl {what} failed (rc={rc}): {msg}")

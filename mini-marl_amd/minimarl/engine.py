@@ -1,0 +1,146 @@
+"""Device-resident rollout engine: E lockstep envs x N agents, chunked into the PER store.
+
+Replaces the reference runners' per-step loop (vdn/main.py:80-171,
+qmix/main.py:100-237): for every env at every step
+
+  1. behavior Q_Net forward + epsilon-greedy      (sample_action, qmix/_network.py:66-74)
+  2. env step (terminal next obs into the chunk store, auto-reset current obs)
+  3. target Q_Net forward on the next obs -> max_a (qmix/main.py:191-193)
+  4. rollout TD error accumulated into the chunk priority, transition stored
+     (cal_td_error + chunk lists, qmix/_utils.py:86-97, qmix/main.py:204-233)
+  5. every C steps: the E finished chunks go into the prioritized replay at once
+
+Six launches per step, all stream-ordered on one HIP stream, no host sync.
+Hidden states reset at episode ends (the reference re-inits them per episode,
+vdn/main.py:137-138); chunks span episode boundaries like the reference's
+global ``count_step`` (vdn/main.py:151-167).
+
+Chunk store row layout (one chunk per row, ``rows = capacity + E``):
+  obs  [rows, C+1, N, D] f32   slot 0 = s_0, slot t+1 = s'_t (terminal obs at episode ends)
+  act  [rows, C, N] u8, rew [rows, C, N] f32, done [rows, C] u8
+s_t for t >= 1 is s'_{t-1} unless done_{t-1} (then the reset obs). The PER maps
+slot -> row; inserts swap the finished staging rows in and take the evicted
+rows back as the next staging rows (no chunk copy).
+"""
+import ctypes
+
+import torch
+
+from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, check, lib
+from .env import VecEnv
+from .qnet import AgentQNet, ptr, stream_handle
+from .replay import DevicePER
+
+
+class ChunkStore:
+    def __init__(self, rows, chunk, n_agents, obs_dim, device):
+        self.rows, self.C, self.N, self.D = rows, chunk, n_agents, obs_dim
+        self.obs = torch.zeros(rows, chunk + 1, n_agents, obs_dim, device=device)
+        self.act = torch.zeros(rows, chunk, n_agents, dtype=torch.uint8, device=device)
+        self.rew = torch.zeros(rows, chunk, n_agents, device=device)
+        self.done = torch.zeros(rows, chunk, dtype=torch.uint8, device=device)
+        self.row_stride = (chunk + 1) * n_agents * obs_dim
+
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in (self.obs, self.act, self.rew, self.done))
+
+
+class RolloutEngine:
+    def __init__(self, n_envs, n_agents, obs_dim=None, n_actions=5, f1=64, g=32, h=32, chunk=10,
+                 capacity=None, gamma=0.99, max_steps=100, step_cost=-0.01, full_observable=False,
+                 per_flavor="qmix", per_kwargs=None, seed=0, device="cuda"):
+        self.device = torch.device(device)
+        self.E, self.N, self.C = int(n_envs), int(n_agents), int(chunk)
+        self.gamma = float(gamma)
+        self.env = VecEnv(self.E, self.N, max_steps, step_cost, full_observable, device=self.device)
+        self.D = self.env.obs_dim
+        assert obs_dim is None or obs_dim == self.D
+        self.A = n_actions
+        self.behavior = AgentQNet(self.N, self.D, self.A, f1, g, h, self.device, seed=seed)
+        self.target = AgentQNet(self.N, self.D, self.A, f1, g, h, self.device)
+        self.target.copy_from(self.behavior)
+        self.H = h
+        self.capacity = int(capacity or 4 * self.E)
+        self.per = DevicePER(self.capacity, per_flavor, device=self.device, **(per_kwargs or {}))
+        self.store = ChunkStore(self.capacity + self.E, self.C, self.N, self.D, self.device)
+        self.staging = torch.arange(self.capacity, self.capacity + self.E, dtype=torch.int64, device=self.device)
+        E, N, D, H = self.E, self.N, self.D, self.H
+        dev = self.device
+        self.obs_cur = torch.empty(E, N, D, device=dev)
+        self.h = torch.zeros(E, N, H, device=dev)
+        self.ht = torch.zeros(E, N, H, device=dev)
+        self.done_prev = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self.done = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self.act = torch.zeros(E, N, dtype=torch.int32, device=dev)
+        self.qsel = torch.zeros(E, N, device=dev)
+        self.maxq = torch.zeros(E, N, device=dev)
+        self.rew = torch.zeros(E, N, device=dev)
+        self.chunk_td = torch.zeros(E, device=dev)
+        self.t = 0
+        self.seed = int(seed)
+        self.chunks_inserted = 0
+        self._build_io()
+        self.env.reset(self.obs_cur)
+
+    def _build_io(self):
+        E, N, D, H = self.E, self.N, self.D, self.H
+        b = QFwdIO()
+        b.obs, b.obs_se, b.obs_sa = self.obs_cur.data_ptr(), N * D, D
+        b.h_in = b.h_out = self.h.data_ptr()
+        b.hin_se = b.hout_se = N * H
+        b.hin_sa = b.hout_sa = H
+        b.hin_sf = b.hout_sf = 1
+        b.reset = self.done_prev.data_ptr()
+        b.mode = MM_Q_ACT
+        b.act_out, b.qsel_out = self.act.data_ptr(), self.qsel.data_ptr()
+        b.seed = self.seed
+        self.io_b = b
+        t = QFwdIO()
+        # target reads s'_t straight out of the staging rows of the chunk store (gather by row)
+        t.obs, t.obs_se, t.obs_sa = self.store.obs.data_ptr(), self.store.row_stride, D
+        t.obs_row = self.staging.data_ptr()
+        t.reset_obs = self.env.reset_obs_ptr()
+        t.h_in = t.h_out = self.ht.data_ptr()
+        t.hin_se = t.hout_se = N * H
+        t.hin_sa = t.hout_sa = H
+        t.hin_sf = t.hout_sf = 1
+        t.reset = self.done_prev.data_ptr()
+        t.mode = MM_Q_MAX
+        t.qsel_out = self.maxq.data_ptr()
+        self.io_t = t
+
+    def sync_target(self):
+        self.target.copy_from(self.behavior)
+
+    def step(self, epsilon):
+        """One lockstep env step for all E envs (6 launches, no host sync)."""
+        s = stream_handle(self.device)
+        L = lib()
+        c = self.t % self.C
+        ND = self.N * self.D
+        if c == 0:
+            check(L.mm_chunk_begin(self.E, ND, ptr(self.obs_cur), ptr(self.store.obs), self.store.row_stride,
+                                   ptr(self.staging), s), "chunk_begin")
+        self.io_b.epsilon = float(epsilon)
+        self.io_b.counter = self.t
+        self.behavior.forward_io(self.E, self.io_b, s)
+        nxt = ctypes.c_void_p(self.store.obs.data_ptr() + 4 * (c + 1) * ND)
+        check(L.mm_env_step_rows(self.env.handle(), ptr(self.act), nxt, self.store.row_stride, ptr(self.staging),
+                                 ptr(self.obs_cur), ptr(self.rew), ptr(self.done), s), "env_step")
+        self.io_t.obs_off = (c + 1) * ND
+        self.target.forward_io(self.E, self.io_t, s)
+        check(L.mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done), ptr(self.qsel),
+                                      ptr(self.maxq), ptr(self.act), ptr(self.chunk_td), c, self.C,
+                                      ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
+                                      ptr(self.staging), s), "td_chunk")
+        # done of this step resets hidden states at the next step (episode boundary)
+        self.done_prev, self.done = self.done, self.done_prev
+        self.io_b.reset = self.io_t.reset = self.done_prev.data_ptr()
+        if c == self.C - 1:
+            check(L.mm_per_insert(self.per._h, ptr(self.chunk_td), self.E, ptr(self.staging), None, s), "per_insert")
+            self.chunks_inserted += self.E
+        self.t += 1
+
+    def run(self, n_steps, epsilon):
+        for _ in range(n_steps):
+            self.step(epsilon)

@@ -1,0 +1,74 @@
+"""Lockstep checkers gridworld stepped on the GPU (csrc/env.hip).
+
+Stands in for ``gym.make("ma_gym:Checkers-v0", full_observable, max_steps,
+step_cost)`` (vdn/main.py:61-64, qmix/main.py:66-71): E independent envs x N
+agents, obs laid out [env, agent, feat] in HBM. Dynamics spec: oracle/env.py
+(ma_gym itself is absent: parity with it is unpinned).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import EnvCfg, c_i32, c_vp, check, lib
+from .qnet import ptr, stream_handle
+
+
+class VecEnv:
+    def __init__(self, n_envs, n_agents=2, max_steps=100, step_cost=-0.01, full_observable=False, cols=8,
+                 device="cuda"):
+        self.E, self.N = int(n_envs), int(n_agents)
+        self.device = torch.device(device)
+        self.cfg = EnvCfg(self.N, int(max_steps), int(bool(full_observable)), int(cols), float(step_cost))
+        h = c_vp()
+        check(lib().mm_env_create(ctypes.byref(self.cfg), self.E, 0, ctypes.byref(h)), "env_create")
+        self._h = h
+        self.obs_dim = lib().mm_env_obs_dim(h)
+        self.n_actions = 5
+        r, c = c_i32(), c_i32()
+        lib().mm_env_grid_shape(h, ctypes.byref(r), ctypes.byref(c))
+        self.rows, self.cols = r.value, c.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:
+                pass
+            lib().mm_env_destroy(h)
+            self._h = None
+
+    def handle(self):
+        return self._h
+
+    def reset_obs_ptr(self):
+        return lib().mm_env_reset_obs(self._h)
+
+    def reset(self, out=None):
+        out = out if out is not None else torch.empty(self.E, self.N, self.obs_dim, device=self.device)
+        check(lib().mm_env_reset(self._h, ptr(out), stream_handle(self.device)), "env_reset")
+        return out
+
+    def step(self, actions, autoreset=False):
+        """actions [E,N] (int) -> (next_obs [E,N,D] terminal, reward [E,N], done [E] uint8[, obs_cur])."""
+        actions = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
+        assert actions.shape == (self.E, self.N)
+        nxt = torch.empty(self.E, self.N, self.obs_dim, device=self.device)
+        rew = torch.empty(self.E, self.N, device=self.device)
+        done = torch.empty(self.E, dtype=torch.uint8, device=self.device)
+        cur = torch.empty_like(nxt) if autoreset else None
+        check(lib().mm_env_step(self._h, ptr(actions), ptr(nxt), ptr(cur), ptr(rew), ptr(done),
+                                stream_handle(self.device)), "env_step")
+        if autoreset:
+            return nxt, rew, done, cur
+        return nxt, rew, done
+
+    def get_state(self):
+        pos = np.empty((self.E, self.N, 2), np.int32)
+        grid = np.empty((self.E, self.rows, self.cols), np.int8)
+        steps = np.empty(self.E, np.int32)
+        apples = np.empty(self.E, np.int32)
+        check(lib().mm_env_get_state(self._h, pos.ctypes.data, grid.ctypes.data, steps.ctypes.data,
+                                     apples.ctypes.data), "env_get_state")
+        return pos, grid, steps, apples

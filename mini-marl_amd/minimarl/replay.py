@@ -1,0 +1,101 @@
+"""Device-resident prioritized chunk replay (csrc/per.hip).
+
+Mirrors ``Prioritized_Experience_Replay`` (vdn/replay_buffer/buffer.py:10-90,
+qmix/replay_buffer/per.py:10-81): ``collect_sample`` / ``sample`` / ``update`` with
+the sum tree kept in HBM (f64, reference heap layout). Chunk payloads live in a
+``ChunkStore`` (engine.py); this class manages priorities and slot -> row mapping.
+"""
+import ctypes
+
+import torch
+
+from ._lib import MM_PER_QMIX, MM_PER_VDN, c_vp, check, lib
+from .qnet import ptr, stream_handle
+
+
+class DevicePER:
+    def __init__(self, capacity, flavor="vdn", alpha=0.4, beta=0.4, eps=1e-6, step_weight=0.99,
+                 use_step_weight=True, update_alpha_beta=True, max_episodes=30000, update_iter=10,
+                 device="cuda"):
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        fl = MM_PER_VDN if flavor == "vdn" else MM_PER_QMIX
+        if update_alpha_beta:
+            ai = (1 - alpha) / (max_episodes * update_iter)
+            bi = (1 - beta) / (max_episodes * update_iter)
+        else:
+            ai = bi = 0.0
+        h = c_vp()
+        check(lib().mm_per_create(self.capacity, fl, alpha, beta, eps, step_weight, int(use_step_weight), ai, bi,
+                                  ctypes.byref(h)), "per_create")
+        self._h = h
+
+    @classmethod
+    def from_args(cls, args, flavor, device="cuda"):
+        """Build from a reference-style args namespace (buffer_limit, alpha, beta, eps, ...)."""
+        return cls(args.buffer_limit, flavor, args.alpha, args.beta, args.eps, getattr(args, "step_weight", 0.99),
+                   getattr(args, "use_step_weight", flavor == "vdn"), args.update_alpha_beta, args.max_episodes,
+                   args.update_iter, device)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:
+                pass
+            lib().mm_per_destroy(h)
+            self._h = None
+
+    @property
+    def alpha(self):
+        return lib().mm_per_alpha(self._h)
+
+    @property
+    def beta(self):
+        return lib().mm_per_beta(self._h)
+
+    def __len__(self):
+        return int(lib().mm_per_size(self._h))
+
+    def tree(self):
+        """Copy of the sum tree [2*cap-1] f64 (device)."""
+        out = torch.empty(2 * self.capacity - 1, dtype=torch.float64, device=self.device)
+        check(lib().mm_per_copy_tree(self._h, ptr(out), stream_handle(self.device)), "per_copy_tree")
+        return out
+
+    def slot_rows(self):
+        """Copy of the slot -> chunk-store row table [cap] int64 (device)."""
+        out = torch.empty(self.capacity, dtype=torch.int64, device=self.device)
+        check(lib().mm_per_copy_slot_rows(self._h, ptr(out), stream_handle(self.device)), "per_copy_rows")
+        return out
+
+    def slot_rows_ptr(self):
+        return lib().mm_per_slot_rows(self._h)
+
+    def add(self, td, rows_inout=None):
+        """Insert K chunks (td [K] f32 device) -> data slots [K] (int64 device)."""
+        td = td.to(self.device, torch.float32).contiguous()
+        slots = torch.empty(td.numel(), dtype=torch.int64, device=self.device)
+        check(lib().mm_per_insert(self._h, ptr(td), td.numel(), ptr(rows_inout), ptr(slots),
+                                  stream_handle(self.device)), "per_insert")
+        return slots
+
+    def sample(self, batch, fracs=None, seed=0, counter=0):
+        """-> (tree nodes [B], data slots [B], IS weights [B]) all on device."""
+        nodes = torch.empty(batch, dtype=torch.int64, device=self.device)
+        slots = torch.empty(batch, dtype=torch.int64, device=self.device)
+        w = torch.empty(batch, dtype=torch.float32, device=self.device)
+        if fracs is not None:
+            fr = torch.as_tensor(fracs, dtype=torch.float64).to(self.device).contiguous()
+            check(lib().mm_per_sample(self._h, batch, ptr(fr), ptr(nodes), ptr(slots), ptr(w),
+                                      stream_handle(self.device)), "per_sample")
+        else:
+            check(lib().mm_per_sample_rng(self._h, batch, seed, counter, ptr(nodes), ptr(slots), ptr(w),
+                                          stream_handle(self.device)), "per_sample_rng")
+        return nodes, slots, w
+
+    def update(self, nodes, td):
+        td = td.to(self.device, torch.float32).contiguous().view(-1)
+        check(lib().mm_per_update(self._h, ptr(nodes), ptr(td), td.numel(), stream_handle(self.device)),
+              "per_update")

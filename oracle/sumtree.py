@@ -59,7 +59,8 @@ class SumTreeOracle:
 
     def add_batch(self, tds):
         """Batched insert rule of the device engine: free slots first (in order), then the
-        k smallest leaves (ties -> lowest slot) are replaced by the remaining inserts in order.
+        k smallest leaves (ties -> lowest slot), taken in ascending slot order, receive the
+        remaining inserts in order.
         Identical to sequential add() whenever no new priority is among the evicted minima."""
         tds = list(tds)
         slots = []
@@ -72,7 +73,7 @@ class SumTreeOracle:
             if free > 0:
                 leaves[self.n_data:self.n_data + free] = np.inf   # just-filled slots are not victims
             order = np.lexsort((np.arange(self.cap), leaves))
-            slots.extend(int(x) for x in order[:rest])
+            slots.extend(sorted(int(x) for x in order[:rest]))   # victims in ascending slot order
         for slot, td in zip(slots, tds):
             self.tree[slot + self.cap - 1] = self.priority(td)
         self.n_data = min(self.cap, self.n_data + len(tds))

@@ -1,0 +1,220 @@
+"""GPU parity of the rollout hot path (HIP via the C ABI) against the golden vectors and the oracle.
+
+Tolerances (fp32, stated per SURVEY 8c): single-step Q / hidden rtol 1e-5 atol 1e-5
+(exact-f32 MFMA vs MKL summation order); actions exact; env integer state, rewards and
+obs bit-exact; sum-tree f64 rtol 1e-12 (tree rebuild vs incremental propagation),
+IS weights rtol 1e-6.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nets
+from oracle.env import EnvSpec, VecEnvOracle
+from oracle.sumtree import SumTreeOracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _net_from_fixture(fx, style, f1=64, g=32, h=32):
+    from minimarl.qnet import AgentQNet
+    P = nets.agent_from_state(fx, "p.", style)
+    N, F1, D = P["W1"].shape
+    A = P["Wq"].shape[1]
+    net = AgentQNet(N, D, A, f1, g, h, DEV)
+    net.load_reference_state(fx, "p.", style)
+    return net, P
+
+
+@pytest.mark.parametrize("tag,style", [("qmix_n2", "qmix"), ("qmix_n8", "qmix"), ("vdn_n2", "vdn")])
+def test_qnet_forward_golden(golden, tag, style):
+    fx = golden("qnet_" + tag)
+    net, _ = _net_from_fixture(fx, style)
+    q, h = net.forward(torch.tensor(fx["obs"]).to(DEV), torch.tensor(fx["hidden"]).to(DEV))
+    np.testing.assert_allclose(q.cpu().numpy(), fx["q"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(h.cpu().numpy(), fx["next_hidden"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("tag", ["qmix", "vdn"])
+def test_sample_action_golden_same_seed(golden, tag):
+    """The reference-shaped adapter consumes the torch CPU RNG like the reference: equal actions."""
+    from minimarl.qnet import Q_Net, _Space
+    fx = golden("sample_action_" + tag)
+    N, D = fx["obs"].shape[1:]
+    qn = Q_Net([_Space((D,))] * N, [_Space(n=5)] * N)
+    qn.net.load_reference_state(fx, "p.", tag)
+    torch.manual_seed(1234)
+    act, h2, q = qn.sample_action(torch.tensor(fx["obs"]), torch.tensor(fx["hidden"]), float(fx["epsilon"]))
+    np.testing.assert_array_equal(act.cpu().numpy(), fx["action"])
+    np.testing.assert_allclose(q.cpu().numpy(), fx["q"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(h2.cpu().numpy(), fx["next_hidden"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("f1,g,h,n,d,a,e", [(64, 64, 64, 8, 47, 5, 1000), (64, 32, 32, 8, 47, 5, 257),
+                                            (128, 32, 32, 2, 94, 5, 130), (64, 32, 32, 4, 300, 36, 96)])
+def test_qnet_forward_vs_oracle_shapes(f1, g, h, n, d, a, e):
+    from minimarl.qnet import AgentQNet
+    net = AgentQNet(n, d, a, f1, g, h, DEV, seed=3)
+    P = {k: v.detach().cpu().clone() for k, v in net.params().items()}
+    gen = torch.Generator().manual_seed(9)
+    obs = torch.rand(e, n, d, generator=gen)
+    hid = torch.randn(e, n, h, generator=gen) * 0.5
+    q, h2 = net.forward(obs.to(DEV), hid.to(DEV))
+    qo, ho = nets.agent_forward(P, obs, hid)
+    np.testing.assert_allclose(q.cpu().numpy(), qo.numpy(), rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(h2.cpu().numpy(), ho.numpy(), rtol=1e-5, atol=2e-5)
+    # epilogues: max and act(eps=0) == argmax, q_taken == gathered q
+    qmax, _ = net.max_q(obs.to(DEV), hid.to(DEV))
+    np.testing.assert_allclose(qmax.cpu().numpy(), qo.max(2)[0].numpy(), rtol=1e-5, atol=2e-5)
+    act, qsel, _, qd = net.act(obs.to(DEV), hid.to(DEV), 0.0)
+    greedy = qd.cpu().argmax(2)
+    np.testing.assert_array_equal(act.cpu().numpy(), greedy.numpy())
+    np.testing.assert_allclose(qsel.cpu().numpy(), qd.cpu().gather(2, greedy.unsqueeze(-1)).squeeze(-1).numpy())
+
+
+def test_eps_greedy_device_rng_rate():
+    from minimarl.qnet import AgentQNet
+    net = AgentQNet(8, 47, 5, 64, 32, 32, DEV, seed=1)
+    E = 4096
+    obs = torch.rand(E, 8, 47, device=DEV)
+    hid = torch.zeros(E, 8, 32, device=DEV)
+    act, _, _, q = net.act(obs, hid, 0.3, seed=5, counter=11)
+    greedy = q.argmax(2)
+    rand_rows = (act != greedy).any(1).float().mean().item()
+    # a random row differs from greedy with prob 1 - (1/5)^8 ~ 1
+    assert 0.25 < rand_rows < 0.35
+    assert act.min().item() >= 0 and act.max().item() <= 4
+
+
+@pytest.mark.parametrize("n_agents,full_obs", [(2, False), (2, True), (8, False), (3, False)])
+def test_env_bit_exact_vs_oracle(n_agents, full_obs):
+    from minimarl.env import VecEnv
+    E, steps = 300, 230
+    spec = EnvSpec(n_agents, max_steps=100, full_observable=full_obs)
+    ora = VecEnvOracle(spec, E)
+    env = VecEnv(E, n_agents, 100, -0.01, full_obs, device=DEV)
+    obs0 = env.reset()
+    np.testing.assert_array_equal(obs0.cpu().numpy(), ora.observe())
+    rng = np.random.default_rng(4)
+    for t in range(steps):
+        # biased walk towards the fruit so that apples run out in some envs
+        a = np.where(rng.random((E, n_agents)) < 0.6, 1, rng.integers(0, 5, (E, n_agents))).astype(np.int32)
+        nxt, rew, done, cur = env.step(torch.tensor(a), autoreset=True)
+        onxt, orew, odone = ora.step(a)
+        np.testing.assert_array_equal(nxt.cpu().numpy(), onxt)
+        np.testing.assert_array_equal(rew.cpu().numpy(), orew)
+        np.testing.assert_array_equal(done.cpu().numpy().astype(bool), odone)
+        ora.reset_envs(odone)
+        np.testing.assert_array_equal(cur.cpu().numpy(), ora.observe())
+    pos, grid, st, ap = env.get_state()
+    np.testing.assert_array_equal(pos, ora.pos)
+    np.testing.assert_array_equal(grid, ora.grid)
+    np.testing.assert_array_equal(st, ora.steps)
+    np.testing.assert_array_equal(ap, ora.apples)
+
+
+def _per_pair(flavor, cap):
+    from minimarl.replay import DevicePER
+    if flavor == "vdn":
+        kw = dict(alpha=0.4, beta=0.4, eps=1e-6, step_weight=0.99, use_step_weight=True, update_alpha_beta=True,
+                  max_episodes=30000, update_iter=10)
+        o = SumTreeOracle(cap, "vdn", 0.4, 0.4, alpha_inc=0.6 / 300000, beta_inc=0.6 / 300000)
+    else:
+        kw = dict(alpha=0.8, beta=0.2, eps=1e-6, use_step_weight=False, update_alpha_beta=True,
+                  max_episodes=100000, update_iter=10)
+        o = SumTreeOracle(cap, "qmix", 0.8, 0.2, alpha_inc=0.2 / 1e6, beta_inc=0.8 / 1e6)
+    return DevicePER(cap, flavor, device=DEV, **kw), o
+
+
+@pytest.mark.parametrize("flavor", ["vdn", "qmix"])
+def test_per_golden_sequence_single_inserts(golden, flavor):
+    """Replays the reference's own PER op sequence (K=1 inserts) on the device tree."""
+    fx = golden("per_" + flavor)
+    cap, b = int(fx["capacity"]), int(fx["batch"])
+    dev, _ = _per_pair(flavor, cap)
+    for k in range(int(fx["n_ops"])):
+        kind = int(fx[f"op{k}.kind"])
+        if kind == 0:
+            dev.add(torch.tensor([fx[f"op{k}.td"]], dtype=torch.float32))
+        elif kind == 1:
+            nodes, slots, w = dev.sample(b, fracs=fx[f"op{k}.fracs"])
+            np.testing.assert_array_equal(nodes.cpu().numpy(), fx[f"op{k}.idx"])
+            np.testing.assert_allclose(w.cpu().numpy(), fx[f"op{k}.is_weight"].ravel(), rtol=1e-5)
+            last_nodes = nodes
+        else:
+            dev.update(last_nodes, torch.tensor(fx[f"op{k}.td"]))
+        np.testing.assert_allclose(dev.tree().cpu().numpy(), fx[f"op{k}.tree"], rtol=2e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("flavor,cap", [("vdn", 1000), ("qmix", 4099)])
+def test_per_batched_vs_oracle(flavor, cap):
+    dev, ora = _per_pair(flavor, cap)
+    rng = np.random.default_rng(1)
+    for rnd in range(7):
+        td = (rng.random(700) * 3).astype(np.float32)
+        if rnd == 5:
+            td[:50] = td[50]                       # ties
+        slots = dev.add(torch.tensor(td))
+        oslots = ora.add_batch([float(x) for x in td])
+        np.testing.assert_array_equal(slots.cpu().numpy(), oslots)
+        np.testing.assert_allclose(dev.tree().cpu().numpy(), ora.tree, rtol=1e-6, atol=1e-9)
+        fr = rng.random(256)
+        nodes, s2, w = dev.sample(256, fracs=fr)
+        on, os_, _, ow = ora.sample(256, fr)
+        np.testing.assert_array_equal(nodes.cpu().numpy(), on)
+        np.testing.assert_allclose(w.cpu().numpy(), ow, rtol=1e-5)
+        np.testing.assert_allclose(dev.tree().cpu().numpy(), ora.tree, rtol=1e-6, atol=1e-9)
+        newtd = (rng.random(256)).astype(np.float32)
+        dev.update(nodes, torch.tensor(newtd))
+        # oracle: last duplicate wins; priority computed in f32 like the reference
+        for k in range(256):
+            p32 = np.float32((np.float32(newtd[k]) + np.float32(1e-6)) ** np.float32(ora.alpha))
+            ora.tree[on[k]] = float(p32)
+        ora.rebuild()
+        np.testing.assert_allclose(dev.tree().cpu().numpy(), ora.tree, rtol=1e-6, atol=1e-9)
+
+
+def test_rollout_engine_end_to_end_vs_oracle():
+    """Engine transitions (store contents), TD chunk priorities and actions vs an oracle replay."""
+    from minimarl.engine import RolloutEngine
+    E, N, C = 96, 8, 10
+    eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=C, capacity=512, seed=7, device=DEV)
+    P = {k: v.detach().cpu().clone() for k, v in eng.behavior.params().items()}
+    spec = EnvSpec(N, 100)
+    ora = VecEnvOracle(spec, E)
+    obs = torch.tensor(ora.observe())
+    h = torch.zeros(E, N, 64)
+    ht = torch.zeros(E, N, 64)
+    td_chunk = np.zeros(E, np.float64)
+    steps = 2 * C + 3
+    for t in range(steps):
+        rows = eng.staging.cpu().numpy()          # staging rows of this step (swapped at chunk end)
+        eng.step(epsilon=0.2)
+        torch.cuda.synchronize()
+        c = t % C
+        act = eng.store.act[rows, c].cpu().numpy().astype(np.int64)
+        q, h = nets.agent_forward(P, obs, h)
+        greedy = q.argmax(2).numpy()
+        qs = q.gather(2, torch.tensor(act).unsqueeze(-1)).squeeze(-1)
+        # rows where the engine acted greedily must equal the oracle argmax
+        same = (act == greedy).all(1)
+        assert same.mean() > 0.6
+        nxt, rew, done = ora.step(act)
+        np.testing.assert_array_equal(eng.store.obs[rows, c + 1].cpu().numpy(), nxt)
+        np.testing.assert_array_equal(eng.store.rew[rows, c].cpu().numpy(), rew)
+        np.testing.assert_array_equal(eng.store.done[rows, c].cpu().numpy().astype(bool), done)
+        tq, ht = nets.agent_forward(P, torch.tensor(nxt), ht)
+        td = (torch.tensor(rew).sum(1) + (1 - torch.tensor(done, dtype=torch.float32)) * 0.99 * tq.max(2)[0].sum(1)
+              - qs.sum(1)).abs().numpy()
+        td_chunk = td if c == 0 else td_chunk + td
+        np.testing.assert_allclose(eng.chunk_td.cpu().numpy(), td_chunk, rtol=2e-4, atol=2e-4)
+        keep = torch.tensor(~done, dtype=torch.float32).view(E, 1, 1)
+        h, ht = h * keep, ht * keep
+        ora.reset_envs(done)
+        obs = torch.tensor(ora.observe())
+        np.testing.assert_array_equal(eng.obs_cur.cpu().numpy(), obs.numpy())
+    assert len(eng.per) == 2 * E
+    tree = eng.per.tree().cpu().numpy()
+    assert tree[0] > 0
