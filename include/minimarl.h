@@ -65,6 +65,8 @@ typedef struct mm_qfwd_io {
   int32_t* act_out;                                   /* [E,N] chosen actions (ACT) */
   const int32_t* act_in; int64_t act_se;              /* GATHER: act_in[e*act_se + agent] */
   float* qsel_out;                                    /* [E,N]: Q(a_chosen) (ACT/GATHER) or max_a Q (MAX) */
+  /* optional device scalars overriding epsilon / counter (graph-replayable rollouts) */
+  const float* eps_ptr; const uint64_t* counter_ptr;
 } mm_qfwd_io;
 
 int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,

@@ -200,17 +200,19 @@ __global__ __launch_bounds__(256) void agent_q_fwd_kernel(QFwdParams p) {
   }
   int act = bi;
   if (io.mode == MM_Q_ACT) {
+    const float eps = io.eps_ptr ? *io.eps_ptr : io.epsilon;
+    const uint64_t ctr = io.counter_ptr ? *io.counter_ptr : io.counter;
     float u;
     if (io.u) {
       u = valid ? io.u[e] : 1.0f;
     } else {
-      u = rng_uniform(rng_draw(io.seed, io.counter, (uint64_t)e, 0xFFFFFFFFull));
+      u = rng_uniform(rng_draw(io.seed, ctr, (uint64_t)e, 0xFFFFFFFFull));
     }
-    if (u <= io.epsilon) {
+    if (u <= eps) {
       if (io.rand_act) {
         act = valid ? io.rand_act[(int64_t)e * p.N + agent] : 0;
       } else {
-        act = (int)(rng_draw(io.seed ^ 0x5bd1e995ull, io.counter, (uint64_t)e, (uint64_t)agent) % (uint64_t)p.A);
+        act = (int)(rng_draw(io.seed ^ 0x5bd1e995ull, ctr, (uint64_t)e, (uint64_t)agent) % (uint64_t)p.A);
       }
     }
   } else if (io.mode == MM_Q_GATHER) {

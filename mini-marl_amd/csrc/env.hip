@@ -5,11 +5,13 @@
 // dynamics are the build's own spec, defined in oracle/env.py (parity with
 // ma_gym: UNPINNED; parity with oracle/env.py: bit-exact, integer state).
 //
-// Block = 256 threads, EB = 64 envs. Phase 0 stages the block's grids (bytes,
+// Block = 256 threads, EB = 16 envs (E/16 blocks: 256 for 4096 envs). Phase 0 stages the block's grids (bytes,
 // [E][R*C] so the copy is one contiguous coalesced run) and positions in LDS;
 // phase 1 runs the sequential-in-agent-order dynamics one thread per env;
-// phase 2 generates obs [env, agent, feat] with consecutive threads on
-// consecutive floats (coalesced stores); phase 3 writes state back (or the
+// phase 2 generates obs [env, agent, feat]: each thread decodes its feature
+// positions once, then walks the block's envs, so consecutive lanes store
+// consecutive floats (coalesced) with O(1) LDS lookups (grid + occupancy
+// map) per element; phase 3 writes state back (or the
 // initial state for envs that auto-reset).
 #include <vector>
 
@@ -18,7 +20,7 @@
 
 namespace mm {
 static constexpr int OBS_LOCAL = 47;
-static constexpr int EB = 64;
+static constexpr int EB = 16;
 
 struct EnvDev {
   int E, N, R, C, D, max_steps, full_obs, init_apples;
@@ -105,14 +107,18 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int RC = d.R * d.C;
   const int N = d.N;
-  int32_t* spos = reinterpret_cast<int32_t*>(smem);                        // [EB][N]
-  uint8_t* sdone = reinterpret_cast<uint8_t*>(smem + EB * N * 4);          // [EB]
-  int8_t* sgrid = reinterpret_cast<int8_t*>(smem + EB * N * 4 + EB);       // [EB][RC]
+  int32_t* spos = reinterpret_cast<int32_t*>(smem);                       // [EB][N]
+  uint8_t* sdone = reinterpret_cast<uint8_t*>(smem + EB * N * 4);         // [EB]
+  int8_t* sgrid = reinterpret_cast<int8_t*>(smem + EB * N * 4 + EB);      // [EB][RC]
+  uint8_t* socc = reinterpret_cast<uint8_t*>(sgrid + EB * RC);            // [EB][RC] agent id + 1
   const int e0 = blockIdx.x * EB;
   const int ne = min(EB, d.E - e0);
 
-  // phase 0: stage grids and positions (contiguous runs)
-  for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) sgrid[i] = d.grid[(int64_t)e0 * RC + i];
+  // phase 0: stage grids and positions (contiguous runs), clear occupancy
+  for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) {
+    sgrid[i] = d.grid[(int64_t)e0 * RC + i];
+    socc[i] = 0;
+  }
   for (int i = threadIdx.x; i < ne * N; i += blockDim.x) spos[i] = d.pos[(int64_t)e0 * N + i];
   __syncthreads();
 
@@ -148,16 +154,49 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
     d.apples[e] = dn && obs_cur ? d.init_apples : apples;
   }
   __syncthreads();
+  for (int i = threadIdx.x; i < ne * N; i += blockDim.x) {
+    const int le = i / N, p = spos[i];
+    socc[le * RC + (p >> 8) * d.C + (p & 255)] = (uint8_t)(i % N + 1);
+  }
+  __syncthreads();
 
-  // phase 2: obs (terminal next obs), consecutive threads -> consecutive floats of an env's [N][D] block
+  // phase 2: obs. Each thread owns fixed positions r of an env's [N][D] block (decoded once) and
+  // walks the block's envs: a wave stores 64 consecutive floats of one env per instruction.
   const int ND = N * d.D;
-  for (int i = threadIdx.x; i < ne * ND; i += blockDim.x) {
-    const int le = i / ND, r = i % ND;
+  for (int r = threadIdx.x; r < ND; r += blockDim.x) {
     const int k = r / d.D, f = r % d.D;
-    const float v = obs_elem(d, spos + le * N, sgrid + le * RC, k, f);
-    const int64_t row = next_row ? next_row[e0 + le] : (int64_t)(e0 + le);
-    next_obs[row * next_se + r] = v;
-    if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? d.reset_obs[r] : v;
+    const int src = d.full_obs ? f / OBS_LOCAL : k;
+    const int lf = d.full_obs ? f % OBS_LOCAL : f;
+    const int cellid = lf >= 2 ? (lf - 2) / 5 : 0, ch = lf >= 2 ? (lf - 2) % 5 : 0;
+    const int dr = cellid / 3 - 1, dc = cellid % 3 - 1;
+    const float rs = obs_cur ? d.reset_obs[r] : 0.0f;
+    for (int le = 0; le < ne; ++le) {
+      const int p = spos[le * N + src];
+      const int pr = p >> 8, pc = p & 255;
+      float v;
+      if (lf == 0) {
+        v = (float)pr * d.inv_r;
+      } else if (lf == 1) {
+        v = (float)pc * d.inv_c;
+      } else {
+        const int rr = pr + dr, cc = pc + dc;
+        const bool inside = rr >= 0 && rr < d.R && cc >= 0 && cc < d.C;
+        if (!inside) {
+          v = ch == 4 ? 1.0f : 0.0f;
+        } else {
+          const int cell = rr * d.C + cc;
+          const int item = sgrid[le * RC + cell];
+          const int occ = socc[le * RC + cell];
+          v = (ch == 0) ? (item == 1 ? 1.0f : 0.0f)
+            : (ch == 1) ? (item == 2 ? 1.0f : 0.0f)
+            : (ch == 4) ? 0.0f
+            : ((item == 0 && occ != 0 && ((occ - 1) & 1) == ch - 2) ? 1.0f : 0.0f);
+        }
+      }
+      const int64_t row = next_row ? next_row[e0 + le] : (int64_t)(e0 + le);
+      next_obs[row * next_se + r] = v;
+      if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? rs : v;
+    }
   }
 
   // phase 3: state write-back (initial state for auto-reset envs)
@@ -171,7 +210,7 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
   }
 }
 
-static size_t step_smem(const EnvDev& d) { return (size_t)EB * d.N * 4 + EB + (size_t)EB * d.R * d.C; }
+static size_t step_smem(const EnvDev& d) { return (size_t)EB * d.N * 4 + EB + 2 * (size_t)EB * d.R * d.C; }
 
 int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out) {
   (void)seed;  // the layout is deterministic (ma_gym Checkers resets to a fixed layout)

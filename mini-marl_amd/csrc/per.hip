@@ -25,7 +25,17 @@
 #include "common.h"
 #include "minimarl.h"
 
+namespace mm {
+// Mutable PER scalars live in HBM so that inserts / samples / updates are graph-replayable
+// (the host keeps an identical mirror for queries).
+struct PerDev {
+  int64_t n_data;
+  double alpha, beta, alpha_inc, beta_inc;
+};
+}  // namespace mm
+
 struct mm_per {
+  mm::PerDev* st;
   int64_t cap;
   int32_t flavor;
   double alpha, beta, eps, step_weight, alpha_inc, beta_inc;
@@ -66,9 +76,11 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint32_t v, uint32_t* sh, ui
   return incl - v;
 }
 
-__global__ __launch_bounds__(PT) void per_add_kernel(double* tree, int64_t* slot_row, int64_t cap, int64_t n_data,
-                                                     const float* td, int64_t K, double alpha, double eps,
+__global__ __launch_bounds__(PT) void per_add_kernel(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
+                                                     const float* td, int64_t K, double eps,
                                                      int64_t* rows_inout, int64_t* slots_out, int64_t* scratch) {
+  const int64_t n_data = st->n_data;
+  const double alpha = st->alpha;
   __shared__ uint32_t hist[256];
   __shared__ uint32_t scan_sh[PT];
   __shared__ uint64_t s_prefix;
@@ -148,11 +160,20 @@ __global__ __launch_bounds__(PT) void per_add_kernel(double* tree, int64_t* slot
   }
   __syncthreads();
   rebuild_tree(tree, cap);
+  if (threadIdx.x == 0) st->n_data = min(cap, n_data + K);
 }
 
 __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t cap, int B, const double* fracs,
-                                                        uint64_t seed, uint64_t counter, double beta, double decay,
+                                                        uint64_t seed, uint64_t counter, PerDev* st, double decay,
                                                         int64_t* nodes_out, int64_t* slots_out, float* is_w) {
+  // anneal alpha / beta before the draws (buffer.py:53-56)
+  const double alpha = fmin(1.0, st->alpha + st->alpha_inc);
+  const double beta = fmin(1.0, st->beta + st->beta_inc);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st->alpha = alpha;
+    st->beta = beta;
+  }
   __shared__ double s_w[PT];
   __shared__ double s_p[PT];
   const int64_t n_nodes = 2 * cap - 1;
@@ -202,7 +223,8 @@ __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t ca
 }
 
 __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t cap, const int64_t* nodes, const float* td,
-                                                        int B, float alpha, float eps) {
+                                                        int B, const PerDev* st, float eps) {
+  const float alpha = (float)st->alpha;
   for (int k = threadIdx.x; k < B; k += PT) {
     const int64_t nd = nodes[k];
     bool last = true;
@@ -236,18 +258,21 @@ int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, d
   const size_t row_b = ((size_t)capacity * 8 + 255) & ~size_t(255);
   const size_t scr_b = (size_t)capacity * 8;
   void* base = nullptr;
-  if (hipMalloc(&base, tree_b + row_b + scr_b) != hipSuccess) {
+  if (hipMalloc(&base, tree_b + row_b + scr_b + 256) != hipSuccess) {
     delete p;
     mm::set_error("per_create: hipMalloc failed");
     return MM_ENOMEM;
   }
   p->alloc = base;
   p->tree = static_cast<double*>(base);
+  p->st = reinterpret_cast<mm::PerDev*>(static_cast<char*>(base) + tree_b + row_b + scr_b);
+  const mm::PerDev st0 = {0, alpha, beta, alpha_inc, beta_inc};
   p->slot_row = reinterpret_cast<int64_t*>(static_cast<char*>(base) + tree_b);
   std::vector<int64_t> rows(capacity);
   for (int64_t i = 0; i < capacity; ++i) rows[i] = i;  // slot s reserves row s until first filled
   if (hipMemset(p->tree, 0, tree_b) != hipSuccess ||
-      hipMemcpy(p->slot_row, rows.data(), capacity * 8, hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(p->slot_row, rows.data(), capacity * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(p->st, &st0, sizeof(st0), hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipFree(base);
     delete p;
     mm::set_error("per_create: init failed");
@@ -274,7 +299,7 @@ int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, 
   MM_REQUIRE(k >= 0 && k <= per->cap, "per_add: batch %lld larger than capacity", (long long)k);
   if (k == 0) return MM_OK;
   hipLaunchKernelGGL(mm::per_add_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->slot_row, per->cap,
-                     per->n_data, td, k, per->alpha, per->eps, rows_inout, slots_out, per_scratch(per));
+                     per->st, td, k, per->eps, rows_inout, slots_out, per_scratch(per));
   MM_HIP_CHECK(hipGetLastError());
   per->n_data = std::min(per->cap, per->n_data + k);
   return MM_OK;
@@ -294,7 +319,7 @@ static int per_sample_impl(mm_per* per, int32_t batch, const double* fracs, uint
   per->beta = std::min(1.0, per->beta + per->beta_inc);
   const double decay = per->use_step_weight ? per->step_weight : 1.0;
   hipLaunchKernelGGL(mm::per_sample_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->cap, batch,
-                     fracs, seed, counter, per->beta, decay, nodes_out, slots_out, is_w);
+                     fracs, seed, counter, per->st, decay, nodes_out, slots_out, is_w);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -314,7 +339,7 @@ int mm_per_update(mm_per* per, const int64_t* nodes, const float* td, int32_t ba
   MM_REQUIRE(per && nodes && td, "per_update: null argument");
   MM_REQUIRE(batch >= 1 && batch <= 65536, "per_update: bad batch");
   hipLaunchKernelGGL(mm::per_update_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->cap, nodes, td,
-                     batch, (float)per->alpha, (float)per->eps);
+                     batch, per->st, (float)per->eps);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -325,8 +350,13 @@ int64_t mm_per_size(const mm_per* per) { return per ? per->n_data : -1; }
 int64_t mm_per_capacity(const mm_per* per) { return per ? per->cap : -1; }
 double mm_per_alpha(const mm_per* per) { return per ? per->alpha : 0.0; }
 double mm_per_beta(const mm_per* per) { return per ? per->beta : 0.0; }
+void mm_per_set_size_host(mm_per* per, int64_t n) {
+  if (per) per->n_data = n;  // host mirror only (device state advanced by graph-replayed inserts)
+}
 void mm_per_set_size(mm_per* per, int64_t n) {
-  if (per) per->n_data = n;
+  if (!per) return;
+  per->n_data = n;
+  (void)hipMemcpy(&per->st->n_data, &n, sizeof(n), hipMemcpyHostToDevice);
 }
 int mm_per_copy_tree(mm_per* per, double* dst, mm_stream_t s) {
   MM_REQUIRE(per && dst, "per_copy_tree: null argument");

@@ -19,8 +19,10 @@ __global__ __launch_bounds__(256) void td_chunk_kernel(int E, int N, float gamma
                                                        const int32_t* __restrict__ act, float* __restrict__ chunk_td,
                                                        int t, int C, uint8_t* __restrict__ s_act,
                                                        float* __restrict__ s_rew, uint8_t* __restrict__ s_done,
-                                                       const int64_t* __restrict__ rows) {
+                                                       const int64_t* __restrict__ rows,
+                                                       uint64_t* __restrict__ counter) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (counter && e == 0) *counter += 1;  // rollout step counter (RNG stream) read by the next step
   if (e >= E) return;
   float sr = 0.f, sq = 0.f, st = 0.f;
   const int64_t row = rows ? rows[e] : (int64_t)e;
@@ -57,7 +59,7 @@ extern "C" {
 int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                           const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
                           int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
-                          uint8_t* store_done, const int64_t* rows, mm_stream_t s) {
+                          uint8_t* store_done, const int64_t* rows, uint64_t* counter, mm_stream_t s) {
   MM_REQUIRE(rew && done && q_taken && max_q_next && act && chunk_td, "td_chunk_step: null argument");
   MM_REQUIRE(step_in_chunk >= 0 && step_in_chunk < chunk_len, "td_chunk_step: bad step");
   if (n_envs <= 0) return MM_OK;
@@ -65,7 +67,7 @@ int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const f
   const int blocks = (int)((n_envs + threads - 1) / threads);
   hipLaunchKernelGGL(mm::td_chunk_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)s, (int)n_envs, n_agents,
                      gamma, rew, done, q_taken, max_q_next, act, chunk_td, step_in_chunk, chunk_len, store_act,
-                     store_rew, store_done, rows);
+                     store_rew, store_done, rows, counter);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -76,7 +78,7 @@ int mm_td_chunk_step(int64_t n_envs, int32_t n_agents, float gamma, const float*
                      uint8_t* store_done, int64_t store_row0, mm_stream_t s) {
   (void)store_row0;
   return mm_td_chunk_step_rows(n_envs, n_agents, gamma, rew, done, q_taken, max_q_next, act, chunk_td,
-                               step_in_chunk, chunk_len, store_act, store_rew, store_done, nullptr, s);
+                               step_in_chunk, chunk_len, store_act, store_rew, store_done, nullptr, nullptr, s);
 }
 
 int mm_chunk_begin(int64_t n_envs, int32_t nd, const float* obs_cur, float* store_obs, int64_t row_stride,

@@ -38,6 +38,7 @@ class QFwdIO(ctypes.Structure):
         ("act_out", c_vp),
         ("act_in", c_vp), ("act_se", c_i64),
         ("qsel_out", c_vp),
+        ("eps_ptr", c_vp), ("counter_ptr", c_vp),
     ]
 
 
@@ -67,7 +68,7 @@ _SIGS = [
     ("mm_td_chunk_step", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                                  c_vp, c_vp, c_i64, c_vp]),
     ("mm_td_chunk_step_rows", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
-                                      c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_chunk_begin", c_i32, [c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
     ("mm_per_create", c_i32, [c_i64, c_i32, c_f64, c_f64, c_f64, c_f64, c_i32, c_f64, c_f64,
                               ctypes.POINTER(c_vp)]),
@@ -84,6 +85,7 @@ _SIGS = [
     ("mm_per_alpha", c_f64, [c_vp]),
     ("mm_per_beta", c_f64, [c_vp]),
     ("mm_per_set_size", None, [c_vp, c_i64]),
+    ("mm_per_set_size_host", None, [c_vp, c_i64]),
     ("mm_per_copy_tree", c_i32, [c_vp, c_vp, c_vp]),
     ("mm_per_copy_slot_rows", c_i32, [c_vp, c_vp, c_vp]),
 ]

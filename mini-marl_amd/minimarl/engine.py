@@ -76,6 +76,10 @@ class RolloutEngine:
         self.maxq = torch.zeros(E, N, device=dev)
         self.rew = torch.zeros(E, N, device=dev)
         self.chunk_td = torch.zeros(E, device=dev)
+        self.eps_dev = torch.zeros(1, device=dev)
+        self.counter_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # rollout step (RNG stream)
+        self._eps_host = None
+        self.graph = None
         self.t = 0
         self.seed = int(seed)
         self.chunks_inserted = 0
@@ -94,6 +98,7 @@ class RolloutEngine:
         b.mode = MM_Q_ACT
         b.act_out, b.qsel_out = self.act.data_ptr(), self.qsel.data_ptr()
         b.seed = self.seed
+        b.eps_ptr, b.counter_ptr = self.eps_dev.data_ptr(), self.counter_dev.data_ptr()
         self.io_b = b
         t = QFwdIO()
         # target reads s'_t straight out of the staging rows of the chunk store (gather by row)
@@ -112,8 +117,18 @@ class RolloutEngine:
     def sync_target(self):
         self.target.copy_from(self.behavior)
 
-    def step(self, epsilon):
-        """One lockstep env step for all E envs (6 launches, no host sync)."""
+    def set_epsilon(self, epsilon):
+        if epsilon != self._eps_host:
+            self.eps_dev.fill_(float(epsilon))
+            self._eps_host = epsilon
+
+    def step(self, epsilon=None):
+        """One lockstep env step for all E envs (<= 6 launches, no host sync)."""
+        if epsilon is not None:
+            self.set_epsilon(epsilon)
+        self._step_launch()
+
+    def _step_launch(self):
         s = stream_handle(self.device)
         L = lib()
         c = self.t % self.C
@@ -121,8 +136,6 @@ class RolloutEngine:
         if c == 0:
             check(L.mm_chunk_begin(self.E, ND, ptr(self.obs_cur), ptr(self.store.obs), self.store.row_stride,
                                    ptr(self.staging), s), "chunk_begin")
-        self.io_b.epsilon = float(epsilon)
-        self.io_b.counter = self.t
         self.behavior.forward_io(self.E, self.io_b, s)
         nxt = ctypes.c_void_p(self.store.obs.data_ptr() + 4 * (c + 1) * ND)
         check(L.mm_env_step_rows(self.env.handle(), ptr(self.act), nxt, self.store.row_stride, ptr(self.staging),
@@ -132,7 +145,7 @@ class RolloutEngine:
         check(L.mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done), ptr(self.qsel),
                                       ptr(self.maxq), ptr(self.act), ptr(self.chunk_td), c, self.C,
                                       ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
-                                      ptr(self.staging), s), "td_chunk")
+                                      ptr(self.staging), ptr(self.counter_dev), s), "td_chunk")
         # done of this step resets hidden states at the next step (episode boundary)
         self.done_prev, self.done = self.done, self.done_prev
         self.io_b.reset = self.io_t.reset = self.done_prev.data_ptr()
@@ -140,6 +153,40 @@ class RolloutEngine:
             check(L.mm_per_insert(self.per._h, ptr(self.chunk_td), self.E, ptr(self.staging), None, s), "per_insert")
             self.chunks_inserted += self.E
         self.t += 1
+
+    # ------------------------------------------------------------------ HIP graph replay
+    def graph_steps(self):
+        return self.C if self.C % 2 == 0 else 2 * self.C
+
+    def capture(self):
+        """Capture one chunk of steps (C launches-groups; 2C if C is odd so the done/done_prev
+        ping-pong returns to its start) into a HIP graph. Must start at a chunk boundary."""
+        assert self.t % self.C == 0, "capture must start at a chunk boundary"
+        self.behavior.pack()
+        self.target.pack()
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        t0, ins0, n0 = self.t, self.chunks_inserted, len(self.per)
+        with torch.cuda.graph(g):
+            for _ in range(self.graph_steps()):
+                self._step_launch()
+        # capture does not execute: rewind the host bookkeeping (PER fill-count mirror too)
+        self.t, self.chunks_inserted = t0, ins0
+        lib().mm_per_set_size(self.per._h, n0)
+        self.graph = g
+        return g
+
+    def run_graph(self, epsilon=None):
+        """Replay one captured chunk (graph_steps() env steps)."""
+        if epsilon is not None:
+            self.set_epsilon(epsilon)
+        if self.graph is None:
+            self.capture()
+        self.graph.replay()
+        n = self.graph_steps()
+        self.t += n
+        self.chunks_inserted += self.E * (n // self.C)
+        self.per.n_mirror_add(self.E * (n // self.C))
 
     def run(self, n_steps, epsilon):
         for _ in range(n_steps):

@@ -58,6 +58,10 @@ class DevicePER:
     def __len__(self):
         return int(lib().mm_per_size(self._h))
 
+    def n_mirror_add(self, k):
+        """Keep the host mirror of the fill count in step after graph-replayed inserts."""
+        lib().mm_per_set_size_host(self._h, min(self.capacity, len(self) + int(k)))
+
     def tree(self):
         """Copy of the sum tree [2*cap-1] f64 (device)."""
         out = torch.empty(2 * self.capacity - 1, dtype=torch.float64, device=self.device)
