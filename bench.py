@@ -141,13 +141,13 @@ def main():
     value = steps * E * N * world / elapsed
 
     # roofline of the dominant kernel: the fused agent Q forward (behavior launch of a step)
-    fwd = lambda: eng.behavior.forward_io(E, eng.io_b)  # noqa: E731
-    t_fwd = time_kernel(fwd)
-    flops = qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
+    # (one launch = target net on s'_t + behavior net on s_{t+1}: 2 nets x E x N agent-steps)
+    t_fwd = time_kernel(eng.fused_forward)
+    flops = 2 * qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
     achieved = flops / t_fwd / 1e12
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                "kernel": "agent_q_fwd_kernel<64,64,64,1>", "kernel_us": round(t_fwd * 1e6, 2),
+                "kernel": "agent_q_fwd_kernel<64,64,64,1> (dual: target+behavior)", "kernel_us": round(t_fwd * 1e6, 2),
                 "flop_per_launch": flops}
 
     cpu = None

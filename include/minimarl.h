@@ -72,6 +72,10 @@ typedef struct mm_qfwd_io {
 int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,
                    mm_stream_t s);
 
+/* Two nets of the same dims in ONE launch (e.g. target fwd of step t + behavior fwd of step t+1). */
+int mm_agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
+                    const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
+
 /* Survey-style convenience entry: contiguous obs [E,N,D], hidden [E,N,H] -> q [E,N,A], h_out [E,N,H]. */
 int mm_agent_q_fwd_simple(const mm_qnet_dims* d, const float* packed, const float* obs, const float* h,
                           float* q, float* h_out, int64_t n_envs, mm_stream_t s);

@@ -24,9 +24,10 @@ struct QFwdParams {
   QnetGeo g;
   const float* packed;
   int E, N, D, A;
+  int nblocks;  // blocks of this net inside a (possibly dual) launch
 };
 
-__device__ __forceinline__ void load_frag(const float* base, int lane, float (&a)[16]) {
+__device__ __forceinline__ void load_frag(const float* __restrict__ base, int lane, float (&a)[16]) {
   const float4* p = reinterpret_cast<const float4*>(base + lane * 16);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -38,7 +39,7 @@ __device__ __forceinline__ void load_frag(const float* base, int lane, float (&a
   }
 }
 
-__device__ __forceinline__ f32x16 load_bias(const float* base, int hh) {
+__device__ __forceinline__ f32x16 load_bias(const float* __restrict__ base, int hh) {
   const float4* p = reinterpret_cast<const float4*>(base + hh * 16);
   f32x16 r;
 #pragma unroll
@@ -52,31 +53,53 @@ __device__ __forceinline__ f32x16 load_bias(const float* base, int hh) {
   return r;
 }
 
-// acc += W[rb-block] * X, X given as KB k-blocks of D-layout registers.
-template <int KB>
-__device__ __forceinline__ void mma_layer_block(const float* wl, int rb, const f32x16 (&x)[KB], int lane, f32x16& acc) {
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    float a[16];
-    load_frag(wl + (int64_t)(rb * KB + kb) * 1024, lane, a);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc = mfma32(a[s], x[kb][s], acc);
+// Post-layer-1 weight fragments in consumption order (compile-time index -> packed offset):
+//   L2 (rb < RB2, kb < RB1); per hidden block hb: Wih r,z,n (kb < RB2), Whh r,z,n (kb < HB); Q (ab, kb < HB).
+template <int F1, int G, int H, int AB>
+struct Sched {
+  static constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
+  static constexpr int NF2 = RB2 * RB1, PERHB = 3 * RB2 + 3 * HB, NFG = HB * PERHB, NFQ = AB * HB;
+  static constexpr int NF = NF2 + NFG + NFQ;
+  __device__ static __forceinline__ int64_t off(const QnetGeo& g, int i) {
+    if (i < NF2) return g.off_l2 + (int64_t)((i / RB1) * RB1 + i % RB1) * 1024;
+    i -= NF2;
+    if (i < NFG) {
+      const int hb = i / PERHB;
+      int r = i % PERHB;
+      if (r < 3 * RB2) return g.off_ih + (int64_t)(((r / RB2) * HB + hb) * RB2 + r % RB2) * 1024;
+      r -= 3 * RB2;
+      return g.off_hh + (int64_t)(((r / HB) * HB + hb) * HB + r % HB) * 1024;
+    }
+    i -= NFG;
+    return g.off_q + (int64_t)((i / HB) * HB + i % HB) * 1024;
   }
-}
+};
 
 template <int F1, int G, int H, int AB>
-__global__ __launch_bounds__(256) void agent_q_fwd_kernel(QFwdParams p) {
-  constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
+__device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int bid) {
+  using S = Sched<F1, G, H, AB>;
+  constexpr int RB1 = S::RB1, RB2 = S::RB2, HB = S::HB, NF = S::NF;
   const int lane = threadIdx.x & 63;
   const int j = lane & 31, hh = lane >> 5;
-  const int agent = blockIdx.x % p.N;
-  const int tile = blockIdx.x / p.N;
+  const int agent = bid % p.N;
+  const int tile = bid / p.N;
   const int e = tile * 128 + (threadIdx.x >> 6) * 32 + j;
   const bool valid = e < p.E;
   const mm_qfwd_io& io = p.io;
-  const float* W = p.packed + (int64_t)agent * p.g.agent_stride;
+  const float* __restrict__ W = p.packed + (int64_t)agent * p.g.agent_stride;
 
-  // ---- layer 1: x1 = ReLU(W1 o + b1), K = D streamed in 32-wide k-blocks
+  // fragment pipeline (prefetch distance 1): nxt holds the next fragment of the schedule
+  float cur[16], nxt[16];
+  load_frag(W + S::off(p.g, 0), lane, nxt);
+  auto consume = [&](int i, const f32x16& x, f32x16& acc) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) cur[s] = nxt[s];
+    if (i + 1 < NF) load_frag(W + S::off(p.g, i + 1), lane, nxt);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = mfma32(cur[s], x[s], acc);
+  };
+
+  // ---- layer 1: x1 = ReLU(W1 o + b1), K = D streamed in 32-wide k-blocks (next k-block prefetched)
   const float* orow = nullptr;
   if (valid) {
     const int64_t r = io.obs_row ? io.obs_row[e] : (int64_t)e;
@@ -86,20 +109,36 @@ __global__ __launch_bounds__(256) void agent_q_fwd_kernel(QFwdParams p) {
   f32x16 x1[RB1];
 #pragma unroll
   for (int rb = 0; rb < RB1; ++rb) x1[rb] = load_bias(W + p.g.off_b1 + rb * 32, hh);
+  float xb[16], xn[16];
+  float fa[RB1][16], fn[RB1][16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int k = kperm(s, hh);
+    xn[s] = (valid && k < p.D) ? orow[k] : 0.0f;
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB1; ++rb) load_frag(W + p.g.off_l1 + (int64_t)(rb * p.g.KD) * 1024, lane, fn[rb]);
   for (int kb = 0; kb < p.g.KD; ++kb) {
-    float xb[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int k = kb * 32 + kperm(s, hh);
-      xb[s] = (valid && k < p.D) ? orow[k] : 0.0f;
+    for (int s = 0; s < 16; ++s) xb[s] = xn[s];
+#pragma unroll
+    for (int rb = 0; rb < RB1; ++rb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) fa[rb][s] = fn[rb][s];
+    if (kb + 1 < p.g.KD) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int k = (kb + 1) * 32 + kperm(s, hh);
+        xn[s] = (valid && k < p.D) ? orow[k] : 0.0f;
+      }
+#pragma unroll
+      for (int rb = 0; rb < RB1; ++rb)
+        load_frag(W + p.g.off_l1 + (int64_t)(rb * p.g.KD + kb + 1) * 1024, lane, fn[rb]);
     }
 #pragma unroll
-    for (int rb = 0; rb < RB1; ++rb) {
-      float a[16];
-      load_frag(W + p.g.off_l1 + (int64_t)(rb * p.g.KD + kb) * 1024, lane, a);
+    for (int rb = 0; rb < RB1; ++rb)
 #pragma unroll
-      for (int s = 0; s < 16; ++s) x1[rb] = mfma32(a[s], xb[s], x1[rb]);
-    }
+      for (int s = 0; s < 16; ++s) x1[rb] = mfma32(fa[rb][s], xb[s], x1[rb]);
   }
 #pragma unroll
   for (int rb = 0; rb < RB1; ++rb)
@@ -111,7 +150,8 @@ __global__ __launch_bounds__(256) void agent_q_fwd_kernel(QFwdParams p) {
 #pragma unroll
   for (int rb = 0; rb < RB2; ++rb) {
     x2[rb] = load_bias(W + p.g.off_b2 + rb * 32, hh);
-    mma_layer_block<RB1>(W + p.g.off_l2, rb, x1, lane, x2[rb]);
+#pragma unroll
+    for (int kb = 0; kb < RB1; ++kb) consume(rb * RB1 + kb, x1[kb], x2[rb]);
 #pragma unroll
     for (int s = 0; s < 16; ++s) x2[rb][s] = fmaxf(x2[rb][s], 0.0f);
   }
@@ -131,16 +171,23 @@ __global__ __launch_bounds__(256) void agent_q_fwd_kernel(QFwdParams p) {
   f32x16 h1[HB];
 #pragma unroll
   for (int hb = 0; hb < HB; ++hb) {
+    const int base = S::NF2 + hb * S::PERHB;
     f32x16 ar = load_bias(W + p.g.off_brz + hb * 32, hh);
     f32x16 az = load_bias(W + p.g.off_brz + (HB + hb) * 32, hh);
     f32x16 anx = load_bias(W + p.g.off_bin + hb * 32, hh);
     f32x16 anh = load_bias(W + p.g.off_bhn + hb * 32, hh);
-    mma_layer_block<RB2>(W + p.g.off_ih, hb, x2, lane, ar);
-    mma_layer_block<RB2>(W + p.g.off_ih, HB + hb, x2, lane, az);
-    mma_layer_block<RB2>(W + p.g.off_ih, 2 * HB + hb, x2, lane, anx);
-    mma_layer_block<HB>(W + p.g.off_hh, hb, h0, lane, ar);
-    mma_layer_block<HB>(W + p.g.off_hh, HB + hb, h0, lane, az);
-    mma_layer_block<HB>(W + p.g.off_hh, 2 * HB + hb, h0, lane, anh);
+#pragma unroll
+    for (int kb = 0; kb < RB2; ++kb) consume(base + kb, x2[kb], ar);
+#pragma unroll
+    for (int kb = 0; kb < RB2; ++kb) consume(base + RB2 + kb, x2[kb], az);
+#pragma unroll
+    for (int kb = 0; kb < RB2; ++kb) consume(base + 2 * RB2 + kb, x2[kb], anx);
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) consume(base + 3 * RB2 + kb, h0[kb], ar);
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) consume(base + 3 * RB2 + HB + kb, h0[kb], az);
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) consume(base + 3 * RB2 + 2 * HB + kb, h0[kb], anh);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const float r = sigmoidf_(ar[s]);
@@ -164,7 +211,8 @@ __global__ __launch_bounds__(256) void agent_q_fwd_kernel(QFwdParams p) {
 #pragma unroll
   for (int ab = 0; ab < AB; ++ab) {
     qa[ab] = load_bias(W + p.g.off_bq + ab * 32, hh);
-    mma_layer_block<HB>(W + p.g.off_q, ab, h1, lane, qa[ab]);
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) consume(S::NF2 + S::NFG + ab * HB + kb, h1[kb], qa[ab]);
   }
   if (valid && io.q_out) {
     float* qrow = io.q_out + (int64_t)e * io.q_se + (int64_t)agent * io.q_sa;
@@ -230,6 +278,18 @@ __global__ __launch_bounds__(256) void agent_q_fwd_kernel(QFwdParams p) {
     if (io.act_out && io.mode == MM_Q_ACT) io.act_out[o] = act;
     if (io.qsel_out) io.qsel_out[o] = qsel;
   }
+}
+
+// One launch serves one or two nets (e.g. the target net on s'_t and the behavior net on
+// s_{t+1} of the next rollout step): blocks [0, p0.nblocks) run net 0, the rest net 1.
+// Two waves per SIMD (launch_bounds 256 x 2 blocks/CU) so one wave's fragment loads hide
+// under the other's MFMAs.
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(256, (F1 > 64 ? 1 : 2)) void agent_q_fwd_kernel(QFwdParams p0, QFwdParams p1) {
+  if ((int)blockIdx.x < p0.nblocks)
+    agent_q_fwd_body<F1, G, H, AB>(p0, blockIdx.x);
+  else
+    agent_q_fwd_body<F1, G, H, AB>(p1, blockIdx.x - p0.nblocks);
 }
 
 // ---------------------------------------------------------------- packing
@@ -299,38 +359,60 @@ int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStre
 }
 
 template <int F1, int G, int H, int AB>
-static int launch_fwd(const QFwdParams& p, hipStream_t s) {
-  const int tiles = (p.E + 127) / 128;
-  hipLaunchKernelGGL((agent_q_fwd_kernel<F1, G, H, AB>), dim3(tiles * p.N), dim3(256), 0, s, p);
+static int launch_fwd(const QFwdParams& p0, const QFwdParams* p1, hipStream_t s) {
+  const int nb = p0.nblocks + (p1 ? p1->nblocks : 0);
+  hipLaunchKernelGGL((agent_q_fwd_kernel<F1, G, H, AB>), dim3(nb), dim3(256), 0, s, p0, p1 ? *p1 : p0);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
 
-int agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs, hipStream_t s) {
+static int make_params(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,
+                       QFwdParams* p) {
   MM_REQUIRE(d && packed && io, "agent_q_fwd: null argument");
-  MM_REQUIRE(n_envs >= 0 && n_envs < (1ll << 31), "agent_q_fwd: bad n_envs %lld", (long long)n_envs);
-  if (n_envs == 0) return MM_OK;
-  QFwdParams p;
-  p.io = *io;
+  MM_REQUIRE(n_envs >= 1 && n_envs < (1ll << 31), "agent_q_fwd: bad n_envs %lld", (long long)n_envs);
+  p->io = *io;
   QnetOffsets o;
-  int rc = qnet_geometry(d, &p.g, &o);
+  int rc = qnet_geometry(d, &p->g, &o);
   if (rc) return rc;
-  p.packed = packed;
-  p.E = (int)n_envs;
-  p.N = d->n_agents;
-  p.D = d->obs_dim;
-  p.A = d->n_actions;
-  MM_REQUIRE(io->obs && (io->h_in || true), "agent_q_fwd: obs required");
+  p->packed = packed;
+  p->E = (int)n_envs;
+  p->N = d->n_agents;
+  p->D = d->obs_dim;
+  p->A = d->n_actions;
+  p->nblocks = (int)((n_envs + 127) / 128) * d->n_agents;
+  MM_REQUIRE(io->obs, "agent_q_fwd: obs required");
   MM_REQUIRE(io->h_in || io->reset == nullptr, "agent_q_fwd: h_in required");
   MM_REQUIRE(io->mode != MM_Q_GATHER || io->act_in, "agent_q_fwd: GATHER needs act_in");
   MM_REQUIRE(io->obs_row == nullptr || io->reset_obs, "agent_q_fwd: obs_row needs reset_obs");
+  return MM_OK;
+}
+
+static int dispatch(const mm_qnet_dims* d, const QFwdParams& p0, const QFwdParams* p1, hipStream_t s) {
   const int AB = (d->n_actions + 31) / 32;
-  if (d->f1 == 64 && d->g == 32 && d->h == 32) return AB == 1 ? launch_fwd<64, 32, 32, 1>(p, s) : launch_fwd<64, 32, 32, 2>(p, s);
-  if (d->f1 == 64 && d->g == 64 && d->h == 64) return AB == 1 ? launch_fwd<64, 64, 64, 1>(p, s) : launch_fwd<64, 64, 64, 2>(p, s);
-  if (d->f1 == 128 && d->g == 32 && d->h == 32) return AB == 1 ? launch_fwd<128, 32, 32, 1>(p, s) : launch_fwd<128, 32, 32, 2>(p, s);
-  if (d->f1 == 64 && d->g == 32 && d->h == 64) return AB == 1 ? launch_fwd<64, 32, 64, 1>(p, s) : launch_fwd<64, 32, 64, 2>(p, s);
+  if (d->f1 == 64 && d->g == 32 && d->h == 32) return AB == 1 ? launch_fwd<64, 32, 32, 1>(p0, p1, s) : launch_fwd<64, 32, 32, 2>(p0, p1, s);
+  if (d->f1 == 64 && d->g == 64 && d->h == 64) return AB == 1 ? launch_fwd<64, 64, 64, 1>(p0, p1, s) : launch_fwd<64, 64, 64, 2>(p0, p1, s);
+  if (d->f1 == 128 && d->g == 32 && d->h == 32) return AB == 1 ? launch_fwd<128, 32, 32, 1>(p0, p1, s) : launch_fwd<128, 32, 32, 2>(p0, p1, s);
+  if (d->f1 == 64 && d->g == 32 && d->h == 64) return AB == 1 ? launch_fwd<64, 32, 64, 1>(p0, p1, s) : launch_fwd<64, 32, 64, 2>(p0, p1, s);
   set_error("agent_q_fwd: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
   return MM_EINVAL;
+}
+
+int agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs, hipStream_t s) {
+  if (n_envs == 0) return MM_OK;
+  QFwdParams p;
+  int rc = make_params(d, packed, io, n_envs, &p);
+  if (rc) return rc;
+  return dispatch(d, p, nullptr, s);
+}
+
+int agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
+                 const float* packed1, const mm_qfwd_io* io1, int64_t e1, hipStream_t s) {
+  QFwdParams p0, p1;
+  int rc = make_params(d, packed0, io0, e0, &p0);
+  if (rc) return rc;
+  rc = make_params(d, packed1, io1, e1, &p1);
+  if (rc) return rc;
+  return dispatch(d, p0, &p1, s);
 }
 
 }  // namespace mm

@@ -55,6 +55,8 @@ _SIGS = [
     ("mm_qnet_packed_count", c_i64, [ctypes.POINTER(QnetDims)]),
     ("mm_qnet_pack", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_vp, c_vp]),
     ("mm_agent_q_fwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp]),
+    ("mm_agent_q_fwd2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
+                                ctypes.POINTER(QFwdIO), c_i64, c_vp]),
     ("mm_agent_q_fwd_simple", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     ("mm_env_create", c_i32, [ctypes.POINTER(EnvCfg), c_i64, c_u64, ctypes.POINTER(c_vp)]),
     ("mm_env_destroy", None, [c_vp]),

@@ -10,7 +10,9 @@ qmix/main.py:100-237): for every env at every step
      (cal_td_error + chunk lists, qmix/_utils.py:86-97, qmix/main.py:204-233)
   5. every C steps: the E finished chunks go into the prioritized replay at once
 
-Six launches per step, all stream-ordered on one HIP stream, no host sync.
+Three launches per step (env; target fwd of step t fused with the behavior fwd of
+step t+1 into one launch; TD/store), all stream-ordered on one HIP stream, no host
+sync; a chunk of steps is captured once as a HIP graph and replayed.
 Hidden states reset at episode ends (the reference re-inits them per episode,
 vdn/main.py:137-138); chunks span episode boundaries like the reference's
 global ``count_step`` (vdn/main.py:151-167).
@@ -69,16 +71,17 @@ class RolloutEngine:
         self.obs_cur = torch.empty(E, N, D, device=dev)
         self.h = torch.zeros(E, N, H, device=dev)
         self.ht = torch.zeros(E, N, H, device=dev)
-        self.done_prev = torch.zeros(E, dtype=torch.uint8, device=dev)
-        self.done = torch.zeros(E, dtype=torch.uint8, device=dev)
-        self.act = torch.zeros(E, N, dtype=torch.int32, device=dev)
-        self.qsel = torch.zeros(E, N, device=dev)
+        # ping-pong buffers indexed by step parity: done_t, act_t, q_taken_t live in slot t % 2
+        self.done_buf = [torch.zeros(E, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.act_buf = [torch.zeros(E, N, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.qsel_buf = [torch.zeros(E, N, device=dev) for _ in range(2)]
         self.maxq = torch.zeros(E, N, device=dev)
         self.rew = torch.zeros(E, N, device=dev)
         self.chunk_td = torch.zeros(E, device=dev)
         self.eps_dev = torch.zeros(1, device=dev)
         self.counter_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # rollout step (RNG stream)
         self._eps_host = None
+        self._primed = False
         self.graph = None
         self.t = 0
         self.seed = int(seed)
@@ -86,7 +89,12 @@ class RolloutEngine:
         self._build_io()
         self.env.reset(self.obs_cur)
 
-    def _build_io(self):
+    @property
+    def act(self):
+        return self.act_buf[(self.t - 1) % 2] if self.t > 0 else self.act_buf[0]
+
+    def _io_behavior(self, k):
+        """behavior fwd writing slot k (acts for step t with t % 2 == k); reset = done_{t-1}."""
         E, N, D, H = self.E, self.N, self.D, self.H
         b = QFwdIO()
         b.obs, b.obs_se, b.obs_sa = self.obs_cur.data_ptr(), N * D, D
@@ -94,14 +102,17 @@ class RolloutEngine:
         b.hin_se = b.hout_se = N * H
         b.hin_sa = b.hout_sa = H
         b.hin_sf = b.hout_sf = 1
-        b.reset = self.done_prev.data_ptr()
+        b.reset = self.done_buf[1 - k].data_ptr()
         b.mode = MM_Q_ACT
-        b.act_out, b.qsel_out = self.act.data_ptr(), self.qsel.data_ptr()
+        b.act_out, b.qsel_out = self.act_buf[k].data_ptr(), self.qsel_buf[k].data_ptr()
         b.seed = self.seed
         b.eps_ptr, b.counter_ptr = self.eps_dev.data_ptr(), self.counter_dev.data_ptr()
-        self.io_b = b
+        return b
+
+    def _io_target(self, k):
+        """target fwd of step t (t % 2 == k) on s'_t read from the staging rows; reset = done_{t-1}."""
+        N, D, H = self.N, self.D, self.H
         t = QFwdIO()
-        # target reads s'_t straight out of the staging rows of the chunk store (gather by row)
         t.obs, t.obs_se, t.obs_sa = self.store.obs.data_ptr(), self.store.row_stride, D
         t.obs_row = self.staging.data_ptr()
         t.reset_obs = self.env.reset_obs_ptr()
@@ -109,10 +120,18 @@ class RolloutEngine:
         t.hin_se = t.hout_se = N * H
         t.hin_sa = t.hout_sa = H
         t.hin_sf = t.hout_sf = 1
-        t.reset = self.done_prev.data_ptr()
+        t.reset = self.done_buf[1 - k].data_ptr()
         t.mode = MM_Q_MAX
         t.qsel_out = self.maxq.data_ptr()
-        self.io_t = t
+        return t
+
+    def _build_io(self):
+        self.io_b = [self._io_behavior(0), self._io_behavior(1)]
+        self.io_t = [self._io_target(0), self._io_target(1)]
+        # the prologue behavior fwd (step 0) uses its own RNG counter so it never repeats step 1's draws
+        self.io_b0 = self._io_behavior(0)
+        self.io_b0.counter_ptr = None
+        self.io_b0.counter = 0x7FFFFFFFFFFFFFFF
 
     def sync_target(self):
         self.target.copy_from(self.behavior)
@@ -123,32 +142,41 @@ class RolloutEngine:
             self._eps_host = epsilon
 
     def step(self, epsilon=None):
-        """One lockstep env step for all E envs (<= 6 launches, no host sync)."""
+        """One lockstep env step for all E envs (3-5 launches, no host sync)."""
         if epsilon is not None:
             self.set_epsilon(epsilon)
         self._step_launch()
 
+    def _prologue(self, s):
+        self.behavior.forward_io(self.E, self.io_b0, s)
+        self._primed = True
+
     def _step_launch(self):
+        """Step t: env(t) -> [target fwd(t) + behavior fwd(t+1)] in ONE launch -> TD/store(t)."""
         s = stream_handle(self.device)
         L = lib()
-        c = self.t % self.C
+        t = self.t
+        c, k = t % self.C, t % 2
         ND = self.N * self.D
+        if not self._primed:
+            self._prologue(s)
         if c == 0:
             check(L.mm_chunk_begin(self.E, ND, ptr(self.obs_cur), ptr(self.store.obs), self.store.row_stride,
                                    ptr(self.staging), s), "chunk_begin")
-        self.behavior.forward_io(self.E, self.io_b, s)
         nxt = ctypes.c_void_p(self.store.obs.data_ptr() + 4 * (c + 1) * ND)
-        check(L.mm_env_step_rows(self.env.handle(), ptr(self.act), nxt, self.store.row_stride, ptr(self.staging),
-                                 ptr(self.obs_cur), ptr(self.rew), ptr(self.done), s), "env_step")
-        self.io_t.obs_off = (c + 1) * ND
-        self.target.forward_io(self.E, self.io_t, s)
-        check(L.mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done), ptr(self.qsel),
-                                      ptr(self.maxq), ptr(self.act), ptr(self.chunk_td), c, self.C,
-                                      ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
+        check(L.mm_env_step_rows(self.env.handle(), ptr(self.act_buf[k]), nxt, self.store.row_stride,
+                                 ptr(self.staging), ptr(self.obs_cur), ptr(self.rew), ptr(self.done_buf[k]), s),
+              "env_step")
+        iot, iob = self.io_t[k], self.io_b[1 - k]
+        iot.obs_off = (c + 1) * ND
+        self.behavior.pack(s)
+        self.target.pack(s)
+        check(L.mm_agent_q_fwd2(ctypes.byref(self.target.dims), ptr(self.target.packed), ctypes.byref(iot), self.E,
+                                ptr(self.behavior.packed), ctypes.byref(iob), self.E, s), "agent_q_fwd2")
+        check(L.mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done_buf[k]),
+                                      ptr(self.qsel_buf[k]), ptr(self.maxq), ptr(self.act_buf[k]), ptr(self.chunk_td),
+                                      c, self.C, ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
                                       ptr(self.staging), ptr(self.counter_dev), s), "td_chunk")
-        # done of this step resets hidden states at the next step (episode boundary)
-        self.done_prev, self.done = self.done, self.done_prev
-        self.io_b.reset = self.io_t.reset = self.done_prev.data_ptr()
         if c == self.C - 1:
             check(L.mm_per_insert(self.per._h, ptr(self.chunk_td), self.E, ptr(self.staging), None, s), "per_insert")
             self.chunks_inserted += self.E
@@ -164,6 +192,8 @@ class RolloutEngine:
         assert self.t % self.C == 0, "capture must start at a chunk boundary"
         self.behavior.pack()
         self.target.pack()
+        if not self._primed:
+            self._prologue(stream_handle(self.device))
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         t0, ins0, n0 = self.t, self.chunks_inserted, len(self.per)
@@ -182,6 +212,8 @@ class RolloutEngine:
             self.set_epsilon(epsilon)
         if self.graph is None:
             self.capture()
+        self.behavior.pack()          # weights changed since capture (learner / target sync): repack eagerly
+        self.target.pack()
         self.graph.replay()
         n = self.graph_steps()
         self.t += n
@@ -191,3 +223,10 @@ class RolloutEngine:
     def run(self, n_steps, epsilon):
         for _ in range(n_steps):
             self.step(epsilon)
+
+    def fused_forward(self, k=0):
+        """The step's dominant launch on its own (target fwd + behavior fwd); for timing."""
+        s = stream_handle(self.device)
+        check(lib().mm_agent_q_fwd2(ctypes.byref(self.target.dims), ptr(self.target.packed),
+                                    ctypes.byref(self.io_t[k]), self.E, ptr(self.behavior.packed),
+                                    ctypes.byref(self.io_b[1 - k]), self.E, s), "agent_q_fwd2")
