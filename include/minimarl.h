@@ -67,6 +67,9 @@ typedef struct mm_qfwd_io {
   float* qsel_out;                                    /* [E,N]: Q(a_chosen) (ACT/GATHER) or max_a Q (MAX) */
   /* optional device scalars overriding epsilon / counter (graph-replayable rollouts) */
   const float* eps_ptr; const uint64_t* counter_ptr;
+  /* optional training save: per (e, agent) row of SD = F1+G+6H floats
+   * [x1 | x2 | h_in | r | z | n | W_hn h + b_hn | h_out] at save + (e*N + agent)*SD */
+  float* save;
 } mm_qfwd_io;
 
 int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,

@@ -144,6 +144,14 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int bid) {
   for (int rb = 0; rb < RB1; ++rb)
 #pragma unroll
     for (int s = 0; s < 16; ++s) x1[rb][s] = fmaxf(x1[rb][s], 0.0f);
+  // training save row (see mm_qfwd_io.save): [x1 | x2 | h_in | r | z | n | anh | h_out]
+  float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
+  if (sv) {
+#pragma unroll
+    for (int rb = 0; rb < RB1; ++rb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) sv[rb * 32 + kperm(s, hh)] = x1[rb][s];
+  }
 
   // ---- layer 2: x2 = ReLU(W2 x1 + b2)
   f32x16 x2[RB2];
@@ -154,6 +162,10 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int bid) {
     for (int kb = 0; kb < RB1; ++kb) consume(rb * RB1 + kb, x1[kb], x2[rb]);
 #pragma unroll
     for (int s = 0; s < 16; ++s) x2[rb][s] = fmaxf(x2[rb][s], 0.0f);
+    if (sv) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) sv[F1 + rb * 32 + kperm(s, hh)] = x2[rb][s];
+    }
   }
 
   // ---- GRU cell
@@ -194,6 +206,15 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int bid) {
       const float z = sigmoidf_(az[s]);
       const float n = tanhf(anx[s] + r * anh[s]);
       h1[hb][s] = n + z * (h0[hb][s] - n);
+      if (sv) {
+        float* o = sv + F1 + G + hb * 32 + kperm(s, hh);
+        o[0] = h0[hb][s];
+        o[H] = r;
+        o[2 * H] = z;
+        o[3 * H] = n;
+        o[4 * H] = anh[s];
+        o[5 * H] = h1[hb][s];
+      }
     }
   }
   if (valid && io.h_out) {

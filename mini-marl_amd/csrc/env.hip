@@ -107,9 +107,11 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int RC = d.R * d.C;
   const int N = d.N;
-  int32_t* spos = reinterpret_cast<int32_t*>(smem);                       // [EB][N]
-  uint8_t* sdone = reinterpret_cast<uint8_t*>(smem + EB * N * 4);         // [EB]
-  int8_t* sgrid = reinterpret_cast<int8_t*>(smem + EB * N * 4 + EB);      // [EB][RC]
+  int64_t* srow = reinterpret_cast<int64_t*>(smem);                       // [EB] destination rows
+  int32_t* spos = reinterpret_cast<int32_t*>(smem + EB * 8);              // [EB][N]
+  int32_t* sact = spos + EB * N;                                          // [EB][N]
+  uint8_t* sdone = reinterpret_cast<uint8_t*>(sact + EB * N);             // [EB]
+  int8_t* sgrid = reinterpret_cast<int8_t*>(sdone + EB);                  // [EB][RC]
   uint8_t* socc = reinterpret_cast<uint8_t*>(sgrid + EB * RC);            // [EB][RC] agent id + 1
   const int e0 = blockIdx.x * EB;
   const int ne = min(EB, d.E - e0);
@@ -119,7 +121,11 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
     sgrid[i] = d.grid[(int64_t)e0 * RC + i];
     socc[i] = 0;
   }
-  for (int i = threadIdx.x; i < ne * N; i += blockDim.x) spos[i] = d.pos[(int64_t)e0 * N + i];
+  for (int i = threadIdx.x; i < ne * N; i += blockDim.x) {
+    spos[i] = d.pos[(int64_t)e0 * N + i];
+    sact[i] = act[(int64_t)e0 * N + i];
+  }
+  for (int i = threadIdx.x; i < ne; i += blockDim.x) srow[i] = next_row ? next_row[e0 + i] : (int64_t)(e0 + i);
   __syncthreads();
 
   // phase 1: dynamics, one thread per env, agents in id order (oracle/env.py VecEnvOracle.step)
@@ -130,7 +136,7 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
     int apples = d.apples[e];
     const int steps = d.steps[e] + 1;
     for (int k = 0; k < N; ++k) {
-      const int a = act[(int64_t)e * N + k];
+      const int a = sact[le * N + k];
       const int r = p[k] >> 8, c = p[k] & 255;
       const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
       const int nc = c + (a == 1 ? -1 : (a == 3 ? 1 : 0));
@@ -193,8 +199,7 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
             : ((item == 0 && occ != 0 && ((occ - 1) & 1) == ch - 2) ? 1.0f : 0.0f);
         }
       }
-      const int64_t row = next_row ? next_row[e0 + le] : (int64_t)(e0 + le);
-      next_obs[row * next_se + r] = v;
+      next_obs[srow[le] * next_se + r] = v;
       if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? rs : v;
     }
   }
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
   }
 }
 
-static size_t step_smem(const EnvDev& d) { return (size_t)EB * d.N * 4 + EB + 2 * (size_t)EB * d.R * d.C; }
+static size_t step_smem(const EnvDev& d) { return (size_t)EB * 8 + 2 * (size_t)EB * d.N * 4 + EB + 2 * (size_t)EB * d.R * d.C; }
 
 int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out) {
   (void)seed;  // the layout is deterministic (ma_gym Checkers resets to a fixed layout)

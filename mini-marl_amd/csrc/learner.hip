@@ -1,0 +1,713 @@
+// Learner kernels for the chunked-BPTT QMIX / VDN update (gfx950).
+//
+// Replaces Train_dqn.train (qmix/_train.py:19-121) and Target_Dqn.train
+// (vdn/_train.py:184-235): one update = sample B chunks of C steps from the
+// device PER, forward the behavior and target agent nets (mm_agent_q_fwd with
+// the training save) and mixers over the C steps, loss, backward through time,
+// clip_grad_norm_, Adam, priority update. Reference quirks reproduced
+// (SURVEY App. A): target = w * sum_i(r_i + gamma*(1-d)*Q'_tot) (bootstrap x N,
+// IS weight on the target), MSE mean over B summed over C, hidden states zero at
+// the chunk start and reset on done, priorities from the LAST step's |y - Q_tot|,
+// QMIX clips the agent params only.
+//
+// Structure: the C-step recurrences (forward, mixer backward, agent backward
+// chain) are small dependent launches; every weight gradient is deferred and
+// computed at the end as ONE batched outer-product reduction over all C*B
+// (step, sample) rows — so the sequential part only carries the data-gradient
+// chain. All reductions use a fixed order (bit-reproducible run to run).
+#pragma clang fp contract(off)
+#include "common.h"
+#include "minimarl.h"
+
+namespace mm {
+
+// ------------------------------------------------------------------ gather
+// For sample b (PER slot -> chunk-store row) and step t:
+//   s_off[t][b]  = element offset of s_t in store.obs  (-1 => the env's reset obs)
+//   s2_off[t][b] = element offset of s'_t
+//   acts[t][b][i] (int32), rew[t][b][i] (f32), done[t][b] (f32), done8[t][b] (u8)
+__global__ void lrn_gather_kernel(int B, int C, int N, int64_t row_stride, int64_t nd, const int64_t* slots,
+                                  const int64_t* slot_row, const uint8_t* s_done, const uint8_t* s_act,
+                                  const float* s_rew, int64_t* s_off, int64_t* s2_off, int32_t* acts, float* rew,
+                                  float* done, uint8_t* done8) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i % B, t = i / B;
+  const int64_t row = slot_row[slots[b]];
+  const uint8_t dprev = t > 0 ? s_done[row * C + t - 1] : 0;
+  s_off[i] = (t > 0 && dprev) ? -1 : row * row_stride + (int64_t)t * nd;
+  s2_off[i] = row * row_stride + (int64_t)(t + 1) * nd;
+  const uint8_t dn = s_done[row * C + t];
+  done[i] = dn ? 1.0f : 0.0f;
+  done8[i] = dn;
+  for (int k = 0; k < N; ++k) {
+    acts[(int64_t)i * N + k] = s_act[(row * C + t) * N + k];
+    rew[(int64_t)i * N + k] = s_rew[(row * C + t) * N + k];
+  }
+}
+
+// ------------------------------------------------------------------ block helpers
+// out[r] = (bias ? bias[r] : 0) + sum_k W[r*K + k] * x[k]   for r < rows (x in LDS). fixed-order sums.
+__device__ void block_matvec(const float* __restrict__ W, const float* __restrict__ bias, int rows, int K,
+                             const float* x, float* out) {
+  if (K >= 128) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int r = w; r < rows; r += nw) {
+      float acc = 0.f;
+      for (int k = lane; k < K; k += 64) acc += W[(int64_t)r * K + k] * x[k];
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+      if (lane == 0) out[r] = acc + (bias ? bias[r] : 0.f);
+    }
+  } else {
+    for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+      float acc = 0.f;
+      for (int k = 0; k < K; ++k) acc += W[(int64_t)r * K + k] * x[k];
+      out[r] = acc + (bias ? bias[r] : 0.f);
+    }
+  }
+}
+
+// out[c] (+)= sum_r W[r*K + c] * d[r]   for c < K (transpose matvec, coalesced over c)
+__device__ void block_matvec_t(const float* __restrict__ W, int rows, int K, const float* d, float* out,
+                               bool accumulate) {
+  for (int c = threadIdx.x; c < K; c += blockDim.x) {
+    float acc = 0.f;
+    for (int r = 0; r < rows; ++r) acc += W[(int64_t)r * K + c] * d[r];
+    out[c] = accumulate ? out[c] + acc : acc;
+  }
+}
+
+// ------------------------------------------------------------------ mixer
+// Canonical mixer layout (qmix/_network.py:172-197), oracle/nets.py MIXER_KEYS order.
+struct MixOff {
+  int64_t gWih, gWhh, gbih, gbhh, w1W, w1b, w2W, w2b, b1W, b1b, b2aW, b2ab, b2bW, b2bb, total;
+};
+
+__host__ __device__ inline MixOff mix_offsets(int S, int Hm, int K1, int N) {
+  MixOff o;
+  int64_t c = 0;
+  o.gWih = c; c += (int64_t)3 * Hm * S;
+  o.gWhh = c; c += (int64_t)3 * Hm * Hm;
+  o.gbih = c; c += 3 * Hm;
+  o.gbhh = c; c += 3 * Hm;
+  o.w1W = c; c += (int64_t)N * K1 * Hm;
+  o.w1b = c; c += N * K1;
+  o.w2W = c; c += (int64_t)K1 * Hm;
+  o.w2b = c; c += K1;
+  o.b1W = c; c += (int64_t)K1 * Hm;
+  o.b1b = c; c += K1;
+  o.b2aW = c; c += (int64_t)K1 * Hm;
+  o.b2ab = c; c += K1;
+  o.b2bW = c; c += K1;
+  o.b2bb = c; c += 1;
+  o.total = c;
+  return o;
+}
+
+// per-(t,b) mixer save row: [hm0 | r | z | n | anh | hm1 | w1raw (N*K1) | b1 | w2raw | b2pre | ypre | b2]
+__host__ __device__ inline int mix_save_dim(int Hm, int K1, int N) { return 6 * Hm + N * K1 + 4 * K1 + 1; }
+
+struct MixFwdNet {
+  const float* P;        // mixer params (canonical)
+  const float* q;        // [B][N] agent values fed to the mixer (Q(a) or max Q')
+  const int64_t* s_off;  // [B] state offsets into obs (-1: reset obs)
+  const float* h_in;     // [B][Hm] (nullptr => zero)
+  const uint8_t* reset;  // [B] (nullptr => none)
+  float* h_out;          // [B][Hm]
+  float* qtot;           // [B]
+  float* save;           // [B][MSD] or nullptr
+};
+
+struct MixFwdArgs {
+  MixFwdNet net[2];
+  const float* obs;
+  const float* reset_obs;  // [N*D]
+  int B, N, S, Hm, K1;
+};
+
+// One block per (sample, net): blockIdx.y selects behavior / target.
+__global__ __launch_bounds__(256) void mixer_fwd_kernel(MixFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const MixFwdNet& nt = a.net[blockIdx.y];
+  const int b = blockIdx.x;
+  const int S = a.S, Hm = a.Hm, K1 = a.K1, N = a.N;
+  const MixOff o = mix_offsets(S, Hm, K1, N);
+  float* xs = sm;                  // [S]
+  float* h0 = xs + S;              // [Hm]
+  float* gi = h0 + Hm;             // [3Hm]
+  float* gh = gi + 3 * Hm;         // [3Hm]
+  float* h1 = gh + 3 * Hm;         // [Hm]
+  float* hyp = h1 + Hm;            // [N*K1 + 3*K1]: w1raw | b1 | w2raw | b2pre
+  float* yp = hyp + N * K1 + 3 * K1;  // [K1]
+  const int64_t off = nt.s_off[b];
+  const float* src = off >= 0 ? a.obs + off : a.reset_obs;
+  for (int i = threadIdx.x; i < S; i += blockDim.x) xs[i] = src[i];
+  const bool rz = !nt.h_in || (nt.reset && nt.reset[b]);
+  for (int i = threadIdx.x; i < Hm; i += blockDim.x) h0[i] = rz ? 0.f : nt.h_in[(int64_t)b * Hm + i];
+  __syncthreads();
+  block_matvec(nt.P + o.gWih, nt.P + o.gbih, 3 * Hm, S, xs, gi);
+  block_matvec(nt.P + o.gWhh, nt.P + o.gbhh, 3 * Hm, Hm, h0, gh);
+  __syncthreads();
+  float* sv = nt.save ? nt.save + (int64_t)b * mix_save_dim(Hm, K1, N) : nullptr;
+  for (int i = threadIdx.x; i < Hm; i += blockDim.x) {
+    const float r = sigmoidf_(gi[i] + gh[i]);
+    const float z = sigmoidf_(gi[Hm + i] + gh[Hm + i]);
+    const float n = tanhf(gi[2 * Hm + i] + r * gh[2 * Hm + i]);
+    const float hv = n + z * (h0[i] - n);
+    h1[i] = hv;
+    nt.h_out[(int64_t)b * Hm + i] = hv;
+    if (sv) {
+      sv[i] = h0[i];
+      sv[Hm + i] = r;
+      sv[2 * Hm + i] = z;
+      sv[3 * Hm + i] = n;
+      sv[4 * Hm + i] = gh[2 * Hm + i];
+      sv[5 * Hm + i] = hv;
+    }
+  }
+  __syncthreads();
+  // hypernets on h1: w1raw [N*K1], b1 [K1], w2raw [K1], b2 hidden pre-ReLU [K1]
+  block_matvec(nt.P + o.w1W, nt.P + o.w1b, N * K1, Hm, h1, hyp);
+  block_matvec(nt.P + o.b1W, nt.P + o.b1b, K1, Hm, h1, hyp + N * K1);
+  block_matvec(nt.P + o.w2W, nt.P + o.w2b, K1, Hm, h1, hyp + N * K1 + K1);
+  block_matvec(nt.P + o.b2aW, nt.P + o.b2ab, K1, Hm, h1, hyp + N * K1 + 2 * K1);
+  __syncthreads();
+  // y_pre[k] = sum_i |w1raw[k*N + i]| q_i + b1[k]   (bmm(W1 [K1,N], q [N,1]) + b1)
+  for (int k = threadIdx.x; k < K1; k += blockDim.x) {
+    float acc = 0.f;
+    for (int i = 0; i < N; ++i) acc += fabsf(hyp[k * N + i]) * nt.q[(int64_t)b * N + i];
+    yp[k] = acc + hyp[N * K1 + k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float* w2raw = hyp + N * K1 + K1;
+    const float* b2pre = hyp + N * K1 + 2 * K1;
+    float b2 = 0.f;
+    for (int k = 0; k < K1; ++k) b2 += nt.P[o.b2bW + k] * fmaxf(b2pre[k], 0.f);
+    b2 += nt.P[o.b2bb];
+    float acc = 0.f;
+    for (int k = 0; k < K1; ++k) acc += fabsf(w2raw[k]) * fmaxf(yp[k], 0.f);
+    nt.qtot[b] = acc + b2;
+    if (sv) sv[6 * Hm + N * K1 + 4 * K1] = b2;
+  }
+  if (sv) {
+    // [w1raw | b1 | w2raw | relu(b2 hidden)] (relu'd: the b2 weight gradient needs it, and its
+    // mask relu(x) > 0 equals x > 0)
+    for (int i = threadIdx.x; i < N * K1 + 3 * K1; i += blockDim.x)
+      sv[6 * Hm + i] = i >= N * K1 + 2 * K1 ? fmaxf(hyp[i], 0.f) : hyp[i];
+    for (int k = threadIdx.x; k < K1; k += blockDim.x) sv[6 * Hm + N * K1 + 3 * K1 + k] = yp[k];
+  }
+}
+
+// ------------------------------------------------------------------ loss (all steps at once)
+// y = w * sum_i (r_i + gamma*(1-d)*Q'tot)   (qmix/_train.py:80-82, vdn/_train.py:76-77)
+// dQtot = 2 (Qtot - y) / B ;  loss = sum_t mean_b (y - Qtot)^2 ;  td = |y - Qtot| at t = C-1.
+// VDN (mix_sum): Qtot = sum_i qa_i, Q'tot = sum_i maxq'_i, dqa_i = dQtot.
+__global__ void lrn_loss_kernel(int B, int C, int N, float gamma, const float* rew, const float* done,
+                                const float* isw, const float* qtot, const float* qtot_t, int mix_sum,
+                                const float* qa, const float* maxq, float* dq, float* dqa, float* loss_parts,
+                                float* td_last) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i % B, t = i / B;
+  float qt, qn;
+  if (mix_sum) {
+    qt = 0.f;
+    qn = 0.f;
+    for (int k = 0; k < N; ++k) {
+      qt += qa[(int64_t)i * N + k];
+      qn += maxq[(int64_t)i * N + k];
+    }
+  } else {
+    qt = qtot[i];
+    qn = qtot_t[i];
+  }
+  const float boot = gamma * (1.0f - done[i]) * qn;
+  float acc = 0.f;
+  for (int k = 0; k < N; ++k) acc += rew[(int64_t)i * N + k] + boot;
+  const float y = isw[b] * acc;
+  const float diff = qt - y;
+  const float g = 2.0f * diff / (float)B;
+  dq[i] = g;
+  if (mix_sum)
+    for (int k = 0; k < N; ++k) dqa[(int64_t)i * N + k] = g;
+  loss_parts[i] = diff * diff;
+  if (t == C - 1) td_last[b] = fabsf(diff);
+}
+
+// loss = sum_t (1/B) sum_b parts  (one thread, fixed order)
+__global__ void lrn_loss_reduce_kernel(int B, int C, const float* parts, float* loss) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float tot = 0.f;
+  for (int t = 0; t < C; ++t) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += parts[t * B + b];
+    tot += s / (float)B;
+  }
+  *loss = tot;
+}
+
+// ------------------------------------------------------------------ mixer backward (one step)
+struct MixBwdArgs {
+  const float* P;        // behavior mixer params
+  const float* save;     // [B][MSD] of this step
+  const float* qa;       // [B][N] of this step
+  const float* dq;       // [B] dQtot of this step
+  const float* done;     // [B] done of THIS step (1 => drop the future gradient)
+  float* dhm;            // [B][Hm] in: grad wrt hm1 from step t+1 ; out: grad wrt hm0 (for step t-1)
+  float* dqa;            // [B][N] out
+  float* delta;          // [B][MDD] out: [dgi 3Hm | dgh 3Hm | dw1raw N*K1 | db1 K1 | dw2raw K1 | db2pre K1 | dQ 1]
+  int B, N, S, Hm, K1;
+};
+__host__ __device__ inline int mix_delta_dim(int Hm, int K1, int N) { return 6 * Hm + N * K1 + 3 * K1 + 1; }
+
+__global__ __launch_bounds__(256) void mixer_bwd_kernel(MixBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x;
+  const int Hm = a.Hm, K1 = a.K1, N = a.N;
+  const MixOff o = mix_offsets(a.S, Hm, K1, N);
+  const float* sv = a.save + (int64_t)b * mix_save_dim(Hm, K1, N);
+  const float* hm0 = sv;
+  const float* rg = sv + Hm;
+  const float* zg = sv + 2 * Hm;
+  const float* ng = sv + 3 * Hm;
+  const float* anh = sv + 4 * Hm;
+  const float* w1raw = sv + 6 * Hm;
+  const float* w2raw = w1raw + N * K1 + K1;
+  const float* b2pre = w2raw + K1;
+  const float* ypre = b2pre + K1;
+  float* dl = a.delta + (int64_t)b * mix_delta_dim(Hm, K1, N);
+  float* d_w1 = dl + 6 * Hm;         // [N*K1]
+  float* d_b1 = d_w1 + N * K1;       // [K1]
+  float* d_w2 = d_b1 + K1;           // [K1]
+  float* d_b2pre = d_w2 + K1;        // [K1]
+  float* dhm1 = sm;                  // [Hm]
+  float* dgh = dhm1 + Hm;            // [3Hm]
+  float* shd = dgh + 3 * Hm;         // [N*K1 + 3*K1] local copy of the hypernet deltas
+  const float dQ = a.dq[b];
+  // hypernet / mixing deltas
+  for (int k = threadIdx.x; k < K1; k += blockDim.x) {
+    const float y = fmaxf(ypre[k], 0.f);
+    const float w2 = w2raw[k];
+    const float dw2 = dQ * y * (w2 > 0.f ? 1.f : (w2 < 0.f ? -1.f : 0.f));
+    const float dyp = ypre[k] > 0.f ? dQ * fabsf(w2) : 0.f;
+    const float db2p = b2pre[k] > 0.f ? dQ * a.P[o.b2bW + k] : 0.f;
+    d_b1[k] = dyp;
+    d_w2[k] = dw2;
+    d_b2pre[k] = db2p;
+    shd[N * K1 + k] = dyp;
+    shd[N * K1 + K1 + k] = dw2;
+    shd[N * K1 + 2 * K1 + k] = db2p;
+    for (int i = 0; i < N; ++i) {
+      const float w = w1raw[k * N + i];
+      const float dw1 = dyp * a.qa[(int64_t)b * N + i] * (w > 0.f ? 1.f : (w < 0.f ? -1.f : 0.f));
+      d_w1[k * N + i] = dw1;
+      shd[k * N + i] = dw1;
+    }
+  }
+  if (threadIdx.x == 0) dl[6 * Hm + N * K1 + 3 * K1] = dQ;
+  __syncthreads();
+  // dqa_i = sum_k dy_pre_k |W1[k,i]|
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < K1; ++k) acc += shd[N * K1 + k] * fabsf(w1raw[k * N + i]);
+    a.dqa[(int64_t)b * N + i] = acc;
+  }
+  // dhm1 = (future grad unless done) + hypernet input grads
+  const bool drop = a.done[b] > 0.5f;
+  for (int c = threadIdx.x; c < Hm; c += blockDim.x) dhm1[c] = drop ? 0.f : a.dhm[(int64_t)b * Hm + c];
+  __syncthreads();
+  block_matvec_t(a.P + o.w1W, N * K1, Hm, shd, dhm1, true);
+  __syncthreads();
+  block_matvec_t(a.P + o.b1W, K1, Hm, shd + N * K1, dhm1, true);
+  __syncthreads();
+  block_matvec_t(a.P + o.w2W, K1, Hm, shd + N * K1 + K1, dhm1, true);
+  __syncthreads();
+  block_matvec_t(a.P + o.b2aW, K1, Hm, shd + N * K1 + 2 * K1, dhm1, true);
+  __syncthreads();
+  // GRU backward (h' = n + z (h - n))
+  for (int i = threadIdx.x; i < Hm; i += blockDim.x) {
+    const float dh = dhm1[i];
+    const float r = rg[i], z = zg[i], n = ng[i];
+    const float dn = dh * (1.f - z);
+    const float dz = dh * (hm0[i] - n);
+    const float dpn = dn * (1.f - n * n);
+    const float dr = dpn * anh[i];
+    const float dar = dr * r * (1.f - r);
+    const float daz = dz * z * (1.f - z);
+    dl[i] = dar;
+    dl[Hm + i] = daz;
+    dl[2 * Hm + i] = dpn;
+    dl[3 * Hm + i] = dar;
+    dl[4 * Hm + i] = daz;
+    dl[5 * Hm + i] = dpn * r;
+    dgh[i] = dar;
+    dgh[Hm + i] = daz;
+    dgh[2 * Hm + i] = dpn * r;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < Hm; c += blockDim.x) {
+    float acc = dhm1[c] * zg[c];
+    for (int r = 0; r < 3 * Hm; ++r) acc += a.P[o.gWhh + (int64_t)r * Hm + c] * dgh[r];
+    a.dhm[(int64_t)b * Hm + c] = acc;
+  }
+}
+
+// ------------------------------------------------------------------ agent backward chain (one step)
+struct AgentBwdArgs {
+  const float* P;            // behavior agent params (canonical flat)
+  int64_t oWq, oWhh;         // element offsets of Wq / Whh in P
+  const float* save;         // [B][N][SD] of this step
+  const int32_t* acts;       // [B][N]
+  const float* dqa;          // [B][N]
+  const float* done;         // [B] done of THIS step (drop the future gradient)
+  float* dh;                 // [B][N][H] in: grad wrt h_out from step t+1 ; out: grad wrt h_in
+  float* dgi;                // [B][N][3H] out (also the dgh rows via dgh pointer)
+  float* dgh;                // [B][N][3H] out
+  float* dq;                 // [B][N][A] out (dense one-hot dQ for the Wq gradient)
+  int B, N, F1, G, H, A;
+};
+
+// one wave per (sample, agent); lane = hidden feature
+__global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs a) {
+  __shared__ float sdg[4][3 * 256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pair0 = blockIdx.x * 4 + w;
+  const bool on = pair0 < a.B * a.N;
+  const int pair = on ? pair0 : 0;
+  const int b = pair / a.N, i = pair % a.N;
+  const int H = a.H, A = a.A;
+  const int SD = a.F1 + a.G + 6 * H;
+  const float* sv = a.save + (int64_t)pair * SD;
+  const float* h0 = sv + a.F1 + a.G;
+  const int act = a.acts[pair];
+  const float dqa = a.dqa[pair];
+  const float* Wq = a.P + a.oWq + (int64_t)i * A * H;
+  const float* Whh = a.P + a.oWhh + (int64_t)i * 3 * H * H;
+  const bool drop = a.done[b] > 0.5f;
+  if (on)
+    for (int c = lane; c < A; c += 64) a.dq[(int64_t)pair * A + c] = (c == act) ? dqa : 0.f;
+  for (int f = lane; f < H && on; f += 64) {
+    const float dh1 = Wq[(int64_t)act * H + f] * dqa + (drop ? 0.f : a.dh[(int64_t)pair * H + f]);
+    const float r = h0[H + f], z = h0[2 * H + f], n = h0[3 * H + f], anh = h0[4 * H + f];
+    const float dn = dh1 * (1.f - z);
+    const float dz = dh1 * (h0[f] - n);
+    const float dpn = dn * (1.f - n * n);
+    const float dar = dpn * anh * r * (1.f - r);
+    const float daz = dz * z * (1.f - z);
+    float* gi = a.dgi + (int64_t)pair * 3 * H;
+    float* gh = a.dgh + (int64_t)pair * 3 * H;
+    gi[f] = dar;
+    gi[H + f] = daz;
+    gi[2 * H + f] = dpn;
+    gh[f] = dar;
+    gh[H + f] = daz;
+    gh[2 * H + f] = dpn * r;
+    sdg[w][f] = dar;
+    sdg[w][H + f] = daz;
+    sdg[w][2 * H + f] = dpn * r;
+    // stash dh1*z for the direct path
+    a.dh[(int64_t)pair * H + f] = dh1 * z;
+  }
+  __syncthreads();
+  for (int f = lane; f < H && on; f += 64) {
+    float acc = a.dh[(int64_t)pair * H + f];
+    for (int r = 0; r < 3 * H; ++r) acc += Whh[(int64_t)r * H + f] * sdg[w][r];
+    a.dh[(int64_t)pair * H + f] = acc;
+  }
+}
+
+// ------------------------------------------------------------------ batched reductions
+// dW[g][r][c] (+)= sum_m U[g](m, r) * V[g](m, c) ;  db[g][r] (+)= sum_m U[g](m, r)
+//   U(m, r) = U[g*u_g + m*u_m + r];  V(m, c) = V[g*v_g + m*v_m + c], or, if v_off != nullptr,
+//   V(m, c) = (v_off[m] >= 0 ? V + v_off[m] : v_reset) [g*v_g + c]   (gathered obs rows)
+// Fixed summation order over m (deterministic). Block = 256 threads -> 32 x 32 tile.
+struct OuterArgs {
+  const float* U; int64_t u_g, u_m;
+  const float* V; int64_t v_g, v_m; const int64_t* v_off; const float* v_reset;
+  float* dW; int64_t w_g;   // dW[g*w_g + r*Cc + c]
+  float* db; int64_t b_g;   // db[g*b_g + r] (nullptr: none)
+  int M, R, Cc, accumulate;
+};
+
+__global__ __launch_bounds__(256) void outer_reduce_kernel(OuterArgs a) {
+  __shared__ float su[32][33];
+  __shared__ float svv[32][33];
+  const int g = blockIdx.z;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tr = threadIdx.x / 32, tc = threadIdx.x % 32;  // tr in [0,8): rows tr, tr+8, tr+16, tr+24
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;
+  for (int m0 = 0; m0 < a.M; m0 += 32) {
+    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+      const int mm = k / 32, x = k % 32;
+      const int m = m0 + mm;
+      float u = 0.f, v = 0.f;
+      if (m < a.M) {
+        if (r0 + x < a.R) u = a.U[g * a.u_g + (int64_t)m * a.u_m + r0 + x];
+        if (c0 + x < a.Cc) {
+          if (a.v_off) {
+            const int64_t off = a.v_off[m];
+            const float* base = off >= 0 ? a.V + off : a.v_reset;
+            v = base[g * a.v_g + c0 + x];
+          } else {
+            v = a.V[g * a.v_g + (int64_t)m * a.v_m + c0 + x];
+          }
+        }
+      }
+      su[mm][x] = u;
+      svv[mm][x] = v;
+    }
+    __syncthreads();
+    for (int mm = 0; mm < 32; ++mm) {
+      const float v = svv[mm][tc];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += su[mm][tr + 8 * q] * v;
+    }
+    if (a.db && blockIdx.x == 0 && threadIdx.x < 32)
+      for (int mm = 0; mm < 32; ++mm) accb += su[mm][threadIdx.x];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + tr + 8 * q, c = c0 + tc;
+    if (r < a.R && c < a.Cc) {
+      float* o = a.dW + g * a.w_g + (int64_t)r * a.Cc + c;
+      *o = a.accumulate ? *o + acc[q] : acc[q];
+    }
+  }
+  if (a.db && blockIdx.x == 0 && threadIdx.x < 32 && r0 + threadIdx.x < a.R) {
+    float* o = a.db + g * a.b_g + r0 + threadIdx.x;
+    *o = a.accumulate ? *o + accb : accb;
+  }
+}
+
+// Y[g](m, c) = gate(m, c) * sum_r W[g][r][c] * X[g](m, r)      (batched transpose matvec, gated by x > 0)
+//   W[g*w_g + r*Cc + c], X[g*x_g + m*x_m + r], gate = Z[g*z_g + m*z_m + c] > 0 (if Z), Y[g*y_g + m*y_m + c]
+struct TmvArgs {
+  const float* W; int64_t w_g;
+  const float* X; int64_t x_g, x_m;
+  const float* Z; int64_t z_g, z_m;
+  float* Y; int64_t y_g, y_m;
+  int M, R, Cc;
+};
+
+__global__ __launch_bounds__(256) void tmv_kernel(TmvArgs a) {
+  __shared__ float sx[32][33];
+  __shared__ float sw[32][33];
+  const int g = blockIdx.z;
+  const int m0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tm = threadIdx.x / 32, tc = threadIdx.x % 32;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int rr = 0; rr < a.R; rr += 32) {
+    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+      const int p = k / 32, x = k % 32;
+      const int m = m0 + p, r = rr + x;
+      sx[p][x] = (m < a.M && r < a.R) ? a.X[g * a.x_g + (int64_t)m * a.x_m + r] : 0.f;
+      const int r2 = rr + p, c = c0 + x;
+      sw[p][x] = (r2 < a.R && c < a.Cc) ? a.W[g * a.w_g + (int64_t)r2 * a.Cc + c] : 0.f;
+    }
+    __syncthreads();
+    for (int r = 0; r < 32; ++r) {
+      const float w = sw[r][tc];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += sx[tm + 8 * q][r] * w;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + tm + 8 * q, c = c0 + tc;
+    if (m < a.M && c < a.Cc) {
+      float v = acc[q];
+      if (a.Z && !(a.Z[g * a.z_g + (int64_t)m * a.z_m + c] > 0.f)) v = 0.f;
+      a.Y[g * a.y_g + (int64_t)m * a.y_m + c] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ clip + Adam
+// partial sums of squares of G[0:n_clip] ; also advances the Adam step counter
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* G, int64_t n, float* partials, float* step) {
+  __shared__ float sh[256];
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    acc += G[i] * G[i];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partials[blockIdx.x] = sh[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *step += 1.0f;
+}
+
+// torch.optim.Adam (no amsgrad / weight decay) with clip_grad_norm_ applied to G[0:n_clip]
+__global__ __launch_bounds__(256) void adam_kernel(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip,
+                                                   const float* partials, int n_part, float max_norm, float lr,
+                                                   float b1, float b2, float eps, const float* step, float* norm_out) {
+  __shared__ float s_coef;
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int i = 0; i < n_part; ++i) tot += partials[i];
+    const float norm = sqrtf(tot);
+    s_coef = max_norm > 0.f ? fminf(1.0f, max_norm / (norm + 1e-6f)) : 1.0f;
+    if (norm_out && blockIdx.x == 0) *norm_out = norm;
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  const float t = *step;
+  const float bc1 = 1.0f - powf(b1, t);
+  const float bc2 = 1.0f - powf(b2, t);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float g = G[i];
+    if (i < n_clip) g *= coef;
+    const float mi = m[i] + (g - m[i]) * (1.0f - b1);
+    const float vi = v[i] * b2 + g * g * (1.0f - b2);
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    P[i] = P[i] - step_size * (mi / denom);
+  }
+}
+
+}  // namespace mm
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+int mm_mixer_param_count(int32_t state_dim, int32_t hm, int32_t k1, int32_t n_agents, int64_t* count) {
+  MM_REQUIRE(count && state_dim > 0 && hm > 0 && k1 > 0 && n_agents > 0, "mixer_param_count: bad dims");
+  *count = mm::mix_offsets(state_dim, hm, k1, n_agents).total;
+  return MM_OK;
+}
+int mm_mixer_save_dim(int32_t hm, int32_t k1, int32_t n_agents) { return mm::mix_save_dim(hm, k1, n_agents); }
+int mm_mixer_delta_dim(int32_t hm, int32_t k1, int32_t n_agents) { return mm::mix_delta_dim(hm, k1, n_agents); }
+
+int mm_lrn_gather(int32_t B, int32_t C, int32_t N, int64_t row_stride, int64_t nd, const int64_t* slots,
+                  const int64_t* slot_row, const uint8_t* s_done, const uint8_t* s_act, const float* s_rew,
+                  int64_t* s_off, int64_t* s2_off, int32_t* acts, float* rew, float* done, uint8_t* done8,
+                  mm_stream_t s) {
+  MM_REQUIRE(B > 0 && C > 0 && N > 0, "lrn_gather: bad dims");
+  const int n = B * C;
+  hipLaunchKernelGGL(mm::lrn_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, B, C, N,
+                     row_stride, nd, slots, slot_row, s_done, s_act, s_rew, s_off, s2_off, acts, rew, done, done8);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+typedef struct mm_mix_net {
+  const float* P; const float* q; const int64_t* s_off; const float* h_in; const uint8_t* reset;
+  float* h_out; float* qtot; float* save;
+} mm_mix_net;
+
+int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
+                 const mm_mix_net* nets, int32_t n_nets, mm_stream_t s) {
+  MM_REQUIRE(nets && n_nets >= 1 && n_nets <= 2 && B > 0, "mixer_fwd: bad args");
+  MM_REQUIRE(3 * Hm <= 4096 && N * K1 <= 4096, "mixer_fwd: dims too large");
+  mm::MixFwdArgs a;
+  for (int i = 0; i < 2; ++i) {
+    const mm_mix_net& n = nets[i < n_nets ? i : 0];
+    a.net[i] = {n.P, n.q, n.s_off, n.h_in, n.reset, n.h_out, n.qtot, n.save};
+  }
+  a.obs = obs;
+  a.reset_obs = reset_obs;
+  a.B = B;
+  a.N = N;
+  a.S = S;
+  a.Hm = Hm;
+  a.K1 = K1;
+  const size_t sm = sizeof(float) * ((size_t)S + 9 * Hm + N * K1 + 4 * K1);
+  MM_REQUIRE(sm <= 64 * 1024, "mixer_fwd: state too large for LDS (%zu B)", sm);
+  hipLaunchKernelGGL(mm::mixer_fwd_kernel, dim3(B, n_nets), dim3(256), sm, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, const float* done, const float* isw,
+                const float* qtot, const float* qtot_t, int32_t mix_sum, const float* qa, const float* maxq,
+                float* dq, float* dqa, float* loss_parts, float* td_last, float* loss, mm_stream_t s) {
+  const int n = B * C;
+  hipLaunchKernelGGL(mm::lrn_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, B, C, N, gamma, rew,
+                     done, isw, qtot, qtot_t, mix_sum, qa, maxq, dq, dqa, loss_parts, td_last);
+  MM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(mm::lrn_loss_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, B, C, loss_parts, loss);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mixer_bwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                 const float* qa, const float* dq, const float* done, float* dhm, float* dqa, float* delta,
+                 mm_stream_t s) {
+  mm::MixBwdArgs a = {P, save, qa, dq, done, dhm, dqa, delta, B, N, S, Hm, K1};
+  const size_t sm = sizeof(float) * ((size_t)4 * Hm + N * K1 + 3 * K1);
+  hipLaunchKernelGGL(mm::mixer_bwd_kernel, dim3(B), dim3(256), sm, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_agent_bwd(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B, const float* save,
+                 const int32_t* acts, const float* dqa, const float* done, float* dh, float* dgi, float* dgh,
+                 float* dq, mm_stream_t s) {
+  MM_REQUIRE(d && d->h <= 256, "agent_bwd: H must be <= 256");
+  mm::AgentBwdArgs a = {P, oWq, oWhh, save, acts, dqa, done, dh, dgi, dgh, dq,
+                        B, d->n_agents, d->f1, d->g, d->h, d->n_actions};
+  const int pairs = B * d->n_agents;
+  hipLaunchKernelGGL(mm::agent_bwd_kernel, dim3((pairs + 3) / 4), dim3(256), 0, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+typedef struct mm_outer_args {
+  const float* U; int64_t u_g, u_m;
+  const float* V; int64_t v_g, v_m; const int64_t* v_off; const float* v_reset;
+  float* dW; int64_t w_g;
+  float* db; int64_t b_g;
+  int32_t M, R, Cc, accumulate, groups;
+} mm_outer_args;
+
+int mm_outer_reduce(const mm_outer_args* x, mm_stream_t s) {
+  MM_REQUIRE(x && x->M >= 0 && x->R > 0 && x->Cc > 0 && x->groups > 0, "outer_reduce: bad args");
+  mm::OuterArgs a = {x->U, x->u_g, x->u_m, x->V, x->v_g, x->v_m, x->v_off, x->v_reset, x->dW, x->w_g,
+                     x->db, x->b_g, x->M, x->R, x->Cc, x->accumulate};
+  dim3 grid((x->Cc + 31) / 32, (x->R + 31) / 32, x->groups);
+  hipLaunchKernelGGL(mm::outer_reduce_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+typedef struct mm_tmv_args {
+  const float* W; int64_t w_g;
+  const float* X; int64_t x_g, x_m;
+  const float* Z; int64_t z_g, z_m;
+  float* Y; int64_t y_g, y_m;
+  int32_t M, R, Cc, groups;
+} mm_tmv_args;
+
+int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
+  MM_REQUIRE(x && x->M > 0 && x->R > 0 && x->Cc > 0 && x->groups > 0, "tmv: bad args");
+  mm::TmvArgs a = {x->W, x->w_g, x->X, x->x_g, x->x_m, x->Z, x->z_g, x->z_m, x->Y, x->y_g, x->y_m,
+                   x->M, x->R, x->Cc};
+  dim3 grid((x->Cc + 31) / 32, (x->M + 31) / 32, x->groups);
+  hipLaunchKernelGGL(mm::tmv_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+// clip_grad_norm_(G[0:n_clip], max_norm) then Adam over P[0:n]; partials: >= 256 floats scratch
+int mm_clip_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip, float max_norm, float lr,
+                 float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, mm_stream_t s) {
+  MM_REQUIRE(P && G && m && v && step && partials && n > 0 && n_clip >= 0 && n_clip <= n, "clip_adam: bad args");
+  const int nb = 256;
+  hipLaunchKernelGGL(mm::sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, G, n_clip, partials, step);
+  MM_HIP_CHECK(hipGetLastError());
+  const int nb2 = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(mm::adam_kernel, dim3(nb2), dim3(256), 0, (hipStream_t)s, P, G, m, v, n, n_clip, partials, nb,
+                     max_norm, lr, beta1, beta2, eps, step, norm_out);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+}

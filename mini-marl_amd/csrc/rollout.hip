@@ -12,6 +12,7 @@
 
 namespace mm {
 
+// One thread per (env, agent): coalesced loads/stores; per-env sums over agents through LDS.
 __global__ __launch_bounds__(256) void td_chunk_kernel(int E, int N, float gamma, const float* __restrict__ rew,
                                                        const uint8_t* __restrict__ done,
                                                        const float* __restrict__ q_taken,
@@ -21,24 +22,38 @@ __global__ __launch_bounds__(256) void td_chunk_kernel(int E, int N, float gamma
                                                        float* __restrict__ s_rew, uint8_t* __restrict__ s_done,
                                                        const int64_t* __restrict__ rows,
                                                        uint64_t* __restrict__ counter) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (counter && e == 0) *counter += 1;  // rollout step counter (RNG stream) read by the next step
-  if (e >= E) return;
-  float sr = 0.f, sq = 0.f, st = 0.f;
-  const int64_t row = rows ? rows[e] : (int64_t)e;
-  for (int k = 0; k < N; ++k) {
+  __shared__ float sh[3][256];
+  const int epb = blockDim.x / N;                    // envs per block
+  const int le = threadIdx.x / N, k = threadIdx.x % N;
+  const int e = blockIdx.x * epb + le;
+  if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;  // RNG stream of the next step
+  const bool on = le < epb && e < E;
+  float r = 0.f, q = 0.f, m = 0.f;
+  if (on) {
     const int64_t o = (int64_t)e * N + k;
-    const float r = rew[o];
-    sr += r;
-    sq += q_taken[o];
-    st += maxq_next[o];
+    const int64_t row = rows ? rows[e] : (int64_t)e;
+    r = rew[o];
+    q = q_taken[o];
+    m = maxq_next[o];
     if (s_act) s_act[(row * C + t) * N + k] = (uint8_t)act[o];
     if (s_rew) s_rew[(row * C + t) * N + k] = r;
+    if (k == 0 && s_done) s_done[row * C + t] = done[e];
   }
-  const float d = done[e] ? 1.0f : 0.0f;
-  const float td = fabsf(sr + (1.0f - d) * gamma * st - sq);
-  chunk_td[e] = (t == 0 ? 0.0f : chunk_td[e]) + td;
-  if (s_done) s_done[row * C + t] = done[e];
+  sh[0][threadIdx.x] = r;
+  sh[1][threadIdx.x] = q;
+  sh[2][threadIdx.x] = m;
+  __syncthreads();
+  if (on && k == 0) {
+    float sr = 0.f, sq = 0.f, st = 0.f;   // agent order, like the reference's sum over dim 1
+    for (int j = 0; j < N; ++j) {
+      sr += sh[0][threadIdx.x + j];
+      sq += sh[1][threadIdx.x + j];
+      st += sh[2][threadIdx.x + j];
+    }
+    const float d = done[e] ? 1.0f : 0.0f;
+    const float td = fabsf(sr + (1.0f - d) * gamma * st - sq);
+    chunk_td[e] = (t == 0 ? 0.0f : chunk_td[e]) + td;
+  }
 }
 
 // chunk begin: obs_cur [E][ND] -> store slot 0 of each env's staging row
@@ -63,8 +78,10 @@ int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const f
   MM_REQUIRE(rew && done && q_taken && max_q_next && act && chunk_td, "td_chunk_step: null argument");
   MM_REQUIRE(step_in_chunk >= 0 && step_in_chunk < chunk_len, "td_chunk_step: bad step");
   if (n_envs <= 0) return MM_OK;
-  const int threads = 256;
-  const int blocks = (int)((n_envs + threads - 1) / threads);
+  MM_REQUIRE(n_agents >= 1 && n_agents <= 256, "td_chunk_step: n_agents must be in [1,256]");
+  const int epb = 256 / n_agents;
+  const int threads = epb * n_agents;
+  const int blocks = (int)((n_envs + epb - 1) / epb);
   hipLaunchKernelGGL(mm::td_chunk_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)s, (int)n_envs, n_agents,
                      gamma, rew, done, q_taken, max_q_next, act, chunk_td, step_in_chunk, chunk_len, store_act,
                      store_rew, store_done, rows, counter);

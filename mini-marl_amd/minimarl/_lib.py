@@ -39,6 +39,7 @@ class QFwdIO(ctypes.Structure):
         ("act_in", c_vp), ("act_se", c_i64),
         ("qsel_out", c_vp),
         ("eps_ptr", c_vp), ("counter_ptr", c_vp),
+        ("save", c_vp),
     ]
 
 
@@ -119,3 +120,41 @@ def check(rc, what=""):
     if rc != 0:
         msg = lib().mm_last_error().decode(errors="replace")
         raise RuntimeError(f"minimarl {what} failed (rc={rc}): {msg}")
+
+
+class MixNetIO(ctypes.Structure):
+    _fields_ = [("P", c_vp), ("q", c_vp), ("s_off", c_vp), ("h_in", c_vp), ("reset", c_vp), ("h_out", c_vp),
+                ("qtot", c_vp), ("save", c_vp)]
+
+
+class OuterArgs(ctypes.Structure):
+    _fields_ = [("U", c_vp), ("u_g", c_i64), ("u_m", c_i64),
+                ("V", c_vp), ("v_g", c_i64), ("v_m", c_i64), ("v_off", c_vp), ("v_reset", c_vp),
+                ("dW", c_vp), ("w_g", c_i64), ("db", c_vp), ("b_g", c_i64),
+                ("M", c_i32), ("R", c_i32), ("Cc", c_i32), ("accumulate", c_i32), ("groups", c_i32)]
+
+
+class TmvArgs(ctypes.Structure):
+    _fields_ = [("W", c_vp), ("w_g", c_i64), ("X", c_vp), ("x_g", c_i64), ("x_m", c_i64),
+                ("Z", c_vp), ("z_g", c_i64), ("z_m", c_i64), ("Y", c_vp), ("y_g", c_i64), ("y_m", c_i64),
+                ("M", c_i32), ("R", c_i32), ("Cc", c_i32), ("groups", c_i32)]
+
+
+_SIGS += [
+    ("mm_mixer_param_count", c_i32, [c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_i64)]),
+    ("mm_mixer_save_dim", c_i32, [c_i32, c_i32, c_i32]),
+    ("mm_mixer_delta_dim", c_i32, [c_i32, c_i32, c_i32]),
+    ("mm_lrn_gather", c_i32, [c_i32, c_i32, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                              c_vp, c_vp, c_vp, c_vp]),
+    ("mm_mixer_fwd", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(MixNetIO), c_i32, c_vp]),
+    ("mm_lrn_loss", c_i32, [c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
+                            c_vp, c_vp, c_vp, c_vp]),
+    ("mm_mixer_bwd", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_vp]),
+    ("mm_agent_bwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_vp, c_vp, c_vp, c_vp]),
+    ("mm_outer_reduce", c_i32, [ctypes.POINTER(OuterArgs), c_vp]),
+    ("mm_tmv", c_i32, [ctypes.POINTER(TmvArgs), c_vp]),
+    ("mm_clip_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
+                             c_vp, c_vp]),
+]

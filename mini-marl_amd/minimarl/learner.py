@@ -1,0 +1,362 @@
+"""Device learner for chunked-BPTT QMIX / VDN (csrc/learner.hip + the fused agent forward).
+
+Mirrors ``Train_dqn`` (qmix/_train.py:7-121) and ``Target_Dqn`` (vdn/_train.py:184-235):
+one ``update()`` = PER sample of B chunks x C steps, behavior + target agent nets and
+mixers forward over the C steps, loss, backward through time, clip_grad_norm_ (QMIX:
+agent params only, qmix/_train.py:111-115; VDN: all), Adam, priority update with the
+last step's |y - Q_tot|. Everything is enqueued on the current HIP stream with no host
+sync, so an update can be captured as one HIP graph and replayed.
+
+Parameters live in ONE flat fp32 buffer ``P = [agent theta | mixer phi]`` (grads,
+Adam moments alike), the layout the RCCL gradient all-reduce works on.
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from ._lib import (MM_Q_GATHER, MM_Q_MAX, MixNetIO, OuterArgs, QFwdIO, TmvArgs, c_i64, check, lib)
+from .qnet import KEYS as AGENT_KEYS
+from .qnet import AgentQNet, ptr, stream_handle
+
+MIX_KEYS = ["gWih", "gWhh", "gbih", "gbhh", "w1W", "w1b", "w2W", "w2b", "b1W", "b1b", "b2aW", "b2ab", "b2bW",
+            "b2bb"]
+_MIX_FMT = {
+    "gWih": "gru.weight_ih", "gWhh": "gru.weight_hh", "gbih": "gru.bias_ih", "gbhh": "gru.bias_hh",
+    "w1W": "hyper_net_weight_1.weight", "w1b": "hyper_net_weight_1.bias",
+    "w2W": "hyper_net_weight_2.weight", "w2b": "hyper_net_weight_2.bias",
+    "b1W": "hyper_net_bias_1.weight", "b1b": "hyper_net_bias_1.bias",
+    "b2aW": "hyper_net_bias_2.0.weight", "b2ab": "hyper_net_bias_2.0.bias",
+    "b2bW": "hyper_net_bias_2.2.weight", "b2bb": "hyper_net_bias_2.2.bias",
+}
+
+
+class Mixer:
+    """QMIX Mix_Net parameters (qmix/_network.py:172-220): GRUCell(N*D -> Hm) + hypernetworks."""
+
+    def __init__(self, n_agents, state_dim, hm=32, k1=32, device="cuda", flat=None, seed=None):
+        self.N, self.S, self.Hm, self.K1 = n_agents, state_dim, hm, k1
+        self.device = torch.device(device)
+        n = c_i64()
+        check(lib().mm_mixer_param_count(state_dim, hm, k1, n_agents, ctypes.byref(n)), "mixer_param_count")
+        self.n_params = n.value
+        self.flat = flat if flat is not None else torch.zeros(self.n_params, device=self.device)
+        assert self.flat.numel() == self.n_params
+        sh = self.shapes()
+        self.offs = [0]
+        for k in MIX_KEYS:
+            self.offs.append(self.offs[-1] + int(np.prod(sh[k])))
+        assert self.offs[-1] == self.n_params
+        if seed is not None:
+            self.init_default(seed)
+
+    def shapes(self):
+        N, S, Hm, K1 = self.N, self.S, self.Hm, self.K1
+        return {"gWih": (3 * Hm, S), "gWhh": (3 * Hm, Hm), "gbih": (3 * Hm,), "gbhh": (3 * Hm,),
+                "w1W": (N * K1, Hm), "w1b": (N * K1,), "w2W": (K1, Hm), "w2b": (K1,), "b1W": (K1, Hm),
+                "b1b": (K1,), "b2aW": (K1, Hm), "b2ab": (K1,), "b2bW": (1, K1), "b2bb": (1,)}
+
+    def view(self, key, t=None):
+        t = self.flat if t is None else t
+        i = MIX_KEYS.index(key)
+        return t[self.offs[i]:self.offs[i + 1]].view(self.shapes()[key])
+
+    def init_default(self, seed):
+        g = torch.Generator().manual_seed(int(seed))
+        fan = {"gWih": self.Hm, "gWhh": self.Hm, "gbih": self.Hm, "gbhh": self.Hm, "w1W": self.Hm,
+               "w1b": self.Hm, "w2W": self.Hm, "w2b": self.Hm, "b1W": self.Hm, "b1b": self.Hm, "b2aW": self.Hm,
+               "b2ab": self.Hm, "b2bW": self.K1, "b2bb": self.K1}
+        host = torch.empty(self.n_params)
+        for i, k in enumerate(MIX_KEYS):
+            b = 1.0 / math.sqrt(fan[k])
+            host[self.offs[i]:self.offs[i + 1]] = (torch.rand(self.offs[i + 1] - self.offs[i], generator=g) * 2 - 1) * b
+        self.flat.copy_(host.to(self.device))
+
+    def load_reference_state(self, sd, prefix=""):
+        host = torch.cat([torch.as_tensor(np.asarray(sd[prefix + _MIX_FMT[k]]), dtype=torch.float32).reshape(-1)
+                          for k in MIX_KEYS])
+        self.flat.copy_(host.to(self.device))
+
+    def state_dict(self):
+        host = self.flat.detach().cpu()
+        return {_MIX_FMT[k]: self.view(k, host).clone() for k in MIX_KEYS}
+
+
+class QLearner:
+    """mode "qmix" (Train_dqn) or "vdn" (Target_Dqn: Q_tot = sum_i Q_i, no mixer)."""
+
+    def __init__(self, behavior, target, mixer=None, target_mixer=None, batch=32, chunk=10, gamma=0.99, lr=1e-3,
+                 grad_clip=5.0, betas=(0.9, 0.999), adam_eps=1e-8, mode="qmix", clip_mixer=False, device="cuda"):
+        assert mode in ("qmix", "vdn")
+        self.mode = mode
+        self.dev = torch.device(device)
+        self.beh, self.tgt = behavior, target
+        self.mix, self.tmix = mixer, target_mixer
+        if mode == "qmix":
+            assert mixer is not None and target_mixer is not None
+        self.B, self.C = int(batch), int(chunk)
+        self.gamma, self.lr, self.clip = float(gamma), float(lr), float(grad_clip)
+        self.b1, self.b2, self.aeps = float(betas[0]), float(betas[1]), float(adam_eps)
+        d = behavior
+        self.N, self.D, self.F1, self.G, self.H, self.A = d.N, d.D, d.F1, d.G, d.H, d.A
+        self.SD = self.F1 + self.G + 6 * self.H
+        # one flat buffer [theta | phi]; the nets become views into it
+        n_t = d.n_params
+        n_m = mixer.n_params if mixer is not None else 0
+        self.n_agent, self.n = n_t, n_t + n_m
+        self.P = torch.empty(self.n, device=self.dev)
+        self.P[:n_t].copy_(behavior.flat)
+        behavior.flat = self.P[:n_t]
+        behavior.mark_dirty()
+        if mixer is not None:
+            self.P[n_t:].copy_(mixer.flat)
+            mixer.flat = self.P[n_t:]
+        self.Gr = torch.zeros(self.n, device=self.dev)
+        self.m = torch.zeros(self.n, device=self.dev)
+        self.v = torch.zeros(self.n, device=self.dev)
+        self.step_dev = torch.zeros(1, device=self.dev)
+        self.partials = torch.zeros(256, device=self.dev)
+        self.norm = torch.zeros(1, device=self.dev)
+        self.n_clip = self.n if (mode == "vdn" or clip_mixer) else n_t
+        self._alloc()
+        self.updates = 0
+
+    # ------------------------------------------------------------------ workspace
+    def _alloc(self):
+        B, C, N, H, A, dev = self.B, self.C, self.N, self.H, self.A, self.dev
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.s_off = torch.zeros(C * B, dtype=torch.int64, device=dev)
+        self.s2_off = torch.zeros(C * B, dtype=torch.int64, device=dev)
+        self.acts = torch.zeros(C * B * N, dtype=torch.int32, device=dev)
+        self.rew = torch.zeros(C * B * N, **f32)
+        self.done = torch.zeros(C * B, **f32)
+        self.done8 = torch.zeros(C * B, dtype=torch.uint8, device=dev)
+        self.isw = torch.ones(B, **f32)
+        self.ones8 = torch.ones(B, dtype=torch.uint8, device=dev)
+        self.ones_f = torch.ones(B, **f32)
+        self.hb = torch.zeros(2, B, N, H, **f32)
+        self.ht = torch.zeros(2, B, N, H, **f32)
+        self.asave = torch.zeros(C, B, N, self.SD, **f32)
+        self.qa = torch.zeros(C, B, N, **f32)
+        self.maxq = torch.zeros(C, B, N, **f32)
+        self.qtot = torch.zeros(C, B, **f32)
+        self.qtot_t = torch.zeros(C, B, **f32)
+        self.dq = torch.zeros(C, B, **f32)
+        self.dqa = torch.zeros(C, B, N, **f32)
+        self.loss_parts = torch.zeros(C, B, **f32)
+        self.td_last = torch.zeros(B, **f32)
+        self.loss = torch.zeros(1, **f32)
+        self.dh = torch.zeros(B, N, H, **f32)
+        self.dgi = torch.zeros(C, B, N, 3 * H, **f32)
+        self.dgh = torch.zeros(C, B, N, 3 * H, **f32)
+        self.dqv = torch.zeros(C, B, N, A, **f32)
+        self.dpre2 = torch.zeros(C, B, N, self.G, **f32)
+        self.dpre1 = torch.zeros(C, B, N, self.F1, **f32)
+        self.nodes = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.slots = torch.zeros(B, dtype=torch.int64, device=dev)
+        if self.mode == "qmix":
+            Hm, K1 = self.mix.Hm, self.mix.K1
+            self.MSD = lib().mm_mixer_save_dim(Hm, K1, N)
+            self.MDD = lib().mm_mixer_delta_dim(Hm, K1, N)
+            self.hm = torch.zeros(2, B, Hm, **f32)
+            self.hmt = torch.zeros(2, B, Hm, **f32)
+            self.msave = torch.zeros(C, B, self.MSD, **f32)
+            self.mdelta = torch.zeros(C, B, self.MDD, **f32)
+            self.dhm = torch.zeros(B, Hm, **f32)
+
+    # ------------------------------------------------------------------ batch in
+    def gather(self, per, store):
+        """PER slots (self.slots) -> chunk-store rows -> offsets / actions / rewards / dones."""
+        check(lib().mm_lrn_gather(self.B, self.C, self.N, store.row_stride, self.N * self.D, ptr(self.slots),
+                                  ctypes.c_void_p(per.slot_rows_ptr()), ptr(store.done), ptr(store.act),
+                                  ptr(store.rew), ptr(self.s_off), ptr(self.s2_off), ptr(self.acts), ptr(self.rew),
+                                  ptr(self.done), ptr(self.done8), stream_handle(self.dev)), "lrn_gather")
+
+    def load_batch(self, states, actions, rewards, next_states, dones, is_weight):
+        """Reference-shaped batch (Replay_buffer.sample outputs, qmix/replay_buffer/per.py:77-81) as the
+        learner input: obs rows are laid out in a private buffer and addressed through the offsets."""
+        B, C, N, D = self.B, self.C, self.N, self.D
+        st = torch.as_tensor(states, dtype=torch.float32).to(self.dev).contiguous()
+        ns = torch.as_tensor(next_states, dtype=torch.float32).to(self.dev).contiguous()
+        assert st.shape == (B, C, N, D) and ns.shape == (B, C, N, D)
+        self._obs_buf = torch.cat([st.reshape(-1), ns.reshape(-1)])
+        t = torch.arange(C, device=self.dev).view(C, 1)
+        b = torch.arange(B, device=self.dev).view(1, B)
+        base = (b * C + t) * (N * D)
+        self.s_off.copy_(base.reshape(-1))
+        self.s2_off.copy_((base + B * C * N * D).reshape(-1))
+        self.acts.copy_(torch.as_tensor(actions).to(self.dev).permute(1, 0, 2).reshape(-1).to(torch.int32))
+        self.rew.copy_(torch.as_tensor(rewards, dtype=torch.float32).to(self.dev).permute(1, 0, 2).reshape(-1))
+        dn = torch.as_tensor(dones, dtype=torch.float32).to(self.dev).view(B, C).t().reshape(-1)
+        self.done.copy_(dn)
+        self.done8.copy_((dn > 0.5).to(torch.uint8))
+        self.isw.copy_(torch.as_tensor(is_weight, dtype=torch.float32).to(self.dev).view(-1))
+        self._obs_ptr = self._obs_buf
+        self._reset_obs = self._obs_buf      # never addressed (no -1 offsets in an explicit batch)
+
+    # ------------------------------------------------------------------ the update
+    def train_step(self, obs_base, reset_obs_ptr):
+        """Forward C steps, loss, BPTT, clip, Adam on the gathered batch (all async)."""
+        L, s = lib(), stream_handle(self.dev)
+        B, C, N, H, D = self.B, self.C, self.N, self.H, self.D
+        CB = C * B
+        self.beh.pack(s)
+        self.tgt.pack(s)
+        obs_p = ctypes.c_void_p(obs_base) if isinstance(obs_base, int) else ptr(obs_base)
+        reset_p = ctypes.c_void_p(reset_obs_ptr) if isinstance(reset_obs_ptr, int) else ptr(reset_obs_ptr)
+        ND = N * D
+        # ---- forward over the chunk (behavior GATHER + save, target MAX) in dual launches
+        for t in range(C):
+            ib, it = QFwdIO(), QFwdIO()
+            for io, off, h in ((ib, self.s_off, self.hb), (it, self.s2_off, self.ht)):
+                io.obs, io.obs_se, io.obs_sa, io.obs_off = obs_p.value, 1, D, 0
+                io.obs_row = off.data_ptr() + 8 * t * B
+                io.reset_obs = reset_p.value
+                io.h_in = h[t % 2].data_ptr()
+                io.h_out = h[(t + 1) % 2].data_ptr()
+                io.hin_se = io.hout_se = N * H
+                io.hin_sa = io.hout_sa = H
+                io.hin_sf = io.hout_sf = 1
+                io.reset = self.ones8.data_ptr() if t == 0 else self.done8.data_ptr() + (t - 1) * B
+            ib.mode = MM_Q_GATHER
+            ib.act_in, ib.act_se = self.acts.data_ptr() + 4 * t * B * N, N
+            ib.qsel_out = self.qa[t].data_ptr()
+            ib.save = self.asave[t].data_ptr()
+            it.mode = MM_Q_MAX
+            it.qsel_out = self.maxq[t].data_ptr()
+            check(L.mm_agent_q_fwd2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
+                                    ptr(self.tgt.packed), ctypes.byref(it), B, s), "learner fwd")
+            if self.mode == "qmix":
+                mx = self.mix
+                nets = (MixNetIO * 2)()
+                for k, (P, q, off, h, qt, sv) in enumerate(
+                        ((self.mix.flat, self.qa[t], self.s_off, self.hm, self.qtot[t], self.msave[t]),
+                         (self.tmix.flat, self.maxq[t], self.s2_off, self.hmt, self.qtot_t[t], None))):
+                    n = nets[k]
+                    n.P, n.q = P.data_ptr(), q.data_ptr()
+                    n.s_off = off.data_ptr() + 8 * t * B
+                    n.h_in, n.h_out = h[t % 2].data_ptr(), h[(t + 1) % 2].data_ptr()
+                    n.reset = self.ones8.data_ptr() if t == 0 else self.done8.data_ptr() + (t - 1) * B
+                    n.qtot = qt.data_ptr()
+                    n.save = sv.data_ptr() if sv is not None else None
+                check(L.mm_mixer_fwd(B, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, nets, 2, s), "mixer fwd")
+        # ---- loss, dQ_tot, priorities
+        check(L.mm_lrn_loss(B, C, N, self.gamma, ptr(self.rew), ptr(self.done), ptr(self.isw), ptr(self.qtot),
+                            ptr(self.qtot_t), int(self.mode == "vdn"), ptr(self.qa), ptr(self.maxq), ptr(self.dq),
+                            ptr(self.dqa), ptr(self.loss_parts), ptr(self.td_last), ptr(self.loss), s), "loss")
+        # ---- backward through time (data-gradient chains only)
+        o = self.beh.offs
+        P = self.P
+        for t in range(C - 1, -1, -1):
+            dn = self.ones_f if t == C - 1 else self.done[t * B:(t + 1) * B]
+            if self.mode == "qmix":
+                mx = self.mix
+                check(L.mm_mixer_bwd(B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.msave[t]), ptr(self.qa[t]),
+                                     ptr(self.dq[t]), ptr(dn), ptr(self.dhm), ptr(self.dqa[t]), ptr(self.mdelta[t]),
+                                     s), "mixer bwd")
+            check(L.mm_agent_bwd(ctypes.byref(self.beh.dims), ptr(P), o[8], o[5], B, ptr(self.asave[t]),
+                                 ctypes.c_void_p(self.acts.data_ptr() + 4 * t * B * N), ptr(self.dqa[t]), ptr(dn),
+                                 ptr(self.dh), ptr(self.dgi[t]), ptr(self.dgh[t]), ptr(self.dqv[t]), s), "agent bwd")
+        # ---- deferred weight gradients: batched over all C*B rows, grouped by agent
+        self._agent_wgrad(L, s, obs_p, reset_p, CB)
+        if self.mode == "qmix":
+            self._mixer_wgrad(L, s, obs_p, reset_p, CB)
+        # ---- clip_grad_norm_ + Adam, then repack the behavior fragments for the next forward
+        check(L.mm_clip_adam(ptr(self.P), ptr(self.Gr), ptr(self.m), ptr(self.v), self.n, self.n_clip, self.clip,
+                             self.lr, self.b1, self.b2, self.aeps, ptr(self.step_dev), ptr(self.partials),
+                             ptr(self.norm), s), "clip_adam")
+        self.beh.mark_dirty()
+        self.beh.pack(s)
+        self.updates += 1
+
+    def _outer(self, L, s, U, u_g, u_m, V, v_g, v_m, dW, w_g, db, b_g, M, R, Cc, groups, v_off=None, v_reset=None):
+        a = OuterArgs()
+        a.U, a.u_g, a.u_m = U, u_g, u_m
+        a.V, a.v_g, a.v_m = V, v_g, v_m
+        a.v_off = v_off
+        a.v_reset = v_reset
+        a.dW, a.w_g = dW, w_g
+        a.db, a.b_g = db, b_g
+        a.M, a.R, a.Cc, a.accumulate, a.groups = M, R, Cc, 0, groups
+        check(L.mm_outer_reduce(ctypes.byref(a), s), "outer_reduce")
+
+    def _tmv(self, L, s, W, w_g, X, x_g, x_m, Z, z_g, z_m, Y, y_g, y_m, M, R, Cc, groups):
+        a = TmvArgs()
+        a.W, a.w_g, a.X, a.x_g, a.x_m, a.Z, a.z_g, a.z_m, a.Y, a.y_g, a.y_m = W, w_g, X, x_g, x_m, Z, z_g, z_m, Y, y_g, y_m
+        a.M, a.R, a.Cc, a.groups = M, R, Cc, groups
+        check(L.mm_tmv(ctypes.byref(a), s), "tmv")
+
+    def _agent_wgrad(self, L, s, obs_p, reset_p, M):
+        N, D, F1, G, H, A, SD = self.N, self.D, self.F1, self.G, self.H, self.A, self.SD
+        o = self.beh.offs          # W1 b1 W2 b2 Wih Whh bih bhh Wq bq
+        gp, pp = self.Gr.data_ptr(), self.P.data_ptr()
+        sv = self.asave.data_ptr()
+        f = 4
+        # Wq, bq <- dq (one-hot) x h_out
+        self._outer(L, s, self.dqv.data_ptr(), A, N * A, sv + f * (F1 + G + 5 * H), SD, N * SD,
+                    gp + f * o[8], A * H, gp + f * o[9], A, M, A, H, N)
+        # Whh, bhh <- dgh x h_in
+        self._outer(L, s, self.dgh.data_ptr(), 3 * H, N * 3 * H, sv + f * (F1 + G), SD, N * SD,
+                    gp + f * o[5], 3 * H * H, gp + f * o[7], 3 * H, M, 3 * H, H, N)
+        # Wih, bih <- dgi x x2
+        self._outer(L, s, self.dgi.data_ptr(), 3 * H, N * 3 * H, sv + f * F1, SD, N * SD,
+                    gp + f * o[4], 3 * H * G, gp + f * o[6], 3 * H, M, 3 * H, G, N)
+        # dpre2 = (x2 > 0) * Wih^T dgi
+        self._tmv(L, s, pp + f * o[4], 3 * H * G, self.dgi.data_ptr(), 3 * H, N * 3 * H, sv + f * F1, SD, N * SD,
+                  self.dpre2.data_ptr(), G, N * G, M, 3 * H, G, N)
+        # W2, b2 <- dpre2 x x1
+        self._outer(L, s, self.dpre2.data_ptr(), G, N * G, sv, SD, N * SD,
+                    gp + f * o[2], G * F1, gp + f * o[3], G, M, G, F1, N)
+        # dpre1 = (x1 > 0) * W2^T dpre2
+        self._tmv(L, s, pp + f * o[2], G * F1, self.dpre2.data_ptr(), G, N * G, sv, SD, N * SD,
+                  self.dpre1.data_ptr(), F1, N * F1, M, G, F1, N)
+        # W1, b1 <- dpre1 x obs (gathered through the s_t offsets)
+        self._outer(L, s, self.dpre1.data_ptr(), F1, N * F1, obs_p.value, D, 0,
+                    gp + f * o[0], F1 * D, gp + f * o[1], F1, M, F1, D, N,
+                    v_off=self.s_off.data_ptr(), v_reset=reset_p.value)
+
+    def _mixer_wgrad(self, L, s, obs_p, reset_p, M):
+        mx = self.mix
+        Hm, K1, N, S = mx.Hm, mx.K1, self.N, mx.S
+        MSD, MDD = self.MSD, self.MDD
+        base = self.Gr.data_ptr() + 4 * self.n_agent
+        mo = {k: base + 4 * mx.offs[i] for i, k in enumerate(MIX_KEYS)}
+        dl, sv = self.mdelta.data_ptr(), self.msave.data_ptr()
+        f = 4
+        hm1 = sv + f * 5 * Hm
+        # GRU input weights <- dgi x state (gathered), recurrent <- dgh x hm0
+        self._outer(L, s, dl, 0, MDD, obs_p.value, 0, 0, mo["gWih"], 0, mo["gbih"], 0, M, 3 * Hm, S, 1,
+                    v_off=self.s_off.data_ptr(), v_reset=reset_p.value)
+        self._outer(L, s, dl + f * 3 * Hm, 0, MDD, sv, 0, MSD, mo["gWhh"], 0, mo["gbhh"], 0, M, 3 * Hm, Hm, 1)
+        # hypernetworks <- deltas x hm1
+        self._outer(L, s, dl + f * 6 * Hm, 0, MDD, hm1, 0, MSD, mo["w1W"], 0, mo["w1b"], 0, M, N * K1, Hm, 1)
+        self._outer(L, s, dl + f * (6 * Hm + N * K1), 0, MDD, hm1, 0, MSD, mo["b1W"], 0, mo["b1b"], 0, M, K1, Hm, 1)
+        self._outer(L, s, dl + f * (6 * Hm + N * K1 + K1), 0, MDD, hm1, 0, MSD, mo["w2W"], 0, mo["w2b"], 0, M, K1,
+                    Hm, 1)
+        self._outer(L, s, dl + f * (6 * Hm + N * K1 + 2 * K1), 0, MDD, hm1, 0, MSD, mo["b2aW"], 0, mo["b2ab"], 0, M,
+                    K1, Hm, 1)
+        # final b2 layer <- dQ x relu(b2 hidden)
+        self._outer(L, s, dl + f * (6 * Hm + N * K1 + 3 * K1), 0, MDD, sv + f * (6 * Hm + N * K1 + 2 * K1), 0, MSD,
+                    mo["b2bW"], 0, mo["b2bb"], 0, M, 1, K1, 1)
+
+    # ------------------------------------------------------------------ full update from the PER
+    def update(self, per, store, reset_obs_ptr, fracs=None, seed=0, counter=0):
+        """One reference update iteration: sample -> gather -> train -> priority update."""
+        L, s = lib(), stream_handle(self.dev)
+        if fracs is not None:
+            fr = torch.as_tensor(fracs, dtype=torch.float64).to(self.dev).contiguous()
+            check(L.mm_per_sample(per._h, self.B, ptr(fr), ptr(self.nodes), ptr(self.slots), ptr(self.isw), s),
+                  "per_sample")
+        else:
+            check(L.mm_per_sample_rng(per._h, self.B, seed, counter, ptr(self.nodes), ptr(self.slots),
+                                      ptr(self.isw), s), "per_sample_rng")
+        self.gather(per, store)
+        self.train_step(store.obs, reset_obs_ptr)
+        check(L.mm_per_update(per._h, ptr(self.nodes), ptr(self.td_last), self.B, s), "per_update")
+
+    def sync_target(self, mixer=False):
+        """target <- behavior (qmix/main.py:255-256 syncs the agent net only; mixer=True also the mixer)."""
+        self.tgt.copy_from(self.beh)
+        if mixer and self.mix is not None:
+            self.tmix.flat.copy_(self.mix.flat)

@@ -42,7 +42,7 @@ def ptr(t):
 class AgentQNet:
     """Device-resident parameters of N per-agent Q-networks + their MFMA fragment image."""
 
-    def __init__(self, n_agents, obs_dim, n_actions, f1=64, g=32, h=32, device="cuda", seed=None):
+    def __init__(self, n_agents, obs_dim, n_actions, f1=64, g=32, h=32, device="cuda", seed=None, flat=None):
         self.N, self.D, self.A, self.F1, self.G, self.H = n_agents, obs_dim, n_actions, f1, g, h
         self.device = torch.device(device)
         self.dims = QnetDims(n_agents, obs_dim, f1, g, h, n_actions)
@@ -50,7 +50,11 @@ class AgentQNet:
         check(lib().mm_qnet_param_offsets(ctypes.byref(self.dims), offs), "qnet_param_offsets")
         self.offs = list(offs)
         self.n_params = self.offs[10]
-        self.flat = torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
+        if flat is not None:          # a view into a larger buffer (e.g. the learner's [agent | mixer] params)
+            assert flat.numel() == self.n_params and flat.is_contiguous() and flat.dtype == torch.float32
+            self.flat = flat
+        else:
+            self.flat = torch.zeros(self.n_params, dtype=torch.float32, device=self.device)
         n_packed = lib().mm_qnet_packed_count(ctypes.byref(self.dims))
         if n_packed < 0:
             check(-22, "qnet_packed_count")

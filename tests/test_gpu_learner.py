@@ -1,0 +1,146 @@
+"""GPU parity of the HIP learner (QMIX Train_dqn / VDN Target_Dqn) against the reference's own update.
+
+Golden fixtures tests/golden/{qmix,vdn}_train.npz hold the reference's weights, its sampled
+batch and its outputs after ONE update. Tolerances (fp32, 10-step BPTT): loss rtol 1e-4;
+gradients |g - g_ref| <= 2e-4 * max|g_ref| + 1e-3 * |g_ref|; new priorities rtol 1e-4;
+post-Adam params atol 2e-6 where |g_ref| > 1e-4 * max|g_ref| (Adam's first step is
+lr * sign(g), so near-zero gradients are compared through the gradient check instead).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nets
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _grad_view(learner, key):
+    return learner.beh.view(key, learner.Gr[:learner.n_agent])
+
+
+def _check_grads(g_dev, g_ref):
+    scale = np.abs(g_ref).max()
+    np.testing.assert_array_less(np.abs(g_dev - g_ref), 2e-4 * scale + 1e-3 * np.abs(g_ref) + 1e-12)
+
+
+def _make(fx, style, mode):
+    from minimarl.learner import Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    pre = {"qmix": ("before_q.", "target_q."), "vdn": ("before.", "target.")}[mode]
+    P = nets.agent_from_state(fx, pre[0], style)
+    N, F1, D = P["W1"].shape
+    A = P["Wq"].shape[1]
+    beh = AgentQNet(N, D, A, 64, 32, 32, DEV)
+    beh.load_reference_state(fx, pre[0], style)
+    tgt = AgentQNet(N, D, A, 64, 32, 32, DEV)
+    tgt.load_reference_state(fx, pre[1], style)
+    mix = tmix = None
+    if mode == "qmix":
+        mix = Mixer(N, N * D, 32, 32, DEV)
+        mix.load_reference_state(fx, "before_m.")
+        tmix = Mixer(N, N * D, 32, 32, DEV)
+        tmix.load_reference_state(fx, "target_m.")
+    L = QLearner(beh, tgt, mix, tmix, batch=32, chunk=10, gamma=float(fx["gamma"]), lr=float(fx["lr"]),
+                 grad_clip=float(fx["grad_clip"]), mode=mode, device=DEV)
+    L.load_batch(fx["states"], fx["actions"], fx["rewards"], fx["next_states"], fx["dones"], fx["is_weight"])
+    return L, P
+
+
+@pytest.mark.parametrize("mode", ["qmix", "vdn"])
+def test_learner_matches_reference_update(golden, mode):
+    fx = golden(mode + "_train")
+    style = "qmix" if mode == "qmix" else "vdn"
+    L, P = _make(fx, style, mode)
+    L.train_step(L._obs_buf, L._obs_buf)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(float(L.loss.item()), float(fx["loss"]), rtol=1e-4)
+    np.testing.assert_allclose(L.td_last.cpu().numpy(), fx["new_td"], rtol=1e-4, atol=1e-4)
+    # gradients (the reference captured them after clip_grad_norm_; apply our clip coefficient)
+    norm = float(L.norm.item())
+    coef = min(1.0, float(fx["grad_clip"]) / (norm + 1e-6))
+    N = P["W1"].shape[0]
+    for i in range(N):
+        for k, key in enumerate(nets.AGENT_KEYS):
+            g_ref = fx[f"g0.{10 * i + k}"]
+            g_dev = _grad_view(L, key)[i].cpu().numpy() * coef
+            _check_grads(g_dev, g_ref)
+    after = nets.agent_from_state(fx, "after_q." if mode == "qmix" else "after.", style)
+    for key in nets.AGENT_KEYS:
+        g_all = np.stack([fx[f"g0.{10 * i + nets.AGENT_KEYS.index(key)}"] for i in range(N)])
+        sel = np.abs(g_all) > 1e-4 * np.abs(g_all).max()
+        got = L.beh.view(key).cpu().numpy()
+        np.testing.assert_allclose(got[sel], after[key].numpy()[sel], rtol=0, atol=2e-6)
+    if mode == "qmix":
+        from minimarl.learner import MIX_KEYS
+        afterM = nets.mixer_from_state(fx, "after_m.")
+        for j, key in enumerate(MIX_KEYS):
+            g_ref = fx[f"g1.{j}"]
+            g_dev = L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy()   # mixer grads are not clipped
+            _check_grads(g_dev, g_ref)
+            sel = np.abs(g_ref) > 1e-4 * np.abs(g_ref).max()
+            np.testing.assert_allclose(L.mix.view(key).cpu().numpy()[sel], afterM[key].numpy()[sel], atol=2e-6)
+
+
+def test_learner_gru64_vs_oracle():
+    """GRU-64 agents + Hm=64 mixer (the cfg2 shapes; no reference sizes exist) vs the torch-CPU oracle."""
+    from minimarl.learner import MIX_KEYS, Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    N, D, A, B, C = 4, 47, 5, 48, 6
+    beh = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=1)
+    tgt = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=2)
+    mix = Mixer(N, N * D, 64, 32, DEV, seed=3)
+    tmix = Mixer(N, N * D, 64, 32, DEV, seed=4)
+    P0 = {k: v.detach().cpu().clone() for k, v in beh.params().items()}
+    T0 = {k: v.detach().cpu().clone() for k, v in tgt.params().items()}
+    M0 = {k: mix.view(k).detach().cpu().clone() for k in MIX_KEYS}
+    TM0 = {k: tmix.view(k).detach().cpu().clone() for k in MIX_KEYS}
+    L = QLearner(beh, tgt, mix, tmix, batch=B, chunk=C, mode="qmix", device=DEV)
+    g = torch.Generator().manual_seed(0)
+    st = torch.rand(B, C, N, D, generator=g)
+    ns = torch.rand(B, C, N, D, generator=g)
+    act = torch.randint(0, A, (B, C, N), generator=g).float()
+    rew = torch.randn(B, C, N, generator=g) * 0.5
+    dn = (torch.rand(B, C, 1, generator=g) < 0.2).float()
+    w = torch.rand(B, 1, generator=g) * 0.5 + 0.5
+    L.load_batch(st, act, rew, ns, dn, w)
+    L.train_step(L._obs_buf, L._obs_buf)
+    torch.cuda.synchronize()
+    newP, newM, grads, loss, td = nets.qmix_train_step(P0, M0, T0, TM0, (st, act, rew, ns, dn, w), 0.99, 1e-3, 5.0)
+    np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=1e-4)
+    np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=1e-4, atol=1e-4)
+    coef = min(1.0, 5.0 / (float(L.norm.item()) + 1e-6))
+    for key in nets.AGENT_KEYS:
+        _check_grads(_grad_view(L, key).cpu().numpy() * coef, grads[key].numpy())
+    for key in MIX_KEYS:
+        _check_grads(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy(), grads["m." + key].numpy())
+
+
+def test_learner_update_from_device_per():
+    """sample -> gather -> train -> priority update through the engine's PER and chunk store."""
+    from minimarl.engine import RolloutEngine
+    from minimarl.learner import Mixer, QLearner
+    E, N = 128, 4
+    eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=10, capacity=512, seed=5, device=DEV)
+    for _ in range(3):
+        eng.run_graph(0.5)
+    mix = Mixer(N, N * eng.D, 64, 32, DEV, seed=1)
+    tmix = Mixer(N, N * eng.D, 64, 32, DEV, seed=1)
+    L = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device=DEV)
+    tree0 = eng.per.tree().cpu().numpy()
+    p0 = L.P.clone()
+    for k in range(3):
+        L.update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=9, counter=k)
+    torch.cuda.synchronize()
+    assert np.isfinite(L.loss.item())
+    assert not torch.equal(p0, L.P)
+    tree1 = eng.per.tree().cpu().numpy()
+    assert not np.array_equal(tree0, tree1)
+    # the tree stays a consistent sum tree
+    cap = eng.per.capacity
+    for node in range(cap - 1):
+        assert abs(tree1[node] - tree1[2 * node + 1] - tree1[2 * node + 2]) <= 1e-9 * max(1.0, tree1[node])
+    # rollout keeps running with the updated weights (packed fragments refreshed)
+    eng.run_graph(0.5)
+    torch.cuda.synchronize()
