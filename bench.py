@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=64)
     ap.add_argument("--epsilon", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--learner-steps", type=int, default=100)
+    ap.add_argument("--batch", type=int, default=32)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +118,15 @@ def main():
     F1, G = 64, Hh
     eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=16 * E, seed=1234 + rank, device=dev)
     D = eng.D
+    from minimarl.learner import Mixer, QLearner
+    mix = Mixer(N, N * D, 64, 32, dev, seed=7)
+    tmix = Mixer(N, N * D, 64, 32, dev, seed=7)
+    learner = QLearner(eng.behavior, eng.target, mix, tmix, batch=args.batch, chunk=10, mode="qmix", device=dev)
+    if dist:   # identical replicas: rank 0's parameters everywhere
+        dist.broadcast(learner.P, 0)
+        eng.sync_target()
+        tmix.flat.copy_(mix.flat)
+        eng.behavior.mark_dirty()
     GS = eng.graph_steps()                      # one HIP graph = one chunk of GS lockstep steps
     warm_rep = max(1, -(-args.warmup // GS))
     n_rep = max(1, -(-args.steps // GS))
@@ -140,6 +151,35 @@ def main():
         elapsed = float(t.item())
     value = steps * E * N * world / elapsed
 
+    # learner: one QMIX update = PER sample (B chunks) -> C-step fwd/BPTT -> [RCCL all-reduce of the
+    # flat grads] -> clip/Adam -> reprioritize; replayed as two HIP graphs
+    allreduce = None
+    if dist:
+        def allreduce(g):
+            dist.all_reduce(g)
+            return world
+        learner._graph_scale = 1.0 / world
+    learner.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=99 + rank)
+    for _ in range(5):
+        learner.replay_update(allreduce)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.learner_steps):
+        learner.replay_update(allreduce)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el_l = time.perf_counter() - t1
+    if dist:
+        t = torch.tensor([el_l], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_l = float(t.item())
+    upd_per_s = args.learner_steps / el_l
+
     # roofline of the dominant kernel: the fused agent Q forward (behavior launch of a step)
     # (one launch = target net on s'_t + behavior net on s_{t+1}: 2 nets x E x N agent-steps)
     t_fwd = time_kernel(eng.fused_forward)
@@ -163,7 +203,11 @@ def main():
             "config": {"workload": "QMIX 8-agent gridworld rollout, 4096 envs/GPU, GRU-64 agents, chunk 10, PER",
                        "envs_per_gpu": E, "agents": N, "obs_dim": D, "f1": F1, "gru": Hh, "chunk": 10,
                        "parallelism": f"env-shard x{world}"},
-            "learner_updates_per_s": None,
+            "learner_updates_per_s": round(upd_per_s, 1),
+            "learner": {"algo": "QMIX Train_dqn update", "batch_chunks": args.batch, "chunk": 10,
+                        "mixer_hidden": 64, "ms_per_update": round(el_l / args.learner_steps * 1e3, 4),
+                        "updates": args.learner_steps, "grad_allreduce": "rccl" if dist else None,
+                        "reference_cpu_updates_per_s": 12.0},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

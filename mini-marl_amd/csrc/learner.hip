@@ -546,12 +546,13 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* G, int64_t n, f
 // torch.optim.Adam (no amsgrad / weight decay) with clip_grad_norm_ applied to G[0:n_clip]
 __global__ __launch_bounds__(256) void adam_kernel(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip,
                                                    const float* partials, int n_part, float max_norm, float lr,
-                                                   float b1, float b2, float eps, const float* step, float* norm_out) {
+                                                   float b1, float b2, float eps, const float* step, float* norm_out,
+                                                   float grad_scale) {
   __shared__ float s_coef;
   if (threadIdx.x == 0) {
     float tot = 0.f;
     for (int i = 0; i < n_part; ++i) tot += partials[i];
-    const float norm = sqrtf(tot);
+    const float norm = sqrtf(tot) * grad_scale;
     s_coef = max_norm > 0.f ? fminf(1.0f, max_norm / (norm + 1e-6f)) : 1.0f;
     if (norm_out && blockIdx.x == 0) *norm_out = norm;
   }
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* P, float* G, float* m,
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float g = G[i];
+    float g = G[i] * grad_scale;
     if (i < n_clip) g *= coef;
     const float mi = m[i] + (g - m[i]) * (1.0f - b1);
     const float vi = v[i] * b2 + g * g * (1.0f - b2);
@@ -697,16 +698,18 @@ int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
   return MM_OK;
 }
 
-// clip_grad_norm_(G[0:n_clip], max_norm) then Adam over P[0:n]; partials: >= 256 floats scratch
+// G *= grad_scale (e.g. 1/world after the RCCL sum), clip_grad_norm_(G[0:n_clip], max_norm), then Adam
+// over P[0:n]; partials: >= 256 floats scratch
 int mm_clip_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip, float max_norm, float lr,
-                 float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, mm_stream_t s) {
+                 float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, float grad_scale,
+                 mm_stream_t s) {
   MM_REQUIRE(P && G && m && v && step && partials && n > 0 && n_clip >= 0 && n_clip <= n, "clip_adam: bad args");
   const int nb = 256;
   hipLaunchKernelGGL(mm::sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, G, n_clip, partials, step);
   MM_HIP_CHECK(hipGetLastError());
   const int nb2 = (int)std::min<int64_t>((n + 255) / 256, 2048);
   hipLaunchKernelGGL(mm::adam_kernel, dim3(nb2), dim3(256), 0, (hipStream_t)s, P, G, m, v, n, n_clip, partials, nb,
-                     max_norm, lr, beta1, beta2, eps, step, norm_out);
+                     max_norm, lr, beta1, beta2, eps, step, norm_out, grad_scale);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

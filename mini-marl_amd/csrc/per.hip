@@ -31,6 +31,7 @@ namespace mm {
 struct PerDev {
   int64_t n_data;
   double alpha, beta, alpha_inc, beta_inc;
+  uint64_t n_samples;
 };
 }  // namespace mm
 
@@ -169,10 +170,13 @@ __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t ca
   // anneal alpha / beta before the draws (buffer.py:53-56)
   const double alpha = fmin(1.0, st->alpha + st->alpha_inc);
   const double beta = fmin(1.0, st->beta + st->beta_inc);
+  // device-side draw counter: every (graph-replayed) sample call gets a fresh RNG stream
+  const uint64_t ctr = counter + st->n_samples;
   __syncthreads();
   if (threadIdx.x == 0) {
     st->alpha = alpha;
     st->beta = beta;
+    st->n_samples += 1;
   }
   __shared__ double s_w[PT];
   __shared__ double s_p[PT];
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t ca
   const double total = tree[0];
   const double seg = total / (double)B;
   for (int k = threadIdx.x; k < B; k += PT) {
-    double f = fracs ? fracs[k] : (double)(rng_draw(seed, counter, (uint64_t)k, 77) >> 11) * (1.0 / 9007199254740992.0);
+    double f = fracs ? fracs[k] : (double)(rng_draw(seed, ctr, (uint64_t)k, 77) >> 11) * (1.0 / 9007199254740992.0);
     const double a = seg * (double)k;
     const double b = seg * (double)(k + 1);
     double s = a + (b - a) * f;
@@ -266,7 +270,7 @@ int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, d
   p->alloc = base;
   p->tree = static_cast<double*>(base);
   p->st = reinterpret_cast<mm::PerDev*>(static_cast<char*>(base) + tree_b + row_b + scr_b);
-  const mm::PerDev st0 = {0, alpha, beta, alpha_inc, beta_inc};
+  const mm::PerDev st0 = {0, alpha, beta, alpha_inc, beta_inc, 0};
   p->slot_row = reinterpret_cast<int64_t*>(static_cast<char*>(base) + tree_b);
   std::vector<int64_t> rows(capacity);
   for (int64_t i = 0; i < capacity; ++i) rows[i] = i;  // slot s reserves row s until first filled

@@ -156,5 +156,5 @@ _SIGS += [
     ("mm_outer_reduce", c_i32, [ctypes.POINTER(OuterArgs), c_vp]),
     ("mm_tmv", c_i32, [ctypes.POINTER(TmvArgs), c_vp]),
     ("mm_clip_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
-                             c_vp, c_vp]),
+                             c_vp, c_f32, c_vp]),
 ]

@@ -196,8 +196,8 @@ class QLearner:
         self._reset_obs = self._obs_buf      # never addressed (no -1 offsets in an explicit batch)
 
     # ------------------------------------------------------------------ the update
-    def train_step(self, obs_base, reset_obs_ptr):
-        """Forward C steps, loss, BPTT, clip, Adam on the gathered batch (all async)."""
+    def compute_grads(self, obs_base, reset_obs_ptr):
+        """Forward C steps, loss, BPTT and all weight gradients into self.Gr (all async)."""
         L, s = lib(), stream_handle(self.dev)
         B, C, N, H, D = self.B, self.C, self.N, self.H, self.D
         CB = C * B
@@ -262,13 +262,21 @@ class QLearner:
         self._agent_wgrad(L, s, obs_p, reset_p, CB)
         if self.mode == "qmix":
             self._mixer_wgrad(L, s, obs_p, reset_p, CB)
-        # ---- clip_grad_norm_ + Adam, then repack the behavior fragments for the next forward
-        check(L.mm_clip_adam(ptr(self.P), ptr(self.Gr), ptr(self.m), ptr(self.v), self.n, self.n_clip, self.clip,
-                             self.lr, self.b1, self.b2, self.aeps, ptr(self.step_dev), ptr(self.partials),
-                             ptr(self.norm), s), "clip_adam")
+
+    def apply_grads(self, grad_scale=1.0):
+        """clip_grad_norm_ + Adam (grads scaled first, e.g. 1/world after an all-reduce), then repack
+        the behavior fragments for the next forward."""
+        s = stream_handle(self.dev)
+        check(lib().mm_clip_adam(ptr(self.P), ptr(self.Gr), ptr(self.m), ptr(self.v), self.n, self.n_clip,
+                                 self.clip, self.lr, self.b1, self.b2, self.aeps, ptr(self.step_dev),
+                                 ptr(self.partials), ptr(self.norm), float(grad_scale), s), "clip_adam")
         self.beh.mark_dirty()
         self.beh.pack(s)
         self.updates += 1
+
+    def train_step(self, obs_base, reset_obs_ptr):
+        self.compute_grads(obs_base, reset_obs_ptr)
+        self.apply_grads()
 
     def _outer(self, L, s, U, u_g, u_m, V, v_g, v_m, dW, w_g, db, b_g, M, R, Cc, groups, v_off=None, v_reset=None):
         a = OuterArgs()
@@ -341,8 +349,8 @@ class QLearner:
                     mo["b2bW"], 0, mo["b2bb"], 0, M, 1, K1, 1)
 
     # ------------------------------------------------------------------ full update from the PER
-    def update(self, per, store, reset_obs_ptr, fracs=None, seed=0, counter=0):
-        """One reference update iteration: sample -> gather -> train -> priority update."""
+    def sample_and_grads(self, per, store, reset_obs_ptr, fracs=None, seed=0, counter=0):
+        """PER sample (injected fractions or the device counter RNG) -> gather -> forward/backward."""
         L, s = lib(), stream_handle(self.dev)
         if fracs is not None:
             fr = torch.as_tensor(fracs, dtype=torch.float64).to(self.dev).contiguous()
@@ -352,8 +360,51 @@ class QLearner:
             check(L.mm_per_sample_rng(per._h, self.B, seed, counter, ptr(self.nodes), ptr(self.slots),
                                       ptr(self.isw), s), "per_sample_rng")
         self.gather(per, store)
-        self.train_step(store.obs, reset_obs_ptr)
-        check(L.mm_per_update(per._h, ptr(self.nodes), ptr(self.td_last), self.B, s), "per_update")
+        self.compute_grads(store.obs, reset_obs_ptr)
+
+    def apply_and_reprioritize(self, per, grad_scale=1.0):
+        self.apply_grads(grad_scale)
+        check(lib().mm_per_update(per._h, ptr(self.nodes), ptr(self.td_last), self.B, stream_handle(self.dev)),
+              "per_update")
+
+    def update(self, per, store, reset_obs_ptr, fracs=None, seed=0, counter=0, allreduce=None):
+        """One reference update iteration: sample -> gather -> grads [-> all-reduce] -> clip/Adam ->
+        priority update. ``allreduce(G)`` sums the flat gradient over ranks (RCCL); grads are then
+        averaged by 1/world inside the clip/Adam kernel."""
+        self.sample_and_grads(per, store, reset_obs_ptr, fracs, seed, counter)
+        scale = 1.0
+        if allreduce is not None:
+            scale = 1.0 / allreduce(self.Gr)
+        self.apply_and_reprioritize(per, scale)
+
+    # ------------------------------------------------------------------ HIP graph of an update
+    def capture_update(self, per, store, reset_obs_ptr, seed=0):
+        """Capture [sample -> gather -> fwd/bwd] and [clip/Adam -> repack -> reprioritize] as two HIP
+        graphs (the RCCL all-reduce, when used, runs between them eagerly)."""
+        self.beh.pack()
+        self.tgt.pack()
+        torch.cuda.synchronize(self.dev)
+        n0 = self.updates
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            self.sample_and_grads(per, store, reset_obs_ptr, seed=seed)
+        with torch.cuda.graph(g2):
+            self.apply_and_reprioritize(per, self._graph_scale)
+        self.updates = n0
+        self.graphs = (g1, g2)
+        return self.graphs
+
+    _graph_scale = 1.0
+
+    def replay_update(self, allreduce=None):
+        g1, g2 = self.graphs
+        self.tgt.pack()                 # target synced since capture: repack eagerly (no-op otherwise)
+        self.beh.pack()
+        g1.replay()
+        if allreduce is not None:
+            allreduce(self.Gr)          # the 1/world scale was baked at capture (set _graph_scale first)
+        g2.replay()
+        self.updates += 1
 
     def sync_target(self, mixer=False):
         """target <- behavior (qmix/main.py:255-256 syncs the agent net only; mixer=True also the mixer)."""

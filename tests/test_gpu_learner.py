@@ -61,14 +61,22 @@ def test_learner_matches_reference_update(golden, mode):
     norm = float(L.norm.item())
     coef = min(1.0, float(fx["grad_clip"]) / (norm + 1e-6))
     N = P["W1"].shape[0]
+
+    def gidx(i, k):
+        # parameters() order: qmix registers per agent (feature, gru, action); vdn registers the
+        # ParameterLists feature_net[*], gru_net[*], action_net[*] (vdn/_network.py:21-25)
+        if mode == "qmix":
+            return 10 * i + k
+        return 4 * i + k if k < 4 else (4 * N + 4 * i + k - 4 if k < 8 else 8 * N + 2 * i + k - 8)
+
     for i in range(N):
         for k, key in enumerate(nets.AGENT_KEYS):
-            g_ref = fx[f"g0.{10 * i + k}"]
+            g_ref = fx[f"g0.{gidx(i, k)}"]
             g_dev = _grad_view(L, key)[i].cpu().numpy() * coef
             _check_grads(g_dev, g_ref)
     after = nets.agent_from_state(fx, "after_q." if mode == "qmix" else "after.", style)
     for key in nets.AGENT_KEYS:
-        g_all = np.stack([fx[f"g0.{10 * i + nets.AGENT_KEYS.index(key)}"] for i in range(N)])
+        g_all = np.stack([fx[f"g0.{gidx(i, nets.AGENT_KEYS.index(key))}"] for i in range(N)])
         sel = np.abs(g_all) > 1e-4 * np.abs(g_all).max()
         got = L.beh.view(key).cpu().numpy()
         np.testing.assert_allclose(got[sel], after[key].numpy()[sel], rtol=0, atol=2e-6)
