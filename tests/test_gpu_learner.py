@@ -152,3 +152,28 @@ def test_learner_update_from_device_per():
     # rollout keeps running with the updated weights (packed fragments refreshed)
     eng.run_graph(0.5)
     torch.cuda.synchronize()
+
+
+def test_learner_graph_replay_matches_eager():
+    from minimarl.engine import RolloutEngine
+    from minimarl.learner import Mixer, QLearner
+
+    def build():
+        eng = RolloutEngine(64, 4, f1=64, g=64, h=64, chunk=10, capacity=256, seed=3, device=DEV)
+        for _ in range(2):
+            eng.run_graph(0.5)
+        mix = Mixer(4, 4 * eng.D, 64, 32, DEV, seed=1)
+        tmix = Mixer(4, 4 * eng.D, 64, 32, DEV, seed=2)
+        return eng, QLearner(eng.behavior, eng.target, mix, tmix, batch=16, chunk=10, mode="qmix", device=DEV)
+
+    e1, l1 = build()
+    e2, l2 = build()
+    for _ in range(3):
+        l1.update(e1.per, e1.store, e1.env.reset_obs_ptr(), seed=5, counter=0)
+    l2.capture_update(e2.per, e2.store, e2.env.reset_obs_ptr(), seed=5)
+    for _ in range(3):
+        l2.replay_update()
+    torch.cuda.synchronize()
+    assert torch.equal(l1.P, l2.P)
+    assert torch.equal(e1.per.tree(), e2.per.tree())
+    assert torch.equal(l1.loss, l2.loss)
