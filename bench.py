@@ -12,6 +12,7 @@ torch.distributed.run (one process per GPU, RCCL). Envs shard across ranks with 
 data-path collective (weak scaling); rank 0 prints ONE JSON line.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -185,10 +186,19 @@ def main():
     t_fwd = time_kernel(eng.fused_forward)
     flops = 2 * qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
     achieved = flops / t_fwd / 1e12
+    # algorithmic HBM bytes per launch: per agent-step obs 4D + hidden in/out 8H + outputs (act/q 8 or max 4)
+    alg_bytes = E * N * ((4 * D + 8 * Hh + 8) + (4 * D + 8 * Hh + 4))
+    traffic = None
+    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_agent_fwd.json")))
+    if prof and E == 4096 and N == 8 and Hh == 64:
+        pm = json.load(open(prof[-1]))
+        traffic = int(pm["traffic_bytes_corrected"])
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                "traffic_source": os.path.basename(prof[-1]) if traffic else None,
                 "kernel": "agent_q_fwd_kernel<64,64,64,1> (dual: target+behavior)", "kernel_us": round(t_fwd * 1e6, 2),
-                "flop_per_launch": flops}
+                "flop_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
+                "hbm_frac": round(alg_bytes / t_fwd / (PEAK_HBM_GBS * 1e9), 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
