@@ -9,8 +9,8 @@
 // Mapping: one wave = 32 envs of one agent; features on MFMA rows, envs on
 // columns, so every layer's D registers are directly the next layer's B
 // operand (see common.h kperm) — no LDS, no transposes. Weights are the A
-// operand, read as 16-float contiguous per-lane fragments from the packed image
-// (4 x dwordx4 per 16 MFMAs), L2/L1-resident: block b serves agent b % N, so
+// operand, read from the packed fragment image (4 x dwordx4 wave-instructions of
+// 1 KiB each per 16 MFMAs), L2/L1-resident: block b serves agent b % N, so
 // with N = 8 each XCD's L2 only ever holds one agent's weights.
 // Arithmetic: exact-f32 MFMA v_mfma_f32_32x32x2_f32 (fp32 in, fp32 accumulate).
 #include "common.h"
@@ -27,11 +27,12 @@ struct QFwdParams {
   int nblocks;  // blocks of this net inside a (possibly dual) launch
 };
 
+// Fragment image of one 32x32 k-block: [q = s>>2][lane][s&3] floats, so each of the 4 dwordx4
+// wave-instructions reads 1 KiB contiguous (and an LDS copy would be conflict-free).
 __device__ __forceinline__ void load_frag(const float* __restrict__ base, int lane, float (&a)[16]) {
-  const float4* p = reinterpret_cast<const float4*>(base + lane * 16);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    float4 v = p[q];
+    float4 v = *reinterpret_cast<const float4*>(base + q * 256 + lane * 4);
     a[4 * q + 0] = v.x;
     a[4 * q + 1] = v.y;
     a[4 * q + 2] = v.z;
@@ -76,17 +77,14 @@ struct Sched {
 };
 
 template <int F1, int G, int H, int AB>
-__device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int bid) {
+__device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent, int e,
+                                                 const float* __restrict__ W) {
   using S = Sched<F1, G, H, AB>;
   constexpr int RB1 = S::RB1, RB2 = S::RB2, HB = S::HB, NF = S::NF;
   const int lane = threadIdx.x & 63;
-  const int j = lane & 31, hh = lane >> 5;
-  const int agent = bid % p.N;
-  const int tile = bid / p.N;
-  const int e = tile * 128 + (threadIdx.x >> 6) * 32 + j;
+  const int hh = lane >> 5;
   const bool valid = e < p.E;
   const mm_qfwd_io& io = p.io;
-  const float* __restrict__ W = p.packed + (int64_t)agent * p.g.agent_stride;
 
   // fragment pipeline (prefetch distance 1): nxt holds the next fragment of the schedule
   float cur[16], nxt[16];
@@ -307,10 +305,32 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int bid) {
 // under the other's MFMAs.
 template <int F1, int G, int H, int AB>
 __global__ __launch_bounds__(256, (F1 > 64 ? 1 : 2)) void agent_q_fwd_kernel(QFwdParams p0, QFwdParams p1) {
-  if ((int)blockIdx.x < p0.nblocks)
-    agent_q_fwd_body<F1, G, H, AB>(p0, blockIdx.x);
-  else
-    agent_q_fwd_body<F1, G, H, AB>(p1, blockIdx.x - p0.nblocks);
+  const bool second = (int)blockIdx.x >= p0.nblocks;
+  const QFwdParams& p = second ? p1 : p0;
+  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
+  const int agent = bid % p.N, tile = bid / p.N;
+  const int e = tile * 128 + (threadIdx.x >> 6) * 32 + (threadIdx.x & 31);
+  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, p.packed + (int64_t)agent * p.g.agent_stride);
+}
+
+// Large-E variant: a 512-thread block (8 waves = 256 envs of one agent) first copies the agent's
+// whole fragment image into LDS (one contiguous float4 stream, L2-resident: with N = 8 an XCD only
+// serves one agent), then every A-operand read is a conflict-free ds_read_b128 ([q][lane][4]
+// image) instead of an L2 round trip. One block per CU, two waves per SIMD.
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(512, 2) void agent_q_fwd_lds_kernel(QFwdParams p0, QFwdParams p1) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  const bool second = (int)blockIdx.x >= p0.nblocks;
+  const QFwdParams& p = second ? p1 : p0;
+  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
+  const int agent = bid % p.N, tile = bid / p.N;
+  const float4* src = reinterpret_cast<const float4*>(p.packed + (int64_t)agent * p.g.agent_stride);
+  float4* dst = reinterpret_cast<float4*>(wsm);
+  const int n4 = (int)(p.g.agent_stride / 4);
+  for (int i = threadIdx.x; i < n4; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  const int e = tile * 256 + (threadIdx.x >> 6) * 32 + (threadIdx.x & 31);
+  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, wsm);
 }
 
 // ---------------------------------------------------------------- packing
@@ -325,12 +345,13 @@ __global__ void qnet_pack_kernel(const float* __restrict__ params, float* __rest
     const int agent = (int)(idx / per_agent);
     int64_t r = idx % per_agent;
     float v = 0.0f;
-    // weight images: [rb][kb][lane][s]
+    // weight images: [rb][kb][q][lane][s & 3] (see load_frag)
     auto wimg = [&](int64_t off, int KB, int rows, int cols, int64_t src, int64_t& rr, bool& hit) {
       const int64_t sz = (int64_t)((rows + 31) / 32) * KB * 1024;
       if (rr >= off && rr < off + sz) {
         const int64_t t = rr - off;
-        const int s = (int)(t & 15), lane = (int)((t >> 4) & 63);
+        // [rb][kb][q][lane][s&3]
+        const int lane = (int)((t >> 2) & 63), s = (int)(((t >> 8) & 3) * 4 + (t & 3));
         const int64_t blk = t >> 10;
         const int kb = (int)(blk % KB), rb = (int)(blk / KB);
         const int row = rb * 32 + (lane & 31), col = kb * 32 + kperm(s, lane >> 5);
@@ -379,10 +400,25 @@ int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStre
   return MM_OK;
 }
 
+// LDS-staged variant when every net of the launch has >= 2048 envs and the image fits in LDS.
+static bool use_lds(const QFwdParams& p0, const QFwdParams* p1) {
+  const size_t bytes = (size_t)p0.g.agent_stride * 4;
+  return bytes <= 160 * 1024 && p0.E >= 2048 && (!p1 || p1->E >= 2048);
+}
+
 template <int F1, int G, int H, int AB>
-static int launch_fwd(const QFwdParams& p0, const QFwdParams* p1, hipStream_t s) {
-  const int nb = p0.nblocks + (p1 ? p1->nblocks : 0);
-  hipLaunchKernelGGL((agent_q_fwd_kernel<F1, G, H, AB>), dim3(nb), dim3(256), 0, s, p0, p1 ? *p1 : p0);
+static int launch_fwd(QFwdParams p0, const QFwdParams* p1in, hipStream_t s) {
+  QFwdParams p1 = p1in ? *p1in : p0;
+  if (use_lds(p0, p1in)) {
+    p0.nblocks = (p0.E + 255) / 256 * p0.N;
+    p1.nblocks = (p1.E + 255) / 256 * p1.N;
+    const int nb = p0.nblocks + (p1in ? p1.nblocks : 0);
+    const size_t sm = (size_t)p0.g.agent_stride * 4;
+    hipLaunchKernelGGL((agent_q_fwd_lds_kernel<F1, G, H, AB>), dim3(nb), dim3(512), sm, s, p0, p1);
+  } else {
+    const int nb = p0.nblocks + (p1in ? p1.nblocks : 0);
+    hipLaunchKernelGGL((agent_q_fwd_kernel<F1, G, H, AB>), dim3(nb), dim3(256), 0, s, p0, p1);
+  }
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

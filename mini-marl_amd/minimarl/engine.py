@@ -69,8 +69,10 @@ class RolloutEngine:
         E, N, D, H = self.E, self.N, self.D, self.H
         dev = self.device
         self.obs_cur = torch.empty(E, N, D, device=dev)
-        self.h = torch.zeros(E, N, H, device=dev)
-        self.ht = torch.zeros(E, N, H, device=dev)
+        # hidden states feature-major [N, H, E] (env fastest): the forward's lane = env, so every
+        # hidden load / store of a wave is one coalesced 128-byte run per feature row
+        self.h = torch.zeros(N, H, E, device=dev)
+        self.ht = torch.zeros(N, H, E, device=dev)
         # ping-pong buffers indexed by step parity: done_t, act_t, q_taken_t live in slot t % 2
         self.done_buf = [torch.zeros(E, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.act_buf = [torch.zeros(E, N, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -99,9 +101,9 @@ class RolloutEngine:
         b = QFwdIO()
         b.obs, b.obs_se, b.obs_sa = self.obs_cur.data_ptr(), N * D, D
         b.h_in = b.h_out = self.h.data_ptr()
-        b.hin_se = b.hout_se = N * H
-        b.hin_sa = b.hout_sa = H
-        b.hin_sf = b.hout_sf = 1
+        b.hin_se = b.hout_se = 1
+        b.hin_sa = b.hout_sa = H * self.E
+        b.hin_sf = b.hout_sf = self.E
         b.reset = self.done_buf[1 - k].data_ptr()
         b.mode = MM_Q_ACT
         b.act_out, b.qsel_out = self.act_buf[k].data_ptr(), self.qsel_buf[k].data_ptr()
@@ -117,9 +119,9 @@ class RolloutEngine:
         t.obs_row = self.staging.data_ptr()
         t.reset_obs = self.env.reset_obs_ptr()
         t.h_in = t.h_out = self.ht.data_ptr()
-        t.hin_se = t.hout_se = N * H
-        t.hin_sa = t.hout_sa = H
-        t.hin_sf = t.hout_sf = 1
+        t.hin_se = t.hout_se = 1
+        t.hin_sa = t.hout_sa = H * self.E
+        t.hin_sf = t.hout_sf = self.E
         t.reset = self.done_buf[1 - k].data_ptr()
         t.mode = MM_Q_MAX
         t.qsel_out = self.maxq.data_ptr()
