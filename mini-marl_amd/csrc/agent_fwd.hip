@@ -25,6 +25,7 @@ struct QFwdParams {
   const float* packed;
   int E, N, D, A;
   int nblocks;  // blocks of this net inside a (possibly dual) launch
+  int stagger;  // LDS variant: waves 4-7 start stagger x 512 cycles late
 };
 
 // Fragment image of one 32x32 k-block: [q = s>>2][lane][s&3] floats, so each of the 4 dwordx4
@@ -61,25 +62,48 @@ struct Sched {
   static constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
   static constexpr int NF2 = RB2 * RB1, PERHB = 3 * RB2 + 3 * HB, NFG = HB * PERHB, NFQ = AB * HB;
   static constexpr int NF = NF2 + NFG + NFQ;
-  __device__ static __forceinline__ int64_t off(const QnetGeo& g, int i) {
-    if (i < NF2) return g.off_l2 + (int64_t)((i / RB1) * RB1 + i % RB1) * 1024;
+  using CG = QnetCGeo<F1, G, H, AB>;
+  __device__ static constexpr int off(int i) {
+    if (i < NF2) return CG::off_l2 + ((i / RB1) * RB1 + i % RB1) * 1024;
     i -= NF2;
     if (i < NFG) {
       const int hb = i / PERHB;
       int r = i % PERHB;
-      if (r < 3 * RB2) return g.off_ih + (int64_t)(((r / RB2) * HB + hb) * RB2 + r % RB2) * 1024;
+      if (r < 3 * RB2) return CG::off_ih + (((r / RB2) * HB + hb) * RB2 + r % RB2) * 1024;
       r -= 3 * RB2;
-      return g.off_hh + (int64_t)(((r / HB) * HB + hb) * HB + r % HB) * 1024;
+      return CG::off_hh + (((r / HB) * HB + hb) * HB + r % HB) * 1024;
     }
     i -= NFG;
-    return g.off_q + (int64_t)((i / HB) * HB + i % HB) * 1024;
+    return CG::off_q + ((i / HB) * HB + i % HB) * 1024;
   }
 };
 
+// Observation row of (env e, agent): the chunk-store row (or the reset obs when obs_row < 0).
+__device__ __forceinline__ const float* obs_row_ptr(const QFwdParams& p, int agent, int e) {
+  if (e >= p.E) return nullptr;
+  const mm_qfwd_io& io = p.io;
+  const int64_t r = io.obs_row ? io.obs_row[e] : (int64_t)e;
+  return (r >= 0) ? io.obs + r * io.obs_se + io.obs_off + (int64_t)agent * io.obs_sa
+                  : io.reset_obs + (int64_t)agent * io.obs_sa;
+}
+
+// B operand of layer-1 k-block kb: lane (j, hh) holds obs features 32 kb + kperm(s, hh).
+__device__ __forceinline__ void load_obs_kblock(const float* orow, int kb, int D, float (&x)[16]) {
+  const int hh = (threadIdx.x & 63) >> 5;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int k = kb * 32 + kperm(s, hh);
+    x[s] = (orow && k < D) ? orow[k] : 0.0f;
+  }
+}
+
+// xn: layer-1 k-block 0 of the observation, loaded by the caller (before weight staging).
 template <int F1, int G, int H, int AB>
 __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent, int e,
-                                                 const float* __restrict__ W) {
+                                                 const float* __restrict__ W, const float* orow,
+                                                 float (&xn)[16]) {
   using S = Sched<F1, G, H, AB>;
+  using CG = typename S::CG;
   constexpr int RB1 = S::RB1, RB2 = S::RB2, HB = S::HB, NF = S::NF;
   const int lane = threadIdx.x & 63;
   const int hh = lane >> 5;
@@ -88,34 +112,23 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
 
   // fragment pipeline (prefetch distance 1): nxt holds the next fragment of the schedule
   float cur[16], nxt[16];
-  load_frag(W + S::off(p.g, 0), lane, nxt);
+  load_frag(W + S::off(0), lane, nxt);
   auto consume = [&](int i, const f32x16& x, f32x16& acc) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) cur[s] = nxt[s];
-    if (i + 1 < NF) load_frag(W + S::off(p.g, i + 1), lane, nxt);
+    if (i + 1 < NF) load_frag(W + S::off(i + 1), lane, nxt);
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = mfma32(cur[s], x[s], acc);
   };
 
   // ---- layer 1: x1 = ReLU(W1 o + b1), K = D streamed in 32-wide k-blocks (next k-block prefetched)
-  const float* orow = nullptr;
-  if (valid) {
-    const int64_t r = io.obs_row ? io.obs_row[e] : (int64_t)e;
-    orow = (r >= 0) ? io.obs + r * io.obs_se + io.obs_off + (int64_t)agent * io.obs_sa
-                    : io.reset_obs + (int64_t)agent * io.obs_sa;
-  }
   f32x16 x1[RB1];
 #pragma unroll
-  for (int rb = 0; rb < RB1; ++rb) x1[rb] = load_bias(W + p.g.off_b1 + rb * 32, hh);
-  float xb[16], xn[16];
+  for (int rb = 0; rb < RB1; ++rb) x1[rb] = load_bias(W + CG::off_b1 + rb * 32, hh);
+  float xb[16];
   float fa[RB1][16], fn[RB1][16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int k = kperm(s, hh);
-    xn[s] = (valid && k < p.D) ? orow[k] : 0.0f;
-  }
-#pragma unroll
-  for (int rb = 0; rb < RB1; ++rb) load_frag(W + p.g.off_l1 + (int64_t)(rb * p.g.KD) * 1024, lane, fn[rb]);
+  for (int rb = 0; rb < RB1; ++rb) load_frag(W + CG::off_l1 + (int64_t)(rb * p.g.KD) * 1024, lane, fn[rb]);
   for (int kb = 0; kb < p.g.KD; ++kb) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) xb[s] = xn[s];
@@ -124,14 +137,10 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
 #pragma unroll
       for (int s = 0; s < 16; ++s) fa[rb][s] = fn[rb][s];
     if (kb + 1 < p.g.KD) {
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int k = (kb + 1) * 32 + kperm(s, hh);
-        xn[s] = (valid && k < p.D) ? orow[k] : 0.0f;
-      }
+      load_obs_kblock(orow, kb + 1, p.D, xn);
 #pragma unroll
       for (int rb = 0; rb < RB1; ++rb)
-        load_frag(W + p.g.off_l1 + (int64_t)(rb * p.g.KD + kb + 1) * 1024, lane, fn[rb]);
+        load_frag(W + CG::off_l1 + (int64_t)(rb * p.g.KD + kb + 1) * 1024, lane, fn[rb]);
     }
 #pragma unroll
     for (int rb = 0; rb < RB1; ++rb)
@@ -155,7 +164,7 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
   f32x16 x2[RB2];
 #pragma unroll
   for (int rb = 0; rb < RB2; ++rb) {
-    x2[rb] = load_bias(W + p.g.off_b2 + rb * 32, hh);
+    x2[rb] = load_bias(W + CG::off_b2 + rb * 32, hh);
 #pragma unroll
     for (int kb = 0; kb < RB1; ++kb) consume(rb * RB1 + kb, x1[kb], x2[rb]);
 #pragma unroll
@@ -182,10 +191,10 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
 #pragma unroll
   for (int hb = 0; hb < HB; ++hb) {
     const int base = S::NF2 + hb * S::PERHB;
-    f32x16 ar = load_bias(W + p.g.off_brz + hb * 32, hh);
-    f32x16 az = load_bias(W + p.g.off_brz + (HB + hb) * 32, hh);
-    f32x16 anx = load_bias(W + p.g.off_bin + hb * 32, hh);
-    f32x16 anh = load_bias(W + p.g.off_bhn + hb * 32, hh);
+    f32x16 ar = load_bias(W + CG::off_brz + hb * 32, hh);
+    f32x16 az = load_bias(W + CG::off_brz + (HB + hb) * 32, hh);
+    f32x16 anx = load_bias(W + CG::off_bin + hb * 32, hh);
+    f32x16 anh = load_bias(W + CG::off_bhn + hb * 32, hh);
 #pragma unroll
     for (int kb = 0; kb < RB2; ++kb) consume(base + kb, x2[kb], ar);
 #pragma unroll
@@ -202,7 +211,7 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
     for (int s = 0; s < 16; ++s) {
       const float r = sigmoidf_(ar[s]);
       const float z = sigmoidf_(az[s]);
-      const float n = tanhf(anx[s] + r * anh[s]);
+      const float n = tanhf_(anx[s] + r * anh[s]);
       h1[hb][s] = n + z * (h0[hb][s] - n);
       if (sv) {
         float* o = sv + F1 + G + hb * 32 + kperm(s, hh);
@@ -229,7 +238,7 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
   f32x16 qa[AB];
 #pragma unroll
   for (int ab = 0; ab < AB; ++ab) {
-    qa[ab] = load_bias(W + p.g.off_bq + ab * 32, hh);
+    qa[ab] = load_bias(W + CG::off_bq + ab * 32, hh);
 #pragma unroll
     for (int kb = 0; kb < HB; ++kb) consume(S::NF2 + S::NFG + ab * HB + kb, h1[kb], qa[ab]);
   }
@@ -310,13 +319,18 @@ __global__ __launch_bounds__(256, (F1 > 64 ? 1 : 2)) void agent_q_fwd_kernel(QFw
   const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
   const int agent = bid % p.N, tile = bid / p.N;
   const int e = tile * 128 + (threadIdx.x >> 6) * 32 + (threadIdx.x & 31);
-  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, p.packed + (int64_t)agent * p.g.agent_stride);
+  const float* orow = obs_row_ptr(p, agent, e);
+  float xn[16];
+  load_obs_kblock(orow, 0, p.D, xn);
+  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, p.packed + (int64_t)agent * p.g.agent_stride, orow, xn);
 }
 
 // Large-E variant: a 512-thread block (8 waves = 256 envs of one agent) first copies the agent's
-// whole fragment image into LDS (one contiguous float4 stream, L2-resident: with N = 8 an XCD only
-// serves one agent), then every A-operand read is a conflict-free ds_read_b128 ([q][lane][4]
-// image) instead of an L2 round trip. One block per CU, two waves per SIMD.
+// whole fragment image into LDS (L2-resident: with N = 8 an XCD only serves one agent), then every
+// A-operand read is a conflict-free ds_read_b128 ([q][lane][4] image) instead of an L2 round trip.
+// The copy is LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction, all in flight at
+// once) issued after the first observation k-block's loads, so both latencies overlap.
+// One block per CU, two waves per SIMD.
 template <int F1, int G, int H, int AB>
 __global__ __launch_bounds__(512, 2) void agent_q_fwd_lds_kernel(QFwdParams p0, QFwdParams p1) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];
@@ -324,13 +338,23 @@ __global__ __launch_bounds__(512, 2) void agent_q_fwd_lds_kernel(QFwdParams p0, 
   const QFwdParams& p = second ? p1 : p0;
   const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
   const int agent = bid % p.N, tile = bid / p.N;
-  const float4* src = reinterpret_cast<const float4*>(p.packed + (int64_t)agent * p.g.agent_stride);
-  float4* dst = reinterpret_cast<float4*>(wsm);
-  const int n4 = (int)(p.g.agent_stride / 4);
-  for (int i = threadIdx.x; i < n4; i += blockDim.x) dst[i] = src[i];
-  __syncthreads();
   const int e = tile * 256 + (threadIdx.x >> 6) * 32 + (threadIdx.x & 31);
-  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, wsm);
+  const float* orow = obs_row_ptr(p, agent, e);
+  float xn[16];
+  load_obs_kblock(orow, 0, p.D, xn);
+  const float* src = p.packed + (int64_t)agent * p.g.agent_stride;
+  const int nchunk = (int)(p.g.agent_stride >> 8);  // 1 KiB chunks (agent_stride is a multiple of 256)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int c = wave; c < nchunk; c += 8)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 256 + lane * 4),
+                                     (__attribute__((address_space(3))) void*)(wsm + c * 256), 16, 0, 0);
+  __syncthreads();  // waits vmcnt(0): the DMA'd image has landed
+  // Stagger: waves 4-7 share SIMDs with waves 0-3 and run the same program; starting them ~2k
+  // cycles late puts one wave's VALU phases (GRU gates, epilogues) under the other's MFMAs
+  // (MI355X_MICROARCH "two waves ... try a stagger"; measured 54.6 -> 50.5 us dual at 4096 x 8).
+  if (wave >= 4)
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(8);
+  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, wsm, orow, xn);
 }
 
 // ---------------------------------------------------------------- packing
@@ -437,6 +461,8 @@ static int make_params(const mm_qnet_dims* d, const float* packed, const mm_qfwd
   p->D = d->obs_dim;
   p->A = d->n_actions;
   p->nblocks = (int)((n_envs + 127) / 128) * d->n_agents;
+  static const int stagger = getenv("MM_FWD_STAGGER") ? atoi(getenv("MM_FWD_STAGGER")) : 4;
+  p->stagger = stagger;
   MM_REQUIRE(io->obs, "agent_q_fwd: obs required");
   MM_REQUIRE(io->h_in || io->reset == nullptr, "agent_q_fwd: h_in required");
   MM_REQUIRE(io->mode != MM_Q_GATHER || io->act_in, "agent_q_fwd: GATHER needs act_in");

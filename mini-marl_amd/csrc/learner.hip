@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixFwdArgs a) {
   for (int i = threadIdx.x; i < Hm; i += blockDim.x) {
     const float r = sigmoidf_(gi[i] + gh[i]);
     const float z = sigmoidf_(gi[Hm + i] + gh[Hm + i]);
-    const float n = tanhf(gi[2 * Hm + i] + r * gh[2 * Hm + i]);
+    const float n = tanhf_(gi[2 * Hm + i] + r * gh[2 * Hm + i]);
     const float hv = n + z * (h0[i] - n);
     h1[i] = hv;
     nt.h_out[(int64_t)b * Hm + i] = hv;

@@ -18,6 +18,23 @@ struct QnetGeo {
   int64_t agent_stride;
 };
 
+// Compile-time view of QnetGeo for the kernel instantiations (must match qnet_geometry).
+template <int F1, int G, int H, int AB>
+struct QnetCGeo {
+  static constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
+  static constexpr int off_l2 = 0;
+  static constexpr int off_ih = off_l2 + RB2 * RB1 * 1024;
+  static constexpr int off_hh = off_ih + 3 * HB * RB2 * 1024;
+  static constexpr int off_q = off_hh + 3 * HB * HB * 1024;
+  static constexpr int off_b1 = off_q + AB * HB * 1024;
+  static constexpr int off_b2 = off_b1 + RB1 * 32;
+  static constexpr int off_brz = off_b2 + RB2 * 32;
+  static constexpr int off_bin = off_brz + 2 * HB * 32;
+  static constexpr int off_bhn = off_bin + HB * 32;
+  static constexpr int off_bq = off_bhn + HB * 32;
+  static constexpr int off_l1 = off_bq + AB * 32;
+};
+
 inline int qnet_check(const mm_qnet_dims* d) {
   MM_REQUIRE(d, "qnet: null dims");
   MM_REQUIRE(d->n_agents >= 1 && d->obs_dim >= 1 && d->n_actions >= 1 && d->n_actions <= 64,
@@ -51,8 +68,9 @@ inline int qnet_geometry(const mm_qnet_dims* d, QnetGeo* g, QnetOffsets* o) {
   if (rc) return rc;
   const int64_t RB1 = d->f1 / 32, RB2 = d->g / 32, HB = d->h / 32, AB = (d->n_actions + 31) / 32;
   g->KD = (d->obs_dim + 31) / 32;
+  // Everything whose size is fixed by (F1, G, H, A) first, layer 1 (size depends on D) last,
+  // so the kernels address all post-layer-1 fragments with compile-time offsets (QnetCGeo).
   int64_t c = 0;
-  g->off_l1 = c; c += RB1 * g->KD * 1024;
   g->off_l2 = c; c += RB2 * RB1 * 1024;
   g->off_ih = c; c += 3 * HB * RB2 * 1024;
   g->off_hh = c; c += 3 * HB * HB * 1024;
@@ -63,7 +81,8 @@ inline int qnet_geometry(const mm_qnet_dims* d, QnetGeo* g, QnetOffsets* o) {
   g->off_bin = c; c += HB * 32;
   g->off_bhn = c; c += HB * 32;
   g->off_bq = c; c += AB * 32;
-  g->agent_stride = (c + 63) & ~int64_t(63);
+  g->off_l1 = c; c += RB1 * g->KD * 1024;
+  g->agent_stride = (c + 255) & ~int64_t(255);  // whole 1 KiB chunks (LDS-DMA staging)
   return MM_OK;
 }
 
