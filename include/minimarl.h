@@ -139,6 +139,95 @@ int64_t mm_per_size(const mm_per* per);
 double mm_per_alpha(const mm_per* per);
 double mm_per_beta(const mm_per* per);
 
+/* ------------------------------------------------------------------ MAPPO (rmappo, shared policy)
+ * Replaces R_MAPPOPolicy.get_actions / get_values / evaluate_actions
+ * (mappo/algorithms/rmappo_policy.py:57-136), SharedReplayBuffer.compute_returns + insert
+ * (mappo/runner/shared/shared_buffer.py:82-157, magym_runner.py:138-195) and R_MAPPO.train /
+ * ppo_update / cal_value_loss (mappo/algorithms/ramppo_network.py:56-287).
+ * Net 0 = actor (head: A logits), net 1 = critic (head: 1 value). Per-net flat parameters in the
+ * layout of mm_mappo_param_offsets (18 tensors: ln0_w ln0_b W1 b1 ln1_w ln1_b W2 b2 ln2_w ln2_b
+ * Wih Whh bih bhh lnr_w lnr_b Wo bo + total; W1 rows padded to Dp = ceil4(D), Wo/bo to ceil4(O)).
+ * Buffer arrays are [T(+1), EN] row-major with EN = envs*agents (row = t*EN + en); obs rows [.., D],
+ * hiddens [.., H]. Supported: H = 32, A = 5, D in {47, 94}. */
+typedef struct mm_mappo_dims {
+  int32_t obs_dim, hidden, n_actions;
+} mm_mappo_dims;
+enum { MM_MAPPO_ROLLOUT = 0, MM_MAPPO_VALUES = 1, MM_MAPPO_TRAIN = 2 };
+enum { MM_MAPPO_MAX_JOBS = 16 };
+/* device scalar slots of the stats vector (float[8]) */
+enum { MM_MST_ADV_MEAN = 0, MM_MST_ADV_STD = 1, MM_MST_ACTIVE_SUM = 2, MM_MST_RET_MEAN = 3, MM_MST_RET_SQ_MEAN = 4,
+       MM_MST_VN_MEAN = 5, MM_MST_VN_STD = 6 };
+/* loss accumulator slots (float[4], logging only): masked means as in train_info */
+enum { MM_MLOSS_POLICY = 0, MM_MLOSS_ENTROPY = 1, MM_MLOSS_VALUE = 2, MM_MLOSS_RATIO = 3 };
+typedef struct mm_mappo_net_io {
+  const float* P;     /* flat parameters */
+  const float* h_in;  /* rollout: [rows, H]; train: stored hiddens [T+1, EN, H] */
+  float* h_out;       /* rollout: [rows, H] (may alias the next buffer slot) */
+  float* out;         /* rollout: actor log-prob of the action / critic value, [rows] */
+  float* save;        /* train: SoA scratch [mm_mappo_save_fields][rs] */
+} mm_mappo_net_io;
+typedef struct mm_mappo_fwd_args {
+  mm_mappo_net_io net[2];
+  const float* obs;      /* rollout [rows, D]; train [T+1, EN, D] */
+  const float* mask;     /* rollout [rows] (NULL = ones); train masks [T+1, EN] */
+  const int32_t* act_in; /* rollout: evaluate given actions instead of sampling */
+  int32_t* act_out;      /* rollout: sampled actions [rows] */
+  const float* u;        /* rollout: injected uniforms [rows] (NULL = counter RNG) */
+  uint64_t seed;
+  const uint64_t* counter_ptr; /* device RNG step counter (NULL = counter) */
+  uint64_t counter;
+  int64_t rows;
+  int64_t en;
+  int32_t T, L;
+  int64_t rs;            /* SoA row stride (>= T*EN, multiple of 64; tail rows must stay zero) */
+  int32_t mode;
+} mm_mappo_fwd_args;
+typedef struct mm_mappo_bwd_args {
+  const float* P[2];
+  const float* save[2];  /* forward SoA scratch of each net */
+  float* gsoa[2];        /* out: SoA operands of the weight gradients [mm_mappo_grad_fields][rs] */
+  const float* obs;      /* [T+1, EN, D] */
+  const float* mask;     /* masks [T+1, EN] */
+  const float* active;   /* active masks [T+1, EN] */
+  const int32_t* act;    /* actions [T, EN] */
+  const float* adv;      /* raw advantages [T, EN] (normalised with stats) */
+  const float* old_logp; /* action_log_probs [T, EN] */
+  const float* old_value;/* value_preds [T+1, EN] */
+  const float* returns;  /* [T+1, EN] */
+  const float* stats;    /* float[8], see MM_MST_* */
+  float* loss_acc;       /* float[4] or NULL */
+  float clip, huber_delta, entropy_coef, value_coef;
+  int64_t en;
+  int32_t T, L;
+  int64_t rs;
+} mm_mappo_bwd_args;
+int64_t mm_mappo_param_count(const mm_mappo_dims* d, int32_t net);
+int mm_mappo_param_offsets(const mm_mappo_dims* d, int32_t net, int64_t offs[19]);
+int mm_mappo_save_fields(const mm_mappo_dims* d, int32_t net);
+int mm_mappo_grad_fields(const mm_mappo_dims* d, int32_t net);
+/* Actor + critic forward: ROLLOUT (sample or evaluate act_in; new hiddens), VALUES (critic only),
+ * TRAIN (every L-step chunk from its stored hidden, h <- h*mask each step; saves activations). */
+int mm_mappo_fwd(const mm_mappo_dims* d, const mm_mappo_fwd_args* a, mm_stream_t s);
+/* Loss seeds + chunked BPTT of both nets (after a TRAIN forward of the same data). */
+int mm_mappo_bwd(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, mm_stream_t s);
+/* Weight gradients of one net from mm_mappo_bwd's SoA operands into its flat gradient vector. */
+int64_t mm_mappo_wgrad_partial_count(const mm_mappo_dims* d, int64_t rs);
+int mm_mappo_wgrad(const mm_mappo_dims* d, int32_t net, const float* gsoa, int64_t rs, float* grad, float* partial,
+                   mm_stream_t s);
+/* GAE with ValueNorm denormalisation (vn = float[3]: running mean, mean sq, debias): returns[t<T]. */
+int mm_mappo_gae(const float* rew, const float* value_preds, const float* masks, float* returns, const float* vn,
+                 int32_t T, int64_t en, float gamma, float gae_lambda, mm_stream_t s);
+/* adv = returns - denorm(value_preds) over rows = T*EN; masked mean/std, active count, return
+ * moments into stats. partial: device double[5 * 256]. */
+int mm_mappo_adv_stats(const float* returns, const float* value_preds, const float* active, const float* vn,
+                       float* adv, int64_t rows, double* partial, float* stats, mm_stream_t s);
+/* One ValueNorm.update with the batch moments in stats, then stats[VN_MEAN/VN_STD]. */
+int mm_mappo_vn_update(float* vn, float* stats, double beta, mm_stream_t s);
+/* After env.step: masks/active of slot t+1, zero hiddens of done envs (done [E] u8); increments
+ * the device RNG step counter (u64, may be NULL). */
+int mm_mappo_insert(const uint8_t* done, int32_t n_agents, int32_t hidden, int64_t n_envs, float* mask_next,
+                    float* active_next, float* h_actor, float* h_critic, uint64_t* counter, mm_stream_t s);
+
 #ifdef __cplusplus
 }
 #endif

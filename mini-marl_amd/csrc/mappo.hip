@@ -1,0 +1,1086 @@
+// MAPPO (rmappo, shared policy) hot path on gfx950: actor/critic trunk forward (rollout and
+// chunked training), PPO + clipped-Huber value loss fused into the chunked BPTT backward,
+// weight-gradient reduction on MFMA, GAE scan, advantage statistics, ValueNorm.
+//
+// Reference (behaviour restated in oracle/mappo.py, pinned by tests/golden/mappo_*.npz):
+//   trunk  mappo/utils/algorithm_utils/mlp.py:31-55 (LN(D); [Linear, ReLU, LN] x 2),
+//          rnn.py:24-29,79 (GRU on h*mask, LayerNorm on the output), act.py/distributions.py
+//          (Categorical), r_actor_critic.py:189-208 (v_out)
+//   train  mappo/algorithms/ramppo_network.py:56-209 (ppo_update, cal_value_loss),
+//          shared_buffer.py:318-427 (chunks of L steps; start hidden = stored hidden)
+//   GAE    shared_buffer.py:131-153 (+ valuenorm.py denormalize), f64 accumulator
+//
+// Design: hidden = 32, so one thread owns one row (rollout) or one L-step chunk (training):
+// LayerNorm / softmax / GRU gates are plain per-thread code, every weight read is an LDS
+// broadcast (the net's whole parameter vector, ~38 KB, is staged per block). The canonical
+// flat parameter layout (MGeo) is 16-byte aligned with W1 rows padded to Dp, so it IS the LDS
+// image (no pack step) and the Adam state shares it (pads stay exactly zero).
+#include "common.h"
+#include "minimarl.h"
+
+namespace mm {
+
+constexpr float kLnEps = 1e-5f;
+
+template <int D, int H, int O>
+struct MGeo {
+  static constexpr int Dp = (D + 3) & ~3, Op = (O + 3) & ~3;
+  static constexpr int ln0_w = 0, ln0_b = Dp, W1 = 2 * Dp, b1 = W1 + H * Dp, ln1_w = b1 + H, ln1_b = ln1_w + H;
+  static constexpr int W2 = ln1_b + H, b2 = W2 + H * H, ln2_w = b2 + H, ln2_b = ln2_w + H;
+  static constexpr int Wih = ln2_b + H, Whh = Wih + 3 * H * H, bih = Whh + 3 * H * H, bhh = bih + 3 * H;
+  static constexpr int lnr_w = bhh + 3 * H, lnr_b = lnr_w + H, Wo = lnr_b + H, bo = Wo + Op * H;
+  static constexpr int total = bo + Op;
+};
+
+// forward save fields (tiled SoA, see soa_col; row = t*EN + en), per net
+template <int H, int O>
+struct SF {
+  static constexpr int MU0 = 0, RS0 = 1, A1 = 2, MU1 = A1 + H, RS1 = MU1 + 1, A2 = RS1 + 1, MU2 = A2 + H,
+                       RS2 = MU2 + 1, HIN = RS2 + 1, R = HIN + H, Z = R + H, N = Z + H, GHN = N + H, H2 = GHN + H,
+                       MUR = H2 + H, RSR = MUR + 1, OUT = RSR + 1, NS = OUT + O;
+};
+// backward output fields (SoA), operands of the weight-gradient reduction
+template <int D, int H, int O>
+struct GF {
+  static constexpr int DOUT = 0, Y = DOUT + O, DGI = Y + H, X2 = DGI + 3 * H, DGH = X2 + H, HIN = DGH + 3 * H,
+                       DPRE2 = HIN + H, F1 = DPRE2 + H, DPRE1 = F1 + H, F0 = DPRE1 + H, DY = F0 + D, PY = DY + H,
+                       DX2 = PY + H, P2 = DX2 + H, DX1 = P2 + H, P1 = DX1 + H, DF0 = P1 + H, P0 = DF0 + D,
+                       NG = P0 + D;
+};
+
+// ------------------------------------------------------------------ per-thread building blocks
+template <int OUT, int IN, int LD>
+__device__ __forceinline__ void matvec(const float* __restrict__ W, const float* __restrict__ b, const float (&x)[IN],
+                                       float (&y)[OUT]) {
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+    float acc = b[o];
+#pragma unroll
+    for (int i = 0; i < IN; ++i) acc = fmaf(W[o * LD + i], x[i], acc);
+    y[o] = acc;
+  }
+}
+
+template <int OUT, int IN, int LD>
+__device__ __forceinline__ void matvec_t(const float* __restrict__ W, const float (&d)[OUT], float (&dx)[IN]) {
+#pragma unroll
+  for (int i = 0; i < IN; ++i) dx[i] = 0.0f;
+#pragma unroll
+  for (int o = 0; o < OUT; ++o)
+#pragma unroll
+    for (int i = 0; i < IN; ++i) dx[i] = fmaf(W[o * LD + i], d[o], dx[i]);
+}
+
+template <int N>
+__device__ __forceinline__ void ln_stats(const float (&x)[N], float& mu, float& rs) {
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s += x[i];
+  mu = s / (float)N;
+  float v = 0.0f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v = fmaf(x[i] - mu, x[i] - mu, v);
+  rs = 1.0f / sqrtf(v / (float)N + kLnEps);
+}
+
+template <int N>
+__device__ __forceinline__ void ln_apply(const float (&x)[N], float mu, float rs, const float* w, const float* b,
+                                         float (&y)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) y[i] = (x[i] - mu) * rs * w[i] + b[i];
+}
+
+// dx = rs * (g - mean(g) - xhat * mean(g * xhat)), g = dy * w
+template <int N>
+__device__ __forceinline__ void ln_bwd(const float (&dy)[N], const float (&xh)[N], float rs, const float* w,
+                                       float (&dx)[N]) {
+  float sg = 0.0f, sgx = 0.0f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float g = dy[i] * w[i];
+    sg += g;
+    sgx = fmaf(g, xh[i], sgx);
+  }
+  sg /= (float)N;
+  sgx /= (float)N;
+#pragma unroll
+  for (int i = 0; i < N; ++i) dx[i] = rs * (dy[i] * w[i] - sg - xh[i] * sgx);
+}
+
+// Tiled SoA arrays: rows in tiles of 64, [tile][field][64] -> a field's 64 rows are contiguous
+// (coalesced per wave) and the field stride is the compile-time 64 floats.
+__device__ __forceinline__ float* soa_col(float* base, int64_t row, int nf) {
+  return base + (row >> 6) * (int64_t)nf * 64 + (row & 63);
+}
+__device__ __forceinline__ const float* soa_col(const float* base, int64_t row, int nf) {
+  return base + (row >> 6) * (int64_t)nf * 64 + (row & 63);
+}
+
+template <int D>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, float (&x)[D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i) x[i] = p[i];
+}
+
+// Stage a net's flat parameters (multiple of 4 floats) into LDS.
+__device__ __forceinline__ void stage_params(float* sm, const float* __restrict__ P, int n) {
+  const float4* s = reinterpret_cast<const float4*>(P);
+  float4* d = reinterpret_cast<float4*>(sm);
+  for (int i = threadIdx.x; i < n / 4; i += blockDim.x) d[i] = s[i];
+  __syncthreads();
+}
+
+// One trunk step; fills the save slots if sv != nullptr.
+template <int D, int H, int O>
+struct Trunk {
+  using G = MGeo<D, H, O>;
+  using S = SF<H, O>;
+  // sv: this row's column of a tiled SoA array (field stride 64, see soa_col)
+  __device__ static __forceinline__ void step(const float* W, const float (&x)[D], float (&h)[H], float (&out)[O],
+                                              float* sv) {
+    float mu, rs;
+    ln_stats<D>(x, mu, rs);
+    float f0[D];
+    ln_apply<D>(x, mu, rs, W + G::ln0_w, W + G::ln0_b, f0);
+    if (sv) {
+      sv[S::MU0 * 64] = mu;
+      sv[S::RS0 * 64] = rs;
+    }
+    float a[H], f[H];
+    matvec<H, D, G::Dp>(W + G::W1, W + G::b1, f0, a);
+#pragma unroll
+    for (int i = 0; i < H; ++i) a[i] = fmaxf(a[i], 0.0f);
+    ln_stats<H>(a, mu, rs);
+    if (sv) {
+#pragma unroll
+      for (int i = 0; i < H; ++i) sv[(S::A1 + i) * 64] = a[i];
+      sv[S::MU1 * 64] = mu;
+      sv[S::RS1 * 64] = rs;
+    }
+    ln_apply<H>(a, mu, rs, W + G::ln1_w, W + G::ln1_b, f);
+    matvec<H, H, H>(W + G::W2, W + G::b2, f, a);
+#pragma unroll
+    for (int i = 0; i < H; ++i) a[i] = fmaxf(a[i], 0.0f);
+    ln_stats<H>(a, mu, rs);
+    if (sv) {
+#pragma unroll
+      for (int i = 0; i < H; ++i) sv[(S::A2 + i) * 64] = a[i];
+      sv[S::MU2 * 64] = mu;
+      sv[S::RS2 * 64] = rs;
+    }
+    ln_apply<H>(a, mu, rs, W + G::ln2_w, W + G::ln2_b, f);
+    // GRU (torch gate order r, z, n; h' = n + z * (h - n))
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      float gir = W[G::bih + j], giz = W[G::bih + H + j], gin = W[G::bih + 2 * H + j];
+      float ghr = W[G::bhh + j], ghz = W[G::bhh + H + j], ghn = W[G::bhh + 2 * H + j];
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        gir = fmaf(W[G::Wih + j * H + i], f[i], gir);
+        giz = fmaf(W[G::Wih + (H + j) * H + i], f[i], giz);
+        gin = fmaf(W[G::Wih + (2 * H + j) * H + i], f[i], gin);
+        ghr = fmaf(W[G::Whh + j * H + i], h[i], ghr);
+        ghz = fmaf(W[G::Whh + (H + j) * H + i], h[i], ghz);
+        ghn = fmaf(W[G::Whh + (2 * H + j) * H + i], h[i], ghn);
+      }
+      const float r = sigmoidf_(gir + ghr);
+      const float z = sigmoidf_(giz + ghz);
+      const float n = tanhf_(gin + r * ghn);
+      a[j] = n + z * (h[j] - n);  // new hidden (h still needed by later j)
+      if (sv) {
+        sv[(S::HIN + j) * 64] = h[j];
+        sv[(S::R + j) * 64] = r;
+        sv[(S::Z + j) * 64] = z;
+        sv[(S::N + j) * 64] = n;
+        sv[(S::GHN + j) * 64] = ghn;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) h[j] = a[j];
+    ln_stats<H>(h, mu, rs);
+    if (sv) {
+#pragma unroll
+      for (int j = 0; j < H; ++j) sv[(S::H2 + j) * 64] = h[j];
+      sv[S::MUR * 64] = mu;
+      sv[S::RSR * 64] = rs;
+    }
+    ln_apply<H>(h, mu, rs, W + G::lnr_w, W + G::lnr_b, f);
+    matvec<O, H, H>(W + G::Wo, W + G::bo, f, out);
+  }
+};
+
+// log-softmax in place (logits -> logp), returns entropy
+template <int A>
+__device__ __forceinline__ float log_softmax(float (&l)[A]) {
+  float mx = l[0];
+#pragma unroll
+  for (int a = 1; a < A; ++a) mx = fmaxf(mx, l[a]);
+  float s = 0.0f;
+#pragma unroll
+  for (int a = 0; a < A; ++a) s += expf(l[a] - mx);
+  const float lse = mx + logf(s);
+  float ent = 0.0f;
+#pragma unroll
+  for (int a = 0; a < A; ++a) {
+    l[a] -= lse;
+    ent -= expf(l[a]) * l[a];
+  }
+  return ent;
+}
+
+// ------------------------------------------------------------------ forward kernel
+template <int D, int H, int A>
+__device__ __forceinline__ void fwd_body(const mm_mappo_fwd_args& a, int net, float* sm) {
+  using TA = Trunk<D, H, A>;
+  using TC = Trunk<D, H, 1>;
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const mm_mappo_net_io& io = a.net[net];
+  if (a.mode != MM_MAPPO_TRAIN) {
+    // rollout / get_values: one row per thread
+    if (tid >= a.rows) return;
+    float x[D], h[H];
+    load_row<D>(a.obs + tid * D, x);
+    const float m = a.mask ? a.mask[tid] : 1.0f;
+    load_row<H>(io.h_in + tid * H, h);
+#pragma unroll
+    for (int i = 0; i < H; ++i) h[i] *= m;
+    if (net == 0) {
+      float l[A];
+      TA::step(sm, x, h, l, nullptr);
+      log_softmax<A>(l);
+      int act;
+      if (a.act_in) {
+        act = a.act_in[tid];
+      } else {
+        float u;
+        if (a.u) {
+          u = a.u[tid];
+        } else {
+          const uint64_t ctr = a.counter_ptr ? *a.counter_ptr : a.counter;
+          u = rng_uniform(rng_draw(a.seed, ctr, (uint64_t)tid, 0x9E37ull));
+        }
+        // inverse CDF: first k with u < cumsum(p)[k], the last action if rounding leaves none
+        act = A - 1;
+        bool found = false;
+        float cs = 0.0f;
+#pragma unroll
+        for (int q = 0; q < A; ++q) {
+          cs += expf(l[q]);
+          if (!found && u < cs) {
+            act = q;
+            found = true;
+          }
+        }
+        if (a.act_out) a.act_out[tid] = act;
+      }
+      float lp = l[0];
+#pragma unroll
+      for (int k = 1; k < A; ++k)
+        if (k == act) lp = l[k];
+      if (io.out) io.out[tid] = lp;
+    } else {
+      float v[1];
+      TC::step(sm, x, h, v, nullptr);
+      if (io.out) io.out[tid] = v[0];
+    }
+    if (io.h_out) {
+#pragma unroll
+      for (int i = 0; i < H; ++i) io.h_out[tid * H + i] = h[i];
+    }
+    return;
+  }
+  // training: one L-step chunk per thread; chunk c = k * EN + en covers t = k*L .. k*L+L-1
+  const int64_t EN = a.en, n_chunks = (int64_t)(a.T / a.L) * EN;
+  if (tid >= n_chunks) return;
+  const int64_t k = tid / EN, en = tid - k * EN;
+  float h[H];
+  load_row<H>(io.h_in + ((k * a.L) * EN + en) * H, h);
+  for (int l = 0; l < a.L; ++l) {
+    const int64_t row = (k * a.L + l) * EN + en;
+    float x[D];
+    load_row<D>(a.obs + row * D, x);
+    const float m = a.mask[row];
+#pragma unroll
+    for (int i = 0; i < H; ++i) h[i] *= m;
+    if (net == 0) {
+      float* sv = soa_col(io.save, row, SF<H, A>::NS);
+      float lg[A];
+      TA::step(sm, x, h, lg, sv);
+      log_softmax<A>(lg);
+#pragma unroll
+      for (int q = 0; q < A; ++q) sv[(SF<H, A>::OUT + q) * 64] = lg[q];
+    } else {
+      float* sv = soa_col(io.save, row, SF<H, 1>::NS);
+      float v[1];
+      TC::step(sm, x, h, v, sv);
+      sv[SF<H, 1>::OUT * 64] = v[0];
+    }
+  }
+}
+
+template <int D, int H, int A>
+__global__ __launch_bounds__(256) void mappo_fwd_kernel(mm_mappo_fwd_args a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int net = (int)blockIdx.y + (a.mode == MM_MAPPO_VALUES ? 1 : 0);
+  const int n = net == 0 ? MGeo<D, H, A>::total : MGeo<D, H, 1>::total;
+  stage_params(sm, a.net[net].P, n);
+  if (net == 0)
+    fwd_body<D, H, A>(a, 0, sm);
+  else
+    fwd_body<D, H, A>(a, 1, sm);
+}
+
+// ------------------------------------------------------------------ backward kernel
+// Per chunk, reverse over its L steps: loss seed (PPO clipped surrogate + entropy for the
+// actor, ValueNorm-targeted clipped Huber for the critic), then BPTT through head, LN_r, GRU,
+// LN2/L2, LN1/L1, LN0. Writes the (delta, input) operand pairs of every weight gradient.
+struct LossSeed {
+  float clip, huber_delta, entropy_coef, value_coef;
+};
+
+__device__ __forceinline__ float huber_d(float e, float d) { return fabsf(e) <= d ? e : (e > 0.f ? d : -d); }
+__device__ __forceinline__ float huber_f(float e, float d) {
+  return fabsf(e) <= d ? e * e * 0.5f : d * (fabsf(e) - d * 0.5f);
+}
+
+// SoA column access with the address kept in VGPRs: every 16-field window starts from an
+// opaque pointer (asm barrier) and uses immediate offsets, so the compiler cannot hoist ~1000
+// uniform field offsets into SGPRs (which spilled thousands of SGPRs).
+template <int N>
+__device__ __forceinline__ void soa_st(float* col, int f0, const float (&v)[N]) {
+#pragma unroll
+  for (int c = 0; c < N; c += 16) {
+    float* q = col + (f0 + c) * 64;
+    asm volatile("" : "+v"(q));
+#pragma unroll
+    for (int i = c; i < (N < c + 16 ? N : c + 16); ++i) q[(i - c) * 64] = v[i];
+  }
+}
+template <int N>
+__device__ __forceinline__ void soa_ld(const float* col, int f0, float (&v)[N]) {
+#pragma unroll
+  for (int c = 0; c < N; c += 16) {
+    const float* q = col + (f0 + c) * 64;
+    asm volatile("" : "+v"(q));
+#pragma unroll
+    for (int i = c; i < (N < c + 16 ? N : c + 16); ++i) v[i] = q[(i - c) * 64];
+  }
+}
+__device__ __forceinline__ float soa_ld1(const float* col, int f) {
+  const float* q = col + f * 64;
+  asm volatile("" : "+v"(q));
+  return *q;
+}
+
+template <int D, int H, int A, int O>
+__device__ __forceinline__ void bwd_body(const mm_mappo_bwd_args& a, int net, const float* W) {
+  using G = MGeo<D, H, O>;
+  using S = SF<H, O>;
+  using GF_ = GF<D, H, O>;
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t EN = a.en, n_chunks = (int64_t)(a.T / a.L) * EN;
+  if (tid >= n_chunks) return;
+  const int64_t k = tid / EN, en = tid - k * EN;
+  const float* sv0 = a.save[net];
+  float* go0 = a.gsoa[net];
+  const float inv_m = 1.0f / a.stats[MM_MST_ACTIVE_SUM];
+  float dh_next[H];
+#pragma unroll
+  for (int i = 0; i < H; ++i) dh_next[i] = 0.0f;
+  float lsum0 = 0.f, lsum1 = 0.f, lsum2 = 0.f;
+  for (int l = a.L - 1; l >= 0; --l) {
+    const int64_t row = (k * a.L + l) * EN + en;
+    const float* sv = soa_col(sv0, row, S::NS);
+    float* go = soa_col(go0, row, GF_::NG);
+    const float m = a.active[row];
+    // ---- loss seed d(out)
+    float dout[O];
+    if constexpr (O == A) {
+      float lp[A];
+      soa_ld<A>(sv, S::OUT, lp);
+      float ent = 0.0f;
+#pragma unroll
+      for (int q = 0; q < A; ++q) ent -= expf(lp[q]) * lp[q];
+      const int act = a.act[row];
+      float lpa = lp[0];
+#pragma unroll
+      for (int q = 1; q < A; ++q)
+        if (q == act) lpa = lp[q];
+      const float adv = (a.adv[row] - a.stats[MM_MST_ADV_MEAN]) / (a.stats[MM_MST_ADV_STD] + 1e-5f);
+      const float ratio = expf(lpa - a.old_logp[row]);
+      const float s1 = ratio * adv;
+      const float rc = fminf(fmaxf(ratio, 1.0f - a.clip), 1.0f + a.clip);
+      const float s2 = rc * adv;
+      const float inr = (ratio >= 1.0f - a.clip && ratio <= 1.0f + a.clip) ? 1.0f : 0.0f;
+      // torch.min backward: the smaller side gets the gradient, ties split it in half
+      const float g = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f + 0.5f * inr);
+      const float dlpa = -m * inv_m * adv * ratio * g;
+      const float dent = -a.entropy_coef * m * inv_m;
+      lsum0 += -fminf(s1, s2) * m;
+      lsum1 += ent * m;
+      lsum2 += ratio;
+#pragma unroll
+      for (int q = 0; q < A; ++q) {
+        const float p = expf(lp[q]);
+        dout[q] = dlpa * ((q == act ? 1.0f : 0.0f) - p) + dent * (-p * (lp[q] + ent));
+      }
+    } else {
+      const float v = soa_ld1(sv, S::OUT);
+      const float old = a.old_value[row];
+      const float tgt = (a.returns[row] - a.stats[MM_MST_VN_MEAN]) / a.stats[MM_MST_VN_STD];
+      const float dv = v - old;
+      const float vc = old + fminf(fmaxf(dv, -a.clip), a.clip);
+      const float eo = tgt - v, ec = tgt - vc;
+      const float lo = huber_f(eo, a.huber_delta), lc = huber_f(ec, a.huber_delta);
+      const float go_ = -huber_d(eo, a.huber_delta);
+      const float gc = -huber_d(ec, a.huber_delta) * ((dv >= -a.clip && dv <= a.clip) ? 1.0f : 0.0f);
+      const float d = lo > lc ? go_ : (lc > lo ? gc : 0.5f * (go_ + gc));
+      dout[0] = a.value_coef * m * inv_m * d;
+      lsum0 += fmaxf(lo, lc) * m;
+    }
+    // ---- head: y = LN_r(h2); out = Wo y + bo
+    float xr[H], t[H];
+    soa_ld<H>(sv, S::H2, t);
+    {
+      const float mur = soa_ld1(sv, S::MUR), rsr = soa_ld1(sv, S::RSR);
+      float y[H];
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        xr[i] = (t[i] - mur) * rsr;
+        y[i] = xr[i] * W[G::lnr_w + i] + W[G::lnr_b + i];
+      }
+      soa_st<O>(go, GF_::DOUT, dout);
+      soa_st<H>(go, GF_::Y, y);
+      float dy[H], dh[H];
+      matvec_t<O, H, H>(W + G::Wo, dout, dy);
+      ln_bwd<H>(dy, xr, rsr, W + G::lnr_w, dh);
+      soa_st<H>(go, GF_::DY, dy);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        t[i] = dy[i] * xr[i];
+        xr[i] = dh[i] + dh_next[i];  // xr now holds d(h2)
+      }
+      soa_st<H>(go, GF_::PY, t);
+    }
+    // ---- GRU (h2 = n + z (h - n), gates r, z, n)
+    float dgi[3 * H], dgh[3 * H], hin[H];
+    {
+      float r[H], z[H], n[H], ghn[H];
+      soa_ld<H>(sv, S::R, r);
+      soa_ld<H>(sv, S::Z, z);
+      soa_ld<H>(sv, S::N, n);
+      soa_ld<H>(sv, S::GHN, ghn);
+      soa_ld<H>(sv, S::HIN, hin);
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        const float dh = xr[j];
+        const float dn = dh * (1.0f - z[j]);
+        const float dz = dh * (hin[j] - n[j]);
+        dh_next[j] = dh * z[j];  // direct path; Whh^T dgh added below
+        const float dpn = dn * (1.0f - n[j] * n[j]);
+        const float dr = dpn * ghn[j];
+        dgi[j] = dr * r[j] * (1.0f - r[j]);
+        dgi[H + j] = dz * z[j] * (1.0f - z[j]);
+        dgi[2 * H + j] = dpn;
+        dgh[j] = dgi[j];
+        dgh[H + j] = dgi[H + j];
+        dgh[2 * H + j] = dpn * r[j];
+      }
+    }
+    soa_st<3 * H>(go, GF_::DGI, dgi);
+    soa_st<3 * H>(go, GF_::DGH, dgh);
+    soa_st<H>(go, GF_::HIN, hin);
+    {
+      matvec_t<3 * H, H, H>(W + G::Whh, dgh, t);
+      const float mk = a.mask[row];
+#pragma unroll
+      for (int i = 0; i < H; ++i) dh_next[i] = (dh_next[i] + t[i]) * mk;
+    }
+    // ---- x2 = LN2(a2) (input of the GRU)
+    float ah[H], xh[H], dx[H], da[H];
+    {
+      soa_ld<H>(sv, S::A2, ah);
+      const float mu = soa_ld1(sv, S::MU2), rs = soa_ld1(sv, S::RS2);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        xh[i] = (ah[i] - mu) * rs;
+        t[i] = xh[i] * W[G::ln2_w + i] + W[G::ln2_b + i];
+      }
+      soa_st<H>(go, GF_::X2, t);
+      matvec_t<3 * H, H, H>(W + G::Wih, dgi, dx);
+      ln_bwd<H>(dx, xh, rs, W + G::ln2_w, da);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        t[i] = dx[i] * xh[i];
+        da[i] = ah[i] > 0.0f ? da[i] : 0.0f;
+      }
+      soa_st<H>(go, GF_::DX2, dx);
+      soa_st<H>(go, GF_::P2, t);
+      soa_st<H>(go, GF_::DPRE2, da);
+    }
+    // ---- x1 = LN1(a1) (input of L2)
+    {
+      soa_ld<H>(sv, S::A1, ah);
+      const float mu = soa_ld1(sv, S::MU1), rs = soa_ld1(sv, S::RS1);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        xh[i] = (ah[i] - mu) * rs;
+        t[i] = xh[i] * W[G::ln1_w + i] + W[G::ln1_b + i];
+      }
+      soa_st<H>(go, GF_::F1, t);
+      matvec_t<H, H, H>(W + G::W2, da, dx);
+      ln_bwd<H>(dx, xh, rs, W + G::ln1_w, da);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        t[i] = dx[i] * xh[i];
+        da[i] = ah[i] > 0.0f ? da[i] : 0.0f;
+      }
+      soa_st<H>(go, GF_::DX1, dx);
+      soa_st<H>(go, GF_::P1, t);
+      soa_st<H>(go, GF_::DPRE1, da);
+    }
+    // ---- f0 = LN0(obs) (input of L1)
+    {
+      float x0[D], df0[D];
+      load_row<D>(a.obs + row * D, x0);
+      const float mu = soa_ld1(sv, S::MU0), rs = soa_ld1(sv, S::RS0);
+      matvec_t<H, D, G::Dp>(W + G::W1, da, df0);
+      soa_st<D>(go, GF_::DF0, df0);
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const float xh0 = (x0[i] - mu) * rs;
+        df0[i] *= xh0;
+        x0[i] = xh0 * W[G::ln0_w + i] + W[G::ln0_b + i];
+      }
+      soa_st<D>(go, GF_::P0, df0);
+      soa_st<D>(go, GF_::F0, x0);
+    }
+  }
+  if (a.loss_acc) {
+    // logging only (train_info): wave-level sums, one atomic per wave
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lsum0 += __shfl_xor(lsum0, o);
+      lsum1 += __shfl_xor(lsum1, o);
+      lsum2 += __shfl_xor(lsum2, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      if constexpr (O == A) {
+        atomicAdd(&a.loss_acc[MM_MLOSS_POLICY], lsum0 * inv_m);
+        atomicAdd(&a.loss_acc[MM_MLOSS_ENTROPY], lsum1 * inv_m);
+        atomicAdd(&a.loss_acc[MM_MLOSS_RATIO], lsum2);
+      } else {
+        atomicAdd(&a.loss_acc[MM_MLOSS_VALUE], lsum0 * inv_m);
+      }
+    }
+  }
+}
+
+template <int D, int H, int A>
+__global__ __launch_bounds__(256) void mappo_bwd_kernel(mm_mappo_bwd_args a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int net = blockIdx.y;
+  const int n = net == 0 ? MGeo<D, H, A>::total : MGeo<D, H, 1>::total;
+  stage_params(sm, a.P[net], n);
+  if (net == 0)
+    bwd_body<D, H, A, A>(a, 0, sm);
+  else
+    bwd_body<D, H, A, 1>(a, 1, sm);
+}
+
+// ------------------------------------------------------------------ weight-gradient reduction
+// dW[M][K] = sum_r A[m][r] * B[k][r], db[m] = sum_r A[m][r] over tiled SoA operands (soa_col),
+// on v_mfma_f32_32x32x2_f32 with the reduction (row) index on the MFMA k dimension: lane (i, h)
+// of k-step s supplies row r0 + 16 h + s of feature i, so each lane streams 64 contiguous bytes
+// per operand per 32 rows. Every block reduces one job over one row range for all (m, k) tiles
+// of the job (operands read from HBM once) and writes a partial; a second kernel sums partials.
+struct WgJobDev {
+  const float* A;
+  const float* B;
+  float* dW;
+  float* db;
+  int M, K, ldw, blk0, nblk;
+  int64_t part;  // offset of this job's partials: (nblk * 4 waves) x (M*K + M)
+};
+struct WgArgsDev {
+  WgJobDev job[MM_MAPPO_MAX_JOBS];
+  int njobs;
+  int nf;  // fields of the tiled SoA operand array (tile stride nf * 64)
+  int64_t Rs, rows_per_block;
+  float* partial;
+};
+
+__device__ __forceinline__ void load16(const float* p, bool ok, float (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 t = ok ? *reinterpret_cast<const float4*>(p + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[4 * q] = t.x;
+    v[4 * q + 1] = t.y;
+    v[4 * q + 2] = t.z;
+    v[4 * q + 3] = t.w;
+  }
+}
+
+// Jobs are split on the host so that M <= 96 (3 m-tiles) and K <= 64 (2 k-tiles).
+__global__ __launch_bounds__(256) void mappo_wgrad_kernel(WgArgsDev a) {
+  int j = 0;
+  while (j + 1 < a.njobs && (int)blockIdx.x >= a.job[j + 1].blk0) ++j;
+  const WgJobDev& jb = a.job[j];
+  const int b = blockIdx.x - jb.blk0;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hh = lane >> 5;
+  const int MT = (jb.M + 31) / 32, KT = (jb.K + 31) / 32;
+  const int64_t r_begin = (int64_t)b * a.rows_per_block;
+  const int64_t r_end = min(r_begin + a.rows_per_block, a.Rs);
+  const int64_t tile = (int64_t)a.nf * 64;
+  f32x16 acc[3][2];
+  float cs[3];
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt) {
+    cs[mt] = 0.0f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc[mt][kt][s] = 0.0f;
+  }
+  for (int64_t r = r_begin + wave * 32; r < r_end; r += 128) {
+    float av[3][16], bv[2][16];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) {
+      const int m = mt * 32 + i;
+      const bool ok = mt < MT && m < jb.M;
+      load16(jb.A + (ok ? (r >> 6) * tile + m * 64 + (r & 63) + 16 * hh : 0), ok, av[mt]);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) cs[mt] += av[mt][s];
+    }
+    if (KT > 0) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int kk = kt * 32 + i;
+        const bool ok = kt < KT && kk < jb.K;
+        load16(jb.B + (ok ? (r >> 6) * tile + kk * 64 + (r & 63) + 16 * hh : 0), ok, bv[kt]);
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+            if (mt < MT && kt < KT) acc[mt][kt] = mfma32(av[mt][s], bv[kt][s], acc[mt][kt]);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt) cs[mt] += __shfl_xor(cs[mt], 32);
+  float* out = a.partial + jb.part + (int64_t)(b * 4 + wave) * (jb.M * jb.K + jb.M);
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int m = mt * 32 + kperm(s, hh), kk = kt * 32 + i;
+        if (m < jb.M && kk < jb.K) out[m * jb.K + kk] = acc[mt][kt][s];
+      }
+    const int m = mt * 32 + i;
+    if (hh == 0 && m < jb.M) out[jb.M * jb.K + m] = cs[mt];
+  }
+}
+
+__global__ __launch_bounds__(256) void mappo_wgrad_sum_kernel(WgArgsDev a) {
+  const WgJobDev& jb = a.job[blockIdx.y];
+  const int per = jb.M * jb.K + jb.M;
+  const int nw = jb.nblk * 4;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < per; e += gridDim.x * 256) {
+    float s = 0.0f;
+    const float* p = a.partial + jb.part + e;
+    for (int w = 0; w < nw; ++w) s += p[(int64_t)w * per];
+    if (e < jb.M * jb.K) {
+      if (jb.dW) jb.dW[(e / jb.K) * jb.ldw + e % jb.K] = s;
+    } else if (jb.db) {
+      jb.db[e - jb.M * jb.K] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ GAE, advantages, ValueNorm
+// ValueNorm state (f32, valuenorm.py): vn[0] running_mean, vn[1] running_mean_sq, vn[2] debias.
+__device__ __forceinline__ void vn_mean_var(const float* vn, float& mean, float& var) {
+  const float d = fmaxf(vn[2], 1e-5f);
+  mean = vn[0] / d;
+  const float msq = vn[1] / d;
+  var = fmaxf(msq - mean * mean, 1e-2f);
+}
+
+// returns[t] for t < T, one thread per (env, agent) column; delta in f32, gae in f64 (shared_buffer.py:141-148)
+__global__ __launch_bounds__(256) void mappo_gae_kernel(const float* __restrict__ rew, const float* __restrict__ vp,
+                                                        const float* __restrict__ masks, float* __restrict__ ret,
+                                                        const float* __restrict__ vn, int T, int64_t EN, float gamma,
+                                                        float gl) {
+#pragma clang fp contract(off)
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (c >= EN) return;
+  float mean, var;
+  vn_mean_var(vn, mean, var);
+  const float sd = sqrtf(var);
+  double gae = 0.0;
+  float dn1 = vp[(int64_t)T * EN + c] * sd + mean;
+  for (int t = T - 1; t >= 0; --t) {
+    const float dn0 = vp[(int64_t)t * EN + c] * sd + mean;
+    const float m1 = masks[(int64_t)(t + 1) * EN + c];
+    const float delta = (rew[(int64_t)t * EN + c] + (gamma * dn1) * m1) - dn0;
+    gae = (double)delta + (double)(gl * m1) * gae;
+    ret[(int64_t)t * EN + c] = (float)(gae + (double)dn0);
+    dn1 = dn0;
+  }
+}
+
+// adv = returns - denorm(value_preds) over t < T; block partials of (sum, count) over active rows,
+// plus (sum ret, sum ret^2) over all rows for the ValueNorm batch statistics.
+__global__ __launch_bounds__(256) void mappo_adv_kernel(const float* __restrict__ ret, const float* __restrict__ vp,
+                                                        const float* __restrict__ active, const float* __restrict__ vn,
+                                                        float* __restrict__ adv, int64_t R, double* __restrict__ part) {
+#pragma clang fp contract(off)
+  __shared__ double sh[4][256];
+  float mean, var;
+  vn_mean_var(vn, mean, var);
+  const float sd = sqrtf(var);
+  double s = 0, n = 0, sr = 0, sr2 = 0;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < R; i += (int64_t)gridDim.x * 256) {
+    const float v = ret[i] - (vp[i] * sd + mean);
+    adv[i] = v;
+    if (active[i] != 0.0f) {
+      s += v;
+      n += 1.0;
+    }
+    sr += ret[i];
+    sr2 += (double)ret[i] * ret[i];
+  }
+  sh[0][threadIdx.x] = s;
+  sh[1][threadIdx.x] = n;
+  sh[2][threadIdx.x] = sr;
+  sh[3][threadIdx.x] = sr2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int q = 0; q < 4; ++q) sh[q][threadIdx.x] += sh[q][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) part[blockIdx.x * 4 + threadIdx.x] = sh[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(256) void mappo_adv_var_kernel(const float* __restrict__ adv,
+                                                            const float* __restrict__ active, int64_t R,
+                                                            const double* __restrict__ part, int nb,
+                                                            double* __restrict__ part2) {
+  __shared__ double sh[256];
+  __shared__ double s_mean;
+  if (threadIdx.x == 0) {
+    double s = 0, n = 0;
+    for (int b = 0; b < nb; ++b) {
+      s += part[b * 4];
+      n += part[b * 4 + 1];
+    }
+    s_mean = n > 0 ? s / n : 0.0;
+  }
+  __syncthreads();
+  const double mu = s_mean;
+  double q = 0;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < R; i += (int64_t)gridDim.x * 256)
+    if (active[i] != 0.0f) q += ((double)adv[i] - mu) * ((double)adv[i] - mu);
+  sh[threadIdx.x] = q;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part2[blockIdx.x] = sh[0];
+}
+
+// stats[]: adv mean/std, active count, ValueNorm batch moments (mean of returns, of returns^2)
+__global__ void mappo_stats_kernel(const double* part, const double* part2, int nb, int64_t R, float* stats) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0, n = 0, sr = 0, sr2 = 0, q = 0;
+  for (int b = 0; b < nb; ++b) {
+    s += part[b * 4];
+    n += part[b * 4 + 1];
+    sr += part[b * 4 + 2];
+    sr2 += part[b * 4 + 3];
+    q += part2[b];
+  }
+  stats[MM_MST_ADV_MEAN] = (float)(n > 0 ? s / n : 0.0);
+  stats[MM_MST_ADV_STD] = (float)(n > 0 ? sqrt(q / n) : 0.0);
+  stats[MM_MST_ACTIVE_SUM] = (float)n;
+  stats[MM_MST_RET_MEAN] = (float)(sr / (double)R);
+  stats[MM_MST_RET_SQ_MEAN] = (float)(sr2 / (double)R);
+}
+
+// One ValueNorm.update(returns) (valuenorm.py:37-54, f32, weight = beta) followed by the
+// normalisation constants for this epoch's value loss.
+__global__ void mappo_vn_update_kernel(float* vn, float* stats, float w, float omw) {
+#pragma clang fp contract(off)
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  vn[0] = vn[0] * w + stats[MM_MST_RET_MEAN] * omw;
+  vn[1] = vn[1] * w + stats[MM_MST_RET_SQ_MEAN] * omw;
+  vn[2] = vn[2] * w + omw;
+  float mean, var;
+  vn_mean_var(vn, mean, var);
+  stats[MM_MST_VN_MEAN] = mean;
+  stats[MM_MST_VN_STD] = sqrtf(var);
+}
+
+// Rollout insert after env.step (magym_runner.py:151-195): masks[t+1] = 0 and zero hiddens for
+// done envs, active masks 1 (env-level done: every agent finishes together).
+__global__ __launch_bounds__(256) void mappo_insert_kernel(const uint8_t* __restrict__ done, int N, int H, int64_t E,
+                                                           float* __restrict__ mask_next, float* __restrict__ active_next,
+                                                           float* __restrict__ ha, float* __restrict__ hc,
+                                                           uint64_t* counter) {
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;  // (env, agent, feature) over E*N*H
+  if (i == 0 && counter) *counter += 1;  // device RNG step counter of the next rollout step
+  if (i >= E * N * H) return;
+  const int64_t row = i / H, e = row / N;
+  const bool d = done[e] != 0;
+  if (d) {
+    ha[i] = 0.0f;
+    hc[i] = 0.0f;
+  }
+  if (i % H == 0) {
+    mask_next[row] = d ? 0.0f : 1.0f;
+    active_next[row] = 1.0f;
+  }
+}
+
+// ------------------------------------------------------------------ host dispatch
+template <int D, int H, int A>
+struct MappoShape {
+  using GA = MGeo<D, H, A>;
+  using GC = MGeo<D, H, 1>;
+  static int fwd(const mm_mappo_fwd_args* a, hipStream_t s) {
+    const int64_t n = a->mode == MM_MAPPO_TRAIN ? (int64_t)(a->T / a->L) * a->en : a->rows;
+    if (n <= 0) return MM_OK;
+    const int nets = a->mode == MM_MAPPO_VALUES ? 1 : 2;
+    hipLaunchKernelGGL((mappo_fwd_kernel<D, H, A>), dim3((unsigned)((n + 255) / 256), nets), dim3(256),
+                       (size_t)GA::total * 4, s, *a);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
+  static int bwd(const mm_mappo_bwd_args* a, hipStream_t s) {
+    const int64_t n = (int64_t)(a->T / a->L) * a->en;
+    if (n <= 0) return MM_OK;
+    hipLaunchKernelGGL((mappo_bwd_kernel<D, H, A>), dim3((unsigned)((n + 255) / 256), 2), dim3(256),
+                       (size_t)GA::total * 4, s, *a);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
+  // job list of one net's weight gradients (outputs in the net's flat gradient vector)
+  template <int O>
+  static int jobs(const float* gsoa, int64_t Rs, float* grad, WgJobDev* jv) {
+    using G = MGeo<D, H, O>;
+    using F = GF<D, H, O>;
+    int nj = 0;
+    auto add = [&](int fa, int M, int fb, int K, int wofs, int ld, int bofs) {
+      for (int m0 = 0; m0 < M; m0 += 96)
+        for (int k0 = 0; k0 < (K > 0 ? K : 1); k0 += 64) {
+          WgJobDev& j = jv[nj++];
+          j.M = M - m0 < 96 ? M - m0 : 96;
+          j.K = K > 0 ? (K - k0 < 64 ? K - k0 : 64) : 0;
+          j.A = gsoa + (int64_t)(fa + m0) * 64;
+          j.B = K > 0 ? gsoa + (int64_t)(fb + k0) * 64 : nullptr;
+          j.dW = K > 0 ? grad + wofs + m0 * ld + k0 : nullptr;
+          j.ldw = ld;
+          j.db = (k0 == 0 && bofs >= 0) ? grad + bofs + m0 : nullptr;
+        }
+    };
+    add(F::DOUT, O, F::Y, H, G::Wo, H, G::bo);
+    add(F::DGI, 3 * H, F::X2, H, G::Wih, H, G::bih);
+    add(F::DGH, 3 * H, F::HIN, H, G::Whh, H, G::bhh);
+    add(F::DPRE2, H, F::F1, H, G::W2, H, G::b2);
+    add(F::DPRE1, H, F::F0, D, G::W1, G::Dp, G::b1);
+    add(F::DY, H, 0, 0, 0, 0, G::lnr_b);
+    add(F::PY, H, 0, 0, 0, 0, G::lnr_w);
+    add(F::DX2, H, 0, 0, 0, 0, G::ln2_b);
+    add(F::P2, H, 0, 0, 0, 0, G::ln2_w);
+    add(F::DX1, H, 0, 0, 0, 0, G::ln1_b);
+    add(F::P1, H, 0, 0, 0, 0, G::ln1_w);
+    add(F::DF0, D, 0, 0, 0, 0, G::ln0_b);
+    add(F::P0, D, 0, 0, 0, 0, G::ln0_w);
+    return nj;
+  }
+  static int64_t rows_per_block(int64_t Rs) {
+    int64_t rpb = (Rs + 399) / 400;
+    rpb = (rpb + 127) / 128 * 128;
+    return rpb < 128 ? 128 : rpb;
+  }
+  static int64_t partial_count(int64_t Rs) {
+    WgJobDev jv[2 * MM_MAPPO_MAX_JOBS];
+    const int64_t nblk = (Rs + rows_per_block(Rs) - 1) / rows_per_block(Rs);
+    int64_t tot = 0;
+    for (int net = 0; net < 2; ++net) {
+      const int nj = net == 0 ? jobs<A>(nullptr, Rs, nullptr, jv) : jobs<1>(nullptr, Rs, nullptr, jv);
+      for (int q = 0; q < nj; ++q) tot += nblk * 4 * (int64_t)(jv[q].M * jv[q].K + jv[q].M);
+    }
+    return tot;
+  }
+  static int wgrad(int net, const float* gsoa, int64_t Rs, float* grad, float* partial, hipStream_t s) {
+    WgArgsDev w = {};
+    w.Rs = Rs;
+    w.rows_per_block = rows_per_block(Rs);
+    w.partial = partial;
+    w.njobs = net == 0 ? jobs<A>(gsoa, Rs, grad, w.job) : jobs<1>(gsoa, Rs, grad, w.job);
+    w.nf = net == 0 ? GF<D, H, A>::NG : GF<D, H, 1>::NG;
+    const int nblk = (int)((Rs + w.rows_per_block - 1) / w.rows_per_block);
+    int64_t part = 0;
+    int blk = 0, maxper = 0;
+    for (int q = 0; q < w.njobs; ++q) {
+      w.job[q].blk0 = blk;
+      w.job[q].nblk = nblk;
+      w.job[q].part = part;
+      const int per = w.job[q].M * w.job[q].K + w.job[q].M;
+      part += (int64_t)nblk * 4 * per;
+      blk += nblk;
+      maxper = per > maxper ? per : maxper;
+    }
+    hipLaunchKernelGGL(mappo_wgrad_kernel, dim3(blk), dim3(256), 0, s, w);
+    MM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(mappo_wgrad_sum_kernel, dim3((maxper + 255) / 256, w.njobs), dim3(256), 0, s, w);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
+};
+
+#define MM_MAPPO_DISPATCH(d, CALL)                                                  \
+  do {                                                                              \
+    if ((d)->hidden == 32 && (d)->n_actions == 5 && (d)->obs_dim == 47) {           \
+      using SH = mm::MappoShape<47, 32, 5>;                                           \
+      return CALL;                                                                  \
+    }                                                                               \
+    if ((d)->hidden == 32 && (d)->n_actions == 5 && (d)->obs_dim == 94) {           \
+      using SH = mm::MappoShape<94, 32, 5>;                                           \
+      return CALL;                                                                  \
+    }                                                                               \
+    mm::set_error("mappo: unsupported dims D=%d H=%d A=%d (supported: D 47|94, H 32, A 5)", (d)->obs_dim, \
+              (d)->hidden, (d)->n_actions);                                         \
+    return MM_EINVAL;                                                               \
+  } while (0)
+
+static int64_t param_count(const mm_mappo_dims* d, int net) {
+  if (d->hidden == 32 && d->n_actions == 5 && d->obs_dim == 47)
+    return net == 0 ? MGeo<47, 32, 5>::total : MGeo<47, 32, 1>::total;
+  if (d->hidden == 32 && d->n_actions == 5 && d->obs_dim == 94)
+    return net == 0 ? MGeo<94, 32, 5>::total : MGeo<94, 32, 1>::total;
+  return -1;
+}
+
+}  // namespace mm
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+int64_t mm_mappo_param_count(const mm_mappo_dims* d, int32_t net) {
+  if (!d || net < 0 || net > 1) return -1;
+  return mm::param_count(d, net);
+}
+
+int mm_mappo_param_offsets(const mm_mappo_dims* d, int32_t net, int64_t offs[19]) {
+  MM_REQUIRE(d && offs && (net == 0 || net == 1), "mappo_param_offsets: bad args");
+  MM_REQUIRE(mm::param_count(d, net) > 0, "mappo: unsupported dims D=%d H=%d A=%d", d->obs_dim, d->hidden,
+             d->n_actions);
+  const int H = d->hidden, O = net == 0 ? d->n_actions : 1;
+  const int Dp = (d->obs_dim + 3) & ~3, Op = (O + 3) & ~3;
+  int64_t c = 0;
+  const int64_t sz[18] = {Dp, Dp, (int64_t)H * Dp, H, H, H, (int64_t)H * H, H, H, H, 3ll * H * H, 3ll * H * H,
+                          3 * H, 3 * H, H, H, (int64_t)Op * H, Op};
+  for (int i = 0; i < 18; ++i) {
+    offs[i] = c;
+    c += sz[i];
+  }
+  offs[18] = c;
+  return MM_OK;
+}
+
+int mm_mappo_save_fields(const mm_mappo_dims* d, int32_t net) {
+  if (!d) return -1;
+  return 8 + 8 * d->hidden + (net == 0 ? d->n_actions : 1);
+}
+
+int mm_mappo_grad_fields(const mm_mappo_dims* d, int32_t net) {
+  if (!d) return -1;
+  return (net == 0 ? d->n_actions : 1) + 18 * d->hidden + 3 * d->obs_dim;
+}
+
+int mm_mappo_fwd(const mm_mappo_dims* d, const mm_mappo_fwd_args* a, mm_stream_t s) {
+  MM_REQUIRE(d && a, "mappo_fwd: null argument");
+  MM_REQUIRE(a->obs && a->net[1].P && a->net[1].h_in, "mappo_fwd: obs / critic params / hiddens required");
+  MM_REQUIRE(a->mode == MM_MAPPO_VALUES || (a->net[0].P && a->net[0].h_in), "mappo_fwd: actor params required");
+  MM_REQUIRE(a->mode != MM_MAPPO_TRAIN ||
+                 (a->L > 0 && a->T % a->L == 0 && a->mask && a->net[0].save && a->net[1].save && a->rs >= a->T * a->en),
+             "mappo_fwd: train mode needs L | T, masks, save buffers and rs >= T*EN");
+  MM_MAPPO_DISPATCH(d, SH::fwd(a, (hipStream_t)s));
+}
+
+int mm_mappo_bwd(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, mm_stream_t s) {
+  MM_REQUIRE(d && a, "mappo_bwd: null argument");
+  MM_REQUIRE(a->L > 0 && a->T % a->L == 0 && a->rs >= a->T * a->en && a->rs % 64 == 0,
+             "mappo_bwd: need L | T and rs >= T*EN, rs % 64 == 0");
+  MM_REQUIRE(a->P[0] && a->P[1] && a->save[0] && a->save[1] && a->gsoa[0] && a->gsoa[1] && a->obs && a->mask &&
+                 a->active && a->act && a->adv && a->old_logp && a->old_value && a->returns && a->stats,
+             "mappo_bwd: null pointer");
+  MM_MAPPO_DISPATCH(d, SH::bwd(a, (hipStream_t)s));
+}
+
+int64_t mm_mappo_wgrad_partial_count(const mm_mappo_dims* d, int64_t rs) {
+  if (!d || mm::param_count(d, 0) < 0) return -1;
+  if (d->obs_dim == 47) return mm::MappoShape<47, 32, 5>::partial_count(rs);
+  return mm::MappoShape<94, 32, 5>::partial_count(rs);
+}
+
+int mm_mappo_wgrad(const mm_mappo_dims* d, int32_t net, const float* gsoa, int64_t rs, float* grad, float* partial,
+                   mm_stream_t s) {
+  MM_REQUIRE(d && gsoa && grad && partial && (net == 0 || net == 1) && rs % 64 == 0, "mappo_wgrad: bad args");
+  MM_MAPPO_DISPATCH(d, SH::wgrad(net, gsoa, rs, grad, partial, (hipStream_t)s));
+}
+
+int mm_mappo_gae(const float* rew, const float* value_preds, const float* masks, float* returns, const float* vn,
+                 int32_t T, int64_t en, float gamma, float gae_lambda, mm_stream_t s) {
+  MM_REQUIRE(rew && value_preds && masks && returns && vn && T > 0 && en > 0, "mappo_gae: bad args");
+  const float gl = (float)((double)gamma * (double)gae_lambda);
+  hipLaunchKernelGGL(mm::mappo_gae_kernel, dim3((unsigned)((en + 255) / 256)), dim3(256), 0, (hipStream_t)s, rew,
+                     value_preds, masks, returns, vn, T, en, gamma, gl);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mappo_adv_stats(const float* returns, const float* value_preds, const float* active, const float* vn,
+                       float* adv, int64_t rows, double* partial, float* stats, mm_stream_t s) {
+  MM_REQUIRE(returns && value_preds && active && vn && adv && partial && stats && rows > 0, "mappo_adv_stats: bad args");
+  const int nb = 256;
+  hipLaunchKernelGGL(mm::mappo_adv_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, returns, value_preds, active, vn,
+                     adv, rows, partial);
+  MM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(mm::mappo_adv_var_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, adv, active, rows, partial, nb,
+                     partial + 4 * nb);
+  MM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(mm::mappo_stats_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, partial, partial + 4 * nb, nb, rows,
+                     stats);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mappo_vn_update(float* vn, float* stats, double beta, mm_stream_t s) {
+  MM_REQUIRE(vn && stats, "mappo_vn_update: null pointer");
+  // torch: running.mul_(beta) casts the double beta to f32; (1.0 - beta) is formed in double first
+  hipLaunchKernelGGL(mm::mappo_vn_update_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, vn, stats, (float)beta,
+                     (float)(1.0 - beta));
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mappo_insert(const uint8_t* done, int32_t n_agents, int32_t hidden, int64_t n_envs, float* mask_next,
+                    float* active_next, float* h_actor, float* h_critic, uint64_t* counter, mm_stream_t s) {
+  MM_REQUIRE(done && mask_next && active_next && h_actor && h_critic, "mappo_insert: null pointer");
+  const int64_t n = n_envs * n_agents * hidden;
+  hipLaunchKernelGGL(mm::mappo_insert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)s, done,
+                     n_agents, hidden, n_envs, mask_next, active_next, h_actor, h_critic, counter);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+}  // extern "C"

@@ -158,3 +158,49 @@ _SIGS += [
     ("mm_clip_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
                              c_vp, c_f32, c_vp]),
 ]
+
+
+# ------------------------------------------------------------------ MAPPO (include/minimarl.h)
+MM_MAPPO_ROLLOUT, MM_MAPPO_VALUES, MM_MAPPO_TRAIN = 0, 1, 2
+MM_MST_ADV_MEAN, MM_MST_ADV_STD, MM_MST_ACTIVE_SUM, MM_MST_RET_MEAN, MM_MST_RET_SQ_MEAN, MM_MST_VN_MEAN, \
+    MM_MST_VN_STD = range(7)
+MM_MLOSS_POLICY, MM_MLOSS_ENTROPY, MM_MLOSS_VALUE, MM_MLOSS_RATIO = range(4)
+
+
+class MappoDims(ctypes.Structure):
+    _fields_ = [("obs_dim", c_i32), ("hidden", c_i32), ("n_actions", c_i32)]
+
+
+class MappoNetIO(ctypes.Structure):
+    _fields_ = [("P", c_vp), ("h_in", c_vp), ("h_out", c_vp), ("out", c_vp), ("save", c_vp)]
+
+
+class MappoFwdArgs(ctypes.Structure):
+    _fields_ = [("net", MappoNetIO * 2), ("obs", c_vp), ("mask", c_vp), ("act_in", c_vp), ("act_out", c_vp),
+                ("u", c_vp), ("seed", c_u64), ("counter_ptr", c_vp), ("counter", c_u64), ("rows", c_i64),
+                ("en", c_i64), ("T", c_i32), ("L", c_i32), ("rs", c_i64), ("mode", c_i32)]
+
+
+class MappoBwdArgs(ctypes.Structure):
+    _fields_ = [("P", c_vp * 2), ("save", c_vp * 2), ("gsoa", c_vp * 2), ("obs", c_vp), ("mask", c_vp),
+                ("active", c_vp), ("act", c_vp), ("adv", c_vp), ("old_logp", c_vp), ("old_value", c_vp),
+                ("returns", c_vp), ("stats", c_vp), ("loss_acc", c_vp), ("clip", c_f32), ("huber_delta", c_f32),
+                ("entropy_coef", c_f32), ("value_coef", c_f32), ("en", c_i64), ("T", c_i32), ("L", c_i32),
+                ("rs", c_i64)]
+
+
+_MD = ctypes.POINTER(MappoDims)
+_SIGS += [
+    ("mm_mappo_param_count", c_i64, [_MD, c_i32]),
+    ("mm_mappo_param_offsets", c_i32, [_MD, c_i32, ctypes.POINTER(c_i64)]),
+    ("mm_mappo_save_fields", c_i32, [_MD, c_i32]),
+    ("mm_mappo_grad_fields", c_i32, [_MD, c_i32]),
+    ("mm_mappo_fwd", c_i32, [_MD, ctypes.POINTER(MappoFwdArgs), c_vp]),
+    ("mm_mappo_bwd", c_i32, [_MD, ctypes.POINTER(MappoBwdArgs), c_vp]),
+    ("mm_mappo_wgrad_partial_count", c_i64, [_MD, c_i64]),
+    ("mm_mappo_wgrad", c_i32, [_MD, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ("mm_mappo_gae", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_f32, c_f32, c_vp]),
+    ("mm_mappo_adv_stats", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ("mm_mappo_vn_update", c_i32, [c_vp, c_vp, c_f64, c_vp]),
+    ("mm_mappo_insert", c_i32, [c_vp, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+]
