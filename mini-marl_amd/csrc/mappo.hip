@@ -366,6 +366,11 @@ __device__ __forceinline__ void soa_ld(const float* col, int f0, float (&v)[N]) 
     for (int i = c; i < (N < c + 16 ? N : c + 16); ++i) v[i] = q[(i - c) * 64];
   }
 }
+__device__ __forceinline__ void soa_st1(float* col, int f, float v) {
+  float* q = col + f * 64;
+  asm volatile("" : "+v"(q));
+  *q = v;
+}
 __device__ __forceinline__ float soa_ld1(const float* col, int f) {
   const float* q = col + f * 64;
   asm volatile("" : "+v"(q));
@@ -462,42 +467,50 @@ __device__ __forceinline__ void bwd_body(const mm_mappo_bwd_args& a, int net, co
       }
       soa_st<H>(go, GF_::PY, t);
     }
-    // ---- GRU (h2 = n + z (h - n), gates r, z, n)
-    float dgi[3 * H], dgh[3 * H], hin[H];
-    {
-      float r[H], z[H], n[H], ghn[H];
-      soa_ld<H>(sv, S::R, r);
-      soa_ld<H>(sv, S::Z, z);
-      soa_ld<H>(sv, S::N, n);
-      soa_ld<H>(sv, S::GHN, ghn);
-      soa_ld<H>(sv, S::HIN, hin);
+    // ---- GRU (h2 = n + z (h - n), gates r, z, n), streamed over hidden units j so that only the
+    // accumulators Wih^T dgi (-> dx2) and Whh^T dgh (-> dh_prev) stay live
+    float dx[H], dhh[H];
 #pragma unroll
-      for (int j = 0; j < H; ++j) {
-        const float dh = xr[j];
-        const float dn = dh * (1.0f - z[j]);
-        const float dz = dh * (hin[j] - n[j]);
-        dh_next[j] = dh * z[j];  // direct path; Whh^T dgh added below
-        const float dpn = dn * (1.0f - n[j] * n[j]);
-        const float dr = dpn * ghn[j];
-        dgi[j] = dr * r[j] * (1.0f - r[j]);
-        dgi[H + j] = dz * z[j] * (1.0f - z[j]);
-        dgi[2 * H + j] = dpn;
-        dgh[j] = dgi[j];
-        dgh[H + j] = dgi[H + j];
-        dgh[2 * H + j] = dpn * r[j];
+    for (int i = 0; i < H; ++i) {
+      dx[i] = 0.0f;
+      dhh[i] = 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const float r = soa_ld1(sv, S::R + j), z = soa_ld1(sv, S::Z + j), n = soa_ld1(sv, S::N + j);
+      const float ghn = soa_ld1(sv, S::GHN + j), hin = soa_ld1(sv, S::HIN + j);
+      const float dh = xr[j];
+      const float dn = dh * (1.0f - z);
+      const float dz = dh * (hin - n);
+      const float dpn = dn * (1.0f - n * n);
+      const float dgr = dpn * ghn * r * (1.0f - r);
+      const float dgz = dz * z * (1.0f - z);
+      const float dghn = dpn * r;
+      dh_next[j] = dh * z;  // direct path; Whh^T dgh added below
+      soa_st1(go, GF_::DGI + j, dgr);
+      soa_st1(go, GF_::DGI + H + j, dgz);
+      soa_st1(go, GF_::DGI + 2 * H + j, dpn);
+      soa_st1(go, GF_::DGH + j, dgr);
+      soa_st1(go, GF_::DGH + H + j, dgz);
+      soa_st1(go, GF_::DGH + 2 * H + j, dghn);
+      soa_st1(go, GF_::HIN + j, hin);
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        dx[i] = fmaf(W[G::Wih + j * H + i], dgr, dx[i]);
+        dx[i] = fmaf(W[G::Wih + (H + j) * H + i], dgz, dx[i]);
+        dx[i] = fmaf(W[G::Wih + (2 * H + j) * H + i], dpn, dx[i]);
+        dhh[i] = fmaf(W[G::Whh + j * H + i], dgr, dhh[i]);
+        dhh[i] = fmaf(W[G::Whh + (H + j) * H + i], dgz, dhh[i]);
+        dhh[i] = fmaf(W[G::Whh + (2 * H + j) * H + i], dghn, dhh[i]);
       }
     }
-    soa_st<3 * H>(go, GF_::DGI, dgi);
-    soa_st<3 * H>(go, GF_::DGH, dgh);
-    soa_st<H>(go, GF_::HIN, hin);
     {
-      matvec_t<3 * H, H, H>(W + G::Whh, dgh, t);
       const float mk = a.mask[row];
 #pragma unroll
-      for (int i = 0; i < H; ++i) dh_next[i] = (dh_next[i] + t[i]) * mk;
+      for (int i = 0; i < H; ++i) dh_next[i] = (dh_next[i] + dhh[i]) * mk;
     }
-    // ---- x2 = LN2(a2) (input of the GRU)
-    float ah[H], xh[H], dx[H], da[H];
+    // ---- x2 = LN2(a2) (input of the GRU); dx = d x2 from the GRU
+    float ah[H], xh[H], da[H];
     {
       soa_ld<H>(sv, S::A2, ah);
       const float mu = soa_ld1(sv, S::MU2), rs = soa_ld1(sv, S::RS2);
@@ -507,7 +520,6 @@ __device__ __forceinline__ void bwd_body(const mm_mappo_bwd_args& a, int net, co
         t[i] = xh[i] * W[G::ln2_w + i] + W[G::ln2_b + i];
       }
       soa_st<H>(go, GF_::X2, t);
-      matvec_t<3 * H, H, H>(W + G::Wih, dgi, dx);
       ln_bwd<H>(dx, xh, rs, W + G::ln2_w, da);
 #pragma unroll
       for (int i = 0; i < H; ++i) {
@@ -577,7 +589,7 @@ __device__ __forceinline__ void bwd_body(const mm_mappo_bwd_args& a, int net, co
 }
 
 template <int D, int H, int A>
-__global__ __launch_bounds__(256) void mappo_bwd_kernel(mm_mappo_bwd_args a) {
+__global__ __launch_bounds__(256, 2) void mappo_bwd_kernel(mm_mappo_bwd_args a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int net = blockIdx.y;
   const int n = net == 0 ? MGeo<D, H, A>::total : MGeo<D, H, 1>::total;
@@ -600,7 +612,7 @@ struct WgJobDev {
   float* dW;
   float* db;
   int M, K, ldw, blk0, nblk;
-  int64_t part;  // offset of this job's partials: (nblk * 4 waves) x (M*K + M)
+  int64_t part;  // offset of this job's partials: nblk x (M*K + M)
 };
 struct WgArgsDev {
   WgJobDev job[MM_MAPPO_MAX_JOBS];
@@ -670,29 +682,54 @@ __global__ __launch_bounds__(256) void mappo_wgrad_kernel(WgArgsDev a) {
   }
 #pragma unroll
   for (int mt = 0; mt < 3; ++mt) cs[mt] += __shfl_xor(cs[mt], 32);
-  float* out = a.partial + jb.part + (int64_t)(b * 4 + wave) * (jb.M * jb.K + jb.M);
+  // combine the 4 waves in LDS (waves add in turn), then one partial per block
+  __shared__ float red[3 * 2 * 1024 + 3 * 32];
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
 #pragma unroll
-  for (int mt = 0; mt < 3; ++mt) {
+      for (int mt = 0; mt < 3; ++mt) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int m = mt * 32 + kperm(s, hh), kk = kt * 32 + i;
-        if (m < jb.M && kk < jb.K) out[m * jb.K + kk] = acc[mt][kt][s];
+          for (int s = 0; s < 16; ++s) {
+            const int idx = (mt * 2 + kt) * 1024 + kperm(s, hh) * 32 + i;
+            red[idx] = (w == 0 ? 0.0f : red[idx]) + acc[mt][kt][s];
+          }
+        if (hh == 0) red[6 * 1024 + mt * 32 + i] = (w == 0 ? 0.0f : red[6 * 1024 + mt * 32 + i]) + cs[mt];
       }
-    const int m = mt * 32 + i;
-    if (hh == 0 && m < jb.M) out[jb.M * jb.K + m] = cs[mt];
+    }
+    __syncthreads();
+  }
+  float* out = a.partial + jb.part + (int64_t)b * (jb.M * jb.K + jb.M);
+  const int nW = jb.M * jb.K;
+  for (int e = threadIdx.x; e < nW + jb.M; e += 256) {
+    int idx;
+    if (e < nW) {
+      const int m = e / jb.K, kk = e % jb.K;
+      idx = ((m >> 5) * 2 + (kk >> 5)) * 1024 + (m & 31) * 32 + (kk & 31);
+    } else {
+      idx = 6 * 1024 + (e - nW);
+    }
+    out[e] = red[idx];
   }
 }
 
+// Sum the per-block partials: block = 64 outputs x 4 waves, each wave a quarter of the partials.
 __global__ __launch_bounds__(256) void mappo_wgrad_sum_kernel(WgArgsDev a) {
+  __shared__ float sh[4][64];
   const WgJobDev& jb = a.job[blockIdx.y];
   const int per = jb.M * jb.K + jb.M;
-  const int nw = jb.nblk * 4;
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < per; e += gridDim.x * 256) {
-    float s = 0.0f;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 64 + lane;
+  float s = 0.0f;
+  if (e < per) {
     const float* p = a.partial + jb.part + e;
-    for (int w = 0; w < nw; ++w) s += p[(int64_t)w * per];
+    for (int b = wave; b < jb.nblk; b += 4) s += p[(int64_t)b * per];
+  }
+  sh[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && e < per) {
+    s = sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane];
     if (e < jb.M * jb.K) {
       if (jb.dW) jb.dW[(e / jb.K) * jb.ldw + e % jb.K] = s;
     } else if (jb.db) {
@@ -915,7 +952,7 @@ struct MappoShape {
     int64_t tot = 0;
     for (int net = 0; net < 2; ++net) {
       const int nj = net == 0 ? jobs<A>(nullptr, Rs, nullptr, jv) : jobs<1>(nullptr, Rs, nullptr, jv);
-      for (int q = 0; q < nj; ++q) tot += nblk * 4 * (int64_t)(jv[q].M * jv[q].K + jv[q].M);
+      for (int q = 0; q < nj; ++q) tot += nblk * (int64_t)(jv[q].M * jv[q].K + jv[q].M);
     }
     return tot;
   }
@@ -934,13 +971,13 @@ struct MappoShape {
       w.job[q].nblk = nblk;
       w.job[q].part = part;
       const int per = w.job[q].M * w.job[q].K + w.job[q].M;
-      part += (int64_t)nblk * 4 * per;
+      part += (int64_t)nblk * per;
       blk += nblk;
       maxper = per > maxper ? per : maxper;
     }
     hipLaunchKernelGGL(mappo_wgrad_kernel, dim3(blk), dim3(256), 0, s, w);
     MM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(mappo_wgrad_sum_kernel, dim3((maxper + 255) / 256, w.njobs), dim3(256), 0, s, w);
+    hipLaunchKernelGGL(mappo_wgrad_sum_kernel, dim3((maxper + 63) / 64, w.njobs), dim3(256), 0, s, w);
     MM_HIP_CHECK(hipGetLastError());
     return MM_OK;
   }
