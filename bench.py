@@ -7,6 +7,9 @@ target Q forward on the next obs, TD error + transition store, and every 10th st
 the chunk insert into the prioritized replay. Synthetic data = the build's own
 gridworld (the reference's ma_gym env is absent); random-init weights.
 
+The JSON line also carries the QMIX learner (updates/s, configs[1]) and the MAPPO episode
+(configs[2]: rollout + GAE + 15 PPO epochs; agent-env-steps/s including training).
+
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
 torch.distributed.run (one process per GPU, RCCL). Envs shard across ranks with no
 data-path collective (weak scaling); rank 0 prints ONE JSON line.
@@ -102,6 +105,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--learner-steps", type=int, default=100)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--mappo-episodes", type=int, default=2, help="timed MAPPO episodes (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -181,6 +185,57 @@ def main():
         el_l = float(t.item())
     upd_per_s = args.learner_steps / el_l
 
+    # MAPPO (BASELINE configs[2]): 4096 envs x 8 agents per GPU, T=100 rollout steps with the fused
+    # actor/critic kernel, device GAE, then 15 PPO epochs of chunked (L=5) BPTT on the whole buffer
+    mappo = None
+    if args.mappo_episodes > 0:
+        from minimarl.env import VecEnv
+        from minimarl.mappo import MappoPolicy, MappoRunner
+        menv = VecEnv(E, N, max_steps=100, device=dev)
+        mpol = MappoPolicy(menv.obs_dim, 5, 32, dev, seed=3)
+        if dist:
+            dist.broadcast(mpol.actor.flat, 0)
+            dist.broadcast(mpol.critic.flat, 0)
+        mr = MappoRunner(menv, mpol, T=100, L=5, ppo_epoch=15, seed=11 + rank, grad_allreduce=allreduce)
+        mr.warmup()
+        mr.run_episode()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        t_ro = t_tr = 0.0
+        t2 = time.perf_counter()
+        for _ in range(args.mappo_episodes):
+            ev[0].record()
+            mr.rollout()
+            mr.compute()
+            ev[1].record()
+            info = mr.train()
+            ev[2].record()
+            torch.cuda.synchronize()
+            t_ro += ev[0].elapsed_time(ev[1])
+            t_tr += ev[1].elapsed_time(ev[2])
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el_m = time.perf_counter() - t2
+        if dist:
+            t = torch.tensor([el_m], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_m = float(t.item())
+        k = args.mappo_episodes
+        mappo = {"algo": "rmappo shared policy (MLP-LN + GRU-32 actor/critic, ValueNorm, GAE, 15 PPO epochs)",
+                 "envs_per_gpu": E, "agents": N, "episode_length": 100, "data_chunk_length": 5, "ppo_epoch": 15,
+                 "ms_per_episode": round(el_m / k * 1e3, 3),
+                 "agent_env_steps_per_s_incl_train": round(E * N * 100 * world * k / el_m, 1),
+                 "rollout_ms_per_step": round(t_ro / k / 100, 4), "train_ms": round(t_tr / k, 3),
+                 "ppo_updates_per_s": round(15 * k / el_m, 2),
+                 "train_info": {kk: round(float(v), 6) for kk, v in info.items()},
+                 "grad_allreduce": "rccl" if dist else None}
+        del mr, menv, mpol
+        torch.cuda.empty_cache()
+
     # roofline of the dominant kernel: the fused agent Q forward (behavior launch of a step)
     # (one launch = target net on s'_t + behavior net on s_{t+1}: 2 nets x E x N agent-steps)
     t_fwd = time_kernel(eng.fused_forward)
@@ -218,6 +273,7 @@ def main():
                         "mixer_hidden": 64, "ms_per_update": round(el_l / args.learner_steps * 1e3, 4),
                         "updates": args.learner_steps, "grad_allreduce": "rccl" if dist else None,
                         "reference_cpu_updates_per_s": 12.0},
+            "mappo": mappo,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

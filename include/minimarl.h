@@ -217,10 +217,13 @@ int mm_mappo_wgrad(const mm_mappo_dims* d, int32_t net, const float* gsoa, int64
 /* GAE with ValueNorm denormalisation (vn = float[3]: running mean, mean sq, debias): returns[t<T]. */
 int mm_mappo_gae(const float* rew, const float* value_preds, const float* masks, float* returns, const float* vn,
                  int32_t T, int64_t en, float gamma, float gae_lambda, mm_stream_t s);
-/* adv = returns - denorm(value_preds) over rows = T*EN; masked mean/std, active count, return
- * moments into stats. partial: device double[5 * 256]. */
+/* adv = returns - denorm(value_preds) over rows = T*EN; masked mean/std (two-pass, as np.nanstd),
+ * active count, return moments into stats. partial: device double[7 * 256 + 5]; its last 5
+ * entries (partial + 1792) receive the raw sums (adv, count, ret, ret^2, adv^2) for a
+ * data-parallel all-reduce followed by mm_mappo_stats_from_sums (rows = global row count). */
 int mm_mappo_adv_stats(const float* returns, const float* value_preds, const float* active, const float* vn,
                        float* adv, int64_t rows, double* partial, float* stats, mm_stream_t s);
+int mm_mappo_stats_from_sums(const double* sums, int64_t rows, float* stats, mm_stream_t s);
 /* One ValueNorm.update with the batch moments in stats, then stats[VN_MEAN/VN_STD]. */
 int mm_mappo_vn_update(float* vn, float* stats, double beta, mm_stream_t s);
 /* After env.step: masks/active of slot t+1, zero hiddens of done envs (done [E] u8); increments

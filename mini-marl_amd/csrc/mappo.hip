@@ -770,23 +770,24 @@ __global__ __launch_bounds__(256) void mappo_gae_kernel(const float* __restrict_
   }
 }
 
-// adv = returns - denorm(value_preds) over t < T; block partials of (sum, count) over active rows,
-// plus (sum ret, sum ret^2) over all rows for the ValueNorm batch statistics.
+// adv = returns - denorm(value_preds) over t < T; block partials [5] of (sum, count, sum of squares)
+// over active rows plus (sum ret, sum ret^2) over all rows (the ValueNorm batch moments).
 __global__ __launch_bounds__(256) void mappo_adv_kernel(const float* __restrict__ ret, const float* __restrict__ vp,
                                                         const float* __restrict__ active, const float* __restrict__ vn,
                                                         float* __restrict__ adv, int64_t R, double* __restrict__ part) {
 #pragma clang fp contract(off)
-  __shared__ double sh[4][256];
+  __shared__ double sh[5][256];
   float mean, var;
   vn_mean_var(vn, mean, var);
   const float sd = sqrtf(var);
-  double s = 0, n = 0, sr = 0, sr2 = 0;
+  double s = 0, n = 0, sr = 0, sr2 = 0, s2 = 0;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < R; i += (int64_t)gridDim.x * 256) {
     const float v = ret[i] - (vp[i] * sd + mean);
     adv[i] = v;
     if (active[i] != 0.0f) {
       s += v;
       n += 1.0;
+      s2 += (double)v * v;
     }
     sr += ret[i];
     sr2 += (double)ret[i] * ret[i];
@@ -795,15 +796,17 @@ __global__ __launch_bounds__(256) void mappo_adv_kernel(const float* __restrict_
   sh[1][threadIdx.x] = n;
   sh[2][threadIdx.x] = sr;
   sh[3][threadIdx.x] = sr2;
+  sh[4][threadIdx.x] = s2;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if (threadIdx.x < w)
-      for (int q = 0; q < 4; ++q) sh[q][threadIdx.x] += sh[q][threadIdx.x + w];
+      for (int q = 0; q < 5; ++q) sh[q][threadIdx.x] += sh[q][threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x < 4) part[blockIdx.x * 4 + threadIdx.x] = sh[threadIdx.x][0];
+  if (threadIdx.x < 5) part[blockIdx.x * 5 + threadIdx.x] = sh[threadIdx.x][0];
 }
 
+// second pass (np.nanstd is two-pass): sum of squared deviations from the masked mean
 __global__ __launch_bounds__(256) void mappo_adv_var_kernel(const float* __restrict__ adv,
                                                             const float* __restrict__ active, int64_t R,
                                                             const double* __restrict__ part, int nb,
@@ -813,8 +816,8 @@ __global__ __launch_bounds__(256) void mappo_adv_var_kernel(const float* __restr
   if (threadIdx.x == 0) {
     double s = 0, n = 0;
     for (int b = 0; b < nb; ++b) {
-      s += part[b * 4];
-      n += part[b * 4 + 1];
+      s += part[b * 5];
+      n += part[b * 5 + 1];
     }
     s_mean = n > 0 ? s / n : 0.0;
   }
@@ -832,19 +835,39 @@ __global__ __launch_bounds__(256) void mappo_adv_var_kernel(const float* __restr
   if (threadIdx.x == 0) part2[blockIdx.x] = sh[0];
 }
 
-// stats[]: adv mean/std, active count, ValueNorm batch moments (mean of returns, of returns^2)
-__global__ void mappo_stats_kernel(const double* part, const double* part2, int nb, int64_t R, float* stats) {
+// stats[]: adv mean/std, active count, ValueNorm batch moments; sums[5] = the raw sums
+// (sum adv, count, sum ret, sum ret^2, sum adv^2) for a data-parallel all-reduce.
+__global__ void mappo_stats_kernel(const double* part, const double* part2, int nb, int64_t R, float* stats,
+                                   double* sums) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double s = 0, n = 0, sr = 0, sr2 = 0, q = 0;
+  double s = 0, n = 0, sr = 0, sr2 = 0, s2 = 0, q = 0;
   for (int b = 0; b < nb; ++b) {
-    s += part[b * 4];
-    n += part[b * 4 + 1];
-    sr += part[b * 4 + 2];
-    sr2 += part[b * 4 + 3];
+    s += part[b * 5];
+    n += part[b * 5 + 1];
+    sr += part[b * 5 + 2];
+    sr2 += part[b * 5 + 3];
+    s2 += part[b * 5 + 4];
     q += part2[b];
   }
   stats[MM_MST_ADV_MEAN] = (float)(n > 0 ? s / n : 0.0);
   stats[MM_MST_ADV_STD] = (float)(n > 0 ? sqrt(q / n) : 0.0);
+  stats[MM_MST_ACTIVE_SUM] = (float)n;
+  stats[MM_MST_RET_MEAN] = (float)(sr / (double)R);
+  stats[MM_MST_RET_SQ_MEAN] = (float)(sr2 / (double)R);
+  sums[0] = s;
+  sums[1] = n;
+  sums[2] = sr;
+  sums[3] = sr2;
+  sums[4] = s2;
+}
+
+// stats from all-reduced sums (replicas of a data-parallel job see the global statistics)
+__global__ void mappo_stats_from_sums_kernel(const double* sums, int64_t R, float* stats) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double s = sums[0], n = sums[1], sr = sums[2], sr2 = sums[3], s2 = sums[4];
+  const double mu = n > 0 ? s / n : 0.0;
+  stats[MM_MST_ADV_MEAN] = (float)mu;
+  stats[MM_MST_ADV_STD] = (float)(n > 0 ? sqrt(fmax(s2 / n - mu * mu, 0.0)) : 0.0);
   stats[MM_MST_ACTIVE_SUM] = (float)n;
   stats[MM_MST_RET_MEAN] = (float)(sr / (double)R);
   stats[MM_MST_RET_SQ_MEAN] = (float)(sr2 / (double)R);
@@ -1093,10 +1116,17 @@ int mm_mappo_adv_stats(const float* returns, const float* value_preds, const flo
                      adv, rows, partial);
   MM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(mm::mappo_adv_var_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, adv, active, rows, partial, nb,
-                     partial + 4 * nb);
+                     partial + 5 * nb);
   MM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(mm::mappo_stats_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, partial, partial + 4 * nb, nb, rows,
-                     stats);
+  hipLaunchKernelGGL(mm::mappo_stats_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, partial, partial + 5 * nb, nb, rows,
+                     stats, partial + 6 * nb);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mappo_stats_from_sums(const double* sums, int64_t rows, float* stats, mm_stream_t s) {
+  MM_REQUIRE(sums && stats && rows > 0, "mappo_stats_from_sums: bad args");
+  hipLaunchKernelGGL(mm::mappo_stats_from_sums_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, sums, rows, stats);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

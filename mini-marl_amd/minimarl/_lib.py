@@ -202,5 +202,6 @@ _SIGS += [
     ("mm_mappo_gae", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_f32, c_f32, c_vp]),
     ("mm_mappo_adv_stats", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     ("mm_mappo_vn_update", c_i32, [c_vp, c_vp, c_f64, c_vp]),
+    ("mm_mappo_stats_from_sums", c_i32, [c_vp, c_i64, c_vp, c_vp]),
     ("mm_mappo_insert", c_i32, [c_vp, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 ]

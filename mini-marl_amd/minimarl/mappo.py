@@ -240,7 +240,7 @@ class MappoTrainer:
         self.vn = torch.zeros(3, device=dev)          # ValueNorm running mean, mean sq, debias (f32)
         self.stats = torch.zeros(8, device=dev)
         self.adv = torch.zeros(self.rows, device=dev)
-        self.adv_part = torch.zeros(5 * 256, dtype=torch.float64, device=dev)
+        self.adv_part = torch.zeros(7 * 256 + 5, dtype=torch.float64, device=dev)
         self.loss_acc = torch.zeros(4, device=dev)
 
     # -- ValueNorm (utils/valuenorm.py) ------------------------------------------------------
@@ -280,10 +280,18 @@ class MappoTrainer:
         return b
 
     def prepare(self, buf):
-        """Advantages (returns - denorm(V)), their masked mean/std and the return moments."""
+        """Advantages (returns - denorm(V)), their masked mean/std and the return moments. Data
+        parallel: the raw sums are all-reduced so every replica normalises with the global
+        statistics and applies the same ValueNorm updates."""
+        s = stream_handle(self.device)
         check(lib().mm_mappo_adv_stats(ptr(buf.returns), ptr(buf.value_preds), ptr(buf.active_masks), ptr(self.vn),
-                                       ptr(self.adv), self.rows, ptr(self.adv_part), ptr(self.stats),
-                                       stream_handle(self.device)), "mappo_adv_stats")
+                                       ptr(self.adv), self.rows, ptr(self.adv_part), ptr(self.stats), s),
+              "mappo_adv_stats")
+        if self.allreduce is not None:
+            sums = self.adv_part[7 * 256:7 * 256 + 5]
+            world = self.allreduce(sums)
+            check(lib().mm_mappo_stats_from_sums(ptr(sums), self.rows * world, ptr(self.stats), s),
+                  "mappo_stats_from_sums")
         self.loss_acc.zero_()
 
     def epoch(self, buf, ep, fa=None, ba=None):
