@@ -251,7 +251,7 @@ def main():
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                 "traffic_source": os.path.basename(prof[-1]) if traffic else None,
-                "kernel": "agent_q_fwd_kernel<64,64,64,1> (dual: target+behavior)", "kernel_us": round(t_fwd * 1e6, 2),
+                "kernel": "agent_q_fwd_lds_kernel<64,64,64,1> (dual: target+behavior)", "kernel_us": round(t_fwd * 1e6, 2),
                 "flop_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
                 "hbm_frac": round(alg_bytes / t_fwd / (PEAK_HBM_GBS * 1e9), 4)}
 
