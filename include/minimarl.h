@@ -15,10 +15,10 @@
  *   mm_td_chunk_step     cal_td_error + chunk assembly               vdn/_utils.py:44-52; vdn/main.py:140-167
  *   mm_per_*             Prioritized_Experience_Replay + SumTree     vdn/replay_buffer/{buffer,sumtree}.py; qmix/replay_buffer/{per,sumtree}.py
  *   mm_mixer_fwd         Mix_Net.forward                             qmix/_network.py:199-217
- *   mm_lrn_*/mm_*_bwd    Train_dqn.train / Target_Dqn.train          qmix/_train.py:19-121; vdn/_train.py:184-235
+ *   mm_lrn_, mm_..._bwd  Train_dqn.train / Target_Dqn.train          qmix/_train.py:19-121; vdn/_train.py:184-235
  *   mm_mappo_fwd         R_MAPPOPolicy.get_actions/get_values/evaluate_actions  mappo/algorithms/rmappo_policy.py:57-136
- *   mm_mappo_bwd/wgrad   R_MAPPO.ppo_update/cal_value_loss/train     mappo/algorithms/ramppo_network.py:56-287
- *   mm_mappo_gae/insert  SharedReplayBuffer.compute_returns/insert   mappo/runner/shared/shared_buffer.py:82-157
+ *   mm_mappo_bwd, wgrad  R_MAPPO.ppo_update/cal_value_loss/train     mappo/algorithms/ramppo_network.py:56-287
+ *   mm_mappo_gae, insert SharedReplayBuffer.compute_returns/insert   mappo/runner/shared/shared_buffer.py:82-157
  */
 #ifndef MINIMARL_H
 #define MINIMARL_H
