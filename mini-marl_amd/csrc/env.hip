@@ -5,8 +5,9 @@
 // dynamics are the build's own spec, defined in oracle/env.py (parity with
 // ma_gym: UNPINNED; parity with oracle/env.py: bit-exact, integer state).
 //
-// Block = 256 threads, EB = 16 envs (E/16 blocks: 256 for 4096 envs). Phase 0 stages the block's grids (bytes,
-// [E][R*C] so the copy is one contiguous coalesced run) and positions in LDS;
+// Block = 256 threads, EB = 4 envs (E/4 blocks: 1024 for 4096 envs, 4 resident per CU). Phase 0 stages
+// every global input of the step (grids as bytes [E][R*C] so the copy is one contiguous coalesced run,
+// positions, actions, counters, reset tables) in LDS in ONE round trip;
 // phase 1 runs the sequential-in-agent-order dynamics one thread per env;
 // phase 2 generates obs [env, agent, feat]: each thread decodes its feature
 // positions once, then walks the block's envs, so consecutive lanes store
@@ -20,10 +21,11 @@
 
 namespace mm {
 static constexpr int OBS_LOCAL = 47;
-static constexpr int EB = 16;
+static constexpr int EB_DEFAULT = 4;
 
 struct EnvDev {
   int E, N, R, C, D, max_steps, full_obs, init_apples;
+  int eb;  // envs per block of the step kernel
   float step_cost, inv_r, inv_c;
   int32_t* pos;     // [E][N] r*256 + c
   int8_t* grid;     // [E][R*C] 0 empty, 1 lemon, 2 apple
@@ -82,8 +84,8 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvDev d, float* obs, in
     for (int i = threadIdx.x; i < d.N * d.D; i += blockDim.x)
       d.reset_obs[i] = obs_elem(d, spos, sgrid, i / d.D, i % d.D);
   }
-  const int e0 = blockIdx.x * EB;
-  const int ne = min(EB, d.E - e0);
+  const int e0 = blockIdx.x * d.eb;
+  const int ne = min(d.eb, d.E - e0);
   for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) d.grid[(int64_t)e0 * RC + i] = sgrid[i % RC];
   for (int i = threadIdx.x; i < ne * d.N; i += blockDim.x) d.pos[(int64_t)e0 * d.N + i] = spos[i % d.N];
   for (int i = threadIdx.x; i < ne; i += blockDim.x) {
@@ -102,21 +104,30 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvDev d, float* obs, in
 __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* __restrict__ act,
                                                        float* __restrict__ next_obs, int64_t next_se,
                                                        const int64_t* __restrict__ next_row,
-                                                       float* __restrict__ obs_cur, float* __restrict__ rew,
-                                                       uint8_t* __restrict__ done_out) {
+                                                       float* __restrict__ obs_cur, int64_t* __restrict__ cur_row,
+                                                       float* __restrict__ rew, uint8_t* __restrict__ done_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int RC = d.R * d.C;
   const int N = d.N;
+  const int EB = d.eb;
+  const bool autoreset = obs_cur || cur_row;
+  const int ND = N * d.D;
   int64_t* srow = reinterpret_cast<int64_t*>(smem);                       // [EB] destination rows
-  int32_t* spos = reinterpret_cast<int32_t*>(smem + EB * 8);              // [EB][N]
+  float* sreset = reinterpret_cast<float*>(srow + EB);                    // [N*D] reset obs table
+  int32_t* spos = reinterpret_cast<int32_t*>(sreset + ND);                // [EB][N]
   int32_t* sact = spos + EB * N;                                          // [EB][N]
-  uint8_t* sdone = reinterpret_cast<uint8_t*>(sact + EB * N);             // [EB]
+  int32_t* sapl = sact + EB * N;                                          // [EB] apples
+  int32_t* sstp = sapl + EB;                                              // [EB] steps
+  int32_t* sipos = sstp + EB;                                             // [N] initial positions
+  uint8_t* sdone = reinterpret_cast<uint8_t*>(sipos + N);                 // [EB]
   int8_t* sgrid = reinterpret_cast<int8_t*>(sdone + EB);                  // [EB][RC]
   uint8_t* socc = reinterpret_cast<uint8_t*>(sgrid + EB * RC);            // [EB][RC] agent id + 1
+  int8_t* sigrid = reinterpret_cast<int8_t*>(socc + EB * RC);             // [RC] initial grid
   const int e0 = blockIdx.x * EB;
   const int ne = min(EB, d.E - e0);
 
-  // phase 0: stage grids and positions (contiguous runs), clear occupancy
+  // phase 0: every global read of the step in one round trip (grids, positions, actions, counters,
+  // reset tables); the later phases only touch LDS and issue stores
   for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) {
     sgrid[i] = d.grid[(int64_t)e0 * RC + i];
     socc[i] = 0;
@@ -125,39 +136,85 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
     spos[i] = d.pos[(int64_t)e0 * N + i];
     sact[i] = act[(int64_t)e0 * N + i];
   }
-  for (int i = threadIdx.x; i < ne; i += blockDim.x) srow[i] = next_row ? next_row[e0 + i] : (int64_t)(e0 + i);
+  for (int i = threadIdx.x; i < ne; i += blockDim.x) {
+    srow[i] = next_row ? next_row[e0 + i] : (int64_t)(e0 + i);
+    sapl[i] = d.apples[e0 + i];
+    sstp[i] = d.steps[e0 + i];
+  }
+  if (autoreset) {
+    for (int i = threadIdx.x; i < ND; i += blockDim.x) sreset[i] = d.reset_obs[i];
+    for (int i = threadIdx.x; i < RC; i += blockDim.x) sigrid[i] = d.init_grid[i];
+    for (int i = threadIdx.x; i < N; i += blockDim.x) sipos[i] = d.init_pos[i];
+  }
   __syncthreads();
 
-  // phase 1: dynamics, one thread per env, agents in id order (oracle/env.py VecEnvOracle.step)
+  // phase 1: dynamics, one thread per env, agents in id order (oracle/env.py VecEnvOracle.step).
+  // Positions live in registers (N <= 16; fully unrolled collision checks), so the only LDS
+  // round trips on the sequential chain are the grid cell reads.
   if (threadIdx.x < ne) {
     const int le = threadIdx.x, e = e0 + le;
-    int32_t* p = spos + le * N;
     int8_t* g = sgrid + le * RC;
-    int apples = d.apples[e];
-    const int steps = d.steps[e] + 1;
-    for (int k = 0; k < N; ++k) {
-      const int a = sact[le * N + k];
-      const int r = p[k] >> 8, c = p[k] & 255;
-      const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
-      const int nc = c + (a == 1 ? -1 : (a == 3 ? 1 : 0));
-      bool ok = nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
-      const int key = (nr << 8) | nc;
-      for (int j = 0; j < N; ++j) ok = ok && (j == k || p[j] != key);
-      if (ok) p[k] = key;
-      const int cell = (p[k] >> 8) * d.C + (p[k] & 255);
-      const int item = g[cell];
-      float rk = d.step_cost;
-      const bool big = (k & 1) == 0;
-      rk += item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f);
-      apples -= item == 2 ? 1 : 0;
-      g[cell] = 0;
-      rew[(int64_t)e * N + k] = rk;
+    int apples = sapl[le];
+    const int steps = sstp[le] + 1;
+    if (N <= 16) {
+      int p[16], a[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        p[k] = k < N ? spos[le * N + k] : -1;
+        a[k] = k < N ? sact[le * N + k] : 4;
+      }
+      float rk[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k >= N) break;
+        const int r = p[k] >> 8, c = p[k] & 255;
+        const int nr = r + (a[k] == 0 ? 1 : (a[k] == 2 ? -1 : 0));
+        const int nc = c + (a[k] == 1 ? -1 : (a[k] == 3 ? 1 : 0));
+        bool ok = nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
+        const int key = (nr << 8) | nc;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) ok = ok && (j == k || p[j] != key);
+        if (ok) p[k] = key;
+        const int cell = (p[k] >> 8) * d.C + (p[k] & 255);
+        const int item = g[cell];
+        const bool big = (k & 1) == 0;
+        rk[k] = d.step_cost + (item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f));
+        apples -= item == 2 ? 1 : 0;
+        g[cell] = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k >= N) break;
+        spos[le * N + k] = p[k];
+        rew[(int64_t)e * N + k] = rk[k];
+      }
+    } else {
+      int32_t* p = spos + le * N;
+      for (int k = 0; k < N; ++k) {
+        const int a = sact[le * N + k];
+        const int r = p[k] >> 8, c = p[k] & 255;
+        const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
+        const int nc = c + (a == 1 ? -1 : (a == 3 ? 1 : 0));
+        bool ok = nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
+        const int key = (nr << 8) | nc;
+        for (int j = 0; j < N; ++j) ok = ok && (j == k || p[j] != key);
+        if (ok) p[k] = key;
+        const int cell = (p[k] >> 8) * d.C + (p[k] & 255);
+        const int item = g[cell];
+        float rk = d.step_cost;
+        const bool big = (k & 1) == 0;
+        rk += item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f);
+        apples -= item == 2 ? 1 : 0;
+        g[cell] = 0;
+        rew[(int64_t)e * N + k] = rk;
+      }
     }
     const bool dn = steps >= d.max_steps || apples == 0;
     sdone[le] = dn ? 1 : 0;
     done_out[e] = dn ? 1 : 0;
-    d.steps[e] = dn && obs_cur ? 0 : steps;
-    d.apples[e] = dn && obs_cur ? d.init_apples : apples;
+    if (cur_row) cur_row[e] = dn ? -1 : srow[le];
+    d.steps[e] = dn && autoreset ? 0 : steps;
+    d.apples[e] = dn && autoreset ? d.init_apples : apples;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < ne * N; i += blockDim.x) {
@@ -168,14 +225,13 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
 
   // phase 2: obs. Each thread owns fixed positions r of an env's [N][D] block (decoded once) and
   // walks the block's envs: a wave stores 64 consecutive floats of one env per instruction.
-  const int ND = N * d.D;
   for (int r = threadIdx.x; r < ND; r += blockDim.x) {
     const int k = r / d.D, f = r % d.D;
     const int src = d.full_obs ? f / OBS_LOCAL : k;
     const int lf = d.full_obs ? f % OBS_LOCAL : f;
     const int cellid = lf >= 2 ? (lf - 2) / 5 : 0, ch = lf >= 2 ? (lf - 2) % 5 : 0;
     const int dr = cellid / 3 - 1, dc = cellid % 3 - 1;
-    const float rs = obs_cur ? d.reset_obs[r] : 0.0f;
+    const float rs = obs_cur ? sreset[r] : 0.0f;
     for (int le = 0; le < ne; ++le) {
       const int p = spos[le * N + src];
       const int pr = p >> 8, pc = p & 255;
@@ -199,7 +255,7 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
             : ((item == 0 && occ != 0 && ((occ - 1) & 1) == ch - 2) ? 1.0f : 0.0f);
         }
       }
-      next_obs[srow[le] * next_se + r] = v;
+      if (next_obs) next_obs[srow[le] * next_se + r] = v;
       if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? rs : v;
     }
   }
@@ -207,15 +263,19 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
   // phase 3: state write-back (initial state for auto-reset envs)
   for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) {
     const int le = i / RC;
-    d.grid[(int64_t)e0 * RC + i] = (obs_cur && sdone[le]) ? d.init_grid[i % RC] : sgrid[i];
+    d.grid[(int64_t)e0 * RC + i] = (autoreset && sdone[le]) ? sigrid[i % RC] : sgrid[i];
   }
   for (int i = threadIdx.x; i < ne * N; i += blockDim.x) {
     const int le = i / N;
-    d.pos[(int64_t)e0 * N + i] = (obs_cur && sdone[le]) ? d.init_pos[i % N] : spos[i];
+    d.pos[(int64_t)e0 * N + i] = (autoreset && sdone[le]) ? sipos[i % N] : spos[i];
   }
 }
 
-static size_t step_smem(const EnvDev& d) { return (size_t)EB * 8 + 2 * (size_t)EB * d.N * 4 + EB + 2 * (size_t)EB * d.R * d.C; }
+static size_t step_smem(const EnvDev& d) {
+  const size_t EB = d.eb;
+  return EB * 8 + (size_t)d.N * d.D * 4 + 2 * EB * d.N * 4 + 2 * EB * 4 + d.N * 4 + EB + 2 * EB * d.R * d.C +
+         d.R * d.C;
+}
 
 int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out) {
   (void)seed;  // the layout is deterministic (ma_gym Checkers resets to a fixed layout)
@@ -227,6 +287,8 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   EnvDev d;
   d.E = (int)n_envs;
   d.N = cfg->n_agents;
+  d.eb = getenv("MM_ENV_EB") ? atoi(getenv("MM_ENV_EB")) : EB_DEFAULT;
+  MM_REQUIRE(d.eb >= 1 && d.eb <= 64, "env_create: bad envs-per-block");
   d.R = 3 * ((d.N + 1) / 2);
   d.C = cols;
   MM_REQUIRE(d.R <= 255, "env_create: too many agents for the grid");
@@ -273,7 +335,7 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   mm_env* env = new mm_env;
   env->d = d;
   env->alloc = base;
-  const int blocks = (d.E + EB - 1) / EB;
+  const int blocks = (d.E + d.eb - 1) / d.eb;
   const size_t sm = ((d.N * 4 + 15) & ~15) + RC;
   hipLaunchKernelGGL(env_reset_kernel, dim3(blocks), dim3(256), sm, 0, d, (float*)nullptr, 1);
   hipError_t e = hipDeviceSynchronize();
@@ -290,7 +352,7 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
 int env_reset(mm_env* env, float* obs, hipStream_t s) {
   MM_REQUIRE(env, "env_reset: null env");
   const EnvDev& d = env->d;
-  const int blocks = (d.E + EB - 1) / EB;
+  const int blocks = (d.E + d.eb - 1) / d.eb;
   const size_t sm = ((d.N * 4 + 15) & ~15) + d.R * d.C;
   hipLaunchKernelGGL(env_reset_kernel, dim3(blocks), dim3(256), sm, s, d, obs, 0);
   MM_HIP_CHECK(hipGetLastError());
@@ -298,12 +360,13 @@ int env_reset(mm_env* env, float* obs, hipStream_t s) {
 }
 
 int env_step(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
-             float* obs_cur, float* rew, uint8_t* done, hipStream_t s) {
-  MM_REQUIRE(env && act && next_obs && rew && done, "env_step: null argument");
+             float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, hipStream_t s) {
+  MM_REQUIRE(env && act && rew && done, "env_step: null argument");
+  MM_REQUIRE(next_obs || obs_cur, "env_step: no obs output");
   const EnvDev& d = env->d;
-  const int blocks = (d.E + EB - 1) / EB;
+  const int blocks = (d.E + d.eb - 1) / d.eb;
   hipLaunchKernelGGL(env_step_kernel, dim3(blocks), dim3(256), step_smem(d), s, d, act, next_obs,
-                     next_se > 0 ? next_se : (int64_t)d.N * d.D, next_row, obs_cur, rew, done);
+                     next_se > 0 ? next_se : (int64_t)d.N * d.D, next_row, obs_cur, cur_row, rew, done);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -331,11 +394,11 @@ int mm_env_grid_shape(const mm_env* env, int32_t* rows, int32_t* cols) {
 int mm_env_reset(mm_env* env, float* obs, mm_stream_t s) { return mm::env_reset(env, obs, (hipStream_t)s); }
 int mm_env_step(mm_env* env, const int32_t* act, float* next_obs, float* obs_cur, float* rew, uint8_t* done,
                 mm_stream_t s) {
-  return mm::env_step(env, act, next_obs, 0, nullptr, obs_cur, rew, done, (hipStream_t)s);
+  return mm::env_step(env, act, next_obs, 0, nullptr, obs_cur, nullptr, rew, done, (hipStream_t)s);
 }
 int mm_env_step_rows(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
-                     float* obs_cur, float* rew, uint8_t* done, mm_stream_t s) {
-  return mm::env_step(env, act, next_obs, next_se, next_row, obs_cur, rew, done, (hipStream_t)s);
+                     float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s) {
+  return mm::env_step(env, act, next_obs, next_se, next_row, obs_cur, cur_row, rew, done, (hipStream_t)s);
 }
 const float* mm_env_reset_obs(const mm_env* env) { return env ? env->d.reset_obs : nullptr; }
 int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples) {

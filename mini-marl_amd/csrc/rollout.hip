@@ -68,9 +68,38 @@ __global__ __launch_bounds__(256) void chunk_begin_kernel(int E, int ND, const f
   }
 }
 
+// Chunk start from the store itself: slot 0 of row dst_rows[e] = slot src_off of row src_rows[e]
+// (the previous step's next obs), or the env's reset obs where src_rows[e] < 0 (env just reset).
+__global__ __launch_bounds__(256) void chunk_begin_rows_kernel(int E, int ND, float* __restrict__ s_obs,
+                                                               int64_t row_stride,
+                                                               const int64_t* __restrict__ src_rows, int64_t src_off,
+                                                               const float* __restrict__ reset_obs,
+                                                               const int64_t* __restrict__ dst_rows) {
+  const int64_t total = (int64_t)E * ND;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i / ND, r = i % ND;
+    const int64_t src = src_rows[e];
+    const float v = src >= 0 ? s_obs[src * row_stride + src_off + r] : reset_obs[r];
+    s_obs[dst_rows[e] * row_stride + r] = v;
+  }
+}
+
 }  // namespace mm
 
 extern "C" {
+int mm_chunk_begin_rows(int64_t n_envs, int32_t nd, float* store_obs, int64_t row_stride, const int64_t* src_rows,
+                        int64_t src_off, const float* reset_obs, const int64_t* dst_rows, mm_stream_t s) {
+  MM_REQUIRE(store_obs && src_rows && reset_obs && dst_rows, "chunk_begin_rows: null argument");
+  if (n_envs <= 0) return MM_OK;
+  const int threads = 256;
+  const int64_t total = n_envs * nd;
+  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 8192);
+  hipLaunchKernelGGL(mm::chunk_begin_rows_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)s, (int)n_envs, nd,
+                     store_obs, row_stride, src_rows, src_off, reset_obs, dst_rows);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                           const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
                           int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,

@@ -64,7 +64,7 @@ _SIGS = [
     ("mm_env_obs_dim", c_i32, [c_vp]),
     ("mm_env_reset", c_i32, [c_vp, c_vp, c_vp]),
     ("mm_env_step", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    ("mm_env_step_rows", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_step_rows", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_reset_obs", c_vp, [c_vp]),
     ("mm_env_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_grid_shape", c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
@@ -73,6 +73,7 @@ _SIGS = [
     ("mm_td_chunk_step_rows", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_chunk_begin", c_i32, [c_i64, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    ("mm_chunk_begin_rows", c_i32, [c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
     ("mm_per_create", c_i32, [c_i64, c_i32, c_f64, c_f64, c_f64, c_f64, c_i32, c_f64, c_f64,
                               ctypes.POINTER(c_vp)]),
     ("mm_per_destroy", None, [c_vp]),

@@ -68,7 +68,10 @@ class RolloutEngine:
         self.staging = torch.arange(self.capacity, self.capacity + self.E, dtype=torch.int64, device=self.device)
         E, N, D, H = self.E, self.N, self.D, self.H
         dev = self.device
-        self.obs_cur = torch.empty(E, N, D, device=dev)
+        # current obs s_{t+1} is never materialised: it is slot c+1 of row cur_row[e] of the chunk
+        # store (the env's terminal next obs), or the env's reset obs where cur_row[e] = -1
+        self.cur_row = torch.full((E,), -1, dtype=torch.int64, device=dev)
+        self.init_obs = torch.empty(E, N, D, device=dev)
         # hidden states feature-major [N, H, E] (env fastest): the forward's lane = env, so every
         # hidden load / store of a wave is one coalesced 128-byte run per feature row
         self.h = torch.zeros(N, H, E, device=dev)
@@ -89,7 +92,15 @@ class RolloutEngine:
         self.seed = int(seed)
         self.chunks_inserted = 0
         self._build_io()
-        self.env.reset(self.obs_cur)
+        self.env.reset(self.init_obs)
+
+    def current_obs(self):
+        """s_{t+1} [E,N,D] as the next behavior forward reads it (materialised for tests only)."""
+        c = (self.t - 1) % self.C + 1 if self.t > 0 else 0
+        out = self.init_obs.clone()
+        valid = self.cur_row >= 0
+        out[valid] = self.store.obs[self.cur_row[valid], c]
+        return out
 
     @property
     def act(self):
@@ -99,7 +110,9 @@ class RolloutEngine:
         """behavior fwd writing slot k (acts for step t with t % 2 == k); reset = done_{t-1}."""
         E, N, D, H = self.E, self.N, self.D, self.H
         b = QFwdIO()
-        b.obs, b.obs_se, b.obs_sa = self.obs_cur.data_ptr(), N * D, D
+        b.obs, b.obs_se, b.obs_sa = self.store.obs.data_ptr(), self.store.row_stride, D
+        b.obs_row = self.cur_row.data_ptr()
+        b.reset_obs = self.env.reset_obs_ptr()
         b.h_in = b.h_out = self.h.data_ptr()
         b.hin_se = b.hout_se = 1
         b.hin_sa = b.hout_sa = H * self.E
@@ -163,14 +176,14 @@ class RolloutEngine:
         if not self._primed:
             self._prologue(s)
         if c == 0:
-            check(L.mm_chunk_begin(self.E, ND, ptr(self.obs_cur), ptr(self.store.obs), self.store.row_stride,
-                                   ptr(self.staging), s), "chunk_begin")
+            check(L.mm_chunk_begin_rows(self.E, ND, ptr(self.store.obs), self.store.row_stride, ptr(self.cur_row),
+                                        self.C * ND, self.env.reset_obs_ptr(), ptr(self.staging), s), "chunk_begin")
         nxt = ctypes.c_void_p(self.store.obs.data_ptr() + 4 * (c + 1) * ND)
         check(L.mm_env_step_rows(self.env.handle(), ptr(self.act_buf[k]), nxt, self.store.row_stride,
-                                 ptr(self.staging), ptr(self.obs_cur), ptr(self.rew), ptr(self.done_buf[k]), s),
+                                 ptr(self.staging), None, ptr(self.cur_row), ptr(self.rew), ptr(self.done_buf[k]), s),
               "env_step")
         iot, iob = self.io_t[k], self.io_b[1 - k]
-        iot.obs_off = (c + 1) * ND
+        iot.obs_off = iob.obs_off = (c + 1) * ND
         self.behavior.pack(s)
         self.target.pack(s)
         check(L.mm_agent_q_fwd2(ctypes.byref(self.target.dims), ptr(self.target.packed), ctypes.byref(iot), self.E,

@@ -345,7 +345,6 @@ class MappoRunner:
         self.trainer = MappoTrainer(policy, T, self.E * self.N, L, ppo_epoch, grad_allreduce=grad_allreduce)
         self.seed = int(seed)
         self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.term = torch.empty(self.E, self.N, self.D, device=dev)
         self.done = torch.zeros(self.E, dtype=torch.uint8, device=dev)
         self.args = []
         b = self.buf
@@ -362,7 +361,8 @@ class MappoRunner:
     def collect_step(self, t):
         L_, s, b = lib(), stream_handle(self.device), self.buf
         check(L_.mm_mappo_fwd(ctypes.byref(self.p.dims), ctypes.byref(self.args[t]), s), "mappo_fwd")
-        check(L_.mm_env_step(self.env.handle(), ptr(b.actions[t]), ptr(self.term), ptr(b.obs[t + 1]),
+        # no terminal obs needed (MAPPO bootstraps through masks): only the auto-reset current obs
+        check(L_.mm_env_step(self.env.handle(), ptr(b.actions[t]), None, ptr(b.obs[t + 1]),
                              ptr(b.rewards[t]), ptr(self.done), s), "env_step")
         check(L_.mm_mappo_insert(ptr(self.done), self.N, self.p.H, self.E, ptr(b.masks[t + 1]),
                                  ptr(b.active_masks[t + 1]), ptr(b.rnn_states[t + 1]), ptr(b.rnn_states_critic[t + 1]),

@@ -215,7 +215,7 @@ def test_rollout_engine_end_to_end_vs_oracle():
         h, ht = h * keep, ht * keep
         ora.reset_envs(done)
         obs = torch.tensor(ora.observe())
-        np.testing.assert_array_equal(eng.obs_cur.cpu().numpy(), obs.numpy())
+        np.testing.assert_array_equal(eng.current_obs().cpu().numpy(), obs.numpy())
     assert len(eng.per) == 2 * E
     tree = eng.per.tree().cpu().numpy()
     assert tree[0] > 0
@@ -234,6 +234,6 @@ def test_graph_replay_matches_eager():
     torch.cuda.synchronize()
     assert a.t == b.t == 30 and len(a.per) == len(b.per) == 192
     for x, y in [(a.store.obs, b.store.obs), (a.store.act, b.store.act), (a.store.rew, b.store.rew),
-                 (a.store.done, b.store.done), (a.h, b.h), (a.ht, b.ht), (a.obs_cur, b.obs_cur),
+                 (a.store.done, b.store.done), (a.h, b.h), (a.ht, b.ht), (a.cur_row, b.cur_row),
                  (a.staging, b.staging), (a.per.tree(), b.per.tree()), (a.per.slot_rows(), b.per.slot_rows())]:
         assert torch.equal(x, y)
