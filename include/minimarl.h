@@ -143,6 +143,89 @@ int64_t mm_per_size(const mm_per* per);
 double mm_per_alpha(const mm_per* per);
 double mm_per_beta(const mm_per* per);
 
+/* ------------------------------------------------------------------ rollout engine plumbing
+ * (the device chunk store of mini-marl_amd/minimarl/engine.py; replaces the per-step Python chunk
+ *  lists of vdn/main.py:140-167 / qmix/main.py:186-237) */
+/* Step with destination rows: the terminal next obs of env e goes to next_obs + next_row[e]*next_se
+ * (NULL next_obs: not written); obs_cur (may be NULL) gets the auto-reset current obs; cur_row (may be
+ * NULL) gets next_row[e], or -1 where the env finished and was reset. Auto-reset happens when either
+ * obs_cur or cur_row is given. */
+int mm_env_step_rows(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
+                     float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s);
+const float* mm_env_reset_obs(const mm_env* env); /* device [N, D]: the (deterministic) reset obs */
+/* TD step writing into store rows rows[e]; increments the device RNG step counter (may be NULL). */
+int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                          const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
+                          int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
+                          uint8_t* store_done, const int64_t* rows, uint64_t* counter, mm_stream_t s);
+/* Slot 0 of each staging row: obs_cur[e] (mm_chunk_begin) or, without materialising the current obs,
+ * slot src_off of row src_rows[e] / the reset obs where src_rows[e] < 0 (mm_chunk_begin_rows). */
+int mm_chunk_begin(int64_t n_envs, int32_t nd, const float* obs_cur, float* store_obs, int64_t row_stride,
+                   const int64_t* rows, mm_stream_t s);
+int mm_chunk_begin_rows(int64_t n_envs, int32_t nd, float* store_obs, int64_t row_stride, const int64_t* src_rows,
+                        int64_t src_off, const float* reset_obs, const int64_t* dst_rows, mm_stream_t s);
+/* PER insert with store-row indirection: slot_row[slot] <-> rows_inout[j] (the evicted row is handed
+ * back as the next staging row; chunk data is never copied). */
+int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s);
+int64_t* mm_per_slot_rows(mm_per* per);             /* device int64 [cap] */
+int64_t mm_per_capacity(const mm_per* per);
+void mm_per_set_size(mm_per* per, int64_t n);      /* host + device fill count (synchronous) */
+void mm_per_set_size_host(mm_per* per, int64_t n); /* host mirror only (graph-replayed inserts) */
+int mm_per_copy_tree(mm_per* per, double* dst, mm_stream_t s);
+int mm_per_copy_slot_rows(mm_per* per, int64_t* dst, mm_stream_t s);
+
+/* ------------------------------------------------------------------ QMIX / VDN learner
+ * (Train_dqn.train qmix/_train.py:19-121, Target_Dqn.train vdn/_train.py:184-235; orchestrated by
+ *  mini-marl_amd/minimarl/learner.py). Mixer = Mix_Net (qmix/_network.py:172-217). */
+int mm_mixer_param_count(int32_t state_dim, int32_t hm, int32_t k1, int32_t n_agents, int64_t* count);
+int mm_mixer_save_dim(int32_t hm, int32_t k1, int32_t n_agents);
+int mm_mixer_delta_dim(int32_t hm, int32_t k1, int32_t n_agents);
+/* Gather B sampled chunks (PER slots -> store rows): obs offsets, acts, rewards, dones. */
+int mm_lrn_gather(int32_t B, int32_t C, int32_t N, int64_t row_stride, int64_t nd, const int64_t* slots,
+                  const int64_t* slot_row, const uint8_t* s_done, const uint8_t* s_act, const float* s_rew,
+                  int64_t* s_off, int64_t* s2_off, int32_t* acts, float* rew, float* done, uint8_t* done8,
+                  mm_stream_t s);
+typedef struct mm_mix_net {
+  const float* P; const float* q; const int64_t* s_off; const float* h_in; const uint8_t* reset;
+  float* h_out; float* qtot; float* save;
+} mm_mix_net;
+/* One mixer time step for 1-2 nets (behavior / target) in one launch. */
+int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
+                 const mm_mix_net* nets, int32_t n_nets, mm_stream_t s);
+/* TD loss terms and their gradient seeds (reference quirks: bootstrap x N, IS weight on the target). */
+int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, const float* done, const float* isw,
+                const float* qtot, const float* qtot_t, int32_t mix_sum, const float* qa, const float* maxq,
+                float* dq, float* dqa, float* loss_parts, float* td_last, float* loss, mm_stream_t s);
+int mm_mixer_bwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                 const float* qa, const float* dq, const float* done, float* dhm, float* dqa, float* delta,
+                 mm_stream_t s);
+int mm_agent_bwd(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B, const float* save,
+                 const int32_t* acts, const float* dqa, const float* done, float* dh, float* dgi, float* dgh,
+                 float* dq, mm_stream_t s);
+/* Batched outer-product weight gradients dW[g] (+)= sum_r U[g,r,:]^T V[g,r,:] (+ db). */
+typedef struct mm_outer_args {
+  const float* U; int64_t u_g, u_m;
+  const float* V; int64_t v_g, v_m; const int64_t* v_off; const float* v_reset;
+  float* dW; int64_t w_g;
+  float* db; int64_t b_g;
+  int32_t M, R, Cc, accumulate, groups;
+} mm_outer_args;
+int mm_outer_reduce(const mm_outer_args* x, mm_stream_t s);
+/* Batched (gated) transposed mat-vec Y[g] = (W[g]^T X[g]) * Z[g]. */
+typedef struct mm_tmv_args {
+  const float* W; int64_t w_g;
+  const float* X; int64_t x_g, x_m;
+  const float* Z; int64_t z_g, z_m;
+  float* Y; int64_t y_g, y_m;
+  int32_t M, R, Cc, groups;
+} mm_tmv_args;
+int mm_tmv(const mm_tmv_args* x, mm_stream_t s);
+/* Global-norm clip (torch clip_grad_norm_ over G[0:n_clip]) scaled by grad_scale (1/world after an
+ * all-reduce), then Adam on P[0:n]; step is a device counter, norm_out receives the pre-clip norm. */
+int mm_clip_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip, float max_norm, float lr,
+                 float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, float grad_scale,
+                 mm_stream_t s);
+
 /* ------------------------------------------------------------------ MAPPO (rmappo, shared policy)
  * Replaces R_MAPPOPolicy.get_actions / get_values / evaluate_actions
  * (mappo/algorithms/rmappo_policy.py:57-136), SharedReplayBuffer.compute_returns + insert

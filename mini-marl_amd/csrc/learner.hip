@@ -600,11 +600,6 @@ int mm_lrn_gather(int32_t B, int32_t C, int32_t N, int64_t row_stride, int64_t n
   return MM_OK;
 }
 
-typedef struct mm_mix_net {
-  const float* P; const float* q; const int64_t* s_off; const float* h_in; const uint8_t* reset;
-  float* h_out; float* qtot; float* save;
-} mm_mix_net;
-
 int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
                  const mm_mix_net* nets, int32_t n_nets, mm_stream_t s) {
   MM_REQUIRE(nets && n_nets >= 1 && n_nets <= 2 && B > 0, "mixer_fwd: bad args");
@@ -662,14 +657,6 @@ int mm_agent_bwd(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWh
   return MM_OK;
 }
 
-typedef struct mm_outer_args {
-  const float* U; int64_t u_g, u_m;
-  const float* V; int64_t v_g, v_m; const int64_t* v_off; const float* v_reset;
-  float* dW; int64_t w_g;
-  float* db; int64_t b_g;
-  int32_t M, R, Cc, accumulate, groups;
-} mm_outer_args;
-
 int mm_outer_reduce(const mm_outer_args* x, mm_stream_t s) {
   MM_REQUIRE(x && x->M >= 0 && x->R > 0 && x->Cc > 0 && x->groups > 0, "outer_reduce: bad args");
   mm::OuterArgs a = {x->U, x->u_g, x->u_m, x->V, x->v_g, x->v_m, x->v_off, x->v_reset, x->dW, x->w_g,
@@ -679,14 +666,6 @@ int mm_outer_reduce(const mm_outer_args* x, mm_stream_t s) {
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
-
-typedef struct mm_tmv_args {
-  const float* W; int64_t w_g;
-  const float* X; int64_t x_g, x_m;
-  const float* Z; int64_t z_g, z_m;
-  float* Y; int64_t y_g, y_m;
-  int32_t M, R, Cc, groups;
-} mm_tmv_args;
 
 int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
   MM_REQUIRE(x && x->M > 0 && x->R > 0 && x->Cc > 0 && x->groups > 0, "tmv: bad args");

@@ -164,6 +164,210 @@ __global__ __launch_bounds__(PT) void per_add_kernel(double* tree, int64_t* slot
   if (threadIdx.x == 0) st->n_data = min(cap, n_data + K);
 }
 
+// Fast insert for a power-of-two capacity cap = PT * VPT (VPT <= 64): thread t keeps the VPT
+// contiguous leaves [t*VPT, (t+1)*VPT) in registers, so the 8 radix passes re-scan registers
+// instead of HBM, slot-ordered compaction is ONE block scan of per-thread counts, and the tree
+// rebuild is a register subtree per thread plus a 1024-leaf LDS top tree (same pairwise f64
+// sums as rebuild_tree, hence identical trees).
+constexpr int FAST_MAX_VICTIMS = 8192;
+
+template <int VPT>
+__global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
+                                                          const float* td, int64_t K, double eps,
+                                                          int64_t* rows_inout, int64_t* slots_out) {
+  __shared__ uint32_t hist[PT / 64][256];
+  __shared__ uint32_t binsum[256];
+  __shared__ uint32_t scan_sh[PT];
+  __shared__ int32_t victims[FAST_MAX_VICTIMS];
+  __shared__ double top[PT];
+  __shared__ uint64_t s_prefix;
+  __shared__ int64_t s_need;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int64_t n_data = st->n_data;
+  const double alpha = st->alpha;
+  double* leaves = tree + (cap - 1);
+  const int64_t free_n = min(K, cap - n_data);
+  const int64_t rest = K - free_n;
+  const int64_t s0 = (int64_t)t * VPT;
+  if (rest > 0) {
+    // candidates: slots [0, n_data) (this batch's free slots are never victims). Registers hold
+    // only the top 16 bits of each key (sign, exponent, 4 mantissa bits; two per VGPR); the full
+    // key is re-read from the leaf only when those bits tie the selected prefix.
+    uint32_t kp[VPT / 2];
+#pragma unroll
+    for (int i = 0; i < VPT; i += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(leaves + s0 + i);
+      const uint32_t a = (s0 + i < n_data) ? (uint32_t)((uint64_t)__double_as_longlong(v.x) >> 48) : 0xffffu;
+      const uint32_t b = (s0 + i + 1 < n_data) ? (uint32_t)((uint64_t)__double_as_longlong(v.y) >> 48) : 0xffffu;
+      kp[i / 2] = a | (b << 16);
+      if ((i & 15) == 14) asm volatile("" ::: "memory");  // bound the loads in flight (VGPRs)
+    }
+    auto top16 = [&](int i) -> uint32_t { return (kp[i >> 1] >> ((i & 1) * 16)) & 0xffffu; };
+    // base pointer re-made opaque per pass so the VPT full-key loads are not hoisted out of the
+    // pass loop (they would pin 2*VPT VGPRs and spill)
+    const double* lv = leaves + s0;
+    auto full = [&](int i) -> uint64_t { return (uint64_t)__double_as_longlong(lv[i]); };
+    if (t == 0) {
+      s_prefix = 0;
+      s_need = rest;
+    }
+    for (int pass = 7; pass >= 0; --pass) {
+      for (int i = lane; i < 256; i += 64) hist[wave][i] = 0;
+      asm volatile("" : "+v"(lv));
+      __syncthreads();
+      const int shift = pass * 8;
+      const uint64_t hi_mask = (pass == 7) ? 0ull : (~0ull << (shift + 8));
+      const uint64_t pre = s_prefix & hi_mask;
+      if (pass >= 6) {
+        const uint32_t pre16 = (uint32_t)(pre >> 48), mask16 = (uint32_t)(hi_mask >> 48);
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+          const uint32_t k = top16(i);
+          if ((k & mask16) == pre16) atomicAdd(&hist[wave][(k >> (shift - 48)) & 255], 1u);
+        }
+      } else {
+        const uint32_t pre16 = (uint32_t)(s_prefix >> 48);
+#pragma unroll
+        for (int i = 0; i < VPT; ++i)
+          if (top16(i) == pre16 && s0 + i < n_data) {
+            const uint64_t k = full(i);
+            if ((k & hi_mask) == pre) atomicAdd(&hist[wave][(k >> shift) & 255], 1u);
+          }
+      }
+      __syncthreads();
+      if (t < 256) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < PT / 64; ++w) c += hist[w][t];
+        binsum[t] = c;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        // wave 0 scans the 256 bins (4 per lane) and picks the bin holding the need-th key
+        uint32_t b4[4], loc = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          b4[q] = binsum[lane * 4 + q];
+          loc += b4[q];
+        }
+        uint32_t incl = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(incl, o);
+          if (lane >= o) incl += y;
+        }
+        const int64_t need = s_need;
+        const uint32_t excl = incl - loc;
+        int found = -1;
+        int64_t rem = 0;
+        if ((int64_t)excl < need && (int64_t)incl >= need) {
+          int64_t n2 = need - excl;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (found < 0) {
+              if ((int64_t)b4[q] >= n2) {
+                found = lane * 4 + q;
+                rem = n2;
+              } else {
+                n2 -= b4[q];
+              }
+            }
+          }
+        }
+        if (found >= 0) {
+          s_prefix |= ((uint64_t)found << shift);
+          s_need = rem;
+        }
+      }
+      __syncthreads();
+    }
+    const uint64_t T = s_prefix;
+    const uint32_t T16 = (uint32_t)(T >> 48);
+    asm volatile("" : "+v"(lv));
+    const int64_t take_eq = s_need;
+    // 0: key < T, 1: key == T, 2: key > T
+    auto cmp = [&](int i) -> int {
+      const uint32_t k = top16(i);
+      if (k != T16) return k < T16 ? 0 : 2;
+      if (s0 + i >= n_data) return 2;
+      const uint64_t f = full(i);
+      return f < T ? 0 : (f == T ? 1 : 2);
+    };
+    uint64_t mlt = 0, meq = 0;  // classification bitmasks of the thread's VPT keys
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = cmp(i);
+      mlt |= (c == 0 ? 1ull : 0ull) << i;
+      meq |= (c == 1 ? 1ull : 0ull) << i;
+    }
+    const uint32_t nlt = (uint32_t)__popcll(mlt), neq = (uint32_t)__popcll(meq);
+    uint32_t tot;
+    const uint32_t lt0 = (uint32_t)block_excl_scan(nlt, scan_sh, &tot);
+    const uint32_t eq0 = (uint32_t)block_excl_scan(neq, scan_sh, &tot);
+    int64_t lt_rank = lt0, eq_rank = eq0;
+    for (uint64_t m = mlt | meq; m; m &= m - 1) {
+      const int i = __ffsll((unsigned long long)m) - 1;
+      const bool lt = (mlt >> i) & 1ull;
+      if (lt) {
+        victims[lt_rank + min(eq_rank, take_eq)] = (int32_t)(s0 + i);
+        ++lt_rank;
+      } else {
+        if (eq_rank < take_eq) victims[lt_rank + eq_rank] = (int32_t)(s0 + i);
+        ++eq_rank;
+      }
+    }
+    __syncthreads();
+  }
+  // priorities, slot assignment, row swap
+  for (int64_t j = t; j < K; j += PT) {
+    const int64_t slot = j < free_n ? n_data + j : (int64_t)victims[j - free_n];
+    leaves[slot] = pow((double)td[j] + eps, alpha);
+    if (slots_out) slots_out[j] = slot;
+    if (rows_inout) {
+      const int64_t old = slot_row[slot];
+      slot_row[slot] = rows_inout[j];
+      rows_inout[j] = old;
+    }
+  }
+  __syncthreads();
+  // rebuild: register subtree of the thread's VPT leaves, then the PT-leaf top tree in LDS
+  double v[VPT / 2];
+  int64_t lvl_nodes = cap >> 1;  // nodes on the current level (first: the leaves' parents)
+  {
+    const int64_t base = lvl_nodes - 1 + (int64_t)t * (VPT / 2);
+#pragma unroll
+    for (int i = 0; i < VPT / 2; ++i) {
+      const double2 x = *reinterpret_cast<const double2*>(leaves + s0 + 2 * i);
+      v[i] = x.x + x.y;
+      tree[base + i] = v[i];
+      if ((i & 7) == 7) asm volatile("" ::: "memory");  // bound the loads in flight (VGPRs)
+    }
+  }
+#pragma unroll
+  for (int w = VPT / 2; w > 1; w >>= 1) {
+    lvl_nodes >>= 1;
+    const int64_t base = lvl_nodes - 1 + (int64_t)t * (w / 2);
+#pragma unroll
+    for (int i = 0; i < w / 2; ++i) {
+      v[i] = v[2 * i] + v[2 * i + 1];
+      tree[base + i] = v[i];
+    }
+  }
+  top[t] = v[0];
+  __syncthreads();
+  for (int n = PT / 2; n >= 1; n >>= 1) {
+    double x = 0.0;
+    if (t < n) x = top[2 * t] + top[2 * t + 1];
+    __syncthreads();
+    if (t < n) {
+      top[t] = x;
+      tree[n - 1 + t] = x;
+    }
+    __syncthreads();
+  }
+  if (t == 0) st->n_data = min(cap, n_data + K);
+}
+
 __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t cap, int B, const double* fracs,
                                                         uint64_t seed, uint64_t counter, PerDev* st, double decay,
                                                         int64_t* nodes_out, int64_t* slots_out, float* is_w) {
@@ -302,8 +506,28 @@ int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, 
   MM_REQUIRE(per && (td || k == 0), "per_add: null argument");
   MM_REQUIRE(k >= 0 && k <= per->cap, "per_add: batch %lld larger than capacity", (long long)k);
   if (k == 0) return MM_OK;
-  hipLaunchKernelGGL(mm::per_add_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->slot_row, per->cap,
-                     per->st, td, k, per->eps, rows_inout, slots_out, per_scratch(per));
+  const int64_t cap = per->cap;
+  const bool pow2 = (cap & (cap - 1)) == 0;
+  const int64_t vpt = cap / mm::PT;
+  if (pow2 && cap >= 2 * mm::PT && vpt <= 64 && k <= mm::FAST_MAX_VICTIMS) {
+#define MM_PER_FAST(V)                                                                                        \
+  case V:                                                                                                     \
+    hipLaunchKernelGGL(mm::per_add_fast_kernel<V>, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree,      \
+                       per->slot_row, cap, per->st, td, k, per->eps, rows_inout, slots_out);                 \
+    break;
+    switch (vpt) {
+      MM_PER_FAST(2)
+      MM_PER_FAST(4)
+      MM_PER_FAST(8)
+      MM_PER_FAST(16)
+      MM_PER_FAST(32)
+      MM_PER_FAST(64)
+    }
+#undef MM_PER_FAST
+  } else {
+    hipLaunchKernelGGL(mm::per_add_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->slot_row, cap,
+                       per->st, td, k, per->eps, rows_inout, slots_out, per_scratch(per));
+  }
   MM_HIP_CHECK(hipGetLastError());
   per->n_data = std::min(per->cap, per->n_data + k);
   return MM_OK;

@@ -115,3 +115,58 @@ def test_env_shards_are_independent():
         whole.reset_envs(d)
         for k in range(2):
             parts[k].reset_envs(d[k * E:(k + 1) * E])
+
+
+def _mappo_worker(rank, world, port, out):
+    """MAPPO data-parallel statistics protocol (MappoTrainer.prepare): each rank reduces its own
+    buffer to the 5 raw sums (adv, count, ret, ret^2, adv^2 over active rows), one all-reduce,
+    then every rank derives the same global statistics (mm_mappo_stats_from_sums formula)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mini-marl_amd"))
+    from minimarl import dist as mdist
+    torch.set_num_threads(1)
+    mdist.init_from_env(backend="gloo")
+    rng = np.random.default_rng(10 + rank)
+    adv = rng.standard_normal(3000) * (1 + rank)
+    ret = rng.standard_normal(3000) + rank
+    act = (rng.random(3000) > 0.15).astype(np.float64)
+    sums = torch.tensor([(adv * act).sum(), act.sum(), ret.sum(), (ret ** 2).sum(), (adv ** 2 * act).sum()],
+                        dtype=torch.float64)
+    world_n = mdist.make_allreduce()(sums)
+    s, n, sr, sr2, s2 = sums.tolist()
+    R = 3000 * world_n
+    mu = s / n
+    out[rank] = (mu, float(np.sqrt(max(s2 / n - mu * mu, 0.0))), n, sr / R, sr2 / R)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_two_rank_mappo_statistics_are_global():
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    with ctx.Manager() as m:
+        out = m.dict()
+        procs = [ctx.Process(target=_mappo_worker, args=(r, 2, port, out)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+            assert p.exitcode == 0
+        res = dict(out)
+    assert res[0] == res[1]                         # replicas normalise identically
+    adv, ret, act = [], [], []
+    for r in range(2):
+        rng = np.random.default_rng(10 + r)
+        adv.append(rng.standard_normal(3000) * (1 + r))
+        ret.append(rng.standard_normal(3000) + r)
+        act.append(rng.random(3000) > 0.15)
+    adv, ret, act = np.concatenate(adv), np.concatenate(ret), np.concatenate(act)
+    a = adv.copy()
+    a[~act] = np.nan                                # ramppo_network.py:227-231 (nan-masked)
+    mu, sd, n, rm, rsq = res[0]
+    np.testing.assert_allclose(mu, np.nanmean(a), rtol=1e-10)
+    np.testing.assert_allclose(sd, np.nanstd(a), rtol=1e-9)
+    assert n == act.sum()
+    np.testing.assert_allclose(rm, ret.mean(), rtol=1e-12)
+    np.testing.assert_allclose(rsq, (ret ** 2).mean(), rtol=1e-12)

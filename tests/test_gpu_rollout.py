@@ -149,13 +149,16 @@ def test_per_golden_sequence_single_inserts(golden, flavor):
         np.testing.assert_allclose(dev.tree().cpu().numpy(), fx[f"op{k}.tree"], rtol=2e-6, atol=1e-9)
 
 
-@pytest.mark.parametrize("flavor,cap", [("vdn", 1000), ("qmix", 4099)])
-def test_per_batched_vs_oracle(flavor, cap):
+@pytest.mark.parametrize("flavor,cap,kb,rounds", [("vdn", 1000, 700, 7), ("qmix", 4099, 700, 7),
+                                                  # power-of-two capacities: register-resident fast insert
+                                                  ("vdn", 2048, 700, 7), ("qmix", 8192, 3000, 6),
+                                                  ("qmix", 65536, 8192, 10)])
+def test_per_batched_vs_oracle(flavor, cap, kb, rounds):
     dev, ora = _per_pair(flavor, cap)
     rng = np.random.default_rng(1)
-    for rnd in range(7):
-        td = (rng.random(700) * 3).astype(np.float32)
-        if rnd == 5:
+    for rnd in range(rounds):
+        td = (rng.random(kb) * 3).astype(np.float32)
+        if rnd == rounds - 2:
             td[:50] = td[50]                       # ties
         slots = dev.add(torch.tensor(td))
         oslots = ora.add_batch([float(x) for x in td])
