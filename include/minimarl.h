@@ -186,9 +186,15 @@ int mm_lrn_gather(int32_t B, int32_t C, int32_t N, int64_t row_stride, int64_t n
                   int64_t* s_off, int64_t* s2_off, int32_t* acts, float* rew, float* done, uint8_t* done8,
                   mm_stream_t s);
 typedef struct mm_mix_net {
-  const float* P; const float* q; const int64_t* s_off; const float* h_in; const uint8_t* reset;
+  const float* P;
+  const float* gi;  /* [B, 3Hm] precomputed input projection of this step (mm_mixer_gi) or NULL */
+  const float* q; const int64_t* s_off; const float* h_in; const uint8_t* reset;
   float* h_out; float* qtot; float* save;
 } mm_mix_net;
+/* Mixer GRU input projection W_ih s + b_ih for all R = C*B gathered states of 1-2 nets at once. */
+int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
+                const float* P0, const int64_t* s_off0, float* gi0, const float* P1, const int64_t* s_off1, float* gi1,
+                mm_stream_t s);
 /* One mixer time step for 1-2 nets (behavior / target) in one launch. */
 int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
                  const mm_mix_net* nets, int32_t n_nets, mm_stream_t s);

@@ -109,6 +109,7 @@ __host__ __device__ inline int mix_save_dim(int Hm, int K1, int N) { return 6 * 
 
 struct MixFwdNet {
   const float* P;        // mixer params (canonical)
+  const float* gi;       // [B][3Hm] precomputed W_ih s + b_ih of this step (mixer_gi_kernel) or nullptr
   const float* q;        // [B][N] agent values fed to the mixer (Q(a) or max Q')
   const int64_t* s_off;  // [B] state offsets into obs (-1: reset obs)
   const float* h_in;     // [B][Hm] (nullptr => zero)
@@ -125,6 +126,57 @@ struct MixFwdArgs {
   int B, N, S, Hm, K1;
 };
 
+// Mixer GRU input projection for every (t, b) of the chunk batch at once (the state input does
+// not depend on the recurrence): gi[r][m] = b_ih[m] + sum_k W_ih[m][k] s_r[k] with s_r gathered
+// through the state offsets (reset obs where off < 0). v_mfma_f32_32x32x2_f32, features of W_ih
+// on rows, samples on columns; block = 4 waves splitting K, reduced through LDS.
+struct MixGiNet {
+  const float* P;
+  const int64_t* s_off;  // [R]
+  float* gi;             // [R][3Hm]
+};
+struct MixGiArgs {
+  MixGiNet net[2];
+  const float* obs;
+  const float* reset_obs;
+  int R, S, Hm, K1, N;
+};
+
+__global__ __launch_bounds__(256) void mixer_gi_kernel(MixGiArgs a) {
+  __shared__ float red[4][1024];
+  const MixGiNet& nt = a.net[blockIdx.z];
+  const int S = a.S, M3 = 3 * a.Hm;
+  const MixOff o = mix_offsets(S, a.Hm, a.K1, a.N);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hh = lane >> 5;
+  const int rb = blockIdx.y, col = blockIdx.x * 32 + i;
+  const int row = rb * 32 + i;
+  const float* W = nt.P + o.gWih + (int64_t)(row < M3 ? row : 0) * S;
+  const int64_t off = col < a.R ? nt.s_off[col] : -1;
+  const float* x = off >= 0 ? a.obs + off : a.reset_obs;
+  const int KD = (S + 31) / 32;
+  f32x16 acc = {0};
+  for (int kb = wave; kb < KD; kb += 4) {
+    float av[16], bv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = kb * 32 + kperm(s, hh);
+      const bool ok = k < S;
+      av[s] = (ok && row < M3) ? W[k] : 0.0f;
+      bv[s] = (ok && col < a.R) ? x[k] : 0.0f;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = mfma32(av[s], bv[s], acc);
+  }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) red[wave][kperm(s, hh) * 32 + i] = acc[s];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const int m = rb * 32 + (e >> 5), c = blockIdx.x * 32 + (e & 31);
+    if (m < M3 && c < a.R)
+      nt.gi[(int64_t)c * M3 + m] = nt.P[o.gbih + m] + ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e]));
+  }
+}
+
 // One block per (sample, net): blockIdx.y selects behavior / target.
 __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -139,13 +191,18 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixFwdArgs a) {
   float* h1 = gh + 3 * Hm;         // [Hm]
   float* hyp = h1 + Hm;            // [N*K1 + 3*K1]: w1raw | b1 | w2raw | b2pre
   float* yp = hyp + N * K1 + 3 * K1;  // [K1]
-  const int64_t off = nt.s_off[b];
-  const float* src = off >= 0 ? a.obs + off : a.reset_obs;
-  for (int i = threadIdx.x; i < S; i += blockDim.x) xs[i] = src[i];
   const bool rz = !nt.h_in || (nt.reset && nt.reset[b]);
   for (int i = threadIdx.x; i < Hm; i += blockDim.x) h0[i] = rz ? 0.f : nt.h_in[(int64_t)b * Hm + i];
-  __syncthreads();
-  block_matvec(nt.P + o.gWih, nt.P + o.gbih, 3 * Hm, S, xs, gi);
+  if (nt.gi) {
+    for (int i = threadIdx.x; i < 3 * Hm; i += blockDim.x) gi[i] = nt.gi[(int64_t)b * 3 * Hm + i];
+    __syncthreads();
+  } else {
+    const int64_t off = nt.s_off[b];
+    const float* src = off >= 0 ? a.obs + off : a.reset_obs;
+    for (int i = threadIdx.x; i < S; i += blockDim.x) xs[i] = src[i];
+    __syncthreads();
+    block_matvec(nt.P + o.gWih, nt.P + o.gbih, 3 * Hm, S, xs, gi);
+  }
   block_matvec(nt.P + o.gWhh, nt.P + o.gbhh, 3 * Hm, Hm, h0, gh);
   __syncthreads();
   float* sv = nt.save ? nt.save + (int64_t)b * mix_save_dim(Hm, K1, N) : nullptr;
@@ -607,7 +664,7 @@ int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const 
   mm::MixFwdArgs a;
   for (int i = 0; i < 2; ++i) {
     const mm_mix_net& n = nets[i < n_nets ? i : 0];
-    a.net[i] = {n.P, n.q, n.s_off, n.h_in, n.reset, n.h_out, n.qtot, n.save};
+    a.net[i] = {n.P, n.gi, n.q, n.s_off, n.h_in, n.reset, n.h_out, n.qtot, n.save};
   }
   a.obs = obs;
   a.reset_obs = reset_obs;
@@ -619,6 +676,26 @@ int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const 
   const size_t sm = sizeof(float) * ((size_t)S + 9 * Hm + N * K1 + 4 * K1);
   MM_REQUIRE(sm <= 64 * 1024, "mixer_fwd: state too large for LDS (%zu B)", sm);
   hipLaunchKernelGGL(mm::mixer_fwd_kernel, dim3(B, n_nets), dim3(256), sm, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
+                const float* P0, const int64_t* s_off0, float* gi0, const float* P1, const int64_t* s_off1, float* gi1,
+                mm_stream_t s) {
+  MM_REQUIRE(R > 0 && P0 && s_off0 && gi0 && obs && reset_obs, "mixer_gi: bad args");
+  mm::MixGiArgs a;
+  a.net[0] = {P0, s_off0, gi0};
+  a.net[1] = {P1 ? P1 : P0, P1 ? s_off1 : s_off0, P1 ? gi1 : gi0};
+  a.obs = obs;
+  a.reset_obs = reset_obs;
+  a.R = R;
+  a.S = S;
+  a.Hm = Hm;
+  a.K1 = K1;
+  a.N = N;
+  dim3 grid((R + 31) / 32, (3 * Hm + 31) / 32, P1 ? 2 : 1);
+  hipLaunchKernelGGL(mm::mixer_gi_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

@@ -124,8 +124,8 @@ def check(rc, what=""):
 
 
 class MixNetIO(ctypes.Structure):
-    _fields_ = [("P", c_vp), ("q", c_vp), ("s_off", c_vp), ("h_in", c_vp), ("reset", c_vp), ("h_out", c_vp),
-                ("qtot", c_vp), ("save", c_vp)]
+    _fields_ = [("P", c_vp), ("gi", c_vp), ("q", c_vp), ("s_off", c_vp), ("h_in", c_vp), ("reset", c_vp),
+                ("h_out", c_vp), ("qtot", c_vp), ("save", c_vp)]
 
 
 class OuterArgs(ctypes.Structure):
@@ -148,6 +148,8 @@ _SIGS += [
     ("mm_lrn_gather", c_i32, [c_i32, c_i32, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp, c_vp, c_vp, c_vp]),
     ("mm_mixer_fwd", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(MixNetIO), c_i32, c_vp]),
+    ("mm_mixer_gi", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                            c_vp]),
     ("mm_lrn_loss", c_i32, [c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                             c_vp, c_vp, c_vp, c_vp]),
     ("mm_mixer_bwd", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

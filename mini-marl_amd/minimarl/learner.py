@@ -164,6 +164,8 @@ class QLearner:
             self.msave = torch.zeros(C, B, self.MSD, **f32)
             self.mdelta = torch.zeros(C, B, self.MDD, **f32)
             self.dhm = torch.zeros(B, Hm, **f32)
+            self.gi_b = torch.zeros(C, B, 3 * Hm, **f32)
+            self.gi_t = torch.zeros(C, B, 3 * Hm, **f32)
 
     # ------------------------------------------------------------------ batch in
     def gather(self, per, store):
@@ -206,6 +208,11 @@ class QLearner:
         obs_p = ctypes.c_void_p(obs_base) if isinstance(obs_base, int) else ptr(obs_base)
         reset_p = ctypes.c_void_p(reset_obs_ptr) if isinstance(reset_obs_ptr, int) else ptr(reset_obs_ptr)
         ND = N * D
+        if self.mode == "qmix":
+            # mixer GRU input projections of every (t, b) for both mixers: one MFMA launch
+            mx = self.mix
+            check(L.mm_mixer_gi(CB, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, ptr(mx.flat), ptr(self.s_off),
+                                ptr(self.gi_b), ptr(self.tmix.flat), ptr(self.s2_off), ptr(self.gi_t), s), "mixer gi")
         # ---- forward over the chunk (behavior GATHER + save, target MAX) in dual launches
         for t in range(C):
             ib, it = QFwdIO(), QFwdIO()
@@ -230,11 +237,11 @@ class QLearner:
             if self.mode == "qmix":
                 mx = self.mix
                 nets = (MixNetIO * 2)()
-                for k, (P, q, off, h, qt, sv) in enumerate(
-                        ((self.mix.flat, self.qa[t], self.s_off, self.hm, self.qtot[t], self.msave[t]),
-                         (self.tmix.flat, self.maxq[t], self.s2_off, self.hmt, self.qtot_t[t], None))):
+                for k, (P, q, off, h, qt, sv, gi) in enumerate(
+                        ((self.mix.flat, self.qa[t], self.s_off, self.hm, self.qtot[t], self.msave[t], self.gi_b[t]),
+                         (self.tmix.flat, self.maxq[t], self.s2_off, self.hmt, self.qtot_t[t], None, self.gi_t[t]))):
                     n = nets[k]
-                    n.P, n.q = P.data_ptr(), q.data_ptr()
+                    n.P, n.q, n.gi = P.data_ptr(), q.data_ptr(), gi.data_ptr()
                     n.s_off = off.data_ptr() + 8 * t * B
                     n.h_in, n.h_out = h[t % 2].data_ptr(), h[(t + 1) % 2].data_ptr()
                     n.reset = self.ones8.data_ptr() if t == 0 else self.done8.data_ptr() + (t - 1) * B

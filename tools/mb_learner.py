@@ -1,0 +1,27 @@
+"""Microbenchmark: one QMIX learner update (B=32, C=10, GRU-64, Hm=64) from a filled device PER."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mini-marl_amd"))
+import torch  # noqa: E402
+from minimarl.engine import RolloutEngine  # noqa: E402
+from minimarl.learner import Mixer, QLearner  # noqa: E402
+
+E, N = 512, 8
+eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=10, capacity=4 * E, seed=1, device="cuda")
+for _ in range(4):
+    eng.run_graph(0.1)
+mix, tmix = Mixer(N, N * eng.D, 64, 32, "cuda", seed=7), Mixer(N, N * eng.D, 64, 32, "cuda", seed=7)
+L = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda")
+L.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=3)
+for _ in range(5):
+    L.replay_update()
+torch.cuda.synchronize()
+a, b = torch.cuda.Event(True), torch.cuda.Event(True)
+a.record()
+for _ in range(50):
+    L.replay_update()
+b.record()
+torch.cuda.synchronize()
+print(json.dumps({"dbg": os.environ.get("MM_MIX_DBG", "0"), "ms_per_update": a.elapsed_time(b) / 50}))
