@@ -217,6 +217,12 @@ typedef struct mm_outer_args {
   int32_t M, R, Cc, accumulate, groups;
 } mm_outer_args;
 int mm_outer_reduce(const mm_outer_args* x, mm_stream_t s);
+/* Up to 16 independent outer-reduce jobs in one launch (M split into 32-row slices, partials summed
+ * in fixed order by a second launch: deterministic). partial: device floats, size from
+ * mm_outer_reduce_batch_partial(jobs, n). */
+int64_t mm_outer_reduce_batch_partial(const mm_outer_args* x, int32_t n_jobs);
+int mm_outer_reduce_batch(const mm_outer_args* x, int32_t n_jobs, float* partial, int64_t partial_count,
+                          mm_stream_t s);
 /* Batched (gated) transposed mat-vec Y[g] = (W[g]^T X[g]) * Z[g]. */
 typedef struct mm_tmv_args {
   const float* W; int64_t w_g;

@@ -488,15 +488,20 @@ struct OuterArgs {
 };
 
 __global__ __launch_bounds__(256) void outer_reduce_kernel(OuterArgs a) {
-  __shared__ float su[32][33];
-  __shared__ float svv[32][33];
+  // LDS double buffer + register prefetch: chunk m0+32 is loaded while chunk m0 is reduced, so
+  // the M/32 sequential steps pay one memory latency instead of one each.
+  __shared__ float su[2][32][33];
+  __shared__ float svv[2][32][33];
   const int g = blockIdx.z;
   const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
   const int tr = threadIdx.x / 32, tc = threadIdx.x % 32;  // tr in [0,8): rows tr, tr+8, tr+16, tr+24
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float accb = 0.f;
-  for (int m0 = 0; m0 < a.M; m0 += 32) {
-    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+  float pu[4], pv[4];
+  auto fetch = [&](int m0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = threadIdx.x + 256 * q;
       const int mm = k / 32, x = k % 32;
       const int m = m0 + mm;
       float u = 0.f, v = 0.f;
@@ -512,18 +517,35 @@ __global__ __launch_bounds__(256) void outer_reduce_kernel(OuterArgs a) {
           }
         }
       }
-      su[mm][x] = u;
-      svv[mm][x] = v;
+      pu[q] = u;
+      pv[q] = v;
     }
-    __syncthreads();
-    for (int mm = 0; mm < 32; ++mm) {
-      const float v = svv[mm][tc];
+  };
+  auto stash = [&](int buf) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] += su[mm][tr + 8 * q] * v;
+    for (int q = 0; q < 4; ++q) {
+      const int k = threadIdx.x + 256 * q;
+      su[buf][k / 32][k % 32] = pu[q];
+      svv[buf][k / 32][k % 32] = pv[q];
+    }
+  };
+  fetch(0);
+  stash(0);
+  __syncthreads();
+  int buf = 0;
+  for (int m0 = 0; m0 < a.M; m0 += 32) {
+    const bool more = m0 + 32 < a.M;
+    if (more) fetch(m0 + 32);
+    for (int mm = 0; mm < 32; ++mm) {
+      const float v = svv[buf][mm][tc];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += su[buf][mm][tr + 8 * q] * v;
     }
     if (a.db && blockIdx.x == 0 && threadIdx.x < 32)
-      for (int mm = 0; mm < 32; ++mm) accb += su[mm][threadIdx.x];
+      for (int mm = 0; mm < 32; ++mm) accb += su[buf][mm][threadIdx.x];
+    if (more) stash(buf ^ 1);
     __syncthreads();
+    buf ^= 1;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -536,6 +558,91 @@ __global__ __launch_bounds__(256) void outer_reduce_kernel(OuterArgs a) {
   if (a.db && blockIdx.x == 0 && threadIdx.x < 32 && r0 + threadIdx.x < a.R) {
     float* o = a.db + g * a.b_g + r0 + threadIdx.x;
     *o = a.accumulate ? *o + accb : accb;
+  }
+}
+
+// Batched split-M outer reduce: many independent OuterArgs jobs in ONE launch, each job's M rows
+// split into 32-row slices; block (job, tile, group, slice) reduces one 32x32 tile over one slice
+// into a partial, outer_sum_kernel adds the slices in fixed order (deterministic).
+constexpr int OB_MAX = 16;
+struct OuterBatch {
+  OuterArgs job[OB_MAX];
+  int tiles_c[OB_MAX], tiles_r[OB_MAX], groups[OB_MAX], slices[OB_MAX];
+  int blk0[OB_MAX + 1];
+  int64_t part[OB_MAX];  // partial offset: [slice][group][R*Cc + R]
+  int njobs;
+  float* partial;
+};
+
+__global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
+  __shared__ float su[32][33];
+  __shared__ float svv[32][33];
+  int j = 0;
+  while (j + 1 < ob.njobs && (int)blockIdx.x >= ob.blk0[j + 1]) ++j;
+  const OuterArgs& a = ob.job[j];
+  int t = blockIdx.x - ob.blk0[j];
+  const int tc_ = t % ob.tiles_c[j];
+  t /= ob.tiles_c[j];
+  const int tr_ = t % ob.tiles_r[j];
+  t /= ob.tiles_r[j];
+  const int g = t % ob.groups[j];
+  const int sl = t / ob.groups[j];
+  const int r0 = tr_ * 32, c0 = tc_ * 32, m0 = sl * 32;
+  for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+    const int mm = k / 32, x = k % 32;
+    const int m = m0 + mm;
+    float u = 0.f, v = 0.f;
+    if (m < a.M) {
+      if (r0 + x < a.R) u = a.U[g * a.u_g + (int64_t)m * a.u_m + r0 + x];
+      if (c0 + x < a.Cc) {
+        if (a.v_off) {
+          const int64_t off = a.v_off[m];
+          const float* base = off >= 0 ? a.V + off : a.v_reset;
+          v = base[g * a.v_g + c0 + x];
+        } else {
+          v = a.V[g * a.v_g + (int64_t)m * a.v_m + c0 + x];
+        }
+      }
+    }
+    su[mm][x] = u;
+    svv[mm][x] = v;
+  }
+  __syncthreads();
+  const int tr = threadIdx.x / 32, tc = threadIdx.x % 32;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int mm = 0; mm < 32; ++mm) {
+    const float v = svv[mm][tc];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += su[mm][tr + 8 * q] * v;
+  }
+  const int64_t per = (int64_t)a.R * a.Cc + a.R;
+  float* out = ob.partial + ob.part[j] + ((int64_t)sl * ob.groups[j] + g) * per;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + tr + 8 * q, c = c0 + tc;
+    if (r < a.R && c < a.Cc) out[(int64_t)r * a.Cc + c] = acc[q];
+  }
+  if (a.db && tc_ == 0 && threadIdx.x < 32 && r0 + threadIdx.x < a.R) {
+    float sb = 0.f;
+    for (int mm = 0; mm < 32; ++mm) sb += su[mm][threadIdx.x];
+    out[(int64_t)a.R * a.Cc + r0 + threadIdx.x] = sb;
+  }
+}
+
+__global__ __launch_bounds__(256) void outer_sum_kernel(OuterBatch ob) {
+  const int j = blockIdx.y;
+  const OuterArgs& a = ob.job[j];
+  const int64_t per = (int64_t)a.R * a.Cc + a.R;
+  const int64_t total = per * ob.groups[j];
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int g = (int)(e / per);
+    const int64_t w = e % per;
+    if (w >= (int64_t)a.R * a.Cc && !a.db) continue;
+    float s = 0.f;
+    const float* p = ob.partial + ob.part[j] + e;
+    for (int sl = 0; sl < ob.slices[j]; ++sl) s += p[(int64_t)sl * total];
+    float* o = w < (int64_t)a.R * a.Cc ? a.dW + g * a.w_g + w : a.db + g * a.b_g + (w - (int64_t)a.R * a.Cc);
+    *o = a.accumulate ? *o + s : s;
   }
 }
 
@@ -740,6 +847,54 @@ int mm_outer_reduce(const mm_outer_args* x, mm_stream_t s) {
                      x->db, x->b_g, x->M, x->R, x->Cc, x->accumulate};
   dim3 grid((x->Cc + 31) / 32, (x->R + 31) / 32, x->groups);
   hipLaunchKernelGGL(mm::outer_reduce_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+static int64_t outer_batch_layout(const mm_outer_args* x, int n, mm::OuterBatch* ob) {
+  int blk = 0;
+  int64_t part = 0;
+  for (int j = 0; j < n; ++j) {
+    const mm_outer_args& q = x[j];
+    ob->job[j] = {q.U, q.u_g, q.u_m, q.V, q.v_g, q.v_m, q.v_off, q.v_reset, q.dW, q.w_g, q.db, q.b_g, q.M, q.R,
+                  q.Cc, q.accumulate};
+    ob->tiles_c[j] = (q.Cc + 31) / 32;
+    ob->tiles_r[j] = (q.R + 31) / 32;
+    ob->groups[j] = q.groups;
+    ob->slices[j] = (q.M + 31) / 32;
+    ob->blk0[j] = blk;
+    ob->part[j] = part;
+    blk += ob->tiles_c[j] * ob->tiles_r[j] * q.groups * ob->slices[j];
+    part += (int64_t)ob->slices[j] * q.groups * ((int64_t)q.R * q.Cc + q.R);
+  }
+  ob->blk0[n] = blk;
+  ob->njobs = n;
+  return part;
+}
+
+int64_t mm_outer_reduce_batch_partial(const mm_outer_args* x, int32_t n_jobs) {
+  if (!x || n_jobs < 1 || n_jobs > mm::OB_MAX) return -1;
+  mm::OuterBatch ob;
+  return outer_batch_layout(x, n_jobs, &ob);
+}
+
+int mm_outer_reduce_batch(const mm_outer_args* x, int32_t n_jobs, float* partial, int64_t partial_count,
+                          mm_stream_t s) {
+  MM_REQUIRE(x && partial && n_jobs >= 1 && n_jobs <= mm::OB_MAX, "outer_reduce_batch: bad args");
+  mm::OuterBatch ob;
+  int64_t maxper = 0;
+  for (int j = 0; j < n_jobs; ++j) {
+    MM_REQUIRE(x[j].M > 0 && x[j].R > 0 && x[j].Cc > 0 && x[j].groups > 0, "outer_reduce_batch: bad job %d", j);
+    maxper = std::max<int64_t>(maxper, ((int64_t)x[j].R * x[j].Cc + x[j].R) * x[j].groups);
+  }
+  const int64_t need = outer_batch_layout(x, n_jobs, &ob);
+  MM_REQUIRE(need <= partial_count, "outer_reduce_batch: partial buffer too small (%lld < %lld)",
+             (long long)partial_count, (long long)need);
+  ob.partial = partial;
+  hipLaunchKernelGGL(mm::outer_batch_kernel, dim3(ob.blk0[n_jobs]), dim3(256), 0, (hipStream_t)s, ob);
+  MM_HIP_CHECK(hipGetLastError());
+  const int gx = (int)std::min<int64_t>((maxper + 255) / 256, 1024);
+  hipLaunchKernelGGL(mm::outer_sum_kernel, dim3(gx, n_jobs), dim3(256), 0, (hipStream_t)s, ob);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

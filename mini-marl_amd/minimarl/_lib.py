@@ -157,6 +157,8 @@ _SIGS += [
     ("mm_agent_bwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp, c_vp, c_vp, c_vp]),
     ("mm_outer_reduce", c_i32, [ctypes.POINTER(OuterArgs), c_vp]),
+    ("mm_outer_reduce_batch_partial", c_i64, [ctypes.POINTER(OuterArgs), c_i32]),
+    ("mm_outer_reduce_batch", c_i32, [ctypes.POINTER(OuterArgs), c_i32, c_vp, c_i64, c_vp]),
     ("mm_tmv", c_i32, [ctypes.POINTER(TmvArgs), c_vp]),
     ("mm_clip_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
                              c_vp, c_f32, c_vp]),

@@ -166,6 +166,14 @@ class QLearner:
             self.dhm = torch.zeros(B, Hm, **f32)
             self.gi_b = torch.zeros(C, B, 3 * Hm, **f32)
             self.gi_t = torch.zeros(C, B, 3 * Hm, **f32)
+        # split-M outer-reduce partials: the job geometry is fixed, size it once (no launches here)
+        jobs = []
+        zero = ctypes.c_void_p(0)
+        self._agent_wgrad(None, None, zero, zero, C * B, jobs)
+        if self.mode == "qmix":
+            self._mixer_wgrad(None, None, zero, zero, C * B, jobs)
+        arr = (OuterArgs * len(jobs))(*jobs)
+        self._opart = torch.zeros(int(lib().mm_outer_reduce_batch_partial(arr, len(jobs))), **f32)
 
     # ------------------------------------------------------------------ batch in
     def gather(self, per, store):
@@ -265,10 +273,14 @@ class QLearner:
             check(L.mm_agent_bwd(ctypes.byref(self.beh.dims), ptr(P), o[8], o[5], B, ptr(self.asave[t]),
                                  ctypes.c_void_p(self.acts.data_ptr() + 4 * t * B * N), ptr(self.dqa[t]), ptr(dn),
                                  ptr(self.dh), ptr(self.dgi[t]), ptr(self.dgh[t]), ptr(self.dqv[t]), s), "agent bwd")
-        # ---- deferred weight gradients: batched over all C*B rows, grouped by agent
-        self._agent_wgrad(L, s, obs_p, reset_p, CB)
+        # ---- deferred weight gradients: batched over all C*B rows, grouped by agent; every
+        # outer product of the update (agent + mixer) in ONE split-M launch (+ its partial sum)
+        jobs = []
+        self._agent_wgrad(L, s, obs_p, reset_p, CB, jobs)
         if self.mode == "qmix":
-            self._mixer_wgrad(L, s, obs_p, reset_p, CB)
+            self._mixer_wgrad(L, s, obs_p, reset_p, CB, jobs)
+        arr = (OuterArgs * len(jobs))(*jobs)
+        check(L.mm_outer_reduce_batch(arr, len(jobs), ptr(self._opart), self._opart.numel(), s), "outer batch")
 
     def apply_grads(self, grad_scale=1.0):
         """clip_grad_norm_ + Adam (grads scaled first, e.g. 1/world after an all-reduce), then repack
@@ -285,7 +297,8 @@ class QLearner:
         self.compute_grads(obs_base, reset_obs_ptr)
         self.apply_grads()
 
-    def _outer(self, L, s, U, u_g, u_m, V, v_g, v_m, dW, w_g, db, b_g, M, R, Cc, groups, v_off=None, v_reset=None):
+    def _outer(self, L, s, U, u_g, u_m, V, v_g, v_m, dW, w_g, db, b_g, M, R, Cc, groups, v_off=None, v_reset=None,
+               jobs=None):
         a = OuterArgs()
         a.U, a.u_g, a.u_m = U, u_g, u_m
         a.V, a.v_g, a.v_m = V, v_g, v_m
@@ -294,7 +307,10 @@ class QLearner:
         a.dW, a.w_g = dW, w_g
         a.db, a.b_g = db, b_g
         a.M, a.R, a.Cc, a.accumulate, a.groups = M, R, Cc, 0, groups
-        check(L.mm_outer_reduce(ctypes.byref(a), s), "outer_reduce")
+        if jobs is not None:
+            jobs.append(a)
+        else:
+            check(L.mm_outer_reduce(ctypes.byref(a), s), "outer_reduce")
 
     def _tmv(self, L, s, W, w_g, X, x_g, x_m, Z, z_g, z_m, Y, y_g, y_m, M, R, Cc, groups):
         a = TmvArgs()
@@ -302,36 +318,37 @@ class QLearner:
         a.M, a.R, a.Cc, a.groups = M, R, Cc, groups
         check(L.mm_tmv(ctypes.byref(a), s), "tmv")
 
-    def _agent_wgrad(self, L, s, obs_p, reset_p, M):
+    def _agent_wgrad(self, L, s, obs_p, reset_p, M, jobs):
         N, D, F1, G, H, A, SD = self.N, self.D, self.F1, self.G, self.H, self.A, self.SD
         o = self.beh.offs          # W1 b1 W2 b2 Wih Whh bih bhh Wq bq
         gp, pp = self.Gr.data_ptr(), self.P.data_ptr()
         sv = self.asave.data_ptr()
         f = 4
+        # data gradients of the feed-forward layers first (the outer products below only read them)
+        # dpre2 = (x2 > 0) * Wih^T dgi ; dpre1 = (x1 > 0) * W2^T dpre2
+        if L is not None:
+            self._tmv(L, s, pp + f * o[4], 3 * H * G, self.dgi.data_ptr(), 3 * H, N * 3 * H, sv + f * F1, SD,
+                      N * SD, self.dpre2.data_ptr(), G, N * G, M, 3 * H, G, N)
+            self._tmv(L, s, pp + f * o[2], G * F1, self.dpre2.data_ptr(), G, N * G, sv, SD, N * SD,
+                      self.dpre1.data_ptr(), F1, N * F1, M, G, F1, N)
         # Wq, bq <- dq (one-hot) x h_out
         self._outer(L, s, self.dqv.data_ptr(), A, N * A, sv + f * (F1 + G + 5 * H), SD, N * SD,
-                    gp + f * o[8], A * H, gp + f * o[9], A, M, A, H, N)
+                    gp + f * o[8], A * H, gp + f * o[9], A, M, A, H, N, jobs=jobs)
         # Whh, bhh <- dgh x h_in
         self._outer(L, s, self.dgh.data_ptr(), 3 * H, N * 3 * H, sv + f * (F1 + G), SD, N * SD,
-                    gp + f * o[5], 3 * H * H, gp + f * o[7], 3 * H, M, 3 * H, H, N)
+                    gp + f * o[5], 3 * H * H, gp + f * o[7], 3 * H, M, 3 * H, H, N, jobs=jobs)
         # Wih, bih <- dgi x x2
         self._outer(L, s, self.dgi.data_ptr(), 3 * H, N * 3 * H, sv + f * F1, SD, N * SD,
-                    gp + f * o[4], 3 * H * G, gp + f * o[6], 3 * H, M, 3 * H, G, N)
-        # dpre2 = (x2 > 0) * Wih^T dgi
-        self._tmv(L, s, pp + f * o[4], 3 * H * G, self.dgi.data_ptr(), 3 * H, N * 3 * H, sv + f * F1, SD, N * SD,
-                  self.dpre2.data_ptr(), G, N * G, M, 3 * H, G, N)
+                    gp + f * o[4], 3 * H * G, gp + f * o[6], 3 * H, M, 3 * H, G, N, jobs=jobs)
         # W2, b2 <- dpre2 x x1
         self._outer(L, s, self.dpre2.data_ptr(), G, N * G, sv, SD, N * SD,
-                    gp + f * o[2], G * F1, gp + f * o[3], G, M, G, F1, N)
-        # dpre1 = (x1 > 0) * W2^T dpre2
-        self._tmv(L, s, pp + f * o[2], G * F1, self.dpre2.data_ptr(), G, N * G, sv, SD, N * SD,
-                  self.dpre1.data_ptr(), F1, N * F1, M, G, F1, N)
+                    gp + f * o[2], G * F1, gp + f * o[3], G, M, G, F1, N, jobs=jobs)
         # W1, b1 <- dpre1 x obs (gathered through the s_t offsets)
         self._outer(L, s, self.dpre1.data_ptr(), F1, N * F1, obs_p.value, D, 0,
                     gp + f * o[0], F1 * D, gp + f * o[1], F1, M, F1, D, N,
-                    v_off=self.s_off.data_ptr(), v_reset=reset_p.value)
+                    v_off=self.s_off.data_ptr(), v_reset=reset_p.value, jobs=jobs)
 
-    def _mixer_wgrad(self, L, s, obs_p, reset_p, M):
+    def _mixer_wgrad(self, L, s, obs_p, reset_p, M, jobs):
         mx = self.mix
         Hm, K1, N, S = mx.Hm, mx.K1, self.N, mx.S
         MSD, MDD = self.MSD, self.MDD
@@ -342,18 +359,18 @@ class QLearner:
         hm1 = sv + f * 5 * Hm
         # GRU input weights <- dgi x state (gathered), recurrent <- dgh x hm0
         self._outer(L, s, dl, 0, MDD, obs_p.value, 0, 0, mo["gWih"], 0, mo["gbih"], 0, M, 3 * Hm, S, 1,
-                    v_off=self.s_off.data_ptr(), v_reset=reset_p.value)
-        self._outer(L, s, dl + f * 3 * Hm, 0, MDD, sv, 0, MSD, mo["gWhh"], 0, mo["gbhh"], 0, M, 3 * Hm, Hm, 1)
+                    v_off=self.s_off.data_ptr(), v_reset=reset_p.value, jobs=jobs)
+        self._outer(L, s, dl + f * 3 * Hm, 0, MDD, sv, 0, MSD, mo["gWhh"], 0, mo["gbhh"], 0, M, 3 * Hm, Hm, 1, jobs=jobs)
         # hypernetworks <- deltas x hm1
-        self._outer(L, s, dl + f * 6 * Hm, 0, MDD, hm1, 0, MSD, mo["w1W"], 0, mo["w1b"], 0, M, N * K1, Hm, 1)
-        self._outer(L, s, dl + f * (6 * Hm + N * K1), 0, MDD, hm1, 0, MSD, mo["b1W"], 0, mo["b1b"], 0, M, K1, Hm, 1)
+        self._outer(L, s, dl + f * 6 * Hm, 0, MDD, hm1, 0, MSD, mo["w1W"], 0, mo["w1b"], 0, M, N * K1, Hm, 1, jobs=jobs)
+        self._outer(L, s, dl + f * (6 * Hm + N * K1), 0, MDD, hm1, 0, MSD, mo["b1W"], 0, mo["b1b"], 0, M, K1, Hm, 1, jobs=jobs)
         self._outer(L, s, dl + f * (6 * Hm + N * K1 + K1), 0, MDD, hm1, 0, MSD, mo["w2W"], 0, mo["w2b"], 0, M, K1,
-                    Hm, 1)
+                    Hm, 1, jobs=jobs)
         self._outer(L, s, dl + f * (6 * Hm + N * K1 + 2 * K1), 0, MDD, hm1, 0, MSD, mo["b2aW"], 0, mo["b2ab"], 0, M,
-                    K1, Hm, 1)
+                    K1, Hm, 1, jobs=jobs)
         # final b2 layer <- dQ x relu(b2 hidden)
         self._outer(L, s, dl + f * (6 * Hm + N * K1 + 3 * K1), 0, MDD, sv + f * (6 * Hm + N * K1 + 2 * K1), 0, MSD,
-                    mo["b2bW"], 0, mo["b2bb"], 0, M, 1, K1, 1)
+                    mo["b2bW"], 0, mo["b2bb"], 0, M, 1, K1, 1, jobs=jobs)
 
     # ------------------------------------------------------------------ full update from the PER
     def sample_and_grads(self, per, store, reset_obs_ptr, fracs=None, seed=0, counter=0):
