@@ -74,6 +74,9 @@ typedef struct mm_qfwd_io {
   /* optional training save: per (e, agent) row of SD = F1+G+6H floats
    * [x1 | x2 | h_in | r | z | n | W_hn h + b_hn | h_out] at save + (e*N + agent)*SD */
   float* save;
+  /* split forward (mm_agent_q_pre2 / mm_agent_q_rec2): the GRU input projection per (e, agent),
+   * [e][agent][3H] = (b_ih + b_hh for r, z | b_ih for n) + W_ih x2 */
+  float* gi;
 } mm_qfwd_io;
 
 int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,
@@ -81,6 +84,15 @@ int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io*
 
 /* Two nets of the same dims in ONE launch (e.g. target fwd of step t + behavior fwd of step t+1). */
 int mm_agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
+                    const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
+
+/* Split forward for training over a whole chunk batch: PRE runs the non-recurrent part (layers 1-2
+ * and W_ih x2, writing io.gi and the x1|x2 save columns) for all E = C*B rows of two nets in one
+ * launch; REC runs one recurrent step (W_hh h, gates, Q head, epilogue) reading io.gi. Together
+ * bit-identical to mm_agent_q_fwd2 (same MFMA accumulation order). */
+int mm_agent_q_pre2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
+                    const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
+int mm_agent_q_rec2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
                     const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
 
 /* Survey-style convenience entry: contiguous obs [E,N,D], hidden [E,N,H] -> q [E,N,A], h_out [E,N,H]. */

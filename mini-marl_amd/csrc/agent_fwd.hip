@@ -97,6 +97,77 @@ __device__ __forceinline__ void load_obs_kblock(const float* orow, int kb, int D
   }
 }
 
+// Q output / argmax / eps-greedy / gather epilogue shared by the fused and the split forward.
+template <int AB>
+__device__ __forceinline__ void q_epilogue(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB]) {
+  const int hh = (threadIdx.x & 63) >> 5;
+  const mm_qfwd_io& io = p.io;
+  if (valid && io.q_out) {
+    float* qrow = io.q_out + (int64_t)e * io.q_se + (int64_t)agent * io.q_sa;
+#pragma unroll
+    for (int ab = 0; ab < AB; ++ab)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int row = ab * 32 + kperm(s, hh);
+        if (row < p.A) qrow[row] = qa[ab][s];
+      }
+  }
+  if (io.mode == MM_Q_NONE) return;
+
+  // ---- epilogue: first-index argmax over A rows spread across the two lane halves
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int ab = 0; ab < AB; ++ab)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int row = ab * 32 + kperm(s, hh);
+      const float v = qa[ab][s];
+      if (row < p.A && (v > best || (v == best && row < bi))) {
+        best = v;
+        bi = row;
+      }
+    }
+  const float ob = __shfl_xor(best, 32);
+  const int oi = __shfl_xor(bi, 32);
+  if (ob > best || (ob == best && oi < bi)) {
+    best = ob;
+    bi = oi;
+  }
+  int act = bi;
+  if (io.mode == MM_Q_ACT) {
+    const float eps = io.eps_ptr ? *io.eps_ptr : io.epsilon;
+    const uint64_t ctr = io.counter_ptr ? *io.counter_ptr : io.counter;
+    float u;
+    if (io.u) {
+      u = valid ? io.u[e] : 1.0f;
+    } else {
+      u = rng_uniform(rng_draw(io.seed, ctr, (uint64_t)e, 0xFFFFFFFFull));
+    }
+    if (u <= eps) {
+      if (io.rand_act) {
+        act = valid ? io.rand_act[(int64_t)e * p.N + agent] : 0;
+      } else {
+        act = (int)(rng_draw(io.seed ^ 0x5bd1e995ull, ctr, (uint64_t)e, (uint64_t)agent) % (uint64_t)p.A);
+      }
+    }
+  } else if (io.mode == MM_Q_GATHER) {
+    act = valid ? io.act_in[(int64_t)e * io.act_se + agent] : 0;
+  }
+  float mine = 0.0f;
+#pragma unroll
+  for (int ab = 0; ab < AB; ++ab)
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      if (ab * 32 + kperm(s, hh) == act) mine = qa[ab][s];
+  const float qsel = (io.mode == MM_Q_MAX) ? best : mine + __shfl_xor(mine, 32);
+  if (valid && hh == 0) {
+    const int64_t o = (int64_t)e * p.N + agent;
+    if (io.act_out && io.mode == MM_Q_ACT) io.act_out[o] = act;
+    if (io.qsel_out) io.qsel_out[o] = qsel;
+  }
+}
+
 // xn: layer-1 k-block 0 of the observation, loaded by the caller (before weight staging).
 template <int F1, int G, int H, int AB>
 __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent, int e,
@@ -242,69 +313,203 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
 #pragma unroll
     for (int kb = 0; kb < HB; ++kb) consume(S::NF2 + S::NFG + ab * HB + kb, h1[kb], qa[ab]);
   }
-  if (valid && io.q_out) {
-    float* qrow = io.q_out + (int64_t)e * io.q_se + (int64_t)agent * io.q_sa;
-#pragma unroll
-    for (int ab = 0; ab < AB; ++ab)
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int row = ab * 32 + kperm(s, hh);
-        if (row < p.A) qrow[row] = qa[ab][s];
-      }
-  }
-  if (io.mode == MM_Q_NONE) return;
+  q_epilogue<AB>(p, agent, e, valid, qa);
+}
 
-  // ---- epilogue: first-index argmax over A rows spread across the two lane halves
-  float best = -INFINITY;
-  int bi = 0x7fffffff;
+// ---------------------------------------------------------------- split forward (training)
+// PRE: layers 1-2 and the GRU input projection for every (row, agent) of a chunk batch; REC: one
+// recurrent step from those projections. Same MFMA accumulation order as the fused body (biases,
+// then W_ih x2, then W_hh h), so PRE + REC reproduce agent_q_fwd_body bit for bit.
+template <int F1, int G, int H, int AB>
+__device__ __forceinline__ void agent_pre_body(const QFwdParams& p, int agent, int e, const float* __restrict__ W,
+                                               const float* orow) {
+  using S = Sched<F1, G, H, AB>;
+  using CG = typename S::CG;
+  constexpr int RB1 = S::RB1, RB2 = S::RB2, HB = S::HB;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const bool valid = e < p.E;
+  const mm_qfwd_io& io = p.io;
+  float fr[16], xk[16];
+  f32x16 x1[RB1];
 #pragma unroll
-  for (int ab = 0; ab < AB; ++ab)
+  for (int rb = 0; rb < RB1; ++rb) x1[rb] = load_bias(W + CG::off_b1 + rb * 32, hh);
+  for (int kb = 0; kb < p.g.KD; ++kb) {
+    load_obs_kblock(orow, kb, p.D, xk);
+#pragma unroll
+    for (int rb = 0; rb < RB1; ++rb) {
+      load_frag(W + CG::off_l1 + (int64_t)(rb * p.g.KD + kb) * 1024, lane, fr);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) x1[rb] = mfma32(fr[s], xk[s], x1[rb]);
+    }
+  }
+  float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
+#pragma unroll
+  for (int rb = 0; rb < RB1; ++rb)
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int row = ab * 32 + kperm(s, hh);
-      const float v = qa[ab][s];
-      if (row < p.A && (v > best || (v == best && row < bi))) {
-        best = v;
-        bi = row;
+      x1[rb][s] = fmaxf(x1[rb][s], 0.0f);
+      if (sv) sv[rb * 32 + kperm(s, hh)] = x1[rb][s];
+    }
+  f32x16 x2[RB2];
+#pragma unroll
+  for (int rb = 0; rb < RB2; ++rb) {
+    x2[rb] = load_bias(W + CG::off_b2 + rb * 32, hh);
+#pragma unroll
+    for (int kb = 0; kb < RB1; ++kb) {
+      load_frag(W + S::off(rb * RB1 + kb), lane, fr);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) x2[rb] = mfma32(fr[s], x1[kb][s], x2[rb]);
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      x2[rb][s] = fmaxf(x2[rb][s], 0.0f);
+      if (sv) sv[F1 + rb * 32 + kperm(s, hh)] = x2[rb][s];
+    }
+  }
+  float* gi = valid ? io.gi + ((int64_t)e * p.N + agent) * 3 * H : nullptr;
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb) {
+#pragma unroll
+    for (int gte = 0; gte < 3; ++gte) {
+      f32x16 acc = gte < 2 ? load_bias(W + CG::off_brz + (gte * HB + hb) * 32, hh)
+                           : load_bias(W + CG::off_bin + hb * 32, hh);
+#pragma unroll
+      for (int kb = 0; kb < RB2; ++kb) {
+        load_frag(W + S::off(S::NF2 + hb * S::PERHB + gte * RB2 + kb), lane, fr);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = mfma32(fr[s], x2[kb][s], acc);
+      }
+      if (gi) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) gi[gte * H + hb * 32 + kperm(s, hh)] = acc[s];
       }
     }
-  const float ob = __shfl_xor(best, 32);
-  const int oi = __shfl_xor(bi, 32);
-  if (ob > best || (ob == best && oi < bi)) {
-    best = ob;
-    bi = oi;
   }
-  int act = bi;
-  if (io.mode == MM_Q_ACT) {
-    const float eps = io.eps_ptr ? *io.eps_ptr : io.epsilon;
-    const uint64_t ctr = io.counter_ptr ? *io.counter_ptr : io.counter;
-    float u;
-    if (io.u) {
-      u = valid ? io.u[e] : 1.0f;
-    } else {
-      u = rng_uniform(rng_draw(io.seed, ctr, (uint64_t)e, 0xFFFFFFFFull));
+}
+
+// REC for small batches: the HB hidden blocks of one 32-env tile run on HB waves of the block (each
+// loads all its W_hh fragments, gi and h up front: one memory latency per step instead of one per
+// fragment); the Q head + epilogue run on wave 0 after an LDS exchange of the new hidden blocks.
+template <int F1, int G, int H, int AB>
+__device__ __forceinline__ void agent_rec_body(const QFwdParams& p, int agent, int tile, const float* __restrict__ W) {
+  using S = Sched<F1, G, H, AB>;
+  using CG = typename S::CG;
+  constexpr int RB2 = S::RB2, HB = S::HB;
+  __shared__ float hx[HB][16][64];
+  const int lane = threadIdx.x & 63, hh = lane >> 5, hb = threadIdx.x >> 6;
+  const int e = tile * 32 + (lane & 31);
+  const bool valid = e < p.E;
+  const mm_qfwd_io& io = p.io;
+  const bool zero_h = !valid || (io.reset && io.reset[e]);
+  float fz[3][HB][16];
+  const int base = S::NF2 + hb * S::PERHB + 3 * RB2;
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) load_frag(W + S::off(base + g * HB + kb), lane, fz[g][kb]);
+  f32x16 h0[HB];
+#pragma unroll
+  for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int f = kb * 32 + kperm(s, hh);
+      h0[kb][s] = zero_h ? 0.0f
+                         : io.h_in[(int64_t)e * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)f * io.hin_sf];
     }
-    if (u <= eps) {
-      if (io.rand_act) {
-        act = valid ? io.rand_act[(int64_t)e * p.N + agent] : 0;
-      } else {
-        act = (int)(rng_draw(io.seed ^ 0x5bd1e995ull, ctr, (uint64_t)e, (uint64_t)agent) % (uint64_t)p.A);
-      }
-    }
-  } else if (io.mode == MM_Q_GATHER) {
-    act = valid ? io.act_in[(int64_t)e * io.act_se + agent] : 0;
+  const float* gi = io.gi + ((int64_t)(valid ? e : 0) * p.N + agent) * 3 * H;
+  f32x16 ar, az, anx;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int f = hb * 32 + kperm(s, hh);
+    ar[s] = gi[f];
+    az[s] = gi[H + f];
+    anx[s] = gi[2 * H + f];
   }
-  float mine = 0.0f;
+  f32x16 anh = load_bias(W + CG::off_bhn + hb * 32, hh);
 #pragma unroll
-  for (int ab = 0; ab < AB; ++ab)
+  for (int kb = 0; kb < HB; ++kb)
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
-      if (ab * 32 + kperm(s, hh) == act) mine = qa[ab][s];
-  const float qsel = (io.mode == MM_Q_MAX) ? best : mine + __shfl_xor(mine, 32);
-  if (valid && hh == 0) {
-    const int64_t o = (int64_t)e * p.N + agent;
-    if (io.act_out && io.mode == MM_Q_ACT) io.act_out[o] = act;
-    if (io.qsel_out) io.qsel_out[o] = qsel;
+    for (int s = 0; s < 16; ++s) ar = mfma32(fz[0][kb][s], h0[kb][s], ar);
+#pragma unroll
+  for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) az = mfma32(fz[1][kb][s], h0[kb][s], az);
+#pragma unroll
+  for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) anh = mfma32(fz[2][kb][s], h0[kb][s], anh);
+  float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
+  float h1v[16];
+  float h0v[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    // h0 of this wave's hidden block (compile-time register selection)
+    float v = h0[0][s];
+#pragma unroll
+    for (int kb = 1; kb < HB; ++kb)
+      if (kb == hb) v = h0[kb][s];
+    h0v[s] = v;
+  }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const float r = sigmoidf_(ar[s]);
+    const float z = sigmoidf_(az[s]);
+    const float n = tanhf_(anx[s] + r * anh[s]);
+    h1v[s] = n + z * (h0v[s] - n);
+    hx[hb][s][lane] = h1v[s];
+    if (sv) {
+      float* o = sv + F1 + G + hb * 32 + kperm(s, hh);
+      o[0] = h0v[s];
+      o[H] = r;
+      o[2 * H] = z;
+      o[3 * H] = n;
+      o[4 * H] = anh[s];
+      o[5 * H] = h1v[s];
+    }
+  }
+  if (valid && io.h_out) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int f = hb * 32 + kperm(s, hh);
+      io.h_out[(int64_t)e * io.hout_se + (int64_t)agent * io.hout_sa + (int64_t)f * io.hout_sf] = h1v[s];
+    }
+  }
+  __syncthreads();
+  if (hb != 0) return;
+  f32x16 h1[HB];
+#pragma unroll
+  for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) h1[kb][s] = hx[kb][s][lane];
+  f32x16 qa[AB];
+  float fr[16];
+#pragma unroll
+  for (int ab = 0; ab < AB; ++ab) {
+    qa[ab] = load_bias(W + CG::off_bq + ab * 32, hh);
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) {
+      load_frag(W + S::off(S::NF2 + S::NFG + ab * HB + kb), lane, fr);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) qa[ab] = mfma32(fr[s], h1[kb][s], qa[ab]);
+    }
+  }
+  q_epilogue<AB>(p, agent, e, valid, qa);
+}
+
+// PHASE 1 = PRE: 128 rows of one agent per block (4 waves x 32). PHASE 2 = REC: one 32-env tile of
+// one agent per block (H/32 waves). Block b serves agent b % N.
+template <int F1, int G, int H, int AB, int PHASE>
+__global__ __launch_bounds__(256, 2) void agent_split_kernel(QFwdParams p0, QFwdParams p1) {
+  const bool second = (int)blockIdx.x >= p0.nblocks;
+  const QFwdParams& p = second ? p1 : p0;
+  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
+  const int agent = bid % p.N, tile = bid / p.N;
+  const float* W = p.packed + (int64_t)agent * p.g.agent_stride;
+  if constexpr (PHASE == 1) {
+    const int e = tile * 128 + (threadIdx.x >> 6) * 32 + (threadIdx.x & 31);
+    agent_pre_body<F1, G, H, AB>(p, agent, e, W, obs_row_ptr(p, agent, e));
+  } else {
+    agent_rec_body<F1, G, H, AB>(p, agent, tile, W);
   }
 }
 
@@ -478,6 +683,48 @@ static int dispatch(const mm_qnet_dims* d, const QFwdParams& p0, const QFwdParam
   if (d->f1 == 64 && d->g == 32 && d->h == 64) return AB == 1 ? launch_fwd<64, 32, 64, 1>(p0, p1, s) : launch_fwd<64, 32, 64, 2>(p0, p1, s);
   set_error("agent_q_fwd: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
   return MM_EINVAL;
+}
+
+template <int F1, int G, int H, int AB>
+static int launch_split(int phase, QFwdParams p0, QFwdParams p1, hipStream_t s) {
+  if (phase == 1) {
+    const int nb = p0.nblocks + p1.nblocks;
+    hipLaunchKernelGGL((agent_split_kernel<F1, G, H, AB, 1>), dim3(nb), dim3(256), 0, s, p0, p1);
+  } else {
+    p0.nblocks = (p0.E + 31) / 32 * p0.N;
+    p1.nblocks = (p1.E + 31) / 32 * p1.N;
+    const int nb = p0.nblocks + p1.nblocks;
+    hipLaunchKernelGGL((agent_split_kernel<F1, G, H, AB, 2>), dim3(nb), dim3(64 * (H / 32)), 0, s, p0, p1);
+  }
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+static int dispatch_split(const mm_qnet_dims* d, int phase, const QFwdParams& p0, const QFwdParams& p1,
+                          hipStream_t s) {
+  const int AB = (d->n_actions + 31) / 32;
+#define MM_SPLIT(F1_, G_, H_)                                                                               \
+  if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                             \
+    return AB == 1 ? launch_split<F1_, G_, H_, 1>(phase, p0, p1, s) : launch_split<F1_, G_, H_, 2>(phase, p0, p1, s);
+  MM_SPLIT(64, 32, 32)
+  MM_SPLIT(64, 64, 64)
+  MM_SPLIT(128, 32, 32)
+  MM_SPLIT(64, 32, 64)
+#undef MM_SPLIT
+  set_error("agent_q_split: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
+  return MM_EINVAL;
+}
+
+int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
+                   const float* packed1, const mm_qfwd_io* io1, int64_t e1, hipStream_t s) {
+  QFwdParams p0, p1;
+  int rc = make_params(d, packed0, io0, e0, &p0);
+  if (rc) return rc;
+  rc = make_params(d, packed1, io1, e1, &p1);
+  if (rc) return rc;
+  MM_REQUIRE(io0->gi && io1->gi, "agent_q_split: io.gi required");
+  MM_REQUIRE(phase == 2 || (io0->obs && io1->obs), "agent_q_pre: obs required");
+  return dispatch_split(d, phase, p0, p1, s);
 }
 
 int agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs, hipStream_t s) {

@@ -40,6 +40,7 @@ class QFwdIO(ctypes.Structure):
         ("qsel_out", c_vp),
         ("eps_ptr", c_vp), ("counter_ptr", c_vp),
         ("save", c_vp),
+        ("gi", c_vp),
     ]
 
 
@@ -157,6 +158,10 @@ _SIGS += [
     ("mm_agent_bwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp, c_vp, c_vp, c_vp]),
     ("mm_outer_reduce", c_i32, [ctypes.POINTER(OuterArgs), c_vp]),
+    ("mm_agent_q_pre2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
+                                ctypes.POINTER(QFwdIO), c_i64, c_vp]),
+    ("mm_agent_q_rec2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
+                                ctypes.POINTER(QFwdIO), c_i64, c_vp]),
     ("mm_outer_reduce_batch_partial", c_i64, [ctypes.POINTER(OuterArgs), c_i32]),
     ("mm_outer_reduce_batch", c_i32, [ctypes.POINTER(OuterArgs), c_i32, c_vp, c_i64, c_vp]),
     ("mm_tmv", c_i32, [ctypes.POINTER(TmvArgs), c_vp]),

@@ -138,6 +138,8 @@ class QLearner:
         self.hb = torch.zeros(2, B, N, H, **f32)
         self.ht = torch.zeros(2, B, N, H, **f32)
         self.asave = torch.zeros(C, B, N, self.SD, **f32)
+        self.gi_ab = torch.zeros(C, B, N, 3 * H, **f32)   # agent GRU input projections (split forward)
+        self.gi_at = torch.zeros(C, B, N, 3 * H, **f32)
         self.qa = torch.zeros(C, B, N, **f32)
         self.maxq = torch.zeros(C, B, N, **f32)
         self.qtot = torch.zeros(C, B, **f32)
@@ -221,27 +223,38 @@ class QLearner:
             mx = self.mix
             check(L.mm_mixer_gi(CB, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, ptr(mx.flat), ptr(self.s_off),
                                 ptr(self.gi_b), ptr(self.tmix.flat), ptr(self.s2_off), ptr(self.gi_t), s), "mixer gi")
-        # ---- forward over the chunk (behavior GATHER + save, target MAX) in dual launches
+        # ---- forward over the chunk: the non-recurrent part (layers 1-2, W_ih x2) of every (t, b) of
+        # both nets in ONE launch, then one recurrent step (W_hh h, gates, Q head) per t
+        pb, pt = QFwdIO(), QFwdIO()
+        for io, off, gi in ((pb, self.s_off, self.gi_ab), (pt, self.s2_off, self.gi_at)):
+            io.obs, io.obs_se, io.obs_sa, io.obs_off = obs_p.value, 1, D, 0
+            io.obs_row = off.data_ptr()
+            io.reset_obs = reset_p.value
+            io.h_in = self.hb.data_ptr()       # unused by PRE
+            io.gi = gi.data_ptr()
+        pb.save = self.asave.data_ptr()
+        check(L.mm_agent_q_pre2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pb), CB,
+                                ptr(self.tgt.packed), ctypes.byref(pt), CB, s), "learner fwd pre")
+        gstep = 4 * B * N * 3 * H
         for t in range(C):
             ib, it = QFwdIO(), QFwdIO()
-            for io, off, h in ((ib, self.s_off, self.hb), (it, self.s2_off, self.ht)):
-                io.obs, io.obs_se, io.obs_sa, io.obs_off = obs_p.value, 1, D, 0
-                io.obs_row = off.data_ptr() + 8 * t * B
-                io.reset_obs = reset_p.value
+            for io, h, gi in ((ib, self.hb, self.gi_ab), (it, self.ht, self.gi_at)):
+                io.obs = obs_p.value               # unused by REC
                 io.h_in = h[t % 2].data_ptr()
                 io.h_out = h[(t + 1) % 2].data_ptr()
                 io.hin_se = io.hout_se = N * H
                 io.hin_sa = io.hout_sa = H
                 io.hin_sf = io.hout_sf = 1
                 io.reset = self.ones8.data_ptr() if t == 0 else self.done8.data_ptr() + (t - 1) * B
+                io.gi = gi.data_ptr() + t * gstep
             ib.mode = MM_Q_GATHER
             ib.act_in, ib.act_se = self.acts.data_ptr() + 4 * t * B * N, N
             ib.qsel_out = self.qa[t].data_ptr()
             ib.save = self.asave[t].data_ptr()
             it.mode = MM_Q_MAX
             it.qsel_out = self.maxq[t].data_ptr()
-            check(L.mm_agent_q_fwd2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
-                                    ptr(self.tgt.packed), ctypes.byref(it), B, s), "learner fwd")
+            check(L.mm_agent_q_rec2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
+                                    ptr(self.tgt.packed), ctypes.byref(it), B, s), "learner fwd rec")
             if self.mode == "qmix":
                 mx = self.mix
                 nets = (MixNetIO * 2)()
