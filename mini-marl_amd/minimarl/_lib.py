@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libminimarl.so")
+LIB_PATH = os.environ.get("MM_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libminimarl.so")  # A/B runs
 
 c_i32 = ctypes.c_int32
 c_i64 = ctypes.c_int64
