@@ -125,6 +125,41 @@ def test_learner_gru64_vs_oracle():
         _check_grads(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy(), grads["m." + key].numpy())
 
 
+def test_learner_cfg5_shapes_vs_oracle():
+    """cfg5 SMAC-scale shapes (27 agents, obs 300, 36 actions, GRU-32 agents, Hm=32 mixer over an
+    8100-wide state) through the whole QMIX update vs the torch-CPU oracle."""
+    from minimarl.learner import MIX_KEYS, Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    N, D, A, B, C = 27, 300, 36, 32, 3
+    beh = AgentQNet(N, D, A, 64, 32, 32, DEV, seed=5)
+    tgt = AgentQNet(N, D, A, 64, 32, 32, DEV, seed=6)
+    mix = Mixer(N, N * D, 32, 32, DEV, seed=7)
+    tmix = Mixer(N, N * D, 32, 32, DEV, seed=8)
+    P0 = {k: v.detach().cpu().clone() for k, v in beh.params().items()}
+    T0 = {k: v.detach().cpu().clone() for k, v in tgt.params().items()}
+    M0 = {k: mix.view(k).detach().cpu().clone() for k in MIX_KEYS}
+    TM0 = {k: tmix.view(k).detach().cpu().clone() for k in MIX_KEYS}
+    L = QLearner(beh, tgt, mix, tmix, batch=B, chunk=C, mode="qmix", device=DEV)
+    g = torch.Generator().manual_seed(1)
+    st = (torch.rand(B, C, N, D, generator=g) < 0.2).float()
+    ns = (torch.rand(B, C, N, D, generator=g) < 0.2).float()
+    act = torch.randint(0, A, (B, C, N), generator=g).float()
+    rew = torch.randn(B, C, N, generator=g) * 0.5
+    dn = (torch.rand(B, C, 1, generator=g) < 0.2).float()
+    w = torch.rand(B, 1, generator=g) * 0.5 + 0.5
+    L.load_batch(st, act, rew, ns, dn, w)
+    L.train_step(L._obs_buf, L._obs_buf)
+    torch.cuda.synchronize()
+    newP, newM, grads, loss, td = nets.qmix_train_step(P0, M0, T0, TM0, (st, act, rew, ns, dn, w), 0.99, 1e-3, 5.0)
+    np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=1e-4)
+    np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=1e-4, atol=1e-4)
+    coef = min(1.0, 5.0 / (float(L.norm.item()) + 1e-6))
+    for key in nets.AGENT_KEYS:
+        _check_grads(_grad_view(L, key).cpu().numpy() * coef, grads[key].numpy())
+    for key in MIX_KEYS:
+        _check_grads(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy(), grads["m." + key].numpy())
+
+
 def test_learner_update_from_device_per():
     """sample -> gather -> train -> priority update through the engine's PER and chunk store."""
     from minimarl.engine import RolloutEngine

@@ -54,7 +54,9 @@ def test_sample_action_golden_same_seed(golden, tag):
 
 @pytest.mark.parametrize("f1,g,h,n,d,a,e", [(64, 64, 64, 8, 47, 5, 1000), (64, 32, 32, 8, 47, 5, 257),
                                             (64, 64, 64, 8, 47, 5, 2304), (64, 32, 32, 2, 94, 5, 4096),
-                                            (128, 32, 32, 2, 94, 5, 130), (64, 32, 32, 4, 300, 36, 96)])
+                                            (128, 32, 32, 2, 94, 5, 130), (64, 32, 32, 4, 300, 36, 96),
+                                            # cfg5 SMAC-scale agent net (N=27, D=300, A=36) on the LDS path
+                                            (64, 32, 32, 27, 300, 36, 2048)])
 def test_qnet_forward_vs_oracle_shapes(f1, g, h, n, d, a, e):
     from minimarl.qnet import AgentQNet
     net = AgentQNet(n, d, a, f1, g, h, DEV, seed=3)
