@@ -67,14 +67,32 @@ __device__ void block_matvec(const float* __restrict__ W, const float* __restric
   }
 }
 
-// out[c] (+)= sum_r W[r*K + c] * d[r]   for c < K (transpose matvec, coalesced over c)
+// out[c] (+)= sum_r W[r*K + c] * d[r]   for c < K (transpose matvec, coalesced over c). The rows are
+// split over the block's waves (wave w takes r = w mod nw, unrolled by 4 so loads overlap) and the
+// per-wave partials are combined in a fixed order through LDS (red: >= nw*K floats of scratch).
+// Ends with __syncthreads.
 __device__ void block_matvec_t(const float* __restrict__ W, int rows, int K, const float* d, float* out,
-                               bool accumulate) {
+                               bool accumulate, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int c = lane; c < K; c += 64) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = w;
+    for (; r + 3 * nw < rows; r += 4 * nw) {
+      a0 += W[(int64_t)r * K + c] * d[r];
+      a1 += W[(int64_t)(r + nw) * K + c] * d[r + nw];
+      a2 += W[(int64_t)(r + 2 * nw) * K + c] * d[r + 2 * nw];
+      a3 += W[(int64_t)(r + 3 * nw) * K + c] * d[r + 3 * nw];
+    }
+    for (; r < rows; r += nw) a0 += W[(int64_t)r * K + c] * d[r];
+    red[w * K + c] = (a0 + a1) + (a2 + a3);
+  }
+  __syncthreads();
   for (int c = threadIdx.x; c < K; c += blockDim.x) {
     float acc = 0.f;
-    for (int r = 0; r < rows; ++r) acc += W[(int64_t)r * K + c] * d[r];
+    for (int q = 0; q < nw; ++q) acc += red[q * K + c];
     out[c] = accumulate ? out[c] + acc : acc;
   }
+  __syncthreads();
 }
 
 // ------------------------------------------------------------------ mixer
@@ -341,6 +359,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixBwdArgs a) {
   float* dhm1 = sm;                  // [Hm]
   float* dgh = dhm1 + Hm;            // [3Hm]
   float* shd = dgh + 3 * Hm;         // [N*K1 + 3*K1] local copy of the hypernet deltas
+  float* red = shd + N * K1 + 3 * K1;  // [4*Hm] wave partials of the transposed mat-vecs
   const float dQ = a.dq[b];
   // hypernet / mixing deltas
   for (int k = threadIdx.x; k < K1; k += blockDim.x) {
@@ -374,14 +393,10 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixBwdArgs a) {
   const bool drop = a.done[b] > 0.5f;
   for (int c = threadIdx.x; c < Hm; c += blockDim.x) dhm1[c] = drop ? 0.f : a.dhm[(int64_t)b * Hm + c];
   __syncthreads();
-  block_matvec_t(a.P + o.w1W, N * K1, Hm, shd, dhm1, true);
-  __syncthreads();
-  block_matvec_t(a.P + o.b1W, K1, Hm, shd + N * K1, dhm1, true);
-  __syncthreads();
-  block_matvec_t(a.P + o.w2W, K1, Hm, shd + N * K1 + K1, dhm1, true);
-  __syncthreads();
-  block_matvec_t(a.P + o.b2aW, K1, Hm, shd + N * K1 + 2 * K1, dhm1, true);
-  __syncthreads();
+  block_matvec_t(a.P + o.w1W, N * K1, Hm, shd, dhm1, true, red);
+  block_matvec_t(a.P + o.b1W, K1, Hm, shd + N * K1, dhm1, true, red);
+  block_matvec_t(a.P + o.w2W, K1, Hm, shd + N * K1 + K1, dhm1, true, red);
+  block_matvec_t(a.P + o.b2aW, K1, Hm, shd + N * K1 + 2 * K1, dhm1, true, red);
   // GRU backward (h' = n + z (h - n))
   for (int i = threadIdx.x; i < Hm; i += blockDim.x) {
     const float dh = dhm1[i];
@@ -403,11 +418,11 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixBwdArgs a) {
     dgh[2 * Hm + i] = dpn * r;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < Hm; c += blockDim.x) {
-    float acc = dhm1[c] * zg[c];
-    for (int r = 0; r < 3 * Hm; ++r) acc += a.P[o.gWhh + (int64_t)r * Hm + c] * dgh[r];
-    a.dhm[(int64_t)b * Hm + c] = acc;
-  }
+  // dhm0 = z * dhm1 + W_hh^T dgh
+  for (int c = threadIdx.x; c < Hm; c += blockDim.x) shd[c] = dhm1[c] * zg[c];
+  __syncthreads();
+  block_matvec_t(a.P + o.gWhh, 3 * Hm, Hm, dgh, shd, true, red);
+  for (int c = threadIdx.x; c < Hm; c += blockDim.x) a.dhm[(int64_t)b * Hm + c] = shd[c];
 }
 
 // ------------------------------------------------------------------ agent backward chain (one step)
@@ -823,7 +838,7 @@ int mm_mixer_bwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const 
                  const float* qa, const float* dq, const float* done, float* dhm, float* dqa, float* delta,
                  mm_stream_t s) {
   mm::MixBwdArgs a = {P, save, qa, dq, done, dhm, dqa, delta, B, N, S, Hm, K1};
-  const size_t sm = sizeof(float) * ((size_t)4 * Hm + N * K1 + 3 * K1);
+  const size_t sm = sizeof(float) * ((size_t)8 * Hm + N * K1 + 3 * K1);
   hipLaunchKernelGGL(mm::mixer_bwd_kernel, dim3(B), dim3(256), sm, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
