@@ -165,6 +165,16 @@ double mm_per_beta(const mm_per* per);
 int mm_env_step_rows(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
                      float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s);
 const float* mm_env_reset_obs(const mm_env* env); /* device [N, D]: the (deterministic) reset obs */
+/* mm_env_step_rows (auto-reset via cur_row, no obs_cur) fused with mm_td_chunk_step_rows of the
+ * PREVIOUS step (td_* inputs, slot step_in_chunk of store rows td_rows): one launch instead of two
+ * for every in-chunk step of the rollout engine (cal_td_error + chunk lists, vdn/_utils.py:44-52,
+ * vdn/main.py:140-167). Identical results to the two separate calls. */
+int mm_env_step_rows_td(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
+                        int64_t* cur_row, float* rew, uint8_t* done, float gamma, const float* td_rew,
+                        const uint8_t* td_done, const float* q_taken, const float* max_q_next, const int32_t* td_act,
+                        float* chunk_td, int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act,
+                        float* store_rew, uint8_t* store_done, const int64_t* td_rows, uint64_t* counter,
+                        mm_stream_t s);
 /* TD step writing into store rows rows[e]; increments the device RNG step counter (may be NULL). */
 int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                           const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,

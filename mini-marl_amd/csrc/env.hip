@@ -101,61 +101,116 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvDev d, float* obs, in
   }
 }
 
-__global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* __restrict__ act,
-                                                       float* __restrict__ next_obs, int64_t next_se,
-                                                       const int64_t* __restrict__ next_row,
-                                                       float* __restrict__ obs_cur, int64_t* __restrict__ cur_row,
-                                                       float* __restrict__ rew, uint8_t* __restrict__ done_out) {
+// Fused TD/store of the PREVIOUS rollout step (td_chunk_kernel's work, rollout.hip) done by the
+// env kernel of the next step: its inputs (rew, done, Q(a), max Q') are final once the dual forward
+// of that step has run, and the env kernel of step t+1 is the next launch on the stream. Saves one
+// launch per in-chunk step. Same arithmetic and agent-order sums as td_chunk_kernel.
+struct TdFuse {
+  const float* rew;       // [E][N] rewards of the previous step (overwritten by this step later)
+  const uint8_t* done;    // [E]
+  const float* q_taken;   // [E][N]
+  const float* maxq;      // [E][N]
+  const int32_t* act;     // [E][N]
+  float* chunk_td;        // [E]
+  uint8_t* s_act;         // store [rows][C][N]
+  float* s_rew;           // store [rows][C][N]
+  uint8_t* s_done;        // store [rows][C]
+  const int64_t* rows;    // [E] store rows of the previous step
+  uint64_t* counter;      // RNG step counter (may be null)
+  float gamma;
+  int slot, C, on;
+};
+
+// One wave per block, EPW = 64 / N envs per wave (lane = env-slot * N + agent). Phase 0 issues
+// every global read of the step at once (positions, actions, grid words, counters, destination
+// rows, the fused TD inputs); phase 1 runs the sequential-in-agent-order dynamics, one lane per
+// env with positions in registers; phase 2 builds the occupancy map, then every (env, agent)
+// lane writes its 47 local features into an LDS tile; phase 3 streams the tile out as 16-byte
+// stores (one contiguous N*D run per env, coalesced across the wave) and writes the state back.
+static constexpr int WT = 64;
+
+__global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32_t* __restrict__ act,
+                                                           float* __restrict__ next_obs, int64_t next_se,
+                                                           const int64_t* __restrict__ next_row,
+                                                           float* __restrict__ obs_cur,
+                                                           int64_t* __restrict__ cur_row, float* rew,  // rew may alias tdf.rew
+                                                           uint8_t* __restrict__ done_out, TdFuse tdf) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int RC = d.R * d.C;
   const int N = d.N;
-  const int EB = d.eb;
+  const int EPW = WT / N;
+  const int lane = threadIdx.x;
   const bool autoreset = obs_cur || cur_row;
   const int ND = N * d.D;
-  int64_t* srow = reinterpret_cast<int64_t*>(smem);                       // [EB] destination rows
-  float* sreset = reinterpret_cast<float*>(srow + EB);                    // [N*D] reset obs table
-  int32_t* spos = reinterpret_cast<int32_t*>(sreset + ND);                // [EB][N]
-  int32_t* sact = spos + EB * N;                                          // [EB][N]
-  int32_t* sapl = sact + EB * N;                                          // [EB] apples
-  int32_t* sstp = sapl + EB;                                              // [EB] steps
-  int32_t* sipos = sstp + EB;                                             // [N] initial positions
-  uint8_t* sdone = reinterpret_cast<uint8_t*>(sipos + N);                 // [EB]
-  int8_t* sgrid = reinterpret_cast<int8_t*>(sdone + EB);                  // [EB][RC]
-  uint8_t* socc = reinterpret_cast<uint8_t*>(sgrid + EB * RC);            // [EB][RC] agent id + 1
-  int8_t* sigrid = reinterpret_cast<int8_t*>(socc + EB * RC);             // [RC] initial grid
-  const int e0 = blockIdx.x * EB;
-  const int ne = min(EB, d.E - e0);
+  const int LD = N * OBS_LOCAL;                                              // local tile per env
+  float* sloc = reinterpret_cast<float*>(smem);                              // [EPW][N][47]
+  int64_t* srow = reinterpret_cast<int64_t*>(sloc + EPW * LD);               // [EPW]
+  float* std3 = reinterpret_cast<float*>(srow + EPW);                        // [3][EPW*N] td inputs
+  int32_t* spos = reinterpret_cast<int32_t*>(std3 + 3 * EPW * N);            // [EPW*N]
+  int32_t* sact = spos + EPW * N;                                            // [EPW*N]
+  uint8_t* sdone = reinterpret_cast<uint8_t*>(sact + EPW * N);               // [EPW]
+  int8_t* sgrid = reinterpret_cast<int8_t*>(sdone + ((EPW + 15) & ~15));     // [EPW][RC]
+  uint8_t* socc = reinterpret_cast<uint8_t*>(sgrid + ((EPW * RC + 15) & ~15));  // [EPW][RC]
+  const int e0 = blockIdx.x * EPW;
+  const int ne = min(EPW, d.E - e0);
+  const int nl = ne * N;                   // active (env, agent) lanes
+  const int le_l = lane / N, k_l = lane % N;
+  const int e_l = e0 + le_l;
 
-  // phase 0: every global read of the step in one round trip (grids, positions, actions, counters,
-  // reset tables); the later phases only touch LDS and issue stores
-  for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) {
-    sgrid[i] = d.grid[(int64_t)e0 * RC + i];
-    socc[i] = 0;
+  // ---- phase 0: all global reads
+  if (lane < nl) {
+    const int64_t o = (int64_t)e0 * N + lane;
+    spos[lane] = d.pos[o];
+    sact[lane] = act[o];
+    if (tdf.on) {
+      std3[lane] = tdf.rew[o];
+      std3[EPW * N + lane] = tdf.q_taken[o];
+      std3[2 * EPW * N + lane] = tdf.maxq[o];
+      const int64_t row = tdf.rows[e_l];
+      tdf.s_act[(row * tdf.C + tdf.slot) * N + k_l] = (uint8_t)tdf.act[o];
+      tdf.s_rew[(row * tdf.C + tdf.slot) * N + k_l] = std3[lane];
+    }
   }
-  for (int i = threadIdx.x; i < ne * N; i += blockDim.x) {
-    spos[i] = d.pos[(int64_t)e0 * N + i];
-    sact[i] = act[(int64_t)e0 * N + i];
+  if ((RC & 3) == 0) {
+    const int nw = ne * RC / 4;
+    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(d.grid + (int64_t)e0 * RC);
+    for (int i = lane; i < nw; i += WT) reinterpret_cast<uint32_t*>(sgrid)[i] = g32[i];
+  } else {
+    for (int i = lane; i < ne * RC; i += WT) sgrid[i] = d.grid[(int64_t)e0 * RC + i];
   }
-  for (int i = threadIdx.x; i < ne; i += blockDim.x) {
-    srow[i] = next_row ? next_row[e0 + i] : (int64_t)(e0 + i);
-    sapl[i] = d.apples[e0 + i];
-    sstp[i] = d.steps[e0 + i];
-  }
-  if (autoreset) {
-    for (int i = threadIdx.x; i < ND; i += blockDim.x) sreset[i] = d.reset_obs[i];
-    for (int i = threadIdx.x; i < RC; i += blockDim.x) sigrid[i] = d.init_grid[i];
-    for (int i = threadIdx.x; i < N; i += blockDim.x) sipos[i] = d.init_pos[i];
+  for (int i = lane; i < ne * RC; i += WT) socc[i] = 0;
+  int apples0 = 0, steps0 = 0;
+  if (lane < ne) {
+    srow[lane] = next_row ? next_row[e0 + lane] : (int64_t)(e0 + lane);
+    apples0 = d.apples[e0 + lane];
+    steps0 = d.steps[e0 + lane];
   }
   __syncthreads();
 
-  // phase 1: dynamics, one thread per env, agents in id order (oracle/env.py VecEnvOracle.step).
-  // Positions live in registers (N <= 16; fully unrolled collision checks), so the only LDS
-  // round trips on the sequential chain are the grid cell reads.
-  if (threadIdx.x < ne) {
-    const int le = threadIdx.x, e = e0 + le;
+  // fused TD of the previous step: agent-order sums per env (one lane per env)
+  if (tdf.on && lane < ne) {
+    const int e = e0 + lane;
+    float sr = 0.f, sq = 0.f, st = 0.f;
+    for (int j = 0; j < N; ++j) {
+      sr += std3[lane * N + j];
+      sq += std3[EPW * N + lane * N + j];
+      st += std3[2 * EPW * N + lane * N + j];
+    }
+    const uint8_t dn8 = tdf.done[e];
+    const float dn = dn8 ? 1.0f : 0.0f;
+    const float td = fabsf(sr + (1.0f - dn) * tdf.gamma * st - sq);
+    tdf.chunk_td[e] = (tdf.slot == 0 ? 0.0f : tdf.chunk_td[e]) + td;
+    const int64_t row = tdf.rows[e];
+    tdf.s_done[row * tdf.C + tdf.slot] = dn8;
+    if (tdf.counter && blockIdx.x == 0 && lane == 0) *tdf.counter += 1;
+  }
+
+  // ---- phase 1: dynamics, one lane per env, agents in id order (oracle/env.py VecEnvOracle.step).
+  if (lane < ne) {
+    const int le = lane, e = e0 + lane;
     int8_t* g = sgrid + le * RC;
-    int apples = sapl[le];
-    const int steps = sstp[le] + 1;
+    int apples = apples0;
+    const int steps = steps0 + 1;
     if (N <= 16) {
       int p[16], a[16];
 #pragma unroll
@@ -217,64 +272,101 @@ __global__ __launch_bounds__(256) void env_step_kernel(EnvDev d, const int32_t* 
     d.apples[e] = dn && autoreset ? d.init_apples : apples;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < ne * N; i += blockDim.x) {
-    const int le = i / N, p = spos[i];
-    socc[le * RC + (p >> 8) * d.C + (p & 255)] = (uint8_t)(i % N + 1);
+  int mypos = 0;
+  if (lane < nl) {
+    mypos = spos[lane];
+    socc[le_l * RC + (mypos >> 8) * d.C + (mypos & 255)] = (uint8_t)(k_l + 1);
   }
   __syncthreads();
 
-  // phase 2: obs. Each thread owns fixed positions r of an env's [N][D] block (decoded once) and
-  // walks the block's envs: a wave stores 64 consecutive floats of one env per instruction.
-  for (int r = threadIdx.x; r < ND; r += blockDim.x) {
-    const int k = r / d.D, f = r % d.D;
-    const int src = d.full_obs ? f / OBS_LOCAL : k;
-    const int lf = d.full_obs ? f % OBS_LOCAL : f;
-    const int cellid = lf >= 2 ? (lf - 2) / 5 : 0, ch = lf >= 2 ? (lf - 2) % 5 : 0;
-    const int dr = cellid / 3 - 1, dc = cellid % 3 - 1;
-    const float rs = obs_cur ? sreset[r] : 0.0f;
-    for (int le = 0; le < ne; ++le) {
-      const int p = spos[le * N + src];
-      const int pr = p >> 8, pc = p & 255;
-      float v;
-      if (lf == 0) {
-        v = (float)pr * d.inv_r;
-      } else if (lf == 1) {
-        v = (float)pc * d.inv_c;
-      } else {
-        const int rr = pr + dr, cc = pc + dc;
-        const bool inside = rr >= 0 && rr < d.R && cc >= 0 && cc < d.C;
-        if (!inside) {
-          v = ch == 4 ? 1.0f : 0.0f;
-        } else {
-          const int cell = rr * d.C + cc;
-          const int item = sgrid[le * RC + cell];
-          const int occ = socc[le * RC + cell];
-          v = (ch == 0) ? (item == 1 ? 1.0f : 0.0f)
-            : (ch == 1) ? (item == 2 ? 1.0f : 0.0f)
-            : (ch == 4) ? 0.0f
-            : ((item == 0 && occ != 0 && ((occ - 1) & 1) == ch - 2) ? 1.0f : 0.0f);
-        }
+  // ---- phase 2: local obs of (env le_l, agent k_l) into the LDS tile
+  if (lane < nl) {
+    float* o = sloc + le_l * LD + k_l * OBS_LOCAL;
+    const int pr = mypos >> 8, pc = mypos & 255;
+    o[0] = (float)pr * d.inv_r;
+    o[1] = (float)pc * d.inv_c;
+    const int8_t* g = sgrid + le_l * RC;
+    const uint8_t* oc = socc + le_l * RC;
+#pragma unroll
+    for (int cell = 0; cell < 9; ++cell) {
+      const int rr = pr + cell / 3 - 1, cc = pc + cell % 3 - 1;
+      const bool inside = rr >= 0 && rr < d.R && cc >= 0 && cc < d.C;
+      float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f, v4 = 1.f;
+      if (inside) {
+        const int ci = rr * d.C + cc;
+        const int item = g[ci];
+        const int occ = oc[ci];
+        v0 = item == 1 ? 1.f : 0.f;
+        v1 = item == 2 ? 1.f : 0.f;
+        const bool ag = item == 0 && occ != 0;
+        v2 = (ag && ((occ - 1) & 1) == 0) ? 1.f : 0.f;
+        v3 = (ag && ((occ - 1) & 1) == 1) ? 1.f : 0.f;
+        v4 = 0.f;
       }
-      if (next_obs) next_obs[srow[le] * next_se + r] = v;
-      if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? rs : v;
+      float* q = o + 2 + 5 * cell;
+      q[0] = v0;
+      q[1] = v1;
+      q[2] = v2;
+      q[3] = v3;
+      q[4] = v4;
     }
   }
+  __syncthreads();
 
-  // phase 3: state write-back (initial state for auto-reset envs)
-  for (int i = threadIdx.x; i < ne * RC; i += blockDim.x) {
-    const int le = i / RC;
-    d.grid[(int64_t)e0 * RC + i] = (autoreset && sdone[le]) ? sigrid[i % RC] : sgrid[i];
+  // ---- phase 3: stream the obs out (env le's N*D run from its local tile) and write state back
+  const bool full = d.full_obs != 0;
+  const float* robs = d.reset_obs;
+  const bool vec = (ND & 3) == 0 && (next_se & 3) == 0 && ((uintptr_t)next_obs & 15) == 0 &&
+                   ((uintptr_t)obs_cur & 15) == 0;
+  if (vec) {
+    const int ND4 = ND >> 2;
+    for (int i = lane; i < ne * ND4; i += WT) {
+      const int le = i / ND4, r = (i - le * ND4) * 4;
+      const float* t = sloc + le * LD;
+      float4 v;
+      if (!full) {
+        v = *reinterpret_cast<const float4*>(t + r);
+      } else {
+        v.x = t[(r + 0) % LD];  // full obs: every agent sees the whole [N][47] tile
+        v.y = t[(r + 1) % LD];
+        v.z = t[(r + 2) % LD];
+        v.w = t[(r + 3) % LD];
+      }
+      if (next_obs) *reinterpret_cast<float4*>(next_obs + srow[le] * next_se + r) = v;
+      if (obs_cur) {
+        if (sdone[le]) v = *reinterpret_cast<const float4*>(robs + r);
+        *reinterpret_cast<float4*>(obs_cur + (int64_t)(e0 + le) * ND + r) = v;
+      }
+    }
+  } else {
+    for (int i = lane; i < ne * ND; i += WT) {
+      const int le = i / ND, r = i - le * ND;
+      const float v = sloc[le * LD + (full ? r % LD : r)];
+      if (next_obs) next_obs[srow[le] * next_se + r] = v;
+      if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? robs[r] : v;
+    }
   }
-  for (int i = threadIdx.x; i < ne * N; i += blockDim.x) {
-    const int le = i / N;
-    d.pos[(int64_t)e0 * N + i] = (autoreset && sdone[le]) ? sipos[i % N] : spos[i];
+  if ((RC & 3) == 0) {
+    uint32_t* g32 = reinterpret_cast<uint32_t*>(d.grid + (int64_t)e0 * RC);
+    const uint32_t* ig32 = reinterpret_cast<const uint32_t*>(d.init_grid);
+    const int RC4 = RC >> 2;
+    for (int i = lane; i < ne * RC4; i += WT) {
+      const int le = i / RC4;
+      g32[i] = (autoreset && sdone[le]) ? ig32[i - le * RC4] : reinterpret_cast<const uint32_t*>(sgrid)[i];
+    }
+  } else {
+    for (int i = lane; i < ne * RC; i += WT) {
+      const int le = i / RC;
+      d.grid[(int64_t)e0 * RC + i] = (autoreset && sdone[le]) ? d.init_grid[i % RC] : sgrid[i];
+    }
   }
+  if (lane < nl) d.pos[(int64_t)e0 * N + lane] = (autoreset && sdone[le_l]) ? d.init_pos[k_l] : mypos;
 }
 
 static size_t step_smem(const EnvDev& d) {
-  const size_t EB = d.eb;
-  return EB * 8 + (size_t)d.N * d.D * 4 + 2 * EB * d.N * 4 + 2 * EB * 4 + d.N * 4 + EB + 2 * EB * d.R * d.C +
-         d.R * d.C;
+  const size_t EPW = WT / d.N, RC = (size_t)d.R * d.C;
+  return EPW * d.N * OBS_LOCAL * 4 + EPW * 8 + 3 * EPW * d.N * 4 + 2 * EPW * d.N * 4 + ((EPW + 15) & ~15ull) +
+         ((EPW * RC + 15) & ~15ull) + EPW * RC;
 }
 
 int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out) {
@@ -360,13 +452,16 @@ int env_reset(mm_env* env, float* obs, hipStream_t s) {
 }
 
 int env_step(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
-             float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, hipStream_t s) {
+             float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, const TdFuse* tdf, hipStream_t s) {
   MM_REQUIRE(env && act && rew && done, "env_step: null argument");
   MM_REQUIRE(next_obs || obs_cur, "env_step: no obs output");
   const EnvDev& d = env->d;
-  const int blocks = (d.E + d.eb - 1) / d.eb;
-  hipLaunchKernelGGL(env_step_kernel, dim3(blocks), dim3(256), step_smem(d), s, d, act, next_obs,
-                     next_se > 0 ? next_se : (int64_t)d.N * d.D, next_row, obs_cur, cur_row, rew, done);
+  const int epw = WT / d.N;
+  const int blocks = (d.E + epw - 1) / epw;
+  TdFuse t{};
+  if (tdf) t = *tdf;
+  hipLaunchKernelGGL(env_step_wave_kernel, dim3(blocks), dim3(WT), step_smem(d), s, d, act, next_obs,
+                     next_se > 0 ? next_se : (int64_t)d.N * d.D, next_row, obs_cur, cur_row, rew, done, t);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -394,11 +489,24 @@ int mm_env_grid_shape(const mm_env* env, int32_t* rows, int32_t* cols) {
 int mm_env_reset(mm_env* env, float* obs, mm_stream_t s) { return mm::env_reset(env, obs, (hipStream_t)s); }
 int mm_env_step(mm_env* env, const int32_t* act, float* next_obs, float* obs_cur, float* rew, uint8_t* done,
                 mm_stream_t s) {
-  return mm::env_step(env, act, next_obs, 0, nullptr, obs_cur, nullptr, rew, done, (hipStream_t)s);
+  return mm::env_step(env, act, next_obs, 0, nullptr, obs_cur, nullptr, rew, done, nullptr, (hipStream_t)s);
 }
 int mm_env_step_rows(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
                      float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s) {
-  return mm::env_step(env, act, next_obs, next_se, next_row, obs_cur, cur_row, rew, done, (hipStream_t)s);
+  return mm::env_step(env, act, next_obs, next_se, next_row, obs_cur, cur_row, rew, done, nullptr, (hipStream_t)s);
+}
+int mm_env_step_rows_td(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
+                        int64_t* cur_row, float* rew, uint8_t* done, float gamma, const float* td_rew,
+                        const uint8_t* td_done, const float* q_taken, const float* max_q_next, const int32_t* td_act,
+                        float* chunk_td, int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act,
+                        float* store_rew, uint8_t* store_done, const int64_t* td_rows, uint64_t* counter,
+                        mm_stream_t s) {
+  MM_REQUIRE(td_rew && td_done && q_taken && max_q_next && td_act && chunk_td && store_act && store_rew &&
+                 store_done && td_rows, "env_step_rows_td: null TD argument");
+  MM_REQUIRE(step_in_chunk >= 0 && step_in_chunk < chunk_len, "env_step_rows_td: bad step");
+  mm::TdFuse t{td_rew, td_done, q_taken, max_q_next, td_act, chunk_td, store_act, store_rew, store_done, td_rows,
+               counter, gamma, step_in_chunk, chunk_len, 1};
+  return mm::env_step(env, act, next_obs, next_se, next_row, nullptr, cur_row, rew, done, &t, (hipStream_t)s);
 }
 const float* mm_env_reset_obs(const mm_env* env) { return env ? env->d.reset_obs : nullptr; }
 int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples) {

@@ -66,6 +66,8 @@ _SIGS = [
     ("mm_env_reset", c_i32, [c_vp, c_vp, c_vp]),
     ("mm_env_step", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_step_rows", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_step_rows_td", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_reset_obs", c_vp, [c_vp]),
     ("mm_env_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_grid_shape", c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),

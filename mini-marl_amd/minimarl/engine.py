@@ -10,9 +10,11 @@ qmix/main.py:100-237): for every env at every step
      (cal_td_error + chunk lists, qmix/_utils.py:86-97, qmix/main.py:204-233)
   5. every C steps: the E finished chunks go into the prioritized replay at once
 
-Three launches per step (env; target fwd of step t fused with the behavior fwd of
-step t+1 into one launch; TD/store), all stream-ordered on one HIP stream, no host
-sync; a chunk of steps is captured once as a HIP graph and replayed.
+Two launches per in-chunk step: env(t) fused with the TD/store of step t-1, and the
+target fwd of step t fused with the behavior fwd of step t+1; the chunk's last step adds
+a standalone TD/store and the PER insert. All stream-ordered on one HIP stream, no host
+sync; a chunk of steps is captured once as a HIP graph and replayed. The store/TD of the
+last executed step therefore lands with the next step (``flush_td()`` writes it now).
 Hidden states reset at episode ends (the reference re-inits them per episode,
 vdn/main.py:137-138); chunks span episode boundaries like the reference's
 global ``count_step`` (vdn/main.py:151-167).
@@ -87,6 +89,8 @@ class RolloutEngine:
         self.counter_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # rollout step (RNG stream)
         self._eps_host = None
         self._primed = False
+        self._td_pending = False     # last step's TD/store not yet written (fused into the next env step)
+        self._td_flushed = False
         self.graph = None
         self.t = 0
         self.seed = int(seed)
@@ -179,23 +183,51 @@ class RolloutEngine:
             check(L.mm_chunk_begin_rows(self.E, ND, ptr(self.store.obs), self.store.row_stride, ptr(self.cur_row),
                                         self.C * ND, self.env.reset_obs_ptr(), ptr(self.staging), s), "chunk_begin")
         nxt = ctypes.c_void_p(self.store.obs.data_ptr() + 4 * (c + 1) * ND)
-        check(L.mm_env_step_rows(self.env.handle(), ptr(self.act_buf[k]), nxt, self.store.row_stride,
-                                 ptr(self.staging), None, ptr(self.cur_row), ptr(self.rew), ptr(self.done_buf[k]), s),
-              "env_step")
+        if c > 0 and not self._td_flushed:
+            # env(t) fused with the TD/store of step t-1 (same staging rows inside a chunk)
+            kp = 1 - k
+            check(L.mm_env_step_rows_td(self.env.handle(), ptr(self.act_buf[k]), nxt, self.store.row_stride,
+                                        ptr(self.staging), ptr(self.cur_row), ptr(self.rew), ptr(self.done_buf[k]),
+                                        self.gamma, ptr(self.rew), ptr(self.done_buf[kp]), ptr(self.qsel_buf[kp]),
+                                        ptr(self.maxq), ptr(self.act_buf[kp]), ptr(self.chunk_td), c - 1, self.C,
+                                        ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
+                                        ptr(self.staging), ptr(self.counter_dev), s), "env_step_td")
+        else:
+            check(L.mm_env_step_rows(self.env.handle(), ptr(self.act_buf[k]), nxt, self.store.row_stride,
+                                     ptr(self.staging), None, ptr(self.cur_row), ptr(self.rew),
+                                     ptr(self.done_buf[k]), s), "env_step")
+        self._td_flushed = False
         iot, iob = self.io_t[k], self.io_b[1 - k]
         iot.obs_off = iob.obs_off = (c + 1) * ND
         self.behavior.pack(s)
         self.target.pack(s)
         check(L.mm_agent_q_fwd2(ctypes.byref(self.target.dims), ptr(self.target.packed), ctypes.byref(iot), self.E,
                                 ptr(self.behavior.packed), ctypes.byref(iob), self.E, s), "agent_q_fwd2")
-        check(L.mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done_buf[k]),
-                                      ptr(self.qsel_buf[k]), ptr(self.maxq), ptr(self.act_buf[k]), ptr(self.chunk_td),
-                                      c, self.C, ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
-                                      ptr(self.staging), ptr(self.counter_dev), s), "td_chunk")
         if c == self.C - 1:
+            # the chunk's last TD/store runs on its own (the insert needs it before the next env step)
+            self._td_standalone(s, k, c)
             check(L.mm_per_insert(self.per._h, ptr(self.chunk_td), self.E, ptr(self.staging), None, s), "per_insert")
             self.chunks_inserted += self.E
+            self._td_pending = False
+        else:
+            self._td_pending = True
         self.t += 1
+
+    def flush_td(self):
+        """Write the last step's TD / transition store now (eager use: it is otherwise fused into the
+        next step's env launch); the next step then runs the unfused env kernel."""
+        if self._td_pending:
+            t = self.t - 1
+            self._td_standalone(stream_handle(self.device), t % 2, t % self.C)
+            self._td_pending = False
+            self._td_flushed = True
+
+    def _td_standalone(self, s, k, c):
+        check(lib().mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done_buf[k]),
+                                          ptr(self.qsel_buf[k]), ptr(self.maxq), ptr(self.act_buf[k]),
+                                          ptr(self.chunk_td), c, self.C, ptr(self.store.act), ptr(self.store.rew),
+                                          ptr(self.store.done), ptr(self.staging), ptr(self.counter_dev), s),
+              "td_chunk")
 
     # ------------------------------------------------------------------ HIP graph replay
     def graph_steps(self):

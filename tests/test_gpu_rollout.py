@@ -91,7 +91,7 @@ def test_eps_greedy_device_rng_rate():
     assert act.min().item() >= 0 and act.max().item() <= 4
 
 
-@pytest.mark.parametrize("n_agents,full_obs", [(2, False), (2, True), (8, False), (3, False)])
+@pytest.mark.parametrize("n_agents,full_obs", [(2, False), (2, True), (8, False), (3, False), (17, False), (5, True)])
 def test_env_bit_exact_vs_oracle(n_agents, full_obs):
     from minimarl.env import VecEnv
     E, steps = 300, 230
@@ -183,7 +183,9 @@ def test_per_batched_vs_oracle(flavor, cap, kb, rounds):
 
 
 def test_rollout_engine_end_to_end_vs_oracle():
-    """Engine transitions (store contents), TD chunk priorities and actions vs an oracle replay."""
+    """Engine transitions (store contents), TD chunk priorities and actions vs an oracle replay.
+    In-chunk steps run the env kernel fused with the previous step's TD/store, so the store rows
+    and chunk priorities are checked once each chunk is complete (and mid-chunk after flush_td)."""
     from minimarl.engine import RolloutEngine
     E, N, C = 96, 8, 10
     eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=C, capacity=512, seed=7, device=DEV)
@@ -194,13 +196,16 @@ def test_rollout_engine_end_to_end_vs_oracle():
     h = torch.zeros(E, N, 64)
     ht = torch.zeros(E, N, 64)
     td_chunk = np.zeros(E, np.float64)
+    hist = []
     steps = 2 * C + 3
     for t in range(steps):
         rows = eng.staging.cpu().numpy()          # staging rows of this step (swapped at chunk end)
         eng.step(epsilon=0.2)
-        torch.cuda.synchronize()
         c = t % C
-        act = eng.store.act[rows, c].cpu().numpy().astype(np.int64)
+        if t == C + 4:
+            eng.flush_td()                        # exercise the unfused path mid-chunk once
+        torch.cuda.synchronize()
+        act = eng.act.cpu().numpy().astype(np.int64)
         q, h = nets.agent_forward(P, obs, h)
         greedy = q.argmax(2).numpy()
         qs = q.gather(2, torch.tensor(act).unsqueeze(-1)).squeeze(-1)
@@ -209,13 +214,21 @@ def test_rollout_engine_end_to_end_vs_oracle():
         assert same.mean() > 0.6
         nxt, rew, done = ora.step(act)
         np.testing.assert_array_equal(eng.store.obs[rows, c + 1].cpu().numpy(), nxt)
-        np.testing.assert_array_equal(eng.store.rew[rows, c].cpu().numpy(), rew)
-        np.testing.assert_array_equal(eng.store.done[rows, c].cpu().numpy().astype(bool), done)
+        np.testing.assert_array_equal(eng.rew.cpu().numpy(), rew)
+        np.testing.assert_array_equal(eng.done_buf[t % 2].cpu().numpy().astype(bool), done)
         tq, ht = nets.agent_forward(P, torch.tensor(nxt), ht)
         td = (torch.tensor(rew).sum(1) + (1 - torch.tensor(done, dtype=torch.float32)) * 0.99 * tq.max(2)[0].sum(1)
               - qs.sum(1)).abs().numpy()
         td_chunk = td if c == 0 else td_chunk + td
-        np.testing.assert_allclose(eng.chunk_td.cpu().numpy(), td_chunk, rtol=2e-4, atol=2e-4)
+        hist.append((act, rew, done))
+        if c == C - 1 or t == C + 4:
+            # complete chunk (or flushed step): store rows and the chunk priority so far
+            for cc in range(c + 1):
+                a_, r_, d_ = hist[t - c + cc]
+                np.testing.assert_array_equal(eng.store.act[rows, cc].cpu().numpy(), a_)
+                np.testing.assert_array_equal(eng.store.rew[rows, cc].cpu().numpy(), r_)
+                np.testing.assert_array_equal(eng.store.done[rows, cc].cpu().numpy().astype(bool), d_)
+            np.testing.assert_allclose(eng.chunk_td.cpu().numpy(), td_chunk, rtol=2e-4, atol=2e-4)
         keep = torch.tensor(~done, dtype=torch.float32).view(E, 1, 1)
         h, ht = h * keep, ht * keep
         ora.reset_envs(done)
@@ -224,6 +237,24 @@ def test_rollout_engine_end_to_end_vs_oracle():
     assert len(eng.per) == 2 * E
     tree = eng.per.tree().cpu().numpy()
     assert tree[0] > 0
+
+
+def test_fused_td_matches_unfused():
+    """env+TD fused launches give bit-identical stores, priorities and PER to the unfused path."""
+    from minimarl.engine import RolloutEngine
+    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=512, seed=5, device=DEV)
+    a = RolloutEngine(64, 8, **kw)
+    b = RolloutEngine(64, 8, **kw)
+    for _ in range(25):
+        a.step(0.3)
+        b.step(0.3)
+        b.flush_td()
+    a.flush_td()
+    torch.cuda.synchronize()
+    for x, y in [(a.store.obs, b.store.obs), (a.store.act, b.store.act), (a.store.rew, b.store.rew),
+                 (a.store.done, b.store.done), (a.h, b.h), (a.ht, b.ht), (a.chunk_td, b.chunk_td),
+                 (a.counter_dev, b.counter_dev), (a.per.tree(), b.per.tree()), (a.per.slot_rows(), b.per.slot_rows())]:
+        assert torch.equal(x, y)
 
 
 def test_graph_replay_matches_eager():
