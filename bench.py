@@ -29,6 +29,7 @@ for _p in (ROOT, os.path.join(ROOT, "mini-marl_amd")):
 import torch  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (vector = f32 MFMA), MI355X_MICROARCH.md
+PEAK_F16_TFLOPS = 16 * PEAK_FP32_TFLOPS   # dense f16/bf16 MFMA (= 16x the f32 MFMA rate), ~2.5 PF
 PEAK_HBM_GBS = 8000.0
 
 
@@ -236,22 +237,31 @@ def main():
         del mr, menv, mpol
         torch.cuda.empty_cache()
 
-    # roofline of the dominant kernel: the fused agent Q forward (behavior launch of a step)
-    # (one launch = target net on s'_t + behavior net on s_{t+1}: 2 nets x E x N agent-steps)
+    # roofline of the dominant kernel: the fused agent Q forward (one launch = target net on s'_t +
+    # behavior net on s_{t+1}: 2 nets x E x N agent-steps). At E >= 2048 it runs the fp16x3-split
+    # kernel: every fp32 product as 3 f16 MFMAs, so its MFMA ceiling for the network's fp32 FLOPs
+    # is the dense f16 peak / 3; the native f32-MFMA peak is reported beside it.
     t_fwd = time_kernel(eng.fused_forward)
     flops = 2 * qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
     achieved = flops / t_fwd / 1e12
+    h3 = E >= 2048 and not os.environ.get("MM_FWD_F32")
+    peak = PEAK_F16_TFLOPS / 3 if h3 else PEAK_FP32_TFLOPS
     # algorithmic HBM bytes per launch: per agent-step obs 4D + hidden in/out 8H + outputs (act/q 8 or max 4)
     alg_bytes = E * N * ((4 * D + 8 * Hh + 8) + (4 * D + 8 * Hh + 4))
     traffic = None
     prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_agent_fwd.json")))
     if prof and E == 4096 and N == 8 and Hh == 64:
         pm = json.load(open(prof[-1]))
-        traffic = int(pm["traffic_bytes_corrected"])
-    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+        if pm.get("kernel", "").startswith("agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"):
+            traffic = int(pm["traffic_bytes_corrected"])
+    kname = "agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_source": os.path.basename(prof[-1]) if traffic else None,
-                "kernel": "agent_q_fwd_lds_kernel<64,64,64,1> (dual: target+behavior)", "kernel_us": round(t_fwd * 1e6, 2),
+                "kernel": f"{kname}<64,64,64,1> (dual: target+behavior)", "kernel_us": round(t_fwd * 1e6, 2),
+                "arith": "fp32 network FLOPs as fp16x3-split MFMA (v_mfma_f32_32x32x16_f16 x3, fp32 accumulate)"
+                         if h3 else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
+                "fp32_native_peak": PEAK_FP32_TFLOPS, "frac_of_fp32_native_peak": round(achieved / PEAK_FP32_TFLOPS, 4),
                 "flop_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
                 "hbm_frac": round(alg_bytes / t_fwd / (PEAK_HBM_GBS * 1e9), 4)}
 

@@ -45,7 +45,9 @@ typedef struct mm_qnet_dims {
  *   W1[N,F1,D] b1[N,F1] W2[N,G,F1] b2[N,G] Wih[N,3H,G] Whh[N,3H,H] bih[N,3H] bhh[N,3H] Wq[N,A,H] bq[N,A]
  * concatenated in that order. offs[0..9] = element offsets, offs[10] = total. */
 int mm_qnet_param_offsets(const mm_qnet_dims* d, int64_t offs[11]);
-/* Size (floats) of the MFMA-fragment-packed weight image used by mm_agent_q_fwd. */
+/* Size (floats) of the MFMA-fragment-packed weight images used by mm_agent_q_fwd: the exact-f32
+ * fragment image followed by the fp16x3-split image of the large-E (LDS-staged) forward
+ * (v_mfma_f32_32x32x16_f16 x3 per product; set MM_FWD_F32=1 to use the f32 MFMA kernel instead). */
 int64_t mm_qnet_packed_count(const mm_qnet_dims* d);
 /* Repack flat params into the fragment image (call after every optimizer step). */
 int mm_qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s);

@@ -42,7 +42,7 @@ int64_t mm_qnet_packed_count(const mm_qnet_dims* d) {
   mm::QnetGeo g;
   mm::QnetOffsets o;
   if (mm::qnet_geometry(d, &g, &o)) return -1;
-  return g.agent_stride * d->n_agents;
+  return 2 * g.agent_stride * d->n_agents;  // [fp32 fragment image | fp16x3-split image]
 }
 
 int mm_qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s) {

@@ -21,11 +21,11 @@
 
 namespace mm {
 static constexpr int OBS_LOCAL = 47;
-static constexpr int EB_DEFAULT = 4;
 
 struct EnvDev {
   int E, N, R, C, D, max_steps, full_obs, init_apples;
   int eb;  // envs per block of the step kernel
+  int dbg;  // debug: stop the step kernel after phase dbg (0 = full run)
   float step_cost, inv_r, inv_c;
   int32_t* pos;     // [E][N] r*256 + c
   int8_t* grid;     // [E][R*C] 0 empty, 1 lemon, 2 apple
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int RC = d.R * d.C;
   const int N = d.N;
-  const int EPW = WT / N;
+  const int EPW = d.eb;  // envs per wave (<= 64 / N)
   const int lane = threadIdx.x;
   const bool autoreset = obs_cur || cur_row;
   const int ND = N * d.D;
@@ -157,34 +157,62 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
   const int le_l = lane / N, k_l = lane % N;
   const int e_l = e0 + le_l;
 
-  // ---- phase 0: all global reads
+  // ---- phase 0: every global read of the step issued into registers first (one memory round
+  // trip for the wave), then staged in LDS
+  constexpr int GWR = 4;                   // grid dwords per lane held in registers
+  const bool g32ok = (RC & 3) == 0;
+  const int nw = g32ok ? ne * RC / 4 : 0;
+  const uint32_t* g32 = reinterpret_cast<const uint32_t*>(d.grid + (int64_t)e0 * RC);
+  uint32_t gr[GWR];
+#pragma unroll
+  for (int w = 0; w < GWR; ++w) gr[w] = (lane + w * WT < nw) ? g32[lane + w * WT] : 0u;
+  int32_t pos_r = 0, act_r = 0, tact_r = 0;
+  float trew = 0.f, tq = 0.f, tm = 0.f;
+  int64_t trow = 0;
   if (lane < nl) {
     const int64_t o = (int64_t)e0 * N + lane;
-    spos[lane] = d.pos[o];
-    sact[lane] = act[o];
+    pos_r = d.pos[o];
+    act_r = act[o];
     if (tdf.on) {
-      std3[lane] = tdf.rew[o];
-      std3[EPW * N + lane] = tdf.q_taken[o];
-      std3[2 * EPW * N + lane] = tdf.maxq[o];
-      const int64_t row = tdf.rows[e_l];
-      tdf.s_act[(row * tdf.C + tdf.slot) * N + k_l] = (uint8_t)tdf.act[o];
-      tdf.s_rew[(row * tdf.C + tdf.slot) * N + k_l] = std3[lane];
+      trew = tdf.rew[o];
+      tq = tdf.q_taken[o];
+      tm = tdf.maxq[o];
+      tact_r = tdf.act[o];
+      trow = tdf.rows[e_l];
     }
   }
-  if ((RC & 3) == 0) {
-    const int nw = ne * RC / 4;
-    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(d.grid + (int64_t)e0 * RC);
-    for (int i = lane; i < nw; i += WT) reinterpret_cast<uint32_t*>(sgrid)[i] = g32[i];
-  } else {
-    for (int i = lane; i < ne * RC; i += WT) sgrid[i] = d.grid[(int64_t)e0 * RC + i];
-  }
-  for (int i = lane; i < ne * RC; i += WT) socc[i] = 0;
   int apples0 = 0, steps0 = 0;
+  int64_t srow_r = 0;
+  uint8_t tdone = 0;
   if (lane < ne) {
-    srow[lane] = next_row ? next_row[e0 + lane] : (int64_t)(e0 + lane);
+    srow_r = next_row ? next_row[e0 + lane] : (int64_t)(e0 + lane);
     apples0 = d.apples[e0 + lane];
     steps0 = d.steps[e0 + lane];
+    if (tdf.on) tdone = tdf.done[e0 + lane];
   }
+  for (int i = lane; i < ne * RC; i += WT) socc[i] = 0;
+#pragma unroll
+  for (int w = 0; w < GWR; ++w)
+    if (lane + w * WT < nw) reinterpret_cast<uint32_t*>(sgrid)[lane + w * WT] = gr[w];
+  for (int i = lane + GWR * WT; i < nw; i += WT) reinterpret_cast<uint32_t*>(sgrid)[i] = g32[i];
+  if (!g32ok)
+    for (int i = lane; i < ne * RC; i += WT) sgrid[i] = d.grid[(int64_t)e0 * RC + i];
+  if (lane < nl) {
+    spos[lane] = pos_r;
+    sact[lane] = act_r;
+    if (tdf.on) {
+      std3[lane] = trew;
+      std3[EPW * N + lane] = tq;
+      std3[2 * EPW * N + lane] = tm;
+      tdf.s_act[(trow * tdf.C + tdf.slot) * N + k_l] = (uint8_t)tact_r;
+      tdf.s_rew[(trow * tdf.C + tdf.slot) * N + k_l] = trew;
+    }
+  }
+  if (lane < ne) srow[lane] = srow_r;
+  __syncthreads();
+  if (d.dbg == 1) return;
+  // occupancy map of the starting positions (agent id + 1)
+  if (lane < nl) socc[le_l * RC + (pos_r >> 8) * d.C + (pos_r & 255)] = (uint8_t)(k_l + 1);
   __syncthreads();
 
   // fused TD of the previous step: agent-order sums per env (one lane per env)
@@ -196,88 +224,62 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
       sq += std3[EPW * N + lane * N + j];
       st += std3[2 * EPW * N + lane * N + j];
     }
-    const uint8_t dn8 = tdf.done[e];
-    const float dn = dn8 ? 1.0f : 0.0f;
+    const float dn = tdone ? 1.0f : 0.0f;
     const float td = fabsf(sr + (1.0f - dn) * tdf.gamma * st - sq);
     tdf.chunk_td[e] = (tdf.slot == 0 ? 0.0f : tdf.chunk_td[e]) + td;
     const int64_t row = tdf.rows[e];
-    tdf.s_done[row * tdf.C + tdf.slot] = dn8;
+    tdf.s_done[row * tdf.C + tdf.slot] = tdone;
     if (tdf.counter && blockIdx.x == 0 && lane == 0) *tdf.counter += 1;
   }
 
+  if (d.dbg == 2) return;
   // ---- phase 1: dynamics, one lane per env, agents in id order (oracle/env.py VecEnvOracle.step).
+  // A move is blocked by the border or by the occupancy map (positions as updated so far this step),
+  // so each agent costs two dependent LDS round trips (occupancy, then the fruit of its cell).
   if (lane < ne) {
     const int le = lane, e = e0 + lane;
     int8_t* g = sgrid + le * RC;
+    uint8_t* oc = socc + le * RC;
+    int32_t* p = spos + le * N;
     int apples = apples0;
     const int steps = steps0 + 1;
-    if (N <= 16) {
-      int p[16], a[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        p[k] = k < N ? spos[le * N + k] : -1;
-        a[k] = k < N ? sact[le * N + k] : 4;
+#pragma unroll 1
+    for (int k = 0; k < N; ++k) {
+      const int a = sact[le * N + k];
+      const int pk = p[k];
+      const int r = pk >> 8, c = pk & 255;
+      const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
+      const int nc = c + (a == 1 ? -1 : (a == 3 ? 1 : 0));
+      const bool inside = nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
+      const int tcell = inside ? nr * d.C + nc : 0;
+      const int occ = inside ? oc[tcell] : 0;
+      const bool ok = inside && (occ == 0 || occ == k + 1);
+      const int ocell = r * d.C + c;
+      const int cell = ok ? tcell : ocell;
+      if (ok) {
+        oc[ocell] = 0;
+        oc[tcell] = (uint8_t)(k + 1);
       }
-      float rk[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        if (k >= N) break;
-        const int r = p[k] >> 8, c = p[k] & 255;
-        const int nr = r + (a[k] == 0 ? 1 : (a[k] == 2 ? -1 : 0));
-        const int nc = c + (a[k] == 1 ? -1 : (a[k] == 3 ? 1 : 0));
-        bool ok = nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
-        const int key = (nr << 8) | nc;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) ok = ok && (j == k || p[j] != key);
-        if (ok) p[k] = key;
-        const int cell = (p[k] >> 8) * d.C + (p[k] & 255);
-        const int item = g[cell];
-        const bool big = (k & 1) == 0;
-        rk[k] = d.step_cost + (item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f));
-        apples -= item == 2 ? 1 : 0;
-        g[cell] = 0;
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        if (k >= N) break;
-        spos[le * N + k] = p[k];
-        rew[(int64_t)e * N + k] = rk[k];
-      }
-    } else {
-      int32_t* p = spos + le * N;
-      for (int k = 0; k < N; ++k) {
-        const int a = sact[le * N + k];
-        const int r = p[k] >> 8, c = p[k] & 255;
-        const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
-        const int nc = c + (a == 1 ? -1 : (a == 3 ? 1 : 0));
-        bool ok = nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
-        const int key = (nr << 8) | nc;
-        for (int j = 0; j < N; ++j) ok = ok && (j == k || p[j] != key);
-        if (ok) p[k] = key;
-        const int cell = (p[k] >> 8) * d.C + (p[k] & 255);
-        const int item = g[cell];
-        float rk = d.step_cost;
-        const bool big = (k & 1) == 0;
-        rk += item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f);
-        apples -= item == 2 ? 1 : 0;
-        g[cell] = 0;
-        rew[(int64_t)e * N + k] = rk;
-      }
+      p[k] = ok ? ((nr << 8) | nc) : pk;
+      const int item = g[cell];
+      const bool big = (k & 1) == 0;
+      const float rk =
+          d.step_cost + (item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f));
+      apples -= item == 2 ? 1 : 0;
+      g[cell] = 0;
+      rew[(int64_t)e * N + k] = rk;
     }
     const bool dn = steps >= d.max_steps || apples == 0;
     sdone[le] = dn ? 1 : 0;
     done_out[e] = dn ? 1 : 0;
-    if (cur_row) cur_row[e] = dn ? -1 : srow[le];
+    if (cur_row) cur_row[e] = dn ? -1 : srow_r;
     d.steps[e] = dn && autoreset ? 0 : steps;
     d.apples[e] = dn && autoreset ? d.init_apples : apples;
   }
   __syncthreads();
   int mypos = 0;
-  if (lane < nl) {
-    mypos = spos[lane];
-    socc[le_l * RC + (mypos >> 8) * d.C + (mypos & 255)] = (uint8_t)(k_l + 1);
-  }
-  __syncthreads();
+  if (lane < nl) mypos = spos[lane];
+  if (d.dbg == 3) return;
 
   // ---- phase 2: local obs of (env le_l, agent k_l) into the LDS tile
   if (lane < nl) {
@@ -313,15 +315,23 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
   }
   __syncthreads();
 
+  if (d.dbg == 4) return;
   // ---- phase 3: stream the obs out (env le's N*D run from its local tile) and write state back
   const bool full = d.full_obs != 0;
   const float* robs = d.reset_obs;
   const bool vec = (ND & 3) == 0 && (next_se & 3) == 0 && ((uintptr_t)next_obs & 15) == 0 &&
                    ((uintptr_t)obs_cur & 15) == 0;
   if (vec) {
+    // flat float4 index i = lane + WT*it over the block's ne x ND4 outputs, walked with a running
+    // (env, offset) pair instead of a division per element
     const int ND4 = ND >> 2;
-    for (int i = lane; i < ne * ND4; i += WT) {
-      const int le = i / ND4, r = (i - le * ND4) * 4;
+    int le = 0, r4 = lane;
+    while (r4 >= ND4 && le < ne) {
+      r4 -= ND4;
+      ++le;
+    }
+    for (; le < ne;) {
+      const int r = r4 * 4;
       const float* t = sloc + le * LD;
       float4 v;
       if (!full) {
@@ -337,6 +347,11 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
         if (sdone[le]) v = *reinterpret_cast<const float4*>(robs + r);
         *reinterpret_cast<float4*>(obs_cur + (int64_t)(e0 + le) * ND + r) = v;
       }
+      r4 += WT;
+      while (r4 >= ND4 && le < ne) {
+        r4 -= ND4;
+        ++le;
+      }
     }
   } else {
     for (int i = lane; i < ne * ND; i += WT) {
@@ -346,6 +361,7 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
       if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? robs[r] : v;
     }
   }
+  if (d.dbg == 5) return;
   if ((RC & 3) == 0) {
     uint32_t* g32 = reinterpret_cast<uint32_t*>(d.grid + (int64_t)e0 * RC);
     const uint32_t* ig32 = reinterpret_cast<const uint32_t*>(d.init_grid);
@@ -364,7 +380,7 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
 }
 
 static size_t step_smem(const EnvDev& d) {
-  const size_t EPW = WT / d.N, RC = (size_t)d.R * d.C;
+  const size_t EPW = d.eb, RC = (size_t)d.R * d.C;
   return EPW * d.N * OBS_LOCAL * 4 + EPW * 8 + 3 * EPW * d.N * 4 + 2 * EPW * d.N * 4 + ((EPW + 15) & ~15ull) +
          ((EPW * RC + 15) & ~15ull) + EPW * RC;
 }
@@ -379,8 +395,9 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   EnvDev d;
   d.E = (int)n_envs;
   d.N = cfg->n_agents;
-  d.eb = getenv("MM_ENV_EB") ? atoi(getenv("MM_ENV_EB")) : EB_DEFAULT;
-  MM_REQUIRE(d.eb >= 1 && d.eb <= 64, "env_create: bad envs-per-block");
+  d.dbg = getenv("MM_ENV_DBG") ? atoi(getenv("MM_ENV_DBG")) : 0;
+  d.eb = getenv("MM_ENV_EB") ? atoi(getenv("MM_ENV_EB")) : WT / d.N;
+  MM_REQUIRE(d.eb >= 1 && d.eb * d.N <= WT, "env_create: bad envs-per-block");
   d.R = 3 * ((d.N + 1) / 2);
   d.C = cols;
   MM_REQUIRE(d.R <= 255, "env_create: too many agents for the grid");
@@ -456,8 +473,7 @@ int env_step(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, 
   MM_REQUIRE(env && act && rew && done, "env_step: null argument");
   MM_REQUIRE(next_obs || obs_cur, "env_step: no obs output");
   const EnvDev& d = env->d;
-  const int epw = WT / d.N;
-  const int blocks = (d.E + epw - 1) / epw;
+  const int blocks = (d.E + d.eb - 1) / d.eb;
   TdFuse t{};
   if (tdf) t = *tdf;
   hipLaunchKernelGGL(env_step_wave_kernel, dim3(blocks), dim3(WT), step_smem(d), s, d, act, next_obs,

@@ -12,6 +12,7 @@ from minimarl.env import VecEnv  # noqa: E402
 from minimarl.qnet import ptr, stream_handle  # noqa: E402
 
 E, N = int(os.environ.get("MB_E", 4096)), 8
+CUR = int(os.environ.get("MB_CUR", 1))
 env = VecEnv(E, N, max_steps=100, device="cuda")
 obs = env.reset()
 act = torch.randint(0, 5, (E, N), dtype=torch.int32, device="cuda")
@@ -22,7 +23,7 @@ s = stream_handle()
 
 
 def step():
-    lib().mm_env_step(env.handle(), ptr(act), ptr(nxt), ptr(cur), ptr(rew), ptr(done), s)
+    lib().mm_env_step(env.handle(), ptr(act), ptr(nxt), ptr(cur) if CUR else None, ptr(rew), ptr(done), s)
 
 
 for _ in range(20):
