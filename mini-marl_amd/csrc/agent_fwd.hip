@@ -26,6 +26,8 @@ struct QFwdParams {
   int E, N, D, A;
   int nblocks;  // blocks of this net inside a (possibly dual) launch
   int stagger;  // LDS variant: waves 4-7 start stagger x 512 cycles late
+  int dbg;      // debug timing (MM_FWD_DBG): stop the fp16x3 kernel after phase dbg (0 = full)
+  int pad_;
 };
 
 // Fragment image of one 32x32 k-block: [q = s>>2][lane][s&3] floats, so each of the 4 dwordx4
@@ -99,7 +101,18 @@ __device__ __forceinline__ void load_obs_kblock(const float* orow, int kb, int D
 
 // Q output / argmax / eps-greedy / gather epilogue shared by the fused and the split forward.
 template <int AB>
+__device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB],
+                                             float eps, uint64_t ctr);
+template <int AB>
 __device__ __forceinline__ void q_epilogue(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB]) {
+  const mm_qfwd_io& io = p.io;
+  const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
+  const uint64_t ctr = (io.mode == MM_Q_ACT && io.counter_ptr) ? *io.counter_ptr : io.counter;
+  q_epilogue_v<AB>(p, agent, e, valid, qa, eps, ctr);
+}
+template <int AB>
+__device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB],
+                                             float eps, uint64_t ctr) {
   const int hh = (threadIdx.x & 63) >> 5;
   const mm_qfwd_io& io = p.io;
   if (valid && io.q_out) {
@@ -136,8 +149,6 @@ __device__ __forceinline__ void q_epilogue(const QFwdParams& p, int agent, int e
   }
   int act = bi;
   if (io.mode == MM_Q_ACT) {
-    const float eps = io.eps_ptr ? *io.eps_ptr : io.epsilon;
-    const uint64_t ctr = io.counter_ptr ? *io.counter_ptr : io.counter;
     float u;
     if (io.u) {
       u = valid ? io.u[e] : 1.0f;
@@ -563,201 +574,365 @@ __global__ __launch_bounds__(512, 2) void agent_q_fwd_lds_kernel(QFwdParams p0, 
 }
 
 // ---------------------------------------------------------------- fp16x3-split forward (large E)
-// Same network, same MFMA dataflow (features on rows, envs on columns, D registers chained into the
-// next layer's B operand), but every fp32 product W*x runs as three v_mfma_f32_32x32x16_f16:
-//   W*x ~= Wh*xh + Wh*xl + Wl*xh,  Wh = f16(W), Wl = f16(W - Wh) (same for x), fp32 accumulate.
-// Each f16 x f16 product is exact in fp32 and the dropped Wl*xl and split residuals are ~2^-22
+// Same network, but every fp32 product W*x runs as three f16 MFMAs with fp32 accumulation:
+//   W*x ~= Wh*xh + Wh*xl + Wl*xh,  Wh = f16(W), Wl = f16(W - Wh) (same split for x).
+// Each f16 x f16 product is exact in fp32; the dropped Wl*xl and the split residuals are ~2^-22
 // relative (fp16 subnormals bound the absolute error of small parts by 2^-25), so results agree
-// with the fp32 network to ~1e-6 relative (tests: rtol 1e-5). Cost per 32-deep k-block: 6 f16
-// MFMAs x 32 cycles instead of 16 f32 MFMAs x 64 cycles (5.3x less MFMA time).
-// Weight image (packed + N*agent_stride, same block geometry as the fp32 image): per 32x32
-// block [k-step s][part hi|lo][lane][8 halves]: 4 KiB, every A fragment one conflict-free
-// ds_read_b128 (lane (i, h) of k-step s holds W[i][kperm(8s + j, h)], j = 0..7).
+// with the fp32 network to ~1e-6 relative (tests: rtol 1e-5 vs the oracle). Per 32-deep k-step:
+// 3 x v_mfma_f32_16x16x32_f16 (16 cycles each) per 16 output rows instead of 16 x 64-cycle f32
+// MFMAs per 32 rows: 5.3x less MFMA time.
+// Mapping: one wave = 16 envs of one agent (16x16 tiles: feature rows x env columns), 16 waves
+// (256 envs of one agent) per 1024-thread block sharing the agent's LDS image: 4 waves per SIMD
+// to hide the per-wave dependency chain. A 16x16 D tile gives lane (c = l&15, g = l>>4) rows
+// 4g..4g+3; two consecutive tiles are directly the next layer's 32-deep k-step B fragment with
+// element j <-> feature 16(j>>2) + 4g + (j&3) (kperm16), so layers chain through registers.
+// Weight image (packed + N*agent_stride, same 32x32-block geometry as the f32 image): per block
+// [16-row half q][part hi|lo][lane][8 halves] = 4 KiB, every A fragment one conflict-free
+// ds_read_b128 (lane (i, g) of half q holds W[32rb + 16q + i][32kb + kperm16(j, g)]); biases in
+// natural order.
+#ifndef MM_H3_LB
+#define MM_H3_LB 1
+#endif
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+__host__ __device__ __forceinline__ int kperm16(int j, int g) { return 16 * (j >> 2) + 4 * g + (j & 3); }
+
+__device__ __forceinline__ f32x4 mfma16x16(const f16x8& a, const f16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// split 8 consecutive f32 registers (x[8s .. 8s+7]) into f16 hi / lo parts
-struct H3 {
-  f16x8 h[2], l[2];  // k-step 0, 1 of one 32-feature tile
+// one 32-deep k-step of B: hi / lo parts
+struct KS {
+  f16x8 h, l;
 };
-__device__ __forceinline__ void split_tile(const float* x, H3& t) {
+__device__ __forceinline__ void split8(const float (&x)[8], KS& t) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 hv = (_Float16)x[j];
+    t.h[j] = hv;
+    t.l[j] = (_Float16)(x[j] - (float)hv);
+  }
+}
+// two consecutive 16-row D tiles -> one k-step
+__device__ __forceinline__ void split_pair(const f32x4& a, const f32x4& b, KS& t) {
+  float x[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float v = x[8 * s + j];
-      const _Float16 hv = (_Float16)v;
-      t.h[s][j] = hv;
-      t.l[s][j] = (_Float16)(v - (float)hv);
+  for (int r = 0; r < 4; ++r) {
+    x[r] = a[r];
+    x[4 + r] = b[r];
+  }
+  split8(x, t);
+}
+// acc (16 rows: half q of block blk) += W * X(k-step)
+__device__ __forceinline__ void mm16(const float* __restrict__ blk, int q, const KS& x, int lane, f32x4& acc) {
+  const f16x8 ah = *reinterpret_cast<const f16x8*>(blk + (q * 2) * 256 + lane * 4);
+  const f16x8 al = *reinterpret_cast<const f16x8*>(blk + (q * 2 + 1) * 256 + lane * 4);
+  acc = mfma16x16(al, x.h, acc);
+  acc = mfma16x16(ah, x.l, acc);
+  acc = mfma16x16(ah, x.h, acc);
+}
+struct Frag {
+  f16x8 h, l;
+};
+__device__ __forceinline__ Frag ldfrag(const float* __restrict__ blk, int q, int lane) {
+  Frag f;
+  f.h = *reinterpret_cast<const f16x8*>(blk + (q * 2) * 256 + lane * 4);
+  f.l = *reinterpret_cast<const f16x8*>(blk + (q * 2 + 1) * 256 + lane * 4);
+  return f;
+}
+__device__ __forceinline__ void mmf(const Frag& a, const KS& x, f32x4& acc) {
+  acc = mfma16x16(a.l, x.h, acc);
+  acc = mfma16x16(a.h, x.l, acc);
+  acc = mfma16x16(a.h, x.h, acc);
+}
+__device__ __forceinline__ f32x4 bias4(const float* __restrict__ b, int t, int g) {
+  return *reinterpret_cast<const f32x4*>(b + 16 * t + 4 * g);
+}
+// obs k-step kb: lane (c, g) holds obs features 32 kb + kperm16(j, g)
+__device__ __forceinline__ void load_obs_ks(const float* orow, int kb, int D, float (&x)[8]) {
+  const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = kb * 32 + kperm16(j, g);
+    x[j] = (orow && k < D) ? orow[k] : 0.0f;
+  }
+}
+
+// Q output / argmax / eps-greedy / gather epilogue for 16-row Q tiles (rows 16t + 4g + r).
+template <int AT>
+__device__ __forceinline__ void q_epilogue16(const QFwdParams& p, int agent, int e, bool valid,
+                                             const f32x4 (&qa)[AT], float eps, uint64_t ctr) {
+  const int g = (threadIdx.x & 63) >> 4;
+  const mm_qfwd_io& io = p.io;
+  if (valid && io.q_out) {
+    float* qrow = io.q_out + (int64_t)e * io.q_se + (int64_t)agent * io.q_sa;
+#pragma unroll
+    for (int t = 0; t < AT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * t + 4 * g + r;
+        if (row < p.A) qrow[row] = qa[t][r];
+      }
+  }
+  if (io.mode == MM_Q_NONE) return;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int t = 0; t < AT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * t + 4 * g + r;
+      const float v = qa[t][r];
+      if (row < p.A && (v > best || (v == best && row < bi))) {
+        best = v;
+        bi = row;
+      }
     }
-}
-__device__ __forceinline__ void split_acc(const f32x16& x, H3& t) {
-  float a[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) a[i] = x[i];
-  split_tile(a, t);
-}
-// acc += W(block) * X(tile): 2 k-steps x 3 MFMAs
-__device__ __forceinline__ void mm_h3(const float* __restrict__ blk, const H3& x, int lane, f32x16& acc) {
+  for (int o = 16; o <= 32; o <<= 1) {
+    const float ob = __shfl_xor(best, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  int act = bi;
+  if (io.mode == MM_Q_ACT) {
+    float u;
+    if (io.u) {
+      u = valid ? io.u[e] : 1.0f;
+    } else {
+      u = rng_uniform(rng_draw(io.seed, ctr, (uint64_t)e, 0xFFFFFFFFull));
+    }
+    if (u <= eps) {
+      if (io.rand_act) {
+        act = valid ? io.rand_act[(int64_t)e * p.N + agent] : 0;
+      } else {
+        act = (int)(rng_draw(io.seed ^ 0x5bd1e995ull, ctr, (uint64_t)e, (uint64_t)agent) % (uint64_t)p.A);
+      }
+    }
+  } else if (io.mode == MM_Q_GATHER) {
+    act = valid ? io.act_in[(int64_t)e * io.act_se + agent] : 0;
+  }
+  float mine = 0.0f;
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const f16x8 ah = *reinterpret_cast<const f16x8*>(blk + (2 * s) * 256 + lane * 4);
-    const f16x8 al = *reinterpret_cast<const f16x8*>(blk + (2 * s + 1) * 256 + lane * 4);
-    acc = mfma16(al, x.h[s], acc);
-    acc = mfma16(ah, x.l[s], acc);
-    acc = mfma16(ah, x.h[s], acc);
+  for (int t = 0; t < AT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (16 * t + 4 * g + r == act) mine = qa[t][r];
+  mine += __shfl_xor(mine, 16);
+  mine += __shfl_xor(mine, 32);
+  const float qsel = (io.mode == MM_Q_MAX) ? best : mine;
+  if (valid && g == 0) {
+    const int64_t o = (int64_t)e * p.N + agent;
+    if (io.act_out && io.mode == MM_Q_ACT) io.act_out[o] = act;
+    if (io.qsel_out) io.qsel_out[o] = qsel;
   }
 }
 
 template <int F1, int G, int H, int AB>
 __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int agent, int e,
                                                     const float* __restrict__ W, const float* orow,
-                                                    float (&xn)[16]) {
+                                                    float (&xn)[8], const f32x4 (&h0)[H / 16], float eps,
+                                                    uint64_t ctr) {
   using CG = QnetCGeo<F1, G, H, AB>;
+  constexpr int T1 = F1 / 16, T2 = G / 16, TH = H / 16, AT = (AB * 32 + 15) / 16;
   constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
   const int lane = threadIdx.x & 63;
-  const int hh = lane >> 5;
+  const int g = lane >> 4;
   const bool valid = e < p.E;
   const mm_qfwd_io& io = p.io;
+  const int ATr = (p.A + 15) / 16;   // Q tiles that hold real actions
 
-  // ---- layer 1 (K = D in 32-wide k-blocks, next obs k-block prefetched)
-  f32x16 x1[RB1];
+  // ---- layer 1 (K = D in 32-deep k-steps, next obs k-step prefetched)
+  f32x4 x1[T1];
 #pragma unroll
-  for (int rb = 0; rb < RB1; ++rb) x1[rb] = load_bias(W + CG::off_b1 + rb * 32, hh);
+  for (int t = 0; t < T1; ++t) x1[t] = bias4(W + CG::off_b1, t, g);
   for (int kb = 0; kb < p.g.KD; ++kb) {
-    H3 ob;
-    split_tile(xn, ob);
-    if (kb + 1 < p.g.KD) load_obs_kblock(orow, kb + 1, p.D, xn);
+    KS ob;
+    split8(xn, ob);
+    if (kb + 1 < p.g.KD) load_obs_ks(orow, kb + 1, p.D, xn);
 #pragma unroll
-    for (int rb = 0; rb < RB1; ++rb) mm_h3(W + CG::off_l1 + (int64_t)(rb * p.g.KD + kb) * 1024, ob, lane, x1[rb]);
+    for (int t = 0; t < T1; ++t) mm16(W + CG::off_l1 + (int64_t)((t >> 1) * p.g.KD + kb) * 1024, t & 1, ob, lane, x1[t]);
   }
-  H3 x1s[RB1];
+  KS x1s[RB1];
 #pragma unroll
-  for (int rb = 0; rb < RB1; ++rb) {
+  for (int t = 0; t < T1; ++t)
 #pragma unroll
-    for (int s = 0; s < 16; ++s) x1[rb][s] = fmaxf(x1[rb][s], 0.0f);
-    split_acc(x1[rb], x1s[rb]);
+    for (int r = 0; r < 4; ++r) x1[t][r] = fmaxf(x1[t][r], 0.0f);
+  if (p.dbg == 2) {
+    if (x1[0][0] + x1[T1 - 1][3] == 12345.f) io.qsel_out[e] = eps;
+    return;
   }
+#pragma unroll
+  for (int kb = 0; kb < RB1; ++kb) split_pair(x1[2 * kb], x1[2 * kb + 1], x1s[kb]);
   float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
   if (sv) {
 #pragma unroll
-    for (int rb = 0; rb < RB1; ++rb)
+    for (int t = 0; t < T1; ++t)
 #pragma unroll
-      for (int s = 0; s < 16; ++s) sv[rb * 32 + kperm(s, hh)] = x1[rb][s];
+      for (int r = 0; r < 4; ++r) sv[16 * t + 4 * g + r] = x1[t][r];
   }
 
   // ---- layer 2
-  H3 x2s[RB2];
+  f32x4 x2[T2];
 #pragma unroll
-  for (int rb = 0; rb < RB2; ++rb) {
-    f32x16 x2 = load_bias(W + CG::off_b2 + rb * 32, hh);
+  for (int t = 0; t < T2; ++t) {
+    x2[t] = bias4(W + CG::off_b2, t, g);
 #pragma unroll
-    for (int kb = 0; kb < RB1; ++kb) mm_h3(W + CG::off_l2 + (rb * RB1 + kb) * 1024, x1s[kb], lane, x2);
+    for (int kb = 0; kb < RB1; ++kb) mm16(W + CG::off_l2 + ((t >> 1) * RB1 + kb) * 1024, t & 1, x1s[kb], lane, x2[t]);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) x2[s] = fmaxf(x2[s], 0.0f);
-    split_acc(x2, x2s[rb]);
+    for (int r = 0; r < 4; ++r) x2[t][r] = fmaxf(x2[t][r], 0.0f);
     if (sv) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) sv[F1 + rb * 32 + kperm(s, hh)] = x2[s];
+      for (int r = 0; r < 4; ++r) sv[F1 + 16 * t + 4 * g + r] = x2[t][r];
     }
+  }
+  KS x2s[RB2];
+#pragma unroll
+  for (int kb = 0; kb < RB2; ++kb) split_pair(x2[2 * kb], x2[2 * kb + 1], x2s[kb]);
+  if (p.dbg == 3) {
+    if (x2[0][0] + x2[T2 - 1][3] == 12345.f) io.qsel_out[e] = eps;
+    return;
   }
 
-  // ---- GRU cell
-  const bool zero_h = !valid || (io.reset && io.reset[e]);
-  f32x16 h0[HB];
-  H3 h0s[HB];
+  // ---- GRU cell (h0 loaded by the caller at kernel start)
+  KS h0s[HB];
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb) {
+  for (int kb = 0; kb < HB; ++kb) split_pair(h0[2 * kb], h0[2 * kb + 1], h0s[kb]);
+  float* hop = (valid && io.h_out) ? io.h_out + (int64_t)e * io.hout_se + (int64_t)agent * io.hout_sa +
+                                         (int64_t)(4 * g) * io.hout_sf
+                                   : nullptr;
+  // GRU: per hidden tile t and k-step, the three gates' fragments are read together and their
+  // 9 MFMAs interleaved (gate r, z, n, r, z, n, ...): consecutive MFMAs are independent, so no
+  // accumulator read-after-write stall between them.
+  f32x4 h1[TH];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int f = hb * 32 + kperm(s, hh);
-      h0[hb][s] = zero_h ? 0.0f
-                         : io.h_in[(int64_t)e * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)f * io.hin_sf];
-    }
-    split_acc(h0[hb], h0s[hb]);
-  }
-  H3 h1s[HB];
+  for (int t = 0; t < TH; ++t) {
+    const int rb = t >> 1, q = t & 1;
+    f32x4 ar = bias4(W + CG::off_brz, t, g);
+    f32x4 az = bias4(W + CG::off_brz + H, t, g);
+    f32x4 anx = bias4(W + CG::off_bin, t, g);
+    f32x4 anh = bias4(W + CG::off_bhn, t, g);
+    auto tri = [&](int base, int gstride, const KS& x, f32x4& a0, f32x4& a1, f32x4& a2) {
+      const Frag f0 = ldfrag(W + base, q, lane);
+      const Frag f1 = ldfrag(W + base + gstride, q, lane);
+      const Frag f2 = ldfrag(W + base + 2 * gstride, q, lane);
+      a0 = mfma16x16(f0.l, x.h, a0);
+      a1 = mfma16x16(f1.l, x.h, a1);
+      a2 = mfma16x16(f2.l, x.h, a2);
+      a0 = mfma16x16(f0.h, x.l, a0);
+      a1 = mfma16x16(f1.h, x.l, a1);
+      a2 = mfma16x16(f2.h, x.l, a2);
+      a0 = mfma16x16(f0.h, x.h, a0);
+      a1 = mfma16x16(f1.h, x.h, a1);
+      a2 = mfma16x16(f2.h, x.h, a2);
+    };
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb) {
-    f32x16 ar = load_bias(W + CG::off_brz + hb * 32, hh);
-    f32x16 az = load_bias(W + CG::off_brz + (HB + hb) * 32, hh);
-    f32x16 anx = load_bias(W + CG::off_bin + hb * 32, hh);
-    f32x16 anh = load_bias(W + CG::off_bhn + hb * 32, hh);
+    for (int kb = 0; kb < RB2; ++kb) tri(CG::off_ih + (rb * RB2 + kb) * 1024, HB * RB2 * 1024, x2s[kb], ar, az, anx);
 #pragma unroll
-    for (int kb = 0; kb < RB2; ++kb) {
-      mm_h3(W + CG::off_ih + ((0 * HB + hb) * RB2 + kb) * 1024, x2s[kb], lane, ar);
-      mm_h3(W + CG::off_ih + ((1 * HB + hb) * RB2 + kb) * 1024, x2s[kb], lane, az);
-      mm_h3(W + CG::off_ih + ((2 * HB + hb) * RB2 + kb) * 1024, x2s[kb], lane, anx);
-    }
+    for (int kb = 0; kb < HB; ++kb) tri(CG::off_hh + (rb * HB + kb) * 1024, HB * HB * 1024, h0s[kb], ar, az, anh);
 #pragma unroll
-    for (int kb = 0; kb < HB; ++kb) {
-      mm_h3(W + CG::off_hh + ((0 * HB + hb) * HB + kb) * 1024, h0s[kb], lane, ar);
-      mm_h3(W + CG::off_hh + ((1 * HB + hb) * HB + kb) * 1024, h0s[kb], lane, az);
-      mm_h3(W + CG::off_hh + ((2 * HB + hb) * HB + kb) * 1024, h0s[kb], lane, anh);
-    }
-    f32x16 h1;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const float r = sigmoidf_(ar[s]);
-      const float z = sigmoidf_(az[s]);
-      const float n = tanhf_(anx[s] + r * anh[s]);
-      h1[s] = n + z * (h0[hb][s] - n);
+    for (int r = 0; r < 4; ++r) {
+      const float rr = sigmoidf_(ar[r]);
+      const float z = sigmoidf_(az[r]);
+      const float n = tanhf_(anx[r] + rr * anh[r]);
+      h1[t][r] = n + z * (h0[t][r] - n);
       if (sv) {
-        float* o = sv + F1 + G + hb * 32 + kperm(s, hh);
-        o[0] = h0[hb][s];
-        o[H] = r;
+        float* o = sv + F1 + G + 16 * t + 4 * g + r;
+        o[0] = h0[t][r];
+        o[H] = rr;
         o[2 * H] = z;
         o[3 * H] = n;
-        o[4 * H] = anh[s];
-        o[5 * H] = h1[s];
+        o[4 * H] = anh[r];
+        o[5 * H] = h1[t][r];
       }
     }
-    if (valid && io.h_out) {
+    if (hop) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int f = hb * 32 + kperm(s, hh);
-        io.h_out[(int64_t)e * io.hout_se + (int64_t)agent * io.hout_sa + (int64_t)f * io.hout_sf] = h1[s];
-      }
+      for (int r = 0; r < 4; ++r) hop[(int64_t)(16 * t + r) * io.hout_sf] = h1[t][r];
     }
-    split_acc(h1, h1s[hb]);
+  }
+  KS h1s[HB];
+#pragma unroll
+  for (int kb = 0; kb < HB; ++kb) split_pair(h1[2 * kb], h1[2 * kb + 1], h1s[kb]);
+  if (p.dbg == 4) {
+    if (h1[0][0] + h1[TH - 1][3] == 12345.f) io.qsel_out[e] = eps;
+    return;
   }
 
-  // ---- Q head
-  f32x16 qa[AB];
+  // ---- Q head (only the 16-row tiles that hold real actions)
+  f32x4 qa[AT];
 #pragma unroll
-  for (int ab = 0; ab < AB; ++ab) {
-    qa[ab] = load_bias(W + CG::off_bq + ab * 32, hh);
+  for (int t = 0; t < AT; ++t) {
+    qa[t] = bias4(W + CG::off_bq, t, g);
+    if (t < ATr) {
 #pragma unroll
-    for (int kb = 0; kb < HB; ++kb) mm_h3(W + CG::off_q + (ab * HB + kb) * 1024, h1s[kb], lane, qa[ab]);
+      for (int kb = 0; kb < HB; ++kb) mm16(W + CG::off_q + ((t >> 1) * HB + kb) * 1024, t & 1, h1s[kb], lane, qa[t]);
+    }
   }
-  q_epilogue<AB>(p, agent, e, valid, qa);
+  q_epilogue16<AT>(p, agent, e, valid, qa, eps, ctr);
 }
 
-// The LDS-staged large-E kernel on the fp16x3 image (see agent_q_fwd_lds_kernel).
+// The LDS-staged large-E kernel on the fp16x3 image: a 1024-thread block (16 waves x 16 envs = 256
+// envs of one agent) first DMAs the agent's image into LDS (global_load_lds_dwordx4, issued after
+// every global read of the wave so the latencies overlap), then runs the body. One block per CU.
 template <int F1, int G, int H, int AB>
-__global__ __launch_bounds__(512, 2) void agent_q_fwd_h3_kernel(QFwdParams p0, QFwdParams p1) {
+__global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdParams p0, QFwdParams p1) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];
   const bool second = (int)blockIdx.x >= p0.nblocks;
-  const QFwdParams& p = second ? p1 : p0;
+  // the selected net's parameters read straight from the kernarg segment (p0, p1 back to back):
+  // uniform scalar loads on demand instead of both structs held (and spilled) in SGPRs
+  const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  static_assert(sizeof(QFwdParams) % 8 == 0, "kernarg layout");
+  const QFwdParams& p = kargs[second ? 1 : 0];
+  (void)p1;
   const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
   const int agent = bid % p.N, tile = bid / p.N;
-  const int e = tile * 256 + (threadIdx.x >> 6) * 32 + (threadIdx.x & 31);
-  const float* orow = obs_row_ptr(p, agent, e);
-  float xn[16];
-  load_obs_kblock(orow, 0, p.D, xn);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int e = tile * 256 + wave * 16 + (lane & 15);
+  const int g = lane >> 4;
+  // weight image DMA first (no dependencies), then the wave's own global reads: the hidden state
+  // (independent of the reset flag: loaded unconditionally, zeroed after), the obs row index and
+  // the obs k-step 0 that depends on it. All latencies overlap before the barrier.
   const float* src = p.packed + (int64_t)p.N * p.g.agent_stride + (int64_t)agent * p.g.agent_stride;
   const int nchunk = (int)(p.g.agent_stride >> 8);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int c = wave; c < nchunk; c += 8)
+  for (int c = wave; c < nchunk; c += 16)
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 256 + lane * 4),
                                      (__attribute__((address_space(3))) void*)(wsm + c * 256), 16, 0, 0);
+  const mm_qfwd_io& io = p.io;
+  const int ec = min(e, p.E - 1);
+  f32x4 h0[H / 16];
+  if (io.h_in) {
+    const float* hp = io.h_in + (int64_t)ec * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)(4 * g) * io.hin_sf;
+#pragma unroll
+    for (int t = 0; t < H / 16; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h0[t][r] = hp[(int64_t)(16 * t + r) * io.hin_sf];
+  } else {
+#pragma unroll
+    for (int t = 0; t < H / 16; ++t) h0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool reset = io.reset && io.reset[ec];
+  const float* orow = obs_row_ptr(p, agent, e);
+  float xn[8];
+  load_obs_ks(orow, 0, p.D, xn);
+  const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
+  const uint64_t ctr = (io.mode == MM_Q_ACT && io.counter_ptr) ? *io.counter_ptr : io.counter;
+  if (e >= p.E || reset) {
+#pragma unroll
+    for (int t = 0; t < H / 16; ++t) h0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   __syncthreads();
-  if (wave >= 4)
+  if (p.dbg == 1) {   // debug timing: stop after the loads + image DMA
+    if (xn[0] + h0[0][0] == 12345.f) p.io.qsel_out[e] = eps;
+    return;
+  }
+  if (wave >= 8)
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(8);
-  agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm, orow, xn);
+  agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm, orow, xn, h0, eps, ctr);
 }
 
 // ---------------------------------------------------------------- packing
@@ -813,8 +988,8 @@ __global__ void qnet_pack_kernel(const float* __restrict__ params, float* __rest
   }
 }
 
-// fp16x3 image (packed + N*agent_stride): weight blocks as [s][part][lane][8 halves] (see
-// agent_q_fwd_body_h3); bias images identical to the fp32 image.
+// fp16x3 image (packed + N*agent_stride): weight blocks as [16-row half q][part][lane][8 halves]
+// (see agent_q_fwd_body_h3); bias vectors in natural order.
 __global__ void qnet_pack_h3_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
                                     int D, int F1, int G, int H, int A, QnetOffsets o) {
   const int64_t per_agent = g.agent_stride;
@@ -823,7 +998,7 @@ __global__ void qnet_pack_h3_kernel(const float* __restrict__ params, float* __r
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int agent = (int)(idx / per_agent);
-    int64_t r = idx % per_agent;
+    const int64_t r = idx % per_agent;
     uint32_t v = 0u;
     bool hit = false;
     auto wimg = [&](int64_t off, int KB, int rows, int cols, int64_t src) {
@@ -832,12 +1007,12 @@ __global__ void qnet_pack_h3_kernel(const float* __restrict__ params, float* __r
         const int64_t t = r - off;
         const int blk = (int)(t >> 10), w = (int)(t & 1023);
         const int kb = blk % KB, rb = blk / KB;
-        const int s = w >> 9, part = (w >> 8) & 1, lane = (w >> 2) & 63, dw = w & 3;
-        const int row = rb * 32 + (lane & 31);
+        const int q = w >> 9, part = (w >> 8) & 1, lane = (w >> 2) & 63, dw = w & 3;
+        const int row = rb * 32 + 16 * q + (lane & 15);
         uint32_t bits = 0u;
         for (int jj = 0; jj < 2; ++jj) {
           const int j = 2 * dw + jj;
-          const int col = kb * 32 + kperm(8 * s + j, lane >> 5);
+          const int col = kb * 32 + kperm16(j, lane >> 4);
           const float x = (row < rows && col < cols) ? params[src + (int64_t)row * cols + col] : 0.0f;
           const _Float16 hv = (_Float16)x;
           const _Float16 pv = part == 0 ? hv : (_Float16)(x - (float)hv);
@@ -847,12 +1022,27 @@ __global__ void qnet_pack_h3_kernel(const float* __restrict__ params, float* __r
         hit = true;
       }
     };
+    auto bnat = [&](int64_t off, int rows, int64_t src, int64_t src2) {
+      const int64_t sz = (int64_t)((rows + 31) / 32) * 32;
+      if (!hit && r >= off && r < off + sz) {
+        const int row = (int)(r - off);
+        const float x = row < rows ? params[src + row] + (src2 >= 0 ? params[src2 + row] : 0.0f) : 0.0f;
+        v = __float_as_uint(x);
+        hit = true;
+      }
+    };
     wimg(g.off_l1, g.KD, F1, D, o.W1 + (int64_t)agent * F1 * D);
     wimg(g.off_l2, F1 / 32, G, F1, o.W2 + (int64_t)agent * G * F1);
     wimg(g.off_ih, G / 32, 3 * H, G, o.Wih + (int64_t)agent * 3 * H * G);
     wimg(g.off_hh, H / 32, 3 * H, H, o.Whh + (int64_t)agent * 3 * H * H);
     wimg(g.off_q, H / 32, A, H, o.Wq + (int64_t)agent * A * H);
-    out[idx] = hit ? v : __float_as_uint(packed[idx]);  // biases / padding: copy of the fp32 image
+    bnat(g.off_b1, F1, o.b1 + (int64_t)agent * F1, -1);
+    bnat(g.off_b2, G, o.b2 + (int64_t)agent * G, -1);
+    bnat(g.off_brz, 2 * H, o.bih + (int64_t)agent * 3 * H, o.bhh + (int64_t)agent * 3 * H);
+    bnat(g.off_bin, H, o.bih + (int64_t)agent * 3 * H + 2 * H, -1);
+    bnat(g.off_bhn, H, o.bhh + (int64_t)agent * 3 * H + 2 * H, -1);
+    bnat(g.off_bq, A, o.bq + (int64_t)agent * A, -1);
+    out[idx] = v;
   }
 }
 
@@ -890,7 +1080,7 @@ static int launch_fwd(QFwdParams p0, const QFwdParams* p1in, hipStream_t s) {
     if (f32_exact)
       hipLaunchKernelGGL((agent_q_fwd_lds_kernel<F1, G, H, AB>), dim3(nb), dim3(512), sm, s, p0, p1);
     else
-      hipLaunchKernelGGL((agent_q_fwd_h3_kernel<F1, G, H, AB>), dim3(nb), dim3(512), sm, s, p0, p1);
+      hipLaunchKernelGGL((agent_q_fwd_h3_kernel<F1, G, H, AB>), dim3(nb), dim3(1024), sm, s, p0, p1);
   } else {
     const int nb = p0.nblocks + (p1in ? p1.nblocks : 0);
     hipLaunchKernelGGL((agent_q_fwd_kernel<F1, G, H, AB>), dim3(nb), dim3(256), 0, s, p0, p1);
@@ -915,6 +1105,8 @@ static int make_params(const mm_qnet_dims* d, const float* packed, const mm_qfwd
   p->nblocks = (int)((n_envs + 127) / 128) * d->n_agents;
   static const int stagger = getenv("MM_FWD_STAGGER") ? atoi(getenv("MM_FWD_STAGGER")) : 4;
   p->stagger = stagger;
+  static const int dbg = getenv("MM_FWD_DBG") ? atoi(getenv("MM_FWD_DBG")) : 0;
+  p->dbg = dbg;
   MM_REQUIRE(io->obs, "agent_q_fwd: obs required");
   MM_REQUIRE(io->h_in || io->reset == nullptr, "agent_q_fwd: h_in required");
   MM_REQUIRE(io->mode != MM_Q_GATHER || io->act_in, "agent_q_fwd: GATHER needs act_in");
