@@ -45,6 +45,7 @@ struct mm_per {
   double* tree;       // [2cap-1]
   int64_t* slot_row;  // [cap]
   void* alloc;
+  void* mb;           // multi-block insert scratch (MbScratch), power-of-two cap >= MB_MIN_CAP
 };
 
 namespace mm {
@@ -75,6 +76,35 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint32_t v, uint32_t* sh, ui
   *total = sh[PT - 1];
   __syncthreads();
   return incl - v;
+}
+
+// Exclusive scan / total of one value per thread over the PT threads: wave prefix by shuffles,
+// the 16 wave totals through LDS (two barriers instead of Hillis-Steele's 2 log2(PT)).
+__device__ __forceinline__ uint32_t block_excl_scan_w(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < PT / 64; ++w) {
+    const uint32_t x = wsum[w];
+    before += w < wave ? x : 0u;
+    tot += x;
+  }
+  *total = tot;
+  __syncthreads();
+  return before + incl - v;
+}
+__device__ __forceinline__ uint32_t block_sum_w(uint32_t v, uint32_t* wsum) {
+  uint32_t tot;
+  (void)block_excl_scan_w(v, wsum, &tot);
+  return tot;
 }
 
 __global__ __launch_bounds__(PT) void per_add_kernel(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
@@ -164,21 +194,25 @@ __global__ __launch_bounds__(PT) void per_add_kernel(double* tree, int64_t* slot
   if (threadIdx.x == 0) st->n_data = min(cap, n_data + K);
 }
 
-// Fast insert for a power-of-two capacity cap = PT * VPT (VPT <= 64): thread t keeps the VPT
-// contiguous leaves [t*VPT, (t+1)*VPT) in registers, so the 8 radix passes re-scan registers
-// instead of HBM, slot-ordered compaction is ONE block scan of per-thread counts, and the tree
-// rebuild is a register subtree per thread plus a 1024-leaf LDS top tree (same pairwise f64
-// sums as rebuild_tree, hence identical trees).
+// Fast insert for a power-of-two capacity cap = PT * VPT (VPT <= 64): thread t keeps the 16-bit
+// tops (sign, exponent, 4 mantissa bits) of its VPT contiguous leaves [t*VPT, (t+1)*VPT) in
+// registers. Selection of the rest-th smallest key without contended histograms: a 16-step binary
+// search on count(top <= mid) (every thread counts its registers, wave-shuffle block sums), then
+// the keys sharing the threshold's top (usually a few hundred) are staged in LDS and an 8-bit
+// radix select over their low 48 bits finds the exact key. Slot-ordered compaction is one block
+// scan of per-thread counts, and the tree rebuild is a register subtree per thread plus a
+// 1024-leaf LDS top tree (same pairwise f64 sums as rebuild_tree, hence identical trees).
 constexpr int FAST_MAX_VICTIMS = 8192;
+constexpr int FAST_MAX_CAND = 4096;   // keys sharing the threshold's 16-bit top staged in LDS
 
 template <int VPT>
 __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
                                                           const float* td, int64_t K, double eps,
-                                                          int64_t* rows_inout, int64_t* slots_out) {
-  __shared__ uint32_t hist[PT / 64][256];
+                                                          int64_t* rows_inout, int64_t* slots_out, int dbg) {
   __shared__ uint32_t binsum[256];
-  __shared__ uint32_t scan_sh[PT];
+  __shared__ uint32_t wsum[PT / 64];
   __shared__ int32_t victims[FAST_MAX_VICTIMS];
+  __shared__ uint64_t cand[FAST_MAX_CAND];
   __shared__ double top[PT];
   __shared__ uint64_t s_prefix;
   __shared__ int64_t s_need;
@@ -203,84 +237,121 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
       if ((i & 15) == 14) asm volatile("" ::: "memory");  // bound the loads in flight (VGPRs)
     }
     auto top16 = [&](int i) -> uint32_t { return (kp[i >> 1] >> ((i & 1) * 16)) & 0xffffu; };
-    // base pointer re-made opaque per pass so the VPT full-key loads are not hoisted out of the
-    // pass loop (they would pin 2*VPT VGPRs and spill)
+    if (dbg == 1) {
+      if (top16(0) == 0x1234 && top16(VPT - 1) == 0x4321) st->n_samples = 7;
+      return;
+    }
     const double* lv = leaves + s0;
     auto full = [&](int i) -> uint64_t { return (uint64_t)__double_as_longlong(lv[i]); };
-    if (t == 0) {
-      s_prefix = 0;
-      s_need = rest;
+    auto valid = [&](int i) -> bool { return s0 + i < n_data; };
+    // (1) the 16-bit top b of the rest-th smallest key: binary search on count(top16 <= mid), every
+    //     thread counting its VPT register keys (contention-free; 16 block sums)
+    uint32_t lo = 0, hi = 0xffffu;   // invariant: cnt_le(hi) >= rest
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      uint32_t c = 0;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) c += (valid(i) && top16(i) <= mid) ? 1u : 0u;
+      if ((int64_t)block_sum_w(c, wsum) >= rest) hi = mid;
+      else lo = mid + 1;
     }
-    for (int pass = 7; pass >= 0; --pass) {
-      for (int i = lane; i < 256; i += 64) hist[wave][i] = 0;
-      asm volatile("" : "+v"(lv));
+    const uint32_t b16 = lo;
+    uint32_t clt = 0, ceq = 0;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      clt += (valid(i) && top16(i) < b16) ? 1u : 0u;
+      ceq += (valid(i) && top16(i) == b16) ? 1u : 0u;
+    }
+    const int64_t n_lt16 = block_sum_w(clt, wsum);
+    uint32_t m;
+    const uint32_t cpos = block_excl_scan_w(ceq, wsum, &m);
+    int64_t need = rest - n_lt16;     // 1 <= need <= m among the keys whose top is b16
+    uint64_t prefix = (uint64_t)b16 << 48;
+    if (m <= (uint32_t)FAST_MAX_CAND) {
+      // (2) candidates' full keys into LDS, then an 8-bit radix select over their low 48 bits
+      uint32_t pos = cpos;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i)
+        if (valid(i) && top16(i) == b16) cand[pos++] = full(i);
       __syncthreads();
-      const int shift = pass * 8;
-      const uint64_t hi_mask = (pass == 7) ? 0ull : (~0ull << (shift + 8));
-      const uint64_t pre = s_prefix & hi_mask;
-      if (pass >= 6) {
-        const uint32_t pre16 = (uint32_t)(pre >> 48), mask16 = (uint32_t)(hi_mask >> 48);
-#pragma unroll
-        for (int i = 0; i < VPT; ++i) {
-          const uint32_t k = top16(i);
-          if ((k & mask16) == pre16) atomicAdd(&hist[wave][(k >> (shift - 48)) & 255], 1u);
+      for (int shift = 40; shift >= 0; shift -= 8) {
+        for (int i = t; i < 256; i += PT) binsum[i] = 0;
+        __syncthreads();
+        const uint64_t hmask = ~0ull << (shift + 8);
+        for (uint32_t i = t; i < m; i += PT) {
+          const uint64_t k = cand[i];
+          if ((k & hmask) == prefix) atomicAdd(&binsum[(k >> shift) & 255], 1u);
         }
-      } else {
-        const uint32_t pre16 = (uint32_t)(s_prefix >> 48);
-#pragma unroll
-        for (int i = 0; i < VPT; ++i)
-          if (top16(i) == pre16 && s0 + i < n_data) {
-            const uint64_t k = full(i);
-            if ((k & hi_mask) == pre) atomicAdd(&hist[wave][(k >> shift) & 255], 1u);
-          }
-      }
-      __syncthreads();
-      if (t < 256) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int w = 0; w < PT / 64; ++w) c += hist[w][t];
-        binsum[t] = c;
-      }
-      __syncthreads();
-      if (wave == 0) {
-        // wave 0 scans the 256 bins (4 per lane) and picks the bin holding the need-th key
-        uint32_t b4[4], loc = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          b4[q] = binsum[lane * 4 + q];
-          loc += b4[q];
-        }
-        uint32_t incl = loc;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t y = __shfl_up(incl, o);
-          if (lane >= o) incl += y;
-        }
-        const int64_t need = s_need;
-        const uint32_t excl = incl - loc;
-        int found = -1;
-        int64_t rem = 0;
-        if ((int64_t)excl < need && (int64_t)incl >= need) {
-          int64_t n2 = need - excl;
+        __syncthreads();
+        if (wave == 0) {
+          uint32_t b4[4], loc = 0;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            if (found < 0) {
-              if ((int64_t)b4[q] >= n2) {
-                found = lane * 4 + q;
-                rem = n2;
-              } else {
-                n2 -= b4[q];
+            b4[q] = binsum[lane * 4 + q];
+            loc += b4[q];
+          }
+          uint32_t incl = loc;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+          }
+          const uint32_t excl = incl - loc;
+          if ((int64_t)excl < need && (int64_t)incl >= need) {
+            int64_t n2 = need - excl;
+            int found = -1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (found < 0) {
+                if ((int64_t)b4[q] >= n2) found = lane * 4 + q;
+                else n2 -= b4[q];
               }
-            }
+            s_prefix = prefix | ((uint64_t)found << shift);
+            s_need = n2;
           }
         }
-        if (found >= 0) {
-          s_prefix |= ((uint64_t)found << shift);
-          s_need = rem;
-        }
+        __syncthreads();
+        prefix = s_prefix;
+        need = s_need;
+        __syncthreads();
       }
-      __syncthreads();
+    } else {
+      // many equal tops (e.g. near-identical priorities): the same radix passes on the full keys
+      // re-read from the leaves
+      for (int shift = 40; shift >= 0; shift -= 8) {
+        for (int i = t; i < 256; i += PT) binsum[i] = 0;
+        asm volatile("" : "+v"(lv));
+        __syncthreads();
+        const uint64_t hmask = ~0ull << (shift + 8);
+#pragma unroll
+        for (int i = 0; i < VPT; ++i)
+          if (valid(i) && top16(i) == b16) {
+            const uint64_t k = full(i);
+            if ((k & hmask) == prefix) atomicAdd(&binsum[(k >> shift) & 255], 1u);
+          }
+        __syncthreads();
+        if (t == 0) {
+          int64_t n2 = need;
+          int bb = 0;
+          for (; bb < 256; ++bb) {
+            if ((int64_t)binsum[bb] >= n2) break;
+            n2 -= binsum[bb];
+          }
+          s_prefix = prefix | ((uint64_t)bb << shift);
+          s_need = n2;
+        }
+        __syncthreads();
+        prefix = s_prefix;
+        need = s_need;
+        __syncthreads();
+      }
     }
+    if (t == 0) {
+      s_prefix = prefix;
+      s_need = need;
+    }
+    __syncthreads();
+    if (dbg == 2) return;
     const uint64_t T = s_prefix;
     const uint32_t T16 = (uint32_t)(T >> 48);
     asm volatile("" : "+v"(lv));
@@ -302,8 +373,8 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
     }
     const uint32_t nlt = (uint32_t)__popcll(mlt), neq = (uint32_t)__popcll(meq);
     uint32_t tot;
-    const uint32_t lt0 = (uint32_t)block_excl_scan(nlt, scan_sh, &tot);
-    const uint32_t eq0 = (uint32_t)block_excl_scan(neq, scan_sh, &tot);
+    const uint32_t lt0 = block_excl_scan_w(nlt, wsum, &tot);
+    const uint32_t eq0 = block_excl_scan_w(neq, wsum, &tot);
     int64_t lt_rank = lt0, eq_rank = eq0;
     for (uint64_t m = mlt | meq; m; m &= m - 1) {
       const int i = __ffsll((unsigned long long)m) - 1;
@@ -318,6 +389,7 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
     }
     __syncthreads();
   }
+  if (dbg == 3) return;
   // priorities, slot assignment, row swap
   for (int64_t j = t; j < K; j += PT) {
     const int64_t slot = j < free_n ? n_data + j : (int64_t)victims[j - free_n];
@@ -330,6 +402,7 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
     }
   }
   __syncthreads();
+  if (dbg == 4) return;
   // rebuild: register subtree of the thread's VPT leaves, then the PT-leaf top tree in LDS
   double v[VPT / 2];
   int64_t lvl_nodes = cap >> 1;  // nodes on the current level (first: the leaves' parents)
@@ -444,6 +517,367 @@ __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t ca
   rebuild_tree(tree, cap);
 }
 
+
+// ---------------------------------------------------------------- multi-block batched insert
+// For large power-of-two capacities the single-workgroup insert is bound by one CU's memory
+// bandwidth over the whole tree. This path spreads every pass over cap/1024 workgroups
+// (seven stream-ordered launches, graph-capturable, same results as per_add_fast_kernel):
+//   1 hist1     12-bit histogram (sign + exponent) of the candidate keys, LDS then global
+//   2 hist2     every block finds the threshold's bin b1 from hist1, then histograms bits 51..40
+//               of the keys in b1
+//   3 cand      every block finds b2; keys with the 24-bit prefix (b1, b2) are appended to a list
+//   4 count     every block radix-selects the exact key T among the listed keys (LDS, 8-bit digits
+//               over bits 39..0) and counts its slots' keys < T and == T
+//   5 victims   slot-ordered compaction: block prefix of the counts + in-block scans
+//   6 write     priorities (td+eps)^alpha into free slots / victims, row swaps
+//   7 rebuild   1024-leaf subtrees in LDS per block; the last block (arrival ticket) builds the
+//               top levels, updates n_data and clears the histograms for the next insert
+constexpr int MB_T = 256, MB_VPT = 4, MB_SLOTS = MB_T * MB_VPT;   // 1024 slots per block
+constexpr int64_t MB_MIN_CAP = 16384;
+constexpr int MB_CAND_LDS = 4096;
+struct MbScratch {
+  uint32_t hist1[4096];
+  uint32_t hist2[4096];
+  uint32_t blk[2 * 1024];    // per block: (#key < T, #key == T)
+  uint32_t cand_n;
+  uint32_t ticket;
+  uint64_t tsel[2];          // (T, number of slots equal to T that are taken)
+  uint64_t cand[1];          // [cap] (reused as int64 victims after the select)
+};
+static size_t mb_bytes(int64_t cap) { return sizeof(MbScratch) + (size_t)cap * 8; }
+
+__device__ __forceinline__ uint64_t leaf_key(const double* leaves, int64_t s) {
+  return (uint64_t)__double_as_longlong(leaves[s]);
+}
+
+// block-wide exclusive scan of one u32 per thread (MB_T threads) + total
+__device__ __forceinline__ uint32_t mb_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < MB_T / 64; ++w) {
+    const uint32_t x = wsum[w];
+    before += w < wave ? x : 0u;
+    tot += x;
+  }
+  *total = tot;
+  __syncthreads();
+  return before + incl - v;
+}
+
+// Find the bin holding the need-th key of a 4096-bin histogram: returns bin, updates need to the
+// rank inside it. Every thread gets the result.
+__device__ __forceinline__ int mb_pick(const uint32_t* __restrict__ h, int64_t& need, uint32_t* wsum, int64_t* sh) {
+  uint32_t loc[16], sum = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    loc[i] = h[threadIdx.x * 16 + i];
+    sum += loc[i];
+  }
+  uint32_t tot;
+  const uint32_t before = mb_scan(sum, wsum, &tot);
+  if ((int64_t)before < need && (int64_t)(before + sum) >= need) {
+    int64_t n2 = need - before;
+    int bin = -1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (bin < 0) {
+        if ((int64_t)loc[i] >= n2) bin = threadIdx.x * 16 + i;
+        else n2 -= loc[i];
+      }
+    sh[0] = bin;
+    sh[1] = n2;
+  }
+  __syncthreads();
+  const int bin = (int)sh[0];
+  need = sh[1];
+  __syncthreads();
+  return bin;
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_hist1(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+                                                     int64_t K, MbScratch* mb) {
+  __shared__ uint32_t h[4096];
+  const int64_t n_data = st->n_data;
+  if (K - min(K, cap - n_data) <= 0) return;
+  const double* leaves = tree + (cap - 1);
+  for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    const int64_t sl = base + threadIdx.x + i * MB_T;
+    if (sl < n_data) atomicAdd(&h[leaf_key(leaves, sl) >> 52], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4096; i += MB_T)
+    if (h[i]) atomicAdd(&mb->hist1[i], h[i]);
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_hist2(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+                                                     int64_t K, MbScratch* mb) {
+  __shared__ uint32_t h[4096];
+  __shared__ uint32_t wsum[MB_T / 64];
+  __shared__ int64_t sh[2];
+  const int64_t n_data = st->n_data;
+  int64_t need = K - min(K, cap - n_data);
+  if (need <= 0) return;
+  const int b1 = mb_pick(mb->hist1, need, wsum, sh);
+  const double* leaves = tree + (cap - 1);
+  for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    const int64_t sl = base + threadIdx.x + i * MB_T;
+    if (sl < n_data) {
+      const uint64_t k = leaf_key(leaves, sl);
+      if ((int)(k >> 52) == b1) atomicAdd(&h[(k >> 40) & 4095], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4096; i += MB_T)
+    if (h[i]) atomicAdd(&mb->hist2[i], h[i]);
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_cand(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+                                                    int64_t K, MbScratch* mb) {
+  __shared__ uint32_t wsum[MB_T / 64];
+  __shared__ int64_t sh[2];
+  const int64_t n_data = st->n_data;
+  int64_t need = K - min(K, cap - n_data);
+  if (need <= 0) return;
+  const uint64_t b1 = (uint64_t)mb_pick(mb->hist1, need, wsum, sh);
+  const uint64_t b2 = (uint64_t)mb_pick(mb->hist2, need, wsum, sh);
+  const uint64_t pre = (b1 << 12) | b2;
+  const double* leaves = tree + (cap - 1);
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    const int64_t sl = base + threadIdx.x + i * MB_T;
+    if (sl < n_data) {
+      const uint64_t k = leaf_key(leaves, sl);
+      if ((k >> 40) == pre) mb->cand[atomicAdd(&mb->cand_n, 1u)] = k;
+    }
+  }
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_count(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+                                                     int64_t K, MbScratch* mb, uint64_t* Tout) {
+  __shared__ uint64_t cl[MB_CAND_LDS];
+  __shared__ uint32_t bins[256];
+  __shared__ uint32_t wsum[MB_T / 64];
+  __shared__ int64_t sh[2];
+  const int64_t n_data = st->n_data;
+  int64_t need = K - min(K, cap - n_data);
+  if (need <= 0) return;
+  const uint64_t b1 = (uint64_t)mb_pick(mb->hist1, need, wsum, sh);
+  const uint64_t b2 = (uint64_t)mb_pick(mb->hist2, need, wsum, sh);
+  uint64_t prefix = ((b1 << 12) | b2) << 40;
+  const uint32_t m = mb->cand_n;
+  const bool in_lds = m <= (uint32_t)MB_CAND_LDS;
+  if (in_lds)
+    for (uint32_t i = threadIdx.x; i < m; i += MB_T) cl[i] = mb->cand[i];
+  __syncthreads();
+  const uint64_t* cs = in_lds ? cl : mb->cand;
+  for (int shift = 32; shift >= 0; shift -= 8) {
+    for (int i = threadIdx.x; i < 256; i += MB_T) bins[i] = 0;
+    __syncthreads();
+    const uint64_t hmask = ~0ull << (shift + 8);
+    for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
+      const uint64_t k = cs[i];
+      if ((k & hmask) == prefix) atomicAdd(&bins[(k >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    const uint32_t v = bins[threadIdx.x];
+    uint32_t tot;
+    const uint32_t before = mb_scan(v, wsum, &tot);
+    if ((int64_t)before < need && (int64_t)(before + v) >= need) {
+      sh[0] = threadIdx.x;
+      sh[1] = need - before;
+    }
+    __syncthreads();
+    prefix |= (uint64_t)sh[0] << shift;
+    need = sh[1];
+    __syncthreads();
+  }
+  const uint64_t T = prefix;   // the rest-th smallest key; take the first `need` slots equal to it
+  const double* leaves = tree + (cap - 1);
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS + threadIdx.x * MB_VPT;
+  uint32_t lt = 0, eq = 0;
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    const int64_t sl = base + i;
+    if (sl < n_data) {
+      const uint64_t k = leaf_key(leaves, sl);
+      lt += k < T ? 1u : 0u;
+      eq += k == T ? 1u : 0u;
+    }
+  }
+  uint32_t tlt, teq;
+  (void)mb_scan(lt, wsum, &tlt);
+  (void)mb_scan(eq, wsum, &teq);
+  if (threadIdx.x == 0) {
+    mb->blk[2 * blockIdx.x] = tlt;
+    mb->blk[2 * blockIdx.x + 1] = teq;
+    if (blockIdx.x == 0) {
+      Tout[0] = T;
+      Tout[1] = (uint64_t)need;
+    }
+  }
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_victims(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+                                                       int64_t K, MbScratch* mb, const uint64_t* Tin) {
+  __shared__ uint32_t wsum[MB_T / 64];
+  const int64_t n_data = st->n_data;
+  if (K - min(K, cap - n_data) <= 0) return;
+  const uint64_t T = Tin[0];
+  const int64_t take_eq = (int64_t)Tin[1];
+  int64_t lt_before = 0, eq_before = 0;
+  for (unsigned b = 0; b < blockIdx.x; ++b) {
+    lt_before += mb->blk[2 * b];
+    eq_before += mb->blk[2 * b + 1];
+  }
+  const double* leaves = tree + (cap - 1);
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS + threadIdx.x * MB_VPT;
+  uint64_t k[MB_VPT];
+  uint32_t lt = 0, eq = 0;
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    k[i] = base + i < n_data ? leaf_key(leaves, base + i) : ~0ull;
+    lt += k[i] < T ? 1u : 0u;
+    eq += k[i] == T ? 1u : 0u;
+  }
+  uint32_t tot;
+  int64_t lt_rank = lt_before + mb_scan(lt, wsum, &tot);
+  int64_t eq_rank = eq_before + mb_scan(eq, wsum, &tot);
+  int64_t* victims = reinterpret_cast<int64_t*>(mb->cand);
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    if (k[i] < T) {
+      victims[lt_rank + min(eq_rank, take_eq)] = base + i;
+      ++lt_rank;
+    } else if (k[i] == T) {
+      if (eq_rank < take_eq) victims[lt_rank + eq_rank] = base + i;
+      ++eq_rank;
+    }
+  }
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_write(double* tree, int64_t* slot_row, int64_t cap, const PerDev* st,
+                                                     const float* td, int64_t K, double eps, int64_t* rows_inout,
+                                                     int64_t* slots_out, const MbScratch* mb) {
+  const int64_t j = (int64_t)blockIdx.x * MB_T + threadIdx.x;
+  if (j >= K) return;
+  const int64_t n_data = st->n_data;
+  const int64_t free_n = min(K, cap - n_data);
+  const int64_t* victims = reinterpret_cast<const int64_t*>(mb->cand);
+  const int64_t slot = j < free_n ? n_data + j : victims[j - free_n];
+  tree[cap - 1 + slot] = pow((double)td[j] + eps, st->alpha);
+  if (slots_out) slots_out[j] = slot;
+  if (rows_inout) {
+    const int64_t old = slot_row[slot];
+    slot_row[slot] = rows_inout[j];
+    rows_inout[j] = old;
+  }
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_rebuild(double* tree, int64_t cap, PerDev* st, int64_t K,
+                                                       MbScratch* mb) {
+  __shared__ double v[2][MB_SLOTS / 2];
+  __shared__ uint32_t s_last;
+  const int L = 63 - __clzll((unsigned long long)cap);      // leaves at level L
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+  const double* leaves = tree + (cap - 1);
+  // levels L-1 .. L-10: node i of level l at heap index 2^l - 1 + i; this block owns i in
+  // [blockIdx * n, (blockIdx + 1) * n) with n = 2^(l - (L - 10)); LDS ping-pong between levels
+  {
+    const int64_t o = ((int64_t)1 << (L - 1)) - 1 + (int64_t)blockIdx.x * (MB_SLOTS / 2);
+    for (int i = threadIdx.x; i < MB_SLOTS / 2; i += MB_T) {
+      const double2 x = *reinterpret_cast<const double2*>(leaves + base + 2 * i);
+      v[0][i] = x.x + x.y;
+      tree[o + i] = v[0][i];
+    }
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int n = MB_SLOTS / 4, l = L - 2; n >= 1; n >>= 1, --l) {
+    const int64_t o = ((int64_t)1 << l) - 1 + (int64_t)blockIdx.x * n;
+    for (int i = threadIdx.x; i < n; i += MB_T) {
+      const double x = v[cur][2 * i] + v[cur][2 * i + 1];
+      v[cur ^ 1][i] = x;
+      tree[o + i] = x;
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+  // arrival ticket: the last block builds the levels above the per-block roots
+  __threadfence();
+  if (threadIdx.x == 0) s_last = atomicAdd(&mb->ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const int G = gridDim.x, lg = L - 10;                     // G = 2^lg roots at level lg (G <= 1024)
+  double* w = &v[0][0];
+  for (int i = threadIdx.x; i < G; i += MB_T)
+    w[i] = __hip_atomic_load(&tree[((int64_t)1 << lg) - 1 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  for (int n = G / 2, l = lg - 1; n >= 1; n >>= 1, --l) {
+    double x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = threadIdx.x + q * MB_T;
+      x[q] = i < n ? w[2 * i] + w[2 * i + 1] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = threadIdx.x + q * MB_T;
+      if (i < n) {
+        w[i] = x[q];
+        tree[((int64_t)1 << l) - 1 + i] = x[q];
+      }
+    }
+    __syncthreads();
+  }
+  // next insert starts from clear histograms / list / ticket
+  for (int i = threadIdx.x; i < 4096; i += MB_T) {
+    mb->hist1[i] = 0;
+    mb->hist2[i] = 0;
+  }
+  if (threadIdx.x == 0) {
+    mb->cand_n = 0;
+    mb->ticket = 0;
+    st->n_data = min(cap, st->n_data + K);
+  }
+}
+
+static int per_insert_mb(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out,
+                         hipStream_t s) {
+  const int64_t cap = per->cap;
+  const int G = (int)(cap / MB_SLOTS);
+  MbScratch* mb = static_cast<MbScratch*>(per->mb);
+  uint64_t* tsel = mb->tsel;
+  hipLaunchKernelGGL(per_mb_hist1, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
+  hipLaunchKernelGGL(per_mb_hist2, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
+  hipLaunchKernelGGL(per_mb_cand, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
+  hipLaunchKernelGGL(per_mb_count, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, tsel);
+  hipLaunchKernelGGL(per_mb_victims, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, tsel);
+  hipLaunchKernelGGL(per_mb_write, dim3((int)((k + MB_T - 1) / MB_T)), dim3(MB_T), 0, s, per->tree, per->slot_row,
+                     cap, per->st, td, k, per->eps, rows_inout, slots_out, mb);
+  hipLaunchKernelGGL(per_mb_rebuild, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
 }  // namespace mm
 
 extern "C" {
@@ -486,6 +920,15 @@ int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, d
     mm::set_error("per_create: init failed");
     return MM_EHIP;
   }
+  p->mb = nullptr;
+  if ((capacity & (capacity - 1)) == 0 && capacity >= mm::MB_MIN_CAP && capacity <= (1ll << 20)) {
+    if (hipMalloc(&p->mb, mm::mb_bytes(capacity)) != hipSuccess || hipMemset(p->mb, 0, mm::mb_bytes(capacity)) != hipSuccess) {
+      (void)hipFree(base);
+      delete p;
+      mm::set_error("per_create: scratch allocation failed");
+      return MM_ENOMEM;
+    }
+  }
   *out = p;
   return MM_OK;
 }
@@ -493,6 +936,7 @@ int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, d
 void mm_per_destroy(mm_per* per) {
   if (!per) return;
   (void)hipFree(per->alloc);
+  if (per->mb) (void)hipFree(per->mb);
   delete per;
 }
 
@@ -509,11 +953,16 @@ int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, 
   const int64_t cap = per->cap;
   const bool pow2 = (cap & (cap - 1)) == 0;
   const int64_t vpt = cap / mm::PT;
-  if (pow2 && cap >= 2 * mm::PT && vpt <= 64 && k <= mm::FAST_MAX_VICTIMS) {
+  static const int dbg = getenv("MM_PER_DBG") ? atoi(getenv("MM_PER_DBG")) : 0;  // debug timing
+  static const bool single_wg = getenv("MM_PER_SINGLE") && atoi(getenv("MM_PER_SINGLE"));  // A/B
+  if (per->mb && !single_wg) {
+    const int rc = mm::per_insert_mb(per, td, k, rows_inout, slots_out, (hipStream_t)s);
+    if (rc) return rc;
+  } else if (pow2 && cap >= 2 * mm::PT && vpt <= 64 && k <= mm::FAST_MAX_VICTIMS) {
 #define MM_PER_FAST(V)                                                                                        \
   case V:                                                                                                     \
     hipLaunchKernelGGL(mm::per_add_fast_kernel<V>, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree,      \
-                       per->slot_row, cap, per->st, td, k, per->eps, rows_inout, slots_out);                 \
+                       per->slot_row, cap, per->st, td, k, per->eps, rows_inout, slots_out, dbg);            \
     break;
     switch (vpt) {
       MM_PER_FAST(2)

@@ -154,7 +154,9 @@ def test_per_golden_sequence_single_inserts(golden, flavor):
 @pytest.mark.parametrize("flavor,cap,kb,rounds", [("vdn", 1000, 700, 7), ("qmix", 4099, 700, 7),
                                                   # power-of-two capacities: register-resident fast insert
                                                   ("vdn", 2048, 700, 7), ("qmix", 8192, 3000, 6),
-                                                  ("qmix", 65536, 8192, 10)])
+                                                  # >= 16384: the multi-block insert
+                                                  ("qmix", 65536, 8192, 10), ("vdn", 16384, 5000, 8),
+                                                  ("qmix", 32768, 4096, 12)])
 def test_per_batched_vs_oracle(flavor, cap, kb, rounds):
     dev, ora = _per_pair(flavor, cap)
     rng = np.random.default_rng(1)
@@ -162,6 +164,8 @@ def test_per_batched_vs_oracle(flavor, cap, kb, rounds):
         td = (rng.random(kb) * 3).astype(np.float32)
         if rnd == rounds - 2:
             td[:50] = td[50]                       # ties
+        if cap == 32768 and rnd in (3, 4, 5, 6, 7, 8, 9):
+            td[:] = 0.5                            # whole rounds of equal priorities (huge tie sets)
         slots = dev.add(torch.tensor(td))
         oslots = ora.add_batch([float(x) for x in td])
         np.testing.assert_array_equal(slots.cpu().numpy(), oslots)
