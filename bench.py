@@ -259,7 +259,7 @@ def main():
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_source": os.path.basename(prof[-1]) if traffic else None,
                 "kernel": f"{kname}<64,64,64,1> (dual: target+behavior)", "kernel_us": round(t_fwd * 1e6, 2),
-                "arith": "fp32 network FLOPs as fp16x3-split MFMA (v_mfma_f32_32x32x16_f16 x3, fp32 accumulate)"
+                "arith": "fp32 network FLOPs as fp16x3-split MFMA (v_mfma_f32_16x16x32_f16 x3, fp32 accumulate)"
                          if h3 else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
                 "fp32_native_peak": PEAK_FP32_TFLOPS, "frac_of_fp32_native_peak": round(achieved / PEAK_FP32_TFLOPS, 4),
                 "flop_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
