@@ -150,6 +150,11 @@ int mm_per_sample(mm_per* per, int32_t batch, const double* fracs, int64_t* node
 /* Same with device-generated fractions from a counter RNG. */
 int mm_per_sample_rng(mm_per* per, int32_t batch, uint64_t seed, uint64_t counter, int64_t* nodes_out,
                       int64_t* slots_out, float* is_w, mm_stream_t s);
+/* Uniform replay of whole stored chunks (the minimal QMIX's ReplayBuffer.sample_chunk,
+ * qmix/qmix.py:19-46, draws uniformly): B slots uniform over the filled slots (device counter RNG,
+ * a fresh stream per call), is_w (may be NULL) = 1. Priorities are not read. */
+int mm_per_sample_uniform(mm_per* per, int32_t batch, uint64_t seed, uint64_t counter, int64_t* slots_out,
+                          float* is_w, mm_stream_t s);
 /* Priority update leaf(nodes[b]) = (td[b]+eps)^alpha; duplicate nodes: last sample index wins. */
 int mm_per_update(mm_per* per, const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s);
 double* mm_per_tree_ptr(mm_per* per);               /* device f64 [2*cap-1] */
@@ -223,6 +228,16 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
 int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
                  const mm_mix_net* nets, int32_t n_nets, mm_stream_t s);
 /* TD loss terms and their gradient seeds (reference quirks: bootstrap x N, IS weight on the target). */
+/* Loss variants for mm_lrn_loss_ex (flags, OR-ed):
+ *   MM_LOSS_MIX_SUM     Q_tot = sum_i Q_i (VDN, vdn/_train.py:23-47)
+ *   MM_LOSS_HUBER       smooth_l1 (beta 1) instead of MSE (qmix/qmix.py:218)
+ *   MM_LOSS_TARGET_SUM  y = sum_i r_i + gamma*(1-d)*Q'_tot, no IS weight (qmix/qmix.py:215-217)
+ * (0 = Train_dqn: y = w * sum_i (r_i + gamma*(1-d)*Q'_tot), MSE, qmix/_train.py:80-82). */
+enum { MM_LOSS_MIX_SUM = 1, MM_LOSS_HUBER = 2, MM_LOSS_TARGET_SUM = 4 };
+int mm_lrn_loss_ex(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, const float* done,
+                   const float* isw, const float* qtot, const float* qtot_t, int32_t flags, const float* qa,
+                   const float* maxq, float* dq, float* dqa, float* loss_parts, float* td_last, float* loss,
+                   mm_stream_t s);
 int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, const float* done, const float* isw,
                 const float* qtot, const float* qtot_t, int32_t mix_sum, const float* qa, const float* maxq,
                 float* dq, float* dqa, float* loss_parts, float* td_last, float* loss, mm_stream_t s);
@@ -258,6 +273,10 @@ typedef struct mm_tmv_args {
 int mm_tmv(const mm_tmv_args* x, mm_stream_t s);
 /* Global-norm clip (torch clip_grad_norm_ over G[0:n_clip]) scaled by grad_scale (1/world after an
  * all-reduce), then Adam on P[0:n]; step is a device counter, norm_out receives the pre-clip norm. */
+/* clip_grad_norm_ on G[0:split] and on G[split:n] separately (qmix/qmix.py:235-238), then Adam. */
+int mm_clip2_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t split, float max_norm, float lr,
+                  float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, float grad_scale,
+                  mm_stream_t s);
 int mm_clip_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip, float max_norm, float lr,
                  float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, float grad_scale,
                  mm_stream_t s);

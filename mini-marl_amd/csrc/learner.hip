@@ -278,10 +278,13 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixFwdArgs a) {
 // y = w * sum_i (r_i + gamma*(1-d)*Q'tot)   (qmix/_train.py:80-82, vdn/_train.py:76-77)
 // dQtot = 2 (Qtot - y) / B ;  loss = sum_t mean_b (y - Qtot)^2 ;  td = |y - Qtot| at t = C-1.
 // VDN (mix_sum): Qtot = sum_i qa_i, Q'tot = sum_i maxq'_i, dqa_i = dQtot.
+// flags: MM_LOSS_MIX_SUM (VDN), MM_LOSS_HUBER (smooth_l1, beta 1: qmix/qmix.py:218),
+// MM_LOSS_TARGET_SUM (y = sum_i r_i + gamma*(1-d)*Q'tot: qmix/qmix.py:215-217, no xN, no IS weight).
 __global__ void lrn_loss_kernel(int B, int C, int N, float gamma, const float* rew, const float* done,
-                                const float* isw, const float* qtot, const float* qtot_t, int mix_sum,
+                                const float* isw, const float* qtot, const float* qtot_t, int flags,
                                 const float* qa, const float* maxq, float* dq, float* dqa, float* loss_parts,
                                 float* td_last) {
+  const int mix_sum = flags & MM_LOSS_MIX_SUM;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * C) return;
   const int b = i % B, t = i / B;
@@ -297,16 +300,31 @@ __global__ void lrn_loss_kernel(int B, int C, int N, float gamma, const float* r
     qt = qtot[i];
     qn = qtot_t[i];
   }
-  const float boot = gamma * (1.0f - done[i]) * qn;
-  float acc = 0.f;
-  for (int k = 0; k < N; ++k) acc += rew[(int64_t)i * N + k] + boot;
-  const float y = isw[b] * acc;
+  float y;
+  if (flags & MM_LOSS_TARGET_SUM) {
+    float rs = 0.f;
+    for (int k = 0; k < N; ++k) rs += rew[(int64_t)i * N + k];
+    y = rs + gamma * qn * (1.0f - done[i]);
+  } else {
+    const float boot = gamma * (1.0f - done[i]) * qn;
+    float acc = 0.f;
+    for (int k = 0; k < N; ++k) acc += rew[(int64_t)i * N + k] + boot;
+    y = isw[b] * acc;
+  }
   const float diff = qt - y;
-  const float g = 2.0f * diff / (float)B;
+  float g, part;
+  if (flags & MM_LOSS_HUBER) {
+    const float ad = fabsf(diff);
+    g = (ad < 1.0f ? diff : copysignf(1.0f, diff)) / (float)B;
+    part = ad < 1.0f ? 0.5f * diff * diff : ad - 0.5f;
+  } else {
+    g = 2.0f * diff / (float)B;
+    part = diff * diff;
+  }
   dq[i] = g;
   if (mix_sum)
     for (int k = 0; k < N; ++k) dqa[(int64_t)i * N + k] = g;
-  loss_parts[i] = diff * diff;
+  loss_parts[i] = part;
   if (t == C - 1) td_last[b] = fabsf(diff);
 }
 
@@ -719,24 +737,33 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* G, int64_t n, f
     __syncthreads();
   }
   if (threadIdx.x == 0) partials[blockIdx.x] = sh[0];
-  if (blockIdx.x == 0 && threadIdx.x == 0) *step += 1.0f;
+  if (step && blockIdx.x == 0 && threadIdx.x == 0) *step += 1.0f;
 }
 
 // torch.optim.Adam (no amsgrad / weight decay) with clip_grad_norm_ applied to G[0:n_clip]
+// With partials2 != null a second clip group [n_clip, n) uses its own norm (partials2) and coefficient
+// (qmix/qmix.py:235-238 clips the agent net and the mixer separately).
 __global__ __launch_bounds__(256) void adam_kernel(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip,
                                                    const float* partials, int n_part, float max_norm, float lr,
                                                    float b1, float b2, float eps, const float* step, float* norm_out,
-                                                   float grad_scale) {
-  __shared__ float s_coef;
+                                                   float grad_scale, const float* partials2) {
+  __shared__ float s_coef, s_coef2;
   if (threadIdx.x == 0) {
-    float tot = 0.f;
+    float tot = 0.f, tot2 = 0.f;
     for (int i = 0; i < n_part; ++i) tot += partials[i];
+    if (partials2)
+      for (int i = 0; i < n_part; ++i) tot2 += partials2[i];
     const float norm = sqrtf(tot) * grad_scale;
+    const float norm2 = sqrtf(tot2) * grad_scale;
     s_coef = max_norm > 0.f ? fminf(1.0f, max_norm / (norm + 1e-6f)) : 1.0f;
-    if (norm_out && blockIdx.x == 0) *norm_out = norm;
+    s_coef2 = (partials2 && max_norm > 0.f) ? fminf(1.0f, max_norm / (norm2 + 1e-6f)) : 1.0f;
+    if (norm_out && blockIdx.x == 0) {
+      norm_out[0] = norm;
+      if (partials2) norm_out[1] = norm2;
+    }
   }
   __syncthreads();
-  const float coef = s_coef;
+  const float coef = s_coef, coef2 = s_coef2;
   const float t = *step;
   const float bc1 = 1.0f - powf(b1, t);
   const float bc2 = 1.0f - powf(b2, t);
@@ -744,7 +771,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* P, float* G, float* m,
   const float bc2s = sqrtf(bc2);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float g = G[i] * grad_scale;
-    if (i < n_clip) g *= coef;
+    g *= i < n_clip ? coef : coef2;
     const float mi = m[i] + (g - m[i]) * (1.0f - b1);
     const float vi = v[i] * b2 + g * g * (1.0f - b2);
     m[i] = mi;
@@ -822,12 +849,28 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
   return MM_OK;
 }
 
+int mm_lrn_loss_ex(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, const float* done,
+                   const float* isw, const float* qtot, const float* qtot_t, int32_t flags, const float* qa,
+                   const float* maxq, float* dq, float* dqa, float* loss_parts, float* td_last, float* loss,
+                   mm_stream_t s) {
+  MM_REQUIRE(B > 0 && C > 0 && N > 0 && rew && done && dq && loss_parts && td_last && loss, "lrn_loss: bad args");
+  MM_REQUIRE((flags & MM_LOSS_MIX_SUM) ? (qa && maxq && dqa) : (qtot && qtot_t), "lrn_loss: missing Q inputs");
+  MM_REQUIRE((flags & MM_LOSS_TARGET_SUM) || isw, "lrn_loss: isw required");
+  const int n = B * C;
+  hipLaunchKernelGGL(mm::lrn_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, B, C, N, gamma, rew,
+                     done, isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts, td_last);
+  MM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(mm::lrn_loss_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, B, C, loss_parts, loss);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, const float* done, const float* isw,
                 const float* qtot, const float* qtot_t, int32_t mix_sum, const float* qa, const float* maxq,
                 float* dq, float* dqa, float* loss_parts, float* td_last, float* loss, mm_stream_t s) {
   const int n = B * C;
   hipLaunchKernelGGL(mm::lrn_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, B, C, N, gamma, rew,
-                     done, isw, qtot, qtot_t, mix_sum, qa, maxq, dq, dqa, loss_parts, td_last);
+                     done, isw, qtot, qtot_t, mix_sum ? MM_LOSS_MIX_SUM : 0, qa, maxq, dq, dqa, loss_parts, td_last);
   MM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(mm::lrn_loss_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, B, C, loss_parts, loss);
   MM_HIP_CHECK(hipGetLastError());
@@ -935,7 +978,27 @@ int mm_clip_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t n_cl
   MM_HIP_CHECK(hipGetLastError());
   const int nb2 = (int)std::min<int64_t>((n + 255) / 256, 2048);
   hipLaunchKernelGGL(mm::adam_kernel, dim3(nb2), dim3(256), 0, (hipStream_t)s, P, G, m, v, n, n_clip, partials, nb,
-                     max_norm, lr, beta1, beta2, eps, step, norm_out, grad_scale);
+                     max_norm, lr, beta1, beta2, eps, step, norm_out, grad_scale, (const float*)nullptr);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+// Two clip groups: clip_grad_norm_(G[0:split]) and clip_grad_norm_(G[split:n]) separately (same
+// max_norm), then Adam over P[0:n]; partials: >= 512 floats scratch; norm_out (may be null) gets
+// both norms.
+int mm_clip2_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t split, float max_norm, float lr,
+                  float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, float grad_scale,
+                  mm_stream_t s) {
+  MM_REQUIRE(P && G && m && v && step && partials && n > 0 && split >= 0 && split <= n, "clip2_adam: bad args");
+  const int nb = 256;
+  hipLaunchKernelGGL(mm::sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, G, split, partials, step);
+  MM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(mm::sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, G + split, n - split, partials + nb,
+                     (float*)nullptr);
+  MM_HIP_CHECK(hipGetLastError());
+  const int nb2 = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(mm::adam_kernel, dim3(nb2), dim3(256), 0, (hipStream_t)s, P, G, m, v, n, split, partials, nb,
+                     max_norm, lr, beta1, beta2, eps, step, norm_out, grad_scale, (const float*)(partials + nb));
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

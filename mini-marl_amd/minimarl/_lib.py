@@ -18,6 +18,7 @@ c_vp = ctypes.c_void_p
 
 MM_Q_NONE, MM_Q_ACT, MM_Q_MAX, MM_Q_GATHER = 0, 1, 2, 3
 MM_PER_VDN, MM_PER_QMIX = 0, 1
+MM_LOSS_MIX_SUM, MM_LOSS_HUBER, MM_LOSS_TARGET_SUM = 1, 2, 4
 
 
 class QnetDims(ctypes.Structure):
@@ -155,6 +156,8 @@ _SIGS += [
                             c_vp]),
     ("mm_lrn_loss", c_i32, [c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                             c_vp, c_vp, c_vp, c_vp]),
+    ("mm_lrn_loss_ex", c_i32, [c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
+                               c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_mixer_bwd", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp]),
     ("mm_agent_bwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -169,6 +172,9 @@ _SIGS += [
     ("mm_tmv", c_i32, [ctypes.POINTER(TmvArgs), c_vp]),
     ("mm_clip_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
                              c_vp, c_f32, c_vp]),
+    ("mm_clip2_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
+                              c_vp, c_f32, c_vp]),
+    ("mm_per_sample_uniform", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
 ]
 
 

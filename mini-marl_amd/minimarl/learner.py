@@ -7,6 +7,11 @@ agent params only, qmix/_train.py:111-115; VDN: all), Adam, priority update with
 last step's |y - Q_tot|. Everything is enqueued on the current HIP stream with no host
 sync, so an update can be captured as one HIP graph and replayed.
 
+Mode "qmix_min" is the minimal QMIX of ``qmix/qmix.py`` (``train``
+qmix/qmix.py:174-238): target Σ_i r_i + γ(1-d)Q'_tot (no xN, no IS weight), smooth-L1 loss,
+clip_grad_norm_ on the agent net and on the mixer separately, uniform chunk replay
+(``sample_uniform_and_grads``); its nets are QNet(D->128->32, GRUCell 32) and MixNet(hx 64).
+
 Parameters live in ONE flat fp32 buffer ``P = [agent theta | mixer phi]`` (grads,
 Adam moments alike), the layout the RCCL gradient all-reduce works on.
 """
@@ -16,7 +21,8 @@ import math
 import numpy as np
 import torch
 
-from ._lib import (MM_Q_GATHER, MM_Q_MAX, MixNetIO, OuterArgs, QFwdIO, TmvArgs, c_i64, check, lib)
+from ._lib import (MM_LOSS_HUBER, MM_LOSS_MIX_SUM, MM_LOSS_TARGET_SUM, MM_Q_GATHER, MM_Q_MAX, MixNetIO, OuterArgs,
+                   QFwdIO, TmvArgs, c_i64, check, lib)
 from .qnet import KEYS as AGENT_KEYS
 from .qnet import AgentQNet, ptr, stream_handle
 
@@ -84,16 +90,19 @@ class Mixer:
 
 
 class QLearner:
-    """mode "qmix" (Train_dqn) or "vdn" (Target_Dqn: Q_tot = sum_i Q_i, no mixer)."""
+    """mode "qmix" (Train_dqn), "vdn" (Target_Dqn: Q_tot = sum_i Q_i, no mixer) or "qmix_min"
+    (qmix/qmix.py train: Huber loss, unweighted sum target, separate agent / mixer clipping)."""
 
     def __init__(self, behavior, target, mixer=None, target_mixer=None, batch=32, chunk=10, gamma=0.99, lr=1e-3,
                  grad_clip=5.0, betas=(0.9, 0.999), adam_eps=1e-8, mode="qmix", clip_mixer=False, device="cuda"):
-        assert mode in ("qmix", "vdn")
+        assert mode in ("qmix", "vdn", "qmix_min")
         self.mode = mode
+        self.has_mixer = mode != "vdn"
+        self.loss_flags = {"qmix": 0, "vdn": MM_LOSS_MIX_SUM, "qmix_min": MM_LOSS_HUBER | MM_LOSS_TARGET_SUM}[mode]
         self.dev = torch.device(device)
         self.beh, self.tgt = behavior, target
         self.mix, self.tmix = mixer, target_mixer
-        if mode == "qmix":
+        if self.has_mixer:
             assert mixer is not None and target_mixer is not None
         self.B, self.C = int(batch), int(chunk)
         self.gamma, self.lr, self.clip = float(gamma), float(lr), float(grad_clip)
@@ -116,8 +125,8 @@ class QLearner:
         self.m = torch.zeros(self.n, device=self.dev)
         self.v = torch.zeros(self.n, device=self.dev)
         self.step_dev = torch.zeros(1, device=self.dev)
-        self.partials = torch.zeros(256, device=self.dev)
-        self.norm = torch.zeros(1, device=self.dev)
+        self.partials = torch.zeros(512, device=self.dev)
+        self.norm = torch.zeros(2, device=self.dev)
         self.n_clip = self.n if (mode == "vdn" or clip_mixer) else n_t
         self._alloc()
         self.updates = 0
@@ -157,7 +166,7 @@ class QLearner:
         self.dpre1 = torch.zeros(C, B, N, self.F1, **f32)
         self.nodes = torch.zeros(B, dtype=torch.int64, device=dev)
         self.slots = torch.zeros(B, dtype=torch.int64, device=dev)
-        if self.mode == "qmix":
+        if self.has_mixer:
             Hm, K1 = self.mix.Hm, self.mix.K1
             self.MSD = lib().mm_mixer_save_dim(Hm, K1, N)
             self.MDD = lib().mm_mixer_delta_dim(Hm, K1, N)
@@ -172,7 +181,7 @@ class QLearner:
         jobs = []
         zero = ctypes.c_void_p(0)
         self._agent_wgrad(None, None, zero, zero, C * B, jobs)
-        if self.mode == "qmix":
+        if self.has_mixer:
             self._mixer_wgrad(None, None, zero, zero, C * B, jobs)
         arr = (OuterArgs * len(jobs))(*jobs)
         self._opart = torch.zeros(int(lib().mm_outer_reduce_batch_partial(arr, len(jobs))), **f32)
@@ -218,7 +227,7 @@ class QLearner:
         obs_p = ctypes.c_void_p(obs_base) if isinstance(obs_base, int) else ptr(obs_base)
         reset_p = ctypes.c_void_p(reset_obs_ptr) if isinstance(reset_obs_ptr, int) else ptr(reset_obs_ptr)
         ND = N * D
-        if self.mode == "qmix":
+        if self.has_mixer:
             # mixer GRU input projections of every (t, b) for both mixers: one MFMA launch
             mx = self.mix
             check(L.mm_mixer_gi(CB, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, ptr(mx.flat), ptr(self.s_off),
@@ -255,7 +264,7 @@ class QLearner:
             it.qsel_out = self.maxq[t].data_ptr()
             check(L.mm_agent_q_rec2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
                                     ptr(self.tgt.packed), ctypes.byref(it), B, s), "learner fwd rec")
-            if self.mode == "qmix":
+            if self.has_mixer:
                 mx = self.mix
                 nets = (MixNetIO * 2)()
                 for k, (P, q, off, h, qt, sv, gi) in enumerate(
@@ -270,15 +279,15 @@ class QLearner:
                     n.save = sv.data_ptr() if sv is not None else None
                 check(L.mm_mixer_fwd(B, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, nets, 2, s), "mixer fwd")
         # ---- loss, dQ_tot, priorities
-        check(L.mm_lrn_loss(B, C, N, self.gamma, ptr(self.rew), ptr(self.done), ptr(self.isw), ptr(self.qtot),
-                            ptr(self.qtot_t), int(self.mode == "vdn"), ptr(self.qa), ptr(self.maxq), ptr(self.dq),
-                            ptr(self.dqa), ptr(self.loss_parts), ptr(self.td_last), ptr(self.loss), s), "loss")
+        check(L.mm_lrn_loss_ex(B, C, N, self.gamma, ptr(self.rew), ptr(self.done), ptr(self.isw), ptr(self.qtot),
+                               ptr(self.qtot_t), self.loss_flags, ptr(self.qa), ptr(self.maxq), ptr(self.dq),
+                               ptr(self.dqa), ptr(self.loss_parts), ptr(self.td_last), ptr(self.loss), s), "loss")
         # ---- backward through time (data-gradient chains only)
         o = self.beh.offs
         P = self.P
         for t in range(C - 1, -1, -1):
             dn = self.ones_f if t == C - 1 else self.done[t * B:(t + 1) * B]
-            if self.mode == "qmix":
+            if self.has_mixer:
                 mx = self.mix
                 check(L.mm_mixer_bwd(B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.msave[t]), ptr(self.qa[t]),
                                      ptr(self.dq[t]), ptr(dn), ptr(self.dhm), ptr(self.dqa[t]), ptr(self.mdelta[t]),
@@ -290,7 +299,7 @@ class QLearner:
         # outer product of the update (agent + mixer) in ONE split-M launch (+ its partial sum)
         jobs = []
         self._agent_wgrad(L, s, obs_p, reset_p, CB, jobs)
-        if self.mode == "qmix":
+        if self.has_mixer:
             self._mixer_wgrad(L, s, obs_p, reset_p, CB, jobs)
         arr = (OuterArgs * len(jobs))(*jobs)
         check(L.mm_outer_reduce_batch(arr, len(jobs), ptr(self._opart), self._opart.numel(), s), "outer batch")
@@ -299,9 +308,14 @@ class QLearner:
         """clip_grad_norm_ + Adam (grads scaled first, e.g. 1/world after an all-reduce), then repack
         the behavior fragments for the next forward."""
         s = stream_handle(self.dev)
-        check(lib().mm_clip_adam(ptr(self.P), ptr(self.Gr), ptr(self.m), ptr(self.v), self.n, self.n_clip,
-                                 self.clip, self.lr, self.b1, self.b2, self.aeps, ptr(self.step_dev),
-                                 ptr(self.partials), ptr(self.norm), float(grad_scale), s), "clip_adam")
+        if self.mode == "qmix_min":   # clip agent net and mixer separately (qmix/qmix.py:235-238)
+            check(lib().mm_clip2_adam(ptr(self.P), ptr(self.Gr), ptr(self.m), ptr(self.v), self.n, self.n_agent,
+                                      self.clip, self.lr, self.b1, self.b2, self.aeps, ptr(self.step_dev),
+                                      ptr(self.partials), ptr(self.norm), float(grad_scale), s), "clip2_adam")
+        else:
+            check(lib().mm_clip_adam(ptr(self.P), ptr(self.Gr), ptr(self.m), ptr(self.v), self.n, self.n_clip,
+                                     self.clip, self.lr, self.b1, self.b2, self.aeps, ptr(self.step_dev),
+                                     ptr(self.partials), ptr(self.norm), float(grad_scale), s), "clip_adam")
         self.beh.mark_dirty()
         self.beh.pack(s)
         self.updates += 1
@@ -398,6 +412,21 @@ class QLearner:
                                       ptr(self.isw), s), "per_sample_rng")
         self.gather(per, store)
         self.compute_grads(store.obs, reset_obs_ptr)
+
+    def sample_uniform_and_grads(self, per, store, reset_obs_ptr, seed=0, counter=0):
+        """Uniform chunk replay (qmix/qmix.py ReplayBuffer.sample_chunk) -> gather -> forward/backward."""
+        check(lib().mm_per_sample_uniform(per._h, self.B, seed, counter, ptr(self.slots), ptr(self.isw),
+                                          stream_handle(self.dev)), "per_sample_uniform")
+        self.gather(per, store)
+        self.compute_grads(store.obs, reset_obs_ptr)
+
+    def update_uniform(self, per, store, reset_obs_ptr, seed=0, counter=0, allreduce=None):
+        """One qmix/qmix.py train iteration from the device chunk store (no priority update)."""
+        self.sample_uniform_and_grads(per, store, reset_obs_ptr, seed, counter)
+        scale = 1.0
+        if allreduce is not None:
+            scale = 1.0 / allreduce(self.Gr)
+        self.apply_grads(scale)
 
     def apply_and_reprioritize(self, per, grad_scale=1.0):
         self.apply_grads(grad_scale)

@@ -30,6 +30,16 @@ _VDN_FMT = {
     "Wq": "action_net.{i}.0.weight", "bq": "action_net.{i}.0.bias",
 }
 
+# minimal QMIX QNet naming (qmix/qmix.py:102-131)
+_MIN_FMT = {
+    "W1": "agent_feature_{i}.0.weight", "b1": "agent_feature_{i}.0.bias",
+    "W2": "agent_feature_{i}.2.weight", "b2": "agent_feature_{i}.2.bias",
+    "Wih": "agent_gru_{i}.weight_ih", "Whh": "agent_gru_{i}.weight_hh",
+    "bih": "agent_gru_{i}.bias_ih", "bhh": "agent_gru_{i}.bias_hh",
+    "Wq": "agent_q_{i}.weight", "bq": "agent_q_{i}.bias",
+}
+_FMTS = {"qmix": _QMIX_FMT, "vdn": _VDN_FMT, "min": _MIN_FMT}
+
 
 def stream_handle(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
@@ -94,8 +104,9 @@ class AgentQNet:
         self.mark_dirty()
 
     def load_reference_state(self, sd, prefix="", style="qmix"):
-        """Load a reference Q_Net state_dict (dict name -> array/tensor)."""
-        fmt = _QMIX_FMT if style == "qmix" else _VDN_FMT
+        """Load a reference Q_Net / QNet state_dict (dict name -> array/tensor); style "qmix"
+        (qmix/_network.py), "vdn" (vdn/_network.py) or "min" (qmix/qmix.py)."""
+        fmt = _FMTS[style]
         host = torch.empty(self.n_params)
         for k in KEYS:
             parts = [torch.as_tensor(np.asarray(sd[prefix + fmt[k].format(i=i)]), dtype=torch.float32)
@@ -106,7 +117,7 @@ class AgentQNet:
         self.mark_dirty()
 
     def state_dict(self, style="qmix"):
-        fmt = _QMIX_FMT if style == "qmix" else _VDN_FMT
+        fmt = _FMTS[style]
         host = self.flat.detach().cpu()
         out = {}
         for k in KEYS:

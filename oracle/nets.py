@@ -32,6 +32,15 @@ _VDN_FMT = {
     "bih": "gru_net.{i}.bias_ih", "bhh": "gru_net.{i}.bias_hh",
     "Wq": "action_net.{i}.0.weight", "bq": "action_net.{i}.0.bias",
 }
+# minimal QMIX QNet (qmix/qmix.py:102-131): agent_feature_i = Linear(D,128) ReLU Linear(128,32) ReLU
+_MIN_FMT = {
+    "W1": "agent_feature_{i}.0.weight", "b1": "agent_feature_{i}.0.bias",
+    "W2": "agent_feature_{i}.2.weight", "b2": "agent_feature_{i}.2.bias",
+    "Wih": "agent_gru_{i}.weight_ih", "Whh": "agent_gru_{i}.weight_hh",
+    "bih": "agent_gru_{i}.bias_ih", "bhh": "agent_gru_{i}.bias_hh",
+    "Wq": "agent_q_{i}.weight", "bq": "agent_q_{i}.bias",
+}
+_FMTS = {"qmix": _QMIX_FMT, "vdn": _VDN_FMT, "min": _MIN_FMT}
 _MIX_FMT = {
     "gWih": "gru.weight_ih", "gWhh": "gru.weight_hh", "gbih": "gru.bias_ih", "gbhh": "gru.bias_hh",
     "w1W": "hyper_net_weight_1.weight", "w1b": "hyper_net_weight_1.bias",
@@ -50,8 +59,8 @@ def _n_agents(sd, fmt):
 
 
 def agent_from_state(sd, prefix="", style="qmix"):
-    """Stack a reference Q_Net state_dict (dict of arrays) into AGENT_KEYS tensors."""
-    fmt = _QMIX_FMT if style == "qmix" else _VDN_FMT
+    """Stack a reference Q_Net / QNet state_dict (dict of arrays) into AGENT_KEYS tensors."""
+    fmt = _FMTS[style]
     sd = {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
     n = _n_agents(sd, fmt)
     return {k: torch.tensor(np.stack([np.asarray(sd[f.format(i=i)]) for i in range(n)]), dtype=torch.float32)
@@ -260,6 +269,58 @@ def qmix_train_step(P, M, T, TM, batch, gamma, lr, grad_clip, adam_state=None, h
     newM = {k: new["m." + k] for k in MIXER_KEYS}
     new_td = (target - qtot.detach()).abs().view(-1)
     return newP, newM, g, loss.detach(), new_td
+
+
+def qmix_min_loss(P, M, T, TM, batch, gamma, hidden_dim=32):
+    """Minimal QMIX train inner loop, qmix/qmix.py:186-230 (recurrent, one iteration).
+
+    Differs from Train_dqn: target = sum_i r_i + gamma*Q'_tot*(1-d) (no xN, no IS weight,
+    :215-217) and smooth_l1 (:218). Hidden handling is the same: done rows reset to zero for the
+    agents (:221-225) and both mixers (:226-232); the target paths are detached.
+    """
+    s, a, r, s2, d = batch[:5]
+    B, C, N, _ = s.shape
+    H = P["Whh"].shape[2]
+    Hm = M["gWhh"].shape[1]
+    h = torch.zeros(B, N, H)
+    ht = torch.zeros(B, N, H)
+    hm = torch.zeros(B, Hm)
+    hmt = torch.zeros(B, Hm)
+    loss = 0.0
+    for t in range(C):
+        q, nh = agent_forward(P, s[:, t], h)
+        qa = q.gather(2, a[:, t].unsqueeze(-1).long()).squeeze(-1)
+        qtot, nhm = mixer_forward(M, qa, s[:, t], hm, hidden_dim)
+        tq, nht = agent_forward(T, s2[:, t], ht.detach())
+        tmax = tq.max(dim=2)[0]
+        tqtot, nhmt = mixer_forward(TM, tmax, s2[:, t], hmt.detach(), hidden_dim)
+        target = r[:, t].sum(dim=1, keepdim=True) + gamma * tqtot * (1 - d[:, t])
+        loss = loss + F.smooth_l1_loss(qtot, target.detach())
+        keep = (1.0 - d[:, t]).view(B, 1)
+        h = nh * keep.view(B, 1, 1)
+        ht = nht * keep.view(B, 1, 1)
+        hm = nhm * keep
+        hmt = nhmt * keep
+    return loss
+
+
+def qmix_min_train_step(P, M, T, TM, batch, gamma, lr, grad_clip=5.0, adam_state=None, hidden_dim=32):
+    """qmix/qmix.py:233-238: backward, clip_grad_norm_ on the agent net and on the mixer
+    separately, one Adam step over both (lr, default betas / eps 1e-8)."""
+    Pg = _requires(P)
+    Mg = _requires(M)
+    loss = qmix_min_loss(Pg, Mg, T, TM, batch, gamma, hidden_dim)
+    allp = [Pg[k] for k in AGENT_KEYS] + [Mg[k] for k in MIXER_KEYS]
+    grads = torch.autograd.grad(loss, allp)
+    ga, _ = clip_grad_norm(list(grads[:len(AGENT_KEYS)]), grad_clip)
+    gm, _ = clip_grad_norm(list(grads[len(AGENT_KEYS):]), grad_clip)
+    g = dict(zip(AGENT_KEYS, ga))
+    g.update(dict(zip(["m." + k for k in MIXER_KEYS], gm)))
+    state = {} if adam_state is None else adam_state
+    params = {k: P[k] for k in AGENT_KEYS}
+    params.update({"m." + k: M[k] for k in MIXER_KEYS})
+    new = adam_step(params, g, state, lr)
+    return ({k: new[k] for k in AGENT_KEYS}, {k: new["m." + k] for k in MIXER_KEYS}, g, loss.detach())
 
 
 def batch_from_fixture(fx):

@@ -58,7 +58,7 @@ def test_learner_matches_reference_update(golden, mode):
     np.testing.assert_allclose(float(L.loss.item()), float(fx["loss"]), rtol=1e-4)
     np.testing.assert_allclose(L.td_last.cpu().numpy(), fx["new_td"], rtol=1e-4, atol=1e-4)
     # gradients (the reference captured them after clip_grad_norm_; apply our clip coefficient)
-    norm = float(L.norm.item())
+    norm = float(L.norm[0].item())
     coef = min(1.0, float(fx["grad_clip"]) / (norm + 1e-6))
     N = P["W1"].shape[0]
 
@@ -118,7 +118,7 @@ def test_learner_gru64_vs_oracle():
     newP, newM, grads, loss, td = nets.qmix_train_step(P0, M0, T0, TM0, (st, act, rew, ns, dn, w), 0.99, 1e-3, 5.0)
     np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=1e-4)
     np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=1e-4, atol=1e-4)
-    coef = min(1.0, 5.0 / (float(L.norm.item()) + 1e-6))
+    coef = min(1.0, 5.0 / (float(L.norm[0].item()) + 1e-6))
     for key in nets.AGENT_KEYS:
         _check_grads(_grad_view(L, key).cpu().numpy() * coef, grads[key].numpy())
     for key in MIX_KEYS:
@@ -153,7 +153,7 @@ def test_learner_cfg5_shapes_vs_oracle():
     newP, newM, grads, loss, td = nets.qmix_train_step(P0, M0, T0, TM0, (st, act, rew, ns, dn, w), 0.99, 1e-3, 5.0)
     np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=1e-4)
     np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=1e-4, atol=1e-4)
-    coef = min(1.0, 5.0 / (float(L.norm.item()) + 1e-6))
+    coef = min(1.0, 5.0 / (float(L.norm[0].item()) + 1e-6))
     for key in nets.AGENT_KEYS:
         _check_grads(_grad_view(L, key).cpu().numpy() * coef, grads[key].numpy())
     for key in MIX_KEYS:
@@ -212,3 +212,62 @@ def test_learner_graph_replay_matches_eager():
     assert torch.equal(l1.P, l2.P)
     assert torch.equal(e1.per.tree(), e2.per.tree())
     assert torch.equal(l1.loss, l2.loss)
+
+
+def test_qmix_min_matches_reference_update(golden):
+    """Minimal QMIX (qmix/qmix.py train, row a15): QNet D->128->32 + GRU-32, MixNet hx 64, Huber loss,
+    unweighted sum target, separate agent / mixer clipping; one update vs the reference's."""
+    from minimarl.learner import MIX_KEYS, Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    fx = golden("qmix_min_train")
+    N, D, A, B, C = (int(x) for x in fx["meta"])
+    gamma, lr = (float(x) for x in fx["gamma_lr"])
+    beh = AgentQNet(N, D, A, 128, 32, 32, DEV)
+    beh.load_reference_state(fx, "q.", "min")
+    tgt = AgentQNet(N, D, A, 128, 32, 32, DEV)
+    tgt.load_reference_state(fx, "qt.", "min")
+    mix, tmix = Mixer(N, N * D, 64, 32, DEV), Mixer(N, N * D, 64, 32, DEV)
+    mix.load_reference_state(fx, "m.")
+    tmix.load_reference_state(fx, "mt.")
+    L = QLearner(beh, tgt, mix, tmix, batch=B, chunk=C, gamma=gamma, lr=lr, grad_clip=5.0, mode="qmix_min",
+                 device=DEV)
+    L.load_batch(fx["s"], fx["a"], fx["r"], fx["s2"], fx["done"], np.ones((B, 1), np.float32))
+    L.train_step(L._obs_buf, L._obs_buf)
+    torch.cuda.synchronize()
+    na, nm = (float(x) for x in L.norm.cpu())
+    ca, cm = min(1.0, 5.0 / (na + 1e-6)), min(1.0, 5.0 / (nm + 1e-6))
+    gref = nets.agent_from_state(fx, "grad.q.", "min")
+    post = nets.agent_from_state(fx, "post.q.", "min")
+    for key in nets.AGENT_KEYS:
+        g_ref = gref[key].numpy()
+        _check_grads(_grad_view(L, key).cpu().numpy() * ca, g_ref)
+        sel = np.abs(g_ref) > 1e-4 * np.abs(g_ref).max()
+        np.testing.assert_allclose(L.beh.view(key).cpu().numpy()[sel], post[key].numpy()[sel], atol=2e-6)
+    gmref = nets.mixer_from_state(fx, "grad.m.")
+    postM = nets.mixer_from_state(fx, "post.m.")
+    for key in MIX_KEYS:
+        g_ref = gmref[key].numpy()
+        _check_grads(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy() * cm, g_ref)
+        sel = np.abs(g_ref) > 1e-4 * np.abs(g_ref).max()
+        np.testing.assert_allclose(L.mix.view(key).cpu().numpy()[sel], postM[key].numpy()[sel], atol=2e-6)
+
+
+def test_qmix_min_uniform_replay_from_engine():
+    """qmix_min updates from the device chunk store with uniform chunk sampling (no priorities)."""
+    from minimarl.engine import RolloutEngine
+    from minimarl.learner import Mixer, QLearner
+    E, N = 128, 4
+    eng = RolloutEngine(E, N, f1=128, g=32, h=32, chunk=10, capacity=512, seed=5, device=DEV)
+    for _ in range(3):
+        eng.run_graph(0.5)
+    mix, tmix = Mixer(N, N * eng.D, 64, 32, DEV, seed=1), Mixer(N, N * eng.D, 64, 32, DEV, seed=1)
+    L = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix_min", device=DEV)
+    tree0 = eng.per.tree().clone()
+    p0 = L.P.clone()
+    for k in range(3):
+        L.update_uniform(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=3, counter=k)
+    torch.cuda.synchronize()
+    assert np.isfinite(L.loss.item()) and not torch.equal(p0, L.P)
+    assert torch.equal(tree0, eng.per.tree())          # uniform replay leaves priorities alone
+    slots = L.slots.cpu().numpy()
+    assert slots.min() >= 0 and slots.max() < len(eng.per)

@@ -114,6 +114,33 @@ def test_qmix_train_step(golden):
     np.testing.assert_allclose(new_td.numpy(), fx["new_td"], rtol=1e-4, atol=1e-4)
 
 
+def _qmix_min_fixture(golden):
+    fx = golden("qmix_min_train")
+    P = nets.agent_from_state(fx, "q.", "min")
+    T = nets.agent_from_state(fx, "qt.", "min")
+    M = nets.mixer_from_state(fx, "m.")
+    TM = nets.mixer_from_state(fx, "mt.")
+    batch = tuple(torch.tensor(fx[k]) for k in ("s", "a", "r", "s2", "done"))
+    gamma, lr = (float(x) for x in fx["gamma_lr"])
+    return fx, P, T, M, TM, batch, gamma, lr
+
+
+def test_qmix_min_train_step(golden):
+    """Oracle of the minimal QMIX (qmix/qmix.py train, row a15) vs the reference's own update."""
+    fx, P, T, M, TM, batch, gamma, lr = _qmix_min_fixture(golden)
+    newP, newM, g, loss = nets.qmix_min_train_step(P, M, T, TM, batch, gamma, lr, 5.0)
+    gref = nets.agent_from_state(fx, "grad.q.", "min")
+    post = nets.agent_from_state(fx, "post.q.", "min")
+    for k in nets.AGENT_KEYS:
+        np.testing.assert_allclose(g[k].numpy(), gref[k].numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(newP[k].numpy(), post[k].numpy(), rtol=1e-5, atol=2e-6)
+    gmref = nets.mixer_from_state(fx, "grad.m.")
+    postM = nets.mixer_from_state(fx, "post.m.")
+    for k in nets.MIXER_KEYS:
+        np.testing.assert_allclose(g["m." + k].numpy(), gmref[k].numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(newM[k].numpy(), postM[k].numpy(), rtol=1e-5, atol=2e-6)
+
+
 def test_per_batched_insert_equals_sequential_when_no_self_eviction():
     rng = np.random.default_rng(0)
     a = SumTreeOracle(13, "vdn")
