@@ -91,7 +91,7 @@ int mm_agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_i
 /* Split forward for training over a whole chunk batch: PRE runs the non-recurrent part (layers 1-2
  * and W_ih x2, writing io.gi and the x1|x2 save columns) for all E = C*B rows of two nets in one
  * launch; REC runs one recurrent step (W_hh h, gates, Q head, epilogue) reading io.gi. Together
- * bit-identical to mm_agent_q_fwd2 (same MFMA accumulation order). */
+ * bit-identical to mm_agent_q_fwd2 (same MFMA accumulation order). io1 == NULL or n_envs1 == 0: one net. */
 int mm_agent_q_pre2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
                     const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
 int mm_agent_q_rec2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,

@@ -1126,12 +1126,13 @@ static int dispatch(const mm_qnet_dims* d, const QFwdParams& p0, const QFwdParam
 
 template <int F1, int G, int H, int AB>
 static int launch_split(int phase, QFwdParams p0, QFwdParams p1, hipStream_t s) {
+  const bool single = p1.nblocks == 0;   // one net only (agent_q_split2 with io1 == NULL)
   if (phase == 1) {
     const int nb = p0.nblocks + p1.nblocks;
     hipLaunchKernelGGL((agent_split_kernel<F1, G, H, AB, 1>), dim3(nb), dim3(256), 0, s, p0, p1);
   } else {
     p0.nblocks = (p0.E + 31) / 32 * p0.N;
-    p1.nblocks = (p1.E + 31) / 32 * p1.N;
+    p1.nblocks = single ? 0 : (p1.E + 31) / 32 * p1.N;
     const int nb = p0.nblocks + p1.nblocks;
     hipLaunchKernelGGL((agent_split_kernel<F1, G, H, AB, 2>), dim3(nb), dim3(64 * (H / 32)), 0, s, p0, p1);
   }
@@ -1159,6 +1160,12 @@ int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const
   QFwdParams p0, p1;
   int rc = make_params(d, packed0, io0, e0, &p0);
   if (rc) return rc;
+  if (!io1 || e1 <= 0) {   // single net
+    MM_REQUIRE(io0->gi, "agent_q_split: io.gi required");
+    p1 = p0;
+    p1.nblocks = 0;
+    return dispatch_split(d, phase, p0, p1, s);
+  }
   rc = make_params(d, packed1, io1, e1, &p1);
   if (rc) return rc;
   MM_REQUIRE(io0->gi && io1->gi, "agent_q_split: io.gi required");

@@ -7,6 +7,11 @@ agent params only, qmix/_train.py:111-115; VDN: all), Adam, priority update with
 last step's |y - Q_tot|. Everything is enqueued on the current HIP stream with no host
 sync, so an update can be captured as one HIP graph and replayed.
 
+Mode "vdn_double" is ``Target_Double_Dqn`` (vdn/_train.py:104-158): the bootstrap is the target
+net's Q at the actions an epsilon-greedy copy of the behavior net picks on s' (its own hidden
+chain), Σ_i Q_tgt(s', a*_i); everything else as "vdn". The draws are injected
+(``set_double_draws``) or come from the device counter RNG.
+
 Mode "qmix_min" is the minimal QMIX of ``qmix/qmix.py`` (``train``
 qmix/qmix.py:174-238): target Σ_i r_i + γ(1-d)Q'_tot (no xN, no IS weight), smooth-L1 loss,
 clip_grad_norm_ on the agent net and on the mixer separately, uniform chunk replay
@@ -21,8 +26,8 @@ import math
 import numpy as np
 import torch
 
-from ._lib import (MM_LOSS_HUBER, MM_LOSS_MIX_SUM, MM_LOSS_TARGET_SUM, MM_Q_GATHER, MM_Q_MAX, MixNetIO, OuterArgs,
-                   QFwdIO, TmvArgs, c_i64, check, lib)
+from ._lib import (MM_LOSS_HUBER, MM_LOSS_MIX_SUM, MM_LOSS_TARGET_SUM, MM_Q_ACT, MM_Q_GATHER, MM_Q_MAX, MixNetIO,
+                   OuterArgs, QFwdIO, TmvArgs, c_i64, check, lib)
 from .qnet import KEYS as AGENT_KEYS
 from .qnet import AgentQNet, ptr, stream_handle
 
@@ -95,10 +100,15 @@ class QLearner:
 
     def __init__(self, behavior, target, mixer=None, target_mixer=None, batch=32, chunk=10, gamma=0.99, lr=1e-3,
                  grad_clip=5.0, betas=(0.9, 0.999), adam_eps=1e-8, mode="qmix", clip_mixer=False, device="cuda"):
-        assert mode in ("qmix", "vdn", "qmix_min")
+        assert mode in ("qmix", "vdn", "qmix_min", "vdn_double")
         self.mode = mode
-        self.has_mixer = mode != "vdn"
-        self.loss_flags = {"qmix": 0, "vdn": MM_LOSS_MIX_SUM, "qmix_min": MM_LOSS_HUBER | MM_LOSS_TARGET_SUM}[mode]
+        self.has_mixer = mode in ("qmix", "qmix_min")
+        self.double = mode == "vdn_double"
+        self.loss_flags = {"qmix": 0, "vdn": MM_LOSS_MIX_SUM, "vdn_double": MM_LOSS_MIX_SUM,
+                           "qmix_min": MM_LOSS_HUBER | MM_LOSS_TARGET_SUM}[mode]
+        self.double_eps = 0.0          # epsilon of the double net's sample_action (vdn/_train.py:124-125)
+        self.double_seed = 0x5eed
+        self._draws = None
         self.dev = torch.device(device)
         self.beh, self.tgt = behavior, target
         self.mix, self.tmix = mixer, target_mixer
@@ -127,7 +137,7 @@ class QLearner:
         self.step_dev = torch.zeros(1, device=self.dev)
         self.partials = torch.zeros(512, device=self.dev)
         self.norm = torch.zeros(2, device=self.dev)
-        self.n_clip = self.n if (mode == "vdn" or clip_mixer) else n_t
+        self.n_clip = self.n if (not self.has_mixer or clip_mixer) else n_t
         self._alloc()
         self.updates = 0
 
@@ -164,6 +174,11 @@ class QLearner:
         self.dqv = torch.zeros(C, B, N, A, **f32)
         self.dpre2 = torch.zeros(C, B, N, self.G, **f32)
         self.dpre1 = torch.zeros(C, B, N, self.F1, **f32)
+        if self.double:
+            self.hd = torch.zeros(2, B, N, H, **f32)
+            self.gi_ad = torch.zeros(C, B, N, 3 * H, **f32)
+            self.act_d = torch.zeros(C, B, N, dtype=torch.int32, device=dev)
+            self.qsel_d = torch.zeros(C, B, N, **f32)
         self.nodes = torch.zeros(B, dtype=torch.int64, device=dev)
         self.slots = torch.zeros(B, dtype=torch.int64, device=dev)
         if self.has_mixer:
@@ -216,6 +231,18 @@ class QLearner:
         self._obs_ptr = self._obs_buf
         self._reset_obs = self._obs_buf      # never addressed (no -1 offsets in an explicit batch)
 
+    def set_double_draws(self, u=None, rand_act=None):
+        """Inject the double net's epsilon-greedy draws per chunk step (the reference's torch.rand(B)
+        and torch.randint rows, vdn/_network.py:52-58): u [C, B] f32, rand_act [C, B, N] (only rows
+        with u <= epsilon are used). None: device counter RNG."""
+        if u is None:
+            self._draws = None
+            return
+        C, B, N = self.C, self.B, self.N
+        uu = torch.as_tensor(u, dtype=torch.float32).to(self.dev).reshape(C, B).contiguous()
+        ra = torch.as_tensor(rand_act).to(self.dev).to(torch.int32).reshape(C, B, N).contiguous()
+        self._draws = (uu, ra)
+
     # ------------------------------------------------------------------ the update
     def compute_grads(self, obs_base, reset_obs_ptr):
         """Forward C steps, loss, BPTT and all weight gradients into self.Gr (all async)."""
@@ -244,6 +271,15 @@ class QLearner:
         pb.save = self.asave.data_ptr()
         check(L.mm_agent_q_pre2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pb), CB,
                                 ptr(self.tgt.packed), ctypes.byref(pt), CB, s), "learner fwd pre")
+        if self.double:   # the double net (behavior weights) on s'
+            pd = QFwdIO()
+            pd.obs, pd.obs_se, pd.obs_sa, pd.obs_off = obs_p.value, 1, D, 0
+            pd.obs_row = self.s2_off.data_ptr()
+            pd.reset_obs = reset_p.value
+            pd.h_in = self.hb.data_ptr()
+            pd.gi = self.gi_ad.data_ptr()
+            check(L.mm_agent_q_pre2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pd), CB,
+                                    None, None, 0, s), "learner fwd pre (double)")
         gstep = 4 * B * N * 3 * H
         for t in range(C):
             ib, it = QFwdIO(), QFwdIO()
@@ -262,8 +298,36 @@ class QLearner:
             ib.save = self.asave[t].data_ptr()
             it.mode = MM_Q_MAX
             it.qsel_out = self.maxq[t].data_ptr()
-            check(L.mm_agent_q_rec2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
-                                    ptr(self.tgt.packed), ctypes.byref(it), B, s), "learner fwd rec")
+            if self.double:
+                # behavior on s_t + the double net's eps-greedy actions on s'_t, then the target net's
+                # Q at those actions (Target_Double_Dqn, vdn/_train.py:121-130)
+                idd = QFwdIO()
+                idd.obs = obs_p.value
+                idd.h_in, idd.h_out = self.hd[t % 2].data_ptr(), self.hd[(t + 1) % 2].data_ptr()
+                idd.hin_se = idd.hout_se = N * H
+                idd.hin_sa = idd.hout_sa = H
+                idd.hin_sf = idd.hout_sf = 1
+                idd.reset = it.reset
+                idd.gi = self.gi_ad.data_ptr() + t * gstep
+                idd.mode = MM_Q_ACT
+                idd.act_out = self.act_d[t].data_ptr()
+                idd.qsel_out = self.qsel_d[t].data_ptr()
+                idd.epsilon = float(self.double_eps)
+                if self._draws is not None:
+                    idd.u = self._draws[0][t].data_ptr()
+                    idd.rand_act = self._draws[1][t].data_ptr()
+                else:
+                    idd.seed = self.double_seed
+                    idd.counter = self.updates * C + t
+                check(L.mm_agent_q_rec2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
+                                        ptr(self.beh.packed), ctypes.byref(idd), B, s), "learner fwd rec")
+                it.mode = MM_Q_GATHER
+                it.act_in, it.act_se = self.act_d[t].data_ptr(), N
+                check(L.mm_agent_q_rec2(ctypes.byref(self.beh.dims), ptr(self.tgt.packed), ctypes.byref(it), B,
+                                        None, None, 0, s), "learner fwd rec (target at double actions)")
+            else:
+                check(L.mm_agent_q_rec2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
+                                        ptr(self.tgt.packed), ctypes.byref(it), B, s), "learner fwd rec")
             if self.has_mixer:
                 mx = self.mix
                 nets = (MixNetIO * 2)()

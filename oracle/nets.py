@@ -216,6 +216,47 @@ def vdn_train_step(P, T, batch, gamma, lr, grad_clip, adam_state=None):
     return newP, g, loss.detach(), new_td
 
 
+def vdn_double_loss(P, T, batch, gamma, epsilon, draws_u, draws_ra):
+    """Target_Double_Dqn.train inner loop, vdn/_train.py:112-141 (one update).
+
+    The double network (a copy of the behavior net, :110) picks eps-greedy actions on s' with its
+    own hidden chain (draws injected: u [C,B], rand actions [C,B,N]); the bootstrap is
+    sum_i Q_tgt(s')_{i, a*_i} (:127-129); target and loss as Target_Dqn (xN quirk, IS weight).
+    """
+    s, a, r, s2, d, w = batch
+    B, C, N, _ = s.shape
+    H = P["Whh"].shape[2]
+    Pd = {k: v.detach() for k, v in P.items()}
+    h = torch.zeros(B, N, H)
+    ht = torch.zeros(B, N, H)
+    hd = torch.zeros(B, N, H)
+    loss = 0.0
+    for t in range(C):
+        q, nh = agent_forward(P, s[:, t], h)
+        sum_q = q.gather(2, a[:, t].unsqueeze(-1).long()).squeeze(-1).sum(1, keepdim=True)
+        tq, nht = agent_forward(T, s2[:, t], ht.detach())
+        dq, nhd = agent_forward(Pd, s2[:, t], hd)
+        act = epsilon_greedy(dq, epsilon, draws_u[t], draws_ra[t])
+        sum_dq = tq.gather(2, act.long().unsqueeze(-1)).squeeze(-1).sum(1, keepdim=True)
+        target = w * (r[:, t] + gamma * (1 - d[:, t]) * sum_dq).sum(dim=1, keepdim=True)
+        loss = loss + F.mse_loss(target.detach(), sum_q)
+        keep = (1.0 - d[:, t]).view(B, 1, 1)
+        h, ht, hd = nh * keep, nht * keep, nhd * keep
+    return loss, target.detach(), sum_q
+
+
+def vdn_double_train_step(P, T, batch, gamma, lr, grad_clip, epsilon, draws_u, draws_ra, adam_state=None):
+    """One Target_Double_Dqn update: loss, backward, clip (behavior params), Adam (vdn/_train.py:143-147)."""
+    Pg = _requires(P)
+    loss, target, sum_q = vdn_double_loss(Pg, T, batch, gamma, epsilon, draws_u, draws_ra)
+    grads = torch.autograd.grad(loss, [Pg[k] for k in AGENT_KEYS])
+    grads, _ = clip_grad_norm(list(grads), grad_clip)
+    g = dict(zip(AGENT_KEYS, grads))
+    state = {} if adam_state is None else adam_state
+    newP = adam_step({k: P[k] for k in AGENT_KEYS}, g, state, lr)
+    return newP, g, loss.detach(), (target - sum_q.detach()).abs().view(-1)
+
+
 def qmix_loss(P, M, T, TM, batch, gamma, hidden_dim=32):
     """Train_dqn.train inner loop, qmix/_train.py:39-103 (one update).
 

@@ -271,3 +271,38 @@ def test_qmix_min_uniform_replay_from_engine():
     assert torch.equal(tree0, eng.per.tree())          # uniform replay leaves priorities alone
     slots = L.slots.cpu().numpy()
     assert slots.min() >= 0 and slots.max() < len(eng.per)
+
+
+def test_vdn_double_matches_reference_update(golden):
+    """VDN Double-DQN (Target_Double_Dqn, vdn/_train.py:104-158): the double net's eps-greedy draws
+    injected from the reference run; loss, priorities, clipped gradients and post-Adam params."""
+    from minimarl.learner import QLearner
+    from minimarl.qnet import AgentQNet
+    fx = golden("vdn_double_train")
+    P = nets.agent_from_state(fx, "before.", "vdn")
+    N, F1, D = P["W1"].shape
+    A = P["Wq"].shape[1]
+    beh = AgentQNet(N, D, A, 64, 32, 32, DEV)
+    beh.load_reference_state(fx, "before.", "vdn")
+    tgt = AgentQNet(N, D, A, 64, 32, 32, DEV)
+    tgt.load_reference_state(fx, "target.", "vdn")
+    L = QLearner(beh, tgt, None, None, batch=32, chunk=10, gamma=float(fx["gamma"]), lr=float(fx["lr"]),
+                 grad_clip=float(fx["grad_clip"]), mode="vdn_double", device=DEV)
+    L.double_eps = float(fx["epsilon"])
+    L.set_double_draws(fx["double_u"], fx["double_rand_act"])
+    L.load_batch(fx["states"], fx["actions"], fx["rewards"], fx["next_states"], fx["dones"], fx["is_weight"])
+    L.train_step(L._obs_buf, L._obs_buf)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(float(L.loss.item()), float(fx["loss"]), rtol=1e-4)
+    np.testing.assert_allclose(L.td_last.cpu().numpy(), fx["new_td"], rtol=1e-4, atol=1e-4)
+    coef = min(1.0, float(fx["grad_clip"]) / (float(L.norm[0].item()) + 1e-6))
+
+    def gidx(i, k):   # vdn parameters() order: feature_net[*], gru_net[*], action_net[*]
+        return 4 * i + k if k < 4 else (4 * N + 4 * i + k - 4 if k < 8 else 8 * N + 2 * i + k - 8)
+
+    after = nets.agent_from_state(fx, "after.", "vdn")
+    for k, key in enumerate(nets.AGENT_KEYS):
+        g_all = np.stack([fx[f"g0.{gidx(i, k)}"] for i in range(N)])
+        _check_grads(_grad_view(L, key).cpu().numpy() * coef, g_all)
+        sel = np.abs(g_all) > 1e-4 * np.abs(g_all).max()
+        np.testing.assert_allclose(L.beh.view(key).cpu().numpy()[sel], after[key].numpy()[sel], atol=2e-6)

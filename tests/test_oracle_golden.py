@@ -114,6 +114,22 @@ def test_qmix_train_step(golden):
     np.testing.assert_allclose(new_td.numpy(), fx["new_td"], rtol=1e-4, atol=1e-4)
 
 
+def test_vdn_double_train_step(golden):
+    """Oracle of Target_Double_Dqn (vdn/_train.py:104-158) vs the reference's update."""
+    fx = golden("vdn_double_train")
+    P = nets.agent_from_state(fx, "before.", "vdn")
+    T = nets.agent_from_state(fx, "target.", "vdn")
+    batch = nets.batch_from_fixture(fx)
+    newP, g, loss, new_td = nets.vdn_double_train_step(P, T, batch, float(fx["gamma"]), float(fx["lr"]),
+                                                       float(fx["grad_clip"]), float(fx["epsilon"]),
+                                                       fx["double_u"], fx["double_rand_act"])
+    np.testing.assert_allclose(float(loss), float(fx["loss"]), rtol=1e-5)
+    np.testing.assert_allclose(new_td.numpy(), fx["new_td"], rtol=1e-4, atol=1e-5)
+    after = nets.agent_from_state(fx, "after.", "vdn")
+    for k in nets.AGENT_KEYS:
+        np.testing.assert_allclose(newP[k].numpy(), after[k].numpy(), rtol=1e-5, atol=2e-6)
+
+
 def _qmix_min_fixture(golden):
     fx = golden("qmix_min_train")
     P = nets.agent_from_state(fx, "q.", "min")
