@@ -134,6 +134,13 @@ int mm_td_chunk_step(int64_t n_envs, int32_t n_agents, float gamma, const float*
                      int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
                      uint8_t* store_done, int64_t store_row0, mm_stream_t s);
 
+/* Greedy-evaluation episode accumulators (vdn/_test.py:22-50, qmix/_test.py:19-36): for envs still
+ * active, score[e] += sum_i rew; if q_taken and max_q_next are given, loss[e] += td^2 (cal_td_error);
+ * done[e] deactivates the env. */
+int mm_eval_accum(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                  const float* q_taken, const float* max_q_next, uint8_t* active, float* score, float* loss,
+                  mm_stream_t s);
+
 /* ------------------------------------------------------------------ prioritized replay */
 enum { MM_PER_VDN = 0, MM_PER_QMIX = 1 };
 typedef struct mm_per mm_per;
@@ -323,6 +330,8 @@ typedef struct mm_mappo_fwd_args {
   int32_t T, L;
   int64_t rs;            /* SoA row stride (>= T*EN, multiple of 64; tail rows must stay zero) */
   int32_t mode;
+  int32_t deterministic; /* rollout: take the mode (first argmax) instead of sampling (policy.act,
+                            rmappo_policy.py:140-153 with deterministic=True) */
 } mm_mappo_fwd_args;
 typedef struct mm_mappo_bwd_args {
   const float* P[2];

@@ -251,6 +251,13 @@ __device__ __forceinline__ void fwd_body(const mm_mappo_fwd_args& a, int net, fl
       int act;
       if (a.act_in) {
         act = a.act_in[tid];
+      } else if (a.deterministic) {
+        // Categorical.mode() = first argmax of the probabilities (distributions.py:61-62)
+        act = 0;
+#pragma unroll
+        for (int q = 1; q < A; ++q)
+          if (l[q] > l[act]) act = q;
+        if (a.act_out) a.act_out[tid] = act;
       } else {
         float u;
         if (a.u) {

@@ -84,9 +84,46 @@ __global__ __launch_bounds__(256) void chunk_begin_rows_kernel(int E, int ND, fl
   }
 }
 
+// Greedy evaluation episode accumulators (vdn/_test.py:22-50, qmix/_test.py:19-36,
+// magym_runner.py:198-241): while env e is still in its episode, score[e] += sum_i r_i and, given
+// Q(a) and max Q', loss[e] += td^2 with td as cal_td_error (vdn/_utils.py:44-52); done ends it.
+__global__ __launch_bounds__(256) void eval_accum_kernel(int E, int N, float gamma, const float* __restrict__ rew,
+                                                         const uint8_t* __restrict__ done,
+                                                         const float* __restrict__ q_taken,
+                                                         const float* __restrict__ maxq_next,
+                                                         uint8_t* __restrict__ active, float* __restrict__ score,
+                                                         float* __restrict__ loss) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E || !active[e]) return;
+  float sr = 0.f, sq = 0.f, st = 0.f;
+  for (int j = 0; j < N; ++j) {
+    sr += rew[(int64_t)e * N + j];
+    if (q_taken) sq += q_taken[(int64_t)e * N + j];
+    if (maxq_next) st += maxq_next[(int64_t)e * N + j];
+  }
+  score[e] += sr;
+  const bool dn = done[e] != 0;
+  if (q_taken && maxq_next && loss) {
+    const float td = fabsf(sr + (dn ? 0.0f : 1.0f) * gamma * st - sq);
+    loss[e] += td * td;
+  }
+  if (dn) active[e] = 0;
+}
+
 }  // namespace mm
 
 extern "C" {
+int mm_eval_accum(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                  const float* q_taken, const float* max_q_next, uint8_t* active, float* score, float* loss,
+                  mm_stream_t s) {
+  MM_REQUIRE(rew && done && active && score && n_agents >= 1, "eval_accum: bad args");
+  if (n_envs <= 0) return MM_OK;
+  hipLaunchKernelGGL(mm::eval_accum_kernel, dim3((int)((n_envs + 255) / 256)), dim3(256), 0, (hipStream_t)s,
+                     (int)n_envs, n_agents, gamma, rew, done, q_taken, max_q_next, active, score, loss);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 int mm_chunk_begin_rows(int64_t n_envs, int32_t nd, float* store_obs, int64_t row_stride, const int64_t* src_rows,
                         int64_t src_off, const float* reset_obs, const int64_t* dst_rows, mm_stream_t s) {
   MM_REQUIRE(store_obs && src_rows && reset_obs && dst_rows, "chunk_begin_rows: null argument");

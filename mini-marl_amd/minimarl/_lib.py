@@ -175,6 +175,7 @@ _SIGS += [
     ("mm_clip2_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
                               c_vp, c_f32, c_vp]),
     ("mm_per_sample_uniform", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
+    ("mm_eval_accum", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 ]
 
 
@@ -196,7 +197,8 @@ class MappoNetIO(ctypes.Structure):
 class MappoFwdArgs(ctypes.Structure):
     _fields_ = [("net", MappoNetIO * 2), ("obs", c_vp), ("mask", c_vp), ("act_in", c_vp), ("act_out", c_vp),
                 ("u", c_vp), ("seed", c_u64), ("counter_ptr", c_vp), ("counter", c_u64), ("rows", c_i64),
-                ("en", c_i64), ("T", c_i32), ("L", c_i32), ("rs", c_i64), ("mode", c_i32)]
+                ("en", c_i64), ("T", c_i32), ("L", c_i32), ("rs", c_i64), ("mode", c_i32),
+                ("deterministic", c_i32)]
 
 
 class MappoBwdArgs(ctypes.Structure):
