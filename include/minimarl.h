@@ -96,6 +96,13 @@ int mm_agent_q_pre2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_i
                     const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
 int mm_agent_q_rec2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
                     const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
+/* REC for all `steps` chunk steps in one launch (the W_hh fragments stay in registers, the hidden
+ * state in LDS): step t reads io.gi / writes io.save, io.qsel_out and reads io.act_in at the step-0
+ * pointers + t * (E*N*3H / E*N*SD / E*N / E*act_se); h_in/h_out are not used (zero start, resets
+ * where reset[(t-1)*E + e] for t >= 1). Bit-identical to `steps` mm_agent_q_rec2 launches. */
+int mm_agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
+                        const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, int32_t steps,
+                        const uint8_t* reset, mm_stream_t s);
 
 /* Survey-style convenience entry: contiguous obs [E,N,D], hidden [E,N,H] -> q [E,N,A], h_out [E,N,H]. */
 int mm_agent_q_fwd_simple(const mm_qnet_dims* d, const float* packed, const float* obs, const float* h,
@@ -232,6 +239,13 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
                 const float* P0, const int64_t* s_off0, float* gi0, const float* P1, const int64_t* s_off1, float* gi1,
                 mm_stream_t s);
 /* One mixer time step for 1-2 nets (behavior / target) in one launch. */
+/* Chunk-sequence mixer backward: all C steps (t = C-1 .. 0) in one launch, a block per sample
+ * carrying dhm. Step t reads save [C][B][MSD], qa [C][B][N], dq [C][B] and writes dqa [C][B][N],
+ * delta [C][B][MDD] at the step-0 pointers + t * (per-step size); the future gradient is dropped at
+ * t = C-1 (ones) and where done[t*B + b]. Bit-identical to C mm_mixer_bwd launches. */
+int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                     const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
+                     float* delta, int32_t steps, mm_stream_t s);
 int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
                  const mm_mix_net* nets, int32_t n_nets, mm_stream_t s);
 /* TD loss terms and their gradient seeds (reference quirks: bootstrap x N, IS weight on the target). */

@@ -101,20 +101,19 @@ __device__ __forceinline__ void load_obs_kblock(const float* orow, int kb, int D
 
 // Q output / argmax / eps-greedy / gather epilogue shared by the fused and the split forward.
 template <int AB>
-__device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB],
-                                             float eps, uint64_t ctr);
+__device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_io& io, int agent, int e, bool valid,
+                                             const f32x16 (&qa)[AB], float eps, uint64_t ctr);
 template <int AB>
 __device__ __forceinline__ void q_epilogue(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB]) {
   const mm_qfwd_io& io = p.io;
   const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
   const uint64_t ctr = (io.mode == MM_Q_ACT && io.counter_ptr) ? *io.counter_ptr : io.counter;
-  q_epilogue_v<AB>(p, agent, e, valid, qa, eps, ctr);
+  q_epilogue_v<AB>(p, io, agent, e, valid, qa, eps, ctr);
 }
 template <int AB>
-__device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB],
-                                             float eps, uint64_t ctr) {
+__device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_io& io, int agent, int e, bool valid,
+                                             const f32x16 (&qa)[AB], float eps, uint64_t ctr) {
   const int hh = (threadIdx.x & 63) >> 5;
-  const mm_qfwd_io& io = p.io;
   if (valid && io.q_out) {
     float* qrow = io.q_out + (int64_t)e * io.q_se + (int64_t)agent * io.q_sa;
 #pragma unroll
@@ -521,6 +520,126 @@ __global__ __launch_bounds__(256, 2) void agent_split_kernel(QFwdParams p0, QFwd
     agent_pre_body<F1, G, H, AB>(p, agent, e, W, obs_row_ptr(p, agent, e));
   } else {
     agent_rec_body<F1, G, H, AB>(p, agent, tile, W);
+  }
+}
+
+// REC over all C steps of a learner chunk in one launch (one block = one 32-env tile of one agent
+// for the whole sequence): the W_hh fragments stay in registers, the hidden state stays in LDS
+// between steps (hx exchange), and step t's pointers are the step-0 ones + t * stride. Same
+// arithmetic as C launches of agent_rec_body (bit-identical results).
+struct RecSeq {
+  int C;
+  int64_t gi_st, save_st, act_st, qsel_st;   // elements per step
+  const uint8_t* reset;                        // step t >= 1 resets where reset[(t-1)*reset_st + e]
+  int64_t reset_st;
+};
+
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(256, 2) void agent_rec_seq_kernel(QFwdParams p0, QFwdParams p1, RecSeq s0,
+                                                               RecSeq s1) {
+  using S = Sched<F1, G, H, AB>;
+  using CG = typename S::CG;
+  constexpr int RB2 = S::RB2, HB = S::HB;
+  __shared__ float hx[HB][16][64];
+  const bool second = (int)blockIdx.x >= p0.nblocks;
+  const QFwdParams& p = second ? p1 : p0;
+  const RecSeq& sq = second ? s1 : s0;
+  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
+  const int agent = bid % p.N, tile = bid / p.N;
+  const float* W = p.packed + (int64_t)agent * p.g.agent_stride;
+  const int lane = threadIdx.x & 63, hh = lane >> 5, hb = threadIdx.x >> 6;
+  const int e = tile * 32 + (lane & 31);
+  const bool valid = e < p.E;
+  float fz[3][HB][16];
+  const int base = S::NF2 + hb * S::PERHB + 3 * RB2;
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) load_frag(W + S::off(base + g * HB + kb), lane, fz[g][kb]);
+  const f32x16 bhn = load_bias(W + CG::off_bhn + hb * 32, hh);
+  mm_qfwd_io io = p.io;
+  const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
+  const uint64_t ctr = (io.mode == MM_Q_ACT && io.counter_ptr) ? *io.counter_ptr : io.counter;
+  for (int t = 0; t < sq.C; ++t) {
+    f32x16 h0[HB];
+    const bool zero_h = !valid || t == 0 || sq.reset[(int64_t)(t - 1) * sq.reset_st + e];
+    if (t > 0) __syncthreads();   // previous step's hx writes visible
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) h0[kb][s] = zero_h ? 0.0f : hx[kb][s][lane];
+    const float* gi = io.gi + t * sq.gi_st + ((int64_t)(valid ? e : 0) * p.N + agent) * 3 * H;
+    f32x16 ar, az, anx;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int f = hb * 32 + kperm(s, hh);
+      ar[s] = gi[f];
+      az[s] = gi[H + f];
+      anx[s] = gi[2 * H + f];
+    }
+    f32x16 anh = bhn;
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) ar = mfma32(fz[0][kb][s], h0[kb][s], ar);
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) az = mfma32(fz[1][kb][s], h0[kb][s], az);
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) anh = mfma32(fz[2][kb][s], h0[kb][s], anh);
+    float* sv = (io.save && valid) ? io.save + t * sq.save_st + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H)
+                                   : nullptr;
+    float h1v[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      float h0v = h0[0][s];
+#pragma unroll
+      for (int kb = 1; kb < HB; ++kb)
+        if (kb == hb) h0v = h0[kb][s];
+      const float r = sigmoidf_(ar[s]);
+      const float z = sigmoidf_(az[s]);
+      const float n = tanhf_(anx[s] + r * anh[s]);
+      h1v[s] = n + z * (h0v - n);
+      if (sv) {
+        float* o = sv + F1 + G + hb * 32 + kperm(s, hh);
+        o[0] = h0v;
+        o[H] = r;
+        o[2 * H] = z;
+        o[3 * H] = n;
+        o[4 * H] = anh[s];
+        o[5 * H] = h1v[s];
+      }
+    }
+    __syncthreads();   // every wave has read hx (its h0) before it is overwritten
+#pragma unroll
+    for (int s = 0; s < 16; ++s) hx[hb][s][lane] = h1v[s];
+    __syncthreads();
+    if (hb == 0) {
+      f32x16 h1[HB];
+#pragma unroll
+      for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) h1[kb][s] = hx[kb][s][lane];
+      f32x16 qa[AB];
+      float fr[16];
+#pragma unroll
+      for (int ab = 0; ab < AB; ++ab) {
+        qa[ab] = load_bias(W + CG::off_bq + ab * 32, hh);
+#pragma unroll
+        for (int kb = 0; kb < HB; ++kb) {
+          load_frag(W + S::off(S::NF2 + S::NFG + ab * HB + kb), lane, fr);
+#pragma unroll
+          for (int s = 0; s < 16; ++s) qa[ab] = mfma32(fr[s], h1[kb][s], qa[ab]);
+        }
+      }
+      mm_qfwd_io it = io;
+      if (it.act_in) it.act_in += t * sq.act_st;
+      if (it.qsel_out) it.qsel_out += t * sq.qsel_st;
+      q_epilogue_v<AB>(p, it, agent, e, valid, qa, eps, ctr);
+    }
   }
 }
 
@@ -1152,6 +1271,58 @@ static int dispatch_split(const mm_qnet_dims* d, int phase, const QFwdParams& p0
   MM_SPLIT(64, 32, 64)
 #undef MM_SPLIT
   set_error("agent_q_split: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
+  return MM_EINVAL;
+}
+
+template <int F1, int G, int H, int AB>
+static int launch_rec_seq(QFwdParams p0, QFwdParams p1, const RecSeq& s0, const RecSeq& s1, bool single,
+                          hipStream_t s) {
+  p0.nblocks = (p0.E + 31) / 32 * p0.N;
+  p1.nblocks = single ? 0 : (p1.E + 31) / 32 * p1.N;
+  hipLaunchKernelGGL((agent_rec_seq_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(64 * (H / 32)), 0, s,
+                     p0, p1, s0, s1);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
+                     const float* packed1, const mm_qfwd_io* io1, int64_t e1, int32_t steps, const uint8_t* reset,
+                     hipStream_t s) {
+  QFwdParams p0, p1;
+  int rc = make_params(d, packed0, io0, e0, &p0);
+  if (rc) return rc;
+  const bool single = !io1 || e1 <= 0;
+  if (single) {
+    p1 = p0;
+  } else {
+    rc = make_params(d, packed1, io1, e1, &p1);
+    if (rc) return rc;
+  }
+  MM_REQUIRE(steps >= 1 && (steps == 1 || reset), "agent_q_rec_seq: steps >= 1 and reset flags required");
+  MM_REQUIRE(io0->gi && (single || io1->gi), "agent_q_rec_seq: io.gi required");
+  auto mk = [&](const QFwdParams& p) {
+    RecSeq q;
+    q.C = steps;
+    q.gi_st = (int64_t)p.E * p.N * 3 * d->h;
+    q.save_st = (int64_t)p.E * p.N * (d->f1 + d->g + 6 * d->h);
+    q.act_st = (int64_t)p.E * p.io.act_se;
+    q.qsel_st = (int64_t)p.E * p.N;
+    q.reset = reset;
+    q.reset_st = p.E;
+    return q;
+  };
+  const RecSeq s0 = mk(p0), s1 = mk(p1);
+  const int AB = (d->n_actions + 31) / 32;
+#define MM_RSEQ(F1_, G_, H_)                                                                                    \
+  if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                                 \
+    return AB == 1 ? launch_rec_seq<F1_, G_, H_, 1>(p0, p1, s0, s1, single, s)                                  \
+                   : launch_rec_seq<F1_, G_, H_, 2>(p0, p1, s0, s1, single, s);
+  MM_RSEQ(64, 32, 32)
+  MM_RSEQ(64, 64, 64)
+  MM_RSEQ(128, 32, 32)
+  MM_RSEQ(64, 32, 64)
+#undef MM_RSEQ
+  set_error("agent_q_rec_seq: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
   return MM_EINVAL;
 }
 

@@ -17,6 +17,9 @@ void set_error(const char* fmt, ...) {
 }
 
 int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s);
+int agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
+                     const float* packed1, const mm_qfwd_io* io1, int64_t e1, int32_t steps, const uint8_t* reset,
+                     hipStream_t s);
 int agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs, hipStream_t s);
 int agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
                  const float* packed1, const mm_qfwd_io* io1, int64_t e1, hipStream_t s);
@@ -63,6 +66,12 @@ int mm_agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_i
 int mm_agent_q_pre2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
                     const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s) {
   return mm::agent_q_split2(1, d, packed0, io0, n_envs0, packed1, io1, n_envs1, (hipStream_t)s);
+}
+
+int mm_agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
+                        const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, int32_t steps,
+                        const uint8_t* reset, mm_stream_t s) {
+  return mm::agent_q_rec_seq2(d, packed0, io0, n_envs0, packed1, io1, n_envs1, steps, reset, (hipStream_t)s);
 }
 
 int mm_agent_q_rec2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,

@@ -196,10 +196,14 @@ __global__ __launch_bounds__(256) void mixer_gi_kernel(MixGiArgs a) {
 }
 
 // One block per (sample, net): blockIdx.y selects behavior / target.
+__device__ __forceinline__ void mixer_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, int b);
+
 __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixFwdArgs a) {
+  mixer_fwd_body(a, a.net[blockIdx.y], blockIdx.x);
+}
+
+__device__ __forceinline__ void mixer_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, int b) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const MixFwdNet& nt = a.net[blockIdx.y];
-  const int b = blockIdx.x;
   const int S = a.S, Hm = a.Hm, K1 = a.K1, N = a.N;
   const MixOff o = mix_offsets(S, Hm, K1, N);
   float* xs = sm;                  // [S]
@@ -354,9 +358,34 @@ struct MixBwdArgs {
 };
 __host__ __device__ inline int mix_delta_dim(int Hm, int K1, int N) { return 6 * Hm + N * K1 + 3 * K1 + 1; }
 
-__global__ __launch_bounds__(256) void mixer_bwd_kernel(MixBwdArgs a) {
+__device__ __forceinline__ void mixer_bwd_body(const MixBwdArgs& a, int b);
+
+__global__ __launch_bounds__(256) void mixer_bwd_kernel(MixBwdArgs a) { mixer_bwd_body(a, blockIdx.x); }
+
+// Chunk-sequence launch: all C steps backwards in one launch (block = one sample; dhm carried by
+// the same threads), step t's pointers = step-0 ones + t * stride.
+// done of step t: ones at t = C-1 (no future), else done + t * done_st.
+struct MixBwdSeq {
+  int C;
+  int64_t save_st, qa_st, dq_st, done_st, dqa_st, delta_st;
+  const float* ones;
+};
+__global__ __launch_bounds__(256) void mixer_bwd_seq_kernel(MixBwdArgs a, MixBwdSeq sq) {
+  for (int t = sq.C - 1; t >= 0; --t) {
+    MixBwdArgs x = a;
+    x.save += t * sq.save_st;
+    x.qa += t * sq.qa_st;
+    x.dq += t * sq.dq_st;
+    x.done = t == sq.C - 1 ? sq.ones : a.done + t * sq.done_st;
+    x.dqa += t * sq.dqa_st;
+    x.delta += t * sq.delta_st;
+    mixer_bwd_body(x, blockIdx.x);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void mixer_bwd_body(const MixBwdArgs& a, int b) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int b = blockIdx.x;
   const int Hm = a.Hm, K1 = a.K1, N = a.N;
   const MixOff o = mix_offsets(a.S, Hm, K1, N);
   const float* sv = a.save + (int64_t)b * mix_save_dim(Hm, K1, N);
@@ -459,7 +488,11 @@ struct AgentBwdArgs {
 };
 
 // one wave per (sample, agent); lane = hidden feature
-__global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs a) {
+__device__ __forceinline__ void agent_bwd_body(const AgentBwdArgs& a);
+
+__global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs a) { agent_bwd_body(a); }
+
+__device__ __forceinline__ void agent_bwd_body(const AgentBwdArgs& a) {
   __shared__ float sdg[4][3 * 256];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int pair0 = blockIdx.x * 4 + w;
@@ -873,6 +906,26 @@ int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, 
                      done, isw, qtot, qtot_t, mix_sum ? MM_LOSS_MIX_SUM : 0, qa, maxq, dq, dqa, loss_parts, td_last);
   MM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(mm::lrn_loss_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, B, C, loss_parts, loss);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                     const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
+                     float* delta, int32_t steps, mm_stream_t s) {
+  MM_REQUIRE(P && save && qa && dq && done && ones && dhm && dqa && delta && steps >= 1, "mixer_bwd_seq: bad args");
+  mm::MixBwdArgs a = {P, save, qa, dq, done, dhm, dqa, delta, B, N, S, Hm, K1};
+  mm::MixBwdSeq q;
+  q.C = steps;
+  q.save_st = (int64_t)B * mm::mix_save_dim(Hm, K1, N);
+  q.qa_st = (int64_t)B * N;
+  q.dq_st = B;
+  q.done_st = B;
+  q.dqa_st = (int64_t)B * N;
+  q.delta_st = (int64_t)B * mm::mix_delta_dim(Hm, K1, N);
+  q.ones = ones;
+  const size_t sm = sizeof(float) * ((size_t)8 * Hm + N * K1 + 3 * K1);
+  hipLaunchKernelGGL(mm::mixer_bwd_seq_kernel, dim3(B), dim3(256), sm, (hipStream_t)s, a, q);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

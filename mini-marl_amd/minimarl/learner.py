@@ -22,6 +22,7 @@ Adam moments alike), the layout the RCCL gradient all-reduce works on.
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -106,6 +107,8 @@ class QLearner:
         self.double = mode == "vdn_double"
         self.loss_flags = {"qmix": 0, "vdn": MM_LOSS_MIX_SUM, "vdn_double": MM_LOSS_MIX_SUM,
                            "qmix_min": MM_LOSS_HUBER | MM_LOSS_TARGET_SUM}[mode]
+        # chunk-sequence launches: agent REC and mixer backward as one launch each for all C steps
+        self.seq = not self.double and os.environ.get("MM_LRN_SEQ", "1") != "0"
         self.double_eps = 0.0          # epsilon of the double net's sample_action (vdn/_train.py:124-125)
         self.double_seed = 0x5eed
         self._draws = None
@@ -281,7 +284,9 @@ class QLearner:
             check(L.mm_agent_q_pre2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pd), CB,
                                     None, None, 0, s), "learner fwd pre (double)")
         gstep = 4 * B * N * 3 * H
-        for t in range(C):
+        if self.seq:
+            self._forward_seq(L, s, obs_p, reset_p)
+        for t in range(0 if not self.seq else C, C):
             ib, it = QFwdIO(), QFwdIO()
             for io, h, gi in ((ib, self.hb, self.gi_ab), (it, self.ht, self.gi_at)):
                 io.obs = obs_p.value               # unused by REC
@@ -349,9 +354,15 @@ class QLearner:
         # ---- backward through time (data-gradient chains only)
         o = self.beh.offs
         P = self.P
+        if self.seq:
+            if self.has_mixer:
+                mx = self.mix
+                check(L.mm_mixer_bwd_seq(B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.msave), ptr(self.qa),
+                                         ptr(self.dq), ptr(self.done), ptr(self.ones_f), ptr(self.dhm), ptr(self.dqa),
+                                         ptr(self.mdelta), C, s), "mixer bwd seq")
         for t in range(C - 1, -1, -1):
             dn = self.ones_f if t == C - 1 else self.done[t * B:(t + 1) * B]
-            if self.has_mixer:
+            if self.has_mixer and not self.seq:
                 mx = self.mix
                 check(L.mm_mixer_bwd(B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.msave[t]), ptr(self.qa[t]),
                                      ptr(self.dq[t]), ptr(dn), ptr(self.dhm), ptr(self.dqa[t]), ptr(self.mdelta[t]),
@@ -367,6 +378,39 @@ class QLearner:
             self._mixer_wgrad(L, s, obs_p, reset_p, CB, jobs)
         arr = (OuterArgs * len(jobs))(*jobs)
         check(L.mm_outer_reduce_batch(arr, len(jobs), ptr(self._opart), self._opart.numel(), s), "outer batch")
+
+    def _forward_seq(self, L, s, obs_p, reset_p):
+        """REC of both nets over all C steps in one chunk-sequence launch, then the mixers per step."""
+        B, C, N, H = self.B, self.C, self.N, self.H
+        ib, it = QFwdIO(), QFwdIO()
+        for io, gi in ((ib, self.gi_ab), (it, self.gi_at)):
+            io.obs = obs_p.value
+            io.gi = gi.data_ptr()
+        ib.mode = MM_Q_GATHER
+        ib.act_in, ib.act_se = self.acts.data_ptr(), N
+        ib.qsel_out = self.qa.data_ptr()
+        ib.save = self.asave.data_ptr()
+        it.mode = MM_Q_MAX
+        it.qsel_out = self.maxq.data_ptr()
+        check(L.mm_agent_q_rec_seq2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
+                                    ptr(self.tgt.packed), ctypes.byref(it), B, C, ptr(self.done8), s), "rec seq")
+        if self.has_mixer:
+            # per-step mixer launches (a one-launch sequence of this kernel measured slower: 32 vs
+            # 13 us per step), reading the REC outputs of every step
+            mx = self.mix
+            for t in range(C):
+                nets = (MixNetIO * 2)()
+                for k, (Pm, q, off, h, qt, sv, gi) in enumerate(
+                        ((self.mix.flat, self.qa[t], self.s_off, self.hm, self.qtot[t], self.msave[t], self.gi_b[t]),
+                         (self.tmix.flat, self.maxq[t], self.s2_off, self.hmt, self.qtot_t[t], None, self.gi_t[t]))):
+                    n = nets[k]
+                    n.P, n.q, n.gi = Pm.data_ptr(), q.data_ptr(), gi.data_ptr()
+                    n.s_off = off.data_ptr() + 8 * t * B
+                    n.h_in, n.h_out = h[t % 2].data_ptr(), h[(t + 1) % 2].data_ptr()
+                    n.reset = self.ones8.data_ptr() if t == 0 else self.done8.data_ptr() + (t - 1) * B
+                    n.qtot = qt.data_ptr()
+                    n.save = sv.data_ptr() if sv is not None else None
+                check(L.mm_mixer_fwd(B, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, nets, 2, s), "mixer fwd")
 
     def apply_grads(self, grad_scale=1.0):
         """clip_grad_norm_ + Adam (grads scaled first, e.g. 1/world after an all-reduce), then repack

@@ -306,3 +306,34 @@ def test_vdn_double_matches_reference_update(golden):
         _check_grads(_grad_view(L, key).cpu().numpy() * coef, g_all)
         sel = np.abs(g_all) > 1e-4 * np.abs(g_all).max()
         np.testing.assert_allclose(L.beh.view(key).cpu().numpy()[sel], after[key].numpy()[sel], atol=2e-6)
+
+
+@pytest.mark.parametrize("mode,f1,g,h,hm", [("qmix", 64, 64, 64, 64), ("vdn", 64, 32, 32, 32),
+                                            ("qmix_min", 128, 32, 32, 64)])
+def test_chunk_sequence_launches_match_per_step(mode, f1, g, h, hm):
+    """REC / mixer fwd / mixer bwd / agent bwd as one launch each for all C steps: bit-identical to
+    the per-step launches."""
+    from minimarl.learner import Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    N, D, A, B, C = 4, 47, 5, 32, 10
+    gen = torch.Generator().manual_seed(3)
+    st, ns = torch.rand(B, C, N, D, generator=gen), torch.rand(B, C, N, D, generator=gen)
+    act = torch.randint(0, A, (B, C, N), generator=gen).float()
+    rew = torch.randn(B, C, N, generator=gen)
+    dn = (torch.rand(B, C, 1, generator=gen) < 0.25).float()
+    w = torch.rand(B, 1, generator=gen) + 0.5
+    out = []
+    for seq in (True, False):
+        beh = AgentQNet(N, D, A, f1, g, h, DEV, seed=1)
+        tgt = AgentQNet(N, D, A, f1, g, h, DEV, seed=2)
+        mix = tmix = None
+        if mode != "vdn":
+            mix, tmix = Mixer(N, N * D, hm, 32, DEV, seed=3), Mixer(N, N * D, hm, 32, DEV, seed=4)
+        L = QLearner(beh, tgt, mix, tmix, batch=B, chunk=C, mode=mode, device=DEV)
+        L.seq = seq
+        L.load_batch(st, act, rew, ns, dn, w)
+        L.train_step(L._obs_buf, L._obs_buf)
+        torch.cuda.synchronize()
+        out.append((L.P.clone(), L.Gr.clone(), L.loss.clone(), L.qa.clone(), L.maxq.clone(), L.dqa.clone()))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
