@@ -396,6 +396,49 @@ int mm_mappo_vn_update(float* vn, float* stats, double beta, mm_stream_t s);
 int mm_mappo_insert(const uint8_t* done, int32_t n_agents, int32_t hidden, int64_t n_envs, float* mask_next,
                     float* active_next, float* h_actor, float* h_critic, uint64_t* counter, mm_stream_t s);
 
+/* ------------------------------------------------------------------ offpolicy episode QMix / VDN
+ * Replaces QMix.train_policy_on_batch (offpolicy/algorithms/qmix/qmix.py:80-210) with the shared
+ * QMixPolicy (algorithm/QMixPolicy.py:51-195; AgentQFunction = LN(D) -> [Linear, ReLU, LN] x 2 ->
+ * GRU(H) -> LN -> Linear(A), agent_q_function.py) and QMixer (2-layer hypernets, ELU,
+ * algorithm/q_mixer.py:6-94) or VDNMixer (vdn/algorithm/vdn_mixer.py), plus soft_update
+ * (utils/util.py:123-134). Agent parameters: the trunk layout of mm_mappo_param_offsets (net 0) with
+ * hidden H; mixer parameters: the 14 QMixer tensors in named_parameters() order (mm_offq_mixer_offsets).
+ * One flat vector [agent | mixer] per net (behavior P, target PT) and for the gradient.
+ * Batch = PrioritizedRecReplayBuffer.sample layout (rec_buffer.py:192-240): obs [N, T+1, B, D],
+ * share_obs [T+1, B, S], acts one-hot [N, T, B, A], rewards [N, T, B] (agent 0's are used,
+ * qmix.py:169), dones_env [T, B], is_weight [B] (NULL: no PER). Supported: H = 64, A = 5,
+ * D in {47, 94}; QMIX: hypernet_layers = 2, any S, N*K <= 4096. */
+enum { MM_OFFQ_VDN = 0, MM_OFFQ_QMIX = 1 };
+typedef struct mm_offq_dims {
+  int32_t n_agents, obs_dim, hidden, n_actions;
+  int32_t mixer;                                   /* MM_OFFQ_VDN / MM_OFFQ_QMIX */
+  int32_t state_dim, mixer_hidden, hyper_hidden;   /* QMIX: S, K (mixer_hidden_dim), hypernet_hidden_dim */
+} mm_offq_dims;
+typedef struct mm_offq_batch {
+  const float* obs; const float* share_obs; const float* acts; const float* rewards; const float* dones_env;
+  const float* is_weight;
+  int32_t T, B;
+  int32_t double_q, huber;
+  float gamma, huber_delta, per_nu, per_eps;
+} mm_offq_batch;
+int mm_offq_param_counts(const mm_offq_dims* d, int64_t* agent, int64_t* mixer);
+int mm_offq_mixer_offsets(const mm_offq_dims* d, int64_t offs[15]);
+int64_t mm_offq_workspace_bytes(const mm_offq_dims* d, int32_t T, int32_t B);
+/* Forward (behavior + target over all T+1 steps), loss, R2D2 priorities and the gradient of the
+ * loss w.r.t. P (written to grad; zero-initialised pads stay zero). stats: float[2] = loss, Q_tot
+ * mean (train_info); priorities [B] (PER only, may be NULL). ws: zero-initialised device scratch of
+ * mm_offq_workspace_bytes for these (T, B), reused across calls. Follow with mm_clip_adam over the
+ * whole [agent | mixer] vector (max_grad_norm, lr, opti_eps) to complete the update. */
+int mm_offq_loss_grad(const mm_offq_dims* d, const mm_offq_batch* b, const float* P, const float* PT, float* grad,
+                      void* ws, int64_t ws_bytes, float* stats, float* priorities, mm_stream_t s);
+/* get_q_values over a sequence: obs [L, R, D] (stacked rows), h0 [R, H] (NULL = zeros) ->
+ * q [L, R, A], h_out [R, H] (may be NULL). ws: mm_offq_qvals_workspace_bytes(d, L, R). */
+int64_t mm_offq_qvals_workspace_bytes(const mm_offq_dims* d, int32_t L, int64_t R);
+int mm_offq_q_values(const mm_offq_dims* d, const float* P, const float* obs, const float* h0, float* q, float* h_out,
+                     int32_t L, int64_t R, void* ws, int64_t ws_bytes, mm_stream_t s);
+/* soft_update: target <- target * (1 - tau) + source * tau over n floats (tau = 1: hard update). */
+int mm_offq_soft_update(float* target, const float* source, int64_t n, double tau, mm_stream_t s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -229,3 +229,30 @@ _SIGS += [
     ("mm_mappo_stats_from_sums", c_i32, [c_vp, c_i64, c_vp, c_vp]),
     ("mm_mappo_insert", c_i32, [c_vp, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 ]
+
+
+# ------------------------------------------------------------------ offpolicy episode QMix / VDN
+MM_OFFQ_VDN, MM_OFFQ_QMIX = 0, 1
+
+
+class OffqDims(ctypes.Structure):
+    _fields_ = [("n_agents", c_i32), ("obs_dim", c_i32), ("hidden", c_i32), ("n_actions", c_i32), ("mixer", c_i32),
+                ("state_dim", c_i32), ("mixer_hidden", c_i32), ("hyper_hidden", c_i32)]
+
+
+class OffqBatch(ctypes.Structure):
+    _fields_ = [("obs", c_vp), ("share_obs", c_vp), ("acts", c_vp), ("rewards", c_vp), ("dones_env", c_vp),
+                ("is_weight", c_vp), ("T", c_i32), ("B", c_i32), ("double_q", c_i32), ("huber", c_i32),
+                ("gamma", c_f32), ("huber_delta", c_f32), ("per_nu", c_f32), ("per_eps", c_f32)]
+
+
+_OD = ctypes.POINTER(OffqDims)
+_SIGS += [
+    ("mm_offq_param_counts", c_i32, [_OD, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+    ("mm_offq_mixer_offsets", c_i32, [_OD, ctypes.POINTER(c_i64)]),
+    ("mm_offq_workspace_bytes", c_i64, [_OD, c_i32, c_i32]),
+    ("mm_offq_loss_grad", c_i32, [_OD, ctypes.POINTER(OffqBatch), c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ("mm_offq_qvals_workspace_bytes", c_i64, [_OD, c_i32, c_i64]),
+    ("mm_offq_q_values", c_i32, [_OD, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_vp, c_i64, c_vp]),
+    ("mm_offq_soft_update", c_i32, [c_vp, c_vp, c_i64, c_f64, c_vp]),
+]
