@@ -28,92 +28,188 @@ constexpr int OQ_MAX_GEMM = 16;
 
 // ------------------------------------------------------------------ workspace layout
 struct OqWs {
-  int64_t sf, gi, hs, gates, act, qa, nqa, z1, w1o, w2o, b2o, qtot, dqtot, dqa, dw1o, dw2o, db2o, dz1, dh2, dg, gsoa,
-      wpart, gpart, red, ones, total;  // float offsets
+  int64_t a1, a2, st, gi, hs, gates, act, qa, nqa, z1, w1o, w2o, b2o, qtot, dqtot, dqa, dw1o, dw2o, db2o, dz1, dh2, dg, gsoa,
+      wpart, gpart, red, aerr, ones, total;  // float offsets
   int64_t NB, R1, Rb, rs1, rsb, TB;
   int NS, NG, ZW, NK;
 };
 
 static inline int64_t al64(int64_t x) { return (x + 63) / 64 * 64; }
 
+__device__ __forceinline__ float rl(float v, int i) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+}
+
 // ------------------------------------------------------------------ forward: non-recurrent layers
+// Saves of the behavior net (plain row-major): a1 / a2 [R][H] (post-ReLU), st [R][8] =
+// mu0, rs0, mu1, rs1, mu2, rs2, mu_r, rs_r.
+enum { ST_MU0 = 0, ST_RS0, ST_MU1, ST_RS1, ST_MU2, ST_RS2, ST_MUR, ST_RSR, ST_N };
+
 struct OqPreArgs {
   const float* P[2];
   const float* obs;
   float* gi[2];
-  float* sf;        // behavior SF save (tiled SoA, NS fields) or NULL
+  float* a1; float* a2; float* st;   // behavior saves or NULL
   int64_t R1, NB;
   int T1, B;        // steps (T+1) and episodes; stacked = 1: obs is [L][R][D] already
   int stacked;
 };
 
+// full-wave sum broadcast to every lane: DPP inside each 16-lane row (quad_perm 1032 / 2301,
+// row_ror 4 / 8), then the four row sums via v_readlane (no LDS round trips)
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x124>(v);
+  v += dpp<0x128>(v);
+  return (rl(v, 0) + rl(v, 16)) + (rl(v, 32) + rl(v, 48));
+}
+
+// Per-wave LDS broadcast of a 64-vector held one element per lane: lane j stores v, every lane then
+// reads the whole vector with 16 ds_read_b128 (same address in all lanes = broadcast). A wave's
+// LDS operations execute in order, so no barrier is needed inside the wave-private slot.
+template <int NV>
+__device__ __forceinline__ void bcast_put(float* slot, int j, const float (&v)[NV]) {
+#pragma unroll
+  for (int c = 0; c < NV; ++c) slot[c * 64 + j] = v[c];
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ float4 bcast_get4(const float* slot, int i4) {
+  return reinterpret_cast<const float4*>(slot)[i4];
+}
+
+__device__ __forceinline__ const float* obs_row(const float* obs, int stacked, int64_t r, int64_t NB, int B, int T1,
+                                                int D) {
+  if (stacked) return obs + r * D;
+  const int64_t t = r / NB, q = r - t * NB;
+  const int64_t i = q / B, b = q - i * B;
+  return obs + ((i * T1 + t) * B + b) * D;
+}
+
+// One wave per row at a time, lane j = feature j (H == 64; D <= 128 as two lane halves): the
+// lane's rows of W1, W2 and the three W_ih gate rows stay in VGPRs for all rows the wave visits;
+// activations are broadcast lane -> SGPR (v_readlane), LayerNorm statistics are wave reductions.
 template <int D, int H, int A>
 __global__ __launch_bounds__(256) void offq_pre_kernel(OqPreArgs a) {
+  static_assert(H == 64 && D <= 128, "lane-per-feature layout");
   using G = MGeo<D, H, A>;
-  using S = SF<H, A>;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int D0 = D < 64 ? D : 64, D1 = D - D0;
   const int y = blockIdx.y;
   const float* P = a.P[y];
-  // stage [0, Whh) and the input-gate bias
-  for (int i = threadIdx.x; i < G::Whh; i += blockDim.x) sm[i] = P[i];
-  for (int i = threadIdx.x; i < 3 * H; i += blockDim.x) sm[G::Whh + i] = P[G::bih + i];
-  __syncthreads();
-  const float* W = sm;
-  const float* bih = sm + G::Whh;
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (r >= a.R1) return;
-  const float* xp;
-  if (a.stacked) {
-    xp = a.obs + r * D;
-  } else {
-    const int64_t t = r / a.NB, q = r - t * a.NB;
-    const int64_t i = q / a.B, b = q - i * a.B;
-    xp = a.obs + ((i * a.T1 + t) * a.B + b) * D;
-  }
-  float x[D];
-  load_row<D>(xp, x);
-  float* sv = (y == 0 && a.sf) ? soa_col(a.sf, r, S::NS) : nullptr;
-  float mu, rs;
-  ln_stats<D>(x, mu, rs);
-  float f0[D];
-  ln_apply<D>(x, mu, rs, W + G::ln0_w, W + G::ln0_b, f0);
-  if (sv) {
-    soa_st1(sv, S::MU0, mu);
-    soa_st1(sv, S::RS0, rs);
-  }
-  float av[H], f[H];
-  matvec<H, D, G::Dp>(W + G::W1, W + G::b1, f0, av);
+  const int j = threadIdx.x & 63;
+  const int64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+  float w1[D], w2[H], wr[H], wz[H], wn[H];
 #pragma unroll
-  for (int i = 0; i < H; ++i) av[i] = fmaxf(av[i], 0.0f);
-  ln_stats<H>(av, mu, rs);
-  if (sv) {
-    soa_st<H>(sv, S::A1, av);
-    soa_st1(sv, S::MU1, mu);
-    soa_st1(sv, S::RS1, rs);
+  for (int k = 0; k < D; ++k) w1[k] = P[G::W1 + j * G::Dp + k];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    w2[k] = P[G::W2 + j * H + k];
+    wr[k] = P[G::Wih + j * H + k];
+    wz[k] = P[G::Wih + (H + j) * H + k];
+    wn[k] = P[G::Wih + (2 * H + j) * H + k];
   }
-  ln_apply<H>(av, mu, rs, W + G::ln1_w, W + G::ln1_b, f);
-  matvec<H, H, H>(W + G::W2, W + G::b2, f, av);
-#pragma unroll
-  for (int i = 0; i < H; ++i) av[i] = fmaxf(av[i], 0.0f);
-  ln_stats<H>(av, mu, rs);
-  if (sv) {
-    soa_st<H>(sv, S::A2, av);
-    soa_st1(sv, S::MU2, mu);
-    soa_st1(sv, S::RS2, rs);
+  const float g0a = j < D0 ? P[G::ln0_w + j] : 0.f, b0a = j < D0 ? P[G::ln0_b + j] : 0.f;
+  const float g0b = j < D1 ? P[G::ln0_w + 64 + j] : 0.f, b0b = j < D1 ? P[G::ln0_b + 64 + j] : 0.f;
+  const float b1 = P[G::b1 + j], g1 = P[G::ln1_w + j], c1 = P[G::ln1_b + j];
+  const float b2 = P[G::b2 + j], g2 = P[G::ln2_w + j], c2 = P[G::ln2_b + j];
+  const float bir = P[G::bih + j], biz = P[G::bih + H + j], bin = P[G::bih + 2 * H + j];
+  const bool save = y == 0 && a.a1;
+  __shared__ __attribute__((aligned(16))) float sm[4][128];
+  float* slot = sm[threadIdx.x >> 6];
+  // the next row's observation is loaded one row ahead
+  float xa_n = 0.f, xb_n = 0.f;
+  if (wid < a.R1) {
+    const float* xp = obs_row(a.obs, a.stacked, wid, a.NB, a.B, a.T1, D);
+    xa_n = j < D0 ? xp[j] : 0.f;
+    xb_n = j < D1 ? xp[64 + j] : 0.f;
   }
-  ln_apply<H>(av, mu, rs, W + G::ln2_w, W + G::ln2_b, f);
-  float* go = a.gi[y] + r * (3 * H);
-  for (int o = 0; o < 3 * H; o += 4) {
-    float4 v;
-    float* vp = &v.x;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float acc = bih[o + u];
-#pragma unroll
-      for (int i = 0; i < H; ++i) acc = fmaf(W[G::Wih + (o + u) * H + i], f[i], acc);
-      vp[u] = acc;
+  for (int64_t r = wid; r < a.R1; r += nw) {
+    const float xa = xa_n, xb = xb_n;
+    if (r + nw < a.R1) {
+      const float* xp = obs_row(a.obs, a.stacked, r + nw, a.NB, a.B, a.T1, D);
+      xa_n = j < D0 ? xp[j] : 0.f;
+      xb_n = j < D1 ? xp[64 + j] : 0.f;
     }
-    *reinterpret_cast<float4*>(go + o) = v;
+    // LN0
+    const float mu0 = wave_sum(xa + xb) / (float)D;
+    const float da = j < D0 ? xa - mu0 : 0.f, db = j < D1 ? xb - mu0 : 0.f;
+    const float rs0 = 1.0f / sqrtf(wave_sum(da * da + db * db) / (float)D + kLnEps);
+    const float fa = da * rs0 * g0a + b0a, fb = db * rs0 * g0b + b0b;
+    // L1 + ReLU + LN1
+    {
+      const float fv[2] = {fa, fb};
+      bcast_put<2>(slot, j, fv);
+    }
+    float s0 = b1, s1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < (D + 3) / 4; ++c) {
+      const float4 t4 = bcast_get4(slot, c);
+      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (4 * c + u < D) {
+          if (u & 1) s1 = fmaf(w1[4 * c + u], tv[u], s1);
+          else s0 = fmaf(w1[4 * c + u], tv[u], s0);
+        }
+    }
+    const float a1 = fmaxf(s0 + s1, 0.0f);
+    const float mu1 = wave_sum(a1) * (1.0f / H);
+    const float e1 = a1 - mu1;
+    const float rs1 = 1.0f / sqrtf(wave_sum(e1 * e1) * (1.0f / H) + kLnEps);
+    const float f1 = e1 * rs1 * g1 + c1;
+    // L2 + ReLU + LN2
+    {
+      const float fv[1] = {f1};
+      bcast_put<1>(slot, j, fv);
+    }
+    s0 = b2;
+    s1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < H / 4; ++c) {
+      const float4 t4 = bcast_get4(slot, c);
+      s0 = fmaf(w2[4 * c], t4.x, s0);
+      s1 = fmaf(w2[4 * c + 1], t4.y, s1);
+      s0 = fmaf(w2[4 * c + 2], t4.z, s0);
+      s1 = fmaf(w2[4 * c + 3], t4.w, s1);
+    }
+    const float a2 = fmaxf(s0 + s1, 0.0f);
+    const float mu2 = wave_sum(a2) * (1.0f / H);
+    const float e2 = a2 - mu2;
+    const float rs2 = 1.0f / sqrtf(wave_sum(e2 * e2) * (1.0f / H) + kLnEps);
+    const float x2 = e2 * rs2 * g2 + c2;
+    // GRU input projection
+    {
+      const float fv[1] = {x2};
+      bcast_put<1>(slot, j, fv);
+    }
+    float gr = bir, gz = biz, gn = bin;
+#pragma unroll
+    for (int c = 0; c < H / 4; ++c) {
+      const float4 t4 = bcast_get4(slot, c);
+      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        gr = fmaf(wr[4 * c + u], tv[u], gr);
+        gz = fmaf(wz[4 * c + u], tv[u], gz);
+        gn = fmaf(wn[4 * c + u], tv[u], gn);
+      }
+    }
+    float* go = a.gi[y] + r * (3 * H);
+    go[j] = gr;
+    go[H + j] = gz;
+    go[2 * H + j] = gn;
+    if (save) {
+      a.a1[r * H + j] = a1;
+      a.a2[r * H + j] = a2;
+      if (j < 6) {
+        const float sv = j == 0 ? mu0 : j == 1 ? rs0 : j == 2 ? mu1 : j == 3 ? rs1 : j == 4 ? mu2 : rs2;
+        a.st[r * ST_N + j] = sv;
+      }
+    }
   }
 }
 
@@ -129,9 +225,6 @@ struct OqRecArgs {
   int L, whh, bhh;
 };
 
-__device__ __forceinline__ float rl(float v, int i) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
-}
 
 // one wave per row q; lane j owns hidden unit j (H == 64)
 template <int H>
@@ -151,22 +244,48 @@ __global__ __launch_bounds__(256) void offq_rec_kernel(OqRecArgs a) {
   }
   const float br = P[a.bhh + j], bz = P[a.bhh + H + j], bn = P[a.bhh + 2 * H + j];
   float h = (a.h0 && y == 0) ? a.h0[q * H + j] : 0.0f;
+  __shared__ __attribute__((aligned(16))) float sm[4][64];
+  float* slot = sm[threadIdx.x >> 6];
   const float* gi = a.gi[y];
   float* hs = a.hs[y];
   float* gates = y == 0 ? a.gates : nullptr;
+  // next step's input projections are loaded one step ahead (off the recurrence's critical path)
+  const float* gp = gi + q * 3 * H + j;
+  float gr = gp[0], gz = gp[H], gn = gp[2 * H];
   for (int t = 0; t < a.L; ++t) {
     const int64_t r = (int64_t)t * a.NB + q;
-    const float gr = gi[r * 3 * H + j], gz = gi[r * 3 * H + H + j], gn = gi[r * 3 * H + 2 * H + j];
-    float ar = br, az = bz, an = bn;
-#pragma unroll
-    for (int i = 0; i < H; ++i) {
-      const float hi = rl(h, i);
-      ar = fmaf(wr[i], hi, ar);
-      az = fmaf(wz[i], hi, az);
-      an = fmaf(wn[i], hi, an);
+    float gr1 = 0.f, gz1 = 0.f, gn1 = 0.f;
+    if (t + 1 < a.L) {
+      const float* np_ = gp + (int64_t)(t + 1) * a.NB * 3 * H;
+      gr1 = np_[0];
+      gz1 = np_[H];
+      gn1 = np_[2 * H];
     }
-    const float rr = sigmoidf_(gr + ar);
-    const float zz = sigmoidf_(gz + az);
+    // two partial sums per gate halve the dependent FMA chain; h is broadcast through LDS
+    {
+      const float fv[1] = {h};
+      bcast_put<1>(slot, j, fv);
+    }
+    float ar0 = br, az0 = bz, an0 = bn, ar1 = 0.f, az1 = 0.f, an1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < H / 4; ++c) {
+      const float4 t4 = bcast_get4(slot, c);
+      ar0 = fmaf(wr[4 * c], t4.x, ar0);
+      az0 = fmaf(wz[4 * c], t4.x, az0);
+      an0 = fmaf(wn[4 * c], t4.x, an0);
+      ar1 = fmaf(wr[4 * c + 1], t4.y, ar1);
+      az1 = fmaf(wz[4 * c + 1], t4.y, az1);
+      an1 = fmaf(wn[4 * c + 1], t4.y, an1);
+      ar0 = fmaf(wr[4 * c + 2], t4.z, ar0);
+      az0 = fmaf(wz[4 * c + 2], t4.z, az0);
+      an0 = fmaf(wn[4 * c + 2], t4.z, an0);
+      ar1 = fmaf(wr[4 * c + 3], t4.w, ar1);
+      az1 = fmaf(wz[4 * c + 3], t4.w, az1);
+      an1 = fmaf(wn[4 * c + 3], t4.w, an1);
+    }
+    const float an = an0 + an1;
+    const float rr = sigmoidf_(gr + (ar0 + ar1));
+    const float zz = sigmoidf_(gz + (az0 + az1));
     const float nn = tanhf_(gn + rr * an);
     h = nn + zz * (h - nn);
     hs[r * H + j] = h;
@@ -177,6 +296,9 @@ __global__ __launch_bounds__(256) void offq_rec_kernel(OqRecArgs a) {
       g[2 * H + j] = nn;
       g[3 * H + j] = an;
     }
+    gr = gr1;
+    gz = gz1;
+    gn = gn1;
   }
   if (a.hout && y == 0) a.hout[q * H + j] = h;
 }
@@ -185,7 +307,7 @@ __global__ __launch_bounds__(256) void offq_rec_kernel(OqRecArgs a) {
 struct OqPostArgs {
   const float* P[2];
   const float* hs[2];
-  float* sf;            // behavior MUR / RSR (or NULL)
+  float* st;            // behavior mu_r / rs_r into st[r][6..7] (or NULL)
   float* q_out;         // [R1][A] of net 0 (or NULL)
   const float* acts;    // one-hot [N][T][B][A] (or NULL: no selection)
   int32_t* act;         // [Rb] chosen action index of the behavior row
@@ -198,7 +320,6 @@ struct OqPostArgs {
 template <int D, int H, int A>
 __global__ __launch_bounds__(256) void offq_post_kernel(OqPostArgs a) {
   using G = MGeo<D, H, A>;
-  using S = SF<H, A>;
   const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (r >= a.R1) return;
   float qv[2][A];
@@ -208,10 +329,9 @@ __global__ __launch_bounds__(256) void offq_post_kernel(OqPostArgs a) {
     load_row<H>(a.hs[y] + r * H, h);
     float mu, rs;
     ln_stats<H>(h, mu, rs);
-    if (y == 0 && a.sf) {
-      float* sv = soa_col(a.sf, r, S::NS);
-      soa_st1(sv, S::MUR, mu);
-      soa_st1(sv, S::RSR, rs);
+    if (y == 0 && a.st) {
+      a.st[r * ST_N + ST_MUR] = mu;
+      a.st[r * ST_N + ST_RSR] = rs;
     }
     ln_apply<H>(h, mu, rs, P + G::lnr_w, P + G::lnr_b, yv);
     float o[A];
@@ -435,28 +555,41 @@ struct OqMixArgs {
 
 __device__ __forceinline__ float elu1(float x) { return x > 0.0f ? x : expm1f(x); }
 
+// KP = pow2 >= K lanes per mixer row (K <= 64): lane k owns mixing unit k; sums over k by shuffles
+__device__ __forceinline__ float lanes_sum(float v, int kp) {
+  for (int o = kp >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void offq_mix_fwd_kernel(OqMixArgs a) {
   const int y = blockIdx.y;
-  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (y >= a.nets || m >= a.TB) return;
-  const float* q = a.q[y] + m * a.N;
+  if (y >= a.nets) return;
   if (a.vdn) {
+    const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (m >= a.TB) return;
+    const float* q = a.q[y] + m * a.N;
     float s = 0.0f;
     for (int i = 0; i < a.N; ++i) s += q[i];
     a.qtot[y][m] = s;
     return;
   }
-  const float* w1 = a.w1o[y] + m * (int64_t)a.N * a.K;
-  const float* b1 = a.z1[y] + m * a.ZW + 2 * a.Hh;
-  const float* w2 = a.w2o[y] + m * a.K;
-  float out = 0.0f;
-  for (int k = 0; k < a.K; ++k) {
+  int kp = 1;
+  while (kp < a.K) kp <<= 1;
+  const int k = threadIdx.x & (kp - 1);
+  const int64_t m = blockIdx.x * (int64_t)(blockDim.x / kp) + threadIdx.x / kp;
+  const bool on = m < a.TB;
+  const int64_t mm_ = on ? m : 0;
+  const float* q = a.q[y] + mm_ * a.N;
+  const float* w1 = a.w1o[y] + mm_ * (int64_t)a.N * a.K;
+  float c = 0.0f;
+  if (on && k < a.K) {
     float s = 0.0f;
     for (int i = 0; i < a.N; ++i) s = fmaf(q[i], fabsf(w1[i * a.K + k]), s);
-    const float hid = elu1(s + b1[k]);
-    out = fmaf(hid, fabsf(w2[k]), out);
+    const float hid = elu1(s + a.z1[y][mm_ * a.ZW + 2 * a.Hh + k]);
+    c = hid * fabsf(a.w2o[y][mm_ * a.K + k]);
   }
-  a.qtot[y][m] = out + a.b2o[y][m];
+  c = lanes_sum(c, kp);
+  if (on && k == 0) a.qtot[y][m] = c + a.b2o[y][m];
 }
 
 // ------------------------------------------------------------------ loss, priorities, dQ_tot
@@ -469,67 +602,70 @@ struct OqLossArgs {
   float* stats;                              // [2]
   float* prio;                               // [B] or NULL
   float* ones;
+  float* aerr;                               // [T][B] scratch |err|
   int T, B, huber;
   float gamma, delta, nu, eps;
 };
 
-__device__ float block_sum256(float v, float* sh) {
-  sh[threadIdx.x] = v;
+__device__ float block_sum1024(float v, float* sh) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
-    __syncthreads();
-  }
-  const float r = sh[0];
+  float r = 0.0f;
+  for (int w = 0; w < 16; ++w) r += sh[w];
   __syncthreads();
   return r;
 }
 
-__global__ __launch_bounds__(256) void offq_loss_kernel(OqLossArgs a) {
-  __shared__ float sh[256];
+// one block of 1024 threads: elementwise over the T*B (t, b) entries, then per-episode priorities
+__global__ __launch_bounds__(1024) void offq_loss_kernel(OqLossArgs a) {
+  __shared__ float sh[16];
   if (threadIdx.x == 0) a.ones[0] = 1.0f;
-  const int T = a.T, B = a.B;
+  const int T = a.T, B = a.B, TB = T * B;
   float cnt = 0.0f, qs = 0.0f;
-  for (int b = threadIdx.x; b < B; b += 256)
-    for (int t = 0; t < T; ++t) {
-      const float keep = 1.0f - (t > 0 ? a.dn[(t - 1) * B + b] : 0.0f);
-      cnt += keep;
-      qs += a.qtot[t * B + b] * keep;
-    }
-  const float denom = block_sum256(cnt, sh);
-  const float qsum = block_sum256(qs, sh);
-  float lsum = 0.0f;
-  for (int b = threadIdx.x; b < B; b += 256) {
-    const float w = a.isw ? a.isw[b] : 1.0f;
-    const float g = w / denom;
-    float le_sum = 0.0f, abs_sum = 0.0f, abs_max = 0.0f;
-    for (int t = 0; t < T; ++t) {
-      const float d = a.dn[t * B + b];
-      const float keep = 1.0f - (t > 0 ? a.dn[(t - 1) * B + b] : 0.0f);
-      const float y = a.rew[t * B + b] + (1.0f - d) * a.gamma * a.qtot_t[t * B + b];
-      const float e = (a.qtot[t * B + b] - y) * keep;
-      const float ae = fabsf(e);
-      float le, dle;
-      if (a.huber) {
-        const bool in = ae <= a.delta;
-        le = in ? e * e / 2.0f : a.delta * (ae - a.delta / 2.0f);
-        dle = in ? e : a.delta * (e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f));
-      } else {
-        le = e * e;
-        dle = 2.0f * e;
-      }
-      le_sum += le;
-      abs_sum += ae;
-      abs_max = fmaxf(abs_max, ae);
-      a.dqtot[t * B + b] = g * dle * keep;
-    }
-    lsum += le_sum * w;
-    if (a.prio) a.prio[b] = (1.0f - a.nu) * (abs_sum / (float)T) + a.nu * abs_max + a.eps;
+  for (int e = threadIdx.x; e < TB; e += 1024) {
+    const float keep = 1.0f - (e >= B ? a.dn[e - B] : 0.0f);
+    cnt += keep;
+    qs += a.qtot[e] * keep;
   }
-  const float loss = block_sum256(lsum, sh);
+  const float denom = block_sum1024(cnt, sh);
+  const float qsum = block_sum1024(qs, sh);
+  float lsum = 0.0f;
+  for (int e = threadIdx.x; e < TB; e += 1024) {
+    const int b = e % B;
+    const float w = a.isw ? a.isw[b] : 1.0f;
+    const float keep = 1.0f - (e >= B ? a.dn[e - B] : 0.0f);
+    const float y = a.rew[e] + (1.0f - a.dn[e]) * a.gamma * a.qtot_t[e];
+    const float er = (a.qtot[e] - y) * keep;
+    const float ae = fabsf(er);
+    float le, dle;
+    if (a.huber) {
+      const bool in = ae <= a.delta;
+      le = in ? er * er / 2.0f : a.delta * (ae - a.delta / 2.0f);
+      dle = in ? er : a.delta * (er > 0.0f ? 1.0f : (er < 0.0f ? -1.0f : 0.0f));
+    } else {
+      le = er * er;
+      dle = 2.0f * er;
+    }
+    a.dqtot[e] = (w / denom) * dle * keep;
+    a.aerr[e] = ae;
+    lsum += le * w;
+  }
+  const float loss = block_sum1024(lsum, sh);  // (its barriers also order the aerr writes)
+  if (a.prio) {
+    for (int b = threadIdx.x; b < B; b += 1024) {
+      float s = 0.0f, mx = 0.0f;
+      for (int t = 0; t < T; ++t) {
+        const float v = a.aerr[t * B + b];
+        s += v;
+        mx = fmaxf(mx, v);
+      }
+      a.prio[b] = (1.0f - a.nu) * (s / (float)T) + a.nu * mx + a.eps;
+    }
+  }
   if (threadIdx.x == 0) {
     a.stats[0] = loss / denom;
-    a.stats[1] = qsum / (float)(T * B);
+    a.stats[1] = qsum / (float)TB;
   }
 }
 
@@ -542,44 +678,50 @@ struct OqMixBwdArgs {
 };
 
 __global__ __launch_bounds__(256) void offq_mix_bwd_kernel(OqMixBwdArgs a) {
-  const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (m >= a.TB) return;
-  const float g = a.dqtot[m];
-  float* dq = a.dqa + m * a.N;
   if (a.vdn) {
-    for (int i = 0; i < a.N; ++i) dq[i] = g;
+    const int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (m >= a.TB) return;
+    const float g = a.dqtot[m];
+    for (int i = 0; i < a.N; ++i) a.dqa[m * a.N + i] = g;
     return;
   }
-  const float* q = a.q + m * a.N;
-  const float* w1 = a.w1o + m * (int64_t)a.N * a.K;
-  const float* b1 = a.z1 + m * a.ZW + 2 * a.Hh;
-  const float* w2 = a.w2o + m * a.K;
-  float* dw1 = a.dw1o + m * (int64_t)a.N * a.K;
-  float* dw2 = a.dw2o + m * a.K;
-  float* db1 = a.dz1 + m * a.ZW + 2 * a.Hh;
-  a.db2o[m] = g;
-  for (int i = 0; i < a.N; ++i) dq[i] = 0.0f;
-  for (int k = 0; k < a.K; ++k) {
+  int kp = 1;
+  while (kp < a.K) kp <<= 1;
+  const int k = threadIdx.x & (kp - 1);
+  const int64_t m = blockIdx.x * (int64_t)(blockDim.x / kp) + threadIdx.x / kp;
+  const bool on = m < a.TB && k < a.K;
+  const int64_t mm_ = m < a.TB ? m : 0;
+  const float g = a.dqtot[mm_];
+  const float* q = a.q + mm_ * a.N;
+  const float* w1 = a.w1o + mm_ * (int64_t)a.N * a.K;
+  float dpre = 0.0f;
+  if (on) {
     float s = 0.0f;
     for (int i = 0; i < a.N; ++i) s = fmaf(q[i], fabsf(w1[i * a.K + k]), s);
-    const float pre = s + b1[k];
+    const float pre = s + a.z1[mm_ * a.ZW + 2 * a.Hh + k];
     const float hid = elu1(pre);
-    const float w2k = w2[k];
+    const float w2k = a.w2o[mm_ * a.K + k];
     // |w2|' = sign(w2) (0 at 0); elu' = 1 (x > 0) or exp(x) = elu(x) + 1
-    dw2[k] = g * hid * (w2k > 0.0f ? 1.0f : (w2k < 0.0f ? -1.0f : 0.0f));
-    const float dpre = g * fabsf(w2k) * (pre > 0.0f ? 1.0f : hid + 1.0f);
-    db1[k] = dpre;
-    for (int i = 0; i < a.N; ++i) {
+    a.dw2o[mm_ * a.K + k] = g * hid * (w2k > 0.0f ? 1.0f : (w2k < 0.0f ? -1.0f : 0.0f));
+    dpre = g * fabsf(w2k) * (pre > 0.0f ? 1.0f : hid + 1.0f);
+    a.dz1[mm_ * a.ZW + 2 * a.Hh + k] = dpre;
+    if (k == 0) a.db2o[mm_] = g;
+  }
+  for (int i = 0; i < a.N; ++i) {
+    float c = 0.0f;
+    if (on) {
       const float wv = w1[i * a.K + k];
-      dw1[i * a.K + k] = q[i] * dpre * (wv > 0.0f ? 1.0f : (wv < 0.0f ? -1.0f : 0.0f));
-      dq[i] = fmaf(fabsf(wv), dpre, dq[i]);
+      a.dw1o[mm_ * (int64_t)a.N * a.K + i * a.K + k] = q[i] * dpre * (wv > 0.0f ? 1.0f : (wv < 0.0f ? -1.0f : 0.0f));
+      c = fabsf(wv) * dpre;
     }
+    c = lanes_sum(c, kp);
+    if (m < a.TB && k == 0) a.dqa[m * a.N + i] = c;
   }
 }
 
 // ------------------------------------------------------------------ agent backward: heads
 struct OqHeadBwdArgs {
-  const float* P; const float* hs; const float* sf; const int32_t* act; const float* dqa;
+  const float* P; const float* hs; const float* st; const int32_t* act; const float* dqa;
   float* gsoa; float* dh2;
   int64_t Rb, NB;
   int B, N;
@@ -588,7 +730,6 @@ struct OqHeadBwdArgs {
 template <int D, int H, int A>
 __global__ __launch_bounds__(256) void offq_head_bwd_kernel(OqHeadBwdArgs a) {
   using G = MGeo<D, H, A>;
-  using S = SF<H, A>;
   using F = GF<D, H, A>;
   const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (r >= a.Rb) return;
@@ -599,12 +740,11 @@ __global__ __launch_bounds__(256) void offq_head_bwd_kernel(OqHeadBwdArgs a) {
   float dout[A];
 #pragma unroll
   for (int k = 0; k < A; ++k) dout[k] = k == ai ? dq : 0.0f;
-  const float* sv = soa_col(a.sf, r, S::NS);
   float* go = soa_col(a.gsoa, r, F::NG);
   const float* W = a.P;
   float h[H], xr[H], yv[H];
   load_row<H>(a.hs + r * H, h);
-  const float mur = soa_ld1(sv, S::MUR), rsr = soa_ld1(sv, S::RSR);
+  const float mur = a.st[r * ST_N + ST_MUR], rsr = a.st[r * ST_N + ST_RSR];
 #pragma unroll
   for (int k = 0; k < H; ++k) {
     xr[k] = (h[k] - mur) * rsr;
@@ -647,12 +787,26 @@ __global__ __launch_bounds__(256) void offq_rec_bwd_kernel(OqRecBwdArgs a) {
     wn[k] = a.P[a.whh + (2 * H + k) * H + j];
   }
   float dnext = 0.0f;
+  __shared__ __attribute__((aligned(16))) float sm[4][3 * 64];
+  float* slot = sm[threadIdx.x >> 6];
+  // operands of step t-1 are loaded one step ahead
+  auto load = [&](int t, float& d2, float& rr, float& zz, float& nn, float& ghn, float& hin) {
+    const int64_t r = (int64_t)t * a.NB + q;
+    d2 = a.dh2[r * H + j];
+    const float* g = a.gates + r * 4 * H;
+    rr = g[j];
+    zz = g[H + j];
+    nn = g[2 * H + j];
+    ghn = g[3 * H + j];
+    hin = t > 0 ? a.hs[(r - a.NB) * H + j] : 0.0f;
+  };
+  float d2, rr, zz, nn, ghn, hin;
+  load(a.T - 1, d2, rr, zz, nn, ghn, hin);
   for (int t = a.T - 1; t >= 0; --t) {
     const int64_t r = (int64_t)t * a.NB + q;
-    const float dh = a.dh2[r * H + j] + dnext;
-    const float* g = a.gates + r * 4 * H;
-    const float rr = g[j], zz = g[H + j], nn = g[2 * H + j], ghn = g[3 * H + j];
-    const float hin = t > 0 ? a.hs[(r - a.NB) * H + j] : 0.0f;
+    float d2n = 0.f, rrn = 0.f, zzn = 0.f, nnn = 0.f, ghnn = 0.f, hinn = 0.f;
+    if (t > 0) load(t - 1, d2n, rrn, zzn, nnn, ghnn, hinn);
+    const float dh = d2 + dnext;
     const float dn = dh * (1.0f - zz);
     const float dz = dh * (hin - nn);
     const float dpn = dn * (1.0f - nn * nn);
@@ -666,20 +820,39 @@ __global__ __launch_bounds__(256) void offq_rec_bwd_kernel(OqRecBwdArgs a) {
     o[3 * H + j] = dgr;
     o[4 * H + j] = dgz;
     o[5 * H + j] = dghn;
-    float acc = dh * zz;
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-      acc = fmaf(wr[k], rl(dgr, k), acc);
-      acc = fmaf(wz[k], rl(dgz, k), acc);
-      acc = fmaf(wn[k], rl(dghn, k), acc);
+    {
+      const float fv[3] = {dgr, dgz, dghn};
+      bcast_put<3>(slot, j, fv);
     }
-    dnext = acc;
+    float acc0 = dh * zz, acc1 = 0.0f, acc2 = 0.0f;
+#pragma unroll
+    for (int c = 0; c < H / 4; ++c) {
+      const float4 tr = bcast_get4(slot, c), tz = bcast_get4(slot, 16 + c), tn = bcast_get4(slot, 32 + c);
+      const float vr[4] = {tr.x, tr.y, tr.z, tr.w}, vz[4] = {tz.x, tz.y, tz.z, tz.w}, vn[4] = {tn.x, tn.y, tn.z, tn.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc0 = fmaf(wr[4 * c + u], vr[u], acc0);
+        acc1 = fmaf(wz[4 * c + u], vz[u], acc1);
+        acc2 = fmaf(wn[4 * c + u], vn[u], acc2);
+      }
+    }
+    dnext = acc0 + acc1 + acc2;
+    d2 = d2n;
+    rr = rrn;
+    zz = zzn;
+    nn = nnn;
+    ghn = ghnn;
+    hin = hinn;
   }
 }
 
 // ------------------------------------------------------------------ agent backward: MLP / LN layers
+// Lane-per-feature like the forward: lane k keeps column k of W_ih (3 gates), W2 and W1 in VGPRs,
+// so every transposed mat-vec is 64 readlane broadcasts + FMAs; the LayerNorm backward sums are
+// wave reductions. Writes the GF operands of the weight-gradient reduction (tiled SoA).
 struct OqPreBwdArgs {
-  const float* P; const float* obs; const float* sf; const float* hs; const float* dg;
+  const float* P; const float* obs; const float* a1; const float* a2; const float* st; const float* hs;
+  const float* dg;
   float* gsoa;
   int64_t Rb, NB;
   int T1, B;
@@ -687,102 +860,129 @@ struct OqPreBwdArgs {
 
 template <int D, int H, int A>
 __global__ __launch_bounds__(256) void offq_pre_bwd_kernel(OqPreBwdArgs a) {
+  static_assert(H == 64 && D <= 128, "lane-per-feature layout");
   using G = MGeo<D, H, A>;
-  using S = SF<H, A>;
   using F = GF<D, H, A>;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  for (int i = threadIdx.x; i < G::Whh; i += blockDim.x) sm[i] = a.P[i];
-  __syncthreads();
-  const float* W = sm;
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (r >= a.Rb) return;
-  const int64_t t = r / a.NB, qq = r - t * a.NB;
-  const int64_t i = qq / a.B, b = qq - i * a.B;
-  const float* sv = soa_col(a.sf, r, S::NS);
-  float* go = soa_col(a.gsoa, r, F::NG);
-  // GRU operands: dgi, dgh, h_in; dx2 = W_ih^T dgi
-  const float* dgp = a.dg + r * 6 * H;
-  float dx[H];
+  constexpr int D0 = D < 64 ? D : 64, D1 = D - D0;
+  const float* P = a.P;
+  const int k = threadIdx.x & 63;
+  const int64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+  constexpr int HB = D1 > 0 ? H : 1;  // second W1 column half only when D > 64
+  float cr[H], cz[H], cn[H], c2[H], c1a[H], c1bb[HB];
 #pragma unroll
-  for (int k = 0; k < H; ++k) dx[k] = 0.0f;
-  for (int o = 0; o < 3 * H; o += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(dgp + o);
-    const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      soa_st1(go, F::DGI + o + u, vv[u]);
-#pragma unroll
-      for (int k = 0; k < H; ++k) dx[k] = fmaf(W[G::Wih + (o + u) * H + k], vv[u], dx[k]);
-    }
+  for (int jj = 0; jj < H; ++jj) {
+    cr[jj] = P[G::Wih + jj * H + k];
+    cz[jj] = P[G::Wih + (H + jj) * H + k];
+    cn[jj] = P[G::Wih + (2 * H + jj) * H + k];
+    c2[jj] = P[G::W2 + jj * H + k];
+    c1a[jj] = k < D0 ? P[G::W1 + jj * G::Dp + k] : 0.f;
   }
-  for (int o = 0; o < 3 * H; ++o) soa_st1(go, F::DGH + o, dgp[3 * H + o]);
-  {
-    float hin[H];
-    if (t > 0) {
-      load_row<H>(a.hs + (r - a.NB) * H, hin);
-    } else {
 #pragma unroll
-      for (int k = 0; k < H; ++k) hin[k] = 0.0f;
+  for (int jj = 0; jj < HB; ++jj) c1bb[jj] = (D1 > 0 && k < D1) ? P[G::W1 + jj * G::Dp + 64 + k] : 0.f;
+  const float g2 = P[G::ln2_w + k], c2b = P[G::ln2_b + k], g1 = P[G::ln1_w + k], c1 = P[G::ln1_b + k];
+  const float g0a = k < D0 ? P[G::ln0_w + k] : 0.f, b0a = k < D0 ? P[G::ln0_b + k] : 0.f;
+  const float g0b = k < D1 ? P[G::ln0_w + 64 + k] : 0.f, b0b = k < D1 ? P[G::ln0_b + 64 + k] : 0.f;
+  __shared__ __attribute__((aligned(16))) float sm[4][3 * 64];
+  float* slot = sm[threadIdx.x >> 6];
+  for (int64_t r = wid; r < a.Rb; r += nw) {
+    float* go = soa_col(a.gsoa, r, F::NG);
+    const float* dgp = a.dg + r * 6 * H;
+    const float dr = dgp[k], dz = dgp[H + k], dn = dgp[2 * H + k];
+    go[(F::DGI + k) * 64] = dr;
+    go[(F::DGI + H + k) * 64] = dz;
+    go[(F::DGI + 2 * H + k) * 64] = dn;
+    go[(F::DGH + k) * 64] = dgp[3 * H + k];
+    go[(F::DGH + H + k) * 64] = dgp[4 * H + k];
+    go[(F::DGH + 2 * H + k) * 64] = dgp[5 * H + k];
+    go[(F::HIN + k) * 64] = r >= a.NB ? a.hs[(r - a.NB) * H + k] : 0.0f;
+    // dx2 = W_ih^T dgi
+    {
+      const float fv[3] = {dr, dz, dn};
+      bcast_put<3>(slot, k, fv);
     }
-    soa_st<H>(go, F::HIN, hin);
-  }
-  // x2 = LN2(a2)
-  float ah[H], xh[H], da[H], tt[H];
-  {
-    soa_ld<H>(sv, S::A2, ah);
-    const float mu = soa_ld1(sv, S::MU2), rs = soa_ld1(sv, S::RS2);
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      xh[k] = (ah[k] - mu) * rs;
-      tt[k] = xh[k] * W[G::ln2_w + k] + W[G::ln2_b + k];
-    }
-    soa_st<H>(go, F::X2, tt);
-    ln_bwd<H>(dx, xh, rs, W + G::ln2_w, da);
+    for (int c = 0; c < H / 4; ++c) {
+      const float4 tr = bcast_get4(slot, c), tz = bcast_get4(slot, 16 + c), tn = bcast_get4(slot, 32 + c);
+      const float vr[4] = {tr.x, tr.y, tr.z, tr.w}, vz[4] = {tz.x, tz.y, tz.z, tz.w}, vn[4] = {tn.x, tn.y, tn.z, tn.w};
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      tt[k] = dx[k] * xh[k];
-      da[k] = ah[k] > 0.0f ? da[k] : 0.0f;
+      for (int u = 0; u < 4; ++u) {
+        x0 = fmaf(cr[4 * c + u], vr[u], x0);
+        x1 = fmaf(cz[4 * c + u], vz[u], x1);
+        x2 = fmaf(cn[4 * c + u], vn[u], x2);
+      }
     }
-    soa_st<H>(go, F::DX2, dx);
-    soa_st<H>(go, F::P2, tt);
-    soa_st<H>(go, F::DPRE2, da);
-  }
-  // x1 = LN1(a1)
-  {
-    soa_ld<H>(sv, S::A1, ah);
-    const float mu = soa_ld1(sv, S::MU1), rs = soa_ld1(sv, S::RS1);
+    const float* sp = a.st + r * ST_N;
+    // LN2 backward (x2 = LN2(a2)), ReLU
+    float dx = x0 + x1 + x2;
+    float av = a.a2[r * H + k];
+    float xh = (av - sp[ST_MU2]) * sp[ST_RS2];
+    go[(F::X2 + k) * 64] = xh * g2 + c2b;
+    float gg = dx * g2;
+    float sg = wave_sum(gg) * (1.0f / H), sgx = wave_sum(gg * xh) * (1.0f / H);
+    float dpre = sp[ST_RS2] * (gg - sg - xh * sgx);
+    dpre = av > 0.0f ? dpre : 0.0f;
+    go[(F::DX2 + k) * 64] = dx;
+    go[(F::P2 + k) * 64] = dx * xh;
+    go[(F::DPRE2 + k) * 64] = dpre;
+    // dx1 = W2^T dpre2, LN1 backward, ReLU
+    {
+      const float fv[1] = {dpre};
+      bcast_put<1>(slot, k, fv);
+    }
+    x0 = 0.f;
+    x1 = 0.f;
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      xh[k] = (ah[k] - mu) * rs;
-      tt[k] = xh[k] * W[G::ln1_w + k] + W[G::ln1_b + k];
+    for (int c = 0; c < H / 4; ++c) {
+      const float4 t4 = bcast_get4(slot, c);
+      x0 = fmaf(c2[4 * c], t4.x, x0);
+      x1 = fmaf(c2[4 * c + 1], t4.y, x1);
+      x0 = fmaf(c2[4 * c + 2], t4.z, x0);
+      x1 = fmaf(c2[4 * c + 3], t4.w, x1);
     }
-    soa_st<H>(go, F::F1, tt);
-    matvec_t<H, H, H>(W + G::W2, da, dx);
-    ln_bwd<H>(dx, xh, rs, W + G::ln1_w, da);
+    dx = x0 + x1;
+    av = a.a1[r * H + k];
+    xh = (av - sp[ST_MU1]) * sp[ST_RS1];
+    go[(F::F1 + k) * 64] = xh * g1 + c1;
+    gg = dx * g1;
+    sg = wave_sum(gg) * (1.0f / H);
+    sgx = wave_sum(gg * xh) * (1.0f / H);
+    dpre = sp[ST_RS1] * (gg - sg - xh * sgx);
+    dpre = av > 0.0f ? dpre : 0.0f;
+    go[(F::DX1 + k) * 64] = dx;
+    go[(F::P1 + k) * 64] = dx * xh;
+    go[(F::DPRE1 + k) * 64] = dpre;
+    // df0 = W1^T dpre1 (lanes k < D0, and 64 + k < D), LN0 operands
+    {
+      const float fv[1] = {dpre};
+      bcast_put<1>(slot, k, fv);
+    }
+    x0 = 0.f;
+    x1 = 0.f;
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      tt[k] = dx[k] * xh[k];
-      da[k] = ah[k] > 0.0f ? da[k] : 0.0f;
-    }
-    soa_st<H>(go, F::DX1, dx);
-    soa_st<H>(go, F::P1, tt);
-    soa_st<H>(go, F::DPRE1, da);
-  }
-  // f0 = LN0(obs)
-  {
-    float x0[D], df0[D];
-    load_row<D>(a.obs + ((i * a.T1 + t) * a.B + b) * D, x0);
-    const float mu = soa_ld1(sv, S::MU0), rs = soa_ld1(sv, S::RS0);
-    matvec_t<H, D, G::Dp>(W + G::W1, da, df0);
-    soa_st<D>(go, F::DF0, df0);
+    for (int c = 0; c < H / 4; ++c) {
+      const float4 t4 = bcast_get4(slot, c);
+      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
-    for (int k = 0; k < D; ++k) {
-      const float xh0 = (x0[k] - mu) * rs;
-      df0[k] *= xh0;
-      x0[k] = xh0 * W[G::ln0_w + k] + W[G::ln0_b + k];
+      for (int u = 0; u < 4; ++u) {
+        x0 = fmaf(c1a[4 * c + u], tv[u], x0);
+        if constexpr (D1 > 0) x1 = fmaf(c1bb[4 * c + u], tv[u], x1);
+      }
     }
-    soa_st<D>(go, F::P0, df0);
-    soa_st<D>(go, F::F0, x0);
+    const float* xp = obs_row(a.obs, 0, r, a.NB, a.B, a.T1, D);
+    const float mu0 = sp[ST_MU0], rs0 = sp[ST_RS0];
+    if (k < D0) {
+      const float xh0 = (xp[k] - mu0) * rs0;
+      go[(F::DF0 + k) * 64] = x0;
+      go[(F::P0 + k) * 64] = x0 * xh0;
+      go[(F::F0 + k) * 64] = xh0 * g0a + b0a;
+    }
+    if (k < D1) {
+      const float xh0 = (xp[64 + k] - mu0) * rs0;
+      go[(F::DF0 + 64 + k) * 64] = x1;
+      go[(F::P0 + 64 + k) * 64] = x1 * xh0;
+      go[(F::F0 + 64 + k) * 64] = xh0 * g0b + b0b;
+    }
   }
 }
 
@@ -795,6 +995,20 @@ __global__ __launch_bounds__(256) void offq_soft_update_kernel(float* __restrict
 }
 
 // ------------------------------------------------------------------ host side
+// lane-per-feature kernels: >= 8 rows per wave (amortises the per-wave weight loads), <= 2048 waves
+static inline unsigned wave_blocks(int64_t rows) {
+  int64_t waves = (rows + 7) / 8;
+  if (waves > 2048) waves = 2048;
+  if (waves < 1) waves = 1;
+  return (unsigned)((waves + 3) / 4);
+}
+
+static inline int mix_rows_per_block(int K, bool qm) {
+  if (!qm) return 256;
+  int kp = 1;
+  while (kp < K) kp <<= 1;
+  return 256 / kp;
+}
 static int64_t mixer_offsets(const mm_offq_dims* d, int64_t o[15]) {
   const int64_t S = d->state_dim, K = d->mixer_hidden, Hh = d->hyper_hidden, NK = (int64_t)d->n_agents * K;
   const int64_t sz[14] = {Hh * S, Hh, NK * Hh, NK, Hh * S, Hh, K * Hh, K, K * S, K, Hh * S, Hh, Hh, 1};
@@ -832,7 +1046,9 @@ struct OffqShape {
       c += al64(n);
       return o;
     };
-    w.sf = take(w.rs1 * w.NS);
+    w.a1 = take(w.R1 * H);
+    w.a2 = take(w.R1 * H);
+    w.st = take(w.R1 * ST_N);
     w.gi = take(2 * w.R1 * 3 * H);
     w.hs = take(2 * w.R1 * H);
     w.gates = take(w.R1 * 4 * H);
@@ -867,6 +1083,7 @@ struct OffqShape {
       w.gpart = take(gl.part > 0 ? gl.part : 1);
     }
     w.red = take(1024);
+    w.aerr = take(w.TB);
     w.ones = take(1);
     w.total = c;
     return w;
@@ -917,7 +1134,6 @@ struct OffqShape {
     const int K = qm ? d->mixer_hidden : 0, Hh = qm ? d->hyper_hidden : 0, S = d->state_dim;
     int64_t mo[15];
     mixer_offsets(d, mo);
-    const size_t lds_pre = (size_t)(G::Whh + 3 * H) * 4, lds_bwd = (size_t)G::Whh * 4;
     // ---- agent forward (behavior + target) over all T+1 steps
     OqPreArgs pa = {};
     pa.P[0] = P;
@@ -925,12 +1141,14 @@ struct OffqShape {
     pa.obs = bt->obs;
     pa.gi[0] = ws + w.gi;
     pa.gi[1] = ws + w.gi + w.R1 * 3 * H;
-    pa.sf = ws + w.sf;
+    pa.a1 = ws + w.a1;
+    pa.a2 = ws + w.a2;
+    pa.st = ws + w.st;
     pa.R1 = w.R1;
     pa.NB = w.NB;
     pa.T1 = T + 1;
     pa.B = B;
-    hipLaunchKernelGGL((offq_pre_kernel<D, H, A>), dim3((unsigned)((w.R1 + 255) / 256), 2), dim3(256), lds_pre, s, pa);
+    hipLaunchKernelGGL((offq_pre_kernel<D, H, A>), dim3(wave_blocks(w.R1), 2), dim3(256), 0, s, pa);
     MM_HIP_CHECK(hipGetLastError());
     OqRecArgs ra = {};
     ra.P[0] = P;
@@ -951,7 +1169,7 @@ struct OffqShape {
     po.P[1] = PT;
     po.hs[0] = ra.hs[0];
     po.hs[1] = ra.hs[1];
-    po.sf = ws + w.sf;
+    po.st = ws + w.st;
     po.acts = bt->acts;
     po.act = reinterpret_cast<int32_t*>(ws + w.act);
     po.qa = ws + w.qa;
@@ -1004,7 +1222,8 @@ struct OffqShape {
     ma.ZW = w.ZW;
     ma.nets = 2;
     ma.vdn = !qm;
-    hipLaunchKernelGGL(offq_mix_fwd_kernel, dim3((unsigned)((w.TB + 255) / 256), 2), dim3(256), 0, s, ma);
+    hipLaunchKernelGGL(offq_mix_fwd_kernel, dim3((unsigned)((w.TB + mix_rows_per_block(K, qm) - 1) / mix_rows_per_block(K, qm)), 2),
+                       dim3(256), 0, s, ma);
     MM_HIP_CHECK(hipGetLastError());
     // ---- loss, priorities, dQ_tot
     OqLossArgs la = {};
@@ -1024,7 +1243,8 @@ struct OffqShape {
     la.delta = bt->huber_delta;
     la.nu = bt->per_nu;
     la.eps = bt->per_eps;
-    hipLaunchKernelGGL(offq_loss_kernel, dim3(1), dim3(256), 0, s, la);
+    la.aerr = ws + w.aerr;
+    hipLaunchKernelGGL(offq_loss_kernel, dim3(1), dim3(1024), 0, s, la);
     MM_HIP_CHECK(hipGetLastError());
     // ---- mixer backward
     OqMixBwdArgs mb = {};
@@ -1044,7 +1264,8 @@ struct OffqShape {
     mb.Hh = Hh;
     mb.ZW = w.ZW;
     mb.vdn = !qm;
-    hipLaunchKernelGGL(offq_mix_bwd_kernel, dim3((unsigned)((w.TB + 255) / 256)), dim3(256), 0, s, mb);
+    hipLaunchKernelGGL(offq_mix_bwd_kernel, dim3((unsigned)((w.TB + mix_rows_per_block(K, qm) - 1) / mix_rows_per_block(K, qm))),
+                       dim3(256), 0, s, mb);
     MM_HIP_CHECK(hipGetLastError());
     if (qm) {
       const float* Pm = P + G::total;
@@ -1066,7 +1287,7 @@ struct OffqShape {
     OqHeadBwdArgs hb = {};
     hb.P = P;
     hb.hs = ws + w.hs;
-    hb.sf = ws + w.sf;
+    hb.st = ws + w.st;
     hb.act = reinterpret_cast<const int32_t*>(ws + w.act);
     hb.dqa = ws + w.dqa;
     hb.gsoa = ws + w.gsoa;
@@ -1091,7 +1312,9 @@ struct OffqShape {
     OqPreBwdArgs pb = {};
     pb.P = P;
     pb.obs = bt->obs;
-    pb.sf = ws + w.sf;
+    pb.a1 = ws + w.a1;
+    pb.a2 = ws + w.a2;
+    pb.st = ws + w.st;
     pb.hs = ws + w.hs;
     pb.dg = ws + w.dg;
     pb.gsoa = ws + w.gsoa;
@@ -1099,7 +1322,7 @@ struct OffqShape {
     pb.NB = w.NB;
     pb.T1 = T + 1;
     pb.B = B;
-    hipLaunchKernelGGL((offq_pre_bwd_kernel<D, H, A>), dim3((unsigned)((w.Rb + 255) / 256)), dim3(256), lds_bwd, s, pb);
+    hipLaunchKernelGGL((offq_pre_bwd_kernel<D, H, A>), dim3(wave_blocks(w.Rb)), dim3(256), 0, s, pb);
     MM_HIP_CHECK(hipGetLastError());
     return TW::template wgrad<A>(ws + w.gsoa, w.rsb, grad, ws + w.wpart, s);
   }
@@ -1109,7 +1332,6 @@ struct OffqShape {
   static int q_values(const float* P, const float* obs, const float* h0, float* q, float* hout, int L, int64_t R,
                       float* ws, hipStream_t s) {
     const int64_t R1 = (int64_t)L * R;
-    const size_t lds_pre = (size_t)(G::Whh + 3 * H) * 4;
     OqPreArgs pa = {};
     pa.P[0] = P;
     pa.obs = obs;
@@ -1119,7 +1341,7 @@ struct OffqShape {
     pa.T1 = L;
     pa.B = 1;
     pa.stacked = 1;
-    hipLaunchKernelGGL((offq_pre_kernel<D, H, A>), dim3((unsigned)((R1 + 255) / 256), 1), dim3(256), lds_pre, s, pa);
+    hipLaunchKernelGGL((offq_pre_kernel<D, H, A>), dim3(wave_blocks(R1), 1), dim3(256), 0, s, pa);
     MM_HIP_CHECK(hipGetLastError());
     OqRecArgs ra = {};
     ra.P[0] = P;
@@ -1145,16 +1367,7 @@ struct OffqShape {
     return MM_OK;
   }
 
-  static int set_lds() {
-    static bool done = false;
-    if (done) return MM_OK;
-    MM_HIP_CHECK(hipFuncSetAttribute((const void*)offq_pre_kernel<D, H, A>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (G::Whh + 3 * H) * 4));
-    MM_HIP_CHECK(hipFuncSetAttribute((const void*)offq_pre_bwd_kernel<D, H, A>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, G::Whh * 4));
-    done = true;
-    return MM_OK;
-  }
+  static int set_lds() { return MM_OK; }
 };
 
 #define MM_OFFQ_DISPATCH(d, CALL)                                                                  \
