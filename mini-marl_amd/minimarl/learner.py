@@ -580,6 +580,24 @@ class QLearner:
         g2.replay()
         self.updates += 1
 
+    # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)
+    def checkpoint_tensors(self):
+        ts = {"P": self.P, "m": self.m, "v": self.v, "step": self.step_dev, "target": self.tgt.flat}
+        if self.tmix is not None:
+            ts["target_mixer"] = self.tmix.flat
+        return ts, {"updates": int(self.updates), "mode": self.mode}
+
+    def restore_tensors(self, ts, scalars):
+        from .checkpoint import copy_into
+        for k, dst in (("P", self.P), ("m", self.m), ("v", self.v), ("step", self.step_dev),
+                       ("target", self.tgt.flat)):
+            copy_into(dst, ts[k], k)
+        if self.tmix is not None:
+            copy_into(self.tmix.flat, ts["target_mixer"], "target_mixer")
+        self.beh.mark_dirty()
+        self.tgt.mark_dirty()
+        self.updates = int(scalars.get("updates", 0))
+
     def sync_target(self, mixer=False):
         """target <- behavior (qmix/main.py:255-256 syncs the agent net only; mixer=True also the mixer)."""
         self.tgt.copy_from(self.beh)

@@ -243,6 +243,23 @@ class MappoTrainer:
         self.adv_part = torch.zeros(7 * 256 + 5, dtype=torch.float64, device=dev)
         self.loss_acc = torch.zeros(4, device=dev)
 
+    # -- checkpoint (minimarl.checkpoint) ------------------------------------------------------
+    def checkpoint_tensors(self):
+        ts = {"actor": self.p.actor.flat, "critic": self.p.critic.flat, "vn": self.vn}
+        for n in (0, 1):
+            ts[f"m{n}"], ts[f"v{n}"], ts[f"step{n}"] = self.m[n], self.v[n], self.step[n]
+        return ts, {}
+
+    def restore_tensors(self, ts, scalars):
+        from .checkpoint import copy_into
+        copy_into(self.p.actor.flat, ts["actor"], "actor")
+        copy_into(self.p.critic.flat, ts["critic"], "critic")
+        copy_into(self.vn, ts["vn"], "vn")
+        for n in (0, 1):
+            copy_into(self.m[n], ts[f"m{n}"], f"m{n}")
+            copy_into(self.v[n], ts[f"v{n}"], f"v{n}")
+            copy_into(self.step[n], ts[f"step{n}"], f"step{n}")
+
     # -- ValueNorm (utils/valuenorm.py) ------------------------------------------------------
     def value_normalizer_state(self):
         v = self.vn.detach().cpu().numpy()

@@ -39,10 +39,6 @@ MIXER_KEYS = ["hyper_w1.0.weight", "hyper_w1.0.bias", "hyper_w1.2.weight", "hype
               "hyper_b2.0.weight", "hyper_b2.0.bias", "hyper_b2.2.weight", "hyper_b2.2.bias"]
 
 
-def _np(x):
-    return x if isinstance(x, np.ndarray) or torch.is_tensor(x) else np.asarray(x)
-
-
 class OffQMix:
     """QMix / VDN trainer + shared recurrent Q policy (one policy, ``policy_0``)."""
 
@@ -208,6 +204,16 @@ class OffQMix:
         """qmix.py:221-226 / utils/util.py:123-134 (tau)."""
         check(lib().mm_offq_soft_update(ptr(self.PT), ptr(self.P), self.total, float(self.tau),
                                         stream_handle(self.device)), "offq_soft_update")
+
+    # -- checkpoint (minimarl.checkpoint) ------------------------------------------------------
+    def checkpoint_tensors(self):
+        return ({"P": self.P, "PT": self.PT, "m": self.m, "v": self.v, "step": self.step},
+                {"mixer": self.mixer_kind})
+
+    def restore_tensors(self, ts, scalars):
+        from .checkpoint import copy_into
+        for k in ("P", "PT", "m", "v", "step"):
+            copy_into(getattr(self, k), ts[k], k)
 
     # -- acting ------------------------------------------------------------------------------
     def init_hidden(self, num_agents, batch_size):

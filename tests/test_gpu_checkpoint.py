@@ -1,0 +1,109 @@
+"""GPU: checkpoint / resume (minimarl.checkpoint) — a learner restored from a checkpoint continues
+bit-identically to the one that kept running (QMIX QLearner, offpolicy OffQMix, MAPPO trainer)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _qlearner(seed_off=0):
+    from minimarl.learner import Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    N, D, A, B, C = 4, 47, 5, 16, 5
+    beh = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=1 + seed_off)
+    tgt = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=2 + seed_off)
+    mix = Mixer(N, N * D, 64, 32, DEV, seed=3 + seed_off)
+    tmix = Mixer(N, N * D, 64, 32, DEV, seed=4 + seed_off)
+    return QLearner(beh, tgt, mix, tmix, batch=B, chunk=C, mode="qmix", device=DEV), (N, D, A, B, C)
+
+
+def _q_batch(dims, seed):
+    N, D, A, B, C = dims
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(B, C, N, D, generator=g), torch.randint(0, A, (B, C, N), generator=g).float(),
+            torch.randn(B, C, N, generator=g) * 0.5, torch.rand(B, C, N, D, generator=g),
+            (torch.rand(B, C, 1, generator=g) < 0.2).float(), torch.rand(B, 1, generator=g) * 0.5 + 0.5)
+
+
+def test_qlearner_resume_is_bit_identical(tmp_path):
+    from minimarl.checkpoint import load_checkpoint, save_checkpoint
+    a, dims = _qlearner()
+    for it in range(2):
+        a.load_batch(*_q_batch(dims, it))
+        a.train_step(a._obs_buf, a._obs_buf)
+    path = str(tmp_path / "q.safetensors")
+    save_checkpoint(path, learner=a)
+    b, _ = _qlearner(seed_off=10)                 # different init: everything must come from the file
+    meta = load_checkpoint(path, learner=b)
+    assert meta["learner"]["scalars"]["mode"] == "qmix"
+    for L in (a, b):
+        L.load_batch(*_q_batch(dims, 7))
+        L.train_step(L._obs_buf, L._obs_buf)
+    torch.cuda.synchronize()
+    assert torch.equal(a.P, b.P) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+    assert torch.equal(a.loss, b.loss)
+
+
+def test_offq_resume_is_bit_identical(tmp_path):
+    from make_golden_offq import make_batch
+    from minimarl.checkpoint import load_checkpoint, save_checkpoint
+    from minimarl.offq import OffQMix
+    N, T, B, D, A = 2, 9, 6, 47, 5
+    a = OffQMix(N, D, A, T, B, seed=1)
+    rng = np.random.default_rng(3)
+    pid = "policy_0"
+
+    def batch():
+        obs, share, acts, rew, dones, dn = make_batch(rng, N, T, B, D, A)
+        w = (0.5 + rng.random(B)).astype(np.float32)
+        return ({pid: obs}, {pid: share}, {pid: acts}, {pid: rew}, {pid: dones}, {pid: dn}, {pid: None}, w, None)
+
+    for _ in range(2):
+        a.train_policy_on_batch(batch())
+        a.soft_target_updates()
+    path = str(tmp_path / "o.safetensors")
+    save_checkpoint(path, offq=a)
+    b = OffQMix(N, D, A, T, B, seed=99)
+    load_checkpoint(path, offq=b)
+    bt = batch()
+    for tr in (a, b):
+        tr.train_policy_on_batch(bt)
+        tr.soft_target_updates()
+    torch.cuda.synchronize()
+    for k in ("P", "PT", "m", "v", "step"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+
+
+def test_mappo_resume_is_bit_identical(tmp_path):
+    from minimarl.checkpoint import load_checkpoint, save_checkpoint
+    from minimarl.env import VecEnv
+    from minimarl.mappo import MappoPolicy, MappoRunner
+    runs = []
+    for seed in (5, 6):
+        env = VecEnv(64, 2, max_steps=20, device=DEV)
+        pol = MappoPolicy(env.obs_dim, 5, 32, DEV, seed=seed)
+        runs.append(MappoRunner(env, pol, T=20, L=5, ppo_epoch=2, seed=0))
+    a, b = runs
+    a.warmup()
+    a.run_episode()
+    path = str(tmp_path / "m.safetensors")
+    save_checkpoint(path, mappo=a.trainer)
+    load_checkpoint(path, mappo=b.trainer)
+    # same data for both: train b's trainer on a copy of a's next buffer
+    a.rollout()
+    a.compute()
+    for k in ("obs", "rnn_states", "rnn_states_critic", "value_preds", "returns", "actions", "action_log_probs",
+              "rewards", "masks", "active_masks"):
+        getattr(b.buf, k).copy_(getattr(a.buf, k))
+    a.trainer.train(a.buf)
+    b.trainer.train(b.buf)
+    torch.cuda.synchronize()
+    assert torch.equal(a.p.actor.flat, b.p.actor.flat)
+    assert torch.equal(a.p.critic.flat, b.p.critic.flat)
+    assert torch.equal(a.trainer.vn, b.trainer.vn)
