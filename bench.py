@@ -26,6 +26,7 @@ for _p in (ROOT, os.path.join(ROOT, "mini-marl_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (vector = f32 MFMA), MI355X_MICROARCH.md
@@ -107,6 +108,8 @@ def main():
     ap.add_argument("--learner-steps", type=int, default=100)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--mappo-episodes", type=int, default=2, help="timed MAPPO episodes (0 = skip)")
+    ap.add_argument("--offq-updates", type=int, default=30,
+                    help="timed offpolicy episode-QMix updates on one GPU (0 = skip; single-GPU runs only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,6 +240,42 @@ def main():
         del mr, menv, mpol
         torch.cuda.empty_cache()
 
+    # offpolicy episode-level QMix (offpolicy/algorithms/qmix/qmix.py:80-210):
+    # train_policy_on_batch + soft target update on a device batch of B = 32 episodes x T = 100
+    # steps, 8 agents, QMixer with 2-layer hypernets, double Q, PER priorities
+    offq = None
+    if args.offq_updates > 0 and world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        from make_golden_offq import make_batch
+        from minimarl.offq import OffQMix
+        oT, oB = 100, 32
+        otr = OffQMix(N, D, 5, oT, oB, seed=5, device=dev)
+        rng = np.random.default_rng(0)
+        obs, share, acts, rew, dones, dn = make_batch(rng, N, oT, oB, D, 5)
+        to = lambda x: torch.as_tensor(x).to(dev).contiguous()  # noqa: E731
+        pid = "policy_0"
+        ob = ({pid: to(obs)}, {pid: to(share)}, {pid: to(acts)}, {pid: to(rew)}, {pid: to(dones)}, {pid: to(dn)},
+              {pid: None}, to((0.5 + rng.random(oB)).astype(np.float32)), None)
+        for _ in range(3):
+            otr.train_policy_on_batch(ob)
+            otr.soft_target_updates()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        for _ in range(args.offq_updates):
+            otr.train_policy_on_batch(ob)
+            otr.soft_target_updates()
+        torch.cuda.synchronize()
+        el_o = time.perf_counter() - t3
+        offq = {"algo": "offpolicy QMix.train_policy_on_batch + soft_update (episode BPTT, QMixer hypernets, "
+                        "double Q, R2D2 priorities)", "agents": N, "episode_length": oT, "batch_episodes": oB,
+                "ms_per_update": round(el_o / args.offq_updates * 1e3, 4),
+                "updates_per_s": round(args.offq_updates / el_o, 1),
+                "reference_cpu_ms_per_update": 115.8,
+                "reference_cpu_note": "reference train_policy_on_batch, same shapes, 8 threads of the build "
+                                      "container (tools/ref_time_offq.py)"}
+        del otr
+        torch.cuda.empty_cache()
+
     # roofline of the dominant kernel: the fused agent Q forward (one launch = target net on s'_t +
     # behavior net on s_{t+1}: 2 nets x E x N agent-steps). At E >= 2048 it runs the fp16x3-split
     # kernel: every fp32 product as 3 f16 MFMAs, so its MFMA ceiling for the network's fp32 FLOPs
@@ -284,6 +323,7 @@ def main():
                         "updates": args.learner_steps, "grad_allreduce": "rccl" if dist else None,
                         "reference_cpu_updates_per_s": 12.0},
             "mappo": mappo,
+            "offpolicy_qmix": offq,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -19,6 +19,8 @@
  *   mm_mappo_fwd         R_MAPPOPolicy.get_actions/get_values/evaluate_actions  mappo/algorithms/rmappo_policy.py:57-136
  *   mm_mappo_bwd, wgrad  R_MAPPO.ppo_update/cal_value_loss/train     mappo/algorithms/ramppo_network.py:56-287
  *   mm_mappo_gae, insert SharedReplayBuffer.compute_returns/insert   mappo/runner/shared/shared_buffer.py:82-157
+ *   mm_offq_*            offpolicy QMix.train_policy_on_batch etc.   offpolicy/algorithms/qmix/qmix.py:80-226
+ *   mm_eval_accum        greedy test loops                           vdn/_test.py:22-50; magym_runner.py:198-241
  */
 #ifndef MINIMARL_H
 #define MINIMARL_H
