@@ -276,6 +276,43 @@ def main():
         del otr
         torch.cuda.empty_cache()
 
+    # cfg5 (SMAC 27m_vs_30m-like shapes, no env of that shape exists here): the dual agent
+    # forward (target + behavior) at E = 8192, N = 27, D = 300, A = 36, GRU-32 on synthetic obs
+    cfg5 = None
+    if rank == 0 and not os.environ.get("MM_BENCH_NO_CFG5"):
+        import ctypes
+        from minimarl._lib import MM_Q_ACT, MM_Q_MAX, lib
+        from minimarl.qnet import AgentQNet, ptr, stream_handle
+        E5, N5, D5, A5, H5 = 8192, 27, 300, 36, 32
+        n5 = [AgentQNet(N5, D5, A5, 64, 32, H5, dev, seed=s) for s in (1, 2)]
+        for n in n5:
+            n.pack()
+        g5 = torch.Generator(device=dev).manual_seed(5)
+        o5 = [(torch.rand(E5, N5, D5, device=dev, generator=g5) < 0.2).float() for _ in range(2)]
+        h5 = [torch.zeros(N5, H5, E5, device=dev).permute(2, 0, 1) for _ in range(2)]
+        hq = [torch.empty(N5, H5, E5, device=dev).permute(2, 0, 1) for _ in range(2)]
+        qs5 = [torch.empty(E5, N5, device=dev) for _ in range(2)]
+        act5 = torch.empty(E5, N5, dtype=torch.int32, device=dev)
+        io5 = []
+        for k, mode in enumerate((MM_Q_MAX, MM_Q_ACT)):
+            io = n5[k].make_io(o5[k], h5[k], hq[k], None, mode)
+            io.qsel_out = qs5[k].data_ptr()
+            if mode == MM_Q_ACT:
+                io.act_out, io.epsilon = act5.data_ptr(), 0.05
+            io5.append(io)
+        L5, st5 = lib(), stream_handle(dev)
+
+        def dual5():
+            L5.mm_agent_q_fwd2(ctypes.byref(n5[0].dims), ptr(n5[0].packed), ctypes.byref(io5[0]), E5,
+                               ptr(n5[1].packed), ctypes.byref(io5[1]), E5, st5)
+        t5 = time_kernel(dual5)
+        f5 = 2 * qnet_flops_per_agent_step(D5, 64, 32, H5, A5) * E5 * N5
+        cfg5 = {"workload": "cfg5 dual agent forward (target + behavior), synthetic obs", "envs": E5, "agents": N5,
+                "obs_dim": D5, "n_actions": A5, "gru": H5, "dual_us": round(t5 * 1e6, 2),
+                "agent_steps_per_s": round(2 * E5 * N5 / t5, 1), "tflops_fp32_equiv": round(f5 / t5 / 1e12, 2)}
+        del n5, o5, h5, hq
+        torch.cuda.empty_cache()
+
     # roofline of the dominant kernel: the fused agent Q forward (one launch = target net on s'_t +
     # behavior net on s_{t+1}: 2 nets x E x N agent-steps). At E >= 2048 it runs the fp16x3-split
     # kernel: every fp32 product as 3 f16 MFMAs, so its MFMA ceiling for the network's fp32 FLOPs
@@ -324,6 +361,7 @@ def main():
                         "reference_cpu_updates_per_s": 12.0},
             "mappo": mappo,
             "offpolicy_qmix": offq,
+            "cfg5_forward": cfg5,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
