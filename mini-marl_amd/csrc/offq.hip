@@ -90,36 +90,54 @@ __device__ __forceinline__ const float* obs_row(const float* obs, int stacked, i
   return obs + ((i * T1 + t) * B + b) * D;
 }
 
-// One wave per row at a time, lane j = feature j (H == 64; D <= 128 as two lane halves): the
-// lane's rows of W1, W2 and the three W_ih gate rows stay in VGPRs for all rows the wave visits;
-// activations are broadcast lane -> SGPR (v_readlane), LayerNorm statistics are wave reductions.
+// One wave per row at a time, lane j = feature j (H == 64; D <= 128 as two lane halves). The net's
+// W1 / W2 / W_ih rows are staged once per 1024-thread block into LDS with row strides of 4 x odd
+// floats (a wave's ds_read_b128 of 64 different rows is conflict-free), so 16 waves per CU share one
+// copy; activations are broadcast through a wave-private LDS slot, LayerNorm sums are DPP wave sums.
+template <int D> struct PreLds {
+  static constexpr int Dp = (D + 3) & ~3;
+  static constexpr int S1 = ((Dp / 4) & 1) ? Dp : Dp + 4;    // W1 row stride (4 x odd)
+  static constexpr int S2 = 68;                              // W2 / W_ih row stride
+  static constexpr int oW2 = 64 * S1, oWih = oW2 + 64 * S2, oSlot = oWih + 192 * S2, total = oSlot + 16 * 128;
+};
+
 template <int D, int H, int A>
-__global__ __launch_bounds__(256) void offq_pre_kernel(OqPreArgs a) {
+__global__ __launch_bounds__(1024) void offq_pre_kernel(OqPreArgs a) {
   static_assert(H == 64 && D <= 128, "lane-per-feature layout");
   using G = MGeo<D, H, A>;
+  using L = PreLds<D>;
   constexpr int D0 = D < 64 ? D : 64, D1 = D - D0;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   const int y = blockIdx.y;
   const float* P = a.P[y];
-  const int j = threadIdx.x & 63;
-  const int64_t wid = blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
-  float w1[D], w2[H], wr[H], wz[H], wn[H];
-#pragma unroll
-  for (int k = 0; k < D; ++k) w1[k] = P[G::W1 + j * G::Dp + k];
-#pragma unroll
-  for (int k = 0; k < H; ++k) {
-    w2[k] = P[G::W2 + j * H + k];
-    wr[k] = P[G::Wih + j * H + k];
-    wz[k] = P[G::Wih + (H + j) * H + k];
-    wn[k] = P[G::Wih + (2 * H + j) * H + k];
+  // stage W1 (Dp-wide rows), W2, W_ih as float4 rows
+  for (int i = threadIdx.x; i < 64 * (G::Dp / 4); i += blockDim.x) {
+    const int rj = i / (G::Dp / 4), c = i % (G::Dp / 4);
+    *reinterpret_cast<float4*>(sm + rj * L::S1 + 4 * c) = *reinterpret_cast<const float4*>(P + G::W1 + rj * G::Dp + 4 * c);
   }
+  for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) {
+    const int rj = i >> 4, c = i & 15;
+    *reinterpret_cast<float4*>(sm + L::oW2 + rj * L::S2 + 4 * c) = *reinterpret_cast<const float4*>(P + G::W2 + rj * H + 4 * c);
+  }
+  for (int i = threadIdx.x; i < 192 * 16; i += blockDim.x) {
+    const int rj = i >> 4, c = i & 15;
+    *reinterpret_cast<float4*>(sm + L::oWih + rj * L::S2 + 4 * c) = *reinterpret_cast<const float4*>(P + G::Wih + rj * H + 4 * c);
+  }
+  __syncthreads();
+  const int j = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t wid = blockIdx.x * 16 + wv, nw = (int64_t)gridDim.x * 16;
+  const float* w1 = sm + j * L::S1;
+  const float* w2 = sm + L::oW2 + j * L::S2;
+  const float* wr = sm + L::oWih + j * L::S2;
+  const float* wz = sm + L::oWih + (H + j) * L::S2;
+  const float* wn = sm + L::oWih + (2 * H + j) * L::S2;
+  float* slot = sm + L::oSlot + wv * 128;
   const float g0a = j < D0 ? P[G::ln0_w + j] : 0.f, b0a = j < D0 ? P[G::ln0_b + j] : 0.f;
   const float g0b = j < D1 ? P[G::ln0_w + 64 + j] : 0.f, b0b = j < D1 ? P[G::ln0_b + 64 + j] : 0.f;
   const float b1 = P[G::b1 + j], g1 = P[G::ln1_w + j], c1 = P[G::ln1_b + j];
   const float b2 = P[G::b2 + j], g2 = P[G::ln2_w + j], c2 = P[G::ln2_b + j];
   const float bir = P[G::bih + j], biz = P[G::bih + H + j], bin = P[G::bih + 2 * H + j];
   const bool save = y == 0 && a.a1;
-  __shared__ __attribute__((aligned(16))) float sm[4][128];
-  float* slot = sm[threadIdx.x >> 6];
   // the next row's observation is loaded one row ahead
   float xa_n = 0.f, xb_n = 0.f;
   if (wid < a.R1) {
@@ -139,22 +157,19 @@ __global__ __launch_bounds__(256) void offq_pre_kernel(OqPreArgs a) {
     const float da = j < D0 ? xa - mu0 : 0.f, db = j < D1 ? xb - mu0 : 0.f;
     const float rs0 = 1.0f / sqrtf(wave_sum(da * da + db * db) / (float)D + kLnEps);
     const float fa = da * rs0 * g0a + b0a, fb = db * rs0 * g0b + b0b;
-    // L1 + ReLU + LN1
+    // L1 + ReLU + LN1 (W1 pad columns are zero)
     {
       const float fv[2] = {fa, fb};
       bcast_put<2>(slot, j, fv);
     }
     float s0 = b1, s1 = 0.f;
 #pragma unroll
-    for (int c = 0; c < (D + 3) / 4; ++c) {
-      const float4 t4 = bcast_get4(slot, c);
-      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (4 * c + u < D) {
-          if (u & 1) s1 = fmaf(w1[4 * c + u], tv[u], s1);
-          else s0 = fmaf(w1[4 * c + u], tv[u], s0);
-        }
+    for (int c = 0; c < G::Dp / 4; ++c) {
+      const float4 t4 = bcast_get4(slot, c), w4 = *reinterpret_cast<const float4*>(w1 + 4 * c);
+      s0 = fmaf(w4.x, t4.x, s0);
+      s1 = fmaf(w4.y, t4.y, s1);
+      s0 = fmaf(w4.z, t4.z, s0);
+      s1 = fmaf(w4.w, t4.w, s1);
     }
     const float a1 = fmaxf(s0 + s1, 0.0f);
     const float mu1 = wave_sum(a1) * (1.0f / H);
@@ -170,11 +185,11 @@ __global__ __launch_bounds__(256) void offq_pre_kernel(OqPreArgs a) {
     s1 = 0.f;
 #pragma unroll
     for (int c = 0; c < H / 4; ++c) {
-      const float4 t4 = bcast_get4(slot, c);
-      s0 = fmaf(w2[4 * c], t4.x, s0);
-      s1 = fmaf(w2[4 * c + 1], t4.y, s1);
-      s0 = fmaf(w2[4 * c + 2], t4.z, s0);
-      s1 = fmaf(w2[4 * c + 3], t4.w, s1);
+      const float4 t4 = bcast_get4(slot, c), w4 = *reinterpret_cast<const float4*>(w2 + 4 * c);
+      s0 = fmaf(w4.x, t4.x, s0);
+      s1 = fmaf(w4.y, t4.y, s1);
+      s0 = fmaf(w4.z, t4.z, s0);
+      s1 = fmaf(w4.w, t4.w, s1);
     }
     const float a2 = fmaxf(s0 + s1, 0.0f);
     const float mu2 = wave_sum(a2) * (1.0f / H);
@@ -190,13 +205,21 @@ __global__ __launch_bounds__(256) void offq_pre_kernel(OqPreArgs a) {
 #pragma unroll
     for (int c = 0; c < H / 4; ++c) {
       const float4 t4 = bcast_get4(slot, c);
-      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        gr = fmaf(wr[4 * c + u], tv[u], gr);
-        gz = fmaf(wz[4 * c + u], tv[u], gz);
-        gn = fmaf(wn[4 * c + u], tv[u], gn);
-      }
+      const float4 r4 = *reinterpret_cast<const float4*>(wr + 4 * c);
+      const float4 z4 = *reinterpret_cast<const float4*>(wz + 4 * c);
+      const float4 n4 = *reinterpret_cast<const float4*>(wn + 4 * c);
+      gr = fmaf(r4.x, t4.x, gr);
+      gz = fmaf(z4.x, t4.x, gz);
+      gn = fmaf(n4.x, t4.x, gn);
+      gr = fmaf(r4.y, t4.y, gr);
+      gz = fmaf(z4.y, t4.y, gz);
+      gn = fmaf(n4.y, t4.y, gn);
+      gr = fmaf(r4.z, t4.z, gr);
+      gz = fmaf(z4.z, t4.z, gz);
+      gn = fmaf(n4.z, t4.z, gn);
+      gr = fmaf(r4.w, t4.w, gr);
+      gz = fmaf(z4.w, t4.w, gz);
+      gn = fmaf(n4.w, t4.w, gn);
     }
     float* go = a.gi[y] + r * (3 * H);
     go[j] = gr;
@@ -995,12 +1018,23 @@ __global__ __launch_bounds__(256) void offq_soft_update_kernel(float* __restrict
 }
 
 // ------------------------------------------------------------------ host side
-// lane-per-feature kernels: >= 8 rows per wave (amortises the per-wave weight loads), <= 2048 waves
+// register-weight lane-per-feature backward: >= 8 rows per wave (amortises the per-wave weight
+// loads), <= 2048 waves
 static inline unsigned wave_blocks(int64_t rows) {
   int64_t waves = (rows + 7) / 8;
   if (waves > 2048) waves = 2048;
   if (waves < 1) waves = 1;
   return (unsigned)((waves + 3) / 4);
+}
+
+// LDS-weight lane-per-feature kernels (16 waves per block, one block per CU): >= 4 rows per wave,
+// at most one block per CU over all nets of the launch
+static inline unsigned lds_blocks(int64_t rows, int nets) {
+  int64_t b = (rows + 63) / 64;
+  const int64_t cap = 256 / nets;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (unsigned)b;
 }
 
 static inline int mix_rows_per_block(int K, bool qm) {
@@ -1148,7 +1182,8 @@ struct OffqShape {
     pa.NB = w.NB;
     pa.T1 = T + 1;
     pa.B = B;
-    hipLaunchKernelGGL((offq_pre_kernel<D, H, A>), dim3(wave_blocks(w.R1), 2), dim3(256), 0, s, pa);
+    hipLaunchKernelGGL((offq_pre_kernel<D, H, A>), dim3(lds_blocks(w.R1, 2), 2), dim3(1024),
+                       (size_t)PreLds<D>::total * 4, s, pa);
     MM_HIP_CHECK(hipGetLastError());
     OqRecArgs ra = {};
     ra.P[0] = P;
@@ -1341,7 +1376,8 @@ struct OffqShape {
     pa.T1 = L;
     pa.B = 1;
     pa.stacked = 1;
-    hipLaunchKernelGGL((offq_pre_kernel<D, H, A>), dim3(wave_blocks(R1), 1), dim3(256), 0, s, pa);
+    hipLaunchKernelGGL((offq_pre_kernel<D, H, A>), dim3(lds_blocks(R1, 1), 1), dim3(1024),
+                       (size_t)PreLds<D>::total * 4, s, pa);
     MM_HIP_CHECK(hipGetLastError());
     OqRecArgs ra = {};
     ra.P[0] = P;
@@ -1367,7 +1403,14 @@ struct OffqShape {
     return MM_OK;
   }
 
-  static int set_lds() { return MM_OK; }
+  static int set_lds() {
+    static bool done = false;
+    if (done) return MM_OK;
+    MM_HIP_CHECK(hipFuncSetAttribute((const void*)offq_pre_kernel<D, H, A>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, PreLds<D>::total * 4));
+    done = true;
+    return MM_OK;
+  }
 };
 
 #define MM_OFFQ_DISPATCH(d, CALL)                                                                  \
