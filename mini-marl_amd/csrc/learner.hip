@@ -332,16 +332,24 @@ __global__ void lrn_loss_kernel(int B, int C, int N, float gamma, const float* r
   if (t == C - 1) td_last[b] = fabsf(diff);
 }
 
-// loss = sum_t (1/B) sum_b parts  (one thread, fixed order)
-__global__ void lrn_loss_reduce_kernel(int B, int C, const float* parts, float* loss) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// loss = sum_t (1/B) sum_b parts: one 256-thread block, per step a strided per-thread sum and a
+// fixed-shape tree over the threads (deterministic), steps accumulated in order
+__global__ __launch_bounds__(256) void lrn_loss_reduce_kernel(int B, int C, const float* parts, float* loss) {
+  __shared__ float sh[256];
   float tot = 0.f;
   for (int t = 0; t < C; ++t) {
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += parts[t * B + b];
-    tot += s / (float)B;
+    for (int b = threadIdx.x; b < B; b += 256) s += parts[(int64_t)t * B + b];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+      __syncthreads();
+    }
+    tot += sh[0] / (float)B;
+    __syncthreads();
   }
-  *loss = tot;
+  if (threadIdx.x == 0) *loss = tot;
 }
 
 // ------------------------------------------------------------------ mixer backward (one step)
@@ -893,7 +901,7 @@ int mm_lrn_loss_ex(int32_t B, int32_t C, int32_t N, float gamma, const float* re
   hipLaunchKernelGGL(mm::lrn_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, B, C, N, gamma, rew,
                      done, isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts, td_last);
   MM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(mm::lrn_loss_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, B, C, loss_parts, loss);
+  hipLaunchKernelGGL(mm::lrn_loss_reduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)s, B, C, loss_parts, loss);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -905,7 +913,7 @@ int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, 
   hipLaunchKernelGGL(mm::lrn_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, B, C, N, gamma, rew,
                      done, isw, qtot, qtot_t, mix_sum ? MM_LOSS_MIX_SUM : 0, qa, maxq, dq, dqa, loss_parts, td_last);
   MM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(mm::lrn_loss_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, B, C, loss_parts, loss);
+  hipLaunchKernelGGL(mm::lrn_loss_reduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)s, B, C, loss_parts, loss);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

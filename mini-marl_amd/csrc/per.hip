@@ -46,6 +46,7 @@ struct mm_per {
   int64_t* slot_row;  // [cap]
   void* alloc;
   void* mb;           // multi-block insert scratch (MbScratch), power-of-two cap >= MB_MIN_CAP
+  int32_t* last;      // [cap] per_update scratch: last sample index per leaf (-1 between calls)
 };
 
 namespace mm {
@@ -459,6 +460,7 @@ __global__ void per_uniform_kernel(int64_t cap, int B, uint64_t seed, uint64_t c
   if (is_w) is_w[k] = 1.0f;
 }
 
+constexpr int PER_SAMPLE_MAXJ = 8;   // per_sample_kernel: batch <= PT * 8
 __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t cap, int B, const double* fracs,
                                                         uint64_t seed, uint64_t counter, PerDev* st, double decay,
                                                         int64_t* nodes_out, int64_t* slots_out, float* is_w) {
@@ -473,12 +475,17 @@ __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t ca
     st->beta = beta;
     st->n_samples += 1;
   }
-  __shared__ double s_w[PT];
-  __shared__ double s_p[PT];
+  // each thread owns samples k = threadIdx.x + j * PT (B <= PT * PER_SAMPLE_MAXJ), leaf priorities and
+  // IS weights kept in registers
+  double pk[PER_SAMPLE_MAXJ], wk[PER_SAMPLE_MAXJ];
   const int64_t n_nodes = 2 * cap - 1;
   const double total = tree[0];
   const double seg = total / (double)B;
-  for (int k = threadIdx.x; k < B; k += PT) {
+#pragma unroll
+  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
+    const int k = threadIdx.x + j * PT;
+    pk[j] = 0.0;
+    if (k >= B) continue;
     double f = fracs ? fracs[k] : (double)(rng_draw(seed, ctr, (uint64_t)k, 77) >> 11) * (1.0 / 9007199254740992.0);
     const double a = seg * (double)k;
     const double b = seg * (double)(k + 1);
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t ca
     }
     nodes_out[k] = idx;
     if (slots_out) slots_out[k] = idx - (cap - 1);
-    s_p[k] = tree[idx];
+    pk[j] = tree[idx];
   }
   __syncthreads();
   // VDN: whole tree x step_weight after sampling (buffer.py:72-73)
@@ -507,29 +514,48 @@ __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t ca
   }
   const double total2 = tree[0];
   double mx = 0.0;
-  for (int k = threadIdx.x; k < B; k += PT) {
-    const double w = pow((double)cap * (s_p[k] / total2), -beta);
-    s_w[k] = w;
+#pragma unroll
+  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
+    const int k = threadIdx.x + j * PT;
+    wk[j] = 0.0;
+    if (k >= B) continue;
+    wk[j] = pow((double)cap * (pk[j] / total2), -beta);
+    mx = fmax(mx, wk[j]);
   }
+  // block max (exact in any order)
+  __shared__ double s_mx[PT / 64];
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = mx;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < B; ++k) mx = fmax(mx, s_w[k]);
-    s_p[0] = mx;  // broadcast (priorities no longer needed)
+  mx = s_mx[0];
+  for (int w = 1; w < PT / 64; ++w) mx = fmax(mx, s_mx[w]);
+#pragma unroll
+  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
+    const int k = threadIdx.x + j * PT;
+    if (k < B) is_w[k] = (float)(wk[j] / mx);
   }
-  __syncthreads();
-  mx = s_p[0];
-  for (int k = threadIdx.x; k < B; k += PT) is_w[k] = (float)(s_w[k] / mx);
 }
 
+// Duplicate nodes: the LAST sample index wins (sequential tree[idx] = p semantics). One workgroup;
+// the per-leaf winner is found with atomicMax into the leaf scratch `last` (all -1 between calls,
+// restored before the rebuild), O(B) instead of comparing every pair.
 __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t cap, const int64_t* nodes, const float* td,
-                                                        int B, const PerDev* st, float eps) {
+                                                        int B, const PerDev* st, float eps, int32_t* last) {
   const float alpha = (float)st->alpha;
   for (int k = threadIdx.x; k < B; k += PT) {
     const int64_t nd = nodes[k];
-    bool last = true;
-    for (int k2 = k + 1; k2 < B; ++k2) last = last && (nodes[k2] != nd);
+    if (nd >= cap - 1 && nd < 2 * cap - 1) atomicMax(&last[nd - (cap - 1)], k);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < B; k += PT) {
+    const int64_t nd = nodes[k];
     // the reference computes (td + eps) ** alpha on a float32 tensor (vdn/_train.py:230-233)
-    if (last && nd >= cap - 1 && nd < 2 * cap - 1) tree[nd] = (double)powf(td[k] + eps, alpha);
+    if (nd >= cap - 1 && nd < 2 * cap - 1 && last[nd - (cap - 1)] == k) tree[nd] = (double)powf(td[k] + eps, alpha);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < B; k += PT) {
+    const int64_t nd = nodes[k];
+    if (nd >= cap - 1 && nd < 2 * cap - 1) last[nd - (cap - 1)] = -1;
   }
   __syncthreads();
   rebuild_tree(tree, cap);
@@ -917,8 +943,9 @@ int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, d
   const size_t tree_b = ((size_t)(2 * capacity - 1) * 8 + 255) & ~size_t(255);
   const size_t row_b = ((size_t)capacity * 8 + 255) & ~size_t(255);
   const size_t scr_b = (size_t)capacity * 8;
+  const size_t last_b = ((size_t)capacity * 4 + 255) & ~size_t(255);
   void* base = nullptr;
-  if (hipMalloc(&base, tree_b + row_b + scr_b + 256) != hipSuccess) {
+  if (hipMalloc(&base, tree_b + row_b + scr_b + 256 + last_b) != hipSuccess) {
     delete p;
     mm::set_error("per_create: hipMalloc failed");
     return MM_ENOMEM;
@@ -928,9 +955,10 @@ int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, d
   p->st = reinterpret_cast<mm::PerDev*>(static_cast<char*>(base) + tree_b + row_b + scr_b);
   const mm::PerDev st0 = {0, alpha, beta, alpha_inc, beta_inc, 0};
   p->slot_row = reinterpret_cast<int64_t*>(static_cast<char*>(base) + tree_b);
+  p->last = reinterpret_cast<int32_t*>(static_cast<char*>(base) + tree_b + row_b + scr_b + 256);
   std::vector<int64_t> rows(capacity);
   for (int64_t i = 0; i < capacity; ++i) rows[i] = i;  // slot s reserves row s until first filled
-  if (hipMemset(p->tree, 0, tree_b) != hipSuccess ||
+  if (hipMemset(p->tree, 0, tree_b) != hipSuccess || hipMemset(p->last, 0xFF, last_b) != hipSuccess ||
       hipMemcpy(p->slot_row, rows.data(), capacity * 8, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(p->st, &st0, sizeof(st0), hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipFree(base);
@@ -1017,7 +1045,8 @@ int mm_per_sample_uniform(mm_per* per, int32_t batch, uint64_t seed, uint64_t co
 static int per_sample_impl(mm_per* per, int32_t batch, const double* fracs, uint64_t seed, uint64_t counter,
                            int64_t* nodes_out, int64_t* slots_out, float* is_w, mm_stream_t s) {
   MM_REQUIRE(per && nodes_out && is_w, "per_sample: null argument");
-  MM_REQUIRE(batch >= 1 && batch <= mm::PT, "per_sample: batch must be in [1, %d]", mm::PT);
+  MM_REQUIRE(batch >= 1 && batch <= mm::PT * mm::PER_SAMPLE_MAXJ, "per_sample: batch must be in [1, %d]",
+             mm::PT * mm::PER_SAMPLE_MAXJ);
   MM_REQUIRE(per->n_data > 0, "per_sample: empty buffer");
   // anneal before the draws (buffer.py:53-56)
   per->alpha = std::min(1.0, per->alpha + per->alpha_inc);
@@ -1044,7 +1073,7 @@ int mm_per_update(mm_per* per, const int64_t* nodes, const float* td, int32_t ba
   MM_REQUIRE(per && nodes && td, "per_update: null argument");
   MM_REQUIRE(batch >= 1 && batch <= 65536, "per_update: bad batch");
   hipLaunchKernelGGL(mm::per_update_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->cap, nodes, td,
-                     batch, per->st, (float)per->eps);
+                     batch, per->st, (float)per->eps, per->last);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
