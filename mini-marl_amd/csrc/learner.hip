@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256) void outer_reduce_kernel(OuterArgs a) {
 constexpr int OB_MAX = 16;
 struct OuterBatch {
   OuterArgs job[OB_MAX];
-  int tiles_c[OB_MAX], tiles_r[OB_MAX], groups[OB_MAX], slices[OB_MAX];
+  int tiles_c[OB_MAX], tiles_r[OB_MAX], groups[OB_MAX], slices[OB_MAX], rps[OB_MAX];
   int blk0[OB_MAX + 1];
   int64_t part[OB_MAX];  // partial offset: [slice][group][R*Cc + R]
   int njobs;
@@ -661,33 +661,41 @@ __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
   t /= ob.tiles_r[j];
   const int g = t % ob.groups[j];
   const int sl = t / ob.groups[j];
-  const int r0 = tr_ * 32, c0 = tc_ * 32, m0 = sl * 32;
-  for (int k = threadIdx.x; k < 32 * 32; k += 256) {
-    const int mm = k / 32, x = k % 32;
-    const int m = m0 + mm;
-    float u = 0.f, v = 0.f;
-    if (m < a.M) {
-      if (r0 + x < a.R) u = a.U[g * a.u_g + (int64_t)m * a.u_m + r0 + x];
-      if (c0 + x < a.Cc) {
-        if (a.v_off) {
-          const int64_t off = a.v_off[m];
-          const float* base = off >= 0 ? a.V + off : a.v_reset;
-          v = base[g * a.v_g + c0 + x];
-        } else {
-          v = a.V[g * a.v_g + (int64_t)m * a.v_m + c0 + x];
-        }
-      }
-    }
-    su[mm][x] = u;
-    svv[mm][x] = v;
-  }
-  __syncthreads();
+  const int r0 = tr_ * 32, c0 = tc_ * 32;
+  const int m_begin = sl * ob.rps[j], m_end = min(a.M, m_begin + ob.rps[j]);
   const int tr = threadIdx.x / 32, tc = threadIdx.x % 32;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int mm = 0; mm < 32; ++mm) {
-    const float v = svv[mm][tc];
+  float sb = 0.f;
+  const bool do_b = a.db && tc_ == 0 && threadIdx.x < 32;
+  for (int m0 = m_begin; m0 < m_end; m0 += 32) {
+    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
+      const int mm = k / 32, x = k % 32;
+      const int m = m0 + mm;
+      float u = 0.f, v = 0.f;
+      if (m < m_end) {
+        if (r0 + x < a.R) u = a.U[g * a.u_g + (int64_t)m * a.u_m + r0 + x];
+        if (c0 + x < a.Cc) {
+          if (a.v_off) {
+            const int64_t off = a.v_off[m];
+            const float* base = off >= 0 ? a.V + off : a.v_reset;
+            v = base[g * a.v_g + c0 + x];
+          } else {
+            v = a.V[g * a.v_g + (int64_t)m * a.v_m + c0 + x];
+          }
+        }
+      }
+      su[mm][x] = u;
+      svv[mm][x] = v;
+    }
+    __syncthreads();
+    for (int mm = 0; mm < 32; ++mm) {
+      const float v = svv[mm][tc];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] += su[mm][tr + 8 * q] * v;
+      for (int q = 0; q < 4; ++q) acc[q] += su[mm][tr + 8 * q] * v;
+    }
+    if (do_b)
+      for (int mm = 0; mm < 32; ++mm) sb += su[mm][threadIdx.x];
+    __syncthreads();
   }
   const int64_t per = (int64_t)a.R * a.Cc + a.R;
   float* out = ob.partial + ob.part[j] + ((int64_t)sl * ob.groups[j] + g) * per;
@@ -696,11 +704,7 @@ __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
     const int r = r0 + tr + 8 * q, c = c0 + tc;
     if (r < a.R && c < a.Cc) out[(int64_t)r * a.Cc + c] = acc[q];
   }
-  if (a.db && tc_ == 0 && threadIdx.x < 32 && r0 + threadIdx.x < a.R) {
-    float sb = 0.f;
-    for (int mm = 0; mm < 32; ++mm) sb += su[mm][threadIdx.x];
-    out[(int64_t)a.R * a.Cc + r0 + threadIdx.x] = sb;
-  }
+  if (do_b && r0 + threadIdx.x < a.R) out[(int64_t)a.R * a.Cc + r0 + threadIdx.x] = sb;
 }
 
 __global__ __launch_bounds__(256) void outer_sum_kernel(OuterBatch ob) {
@@ -980,7 +984,10 @@ static int64_t outer_batch_layout(const mm_outer_args* x, int n, mm::OuterBatch*
     ob->tiles_c[j] = (q.Cc + 31) / 32;
     ob->tiles_r[j] = (q.R + 31) / 32;
     ob->groups[j] = q.groups;
-    ob->slices[j] = (q.M + 31) / 32;
+    // rows per slice: 32-row chunks, at most ~64 slices per job (bounded partials at large batches)
+    const int chunks = (q.M + 31) / 32;
+    ob->rps[j] = 32 * ((chunks + 63) / 64);
+    ob->slices[j] = (q.M + ob->rps[j] - 1) / ob->rps[j];
     ob->blk0[j] = blk;
     ob->part[j] = part;
     blk += ob->tiles_c[j] * ob->tiles_r[j] * q.groups * ob->slices[j];

@@ -91,11 +91,13 @@ def test_learner_matches_reference_update(golden, mode):
             np.testing.assert_allclose(L.mix.view(key).cpu().numpy()[sel], afterM[key].numpy()[sel], atol=2e-6)
 
 
-def test_learner_gru64_vs_oracle():
-    """GRU-64 agents + Hm=64 mixer (the cfg2 shapes; no reference sizes exist) vs the torch-CPU oracle."""
+@pytest.mark.parametrize("B", [48, 1024])
+def test_learner_gru64_vs_oracle(B):
+    """GRU-64 agents + Hm=64 mixer (the cfg2 shapes; no reference sizes exist) vs the torch-CPU oracle;
+    B = 1024 exercises the multi-chunk slices of the batched weight-gradient reduction."""
     from minimarl.learner import MIX_KEYS, Mixer, QLearner
     from minimarl.qnet import AgentQNet
-    N, D, A, B, C = 4, 47, 5, 48, 6
+    N, D, A, C = 4, 47, 5, 6
     beh = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=1)
     tgt = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=2)
     mix = Mixer(N, N * D, 64, 32, DEV, seed=3)
@@ -337,3 +339,32 @@ def test_chunk_sequence_launches_match_per_step(mode, f1, g, h, hm):
         out.append((L.P.clone(), L.Gr.clone(), L.loss.clone(), L.qa.clone(), L.maxq.clone(), L.dqa.clone()))
     for x, y in zip(*out):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("M", [320, 4096 * 10 + 17])
+def test_outer_reduce_batch_large_rows(M):
+    """The batched weight-gradient reduction (mm_outer_reduce_batch) at the learner's row counts for
+    B = 32 and B = 4096 (multi-chunk slices) against a float64 torch reference."""
+    import ctypes
+    from minimarl._lib import OuterArgs, check, lib
+    from minimarl.qnet import ptr, stream_handle
+    g = torch.Generator(device=DEV).manual_seed(1)
+    G, R, Cc = 3, 70, 45
+    U = torch.randn(G, M, R, device=DEV, generator=g)
+    V = torch.randn(G, M, Cc, device=DEV, generator=g)
+    dW = torch.zeros(G, R, Cc, device=DEV)
+    db = torch.zeros(G, R, device=DEV)
+    a = OuterArgs()
+    a.U, a.u_g, a.u_m = ptr(U), M * R, R
+    a.V, a.v_g, a.v_m = ptr(V), M * Cc, Cc
+    a.dW, a.w_g, a.db, a.b_g = ptr(dW), R * Cc, ptr(db), R
+    a.M, a.R, a.Cc, a.accumulate, a.groups = M, R, Cc, 0, G
+    L = lib()
+    n = int(L.mm_outer_reduce_batch_partial(ctypes.byref(a), 1))
+    part = torch.zeros(n, device=DEV)
+    check(L.mm_outer_reduce_batch(ctypes.byref(a), 1, ptr(part), n, stream_handle()), "outer_reduce_batch")
+    torch.cuda.synchronize()
+    ref = torch.einsum("gmr,gmc->grc", U.double(), V.double())
+    np.testing.assert_allclose(dW.double().cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=1e-3 * np.sqrt(M / 320))
+    np.testing.assert_allclose(db.double().cpu().numpy(), U.double().sum(1).cpu().numpy(), rtol=1e-4,
+                               atol=1e-3 * np.sqrt(M / 320))
