@@ -648,9 +648,12 @@ struct OuterBatch {
   float* partial;
 };
 
+// Block = 4 waves = one 64 x 64 tile of (R, Cc); per 32-row chunk the U / V slabs are staged in LDS
+// and every wave accumulates its 32 x 32 sub-tile with 16 exact-f32 MFMAs (v_mfma_f32_32x32x2_f32,
+// the reduction index m on the MFMA k dimension). Bias sums (U^T 1) by VALU in the c-tile-0 blocks.
 __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
-  __shared__ float su[32][33];
-  __shared__ float svv[32][33];
+  __shared__ float su[32][65];
+  __shared__ float svv[32][65];
   int j = 0;
   while (j + 1 < ob.njobs && (int)blockIdx.x >= ob.blk0[j + 1]) ++j;
   const OuterArgs& a = ob.job[j];
@@ -661,15 +664,18 @@ __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
   t /= ob.tiles_r[j];
   const int g = t % ob.groups[j];
   const int sl = t / ob.groups[j];
-  const int r0 = tr_ * 32, c0 = tc_ * 32;
+  const int r0 = tr_ * 64, c0 = tc_ * 64;
   const int m_begin = sl * ob.rps[j], m_end = min(a.M, m_begin + ob.rps[j]);
-  const int tr = threadIdx.x / 32, tc = threadIdx.x % 32;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  const int rw = wave >> 1, cw = wave & 1;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
   float sb = 0.f;
-  const bool do_b = a.db && tc_ == 0 && threadIdx.x < 32;
+  const bool do_b = a.db && tc_ == 0 && threadIdx.x < 64;
   for (int m0 = m_begin; m0 < m_end; m0 += 32) {
-    for (int k = threadIdx.x; k < 32 * 32; k += 256) {
-      const int mm = k / 32, x = k % 32;
+    for (int k = threadIdx.x; k < 32 * 64; k += 256) {
+      const int mm = k >> 6, x = k & 63;
       const int m = m0 + mm;
       float u = 0.f, v = 0.f;
       if (m < m_end) {
@@ -688,20 +694,19 @@ __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
       svv[mm][x] = v;
     }
     __syncthreads();
-    for (int mm = 0; mm < 32; ++mm) {
-      const float v = svv[mm][tc];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] += su[mm][tr + 8 * q] * v;
-    }
+    for (int s2 = 0; s2 < 16; ++s2)
+      acc = mfma32(su[2 * s2 + lh][rw * 32 + li], svv[2 * s2 + lh][cw * 32 + li], acc);
     if (do_b)
       for (int mm = 0; mm < 32; ++mm) sb += su[mm][threadIdx.x];
     __syncthreads();
   }
   const int64_t per = (int64_t)a.R * a.Cc + a.R;
   float* out = ob.partial + ob.part[j] + ((int64_t)sl * ob.groups[j] + g) * per;
+  const int c = c0 + cw * 32 + li;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = r0 + tr + 8 * q, c = c0 + tc;
+  for (int q = 0; q < 16; ++q) {
+    const int r = r0 + rw * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
     if (r < a.R && c < a.Cc) out[(int64_t)r * a.Cc + c] = acc[q];
   }
   if (do_b && r0 + threadIdx.x < a.R) out[(int64_t)a.R * a.Cc + r0 + threadIdx.x] = sb;
@@ -981,8 +986,8 @@ static int64_t outer_batch_layout(const mm_outer_args* x, int n, mm::OuterBatch*
     const mm_outer_args& q = x[j];
     ob->job[j] = {q.U, q.u_g, q.u_m, q.V, q.v_g, q.v_m, q.v_off, q.v_reset, q.dW, q.w_g, q.db, q.b_g, q.M, q.R,
                   q.Cc, q.accumulate};
-    ob->tiles_c[j] = (q.Cc + 31) / 32;
-    ob->tiles_r[j] = (q.R + 31) / 32;
+    ob->tiles_c[j] = (q.Cc + 63) / 64;
+    ob->tiles_r[j] = (q.R + 63) / 64;
     ob->groups[j] = q.groups;
     // rows per slice: 32-row chunks, at most ~64 slices per job (bounded partials at large batches)
     const int chunks = (q.M + 31) / 32;
