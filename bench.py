@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--cfg5", action="store_true",
                     help="also time the cfg5 dual agent forward (E=8192, N=27, D=300, A=36); off by default so "
                          "the default run's h3 dispatches are all the roofline's cfg2 launch")
+    ap.add_argument("--learner-big-steps", type=int, default=10,
+                    help="timed QMIX updates at B=4096 chunks (0 = skip; single-GPU runs only)")
     ap.add_argument("--offq-updates", type=int, default=30,
                     help="timed offpolicy episode-QMix updates on one GPU (0 = skip; single-GPU runs only)")
     args = ap.parse_args()
@@ -191,6 +193,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el_l = float(t.item())
     upd_per_s = args.learner_steps / el_l
+
+    # the same QMIX update at SURVEY 8(d)'s throughput batch (B = 4096 chunks of C = 10), single GPU
+    big = None
+    if args.learner_big_steps > 0 and world == 1:
+        mixb, tmixb = Mixer(N, N * D, 64, 32, dev, seed=7), Mixer(N, N * D, 64, 32, dev, seed=7)
+        lb = QLearner(eng.behavior, eng.target, mixb, tmixb, batch=4096, chunk=10, mode="qmix", device=dev)
+        lb.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=5)
+        for _ in range(2):
+            lb.replay_update()
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        for _ in range(args.learner_big_steps):
+            lb.replay_update()
+        torch.cuda.synchronize()
+        el_b = time.perf_counter() - t4
+        big = {"batch_chunks": 4096, "chunk": 10, "ms_per_update": round(el_b / args.learner_big_steps * 1e3, 3),
+               "updates_per_s": round(args.learner_big_steps / el_b, 1),
+               "chunk_samples_per_s": round(4096 * args.learner_big_steps / el_b, 1)}
+        del lb, mixb, tmixb
+        torch.cuda.empty_cache()
 
     # MAPPO (BASELINE configs[2]): 4096 envs x 8 agents per GPU, T=100 rollout steps with the fused
     # actor/critic kernel, device GAE, then 15 PPO epochs of chunked (L=5) BPTT on the whole buffer
@@ -361,7 +383,7 @@ def main():
             "learner": {"algo": "QMIX Train_dqn update", "batch_chunks": args.batch, "chunk": 10,
                         "mixer_hidden": 64, "ms_per_update": round(el_l / args.learner_steps * 1e3, 4),
                         "updates": args.learner_steps, "grad_allreduce": "rccl" if dist else None,
-                        "reference_cpu_updates_per_s": 12.0},
+                        "reference_cpu_updates_per_s": 12.0, "throughput_batch": big},
             "mappo": mappo,
             "offpolicy_qmix": offq,
             "cfg5_forward": cfg5,
