@@ -278,6 +278,139 @@ __device__ __forceinline__ void mixer_fwd_body(const MixFwdArgs& a, const MixFwd
   }
 }
 
+// Large batches: MIX_SPB samples per block share every weight read (the single-sample block re-reads
+// ~140 KB of W_hh + hypernet weights from L2 per sample). Same per-sample arithmetic and order as
+// mixer_fwd_body (bit-identical); needs the precomputed input projection (nt.gi).
+constexpr int MIX_SPB = 8;
+__global__ __launch_bounds__(256) void mixer_fwd_multi_kernel(MixFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const MixFwdNet& nt = a.net[blockIdx.y];
+  const int Hm = a.Hm, K1 = a.K1, N = a.N, NK = N * K1, RW = NK + 3 * K1;
+  const MixOff o = mix_offsets(a.S, Hm, K1, N);
+  const int b0 = blockIdx.x * MIX_SPB;
+  const int ns = min(MIX_SPB, a.B - b0);
+  float* h0 = sm;                        // [SPB][Hm]
+  float* gi = h0 + MIX_SPB * Hm;         // [SPB][3Hm]
+  float* gh = gi + MIX_SPB * 3 * Hm;     // [SPB][3Hm]
+  float* h1 = gh + MIX_SPB * 3 * Hm;     // [SPB][Hm]
+  float* hyp = h1 + MIX_SPB * Hm;        // [SPB][RW]: w1raw | b1 | w2raw | b2pre
+  float* yp = hyp + MIX_SPB * RW;        // [SPB][K1]
+  for (int idx = threadIdx.x; idx < MIX_SPB * Hm; idx += blockDim.x) {
+    const int sI = idx / Hm, i = idx % Hm, b = b0 + sI;
+    float v = 0.f;
+    if (sI < ns) {
+      const bool rz = !nt.h_in || (nt.reset && nt.reset[b]);
+      v = rz ? 0.f : nt.h_in[(int64_t)b * Hm + i];
+    }
+    h0[idx] = v;
+  }
+  for (int idx = threadIdx.x; idx < MIX_SPB * 3 * Hm; idx += blockDim.x) {
+    const int sI = idx / (3 * Hm);
+    gi[idx] = sI < ns ? nt.gi[(int64_t)b0 * 3 * Hm + idx] : 0.f;
+  }
+  __syncthreads();
+  // gh = W_hh h + b_hh (block_matvec order: sequential k, bias last)
+  for (int r = threadIdx.x; r < 3 * Hm; r += blockDim.x) {
+    float acc[MIX_SPB];
+#pragma unroll
+    for (int q = 0; q < MIX_SPB; ++q) acc[q] = 0.f;
+    const float* w = nt.P + o.gWhh + (int64_t)r * Hm;
+    for (int k = 0; k < Hm; ++k) {
+      const float wk = w[k];
+#pragma unroll
+      for (int q = 0; q < MIX_SPB; ++q) acc[q] += wk * h0[q * Hm + k];
+    }
+    const float bb = nt.P[o.gbhh + r];
+#pragma unroll
+    for (int q = 0; q < MIX_SPB; ++q) gh[q * 3 * Hm + r] = acc[q] + bb;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < ns * Hm; idx += blockDim.x) {
+    const int sI = idx / Hm, i = idx % Hm, b = b0 + sI;
+    const float* gI = gi + sI * 3 * Hm;
+    const float* gH = gh + sI * 3 * Hm;
+    const float r = sigmoidf_(gI[i] + gH[i]);
+    const float z = sigmoidf_(gI[Hm + i] + gH[Hm + i]);
+    const float n = tanhf_(gI[2 * Hm + i] + r * gH[2 * Hm + i]);
+    const float h0v = h0[sI * Hm + i];
+    const float hv = n + z * (h0v - n);
+    h1[sI * Hm + i] = hv;
+    nt.h_out[(int64_t)b * Hm + i] = hv;
+    if (nt.save) {
+      float* sv = nt.save + (int64_t)b * mix_save_dim(Hm, K1, N);
+      sv[i] = h0v;
+      sv[Hm + i] = r;
+      sv[2 * Hm + i] = z;
+      sv[3 * Hm + i] = n;
+      sv[4 * Hm + i] = gH[2 * Hm + i];
+      sv[5 * Hm + i] = hv;
+    }
+  }
+  __syncthreads();
+  // hypernets on h1 (rows: w1 [NK], b1 [K1], w2 [K1], b2 hidden [K1])
+  for (int r = threadIdx.x; r < RW; r += blockDim.x) {
+    const float* w;
+    float bb;
+    if (r < NK) {
+      w = nt.P + o.w1W + (int64_t)r * Hm;
+      bb = nt.P[o.w1b + r];
+    } else if (r < NK + K1) {
+      w = nt.P + o.b1W + (int64_t)(r - NK) * Hm;
+      bb = nt.P[o.b1b + r - NK];
+    } else if (r < NK + 2 * K1) {
+      w = nt.P + o.w2W + (int64_t)(r - NK - K1) * Hm;
+      bb = nt.P[o.w2b + r - NK - K1];
+    } else {
+      w = nt.P + o.b2aW + (int64_t)(r - NK - 2 * K1) * Hm;
+      bb = nt.P[o.b2ab + r - NK - 2 * K1];
+    }
+    float acc[MIX_SPB];
+#pragma unroll
+    for (int q = 0; q < MIX_SPB; ++q) acc[q] = 0.f;
+    for (int k = 0; k < Hm; ++k) {
+      const float wk = w[k];
+#pragma unroll
+      for (int q = 0; q < MIX_SPB; ++q) acc[q] += wk * h1[q * Hm + k];
+    }
+#pragma unroll
+    for (int q = 0; q < MIX_SPB; ++q) hyp[q * RW + r] = acc[q] + bb;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
+    const int sI = idx / K1, k = idx % K1, b = b0 + sI;
+    const float* hp = hyp + sI * RW;
+    float acc = 0.f;
+    for (int i = 0; i < N; ++i) acc += fabsf(hp[k * N + i]) * nt.q[(int64_t)b * N + i];
+    yp[sI * K1 + k] = acc + hp[NK + k];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < ns) {
+    const int sI = threadIdx.x, b = b0 + sI;
+    const float* hp = hyp + sI * RW;
+    const float* w2raw = hp + NK + K1;
+    const float* b2pre = hp + NK + 2 * K1;
+    float b2 = 0.f;
+    for (int k = 0; k < K1; ++k) b2 += nt.P[o.b2bW + k] * fmaxf(b2pre[k], 0.f);
+    b2 += nt.P[o.b2bb];
+    float acc = 0.f;
+    for (int k = 0; k < K1; ++k) acc += fabsf(w2raw[k]) * fmaxf(yp[sI * K1 + k], 0.f);
+    nt.qtot[b] = acc + b2;
+    if (nt.save) nt.save[(int64_t)b * mix_save_dim(Hm, K1, N) + 6 * Hm + NK + 4 * K1] = b2;
+  }
+  if (nt.save) {
+    for (int idx = threadIdx.x; idx < ns * RW; idx += blockDim.x) {
+      const int sI = idx / RW, i = idx % RW;
+      float* sv = nt.save + (int64_t)(b0 + sI) * mix_save_dim(Hm, K1, N);
+      const float v = hyp[sI * RW + i];
+      sv[6 * Hm + i] = i >= NK + 2 * K1 ? fmaxf(v, 0.f) : v;
+    }
+    for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
+      const int sI = idx / K1, k = idx % K1;
+      nt.save[(int64_t)(b0 + sI) * mix_save_dim(Hm, K1, N) + 6 * Hm + NK + 3 * K1 + k] = yp[sI * K1 + k];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ loss (all steps at once)
 // y = w * sum_i (r_i + gamma*(1-d)*Q'tot)   (qmix/_train.py:80-82, vdn/_train.py:76-77)
 // dQtot = 2 (Qtot - y) / B ;  loss = sum_t mean_b (y - Qtot)^2 ;  td = |y - Qtot| at t = C-1.
@@ -874,6 +1007,16 @@ int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const 
   a.K1 = K1;
   const size_t sm = sizeof(float) * ((size_t)S + 9 * Hm + N * K1 + 4 * K1);
   MM_REQUIRE(sm <= 64 * 1024, "mixer_fwd: state too large for LDS (%zu B)", sm);
+  bool all_gi = true;
+  for (int i = 0; i < n_nets; ++i) all_gi = all_gi && nets[i].gi;
+  const size_t smm = sizeof(float) * (size_t)mm::MIX_SPB * (9 * Hm + N * K1 + 4 * K1);
+  const char* mm_env = getenv("MM_MIX_MULTI");   // "0" forces the one-sample-per-block kernel (tests)
+  if (B >= 512 && all_gi && smm <= 64 * 1024 && !(mm_env && mm_env[0] == '0')) {
+    hipLaunchKernelGGL(mm::mixer_fwd_multi_kernel, dim3((B + mm::MIX_SPB - 1) / mm::MIX_SPB, n_nets), dim3(256), smm,
+                       (hipStream_t)s, a);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   hipLaunchKernelGGL(mm::mixer_fwd_kernel, dim3(B, n_nets), dim3(256), sm, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;

@@ -6,6 +6,8 @@ gradients |g - g_ref| <= 2e-4 * max|g_ref| + 1e-3 * |g_ref|; new priorities rtol
 post-Adam params atol 2e-6 where |g_ref| > 1e-4 * max|g_ref| (Adam's first step is
 lr * sign(g), so near-zero gradients are compared through the gradient check instead).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -368,3 +370,34 @@ def test_outer_reduce_batch_large_rows(M):
     np.testing.assert_allclose(dW.double().cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=1e-3 * np.sqrt(M / 320))
     np.testing.assert_allclose(db.double().cpu().numpy(), U.double().sum(1).cpu().numpy(), rtol=1e-4,
                                atol=1e-3 * np.sqrt(M / 320))
+
+
+def test_mixer_multi_sample_blocks_bit_identical():
+    """B >= 512 runs the mixer forward with 8 samples per block (shared weight reads); it must give
+    exactly the one-sample-per-block kernel's results (MM_MIX_MULTI=0)."""
+    from minimarl.learner import Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    N, D, A, B, C = 4, 47, 5, 600, 4
+    res = []
+    for multi in ("1", "0"):
+        os.environ["MM_MIX_MULTI"] = multi
+        try:
+            beh = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=1)
+            tgt = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=2)
+            mix = Mixer(N, N * D, 64, 32, DEV, seed=3)
+            tmix = Mixer(N, N * D, 64, 32, DEV, seed=4)
+            L = QLearner(beh, tgt, mix, tmix, batch=B, chunk=C, mode="qmix", device=DEV)
+            g = torch.Generator().manual_seed(0)
+            st = torch.rand(B, C, N, D, generator=g)
+            ns = torch.rand(B, C, N, D, generator=g)
+            act = torch.randint(0, A, (B, C, N), generator=g).float()
+            rew = torch.randn(B, C, N, generator=g) * 0.5
+            dn = (torch.rand(B, C, 1, generator=g) < 0.2).float()
+            w = torch.rand(B, 1, generator=g) * 0.5 + 0.5
+            L.load_batch(st, act, rew, ns, dn, w)
+            L.train_step(L._obs_buf, L._obs_buf)
+            torch.cuda.synchronize()
+            res.append((L.loss.clone(), L.P.clone(), L.td_last.clone()))
+        finally:
+            os.environ.pop("MM_MIX_MULTI", None)
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
