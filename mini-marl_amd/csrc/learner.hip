@@ -465,10 +465,30 @@ __global__ void lrn_loss_kernel(int B, int C, int N, float gamma, const float* r
   if (t == C - 1) td_last[b] = fabsf(diff);
 }
 
-// loss = sum_t (1/B) sum_b parts: one 256-thread block, per step a strided per-thread sum and a
-// fixed-shape tree over the threads (deterministic), steps accumulated in order
+// loss = sum_t (1/B) sum_b parts (logging value): small batches one thread per step t summing its
+// B parts in order; large batches (B > 256) a strided per-thread sum + fixed-shape tree per step.
+// Steps accumulated in order by thread 0 (deterministic either way).
 __global__ __launch_bounds__(256) void lrn_loss_reduce_kernel(int B, int C, const float* parts, float* loss) {
   __shared__ float sh[256];
+  if (B <= 256) {
+    for (int t = threadIdx.x; t < C; t += 256) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += parts[(int64_t)t * B + b];
+      if (t < 256) sh[t] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float tot = 0.f;
+      for (int t = 0; t < C && t < 256; ++t) tot += sh[t] / (float)B;
+      for (int t = 256; t < C; ++t) {
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += parts[(int64_t)t * B + b];
+        tot += s / (float)B;
+      }
+      *loss = tot;
+    }
+    return;
+  }
   float tot = 0.f;
   for (int t = 0; t < C; ++t) {
     float s = 0.f;
