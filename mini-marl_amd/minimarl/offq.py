@@ -45,7 +45,7 @@ class OffQMix:
     def __init__(self, n_agents, obs_dim, n_actions, episode_length, batch_size, mixer="qmix", hidden=64,
                  mixer_hidden=32, hyper_hidden=64, gamma=0.99, lr=5e-4, opti_eps=1e-5, max_grad_norm=10.0,
                  use_double_q=True, use_per=True, use_huber_loss=False, huber_delta=10.0, per_nu=0.9,
-                 per_eps=1e-6, tau=0.005, device="cuda", seed=None):
+                 per_eps=1e-6, tau=0.005, device="cuda", seed=None, grad_allreduce=None):
         assert mixer in ("qmix", "vdn")
         self.N, self.D, self.A, self.H = int(n_agents), int(obs_dim), int(n_actions), int(hidden)
         self.T, self.B = int(episode_length), int(batch_size)
@@ -55,6 +55,10 @@ class OffQMix:
         self.gamma, self.lr, self.eps, self.max_norm = gamma, lr, opti_eps, max_grad_norm
         self.double_q, self.use_per, self.huber, self.delta = use_double_q, use_per, use_huber_loss, huber_delta
         self.per_nu, self.per_eps, self.tau = per_nu, per_eps, tau
+        # data-parallel replicas (minimarl.dist.make_allreduce): the flat [agent | mixer] gradient is
+        # summed over ranks (one RCCL all-reduce per update) and averaged inside clip/Adam; every rank
+        # samples its own episode shard, so each rank's loss keeps its own mask-count denominator
+        self.allreduce = grad_allreduce
         self.device = torch.device(device)
         self.dims = OffqDims(self.N, self.D, self.H, self.A, MM_OFFQ_QMIX if mixer == "qmix" else MM_OFFQ_VDN,
                              self.S, self.K, self.Hh)
@@ -190,9 +194,12 @@ class OffQMix:
         L, st = lib(), stream_handle(self.device)
         check(L.mm_offq_loss_grad(ctypes.byref(self.dims), ctypes.byref(bt), ptr(self.P), ptr(self.PT), ptr(self.grad),
                                   ptr(self.ws), self.ws_bytes, ptr(self.stats), ptr(self.prio), st), "offq_loss_grad")
+        scale = 1.0
+        if self.allreduce is not None:
+            scale = 1.0 / self.allreduce(self.grad)
         check(L.mm_clip_adam(ptr(self.P), ptr(self.grad), ptr(self.m), ptr(self.v), self.total, self.total,
                              self.max_norm, self.lr, 0.9, 0.999, self.eps, ptr(self.step), ptr(self.partials),
-                             ptr(self.norm), 1.0, st), "clip_adam")
+                             ptr(self.norm), scale, st), "clip_adam")
         info = {"loss": self.stats[0], "grad_norm": self.norm[0], "Q_tot": self.stats[1]}
         return info, (self.prio if w is not None else None), idxes
 

@@ -135,3 +135,21 @@ def test_offq_multi_update_with_soft_target(name):
     if name == "qmix":
         for k in ref.MIXER_KEYS:
             np.testing.assert_allclose(tr.mixer_view(k).cpu().numpy(), M[k].numpy(), rtol=1e-4, atol=2e-6, err_msg=k)
+
+
+def test_offq_grad_allreduce_hook():
+    """Data-parallel hook: a stand-in all-reduce that sums two identical replicas' gradients (x2,
+    returns world = 2) must leave the update bit-identical to the single-replica one."""
+    d, tgt, meta = load_case("qmix")
+    a = make_trainer("qmix", d, tgt, meta)
+    b = make_trainer("qmix", d, tgt, meta)
+
+    def fake_allreduce(g):
+        g.mul_(2.0)
+        return 2
+
+    b.allreduce = fake_allreduce
+    for tr in (a, b):
+        tr.train_policy_on_batch(ref_batch(d))
+    torch.cuda.synchronize()
+    assert torch.equal(a.P, b.P) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
