@@ -195,6 +195,60 @@ __global__ __launch_bounds__(256) void mixer_gi_kernel(MixGiArgs a) {
   }
 }
 
+// LDS-tiled form of the same projection: block = 4 waves = 64 samples x 64 gate rows, per 32-deep
+// k chunk the gathered state rows and the W_ih rows are staged in LDS ([k][sample], [k][row];
+// both loads coalesced along k), every wave accumulates a 32 x 32 sub-tile with 16 exact-f32
+// MFMAs in fixed k order.
+__global__ __launch_bounds__(256) void mixer_gi_tiled_kernel(MixGiArgs a) {
+  __shared__ float sx[32][65];
+  __shared__ float sw[32][65];
+  const MixGiNet& nt = a.net[blockIdx.z];
+  const int S = a.S, M3 = 3 * a.Hm;
+  const MixOff o = mix_offsets(S, a.Hm, a.K1, a.N);
+  const int c0 = blockIdx.y * 64, m0 = blockIdx.x * 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  const int cw = wave >> 1, mw = wave & 1;
+  const float* Wih = nt.P + o.gWih;
+  // the 8 sample rows (c0 + (tid >> 5) + 8p) and 8 weight rows (m0 + ...) this thread stages
+  const float* xr[8];
+  const float* wr[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int rr = (threadIdx.x >> 5) + 8 * p;
+    const int c = c0 + rr;
+    const int64_t off = c < a.R ? nt.s_off[c] : -1;
+    xr[p] = c < a.R ? (off >= 0 ? a.obs + off : a.reset_obs) : nullptr;
+    wr[p] = m0 + rr < M3 ? Wih + (int64_t)(m0 + rr) * S : nullptr;
+  }
+  const int x = threadIdx.x & 31;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+  for (int k0 = 0; k0 < S; k0 += 32) {
+    const bool ok = k0 + x < S;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int rr = (threadIdx.x >> 5) + 8 * p;
+      sx[x][rr] = (ok && xr[p]) ? xr[p][k0 + x] : 0.f;
+      sw[x][rr] = (ok && wr[p]) ? wr[p][k0 + x] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+      acc = mfma32(sx[2 * s2 + lh][cw * 32 + li], sw[2 * s2 + lh][mw * 32 + li], acc);
+    __syncthreads();
+  }
+  const int m = m0 + mw * 32 + li;
+  if (m < M3) {
+    const float bias = nt.P[o.gbih + m];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = c0 + cw * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+      if (c < a.R) nt.gi[(int64_t)c * M3 + m] = bias + acc[q];
+    }
+  }
+}
+
 // One block per (sample, net): blockIdx.y selects behavior / target.
 __device__ __forceinline__ void mixer_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, int b);
 
@@ -701,6 +755,76 @@ __device__ __forceinline__ void agent_bwd_body(const AgentBwdArgs& a) {
   }
 }
 
+// Large-batch variant (H <= 64): one block = one agent x 32 samples, one wave = 8 samples of that
+// agent, lane = hidden feature. Every W_hh element the transposed mat-vec reads serves the wave's
+// 8 samples (the one-pair-per-wave kernel re-reads the agent's 48 KB W_hh per pair, which bounds
+// it on L2 bandwidth at large B). Per-sample arithmetic and summation order are those of
+// agent_bwd_body, so the results are bit-identical (tested).
+constexpr int BWD_SPW = 8;   // samples per wave
+__global__ __launch_bounds__(256) void agent_bwd_multi_kernel(AgentBwdArgs a) {
+  __shared__ float4 sdg[4][3 * 64][BWD_SPW / 4];   // [wave][gate row][sample]
+  const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
+  const int i = blockIdx.y;
+  const int b0 = (blockIdx.x * 4 + w) * BWD_SPW;
+  const int H = a.H, A = a.A;
+  const int SD = a.F1 + a.G + 6 * H;
+  const float* Wq = a.P + a.oWq + (int64_t)i * A * H;
+  const float* Whh = a.P + a.oWhh + (int64_t)i * 3 * H * H;
+  float* sd = reinterpret_cast<float*>(&sdg[w][0][0]);
+  float acc[BWD_SPW];
+#pragma unroll
+  for (int s = 0; s < BWD_SPW; ++s) {
+    const int b = b0 + s;
+    acc[s] = 0.f;
+    if (b >= a.B) continue;
+    const int64_t pair = (int64_t)b * a.N + i;
+    const float* h0 = a.save + pair * SD + a.F1 + a.G;
+    const int act = a.acts[pair];
+    const float dqa = a.dqa[pair];
+    if (f < A) a.dq[pair * A + f] = (f == act) ? dqa : 0.f;
+    if (f < H) {
+      const bool drop = a.done[b] > 0.5f;
+      const float dh1 = Wq[(int64_t)act * H + f] * dqa + (drop ? 0.f : a.dh[pair * H + f]);
+      const float r = h0[H + f], z = h0[2 * H + f], n = h0[3 * H + f], anh = h0[4 * H + f];
+      const float dn = dh1 * (1.f - z);
+      const float dz = dh1 * (h0[f] - n);
+      const float dpn = dn * (1.f - n * n);
+      const float dar = dpn * anh * r * (1.f - r);
+      const float daz = dz * z * (1.f - z);
+      float* gi = a.dgi + pair * 3 * H;
+      float* gh = a.dgh + pair * 3 * H;
+      gi[f] = dar;
+      gi[H + f] = daz;
+      gi[2 * H + f] = dpn;
+      gh[f] = dar;
+      gh[H + f] = daz;
+      gh[2 * H + f] = dpn * r;
+      sd[f * BWD_SPW + s] = dar;
+      sd[(H + f) * BWD_SPW + s] = daz;
+      sd[(2 * H + f) * BWD_SPW + s] = dpn * r;
+      acc[s] = dh1 * z;
+    }
+  }
+  // each wave reads only its own rows of sdg: LDS is in order within a wave
+  __builtin_amdgcn_wave_barrier();
+  if (f >= H) return;
+#pragma unroll 8
+  for (int r = 0; r < 3 * H; ++r) {
+    const float wv = Whh[(int64_t)r * H + f];
+#pragma unroll
+    for (int q = 0; q < BWD_SPW / 4; ++q) {
+      const float4 x = sdg[w][r][q];
+      acc[4 * q + 0] += wv * x.x;
+      acc[4 * q + 1] += wv * x.y;
+      acc[4 * q + 2] += wv * x.z;
+      acc[4 * q + 3] += wv * x.w;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < BWD_SPW; ++s)
+    if (b0 + s < a.B) a.dh[((int64_t)(b0 + s) * a.N + i) * H + f] = acc[s];
+}
+
 // ------------------------------------------------------------------ batched reductions
 // dW[g][r][c] (+)= sum_m U[g](m, r) * V[g](m, c) ;  db[g][r] (+)= sum_m U[g](m, r)
 //   U(m, r) = U[g*u_g + m*u_m + r];  V(m, c) = V[g*v_g + m*v_m + c], or, if v_off != nullptr,
@@ -926,6 +1050,48 @@ __global__ __launch_bounds__(256) void tmv_kernel(TmvArgs a) {
   }
 }
 
+// Same op on exact-f32 MFMA (v_mfma_f32_32x32x2_f32): block = 4 waves = one 64 (m) x 64 (c) tile,
+// per 32-deep r chunk the X / W slabs are staged in LDS (X transposed to [r][m]) and every wave
+// accumulates its 32 x 32 sub-tile with 16 MFMAs (r on the MFMA k dimension; fixed order).
+__global__ __launch_bounds__(256) void tmv_mfma_kernel(TmvArgs a) {
+  __shared__ float sx[32][65];
+  __shared__ float sw[32][65];
+  const int g = blockIdx.z;
+  const int m0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  const int mw = wave >> 1, cw = wave & 1;
+  const float* X = a.X + g * a.x_g;
+  const float* W = a.W + g * a.w_g;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+  for (int rr = 0; rr < a.R; rr += 32) {
+    for (int k = threadIdx.x; k < 32 * 64; k += 256) {
+      const int mm = k >> 5, x = k & 31;          // X: 32 consecutive r of one row per 32 lanes
+      const int m = m0 + mm, r = rr + x;
+      sx[x][mm] = (m < a.M && r < a.R) ? X[(int64_t)m * a.x_m + r] : 0.f;
+      const int kk = k >> 6, y = k & 63;          // W: 64 consecutive c of one r
+      const int r2 = rr + kk, c = c0 + y;
+      sw[kk][y] = (r2 < a.R && c < a.Cc) ? W[(int64_t)r2 * a.Cc + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+      acc = mfma32(sx[2 * s2 + lh][mw * 32 + li], sw[2 * s2 + lh][cw * 32 + li], acc);
+    __syncthreads();
+  }
+  const int c = c0 + cw * 32 + li;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int m = m0 + mw * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+    if (m < a.M && c < a.Cc) {
+      float v = acc[q];
+      if (a.Z && !(a.Z[g * a.z_g + (int64_t)m * a.z_m + c] > 0.f)) v = 0.f;
+      a.Y[g * a.y_g + (int64_t)m * a.y_m + c] = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ clip + Adam
 // partial sums of squares of G[0:n_clip] ; also advances the Adam step counter
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* G, int64_t n, float* partials, float* step) {
@@ -1056,6 +1222,13 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
   a.Hm = Hm;
   a.K1 = K1;
   a.N = N;
+  const char* gm_env = getenv("MM_GI_TILED");   // "0": the register-operand kernel
+  if (!(gm_env && gm_env[0] == '0')) {
+    dim3 grid((3 * Hm + 63) / 64, (R + 63) / 64, P1 ? 2 : 1);
+    hipLaunchKernelGGL(mm::mixer_gi_tiled_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   dim3 grid((R + 31) / 32, (3 * Hm + 31) / 32, P1 ? 2 : 1);
   hipLaunchKernelGGL(mm::mixer_gi_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
@@ -1127,6 +1300,13 @@ int mm_agent_bwd(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWh
   mm::AgentBwdArgs a = {P, oWq, oWhh, save, acts, dqa, done, dh, dgi, dgh, dq,
                         B, d->n_agents, d->f1, d->g, d->h, d->n_actions};
   const int pairs = B * d->n_agents;
+  const char* bm_env = getenv("MM_BWD_MULTI");   // "0" forces the one-pair-per-wave kernel (tests)
+  if (B >= 512 && d->h <= 64 && !(bm_env && bm_env[0] == '0')) {
+    hipLaunchKernelGGL(mm::agent_bwd_multi_kernel, dim3((B + 4 * mm::BWD_SPW - 1) / (4 * mm::BWD_SPW), d->n_agents),
+                       dim3(256), 0, (hipStream_t)s, a);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   hipLaunchKernelGGL(mm::agent_bwd_kernel, dim3((pairs + 3) / 4), dim3(256), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
@@ -1197,6 +1377,13 @@ int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
   MM_REQUIRE(x && x->M > 0 && x->R > 0 && x->Cc > 0 && x->groups > 0, "tmv: bad args");
   mm::TmvArgs a = {x->W, x->w_g, x->X, x->x_g, x->x_m, x->Z, x->z_g, x->z_m, x->Y, x->y_g, x->y_m,
                    x->M, x->R, x->Cc};
+  const char* tm_env = getenv("MM_TMV_MFMA");   // "0": the scalar LDS-tiled kernel
+  if (!(tm_env && tm_env[0] == '0')) {
+    dim3 grid((x->Cc + 63) / 64, (x->M + 63) / 64, x->groups);
+    hipLaunchKernelGGL(mm::tmv_mfma_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   dim3 grid((x->Cc + 31) / 32, (x->M + 31) / 32, x->groups);
   hipLaunchKernelGGL(mm::tmv_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());

@@ -372,15 +372,17 @@ def test_outer_reduce_batch_large_rows(M):
                                atol=1e-3 * np.sqrt(M / 320))
 
 
-def test_mixer_multi_sample_blocks_bit_identical():
-    """B >= 512 runs the mixer forward with 8 samples per block (shared weight reads); it must give
-    exactly the one-sample-per-block kernel's results (MM_MIX_MULTI=0)."""
+@pytest.mark.parametrize("knob", ["MM_MIX_MULTI", "MM_BWD_MULTI"])
+def test_multi_sample_blocks_bit_identical(knob):
+    """B >= 512 runs the mixer forward with 8 samples per block and the agent backward with 8
+    samples per wave (shared weight reads); each must give exactly the one-sample kernel's results
+    (knob = 0)."""
     from minimarl.learner import Mixer, QLearner
     from minimarl.qnet import AgentQNet
     N, D, A, B, C = 4, 47, 5, 600, 4
     res = []
     for multi in ("1", "0"):
-        os.environ["MM_MIX_MULTI"] = multi
+        os.environ[knob] = multi
         try:
             beh = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=1)
             tgt = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=2)
@@ -399,5 +401,5 @@ def test_mixer_multi_sample_blocks_bit_identical():
             torch.cuda.synchronize()
             res.append((L.loss.clone(), L.P.clone(), L.td_last.clone()))
         finally:
-            os.environ.pop("MM_MIX_MULTI", None)
+            os.environ.pop(knob, None)
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
