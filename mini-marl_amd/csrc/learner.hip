@@ -687,6 +687,157 @@ __device__ __forceinline__ void mixer_bwd_body(const MixBwdArgs& a, int b) {
   for (int c = threadIdx.x; c < Hm; c += blockDim.x) a.dhm[(int64_t)b * Hm + c] = shd[c];
 }
 
+// block_matvec_t for MIX_SPB samples at once: out[q][c] += sum_r W[r][c] d[q][r]; every W element
+// read serves all samples. Per sample the partial-sum order is block_matvec_t's (bit-identical).
+// red: [MIX_SPB][nw][K] floats.
+__device__ void block_matvec_t_multi(const float* __restrict__ W, int rows, int K, const float* d, int ds,
+                                     float* out, int os, float* red) {
+  constexpr int Q = MIX_SPB;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int c = lane; c < K; c += 64) {
+    float a0[Q], a1[Q], a2[Q], a3[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) a0[q] = a1[q] = a2[q] = a3[q] = 0.f;
+    int r = w;
+    for (; r + 3 * nw < rows; r += 4 * nw) {
+      const float w0 = W[(int64_t)r * K + c], w1 = W[(int64_t)(r + nw) * K + c];
+      const float w2 = W[(int64_t)(r + 2 * nw) * K + c], w3 = W[(int64_t)(r + 3 * nw) * K + c];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const float* dq = d + q * ds;
+        a0[q] += w0 * dq[r];
+        a1[q] += w1 * dq[r + nw];
+        a2[q] += w2 * dq[r + 2 * nw];
+        a3[q] += w3 * dq[r + 3 * nw];
+      }
+    }
+    for (; r < rows; r += nw) {
+      const float w0 = W[(int64_t)r * K + c];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) a0[q] += w0 * d[q * ds + r];
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) red[(q * nw + w) * K + c] = (a0[q] + a1[q]) + (a2[q] + a3[q]);
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < Q * K; idx += blockDim.x) {
+    const int q = idx / K, c = idx % K;
+    float acc = 0.f;
+    for (int v = 0; v < nw; ++v) acc += red[(q * nw + v) * K + c];
+    out[q * os + c] += acc;
+  }
+  __syncthreads();
+}
+
+// Chunk-sequence mixer backward with MIX_SPB samples per block (B >= 512): the per-sample math of
+// mixer_bwd_body in the same order, the transposed mat-vecs shared over the block's samples.
+__global__ __launch_bounds__(256) void mixer_bwd_seq_multi_kernel(MixBwdArgs a0, MixBwdSeq sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int Q = MIX_SPB;
+  const int Hm = a0.Hm, K1 = a0.K1, N = a0.N, NK = N * K1, SH = NK + 3 * K1;
+  const MixOff o = mix_offsets(a0.S, Hm, K1, N);
+  const int b0 = blockIdx.x * Q;
+  const int ns = min(Q, a0.B - b0);
+  const int nw = blockDim.x >> 6;
+  float* dhm1 = sm;                 // [Q][Hm]
+  float* dgh = dhm1 + Q * Hm;       // [Q][3Hm]
+  float* shd = dgh + Q * 3 * Hm;    // [Q][SH]
+  float* red = shd + Q * SH;        // [Q][nw][Hm]
+  const int svd = mix_save_dim(Hm, K1, N), dld = mix_delta_dim(Hm, K1, N);
+  for (int t = sq.C - 1; t >= 0; --t) {
+    const float* save = a0.save + t * sq.save_st;
+    const float* qa = a0.qa + t * sq.qa_st;
+    const float* dqv = a0.dq + t * sq.dq_st;
+    const float* done = t == sq.C - 1 ? sq.ones : a0.done + t * sq.done_st;
+    float* dqa = a0.dqa + t * sq.dqa_st;
+    float* delta = a0.delta + t * sq.delta_st;
+    // hypernet / mixing deltas
+    for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
+      const int s = idx / K1, k = idx % K1, b = b0 + s;
+      const float* w1raw = save + (int64_t)b * svd + 6 * Hm;
+      const float* w2raw = w1raw + NK + K1;
+      const float* b2pre = w2raw + K1;
+      const float* ypre = b2pre + K1;
+      float* dl = delta + (int64_t)b * dld;
+      float* sh = shd + s * SH;
+      const float dQ = dqv[b];
+      const float y = fmaxf(ypre[k], 0.f);
+      const float w2 = w2raw[k];
+      const float dw2 = dQ * y * (w2 > 0.f ? 1.f : (w2 < 0.f ? -1.f : 0.f));
+      const float dyp = ypre[k] > 0.f ? dQ * fabsf(w2) : 0.f;
+      const float db2p = b2pre[k] > 0.f ? dQ * a0.P[o.b2bW + k] : 0.f;
+      dl[6 * Hm + NK + k] = dyp;
+      dl[6 * Hm + NK + K1 + k] = dw2;
+      dl[6 * Hm + NK + 2 * K1 + k] = db2p;
+      sh[NK + k] = dyp;
+      sh[NK + K1 + k] = dw2;
+      sh[NK + 2 * K1 + k] = db2p;
+      for (int i = 0; i < N; ++i) {
+        const float wv = w1raw[k * N + i];
+        const float dw1 = dyp * qa[(int64_t)b * N + i] * (wv > 0.f ? 1.f : (wv < 0.f ? -1.f : 0.f));
+        dl[6 * Hm + k * N + i] = dw1;
+        sh[k * N + i] = dw1;
+      }
+    }
+    if ((int)threadIdx.x < ns) {
+      const int b = b0 + threadIdx.x;
+      delta[(int64_t)b * dld + 6 * Hm + NK + 3 * K1] = dqv[b];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < ns * N; idx += blockDim.x) {
+      const int s = idx / N, i = idx % N, b = b0 + s;
+      const float* w1raw = save + (int64_t)b * svd + 6 * Hm;
+      float acc = 0.f;
+      for (int k = 0; k < K1; ++k) acc += shd[s * SH + NK + k] * fabsf(w1raw[k * N + i]);
+      dqa[(int64_t)b * N + i] = acc;
+    }
+    for (int idx = threadIdx.x; idx < Q * Hm; idx += blockDim.x) {
+      const int s = idx / Hm, c = idx % Hm, b = b0 + s;
+      dhm1[idx] = (s >= ns || done[b] > 0.5f) ? 0.f : a0.dhm[(int64_t)b * Hm + c];
+    }
+    __syncthreads();
+    block_matvec_t_multi(a0.P + o.w1W, NK, Hm, shd, SH, dhm1, Hm, red);
+    block_matvec_t_multi(a0.P + o.b1W, K1, Hm, shd + NK, SH, dhm1, Hm, red);
+    block_matvec_t_multi(a0.P + o.w2W, K1, Hm, shd + NK + K1, SH, dhm1, Hm, red);
+    block_matvec_t_multi(a0.P + o.b2aW, K1, Hm, shd + NK + 2 * K1, SH, dhm1, Hm, red);
+    // GRU backward (h' = n + z (h - n))
+    for (int idx = threadIdx.x; idx < Q * Hm; idx += blockDim.x) {
+      const int s = idx / Hm, i = idx % Hm, b = b0 + s;
+      if (s >= ns) {
+        dgh[s * 3 * Hm + i] = dgh[s * 3 * Hm + Hm + i] = dgh[s * 3 * Hm + 2 * Hm + i] = 0.f;
+        continue;
+      }
+      const float* sv = save + (int64_t)b * svd;
+      const float dh = dhm1[idx];
+      const float r = sv[Hm + i], z = sv[2 * Hm + i], n = sv[3 * Hm + i];
+      const float dn = dh * (1.f - z);
+      const float dz = dh * (sv[i] - n);
+      const float dpn = dn * (1.f - n * n);
+      const float dr = dpn * sv[4 * Hm + i];
+      const float dar = dr * r * (1.f - r);
+      const float daz = dz * z * (1.f - z);
+      float* dl = delta + (int64_t)b * dld;
+      dl[i] = dar;
+      dl[Hm + i] = daz;
+      dl[2 * Hm + i] = dpn;
+      dl[3 * Hm + i] = dar;
+      dl[4 * Hm + i] = daz;
+      dl[5 * Hm + i] = dpn * r;
+      dgh[s * 3 * Hm + i] = dar;
+      dgh[s * 3 * Hm + Hm + i] = daz;
+      dgh[s * 3 * Hm + 2 * Hm + i] = dpn * r;
+      shd[s * SH + i] = dh * z;   // dhm0 direct path (hypernet deltas are consumed)
+    }
+    __syncthreads();
+    block_matvec_t_multi(a0.P + o.gWhh, 3 * Hm, Hm, dgh, 3 * Hm, shd, SH, red);
+    for (int idx = threadIdx.x; idx < ns * Hm; idx += blockDim.x) {
+      const int s = idx / Hm, c = idx % Hm;
+      a0.dhm[(int64_t)(b0 + s) * Hm + c] = shd[s * SH + c];
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------ agent backward chain (one step)
 struct AgentBwdArgs {
   const float* P;            // behavior agent params (canonical flat)
@@ -1277,6 +1428,14 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
   q.dqa_st = (int64_t)B * N;
   q.delta_st = (int64_t)B * mm::mix_delta_dim(Hm, K1, N);
   q.ones = ones;
+  const size_t smm = sizeof(float) * (size_t)mm::MIX_SPB * (4 * Hm + N * K1 + 3 * K1 + 4 * Hm);
+  const char* mm_env = getenv("MM_MIX_MULTI");   // "0" forces the one-sample-per-block kernel (tests)
+  if (B >= 512 && smm <= 64 * 1024 && !(mm_env && mm_env[0] == '0')) {
+    hipLaunchKernelGGL(mm::mixer_bwd_seq_multi_kernel, dim3((B + mm::MIX_SPB - 1) / mm::MIX_SPB), dim3(256), smm,
+                       (hipStream_t)s, a, q);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   const size_t sm = sizeof(float) * ((size_t)8 * Hm + N * K1 + 3 * K1);
   hipLaunchKernelGGL(mm::mixer_bwd_seq_kernel, dim3(B), dim3(256), sm, (hipStream_t)s, a, q);
   MM_HIP_CHECK(hipGetLastError());
