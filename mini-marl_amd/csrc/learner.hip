@@ -1101,8 +1101,12 @@ __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
   for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
   float sb = 0.f;
   const bool do_b = a.db && tc_ == 0 && threadIdx.x < 64;
-  for (int m0 = m_begin; m0 < m_end; m0 += 32) {
-    for (int k = threadIdx.x; k < 32 * 64; k += 256) {
+  // register prefetch: chunk m0 + 32 is loaded while chunk m0 is reduced
+  float pu[8], pv[8];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int k = threadIdx.x + 256 * p;
       const int mm = k >> 6, x = k & 63;
       const int m = m0 + mm;
       float u = 0.f, v = 0.f;
@@ -1118,10 +1122,20 @@ __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
           }
         }
       }
-      su[mm][x] = u;
-      svv[mm][x] = v;
+      pu[p] = u;
+      pv[p] = v;
+    }
+  };
+  if (m_begin < m_end) load(m_begin);
+  for (int m0 = m_begin; m0 < m_end; m0 += 32) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int k = threadIdx.x + 256 * p;
+      su[k >> 6][k & 63] = pu[p];
+      svv[k >> 6][k & 63] = pv[p];
     }
     __syncthreads();
+    if (m0 + 32 < m_end) load(m0 + 32);
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2)
       acc = mfma32(su[2 * s2 + lh][rw * 32 + li], svv[2 * s2 + lh][cw * 32 + li], acc);
@@ -1374,7 +1388,8 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
   a.K1 = K1;
   a.N = N;
   const char* gm_env = getenv("MM_GI_TILED");   // "0": the register-operand kernel
-  if (!(gm_env && gm_env[0] == '0')) {
+  // small R (B = 32 updates): the split-K register kernel gives more blocks and wins
+  if (R >= 2048 && !(gm_env && gm_env[0] == '0')) {
     dim3 grid((3 * Hm + 63) / 64, (R + 63) / 64, P1 ? 2 : 1);
     hipLaunchKernelGGL(mm::mixer_gi_tiled_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
     MM_HIP_CHECK(hipGetLastError());
@@ -1537,7 +1552,8 @@ int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
   mm::TmvArgs a = {x->W, x->w_g, x->X, x->x_g, x->x_m, x->Z, x->z_g, x->z_m, x->Y, x->y_g, x->y_m,
                    x->M, x->R, x->Cc};
   const char* tm_env = getenv("MM_TMV_MFMA");   // "0": the scalar LDS-tiled kernel
-  if (!(tm_env && tm_env[0] == '0')) {
+  // small M (B = 32 updates): the 32 x 32 scalar tiles give more blocks and win
+  if (x->M >= 2048 && !(tm_env && tm_env[0] == '0')) {
     dim3 grid((x->Cc + 63) / 64, (x->M + 63) / 64, x->groups);
     hipLaunchKernelGGL(mm::tmv_mfma_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
     MM_HIP_CHECK(hipGetLastError());
