@@ -38,9 +38,19 @@ def qnet_flops_per_agent_step(D, F1, G, H, A):
     return 2 * (D * F1 + F1 * G + 3 * G * H + 3 * H * H + H * A)
 
 
-def cpu_baseline(E, N, F1, G, H, budget_s=12.0):
-    """Oracle (CPU port) of the same rollout step on the host cores: numpy env + torch-CPU nets."""
-    import numpy as np
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _cpu_rollout_rate(E, N, F1, G, H, budget_s):
+    """Oracle (CPU port) of the same rollout step: numpy env + torch-CPU nets, behavior + target + TD."""
     from oracle import nets
     from oracle.env import EnvSpec, VecEnvOracle
     torch.manual_seed(0)
@@ -76,10 +86,55 @@ def cpu_baseline(E, N, F1, G, H, budget_s=12.0):
             if time.perf_counter() - t0 > budget_s:
                 break
     dt = time.perf_counter() - t0
-    return {"value": steps * E * N / dt, "unit": "agent-env-steps/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+    return steps * E * N / dt, steps, dt
+
+
+def cpu_baseline(E, N, F1, G, H, budget_s=8.0):
+    """The oracle's rollout step on the host cores, at torch's default thread count and at 1 thread;
+    the better of the two is the baseline."""
+    nthreads = torch.get_num_threads()
+    runs = []
+    for th in (nthreads, 1):
+        torch.set_num_threads(th)
+        rate, steps, dt = _cpu_rollout_rate(E, N, F1, G, H, budget_s)
+        runs.append({"threads": th, "value": round(rate, 1), "steps": steps, "seconds": round(dt, 2)})
+    torch.set_num_threads(nthreads)
+    best = max(runs, key=lambda r: r["value"])
+    return {"value": best["value"], "unit": "agent-env-steps/s", "cores": best["threads"], "kind": "port",
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(), "runs": runs,
             "sample": f"oracle rollout step (numpy env + torch-CPU GRU-{H} nets, behavior+target, TD) at "
-                      f"{E} envs x {N} agents, {steps} steps in {dt:.1f}s"}
+                      f"{E} envs x {N} agents, ~{budget_s:.0f} s per thread setting; best of {nthreads} threads "
+                      f"and 1 thread"}
+
+
+def cpu_learner_baseline(N, D, B=32, C=10, H=64, Hm=64, budget_s=6.0):
+    """The oracle's Train_dqn update (qmix/_train.py:19-121 restated in oracle/nets.py) at the bench
+    learner's shapes, timed on the host cores: the port's updates/s beside the GPU's."""
+    from oracle import nets
+    torch.manual_seed(0)
+    F1, G, A, K1 = 64, H, 5, 32
+    r = lambda *s: torch.randn(*s) * 0.1  # noqa: E731
+    P = {"W1": r(N, F1, D), "b1": r(N, F1), "W2": r(N, G, F1), "b2": r(N, G), "Wih": r(N, 3 * H, G),
+         "Whh": r(N, 3 * H, H), "bih": r(N, 3 * H), "bhh": r(N, 3 * H), "Wq": r(N, A, H), "bq": r(N, A)}
+    S = N * D
+    M = {"gWih": r(3 * Hm, S), "gWhh": r(3 * Hm, Hm), "gbih": r(3 * Hm), "gbhh": r(3 * Hm), "w1W": r(N * K1, Hm),
+         "w1b": r(N * K1), "w2W": r(K1, Hm), "w2b": r(K1), "b1W": r(K1, Hm), "b1b": r(K1), "b2aW": r(K1, Hm),
+         "b2ab": r(K1), "b2bW": r(1, K1), "b2bb": r(1)}
+    g = torch.Generator().manual_seed(1)
+    batch = (torch.rand(B, C, N, D, generator=g), torch.randint(0, A, (B, C, N), generator=g).float(),
+             torch.randn(B, C, N, generator=g), torch.rand(B, C, N, D, generator=g),
+             (torch.rand(B, C, 1, generator=g) < 0.1).float(), torch.ones(B, 1))
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        P, M, _, _, _ = nets.qmix_train_step(P, M, P, M, batch, 0.99, 1e-3, 5.0, hidden_dim=K1)
+        P = {k: v.detach() for k, v in P.items()}
+        M = {k: v.detach() for k, v in M.items()}
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "updates/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle Train_dqn update (torch-CPU autograd) at B={B}, C={C}, N={N}, GRU-{H}, Hm={Hm}: "
+                      f"{n} updates in {dt:.1f} s"}
 
 
 def time_kernel(fn, iters=50):
@@ -93,6 +148,37 @@ def time_kernel(fn, iters=50):
     end.record()
     torch.cuda.synchronize()
     return start.elapsed_time(end) / iters / 1e3
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """``--gpus N`` without an outer launcher: start N ranks (one process per GPU) with
+    torch.distributed.run as a CHILD process, before this process makes any GPU call, and return its
+    exit code. An outer torchrun (WORLD_SIZE set) runs main() directly instead."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def probe_ranks(world, rank):
+    """``--probe-ranks``: rendezvous over gloo (no GPU), gather every rank id, rank 0 prints one JSON line."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    ids = [None] * world
+    dist.all_gather_object(ids, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                                 "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"probe": "ranks", "world": dist.get_world_size(), "ranks": ids}))
+    dist.destroy_process_group()
 
 
 def main():
@@ -115,11 +201,21 @@ def main():
                     help="timed QMIX updates at B=4096 chunks (0 = skip; single-GPU runs only)")
     ap.add_argument("--offq-updates", type=int, default=30,
                     help="timed offpolicy episode-QMix updates on one GPU (0 = skip; single-GPU runs only)")
+    ap.add_argument("--train-episodes", type=int, default=3,
+                    help="timed episodes of the integrated QMIX train loop (0 = skip)")
+    ap.add_argument("--probe-ranks", action="store_true", help="launcher check: gloo rendezvous only, no GPU")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    if args.probe_ranks:
+        probe_ranks(world, rank)
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -130,7 +226,8 @@ def main():
     from minimarl.engine import RolloutEngine
     E, N, Hh = args.envs, args.agents, args.hidden
     F1, G = 64, Hh
-    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=16 * E, seed=1234 + rank, device=dev)
+    cap = 16 * E
+    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=cap, seed=1234 + rank, device=dev)
     D = eng.D
     from minimarl.learner import Mixer, QLearner
     mix = Mixer(N, N * D, 64, 32, dev, seed=7)
@@ -141,19 +238,21 @@ def main():
         eng.sync_target()
         tmix.flat.copy_(mix.flat)
         eng.behavior.mark_dirty()
-    GS = eng.graph_steps()                      # one HIP graph = one chunk of GS lockstep steps
-    warm_rep = max(1, -(-args.warmup // GS))
-    n_rep = max(1, -(-args.steps // GS))
-    steps = n_rep * GS
-    for _ in range(warm_rep):
+    # setup (untimed, not counted as warm-up): fill the PER to capacity so every timed chunk insert
+    # is a steady-state evicting insert
+    fill_chunks = cap // E
+    for _ in range(fill_chunks):
         eng.run_graph(args.epsilon)
+    eng.capture_steps()
+    assert len(eng.per) == cap
+    # warm-up and timed region: exactly W and K lockstep steps (chunk graphs + single-step graphs)
+    eng.run_steps(args.warmup, args.epsilon)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(n_rep):
-        eng.run_graph(args.epsilon)
+    eng.run_steps(args.steps, args.epsilon)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -163,6 +262,7 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    steps = args.steps
     value = steps * E * N * world / elapsed
 
     # learner: one QMIX update = PER sample (B chunks) -> C-step fwd/BPTT -> [RCCL all-reduce of the
@@ -197,8 +297,12 @@ def main():
     # the same QMIX update at SURVEY 8(d)'s throughput batch (B = 4096 chunks of C = 10), single GPU
     big = None
     if args.learner_big_steps > 0 and world == 1:
+        from minimarl.qnet import AgentQNet
         mixb, tmixb = Mixer(N, N * D, 64, 32, dev, seed=7), Mixer(N, N * D, 64, 32, dev, seed=7)
-        lb = QLearner(eng.behavior, eng.target, mixb, tmixb, batch=4096, chunk=10, mode="qmix", device=dev)
+        behb, tgtb = (AgentQNet(N, D, 5, F1, G, Hh, dev) for _ in range(2))
+        behb.copy_from(eng.behavior)
+        tgtb.copy_from(eng.target)
+        lb = QLearner(behb, tgtb, mixb, tmixb, batch=4096, chunk=10, mode="qmix", device=dev)
         lb.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=5)
         for _ in range(2):
             lb.replay_update()
@@ -211,7 +315,46 @@ def main():
         big = {"batch_chunks": 4096, "chunk": 10, "ms_per_update": round(el_b / args.learner_big_steps * 1e3, 3),
                "updates_per_s": round(args.learner_big_steps / el_b, 1),
                "chunk_samples_per_s": round(4096 * args.learner_big_steps / el_b, 1)}
-        del lb, mixb, tmixb
+        del lb, mixb, tmixb, behb, tgtb
+        torch.cuda.empty_cache()
+
+    # integrated QMIX rollout-and-learn (minimarl/train.py; vdn/main.py:127-186, qmix/main.py:172-262):
+    # per training episode 100 lockstep steps of all envs, then update_iter = 10 learner updates of
+    # B = 32 chunks (the reference's 10 updates per episode), hard target sync every 20 episodes;
+    # the replay is filled to capacity by the (untimed) epsilon = 1 warm-up
+    trainer = None
+    if args.train_episodes > 0:
+        from minimarl.config import presets
+        from minimarl.train import QTrainer
+        tcfg = presets()["cfg2"].q
+        tcfg.n_envs, tcfg.n_agents, tcfg.buffer_limit, tcfg.test_interval = E, N, cap, 0
+        tcfg.seed = 17
+        tr = QTrainer(tcfg, device=dev, rank=rank, grad_allreduce=allreduce, world=world, track_score=True)
+        if dist:
+            dist.broadcast(tr.learner.P, 0)
+            tr.eng.behavior.mark_dirty()
+            tr.eng.sync_target()
+            tr.tmix.flat.copy_(tr.mix.flat)
+        tr.warmup()
+        tr.train_episode()                       # captures the learner graphs
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el_t = tr.timed(args.train_episodes)
+        if dist:
+            dist.barrier()
+            t = torch.tensor([el_t], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_t = float(t.item())
+        k = args.train_episodes
+        trainer = {"algo": "QMIX train loop (rollout + 10 Train_dqn updates per episode + target sync)",
+                   "envs_per_gpu": E, "agents": N, "episode_steps": tcfg.max_step, "updates_per_episode":
+                   tcfg.update_iter, "batch_chunks": tcfg.batch_size, "episodes": k,
+                   "ms_per_episode": round(el_t / k * 1e3, 3),
+                   "agent_env_steps_per_s_incl_learning": round(E * N * tcfg.max_step * world * k / el_t, 1),
+                   "learner_updates_per_s": round(tcfg.update_iter * k / el_t, 1),
+                   "train_score": tr.train_score(), "grad_allreduce": "rccl" if dist else None}
+        del tr
         torch.cuda.empty_cache()
 
     # MAPPO (BASELINE configs[2]): 4096 envs x 8 agents per GPU, T=100 rollout steps with the fused
@@ -270,9 +413,8 @@ def main():
     # steps, 8 agents, QMixer with 2-layer hypernets, double Q, PER priorities
     offq = None
     if args.offq_updates > 0 and world == 1:
-        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-        from make_golden_offq import make_batch
         from minimarl.offq import OffQMix
+        from minimarl.synth import offq_episode_batch as make_batch
         oT, oB = 100, 32
         otr = OffQMix(N, D, 5, oT, oB, seed=5, device=dev)
         rng = np.random.default_rng(0)
@@ -366,24 +508,33 @@ def main():
                 "flop_per_launch": flops, "alg_bytes_per_launch": alg_bytes,
                 "hbm_frac": round(alg_bytes / t_fwd / (PEAK_HBM_GBS * 1e9), 4)}
 
-    cpu = None
+    cpu = cpu_l = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(E, N, F1, G, Hh)
+        cpu_l = cpu_learner_baseline(N, D, B=args.batch, C=10, H=Hh, Hm=64)
 
     if rank == 0:
         line = {
             "metric": "agent-env-steps/sec (4096 envs x 8 agents per GPU, QMIX GRU-64 rollout step)",
             "value": round(value, 1), "unit": "agent-env-steps/s", "n_gpus": world, "steps": steps,
-            "warmup": warm_rep * GS, "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (build's gridworld, random init)",
+            "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 (agent forward: fp16x3-split MFMA emulating f32 products, f32 accumulate)",
+            "data": "synthetic (build's gridworld, random init)",
             "config": {"workload": "QMIX 8-agent gridworld rollout, 4096 envs/GPU, GRU-64 agents, chunk 10, PER",
                        "envs_per_gpu": E, "agents": N, "obs_dim": D, "f1": F1, "gru": Hh, "chunk": 10,
+                       "per_capacity_chunks": cap, "per_prefilled_chunks": fill_chunks * E,
                        "parallelism": f"env-shard x{world}"},
+            "rccl_world_size": world,
             "learner_updates_per_s": round(upd_per_s, 1),
             "learner": {"algo": "QMIX Train_dqn update", "batch_chunks": args.batch, "chunk": 10,
                         "mixer_hidden": 64, "ms_per_update": round(el_l / args.learner_steps * 1e3, 4),
                         "updates": args.learner_steps, "grad_allreduce": "rccl" if dist else None,
-                        "reference_cpu_updates_per_s": 12.0, "throughput_batch": big},
+                        "reference_cpu_updates_per_s": 12.0,
+                        "reference_cpu_note": "reference Train_dqn.train at its own shapes (GRU-32), 8 threads of "
+                                              "the build container (BASELINE.md)",
+                        "cpu_baseline": cpu_l, "throughput_batch": big},
+            "train_loop": trainer,
             "mappo": mappo,
             "offpolicy_qmix": offq,
             "cfg5_forward": cfg5,

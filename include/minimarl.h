@@ -149,6 +149,12 @@ int mm_td_chunk_step(int64_t n_envs, int32_t n_agents, float gamma, const float*
 int mm_eval_accum(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                   const float* q_taken, const float* max_q_next, uint8_t* active, float* score, float* loss,
                   mm_stream_t s);
+/* Training score of the rollout (vdn/main.py:173, qmix/main.py:247 train score = the episode's summed
+ * reward): walks the chunk just stored in rows[e] (store rew [rows, C, N], done [rows, C]), carries the
+ * running episode return ep_ret[e] and adds each finished episode's return / count to acc[0] / acc[1]
+ * (f64). Replaces the reference's per-step Python ``score += sum(reward)``. */
+int mm_chunk_score(int64_t n_envs, int32_t chunk, int32_t n_agents, const float* store_rew,
+                   const uint8_t* store_done, const int64_t* rows, float* ep_ret, double* acc, mm_stream_t s);
 
 /* ------------------------------------------------------------------ prioritized replay */
 enum { MM_PER_VDN = 0, MM_PER_QMIX = 1 };

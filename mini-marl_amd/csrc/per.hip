@@ -445,19 +445,22 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
 // Uniform chunk replay (qmix/qmix.py:12-50 ReplayBuffer.sample_chunk draws start indices uniformly;
 // here whole stored chunks): B slots uniform over the filled slots [0, n_data), device counter RNG
 // (fresh stream per call via st->n_samples), unit IS weights; nodes_out = the slots' leaf nodes.
-__global__ void per_uniform_kernel(int64_t cap, int B, uint64_t seed, uint64_t counter, PerDev* st,
-                                   int64_t* nodes_out, int64_t* slots_out, float* is_w) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(1024) void per_uniform_kernel(int64_t cap, int B, uint64_t seed, uint64_t counter,
+                                                          PerDev* st, int64_t* nodes_out, int64_t* slots_out,
+                                                          float* is_w) {
+  // ONE workgroup: every lane reads the draw counter before the single bump below (a multi-block grid
+  // would race the bump against other blocks' reads; __syncthreads orders only this block)
   const uint64_t ctr = counter + st->n_samples;
   const int64_t n = st->n_data;
   __syncthreads();
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) st->n_samples += 1;
-  if (k >= B) return;
-  const double u = (double)(rng_draw(seed, ctr, (uint64_t)k, 91) >> 11) * (1.0 / 9007199254740992.0);
-  const int64_t slot = min(n - 1, (int64_t)(u * (double)n));
-  if (slots_out) slots_out[k] = slot;
-  if (nodes_out) nodes_out[k] = slot + cap - 1;
-  if (is_w) is_w[k] = 1.0f;
+  if (threadIdx.x == 0) st->n_samples += 1;
+  for (int k = threadIdx.x; k < B; k += blockDim.x) {
+    const double u = (double)(rng_draw(seed, ctr, (uint64_t)k, 91) >> 11) * (1.0 / 9007199254740992.0);
+    const int64_t slot = min(n - 1, (int64_t)(u * (double)n));
+    if (slots_out) slots_out[k] = slot;
+    if (nodes_out) nodes_out[k] = slot + cap - 1;
+    if (is_w) is_w[k] = 1.0f;
+  }
 }
 
 constexpr int PER_SAMPLE_MAXJ = 8;   // per_sample_kernel: batch <= PT * 8
@@ -1036,7 +1039,7 @@ int mm_per_sample_uniform(mm_per* per, int32_t batch, uint64_t seed, uint64_t co
                           float* is_w, mm_stream_t s) {
   MM_REQUIRE(per && slots_out && batch >= 1, "per_sample_uniform: bad argument");
   MM_REQUIRE(per->n_data > 0, "per_sample_uniform: empty buffer");
-  hipLaunchKernelGGL(mm::per_uniform_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)s, per->cap, batch,
+  hipLaunchKernelGGL(mm::per_uniform_kernel, dim3(1), dim3(1024), 0, (hipStream_t)s, per->cap, batch,
                      seed, counter, per->st, (int64_t*)nullptr, slots_out, is_w);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;

@@ -110,9 +110,51 @@ __global__ __launch_bounds__(256) void eval_accum_kernel(int E, int N, float gam
   if (dn) active[e] = 0;
 }
 
+// Training score of the rollout (vdn/main.py:173 train_score += sum(reward); qmix/main.py:247): one
+// thread per env walks the C steps of the chunk it just stored (row rows[e]), adds the agents' rewards
+// to the env's running episode return and, at each episode end, moves the return into acc[0] (sum of
+// finished episodes' returns) and acc[1] (their count). f64 accumulators, atomics per finished episode.
+__global__ __launch_bounds__(256) void chunk_score_kernel(int E, int C, int N, const float* __restrict__ store_rew,
+                                                          const uint8_t* __restrict__ store_done,
+                                                          const int64_t* __restrict__ rows,
+                                                          float* __restrict__ ep_ret, double* __restrict__ acc) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int64_t r = rows[e];
+  float ret = ep_ret[e];
+  double fin = 0.0, cnt = 0.0;
+  for (int c = 0; c < C; ++c) {
+    const float* rw = store_rew + (r * C + c) * N;
+    float sr = 0.f;
+    for (int j = 0; j < N; ++j) sr += rw[j];
+    ret += sr;
+    if (store_done[r * C + c]) {
+      fin += (double)ret;
+      cnt += 1.0;
+      ret = 0.f;
+    }
+  }
+  ep_ret[e] = ret;
+  if (cnt > 0.0) {
+    atomicAdd(&acc[0], fin);
+    atomicAdd(&acc[1], cnt);
+  }
+}
+
 }  // namespace mm
 
 extern "C" {
+int mm_chunk_score(int64_t n_envs, int32_t chunk, int32_t n_agents, const float* store_rew,
+                   const uint8_t* store_done, const int64_t* rows, float* ep_ret, double* acc, mm_stream_t s) {
+  MM_REQUIRE(store_rew && store_done && rows && ep_ret && acc && chunk >= 1 && n_agents >= 1,
+             "chunk_score: bad args");
+  if (n_envs <= 0) return MM_OK;
+  hipLaunchKernelGGL(mm::chunk_score_kernel, dim3((int)((n_envs + 255) / 256)), dim3(256), 0, (hipStream_t)s,
+                     (int)n_envs, chunk, n_agents, store_rew, store_done, rows, ep_ret, acc);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 int mm_eval_accum(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                   const float* q_taken, const float* max_q_next, uint8_t* active, float* score, float* loss,
                   mm_stream_t s) {

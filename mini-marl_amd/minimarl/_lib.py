@@ -180,6 +180,7 @@ _SIGS += [
                               c_vp, c_f32, c_vp]),
     ("mm_per_sample_uniform", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
     ("mm_eval_accum", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_chunk_score", c_i32, [c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 ]
 
 

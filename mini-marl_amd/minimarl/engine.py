@@ -264,8 +264,63 @@ class RolloutEngine:
         self.graph.replay()
         n = self.graph_steps()
         self.t += n
+        self._td_pending = False
         self.chunks_inserted += self.E * (n // self.C)
         self.per.n_mirror_add(self.E * (n // self.C))
+
+    def capture_steps(self):
+        """Capture one single-step HIP graph per phase of the graph cycle, so any number of steps
+        (not only whole chunks) can be replayed: ``run_steps``. Same launches as ``capture``."""
+        G = self.graph_steps()
+        self.behavior.pack()
+        self.target.pack()
+        if not self._primed:
+            self._prologue(stream_handle(self.device))
+        torch.cuda.synchronize(self.device)
+        saved = (self.t, self.chunks_inserted, self._td_pending, self._td_flushed)
+        n0 = len(self.per)
+        graphs = []
+        for ph in range(G):
+            self.t = ph
+            self._td_flushed = False
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step_launch()
+            graphs.append(g)
+        self.t, self.chunks_inserted, self._td_pending, self._td_flushed = saved
+        lib().mm_per_set_size(self.per._h, n0)
+        self.step_graphs = graphs
+        return graphs
+
+    step_graphs = None
+
+    def run_steps(self, n_steps, epsilon=None):
+        """Advance exactly ``n_steps`` lockstep steps by graph replay: whole-chunk graphs while the
+        step count is at a graph-cycle boundary, single-step graphs otherwise."""
+        if epsilon is not None:
+            self.set_epsilon(epsilon)
+        assert not self._td_flushed, "run_steps after flush_td(): continue with step() to the chunk end"
+        G = self.graph_steps()
+        left = int(n_steps)
+        while left > 0:
+            if self.t % G == 0 and left >= G:
+                self.run_graph()
+                left -= G
+                continue
+            if self.step_graphs is None:
+                self.capture_steps()
+            self.behavior.pack()
+            self.target.pack()
+            c = self.t % self.C
+            self.step_graphs[self.t % G].replay()
+            self.t += 1
+            if c == self.C - 1:
+                self.chunks_inserted += self.E
+                self.per.n_mirror_add(self.E)
+                self._td_pending = False
+            else:
+                self._td_pending = True
+            left -= 1
 
     def run(self, n_steps, epsilon):
         for _ in range(n_steps):

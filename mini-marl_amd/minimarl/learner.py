@@ -127,13 +127,19 @@ class QLearner:
         n_t = d.n_params
         n_m = mixer.n_params if mixer is not None else 0
         self.n_agent, self.n = n_t, n_t + n_m
+        for net in (behavior, mixer):
+            if net is not None and getattr(net, "_owner", None) is not None:
+                raise ValueError("this net's parameters already live in another QLearner's flat buffer; "
+                                 "give each learner its own AgentQNet / Mixer (copy_from)")
         self.P = torch.empty(self.n, device=self.dev)
         self.P[:n_t].copy_(behavior.flat)
         behavior.flat = self.P[:n_t]
+        behavior._owner = self
         behavior.mark_dirty()
         if mixer is not None:
             self.P[n_t:].copy_(mixer.flat)
             mixer.flat = self.P[n_t:]
+            mixer._owner = self
         self.Gr = torch.zeros(self.n, device=self.dev)
         self.m = torch.zeros(self.n, device=self.dev)
         self.v = torch.zeros(self.n, device=self.dev)
@@ -178,6 +184,11 @@ class QLearner:
         self.dpre2 = torch.zeros(C, B, N, self.G, **f32)
         self.dpre1 = torch.zeros(C, B, N, self.F1, **f32)
         if self.double:
+            # the double net's eps-greedy RNG counters (one per chunk step) and epsilon live on the
+            # device, so a captured update advances them on every replay (counter = update * C + t,
+            # the same values the eager path uses)
+            self.dctr = torch.arange(C, dtype=torch.int64, device=dev) - C
+            self.deps = torch.zeros(1, **f32)
             self.hd = torch.zeros(2, B, N, H, **f32)
             self.gi_ad = torch.zeros(C, B, N, 3 * H, **f32)
             self.act_d = torch.zeros(C, B, N, dtype=torch.int32, device=dev)
@@ -247,9 +258,18 @@ class QLearner:
         self._draws = (uu, ra)
 
     # ------------------------------------------------------------------ the update
+    def _push_double_eps(self):
+        if self.double and self._deps_host != self.double_eps:
+            self.deps.fill_(float(self.double_eps))
+            self._deps_host = self.double_eps
+
+    _deps_host = None
+
     def compute_grads(self, obs_base, reset_obs_ptr):
         """Forward C steps, loss, BPTT and all weight gradients into self.Gr (all async)."""
         L, s = lib(), stream_handle(self.dev)
+        if not torch.cuda.is_current_stream_capturing():
+            self._push_double_eps()
         B, C, N, H, D = self.B, self.C, self.N, self.H, self.D
         CB = C * B
         self.beh.pack(s)
@@ -284,6 +304,8 @@ class QLearner:
             check(L.mm_agent_q_pre2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pd), CB,
                                     None, None, 0, s), "learner fwd pre (double)")
         gstep = 4 * B * N * 3 * H
+        if self.double and self._draws is None:
+            self.dctr.add_(C)             # stream-ordered: captured into the update graph
         if self.seq:
             self._forward_seq(L, s, obs_p, reset_p)
         for t in range(0 if not self.seq else C, C):
@@ -318,12 +340,13 @@ class QLearner:
                 idd.act_out = self.act_d[t].data_ptr()
                 idd.qsel_out = self.qsel_d[t].data_ptr()
                 idd.epsilon = float(self.double_eps)
+                idd.eps_ptr = self.deps.data_ptr()
                 if self._draws is not None:
                     idd.u = self._draws[0][t].data_ptr()
                     idd.rand_act = self._draws[1][t].data_ptr()
                 else:
                     idd.seed = self.double_seed
-                    idd.counter = self.updates * C + t
+                    idd.counter_ptr = self.dctr.data_ptr() + 8 * t
                 check(L.mm_agent_q_rec2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
                                         ptr(self.beh.packed), ctypes.byref(idd), B, s), "learner fwd rec")
                 it.mode = MM_Q_GATHER
@@ -554,16 +577,25 @@ class QLearner:
     # ------------------------------------------------------------------ HIP graph of an update
     def capture_update(self, per, store, reset_obs_ptr, seed=0):
         """Capture [sample -> gather -> fwd/bwd] and [clip/Adam -> repack -> reprioritize] as two HIP
-        graphs (the RCCL all-reduce, when used, runs between them eagerly)."""
+        graphs (the RCCL all-reduce, when used, runs between them eagerly; its 1/world scale is baked
+        into the second graph from ``_graph_scale``). ``per=None`` captures the update of the batch
+        placed by ``load_batch`` instead (no sampling, no priority update)."""
         self.beh.pack()
         self.tgt.pack()
+        self._push_double_eps()
         torch.cuda.synchronize(self.dev)
         n0 = self.updates
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
-            self.sample_and_grads(per, store, reset_obs_ptr, seed=seed)
+            if per is None:          # the batch loaded by load_batch (tests, reference-shaped callers)
+                self.compute_grads(self._obs_ptr, self._reset_obs)
+            else:
+                self.sample_and_grads(per, store, reset_obs_ptr, seed=seed)
         with torch.cuda.graph(g2):
-            self.apply_and_reprioritize(per, self._graph_scale)
+            if per is None:
+                self.apply_grads(self._graph_scale)
+            else:
+                self.apply_and_reprioritize(per, self._graph_scale)
         self.updates = n0
         self.graphs = (g1, g2)
         return self.graphs
@@ -574,6 +606,7 @@ class QLearner:
         g1, g2 = self.graphs
         self.tgt.pack()                 # target synced since capture: repack eagerly (no-op otherwise)
         self.beh.pack()
+        self._push_double_eps()
         g1.replay()
         if allreduce is not None:
             allreduce(self.Gr)          # the 1/world scale was baked at capture (set _graph_scale first)
@@ -597,6 +630,8 @@ class QLearner:
         self.beh.mark_dirty()
         self.tgt.mark_dirty()
         self.updates = int(scalars.get("updates", 0))
+        if self.double:
+            self.dctr.copy_(torch.arange(self.C, dtype=torch.int64) + (self.updates - 1) * self.C)
 
     def sync_target(self, mixer=False):
         """target <- behavior (qmix/main.py:255-256 syncs the agent net only; mixer=True also the mixer)."""

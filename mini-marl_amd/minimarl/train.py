@@ -1,0 +1,177 @@
+"""Integrated QMIX / VDN rollout-and-learn trainer on lockstep device envs.
+
+Maps the reference's training loops (vdn/main.py:80-198, qmix/main.py:100-277) onto the device
+engine:
+
+* warm-up (vdn/main.py:80-125): epsilon = 1 rollout until the prioritized replay holds
+  ``buffer_limit`` chunks;
+* training episode ``ep`` (vdn/main.py:127-186): epsilon = max(min, max - (max - min) * ep / anneal)
+  (:133-134); ``max_step`` lockstep steps of all ``n_envs`` envs (rollout + TD priorities + chunk
+  inserts, HIP-graph replays); then ``update_iter`` learner updates (``Target_Dqn.train`` /
+  ``Train_dqn.train``, :179-180, each = PER sample -> BPTT -> clip/Adam -> reprioritize, replayed
+  HIP graphs); every ``update_target_interval`` episodes (at episode 0 too) the target AGENT net
+  is hard-synced (:184-186; QMIX keeps its target mixer, qmix/main.py:255-256); every
+  ``test_interval`` episodes greedy test episodes (``Test.execute``, :188-190) on separate envs.
+
+One lockstep "episode" advances every env by ``max_step`` steps (envs whose episode ended early
+auto-reset, so env episodes are not aligned; chunks span episode boundaries like the reference's
+global ``count_step``, :151-167). The update-to-data ratio is the reference's: ``update_iter``
+updates of ``batch_size`` chunks per ``max_step`` steps — per env-shard and rank.
+
+Data parallel: one trainer per rank on its own env shard and replay; the flat
+gradient is all-reduced (``grad_allreduce``) between the captured backward and the clip/Adam graph,
+so the replicas stay identical (rank 0's initial parameters are broadcast by the caller).
+"""
+import time
+
+import torch
+
+from ._lib import check, lib
+from .config import QTrainConfig
+from .engine import RolloutEngine
+from .evaluate import QEvaluator
+from .learner import Mixer, QLearner
+from .qnet import ptr, stream_handle
+
+
+class QTrainer:
+    def __init__(self, cfg: QTrainConfig, device="cuda", rank=0, grad_allreduce=None, world=1, track_score=True):
+        self.cfg = c = cfg
+        self.device = torch.device(device)
+        assert c.n_actions == 5, "the gridworld has 5 actions"
+        assert c.algo in ("vdn", "vdn_double", "qmix", "qmix_min")
+        if c.buffer_limit < c.n_envs:
+            raise ValueError(f"buffer_limit ({c.buffer_limit} chunks) must hold one chunk per env ({c.n_envs})")
+        per_kwargs = dict(alpha=c.alpha, beta=c.beta, eps=c.eps, step_weight=c.step_weight,
+                          use_step_weight=c.use_step_weight and c.per_flavor == "vdn",
+                          update_alpha_beta=c.update_alpha_beta, max_episodes=c.max_episodes,
+                          update_iter=c.update_iter)
+        self.eng = RolloutEngine(c.n_envs, c.n_agents, n_actions=c.n_actions, f1=c.f1, g=c.g, h=c.h,
+                                 chunk=c.chunk_size, capacity=c.buffer_limit, gamma=c.gamma, max_steps=c.max_step,
+                                 step_cost=c.step_cost, full_observable=c.full_observable,
+                                 per_flavor=c.per_flavor, per_kwargs=per_kwargs, seed=c.seed + 7919 * rank,
+                                 device=self.device)
+        eng = self.eng
+        # the behavior net's init does not depend on the rank (same seed): replicas start identical
+        eng.behavior.init_default(c.seed)
+        eng.sync_target()
+        self.mix = self.tmix = None
+        if c.algo in ("qmix", "qmix_min"):
+            S = c.n_agents * eng.D
+            self.mix = Mixer(c.n_agents, S, c.mixer_hidden, c.mixer_k1, self.device, seed=c.seed + 1)
+            self.tmix = Mixer(c.n_agents, S, c.mixer_hidden, c.mixer_k1, self.device)
+            self.tmix.flat.copy_(self.mix.flat)          # qmix/_utils.py:40-41 init sync
+        self.learner = QLearner(eng.behavior, eng.target, self.mix, self.tmix, batch=c.batch_size,
+                                chunk=c.chunk_size, gamma=c.gamma, lr=c.lr, grad_clip=c.grad_clip_norm, mode=c.algo,
+                                device=self.device)
+        self.allreduce = grad_allreduce
+        if grad_allreduce is not None:
+            self.learner._graph_scale = 1.0 / world
+        self.rank, self.world = rank, world
+        self.evaluator = None
+        if c.test_interval and c.test_envs > 0:
+            self.evaluator = QEvaluator(c.test_envs, c.n_agents, c.max_step, c.step_cost, c.full_observable,
+                                        c.gamma, device=self.device)
+        self.track_score = track_score
+        self.ep_ret = torch.zeros(c.n_envs, device=self.device)
+        self.score_acc = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self._rows = torch.empty(c.n_envs, dtype=torch.int64, device=self.device)
+        self.episode = 0
+        self.warmed = False
+        self.updates_captured = False
+        self.history = []
+
+    # ------------------------------------------------------------------ rollout
+    def _rollout(self, n_steps, epsilon):
+        """n_steps lockstep steps; whole chunks are replayed one graph at a time so each stored chunk's
+        rewards feed the training score (mm_chunk_score)."""
+        eng, C = self.eng, self.eng.C
+        eng.set_epsilon(epsilon)
+        G = eng.graph_steps()
+        left = int(n_steps)
+        while left > 0:
+            if eng.t % G == 0 and left >= G and self.track_score and G == C:
+                self._rows.copy_(eng.staging)            # rows this chunk is written into
+                eng.run_graph()
+                check(lib().mm_chunk_score(eng.E, C, eng.N, ptr(eng.store.rew), ptr(eng.store.done),
+                                           ptr(self._rows), ptr(self.ep_ret), ptr(self.score_acc),
+                                           stream_handle(self.device)), "chunk_score")
+                left -= G
+            else:
+                k = G if (eng.t % G == 0 and left >= G) else 1
+                eng.run_steps(k)
+                left -= k
+
+    def warmup(self):
+        """vdn/main.py:80-125: epsilon = 1 until the replay holds buffer_limit chunks."""
+        eng = self.eng
+        while len(eng.per) < eng.capacity:
+            self._rollout(eng.graph_steps(), 1.0)
+        self.score_acc.zero_()                          # the train score counts training episodes only
+        self.warmed = True
+
+    # ------------------------------------------------------------------ learning
+    def _capture(self):
+        eng = self.eng
+        self.learner.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=self.cfg.seed + 104729 * self.rank)
+        self.updates_captured = True
+
+    def learn(self, epsilon):
+        """``update_iter`` learner updates (Target_Dqn.train / Train_dqn.train, vdn/_train.py:56-101)."""
+        if not self.updates_captured:
+            self._capture()
+        if self.cfg.algo == "vdn_double":
+            self.learner.double_eps = epsilon if self.cfg.double_epsilon else 0.0
+        for _ in range(self.cfg.update_iter):
+            self.learner.replay_update(self.allreduce)
+
+    def train_episode(self):
+        """One training episode (vdn/main.py:127-196), no host sync."""
+        c, ep = self.cfg, self.episode
+        if not self.warmed:
+            self.warmup()
+        eps = c.epsilon(ep)
+        self._rollout(c.max_step, eps)
+        self.learn(eps)
+        if ep % c.update_target_interval == 0:
+            self.learner.sync_target(mixer=False)
+        self.episode += 1
+        return eps
+
+    def train(self, n_episodes, log=None):
+        """Run n_episodes training episodes; greedy tests every test_interval episodes (host sync)."""
+        for _ in range(int(n_episodes)):
+            eps = self.train_episode()
+            ep = self.episode - 1
+            if self.evaluator is not None and (ep + 1) % self.cfg.test_interval == 0:
+                rec = self.test()
+                rec.update(episode=ep + 1, epsilon=eps, train_score=self.train_score(reset=True),
+                           loss=float(self.learner.loss.item()), alpha=self.eng.per.alpha, beta=self.eng.per.beta)
+                self.history.append(rec)
+                if log is not None:
+                    log(rec)
+        return self.history
+
+    # ------------------------------------------------------------------ scores
+    def train_score(self, reset=False):
+        """Mean return of the training episodes finished since the last reset (None if none)."""
+        s, n = (float(x) for x in self.score_acc.cpu())
+        if reset:
+            self.score_acc.zero_()
+        return s / n if n > 0 else None
+
+    def test(self):
+        """Greedy test episodes (vdn/_test.py:22-50 score + TD^2 loss; qmix/_test.py:19-36 score)."""
+        tgt = self.eng.target if self.cfg.algo.startswith("vdn") else None
+        score, loss, _, _ = self.evaluator.run(self.eng.behavior, tgt)
+        return {"test_score": score, "test_loss": loss}
+
+    # ------------------------------------------------------------------ throughput
+    def timed(self, n_episodes):
+        """Wall time of n_episodes training episodes (rollout + learner), synchronised."""
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        for _ in range(int(n_episodes)):
+            self.train_episode()
+        torch.cuda.synchronize(self.device)
+        return time.perf_counter() - t0

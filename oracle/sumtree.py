@@ -81,8 +81,13 @@ class SumTreeOracle:
         return slots
 
     def rebuild(self):
-        for node in range(self.cap - 2, -1, -1):
-            self.tree[node] = self.tree[2 * node + 1] + self.tree[2 * node + 2]
+        """tree[i] = tree[2i+1] + tree[2i+2] bottom-up, vectorised over index ranges [a, b) whose
+        children all lie above b (2a + 1 >= b), so every range only reads finished nodes."""
+        b = self.cap - 1
+        while b > 0:
+            a = b // 2
+            self.tree[a:b] = self.tree[2 * a + 1:2 * b:2] + self.tree[2 * a + 2:2 * b + 1:2]
+            b = a
 
     def retrieve(self, s):
         """_retrieve_max (sumtree.py:26-35): iterative descent."""

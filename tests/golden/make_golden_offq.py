@@ -77,27 +77,10 @@ def target_perturbation(shapes, seed, scale=0.02):
     return {k: (rng.standard_normal(s) * scale).astype(np.float32) for k, s in shapes}
 
 
-def gen_obs(rng, shape):
-    o = (rng.random(shape) < 0.2).astype(np.float32)
-    o[..., :2] = rng.random(shape[:-1] + (2,)).astype(np.float32)
-    return o
-
-
-def make_batch(rng, N, T, B, D, A):
-    """rec_buffer sample layout: obs [N, T+1, B, D], share_obs [T+1, B, N*D] (obs_sharing =
-    concat of the agents' obs, base_runner.py:337-340), acts one-hot [N, T, B, A], rewards
-    [N, T, B, 1], dones [N, T, B, 1], dones_env [T, B, 1]; episodes end at random steps (then
-    all later steps stay done, like the runner's all-ones initialisation)."""
-    obs = gen_obs(rng, (N, T + 1, B, D))
-    share = np.transpose(obs, (1, 2, 0, 3)).reshape(T + 1, B, N * D).copy()
-    a = rng.integers(0, A, (N, T, B))
-    acts = np.eye(A, dtype=np.float32)[a]
-    rew = rng.choice(np.array([-0.01, 0.99, -1.01, 9.99, -10.01], np.float32), (N, T, B, 1))
-    end = rng.integers(T // 2, T + 2, B)          # >= T: no done inside the episode
-    t = np.arange(T)[:, None]
-    dones_env = (t >= end[None, :]).astype(np.float32)[..., None]
-    dones = np.broadcast_to(dones_env[None], (N, T, B, 1)).copy()
-    return obs, share, acts, rew, dones, dones_env
+# the synthetic batch generator lives in the package (bench.py uses it too); same draws as before
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "mini-marl_amd"))
+from minimarl.synth import gen_obs  # noqa: E402,F401
+from minimarl.synth import offq_episode_batch as make_batch  # noqa: E402
 
 
 def run_variant(m, name, mixer, double_q, use_per, huber, N=2, T=12, B=4, D=47, A=5, seed=5):

@@ -51,7 +51,7 @@ def test_qlearner_resume_is_bit_identical(tmp_path):
 
 
 def test_offq_resume_is_bit_identical(tmp_path):
-    from make_golden_offq import make_batch
+    from minimarl.synth import offq_episode_batch as make_batch
     from minimarl.checkpoint import load_checkpoint, save_checkpoint
     from minimarl.offq import OffQMix
     N, T, B, D, A = 2, 9, 6, 47, 5

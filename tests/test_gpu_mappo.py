@@ -237,3 +237,94 @@ def test_runner_episode_end_to_end():
     assert all(np.isfinite(v) for v in info.values()), info
     assert float((p.actor.flat - before).abs().max()) > 0
     assert np.all(b.obs[0].cpu().numpy() == b.obs[T].cpu().numpy())
+
+
+def _ref_layout(b, E, N):
+    """MappoBuffer [T(+1), E*N, ...] -> the reference SharedReplayBuffer layout [T(+1), E, N, ..., 1]."""
+    c = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    T1 = b.obs.shape[0]
+    d = {"obs": c(b.obs).reshape(T1, E, N, -1),
+         "rnn_states": c(b.rnn_states).reshape(T1, E, N, 1, -1),
+         "rnn_states_critic": c(b.rnn_states_critic).reshape(T1, E, N, 1, -1),
+         "actions": c(b.actions).astype(np.float32).reshape(T1 - 1, E, N, 1)}
+    for k in ("action_log_probs", "rewards"):
+        d[k] = c(getattr(b, k)).reshape(T1 - 1, E, N, 1)
+    for k in ("value_preds", "returns", "masks", "active_masks"):
+        d[k] = c(getattr(b, k)).reshape(T1, E, N, 1)
+    return d
+
+
+def test_cfg3_scale_rollout_and_epoch_gradients_vs_oracle():
+    """cfg3-scale MAPPO (512 envs x 8 agents x T = 100 = 409,600 row-steps; bench.py times 4096 envs with
+    the same kernels and the same tiled-SoA / multi-slice wgrad path) against the oracle:
+    * rollout (magym_runner.py:114-195): every step's obs / rewards / masks bit-exact vs the env oracle
+      driven with the stored actions; log-probs, values and next hiddens vs ``om.get_actions`` from the
+      device's stored input hiddens (rtol 1e-5 atol 2e-6); hiddens zeroed where the env finished;
+    * GAE + ValueNorm (shared_buffer.py:131-157) vs ``om.compute_returns`` (rtol 1e-5 atol 1e-5);
+    * PPO epoch 0 (ramppo_network.py:103-209): every gradient of actor and critic vs the oracle's
+      autograd on the full recurrent minibatch, |g - g_ref| <= 2e-3 max|g_ref| + 2e-3 |g_ref|."""
+    import ctypes
+    from minimarl._lib import lib
+    from minimarl.env import VecEnv
+    from minimarl.mappo import MappoPolicy, MappoRunner
+    from oracle.env import EnvSpec, VecEnvOracle
+    E, N, T, L = 512, 8, 100, 5
+    env = VecEnv(E, N, max_steps=100, device=DEV)
+    p = MappoPolicy(env.obs_dim, 5, 32, DEV, seed=3)
+    PA = {k: p.actor.view(k).detach().cpu().clone() for k in om.NET_KEYS}
+    PC = {k: p.critic.view(k).detach().cpu().clone() for k in om.NET_KEYS}
+    r = MappoRunner(env, p, T=T, L=L, ppo_epoch=1, seed=11)
+    r.warmup()
+    r.rollout()
+    r.compute()
+    torch.cuda.synchronize()
+    b = r.buf
+    EN = E * N
+    obs, acts = b.obs.cpu().numpy(), b.actions.cpu().numpy().astype(np.int64)
+    ha, hc = b.rnn_states.cpu(), b.rnn_states_critic.cpu()
+    masks, rew = b.masks.cpu().numpy(), b.rewards.cpu().numpy()
+    ora = VecEnvOracle(EnvSpec(N, 100), E)
+    np.testing.assert_array_equal(obs[0].reshape(E, N, -1), ora.observe())
+    for t in range(T):
+        _, rw, dn = ora.step(acts[t].reshape(E, N))
+        ora.reset_envs(dn)
+        np.testing.assert_array_equal(obs[t + 1].reshape(E, N, -1), ora.observe())
+        np.testing.assert_array_equal(rew[t].reshape(E, N), rw)
+        np.testing.assert_array_equal(masks[t + 1].reshape(E, N), np.repeat((~dn)[:, None], N, 1).astype(np.float32))
+        if t % 9 == 0 or t == T - 1:
+            v, _, lp, ha2, hc2 = om.get_actions(PA, PC, torch.from_numpy(obs[t]), ha[t], hc[t],
+                                                torch.from_numpy(masks[t]).view(-1, 1),
+                                                actions=torch.from_numpy(acts[t]).view(-1, 1))
+            np.testing.assert_allclose(b.action_log_probs[t].cpu().numpy(), lp.numpy()[:, 0], rtol=1e-5, atol=2e-6)
+            np.testing.assert_allclose(b.value_preds[t].cpu().numpy(), v.numpy()[:, 0], rtol=1e-5, atol=2e-6)
+            keep = torch.from_numpy(masks[t + 1]).view(-1, 1)
+            np.testing.assert_allclose(ha[t + 1].numpy(), (ha2 * keep).numpy(), rtol=1e-5, atol=2e-6)
+            np.testing.assert_allclose(hc[t + 1].numpy(), (hc2 * keep).numpy(), rtol=1e-5, atol=2e-6)
+    assert masks[1:].min() == 0.0          # episodes finished inside the window
+    tr = r.trainer
+    vn0 = [float(x) for x in tr.vn.cpu().numpy()]
+    data = _ref_layout(b, E, N)
+    ret_ref, _ = om.compute_returns(data["rewards"], data["value_preds"], data["masks"], data["value_preds"][T],
+                                    om.ValueNorm(*vn0), 0.99, 0.95)
+    np.testing.assert_allclose(data["returns"][:T], ret_ref[:T], rtol=1e-5, atol=1e-5)
+    # ---- PPO epoch 0 gradients through the tiled SoA forward / backward / wgrad kernels
+    tr.prepare(b)
+    L_, d = lib(), ctypes.byref(p.dims)
+    assert L_.mm_mappo_vn_update(tr.vn.data_ptr(), tr.stats.data_ptr(), 0.99999, None) == 0
+    fa, ba = tr.fwd_args(b), tr.bwd_args(b)
+    assert L_.mm_mappo_fwd(d, ctypes.byref(fa), None) == 0
+    assert L_.mm_mappo_bwd(d, ctypes.byref(ba), None) == 0
+    for n in (0, 1):
+        assert L_.mm_mappo_wgrad(d, n, tr.gsoa[n].data_ptr(), tr.rs, tr.grad[n].data_ptr(),
+                                 tr.partial.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    rec = []
+    om.ppo_train(PA, PC, data, om.ValueNorm(*vn0), 1, L, record=rec)
+    for n, (net, tag) in enumerate(((p.actor, "ga"), (p.critic, "gc"))):
+        nrm = rec[0]["na" if n == 0 else "nc"]
+        coef = min(1.0, 0.5 / (nrm + 1e-6))
+        for k in om.NET_KEYS:
+            g = net.view(k, tr.grad[n]).cpu().numpy()
+            ref = rec[0][tag][k].numpy() / coef
+            np.testing.assert_array_less(np.abs(g - ref), 2e-3 * np.abs(ref).max() + 2e-3 * np.abs(ref) + 1e-9,
+                                         err_msg=f"net {n} {k}")

@@ -111,7 +111,7 @@ def test_offq_multi_update_with_soft_target(name):
     MT = ref.mixer_from_state(tgt) if name == "qmix" else {}
     rng = np.random.default_rng(11)
     st = {}
-    from make_golden_offq import make_batch
+    from minimarl.synth import offq_episode_batch as make_batch
     for it in range(3):
         obs, share, acts, rew, dones, dones_env = make_batch(rng, meta["N"], meta["T"], meta["B"], meta["D"],
                                                              meta["A"])

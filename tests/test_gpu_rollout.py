@@ -277,3 +277,26 @@ def test_graph_replay_matches_eager():
                  (a.store.done, b.store.done), (a.h, b.h), (a.ht, b.ht), (a.cur_row, b.cur_row),
                  (a.staging, b.staging), (a.per.tree(), b.per.tree()), (a.per.slot_rows(), b.per.slot_rows())]:
         assert torch.equal(x, y)
+
+
+def test_run_steps_exact_counts_match_eager():
+    """run_steps (chunk graphs + single-step graphs, bench.py's exact W / K steps) is bit-identical
+    to eager steps, starting and stopping mid-chunk."""
+    from minimarl.engine import RolloutEngine
+    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=256, seed=13, device=DEV)
+    a = RolloutEngine(64, 8, **kw)
+    b = RolloutEngine(64, 8, **kw)
+    for _ in range(37):
+        a.step(0.3)
+    a.flush_td()
+    b.run_steps(3, 0.3)
+    b.run_steps(14, 0.3)
+    b.run_steps(20, 0.3)
+    b.flush_td()
+    torch.cuda.synchronize()
+    assert a.t == b.t == 37 and len(a.per) == len(b.per) == 192
+    for x, y in [(a.store.obs, b.store.obs), (a.store.act, b.store.act), (a.store.rew, b.store.rew),
+                 (a.store.done, b.store.done), (a.h, b.h), (a.ht, b.ht), (a.cur_row, b.cur_row),
+                 (a.staging, b.staging), (a.chunk_td, b.chunk_td), (a.per.tree(), b.per.tree()),
+                 (a.per.slot_rows(), b.per.slot_rows())]:
+        assert torch.equal(x, y)

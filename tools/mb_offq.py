@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(ROOT, "mini-marl_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-from make_golden_offq import make_batch  # noqa: E402
+from minimarl.synth import offq_episode_batch as make_batch  # noqa: E402
 from minimarl.offq import OffQMix  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 2
