@@ -51,6 +51,9 @@ class QTrainConfig:
     test_interval: int = 1
     test_envs: int = 1
     double_epsilon: bool = True         # vdn_double: the double net explores with the current epsilon
+    # True: the reference's TD target w * (sum r + N * gamma * (1-d) * Q'_tot);
+    # False: sum r + gamma * (1-d) * Q'_tot (qmix/qmix.py:215-217)
+    reference_compat: bool = True
     seed: int = 42
 
     @property

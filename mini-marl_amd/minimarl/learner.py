@@ -100,13 +100,21 @@ class QLearner:
     (qmix/qmix.py train: Huber loss, unweighted sum target, separate agent / mixer clipping)."""
 
     def __init__(self, behavior, target, mixer=None, target_mixer=None, batch=32, chunk=10, gamma=0.99, lr=1e-3,
-                 grad_clip=5.0, betas=(0.9, 0.999), adam_eps=1e-8, mode="qmix", clip_mixer=False, device="cuda"):
+                 grad_clip=5.0, betas=(0.9, 0.999), adam_eps=1e-8, mode="qmix", clip_mixer=False, device="cuda",
+                 reference_compat=True):
         assert mode in ("qmix", "vdn", "qmix_min", "vdn_double")
         self.mode = mode
         self.has_mixer = mode in ("qmix", "qmix_min")
         self.double = mode == "vdn_double"
         self.loss_flags = {"qmix": 0, "vdn": MM_LOSS_MIX_SUM, "vdn_double": MM_LOSS_MIX_SUM,
                            "qmix_min": MM_LOSS_HUBER | MM_LOSS_TARGET_SUM}[mode]
+        # reference_compat=False replaces the reference's TD target w * (sum_i r_i + N * gamma * (1-d) * Q'_tot)
+        # (SURVEY App. A 1-2, vdn/_train.py:76-77, qmix/_train.py:80-82: the bootstrap is multiplied by the
+        # agent count and the IS weight scales the target) by the textbook sum_i r_i + gamma * (1-d) * Q'_tot
+        # of qmix/qmix.py:215-217 (no IS weight)
+        self.reference_compat = bool(reference_compat)
+        if not self.reference_compat:
+            self.loss_flags |= MM_LOSS_TARGET_SUM
         # chunk-sequence launches: agent REC and mixer backward as one launch each for all C steps
         self.seq = not self.double and os.environ.get("MM_LRN_SEQ", "1") != "0"
         self.double_eps = 0.0          # epsilon of the double net's sample_action (vdn/_train.py:124-125)

@@ -63,7 +63,7 @@ class QTrainer:
             self.tmix.flat.copy_(self.mix.flat)          # qmix/_utils.py:40-41 init sync
         self.learner = QLearner(eng.behavior, eng.target, self.mix, self.tmix, batch=c.batch_size,
                                 chunk=c.chunk_size, gamma=c.gamma, lr=c.lr, grad_clip=c.grad_clip_norm, mode=c.algo,
-                                device=self.device)
+                                device=self.device, reference_compat=c.reference_compat)
         self.allreduce = grad_allreduce
         if grad_allreduce is not None:
             self.learner._graph_scale = 1.0 / world
