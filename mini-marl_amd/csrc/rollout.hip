@@ -183,7 +183,7 @@ int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const f
                           const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
                           int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
                           uint8_t* store_done, const int64_t* rows, uint64_t* counter, mm_stream_t s) {
-  MM_REQUIRE(rew && done && q_taken && max_q_next && act && chunk_td, "td_chunk_step: null argument");
+  MM_REQUIRE(rew && done && q_taken && max_q_next && (act || !store_act) && chunk_td, "td_chunk_step: null argument");
   MM_REQUIRE(step_in_chunk >= 0 && step_in_chunk < chunk_len, "td_chunk_step: bad step");
   if (n_envs <= 0) return MM_OK;
   MM_REQUIRE(n_agents >= 1 && n_agents <= 256, "td_chunk_step: n_agents must be in [1,256]");

@@ -253,17 +253,41 @@ class Q_Net:
     def __call__(self, obs, hidden):
         return self.forward(obs, hidden)
 
+    def _packed(self):
+        """The fragment image, repacked by the ``minimarl::qnet_pack`` op when the params changed."""
+        from .ops import dims, load
+        if self.net._dirty:
+            load().qnet_pack(self.net.flat, dims(self.net), self.net.packed)
+            self.net._dirty = False
+        return self.net.packed
+
     def forward(self, obs, hidden):
-        return self.net.forward(self._dev(obs), self._dev(hidden))
+        """q [B,N,A], next hidden [B,N,H] through ``torch.ops.minimarl.agent_q_fwd``."""
+        from .ops import dims, load
+        obs, hidden = self._dev(obs).contiguous(), self._dev(hidden)
+        B, N = obs.shape[0], self.num_agents
+        q = torch.empty(B, N, self.n_actions, device=self.net.device)
+        h2 = torch.empty(B, N, self.gru_hidden_size, device=self.net.device)
+        load().agent_q_fwd(self._packed(), dims(self.net), obs, hidden, h2, q)
+        return q, h2
 
     def sample_action(self, obs, hidden, epsilon):
-        obs, hidden = self._dev(obs), self._dev(hidden)
+        """qmix/_network.py:66-74 through ``torch.ops.minimarl.agent_q_act``: the row mask and random
+        actions come from the torch CPU RNG in the reference's order, so equal seeds give equal actions."""
+        from .ops import dims, load
+        obs, hidden = self._dev(obs).contiguous(), self._dev(hidden)
         B, N = obs.shape[0], self.num_agents
         u = torch.rand(size=(B,))                        # qmix/_network.py:68
         mask = u <= epsilon
         ra = torch.zeros(B, N, dtype=torch.int32)
         ra[mask] = torch.randint(low=0, high=self.n_actions, size=(int(mask.sum()), N)).int()
-        act, _, h2, q = self.net.act(obs, hidden, epsilon, u, ra)
+        dev = self.net.device
+        act = torch.empty(B, N, dtype=torch.int32, device=dev)
+        qsel = torch.empty(B, N, device=dev)
+        h2 = torch.empty(B, N, self.gru_hidden_size, device=dev)
+        q = torch.empty(B, N, self.n_actions, device=dev)
+        load().agent_q_act(self._packed(), dims(self.net), obs, hidden, float(epsilon), u.to(dev), ra.to(dev), 0, 0,
+                           h2, act, qsel, q)
         return act.float(), h2, q
 
     def init_hidden(self, batch_size=1):
