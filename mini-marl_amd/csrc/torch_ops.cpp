@@ -16,8 +16,10 @@
 //   Env.reset / Env.step         gym.make("ma_gym:Checkers-v0")       vdn/main.py:61-64,143
 //   PER.insert / sample / update Prioritized_Experience_Replay        vdn/replay_buffer/buffer.py:34-90
 #include <ATen/ATen.h>
-#include <c10/hip/HIPGuard.h>
-#include <c10/hip/HIPStream.h>
+// PyTorch-ROCm reports GPU tensors as DeviceType::CUDA; its HIP guard / stream types for such
+// devices are the "MasqueradingAsCUDA" ones
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/custom_class.h>
 #include <torch/library.h>
 
@@ -29,7 +31,7 @@
 namespace {
 
 mm_stream_t stream_of(const at::Tensor& t) {
-  return (mm_stream_t)c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  return (mm_stream_t)c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
 void ok(int rc, const char* what) { TORCH_CHECK(rc == 0, "minimarl::", what, ": ", mm_last_error()); }
@@ -67,7 +69,7 @@ void qnet_pack(const at::Tensor& params, std::vector<int64_t> dims, at::Tensor p
   TORCH_CHECK(params.numel() == offs[10], "params has ", params.numel(), " elements, the layout needs ", offs[10]);
   TORCH_CHECK(packed.numel() == mm_qnet_packed_count(&d), "packed has ", packed.numel(), " elements, needs ",
               mm_qnet_packed_count(&d));
-  const c10::hip::HIPGuard g(params.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(params.device());
   ok(mm_qnet_pack(&d, params.data_ptr<float>(), packed.data_ptr<float>(), stream_of(params)), "qnet_pack");
 }
 
@@ -122,7 +124,7 @@ void agent_q_fwd(const at::Tensor& packed, std::vector<int64_t> dims, const at::
   io.q_se = q.stride(0);
   io.q_sa = q.stride(1);
   io.mode = MM_Q_NONE;
-  const c10::hip::HIPGuard g(obs.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(obs.device());
   ok(mm_agent_q_fwd(&d, packed.data_ptr<float>(), &io, E, stream_of(obs)), "agent_q_fwd");
 }
 
@@ -158,7 +160,7 @@ void agent_q_act(const at::Tensor& packed, std::vector<int64_t> dims, const at::
   io.counter = (uint64_t)counter;
   io.act_out = act.data_ptr<int32_t>();
   io.qsel_out = q_taken.data_ptr<float>();
-  const c10::hip::HIPGuard g(obs.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(obs.device());
   ok(mm_agent_q_fwd(&d, packed.data_ptr<float>(), &io, E, stream_of(obs)), "agent_q_act");
 }
 
@@ -170,7 +172,7 @@ void agent_q_max(const at::Tensor& packed, std::vector<int64_t> dims, const at::
   en_out(max_q, E, d.n_agents, at::kFloat, obs, "max_q");
   io.mode = MM_Q_MAX;
   io.qsel_out = max_q.data_ptr<float>();
-  const c10::hip::HIPGuard g(obs.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(obs.device());
   ok(mm_agent_q_fwd(&d, packed.data_ptr<float>(), &io, E, stream_of(obs)), "agent_q_max");
 }
 
@@ -189,7 +191,7 @@ void td_error(const at::Tensor& rew, const at::Tensor& done, const at::Tensor& q
   same_device(rew, done, "done");
   same_device(rew, td, "td");
   // cal_td_error of one step = the chunk-TD kernel at step 0 of a 1-step chunk with no store writes
-  const c10::hip::HIPGuard g(rew.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(rew.device());
   ok(mm_td_chunk_step(E, (int32_t)N, (float)gamma, rew.data_ptr<float>(), done.data_ptr<uint8_t>(),
                       q_taken.data_ptr<float>(), max_q_next.data_ptr<float>(), nullptr, td.data_ptr<float>(), 0, 1,
                       nullptr, nullptr, nullptr, 0, stream_of(rew)),
@@ -210,7 +212,7 @@ void gae_scan(const at::Tensor& rewards, const at::Tensor& value_preds, const at
   }
   need(value_norm, at::kFloat, "value_norm");
   TORCH_CHECK(value_norm.numel() == 3, "value_norm = [running_mean, running_mean_sq, debiasing_term]");
-  const c10::hip::HIPGuard g(rewards.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(rewards.device());
   ok(mm_mappo_gae(rewards.data_ptr<float>(), value_preds.data_ptr<float>(), masks.data_ptr<float>(),
                   returns.data_ptr<float>(), value_norm.data_ptr<float>(), (int32_t)T, EN, (float)gamma,
                   (float)gae_lambda, stream_of(rewards)),
@@ -224,7 +226,7 @@ struct Env : torch::CustomClassHolder {
   c10::Device dev;
   Env(int64_t n_envs, int64_t n_agents, int64_t max_steps, double step_cost, bool full_observable, int64_t device)
       : E(n_envs), N(n_agents), dev(c10::DeviceType::CUDA, (c10::DeviceIndex)device) {
-    const c10::hip::HIPGuard g(dev);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(dev);
     mm_env_cfg cfg{(int32_t)n_agents, (int32_t)max_steps, full_observable ? 1 : 0, 8, (float)step_cost};
     ok(mm_env_create(&cfg, n_envs, 0, &h), "Env");
     D = mm_env_obs_dim(h);
@@ -240,7 +242,7 @@ struct Env : torch::CustomClassHolder {
   }
   void reset(at::Tensor obs) {
     check_obs(obs, "obs");
-    const c10::hip::HIPGuard g(dev);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(dev);
     ok(mm_env_reset(h, obs.data_ptr<float>(), stream_of(obs)), "Env.reset");
   }
   // next_obs: terminal next obs; obs_cur: auto-reset current obs (undefined tensor = not written)
@@ -254,7 +256,7 @@ struct Env : torch::CustomClassHolder {
     TORCH_CHECK(rew.device() == dev && rew.numel() == E * N, "rew must be float [E, N] on ", dev);
     need(done, at::kByte, "done");
     TORCH_CHECK(done.device() == dev && done.numel() == E, "done must be uint8 [E] on ", dev);
-    const c10::hip::HIPGuard g(dev);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(dev);
     ok(mm_env_step(h, act.data_ptr<int32_t>(), next_obs.data_ptr<float>(),
                    obs_cur.has_value() ? obs_cur->data_ptr<float>() : nullptr, rew.data_ptr<float>(),
                    done.data_ptr<uint8_t>(), stream_of(act)),
@@ -270,7 +272,7 @@ struct PER : torch::CustomClassHolder {
       bool use_step_weight, double alpha_inc, double beta_inc, int64_t device)
       : dev(c10::DeviceType::CUDA, (c10::DeviceIndex)device) {
     TORCH_CHECK(flavor == "vdn" || flavor == "qmix", "flavor must be 'vdn' or 'qmix'");
-    const c10::hip::HIPGuard g(dev);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(dev);
     ok(mm_per_create(capacity, flavor == "vdn" ? MM_PER_VDN : MM_PER_QMIX, alpha, beta, eps, step_weight,
                      use_step_weight ? 1 : 0, alpha_inc, beta_inc, &h),
        "PER");
@@ -287,7 +289,7 @@ struct PER : torch::CustomClassHolder {
     need(td, at::kFloat, "td");
     need(slots, at::kLong, "slots");
     TORCH_CHECK(td.device() == dev && slots.device() == dev && slots.numel() == td.numel(), "td / slots mismatch");
-    const c10::hip::HIPGuard g(dev);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(dev);
     ok(mm_per_insert(h, td.data_ptr<float>(), td.numel(), nullptr, slots.data_ptr<int64_t>(), stream_of(td)),
        "PER.insert");
   }
@@ -300,7 +302,7 @@ struct PER : torch::CustomClassHolder {
     const int64_t B = nodes.numel();
     TORCH_CHECK(slots.numel() == B && is_weight.numel() == B && nodes.device() == dev, "sample outputs mismatch");
     TORCH_CHECK(size() > 0, "PER.sample: empty replay");
-    const c10::hip::HIPGuard g(dev);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(dev);
     if (fracs.has_value()) {
       need(*fracs, at::kDouble, "fracs");
       TORCH_CHECK(fracs->numel() == B && fracs->device() == dev, "fracs must be f64 [B] on ", dev);
@@ -317,13 +319,13 @@ struct PER : torch::CustomClassHolder {
     need(nodes, at::kLong, "nodes");
     need(td, at::kFloat, "td");
     TORCH_CHECK(nodes.numel() == td.numel() && nodes.device() == dev && td.device() == dev, "nodes / td mismatch");
-    const c10::hip::HIPGuard g(dev);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(dev);
     ok(mm_per_update(h, nodes.data_ptr<int64_t>(), td.data_ptr<float>(), (int32_t)nodes.numel(), stream_of(td)),
        "PER.update");
   }
   at::Tensor tree() const {
     auto out = at::empty({2 * capacity() - 1}, at::TensorOptions().dtype(at::kDouble).device(dev));
-    const c10::hip::HIPGuard g(dev);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(dev);
     ok(mm_per_copy_tree(h, out.data_ptr<double>(), stream_of(out)), "PER.tree");
     return out;
   }

@@ -54,3 +54,18 @@ def test_invalid_dims_report_error():
     offs = (c_i64 * 11)()
     assert lib().mm_qnet_param_offsets(ctypes.byref(d), offs) < 0
     assert b"multiples of 32" in lib().mm_last_error()
+
+
+def test_torch_op_library_registers_every_op():
+    """libminimarl_torch.so (TORCH_LIBRARY(minimarl)) loads on the CPU and registers the hot-path ops
+    and the Env / PER custom classes (no GPU calls)."""
+    import torch
+    from minimarl.ops import TORCH_LIB_PATH, load
+    if not os.path.exists(TORCH_LIB_PATH):
+        pytest.skip("torch op library not built")
+    ops = load()
+    for name in ("qnet_pack", "agent_q_fwd", "agent_q_act", "agent_q_max", "td_error", "gae_scan"):
+        schema = str(getattr(ops, name).default._schema)
+        assert schema.startswith(f"minimarl::{name}("), schema
+        assert "(a!)" in schema          # outputs are caller-allocated mutable arguments
+    assert torch.classes.minimarl.Env is not None and torch.classes.minimarl.PER is not None
