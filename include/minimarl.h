@@ -130,6 +130,9 @@ int mm_env_step(mm_env* env, const int32_t* act, float* next_obs, float* obs_cur
 /* Copy out the integer state (for parity tests): pos [E,N,2] int32, grid [E,R,C] int8, steps [E],
  * apples [E]; host pointers, synchronous. */
 int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples);
+/* Restore the integer state written by mm_env_get_state (checkpoint resume; host pointers, synchronous). */
+int mm_env_set_state(mm_env* env, const int32_t* pos, const int8_t* grid, const int32_t* steps,
+                     const int32_t* apples);
 int mm_env_grid_shape(const mm_env* env, int32_t* rows, int32_t* cols);
 
 /* ------------------------------------------------------------------ TD error + chunk store */
@@ -224,6 +227,12 @@ void mm_per_set_size(mm_per* per, int64_t n);      /* host + device fill count (
 void mm_per_set_size_host(mm_per* per, int64_t n); /* host mirror only (graph-replayed inserts) */
 int mm_per_copy_tree(mm_per* per, double* dst, mm_stream_t s);
 int mm_per_copy_slot_rows(mm_per* per, int64_t* dst, mm_stream_t s);
+/* Checkpoint state of the replay: tree (device f64 [2cap-1]) and slot -> row map (device i64 [cap])
+ * copied stream-ordered; scalars[6] (host) = fill count, alpha, beta, alpha_inc, beta_inc, sample-call
+ * counter (the device RNG stream index). Both calls synchronise the stream (the scalars cross PCIe). */
+int mm_per_save_state(mm_per* per, double* tree_dst, int64_t* rows_dst, double* scalars, mm_stream_t s);
+int mm_per_load_state(mm_per* per, const double* tree_src, const int64_t* rows_src, const double* scalars,
+                      mm_stream_t s);
 
 /* ------------------------------------------------------------------ QMIX / VDN learner
  * (Train_dqn.train qmix/_train.py:19-121, Target_Dqn.train vdn/_train.py:184-235; orchestrated by
@@ -251,6 +260,15 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
  * carrying dhm. Step t reads save [C][B][MSD], qa [C][B][N], dq [C][B] and writes dqa [C][B][N],
  * delta [C][B][MDD] at the step-0 pointers + t * (per-step size); the future gradient is dropped at
  * t = C-1 (ones) and where done[t*B + b]. Bit-identical to C mm_mixer_bwd launches. */
+/* All C steps of the mixer forward for both nets in ONE launch (B < 512): block = (sample, net), the
+ * net's W_hh + hypernet weights staged once into LDS, the mixer hidden carried in LDS. Step t's arrays
+ * are at the step-0 pointers of nets[] + t * (B x width): gi [B][3Hm] (required, mm_mixer_gi), q [B][N],
+ * qtot [B], save [B][mm_mixer_save_dim]; h_out (may be NULL) is rewritten every step; step 0 starts
+ * from nets[].h_in / reset, step t >= 1 resets where reset_steps[(t-1)*B + b]. Results are
+ * bit-identical to C per-step mm_mixer_fwd launches. mm_mixer_fwd_seq_fits tells whether it applies. */
+int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1);
+int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
+                     int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s);
 int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                      const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
                      float* delta, int32_t steps, mm_stream_t s);
@@ -273,6 +291,13 @@ int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, 
 int mm_mixer_bwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                  const float* qa, const float* dq, const float* done, float* dhm, float* dqa, float* delta,
                  mm_stream_t s);
+/* All C steps of the agent BPTT chain in one launch (small batches): step t's arrays at the step-0 pointers
+ * + t x (B x N x width) (save, acts, dqa, dgi, dgh, dq); done of step t < C-1 at done + t*B, step C-1
+ * uses ones; dh carries the hidden gradient (in: zero, out: grad wrt the chunk-start hidden).
+ * Bit-identical to C per-step mm_agent_bwd launches. */
+int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B, const float* save,
+                     const int32_t* acts, const float* dqa, const float* done, const float* ones, float* dh,
+                     float* dgi, float* dgh, float* dq, int32_t steps, mm_stream_t s);
 int mm_agent_bwd(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B, const float* save,
                  const int32_t* acts, const float* dqa, const float* done, float* dh, float* dgi, float* dgh,
                  float* dq, mm_stream_t s);
@@ -446,6 +471,10 @@ int mm_offq_q_values(const mm_offq_dims* d, const float* P, const float* obs, co
                      int32_t L, int64_t R, void* ws, int64_t ws_bytes, mm_stream_t s);
 /* soft_update: target <- target * (1 - tau) + source * tau over n floats (tau = 1: hard update). */
 int mm_offq_soft_update(float* target, const float* source, int64_t n, double tau, mm_stream_t s);
+
+/* Debug: copy the first n (<= 4096) u64 slots of the timing trace buffer that kernels fill when
+ * MM_REC_TRACE=1 is set in the environment (clock64 stamps per phase; tools/trace_rec.py). */
+int mm_debug_trace(uint64_t* host_out, int32_t n);
 
 #ifdef __cplusplus
 }

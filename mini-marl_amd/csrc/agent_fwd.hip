@@ -532,6 +532,7 @@ struct RecSeq {
   int64_t gi_st, save_st, act_st, qsel_st;   // elements per step
   const uint8_t* reset;                        // step t >= 1 resets where reset[(t-1)*reset_st + e]
   int64_t reset_st;
+  uint64_t* trace;                             // timing trace (MM_REC_TRACE), nullptr normally
 };
 
 template <int F1, int G, int H, int AB>
@@ -641,6 +642,182 @@ __global__ __launch_bounds__(256, 2) void agent_rec_seq_kernel(QFwdParams p0, QF
       q_epilogue_v<AB>(p, it, agent, e, valid, qa, eps, ctr);
     }
   }
+}
+
+// Gate-parallel REC sequence (small batches): one block = one 32-env tile of one agent for all C steps,
+// 3 * HB + 1 waves: wave (g, hb) (g = r, z, n) runs only its gate's MFMA chain for hidden block hb
+// (32 MFMAs at HB = 2 instead of 96 on one wave), the r-wave of each hb combines the gates, and the
+// last wave computes the Q head + epilogue of step t while the gate waves already run step t + 1.
+// Every accumulator starts from the same value and accumulates in the same (kb, s) order as
+// agent_rec_body, so the results are bit-identical to the per-step launches.
+template <int F1, int G, int H, int AB>
+__device__ __forceinline__ void rec_seq_gp_body(const QFwdParams& p, const RecSeq& sq, int bid) {
+  const uint64_t t_entry = clock64();
+  using S = Sched<F1, G, H, AB>;
+  using CG = typename S::CG;
+  constexpr int RB2 = S::RB2, HB = S::HB;
+  __shared__ float hx[2][HB][16][64];   // new hidden blocks, double-buffered by step parity
+  __shared__ float gx[2][HB][16][64];   // z / n-hidden gate accumulators handed to the r-wave
+  // save-row staging of the r-waves: [field][feature][env] (env stride 33: conflict-free both ways), so
+  // the training save rows go out as 128-byte runs (one env's 32 features) instead of one 4-byte
+  // write per env and feature (a scattered store costs one cache-line write per lane)
+  __shared__ float svs[HB][6][32][33];
+  const int agent = bid % p.N, tile = bid / p.N;
+  const float* W = p.packed + (int64_t)agent * p.g.agent_stride;
+  const int lane = threadIdx.x & 63, hh = lane >> 5, wv = threadIdx.x >> 6;
+  const bool qwave = wv == 3 * HB;
+  const int g = qwave ? 0 : wv / HB, hb = qwave ? 0 : wv % HB;
+  const int e = tile * 32 + (lane & 31);
+  const bool valid = e < p.E;
+  const mm_qfwd_io io = p.io;
+  float fz[HB][16];
+  if (!qwave) {
+    const int base = S::NF2 + hb * S::PERHB + 3 * RB2;
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) load_frag(W + S::off(base + g * HB + kb), lane, fz[kb]);
+  }
+  const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
+  const uint64_t ctr = (io.mode == MM_Q_ACT && io.counter_ptr) ? *io.counter_ptr : io.counter;
+  // this wave's gate inputs of step t: r-wave gi_r (+ gi_n), z-wave gi_z, n-wave b_hn
+  const int dbg = p.dbg;   // timing knob (MM_REC_DBG bits): 1 no saves, 2 no Q head, 4 no gi loads
+  auto load_gi = [&](int t, f32x16& a0, f32x16& a1) {
+    if (dbg & 4) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a0[s] = a1[s] = 0.0f;
+      return;
+    }
+    const float* gi = io.gi + t * sq.gi_st + ((int64_t)(valid ? e : 0) * p.N + agent) * 3 * H;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int f = hb * 32 + kperm(s, hh);
+      a0[s] = g == 0 ? gi[f] : gi[H + f];
+      a1[s] = g == 0 ? gi[2 * H + f] : 0.0f;
+    }
+  };
+  // Q-head wave: W_q fragments and bias loaded once for the whole sequence
+  float fq[AB][HB][16];
+  f32x16 bq[AB];
+  if (qwave) {
+#pragma unroll
+    for (int ab = 0; ab < AB; ++ab) {
+      bq[ab] = load_bias(W + CG::off_bq + ab * 32, hh);
+#pragma unroll
+      for (int kb = 0; kb < HB; ++kb) load_frag(W + S::off(S::NF2 + S::NFG + ab * HB + kb), lane, fq[ab][kb]);
+    }
+  }
+  f32x16 gin0, gin1, nxt0, nxt1;
+  bool rst_next = !valid;
+  if (!qwave && g < 2) load_gi(0, gin0, gin1);
+  const f32x16 bhn = load_bias(W + CG::off_bhn + hb * 32, hh);
+  uint64_t* tr = (sq.trace && bid == 0 && lane == 0 && (wv == 0 || qwave)) ? sq.trace : nullptr;
+  if (tr && wv == 0) { tr[0] = clock64(); tr[3] = t_entry; }
+  for (int t = 0; t < sq.C; ++t) {
+    uint64_t* ts = tr ? tr + 4 + t * 8 : nullptr;
+    if (!qwave) {
+      if (ts) ts[0] = clock64();
+      if (g < 2 && t + 1 < sq.C) load_gi(t + 1, nxt0, nxt1);   // prefetch next step's inputs
+      const bool zero_h = !valid || t == 0 || rst_next;
+      if (t + 1 < sq.C && valid) rst_next = sq.reset[(int64_t)t * sq.reset_st + e] != 0;
+      f32x16 h0[HB];
+#pragma unroll
+      for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) h0[kb][s] = zero_h ? 0.0f : hx[t & 1][kb][s][lane];
+      f32x16 acc = g == 2 ? bhn : gin0;
+#pragma unroll
+      for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = mfma32(fz[kb][s], h0[kb][s], acc);
+      if (ts) ts[1] = clock64() + (uint64_t)acc[0] * 0;
+      if (g > 0) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) gx[g - 1][hb][s][lane] = acc[s];
+      }
+      lds_sync();   // A: gate accumulators visible
+      if (ts) ts[2] = clock64();
+      if (g == 0) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          float h0v = h0[0][s];
+#pragma unroll
+          for (int kb = 1; kb < HB; ++kb)
+            if (kb == hb) h0v = h0[kb][s];
+          const float r = sigmoidf_(acc[s]);
+          const float z = sigmoidf_(gx[0][hb][s][lane]);
+          const float anh = gx[1][hb][s][lane];
+          const float n = tanhf_(gin1[s] + r * anh);
+          const float h1v = n + z * (h0v - n);
+          hx[(t + 1) & 1][hb][s][lane] = h1v;
+          const int fl = kperm(s, hh), el = lane & 31;
+          svs[hb][0][fl][el] = h0v;
+          svs[hb][1][fl][el] = r;
+          svs[hb][2][fl][el] = z;
+          svs[hb][3][fl][el] = n;
+          svs[hb][4][fl][el] = anh;
+          svs[hb][5][fl][el] = h1v;
+        }
+        if (io.save && !(dbg & 1)) {
+          // lanes 0-31: env 2q, lanes 32-63: env 2q + 1; lane & 31 = feature of this hidden block
+          const int fl = lane & 31;
+#pragma unroll 4
+          for (int q = 0; q < 16; ++q) {
+            const int el = 2 * q + hh, ee = tile * 32 + el;
+            if (ee < p.E) {
+              float* row = io.save + t * sq.save_st + ((int64_t)ee * p.N + agent) * (F1 + G + 6 * H) + F1 + G +
+                           hb * 32 + fl;
+#pragma unroll
+              for (int fld = 0; fld < 6; ++fld) row[fld * H] = svs[hb][fld][fl][el];
+            }
+          }
+        }
+      }
+      if (ts) ts[3] = clock64();
+      lds_sync();   // B: new hidden of step t complete
+      if (ts) ts[4] = clock64();
+      if (g < 2) {
+        gin0 = nxt0;
+        gin1 = nxt1;
+      }
+    } else {
+      lds_sync();   // A
+      lds_sync();   // B
+      if (ts) ts[5] = clock64();
+      if (dbg & 2) continue;
+      f32x16 h1[HB];
+#pragma unroll
+      for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) h1[kb][s] = hx[(t + 1) & 1][kb][s][lane];
+      f32x16 qa[AB];
+#pragma unroll
+      for (int ab = 0; ab < AB; ++ab) {
+        qa[ab] = bq[ab];
+#pragma unroll
+        for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+          for (int s = 0; s < 16; ++s) qa[ab] = mfma32(fq[ab][kb][s], h1[kb][s], qa[ab]);
+      }
+      mm_qfwd_io it = io;
+      if (it.act_in) it.act_in += t * sq.act_st;
+      if (it.qsel_out) it.qsel_out += t * sq.qsel_st;
+      if (ts) ts[6] = clock64() + (uint64_t)qa[0][0] * 0;
+      q_epilogue_v<AB>(p, it, agent, e, valid, qa, eps, ctr);
+      if (ts) ts[7] = clock64();
+    }
+  }
+  if (tr) tr[wv == 0 ? 1 : 2] = clock64();
+}
+
+// The two nets take separate (inlined) copies of the body: each copy reads its own kernel arguments
+// directly (scalar loads), where a reference selected at run time between the two would be read
+// through a generic pointer, one vector-memory round trip per field use inside the step loop.
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(64 * (3 * (H / 32) + 1)) void agent_rec_seq_gp_kernel(QFwdParams p0, QFwdParams p1,
+                                                                                   RecSeq s0, RecSeq s1) {
+  if ((int)blockIdx.x >= p0.nblocks)
+    rec_seq_gp_body<F1, G, H, AB>(p1, s1, (int)blockIdx.x - p0.nblocks);
+  else
+    rec_seq_gp_body<F1, G, H, AB>(p0, s0, (int)blockIdx.x);
 }
 
 // One launch serves one or two nets (e.g. the target net on s'_t and the behavior net on
@@ -1279,8 +1456,19 @@ static int launch_rec_seq(QFwdParams p0, QFwdParams p1, const RecSeq& s0, const 
                           hipStream_t s) {
   p0.nblocks = (p0.E + 31) / 32 * p0.N;
   p1.nblocks = single ? 0 : (p1.E + 31) / 32 * p1.N;
-  hipLaunchKernelGGL((agent_rec_seq_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(64 * (H / 32)), 0, s,
-                     p0, p1, s0, s1);
+  // few tiles (small learner batches): gate-parallel waves shorten each step's dependent MFMA chain 3x;
+  // many tiles: the 2-wave kernel keeps more blocks per CU (MM_REC_GP=0/1 forces one, A/B)
+  const char* gp_env = getenv("MM_REC_GP");
+  static const int rdbg = getenv("MM_REC_DBG") ? atoi(getenv("MM_REC_DBG")) : 0;
+  p0.dbg = p1.dbg = rdbg;
+  const bool gp = gp_env ? gp_env[0] == '1' : (p0.nblocks + p1.nblocks) < 512;
+  if (gp) {
+    hipLaunchKernelGGL((agent_rec_seq_gp_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks),
+                       dim3(64 * (3 * (H / 32) + 1)), 0, s, p0, p1, s0, s1);
+  } else {
+    hipLaunchKernelGGL((agent_rec_seq_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(64 * (H / 32)), 0,
+                       s, p0, p1, s0, s1);
+  }
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -1309,9 +1497,11 @@ int agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_
     q.qsel_st = (int64_t)p.E * p.N;
     q.reset = reset;
     q.reset_st = p.E;
+    q.trace = nullptr;
     return q;
   };
-  const RecSeq s0 = mk(p0), s1 = mk(p1);
+  RecSeq s0 = mk(p0), s1 = mk(p1);
+  s0.trace = debug_trace_buffer("MM_REC_TRACE");
   const int AB = (d->n_actions + 31) / 32;
 #define MM_RSEQ(F1_, G_, H_)                                                                                    \
   if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                                 \

@@ -50,6 +50,31 @@ __device__ __forceinline__ uint64_t rng_draw(uint64_t seed, uint64_t counter, ui
 }
 __device__ __forceinline__ float rng_uniform(uint64_t r) { return (float)(r >> 40) * (1.0f / 16777216.0f); }
 
+// Debug timing traces: a static device buffer of 4096 u64 slots, allocated when the named
+// environment variable is set (kernels record clock64() into it); mm_debug_trace copies it out.
+uint64_t* debug_trace_buffer(const char* env_name);
+
+// Workgroup barrier that orders LDS only: waits for this wave's outstanding LDS operations, then
+// s_barrier. Unlike __syncthreads() it does not wait for outstanding global stores, so a sequence
+// kernel whose waves communicate through LDS does not stall every step on its own result writes.
+// Only for kernels that never read, within the launch, global data written by another wave.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// acc = sum_k w[k * ws] * x[k] in sequential k order (fma chain), fully unrolled for the common widths
+// so every load is in flight before the chain starts; same result as the plain loop.
+template <int K>
+__device__ __forceinline__ float dot_seq(const float* w, const float* x, float acc) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc += w[k] * x[k];
+  return acc;
+}
+__device__ __forceinline__ float dot_seq_n(const float* w, const float* x, int K, float acc) {
+  if (K == 64) return dot_seq<64>(w, x, acc);
+  if (K == 32) return dot_seq<32>(w, x, acc);
+  for (int k = 0; k < K; ++k) acc += w[k] * x[k];
+  return acc;
+}
+
 }  // namespace mm
 
 #define MM_HIP_CHECK(expr)                                                     \

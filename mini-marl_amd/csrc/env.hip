@@ -540,4 +540,22 @@ int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, in
   if (apples && hipMemcpy(apples, d.apples, (size_t)d.E * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
   return MM_OK;
 }
+
+int mm_env_set_state(mm_env* env, const int32_t* pos, const int8_t* grid, const int32_t* steps,
+                     const int32_t* apples) {
+  MM_REQUIRE(env && pos && grid && steps && apples, "env_set_state: null argument");
+  const mm::EnvDev& d = env->d;
+  std::vector<int32_t> p((size_t)d.E * d.N);
+  for (size_t i = 0; i < p.size(); ++i) {
+    MM_REQUIRE(pos[2 * i] >= 0 && pos[2 * i] < d.R && pos[2 * i + 1] >= 0 && pos[2 * i + 1] < d.C,
+               "env_set_state: position out of the grid");
+    p[i] = (pos[2 * i] << 8) | pos[2 * i + 1];
+  }
+  MM_HIP_CHECK(hipDeviceSynchronize());
+  MM_HIP_CHECK(hipMemcpy(d.pos, p.data(), p.size() * 4, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(d.grid, grid, (size_t)d.E * d.R * d.C, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(d.steps, steps, (size_t)d.E * 4, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(d.apples, apples, (size_t)d.E * 4, hipMemcpyHostToDevice));
+  return MM_OK;
+}
 }

@@ -465,6 +465,184 @@ __global__ __launch_bounds__(256) void mixer_fwd_multi_kernel(MixFwdArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ mixer sequences with LDS-resident weights
+// Small batches (B < 512): one block per (sample, net) runs ALL C steps of the mixer forward (or
+// backward) in one launch, with the net's W_hh and hypernet weights staged ONCE into LDS (row
+// stride Hm + 1: conflict-free for both the row-per-lane forward and the column-per-lane transposed
+// backward) and the recurrent state carried in LDS between steps. Per-step arithmetic and summation
+// order are exactly mixer_fwd_body / mixer_bwd_body's (bit-identical to the per-step launches).
+// Image rows: [W_hh (3Hm) | w1W (N*K1) | b1W (K1) | w2W (K1) | b2aW (K1)] = the forward's hypernet
+// row order after W_hh.
+struct MixSeqGeo {
+  int Hm, K1, N, NK, RW, ld, rows;
+  __host__ __device__ MixSeqGeo(int Hm_, int K1_, int N_)
+      : Hm(Hm_), K1(K1_), N(N_), NK(N_ * K1_), RW(N_ * K1_ + 3 * K1_), ld(Hm_ + 1), rows(3 * Hm_ + N_ * K1_ + 3 * K1_) {}
+  __host__ __device__ size_t img() const { return (size_t)rows * ld; }
+  // biases staged with the image: b_hh [3Hm] | hypernet biases [RW] | b2 output weights [K1] + bias [1]
+  __host__ __device__ size_t bias() const { return (size_t)3 * Hm + RW + K1 + 1; }
+  // forward scratch: h0, gi, gh, h1, hyp, yp, q (N), reset flag
+  __host__ __device__ size_t fwd_floats() const { return img() + bias() + 8 * Hm + RW + K1 + N + 4; }
+  // backward scratch: dhm, dhm1, dgh, shd, red, 2 x prefetched step inputs (save row + qa + dq + done)
+  __host__ __device__ size_t step_in() const { return (size_t)mix_save_dim(Hm, K1, N) + N + 2; }
+  __host__ __device__ size_t bwd_floats() const { return img() + bias() + 5 * Hm + RW + 4 * Hm + 2 * step_in(); }
+};
+
+__device__ __forceinline__ const float* mixer_image_row(const float* __restrict__ P, const MixOff& o, const MixSeqGeo& g,
+                                                        int r) {
+  const int M3 = 3 * g.Hm;
+  if (r < M3) return P + o.gWhh + (int64_t)r * g.Hm;
+  if (r < M3 + g.NK) return P + o.w1W + (int64_t)(r - M3) * g.Hm;
+  if (r < M3 + g.NK + g.K1) return P + o.b1W + (int64_t)(r - M3 - g.NK) * g.Hm;
+  if (r < M3 + g.NK + 2 * g.K1) return P + o.w2W + (int64_t)(r - M3 - g.NK - g.K1) * g.Hm;
+  return P + o.b2aW + (int64_t)(r - M3 - g.NK - 2 * g.K1) * g.Hm;
+}
+
+// One wave copies one row at a time (lane = column): every wave keeps 32 rows' loads in flight before
+// the LDS stores, so the staging costs ~rows / (32 * waves) memory round trips, not one per element.
+__device__ void stage_mixer_image(const float* __restrict__ P, const MixOff& o, const MixSeqGeo& g, float* img) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const bool on = lane < g.Hm;
+  for (int r0 = w * 32; r0 < g.rows; r0 += nw * 32) {
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int r = r0 + j;
+      v[j] = (on && r < g.rows) ? mixer_image_row(P, o, g, r)[lane] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (on && r0 + j < g.rows) img[(r0 + j) * g.ld + lane] = v[j];
+  }
+  __syncthreads();
+}
+
+__device__ void stage_mixer_bias(const float* __restrict__ P, const MixOff& o, const MixSeqGeo& g, float* bs) {
+  const int M3 = 3 * g.Hm, NK = g.NK, K1 = g.K1;
+  for (int i = threadIdx.x; i < (int)g.bias(); i += blockDim.x) {
+    float v;
+    if (i < M3) v = P[o.gbhh + i];
+    else if (i < M3 + NK) v = P[o.w1b + i - M3];
+    else if (i < M3 + NK + K1) v = P[o.b1b + i - M3 - NK];
+    else if (i < M3 + NK + 2 * K1) v = P[o.w2b + i - M3 - NK - K1];
+    else if (i < M3 + NK + 3 * K1) v = P[o.b2ab + i - M3 - NK - 2 * K1];
+    else if (i < M3 + NK + 4 * K1) v = P[o.b2bW + i - M3 - NK - 3 * K1];
+    else v = P[o.b2bb];
+    bs[i] = v;
+  }
+}
+
+struct MixFwdSeq {
+  int C;
+  int64_t gi_st, q_st, qtot_st, save_st, hout_st;
+  const uint8_t* reset_steps;  // [C-1][B]: reset flags of steps t >= 1 (step 0 uses net.reset / h_in)
+};
+
+__device__ __forceinline__ void mixer_fwd_seq_body(const MixFwdArgs& a, const MixFwdNet& nt, const MixFwdSeq& sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x;
+  const int S = a.S, Hm = a.Hm, K1 = a.K1, N = a.N;
+  const MixOff o = mix_offsets(S, Hm, K1, N);
+  const MixSeqGeo g(Hm, K1, N);
+  const int NK = g.NK, RW = g.RW, ld = g.ld, M3 = 3 * Hm;
+  float* img = sm;
+  float* bs = img + g.img();   // biases (stage_mixer_bias)
+  float* h0 = bs + g.bias();   // [Hm]
+  float* gi = h0 + Hm;         // [3Hm] this step's input projection
+  float* gh = gi + 3 * Hm;     // [3Hm]
+  float* h1 = gh + 3 * Hm;     // [Hm]
+  float* hyp = h1 + Hm;        // [RW]
+  float* yp = hyp + RW;        // [K1]
+  float* qs = yp + K1;         // [N] this step's agent values
+  float* rst = qs + N;         // [1] reset flag of the next step
+  stage_mixer_image(nt.P, o, g, img);
+  stage_mixer_bias(nt.P, o, g, bs);
+  const float* b_hh = bs;
+  const float* b_hy = bs + M3;
+  const float* b2w = bs + M3 + RW;
+  const int svd = mix_save_dim(Hm, K1, N);
+  {
+    const bool rz = !nt.h_in || (nt.reset && nt.reset[b]);
+    for (int i = threadIdx.x; i < Hm; i += blockDim.x) h0[i] = rz ? 0.f : nt.h_in[(int64_t)b * Hm + i];
+    for (int i = threadIdx.x; i < M3; i += blockDim.x) gi[i] = nt.gi[(int64_t)b * M3 + i];
+    for (int i = threadIdx.x; i < N; i += blockDim.x) qs[i] = nt.q[(int64_t)b * N + i];
+  }
+  __syncthreads();
+  for (int t = 0; t < sq.C; ++t) {
+    // prefetch step t+1's inputs into registers (written to LDS after their last use in step t)
+    const bool more = t + 1 < sq.C;
+    const int ti = (int)threadIdx.x;
+    const float g_nx = (more && ti < M3) ? nt.gi[(t + 1) * sq.gi_st + (int64_t)b * M3 + ti] : 0.f;
+    const float q_nx = (more && ti < N) ? nt.q[(t + 1) * sq.q_st + (int64_t)b * N + ti] : 0.f;
+    const float r_nx = (more && ti == 0) ? (sq.reset_steps[(int64_t)t * a.B + b] != 0 ? 1.f : 0.f) : 0.f;
+    // gh = W_hh h0 + b_hh (block_matvec order: sequential k, bias last)
+    for (int r = threadIdx.x; r < M3; r += blockDim.x) gh[r] = dot_seq_n(img + r * ld, h0, Hm, 0.f) + b_hh[r];
+    lds_sync();
+    float* sv = nt.save ? nt.save + t * sq.save_st + (int64_t)b * svd : nullptr;
+    float* hout = nt.h_out ? nt.h_out + t * sq.hout_st : nullptr;
+    for (int i = threadIdx.x; i < Hm; i += blockDim.x) {
+      const float r = sigmoidf_(gi[i] + gh[i]);
+      const float z = sigmoidf_(gi[Hm + i] + gh[Hm + i]);
+      const float n = tanhf_(gi[2 * Hm + i] + r * gh[2 * Hm + i]);
+      const float hv = n + z * (h0[i] - n);
+      h1[i] = hv;
+      if (hout) hout[(int64_t)b * Hm + i] = hv;
+      if (sv) {
+        sv[i] = h0[i];
+        sv[Hm + i] = r;
+        sv[2 * Hm + i] = z;
+        sv[3 * Hm + i] = n;
+        sv[4 * Hm + i] = gh[2 * Hm + i];
+        sv[5 * Hm + i] = hv;
+      }
+    }
+    lds_sync();
+    // hypernets on h1 (rows w1 [NK] | b1 [K1] | w2 [K1] | b2 hidden [K1]), each row's bias last
+    for (int r = threadIdx.x; r < RW; r += blockDim.x) hyp[r] = dot_seq_n(img + (M3 + r) * ld, h1, Hm, 0.f) + b_hy[r];
+    lds_sync();
+    for (int k = threadIdx.x; k < K1; k += blockDim.x) {
+      float acc = 0.f;
+      for (int i = 0; i < N; ++i) acc += fabsf(hyp[k * N + i]) * qs[i];
+      yp[k] = acc + hyp[NK + k];
+    }
+    lds_sync();
+    if (threadIdx.x == 0) {
+      const float* w2raw = hyp + NK + K1;
+      const float* b2pre = hyp + NK + 2 * K1;
+      float b2 = 0.f;
+      for (int k = 0; k < K1; ++k) b2 += b2w[k] * fmaxf(b2pre[k], 0.f);
+      b2 += b2w[K1];
+      float acc = 0.f;
+      for (int k = 0; k < K1; ++k) acc += fabsf(w2raw[k]) * fmaxf(yp[k], 0.f);
+      nt.qtot[t * sq.qtot_st + b] = acc + b2;
+      if (sv) sv[6 * Hm + NK + 4 * K1] = b2;
+    }
+    if (sv) {
+      for (int i = threadIdx.x; i < RW; i += blockDim.x) sv[6 * Hm + i] = i >= NK + 2 * K1 ? fmaxf(hyp[i], 0.f) : hyp[i];
+      for (int k = threadIdx.x; k < K1; k += blockDim.x) sv[6 * Hm + NK + 3 * K1 + k] = yp[k];
+    }
+    // next step's inputs (gi / q were last read above); h0 <- h1 unless the next step resets
+    if (more) {
+      if (ti < M3) gi[ti] = g_nx;
+      if (ti < N) qs[ti] = q_nx;
+      if (ti == 0) rst[0] = r_nx;
+    }
+    lds_sync();
+    if (more) {
+      const bool rz = rst[0] != 0.f;
+      for (int i = threadIdx.x; i < Hm; i += blockDim.x) h0[i] = rz ? 0.f : h1[i];
+    }
+    lds_sync();
+  }
+}
+
+// one inlined body per net: each reads its own kernel-argument fields with scalar loads
+__global__ __launch_bounds__(256) void mixer_fwd_seq_lds_kernel(MixFwdArgs a, MixFwdSeq sq) {
+  if (blockIdx.y == 0)
+    mixer_fwd_seq_body(a, a.net[0], sq);
+  else
+    mixer_fwd_seq_body(a, a.net[1], sq);
+}
+
 // ------------------------------------------------------------------ loss (all steps at once)
 // y = w * sum_i (r_i + gamma*(1-d)*Q'tot)   (qmix/_train.py:80-82, vdn/_train.py:76-77)
 // dQtot = 2 (Qtot - y) / B ;  loss = sum_t mean_b (y - Qtot)^2 ;  td = |y - Qtot| at t = C-1.
@@ -838,6 +1016,170 @@ __global__ __launch_bounds__(256) void mixer_bwd_seq_multi_kernel(MixBwdArgs a0,
   }
 }
 
+// block_matvec_t over an LDS row-major image with row stride ld (same partial-sum order).
+__device__ void block_matvec_t_ld(const float* W, int ld, int rows, int K, const float* d, float* out, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int c = lane; c < K; c += 64) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = w;
+#pragma unroll 4
+    for (; r + 3 * nw < rows; r += 4 * nw) {
+      a0 += W[r * ld + c] * d[r];
+      a1 += W[(r + nw) * ld + c] * d[r + nw];
+      a2 += W[(r + 2 * nw) * ld + c] * d[r + 2 * nw];
+      a3 += W[(r + 3 * nw) * ld + c] * d[r + 3 * nw];
+    }
+    for (; r < rows; r += nw) a0 += W[r * ld + c] * d[r];
+    red[w * K + c] = (a0 + a1) + (a2 + a3);
+  }
+  lds_sync();
+  for (int c = threadIdx.x; c < K; c += blockDim.x) {
+    float acc = 0.f;
+    for (int q = 0; q < nw; ++q) acc += red[q * K + c];
+    out[c] = out[c] + acc;
+  }
+  lds_sync();
+}
+
+__global__ __launch_bounds__(256) void mixer_bwd_seq_lds_kernel(MixBwdArgs a, MixBwdSeq sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int b = blockIdx.x;
+  const int Hm = a.Hm, K1 = a.K1, N = a.N;
+  const MixOff o = mix_offsets(a.S, Hm, K1, N);
+  const MixSeqGeo g(Hm, K1, N);
+  const int NK = g.NK, ld = g.ld, M3 = 3 * Hm;
+  const int svd = mix_save_dim(Hm, K1, N), dld = mix_delta_dim(Hm, K1, N), SI = (int)g.step_in();
+  float* img = sm;
+  float* bs = img + g.img();
+  float* dhm = bs + g.bias();   // [Hm] carried: grad wrt hm1 of step t (from step t+1)
+  float* dhm1 = dhm + Hm;       // [Hm]
+  float* dgh = dhm1 + Hm;       // [3Hm]
+  float* shd = dgh + 3 * Hm;    // [RW]
+  float* red = shd + g.RW;      // [4][Hm]
+  float* inb = red + 4 * Hm;    // [2][SI]: step inputs (save row | qa [N] | dQ | done), double-buffered
+  const float* b2w = bs + M3 + g.RW;
+  stage_mixer_image(a.P, o, g, img);
+  stage_mixer_bias(a.P, o, g, bs);
+  const int ti = (int)threadIdx.x;
+  auto step_ptr = [&](int t, int i) -> float {   // element i of step t's input block (global)
+    if (i < svd) return a.save[t * sq.save_st + (int64_t)b * svd + i];
+    i -= svd;
+    if (i < N) return a.qa[t * sq.qa_st + (int64_t)b * N + i];
+    if (i == N) return a.dq[t * sq.dq_st + b];
+    const float* done = t == sq.C - 1 ? sq.ones : a.done + t * sq.done_st;
+    return done[b];
+  };
+  for (int i = ti; i < SI; i += blockDim.x) inb[((sq.C - 1) & 1) * SI + i] = step_ptr(sq.C - 1, i);
+  for (int c = ti; c < Hm; c += blockDim.x) dhm[c] = a.dhm[(int64_t)b * Hm + c];
+  __syncthreads();
+  for (int t = sq.C - 1; t >= 0; --t) {
+    // prefetch step t-1's inputs into registers (stored to the other buffer at the end of the step)
+    float nx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = ti + j * 256;
+      nx[j] = (t > 0 && i < SI) ? step_ptr(t - 1, i) : 0.f;
+    }
+    const float* sv = inb + (t & 1) * SI;
+    const float* qa = sv + svd;
+    const float dQ = qa[N];
+    const float done_b = qa[N + 1];
+    float* dqa = a.dqa + t * sq.dqa_st;
+    float* dl = a.delta + t * sq.delta_st + (int64_t)b * dld;
+    const float* hm0 = sv;
+    const float* rg = sv + Hm;
+    const float* zg = sv + 2 * Hm;
+    const float* ng = sv + 3 * Hm;
+    const float* anh = sv + 4 * Hm;
+    const float* w1raw = sv + 6 * Hm;
+    const float* w2raw = w1raw + NK + K1;
+    const float* b2pre = w2raw + K1;
+    const float* ypre = b2pre + K1;
+    float* d_w1 = dl + 6 * Hm;
+    float* d_b1 = d_w1 + NK;
+    float* d_w2 = d_b1 + K1;
+    float* d_b2pre = d_w2 + K1;
+    for (int k = ti; k < K1; k += blockDim.x) {
+      const float y = fmaxf(ypre[k], 0.f);
+      const float w2 = w2raw[k];
+      const float dw2 = dQ * y * (w2 > 0.f ? 1.f : (w2 < 0.f ? -1.f : 0.f));
+      const float dyp = ypre[k] > 0.f ? dQ * fabsf(w2) : 0.f;
+      const float db2p = b2pre[k] > 0.f ? dQ * b2w[k] : 0.f;
+      d_b1[k] = dyp;
+      d_w2[k] = dw2;
+      d_b2pre[k] = db2p;
+      shd[NK + k] = dyp;
+      shd[NK + K1 + k] = dw2;
+      shd[NK + 2 * K1 + k] = db2p;
+      for (int i = 0; i < N; ++i) {
+        const float w = w1raw[k * N + i];
+        const float dw1 = dyp * qa[i] * (w > 0.f ? 1.f : (w < 0.f ? -1.f : 0.f));
+        d_w1[k * N + i] = dw1;
+        shd[k * N + i] = dw1;
+      }
+    }
+    if (ti == 0) dl[6 * Hm + NK + 3 * K1] = dQ;
+    lds_sync();
+    for (int i = ti; i < N; i += blockDim.x) {
+      float acc = 0.f;
+      for (int k = 0; k < K1; ++k) acc += shd[NK + k] * fabsf(w1raw[k * N + i]);
+      dqa[(int64_t)b * N + i] = acc;
+    }
+    const bool drop = done_b > 0.5f;
+    for (int c = ti; c < Hm; c += blockDim.x) dhm1[c] = drop ? 0.f : dhm[c];
+    lds_sync();
+    block_matvec_t_ld(img + M3 * ld, ld, NK, Hm, shd, dhm1, red);
+    block_matvec_t_ld(img + (M3 + NK) * ld, ld, K1, Hm, shd + NK, dhm1, red);
+    block_matvec_t_ld(img + (M3 + NK + K1) * ld, ld, K1, Hm, shd + NK + K1, dhm1, red);
+    block_matvec_t_ld(img + (M3 + NK + 2 * K1) * ld, ld, K1, Hm, shd + NK + 2 * K1, dhm1, red);
+    for (int i = ti; i < Hm; i += blockDim.x) {
+      const float dh = dhm1[i];
+      const float r = rg[i], z = zg[i], n = ng[i];
+      const float dn = dh * (1.f - z);
+      const float dz = dh * (hm0[i] - n);
+      const float dpn = dn * (1.f - n * n);
+      const float dr = dpn * anh[i];
+      const float dar = dr * r * (1.f - r);
+      const float daz = dz * z * (1.f - z);
+      dl[i] = dar;
+      dl[Hm + i] = daz;
+      dl[2 * Hm + i] = dpn;
+      dl[3 * Hm + i] = dar;
+      dl[4 * Hm + i] = daz;
+      dl[5 * Hm + i] = dpn * r;
+      dgh[i] = dar;
+      dgh[Hm + i] = daz;
+      dgh[2 * Hm + i] = dpn * r;
+    }
+    lds_sync();
+    for (int c = ti; c < Hm; c += blockDim.x) shd[c] = dhm1[c] * zg[c];
+    lds_sync();
+    block_matvec_t_ld(img, ld, M3, Hm, dgh, shd, red);
+    for (int c = ti; c < Hm; c += blockDim.x) dhm[c] = shd[c];
+    if (t > 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = ti + j * 256;
+        if (i < SI) inb[((t - 1) & 1) * SI + i] = nx[j];
+      }
+    }
+    lds_sync();
+  }
+  for (int c = ti; c < Hm; c += blockDim.x) a.dhm[(int64_t)b * Hm + c] = dhm[c];
+}
+
+// dynamic-LDS limit of the sequence kernels (MI355X: 160 KB per CU, one block per CU)
+constexpr size_t kMixSeqLds = 160 * 1024;
+static int mix_seq_lds_setup() {
+  static bool done = false;
+  if (done) return MM_OK;
+  MM_HIP_CHECK(hipFuncSetAttribute((const void*)mixer_fwd_seq_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kMixSeqLds));
+  MM_HIP_CHECK(hipFuncSetAttribute((const void*)mixer_bwd_seq_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kMixSeqLds));
+  done = true;
+  return MM_OK;
+}
 // ------------------------------------------------------------------ agent backward chain (one step)
 struct AgentBwdArgs {
   const float* P;            // behavior agent params (canonical flat)
@@ -904,6 +1246,111 @@ __device__ __forceinline__ void agent_bwd_body(const AgentBwdArgs& a) {
     for (int r = 0; r < 3 * H; ++r) acc += Whh[(int64_t)r * H + f] * sdg[w][r];
     a.dh[(int64_t)pair * H + f] = acc;
   }
+}
+
+// Chunk-sequence agent backward (small batches): block = one agent x 4 samples (one wave each, lane =
+// hidden feature) for ALL C steps, the agent's W_hh staged once into LDS (48 KB at H = 64) and the
+// hidden-state gradient carried in registers between steps. Per-step arithmetic and summation order
+// are agent_bwd_body's (bit-identical to the per-step launches).
+struct AgentBwdSeq {
+  int C;
+  int64_t save_st, acts_st, dqa_st, dgi_st, dq_st, done_st;
+  const float* ones;
+};
+__global__ __launch_bounds__(256) void agent_bwd_seq_kernel(AgentBwdArgs a, AgentBwdSeq sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int H = a.H, A = a.A, H3 = 3 * H;
+  float* whh = sm;                 // [3H][H]
+  float* sdg = whh + H3 * H;       // [4][3H]
+  float* wq = sdg + 4 * H3;        // [A][H]
+  const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
+  const int i = blockIdx.y;
+  const int b = blockIdx.x * 4 + w;
+  const bool on = b < a.B && f < H;
+  const int64_t pair = (int64_t)(b < a.B ? b : 0) * a.N + i;
+  const int SD = a.F1 + a.G + 6 * H;
+  const float* Wq_g = a.P + a.oWq + (int64_t)i * A * H;
+  for (int idx = threadIdx.x; idx < A * H; idx += blockDim.x) wq[idx] = Wq_g[idx];
+  const float* Whh = a.P + a.oWhh + (int64_t)i * H3 * H;
+  for (int q0 = threadIdx.x; q0 < H3 * H / 4; q0 += 8 * blockDim.x) {   // 8 float4 loads in flight
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int q = q0 + j * blockDim.x;
+      v[j] = q < H3 * H / 4 ? reinterpret_cast<const float4*>(Whh)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int q = q0 + j * blockDim.x;
+      if (q < H3 * H / 4) reinterpret_cast<float4*>(whh)[q] = v[j];
+    }
+  }
+  float dh = on ? a.dh[pair * H + f] : 0.f;
+  // step inputs, prefetched one step ahead: h0 / r / z / n / anh of this lane's feature, action,
+  // dQ(a), done flag
+  struct In { float h0, r, z, n, anh, dqa, done; int act; };
+  auto load_in = [&](int t) {
+    In x{};
+    if (b < a.B) {
+      const float* h0 = a.save + t * sq.save_st + pair * SD + a.F1 + a.G;
+      const float* done = t == sq.C - 1 ? sq.ones : a.done + t * sq.done_st;
+      x.act = a.acts[t * sq.acts_st + pair];
+      x.dqa = a.dqa[t * sq.dqa_st + pair];
+      x.done = done[b];
+      if (f < H) {
+        x.h0 = h0[f];
+        x.r = h0[H + f];
+        x.z = h0[2 * H + f];
+        x.n = h0[3 * H + f];
+        x.anh = h0[4 * H + f];
+      }
+    }
+    return x;
+  };
+  In cur = load_in(sq.C - 1);
+  __syncthreads();   // the W_hh / W_q images (global -> LDS) visible
+  for (int t = sq.C - 1; t >= 0; --t) {
+    const In nxt = t > 0 ? load_in(t - 1) : In{};
+    float stash = 0.f;
+    if (b < a.B) {
+      const int act = cur.act;
+      const float dqa = cur.dqa;
+      if (f < A) a.dq[t * sq.dq_st + pair * A + f] = (f == act) ? dqa : 0.f;
+      if (f < H) {
+        const bool drop = cur.done > 0.5f;
+        const float dh1 = wq[act * H + f] * dqa + (drop ? 0.f : dh);
+        const float r = cur.r, z = cur.z, n = cur.n, anh = cur.anh;
+        const float dn = dh1 * (1.f - z);
+        const float dz = dh1 * (cur.h0 - n);
+        const float dpn = dn * (1.f - n * n);
+        const float dar = dpn * anh * r * (1.f - r);
+        const float daz = dz * z * (1.f - z);
+        float* gi = a.dgi + t * sq.dgi_st + pair * H3;
+        float* gh = a.dgh + t * sq.dgi_st + pair * H3;
+        gi[f] = dar;
+        gi[H + f] = daz;
+        gi[2 * H + f] = dpn;
+        gh[f] = dar;
+        gh[H + f] = daz;
+        gh[2 * H + f] = dpn * r;
+        sdg[w * H3 + f] = dar;
+        sdg[w * H3 + H + f] = daz;
+        sdg[w * H3 + 2 * H + f] = dpn * r;
+        stash = dh1 * z;
+      }
+    }
+
+    lds_sync();        // sdg visible
+    if (on) {
+      float acc = stash;
+#pragma unroll 16
+      for (int r = 0; r < H3; ++r) acc += whh[r * H + f] * sdg[w * H3 + r];
+      dh = acc;
+    }
+    cur = nxt;
+    lds_sync();        // sdg reads done before the next step overwrites it
+  }
+  if (on) a.dh[pair * H + f] = dh;
 }
 
 // Large-batch variant (H <= 64): one block = one agent x 32 samples, one wave = 8 samples of that
@@ -1451,8 +1898,60 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
     MM_HIP_CHECK(hipGetLastError());
     return MM_OK;
   }
+  const mm::MixSeqGeo g(Hm, K1, N);
+  const char* lds_env = getenv("MM_MIX_LDS");   // "0" forces the L2-streamed kernel (A/B, tests)
+  if (g.bwd_floats() * 4 <= mm::kMixSeqLds && g.step_in() <= 1024 && !(lds_env && lds_env[0] == '0')) {
+    const int rc = mm::mix_seq_lds_setup();
+    if (rc) return rc;
+    hipLaunchKernelGGL(mm::mixer_bwd_seq_lds_kernel, dim3(B), dim3(256), g.bwd_floats() * 4, (hipStream_t)s, a, q);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   const size_t sm = sizeof(float) * ((size_t)8 * Hm + N * K1 + 3 * K1);
   hipLaunchKernelGGL(mm::mixer_bwd_seq_kernel, dim3(B), dim3(256), sm, (hipStream_t)s, a, q);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1) {
+  const mm::MixSeqGeo g(Hm, K1, N);
+  const char* lds_env = getenv("MM_MIX_LDS");
+  if (lds_env && lds_env[0] == '0') return 0;
+  return B < 512 && g.fwd_floats() * 4 <= mm::kMixSeqLds && 3 * Hm <= 256 && N <= 256;
+}
+
+int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
+                     int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s) {
+  MM_REQUIRE(nets && n_nets >= 1 && n_nets <= 2 && B > 0 && steps >= 1, "mixer_fwd_seq: bad args");
+  MM_REQUIRE(steps == 1 || reset_steps, "mixer_fwd_seq: reset_steps required for steps > 1");
+  MM_REQUIRE(mm_mixer_fwd_seq_fits(B, N, Hm, K1), "mixer_fwd_seq: B >= 512 or the weights exceed the LDS");
+  for (int i = 0; i < n_nets; ++i)
+    MM_REQUIRE(nets[i].gi && nets[i].q && nets[i].qtot, "mixer_fwd_seq: gi / q / qtot required");
+  mm::MixFwdArgs a;
+  for (int i = 0; i < 2; ++i) {
+    const mm_mix_net& n = nets[i < n_nets ? i : 0];
+    a.net[i] = {n.P, n.gi, n.q, n.s_off, n.h_in, n.reset, n.h_out, n.qtot, n.save};
+  }
+  a.obs = nullptr;
+  a.reset_obs = nullptr;
+  a.B = B;
+  a.N = N;
+  a.S = S;
+  a.Hm = Hm;
+  a.K1 = K1;
+  mm::MixFwdSeq q;
+  q.C = steps;
+  q.gi_st = (int64_t)B * 3 * Hm;
+  q.q_st = (int64_t)B * N;
+  q.qtot_st = B;
+  q.save_st = (int64_t)B * mm::mix_save_dim(Hm, K1, N);
+  q.hout_st = 0;
+  q.reset_steps = reset_steps;
+  const int rc = mm::mix_seq_lds_setup();
+  if (rc) return rc;
+  const mm::MixSeqGeo g(Hm, K1, N);
+  hipLaunchKernelGGL(mm::mixer_fwd_seq_lds_kernel, dim3(B, n_nets), dim3(256), g.fwd_floats() * 4, (hipStream_t)s, a,
+                     q);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -1463,6 +1962,31 @@ int mm_mixer_bwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const 
   mm::MixBwdArgs a = {P, save, qa, dq, done, dhm, dqa, delta, B, N, S, Hm, K1};
   const size_t sm = sizeof(float) * ((size_t)8 * Hm + N * K1 + 3 * K1);
   hipLaunchKernelGGL(mm::mixer_bwd_kernel, dim3(B), dim3(256), sm, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B, const float* save,
+                     const int32_t* acts, const float* dqa, const float* done, const float* ones, float* dh,
+                     float* dgi, float* dgh, float* dq, int32_t steps, mm_stream_t s) {
+  MM_REQUIRE(d && P && save && acts && dqa && done && ones && dh && dgi && dgh && dq && steps >= 1 && B > 0,
+             "agent_bwd_seq: bad args");
+  MM_REQUIRE(d->h <= 64 && d->n_actions <= 64, "agent_bwd_seq: needs H <= 64 and A <= 64");
+  const size_t smem = sizeof(float) * (3 * (size_t)d->h * d->h + 4 * 3 * (size_t)d->h + (size_t)d->n_actions * d->h);
+  MM_REQUIRE(smem <= 64 * 1024, "agent_bwd_seq: W_hh too large for LDS");
+  mm::AgentBwdArgs a = {P, oWq, oWhh, save, acts, dqa, done, dh, dgi, dgh, dq, B, d->n_agents, d->f1, d->g, d->h,
+                        d->n_actions};
+  const int64_t BN = (int64_t)B * d->n_agents;
+  mm::AgentBwdSeq q;
+  q.C = steps;
+  q.save_st = BN * (d->f1 + d->g + 6 * d->h);
+  q.acts_st = BN;
+  q.dqa_st = BN;
+  q.dgi_st = BN * 3 * d->h;
+  q.dq_st = BN * d->n_actions;
+  q.done_st = B;
+  q.ones = ones;
+  hipLaunchKernelGGL(mm::agent_bwd_seq_kernel, dim3((B + 3) / 4, d->n_agents), dim3(256), smem, (hipStream_t)s, a, q);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

@@ -1105,4 +1105,43 @@ int mm_per_copy_slot_rows(mm_per* per, int64_t* dst, mm_stream_t s) {
   MM_HIP_CHECK(hipMemcpyAsync(dst, per->slot_row, (size_t)per->cap * 8, hipMemcpyDeviceToDevice, (hipStream_t)s));
   return MM_OK;
 }
+
+int mm_per_save_state(mm_per* per, double* tree_dst, int64_t* rows_dst, double* scalars, mm_stream_t s) {
+  MM_REQUIRE(per && tree_dst && rows_dst && scalars, "per_save_state: null argument");
+  MM_HIP_CHECK(hipMemcpyAsync(tree_dst, per->tree, (size_t)(2 * per->cap - 1) * 8, hipMemcpyDeviceToDevice,
+                              (hipStream_t)s));
+  MM_HIP_CHECK(hipMemcpyAsync(rows_dst, per->slot_row, (size_t)per->cap * 8, hipMemcpyDeviceToDevice, (hipStream_t)s));
+  mm::PerDev h;
+  MM_HIP_CHECK(hipMemcpyAsync(&h, per->st, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)s));
+  MM_HIP_CHECK(hipStreamSynchronize((hipStream_t)s));
+  scalars[0] = (double)h.n_data;
+  scalars[1] = h.alpha;
+  scalars[2] = h.beta;
+  scalars[3] = h.alpha_inc;
+  scalars[4] = h.beta_inc;
+  scalars[5] = (double)h.n_samples;
+  return MM_OK;
+}
+
+int mm_per_load_state(mm_per* per, const double* tree_src, const int64_t* rows_src, const double* scalars,
+                      mm_stream_t s) {
+  MM_REQUIRE(per && tree_src && rows_src && scalars, "per_load_state: null argument");
+  MM_REQUIRE(scalars[0] >= 0 && scalars[0] <= (double)per->cap, "per_load_state: fill count out of range");
+  MM_HIP_CHECK(hipMemcpyAsync(per->tree, tree_src, (size_t)(2 * per->cap - 1) * 8, hipMemcpyDeviceToDevice,
+                              (hipStream_t)s));
+  MM_HIP_CHECK(hipMemcpyAsync(per->slot_row, rows_src, (size_t)per->cap * 8, hipMemcpyDeviceToDevice, (hipStream_t)s));
+  mm::PerDev h;
+  h.n_data = (int64_t)scalars[0];
+  h.alpha = scalars[1];
+  h.beta = scalars[2];
+  h.alpha_inc = scalars[3];
+  h.beta_inc = scalars[4];
+  h.n_samples = (uint64_t)scalars[5];
+  MM_HIP_CHECK(hipMemcpyAsync(per->st, &h, sizeof(h), hipMemcpyHostToDevice, (hipStream_t)s));
+  MM_HIP_CHECK(hipStreamSynchronize((hipStream_t)s));
+  per->n_data = h.n_data;
+  per->alpha = h.alpha;
+  per->beta = h.beta;
+  return MM_OK;
+}
 }

@@ -162,6 +162,8 @@ _SIGS += [
                              c_vp]),
     ("mm_agent_bwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp, c_vp, c_vp, c_vp]),
+    ("mm_agent_bwd_seq", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                 c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
     ("mm_outer_reduce", c_i32, [ctypes.POINTER(OuterArgs), c_vp]),
     ("mm_agent_q_pre2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
                                 ctypes.POINTER(QFwdIO), c_i64, c_vp]),
@@ -180,7 +182,14 @@ _SIGS += [
                               c_vp, c_f32, c_vp]),
     ("mm_per_sample_uniform", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
     ("mm_eval_accum", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_set_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_per_save_state", c_i32, [c_vp, c_vp, c_vp, ctypes.POINTER(c_f64), c_vp]),
+    ("mm_per_load_state", c_i32, [c_vp, c_vp, c_vp, ctypes.POINTER(c_f64), c_vp]),
+    ("mm_debug_trace", c_i32, [c_vp, c_i32]),
     ("mm_chunk_score", c_i32, [c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_mixer_fwd_seq_fits", c_i32, [c_i32, c_i32, c_i32, c_i32]),
+    ("mm_mixer_fwd_seq", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(MixNetIO), c_i32, c_i32, c_vp,
+                                 c_vp]),
 ]
 
 

@@ -72,3 +72,22 @@ class VecEnv:
         check(lib().mm_env_get_state(self._h, pos.ctypes.data, grid.ctypes.data, steps.ctypes.data,
                                      apples.ctypes.data), "env_get_state")
         return pos, grid, steps, apples
+
+    def set_state(self, pos, grid, steps, apples):
+        """Restore the state returned by get_state (checkpoint resume)."""
+        pos = np.ascontiguousarray(pos, np.int32)
+        grid = np.ascontiguousarray(grid, np.int8)
+        steps = np.ascontiguousarray(steps, np.int32)
+        apples = np.ascontiguousarray(apples, np.int32)
+        assert pos.shape == (self.E, self.N, 2) and grid.shape == (self.E, self.rows, self.cols)
+        check(lib().mm_env_set_state(self._h, pos.ctypes.data, grid.ctypes.data, steps.ctypes.data,
+                                     apples.ctypes.data), "env_set_state")
+
+    # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)
+    def checkpoint_tensors(self):
+        pos, grid, steps, apples = self.get_state()
+        return {"pos": torch.from_numpy(pos), "grid": torch.from_numpy(grid), "steps": torch.from_numpy(steps),
+                "apples": torch.from_numpy(apples)}, {}
+
+    def restore_tensors(self, ts, scalars=None):
+        self.set_state(ts["pos"].numpy(), ts["grid"].numpy(), ts["steps"].numpy(), ts["apples"].numpy())

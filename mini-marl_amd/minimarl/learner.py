@@ -391,7 +391,14 @@ class QLearner:
                 check(L.mm_mixer_bwd_seq(B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.msave), ptr(self.qa),
                                          ptr(self.dq), ptr(self.done), ptr(self.ones_f), ptr(self.dhm), ptr(self.dqa),
                                          ptr(self.mdelta), C, s), "mixer bwd seq")
+        if self.seq and B < 512:
+            # the agent BPTT chain over all C steps in one launch (W_hh in LDS, dh carried in registers)
+            check(L.mm_agent_bwd_seq(ctypes.byref(self.beh.dims), ptr(P), o[8], o[5], B, ptr(self.asave),
+                                     ptr(self.acts), ptr(self.dqa), ptr(self.done), ptr(self.ones_f), ptr(self.dh),
+                                     ptr(self.dgi), ptr(self.dgh), ptr(self.dqv), C, s), "agent bwd seq")
         for t in range(C - 1, -1, -1):
+            if self.seq and B < 512:
+                break
             dn = self.ones_f if t == C - 1 else self.done[t * B:(t + 1) * B]
             if self.has_mixer and not self.seq:
                 mx = self.mix
@@ -426,9 +433,23 @@ class QLearner:
         check(L.mm_agent_q_rec_seq2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
                                     ptr(self.tgt.packed), ctypes.byref(it), B, C, ptr(self.done8), s), "rec seq")
         if self.has_mixer:
-            # per-step mixer launches (a one-launch sequence of this kernel measured slower: 32 vs
-            # 13 us per step), reading the REC outputs of every step
             mx = self.mix
+            if L.mm_mixer_fwd_seq_fits(B, N, mx.Hm, mx.K1):
+                # all C steps of both mixers in ONE launch: weights staged once into LDS, the mixer
+                # hidden carried in LDS (bit-identical to the per-step launches below)
+                nets = (MixNetIO * 2)()
+                for k, (Pm, q, qt, sv, gi) in enumerate(((self.mix.flat, self.qa, self.qtot, self.msave, self.gi_b),
+                                                          (self.tmix.flat, self.maxq, self.qtot_t, None, self.gi_t))):
+                    n = nets[k]
+                    n.P, n.q, n.gi, n.qtot = Pm.data_ptr(), q.data_ptr(), gi.data_ptr(), qt.data_ptr()
+                    n.s_off = self.s_off.data_ptr()
+                    n.h_in, n.h_out = self.hm[0].data_ptr(), None
+                    n.reset = self.ones8.data_ptr()
+                    n.save = sv.data_ptr() if sv is not None else None
+                check(L.mm_mixer_fwd_seq(B, N, mx.S, mx.Hm, mx.K1, nets, 2, C, ptr(self.done8), s), "mixer fwd seq")
+                return
+            # per-step mixer launches (B >= 512: 8 samples per block share the weight reads), reading
+            # the REC outputs of every step
             for t in range(C):
                 nets = (MixNetIO * 2)()
                 for k, (Pm, q, off, h, qt, sv, gi) in enumerate(

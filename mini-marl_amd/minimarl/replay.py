@@ -49,11 +49,34 @@ class DevicePER:
 
     @property
     def alpha(self):
-        return lib().mm_per_alpha(self._h)
+        """Current alpha (the device value: graph-replayed sample calls anneal it on the device)."""
+        return self.device_scalars()[1]
 
     @property
     def beta(self):
-        return lib().mm_per_beta(self._h)
+        return self.device_scalars()[2]
+
+    def device_scalars(self):
+        """(fill count, alpha, beta, alpha_inc, beta_inc, sample calls) read from the device (syncs)."""
+        ts, sc = self.checkpoint_tensors()
+        return [float(x) for x in ts["scalars"]]
+
+    # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)
+    def checkpoint_tensors(self):
+        tree = torch.empty(2 * self.capacity - 1, dtype=torch.float64, device=self.device)
+        rows = torch.empty(self.capacity, dtype=torch.int64, device=self.device)
+        sc = (ctypes.c_double * 6)()
+        check(lib().mm_per_save_state(self._h, ptr(tree), ptr(rows), sc, stream_handle(self.device)), "per_save_state")
+        return {"tree": tree, "slot_rows": rows, "scalars": torch.tensor(list(sc), dtype=torch.float64)}, {}
+
+    def restore_tensors(self, ts, scalars=None):
+        from .checkpoint import copy_into
+        tree = torch.empty(2 * self.capacity - 1, dtype=torch.float64, device=self.device)
+        rows = torch.empty(self.capacity, dtype=torch.int64, device=self.device)
+        copy_into(tree, ts["tree"], "tree")
+        copy_into(rows, ts["slot_rows"], "slot_rows")
+        sc = (ctypes.c_double * 6)(*[float(x) for x in ts["scalars"]])
+        check(lib().mm_per_load_state(self._h, ptr(tree), ptr(rows), sc, stream_handle(self.device)), "per_load_state")
 
     def __len__(self):
         return int(lib().mm_per_size(self._h))

@@ -166,6 +166,63 @@ class QTrainer:
         score, loss, _, _ = self.evaluator.run(self.eng.behavior, tgt)
         return {"test_score": score, "test_loss": loss}
 
+    # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)
+    _ENGINE_BUFFERS = ("cur_row", "init_obs", "h", "ht", "maxq", "rew", "chunk_td", "eps_dev", "counter_dev",
+                       "staging")
+
+    def checkpoint_tensors(self, include_replay=True):
+        """Learner (params, targets, Adam), replay (tree, slot map, annealed alpha / beta, sample counter),
+        engine (hiddens, RNG step counter, current-obs rows, staging rows), env integer state and, with
+        ``include_replay``, the chunk store itself — a resumed trainer continues bit-identically."""
+        torch.cuda.synchronize(self.device)
+        eng = self.eng
+        ts, sc = self.learner.checkpoint_tensors()
+        out = {"learner/" + k: v for k, v in ts.items()}
+        pts, _ = eng.per.checkpoint_tensors()
+        out.update({"per/" + k: v for k, v in pts.items()})
+        ets, _ = eng.env.checkpoint_tensors()
+        out.update({"env/" + k: v for k, v in ets.items()})
+        for k in self._ENGINE_BUFFERS:
+            out["engine/" + k] = getattr(eng, k)
+        for k in range(2):
+            out[f"engine/done_buf{k}"] = eng.done_buf[k]
+            out[f"engine/act_buf{k}"] = eng.act_buf[k]
+            out[f"engine/qsel_buf{k}"] = eng.qsel_buf[k]
+        if include_replay:
+            for k in ("obs", "act", "rew", "done"):
+                out["store/" + k] = getattr(eng.store, k)
+        out["trainer/ep_ret"] = self.ep_ret
+        out["trainer/score_acc"] = self.score_acc
+        scalars = {"learner": sc, "t": eng.t, "chunks_inserted": eng.chunks_inserted, "primed": eng._primed,
+                   "td_pending": eng._td_pending, "episode": self.episode, "warmed": self.warmed,
+                   "replay_saved": bool(include_replay)}
+        return out, scalars
+
+    def restore_tensors(self, ts, scalars):
+        from .checkpoint import copy_into
+        eng = self.eng
+        self.learner.restore_tensors({k[8:]: v for k, v in ts.items() if k.startswith("learner/")}, scalars["learner"])
+        eng.per.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("per/")})
+        eng.env.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("env/")})
+        for k in self._ENGINE_BUFFERS:
+            copy_into(getattr(eng, k), ts["engine/" + k], k)
+        for k in range(2):
+            copy_into(eng.done_buf[k], ts[f"engine/done_buf{k}"], "done_buf")
+            copy_into(eng.act_buf[k], ts[f"engine/act_buf{k}"], "act_buf")
+            copy_into(eng.qsel_buf[k], ts[f"engine/qsel_buf{k}"], "qsel_buf")
+        if scalars.get("replay_saved"):
+            for k in ("obs", "act", "rew", "done"):
+                copy_into(getattr(eng.store, k), ts["store/" + k], k)
+        copy_into(self.ep_ret, ts["trainer/ep_ret"], "ep_ret")
+        copy_into(self.score_acc, ts["trainer/score_acc"], "score_acc")
+        eng.t, eng.chunks_inserted = int(scalars["t"]), int(scalars["chunks_inserted"])
+        eng._primed, eng._td_pending = bool(scalars["primed"]), bool(scalars["td_pending"])
+        eng._eps_host = None
+        eng.behavior.mark_dirty()
+        eng.target.mark_dirty()
+        self.episode, self.warmed = int(scalars["episode"]), bool(scalars["warmed"])
+        torch.cuda.synchronize(self.device)
+
     # ------------------------------------------------------------------ throughput
     def timed(self, n_episodes):
         """Wall time of n_episodes training episodes (rollout + learner), synchronised."""

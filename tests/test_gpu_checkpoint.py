@@ -107,3 +107,35 @@ def test_mappo_resume_is_bit_identical(tmp_path):
     assert torch.equal(a.p.actor.flat, b.p.actor.flat)
     assert torch.equal(a.p.critic.flat, b.p.critic.flat)
     assert torch.equal(a.trainer.vn, b.trainer.vn)
+
+
+def test_trainer_resume_bit_identical(tmp_path):
+    """QTrainer checkpoint = learner + replay (tree, slot map, annealed alpha / beta, sample counter) +
+    engine hiddens / RNG counters + env state + chunk store: a resumed trainer's next episodes (rollout,
+    PER sampling, updates, reprioritisation) are bit-identical to the uninterrupted run."""
+    from minimarl.checkpoint import load_checkpoint, save_checkpoint
+    from minimarl.config import QTrainConfig
+    from minimarl.train import QTrainer
+    cfg = QTrainConfig(algo="qmix", n_envs=64, n_agents=4, full_observable=False, buffer_limit=512, max_step=20,
+                       update_iter=3, update_target_interval=2, test_interval=0, test_envs=0,
+                       epsilon_anneal_episode=10, seed=9)
+    a = QTrainer(cfg, device=DEV)
+    for _ in range(3):
+        a.train_episode()
+    path = str(tmp_path / "trainer.safetensors")
+    save_checkpoint(path, trainer=a)
+    alpha_saved = a.eng.per.alpha
+    for _ in range(2):
+        a.train_episode()
+    b = QTrainer(cfg, device=DEV)
+    load_checkpoint(path, trainer=b)
+    assert b.episode == 3 and b.eng.t == a.eng.t - 40 and abs(b.eng.per.alpha - alpha_saved) < 1e-15
+    for _ in range(2):
+        b.train_episode()
+    torch.cuda.synchronize()
+    for x, y in [(a.learner.P, b.learner.P), (a.learner.m, b.learner.m), (a.eng.target.flat, b.eng.target.flat),
+                 (a.eng.per.tree(), b.eng.per.tree()), (a.eng.per.slot_rows(), b.eng.per.slot_rows()),
+                 (a.eng.store.obs, b.eng.store.obs), (a.eng.store.act, b.eng.store.act), (a.eng.h, b.eng.h),
+                 (a.score_acc, b.score_acc)]:
+        assert torch.equal(x, y)
+    assert a.eng.per.alpha == b.eng.per.alpha and a.eng.per.alpha > cfg.alpha
