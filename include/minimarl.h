@@ -259,11 +259,15 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
 /* Chunk-sequence mixer backward: all C steps (t = C-1 .. 0) in one launch, a block per sample
  * carrying dhm. Step t reads save [C][B][MSD], qa [C][B][N], dq [C][B] and writes dqa [C][B][N],
  * delta [C][B][MDD] at the step-0 pointers + t * (per-step size); the future gradient is dropped at
- * t = C-1 (ones) and where done[t*B + b]. Bit-identical to C mm_mixer_bwd launches. */
-/* All C steps of the mixer forward for both nets in ONE launch (B < 512): block = (sample, net), the
- * net's W_hh + hypernet weights staged once into LDS, the mixer hidden carried in LDS. Step t's arrays
+ * t = C-1 (ones) and where done[t*B + b]. Bit-identical to C mm_mixer_bwd launches.
+ * ws: [C][B][4][Hm] floats of workspace (B < 512: the hypernet input gradients of every step are
+ * computed for all rows at once, then one block per sample runs the serial GRU chain); may be NULL
+ * (then the single-launch LDS kernel runs). */
+/* All C steps of the mixer forward for both nets (B < 512): a serial launch with block = (sample, net),
+ * the net's W_hh staged once into LDS and the mixer hidden carried in LDS, then the hypernets. Step t's arrays
  * are at the step-0 pointers of nets[] + t * (B x width): gi [B][3Hm] (required, mm_mixer_gi), q [B][N],
- * qtot [B], save [B][mm_mixer_save_dim]; h_out (may be NULL) is rewritten every step; step 0 starts
+ * qtot [B], save [B][mm_mixer_save_dim]; h_out [C][B][Hm] receives the hidden sequence (required: the
+ * serial GRU kernel writes it, then one launch runs the hypernets of all C*B rows); step 0 starts
  * from nets[].h_in / reset, step t >= 1 resets where reset_steps[(t-1)*B + b]. Results are
  * bit-identical to C per-step mm_mixer_fwd launches. mm_mixer_fwd_seq_fits tells whether it applies. */
 int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1);
@@ -271,7 +275,7 @@ int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
                      int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s);
 int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                      const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
-                     float* delta, int32_t steps, mm_stream_t s);
+                     float* delta, float* ws, int32_t steps, mm_stream_t s);
 int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
                  const mm_mix_net* nets, int32_t n_nets, mm_stream_t s);
 /* TD loss terms and their gradient seeds (reference quirks: bootstrap x N, IS weight on the target). */
@@ -473,7 +477,8 @@ int mm_offq_q_values(const mm_offq_dims* d, const float* P, const float* obs, co
 int mm_offq_soft_update(float* target, const float* source, int64_t n, double tau, mm_stream_t s);
 
 /* Debug: copy the first n (<= 4096) u64 slots of the timing trace buffer that kernels fill when
- * MM_REC_TRACE=1 is set in the environment (clock64 stamps per phase; tools/trace_rec.py). */
+ * MM_REC_TRACE=1 is set in the environment (clock64 stamps per phase; tools/trace_rec.py). mm_debug_trace(NULL, 0) allocates the buffer
+ * (call it before any graph capture). */
 int mm_debug_trace(uint64_t* host_out, int32_t n);
 
 #ifdef __cplusplus

@@ -102,7 +102,7 @@ __device__ __forceinline__ void load_obs_kblock(const float* orow, int kb, int D
 // Q output / argmax / eps-greedy / gather epilogue shared by the fused and the split forward.
 template <int AB>
 __device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_io& io, int agent, int e, bool valid,
-                                             const f32x16 (&qa)[AB], float eps, uint64_t ctr);
+                                             const f32x16 (&qa)[AB], float eps, uint64_t ctr, int act_pre = -1);
 template <int AB>
 __device__ __forceinline__ void q_epilogue(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB]) {
   const mm_qfwd_io& io = p.io;
@@ -112,7 +112,7 @@ __device__ __forceinline__ void q_epilogue(const QFwdParams& p, int agent, int e
 }
 template <int AB>
 __device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_io& io, int agent, int e, bool valid,
-                                             const f32x16 (&qa)[AB], float eps, uint64_t ctr) {
+                                             const f32x16 (&qa)[AB], float eps, uint64_t ctr, int act_pre) {
   const int hh = (threadIdx.x & 63) >> 5;
   if (valid && io.q_out) {
     float* qrow = io.q_out + (int64_t)e * io.q_se + (int64_t)agent * io.q_sa;
@@ -162,7 +162,7 @@ __device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_
       }
     }
   } else if (io.mode == MM_Q_GATHER) {
-    act = valid ? io.act_in[(int64_t)e * io.act_se + agent] : 0;
+    act = act_pre >= 0 ? act_pre : (valid ? io.act_in[(int64_t)e * io.act_se + agent] : 0);
   }
   float mine = 0.0f;
 #pragma unroll
@@ -394,6 +394,110 @@ __device__ __forceinline__ void agent_pre_body(const QFwdParams& p, int agent, i
         for (int s = 0; s < 16; ++s) gi[gte * H + hb * 32 + kperm(s, hh)] = acc[s];
       }
     }
+  }
+}
+
+// PRE for small batches: one block = one 32-env tile of one agent, the row blocks of each layer on
+// separate waves (layer 1: RB1 waves, layer 2: RB2 waves, W_ih: 3 HB waves), activations handed over
+// through LDS. Every wave issues ALL its loads (weight fragments of the layers it computes, the
+// observation k-blocks, biases) before its first MFMA: one memory round trip per launch instead of one
+// per fragment, and a critical path of KD + RB1 + RB2 k-blocks of MFMAs instead of the whole network
+// on one wave. Per output the accumulation order is agent_pre_body's (bit-identical).
+constexpr int kPreRbMaxKD = 2;   // observation k-blocks (D <= 64) supported by the row-block PRE
+template <int F1, int G, int H, int AB>
+__device__ __forceinline__ void agent_pre_rb_body(const QFwdParams& p, int agent, int tile) {
+  using S = Sched<F1, G, H, AB>;
+  using CG = typename S::CG;
+  constexpr int RB1 = S::RB1, RB2 = S::RB2, HB = S::HB;
+  __shared__ float x1s[RB1][16][64];
+  __shared__ float x2s[RB2][16][64];
+  const float* W = p.packed + (int64_t)agent * p.g.agent_stride;
+  const int lane = threadIdx.x & 63, hh = lane >> 5, wv = threadIdx.x >> 6;
+  const int e = tile * 32 + (lane & 31);
+  const bool valid = e < p.E;
+  const mm_qfwd_io& io = p.io;
+  const float* orow = obs_row_ptr(p, agent, e);
+  const int KD = p.g.KD;
+  // ---- every load of this wave first
+  float f1[kPreRbMaxKD][16], xo[kPreRbMaxKD][16], f2[RB1][16], f3[RB2][16];
+  f32x16 b1, b2, b3;
+  const int hb3 = wv % HB, gte = wv / HB;
+  if (wv < RB1) {
+    b1 = load_bias(W + CG::off_b1 + wv * 32, hh);
+#pragma unroll
+    for (int kb = 0; kb < kPreRbMaxKD; ++kb)
+      if (kb < KD) {
+        load_frag(W + CG::off_l1 + (int64_t)(wv * KD + kb) * 1024, lane, f1[kb]);
+        load_obs_kblock(orow, kb, p.D, xo[kb]);
+      }
+  }
+  if (wv < RB2) {
+    b2 = load_bias(W + CG::off_b2 + wv * 32, hh);
+#pragma unroll
+    for (int kb = 0; kb < RB1; ++kb) load_frag(W + S::off(wv * RB1 + kb), lane, f2[kb]);
+  }
+  if (wv < 3 * HB) {
+    b3 = gte < 2 ? load_bias(W + CG::off_brz + (gte * HB + hb3) * 32, hh) : load_bias(W + CG::off_bin + hb3 * 32, hh);
+#pragma unroll
+    for (int kb = 0; kb < RB2; ++kb) load_frag(W + S::off(S::NF2 + hb3 * S::PERHB + gte * RB2 + kb), lane, f3[kb]);
+  }
+  float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
+  // ---- layer 1 (row block wv)
+  if (wv < RB1) {
+    f32x16 acc = b1;
+#pragma unroll
+    for (int kb = 0; kb < kPreRbMaxKD; ++kb)
+      if (kb < KD) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = mfma32(f1[kb][s], xo[kb][s], acc);
+      }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float v = fmaxf(acc[s], 0.0f);
+      x1s[wv][s][lane] = v;
+      if (sv) sv[wv * 32 + kperm(s, hh)] = v;
+    }
+  }
+  __syncthreads();
+  // ---- layer 2 (row block wv)
+  if (wv < RB2) {
+    f32x16 acc = b2;
+#pragma unroll
+    for (int kb = 0; kb < RB1; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = mfma32(f2[kb][s], x1s[kb][s][lane], acc);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float v = fmaxf(acc[s], 0.0f);
+      x2s[wv][s][lane] = v;
+      if (sv) sv[F1 + wv * 32 + kperm(s, hh)] = v;
+    }
+  }
+  __syncthreads();
+  // ---- GRU input projection (gate gte, hidden block hb3)
+  if (wv < 3 * HB) {
+    f32x16 acc = b3;
+#pragma unroll
+    for (int kb = 0; kb < RB2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = mfma32(f3[kb][s], x2s[kb][s][lane], acc);
+    if (valid) {
+      float* gi = io.gi + ((int64_t)e * p.N + agent) * 3 * H;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) gi[gte * H + hb3 * 32 + kperm(s, hh)] = acc[s];
+    }
+  }
+}
+
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(64 * (3 * (H / 32) > F1 / 32 ? 3 * (H / 32) : F1 / 32)) void agent_pre_rb_kernel(
+    QFwdParams p0, QFwdParams p1) {
+  if ((int)blockIdx.x >= p0.nblocks) {
+    const int bid = (int)blockIdx.x - p0.nblocks;
+    agent_pre_rb_body<F1, G, H, AB>(p1, bid % p1.N, bid / p1.N);
+  } else {
+    const int bid = (int)blockIdx.x;
+    agent_pre_rb_body<F1, G, H, AB>(p0, bid % p0.N, bid / p0.N);
   }
 }
 
@@ -650,18 +754,25 @@ __global__ __launch_bounds__(256, 2) void agent_rec_seq_kernel(QFwdParams p0, QF
 // last wave computes the Q head + epilogue of step t while the gate waves already run step t + 1.
 // Every accumulator starts from the same value and accumulates in the same (kb, s) order as
 // agent_rec_body, so the results are bit-identical to the per-step launches.
+//
+// Memory-counter discipline (gfx9 counts stores in vmcnt, so any load wait also drains every store
+// issued before it): the r- and z-waves only LOAD (next step's gate inputs, one step ahead), the
+// n-wave only STORES (the training save rows of step t - 1, staged in LDS by the r-wave and written
+// out while the r-wave computes step t's gates), and the Q wave loads its gathered action before
+// issuing its stores. No wave on the recurrence's critical path ever waits for a store.
 template <int F1, int G, int H, int AB>
 __device__ __forceinline__ void rec_seq_gp_body(const QFwdParams& p, const RecSeq& sq, int bid) {
   const uint64_t t_entry = clock64();
   using S = Sched<F1, G, H, AB>;
   using CG = typename S::CG;
   constexpr int RB2 = S::RB2, HB = S::HB;
+  constexpr int SROW = F1 + G + 6 * H;   // training save row of one (env, agent)
   __shared__ float hx[2][HB][16][64];   // new hidden blocks, double-buffered by step parity
   __shared__ float gx[2][HB][16][64];   // z / n-hidden gate accumulators handed to the r-wave
-  // save-row staging of the r-waves: [field][feature][env] (env stride 33: conflict-free both ways), so
-  // the training save rows go out as 128-byte runs (one env's 32 features) instead of one 4-byte
-  // write per env and feature (a scattered store costs one cache-line write per lane)
-  __shared__ float svs[HB][6][32][33];
+  // save-row staging [step parity][hb][field][feature][env] (env stride 33: conflict-free both ways), so
+  // the save rows go out as 128-byte runs (one env's 32 features of one field)
+  __shared__ float svs[2][HB][6][32][33];
+  __shared__ int zreset[64];   // reset flag of the next step, written by the r-wave of hb 0 in the gate phase
   const int agent = bid % p.N, tile = bid / p.N;
   const float* W = p.packed + (int64_t)agent * p.g.agent_stride;
   const int lane = threadIdx.x & 63, hh = lane >> 5, wv = threadIdx.x >> 6;
@@ -670,119 +781,33 @@ __device__ __forceinline__ void rec_seq_gp_body(const QFwdParams& p, const RecSe
   const int e = tile * 32 + (lane & 31);
   const bool valid = e < p.E;
   const mm_qfwd_io io = p.io;
-  float fz[HB][16];
-  if (!qwave) {
-    const int base = S::NF2 + hb * S::PERHB + 3 * RB2;
-#pragma unroll
-    for (int kb = 0; kb < HB; ++kb) load_frag(W + S::off(base + g * HB + kb), lane, fz[kb]);
-  }
   const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
   const uint64_t ctr = (io.mode == MM_Q_ACT && io.counter_ptr) ? *io.counter_ptr : io.counter;
-  // this wave's gate inputs of step t: r-wave gi_r (+ gi_n), z-wave gi_z, n-wave b_hn
-  const int dbg = p.dbg;   // timing knob (MM_REC_DBG bits): 1 no saves, 2 no Q head, 4 no gi loads
-  auto load_gi = [&](int t, f32x16& a0, f32x16& a1) {
-    if (dbg & 4) {
-#pragma unroll
-      for (int s = 0; s < 16; ++s) a0[s] = a1[s] = 0.0f;
-      return;
-    }
-    const float* gi = io.gi + t * sq.gi_st + ((int64_t)(valid ? e : 0) * p.N + agent) * 3 * H;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int f = hb * 32 + kperm(s, hh);
-      a0[s] = g == 0 ? gi[f] : gi[H + f];
-      a1[s] = g == 0 ? gi[2 * H + f] : 0.0f;
-    }
-  };
-  // Q-head wave: W_q fragments and bias loaded once for the whole sequence
-  float fq[AB][HB][16];
-  f32x16 bq[AB];
+  uint64_t* tr = (sq.trace && bid == 0 && lane == 0 && (wv == 0 || qwave)) ? sq.trace : nullptr;
+  if (tr && wv == 0) {
+    tr[0] = clock64();
+    tr[3] = t_entry;
+  }
+  // The Q wave and the gate waves run separate loops, so the register allocator sees their
+  // loop-carried state (W_q fragments vs. gate fragments + prefetched inputs) as disjoint.
   if (qwave) {
+    // Q-head wave: W_q fragments and bias loaded once for the whole sequence
+    float fq[AB][HB][16];
+    f32x16 bq[AB];
 #pragma unroll
     for (int ab = 0; ab < AB; ++ab) {
       bq[ab] = load_bias(W + CG::off_bq + ab * 32, hh);
 #pragma unroll
       for (int kb = 0; kb < HB; ++kb) load_frag(W + S::off(S::NF2 + S::NFG + ab * HB + kb), lane, fq[ab][kb]);
     }
-  }
-  f32x16 gin0, gin1, nxt0, nxt1;
-  bool rst_next = !valid;
-  if (!qwave && g < 2) load_gi(0, gin0, gin1);
-  const f32x16 bhn = load_bias(W + CG::off_bhn + hb * 32, hh);
-  uint64_t* tr = (sq.trace && bid == 0 && lane == 0 && (wv == 0 || qwave)) ? sq.trace : nullptr;
-  if (tr && wv == 0) { tr[0] = clock64(); tr[3] = t_entry; }
-  for (int t = 0; t < sq.C; ++t) {
-    uint64_t* ts = tr ? tr + 4 + t * 8 : nullptr;
-    if (!qwave) {
-      if (ts) ts[0] = clock64();
-      if (g < 2 && t + 1 < sq.C) load_gi(t + 1, nxt0, nxt1);   // prefetch next step's inputs
-      const bool zero_h = !valid || t == 0 || rst_next;
-      if (t + 1 < sq.C && valid) rst_next = sq.reset[(int64_t)t * sq.reset_st + e] != 0;
-      f32x16 h0[HB];
-#pragma unroll
-      for (int kb = 0; kb < HB; ++kb)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) h0[kb][s] = zero_h ? 0.0f : hx[t & 1][kb][s][lane];
-      f32x16 acc = g == 2 ? bhn : gin0;
-#pragma unroll
-      for (int kb = 0; kb < HB; ++kb)
-#pragma unroll
-        for (int s = 0; s < 16; ++s) acc = mfma32(fz[kb][s], h0[kb][s], acc);
-      if (ts) ts[1] = clock64() + (uint64_t)acc[0] * 0;
-      if (g > 0) {
-#pragma unroll
-        for (int s = 0; s < 16; ++s) gx[g - 1][hb][s][lane] = acc[s];
-      }
-      lds_sync();   // A: gate accumulators visible
-      if (ts) ts[2] = clock64();
-      if (g == 0) {
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          float h0v = h0[0][s];
-#pragma unroll
-          for (int kb = 1; kb < HB; ++kb)
-            if (kb == hb) h0v = h0[kb][s];
-          const float r = sigmoidf_(acc[s]);
-          const float z = sigmoidf_(gx[0][hb][s][lane]);
-          const float anh = gx[1][hb][s][lane];
-          const float n = tanhf_(gin1[s] + r * anh);
-          const float h1v = n + z * (h0v - n);
-          hx[(t + 1) & 1][hb][s][lane] = h1v;
-          const int fl = kperm(s, hh), el = lane & 31;
-          svs[hb][0][fl][el] = h0v;
-          svs[hb][1][fl][el] = r;
-          svs[hb][2][fl][el] = z;
-          svs[hb][3][fl][el] = n;
-          svs[hb][4][fl][el] = anh;
-          svs[hb][5][fl][el] = h1v;
-        }
-        if (io.save && !(dbg & 1)) {
-          // lanes 0-31: env 2q, lanes 32-63: env 2q + 1; lane & 31 = feature of this hidden block
-          const int fl = lane & 31;
-#pragma unroll 4
-          for (int q = 0; q < 16; ++q) {
-            const int el = 2 * q + hh, ee = tile * 32 + el;
-            if (ee < p.E) {
-              float* row = io.save + t * sq.save_st + ((int64_t)ee * p.N + agent) * (F1 + G + 6 * H) + F1 + G +
-                           hb * 32 + fl;
-#pragma unroll
-              for (int fld = 0; fld < 6; ++fld) row[fld * H] = svs[hb][fld][fl][el];
-            }
-          }
-        }
-      }
-      if (ts) ts[3] = clock64();
-      lds_sync();   // B: new hidden of step t complete
-      if (ts) ts[4] = clock64();
-      if (g < 2) {
-        gin0 = nxt0;
-        gin1 = nxt1;
-      }
-    } else {
+    for (int t = 0; t < sq.C; ++t) {
+      uint64_t* ts = tr ? tr + 4 + t * 8 : nullptr;
+      // gathered action of step t, loaded before this wave's stores of step t (see above)
+      const int act_t =
+          (io.mode == MM_Q_GATHER && valid) ? io.act_in[t * sq.act_st + (int64_t)e * io.act_se + agent] : 0;
       lds_sync();   // A
       lds_sync();   // B
       if (ts) ts[5] = clock64();
-      if (dbg & 2) continue;
       f32x16 h1[HB];
 #pragma unroll
       for (int kb = 0; kb < HB; ++kb)
@@ -801,11 +826,143 @@ __device__ __forceinline__ void rec_seq_gp_body(const QFwdParams& p, const RecSe
       if (it.act_in) it.act_in += t * sq.act_st;
       if (it.qsel_out) it.qsel_out += t * sq.qsel_st;
       if (ts) ts[6] = clock64() + (uint64_t)qa[0][0] * 0;
-      q_epilogue_v<AB>(p, it, agent, e, valid, qa, eps, ctr);
+      q_epilogue_v<AB>(p, it, agent, e, valid, qa, eps, ctr, act_t);
       if (ts) ts[7] = clock64();
     }
+    if (tr) tr[2] = clock64();
+    return;
   }
-  if (tr) tr[wv == 0 ? 1 : 2] = clock64();
+
+  // ---- gate waves
+  float fz[HB][16];
+  {
+    const int base = S::NF2 + hb * S::PERHB + 3 * RB2;
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb) load_frag(W + S::off(base + g * HB + kb), lane, fz[kb]);
+  }
+  // gate inputs of this wave: r-wave gi_r (+ gi_n at +2H), z-wave gi_z; the n-wave's accumulator
+  // starts from b_hn (held in gin0, never replaced)
+  const float* gsrc =
+      io.gi ? io.gi + ((int64_t)(valid ? e : 0) * p.N + agent) * 3 * H + hb * 32 + (g == 1 ? H : 0) : nullptr;
+  auto load_gi = [&](int t, float (&a0)[16], float (&a1)[16]) {
+    const float* src = gsrc + (int64_t)t * sq.gi_st;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) a0[s] = src[kperm(s, hh)];
+    if (g == 0) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a1[s] = src[2 * H + kperm(s, hh)];
+    }
+  };
+  float gin0[16], gin1[16], nxt0[16], nxt1[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) gin1[s] = nxt1[s] = 0.0f;
+  if (g < 2) {
+    load_gi(0, gin0, gin1);
+  } else {
+    const f32x16 bhn = load_bias(W + CG::off_bhn + hb * 32, hh);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) gin0[s] = bhn[s];
+  }
+  // reset flag of the next step: loaded one step ahead by the r-wave of hb 0 (a loader wave), handed to
+  // all gate waves through LDS (zreset) so the n-wave never waits on a load
+  int rst_raw = 0;
+  const bool rst_loader = g == 0 && hb == 0;
+  // n-wave: write the save rows of step ts (staged in svs[ts & 1][hb]) as 128-byte runs
+  auto write_saves = [&](int ts) {
+    const int fl = lane & 31;   // lanes 0-31: env 2q, lanes 32-63: env 2q + 1
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int el = 2 * q + hh, ee = tile * 32 + el;
+      float v[6];
+#pragma unroll
+      for (int fld = 0; fld < 6; ++fld) v[fld] = svs[ts & 1][hb][fld][fl][el];
+      if (ee < p.E) {
+        float* row = io.save + ts * sq.save_st + ((int64_t)ee * p.N + agent) * SROW + F1 + G + hb * 32 + fl;
+#pragma unroll
+        for (int fld = 0; fld < 6; ++fld) row[fld * H] = v[fld];
+      }
+    }
+  };
+  const bool saver = g == 2 && io.save != nullptr;
+  // drain the prologue loads here, so the loop's wait analysis starts from an empty counter (otherwise
+  // it waits for the whole next-step prefetch before the first MFMA of every step)
+  __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0) (builtin, so the compiler's wait analysis sees it)
+  for (int t = 0; t < sq.C; ++t) {
+    uint64_t* ts = tr ? tr + 4 + t * 8 : nullptr;
+    if (ts) ts[0] = clock64();
+    const bool zero_h = !valid || t == 0 || zreset[lane] != 0;
+    if (g < 2 && t + 1 < sq.C) load_gi(t + 1, nxt0, nxt1);   // prefetch next step's inputs
+    if (rst_loader && t + 1 < sq.C && valid) rst_raw = sq.reset[(int64_t)t * sq.reset_st + e];
+    // h_{t-1} (+0.0 after a reset): unconditional LDS reads masked bitwise, no per-element branches
+    const uint32_t keep = zero_h ? 0u : 0xFFFFFFFFu;
+    f32x16 h0[HB];
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) h0[kb][s] = __uint_as_float(__float_as_uint(hx[t & 1][kb][s][lane]) & keep);
+    f32x16 acc;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc[s] = gin0[s];
+#pragma unroll
+    for (int kb = 0; kb < HB; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = mfma32(fz[kb][s], h0[kb][s], acc);
+    if (ts) ts[1] = clock64() + (uint64_t)acc[0] * 0;
+    // each gate wave finishes its own gate before the hand-over (the r-wave's critical section after
+    // barrier A is then only n and h'): z-wave z = sigmoid, n-wave the raw W_hn h + b_hn; both stage
+    // their save field
+    const int el0 = lane & 31;
+    if (g == 0) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc[s] = sigmoidf_(acc[s]);   // r
+    } else {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const float v = g == 1 ? sigmoidf_(acc[s]) : acc[s];
+        gx[g - 1][hb][s][lane] = v;
+        if (io.save) svs[t & 1][hb][g == 1 ? 2 : 4][kperm(s, hh)][el0] = v;
+      }
+    }
+    lds_sync();   // A: gate values visible
+    if (ts) ts[2] = clock64();
+    if (g == 0) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        float h0v = h0[0][s];
+#pragma unroll
+        for (int kb = 1; kb < HB; ++kb)
+          if (kb == hb) h0v = h0[kb][s];
+        const float r = acc[s];
+        const float z = gx[0][hb][s][lane];
+        const float anh = gx[1][hb][s][lane];
+        const float n = tanhf_(gin1[s] + r * anh);
+        const float h1v = n + z * (h0v - n);
+        hx[(t + 1) & 1][hb][s][lane] = h1v;
+        if (s == 0 && rst_loader) zreset[lane] = rst_raw;   // read by every gate wave after barrier B
+        if (io.save) {
+          const int fs = kperm(s, hh);
+          svs[t & 1][hb][0][fs][el0] = h0v;
+          svs[t & 1][hb][1][fs][el0] = r;
+          svs[t & 1][hb][3][fs][el0] = n;
+          svs[t & 1][hb][5][fs][el0] = h1v;
+        }
+      }
+    } else if (saver && t > 0) {
+      write_saves(t - 1);   // step t-1 rows, complete since barrier B of step t-1
+    }
+    if (ts) ts[3] = clock64();
+    lds_sync();   // B: new hidden of step t complete
+    if (ts) ts[4] = clock64();
+    if (g < 2) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        gin0[s] = nxt0[s];
+        gin1[s] = nxt1[s];
+      }
+    }
+  }
+  if (saver) write_saves(sq.C - 1);
+  if (tr) tr[1] = clock64();
 }
 
 // The two nets take separate (inlined) copies of the body: each copy reads its own kernel arguments
@@ -1424,6 +1581,18 @@ template <int F1, int G, int H, int AB>
 static int launch_split(int phase, QFwdParams p0, QFwdParams p1, hipStream_t s) {
   const bool single = p1.nblocks == 0;   // one net only (agent_q_split2 with io1 == NULL)
   if (phase == 1) {
+    const int t0 = (p0.E + 31) / 32 * p0.N, t1 = single ? 0 : (p1.E + 31) / 32 * p1.N;
+    static const char* rb_env = getenv("MM_PRE_RB");   // "0": the 128-rows-per-block PRE (A/B)
+    if (t0 + t1 <= 2048 && p0.g.KD <= kPreRbMaxKD && !(rb_env && rb_env[0] == '0')) {
+      // small batches: row blocks of each layer on separate waves (latency-bound regime)
+      p0.nblocks = t0;
+      p1.nblocks = t1;
+      constexpr int NW = 3 * (H / 32) > F1 / 32 ? 3 * (H / 32) : F1 / 32;
+      static_assert(NW >= G / 32, "layer-2 row blocks need a wave each");
+      hipLaunchKernelGGL((agent_pre_rb_kernel<F1, G, H, AB>), dim3(t0 + t1), dim3(64 * NW), 0, s, p0, p1);
+      MM_HIP_CHECK(hipGetLastError());
+      return MM_OK;
+    }
     const int nb = p0.nblocks + p1.nblocks;
     hipLaunchKernelGGL((agent_split_kernel<F1, G, H, AB, 1>), dim3(nb), dim3(256), 0, s, p0, p1);
   } else {

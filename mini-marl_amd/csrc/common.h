@@ -54,6 +54,50 @@ __device__ __forceinline__ float rng_uniform(uint64_t r) { return (float)(r >> 4
 // environment variable is set (kernels record clock64() into it); mm_debug_trace copies it out.
 uint64_t* debug_trace_buffer(const char* env_name);
 
+// ---- LDS-DMA (global_load_lds_dword): loads that write LDS directly, no VGPR destination. The LDS
+// address of lane L is (wave-uniform base) + 4 L; the global address is per lane, so a rolled loop of
+// these is a compact gather (no unrolled register staging: the code of a one-pass prologue costs
+// instruction-cache misses) whose loads are all in flight at once. Completion: vmcnt, so a
+// __syncthreads() (whose fence waits vmcnt(0) while an LDS-DMA is pending) before the data is read.
+typedef __attribute__((address_space(3))) void lds_void_t;
+__device__ __forceinline__ void glds_dword(const void* g, float* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_base, 4, 0, 0);
+}
+// dst[i] = *addr(i) for i < n (dst contiguous in LDS)
+template <typename A>
+__device__ __forceinline__ void glds_gather(float* dst, int n, A addr) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int c0 = (int)(threadIdx.x >> 6) * 64; c0 < n; c0 += nw * 64)
+    if (c0 + lane < n) glds_dword(addr(c0 + lane), dst + c0);
+}
+// dst[r * ld + j] = *addr(r, j) for r < rows, j < rowlen (a padded LDS image: one wave-instruction
+// per 64-word piece of a row, so no instruction's words cross a row)
+template <typename A>
+__device__ __forceinline__ void glds_rows(float* dst, int rows, int rowlen, int ld, A addr) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int pr = (rowlen + 63) >> 6;   // pieces per row
+  for (int q = (int)(threadIdx.x >> 6); q < rows * pr; q += nw) {
+    const int r = q / pr, c0 = (q - r * pr) * 64;
+    if (c0 + lane < rowlen) glds_dword(addr(r, c0 + lane), dst + r * ld + c0);
+  }
+}
+
+// 16-byte LDS-DMA: LDS[base + 16 L .. +15] = 16 bytes at g (16-byte aligned on both sides)
+__device__ __forceinline__ void glds_dwordx4(const void* g, float* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds_base, 16, 0, 0);
+}
+// dst[r * ld + j] = src(r)[j] for r < rows, j < rowlen: contiguous source rows, 16-byte pieces (rowlen,
+// ld multiples of 4 floats; src(r) and dst 16-byte aligned); one wave-instruction per 256-float piece
+template <typename S>
+__device__ __forceinline__ void glds_rows16(float* dst, int rows, int rowlen, int ld, S src) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int pr = (rowlen + 255) >> 8;   // pieces per row
+  for (int q = (int)(threadIdx.x >> 6); q < rows * pr; q += nw) {
+    const int r = q / pr, c0 = (q - r * pr) * 256;
+    if (c0 + 4 * lane < rowlen) glds_dwordx4(src(r) + c0 + 4 * lane, dst + r * ld + c0);
+  }
+}
+
 // Workgroup barrier that orders LDS only: waits for this wave's outstanding LDS operations, then
 // s_barrier. Unlike __syncthreads() it does not wait for outstanding global stores, so a sequence
 // kernel whose waves communicate through LDS does not stall every step on its own result writes.

@@ -332,10 +332,81 @@ __device__ __forceinline__ void mixer_fwd_body(const MixFwdArgs& a, const MixFwd
   }
 }
 
+constexpr int MIX_SPB = 8;
+// Hypernets + mixing of MIX_SPB rows b0 .. b0 + ns - 1 whose new mixer hidden is in h1 [SPB][Hm]
+// (LDS; rows >= ns zero): hyp = W_hyp h1 + b (sequential k, bias last), y_pre, Q_tot, the save-row tail.
+// hyp [SPB][RW], yp [SPB][K1] LDS scratch. Rows index nt.q / qtot / save directly (a flat row range).
+__device__ __forceinline__ void mixer_hyper_rows(const MixFwdArgs& a, const MixFwdNet& nt, int b0, int ns,
+                                                 const float* h1, float* hyp, float* yp) {
+  const int Hm = a.Hm, K1 = a.K1, N = a.N, NK = N * K1, RW = NK + 3 * K1;
+  const MixOff o = mix_offsets(a.S, Hm, K1, N);
+  // hypernets on h1 (rows: w1 [NK], b1 [K1], w2 [K1], b2 hidden [K1])
+  for (int r = threadIdx.x; r < RW; r += blockDim.x) {
+    const float* w;
+    float bb;
+    if (r < NK) {
+      w = nt.P + o.w1W + (int64_t)r * Hm;
+      bb = nt.P[o.w1b + r];
+    } else if (r < NK + K1) {
+      w = nt.P + o.b1W + (int64_t)(r - NK) * Hm;
+      bb = nt.P[o.b1b + r - NK];
+    } else if (r < NK + 2 * K1) {
+      w = nt.P + o.w2W + (int64_t)(r - NK - K1) * Hm;
+      bb = nt.P[o.w2b + r - NK - K1];
+    } else {
+      w = nt.P + o.b2aW + (int64_t)(r - NK - 2 * K1) * Hm;
+      bb = nt.P[o.b2ab + r - NK - 2 * K1];
+    }
+    float acc[MIX_SPB];
+#pragma unroll
+    for (int q = 0; q < MIX_SPB; ++q) acc[q] = 0.f;
+    for (int k = 0; k < Hm; ++k) {
+      const float wk = w[k];
+#pragma unroll
+      for (int q = 0; q < MIX_SPB; ++q) acc[q] += wk * h1[q * Hm + k];
+    }
+#pragma unroll
+    for (int q = 0; q < MIX_SPB; ++q) hyp[q * RW + r] = acc[q] + bb;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
+    const int sI = idx / K1, k = idx % K1, b = b0 + sI;
+    const float* hp = hyp + sI * RW;
+    float acc = 0.f;
+    for (int i = 0; i < N; ++i) acc += fabsf(hp[k * N + i]) * nt.q[(int64_t)b * N + i];
+    yp[sI * K1 + k] = acc + hp[NK + k];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < ns) {
+    const int sI = threadIdx.x, b = b0 + sI;
+    const float* hp = hyp + sI * RW;
+    const float* w2raw = hp + NK + K1;
+    const float* b2pre = hp + NK + 2 * K1;
+    float b2 = 0.f;
+    for (int k = 0; k < K1; ++k) b2 += nt.P[o.b2bW + k] * fmaxf(b2pre[k], 0.f);
+    b2 += nt.P[o.b2bb];
+    float acc = 0.f;
+    for (int k = 0; k < K1; ++k) acc += fabsf(w2raw[k]) * fmaxf(yp[sI * K1 + k], 0.f);
+    nt.qtot[b] = acc + b2;
+    if (nt.save) nt.save[(int64_t)b * mix_save_dim(Hm, K1, N) + 6 * Hm + NK + 4 * K1] = b2;
+  }
+  if (nt.save) {
+    for (int idx = threadIdx.x; idx < ns * RW; idx += blockDim.x) {
+      const int sI = idx / RW, i = idx % RW;
+      float* sv = nt.save + (int64_t)(b0 + sI) * mix_save_dim(Hm, K1, N);
+      const float v = hyp[sI * RW + i];
+      sv[6 * Hm + i] = i >= NK + 2 * K1 ? fmaxf(v, 0.f) : v;
+    }
+    for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
+      const int sI = idx / K1, k = idx % K1;
+      nt.save[(int64_t)(b0 + sI) * mix_save_dim(Hm, K1, N) + 6 * Hm + NK + 3 * K1 + k] = yp[sI * K1 + k];
+    }
+  }
+}
+
 // Large batches: MIX_SPB samples per block share every weight read (the single-sample block re-reads
 // ~140 KB of W_hh + hypernet weights from L2 per sample). Same per-sample arithmetic and order as
 // mixer_fwd_body (bit-identical); needs the precomputed input projection (nt.gi).
-constexpr int MIX_SPB = 8;
 __global__ __launch_bounds__(256) void mixer_fwd_multi_kernel(MixFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const MixFwdNet& nt = a.net[blockIdx.y];
@@ -401,68 +472,7 @@ __global__ __launch_bounds__(256) void mixer_fwd_multi_kernel(MixFwdArgs a) {
     }
   }
   __syncthreads();
-  // hypernets on h1 (rows: w1 [NK], b1 [K1], w2 [K1], b2 hidden [K1])
-  for (int r = threadIdx.x; r < RW; r += blockDim.x) {
-    const float* w;
-    float bb;
-    if (r < NK) {
-      w = nt.P + o.w1W + (int64_t)r * Hm;
-      bb = nt.P[o.w1b + r];
-    } else if (r < NK + K1) {
-      w = nt.P + o.b1W + (int64_t)(r - NK) * Hm;
-      bb = nt.P[o.b1b + r - NK];
-    } else if (r < NK + 2 * K1) {
-      w = nt.P + o.w2W + (int64_t)(r - NK - K1) * Hm;
-      bb = nt.P[o.w2b + r - NK - K1];
-    } else {
-      w = nt.P + o.b2aW + (int64_t)(r - NK - 2 * K1) * Hm;
-      bb = nt.P[o.b2ab + r - NK - 2 * K1];
-    }
-    float acc[MIX_SPB];
-#pragma unroll
-    for (int q = 0; q < MIX_SPB; ++q) acc[q] = 0.f;
-    for (int k = 0; k < Hm; ++k) {
-      const float wk = w[k];
-#pragma unroll
-      for (int q = 0; q < MIX_SPB; ++q) acc[q] += wk * h1[q * Hm + k];
-    }
-#pragma unroll
-    for (int q = 0; q < MIX_SPB; ++q) hyp[q * RW + r] = acc[q] + bb;
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
-    const int sI = idx / K1, k = idx % K1, b = b0 + sI;
-    const float* hp = hyp + sI * RW;
-    float acc = 0.f;
-    for (int i = 0; i < N; ++i) acc += fabsf(hp[k * N + i]) * nt.q[(int64_t)b * N + i];
-    yp[sI * K1 + k] = acc + hp[NK + k];
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < ns) {
-    const int sI = threadIdx.x, b = b0 + sI;
-    const float* hp = hyp + sI * RW;
-    const float* w2raw = hp + NK + K1;
-    const float* b2pre = hp + NK + 2 * K1;
-    float b2 = 0.f;
-    for (int k = 0; k < K1; ++k) b2 += nt.P[o.b2bW + k] * fmaxf(b2pre[k], 0.f);
-    b2 += nt.P[o.b2bb];
-    float acc = 0.f;
-    for (int k = 0; k < K1; ++k) acc += fabsf(w2raw[k]) * fmaxf(yp[sI * K1 + k], 0.f);
-    nt.qtot[b] = acc + b2;
-    if (nt.save) nt.save[(int64_t)b * mix_save_dim(Hm, K1, N) + 6 * Hm + NK + 4 * K1] = b2;
-  }
-  if (nt.save) {
-    for (int idx = threadIdx.x; idx < ns * RW; idx += blockDim.x) {
-      const int sI = idx / RW, i = idx % RW;
-      float* sv = nt.save + (int64_t)(b0 + sI) * mix_save_dim(Hm, K1, N);
-      const float v = hyp[sI * RW + i];
-      sv[6 * Hm + i] = i >= NK + 2 * K1 ? fmaxf(v, 0.f) : v;
-    }
-    for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
-      const int sI = idx / K1, k = idx % K1;
-      nt.save[(int64_t)(b0 + sI) * mix_save_dim(Hm, K1, N) + 6 * Hm + NK + 3 * K1 + k] = yp[sI * K1 + k];
-    }
-  }
+  mixer_hyper_rows(a, nt, b0, ns, h1, hyp, yp);
 }
 
 // ------------------------------------------------------------------ mixer sequences with LDS-resident weights
@@ -868,6 +878,7 @@ __device__ __forceinline__ void mixer_bwd_body(const MixBwdArgs& a, int b) {
 // block_matvec_t for MIX_SPB samples at once: out[q][c] += sum_r W[r][c] d[q][r]; every W element
 // read serves all samples. Per sample the partial-sum order is block_matvec_t's (bit-identical).
 // red: [MIX_SPB][nw][K] floats.
+template <bool ACC = true>
 __device__ void block_matvec_t_multi(const float* __restrict__ W, int rows, int K, const float* d, int ds,
                                      float* out, int os, float* red) {
   constexpr int Q = MIX_SPB;
@@ -902,7 +913,10 @@ __device__ void block_matvec_t_multi(const float* __restrict__ W, int rows, int 
     const int q = idx / K, c = idx % K;
     float acc = 0.f;
     for (int v = 0; v < nw; ++v) acc += red[(q * nw + v) * K + c];
-    out[q * os + c] += acc;
+    if (ACC)
+      out[q * os + c] += acc;
+    else
+      out[q * os + c] = acc;
   }
   __syncthreads();
 }
@@ -916,7 +930,6 @@ __global__ __launch_bounds__(256) void mixer_bwd_seq_multi_kernel(MixBwdArgs a0,
   const MixOff o = mix_offsets(a0.S, Hm, K1, N);
   const int b0 = blockIdx.x * Q;
   const int ns = min(Q, a0.B - b0);
-  const int nw = blockDim.x >> 6;
   float* dhm1 = sm;                 // [Q][Hm]
   float* dgh = dhm1 + Q * Hm;       // [Q][3Hm]
   float* shd = dgh + Q * 3 * Hm;    // [Q][SH]
@@ -1168,6 +1181,429 @@ __global__ __launch_bounds__(256) void mixer_bwd_seq_lds_kernel(MixBwdArgs a, Mi
   for (int c = ti; c < Hm; c += blockDim.x) a.dhm[(int64_t)b * Hm + c] = dhm[c];
 }
 
+// ------------------------------------------------------------------ split mixer sequences (B < 512)
+// The mixer GRU over Hm is the only serial part of a chunk: the hypernets and the mixing read a step's
+// new hidden but feed nothing back into the recurrence. So each direction runs as two launches:
+//   forward : mixer_rec_fwd_kernel  (block per (sample, net): W_hh in LDS, C steps of gh + gates,
+//                                    writes the hidden sequence) ->
+//             mixer_hyper_fwd_kernel (all C*B rows at once, MIX_SPB rows per block: mixer_hyper_rows)
+//   backward: mixer_hyper_bwd_kernel (all rows at once: hypernet deltas, dqa and the four hypernet
+//                                    input-gradient mat-vecs X_j = W_j^T d_j, kept apart) ->
+//             mixer_rec_bwd_kernel  (block per sample: dh = ((((future + X_0) + X_1) + X_2) + X_3),
+//                                    GRU backward, dh_prev = dh z + W_hh^T dgh)
+// Each value keeps mixer_fwd_body / mixer_bwd_body's arithmetic and summation order (bit-identical to
+// the per-step launches). The serial kernels load a window of steps' inputs into LDS with one round
+// of loads, so their step loops issue only stores (on gfx9 every load wait also drains the stores
+// issued before it) and synchronise with two LDS-only barriers per step.
+struct MixRecFwd {
+  int C, win;
+  int64_t gi_st, hout_st, save_st;
+  const uint8_t* reset_steps;   // [C-1][B]: step t >= 1 starts from zero hidden where set
+  uint64_t* trace;              // clock64 stamps of block 0 (MM_MIX_TRACE), nullptr normally
+};
+struct MixRecBwd {
+  int C, win;
+  int64_t save_st, delta_st, done_st;
+  const float* done;   // [C][B] done of step t (t = C-1: no future, always dropped)
+  const float* xws;    // [C][B][4][Hm] hypernet input gradients (mixer_hyper_bwd_kernel)
+  const float* ones;   // [B] of 1.0 (done of the last step)
+  uint64_t* trace;     // clock64 stamps of block 0 (MM_MIX_TRACE), nullptr normally
+};
+
+// rows x K row-major global matrix -> LDS image with row stride ld; each wave keeps 32 rows' loads in
+// flight (lane = column, K <= 64 per pass). No trailing barrier.
+__device__ void stage_rows(const float* __restrict__ src, int rows, int K, int ld, float* img) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int c0 = 0; c0 < K; c0 += 64) {
+    const int c = c0 + lane;
+    const bool on = c < K;
+    for (int r0 = w * 32; r0 < rows; r0 += nw * 32) {
+      float v[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) v[j] = (on && r0 + j < rows) ? src[(int64_t)(r0 + j) * K + c] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if (on && r0 + j < rows) img[(r0 + j) * ld + c] = v[j];
+    }
+  }
+}
+
+// Prologue gathers. The address lambdas return a pointer to the 32-bit word to load; the loads are
+// issued UNCONDITIONALLY (out-of-range lanes load the last valid element and discard it): a load
+// under a branch becomes a copy at the join, and copying a pending load result forces the wave to wait
+// for it, serialising one memory round trip per element.
+//
+// dst[row * rowlen + j] = *addr(row, j) for row < nrows, j < rowlen, by the whole block, 16 loads in
+// flight per thread before their LDS stores, (row, j) stepped incrementally (no integer division).
+// No trailing barrier.
+template <typename A>
+__device__ __forceinline__ void block_gather_rows(float* dst, int nrows, int rowlen, A addr) {
+  constexpr int U = 16;
+  const int bd = blockDim.x, n = nrows * rowlen;
+  if (n <= 0) return;
+  int row = 0, j = threadIdx.x;
+  while (j >= rowlen) {
+    j -= rowlen;
+    ++row;
+  }
+  for (int base = threadIdx.x; base < n; base += U * bd) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = base + u * bd < n;
+      v[u] = *addr(ok ? row : nrows - 1, ok ? j : rowlen - 1);
+      j += bd;
+      while (j >= rowlen) {
+        j -= rowlen;
+        ++row;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * bd < n) dst[base + u * bd] = v[u];
+  }
+}
+
+// Register-staged gathers: every load of a prologue is issued (gather_issue: v[u] = *addr(i) for
+// i = tid + u * blockDim, clamped to n - 1) before the first LDS store that consumes one
+// (gather_commit: put(i, v) for i < n), so the prologue costs one memory round trip, not one per
+// gather (a store waits for its load and, vmcnt being in order, for all loads issued before it).
+template <int U, typename A>
+__device__ __forceinline__ void gather_issue(float (&v)[U], int n, A addr) {
+  if (n <= 0) return;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = min((int)(threadIdx.x + u * blockDim.x), n - 1);
+    v[u] = *addr(i);
+  }
+}
+template <int U, typename D>
+__device__ __forceinline__ void gather_commit(const float (&v)[U], int n, D put) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = threadIdx.x + u * blockDim.x;
+    if (i < n) put(i, v[u]);
+  }
+}
+
+// LDS row strides of the W_hh images: forward rows are read along k by one lane (b128 reads: stride
+// HM + 4 keeps 16-byte alignment and spreads 16 lanes over all 64 banks); backward columns are read
+// along r by 64 lanes (b32 reads: stride HM + 1 is conflict-free)
+template <int HM>
+struct MixRecGeo {
+  static constexpr int M3 = 3 * HM, LDF = HM + 4, LDB = HM + 1;
+  static constexpr size_t fwd_floats(int win) {
+    return (size_t)M3 * LDF + 2 * HM + 2 * M3 + (size_t)win * M3 + win + 1;
+  }
+  static constexpr size_t bwd_floats(int win) {
+    return (((size_t)M3 * LDB + M3 + 4 * HM + 3) & ~(size_t)3) + (size_t)win * (9 * HM + 1);
+  }
+};
+__host__ __device__ inline size_t mix_rec_fwd_floats(int Hm, int win) {
+  return Hm == 32 ? MixRecGeo<32>::fwd_floats(win) : MixRecGeo<64>::fwd_floats(win);
+}
+__host__ __device__ inline size_t mix_rec_bwd_floats(int Hm, int win) {
+  return Hm == 32 ? MixRecGeo<32>::bwd_floats(win) : MixRecGeo<64>::bwd_floats(win);
+}
+inline bool mix_rec_supported(int Hm) { return Hm == 32 || Hm == 64; }
+
+template <int HM>
+__device__ __forceinline__ void mixer_rec_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, const MixRecFwd& sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  using Geo = MixRecGeo<HM>;
+  constexpr int M3 = Geo::M3, LD = Geo::LDF;
+  const int b = blockIdx.x, ti = (int)threadIdx.x;
+  const MixOff o = mix_offsets(a.S, HM, a.K1, a.N);
+  float* img = sm;                 // W_hh [M3][LD]
+  float* hb = img + M3 * LD;       // [2][HM] hidden by step parity (already zero where the step resets)
+  float* gh = hb + 2 * HM;         // [M3]
+  float* bhh = gh + M3;            // [M3]
+  float* gin = bhh + M3;           // [win][M3] input projections of the window's steps
+  float* rs = gin + sq.win * M3;   // [win + 1] 1: step w0 + tt starts from zero hidden
+  uint64_t* tr = (sq.trace && b == 0 && blockIdx.y == 0 && ti == 0) ? sq.trace : nullptr;
+  if (tr) tr[0] = clock64();
+  // prologue: W_hh image, b_hh, h_in and the first window's input projections by LDS-DMA (one round
+  // trip, compact code); the reset flags by a plain load issued first
+  const int nr0 = min(sq.win, sq.C) + 1;
+  const int tr0 = min(max(ti, 1), sq.C - 1);
+  const uint8_t* rp = sq.C > 1 ? sq.reset_steps + (int64_t)(tr0 - 1) * a.B + b : (const uint8_t*)nt.P;
+  const uint8_t rflag = *rp;   // (unused when C == 1)
+  glds_rows(img, M3, HM, LD, [&](int r, int j) { return nt.P + o.gWhh + r * HM + j; });
+  glds_gather(bhh, M3, [&](int i) { return nt.P + o.gbhh + i; });
+  const bool rz = !nt.h_in || (nt.reset && nt.reset[b]);
+  if (rz) {
+    for (int i = ti; i < HM; i += blockDim.x) hb[i] = 0.f;
+  } else {
+    glds_gather(hb, HM, [&](int i) { return nt.h_in + (int64_t)b * HM + i; });
+  }
+  glds_rows16(gin, min(sq.win, sq.C), M3, M3, [&](int tt) { return nt.gi + tt * sq.gi_st + (int64_t)b * M3; });
+  if (ti < nr0) rs[ti] = (ti >= 1 && ti < sq.C && rflag != 0) ? 1.f : 0.f;
+  const int svd = mix_save_dim(HM, a.K1, a.N);
+  for (int w0 = 0; w0 < sq.C; w0 += sq.win) {
+    const int wn = min(sq.win, sq.C - w0);
+    if (w0 > 0) {   // later windows (the first one came with the prologue)
+      __syncthreads();
+      glds_rows16(gin, wn, M3, M3, [&](int tt) { return nt.gi + (w0 + tt) * sq.gi_st + (int64_t)b * M3; });
+    }
+    if (w0 > 0 || nr0 > (int)blockDim.x)
+      for (int tt = ti; tt <= wn; tt += blockDim.x) {
+        const int t = w0 + tt;
+        rs[tt] = (t >= 1 && t < sq.C && sq.reset_steps[(int64_t)(t - 1) * a.B + b] != 0) ? 1.f : 0.f;
+      }
+    __syncthreads();
+    if (tr) tr[1] = clock64();
+    for (int tt = 0; tt < wn; ++tt) {
+      const int t = w0 + tt;
+      uint64_t* ts = tr ? tr + 4 + 4 * t : nullptr;
+      const float* h0 = hb + (t & 1) * HM;
+      float* h1 = hb + ((t + 1) & 1) * HM;
+      if (ts) ts[0] = clock64();
+      // gh = W_hh h0 + b_hh (block_matvec order: sequential k from 0, bias last), 4 k per LDS read
+      for (int r = ti; r < M3; r += blockDim.x) {
+        const float* wr = img + r * LD;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < HM; k += 4) {
+          const float4 w4 = *reinterpret_cast<const float4*>(wr + k);
+          const float4 x4 = *reinterpret_cast<const float4*>(h0 + k);
+          acc += w4.x * x4.x;
+          acc += w4.y * x4.y;
+          acc += w4.z * x4.z;
+          acc += w4.w * x4.w;
+        }
+        gh[r] = acc + bhh[r];
+      }
+      if (ts) ts[1] = clock64() + (uint64_t)gh[0] * 0;
+      lds_sync();
+      if (ts) ts[2] = clock64();
+      const float* gI = gin + tt * M3;
+      const bool zero_next = rs[tt + 1] != 0.f;
+      float* sv = nt.save ? nt.save + t * sq.save_st + (int64_t)b * svd : nullptr;
+      for (int i = ti; i < HM; i += blockDim.x) {
+        const float r = sigmoidf_(gI[i] + gh[i]);
+        const float z = sigmoidf_(gI[HM + i] + gh[HM + i]);
+        const float n = tanhf_(gI[2 * HM + i] + r * gh[2 * HM + i]);
+        const float h0v = h0[i];
+        const float hv = n + z * (h0v - n);
+        h1[i] = zero_next ? 0.f : hv;
+        nt.h_out[t * sq.hout_st + (int64_t)b * HM + i] = hv;
+        if (sv) {
+          sv[i] = h0v;
+          sv[HM + i] = r;
+          sv[2 * HM + i] = z;
+          sv[3 * HM + i] = n;
+          sv[4 * HM + i] = gh[2 * HM + i];
+          sv[5 * HM + i] = hv;
+        }
+      }
+      if (ts) ts[3] = clock64();
+      lds_sync();
+    }
+  }
+  if (tr) tr[2] = clock64();
+}
+
+// one inlined body per net: each reads its own kernel-argument fields with scalar loads
+template <int HM>
+__global__ __launch_bounds__(256) void mixer_rec_fwd_kernel(MixFwdArgs a, MixRecFwd sq) {
+  if (blockIdx.y == 0)
+    mixer_rec_fwd_body<HM>(a, a.net[0], sq);
+  else
+    mixer_rec_fwd_body<HM>(a, a.net[1], sq);
+}
+
+// all R = C*B rows of one net: the hidden sequence (h_out) -> hypernets, Q_tot, save-row tail
+__device__ __forceinline__ void mixer_hyper_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, int R) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int Hm = a.Hm, K1 = a.K1, RW = a.N * K1 + 3 * K1;
+  const int b0 = blockIdx.x * MIX_SPB;
+  const int ns = min(MIX_SPB, R - b0);
+  float* h1 = sm;                    // [SPB][Hm]
+  float* hyp = h1 + MIX_SPB * Hm;    // [SPB][RW]
+  float* yp = hyp + MIX_SPB * RW;    // [SPB][K1]
+  for (int idx = threadIdx.x; idx < MIX_SPB * Hm; idx += blockDim.x)
+    h1[idx] = idx / Hm < ns ? nt.h_out[(int64_t)b0 * Hm + idx] : 0.f;
+  __syncthreads();
+  mixer_hyper_rows(a, nt, b0, ns, h1, hyp, yp);
+}
+__global__ __launch_bounds__(256) void mixer_hyper_fwd_kernel(MixFwdArgs a, int R) {
+  if (blockIdx.y == 0)
+    mixer_hyper_fwd_body(a, a.net[0], R);
+  else
+    mixer_hyper_fwd_body(a, a.net[1], R);
+}
+__host__ __device__ inline size_t mix_hyper_fwd_floats(int Hm, int K1, int N) {
+  return (size_t)MIX_SPB * (Hm + N * K1 + 3 * K1 + K1);
+}
+
+// all R = C*B rows at once (flat row arrays: save [R][MSD], qa [R][N], dq [R], dqa [R][N],
+// delta [R][MDD]): mixer_bwd_body's hypernet deltas + dqa, and X_j = W_j^T d_j (j = w1, b1, w2, b2a)
+// stored apart in xws [R][4][Hm] (the serial kernel adds them to the future gradient in order).
+__global__ __launch_bounds__(256) void mixer_hyper_bwd_kernel(MixBwdArgs a, int R, float* xws) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int Q = MIX_SPB;
+  const int Hm = a.Hm, K1 = a.K1, N = a.N, NK = N * K1, SH = NK + 3 * K1;
+  const MixOff o = mix_offsets(a.S, Hm, K1, N);
+  const int b0 = blockIdx.x * Q;
+  const int ns = min(Q, R - b0);
+  float* shd = sm;                  // [Q][SH]
+  float* xo = shd + Q * SH;         // [Q][4][Hm]
+  float* red = xo + Q * 4 * Hm;     // [Q][4 waves][Hm]
+  const int svd = mix_save_dim(Hm, K1, N), dld = mix_delta_dim(Hm, K1, N);
+  for (int idx = threadIdx.x; idx < Q * SH; idx += blockDim.x) shd[idx] = 0.f;
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
+    const int s = idx / K1, k = idx % K1, b = b0 + s;
+    const float* w1raw = a.save + (int64_t)b * svd + 6 * Hm;
+    const float* w2raw = w1raw + NK + K1;
+    const float* b2pre = w2raw + K1;
+    const float* ypre = b2pre + K1;
+    float* dl = a.delta + (int64_t)b * dld;
+    float* sh = shd + s * SH;
+    const float dQ = a.dq[b];
+    const float y = fmaxf(ypre[k], 0.f);
+    const float w2 = w2raw[k];
+    const float dw2 = dQ * y * (w2 > 0.f ? 1.f : (w2 < 0.f ? -1.f : 0.f));
+    const float dyp = ypre[k] > 0.f ? dQ * fabsf(w2) : 0.f;
+    const float db2p = b2pre[k] > 0.f ? dQ * a.P[o.b2bW + k] : 0.f;
+    dl[6 * Hm + NK + k] = dyp;
+    dl[6 * Hm + NK + K1 + k] = dw2;
+    dl[6 * Hm + NK + 2 * K1 + k] = db2p;
+    sh[NK + k] = dyp;
+    sh[NK + K1 + k] = dw2;
+    sh[NK + 2 * K1 + k] = db2p;
+    for (int i = 0; i < N; ++i) {
+      const float wv = w1raw[k * N + i];
+      const float dw1 = dyp * a.qa[(int64_t)b * N + i] * (wv > 0.f ? 1.f : (wv < 0.f ? -1.f : 0.f));
+      dl[6 * Hm + k * N + i] = dw1;
+      sh[k * N + i] = dw1;
+    }
+  }
+  if ((int)threadIdx.x < ns) {
+    const int b = b0 + threadIdx.x;
+    a.delta[(int64_t)b * dld + 6 * Hm + NK + 3 * K1] = a.dq[b];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < ns * N; idx += blockDim.x) {
+    const int s = idx / N, i = idx % N, b = b0 + s;
+    const float* w1raw = a.save + (int64_t)b * svd + 6 * Hm;
+    float acc = 0.f;
+    for (int k = 0; k < K1; ++k) acc += shd[s * SH + NK + k] * fabsf(w1raw[k * N + i]);
+    a.dqa[(int64_t)b * N + i] = acc;
+  }
+  block_matvec_t_multi<false>(a.P + o.w1W, NK, Hm, shd, SH, xo, 4 * Hm, red);
+  block_matvec_t_multi<false>(a.P + o.b1W, K1, Hm, shd + NK, SH, xo + Hm, 4 * Hm, red);
+  block_matvec_t_multi<false>(a.P + o.w2W, K1, Hm, shd + NK + K1, SH, xo + 2 * Hm, 4 * Hm, red);
+  block_matvec_t_multi<false>(a.P + o.b2aW, K1, Hm, shd + NK + 2 * K1, SH, xo + 3 * Hm, 4 * Hm, red);
+  for (int idx = threadIdx.x; idx < ns * 4 * Hm; idx += blockDim.x) xws[(int64_t)b0 * 4 * Hm + idx] = xo[idx];
+}
+__host__ __device__ inline size_t mix_hyper_bwd_floats(int Hm, int K1, int N) {
+  return (size_t)MIX_SPB * (N * K1 + 3 * K1 + 4 * Hm + 4 * Hm);
+}
+
+template <int HM>
+__global__ __launch_bounds__(256) void mixer_rec_bwd_kernel(MixBwdArgs a, MixRecBwd sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  using Geo = MixRecGeo<HM>;
+  constexpr int M3 = Geo::M3, LD = Geo::LDB, NW = 4;   // 256 threads = 4 waves
+  static_assert(M3 % (4 * NW) == 0, "W_hh^T partial loop assumes 16 | 3 Hm");
+  const int b = blockIdx.x, ti = (int)threadIdx.x;
+  const MixOff o = mix_offsets(a.S, HM, a.K1, a.N);
+  const int svd = mix_save_dim(HM, a.K1, a.N), dld = mix_delta_dim(HM, a.K1, a.N);
+  constexpr int SI = 9 * HM;       // per-step inputs: hm0 r z n anh (5Hm) | X_0..X_3 (4Hm); done apart
+  float* img = sm;                 // W_hh [M3][LD]
+  float* dgh = img + M3 * LD;      // [M3]
+  float* red = dgh + M3;           // [4][HM] wave partials of W_hh^T dgh
+  static_assert(SI % 4 == 0, "16-byte rows");
+  float* inw = sm + ((M3 * LD + M3 + 4 * HM + 3) & ~3);   // [win][SI] (16-byte aligned)
+  float* dnw = inw + sq.win * SI;  // [win] done flags
+  uint64_t* tr = (sq.trace && b == 0 && ti == 0) ? sq.trace : nullptr;
+  if (tr) tr[0] = clock64();
+  const int lane = ti & 63, w = ti >> 6;
+  // a window of step inputs: save rows (word pieces: rows are not 16-byte aligned), the X rows
+  // (16-byte pieces) and the done flags
+  auto load_window = [&](int w0, int wn) {
+    glds_rows(inw, wn, 5 * HM, SI, [&](int tt, int j) { return a.save + (w0 + tt) * sq.save_st + (int64_t)b * svd + j; });
+    glds_rows16(inw + 5 * HM, wn, 4 * HM, SI, [&](int tt) { return sq.xws + ((int64_t)(w0 + tt) * a.B + b) * 4 * HM; });
+    glds_gather(dnw, wn, [&](int tt) {
+      const int t = w0 + tt;
+      return t == sq.C - 1 ? sq.ones + b : sq.done + t * sq.done_st + b;
+    });
+  };
+  // prologue: W_hh image + the last window's step inputs by LDS-DMA (one round trip, compact code)
+  const int wfirst = min(sq.win, sq.C);
+  glds_rows(img, M3, HM, LD, [&](int r, int j) { return a.P + o.gWhh + r * HM + j; });
+  load_window(sq.C - wfirst, wfirst);
+  float dhm_c = a.dhm[(int64_t)b * HM + min(ti, HM - 1)];   // carried by thread c = ti (>= HM: unused)
+  for (int w1 = sq.C; w1 > 0; w1 -= sq.win) {
+    const int w0 = max(0, w1 - sq.win), wn = w1 - w0;
+    if (w1 != sq.C) {   // later windows (the first one came with the prologue)
+      __syncthreads();
+      load_window(w0, wn);
+    }
+    __syncthreads();
+    if (tr) tr[1] = clock64();
+    for (int tt = wn - 1; tt >= 0; --tt) {
+      const int t = w0 + tt;
+      uint64_t* ts = tr ? tr + 4 + 4 * t : nullptr;
+      if (ts) ts[0] = clock64();
+      const float* in = inw + tt * SI;
+      float shd_c = 0.f;
+      if (ti < HM) {
+        const int i = ti;
+        float dh = dnw[tt] > 0.5f ? 0.f : dhm_c;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dh = dh + in[(5 + j) * HM + i];
+        const float r = in[HM + i], z = in[2 * HM + i], n = in[3 * HM + i];
+        const float dn = dh * (1.f - z);
+        const float dz = dh * (in[i] - n);
+        const float dpn = dn * (1.f - n * n);
+        const float dr = dpn * in[4 * HM + i];
+        const float dar = dr * r * (1.f - r);
+        const float daz = dz * z * (1.f - z);
+        float* dl = a.delta + t * sq.delta_st + (int64_t)b * dld;
+        dl[i] = dar;
+        dl[HM + i] = daz;
+        dl[2 * HM + i] = dpn;
+        dl[3 * HM + i] = dar;
+        dl[4 * HM + i] = daz;
+        dl[5 * HM + i] = dpn * r;
+        dgh[i] = dar;
+        dgh[HM + i] = daz;
+        dgh[2 * HM + i] = dpn * r;
+        shd_c = dh * z;
+      }
+      if (ts) ts[1] = clock64();
+      lds_sync();
+      // W_hh^T dgh: block_matvec_t_ld's per-wave partials (rows r = w mod 4, 4 interleaved sums)
+      if (lane < HM) {
+        const int c = lane;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+        for (int q = 0; q < M3 / (4 * NW); ++q) {
+          const int r = w + 4 * NW * q;
+          a0 += img[r * LD + c] * dgh[r];
+          a1 += img[(r + NW) * LD + c] * dgh[r + NW];
+          a2 += img[(r + 2 * NW) * LD + c] * dgh[r + 2 * NW];
+          a3 += img[(r + 3 * NW) * LD + c] * dgh[r + 3 * NW];
+        }
+        red[w * HM + c] = (a0 + a1) + (a2 + a3);
+      }
+      if (ts) ts[2] = clock64();
+      lds_sync();
+      if (ti < HM) {
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) acc += red[q * HM + ti];
+        dhm_c = shd_c + acc;
+      }
+      if (ts) ts[3] = clock64() + (uint64_t)dhm_c * 0;
+    }
+  }
+  if (tr) tr[2] = clock64();
+  if (ti < HM) a.dhm[(int64_t)b * HM + ti] = dhm_c;
+}
+
 // dynamic-LDS limit of the sequence kernels (MI355X: 160 KB per CU, one block per CU)
 constexpr size_t kMixSeqLds = 160 * 1024;
 static int mix_seq_lds_setup() {
@@ -1177,6 +1613,10 @@ static int mix_seq_lds_setup() {
                                    (int)kMixSeqLds));
   MM_HIP_CHECK(hipFuncSetAttribute((const void*)mixer_bwd_seq_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)kMixSeqLds));
+  const void* serial[] = {(const void*)mixer_rec_fwd_kernel<32>, (const void*)mixer_rec_fwd_kernel<64>,
+                          (const void*)mixer_rec_bwd_kernel<32>, (const void*)mixer_rec_bwd_kernel<64>};
+  for (const void* k : serial)
+    MM_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMixSeqLds));
   done = true;
   return MM_OK;
 }
@@ -1249,107 +1689,151 @@ __device__ __forceinline__ void agent_bwd_body(const AgentBwdArgs& a) {
 }
 
 // Chunk-sequence agent backward (small batches): block = one agent x 4 samples (one wave each, lane =
-// hidden feature) for ALL C steps, the agent's W_hh staged once into LDS (48 KB at H = 64) and the
-// hidden-state gradient carried in registers between steps. Per-step arithmetic and summation order
-// are agent_bwd_body's (bit-identical to the per-step launches).
+// hidden feature) for ALL C steps. The agent's W_hh is staged once into LDS TRANSPOSED ([f][r], row
+// stride 3H + 4: a lane's 4 consecutive r are one conflict-free ds_read_b128), the step inputs of a
+// window of steps are loaded into LDS with one round of loads (the step loop then issues only stores,
+// so no load wait ever drains them), and the hidden-state gradient is carried in registers. The waves
+// never exchange data, so the step loop has no block barrier. Per-step arithmetic and the sequential
+// r order of the W_hh^T mat-vec are agent_bwd_body's (bit-identical to the per-step launches).
 struct AgentBwdSeq {
-  int C;
+  int C, win;
   int64_t save_st, acts_st, dqa_st, dgi_st, dq_st, done_st;
   const float* ones;
+  uint64_t* trace;     // clock64 stamps of block 0 wave 0 (MM_ABWD_TRACE), nullptr normally
 };
+__host__ __device__ inline size_t agent_bwd_seq_floats(int H, int A, int win) {
+  return (size_t)H * (3 * H + 4) + 3 * (size_t)H * H + 4 * 3 * (size_t)H + (size_t)A * H + 4 +
+         4 * (size_t)win * (5 * H + 3);
+}
+template <int H>
 __global__ __launch_bounds__(256) void agent_bwd_seq_kernel(AgentBwdArgs a, AgentBwdSeq sq) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int H = a.H, A = a.A, H3 = 3 * H;
-  float* whh = sm;                 // [3H][H]
-  float* sdg = whh + H3 * H;       // [4][3H]
+  constexpr int H3 = 3 * H, LDT = H3 + 4, SI = 5 * H;   // input rows: 16-byte aligned (H % 4 == 0)
+  const int A = a.A;
+  float* whT = sm;                 // [H][LDT]: whT[f * LDT + r] = W_hh[r][f]
+  float* whr = whT + H * LDT;      // [3H][H] W_hh as loaded (row-major), transposed into whT
+  float* sdg = whr + H3 * H;       // [4][3H] this wave's gate gradients
   float* wq = sdg + 4 * H3;        // [A][H]
+  float* inw = wq + ((A * H + 3) & ~3);   // [win][4][5H]: h0 r z n anh of (step, wave)
+  float* scw = inw + sq.win * 4 * SI;      // [win][4][3]: act (int bits) | dQ(a) | done
   const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
   const int i = blockIdx.y;
   const int b = blockIdx.x * 4 + w;
   const bool on = b < a.B && f < H;
   const int64_t pair = (int64_t)(b < a.B ? b : 0) * a.N + i;
   const int SD = a.F1 + a.G + 6 * H;
+  uint64_t* tr = (sq.trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) ? sq.trace : nullptr;
+  if (tr) tr[0] = clock64();
   const float* Wq_g = a.P + a.oWq + (int64_t)i * A * H;
-  for (int idx = threadIdx.x; idx < A * H; idx += blockDim.x) wq[idx] = Wq_g[idx];
   const float* Whh = a.P + a.oWhh + (int64_t)i * H3 * H;
-  for (int q0 = threadIdx.x; q0 < H3 * H / 4; q0 += 8 * blockDim.x) {   // 8 float4 loads in flight
-    float4 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int q = q0 + j * blockDim.x;
-      v[j] = q < H3 * H / 4 ? reinterpret_cast<const float4*>(Whh)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int q = q0 + j * blockDim.x;
-      if (q < H3 * H / 4) reinterpret_cast<float4*>(whh)[q] = v[j];
-    }
-  }
-  float dh = on ? a.dh[pair * H + f] : 0.f;
-  // step inputs, prefetched one step ahead: h0 / r / z / n / anh of this lane's feature, action,
-  // dQ(a), done flag
-  struct In { float h0, r, z, n, anh, dqa, done; int act; };
-  auto load_in = [&](int t) {
-    In x{};
-    if (b < a.B) {
-      const float* h0 = a.save + t * sq.save_st + pair * SD + a.F1 + a.G;
-      const float* done = t == sq.C - 1 ? sq.ones : a.done + t * sq.done_st;
-      x.act = a.acts[t * sq.acts_st + pair];
-      x.dqa = a.dqa[t * sq.dqa_st + pair];
-      x.done = done[b];
-      if (f < H) {
-        x.h0 = h0[f];
-        x.r = h0[H + f];
-        x.z = h0[2 * H + f];
-        x.n = h0[3 * H + f];
-        x.anh = h0[4 * H + f];
-      }
-    }
-    return x;
+  // input row (step w0 + row / 4, wave row % 4): the 5H saved GRU values (16-byte pieces), then the
+  // action (raw int bits), dQ(a) and the done flag (one word each)
+  auto save_row = [&](int w0, int row) -> const float* {
+    const int t = w0 + (row >> 2), bb = min((int)blockIdx.x * 4 + (row & 3), a.B - 1);
+    return a.save + t * sq.save_st + ((int64_t)bb * a.N + i) * SD + a.F1 + a.G;
   };
-  In cur = load_in(sq.C - 1);
-  __syncthreads();   // the W_hh / W_q images (global -> LDS) visible
-  for (int t = sq.C - 1; t >= 0; --t) {
-    const In nxt = t > 0 ? load_in(t - 1) : In{};
-    float stash = 0.f;
-    if (b < a.B) {
-      const int act = cur.act;
-      const float dqa = cur.dqa;
-      if (f < A) a.dq[t * sq.dq_st + pair * A + f] = (f == act) ? dqa : 0.f;
-      if (f < H) {
-        const bool drop = cur.done > 0.5f;
-        const float dh1 = wq[act * H + f] * dqa + (drop ? 0.f : dh);
-        const float r = cur.r, z = cur.z, n = cur.n, anh = cur.anh;
-        const float dn = dh1 * (1.f - z);
-        const float dz = dh1 * (cur.h0 - n);
-        const float dpn = dn * (1.f - n * n);
-        const float dar = dpn * anh * r * (1.f - r);
-        const float daz = dz * z * (1.f - z);
-        float* gi = a.dgi + t * sq.dgi_st + pair * H3;
-        float* gh = a.dgh + t * sq.dgi_st + pair * H3;
-        gi[f] = dar;
-        gi[H + f] = daz;
-        gi[2 * H + f] = dpn;
-        gh[f] = dar;
-        gh[H + f] = daz;
-        gh[2 * H + f] = dpn * r;
-        sdg[w * H3 + f] = dar;
-        sdg[w * H3 + H + f] = daz;
-        sdg[w * H3 + 2 * H + f] = dpn * r;
-        stash = dh1 * z;
-      }
-    }
-
-    lds_sync();        // sdg visible
-    if (on) {
-      float acc = stash;
-#pragma unroll 16
-      for (int r = 0; r < H3; ++r) acc += whh[r * H + f] * sdg[w * H3 + r];
-      dh = acc;
-    }
-    cur = nxt;
-    lds_sync();        // sdg reads done before the next step overwrites it
+  auto scalar_in = [&](int w0, int row, int j) -> const float* {   // j = 0 act, 1 dQ(a), 2 done
+    const int t = w0 + (row >> 2), bb = min((int)blockIdx.x * 4 + (row & 3), a.B - 1);
+    const int64_t pr = (int64_t)bb * a.N + i;
+    if (j == 0) return reinterpret_cast<const float*>(a.acts + t * sq.acts_st + pr);
+    if (j == 1) return a.dqa + t * sq.dqa_st + pr;
+    return t == sq.C - 1 ? sq.ones + bb : a.done + t * sq.done_st + bb;
+  };
+  auto load_window = [&](int w0, int wn) {
+    glds_rows16(inw, 4 * wn, SI, SI, [&](int row) { return save_row(w0, row); });
+    glds_gather(scw, 3 * 4 * wn, [&](int e) {
+      const int row = e / 3;
+      return scalar_in(w0, row, e - 3 * row);
+    });
+  };
+  // prologue: W_hh (row-major image, transposed in LDS below), W_q and the last window's step inputs
+  // by LDS-DMA (one round trip, compact code)
+  const int wfirst = min(sq.win, sq.C);
+  glds_rows16(whr, 1, H3 * H, H3 * H, [&](int) { return Whh; });
+  if (tr) tr[103] = clock64();
+  glds_gather(wq, A * H, [&](int idx) { return Wq_g + idx; });
+  if (tr) tr[104] = clock64();
+  load_window(sq.C - wfirst, wfirst);
+  float dh = a.dh[pair * H + min(f, H - 1)];   // (lanes f >= H: unused)
+  if (tr) tr[100] = clock64();
+  __syncthreads();
+  if (tr) tr[101] = clock64();
+#pragma unroll 4
+  for (int q = threadIdx.x; q < H3 * H / 4; q += blockDim.x) {
+    const int r = (4 * q) / H, c = (4 * q) % H;
+    const float4 v = *reinterpret_cast<const float4*>(whr + 4 * q);
+    whT[(c + 0) * LDT + r] = v.x;
+    whT[(c + 1) * LDT + r] = v.y;
+    whT[(c + 2) * LDT + r] = v.z;
+    whT[(c + 3) * LDT + r] = v.w;
   }
+  if (tr) tr[102] = clock64();
+  const float* whrow = whT + f * LDT;
+  float* sdw = sdg + w * H3;
+  for (int w1 = sq.C; w1 > 0; w1 -= sq.win) {
+    const int w0 = max(0, w1 - sq.win), wn = w1 - w0;
+    if (w1 != sq.C) {   // later windows (the first one came with the prologue)
+      __syncthreads();
+      load_window(w0, wn);
+    }
+    __syncthreads();   // window (and, first pass, the transposed W_hh) visible
+    if (tr) tr[1] = clock64();
+    for (int tt = wn - 1; tt >= 0; --tt) {
+      const int t = w0 + tt;
+      uint64_t* ts = tr ? tr + 4 + 4 * t : nullptr;
+      if (ts) ts[0] = clock64();
+      const float* in = inw + (tt * 4 + w) * SI;
+      const float* sc = scw + (tt * 4 + w) * 3;
+      float stash = 0.f;
+      if (b < a.B) {
+        const int act = __float_as_int(sc[0]);
+        const float dqa = sc[1];
+        if (f < A) a.dq[t * sq.dq_st + pair * A + f] = (f == act) ? dqa : 0.f;
+        if (f < H) {
+          const bool drop = sc[2] > 0.5f;
+          const float dh1 = wq[act * H + f] * dqa + (drop ? 0.f : dh);
+          const float r = in[H + f], z = in[2 * H + f], n = in[3 * H + f], anh = in[4 * H + f];
+          const float dn = dh1 * (1.f - z);
+          const float dz = dh1 * (in[f] - n);
+          const float dpn = dn * (1.f - n * n);
+          const float dar = dpn * anh * r * (1.f - r);
+          const float daz = dz * z * (1.f - z);
+          float* gi = a.dgi + t * sq.dgi_st + pair * H3;
+          float* gh = a.dgh + t * sq.dgi_st + pair * H3;
+          gi[f] = dar;
+          gi[H + f] = daz;
+          gi[2 * H + f] = dpn;
+          gh[f] = dar;
+          gh[H + f] = daz;
+          gh[2 * H + f] = dpn * r;
+          sdw[f] = dar;
+          sdw[H + f] = daz;
+          sdw[2 * H + f] = dpn * r;
+          stash = dh1 * z;
+        }
+      }
+      if (ts) ts[1] = clock64();
+      // sdw is written and read by this wave only: LDS ops of one wave complete in order, so a
+      // compiler fence is all the hand-over needs
+      __builtin_amdgcn_wave_barrier();
+      if (on) {
+        float acc = stash;
+#pragma unroll
+        for (int r4 = 0; r4 < H3; r4 += 4) {
+          const float4 wv = *reinterpret_cast<const float4*>(whrow + r4);
+          const float4 dv = *reinterpret_cast<const float4*>(sdw + r4);
+          acc += wv.x * dv.x;
+          acc += wv.y * dv.y;
+          acc += wv.z * dv.z;
+          acc += wv.w * dv.w;
+        }
+        dh = acc;
+      }
+      if (ts) ts[2] = clock64() + (uint64_t)dh * 0;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (tr) tr[2] = clock64();
   if (on) a.dh[pair * H + f] = dh;
 }
 
@@ -1662,6 +2146,42 @@ __global__ __launch_bounds__(256) void tmv_kernel(TmvArgs a) {
   }
 }
 
+// Same op and summation order, with the whole r range of the block's X rows and W columns staged in
+// ONE round of loads (R <= 256: sx [32][R], sw [R][32] in dynamic LDS) instead of one memory round
+// trip per 32-deep chunk.
+__global__ __launch_bounds__(256) void tmv_full_kernel(TmvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int R = a.R;
+  float* sx = sm;             // [32][R] (a wave reads 2 rows: broadcasts)
+  float* sw = sx + 32 * R;    // [R][32]
+  const int g = blockIdx.z;
+  const int m0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tm = threadIdx.x / 32, tc = threadIdx.x % 32;
+  // rows m >= M / columns c >= Cc load a valid neighbour; their results are never stored
+  block_gather_rows(sx, 32, R, [&](int p, int r) {
+    return a.X + g * a.x_g + (int64_t)min(m0 + p, a.M - 1) * a.x_m + r;
+  });
+  block_gather_rows(sw, R, 32, [&](int r, int x) {
+    return a.W + g * a.w_g + (int64_t)r * a.Cc + min(c0 + x, a.Cc - 1);
+  });
+  __syncthreads();
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = 0; r < R; ++r) {
+    const float w = sw[r * 32 + tc];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += sx[(tm + 8 * q) * R + r] * w;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int m = m0 + tm + 8 * q, c = c0 + tc;
+    if (m < a.M && c < a.Cc) {
+      float v = acc[q];
+      if (a.Z && !(a.Z[g * a.z_g + (int64_t)m * a.z_m + c] > 0.f)) v = 0.f;
+      a.Y[g * a.y_g + (int64_t)m * a.y_m + c] = v;
+    }
+  }
+}
+
 // Same op on exact-f32 MFMA (v_mfma_f32_32x32x2_f32): block = 4 waves = one 64 (m) x 64 (c) tile,
 // per 32-deep r chunk the X / W slabs are staged in LDS (X transposed to [r][m]) and every wave
 // accumulates its 32 x 32 sub-tile with 16 MFMAs (r on the MFMA k dimension; fixed order).
@@ -1729,11 +2249,28 @@ __global__ __launch_bounds__(256) void adam_kernel(float* P, float* G, float* m,
                                                    float b1, float b2, float eps, const float* step, float* norm_out,
                                                    float grad_scale, const float* partials2) {
   __shared__ float s_coef, s_coef2;
+  __shared__ float red[2][256];
+  // sum the sumsq partials with the whole block (one load per thread, fixed-order tree), not one
+  // thread's sequential loop (one memory round trip per few partials)
+  {
+    float p1 = 0.f, p2 = 0.f;
+    for (int i = threadIdx.x; i < n_part; i += blockDim.x) {
+      p1 += partials[i];
+      if (partials2) p2 += partials2[i];
+    }
+    red[0][threadIdx.x] = p1;
+    red[1][threadIdx.x] = p2;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+      if ((int)threadIdx.x < st) {
+        red[0][threadIdx.x] += red[0][threadIdx.x + st];
+        red[1][threadIdx.x] += red[1][threadIdx.x + st];
+      }
+      __syncthreads();
+    }
+  }
   if (threadIdx.x == 0) {
-    float tot = 0.f, tot2 = 0.f;
-    for (int i = 0; i < n_part; ++i) tot += partials[i];
-    if (partials2)
-      for (int i = 0; i < n_part; ++i) tot2 += partials2[i];
+    const float tot = red[0][0], tot2 = red[1][0];
     const float norm = sqrtf(tot) * grad_scale;
     const float norm2 = sqrtf(tot2) * grad_scale;
     s_coef = max_norm > 0.f ? fminf(1.0f, max_norm / (norm + 1e-6f)) : 1.0f;
@@ -1876,9 +2413,21 @@ int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, 
   return MM_OK;
 }
 
+static bool mix_split_enabled() {
+  const char* e = getenv("MM_MIX_SPLIT");   // "0": the one-kernel LDS sequence paths (A/B, tests)
+  return !(e && e[0] == '0');
+}
+// steps per LDS window of the serial mixer kernels
+static int mix_rec_win(int C, int Hm, bool bwd) {
+  int win = C;
+  while (win > 1 && (bwd ? mm::mix_rec_bwd_floats(Hm, win) : mm::mix_rec_fwd_floats(Hm, win)) * 4 > mm::kMixSeqLds)
+    win = (win + 1) / 2;
+  return win;
+}
+
 int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                      const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
-                     float* delta, int32_t steps, mm_stream_t s) {
+                     float* delta, float* ws, int32_t steps, mm_stream_t s) {
   MM_REQUIRE(P && save && qa && dq && done && ones && dhm && dqa && delta && steps >= 1, "mixer_bwd_seq: bad args");
   mm::MixBwdArgs a = {P, save, qa, dq, done, dhm, dqa, delta, B, N, S, Hm, K1};
   mm::MixBwdSeq q;
@@ -1895,6 +2444,35 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
   if (B >= 512 && smm <= 64 * 1024 && !(mm_env && mm_env[0] == '0')) {
     hipLaunchKernelGGL(mm::mixer_bwd_seq_multi_kernel, dim3((B + mm::MIX_SPB - 1) / mm::MIX_SPB), dim3(256), smm,
                        (hipStream_t)s, a, q);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
+  const int win = mix_rec_win(steps, Hm, true);
+  MM_REQUIRE(!ws || (uintptr_t)ws % 16 == 0, "mixer_bwd_seq: ws must be 16-byte aligned");
+  if (ws && mix_split_enabled() && mm::mix_rec_supported(Hm) && mm::mix_rec_bwd_floats(Hm, win) * 4 <= mm::kMixSeqLds &&
+      mm::mix_hyper_bwd_floats(Hm, K1, N) * 4 <= 64 * 1024) {
+    const int rc = mm::mix_seq_lds_setup();
+    if (rc) return rc;
+    const int R = B * steps;
+    hipLaunchKernelGGL(mm::mixer_hyper_bwd_kernel, dim3((R + mm::MIX_SPB - 1) / mm::MIX_SPB), dim3(256),
+                       mm::mix_hyper_bwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R, ws);
+    MM_HIP_CHECK(hipGetLastError());
+    mm::MixRecBwd rq;
+    rq.C = steps;
+    rq.win = win;
+    rq.save_st = q.save_st;
+    rq.delta_st = q.delta_st;
+    rq.done_st = B;
+    rq.done = done;
+    rq.xws = ws;
+    rq.ones = ones;
+    rq.trace = mm::debug_trace_buffer("MM_MIX_TRACE_BWD");
+    if (Hm == 32)
+      hipLaunchKernelGGL(mm::mixer_rec_bwd_kernel<32>, dim3(B), dim3(256), mm::mix_rec_bwd_floats(Hm, win) * 4,
+                         (hipStream_t)s, a, rq);
+    else
+      hipLaunchKernelGGL(mm::mixer_rec_bwd_kernel<64>, dim3(B), dim3(256), mm::mix_rec_bwd_floats(Hm, win) * 4,
+                         (hipStream_t)s, a, rq);
     MM_HIP_CHECK(hipGetLastError());
     return MM_OK;
   }
@@ -1917,6 +2495,9 @@ int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1) {
   const mm::MixSeqGeo g(Hm, K1, N);
   const char* lds_env = getenv("MM_MIX_LDS");
   if (lds_env && lds_env[0] == '0') return 0;
+  if (mix_split_enabled())
+    return B < 512 && mm::mix_rec_supported(Hm) && mm::mix_rec_fwd_floats(Hm, 1) * 4 <= mm::kMixSeqLds &&
+           mm::mix_hyper_fwd_floats(Hm, K1, N) * 4 <= 64 * 1024;
   return B < 512 && g.fwd_floats() * 4 <= mm::kMixSeqLds && 3 * Hm <= 256 && N <= 256;
 }
 
@@ -1949,6 +2530,32 @@ int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
   q.reset_steps = reset_steps;
   const int rc = mm::mix_seq_lds_setup();
   if (rc) return rc;
+  if (mix_split_enabled()) {
+    for (int i = 0; i < n_nets; ++i) {
+      MM_REQUIRE(nets[i].h_out, "mixer_fwd_seq: h_out [C][B][Hm] required");
+      MM_REQUIRE((uintptr_t)nets[i].gi % 16 == 0, "mixer_fwd_seq: gi must be 16-byte aligned");
+    }
+    mm::MixRecFwd rq;
+    rq.C = steps;
+    rq.win = mix_rec_win(steps, Hm, false);
+    rq.gi_st = q.gi_st;
+    rq.hout_st = (int64_t)B * Hm;
+    rq.save_st = q.save_st;
+    rq.reset_steps = reset_steps;
+    rq.trace = mm::debug_trace_buffer("MM_MIX_TRACE_FWD");
+    if (Hm == 32)
+      hipLaunchKernelGGL(mm::mixer_rec_fwd_kernel<32>, dim3(B, n_nets), dim3(256),
+                         mm::mix_rec_fwd_floats(Hm, rq.win) * 4, (hipStream_t)s, a, rq);
+    else
+      hipLaunchKernelGGL(mm::mixer_rec_fwd_kernel<64>, dim3(B, n_nets), dim3(256),
+                         mm::mix_rec_fwd_floats(Hm, rq.win) * 4, (hipStream_t)s, a, rq);
+    MM_HIP_CHECK(hipGetLastError());
+    const int R = B * steps;
+    hipLaunchKernelGGL(mm::mixer_hyper_fwd_kernel, dim3((R + mm::MIX_SPB - 1) / mm::MIX_SPB, n_nets), dim3(256),
+                       mm::mix_hyper_fwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   const mm::MixSeqGeo g(Hm, K1, N);
   hipLaunchKernelGGL(mm::mixer_fwd_seq_lds_kernel, dim3(B, n_nets), dim3(256), g.fwd_floats() * 4, (hipStream_t)s, a,
                      q);
@@ -1971,9 +2578,23 @@ int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t
                      float* dgi, float* dgh, float* dq, int32_t steps, mm_stream_t s) {
   MM_REQUIRE(d && P && save && acts && dqa && done && ones && dh && dgi && dgh && dq && steps >= 1 && B > 0,
              "agent_bwd_seq: bad args");
-  MM_REQUIRE(d->h <= 64 && d->n_actions <= 64, "agent_bwd_seq: needs H <= 64 and A <= 64");
-  const size_t smem = sizeof(float) * (3 * (size_t)d->h * d->h + 4 * 3 * (size_t)d->h + (size_t)d->n_actions * d->h);
-  MM_REQUIRE(smem <= 64 * 1024, "agent_bwd_seq: W_hh too large for LDS");
+  MM_REQUIRE((d->h == 32 || d->h == 64) && d->n_actions <= 64, "agent_bwd_seq: needs H in {32, 64} and A <= 64");
+  MM_REQUIRE(oWhh % 4 == 0 && (uintptr_t)P % 16 == 0 && (uintptr_t)save % 16 == 0 && (d->f1 + d->g) % 4 == 0,
+             "agent_bwd_seq: W_hh / save rows must be 16-byte aligned (16-byte LDS-DMA)");
+  int win = steps;
+  while (win > 1 && mm::agent_bwd_seq_floats(d->h, d->n_actions, win) * 4 > mm::kMixSeqLds) win = (win + 1) / 2;
+  const size_t smem = sizeof(float) * mm::agent_bwd_seq_floats(d->h, d->n_actions, win);
+  MM_REQUIRE(smem <= mm::kMixSeqLds, "agent_bwd_seq: W_hh too large for LDS");
+  {
+    static bool attr = false;
+    if (!attr) {
+      MM_HIP_CHECK(hipFuncSetAttribute((const void*)mm::agent_bwd_seq_kernel<32>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)mm::kMixSeqLds));
+      MM_HIP_CHECK(hipFuncSetAttribute((const void*)mm::agent_bwd_seq_kernel<64>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)mm::kMixSeqLds));
+      attr = true;
+    }
+  }
   mm::AgentBwdArgs a = {P, oWq, oWhh, save, acts, dqa, done, dh, dgi, dgh, dq, B, d->n_agents, d->f1, d->g, d->h,
                         d->n_actions};
   const int64_t BN = (int64_t)B * d->n_agents;
@@ -1986,7 +2607,14 @@ int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t
   q.dq_st = BN * d->n_actions;
   q.done_st = B;
   q.ones = ones;
-  hipLaunchKernelGGL(mm::agent_bwd_seq_kernel, dim3((B + 3) / 4, d->n_agents), dim3(256), smem, (hipStream_t)s, a, q);
+  q.win = win;
+  q.trace = mm::debug_trace_buffer("MM_ABWD_TRACE");
+  if (d->h == 32)
+    hipLaunchKernelGGL(mm::agent_bwd_seq_kernel<32>, dim3((B + 3) / 4, d->n_agents), dim3(256), smem, (hipStream_t)s,
+                       a, q);
+  else
+    hipLaunchKernelGGL(mm::agent_bwd_seq_kernel<64>, dim3((B + 3) / 4, d->n_agents), dim3(256), smem, (hipStream_t)s,
+                       a, q);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -2084,6 +2712,12 @@ int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
     return MM_OK;
   }
   dim3 grid((x->Cc + 31) / 32, (x->M + 31) / 32, x->groups);
+  if (x->R <= 256) {   // whole r range staged at once
+    hipLaunchKernelGGL(mm::tmv_full_kernel, grid, dim3(256), sizeof(float) * (64 * (size_t)x->R),
+                       (hipStream_t)s, a);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   hipLaunchKernelGGL(mm::tmv_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;

@@ -121,6 +121,32 @@ def symbols():
     return [s[0] for s in _SIGS]
 
 
+_pending_destroy = []
+
+
+def release(fn_name, h):
+    """Destroy a native handle (``mm_env_destroy`` / ``mm_per_destroy``) from a ``__del__``.
+
+    A garbage collection can run a ``__del__`` while some stream is being captured into a graph, where
+    a device synchronisation or a free would invalidate the capture (and can abort). Such releases are
+    deferred to the next call made outside a capture."""
+    import torch
+    try:
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    except Exception:
+        capturing = False
+    _pending_destroy.append((fn_name, h))
+    if capturing:
+        return
+    while _pending_destroy:
+        name, hh = _pending_destroy.pop()
+        try:
+            torch.cuda.synchronize()
+        except Exception:
+            pass
+        getattr(lib(), name)(hh)
+
+
 def check(rc, what=""):
     if rc != 0:
         msg = lib().mm_last_error().decode(errors="replace")
@@ -170,7 +196,7 @@ _SIGS += [
     ("mm_agent_q_rec_seq2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
                                     ctypes.POINTER(QFwdIO), c_i64, c_i32, c_vp, c_vp]),
     ("mm_mixer_bwd_seq", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                 c_vp, c_i32, c_vp]),
+                                 c_vp, c_vp, c_i32, c_vp]),
     ("mm_agent_q_rec2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
                                 ctypes.POINTER(QFwdIO), c_i64, c_vp]),
     ("mm_outer_reduce_batch_partial", c_i64, [ctypes.POINTER(OuterArgs), c_i32]),

@@ -32,7 +32,7 @@ import torch
 
 from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, check, lib
 from .env import VecEnv
-from .qnet import AgentQNet, ptr, stream_handle
+from .qnet import AgentQNet, graph_capture, ptr, stream_handle
 from .replay import DevicePER
 
 
@@ -244,7 +244,7 @@ class RolloutEngine:
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         t0, ins0, n0 = self.t, self.chunks_inserted, len(self.per)
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             for _ in range(self.graph_steps()):
                 self._step_launch()
         # capture does not execute: rewind the host bookkeeping (PER fill-count mirror too)
@@ -284,7 +284,7 @@ class RolloutEngine:
             self.t = ph
             self._td_flushed = False
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with graph_capture(g):
                 self._step_launch()
             graphs.append(g)
         self.t, self.chunks_inserted, self._td_pending, self._td_flushed = saved

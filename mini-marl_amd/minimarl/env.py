@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import EnvCfg, c_i32, c_vp, check, lib
+from ._lib import release, EnvCfg, c_i32, c_vp, check, lib
 from .qnet import ptr, stream_handle
 
 
@@ -32,12 +32,11 @@ class VecEnv:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
-            try:
-                torch.cuda.synchronize(self.device)
-            except Exception:
-                pass
-            lib().mm_env_destroy(h)
             self._h = None
+            try:
+                release("mm_env_destroy", h)   # deferred while a graph capture is running
+            except Exception:   # interpreter shutdown: module globals already gone
+                pass
 
     def handle(self):
         return self._h

@@ -30,7 +30,7 @@ import torch
 from ._lib import (MM_LOSS_HUBER, MM_LOSS_MIX_SUM, MM_LOSS_TARGET_SUM, MM_Q_ACT, MM_Q_GATHER, MM_Q_MAX, MixNetIO,
                    OuterArgs, QFwdIO, TmvArgs, c_i64, check, lib)
 from .qnet import KEYS as AGENT_KEYS
-from .qnet import AgentQNet, ptr, stream_handle
+from .qnet import AgentQNet, graph_capture, ptr, stream_handle
 
 MIX_KEYS = ["gWih", "gWhh", "gbih", "gbhh", "w1W", "w1b", "w2W", "w2b", "b1W", "b1b", "b2aW", "b2ab", "b2bW",
             "b2bb"]
@@ -212,6 +212,8 @@ class QLearner:
             self.msave = torch.zeros(C, B, self.MSD, **f32)
             self.mdelta = torch.zeros(C, B, self.MDD, **f32)
             self.dhm = torch.zeros(B, Hm, **f32)
+            self.mhseq = torch.zeros(2, C, B, Hm, **f32)   # mixer hidden sequences (behavior, target)
+            self.mxws = torch.zeros(C, B, 4, Hm, **f32)    # hypernet input gradients (mm_mixer_bwd_seq)
             self.gi_b = torch.zeros(C, B, 3 * Hm, **f32)
             self.gi_t = torch.zeros(C, B, 3 * Hm, **f32)
         # split-M outer-reduce partials: the job geometry is fixed, size it once (no launches here)
@@ -390,14 +392,15 @@ class QLearner:
                 mx = self.mix
                 check(L.mm_mixer_bwd_seq(B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.msave), ptr(self.qa),
                                          ptr(self.dq), ptr(self.done), ptr(self.ones_f), ptr(self.dhm), ptr(self.dqa),
-                                         ptr(self.mdelta), C, s), "mixer bwd seq")
-        if self.seq and B < 512:
+                                         ptr(self.mdelta), ptr(self.mxws), C, s), "mixer bwd seq")
+        agent_seq = self.seq and B < 512 and self.H in (32, 64)
+        if agent_seq:
             # the agent BPTT chain over all C steps in one launch (W_hh in LDS, dh carried in registers)
             check(L.mm_agent_bwd_seq(ctypes.byref(self.beh.dims), ptr(P), o[8], o[5], B, ptr(self.asave),
                                      ptr(self.acts), ptr(self.dqa), ptr(self.done), ptr(self.ones_f), ptr(self.dh),
                                      ptr(self.dgi), ptr(self.dgh), ptr(self.dqv), C, s), "agent bwd seq")
         for t in range(C - 1, -1, -1):
-            if self.seq and B < 512:
+            if agent_seq:
                 break
             dn = self.ones_f if t == C - 1 else self.done[t * B:(t + 1) * B]
             if self.has_mixer and not self.seq:
@@ -443,7 +446,7 @@ class QLearner:
                     n = nets[k]
                     n.P, n.q, n.gi, n.qtot = Pm.data_ptr(), q.data_ptr(), gi.data_ptr(), qt.data_ptr()
                     n.s_off = self.s_off.data_ptr()
-                    n.h_in, n.h_out = self.hm[0].data_ptr(), None
+                    n.h_in, n.h_out = self.hm[0].data_ptr(), self.mhseq[k].data_ptr()
                     n.reset = self.ones8.data_ptr()
                     n.save = sv.data_ptr() if sv is not None else None
                 check(L.mm_mixer_fwd_seq(B, N, mx.S, mx.Hm, mx.K1, nets, 2, C, ptr(self.done8), s), "mixer fwd seq")
@@ -615,12 +618,12 @@ class QLearner:
         torch.cuda.synchronize(self.dev)
         n0 = self.updates
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1):
+        with graph_capture(g1):
             if per is None:          # the batch loaded by load_batch (tests, reference-shaped callers)
                 self.compute_grads(self._obs_ptr, self._reset_obs)
             else:
                 self.sample_and_grads(per, store, reset_obs_ptr, seed=seed)
-        with torch.cuda.graph(g2):
+        with graph_capture(g2):
             if per is None:
                 self.apply_grads(self._graph_scale)
             else:

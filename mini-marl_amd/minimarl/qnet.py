@@ -5,7 +5,9 @@ N agents with their OWN weights, Linear(D,F1)+ReLU, Linear(F1,G)+ReLU,
 GRUCell(G,H), Linear(H,A). The forward is one ``mm_agent_q_fwd`` launch for all
 envs x agents (see csrc/agent_fwd.hip).
 """
+import contextlib
 import ctypes
+import gc
 import math
 
 import numpy as np
@@ -43,6 +45,21 @@ _FMTS = {"qmix": _QMIX_FMT, "vdn": _VDN_FMT, "min": _MIN_FMT}
 
 def stream_handle(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+@contextlib.contextmanager
+def graph_capture(g):
+    """``torch.cuda.graph(g)`` with the garbage collector held off: a collection inside the capture can
+    destroy an earlier graph or native handle, whose device calls are illegal mid-capture (abort)."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def ptr(t):

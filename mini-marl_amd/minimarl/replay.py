@@ -9,7 +9,7 @@ import ctypes
 
 import torch
 
-from ._lib import MM_PER_QMIX, MM_PER_VDN, c_vp, check, lib
+from ._lib import release, MM_PER_QMIX, MM_PER_VDN, c_vp, check, lib
 from .qnet import ptr, stream_handle
 
 
@@ -40,12 +40,11 @@ class DevicePER:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
-            try:
-                torch.cuda.synchronize(self.device)
-            except Exception:
-                pass
-            lib().mm_per_destroy(h)
             self._h = None
+            try:
+                release("mm_per_destroy", h)   # deferred while a graph capture is running
+            except Exception:   # interpreter shutdown: module globals already gone
+                pass
 
     @property
     def alpha(self):

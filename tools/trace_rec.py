@@ -17,6 +17,7 @@ from minimarl.engine import RolloutEngine  # noqa: E402
 from minimarl.learner import Mixer, QLearner  # noqa: E402
 
 E, N, C = 512, 8, 10
+assert _lib.lib().mm_debug_trace(None, 0) == 0
 eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=C, capacity=4 * E, seed=1, device="cuda")
 for _ in range(4):
     eng.run_graph(0.1)
@@ -28,6 +29,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 buf = (ctypes.c_uint64 * 4096)()
 lib = _lib.lib()
+torch.cuda.synchronize()
 
 assert lib.mm_debug_trace(ctypes.addressof(buf), 4096) == 0
 t = list(buf)
