@@ -1391,8 +1391,8 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
 // ---------------------------------------------------------------- packing
 // One thread per packed element: gathers the canonical flat parameters into
 // the per-lane MFMA fragment image (zero padding outside the real shape).
-__global__ void qnet_pack_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
-                                 int D, int F1, int G, int H, int A, QnetOffsets o) {
+__device__ __forceinline__ void qnet_pack_body(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g,
+                                               int N, int D, int F1, int G, int H, int A, QnetOffsets o) {
   const int64_t per_agent = g.agent_stride;
   const int64_t total = per_agent * N;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
@@ -1443,8 +1443,8 @@ __global__ void qnet_pack_kernel(const float* __restrict__ params, float* __rest
 
 // fp16x3 image (packed + N*agent_stride): weight blocks as [16-row half q][part][lane][8 halves]
 // (see agent_q_fwd_body_h3); bias vectors in natural order.
-__global__ void qnet_pack_h3_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
-                                    int D, int F1, int G, int H, int A, QnetOffsets o) {
+__device__ __forceinline__ void qnet_pack_h3_body(const float* __restrict__ params, float* __restrict__ packed,
+                                                  QnetGeo g, int N, int D, int F1, int G, int H, int A, QnetOffsets o) {
   const int64_t per_agent = g.agent_stride;
   const int64_t total = per_agent * N;
   uint32_t* out = reinterpret_cast<uint32_t*>(packed + total);
@@ -1499,6 +1499,13 @@ __global__ void qnet_pack_h3_kernel(const float* __restrict__ params, float* __r
   }
 }
 
+// both images (f32 fragments, fp16x3 split) from the canonical parameters in ONE launch
+__global__ void qnet_pack_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
+                                 int D, int F1, int G, int H, int A, QnetOffsets o) {
+  qnet_pack_body(params, packed, g, N, D, F1, G, H, A, o);
+  qnet_pack_h3_body(params, packed, g, N, D, F1, G, H, A, o);
+}
+
 int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s) {
   QnetGeo g;
   QnetOffsets o;
@@ -1508,8 +1515,6 @@ int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStre
   const int threads = 256;
   const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 4096);
   hipLaunchKernelGGL(qnet_pack_kernel, dim3(blocks), dim3(threads), 0, s, params, packed, g, d->n_agents,
-                     d->obs_dim, d->f1, d->g, d->h, d->n_actions, o);
-  hipLaunchKernelGGL(qnet_pack_h3_kernel, dim3(blocks), dim3(threads), 0, s, params, packed, g, d->n_agents,
                      d->obs_dim, d->f1, d->g, d->h, d->n_actions, o);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;

@@ -98,6 +98,15 @@ __device__ __forceinline__ void glds_rows16(float* dst, int rows, int rowlen, in
   }
 }
 
+// dst[4 i .. 4 i + 3] = 16 bytes at addr(i) for i < n4 (dst contiguous and 16-byte aligned; each
+// source 16-byte aligned): 64 float4 per wave-instruction, the source address per lane
+template <typename A>
+__device__ __forceinline__ void glds16_gather(float* dst, int n4, A addr) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int c0 = (int)(threadIdx.x >> 6) * 64; c0 < n4; c0 += nw * 64)
+    if (c0 + lane < n4) glds_dwordx4(addr(c0 + lane), dst + 4 * c0);
+}
+
 // Workgroup barrier that orders LDS only: waits for this wave's outstanding LDS operations, then
 // s_barrier. Unlike __syncthreads() it does not wait for outstanding global stores, so a sequence
 // kernel whose waves communicate through LDS does not stall every step on its own result writes.

@@ -879,7 +879,7 @@ __device__ __forceinline__ void mixer_bwd_body(const MixBwdArgs& a, int b) {
 // read serves all samples. Per sample the partial-sum order is block_matvec_t's (bit-identical).
 // red: [MIX_SPB][nw][K] floats.
 template <bool ACC = true>
-__device__ void block_matvec_t_multi(const float* __restrict__ W, int rows, int K, const float* d, int ds,
+__device__ __forceinline__ void block_matvec_t_multi(const float* __restrict__ W, int rows, int K, const float* d, int ds,
                                      float* out, int os, float* red) {
   constexpr int Q = MIX_SPB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -1439,19 +1439,32 @@ __host__ __device__ inline size_t mix_hyper_fwd_floats(int Hm, int K1, int N) {
 // all R = C*B rows at once (flat row arrays: save [R][MSD], qa [R][N], dq [R], dqa [R][N],
 // delta [R][MDD]): mixer_bwd_body's hypernet deltas + dqa, and X_j = W_j^T d_j (j = w1, b1, w2, b2a)
 // stored apart in xws [R][4][Hm] (the serial kernel adds them to the future gradient in order).
-__global__ __launch_bounds__(256) void mixer_hyper_bwd_kernel(MixBwdArgs a, int R, float* xws) {
+__global__ __launch_bounds__(256) void mixer_hyper_bwd_kernel(MixBwdArgs a, int R, float* xws, uint64_t* trace) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int Q = MIX_SPB;
   const int Hm = a.Hm, K1 = a.K1, N = a.N, NK = N * K1, SH = NK + 3 * K1;
   const MixOff o = mix_offsets(a.S, Hm, K1, N);
   const int b0 = blockIdx.x * Q;
   const int ns = min(Q, R - b0);
-  float* shd = sm;                  // [Q][SH]
-  float* xo = shd + Q * SH;         // [Q][4][Hm]
-  float* red = xo + Q * 4 * Hm;     // [Q][4 waves][Hm]
+  // the four hypernet weight matrices (w1 [NK][Hm] | b1, w2, b2a [K1][Hm]) staged in LDS by 16-byte
+  // LDS-DMA (row-major: the transposed mat-vecs read a row with lane = column, conflict-free)
+  float* wim = sm;                          // [SH][Hm]
+  float* shd = wim + SH * Hm;               // [Q][SH]
+  float* xo = shd + Q * SH;                 // [Q][4][Hm]
+  float* red = xo + Q * 4 * Hm;             // [Q][4 waves][Hm]
   const int svd = mix_save_dim(Hm, K1, N), dld = mix_delta_dim(Hm, K1, N);
+  uint64_t* tr = (trace && blockIdx.x == 0 && threadIdx.x == 0) ? trace : nullptr;
+  if (tr) tr[0] = clock64();
+  {
+    const int n1 = NK * Hm / 4, n2 = K1 * Hm / 4;
+    glds16_gather(wim, n1, [&](int i) { return a.P + o.w1W + 4 * i; });
+    glds16_gather(wim + NK * Hm, n2, [&](int i) { return a.P + o.b1W + 4 * i; });
+    glds16_gather(wim + (NK + K1) * Hm, n2, [&](int i) { return a.P + o.w2W + 4 * i; });
+    glds16_gather(wim + (NK + 2 * K1) * Hm, n2, [&](int i) { return a.P + o.b2aW + 4 * i; });
+  }
   for (int idx = threadIdx.x; idx < Q * SH; idx += blockDim.x) shd[idx] = 0.f;
   __syncthreads();
+  if (tr) tr[1] = clock64();
   for (int idx = threadIdx.x; idx < ns * K1; idx += blockDim.x) {
     const int s = idx / K1, k = idx % K1, b = b0 + s;
     const float* w1raw = a.save + (int64_t)b * svd + 6 * Hm;
@@ -1483,7 +1496,9 @@ __global__ __launch_bounds__(256) void mixer_hyper_bwd_kernel(MixBwdArgs a, int 
     const int b = b0 + threadIdx.x;
     a.delta[(int64_t)b * dld + 6 * Hm + NK + 3 * K1] = a.dq[b];
   }
+  if (tr) tr[2] = clock64();
   __syncthreads();
+  if (tr) tr[3] = clock64();
   for (int idx = threadIdx.x; idx < ns * N; idx += blockDim.x) {
     const int s = idx / N, i = idx % N, b = b0 + s;
     const float* w1raw = a.save + (int64_t)b * svd + 6 * Hm;
@@ -1491,14 +1506,18 @@ __global__ __launch_bounds__(256) void mixer_hyper_bwd_kernel(MixBwdArgs a, int 
     for (int k = 0; k < K1; ++k) acc += shd[s * SH + NK + k] * fabsf(w1raw[k * N + i]);
     a.dqa[(int64_t)b * N + i] = acc;
   }
-  block_matvec_t_multi<false>(a.P + o.w1W, NK, Hm, shd, SH, xo, 4 * Hm, red);
-  block_matvec_t_multi<false>(a.P + o.b1W, K1, Hm, shd + NK, SH, xo + Hm, 4 * Hm, red);
-  block_matvec_t_multi<false>(a.P + o.w2W, K1, Hm, shd + NK + K1, SH, xo + 2 * Hm, 4 * Hm, red);
-  block_matvec_t_multi<false>(a.P + o.b2aW, K1, Hm, shd + NK + 2 * K1, SH, xo + 3 * Hm, 4 * Hm, red);
+  if (tr) tr[4] = clock64();
+  block_matvec_t_multi<false>(wim, NK, Hm, shd, SH, xo, 4 * Hm, red);
+  if (tr) tr[5] = clock64();
+  block_matvec_t_multi<false>(wim + NK * Hm, K1, Hm, shd + NK, SH, xo + Hm, 4 * Hm, red);
+  block_matvec_t_multi<false>(wim + (NK + K1) * Hm, K1, Hm, shd + NK + K1, SH, xo + 2 * Hm, 4 * Hm, red);
+  block_matvec_t_multi<false>(wim + (NK + 2 * K1) * Hm, K1, Hm, shd + NK + 2 * K1, SH, xo + 3 * Hm, 4 * Hm, red);
+  if (tr) tr[6] = clock64();
   for (int idx = threadIdx.x; idx < ns * 4 * Hm; idx += blockDim.x) xws[(int64_t)b0 * 4 * Hm + idx] = xo[idx];
+  if (tr) tr[7] = clock64();
 }
 __host__ __device__ inline size_t mix_hyper_bwd_floats(int Hm, int K1, int N) {
-  return (size_t)MIX_SPB * (N * K1 + 3 * K1 + 4 * Hm + 4 * Hm);
+  return (size_t)(N * K1 + 3 * K1) * Hm + (size_t)MIX_SPB * (N * K1 + 3 * K1 + 4 * Hm + 4 * Hm);
 }
 
 template <int HM>
@@ -1614,7 +1633,8 @@ static int mix_seq_lds_setup() {
   MM_HIP_CHECK(hipFuncSetAttribute((const void*)mixer_bwd_seq_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)kMixSeqLds));
   const void* serial[] = {(const void*)mixer_rec_fwd_kernel<32>, (const void*)mixer_rec_fwd_kernel<64>,
-                          (const void*)mixer_rec_bwd_kernel<32>, (const void*)mixer_rec_bwd_kernel<64>};
+                          (const void*)mixer_rec_bwd_kernel<32>, (const void*)mixer_rec_bwd_kernel<64>,
+                          (const void*)mixer_hyper_bwd_kernel};
   for (const void* k : serial)
     MM_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMixSeqLds));
   done = true;
@@ -2110,6 +2130,7 @@ struct TmvArgs {
   const float* Z; int64_t z_g, z_m;
   float* Y; int64_t y_g, y_m;
   int M, R, Cc;
+  int aligned16;   // tmv_full_kernel: 16-byte LDS-DMA staging allowed
 };
 
 __global__ __launch_bounds__(256) void tmv_kernel(TmvArgs a) {
@@ -2158,12 +2179,24 @@ __global__ __launch_bounds__(256) void tmv_full_kernel(TmvArgs a) {
   const int m0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
   const int tm = threadIdx.x / 32, tc = threadIdx.x % 32;
   // rows m >= M / columns c >= Cc load a valid neighbour; their results are never stored
-  block_gather_rows(sx, 32, R, [&](int p, int r) {
-    return a.X + g * a.x_g + (int64_t)min(m0 + p, a.M - 1) * a.x_m + r;
-  });
-  block_gather_rows(sw, R, 32, [&](int r, int x) {
-    return a.W + g * a.w_g + (int64_t)r * a.Cc + min(c0 + x, a.Cc - 1);
-  });
+  if (a.aligned16) {   // 16-byte LDS-DMA (R, x_m, Cc, c0 multiples of 4; 16-byte aligned bases)
+    const int R4 = R >> 2;
+    glds16_gather(sx, 32 * R4, [&](int i) {
+      const int p = i / R4;
+      return a.X + g * a.x_g + (int64_t)min(m0 + p, a.M - 1) * a.x_m + 4 * (i - p * R4);
+    });
+    glds16_gather(sw, R * 8, [&](int i) {
+      const int r = i >> 3;
+      return a.W + g * a.w_g + (int64_t)r * a.Cc + min(c0 + 4 * (i & 7), a.Cc - 4);
+    });
+  } else {
+    block_gather_rows(sx, 32, R, [&](int p, int r) {
+      return a.X + g * a.x_g + (int64_t)min(m0 + p, a.M - 1) * a.x_m + r;
+    });
+    block_gather_rows(sw, R, 32, [&](int r, int x) {
+      return a.W + g * a.w_g + (int64_t)r * a.Cc + min(c0 + x, a.Cc - 1);
+    });
+  }
   __syncthreads();
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int r = 0; r < R; ++r) {
@@ -2450,12 +2483,14 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
   const int win = mix_rec_win(steps, Hm, true);
   MM_REQUIRE(!ws || (uintptr_t)ws % 16 == 0, "mixer_bwd_seq: ws must be 16-byte aligned");
   if (ws && mix_split_enabled() && mm::mix_rec_supported(Hm) && mm::mix_rec_bwd_floats(Hm, win) * 4 <= mm::kMixSeqLds &&
-      mm::mix_hyper_bwd_floats(Hm, K1, N) * 4 <= 64 * 1024) {
+      mm::mix_hyper_bwd_floats(Hm, K1, N) * 4 <= mm::kMixSeqLds && Hm % 4 == 0 && K1 % 4 == 0 &&
+      mm::mix_offsets(S, Hm, K1, N).w1W % 4 == 0 && (uintptr_t)P % 16 == 0) {
     const int rc = mm::mix_seq_lds_setup();
     if (rc) return rc;
     const int R = B * steps;
     hipLaunchKernelGGL(mm::mixer_hyper_bwd_kernel, dim3((R + mm::MIX_SPB - 1) / mm::MIX_SPB), dim3(256),
-                       mm::mix_hyper_bwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R, ws);
+                       mm::mix_hyper_bwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R, ws,
+                       mm::debug_trace_buffer("MM_HYB_TRACE"));
     MM_HIP_CHECK(hipGetLastError());
     mm::MixRecBwd rq;
     rq.C = steps;
@@ -2702,7 +2737,9 @@ int mm_outer_reduce_batch(const mm_outer_args* x, int32_t n_jobs, float* partial
 int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
   MM_REQUIRE(x && x->M > 0 && x->R > 0 && x->Cc > 0 && x->groups > 0, "tmv: bad args");
   mm::TmvArgs a = {x->W, x->w_g, x->X, x->x_g, x->x_m, x->Z, x->z_g, x->z_m, x->Y, x->y_g, x->y_m,
-                   x->M, x->R, x->Cc};
+                   x->M, x->R, x->Cc, 0};
+  a.aligned16 = (x->R % 4 == 0 && x->x_m % 4 == 0 && x->x_g % 4 == 0 && x->Cc % 4 == 0 && x->w_g % 4 == 0 &&
+                 (uintptr_t)x->X % 16 == 0 && (uintptr_t)x->W % 16 == 0);
   const char* tm_env = getenv("MM_TMV_MFMA");   // "0": the scalar LDS-tiled kernel
   // small M (B = 32 updates): the 32 x 32 scalar tiles give more blocks and win
   if (x->M >= 2048 && !(tm_env && tm_env[0] == '0')) {

@@ -33,7 +33,7 @@ buf = (ctypes.c_uint64 * 4096)()
 assert _lib.lib().mm_debug_trace(ctypes.addressof(buf), 4096) == 0
 t = list(buf)
 k = 4
-out = {"var": var, "prologue": [int(t[i] - t[0]) if t[i] else None for i in range(4)],
+out = {"var": var, "prologue": [int(t[i] - t[0]) if t[i] else None for i in range(8)],
        "sub": [int(t[i] - t[0]) if t[i] else None for i in range(100, 106)], "steps": []}
 for s in range(C):
     r = t[4 + k * s: 4 + k * s + k]
