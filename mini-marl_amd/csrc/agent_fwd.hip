@@ -1345,6 +1345,22 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
   const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
   const int agent = bid % p.N, tile = bid / p.N;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // range guard (qnet_h3_bound_block): an agent whose split operands could leave the f16 range runs
+  // this block on the exact-f32 image (8 waves x 32 envs = the same 256 envs), the rest idle
+  if (reinterpret_cast<const int*>(p.packed + 2 * p.g.agent_stride * p.N)[agent]) {
+    const int e32 = tile * 256 + wave * 32 + (lane & 31);
+    const float* src32 = p.packed + (int64_t)agent * p.g.agent_stride;
+    const int nch = (int)(p.g.agent_stride >> 8);
+    for (int c = wave; c < nch; c += 16)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src32 + c * 256 + lane * 4),
+                                       (__attribute__((address_space(3))) void*)(wsm + c * 256), 16, 0, 0);
+    const float* orow32 = obs_row_ptr(p, agent, e32);
+    float x32[16];
+    load_obs_kblock(orow32, 0, p.D, x32);
+    __syncthreads();
+    if (wave < 8) agent_q_fwd_body<F1, G, H, AB>(p, agent, e32, wsm, orow32, x32);
+    return;
+  }
   const int e = tile * 256 + wave * 16 + (lane & 15);
   const int g = lane >> 4;
   // weight image DMA first (no dependencies), then the wave's own global reads: the hidden state
@@ -1392,11 +1408,11 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
 // One thread per packed element: gathers the canonical flat parameters into
 // the per-lane MFMA fragment image (zero padding outside the real shape).
 __device__ __forceinline__ void qnet_pack_body(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g,
-                                               int N, int D, int F1, int G, int H, int A, QnetOffsets o) {
+                                               int N, int D, int F1, int G, int H, int A, QnetOffsets o, int nblk) {
   const int64_t per_agent = g.agent_stride;
   const int64_t total = per_agent * N;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+       idx += (int64_t)nblk * blockDim.x) {
     const int agent = (int)(idx / per_agent);
     int64_t r = idx % per_agent;
     float v = 0.0f;
@@ -1444,12 +1460,13 @@ __device__ __forceinline__ void qnet_pack_body(const float* __restrict__ params,
 // fp16x3 image (packed + N*agent_stride): weight blocks as [16-row half q][part][lane][8 halves]
 // (see agent_q_fwd_body_h3); bias vectors in natural order.
 __device__ __forceinline__ void qnet_pack_h3_body(const float* __restrict__ params, float* __restrict__ packed,
-                                                  QnetGeo g, int N, int D, int F1, int G, int H, int A, QnetOffsets o) {
+                                                  QnetGeo g, int N, int D, int F1, int G, int H, int A, QnetOffsets o,
+                                                  int nblk) {
   const int64_t per_agent = g.agent_stride;
   const int64_t total = per_agent * N;
   uint32_t* out = reinterpret_cast<uint32_t*>(packed + total);
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+       idx += (int64_t)nblk * blockDim.x) {
     const int agent = (int)(idx / per_agent);
     const int64_t r = idx % per_agent;
     uint32_t v = 0u;
@@ -1499,11 +1516,72 @@ __device__ __forceinline__ void qnet_pack_h3_body(const float* __restrict__ para
   }
 }
 
-// both images (f32 fragments, fp16x3 split) from the canonical parameters in ONE launch
+// Range guard of the fp16x3 forward, decided once per pack: a split operand must stay below 65504 in
+// magnitude (the largest finite f16). With |obs| <= kH3ObsBound and the GRU state |h| <= 1, the
+// layer outputs are bounded by m1 = max_r sum_k |W1[r,k]| kH3ObsBound + |b1[r]| and
+// m2 = max_r sum_k |W2[r,k]| m1 + |b2[r]|, and every weight is split as well. Agent a whose bounds
+// or largest weight reach kH3Limit gets flag[a] = 1 (tail of the packed buffer), and the fp16x3
+// kernel runs that agent's blocks on the exact-f32 image instead: a per-block branch, no per-value
+// check in the hot path.
+constexpr float kH3ObsBound = 1.0f, kH3Limit = 32768.0f;
+__device__ void qnet_h3_bound_block(const float* __restrict__ params, int* flags, int agent, int D, int F1, int G,
+                                    int H, int A, QnetOffsets o) {
+  __shared__ float red[256];
+  __shared__ float m1s;
+  const int t = threadIdx.x;
+  // largest |weight| of the agent (every weight matrix is split)
+  float wmax = 0.f;
+  auto scan = [&](int64_t off, int64_t n) {
+    for (int64_t i = t; i < n; i += blockDim.x) wmax = fmaxf(wmax, fabsf(params[off + i]));
+  };
+  scan(o.W1 + (int64_t)agent * F1 * D, (int64_t)F1 * D);
+  scan(o.W2 + (int64_t)agent * G * F1, (int64_t)G * F1);
+  scan(o.Wih + (int64_t)agent * 3 * H * G, (int64_t)3 * H * G);
+  scan(o.Whh + (int64_t)agent * 3 * H * H, (int64_t)3 * H * H);
+  scan(o.Wq + (int64_t)agent * A * H, (int64_t)A * H);
+  // layer-1 output bound (one row per thread)
+  float m1 = 0.f;
+  for (int r = t; r < F1; r += blockDim.x) {
+    float acc = fabsf(params[o.b1 + (int64_t)agent * F1 + r]);
+    for (int k = 0; k < D; ++k) acc += fabsf(params[o.W1 + ((int64_t)agent * F1 + r) * D + k]) * kH3ObsBound;
+    m1 = fmaxf(m1, acc);
+  }
+  red[t] = m1;
+  __syncthreads();
+  if (t == 0) {
+    float m = 0.f;
+    for (int i = 0; i < (int)blockDim.x; ++i) m = fmaxf(m, red[i]);
+    m1s = m;
+  }
+  __syncthreads();
+  float m2 = 0.f;
+  for (int r = t; r < G; r += blockDim.x) {
+    float acc = fabsf(params[o.b2 + (int64_t)agent * G + r]);
+    for (int k = 0; k < F1; ++k) acc += fabsf(params[o.W2 + ((int64_t)agent * G + r) * F1 + k]) * m1s;
+    m2 = fmaxf(m2, acc);
+  }
+  __syncthreads();
+  red[t] = fmaxf(fmaxf(m2, wmax), m1s);
+  __syncthreads();
+  if (t == 0) {
+    float m = 0.f;
+    for (int i = 0; i < (int)blockDim.x; ++i) m = fmaxf(m, red[i]);
+    flags[agent] = !(m < kH3Limit);   // NaN weights: unsafe as well
+  }
+}
+
+// both images (f32 fragments, fp16x3 split) from the canonical parameters in ONE launch; the last N
+// blocks compute the per-agent fp16x3 safety flags
 __global__ void qnet_pack_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
                                  int D, int F1, int G, int H, int A, QnetOffsets o) {
-  qnet_pack_body(params, packed, g, N, D, F1, G, H, A, o);
-  qnet_pack_h3_body(params, packed, g, N, D, F1, G, H, A, o);
+  const int nb = (int)gridDim.x - N;
+  if ((int)blockIdx.x >= nb) {
+    qnet_h3_bound_block(params, reinterpret_cast<int*>(packed + 2 * g.agent_stride * N), (int)blockIdx.x - nb, D,
+                        F1, G, H, A, o);
+    return;
+  }
+  qnet_pack_body(params, packed, g, N, D, F1, G, H, A, o, nb);
+  qnet_pack_h3_body(params, packed, g, N, D, F1, G, H, A, o, nb);
 }
 
 int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s) {
@@ -1513,7 +1591,7 @@ int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStre
   if (rc) return rc;
   const int64_t total = g.agent_stride * d->n_agents;
   const int threads = 256;
-  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 4096);
+  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 4096) + d->n_agents;
   hipLaunchKernelGGL(qnet_pack_kernel, dim3(blocks), dim3(threads), 0, s, params, packed, g, d->n_agents,
                      d->obs_dim, d->f1, d->g, d->h, d->n_actions, o);
   MM_HIP_CHECK(hipGetLastError());

@@ -46,7 +46,8 @@ int64_t mm_qnet_packed_count(const mm_qnet_dims* d) {
   mm::QnetGeo g;
   mm::QnetOffsets o;
   if (mm::qnet_geometry(d, &g, &o)) return -1;
-  return 2 * g.agent_stride * d->n_agents;  // [fp32 fragment image | fp16x3-split image]
+  // [fp32 fragment image | fp16x3-split image | per-agent fp16x3 safety flags (int, padded to 64)]
+  return 2 * g.agent_stride * d->n_agents + ((d->n_agents + 63) & ~63);
 }
 
 int mm_qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s) {

@@ -77,6 +77,32 @@ def test_qnet_forward_vs_oracle_shapes(f1, g, h, n, d, a, e):
     np.testing.assert_allclose(qsel.cpu().numpy(), qd.cpu().gather(2, greedy.unsqueeze(-1)).squeeze(-1).numpy())
 
 
+@pytest.mark.parametrize("case", ["activation", "weight"])
+def test_fp16x3_range_guard_falls_back_to_f32(case):
+    """The fp16x3-split forward (E >= 2048 uses the LDS image path) must not overflow silently: an agent
+    whose layer-1 output bound (|obs| <= 1) or largest weight reaches the f16 range is flagged at pack
+    time and runs on the exact-f32 image; results still match the f32 oracle for every agent."""
+    from minimarl.qnet import AgentQNet
+    n, d, a, e = 4, 47, 5, 2304
+    net = AgentQNet(n, d, a, 64, 64, 64, DEV, seed=3)
+    with torch.no_grad():
+        if case == "activation":
+            net.view("W1")[1, 0, :] = 3.0e3          # x1 ~ 3e3 * sum(obs) ~ 7e4 > 65504 for agent 1
+        elif case == "weight":
+            net.view("Whh")[2, 5, 7] = 1.0e5          # not representable in f16: inf in the hi image
+    net.mark_dirty()
+    P = {k: v.detach().cpu().clone() for k, v in net.params().items()}
+    gen = torch.Generator().manual_seed(9)
+    obs = torch.rand(e, n, d, generator=gen)
+    hid = torch.randn(e, n, 64, generator=gen) * 0.5
+    q, h2 = net.forward(obs.to(DEV), hid.to(DEV))
+    qo, ho = nets.agent_forward(P, obs, hid)
+    assert torch.isfinite(q).all() and torch.isfinite(h2).all()
+    scale = max(1.0, float(qo.abs().max()))
+    np.testing.assert_allclose(q.cpu().numpy(), qo.numpy(), rtol=1e-5, atol=2e-5 * scale)
+    np.testing.assert_allclose(h2.cpu().numpy(), ho.numpy(), rtol=1e-5, atol=2e-5)
+
+
 def test_eps_greedy_device_rng_rate():
     from minimarl.qnet import AgentQNet
     net = AgentQNet(8, 47, 5, 64, 32, 32, DEV, seed=1)
