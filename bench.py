@@ -194,9 +194,10 @@ def main():
     ap.add_argument("--learner-steps", type=int, default=100)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--mappo-episodes", type=int, default=2, help="timed MAPPO episodes (0 = skip)")
-    ap.add_argument("--cfg5", action="store_true",
-                    help="also time the cfg5 dual agent forward (E=8192, N=27, D=300, A=36); off by default so "
-                         "the default run's h3 dispatches are all the roofline's cfg2 launch")
+    ap.add_argument("--no-cfg5", action="store_true",
+                    help="skip the cfg5 lines (dual agent forward at E=8192, N=27, D=300, A=36 and the cfg5 "
+                         "QMIX update with the fp16 mixer state projection)")
+    ap.add_argument("--cfg5-batch", type=int, default=4096, help="cfg5 learner batch (chunks of C=10)")
     ap.add_argument("--learner-big-steps", type=int, default=10,
                     help="timed QMIX updates at B=4096 chunks (0 = skip; single-GPU runs only)")
     ap.add_argument("--offq-updates", type=int, default=30,
@@ -446,7 +447,7 @@ def main():
     # cfg5 (SMAC 27m_vs_30m-like shapes, no env of that shape exists here): the dual agent
     # forward (target + behavior) at E = 8192, N = 27, D = 300, A = 36, GRU-32 on synthetic obs
     cfg5 = None
-    if rank == 0 and args.cfg5:
+    if rank == 0 and not args.no_cfg5 and world == 1:
         import ctypes
         from minimarl._lib import MM_Q_ACT, MM_Q_MAX, lib
         from minimarl.qnet import AgentQNet, ptr, stream_handle
@@ -477,7 +478,33 @@ def main():
         cfg5 = {"workload": "cfg5 dual agent forward (target + behavior), synthetic obs", "envs": E5, "agents": N5,
                 "obs_dim": D5, "n_actions": A5, "gru": H5, "dual_us": round(t5 * 1e6, 2),
                 "agent_steps_per_s": round(2 * E5 * N5 / t5, 1), "tflops_fp32_equiv": round(f5 / t5 / 1e12, 2)}
-        del n5, o5, h5, hq
+        # cfg5 QMIX update at the throughput batch: agent nets GRU-32, Hm = 32 mixer over the 8100-wide
+        # state, the state projection on fp16 MFMA (SURVEY 8c tolerance: rtol 2e-3 on Q_tot, tested in
+        # test_gpu_learner.py); synthetic batch resident in HBM
+        B5, C5 = args.cfg5_batch, 10
+        m5 = [Mixer(N5, N5 * D5, 32, 32, dev, seed=7 + k) for k in range(2)]
+        l5 = QLearner(n5[1], n5[0], m5[0], m5[1], batch=B5, chunk=C5, mode="qmix", device=dev, mixer_fp16=True)
+        st5 = (torch.rand(B5, C5, N5, D5, device=dev, generator=g5) < 0.2).float()
+        ns5 = (torch.rand(B5, C5, N5, D5, device=dev, generator=g5) < 0.2).float()
+        act5b = torch.randint(0, A5, (B5, C5, N5), device=dev, generator=g5).float()
+        rew5 = torch.randn(B5, C5, N5, device=dev, generator=g5) * 0.5
+        dn5 = (torch.rand(B5, C5, 1, device=dev, generator=g5) < 0.1).float()
+        w5 = torch.rand(B5, 1, device=dev, generator=g5) * 0.5 + 0.5
+        l5.load_batch(st5, act5b, rew5, ns5, dn5, w5)
+        del st5, ns5
+        l5.capture_update(None, None, None)
+        l5.replay_update()
+        torch.cuda.synchronize()
+        k5 = 3
+        t6 = time.perf_counter()
+        for _ in range(k5):
+            l5.replay_update()
+        torch.cuda.synchronize()
+        el5 = (time.perf_counter() - t6) / k5
+        cfg5["learner"] = {"batch_chunks": B5, "chunk": C5, "mixer_state_projection": "fp16 MFMA (rtol 2e-3 on Q_tot)",
+                           "ms_per_update": round(el5 * 1e3, 3), "chunk_samples_per_s": round(B5 / el5, 1),
+                           "loss_finite": bool(torch.isfinite(l5.loss).all().item())}
+        del n5, o5, h5, hq, l5, m5
         torch.cuda.empty_cache()
 
     # roofline of the dominant kernel: the fused agent Q forward (one launch = target net on s'_t +

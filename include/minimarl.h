@@ -255,6 +255,12 @@ typedef struct mm_mix_net {
 int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
                 const float* P0, const int64_t* s_off0, float* gi0, const float* P1, const int64_t* s_off1, float* gi1,
                 mm_stream_t s);
+/* cfg5 fp16 mode of mm_mixer_gi (rtol 2e-3 on Q_tot, stated apart from the fp32 parity): the
+ * same projection on v_mfma_f32_32x32x16_f16 (state and W_ih rounded to f16, fp32 accumulate and bias);
+ * Hm in {32, 64}. */
+int mm_mixer_gi_f16(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
+                    const float* P0, const int64_t* s_off0, float* gi0, const float* P1, const int64_t* s_off1,
+                    float* gi1, mm_stream_t s);
 /* One mixer time step for 1-2 nets (behavior / target) in one launch. */
 /* Chunk-sequence mixer backward: all C steps (t = C-1 .. 0) in one launch, a block per sample
  * carrying dhm. Step t reads save [C][B][MSD], qa [C][B][N], dq [C][B] and writes dqa [C][B][N],

@@ -249,6 +249,93 @@ __global__ __launch_bounds__(256) void mixer_gi_tiled_kernel(MixGiArgs a) {
   }
 }
 
+// cfg5 fp16 mode (rtol 2e-3 on Q_tot, stated separately from the fp32 parity): the same
+// state projection gi = W_ih s + b_ih on v_mfma_f32_32x32x16_f16 (inputs rounded to f16, fp32
+// accumulate). Block = 64 samples x all 3Hm gate rows (RBK = 3Hm / 32 row blocks; 2 RBK waves, each one
+// 32 x 32 tile), the K = S state width in 64-deep chunks staged as f16 in LDS (row pitch 72 halves:
+// conflict-free 16-byte fragment reads), the next chunk's global loads in flight during the MFMAs.
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+template <int RBK>
+__global__ __launch_bounds__(64 * 2 * RBK) void mixer_gi_f16_kernel(MixGiArgs a) {
+  constexpr int NT = 64 * 2 * RBK, ROWS = 32 * RBK, PITCH = 72, KC = 64;
+  constexpr int NLD = (64 * KC + ROWS * KC + NT - 1) / NT;   // staged elements per thread per chunk
+  __shared__ __attribute__((aligned(16))) _Float16 sx[2][64 * PITCH];
+  __shared__ __attribute__((aligned(16))) _Float16 sw[2][ROWS * PITCH];
+  const MixGiNet& nt = a.net[blockIdx.y];
+  const int S = a.S, M3 = 3 * a.Hm;
+  const MixOff o = mix_offsets(S, a.Hm, a.K1, a.N);
+  const int c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  const int cw = wave & 1, rw = wave >> 1;   // this wave's 32 samples / 32 gate rows
+  // source row pointers of the elements this thread stages (fixed across chunks)
+  const float* src[NLD];
+  int dst[NLD], kk[NLD];
+#pragma unroll
+  for (int j = 0; j < NLD; ++j) {
+    const int idx = tid + j * NT;
+    if (idx < 64 * KC) {
+      const int p = idx / KC, x = idx % KC, c = min(c0 + p, a.R - 1);
+      const int64_t off = nt.s_off[c];
+      src[j] = (off >= 0 ? a.obs + off : a.reset_obs);
+      dst[j] = p * PITCH + x;
+      kk[j] = x;
+    } else {
+      const int i2 = min(idx - 64 * KC, ROWS * KC - 1);
+      const int m = i2 / KC, x = i2 % KC;
+      src[j] = nt.P + o.gWih + (int64_t)min(m, M3 - 1) * S;
+      dst[j] = -1 - (m * PITCH + x);   // negative: the W image
+      kk[j] = x;
+    }
+  }
+  float v[NLD];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) {
+      const int k = k0 + kk[j];
+      v[j] = src[j][min(k, S - 1)];
+      if (k >= S) v[j] = 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) {
+      if (tid + j * NT >= 64 * KC + ROWS * KC) continue;
+      if (dst[j] >= 0)
+        sx[buf][dst[j]] = (_Float16)v[j];
+      else
+        sw[buf][-1 - dst[j]] = (_Float16)v[j];
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  const int nch = (S + KC - 1) / KC;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nch) load((ch + 1) * KC);   // next chunk in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < KC / 16; ++ks) {
+      const h16x8 av = *reinterpret_cast<const h16x8*>(&sw[buf][(rw * 32 + li) * PITCH + ks * 16 + 8 * lh]);
+      const h16x8 bv = *reinterpret_cast<const h16x8*>(&sx[buf][(cw * 32 + li) * PITCH + ks * 16 + 8 * lh]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc, 0, 0, 0);
+    }
+    if (ch + 1 < nch) store(buf ^ 1);
+    __syncthreads();
+  }
+  // D: col = sample li, row = (q & 3) + 8 (q >> 2) + 4 lh
+  const int c = c0 + cw * 32 + li;
+  if (c < a.R) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int m = rw * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+      if (m < M3) nt.gi[(int64_t)c * M3 + m] = nt.P[o.gbih + m] + acc[q];
+    }
+  }
+}
+
 // One block per (sample, net): blockIdx.y selects behavior / target.
 __device__ __forceinline__ void mixer_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, int b);
 
@@ -2414,6 +2501,30 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
   }
   dim3 grid((R + 31) / 32, (3 * Hm + 31) / 32, P1 ? 2 : 1);
   hipLaunchKernelGGL(mm::mixer_gi_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_mixer_gi_f16(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
+                    const float* P0, const int64_t* s_off0, float* gi0, const float* P1, const int64_t* s_off1,
+                    float* gi1, mm_stream_t s) {
+  MM_REQUIRE(R > 0 && P0 && s_off0 && gi0 && obs && reset_obs, "mixer_gi_f16: bad args");
+  MM_REQUIRE(Hm == 32 || Hm == 64, "mixer_gi_f16: Hm must be 32 or 64");
+  mm::MixGiArgs a;
+  a.net[0] = {P0, s_off0, gi0};
+  a.net[1] = {P1 ? P1 : P0, P1 ? s_off1 : s_off0, P1 ? gi1 : gi0};
+  a.obs = obs;
+  a.reset_obs = reset_obs;
+  a.R = R;
+  a.S = S;
+  a.Hm = Hm;
+  a.K1 = K1;
+  a.N = N;
+  dim3 grid((R + 63) / 64, P1 ? 2 : 1);
+  if (Hm == 32)
+    hipLaunchKernelGGL(mm::mixer_gi_f16_kernel<3>, grid, dim3(384), 0, (hipStream_t)s, a);
+  else
+    hipLaunchKernelGGL(mm::mixer_gi_f16_kernel<6>, grid, dim3(768), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

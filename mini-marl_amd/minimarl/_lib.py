@@ -180,6 +180,8 @@ _SIGS += [
     ("mm_mixer_fwd", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, ctypes.POINTER(MixNetIO), c_i32, c_vp]),
     ("mm_mixer_gi", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                             c_vp]),
+    ("mm_mixer_gi_f16", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                            c_vp]),
     ("mm_lrn_loss", c_i32, [c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                             c_vp, c_vp, c_vp, c_vp]),
     ("mm_lrn_loss_ex", c_i32, [c_i32, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,

@@ -101,7 +101,7 @@ class QLearner:
 
     def __init__(self, behavior, target, mixer=None, target_mixer=None, batch=32, chunk=10, gamma=0.99, lr=1e-3,
                  grad_clip=5.0, betas=(0.9, 0.999), adam_eps=1e-8, mode="qmix", clip_mixer=False, device="cuda",
-                 reference_compat=True):
+                 reference_compat=True, mixer_fp16=False):
         assert mode in ("qmix", "vdn", "qmix_min", "vdn_double")
         self.mode = mode
         self.has_mixer = mode in ("qmix", "qmix_min")
@@ -113,6 +113,9 @@ class QLearner:
         # agent count and the IS weight scales the target) by the textbook sum_i r_i + gamma * (1-d) * Q'_tot
         # of qmix/qmix.py:215-217 (no IS weight)
         self.reference_compat = bool(reference_compat)
+        # cfg5 mode: the mixer state projection [B*C, N*D] x [N*D, 3Hm] on fp16 MFMA (rtol 2e-3
+        # on Q_tot, a tolerance stated apart from the fp32 parity)
+        self.mixer_fp16 = bool(mixer_fp16)
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM
         # chunk-sequence launches: agent REC and mixer backward as one launch each for all C steps
@@ -290,8 +293,9 @@ class QLearner:
         if self.has_mixer:
             # mixer GRU input projections of every (t, b) for both mixers: one MFMA launch
             mx = self.mix
-            check(L.mm_mixer_gi(CB, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, ptr(mx.flat), ptr(self.s_off),
-                                ptr(self.gi_b), ptr(self.tmix.flat), ptr(self.s2_off), ptr(self.gi_t), s), "mixer gi")
+            gi_fn = L.mm_mixer_gi_f16 if self.mixer_fp16 else L.mm_mixer_gi
+            check(gi_fn(CB, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, ptr(mx.flat), ptr(self.s_off),
+                        ptr(self.gi_b), ptr(self.tmix.flat), ptr(self.s2_off), ptr(self.gi_t), s), "mixer gi")
         # ---- forward over the chunk: the non-recurrent part (layers 1-2, W_ih x2) of every (t, b) of
         # both nets in ONE launch, then one recurrent step (W_hh h, gates, Q head) per t
         pb, pt = QFwdIO(), QFwdIO()

@@ -290,6 +290,28 @@ def qmix_loss(P, M, T, TM, batch, gamma, hidden_dim=32):
     return loss, target.detach(), qtot
 
 
+def qmix_qtot(P, M, batch, hidden_dim=32):
+    """Behavior Q_tot of every (t, b) of a chunk batch, [C, B] (the forward half of qmix_loss,
+    qmix/_train.py:55-75, hiddens reset where done)."""
+    s, a, _, _, d, _ = batch
+    B, C, N, _ = s.shape
+    H = P["Whh"].shape[2]
+    Hm = M["gWhh"].shape[1]
+    h = torch.zeros(B, N, H)
+    hm = torch.zeros(B, Hm)
+    out = []
+    with torch.no_grad():
+        for t in range(C):
+            q, nh = agent_forward(P, s[:, t], h)
+            qa = q.gather(2, a[:, t].unsqueeze(-1).long()).squeeze(-1)
+            qtot, nhm = mixer_forward(M, qa, s[:, t], hm, hidden_dim)
+            out.append(qtot.view(B))
+            keep = (1.0 - d[:, t]).view(B, 1)
+            h = nh * keep.view(B, 1, 1)
+            hm = nhm * keep
+    return torch.stack(out)
+
+
 def qmix_train_step(P, M, T, TM, batch, gamma, lr, grad_clip, adam_state=None, hidden_dim=32):
     """One Train_dqn update: backward, clip_grad_norm_ over AGENT params only
     (qmix/_train.py:111-115), Adam over agent + mixer (qmix/main.py:79-85)."""
