@@ -18,6 +18,7 @@
  *   mm_lrn_, mm_..._bwd  Train_dqn.train / Target_Dqn.train          qmix/_train.py:19-121; vdn/_train.py:184-235
  *   mm_mappo_fwd         R_MAPPOPolicy.get_actions/get_values/evaluate_actions  mappo/algorithms/rmappo_policy.py:57-136
  *   mm_mappo_bwd, wgrad  R_MAPPO.ppo_update/cal_value_loss/train     mappo/algorithms/ramppo_network.py:56-287
+ *   mm_mappo_grad        (fused: forward recompute + BPTT + weight grads of one epoch, same lines)
  *   mm_mappo_gae, insert SharedReplayBuffer.compute_returns/insert   mappo/runner/shared/shared_buffer.py:82-157
  *   mm_offq_*            offpolicy QMix.train_policy_on_batch etc.   offpolicy/algorithms/qmix/qmix.py:80-226
  *   mm_eval_accum        greedy test loops                           vdn/_test.py:22-50; magym_runner.py:198-241
@@ -419,6 +420,17 @@ int mm_mappo_fwd(const mm_mappo_dims* d, const mm_mappo_fwd_args* a, mm_stream_t
 /* Loss seeds + chunked BPTT of both nets (after a TRAIN forward of the same data). */
 int mm_mappo_bwd(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, mm_stream_t s);
 /* Weight gradients of one net from mm_mappo_bwd's SoA operands into its flat gradient vector. */
+/* One PPO epoch's gradients of both nets in one pass (mappo_grad.hip; replaces mm_mappo_fwd TRAIN +
+ * mm_mappo_bwd + mm_mappo_wgrad, ramppo_network.py:56-209): per tile of 32 L-step chunks the forward
+ * is run from the stored chunk-start hiddens (h_actor / h_critic = rnn_states / rnn_states_critic
+ * [T+1, EN, H], 16-byte aligned), recomputed step by step in reverse for the BPTT, and the weight
+ * gradients are reduced on MFMA inside the kernel. Uses a's P, obs, mask, active, act, adv, old_logp,
+ * old_value, returns, stats, loss_acc, coefficients, en, T, L (save / gsoa / rs ignored). Writes the
+ * full flat gradient vectors. scratch: mm_mappo_grad_scratch_count(d, L) floats, 16-byte aligned.
+ * H 32, A 5, D 47 | 94. */
+int64_t mm_mappo_grad_scratch_count(const mm_mappo_dims* d, int32_t L);
+int mm_mappo_grad(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, const float* h_actor, const float* h_critic,
+                  float* grad_actor, float* grad_critic, float* scratch, mm_stream_t s);
 int64_t mm_mappo_wgrad_partial_count(const mm_mappo_dims* d, int64_t rs);
 int mm_mappo_wgrad(const mm_mappo_dims* d, int32_t net, const float* gsoa, int64_t rs, float* grad, float* partial,
                    mm_stream_t s);

@@ -1,0 +1,908 @@
+// MAPPO training gradients on MFMA, one pass over the buffer per PPO epoch (replaces the per-thread
+// TRAIN forward + saves, the BPTT backward writing per-row gradient operands and the separate
+// weight-gradient reduction: no per-row arrays leave the chip except one hidden state per step).
+//
+// Reference (restated in oracle/mappo.py, pinned by tests/golden/mappo_*.npz):
+//   trunk  mappo/utils/algorithm_utils/mlp.py:31-55, rnn.py:24-29,79, act.py / distributions.py,
+//          r_actor_critic.py:189-208
+//   loss   mappo/algorithms/ramppo_network.py:56-209 (ppo_update, cal_value_loss)
+//   chunks mappo/runner/shared/shared_buffer.py:318-427 (L steps, start hidden = stored hidden)
+//
+// Layout: one wave = one tile of 32 chunks. Activations live in the MFMA "act-frag" layout: lane
+// (c, h) = (lane & 31, lane >> 5) holds, for chunk c, the 16 features kperm(q, h) of a 32-wide
+// vector (q = 0..15), which is exactly the D layout of v_mfma_f32_32x32x2_f32 with features on M and
+// chunks on N and, with the same k permutation, the B operand of the next layer — forward and
+// backward layer chains need no data movement. Weight gradients dW[m][n] = sum_c delta[m][c] x[n][c]
+// put the chunk index on the MFMA k dimension: delta and x tiles are transposed through a per-wave
+// LDS tile (4 x ds_write_b128 + 16 x ds_read_b32 per lane), and the same transposed reads give the
+// bias and LayerNorm column sums. Each wave keeps its weight-gradient accumulators in registers
+// across all its tiles; a block reduces its 4 waves in LDS and writes one partial; a second kernel
+// sums the partials in a fixed order (deterministic).
+//
+// Per tile: pass 1 runs the trunk forward over the L steps from the stored chunk-start hidden and
+// keeps the L input hiddens in a per-wave global scratch (L2-resident, reused across tiles); pass 2
+// walks the steps backwards, recomputes each step's forward from its input hidden and runs the
+// backward. Weights: the net's matrices are staged once per block into LDS with padded row pitches
+// (16-byte A-fragment reads) plus transposed copies of W_ih / W_hh for the backward data chain.
+#include "common.h"
+#include "minimarl.h"
+#include "trunk.h"
+
+namespace mm {
+namespace mgr {
+
+constexpr int H = 32;          // hidden width this kernel is written for
+constexpr int TP = 36;         // pitch of a transpose tile row (one chunk)
+constexpr int TILE = 32 * TP;  // floats per transpose tile
+constexpr int NTW = 4;         // transpose tiles per wave
+constexpr int NWAVE = 4;       // waves per block (one block per CU: ~140 KB of LDS)
+constexpr int NB = 128;        // blocks per net
+
+template <int D, int O>
+struct Geo {
+  static constexpr int DT = (D + 31) / 32, DPT = 32 * DT, P1 = DPT + 4, PW = 36, PT = 100;
+  static constexpr int W1 = 0, W2 = W1 + 32 * P1, Wih = W2 + 32 * PW, Whh = Wih + 96 * PW, WihT = Whh + 96 * PW,
+                       WhhT = WihT + 32 * PT, ln0w = WhhT + 32 * PT, ln0b = ln0w + DPT, b1 = ln0b + DPT,
+                       ln1w = b1 + 32, ln1b = ln1w + 32, b2 = ln1b + 32, ln2w = b2 + 32, ln2b = ln2w + 32,
+                       bih = ln2b + 32, bhh = bih + 96, lnrw = bhh + 96, lnrb = lnrw + 32, Wo = lnrb + 32,
+                       bo = Wo + 8 * 32, scr = bo + 8, total = scr + NWAVE * NTW * TILE;
+  static_assert(O <= 8, "head wider than 8 outputs");
+};
+
+__device__ __forceinline__ float xsum(float v) { return v + __shfl_xor(v, 32); }
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// a zero the compiler cannot see through: LDS bases offset by it are re-derived per step, so the
+// loop-invariant weight / LayerNorm reads are not hoisted out of the tile loop into hundreds of VGPRs
+__device__ __forceinline__ int opaque0() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+// scheduling fence between the phases of a step: one step is a single basic block of ~1000
+// instructions, and without fences the scheduler hoists every LDS / global load of later phases
+// (occupancy 1 looks like 512 free registers to it) and spills
+#define MG_PHASE() __builtin_amdgcn_sched_barrier(0)
+__device__ __forceinline__ int lane_c() { return (int)(threadIdx.x & 31); }
+__device__ __forceinline__ int lane_h() { return (int)((threadIdx.x >> 5) & 1); }
+
+// acc += W[(lane & 31)][kperm(s, h)] * v[s] over s < 16 (row-major LDS W, pitch P): W v in act-frag
+template <int P>
+__device__ __forceinline__ void mm_rows(const float* W, const float (&v)[16], f32x16& acc) {
+  const float* wr = W + lane_c() * P + 4 * lane_h();
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 a4 = *reinterpret_cast<const float4*>(wr + 8 * g);
+    acc = mfma32(a4.x, v[4 * g], acc);
+    acc = mfma32(a4.y, v[4 * g + 1], acc);
+    acc = mfma32(a4.z, v[4 * g + 2], acc);
+    acc = mfma32(a4.w, v[4 * g + 3], acc);
+  }
+}
+// acc += W[kperm(s, h)][(lane & 31)] * v[s]: W^T v in act-frag (column reads of row-major W, pitch P)
+template <int P>
+__device__ __forceinline__ void mm_cols(const float* W, const float (&v)[16], f32x16& acc) {
+  const float* wc = W + 4 * lane_h() * P + lane_c();
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma32(wc[kperm(s, 0) * P], v[s], acc);
+}
+
+// transpose tile: lane (c, h) stores its act-frag vector as row c; reads give lane (i, h) feature i of
+// chunk 2 s + h at k-step s
+__device__ __forceinline__ void tput(float* T, const float (&v)[16]) {
+  float* p = T + lane_c() * TP + 4 * lane_h();
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<float4*>(p + 8 * g) = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+}
+__device__ __forceinline__ void tget(const float* T, float (&o)[16]) {
+  const float* p = T + lane_h() * TP + lane_c();
+#pragma unroll
+  for (int s = 0; s < 16; ++s) o[s] = p[2 * s * TP];
+}
+__device__ __forceinline__ float tsum(const float* T) {
+  const float* p = T + lane_h() * TP + lane_c();
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += p[2 * k * TP];
+  return s;
+}
+
+// weight-gradient accumulation: the accumulators stay in AGPRs for the whole kernel (the compiler
+// otherwise shuttles them between the register files under the pressure of the step's activations)
+__device__ __forceinline__ void acc_mfma(f32x16& acc, float a, float b) {
+#ifdef MG_NO_ACC
+  (void)acc; (void)a; (void)b;
+#elif defined(MG_ASM_ACC)
+  asm("v_mfma_f32_32x32x2_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+#else
+  acc = mfma32(a, b, acc);
+#endif
+}
+
+__device__ __forceinline__ void ld16(const float* p, float (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 t = reinterpret_cast<const float4*>(p)[g];
+    v[4 * g] = t.x;
+    v[4 * g + 1] = t.y;
+    v[4 * g + 2] = t.z;
+    v[4 * g + 3] = t.w;
+  }
+}
+__device__ __forceinline__ void st16(float* p, const float (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    reinterpret_cast<float4*>(p)[g] = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+}
+// a pointer the compiler cannot see through (no store-to-load forwarding of parked registers)
+__device__ __forceinline__ const float* opaque_ptr(const float* p) {
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+__device__ __forceinline__ void zero16(f32x16& a) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) a[q] = 0.f;
+}
+
+// LayerNorm statistics of a 32-wide act-frag vector (both lane halves get them)
+__device__ __forceinline__ void ln32(const float (&v)[16], float& mu, float& rs) {
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) s += v[q];
+  mu = xsum(s) / 32.f;
+  float d2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) d2 = fmaf(v[q] - mu, v[q] - mu, d2);
+  rs = 1.0f / sqrtf(xsum(d2) / 32.f + kLnEps);
+}
+// LayerNorm backward (trunk.h ln_bwd) of act-frag dy with normalised input xh, LN weight w (LDS)
+__device__ __forceinline__ void ln32_bwd(const float (&dy)[16], const float (&xh)[16], float rs, const float* w,
+                                         float (&dx)[16]) {
+  const int h = lane_h();
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float g = dy[q] * w[kperm(q, h)];
+    sg += g;
+    sgx = fmaf(g, xh[q], sgx);
+  }
+  sg = xsum(sg) / 32.f;
+  sgx = xsum(sgx) / 32.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) dx[q] = rs * (dy[q] * w[kperm(q, h)] - sg - xh[q] * sgx);
+}
+
+// stage the net's flat MGeo parameters into the padded LDS image
+template <int D, int O>
+__device__ void stage(float* sm, const float* __restrict__ P) {
+  using G = Geo<D, O>;
+  using F = MGeo<D, H, O>;
+  for (int e = threadIdx.x; e < G::scr; e += blockDim.x) {
+    float v = 0.f;
+    if (e < G::W2) {
+      const int m = e / G::P1, k = e - m * G::P1;
+      if (k < D) v = P[F::W1 + m * F::Dp + k];
+    } else if (e < G::Wih) {
+      const int r = e - G::W2, m = r / G::PW, k = r - m * G::PW;
+      if (k < H) v = P[F::W2 + m * H + k];
+    } else if (e < G::Whh) {
+      const int r = e - G::Wih, m = r / G::PW, k = r - m * G::PW;
+      if (k < H) v = P[F::Wih + m * H + k];
+    } else if (e < G::WihT) {
+      const int r = e - G::Whh, m = r / G::PW, k = r - m * G::PW;
+      if (k < H) v = P[F::Whh + m * H + k];
+    } else if (e < G::WhhT) {
+      const int r = e - G::WihT, i = r / G::PT, j = r - i * G::PT;
+      if (j < 3 * H) v = P[F::Wih + j * H + i];
+    } else if (e < G::ln0w) {
+      const int r = e - G::WhhT, i = r / G::PT, j = r - i * G::PT;
+      if (j < 3 * H) v = P[F::Whh + j * H + i];
+    } else if (e < G::ln0b) {
+      const int k = e - G::ln0w;
+      if (k < D) v = P[F::ln0_w + k];
+    } else if (e < G::b1) {
+      const int k = e - G::ln0b;
+      if (k < D) v = P[F::ln0_b + k];
+    } else if (e < G::bih) {
+      const int r = e - G::b1, seg = r >> 5, i = r & 31;
+      const int src[6] = {F::b1, F::ln1_w, F::ln1_b, F::b2, F::ln2_w, F::ln2_b};
+      v = P[src[seg] + i];
+    } else if (e < G::lnrw) {
+      const int r = e - G::bih;
+      v = r < 96 ? P[F::bih + r] : P[F::bhh + r - 96];
+    } else if (e < G::Wo) {
+      const int r = e - G::lnrw;
+      v = r < 32 ? P[F::lnr_w + r] : P[F::lnr_b + r - 32];
+    } else if (e < G::bo) {
+      const int r = e - G::Wo, o = r >> 5, i = r & 31;
+      if (o < O) v = P[F::Wo + o * H + i];
+    } else {
+      const int o = e - G::bo;
+      if (o < O) v = P[F::bo + o];
+    }
+    sm[e] = v;
+  }
+  __syncthreads();
+}
+
+// obs row -> DT act-frag tiles (feature 32 t + kperm(q, h); zero beyond D)
+template <int D, int DT>
+__device__ __forceinline__ void load_obs(const float* __restrict__ orow, float (&x)[DT][16]) {
+  const int h = lane_h();
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int f = 32 * t + kperm(q, h);
+      const float v = orow[f < D ? f : D - 1];
+      x[t][q] = f < D ? v : 0.f;
+    }
+}
+
+template <int D, int DT>
+__device__ __forceinline__ void ln0_stats(const float (&x)[DT][16], float& mu, float& rs) {
+  const int h = lane_h();
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += x[t][q];
+  mu = xsum(s) / (float)D;
+  float d2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float d = 32 * t + kperm(q, h) < D ? x[t][q] - mu : 0.f;
+      d2 = fmaf(d, d, d2);
+    }
+  rs = 1.0f / sqrtf(xsum(d2) / (float)D + kLnEps);
+}
+
+// The trunk forward of one step up to the new hidden (LN0, L1, LN1, L2, LN2, GRU) in act-frag.
+template <int D, int O>
+struct Step {
+  using G = Geo<D, O>;
+  static constexpr int DT = G::DT;
+  float mu0, rs0, a1[16], mu1, rs1, a2[16], mu2, rs2, r[16], z[16], n[16], ghn[16], h2[16];
+
+  __device__ __forceinline__ void run(const float* sm, const float* __restrict__ orow, const float (&hin)[16]) {
+    const int h = lane_h();
+    float x[DT][16];
+    load_obs<D, DT>(orow, x);
+    ln0_stats<D, DT>(x, mu0, rs0);
+    f32x16 acc;
+    zero16(acc);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      float f0[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int f = 32 * t + kperm(q, h);
+        f0[q] = (x[t][q] - mu0) * rs0 * sm[G::ln0w + f] + sm[G::ln0b + f];
+      }
+      mm_rows<G::P1>(sm + G::W1 + 32 * t, f0, acc);
+      MG_PHASE();
+    }
+    float f[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a1[q] = fmaxf(acc[q] + sm[G::b1 + kperm(q, h)], 0.f);
+    ln32(a1, mu1, rs1);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) f[q] = (a1[q] - mu1) * rs1 * sm[G::ln1w + kperm(q, h)] + sm[G::ln1b + kperm(q, h)];
+    zero16(acc);
+    mm_rows<G::PW>(sm + G::W2, f, acc);
+    MG_PHASE();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a2[q] = fmaxf(acc[q] + sm[G::b2 + kperm(q, h)], 0.f);
+    ln32(a2, mu2, rs2);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) f[q] = (a2[q] - mu2) * rs2 * sm[G::ln2w + kperm(q, h)] + sm[G::ln2b + kperm(q, h)];
+    // GRU, torch gate order r, z, n; h' = n + z (h - n)
+    f32x16 ai, ah;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      zero16(ai);
+      zero16(ah);
+      mm_rows<G::PW>(sm + G::Wih + 32 * g * G::PW, f, ai);
+      mm_rows<G::PW>(sm + G::Whh + 32 * g * G::PW, hin, ah);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = 32 * g + kperm(q, h);
+        const float gi = ai[q] + sm[G::bih + j], gh = ah[q] + sm[G::bhh + j];
+        if (g == 0) r[q] = sigmoidf_(gi + gh);
+        if (g == 1) z[q] = sigmoidf_(gi + gh);
+        if (g == 2) {
+          ghn[q] = gh;
+          n[q] = tanhf_(gi + r[q] * gh);
+        }
+      }
+      MG_PHASE();
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) h2[q] = n[q] + z[q] * (hin[q] - n[q]);
+  }
+};
+
+struct GradArgs {
+  mm_mappo_bwd_args a;
+  const float* h_in[2];
+  float* hseq;      // [2][NB * NWAVE][L + 2][64 * 16]: input hidden per step, then a1 / a2 of the step
+  float* partial;   // [2][NB][pstride]
+  int64_t pstride;
+};
+
+template <int D, int A, int O>
+__device__ void grad_body(const GradArgs& k, int net, float* sm) {
+  using G = Geo<D, O>;
+  using F = MGeo<D, H, O>;
+  constexpr int DT = G::DT;
+  const mm_mappo_bwd_args& a = k.a;
+  stage<D, O>(sm, a.P[net]);
+  const int lane = (int)(threadIdx.x & 63), ci = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform: scalar loop control
+  float* S0 = sm + G::scr + w * NTW * TILE;
+  float* S1 = S0 + TILE;
+  float* S2 = S1 + TILE;
+  float* S3 = S2 + TILE;
+  const int L = a.L;
+  const int64_t EN = a.en, nch = (int64_t)(a.T / L) * EN, ntile = (nch + 31) / 32;
+  const int wg = blockIdx.x * NWAVE + w, nwg = gridDim.x * NWAVE;
+  float* hs = k.hseq + ((int64_t)net * nwg + wg) * (L + 2) * 1024 + lane * 16;
+  const float* __restrict__ hin0 = k.h_in[net];
+  const float inv_m = 1.0f / a.stats[MM_MST_ACTIVE_SUM];
+
+  f32x16 aWih[3], aWhh[3], aW2, aW1[DT], aWo;
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    zero16(aWih[g]);
+    zero16(aWhh[g]);
+  }
+  zero16(aW2);
+  zero16(aWo);
+#pragma unroll
+  for (int t = 0; t < DT; ++t) zero16(aW1[t]);
+  float sbr = 0.f, sbz = 0.f, sbn = 0.f, sbhn = 0.f, sb2 = 0.f, sb1 = 0.f, sbo = 0.f;
+  float slrw = 0.f, slrb = 0.f, sl2w = 0.f, sl2b = 0.f, sl1w = 0.f, sl1b = 0.f, sl0w[DT], sl0b[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) sl0w[t] = sl0b[t] = 0.f;
+  float lsum0 = 0.f, lsum1 = 0.f, lsum2 = 0.f;
+
+  for (int64_t tile = wg; tile < ntile; tile += nwg) {
+    const int64_t c = tile * 32 + ci;
+    const bool valid = c < nch;
+    const int64_t cc = valid ? c : 0, kc = cc / EN, en = cc - kc * EN;
+    // ---- pass 1: forward over the chunk, input hidden of every step kept in the wave scratch
+    float hc[16];
+    {
+      const float* hp = hin0 + ((kc * L) * EN + en) * H + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 v = *reinterpret_cast<const float4*>(hp + 8 * g);
+        hc[4 * g] = v.x;
+        hc[4 * g + 1] = v.y;
+        hc[4 * g + 2] = v.z;
+        hc[4 * g + 3] = v.w;
+      }
+    }
+    for (int l = 0; l < L; ++l) {
+      const int64_t row = (kc * L + l) * EN + en;
+      const float m = a.mask[row];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) hc[q] *= m;
+      float4* hsl = reinterpret_cast<float4*>(hs + l * 1024);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) hsl[g] = make_float4(hc[4 * g], hc[4 * g + 1], hc[4 * g + 2], hc[4 * g + 3]);
+      if (l + 1 < L) {
+        Step<D, O> st;
+        st.run(sm + opaque0(), a.obs + row * D, hc);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) hc[q] = st.h2[q];
+      }
+    }
+    // ---- pass 2: backward over the steps, each step's forward recomputed from its input hidden
+    float dhn[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dhn[q] = 0.f;
+    for (int l = L - 1; l >= 0; --l) {
+      const int64_t row = (kc * L + l) * EN + en;
+      float hin[16];
+      ld16(hs + l * 1024, hin);
+      Step<D, O> st;
+      st.run(sm + opaque0(), a.obs + row * D, hin);
+      const float* smb = sm + opaque0();
+      const float mu0 = st.mu0, rs0 = st.rs0, mu1 = st.mu1, rs1 = st.rs1, mu2 = st.mu2, rs2 = st.rs2;
+      // a1 / a2 are needed again only by the LN2 / LN1 backward: parked in the wave scratch (L2) so
+      // the GRU backward has the registers; the GRU weight-gradient inputs x2 / hin go to tiles S0 / S1
+      st16(hs + L * 1024, st.a1);
+      st16(hs + (L + 1) * 1024, st.a2);
+      {
+        float x2[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          x2[q] = (st.a2[q] - mu2) * rs2 * smb[G::ln2w + kperm(q, h)] + smb[G::ln2b + kperm(q, h)];
+        tput(S0, x2);
+        tput(S1, hin);
+      }
+      MG_PHASE();
+      // head: y = LN_r(h2); out = Wo y + bo
+      float mur, rsr, xr[16], y[16];
+      ln32(st.h2, mur, rsr);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        xr[q] = (st.h2[q] - mur) * rsr;
+        y[q] = xr[q] * smb[G::lnrw + kperm(q, h)] + smb[G::lnrb + kperm(q, h)];
+      }
+      float out[O];
+#pragma unroll
+      for (int o = 0; o < O; ++o) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) s = fmaf(smb[G::Wo + o * 32 + kperm(q, h)], y[q], s);
+        out[o] = smb[G::bo + o] + xsum(s);
+      }
+      // ---- loss seed d(out) (mappo.hip bwd_body; ramppo_network.py:56-209)
+      const float m = valid ? a.active[row] : 0.f;
+      float dout[O];
+      if constexpr (O == A) {
+        float mx = out[0];
+#pragma unroll
+        for (int q = 1; q < A; ++q) mx = fmaxf(mx, out[q]);
+        float se = 0.f;
+#pragma unroll
+        for (int q = 0; q < A; ++q) se += expf(out[q] - mx);
+        const float lse = mx + logf(se);
+        float lp[A], ent = 0.f;
+#pragma unroll
+        for (int q = 0; q < A; ++q) {
+          lp[q] = out[q] - lse;
+          ent -= expf(lp[q]) * lp[q];
+        }
+        const int act = a.act[row];
+        float lpa = lp[0];
+#pragma unroll
+        for (int q = 1; q < A; ++q)
+          if (q == act) lpa = lp[q];
+        const float adv = (a.adv[row] - a.stats[MM_MST_ADV_MEAN]) / (a.stats[MM_MST_ADV_STD] + 1e-5f);
+        const float ratio = expf(lpa - a.old_logp[row]);
+        const float s1 = ratio * adv;
+        const float rc = fminf(fmaxf(ratio, 1.0f - a.clip), 1.0f + a.clip);
+        const float s2 = rc * adv;
+        const float inr = (ratio >= 1.0f - a.clip && ratio <= 1.0f + a.clip) ? 1.0f : 0.0f;
+        // torch.min backward: the smaller side gets the gradient, ties split it in half
+        const float g = s1 < s2 ? 1.0f : (s1 > s2 ? inr : 0.5f + 0.5f * inr);
+        const float dlpa = -m * inv_m * adv * ratio * g;
+        const float dent = -a.entropy_coef * m * inv_m;
+        if (h == 0 && valid) {
+          lsum0 += -fminf(s1, s2) * m;
+          lsum1 += ent * m;
+          lsum2 += ratio;
+        }
+#pragma unroll
+        for (int q = 0; q < A; ++q) {
+          const float p = expf(lp[q]);
+          dout[q] = dlpa * ((q == act ? 1.0f : 0.0f) - p) + dent * (-p * (lp[q] + ent));
+        }
+      } else {
+        const float v = out[0];
+        const float old = a.old_value[row];
+        const float tgt = (a.returns[row] - a.stats[MM_MST_VN_MEAN]) / a.stats[MM_MST_VN_STD];
+        const float dv = v - old;
+        const float vc = old + fminf(fmaxf(dv, -a.clip), a.clip);
+        const float eo = tgt - v, ec = tgt - vc;
+        const float hd = a.huber_delta;
+        const float lo = fabsf(eo) <= hd ? eo * eo * 0.5f : hd * (fabsf(eo) - hd * 0.5f);
+        const float lc = fabsf(ec) <= hd ? ec * ec * 0.5f : hd * (fabsf(ec) - hd * 0.5f);
+        const float go = -(fabsf(eo) <= hd ? eo : (eo > 0.f ? hd : -hd));
+        const float gc =
+            -(fabsf(ec) <= hd ? ec : (ec > 0.f ? hd : -hd)) * ((dv >= -a.clip && dv <= a.clip) ? 1.0f : 0.0f);
+        const float d = lo > lc ? go : (lc > lo ? gc : 0.5f * (go + gc));
+        dout[0] = a.value_coef * m * inv_m * d;
+        if (h == 0 && valid) lsum0 += fmaxf(lo, lc) * m;
+      }
+      MG_PHASE();
+      // ---- head gradients: dWo = dout y^T, dbo = dout (MFMA with chunks on k); dy = Wo^T dout
+      float dy[16];
+      {
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int o = kperm(q, h);
+          float d = 0.f, s = 0.f;
+#pragma unroll
+          for (int oo = 0; oo < O; ++oo) {
+            if (oo == o) d = dout[oo];
+            s = fmaf(smb[G::Wo + oo * 32 + o], dout[oo], s);
+          }
+          v[q] = d;
+          dy[q] = s;
+        }
+        tput(S2, v);
+        tput(S3, y);
+        wave_fence();
+        float At[16], Bt[16];
+        tget(S2, At);
+        tget(S3, Bt);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          acc_mfma(aWo, At[s], Bt[s]);
+          sbo += At[s];
+        }
+        wave_fence();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = dy[q] * xr[q];
+        tput(S2, v);
+        tput(S3, dy);
+        wave_fence();
+        slrw += tsum(S2);
+        slrb += tsum(S3);
+        wave_fence();
+      }
+      // LN_r backward -> d h2 (+ the gradient carried from the next step)
+      float dh[16];
+      ln32_bwd(dy, xr, rsr, smb + G::lnrw, dh);
+      // ---- GRU backward (h2 = n + z (hin - n); gates r, z, n)
+      float dgr[16], dgz[16], dpn[16], dghn[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float d = dh[q] + dhn[q];
+        const float r = st.r[q], z = st.z[q], n = st.n[q];
+        const float dn = d * (1.0f - z);
+        const float dz = d * (hin[q] - n);
+        dpn[q] = dn * (1.0f - n * n);
+        dgr[q] = dpn[q] * st.ghn[q] * r * (1.0f - r);
+        dgz[q] = dz * z * (1.0f - z);
+        dghn[q] = dpn[q] * r;
+        dhn[q] = d * z;
+      }
+      MG_PHASE();
+      f32x16 dx2;
+      zero16(dx2);
+      mm_rows<G::PT>(smb + G::WihT, dgr, dx2);
+      mm_rows<G::PT>(smb + G::WihT + 32, dgz, dx2);
+      mm_rows<G::PT>(smb + G::WihT + 64, dpn, dx2);
+      MG_PHASE();
+      {
+        f32x16 dhh;
+        zero16(dhh);
+        mm_rows<G::PT>(smb + G::WhhT, dgr, dhh);
+        mm_rows<G::PT>(smb + G::WhhT + 32, dgz, dhh);
+        mm_rows<G::PT>(smb + G::WhhT + 64, dghn, dhh);
+        const float mk = a.mask[row];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dhn[q] = (dhn[q] + dhh[q]) * mk;
+      }
+      MG_PHASE();
+      // GRU weight gradients: dW_ih += dg x2^T, dW_hh += dgh hin^T (x2 in S0, hin in S1), biases
+      tput(S2, dgr);
+      tput(S3, dgz);
+      wave_fence();
+#pragma unroll
+      for (int s0 = 0; s0 < 16; s0 += 4) {
+        float X[4], Hh[4], R[4], Z[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int off = h * TP + ci + 2 * (s0 + j) * TP;
+          X[j] = S0[off];
+          Hh[j] = S1[off];
+          R[j] = S2[off];
+          Z[j] = S3[off];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc_mfma(aWih[0], R[j], X[j]);
+          acc_mfma(aWhh[0], R[j], Hh[j]);
+          acc_mfma(aWih[1], Z[j], X[j]);
+          acc_mfma(aWhh[1], Z[j], Hh[j]);
+          sbr += R[j];
+          sbz += Z[j];
+        }
+      }
+      wave_fence();
+      tput(S2, dpn);
+      tput(S3, dghn);
+      wave_fence();
+#pragma unroll
+      for (int s0 = 0; s0 < 16; s0 += 4) {
+        float X[4], Hh[4], Nn[4], Nh[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int off = h * TP + ci + 2 * (s0 + j) * TP;
+          X[j] = S0[off];
+          Hh[j] = S1[off];
+          Nn[j] = S2[off];
+          Nh[j] = S3[off];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc_mfma(aWih[2], Nn[j], X[j]);
+          acc_mfma(aWhh[2], Nh[j], Hh[j]);
+          sbn += Nn[j];
+          sbhn += Nh[j];
+        }
+      }
+      wave_fence();
+      // ---- LN2 backward (x2 = LN2(a2), a2 = relu(W2 f1 + b2))
+      float da[16], xh[16], tt[16];
+      {
+        float av[16], dxv[16];
+        ld16(opaque_ptr(hs + (L + 1) * 1024), av);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          xh[q] = (av[q] - mu2) * rs2;
+          dxv[q] = dx2[q];
+        }
+        ln32_bwd(dxv, xh, rs2, smb + G::ln2w, da);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          tt[q] = dxv[q] * xh[q];
+          da[q] = av[q] > 0.f ? da[q] : 0.f;
+        }
+        tput(S2, tt);
+        tput(S3, dxv);
+      }
+      // dW2 += da2 f1^T, db2 (f1 = LN1(a1))
+      float a1v[16];
+      ld16(opaque_ptr(hs + L * 1024), a1v);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        xh[q] = (a1v[q] - mu1) * rs1;
+        tt[q] = xh[q] * smb[G::ln1w + kperm(q, h)] + smb[G::ln1b + kperm(q, h)];
+      }
+      tput(S0, da);
+      tput(S1, tt);
+      wave_fence();
+      sl2w += tsum(S2);
+      sl2b += tsum(S3);
+      {
+        float At[16], Bt[16];
+        tget(S0, At);
+        tget(S1, Bt);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          acc_mfma(aW2, At[s], Bt[s]);
+          sb2 += At[s];
+        }
+      }
+      wave_fence();
+      // ---- LN1 backward: dx1 = W2^T da2
+      {
+        f32x16 acc;
+        zero16(acc);
+        mm_cols<G::PW>(smb + G::W2, da, acc);
+        float dxv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dxv[q] = acc[q];
+        ln32_bwd(dxv, xh, rs1, smb + G::ln1w, da);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          tt[q] = dxv[q] * xh[q];
+          da[q] = a1v[q] > 0.f ? da[q] : 0.f;
+        }
+        tput(S2, tt);
+        tput(S3, dxv);
+        tput(S0, da);
+        wave_fence();
+        sl1w += tsum(S2);
+        sl1b += tsum(S3);
+        wave_fence();
+      }
+      // ---- L1 / LN0: dW1 += da1 f0^T, db1, df0 = W1^T da1 -> LN0 parameter gradients
+      {
+        float x[DT][16];
+        load_obs<D, DT>(a.obs + row * D, x);
+        float At[16];
+        tget(S0, At);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) sb1 += At[s];
+#pragma unroll
+        for (int t = 0; t < DT; ++t) {
+          float x0[16], f0[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int f = 32 * t + kperm(q, h);
+            x0[q] = (x[t][q] - mu0) * rs0;
+            f0[q] = x0[q] * smb[G::ln0w + f] + smb[G::ln0b + f];
+          }
+          tput(S1, f0);
+          f32x16 acc;
+          zero16(acc);
+          mm_cols<G::P1>(smb + G::W1 + 32 * t, da, acc);
+          float dfv[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            dfv[q] = acc[q];
+            tt[q] = acc[q] * x0[q];
+          }
+          tput(S2, tt);
+          tput(S3, dfv);
+          wave_fence();
+          float Bt[16];
+          tget(S1, Bt);
+#pragma unroll
+          for (int s = 0; s < 16; ++s) acc_mfma(aW1[t], At[s], Bt[s]);
+          sl0w[t] += tsum(S2);
+          sl0b[t] += tsum(S3);
+          wave_fence();
+        }
+      }
+    }
+  }
+
+  // ---- loss sums (logging only, train_info): one atomic per wave
+  if (a.loss_acc) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lsum0 += __shfl_xor(lsum0, o);
+      lsum1 += __shfl_xor(lsum1, o);
+      lsum2 += __shfl_xor(lsum2, o);
+    }
+    if (lane == 0) {
+      if constexpr (O == A) {
+        atomicAdd(&a.loss_acc[MM_MLOSS_POLICY], lsum0 * inv_m);
+        atomicAdd(&a.loss_acc[MM_MLOSS_ENTROPY], lsum1 * inv_m);
+        atomicAdd(&a.loss_acc[MM_MLOSS_RATIO], lsum2);
+      } else {
+        atomicAdd(&a.loss_acc[MM_MLOSS_VALUE], lsum0 * inv_m);
+      }
+    }
+  }
+
+  // ---- block reduction of the 4 waves (fixed order) into the flat gradient layout, one partial
+  __syncthreads();
+  float* red = sm;
+  for (int e = threadIdx.x; e < F::total; e += blockDim.x) red[e] = 0.f;
+  sbr = xsum(sbr);
+  sbz = xsum(sbz);
+  sbn = xsum(sbn);
+  sbhn = xsum(sbhn);
+  sb2 = xsum(sb2);
+  sb1 = xsum(sb1);
+  sbo = xsum(sbo);
+  slrw = xsum(slrw);
+  slrb = xsum(slrb);
+  sl2w = xsum(sl2w);
+  sl2b = xsum(sl2b);
+  sl1w = xsum(sl1w);
+  sl1b = xsum(sl1b);
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+    sl0w[t] = xsum(sl0w[t]);
+    sl0b[t] = xsum(sl0b[t]);
+  }
+  __syncthreads();
+  for (int ww = 0; ww < NWAVE; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = kperm(q, h);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          red[F::Wih + (32 * g + m) * H + ci] += aWih[g][q];
+          red[F::Whh + (32 * g + m) * H + ci] += aWhh[g][q];
+        }
+        red[F::W2 + m * H + ci] += aW2[q];
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+          if (32 * t + ci < D) red[F::W1 + m * F::Dp + 32 * t + ci] += aW1[t][q];
+        if (m < O) red[F::Wo + m * H + ci] += aWo[q];
+      }
+      if (h == 0) {
+        red[F::bih + ci] += sbr;
+        red[F::bih + 32 + ci] += sbz;
+        red[F::bih + 64 + ci] += sbn;
+        red[F::bhh + ci] += sbr;
+        red[F::bhh + 32 + ci] += sbz;
+        red[F::bhh + 64 + ci] += sbhn;
+        red[F::b2 + ci] += sb2;
+        red[F::b1 + ci] += sb1;
+        red[F::lnr_w + ci] += slrw;
+        red[F::lnr_b + ci] += slrb;
+        red[F::ln2_w + ci] += sl2w;
+        red[F::ln2_b + ci] += sl2b;
+        red[F::ln1_w + ci] += sl1w;
+        red[F::ln1_b + ci] += sl1b;
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+          if (32 * t + ci < D) {
+            red[F::ln0_w + 32 * t + ci] += sl0w[t];
+            red[F::ln0_b + 32 * t + ci] += sl0b[t];
+          }
+        if (ci < O) red[F::bo + ci] += sbo;
+      }
+    }
+    __syncthreads();
+  }
+  float* outp = k.partial + ((int64_t)net * gridDim.x + blockIdx.x) * k.pstride;
+  for (int e = threadIdx.x; e < F::total; e += blockDim.x) outp[e] = red[e];
+}
+
+template <int D, int A>
+__global__ __launch_bounds__(256, 1) void mappo_grad_kernel(GradArgs k) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (blockIdx.y == 0)
+    grad_body<D, A, A>(k, 0, sm);
+  else
+    grad_body<D, A, 1>(k, 1, sm);
+}
+
+// grad[p] = sum over blocks of partial[b][p], fixed order
+__global__ __launch_bounds__(256) void mappo_grad_sum_kernel(const float* __restrict__ partial, int nb,
+                                                             int64_t pstride, int n0, int n1, float* g0, float* g1) {
+  const int net = blockIdx.y;
+  const int n = net == 0 ? n0 : n1;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const float* src = partial + (int64_t)net * nb * pstride + p;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += src[(int64_t)b * pstride];
+  (net == 0 ? g0 : g1)[p] = s;
+}
+
+template <int D, int A>
+struct GradShape {
+  static int64_t pstride() { return ((int64_t)MGeo<D, H, A>::total + 3) & ~3ll; }
+  static int64_t scratch(int L) { return 2ll * NB * NWAVE * (L + 2) * 1024 + 2ll * NB * pstride(); }
+  static int run(const mm_mappo_bwd_args* a, const float* ha, const float* hc, float* ga, float* gc, float* scratch,
+                 hipStream_t s) {
+    static bool attr = false;
+    constexpr size_t lds = (size_t)Geo<D, A>::total * 4;
+    static_assert(Geo<D, A>::total == Geo<D, 1>::total, "actor / critic LDS images differ");
+    if (!attr) {
+      MM_HIP_CHECK(hipFuncSetAttribute((const void*)mappo_grad_kernel<D, A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+      attr = true;
+    }
+    GradArgs k = {};
+    k.a = *a;
+    k.h_in[0] = ha;
+    k.h_in[1] = hc;
+    k.hseq = scratch;
+    k.partial = scratch + 2ll * NB * NWAVE * (a->L + 2) * 1024;
+    k.pstride = pstride();
+    hipLaunchKernelGGL((mappo_grad_kernel<D, A>), dim3(NB, 2), dim3(64 * NWAVE), lds, s, k);
+    MM_HIP_CHECK(hipGetLastError());
+    const int n0 = MGeo<D, H, A>::total, n1 = MGeo<D, H, 1>::total;
+    hipLaunchKernelGGL(mappo_grad_sum_kernel, dim3((n0 + 255) / 256, 2), dim3(256), 0, s, k.partial, NB, k.pstride, n0,
+                       n1, ga, gc);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
+};
+
+}  // namespace mgr
+}  // namespace mm
+
+extern "C" {
+
+int64_t mm_mappo_grad_scratch_count(const mm_mappo_dims* d, int32_t L) {
+  if (!d || L <= 0 || d->hidden != 32 || d->n_actions != 5) return -1;
+  if (d->obs_dim == 47) return mm::mgr::GradShape<47, 5>::scratch(L);
+  if (d->obs_dim == 94) return mm::mgr::GradShape<94, 5>::scratch(L);
+  return -1;
+}
+
+int mm_mappo_grad(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, const float* h_actor, const float* h_critic,
+                  float* grad_actor, float* grad_critic, float* scratch, mm_stream_t s) {
+  MM_REQUIRE(d && a && h_actor && h_critic && grad_actor && grad_critic && scratch, "mappo_grad: null argument");
+  MM_REQUIRE(a->L > 0 && a->T % a->L == 0 && a->en > 0, "mappo_grad: need L | T");
+  MM_REQUIRE(a->P[0] && a->P[1] && a->obs && a->mask && a->active && a->act && a->adv && a->old_logp &&
+                 a->old_value && a->returns && a->stats,
+             "mappo_grad: null pointer");
+  MM_REQUIRE(((uintptr_t)h_actor & 15) == 0 && ((uintptr_t)h_critic & 15) == 0 && ((uintptr_t)scratch & 15) == 0,
+             "mappo_grad: hiddens and scratch must be 16-byte aligned");
+  MM_REQUIRE(d->hidden == 32 && d->n_actions == 5 && (d->obs_dim == 47 || d->obs_dim == 94),
+             "mappo_grad: unsupported dims D=%d H=%d A=%d (supported: D 47|94, H 32, A 5)", d->obs_dim, d->hidden,
+             d->n_actions);
+  if (d->obs_dim == 47)
+    return mm::mgr::GradShape<47, 5>::run(a, h_actor, h_critic, grad_actor, grad_critic, scratch, (hipStream_t)s);
+  return mm::mgr::GradShape<94, 5>::run(a, h_actor, h_critic, grad_actor, grad_critic, scratch, (hipStream_t)s);
+}
+
+}  // extern "C"

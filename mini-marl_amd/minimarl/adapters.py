@@ -313,7 +313,7 @@ class R_MAPPOPolicy:
         key = (L, n)
         if key not in self._eval:
             buf = MappoBuffer(L, n, 1, self.policy.D, self.hidden, self.device)
-            self._eval[key] = (buf, MappoTrainer(self.policy, L, n, L=L, ppo_epoch=1))
+            self._eval[key] = (buf, MappoTrainer(self.policy, L, n, L=L, ppo_epoch=1, fused=False))
         buf, tr = self._eval[key]
         buf.obs[:L].copy_(obs_t.view(L, n, -1))
         buf.masks[:L].copy_(self._t(masks).view(L, n))

@@ -213,8 +213,12 @@ class MappoTrainer:
 
     def __init__(self, policy, T, EN, L=5, ppo_epoch=15, clip_param=0.2, huber_delta=10.0, entropy_coef=0.01,
                  value_loss_coef=0.5, max_grad_norm=0.5, actor_lr=1e-4, critic_lr=1e-4, opti_eps=1e-5,
-                 grad_allreduce=None):
+                 grad_allreduce=None, fused=True):
+        """fused: one mm_mappo_grad pass per epoch (forward recomputed in the backward, weight gradients
+        reduced on MFMA in the same kernel); False: the TRAIN forward with saved activations, the BPTT
+        kernel writing per-row operands and the separate weight-gradient reduction."""
         assert T % L == 0, "episode length must be a multiple of data_chunk_length"
+        self.fused = bool(fused)
         self.p = policy
         self.T, self.EN, self.L, self.epochs = int(T), int(EN), int(L), int(ppo_epoch)
         self.clip, self.huber, self.ent, self.vcoef = clip_param, huber_delta, entropy_coef, value_loss_coef
@@ -225,11 +229,17 @@ class MappoTrainer:
         d = ctypes.byref(policy.dims)
         self.rows = self.T * self.EN
         self.rs = _rs(self.rows)
-        ns = [L_.mm_mappo_save_fields(d, n) for n in (0, 1)]
-        ng = [L_.mm_mappo_grad_fields(d, n) for n in (0, 1)]
-        self.save = [torch.zeros(self.rs * ns[n], device=dev) for n in (0, 1)]
-        self.gsoa = [torch.zeros(self.rs * ng[n], device=dev) for n in (0, 1)]
-        self.partial = torch.zeros(int(L_.mm_mappo_wgrad_partial_count(d, self.rs)), device=dev)
+        if self.fused:
+            n_scr = int(L_.mm_mappo_grad_scratch_count(d, self.L))
+            if n_scr <= 0:
+                raise RuntimeError("mappo_grad: unsupported dims for the fused gradient pass")
+            self.gscr = torch.zeros(n_scr, device=dev)
+        else:
+            ns = [L_.mm_mappo_save_fields(d, n) for n in (0, 1)]
+            ng = [L_.mm_mappo_grad_fields(d, n) for n in (0, 1)]
+            self.save = [torch.zeros(self.rs * ns[n], device=dev) for n in (0, 1)]
+            self.gsoa = [torch.zeros(self.rs * ng[n], device=dev) for n in (0, 1)]
+            self.partial = torch.zeros(int(L_.mm_mappo_wgrad_partial_count(d, self.rs)), device=dev)
         nets = (policy.actor, policy.critic)
         self.grad = [torch.zeros_like(n.flat) for n in nets]
         self.m = [torch.zeros_like(n.flat) for n in nets]
@@ -277,6 +287,8 @@ class MappoTrainer:
 
     # -- one train() ------------------------------------------------------------------------
     def fwd_args(self, buf):
+        if self.fused:
+            return None
         a = MappoFwdArgs()
         a.net[0].P, a.net[0].h_in, a.net[0].save = _ptrs(self.p.actor.flat, buf.rnn_states, self.save[0])
         a.net[1].P, a.net[1].h_in, a.net[1].save = _ptrs(self.p.critic.flat, buf.rnn_states_critic, self.save[1])
@@ -287,8 +299,9 @@ class MappoTrainer:
     def bwd_args(self, buf):
         b = MappoBwdArgs()
         b.P[0], b.P[1] = ptr(self.p.actor.flat), ptr(self.p.critic.flat)
-        b.save[0], b.save[1] = ptr(self.save[0]), ptr(self.save[1])
-        b.gsoa[0], b.gsoa[1] = ptr(self.gsoa[0]), ptr(self.gsoa[1])
+        if not self.fused:
+            b.save[0], b.save[1] = ptr(self.save[0]), ptr(self.save[1])
+            b.gsoa[0], b.gsoa[1] = ptr(self.gsoa[0]), ptr(self.gsoa[1])
         (b.obs, b.mask, b.active, b.act, b.adv, b.old_logp, b.old_value, b.returns, b.stats,
          b.loss_acc) = _ptrs(buf.obs, buf.masks, buf.active_masks, buf.actions, self.adv, buf.action_log_probs,
                              buf.value_preds, buf.returns, self.stats, self.loss_acc)
@@ -311,16 +324,26 @@ class MappoTrainer:
                   "mappo_stats_from_sums")
         self.loss_acc.zero_()
 
-    def epoch(self, buf, ep, fa=None, ba=None):
+    def gradients(self, buf, fa=None, ba=None):
+        """This epoch's unclipped gradients of both nets into self.grad (loss seeds + chunked BPTT +
+        weight-gradient reduction, ramppo_network.py:56-209)."""
         L_, s, d = lib(), stream_handle(self.device), ctypes.byref(self.p.dims)
-        check(L_.mm_mappo_vn_update(ptr(self.vn), ptr(self.stats), 0.99999, s), "mappo_vn_update")
-        fa = fa or self.fwd_args(buf)
         ba = ba or self.bwd_args(buf)
+        if self.fused:
+            check(L_.mm_mappo_grad(d, ctypes.byref(ba), ptr(buf.rnn_states), ptr(buf.rnn_states_critic),
+                                   ptr(self.grad[0]), ptr(self.grad[1]), ptr(self.gscr), s), "mappo_grad")
+            return
+        fa = fa or self.fwd_args(buf)
         check(L_.mm_mappo_fwd(d, ctypes.byref(fa), s), "mappo_fwd(train)")
         check(L_.mm_mappo_bwd(d, ctypes.byref(ba), s), "mappo_bwd")
         for n in (0, 1):
             check(L_.mm_mappo_wgrad(d, n, ptr(self.gsoa[n]), self.rs, ptr(self.grad[n]), ptr(self.partial), s),
                   "mappo_wgrad")
+
+    def epoch(self, buf, ep, fa=None, ba=None):
+        L_, s, d = lib(), stream_handle(self.device), ctypes.byref(self.p.dims)
+        check(L_.mm_mappo_vn_update(ptr(self.vn), ptr(self.stats), 0.99999, s), "mappo_vn_update")
+        self.gradients(buf, fa, ba)
         scale = 1.0
         if self.allreduce is not None:
             for n in (0, 1):

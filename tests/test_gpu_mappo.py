@@ -101,7 +101,7 @@ def test_train_forward_chunks_match_reference(golden):
     buf.masks[:L] = torch.from_numpy(fx["seq_masks"].reshape(L, n)).to(DEV)
     buf.rnn_states[0] = torch.from_numpy(fx["seq_ha"][:, 0]).to(DEV)
     buf.rnn_states_critic[0] = torch.from_numpy(fx["seq_hc"][:, 0]).to(DEV)
-    tr = MappoTrainer(p, L, n, L=L, ppo_epoch=1)
+    tr = MappoTrainer(p, L, n, L=L, ppo_epoch=1, fused=False)
     import ctypes
     fa = tr.fwd_args(buf)
     assert lib().mm_mappo_fwd(ctypes.byref(p.dims), ctypes.byref(fa), None) == 0
@@ -138,33 +138,31 @@ def test_gae_matches_reference(golden):
                                atol=1e-6)
 
 
-def _trainer_from_fixture(fx):
+def _trainer_from_fixture(fx, fused=True):
     from minimarl.mappo import MappoBuffer, MappoTrainer
     p = _policy(fx, "before.")
     E, N, T, L = (int(fx[k]) for k in ("E", "N", "T", "L"))
     buf = MappoBuffer(T, E, N, p.D, 32, DEV)
     buf.load_reference({k[5:]: fx[k] for k in fx if k.startswith("data.")})
-    tr = MappoTrainer(p, T, E * N, L=L, ppo_epoch=int(fx["epochs"]))
+    tr = MappoTrainer(p, T, E * N, L=L, ppo_epoch=int(fx["epochs"]), fused=fused)
     tr.load_value_normalizer(float(fx["vn0.running_mean"][0]), float(fx["vn0.running_mean_sq"][0]),
                              float(fx["vn0.debiasing_term"]))
     return p, buf, tr
 
 
-def test_first_epoch_gradients_match_reference(golden):
-    """Unclipped gradients of PPO epoch 0 vs the reference's (clipped) ones / its clip coefficient."""
-    import ctypes
+@pytest.mark.parametrize("fused", [True, False], ids=["fused_mfma", "saves_wgrad"])
+def test_first_epoch_gradients_match_reference(golden, fused):
+    """Unclipped gradients of PPO epoch 0 vs the reference's (clipped) ones / its clip coefficient:
+    the fused MFMA pass (mm_mappo_grad, a partial tile of chunks) and the saves + wgrad path."""
     from minimarl._lib import lib
     fx = golden("mappo_train")
-    p, buf, tr = _trainer_from_fixture(fx)
+    p, buf, tr = _trainer_from_fixture(fx, fused)
     tr.prepare(buf)
-    L_, d = lib(), ctypes.byref(p.dims)
-    assert L_.mm_mappo_vn_update(tr.vn.data_ptr(), tr.stats.data_ptr(), 0.99999, None) == 0
-    fa, ba = tr.fwd_args(buf), tr.bwd_args(buf)
-    assert L_.mm_mappo_fwd(d, ctypes.byref(fa), None) == 0
-    assert L_.mm_mappo_bwd(d, ctypes.byref(ba), None) == 0
-    for n in (0, 1):
-        assert L_.mm_mappo_wgrad(d, n, tr.gsoa[n].data_ptr(), tr.rs, tr.grad[n].data_ptr(),
-                                 tr.partial.data_ptr(), None) == 0
+    assert lib().mm_mappo_vn_update(tr.vn.data_ptr(), tr.stats.data_ptr(), 0.99999, None) == 0
+    if fused:
+        tr.grad[0].fill_(float("nan"))      # the fused pass writes every entry (pads included)
+        tr.grad[1].fill_(float("nan"))
+    tr.gradients(buf)
     torch.cuda.synchronize()
     for n, (net, tag) in enumerate(((p.actor, "a"), (p.critic, "c"))):
         coef = min(1.0, 0.5 / (float(fx["norms"][n]) + 1e-6))
@@ -180,9 +178,10 @@ def test_first_epoch_gradients_match_reference(golden):
             sum(float(net.view(k, tr.grad[n]).abs().sum()) for k in om.NET_KEYS), rel=1e-6)
 
 
-def test_ppo_train_matches_reference(golden):
+@pytest.mark.parametrize("fused", [True, False], ids=["fused_mfma", "saves_wgrad"])
+def test_ppo_train_matches_reference(golden, fused):
     fx = golden("mappo_train")
-    p, buf, tr = _trainer_from_fixture(fx)
+    p, buf, tr = _trainer_from_fixture(fx, fused)
     info = tr.train(buf)
     torch.cuda.synchronize()
     for n, (net, kind) in enumerate(((p.actor, "actor"), (p.critic, "critic"))):
@@ -307,16 +306,12 @@ def test_cfg3_scale_rollout_and_epoch_gradients_vs_oracle():
     ret_ref, _ = om.compute_returns(data["rewards"], data["value_preds"], data["masks"], data["value_preds"][T],
                                     om.ValueNorm(*vn0), 0.99, 0.95)
     np.testing.assert_allclose(data["returns"][:T], ret_ref[:T], rtol=1e-5, atol=1e-5)
-    # ---- PPO epoch 0 gradients through the tiled SoA forward / backward / wgrad kernels
+    # ---- PPO epoch 0 gradients through the fused MFMA pass (mm_mappo_grad: 819 tiles of 32 chunks
+    # over 1024 waves, per-block partials) -- the trainer bench.py runs
     tr.prepare(b)
-    L_, d = lib(), ctypes.byref(p.dims)
-    assert L_.mm_mappo_vn_update(tr.vn.data_ptr(), tr.stats.data_ptr(), 0.99999, None) == 0
-    fa, ba = tr.fwd_args(b), tr.bwd_args(b)
-    assert L_.mm_mappo_fwd(d, ctypes.byref(fa), None) == 0
-    assert L_.mm_mappo_bwd(d, ctypes.byref(ba), None) == 0
-    for n in (0, 1):
-        assert L_.mm_mappo_wgrad(d, n, tr.gsoa[n].data_ptr(), tr.rs, tr.grad[n].data_ptr(),
-                                 tr.partial.data_ptr(), None) == 0
+    assert tr.fused
+    assert lib().mm_mappo_vn_update(tr.vn.data_ptr(), tr.stats.data_ptr(), 0.99999, None) == 0
+    tr.gradients(b)
     torch.cuda.synchronize()
     rec = []
     om.ppo_train(PA, PC, data, om.ValueNorm(*vn0), 1, L, record=rec)
@@ -328,3 +323,38 @@ def test_cfg3_scale_rollout_and_epoch_gradients_vs_oracle():
             ref = rec[0][tag][k].numpy() / coef
             np.testing.assert_array_less(np.abs(g - ref), 2e-3 * np.abs(ref).max() + 2e-3 * np.abs(ref) + 1e-9,
                                          err_msg=f"net {n} {k}")
+
+
+@pytest.mark.parametrize("L", [5, 10, 1])
+def test_fused_gradients_match_saves_path_and_are_deterministic(L):
+    """mm_mappo_grad (forward recomputed in the backward, MFMA weight gradients) vs the saves + BPTT +
+    wgrad kernels on the same rollout, several chunk lengths (ragged last tile: 330 chunks at L = 10),
+    |g_fused - g_saves| <= 1e-4 max|g| + 1e-4 |g|; two fused runs are bit-identical."""
+    from minimarl._lib import lib
+    from minimarl.env import VecEnv
+    from minimarl.mappo import MappoPolicy, MappoRunner, MappoTrainer
+    E, N, T = 66, 5, 20
+    env = VecEnv(E, N, max_steps=100, device=DEV)
+    p = MappoPolicy(env.obs_dim, 5, 32, DEV, seed=5)
+    r = MappoRunner(env, p, T=T, L=L, ppo_epoch=1, seed=2)
+    r.warmup()
+    r.rollout()
+    r.compute()
+    b = r.buf
+    grads = {}
+    for fused in (True, False, True):
+        tr = MappoTrainer(p, T, E * N, L=L, ppo_epoch=1, fused=fused)
+        tr.vn.copy_(r.trainer.vn)
+        tr.prepare(b)
+        assert lib().mm_mappo_vn_update(tr.vn.data_ptr(), tr.stats.data_ptr(), 0.99999, None) == 0
+        tr.gradients(b)
+        torch.cuda.synchronize()
+        g = [x.cpu().numpy().copy() for x in tr.grad]
+        if fused and fused in grads:
+            for n in (0, 1):
+                np.testing.assert_array_equal(g[n], grads[True][n])
+        grads.setdefault(fused, g)
+    for n in (0, 1):
+        a, ref = grads[True][n], grads[False][n]
+        assert np.isfinite(a).all()
+        np.testing.assert_array_less(np.abs(a - ref), 1e-4 * np.abs(ref).max() + 1e-4 * np.abs(ref) + 1e-9)
