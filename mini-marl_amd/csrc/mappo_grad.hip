@@ -49,12 +49,16 @@ struct Geo {
   static_assert(O <= 8, "head wider than 8 outputs");
 };
 
-__device__ __forceinline__ float xsum(float v) { return v + __shfl_xor(v, 32); }
+// v(lane) + v(lane ^ 32) with one v_permlane32_swap (no LDS round trip of ds_bpermute)
+__device__ __forceinline__ float xsum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 __device__ __forceinline__ void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);   // measured: without it the transposes' LDS traffic interleaves worse
 }
 // a zero the compiler cannot see through: LDS bases offset by it are re-derived per step, so the
 // loop-invariant weight / LayerNorm reads are not hoisted out of the tile loop into hundreds of VGPRs
@@ -63,19 +67,18 @@ __device__ __forceinline__ int opaque0() {
   asm volatile("" : "+s"(z));
   return z;
 }
-// scheduling fence between the phases of a step: one step is a single basic block of ~1000
-// instructions, and without fences the scheduler hoists every LDS / global load of later phases
-// (occupancy 1 looks like 512 free registers to it) and spills
-#define MG_PHASE() __builtin_amdgcn_sched_barrier(0)
 __device__ __forceinline__ int lane_c() { return (int)(threadIdx.x & 31); }
 __device__ __forceinline__ int lane_h() { return (int)((threadIdx.x >> 5) & 1); }
 
 // acc += W[(lane & 31)][kperm(s, h)] * v[s] over s < 16 (row-major LDS W, pitch P): W v in act-frag
+// k-groups of 8 features (4 per lane half) holding any of the first n features of a 32-wide block
+constexpr int kgroups(int n) { return n >= 32 ? 4 : (n + 7) / 8; }
 template <int P>
-__device__ __forceinline__ void mm_rows(const float* W, const float (&v)[16], f32x16& acc) {
+__device__ __forceinline__ void mm_rows(const float* W, const float (&v)[16], f32x16& acc, int ng = 4) {
   const float* wr = W + lane_c() * P + 4 * lane_h();
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
+    if (g >= ng) break;
     const float4 a4 = *reinterpret_cast<const float4*>(wr + 8 * g);
     acc = mfma32(a4.x, v[4 * g], acc);
     acc = mfma32(a4.y, v[4 * g + 1], acc);
@@ -112,17 +115,8 @@ __device__ __forceinline__ float tsum(const float* T) {
   return s;
 }
 
-// weight-gradient accumulation: the accumulators stay in AGPRs for the whole kernel (the compiler
-// otherwise shuttles them between the register files under the pressure of the step's activations)
-__device__ __forceinline__ void acc_mfma(f32x16& acc, float a, float b) {
-#ifdef MG_NO_ACC
-  (void)acc; (void)a; (void)b;
-#elif defined(MG_ASM_ACC)
-  asm("v_mfma_f32_32x32x2_f32 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-#else
-  acc = mfma32(a, b, acc);
-#endif
-}
+// weight-gradient accumulation (chunks on k)
+__device__ __forceinline__ void acc_mfma(f32x16& acc, float a, float b) { acc = mfma32(a, b, acc); }
 
 __device__ __forceinline__ void ld16(const float* p, float (&v)[16]) {
 #pragma unroll
@@ -287,8 +281,7 @@ struct Step {
         const int f = 32 * t + kperm(q, h);
         f0[q] = (x[t][q] - mu0) * rs0 * sm[G::ln0w + f] + sm[G::ln0b + f];
       }
-      mm_rows<G::P1>(sm + G::W1 + 32 * t, f0, acc);
-      MG_PHASE();
+      mm_rows<G::P1>(sm + G::W1 + 32 * t, f0, acc, kgroups(D - 32 * t));
     }
     float f[16];
 #pragma unroll
@@ -298,7 +291,6 @@ struct Step {
     for (int q = 0; q < 16; ++q) f[q] = (a1[q] - mu1) * rs1 * sm[G::ln1w + kperm(q, h)] + sm[G::ln1b + kperm(q, h)];
     zero16(acc);
     mm_rows<G::PW>(sm + G::W2, f, acc);
-    MG_PHASE();
 #pragma unroll
     for (int q = 0; q < 16; ++q) a2[q] = fmaxf(acc[q] + sm[G::b2 + kperm(q, h)], 0.f);
     ln32(a2, mu2, rs2);
@@ -323,7 +315,6 @@ struct Step {
           n[q] = tanhf_(gi + r[q] * gh);
         }
       }
-      MG_PHASE();
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) h2[q] = n[q] + z[q] * (hin[q] - n[q]);
@@ -430,7 +421,6 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
         tput(S0, x2);
         tput(S1, hin);
       }
-      MG_PHASE();
       // head: y = LN_r(h2); out = Wo y + bo
       float mur, rsr, xr[16], y[16];
       ln32(st.h2, mur, rsr);
@@ -506,7 +496,6 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
         dout[0] = a.value_coef * m * inv_m * d;
         if (h == 0 && valid) lsum0 += fmaxf(lo, lc) * m;
       }
-      MG_PHASE();
       // ---- head gradients: dWo = dout y^T, dbo = dout (MFMA with chunks on k); dy = Wo^T dout
       float dy[16];
       {
@@ -561,13 +550,11 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
         dghn[q] = dpn[q] * r;
         dhn[q] = d * z;
       }
-      MG_PHASE();
       f32x16 dx2;
       zero16(dx2);
       mm_rows<G::PT>(smb + G::WihT, dgr, dx2);
       mm_rows<G::PT>(smb + G::WihT + 32, dgz, dx2);
       mm_rows<G::PT>(smb + G::WihT + 64, dpn, dx2);
-      MG_PHASE();
       {
         f32x16 dhh;
         zero16(dhh);
@@ -578,7 +565,6 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) dhn[q] = (dhn[q] + dhh[q]) * mk;
       }
-      MG_PHASE();
       // GRU weight gradients: dW_ih += dg x2^T, dW_hh += dgh hin^T (x2 in S0, hin in S1), biases
       tput(S2, dgr);
       tput(S3, dgz);
