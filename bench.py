@@ -398,11 +398,20 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el_m = float(t.item())
         k = args.mappo_episodes
+        Dm, Hm_ = menv.obs_dim, 32
+        macs = sum(Hm_ * Dm + Hm_ * Hm_ + 6 * Hm_ * Hm_ + o * Hm_ for o in (5, 1))
+        mflop = 6.0 * macs * E * N * 100
         mappo = {"algo": "rmappo shared policy (MLP-LN + GRU-32 actor/critic, ValueNorm, GAE, 15 PPO epochs)",
                  "envs_per_gpu": E, "agents": N, "episode_length": 100, "data_chunk_length": 5, "ppo_epoch": 15,
                  "ms_per_episode": round(el_m / k * 1e3, 3),
                  "agent_env_steps_per_s_incl_train": round(E * N * 100 * world * k / el_m, 1),
                  "rollout_ms_per_step": round(t_ro / k / 100, 4), "train_ms": round(t_tr / k, 3),
+                 "train_ms_per_epoch": round(t_tr / k / 15, 3),
+                 # algorithmic fp32 work of one epoch's gradients (forward + data backward + weight
+                 # gradients = 3 x 2 x MACs per row-step of both nets; the fused pass also recomputes the forward)
+                 "grad_gflop_per_epoch": round(mflop / 1e9, 1),
+                 "grad_tflops_fp32": round(mflop / (t_tr / k / 15 * 1e-3) / 1e12, 2),
+                 "grad_path": "fused mm_mappo_grad (v_mfma_f32_32x32x2_f32, forward recomputed from chunk-start hiddens)",
                  "ppo_updates_per_s": round(15 * k / el_m, 2),
                  "train_info": {kk: round(float(v), 6) for kk, v in info.items()},
                  "grad_allreduce": "rccl" if dist else None}
