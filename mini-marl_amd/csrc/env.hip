@@ -127,9 +127,13 @@ struct TdFuse {
 // env with positions in registers; phase 2 builds the occupancy map, then every (env, agent)
 // lane writes its 47 local features into an LDS tile; phase 3 streams the tile out as 16-byte
 // stores (one contiguous N*D run per env, coalesced across the wave) and writes the state back.
-static constexpr int WT = 64;
+static constexpr int WT = 64;     // lanes of the (env, agent) work: one wave
+#ifndef MM_ENV_TB
+#define MM_ENV_TB 256
+#endif
+static constexpr int TB = MM_ENV_TB;  // threads per block: the extra waves only help stream the obs / state out
 
-__global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32_t* __restrict__ act,
+__global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32_t* __restrict__ act,
                                                            float* __restrict__ next_obs, int64_t next_se,
                                                            const int64_t* __restrict__ next_row,
                                                            float* __restrict__ obs_cur,
@@ -165,7 +169,7 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
   const uint32_t* g32 = reinterpret_cast<const uint32_t*>(d.grid + (int64_t)e0 * RC);
   uint32_t gr[GWR];
 #pragma unroll
-  for (int w = 0; w < GWR; ++w) gr[w] = (lane + w * WT < nw) ? g32[lane + w * WT] : 0u;
+  for (int w = 0; w < GWR; ++w) gr[w] = (lane + w * TB < nw) ? g32[lane + w * TB] : 0u;
   int32_t pos_r = 0, act_r = 0, tact_r = 0;
   float trew = 0.f, tq = 0.f, tm = 0.f;
   int64_t trow = 0;
@@ -190,13 +194,13 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
     steps0 = d.steps[e0 + lane];
     if (tdf.on) tdone = tdf.done[e0 + lane];
   }
-  for (int i = lane; i < ne * RC; i += WT) socc[i] = 0;
+  for (int i = lane; i < ne * RC; i += TB) socc[i] = 0;
 #pragma unroll
   for (int w = 0; w < GWR; ++w)
-    if (lane + w * WT < nw) reinterpret_cast<uint32_t*>(sgrid)[lane + w * WT] = gr[w];
-  for (int i = lane + GWR * WT; i < nw; i += WT) reinterpret_cast<uint32_t*>(sgrid)[i] = g32[i];
+    if (lane + w * TB < nw) reinterpret_cast<uint32_t*>(sgrid)[lane + w * TB] = gr[w];
+  for (int i = lane + GWR * TB; i < nw; i += TB) reinterpret_cast<uint32_t*>(sgrid)[i] = g32[i];
   if (!g32ok)
-    for (int i = lane; i < ne * RC; i += WT) sgrid[i] = d.grid[(int64_t)e0 * RC + i];
+    for (int i = lane; i < ne * RC; i += TB) sgrid[i] = d.grid[(int64_t)e0 * RC + i];
   if (lane < nl) {
     spos[lane] = pos_r;
     sact[lane] = act_r;
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
   const bool vec = (ND & 3) == 0 && (next_se & 3) == 0 && ((uintptr_t)next_obs & 15) == 0 &&
                    ((uintptr_t)obs_cur & 15) == 0;
   if (vec) {
-    // flat float4 index i = lane + WT*it over the block's ne x ND4 outputs, walked with a running
+    // flat float4 index i = lane + TB*it over the block's ne x ND4 outputs, walked with a running
     // (env, offset) pair instead of a division per element
     const int ND4 = ND >> 2;
     int le = 0, r4 = lane;
@@ -347,14 +351,14 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
         if (sdone[le]) v = *reinterpret_cast<const float4*>(robs + r);
         *reinterpret_cast<float4*>(obs_cur + (int64_t)(e0 + le) * ND + r) = v;
       }
-      r4 += WT;
+      r4 += TB;
       while (r4 >= ND4 && le < ne) {
         r4 -= ND4;
         ++le;
       }
     }
   } else {
-    for (int i = lane; i < ne * ND; i += WT) {
+    for (int i = lane; i < ne * ND; i += TB) {
       const int le = i / ND, r = i - le * ND;
       const float v = sloc[le * LD + (full ? r % LD : r)];
       if (next_obs) next_obs[srow[le] * next_se + r] = v;
@@ -366,12 +370,12 @@ __global__ __launch_bounds__(WT) void env_step_wave_kernel(EnvDev d, const int32
     uint32_t* g32 = reinterpret_cast<uint32_t*>(d.grid + (int64_t)e0 * RC);
     const uint32_t* ig32 = reinterpret_cast<const uint32_t*>(d.init_grid);
     const int RC4 = RC >> 2;
-    for (int i = lane; i < ne * RC4; i += WT) {
+    for (int i = lane; i < ne * RC4; i += TB) {
       const int le = i / RC4;
       g32[i] = (autoreset && sdone[le]) ? ig32[i - le * RC4] : reinterpret_cast<const uint32_t*>(sgrid)[i];
     }
   } else {
-    for (int i = lane; i < ne * RC; i += WT) {
+    for (int i = lane; i < ne * RC; i += TB) {
       const int le = i / RC;
       d.grid[(int64_t)e0 * RC + i] = (autoreset && sdone[le]) ? d.init_grid[i % RC] : sgrid[i];
     }
@@ -476,7 +480,7 @@ int env_step(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, 
   const int blocks = (d.E + d.eb - 1) / d.eb;
   TdFuse t{};
   if (tdf) t = *tdf;
-  hipLaunchKernelGGL(env_step_wave_kernel, dim3(blocks), dim3(WT), step_smem(d), s, d, act, next_obs,
+  hipLaunchKernelGGL(env_step_wave_kernel, dim3(blocks), dim3(TB), step_smem(d), s, d, act, next_obs,
                      next_se > 0 ? next_se : (int64_t)d.N * d.D, next_row, obs_cur, cur_row, rew, done, t);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;

@@ -8,9 +8,10 @@ import torch  # noqa: E402
 from minimarl.engine import RolloutEngine  # noqa: E402
 from minimarl.learner import Mixer, QLearner  # noqa: E402
 
-E, N = 512, 8
-eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=10, capacity=4 * E, seed=1, device="cuda")
-for _ in range(4):
+E, N = int(os.environ.get("MB_E", 512)), 8
+CAP = int(os.environ.get("MB_CAP", 4 * E))     # bench: E = 4096, capacity 65536 chunks
+eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=10, capacity=CAP, seed=1, device="cuda")
+for _ in range(max(4, CAP // E + 1)):
     eng.run_graph(0.1)
 mix, tmix = Mixer(N, N * eng.D, 64, 32, "cuda", seed=7), Mixer(N, N * eng.D, 64, 32, "cuda", seed=7)
 L = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda")
