@@ -1524,28 +1524,50 @@ __device__ __forceinline__ void qnet_pack_h3_body(const float* __restrict__ para
 // kernel runs that agent's blocks on the exact-f32 image instead: a per-block branch, no per-value
 // check in the hot path.
 constexpr float kH3ObsBound = 1.0f, kH3Limit = 32768.0f;
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// max_r (|b[r]| + scale * sum_k |W[r][k]|) over rows r of W [rows][cols]: one wave per row, lanes over k
+// (coalesced, every row's loads independent), 4 rows in flight per wave
+__device__ __forceinline__ float row_abs_bound(const float* __restrict__ W, const float* __restrict__ b, int rows,
+                                               int cols, float scale) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float m = 0.f;
+#pragma unroll 4
+  for (int r = w; r < rows; r += nw) {
+    float acc = 0.f;
+    for (int k = lane; k < cols; k += 64) acc += fabsf(W[(int64_t)r * cols + k]);
+    acc = fabsf(b[r]) + wave_sum(acc) * scale;
+    m = fmaxf(m, acc);
+  }
+  return m;
+}
 __device__ void qnet_h3_bound_block(const float* __restrict__ params, int* flags, int agent, int D, int F1, int G,
                                     int H, int A, QnetOffsets o) {
-  __shared__ float red[256];
+  __shared__ float red[1024];
   __shared__ float m1s;
   const int t = threadIdx.x;
-  // largest |weight| of the agent (every weight matrix is split)
+  // largest |weight| of the agent (every weight matrix is split); 4 independent loads per iteration
   float wmax = 0.f;
   auto scan = [&](int64_t off, int64_t n) {
-    for (int64_t i = t; i < n; i += blockDim.x) wmax = fmaxf(wmax, fabsf(params[off + i]));
+    const float* p = params + off;
+    int64_t i = t;
+    for (; i + 3 * (int64_t)blockDim.x < n; i += 4 * (int64_t)blockDim.x) {
+      const float a0 = p[i], a1 = p[i + blockDim.x], a2 = p[i + 2 * blockDim.x], a3 = p[i + 3 * blockDim.x];
+      wmax = fmaxf(wmax, fmaxf(fmaxf(fabsf(a0), fabsf(a1)), fmaxf(fabsf(a2), fabsf(a3))));
+    }
+    for (; i < n; i += blockDim.x) wmax = fmaxf(wmax, fabsf(p[i]));
   };
   scan(o.W1 + (int64_t)agent * F1 * D, (int64_t)F1 * D);
   scan(o.W2 + (int64_t)agent * G * F1, (int64_t)G * F1);
   scan(o.Wih + (int64_t)agent * 3 * H * G, (int64_t)3 * H * G);
   scan(o.Whh + (int64_t)agent * 3 * H * H, (int64_t)3 * H * H);
   scan(o.Wq + (int64_t)agent * A * H, (int64_t)A * H);
-  // layer-1 output bound (one row per thread)
-  float m1 = 0.f;
-  for (int r = t; r < F1; r += blockDim.x) {
-    float acc = fabsf(params[o.b1 + (int64_t)agent * F1 + r]);
-    for (int k = 0; k < D; ++k) acc += fabsf(params[o.W1 + ((int64_t)agent * F1 + r) * D + k]) * kH3ObsBound;
-    m1 = fmaxf(m1, acc);
-  }
+  // layer-1 output bound, then layer 2 scaled by it
+  const float m1 = row_abs_bound(params + o.W1 + (int64_t)agent * F1 * D, params + o.b1 + (int64_t)agent * F1, F1, D,
+                                 kH3ObsBound);
   red[t] = m1;
   __syncthreads();
   if (t == 0) {
@@ -1554,12 +1576,8 @@ __device__ void qnet_h3_bound_block(const float* __restrict__ params, int* flags
     m1s = m;
   }
   __syncthreads();
-  float m2 = 0.f;
-  for (int r = t; r < G; r += blockDim.x) {
-    float acc = fabsf(params[o.b2 + (int64_t)agent * G + r]);
-    for (int k = 0; k < F1; ++k) acc += fabsf(params[o.W2 + ((int64_t)agent * G + r) * F1 + k]) * m1s;
-    m2 = fmaxf(m2, acc);
-  }
+  const float m2 = row_abs_bound(params + o.W2 + (int64_t)agent * G * F1, params + o.b2 + (int64_t)agent * G, G, F1,
+                                 m1s);
   __syncthreads();
   red[t] = fmaxf(fmaxf(m2, wmax), m1s);
   __syncthreads();
