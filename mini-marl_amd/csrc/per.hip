@@ -561,7 +561,39 @@ __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t ca
     if (nd >= cap - 1 && nd < 2 * cap - 1) last[nd - (cap - 1)] = -1;
   }
   __syncthreads();
-  rebuild_tree(tree, cap);
+  if ((cap & (cap - 1)) == 0 && B <= PT) {
+    // power-of-two capacity: every leaf is at depth log2(cap), so only the changed leaves' paths are
+    // recomputed, 4 levels per barrier: each thread re-sums the height-4 subtree above its node from
+    // the (complete) level below, bottom-up (the same pairwise f64 sums as rebuild_tree, so identical
+    // trees; nodes off the changed paths are recomputed from unchanged children, i.e. unchanged)
+    int64_t nd = -1;
+    if ((int)threadIdx.x < B) {
+      nd = nodes[threadIdx.x];
+      if (nd < cap - 1 || nd >= 2 * cap - 1) nd = -1;
+    }
+    int d = 63 - __clzll((unsigned long long)cap);   // depth of the leaves
+    while (d > 0) {
+      const int h = d < 4 ? d : 4, da = d - h;
+      if (nd >= 0) {
+        const int64_t a = ((nd + 1) >> h) - 1;        // ancestor at depth da
+        double v[16];
+        const int64_t base = ((a + 1) << h) - 1;      // first node of a's subtree at depth d
+        for (int i = 0; i < (1 << h); ++i) v[i] = tree[base + i];
+        for (int l = h - 1; l >= 0; --l) {           // depth da + l, 2^l nodes
+          const int64_t lb = ((a + 1) << l) - 1;
+          for (int i = 0; i < (1 << l); ++i) {
+            v[i] = v[2 * i] + v[2 * i + 1];
+            tree[lb + i] = v[i];
+          }
+        }
+        nd = a;
+      }
+      d = da;
+      __syncthreads();
+    }
+  } else {
+    rebuild_tree(tree, cap);
+  }
 }
 
 
