@@ -10,6 +10,7 @@
  *
  * Which reference interface each entry point replaces (reference @ /root/reference):
  *   mm_env_*             gym.make("ma_gym:Checkers-v0") reset/step   vdn/main.py:61-64,83,93,143; qmix/main.py:66-71,189
+ *   mm_switch_*          gym.make("ma_gym:Switch2-v0") reset/step    qmix/_config.py:14-19; qmix/main.py:66-71,103-115
  *   mm_agent_q_fwd       Q_Net.forward / sample_action               qmix/_network.py:44-74; vdn/_network.py:52-58,71-88
  *   mm_qnet_*            Q_Net parameters (per-agent Linear/GRUCell)  qmix/_network.py:15-42; vdn/_network.py:32-42,61-69
  *   mm_td_chunk_step     cal_td_error + chunk assembly               vdn/_utils.py:44-52; vdn/main.py:140-167
@@ -21,6 +22,7 @@
  *   mm_mappo_grad        (fused: forward recompute + BPTT + weight grads of one epoch, same lines)
  *   mm_mappo_gae, insert SharedReplayBuffer.compute_returns/insert   mappo/runner/shared/shared_buffer.py:82-157
  *   mm_offq_*            offpolicy QMix.train_policy_on_batch etc.   offpolicy/algorithms/qmix/qmix.py:80-226
+ *   mm_erb_*             PrioritizedRecReplayBuffer / RecReplayBuffer offpolicy/utils/rec_buffer.py:10-324; segment_tree.py:18-165
  *   mm_eval_accum        greedy test loops                           vdn/_test.py:22-50; magym_runner.py:198-241
  */
 #ifndef MINIMARL_H
@@ -493,6 +495,84 @@ int mm_offq_q_values(const mm_offq_dims* d, const float* P, const float* obs, co
                      int32_t L, int64_t R, void* ws, int64_t ws_bytes, mm_stream_t s);
 /* soft_update: target <- target * (1 - tau) + source * tau over n floats (tau = 1: hard update). */
 int mm_offq_soft_update(float* target, const float* source, int64_t n, double tau, mm_stream_t s);
+
+/* ------------------------------------------------------- ma_gym Switch corridor env (mm_switch_*) */
+/* gym.make("ma_gym:Switch2-v0", max_steps, step_cost) (qmix/_config.py:14-19, qmix/main.py:66-71,
+ * 103-115): E envs in lockstep, n_agents 2..4 on the 3 x 7 two-room grid. Dynamics spec (ma-gym is
+ * absent: parity unpinned): oracle/switch.py. Obs per agent [row/2, round(col/6, 2)(, step/max_steps)],
+ * D = 2 + clock, or N x that when full_observable; actions 0 down 1 left 2 up 3 right 4 noop. */
+typedef struct mm_switch_cfg {
+  int32_t n_agents, max_steps, full_observable, clock;
+  float step_cost;
+} mm_switch_cfg;
+typedef struct mm_switch mm_switch;
+int mm_switch_create(const mm_switch_cfg* cfg, int64_t n_envs, mm_switch** out);
+void mm_switch_destroy(mm_switch* w);
+int mm_switch_obs_dim(const mm_switch* w);
+/* reset every env; obs [E, N, D] (may be NULL) */
+int mm_switch_reset(mm_switch* w, float* obs, mm_stream_t s);
+/* step with act [E, N] int32: next_obs [E, N, D] (terminal), rew [E, N], agent_done [E, N] u8 (may be
+ * NULL; the env's per-agent done list), done [E] u8 (all agents done). obs_cur != NULL: done envs
+ * auto-reset and obs_cur gets the next current obs. */
+int mm_switch_step(mm_switch* w, const int32_t* act, float* next_obs, float* obs_cur, float* rew,
+                   uint8_t* agent_done, uint8_t* done, mm_stream_t s);
+/* host copies of the state (synchronous): pos [E, N, 2], agent_done [E, N], steps [E] */
+int mm_switch_get_state(mm_switch* w, int32_t* pos, uint8_t* agent_done, int32_t* steps);
+
+/* ------------------------------------------------------- offpolicy episode replay (mm_erb_*) */
+/* RecReplayBuffer / PrioritizedRecReplayBuffer of one policy (offpolicy/utils/rec_buffer.py:10-324)
+ * with its SumSegmentTree / MinSegmentTree (offpolicy/utils/segment_tree.py:18-165), resident in HBM.
+ * Episode store: one ring of buffer_size episodes, each field [slot][L][row] (L = T + 1 for obs /
+ * share_obs, T for the rest). Trees: f64 heaps [2 * itcap], root 1, leaves at itcap + i (itcap = the
+ * next power of two >= buffer_size). The ring cursor (current_i / filled_i) is host state; the trees
+ * and max_priority live on the device, so insert -> sample -> train -> update_priorities never syncs.
+ * leaf_mode 0 = the reference's insert, which writes max_priority ** alpha into leaves 0..n-1
+ * (rec_buffer.py:265-268); 1 = write the inserted slots' leaves instead. */
+typedef struct mm_erb mm_erb;
+typedef struct mm_erb_dims {
+  int32_t T, N, D, S, A;     /* episode_length, agents, obs dim, share_obs dim, act dim (one-hot width) */
+  int32_t same_share;        /* use_same_share_obs: share_obs stored once per step ([L, B, S] samples) */
+  int32_t prioritized;       /* PrioritizedRecReplayBuffer (trees + max_priority) */
+  int32_t leaf_mode;         /* 0 reference (leaves 0..n-1), 1 slots */
+} mm_erb_dims;
+/* Episode fields, device pointers. insert: the reference's insert layout obs [T+1, n, N, D],
+ * share_obs [T+1, n, N, S] (agent 0 is kept when same_share), acts [T, n, N, A], rewards / dones
+ * [T, n, N, 1], dones_env [T, n, 1]. gather (sample_inds, rec_buffer.py:192-240): obs [N, T+1, B, D],
+ * share_obs [T+1, B, S] (same_share) or [N, T+1, B, S], acts [N, T, B, A], rewards / dones
+ * [N, T, B, 1], dones_env [T, B, 1]. Any field may be NULL in a gather (not written). */
+typedef struct mm_erb_fields {
+  float* obs; float* share_obs; float* acts; float* rewards; float* dones; float* dones_env;
+} mm_erb_fields;
+int mm_erb_create(const mm_erb_dims* d, int64_t buffer_size, double alpha, mm_erb** out);
+void mm_erb_destroy(mm_erb* b);
+/* RecPolicyBuffer.insert + the prioritized leaf writes (rec_buffer.py:146-190, 262-270); n <= size.
+ * idx_range_host (may be NULL): int64 [n], the ring slots written (host memory, filled at once). */
+int mm_erb_insert(mm_erb* b, int32_t n, const mm_erb_fields* src, int64_t* idx_range_host, mm_stream_t s);
+int64_t mm_erb_len(const mm_erb* b);          /* filled_i */
+int64_t mm_erb_current(const mm_erb* b);      /* current_i */
+int64_t mm_erb_it_capacity(const mm_erb* b);
+/* Prioritized sample indices + IS weights (rec_buffer.py:272-296): mass_b = u_b * sum(0, len-1),
+ * prefix-sum descent, w_b = (p_b len)^-beta / (p_min len)^-beta. u_b = fracs[b] (device f64 [B],
+ * the injected np.random.random draws) or, when fracs is NULL, the device counter RNG (seed,
+ * counter). idx_out: device int64 [B]; w_out: device f64 [B] (may be NULL); w32_out: device f32 [B]
+ * (may be NULL; the trainer's importance_weights). Requires len > B, beta > 0 (reference asserts). */
+int mm_erb_sample_prioritized(mm_erb* b, int32_t B, double beta, const double* fracs, uint64_t seed,
+                              uint64_t counter, int64_t* idx_out, double* w_out, float* w32_out, mm_stream_t s);
+/* Uniform indices (RecReplayBuffer.sample, rec_buffer.py:76): idx_b = floor(u_b len), device RNG. */
+int mm_erb_sample_uniform(mm_erb* b, int32_t B, uint64_t seed, uint64_t counter, int64_t* idx_out, mm_stream_t s);
+/* sample_inds: gather the B episodes idx [B] (device int64) into the sample layout above. */
+int mm_erb_gather(mm_erb* b, int32_t B, const int64_t* idx, const mm_erb_fields* dst, mm_stream_t s);
+/* update_priorities (rec_buffer.py:306-324): leaves[idx] = prio ** alpha (f32 pow, last duplicate
+ * wins), ancestors re-derived, max_priority = max(max_priority, max prio). idx, prio: device [B]. An
+ * index outside [0, len) or a priority <= 0 (the reference's asserts) skips that entry and sets the
+ * error word (mm_erb_error_word). */
+int mm_erb_update_priorities(mm_erb* b, const int64_t* idx, const float* prio, int32_t B, mm_stream_t s);
+double* mm_erb_sum_tree(mm_erb* b);           /* device f64 [2 * itcap] */
+double* mm_erb_min_tree(mm_erb* b);           /* device f64 [2 * itcap] */
+float* mm_erb_max_priority(mm_erb* b);        /* device f32 [1] */
+int32_t* mm_erb_error_word(mm_erb* b);        /* device i32 [1]: bit 0 bad index, bit 1 priority <= 0 */
+/* Stream-ordered device copies of the trees, max_priority and the error word (any may be NULL). */
+int mm_erb_copy_state(mm_erb* b, double* sum_dst, double* min_dst, float* maxp_dst, int32_t* err_dst, mm_stream_t s);
 
 /* Debug: copy the first n (<= 4096) u64 slots of the timing trace buffer that kernels fill when
  * MM_REC_TRACE=1 is set in the environment (clock64 stamps per phase; tools/trace_rec.py). mm_debug_trace(NULL, 0) allocates the buffer

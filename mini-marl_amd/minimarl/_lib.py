@@ -296,3 +296,50 @@ _SIGS += [
     ("mm_offq_q_values", c_i32, [_OD, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_vp, c_i64, c_vp]),
     ("mm_offq_soft_update", c_i32, [c_vp, c_vp, c_i64, c_f64, c_vp]),
 ]
+
+
+# ------------------------------------------------------------------ offpolicy episode replay (mm_erb_*)
+class ErbDims(ctypes.Structure):
+    _fields_ = [("T", c_i32), ("N", c_i32), ("D", c_i32), ("S", c_i32), ("A", c_i32), ("same_share", c_i32),
+                ("prioritized", c_i32), ("leaf_mode", c_i32)]
+
+
+class ErbFields(ctypes.Structure):
+    _fields_ = [("obs", c_vp), ("share_obs", c_vp), ("acts", c_vp), ("rewards", c_vp), ("dones", c_vp),
+                ("dones_env", c_vp)]
+
+
+_ED = ctypes.POINTER(ErbDims)
+_SIGS += [
+    ("mm_erb_create", c_i32, [_ED, c_i64, c_f64, ctypes.POINTER(c_vp)]),
+    ("mm_erb_destroy", None, [c_vp]),
+    ("mm_erb_insert", c_i32, [c_vp, c_i32, ctypes.POINTER(ErbFields), c_vp, c_vp]),
+    ("mm_erb_len", c_i64, [c_vp]),
+    ("mm_erb_current", c_i64, [c_vp]),
+    ("mm_erb_it_capacity", c_i64, [c_vp]),
+    ("mm_erb_sample_prioritized", c_i32, [c_vp, c_i32, c_f64, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_erb_sample_uniform", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp]),
+    ("mm_erb_gather", c_i32, [c_vp, c_i32, c_vp, ctypes.POINTER(ErbFields), c_vp]),
+    ("mm_erb_update_priorities", c_i32, [c_vp, c_vp, c_vp, c_i32, c_vp]),
+    ("mm_erb_sum_tree", c_vp, [c_vp]),
+    ("mm_erb_min_tree", c_vp, [c_vp]),
+    ("mm_erb_max_priority", c_vp, [c_vp]),
+    ("mm_erb_error_word", c_vp, [c_vp]),
+    ("mm_erb_copy_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+]
+
+
+# ------------------------------------------------------------------ ma_gym Switch env (mm_switch_*)
+class SwitchCfg(ctypes.Structure):
+    _fields_ = [("n_agents", c_i32), ("max_steps", c_i32), ("full_observable", c_i32), ("clock", c_i32),
+                ("step_cost", c_f32)]
+
+
+_SIGS += [
+    ("mm_switch_create", c_i32, [ctypes.POINTER(SwitchCfg), c_i64, ctypes.POINTER(c_vp)]),
+    ("mm_switch_destroy", None, [c_vp]),
+    ("mm_switch_obs_dim", c_i32, [c_vp]),
+    ("mm_switch_reset", c_i32, [c_vp, c_vp, c_vp]),
+    ("mm_switch_step", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_switch_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp]),
+]

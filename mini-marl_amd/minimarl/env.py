@@ -90,3 +90,61 @@ class VecEnv:
 
     def restore_tensors(self, ts, scalars=None):
         self.set_state(ts["pos"].numpy(), ts["grid"].numpy(), ts["steps"].numpy(), ts["apples"].numpy())
+
+
+class SwitchVecEnv:
+    """``gym.make("ma_gym:Switch2-v0", max_steps, step_cost)`` (qmix/_config.py:14-19, qmix/main.py:66-71)
+    for E envs in lockstep on the GPU (csrc/switch.hip; dynamics spec oracle/switch.py, parity with the
+    absent ma-gym unpinned). ``step`` returns the env's per-agent done list as ``agent_done`` [E, N]
+    and ``all(done)`` (what the reference's loops test) as ``done`` [E]."""
+
+    def __init__(self, n_envs, n_agents=2, max_steps=100, step_cost=-0.01, full_observable=False, clock=True,
+                 device="cuda"):
+        from ._lib import SwitchCfg
+        self.E, self.N = int(n_envs), int(n_agents)
+        self.device = torch.device(device)
+        self.cfg = SwitchCfg(self.N, int(max_steps), int(bool(full_observable)), int(bool(clock)), float(step_cost))
+        h = c_vp()
+        with torch.cuda.device(self.device):
+            check(lib().mm_switch_create(ctypes.byref(self.cfg), self.E, ctypes.byref(h)), "switch_create")
+        self._h = h
+        self.obs_dim = lib().mm_switch_obs_dim(h)
+        self.n_actions = 5
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._h = None
+            try:
+                release("mm_switch_destroy", h)
+            except Exception:
+                pass
+
+    def reset(self, out=None):
+        out = out if out is not None else torch.empty(self.E, self.N, self.obs_dim, device=self.device)
+        check(lib().mm_switch_reset(self._h, ptr(out), stream_handle(self.device)), "switch_reset")
+        return out
+
+    def step(self, actions, autoreset=False):
+        """actions [E, N] -> (next_obs [E, N, D], reward [E, N], agent_done [E, N] u8, done [E] u8[, obs_cur])."""
+        actions = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
+        assert actions.shape == (self.E, self.N)
+        nxt = torch.empty(self.E, self.N, self.obs_dim, device=self.device)
+        rew = torch.empty(self.E, self.N, device=self.device)
+        adone = torch.empty(self.E, self.N, dtype=torch.uint8, device=self.device)
+        done = torch.empty(self.E, dtype=torch.uint8, device=self.device)
+        cur = torch.empty_like(nxt) if autoreset else None
+        check(lib().mm_switch_step(self._h, ptr(actions), ptr(nxt), ptr(cur), ptr(rew), ptr(adone), ptr(done),
+                                   stream_handle(self.device)), "switch_step")
+        self._keep = actions
+        if autoreset:
+            return nxt, rew, adone, done, cur
+        return nxt, rew, adone, done
+
+    def get_state(self):
+        pos = np.empty((self.E, self.N, 2), np.int32)
+        adone = np.empty((self.E, self.N), np.uint8)
+        steps = np.empty(self.E, np.int32)
+        check(lib().mm_switch_get_state(self._h, pos.ctypes.data, adone.ctypes.data, steps.ctypes.data),
+              "switch_get_state")
+        return pos, adone, steps
