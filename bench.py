@@ -137,6 +137,29 @@ def cpu_learner_baseline(N, D, B=32, C=10, H=64, Hm=64, budget_s=6.0):
                       f"{n} updates in {dt:.1f} s"}
 
 
+def cpu_offq_baseline(otr, batch_np, budget_s=6.0):
+    """The oracle's offpolicy QMix.train_policy_on_batch (qmix.py:80-210 restated in oracle/offq.py) at
+    the bench's shapes, on the host cores, from the GPU trainer's initial parameters."""
+    from oracle import offq as ref
+    q, m = otr.state_dict()
+    qt, mt = otr.state_dict(target=True)
+    P = ref.agent_from_state({"q." + k: v.numpy() for k, v in q.items()})
+    M = ref.mixer_from_state({"m." + k: v.numpy() for k, v in m.items()})
+    PT = ref.agent_from_state({"q." + k: v.numpy() for k, v in qt.items()})
+    MT = ref.mixer_from_state({"m." + k: v.numpy() for k, v in mt.items()})
+    n, st = 0, {}
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        P, M, _ = ref.train_batch(P, M, PT, MT, batch_np, mixer="qmix", double_q=True, use_per=True,
+                                  adam_state=st)
+        PT, MT = ref.soft_update(PT, P, 0.005), ref.soft_update(MT, M, 0.005)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(dt / n * 1e3, 2), "unit": "ms/update", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle train_policy_on_batch + soft update (torch-CPU autograd), same shapes: {n} updates "
+                      f"in {dt:.1f} s"}
+
+
 def time_kernel(fn, iters=50):
     """Average device time of fn() via events on torch's current stream (our launch stream)."""
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -450,6 +473,10 @@ def main():
                 "reference_cpu_ms_per_update": 115.8,
                 "reference_cpu_note": "reference train_policy_on_batch, same shapes, 8 threads of the build "
                                       "container (tools/ref_time_offq.py)"}
+        if not args.no_cpu_baseline:
+            bnp = {"obs": obs, "share_obs": share, "acts": acts, "rewards": rew, "dones_env": dn,
+                   "is_weight": (0.5 + np.random.default_rng(1).random(oB)).astype(np.float32)}
+            offq["cpu_baseline"] = cpu_offq_baseline(otr, bnp)
         del otr
         torch.cuda.empty_cache()
 

@@ -1544,53 +1544,56 @@ __device__ __forceinline__ float row_abs_bound(const float* __restrict__ W, cons
   }
   return m;
 }
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+// block max (any blockDim <= 1024): wave maxima through LDS, then one wave reduces them
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float m = lane < nw ? red[lane] : 0.f;
+  return wave_max(m);
+}
+// max |p[i]| over i < n with 8 independent loads per thread in flight (addresses clamped, so every
+// load is unconditional and the compiler issues them back to back: the scan costs ~n / (8 blockDim)
+// memory round trips instead of n / (4 blockDim))
+__device__ __forceinline__ float abs_max_scan(const float* __restrict__ p, int64_t n, float m) {
+  const int64_t bd = blockDim.x;
+  for (int64_t i = threadIdx.x; i < n; i += 8 * bd) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[min(i + j * bd, n - 1)];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+  }
+  return m;
+}
 __device__ void qnet_h3_bound_block(const float* __restrict__ params, int* flags, int agent, int D, int F1, int G,
                                     int H, int A, QnetOffsets o) {
-  __shared__ float red[1024];
-  __shared__ float m1s;
-  const int t = threadIdx.x;
-  // largest |weight| of the agent (every weight matrix is split); 4 independent loads per iteration
+  __shared__ float red[16];
+  // largest |weight| of the agent (every weight matrix is split)
   float wmax = 0.f;
-  auto scan = [&](int64_t off, int64_t n) {
-    const float* p = params + off;
-    int64_t i = t;
-    for (; i + 3 * (int64_t)blockDim.x < n; i += 4 * (int64_t)blockDim.x) {
-      const float a0 = p[i], a1 = p[i + blockDim.x], a2 = p[i + 2 * blockDim.x], a3 = p[i + 3 * blockDim.x];
-      wmax = fmaxf(wmax, fmaxf(fmaxf(fabsf(a0), fabsf(a1)), fmaxf(fabsf(a2), fabsf(a3))));
-    }
-    for (; i < n; i += blockDim.x) wmax = fmaxf(wmax, fabsf(p[i]));
-  };
-  scan(o.W1 + (int64_t)agent * F1 * D, (int64_t)F1 * D);
-  scan(o.W2 + (int64_t)agent * G * F1, (int64_t)G * F1);
-  scan(o.Wih + (int64_t)agent * 3 * H * G, (int64_t)3 * H * G);
-  scan(o.Whh + (int64_t)agent * 3 * H * H, (int64_t)3 * H * H);
-  scan(o.Wq + (int64_t)agent * A * H, (int64_t)A * H);
+  wmax = abs_max_scan(params + o.W1 + (int64_t)agent * F1 * D, (int64_t)F1 * D, wmax);
+  wmax = abs_max_scan(params + o.W2 + (int64_t)agent * G * F1, (int64_t)G * F1, wmax);
+  wmax = abs_max_scan(params + o.Wih + (int64_t)agent * 3 * H * G, (int64_t)3 * H * G, wmax);
+  wmax = abs_max_scan(params + o.Whh + (int64_t)agent * 3 * H * H, (int64_t)3 * H * H, wmax);
+  wmax = abs_max_scan(params + o.Wq + (int64_t)agent * A * H, (int64_t)A * H, wmax);
   // layer-1 output bound, then layer 2 scaled by it
-  const float m1 = row_abs_bound(params + o.W1 + (int64_t)agent * F1 * D, params + o.b1 + (int64_t)agent * F1, F1, D,
-                                 kH3ObsBound);
-  red[t] = m1;
-  __syncthreads();
-  if (t == 0) {
-    float m = 0.f;
-    for (int i = 0; i < (int)blockDim.x; ++i) m = fmaxf(m, red[i]);
-    m1s = m;
-  }
-  __syncthreads();
-  const float m2 = row_abs_bound(params + o.W2 + (int64_t)agent * G * F1, params + o.b2 + (int64_t)agent * G, G, F1,
-                                 m1s);
-  __syncthreads();
-  red[t] = fmaxf(fmaxf(m2, wmax), m1s);
-  __syncthreads();
-  if (t == 0) {
-    float m = 0.f;
-    for (int i = 0; i < (int)blockDim.x; ++i) m = fmaxf(m, red[i]);
-    flags[agent] = !(m < kH3Limit);   // NaN weights: unsafe as well
-  }
+  const float m1 = block_max(row_abs_bound(params + o.W1 + (int64_t)agent * F1 * D, params + o.b1 + (int64_t)agent * F1,
+                                           F1, D, kH3ObsBound), red);
+  const float m2 = row_abs_bound(params + o.W2 + (int64_t)agent * G * F1, params + o.b2 + (int64_t)agent * G, G, F1, m1);
+  const float m = block_max(fmaxf(fmaxf(m2, wmax), m1), red);
+  if (threadIdx.x == 0) flags[agent] = !(m < kH3Limit);   // NaN weights: unsafe as well
 }
 
 // both images (f32 fragments, fp16x3 split) from the canonical parameters in ONE launch; the last N
 // blocks compute the per-agent fp16x3 safety flags
-__global__ void qnet_pack_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
+__global__ __launch_bounds__(1024) void qnet_pack_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
                                  int D, int F1, int G, int H, int A, QnetOffsets o) {
   const int nb = (int)gridDim.x - N;
   if ((int)blockIdx.x >= nb) {
@@ -1608,8 +1611,9 @@ int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStre
   int rc = qnet_geometry(d, &g, &o);
   if (rc) return rc;
   const int64_t total = g.agent_stride * d->n_agents;
-  const int threads = 256;
-  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 4096) + d->n_agents;
+  // 1024-thread blocks: the N flag blocks' scans and row bounds are latency chains, 16 waves each
+  const int threads = 1024;
+  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 1024) + d->n_agents;
   hipLaunchKernelGGL(qnet_pack_kernel, dim3(blocks), dim3(threads), 0, s, params, packed, g, d->n_agents,
                      d->obs_dim, d->f1, d->g, d->h, d->n_actions, o);
   MM_HIP_CHECK(hipGetLastError());

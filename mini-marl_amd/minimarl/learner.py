@@ -632,8 +632,19 @@ class QLearner:
                 self.apply_grads(self._graph_scale)
             else:
                 self.apply_and_reprioritize(per, self._graph_scale)
+        # single-replica updates replay ONE graph holding both parts (one graph launch per update
+        # instead of two: the B = 32 update is launch-latency bound)
+        g12 = torch.cuda.CUDAGraph()
+        with graph_capture(g12):
+            if per is None:
+                self.compute_grads(self._obs_ptr, self._reset_obs)
+                self.apply_grads(self._graph_scale)
+            else:
+                self.sample_and_grads(per, store, reset_obs_ptr, seed=seed)
+                self.apply_and_reprioritize(per, self._graph_scale)
         self.updates = n0
         self.graphs = (g1, g2)
+        self.graph_fused = g12
         return self.graphs
 
     _graph_scale = 1.0
@@ -643,10 +654,13 @@ class QLearner:
         self.tgt.pack()                 # target synced since capture: repack eagerly (no-op otherwise)
         self.beh.pack()
         self._push_double_eps()
-        g1.replay()
-        if allreduce is not None:
-            allreduce(self.Gr)          # the 1/world scale was baked at capture (set _graph_scale first)
-        g2.replay()
+        if allreduce is None and getattr(self, "graph_fused", None) is not None:
+            self.graph_fused.replay()
+        else:
+            g1.replay()
+            if allreduce is not None:
+                allreduce(self.Gr)      # the 1/world scale was baked at capture (set _graph_scale first)
+            g2.replay()
         self.updates += 1
 
     # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)

@@ -16,6 +16,8 @@ for _ in range(max(4, CAP // E + 1)):
 mix, tmix = Mixer(N, N * eng.D, 64, 32, "cuda", seed=7), Mixer(N, N * eng.D, 64, 32, "cuda", seed=7)
 L = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda")
 L.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=3)
+if os.environ.get("MB_FUSED", "1") == "0":     # A/B: the two-graph replay path
+    L.graph_fused = None
 for _ in range(5):
     L.replay_update()
 torch.cuda.synchronize()
@@ -25,4 +27,5 @@ for _ in range(50):
     L.replay_update()
 b.record()
 torch.cuda.synchronize()
-print(json.dumps({"dbg": os.environ.get("MM_MIX_DBG", "0"), "ms_per_update": a.elapsed_time(b) / 50}))
+print(json.dumps({"dbg": os.environ.get("MM_MIX_DBG", "0"), "fused": L.graph_fused is not None,
+                  "ms_per_update": a.elapsed_time(b) / 50}))
