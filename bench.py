@@ -240,12 +240,21 @@ def main():
     if args.probe_ranks:
         probe_ranks(world, rank)
         return
+    # MM_BENCH_SHARED_GPU=1 (rehearsal of the N > 1 path on a one-GPU box): every rank on cuda:0 and the
+    # collectives over gloo instead of RCCL (RCCL refuses two ranks on one device); numbers then are not
+    # a scaling measurement
+    shared = os.environ.get("MM_BENCH_SHARED_GPU", "0") == "1"
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from minimarl.engine import RolloutEngine
     E, N, Hh = args.envs, args.agents, args.hidden

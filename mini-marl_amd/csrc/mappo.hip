@@ -788,7 +788,7 @@ int mm_mappo_adv_stats(const float* returns, const float* value_preds, const flo
                      partial + 5 * nb);
   MM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(mm::mappo_stats_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, partial, partial + 5 * nb, nb, rows,
-                     stats, partial + 6 * nb);
+                     stats, partial + 7 * nb);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

@@ -358,3 +358,35 @@ def test_fused_gradients_match_saves_path_and_are_deterministic(L):
         a, ref = grads[True][n], grads[False][n]
         assert np.isfinite(a).all()
         np.testing.assert_array_less(np.abs(a - ref), 1e-4 * np.abs(ref).max() + 1e-4 * np.abs(ref) + 1e-9)
+
+
+def test_data_parallel_hooks_match_single_replica():
+    """The data-parallel train() (raw advantage / return sums all-reduced, stats from the global sums,
+    per-epoch gradient all-reduce averaged in clip/Adam) with a stand-in all-reduce for TWO identical
+    replicas (x2, world 2) equals the single-replica train(): same global statistics and mean gradients.
+    Tolerance rtol 1e-4: the replicated path's advantage std is the one-pass form over f64 sums, the
+    single-GPU path's the two-pass form."""
+    from minimarl.env import VecEnv
+    from minimarl.mappo import MappoPolicy, MappoRunner
+
+    def run(allreduce):
+        E, N, T = 64, 8, 20
+        env = VecEnv(E, N, max_steps=12, device=DEV)
+        p = MappoPolicy(env.obs_dim, 5, 32, DEV, seed=0)
+        r = MappoRunner(env, p, T=T, L=5, ppo_epoch=3, seed=1, grad_allreduce=allreduce)
+        r.warmup()
+        r.rollout()
+        r.compute()
+        info = r.train()
+        torch.cuda.synchronize()
+        return p, info
+
+    def twice(g):
+        g.mul_(2.0)
+        return 2
+
+    p1, i1 = run(None)
+    p2, i2 = run(twice)
+    assert all(np.isfinite(v) for v in i2.values()), i2
+    np.testing.assert_allclose(p2.actor.flat.cpu().numpy(), p1.actor.flat.cpu().numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(p2.critic.flat.cpu().numpy(), p1.critic.flat.cpu().numpy(), rtol=1e-4, atol=1e-6)
