@@ -344,11 +344,13 @@ class MappoTrainer:
         L_, s, d = lib(), stream_handle(self.device), ctypes.byref(self.p.dims)
         check(L_.mm_mappo_vn_update(ptr(self.vn), ptr(self.stats), 0.99999, s), "mappo_vn_update")
         self.gradients(buf, fa, ba)
+        # data parallel: the loss seeds already divide by the GLOBAL active count (stats from the
+        # all-reduced sums in prepare()), so the SUM over replicas is the global-batch gradient: no
+        # further 1/world
         scale = 1.0
         if self.allreduce is not None:
             for n in (0, 1):
-                world = self.allreduce(self.grad[n])
-            scale = 1.0 / world
+                self.allreduce(self.grad[n])
         nets = (self.p.actor, self.p.critic)
         for n in (0, 1):
             check(L_.mm_clip_adam(ptr(nets[n].flat), ptr(self.grad[n]), ptr(self.m[n]), ptr(self.v[n]),
