@@ -386,7 +386,7 @@ def main():
                    "ms_per_episode": round(el_t / k * 1e3, 3),
                    "agent_env_steps_per_s_incl_learning": round(E * N * tcfg.max_step * world * k / el_t, 1),
                    "learner_updates_per_s": round(tcfg.update_iter * k / el_t, 1),
-                   "train_score": tr.train_score(), "grad_allreduce": "rccl" if dist else None}
+                   "train_score": tr.train_score(), "grad_allreduce": (("gloo" if shared else "rccl") if dist else None)}
         del tr
         torch.cuda.empty_cache()
 
@@ -446,7 +446,7 @@ def main():
                  "grad_path": "fused mm_mappo_grad (v_mfma_f32_32x32x2_f32, forward recomputed from chunk-start hiddens)",
                  "ppo_updates_per_s": round(15 * k / el_m, 2),
                  "train_info": {kk: round(float(v), 6) for kk, v in info.items()},
-                 "grad_allreduce": "rccl" if dist else None}
+                 "grad_allreduce": (("gloo" if shared else "rccl") if dist else None)}
         del mr, menv, mpol
         torch.cuda.empty_cache()
 
@@ -601,7 +601,7 @@ def main():
             "learner_updates_per_s": round(upd_per_s, 1),
             "learner": {"algo": "QMIX Train_dqn update", "batch_chunks": args.batch, "chunk": 10,
                         "mixer_hidden": 64, "ms_per_update": round(el_l / args.learner_steps * 1e3, 4),
-                        "updates": args.learner_steps, "grad_allreduce": "rccl" if dist else None,
+                        "updates": args.learner_steps, "grad_allreduce": (("gloo" if shared else "rccl") if dist else None),
                         "reference_cpu_updates_per_s": 12.0,
                         "reference_cpu_note": "reference Train_dqn.train at its own shapes (GRU-32), 8 threads of "
                                               "the build container (BASELINE.md)",
