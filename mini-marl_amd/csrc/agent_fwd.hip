@@ -1048,6 +1048,7 @@ __global__ __launch_bounds__(512, 2) void agent_q_fwd_lds_kernel(QFwdParams p0, 
 #endif
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __host__ __device__ __forceinline__ int kperm16(int j, int g) { return 16 * (j >> 2) + 4 * g + (j & 3); }
 
@@ -1287,6 +1288,60 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
     for (int kb = 0; kb < RB2; ++kb) tri(CG::off_ih + (rb * RB2 + kb) * 1024, HB * RB2 * 1024, x2s[kb], ar, az, anx);
 #pragma unroll
     for (int kb = 0; kb < HB; ++kb) tri(CG::off_hh + (rb * HB + kb) * 1024, HB * HB * 1024, h0s[kb], ar, az, anh);
+#ifndef MM_H3_PK
+#define MM_H3_PK 1
+#endif
+#if MM_H3_PK
+    // gates two rows at a time on packed f32 (v_pk_mul / v_pk_add / v_pk_fma: two values per VALU
+    // issue); the transcendentals stay scalar. Same operations as sigmoidf_ / tanhf_.
+    float rrs[4], zs[4], ns[4];
+#pragma unroll
+    for (int rp = 0; rp < 4; rp += 2) {
+      const f32x2 vr = {ar[rp], ar[rp + 1]}, vz = {az[rp], az[rp + 1]};
+      const f32x2 vx = {anx[rp], anx[rp + 1]}, vh = {anh[rp], anh[rp + 1]}, v0 = {h0[t][rp], h0[t][rp + 1]};
+      f32x2 er = vr * -1.4426950408889634f, ez = vz * -1.4426950408889634f;
+      er.x = __builtin_amdgcn_exp2f(er.x);
+      er.y = __builtin_amdgcn_exp2f(er.y);
+      ez.x = __builtin_amdgcn_exp2f(ez.x);
+      ez.y = __builtin_amdgcn_exp2f(ez.y);
+      er = er + 1.0f;
+      ez = ez + 1.0f;
+      f32x2 rr, z;
+      rr.x = __builtin_amdgcn_rcpf(er.x);
+      rr.y = __builtin_amdgcn_rcpf(er.y);
+      z.x = __builtin_amdgcn_rcpf(ez.x);
+      z.y = __builtin_amdgcn_rcpf(ez.y);
+      f32x2 en = (vx + rr * vh) * 2.8853900817779268f;
+      en.x = __builtin_amdgcn_exp2f(en.x);
+      en.y = __builtin_amdgcn_exp2f(en.y);
+      en = en + 1.0f;
+      f32x2 n;
+      n.x = __builtin_amdgcn_rcpf(en.x);
+      n.y = __builtin_amdgcn_rcpf(en.y);
+      n = 1.0f - 2.0f * n;
+      const f32x2 hn = n + z * (v0 - n);
+      h1[t][rp] = hn.x;
+      h1[t][rp + 1] = hn.y;
+      rrs[rp] = rr.x;
+      rrs[rp + 1] = rr.y;
+      zs[rp] = z.x;
+      zs[rp + 1] = z.y;
+      ns[rp] = n.x;
+      ns[rp + 1] = n.y;
+    }
+    if (sv) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float* o = sv + F1 + G + 16 * t + 4 * g + r;
+        o[0] = h0[t][r];
+        o[H] = rrs[r];
+        o[2 * H] = zs[r];
+        o[3 * H] = ns[r];
+        o[4 * H] = anh[r];
+        o[5 * H] = h1[t][r];
+      }
+    }
+#else
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float rr = sigmoidf_(ar[r]);
@@ -1303,6 +1358,7 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
         o[5 * H] = h1[t][r];
       }
     }
+#endif
     if (hop) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) hop[(int64_t)(16 * t + r) * io.hout_sf] = h1[t][r];
