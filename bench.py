@@ -482,6 +482,51 @@ def main():
                 "reference_cpu_ms_per_update": 115.8,
                 "reference_cpu_note": "reference train_policy_on_batch, same shapes, 8 threads of the build "
                                       "container (tools/ref_time_offq.py)"}
+        # the same update fed by the device episode replay (PrioritizedRecReplayBuffer, rec_buffer.py:243-324,
+        # the reference's default buffer_size 10000 episodes): sample(B, beta) -> train_policy_on_batch ->
+        # update_priorities -> soft update, nothing leaves the GPU
+        from minimarl.recbuf import PrioritizedRecReplayBuffer
+
+        box = lambda n: type("Box", (), {"shape": (n,)})()  # noqa: E731  (gym.spaces stand-ins: .shape / .n)
+        pinfo = {pid: {"obs_space": box(D), "share_obs_space": box(N * D),
+                       "act_space": type("Discrete", (), {"n": 5})()}}
+        rb = PrioritizedRecReplayBuffer(0.6, pinfo, {pid: list(range(N))}, 10000, oT, True, False, device=dev,
+                                        seed=7, leaf_mode="slots")
+        ins = [to(np.ascontiguousarray(np.moveaxis(x, 0, 2))) for x in (obs, acts, rew, dones)]   # -> [L, n, N, X]
+        sh_in = to(np.ascontiguousarray(np.repeat(share[:, :, None], N, axis=2)))                 # [T+1, n, N, S]
+        dn_in = to(dn)
+        for _ in range(10000 // oB + 1):
+            rb.insert(oB, {pid: ins[0]}, {pid: sh_in}, {pid: ins[1]}, {pid: ins[2]}, {pid: ins[3]}, {pid: dn_in})
+        ev_r = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for _ in range(3):
+            smp = rb.sample(oB, 0.4, pid)
+            _, pr, ix = otr.train_policy_on_batch(smp)
+            rb.update_priorities(ix, pr, pid)
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        for _ in range(args.offq_updates):
+            smp = rb.sample(oB, 0.4, pid)
+            _, pr, ix = otr.train_policy_on_batch(smp)
+            rb.update_priorities(ix, pr, pid)
+            otr.soft_target_updates()
+        torch.cuda.synchronize()
+        el_r = time.perf_counter() - t4
+        ev_r[0].record()
+        for _ in range(args.offq_updates):
+            smp = rb.sample(oB, 0.4, pid)
+            rb.update_priorities(smp[8], torch.ones(oB, device=dev), pid)
+        ev_r[1].record()
+        torch.cuda.synchronize()
+        gb = sum(t.numel() * 4 for t in (smp[0][pid], smp[1][pid], smp[2][pid], smp[3][pid], smp[4][pid],
+                                         smp[5][pid])) * 2 / 1e9           # gathered bytes read + written
+        ms_buf = ev_r[0].elapsed_time(ev_r[1]) / args.offq_updates
+        offq["with_episode_replay"] = {
+            "buffer": "PrioritizedRecReplayBuffer (device, 10000 episodes, sum/min segment trees)",
+            "ms_per_update": round(el_r / args.offq_updates * 1e3, 4),
+            "buffer_ms_per_sample_and_update": round(ms_buf, 4),
+            "gather_bytes_per_sample": int(gb * 1e9),
+            "gather_GBps_incl_tree_ops": round(gb / (ms_buf * 1e-3), 1)}
+        del rb
         if not args.no_cpu_baseline:
             bnp = {"obs": obs, "share_obs": share, "acts": acts, "rewards": rew, "dones_env": dn,
                    "is_weight": (0.5 + np.random.default_rng(1).random(oB)).astype(np.float32)}
