@@ -204,7 +204,10 @@ def test_learner_update_from_device_per():
     torch.cuda.synchronize()
 
 
-def test_learner_graph_replay_matches_eager():
+@pytest.mark.parametrize("mode", ["qmix", "vdn_double"])
+def test_learner_graph_replay_matches_eager(mode):
+    """Replays of the captured update (one fused graph per update) equal eager updates, including the
+    double net's device-RNG epsilon-greedy draws (vdn_double, epsilon 0.3: fresh draws per update)."""
     from minimarl.engine import RolloutEngine
     from minimarl.learner import Mixer, QLearner
 
@@ -212,6 +215,10 @@ def test_learner_graph_replay_matches_eager():
         eng = RolloutEngine(64, 4, f1=64, g=64, h=64, chunk=10, capacity=256, seed=3, device=DEV)
         for _ in range(2):
             eng.run_graph(0.5)
+        if mode == "vdn_double":
+            L = QLearner(eng.behavior, eng.target, None, None, batch=16, chunk=10, mode=mode, device=DEV)
+            L.double_eps = 0.3
+            return eng, L
         mix = Mixer(4, 4 * eng.D, 64, 32, DEV, seed=1)
         tmix = Mixer(4, 4 * eng.D, 64, 32, DEV, seed=2)
         return eng, QLearner(eng.behavior, eng.target, mix, tmix, batch=16, chunk=10, mode="qmix", device=DEV)
