@@ -746,13 +746,11 @@ __global__ __launch_bounds__(256) void mixer_fwd_seq_lds_kernel(MixFwdArgs a, Mi
 // VDN (mix_sum): Qtot = sum_i qa_i, Q'tot = sum_i maxq'_i, dqa_i = dQtot.
 // flags: MM_LOSS_MIX_SUM (VDN), MM_LOSS_HUBER (smooth_l1, beta 1: qmix/qmix.py:218),
 // MM_LOSS_TARGET_SUM (y = sum_i r_i + gamma*(1-d)*Q'tot: qmix/qmix.py:215-217, no xN, no IS weight).
-__global__ void lrn_loss_kernel(int B, int C, int N, float gamma, const float* rew, const float* done,
-                                const float* isw, const float* qtot, const float* qtot_t, int flags,
-                                const float* qa, const float* maxq, float* dq, float* dqa, float* loss_parts,
-                                float* td_last) {
+__device__ __forceinline__ void lrn_loss_elem(int i, int B, int C, int N, float gamma, const float* rew,
+                                              const float* done, const float* isw, const float* qtot,
+                                              const float* qtot_t, int flags, const float* qa, const float* maxq,
+                                              float* dq, float* dqa, float* loss_parts, float* td_last) {
   const int mix_sum = flags & MM_LOSS_MIX_SUM;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * C) return;
   const int b = i % B, t = i / B;
   float qt, qn;
   if (mix_sum) {
@@ -793,6 +791,13 @@ __global__ void lrn_loss_kernel(int B, int C, int N, float gamma, const float* r
   loss_parts[i] = part;
   if (t == C - 1) td_last[b] = fabsf(diff);
 }
+__global__ void lrn_loss_kernel(int B, int C, int N, float gamma, const float* rew, const float* done,
+                                const float* isw, const float* qtot, const float* qtot_t, int flags,
+                                const float* qa, const float* maxq, float* dq, float* dqa, float* loss_parts,
+                                float* td_last) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B * C) lrn_loss_elem(i, B, C, N, gamma, rew, done, isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts, td_last);
+}
 
 // loss = sum_t (1/B) sum_b parts (logging value): small batches one thread per step t summing its
 // B parts in order; large batches (B > 256) a strided per-thread sum + fixed-shape tree per step.
@@ -832,6 +837,31 @@ __global__ __launch_bounds__(256) void lrn_loss_reduce_kernel(int B, int C, cons
     __syncthreads();
   }
   if (threadIdx.x == 0) *loss = tot;
+}
+
+// Small batches (B * C <= 1024, B <= 256): the loss terms and the per-step in-order reduction in ONE
+// workgroup (the parts go through global memory inside the block: same values, same summation order as
+// lrn_loss_kernel + lrn_loss_reduce_kernel, one launch fewer per update).
+__global__ __launch_bounds__(1024) void lrn_loss_small_kernel(int B, int C, int N, float gamma, const float* rew,
+                                                              const float* done, const float* isw, const float* qtot,
+                                                              const float* qtot_t, int flags, const float* qa,
+                                                              const float* maxq, float* dq, float* dqa,
+                                                              float* loss_parts, float* td_last, float* loss) {
+  __shared__ float sh[256];
+  const int i = threadIdx.x;
+  if (i < B * C) lrn_loss_elem(i, B, C, N, gamma, rew, done, isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts, td_last);
+  __syncthreads();
+  for (int t = threadIdx.x; t < C; t += blockDim.x) {
+    float sacc = 0.f;
+    for (int b = 0; b < B; ++b) sacc += loss_parts[(int64_t)t * B + b];
+    sh[t] = sacc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int t = 0; t < C; ++t) tot += sh[t] / (float)B;
+    *loss = tot;
+  }
 }
 
 // ------------------------------------------------------------------ mixer backward (one step)
@@ -2537,6 +2567,12 @@ int mm_lrn_loss_ex(int32_t B, int32_t C, int32_t N, float gamma, const float* re
   MM_REQUIRE((flags & MM_LOSS_MIX_SUM) ? (qa && maxq && dqa) : (qtot && qtot_t), "lrn_loss: missing Q inputs");
   MM_REQUIRE((flags & MM_LOSS_TARGET_SUM) || isw, "lrn_loss: isw required");
   const int n = B * C;
+  if (n <= 1024 && B <= 256 && C <= 256) {
+    hipLaunchKernelGGL(mm::lrn_loss_small_kernel, dim3(1), dim3(1024), 0, (hipStream_t)s, B, C, N, gamma, rew, done,
+                       isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts, td_last, loss);
+    MM_HIP_CHECK(hipGetLastError());
+    return MM_OK;
+  }
   hipLaunchKernelGGL(mm::lrn_loss_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, B, C, N, gamma, rew,
                      done, isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts, td_last);
   MM_HIP_CHECK(hipGetLastError());
