@@ -281,20 +281,23 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
     d.apples[e] = dn && autoreset ? d.init_apples : apples;
   }
   __syncthreads();
+  // ---- phase 2: local obs of (env, agent) ea = lane % 64 into the LDS tile; the block's TB / 64 waves
+  // split the 9 neighbourhood cells (wave w: cells w, w + TB/64, ...), wave 0 also writes the coords
+  const int ea = lane & (WT - 1), part = lane / WT;
   int mypos = 0;
-  if (lane < nl) mypos = spos[lane];
+  if (ea < nl) mypos = spos[ea];
   if (d.dbg == 3) return;
-
-  // ---- phase 2: local obs of (env le_l, agent k_l) into the LDS tile
-  if (lane < nl) {
-    float* o = sloc + le_l * LD + k_l * OBS_LOCAL;
+  if (ea < nl) {
+    const int le2 = ea / N, k2 = ea % N;
+    float* o = sloc + le2 * LD + k2 * OBS_LOCAL;
     const int pr = mypos >> 8, pc = mypos & 255;
-    o[0] = (float)pr * d.inv_r;
-    o[1] = (float)pc * d.inv_c;
-    const int8_t* g = sgrid + le_l * RC;
-    const uint8_t* oc = socc + le_l * RC;
-#pragma unroll
-    for (int cell = 0; cell < 9; ++cell) {
+    if (part == 0) {
+      o[0] = (float)pr * d.inv_r;
+      o[1] = (float)pc * d.inv_c;
+    }
+    const int8_t* g = sgrid + le2 * RC;
+    const uint8_t* oc = socc + le2 * RC;
+    for (int cell = part; cell < 9; cell += TB / WT) {
       const int rr = pr + cell / 3 - 1, cc = pc + cell % 3 - 1;
       const bool inside = rr >= 0 && rr < d.R && cc >= 0 && cc < d.C;
       float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f, v4 = 1.f;
