@@ -560,7 +560,8 @@ int mm_erb_sample_prioritized(mm_erb* b, int32_t B, double beta, const double* f
                               uint64_t counter, int64_t* idx_out, double* w_out, float* w32_out, mm_stream_t s);
 /* Uniform indices (RecReplayBuffer.sample, rec_buffer.py:76): idx_b = floor(u_b len), device RNG. */
 int mm_erb_sample_uniform(mm_erb* b, int32_t B, uint64_t seed, uint64_t counter, int64_t* idx_out, mm_stream_t s);
-/* sample_inds: gather the B episodes idx [B] (device int64) into the sample layout above. */
+/* sample_inds: gather the B episodes idx [B] (device int64) into the sample layout above (an index
+ * outside [0, buffer_size) gathers zeros and sets bit 2 of the error word). */
 int mm_erb_gather(mm_erb* b, int32_t B, const int64_t* idx, const mm_erb_fields* dst, mm_stream_t s);
 /* update_priorities (rec_buffer.py:306-324): leaves[idx] = prio ** alpha (f32 pow, last duplicate
  * wins), ancestors re-derived, max_priority = max(max_priority, max prio). idx, prio: device [B]. An
@@ -570,7 +571,8 @@ int mm_erb_update_priorities(mm_erb* b, const int64_t* idx, const float* prio, i
 double* mm_erb_sum_tree(mm_erb* b);           /* device f64 [2 * itcap] */
 double* mm_erb_min_tree(mm_erb* b);           /* device f64 [2 * itcap] */
 float* mm_erb_max_priority(mm_erb* b);        /* device f32 [1] */
-int32_t* mm_erb_error_word(mm_erb* b);        /* device i32 [1]: bit 0 bad index, bit 1 priority <= 0 */
+int32_t* mm_erb_error_word(mm_erb* b);        /* device i32 [1]: bit 0 bad update index, bit 1 priority <= 0,
+                                                 bit 2 bad gather index */
 /* Stream-ordered device copies of the trees, max_priority and the error word (any may be NULL). */
 int mm_erb_copy_state(mm_erb* b, double* sum_dst, double* min_dst, float* maxp_dst, int32_t* err_dst, mm_stream_t s);
 

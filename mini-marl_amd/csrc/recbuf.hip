@@ -60,13 +60,20 @@ __global__ __launch_bounds__(256) void erb_insert_kernel(ErbFieldSet fs, uint32_
 }
 
 // gather (sample_inds): dst[((nf L + l) B + b) X + x] = store[(idx_b L + l) R + nf X + x]
-__global__ __launch_bounds__(256) void erb_gather_kernel(ErbFieldSet fs, uint32_t B, const int64_t* __restrict__ idx) {
+// (an index outside [0, size) reads nothing: its rows are written as 0 and bit 2 of err is set)
+__global__ __launch_bounds__(256) void erb_gather_kernel(ErbFieldSet fs, uint32_t B, const int64_t* __restrict__ idx,
+                                                         int64_t size, int32_t* err) {
   const ErbField& F = fs.f[blockIdx.y];
   const uint32_t X = F.R / F.Nf;
   const uint32_t total = F.L * B * F.R;
   for (uint32_t o = blockIdx.x * 256 + threadIdx.x; o < total; o += gridDim.x * 256) {
     const uint32_t x = o % X, q = o / X, b = q % B, q2 = q / B, l = q2 % F.L, nf = q2 / F.L;
     const int64_t slot = idx[b];
+    if (slot < 0 || slot >= size) {
+      F.dst[o] = 0.0f;
+      if (o == 0 || x + l + nf == 0) atomicOr(err, 4);
+      continue;
+    }
     F.dst[o] = F.store[((size_t)slot * F.L + l) * F.R + nf * X + x];
   }
 }
@@ -338,7 +345,7 @@ int mm_erb_gather(mm_erb* b, int32_t B, const int64_t* idx, const mm_erb_fields*
   }
   if (fs.nf == 0) return MM_OK;
   hipLaunchKernelGGL(mm::erb_gather_kernel, dim3(erb_grid(fs, B), fs.nf), dim3(256), 0, (hipStream_t)s, fs, (uint32_t)B,
-                     idx);
+                     idx, b->size, b->err);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

@@ -140,6 +140,10 @@ class RecReplayBuffer:
             check(lib().mm_erb_sample_uniform(pb0._h, B, self.seed, self._next_counter(), ptr(idx),
                                               stream_handle(self.device)), "erb_sample_uniform")
         else:
+            if not torch.is_tensor(inds):
+                ii = np.asarray(inds)
+                if len(ii) and (ii.min() < 0 or ii.max() >= len(self)):
+                    raise IndexError("sample: episode index outside the filled buffer")
             idx = torch.as_tensor(np.asarray(inds) if not torch.is_tensor(inds) else inds).to(
                 device=self.device, dtype=torch.int64).contiguous()
         return self._gather_all(idx, B) + (None, None)
@@ -153,6 +157,34 @@ class RecReplayBuffer:
                 res[k][p_id] = out[k]
             avail[p_id] = None
         return tuple(res[k] for k in FIELDS) + (avail,)
+
+    # -- inspection (tests, checkpoints) -------------------------------------------------------
+    def state(self, p_id="policy_0"):
+        """Device copies (stream-ordered) of (sum tree f64 [2 itcap], min tree, max_priority f32 [1],
+        error word i32 [1])."""
+        pb = self.policy_buffers[p_id]
+        n = 2 * int(lib().mm_erb_it_capacity(pb._h))
+        st = (torch.empty(n, dtype=torch.float64, device=self.device),
+              torch.empty(n, dtype=torch.float64, device=self.device),
+              torch.empty(1, dtype=torch.float32, device=self.device),
+              torch.empty(1, dtype=torch.int32, device=self.device))
+        check(lib().mm_erb_copy_state(pb._h, *[ptr(t) for t in st], stream_handle(self.device)), "erb_copy_state")
+        return st
+
+    def trees(self, p_id="policy_0"):
+        """(sum tree, min tree) as host f64 arrays."""
+        s, m, _, _ = self.state(p_id)
+        return s.cpu().numpy(), m.cpu().numpy()
+
+    def max_priority(self, p_id="policy_0"):
+        return float(self.state(p_id)[2].cpu()[0])
+
+    def check_errors(self, p_id="policy_0"):
+        """Raise AssertionError if a device-side update_priorities hit the reference's asserts."""
+        e = int(self.state(p_id)[3].cpu()[0])
+        assert e & 1 == 0, "update_priorities: index outside [0, len)"
+        assert e & 2 == 0, "update_priorities: priority <= 0"
+        assert e & 4 == 0, "sample: episode index outside the buffer"
 
 
 class PrioritizedRecReplayBuffer(RecReplayBuffer):
@@ -201,33 +233,6 @@ class PrioritizedRecReplayBuffer(RecReplayBuffer):
         check(lib().mm_erb_update_priorities(pb._h, ptr(idx), ptr(pr), int(idx.numel()), stream_handle(self.device)),
               "erb_update_priorities")
         self._keep_up = (idx, pr)
-
-    # -- inspection (tests, checkpoints) -------------------------------------------------------
-    def state(self, p_id="policy_0"):
-        """Device copies (stream-ordered) of (sum tree f64 [2 itcap], min tree, max_priority f32 [1],
-        error word i32 [1])."""
-        pb = self.policy_buffers[p_id]
-        n = 2 * int(lib().mm_erb_it_capacity(pb._h))
-        st = (torch.empty(n, dtype=torch.float64, device=self.device),
-              torch.empty(n, dtype=torch.float64, device=self.device),
-              torch.empty(1, dtype=torch.float32, device=self.device),
-              torch.empty(1, dtype=torch.int32, device=self.device))
-        check(lib().mm_erb_copy_state(pb._h, *[ptr(t) for t in st], stream_handle(self.device)), "erb_copy_state")
-        return st
-
-    def trees(self, p_id="policy_0"):
-        """(sum tree, min tree) as host f64 arrays."""
-        s, m, _, _ = self.state(p_id)
-        return s.cpu().numpy(), m.cpu().numpy()
-
-    def max_priority(self, p_id="policy_0"):
-        return float(self.state(p_id)[2].cpu()[0])
-
-    def check_errors(self, p_id="policy_0"):
-        """Raise AssertionError if a device-side update_priorities hit the reference's asserts."""
-        e = int(self.state(p_id)[3].cpu()[0])
-        assert e & 1 == 0, "update_priorities: index outside [0, len)"
-        assert e & 2 == 0, "update_priorities: priority <= 0"
 
 
 __all__ = ["RecReplayBuffer", "PrioritizedRecReplayBuffer"]

@@ -169,3 +169,18 @@ def test_recbuf_feeds_offpolicy_trainer():
     tree_close(s, ora.sum.v, "sum")
     tree_close(m, ora.min.v, "min")
     assert np.float32(buf.max_priority()) == np.float32(ora.max_p)
+
+
+def test_recbuf_gather_guards_bad_indices():
+    """Host indices outside the filled buffer raise (the reference's numpy IndexError); device indices
+    outside the ring gather zeros and set the error word instead of reading out of bounds."""
+    SIZE, T, N, D, A = 16, 4, 2, 3, 3
+    rng = np.random.default_rng(1)
+    uni = make(False, SIZE, T, N, D, N * D, A)
+    uni.insert(5, *[{"policy_0": x} for x in _episodes(rng, 5, T, N, D, A)])
+    with pytest.raises(IndexError):
+        uni.sample(2, inds=np.array([0, 7]))
+    out = uni.sample(2, inds=torch.tensor([1, 99], device="cuda"))
+    assert float(out[0]["policy_0"][:, :, 1].abs().sum()) == 0.0
+    with pytest.raises(AssertionError, match="gather|outside the buffer"):
+        uni.check_errors()
