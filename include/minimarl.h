@@ -518,6 +518,20 @@ int mm_switch_step(mm_switch* w, const int32_t* act, float* next_obs, float* obs
                    uint8_t* agent_done, uint8_t* done, mm_stream_t s);
 /* host copies of the state (synchronous): pos [E, N, 2], agent_done [E, N], steps [E] */
 int mm_switch_get_state(mm_switch* w, int32_t* pos, uint8_t* agent_done, int32_t* steps);
+/* restore a state returned by mm_switch_get_state (checkpoint resume; synchronous) */
+int mm_switch_set_state(mm_switch* w, const int32_t* pos, const uint8_t* agent_done, const int32_t* steps);
+const float* mm_switch_reset_obs(const mm_switch* w); /* device [N, D]: the (deterministic) reset obs */
+/* The rollout engine's row steps, same contract as mm_env_step_rows / mm_env_step_rows_td (the env's
+ * done written is all(agent done), what qmix/main.py:199,215 stores): the Switch env behind the same
+ * chunk-store engine as the Checkers env. */
+int mm_switch_step_rows(mm_switch* w, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
+                        float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s);
+int mm_switch_step_rows_td(mm_switch* w, const int32_t* act, float* next_obs, int64_t next_se,
+                           const int64_t* next_row, int64_t* cur_row, float* rew, uint8_t* done, float gamma,
+                           const float* td_rew, const uint8_t* td_done, const float* q_taken, const float* max_q_next,
+                           const int32_t* td_act, float* chunk_td, int32_t step_in_chunk, int32_t chunk_len,
+                           uint8_t* store_act, float* store_rew, uint8_t* store_done, const int64_t* td_rows,
+                           uint64_t* counter, mm_stream_t s);
 
 /* ------------------------------------------------------- offpolicy episode replay (mm_erb_*) */
 /* RecReplayBuffer / PrioritizedRecReplayBuffer of one policy (offpolicy/utils/rec_buffer.py:10-324)

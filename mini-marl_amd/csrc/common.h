@@ -128,6 +128,26 @@ __device__ __forceinline__ float dot_seq_n(const float* w, const float* x, int K
   return acc;
 }
 
+// Fused TD/store of the PREVIOUS rollout step (td_chunk_kernel's work, rollout.hip) done by the
+// env kernels (env.hip, switch.hip) of the next step: its inputs (rew, done, Q(a), max Q') are final once the dual forward
+// of that step has run, and the env kernel of step t+1 is the next launch on the stream. Saves one
+// launch per in-chunk step. Same arithmetic and agent-order sums as td_chunk_kernel.
+struct TdFuse {
+  const float* rew;       // [E][N] rewards of the previous step (overwritten by this step later)
+  const uint8_t* done;    // [E]
+  const float* q_taken;   // [E][N]
+  const float* maxq;      // [E][N]
+  const int32_t* act;     // [E][N]
+  float* chunk_td;        // [E]
+  uint8_t* s_act;         // store [rows][C][N]
+  float* s_rew;           // store [rows][C][N]
+  uint8_t* s_done;        // store [rows][C]
+  const int64_t* rows;    // [E] store rows of the previous step
+  uint64_t* counter;      // RNG step counter (may be null)
+  float gamma;
+  int slot, C, on;
+};
+
 }  // namespace mm
 
 #define MM_HIP_CHECK(expr)                                                     \

@@ -101,26 +101,6 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvDev d, float* obs, in
   }
 }
 
-// Fused TD/store of the PREVIOUS rollout step (td_chunk_kernel's work, rollout.hip) done by the
-// env kernel of the next step: its inputs (rew, done, Q(a), max Q') are final once the dual forward
-// of that step has run, and the env kernel of step t+1 is the next launch on the stream. Saves one
-// launch per in-chunk step. Same arithmetic and agent-order sums as td_chunk_kernel.
-struct TdFuse {
-  const float* rew;       // [E][N] rewards of the previous step (overwritten by this step later)
-  const uint8_t* done;    // [E]
-  const float* q_taken;   // [E][N]
-  const float* maxq;      // [E][N]
-  const int32_t* act;     // [E][N]
-  float* chunk_td;        // [E]
-  uint8_t* s_act;         // store [rows][C][N]
-  float* s_rew;           // store [rows][C][N]
-  uint8_t* s_done;        // store [rows][C]
-  const int64_t* rows;    // [E] store rows of the previous step
-  uint64_t* counter;      // RNG step counter (may be null)
-  float gamma;
-  int slot, C, on;
-};
-
 // One wave per block, EPW = 64 / N envs per wave (lane = env-slot * N + agent). Phase 0 issues
 // every global read of the step at once (positions, actions, grid words, counters, destination
 // rows, the fused TD inputs); phase 1 runs the sequential-in-agent-order dynamics, one lane per

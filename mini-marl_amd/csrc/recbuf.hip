@@ -51,9 +51,9 @@ struct ErbFieldSet {
 // insert: store[(slot(e) L + l) R + r] = src[(l n + e) R_in + r], slot(e) = (current + e) % size
 __global__ __launch_bounds__(256) void erb_insert_kernel(ErbFieldSet fs, uint32_t n, int64_t current, int64_t size) {
   const ErbField& F = fs.f[blockIdx.y];
-  const uint32_t total = F.L * n * F.R;
-  for (uint32_t o = blockIdx.x * 256 + threadIdx.x; o < total; o += gridDim.x * 256) {
-    const uint32_t r = o % F.R, le = o / F.R, e = le % n, l = le / n;
+  const uint64_t total = (uint64_t)F.L * n * F.R;
+  for (uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x; o < total; o += (uint64_t)gridDim.x * 256) {
+    const uint64_t r = o % F.R, le = o / F.R, e = le % n, l = le / n;
     const int64_t slot = (current + e) % size;
     F.store[((size_t)slot * F.L + l) * F.R + r] = F.src[((size_t)l * n + e) * F.R_in + r];
   }
@@ -65,9 +65,9 @@ __global__ __launch_bounds__(256) void erb_gather_kernel(ErbFieldSet fs, uint32_
                                                          int64_t size, int32_t* err) {
   const ErbField& F = fs.f[blockIdx.y];
   const uint32_t X = F.R / F.Nf;
-  const uint32_t total = F.L * B * F.R;
-  for (uint32_t o = blockIdx.x * 256 + threadIdx.x; o < total; o += gridDim.x * 256) {
-    const uint32_t x = o % X, q = o / X, b = q % B, q2 = q / B, l = q2 % F.L, nf = q2 / F.L;
+  const uint64_t total = (uint64_t)F.L * B * F.R;
+  for (uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x; o < total; o += (uint64_t)gridDim.x * 256) {
+    const uint64_t x = o % X, q = o / X, b = q % B, q2 = q / B, l = q2 % F.L, nf = q2 / F.L;
     const int64_t slot = idx[b];
     if (slot < 0 || slot >= size) {
       F.dst[o] = 0.0f;
@@ -140,9 +140,11 @@ __global__ __launch_bounds__(1024) void erb_set_kernel(double* __restrict__ sum,
 
 __device__ __forceinline__ double rng_unit53(uint64_t r) { return (double)(r >> 11) * (1.0 / 9007199254740992.0); }
 
-// Prioritized sample: total = sum(0, len - 1) by the reference's _reduce_helper order (start 0: a right
-// fold of the fully covered left children met on the way down to the node whose range ends at len-1),
-// then per draw the prefix-sum descent and the IS weight.
+// Prioritized sample: total = _it_sums.sum(0, len - 1) (rec_buffer.py:273). SegmentTree.reduce
+// decrements its end (segment_tree.py:71), so the fold covers leaves [0, len - 2] — the last filled
+// leaf is never part of the sampled mass. Folded in the reference's _reduce_helper order (start 0: a
+// right fold of the fully covered left children met on the way down to the node whose range ends at
+// len - 2), then per draw the prefix-sum descent and the IS weight.
 __global__ __launch_bounds__(256) void erb_sample_kernel(const double* __restrict__ sum, const double* __restrict__ mn,
                                                          int64_t itcap, int64_t len, int B, double beta,
                                                          const double* __restrict__ fracs, uint64_t seed,
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(256) void erb_sample_kernel(const double* __restric
   __shared__ double total_s;
   if (threadIdx.x == 0) {
     int64_t node = 1, ns = 0, ne = itcap - 1;
-    const int64_t end = len - 1;
+    const int64_t end = len - 2;   // len > B >= 1 (checked on the host)
     int64_t lefts[64];
     int nl = 0;
     while (end != ne) {

@@ -342,4 +342,9 @@ _SIGS += [
     ("mm_switch_reset", c_i32, [c_vp, c_vp, c_vp]),
     ("mm_switch_step", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_switch_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp]),
+    ("mm_switch_set_state", c_i32, [c_vp, c_vp, c_vp, c_vp]),
+    ("mm_switch_reset_obs", c_vp, [c_vp]),
+    ("mm_switch_step_rows", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_switch_step_rows_td", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp,
+                                       c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 ]

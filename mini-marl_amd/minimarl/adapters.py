@@ -177,13 +177,23 @@ class _LearnerAdapter:
         self._learner, self._key = None, None
 
     def _bind(self, beh, tgt, mix, tmix, optimizer):
-        key = tuple(id(x) for x in (beh, tgt, mix, tmix))
+        """The QLearner for these nets and optimizer hyper-parameters. A change of any net or of lr / betas /
+        eps rebuilds it: the old learner releases its nets first, and when the trained nets are the same
+        objects the Adam moments carry over (the reference's optimizer keeps its state across calls)."""
+        lr, betas, eps = _hyper(optimizer)
+        key = tuple(id(x) for x in (beh, tgt, mix, tmix)) + (lr, tuple(betas), eps)
         if self._learner is None or key != self._key:
-            lr, betas, eps = _hyper(optimizer)
+            adam = None
+            if self._learner is not None:
+                state = self._learner.release()
+                if self._key[0] == key[0] and self._key[2] == key[2]:
+                    adam = state
             self._learner = QLearner(beh.net, tgt.net, mix.mixer if mix is not None else None,
                                      tmix.mixer if tmix is not None else None, batch=self.batch_size,
                                      chunk=self.chunk_size, gamma=self.gamma, lr=lr, grad_clip=self.grad_clip_norm,
                                      betas=betas, adam_eps=eps, mode=self.mode, device=self.device)
+            if adam is not None:
+                self._learner.adopt_adam(adam)
             self._key = key
         return self._learner
 

@@ -13,6 +13,9 @@ from dataclasses import dataclass, field, replace
 @dataclass
 class QTrainConfig:
     algo: str = "vdn"                   # "vdn" | "vdn_double" | "qmix" | "qmix_min"
+    # --env_name (vdn/_config.py:19-24 "ma_gym:Checkers-v0"; qmix/_config.py:14-19 "ma_gym:Switch2-v0"):
+    # "checkers" | "switch"
+    env: str = "checkers"
     n_envs: int = 32
     n_agents: int = 2
     full_observable: bool = True        # vdn/main.py:61-62 (Checkers full obs); QMIX uses partial obs
@@ -72,9 +75,9 @@ def vdn_reference():
 
 
 def qmix_reference():
-    """qmix/_config.py defaults (alpha 0.8, beta 0.2, buffer 1000, eps 0.9 -> 0.05 over 60000 episodes,
-    10 test episodes every 10 episodes, partial obs)."""
-    return QTrainConfig(algo="qmix", full_observable=False, max_epsilon=0.9, epsilon_anneal_episode=60000,
+    """qmix/_config.py defaults: the Switch2 env (2 agents, partial obs), alpha 0.8, beta 0.2, buffer
+    1000, eps 0.9 -> 0.05 over 60000 episodes, 10 test episodes every 10 episodes."""
+    return QTrainConfig(algo="qmix", env="switch", full_observable=False, max_epsilon=0.9, epsilon_anneal_episode=60000,
                         max_episodes=100000, buffer_limit=1000, alpha=0.8, beta=0.2, use_step_weight=False,
                         test_interval=10, test_envs=10)
 
@@ -113,7 +116,8 @@ class Preset:
 
 def presets():
     """BASELINE.json configs[0..4] (SURVEY 8d shapes)."""
-    cfg2 = replace(qmix_reference(), n_agents=8, n_envs=4096, g=64, h=64, mixer_hidden=64, buffer_limit=65536)
+    cfg2 = replace(qmix_reference(), env="checkers", n_agents=8, n_envs=4096, g=64, h=64, mixer_hidden=64,
+                   buffer_limit=65536)
     return {
         "cfg1": Preset("cfg1", "VDN on 2-agent cooperative gridworld, 32 parallel envs (D = 94 full obs, GRU-32)",
                        q=replace(vdn_reference(), n_envs=32)),
@@ -125,7 +129,7 @@ def presets():
                        q=cfg2, gpus=8),
         "cfg5": Preset("cfg5", "QMIX SMAC-scale 27 agents, obs 300, 36 actions, 8192 envs, GRU-32, 8 GPUs "
                                "(no env of that shape exists: synthetic observations)",
-                       q=replace(qmix_reference(), n_agents=27, n_envs=8192, n_actions=36, g=32, h=32,
+                       q=replace(qmix_reference(), env="checkers", n_agents=27, n_envs=8192, n_actions=36, g=32, h=32,
                                  mixer_hidden=32, buffer_limit=65536),
                        gpus=8, extra={"obs_dim": 300}),
     }

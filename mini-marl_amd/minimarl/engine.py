@@ -31,7 +31,7 @@ import ctypes
 import torch
 
 from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, check, lib
-from .env import VecEnv
+from .env import make_env
 from .qnet import AgentQNet, graph_capture, ptr, stream_handle
 from .replay import DevicePER
 
@@ -52,11 +52,12 @@ class ChunkStore:
 class RolloutEngine:
     def __init__(self, n_envs, n_agents, obs_dim=None, n_actions=5, f1=64, g=32, h=32, chunk=10,
                  capacity=None, gamma=0.99, max_steps=100, step_cost=-0.01, full_observable=False,
-                 per_flavor="qmix", per_kwargs=None, seed=0, device="cuda"):
+                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", device="cuda"):
         self.device = torch.device(device)
         self.E, self.N, self.C = int(n_envs), int(n_agents), int(chunk)
         self.gamma = float(gamma)
-        self.env = VecEnv(self.E, self.N, max_steps, step_cost, full_observable, device=self.device)
+        self.env_kind = env
+        self.env = make_env(env, self.E, self.N, max_steps, step_cost, full_observable, device=self.device)
         self.D = self.env.obs_dim
         assert obs_dim is None or obs_dim == self.D
         self.A = n_actions
@@ -186,14 +187,14 @@ class RolloutEngine:
         if c > 0 and not self._td_flushed:
             # env(t) fused with the TD/store of step t-1 (same staging rows inside a chunk)
             kp = 1 - k
-            check(L.mm_env_step_rows_td(self.env.handle(), ptr(self.act_buf[k]), nxt, self.store.row_stride,
+            check(self.env.step_rows_td(ptr(self.act_buf[k]), nxt, self.store.row_stride,
                                         ptr(self.staging), ptr(self.cur_row), ptr(self.rew), ptr(self.done_buf[k]),
                                         self.gamma, ptr(self.rew), ptr(self.done_buf[kp]), ptr(self.qsel_buf[kp]),
                                         ptr(self.maxq), ptr(self.act_buf[kp]), ptr(self.chunk_td), c - 1, self.C,
                                         ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
                                         ptr(self.staging), ptr(self.counter_dev), s), "env_step_td")
         else:
-            check(L.mm_env_step_rows(self.env.handle(), ptr(self.act_buf[k]), nxt, self.store.row_stride,
+            check(self.env.step_rows(ptr(self.act_buf[k]), nxt, self.store.row_stride,
                                      ptr(self.staging), None, ptr(self.cur_row), ptr(self.rew),
                                      ptr(self.done_buf[k]), s), "env_step")
         self._td_flushed = False

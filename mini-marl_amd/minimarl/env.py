@@ -44,6 +44,13 @@ class VecEnv:
     def reset_obs_ptr(self):
         return lib().mm_env_reset_obs(self._h)
 
+    # the rollout engine's chunk-store row steps (mm_env_step_rows / _td, include/minimarl.h)
+    def step_rows(self, *args):
+        return lib().mm_env_step_rows(self._h, *args)
+
+    def step_rows_td(self, *args):
+        return lib().mm_env_step_rows_td(self._h, *args)
+
     def reset(self, out=None):
         out = out if out is not None else torch.empty(self.E, self.N, self.obs_dim, device=self.device)
         check(lib().mm_env_reset(self._h, ptr(out), stream_handle(self.device)), "env_reset")
@@ -120,6 +127,18 @@ class SwitchVecEnv:
             except Exception:
                 pass
 
+    def handle(self):
+        return self._h
+
+    def reset_obs_ptr(self):
+        return lib().mm_switch_reset_obs(self._h)
+
+    def step_rows(self, *args):
+        return lib().mm_switch_step_rows(self._h, *args)
+
+    def step_rows_td(self, *args):
+        return lib().mm_switch_step_rows_td(self._h, *args)
+
     def reset(self, out=None):
         out = out if out is not None else torch.empty(self.E, self.N, self.obs_dim, device=self.device)
         check(lib().mm_switch_reset(self._h, ptr(out), stream_handle(self.device)), "switch_reset")
@@ -148,3 +167,29 @@ class SwitchVecEnv:
         check(lib().mm_switch_get_state(self._h, pos.ctypes.data, adone.ctypes.data, steps.ctypes.data),
               "switch_get_state")
         return pos, adone, steps
+
+    def set_state(self, pos, adone, steps):
+        pos = np.ascontiguousarray(pos, np.int32)
+        adone = np.ascontiguousarray(adone, np.uint8)
+        steps = np.ascontiguousarray(steps, np.int32)
+        assert pos.shape == (self.E, self.N, 2) and adone.shape == (self.E, self.N) and steps.shape == (self.E,)
+        check(lib().mm_switch_set_state(self._h, pos.ctypes.data, adone.ctypes.data, steps.ctypes.data),
+              "switch_set_state")
+
+    def checkpoint_tensors(self):
+        pos, adone, steps = self.get_state()
+        return {"pos": torch.from_numpy(pos), "adone": torch.from_numpy(adone), "steps": torch.from_numpy(steps)}, {}
+
+    def restore_tensors(self, ts, scalars=None):
+        self.set_state(ts["pos"].numpy(), ts["adone"].numpy(), ts["steps"].numpy())
+
+
+def make_env(kind, n_envs, n_agents, max_steps=100, step_cost=-0.01, full_observable=False, device="cuda"):
+    """The lockstep env behind ``gym.make(args.env_name, ...)``: "checkers" (ma_gym:Checkers-v0, the
+    VDN default, vdn/_config.py:19-24) or "switch" (ma_gym:Switch2-v0, the QMIX default,
+    qmix/_config.py:14-19)."""
+    if kind == "checkers":
+        return VecEnv(n_envs, n_agents, max_steps, step_cost, full_observable, device=device)
+    if kind == "switch":
+        return SwitchVecEnv(n_envs, n_agents, max_steps, step_cost, full_observable, device=device)
+    raise ValueError(f"unknown env {kind!r} (checkers | switch)")

@@ -15,7 +15,7 @@ import ctypes
 import torch
 
 from ._lib import MM_MAPPO_ROLLOUT, MappoFwdArgs, check, lib
-from .env import VecEnv
+from .env import VecEnv, make_env
 from .qnet import ptr, stream_handle
 
 
@@ -23,8 +23,9 @@ class QEvaluator:
     """Greedy episodes of a VDN / QMIX agent net (AgentQNet) on a dedicated test VecEnv."""
 
     def __init__(self, n_envs, n_agents, max_steps=100, step_cost=-0.01, full_observable=False, gamma=0.99,
-                 device="cuda"):
-        self.env = VecEnv(n_envs, n_agents, max_steps, step_cost, full_observable, device=device)
+                 env="checkers", device="cuda"):
+        self.env = make_env(env, n_envs, n_agents, max_steps, step_cost, full_observable, device=device)
+        self.switch = env == "switch"
         self.E, self.N, self.max_steps, self.gamma = int(n_envs), int(n_agents), int(max_steps), float(gamma)
         self.device = torch.device(device)
 
@@ -40,7 +41,8 @@ class QEvaluator:
         loss = torch.zeros(E, device=dev) if target is not None else None
         for _ in range(self.max_steps):        # every env is done by max_steps
             act, qsel, h, _ = behavior.act(obs, h, 0.0)
-            nxt, rew, done = self.env.step(act)
+            out = self.env.step(act)
+            nxt, rew, done = (out[0], out[1], out[3]) if self.switch else out   # switch: all(agent done)
             maxq = None
             if target is not None:
                 maxq, ht = target.max_q(nxt, ht)

@@ -664,6 +664,28 @@ class QLearner:
         self.updates += 1
 
     # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)
+    def release(self):
+        """Hand the nets their parameters back as standalone tensors (copies of the current values) and
+        drop the ownership marks, so another QLearner can take them; returns the Adam state (m, v, step)
+        for a successor over the same nets."""
+        torch.cuda.synchronize(self.dev)
+        self.beh.flat = self.P[:self.n_agent].clone()
+        self.beh._owner = None
+        self.beh.mark_dirty()
+        if self.mix is not None:
+            self.mix.flat = self.P[self.n_agent:].clone()
+            self.mix._owner = None
+        return self.m.clone(), self.v.clone(), self.step_dev.clone(), self.updates
+
+    def adopt_adam(self, state):
+        """Continue from a predecessor's Adam state over the same parameter layout (``release``)."""
+        m, v, step, updates = state
+        assert m.numel() == self.n, "adopt_adam: parameter layout differs"
+        self.m.copy_(m)
+        self.v.copy_(v)
+        self.step_dev.copy_(step)
+        self.updates = int(updates)
+
     def checkpoint_tensors(self):
         ts = {"P": self.P, "m": self.m, "v": self.v, "step": self.step_dev, "target": self.tgt.flat}
         if self.tmix is not None:

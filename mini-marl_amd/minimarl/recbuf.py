@@ -141,11 +141,15 @@ class RecReplayBuffer:
                                               stream_handle(self.device)), "erb_sample_uniform")
         else:
             if not torch.is_tensor(inds):
-                ii = np.asarray(inds)
-                if len(ii) and (ii.min() < 0 or ii.max() >= len(self)):
-                    raise IndexError("sample: episode index outside the filled buffer")
-            idx = torch.as_tensor(np.asarray(inds) if not torch.is_tensor(inds) else inds).to(
-                device=self.device, dtype=torch.int64).contiguous()
+                # numpy fancy indexing into the [.., buffer_size, ..] arrays (rec_buffer.py:192-240):
+                # indices in [len, buffer_size) read the never-written defaults (0, dones 1), negative
+                # ones wrap, only |index| beyond buffer_size raises
+                ii = np.asarray(inds, np.int64)
+                size = self.buffer_size
+                if len(ii) and (ii.min() < -size or ii.max() >= size):
+                    raise IndexError(f"sample: index out of bounds for a buffer of size {size}")
+                inds = np.where(ii < 0, ii + size, ii)
+            idx = torch.as_tensor(inds).to(device=self.device, dtype=torch.int64).contiguous()
         return self._gather_all(idx, B) + (None, None)
 
     def _gather_all(self, idx, B):

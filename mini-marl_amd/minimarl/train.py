@@ -38,7 +38,7 @@ class QTrainer:
     def __init__(self, cfg: QTrainConfig, device="cuda", rank=0, grad_allreduce=None, world=1, track_score=True):
         self.cfg = c = cfg
         self.device = torch.device(device)
-        assert c.n_actions == 5, "the gridworld has 5 actions"
+        assert c.n_actions == 5, "the gridworld / switch envs have 5 actions"
         assert c.algo in ("vdn", "vdn_double", "qmix", "qmix_min")
         if c.buffer_limit < c.n_envs:
             raise ValueError(f"buffer_limit ({c.buffer_limit} chunks) must hold one chunk per env ({c.n_envs})")
@@ -50,7 +50,7 @@ class QTrainer:
                                  chunk=c.chunk_size, capacity=c.buffer_limit, gamma=c.gamma, max_steps=c.max_step,
                                  step_cost=c.step_cost, full_observable=c.full_observable,
                                  per_flavor=c.per_flavor, per_kwargs=per_kwargs, seed=c.seed + 7919 * rank,
-                                 device=self.device)
+                                 env=c.env, device=self.device)
         eng = self.eng
         # the behavior net's init does not depend on the rank (same seed): replicas start identical
         eng.behavior.init_default(c.seed)
@@ -71,7 +71,7 @@ class QTrainer:
         self.evaluator = None
         if c.test_interval and c.test_envs > 0:
             self.evaluator = QEvaluator(c.test_envs, c.n_agents, c.max_step, c.step_cost, c.full_observable,
-                                        c.gamma, device=self.device)
+                                        c.gamma, env=c.env, device=self.device)
         self.track_score = track_score
         self.ep_ret = torch.zeros(c.n_envs, device=self.device)
         self.score_acc = torch.zeros(2, dtype=torch.float64, device=self.device)

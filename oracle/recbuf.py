@@ -148,7 +148,9 @@ class RecBufferOracle:
     def sample(self, B, beta, fracs):
         """rec_buffer.py:272-304: returns (batch tuple, weights f64, idx)."""
         assert len(self) > B and beta > 0
-        total = self.sum.reduce_prefix(len(self) - 1)
+        # sum(0, len - 1) = reduce(0, len - 1), whose end -= 1 (segment_tree.py:71) leaves out the
+        # last filled leaf: the fold covers leaves [0, len - 2]
+        total = self.sum.reduce_prefix(len(self) - 2)
         mass = np.asarray(fracs, np.float64) * total
         idx = self.sum.find_prefixsum_idx(mass)
         p_min = self.min.v[1] / self.sum.v[1]

@@ -11,6 +11,8 @@ Recorded after every op: both trees, max_priority, and every sample's indices / 
 
   recbuf_per.npz  PrioritizedRecReplayBuffer, use_same_share_obs=True (the magym runner's setting)
   recbuf_uni.npz  RecReplayBuffer (uniform), use_same_share_obs=False
+  recbuf_per_edge.npz  PrioritizedRecReplayBuffer sampled while the last filled leaf holds mass
+                   (first insert fills leaves 0..len-1; sum(0, len - 1) leaves leaf len-1 out)
 
 Usage (from /root/repo):  python tests/golden/make_golden_recbuf.py
 """
@@ -53,7 +55,16 @@ def episodes(rng, n):
 FIELDS = ["obs", "share_obs", "acts", "rewards", "dones", "dones_env"]
 
 
-def run(rb_mod, prioritized, same_share, seed):
+SCRIPTS = {
+    "main": [("insert", 3), ("insert", 2), ("sample", 4, 0.4), ("update",), ("insert", 5), ("sample", 4, 0.55),
+             ("update",), ("insert", 4), ("sample", 5, 0.7), ("update",), ("insert", 1), ("insert", 1),
+             ("sample", 4, 0.85), ("update",), ("insert", 3), ("sample", 6, 1.0), ("update",), ("sample", 3, 0.9)],
+    "edge": [("insert", 5), ("sample", 4, 0.5), ("update",), ("sample", 4, 0.6), ("insert", 3), ("sample", 7, 0.7),
+             ("update",), ("insert", 6), ("sample", 11, 0.8)],
+}
+
+
+def run(rb_mod, prioritized, same_share, seed, script="main"):
     np.random.seed(seed)
     rng = np.random.default_rng(seed + 1)
     pinfo = {"policy_0": {"obs_space": Box(shape=(D,)), "share_obs_space": Box(shape=(S,)),
@@ -64,9 +75,7 @@ def run(rb_mod, prioritized, same_share, seed):
     else:
         buf = rb_mod.RecReplayBuffer(pinfo, pagents, SIZE, T, same_share, False)
     out, ops = {}, []
-    script = [("insert", 3), ("insert", 2), ("sample", 4, 0.4), ("update",), ("insert", 5), ("sample", 4, 0.55),
-              ("update",), ("insert", 4), ("sample", 5, 0.7), ("update",), ("insert", 1), ("insert", 1),
-              ("sample", 4, 0.85), ("update",), ("insert", 3), ("sample", 6, 1.0), ("update",), ("sample", 3, 0.9)]
+    script = SCRIPTS[script]
     last_idx = None
     for i, op in enumerate(script):
         p = f"op{i}_"
@@ -119,8 +128,9 @@ def run(rb_mod, prioritized, same_share, seed):
 
 def main():
     rb = load()
-    for name, pri, same in (("per", True, True), ("uni", False, False)):
-        out = run(rb, pri, same, seed=11 if pri else 12)
+    for name, pri, same, seed, script in (("per", True, True, 11, "main"), ("uni", False, False, 12, "main"),
+                                          ("per_edge", True, True, 13, "edge")):
+        out = run(rb, pri, same, seed=seed, script=script)
         np.savez_compressed(os.path.join(HERE, f"recbuf_{name}.npz"), **out)
         print(f"wrote recbuf_{name}.npz ({len(out['ops'])} ops)")
 

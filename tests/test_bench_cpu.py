@@ -41,8 +41,11 @@ def test_trainer_config_schedule_and_presets():
     q = qmix_reference()
     assert (q.alpha, q.beta, q.buffer_limit, q.max_epsilon, q.epsilon_anneal_episode) == (0.8, 0.2, 1000, 0.9, 60000)
     assert q.per_flavor == "qmix" and c.per_flavor == "vdn"
+    # env_name defaults: vdn Checkers-v0 (vdn/_config.py:19-24), qmix Switch2-v0 (qmix/_config.py:14-19)
+    assert c.env == "checkers" and q.env == "switch" and q.n_agents == 2
     p = presets()
     assert set(p) == {"cfg1", "cfg2", "cfg3", "cfg4", "cfg5"}
     assert p["cfg2"].q.n_envs == 4096 and p["cfg2"].q.n_agents == 8 and p["cfg2"].q.h == 64
+    assert p["cfg2"].q.env == "checkers" and p["cfg1"].q.env == "checkers"
     assert p["cfg4"].gpus == 8 and p["cfg3"].mappo.ppo_epoch == 15
     assert isinstance(p["cfg1"].q, QTrainConfig) and p["cfg1"].q.full_observable

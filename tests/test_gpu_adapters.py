@@ -107,6 +107,34 @@ def test_target_dqn_adapter_matches_reference(golden):
     _check_updates(rep, fx)
 
 
+def test_learner_adapter_rebinds(golden):
+    """A new target object or a changed optimizer lr rebuilds the adapter's learner over the same nets
+    (the old one releases them first; the Adam moments carry over); a second adapter over the same
+    behavior nets also binds."""
+    from minimarl.adapters import Mix_Net, Q_Net, Train_dqn
+    fx = golden("qmix_train")
+    N, D = fx["states"].shape[2:]
+    obs_sp, act_sp = [_Space((D,))] * N, [_Space(n=5)] * N
+    args = _args(fx)
+    bq, tq, tq2 = (Q_Net(obs_sp, act_sp, args) for _ in range(3))
+    bm, tm = Mix_Net(obs_sp, args), Mix_Net(obs_sp, args)
+    opt = torch.optim.Adam(params=[torch.zeros(1)], lr=1e-3)
+    tr = Train_dqn(args, DEV)
+    tr.train(FixtureReplay(fx), bq, bm, tq, tm, opt, 0.1)
+    L1 = tr._learner
+    m1 = L1.m.clone()
+    tr.train(FixtureReplay(fx), bq, bm, tq2, tm, opt, 0.1)          # new target net
+    assert tr._learner is not L1 and tr._learner.updates == 2
+    assert not torch.equal(tr._learner.m, m1)                       # moments continued, then stepped
+    opt.param_groups[0]["lr"] = 5e-4
+    tr.train(FixtureReplay(fx), bq, bm, tq2, tm, opt, 0.1)          # lr change
+    assert tr._learner.lr == 5e-4 and tr._learner.updates == 3
+    tr._learner.release()
+    Train_dqn(args, DEV).train(FixtureReplay(fx), bq, bm, tq2, tm, opt, 0.1)   # second adapter, same nets
+    q, _ = bq(torch.tensor(fx["states"][:, 0]), bq.init_hidden(32))
+    assert torch.isfinite(q).all()
+
+
 def test_mix_net_adapter_golden(golden):
     from minimarl.adapters import Mix_Net
     fx = golden("mixnet")

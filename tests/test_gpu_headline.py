@@ -229,6 +229,56 @@ def test_dual_forward_two_nets_obs_row_resets(E):
             assert 0.25 < expl.mean() < 0.35
 
 
+def test_cfg5_dual_forward_vs_oracle():
+    """bench.py's cfg5 dual forward exactly as timed (E = 8192, N = 27, D = 300, A = 36, F1 = 64,
+    GRU-32; net 0 MAX mode, net 1 ACT mode with epsilon 0.05, [E, N, D] obs, zero hidden states in the
+    [N, H, E] engine layout) vs the torch-CPU oracle: hiddens, max_a Q and Q(a) rtol 1e-5 (fp16x3
+    products), greedy actions = the oracle argmax except within 2e-5 of a tie, exploring rows = the
+    restated device RNG."""
+    from minimarl._lib import MM_Q_ACT, MM_Q_MAX, check, lib
+    from minimarl.qnet import AgentQNet, ptr, stream_handle
+    E, N, D, A, H = 8192, 27, 300, 36, 32
+    n5 = [AgentQNet(N, D, A, 64, 32, H, DEV, seed=s) for s in (1, 2)]
+    Ps = [{k: v.detach().cpu().clone() for k, v in n.params().items()} for n in n5]
+    for n in n5:
+        n.pack()
+    g = torch.Generator().manual_seed(5)
+    obs = [(torch.rand(E, N, D, generator=g) < 0.2).float() for _ in range(2)]
+    o_dev = [o.to(DEV) for o in obs]
+    h5 = [torch.zeros(N, H, E, device=DEV).permute(2, 0, 1) for _ in range(2)]
+    hq = [torch.empty(N, H, E, device=DEV).permute(2, 0, 1) for _ in range(2)]
+    qs = [torch.empty(E, N, device=DEV) for _ in range(2)]
+    act = torch.empty(E, N, dtype=torch.int32, device=DEV)
+    ios = []
+    for k, mode in enumerate((MM_Q_MAX, MM_Q_ACT)):
+        io = n5[k].make_io(o_dev[k], h5[k], hq[k], None, mode)
+        io.qsel_out = qs[k].data_ptr()
+        if mode == MM_Q_ACT:
+            io.act_out, io.epsilon = act.data_ptr(), 0.05
+            io.seed, io.counter = 77, 5
+        ios.append(io)
+    check(lib().mm_agent_q_fwd2(ctypes.byref(n5[0].dims), ptr(n5[0].packed), ctypes.byref(ios[0]), E,
+                                ptr(n5[1].packed), ctypes.byref(ios[1]), E, stream_handle(DEV)), "fwd2 cfg5")
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        for k in range(2):
+            qo, ho = nets.agent_forward(Ps[k], obs[k], torch.zeros(E, N, H))
+            np.testing.assert_allclose(hq[k].cpu().numpy(), ho.numpy(), rtol=1e-5, atol=2e-5)
+            qn = qo.numpy()
+            if k == 0:
+                np.testing.assert_allclose(qs[0].cpu().numpy(), qn.max(2), rtol=1e-5, atol=2e-5)
+                continue
+            a = act.cpu().numpy().astype(np.int64)
+            qa = np.take_along_axis(qn, a[..., None], 2)[..., 0]
+            np.testing.assert_allclose(qs[1].cpu().numpy(), qa, rtol=1e-5, atol=2e-5)
+            u, ra = eps_greedy_draws(77, 5, E, N, A)
+            expl = u <= np.float32(0.05)
+            np.testing.assert_array_equal(a[expl], ra[expl])
+            gap = qn.max(2) - qa
+            assert (gap[~expl] <= 2e-5).all(), gap[~expl].max()
+            assert 0.03 < expl.mean() < 0.07
+
+
 def _batch_from_store(eng, slots):
     """The reference-shaped batch (qmix/replay_buffer/per.py:36-77 sample outputs) of the sampled
     PER slots, read straight from the chunk store on the host: s_t = slot t of the row unless the

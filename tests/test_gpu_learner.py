@@ -175,6 +175,79 @@ def test_learner_cfg5_shapes_vs_oracle(mixer_fp16):
         _check_grads(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy(), grads["m." + key].numpy())
 
 
+@pytest.mark.parametrize("mixer_fp16", [False, True])
+def test_learner_cfg5_benched_path_vs_oracle(mixer_fp16):
+    """The cfg5 update exactly as bench.py times it (resident batch via load_batch, captured HIP graphs
+    replayed): 27 agents, obs 300, 36 actions, GRU-32 agents, Hm = 32 mixer over the 8100-wide state,
+    C = 10 and B = 512 chunk samples, so the large-batch kernels run: agent_split (row tiles of 32
+    samples), the chunk-sequence REC, the 8-samples-per-block mixer forward / backward (B >= 512) and,
+    with mixer_fp16, mixer_gi_f16 over 5120 rows per net.
+
+    Tolerances. fp32 mode: the file's fp32 bar (loss rtol 1e-4; gradients 2e-4 * max + 1e-3 * |g|;
+    post-Adam params atol 2e-6 where |g| > 1e-3 max). fp16 mode, derived from SURVEY 8c's separate
+    rtol 2e-3 on Q_tot: Q_tot, the loss and the TD errors rtol 2e-3; every gradient tensor
+    |g - g_ref| <= 5e-3 * max|g_ref| + 1e-2 * |g_ref| (gradients inherit the Q_tot error through
+    dQ_tot and the f16-rounded state operand of the mixer's W_ih gradient); post-Adam params atol 2e-6
+    where |g_ref| > 2e-2 * max|g_ref| (Adam's first step is lr * sign(g): only gradients well above the
+    error bar have a pinned sign)."""
+    from minimarl.learner import MIX_KEYS, Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    N, D, A, B, C = 27, 300, 36, 512, 10
+    beh = AgentQNet(N, D, A, 64, 32, 32, DEV, seed=11)
+    tgt = AgentQNet(N, D, A, 64, 32, 32, DEV, seed=12)
+    mix = Mixer(N, N * D, 32, 32, DEV, seed=13)
+    tmix = Mixer(N, N * D, 32, 32, DEV, seed=14)
+    P0 = {k: v.detach().cpu().clone() for k, v in beh.params().items()}
+    T0 = {k: v.detach().cpu().clone() for k, v in tgt.params().items()}
+    M0 = {k: mix.view(k).detach().cpu().clone() for k in MIX_KEYS}
+    TM0 = {k: tmix.view(k).detach().cpu().clone() for k in MIX_KEYS}
+    L = QLearner(beh, tgt, mix, tmix, batch=B, chunk=C, mode="qmix", device=DEV, mixer_fp16=mixer_fp16)
+    g = torch.Generator().manual_seed(3)
+    st = (torch.rand(B, C, N, D, generator=g) < 0.2).float()
+    ns = (torch.rand(B, C, N, D, generator=g) < 0.2).float()
+    act = torch.randint(0, A, (B, C, N), generator=g).float()
+    rew = torch.randn(B, C, N, generator=g) * 0.5
+    dn = (torch.rand(B, C, 1, generator=g) < 0.1).float()
+    w = torch.rand(B, 1, generator=g) * 0.5 + 0.5
+    L.load_batch(st, act, rew, ns, dn, w)
+    L.capture_update(None, None, None)          # bench.py's cfg5 line: resident batch, graph replay
+    L.replay_update()
+    torch.cuda.synchronize()
+    batch = (st, act, rew, ns, dn, w)
+    newP, newM, grads, loss, td = nets.qmix_train_step(P0, M0, T0, TM0, batch, 0.99, 1e-3, 5.0)
+    qtot_ref = nets.qmix_qtot(P0, M0, batch)
+    coef = min(1.0, 5.0 / (float(L.norm[0].item()) + 1e-6))
+    if mixer_fp16:
+        rt, ga, gr, psel = 2e-3, 5e-3, 1e-2, 2e-2
+        np.testing.assert_allclose(L.qtot.cpu().numpy(), qtot_ref.numpy(), rtol=rt,
+                                   atol=rt * float(qtot_ref.abs().max()))
+        np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=rt)
+        np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=rt, atol=rt * float(td.abs().max()))
+    else:
+        ga, gr, psel = 2e-4, 1e-3, 1e-3
+        np.testing.assert_allclose(L.qtot.cpu().numpy(), qtot_ref.numpy(), rtol=1e-4,
+                                   atol=1e-4 * float(qtot_ref.abs().max()))
+        np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=1e-4)
+        np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=1e-4, atol=1e-4)
+
+    def close(g_dev, g_ref, what):
+        scale = np.abs(g_ref).max()
+        np.testing.assert_array_less(np.abs(g_dev - g_ref), ga * scale + gr * np.abs(g_ref) + 1e-12, err_msg=what)
+
+    for key in nets.AGENT_KEYS:
+        g_ref = grads[key].numpy()
+        close(_grad_view(L, key).cpu().numpy() * coef, g_ref, key)
+        sel = np.abs(g_ref) > psel * np.abs(g_ref).max()
+        np.testing.assert_allclose(L.beh.view(key).cpu().numpy()[sel], newP[key].numpy()[sel], atol=2e-6,
+                                   err_msg=key)
+    for key in MIX_KEYS:
+        g_ref = grads["m." + key].numpy()
+        close(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy(), g_ref, "m." + key)
+        sel = np.abs(g_ref) > psel * np.abs(g_ref).max()
+        np.testing.assert_allclose(L.mix.view(key).cpu().numpy()[sel], newM[key].numpy()[sel], atol=2e-6,
+                                   err_msg="m." + key)
+
+
 def test_learner_update_from_device_per():
     """sample -> gather -> train -> priority update through the engine's PER and chunk store."""
     from minimarl.engine import RolloutEngine

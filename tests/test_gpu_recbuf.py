@@ -44,7 +44,7 @@ def tree_close(a, b, what):
     np.testing.assert_allclose(a[fin], b[fin], rtol=4e-7, atol=0, err_msg=what)
 
 
-@pytest.mark.parametrize("name", ["per", "uni"])
+@pytest.mark.parametrize("name", ["per", "uni", "per_edge"])
 def test_recbuf_replays_reference_sequence(name):
     z = np.load(os.path.join(GOLD, f"recbuf_{name}.npz"))
     SIZE, T, N, D, S, A, pri, same = [int(x) for x in z["meta"]]
@@ -172,14 +172,24 @@ def test_recbuf_feeds_offpolicy_trainer():
 
 
 def test_recbuf_gather_guards_bad_indices():
-    """Host indices outside the filled buffer raise (the reference's numpy IndexError); device indices
-    outside the ring gather zeros and set the error word instead of reading out of bounds."""
+    """Host indices follow numpy indexing of the reference's [.., buffer_size, ..] arrays: [len, size)
+    reads the never-written defaults (zeros, dones 1), negatives wrap, beyond the size raises IndexError;
+    device indices outside the ring gather zeros and set the error word instead of reading out of bounds."""
     SIZE, T, N, D, A = 16, 4, 2, 3, 3
     rng = np.random.default_rng(1)
     uni = make(False, SIZE, T, N, D, N * D, A)
-    uni.insert(5, *[{"policy_0": x} for x in _episodes(rng, 5, T, N, D, A)])
+    ep = _episodes(rng, 5, T, N, D, A)
+    uni.insert(5, *[{"policy_0": x} for x in ep])
     with pytest.raises(IndexError):
-        uni.sample(2, inds=np.array([0, 7]))
+        uni.sample(2, inds=np.array([0, SIZE]))
+    with pytest.raises(IndexError):
+        uni.sample(2, inds=np.array([-SIZE - 1, 0]))
+    got = uni.sample(3, inds=np.array([7, -12, 2]))      # -12 -> slot 4
+    obs = got[0]["policy_0"].cpu().numpy()               # [N, T+1, B, D]
+    assert np.all(obs[:, :, 0] == 0)
+    np.testing.assert_array_equal(obs[:, :, 1], ep[0][:, 4].transpose(1, 0, 2))
+    np.testing.assert_array_equal(obs[:, :, 2], ep[0][:, 2].transpose(1, 0, 2))
+    assert np.all(got[4]["policy_0"].cpu().numpy()[:, :, 0] == 1)   # dones default to True
     out = uni.sample(2, inds=torch.tensor([1, 99], device="cuda"))
     assert float(out[0]["policy_0"][:, :, 1].abs().sum()) == 0.0
     with pytest.raises(AssertionError, match="gather|outside the buffer"):

@@ -40,3 +40,130 @@ def test_switch_matches_oracle(N, full, clock, max_steps):
     np.testing.assert_array_equal(steps, ora.steps)
     if N == 2 and max_steps == 100:
         assert arrivals >= 2
+
+
+def _counter_of_step(t):
+    return 0x7FFFFFFFFFFFFFFF if t == 0 else t - 1
+
+
+@pytest.mark.parametrize("E,N", [(2048, 2), (256, 3)])
+def test_engine_on_switch_vs_oracle_through_eviction(E, N):
+    """RolloutEngine(env="switch") — the QMIX default env (qmix/_config.py:14-19) behind the same
+    chunk-store engine as the Checkers env: the fused switch + TD kernel, the dual forward on D = 3 obs
+    (fp16x3 kernel at E = 2048, exact f32 below), the PER insert past the point where it evicts. Per
+    chunk: stored s_0 / s'_t / actions / rewards / dones (= all(agent done), qmix/main.py:199,215)
+    bit-exact vs oracle/switch.py driven with the stored actions; exploring actions vs the restated
+    device RNG; greedy actions vs the torch-CPU oracle nets run along the whole trajectory (near-ties
+    within 2e-5 allowed); chunk TD priorities (cal_td_error summed over the chunk) rtol 1e-4; the PER
+    tree / slot -> row map vs SumTreeOracle fed the device priorities."""
+    from minimarl.engine import RolloutEngine
+    from oracle import nets
+    from oracle.rng import eps_greedy_draws
+    from oracle.sumtree import SumTreeOracle
+    C, H, eps, seed = 10, 32, 0.2, 99
+    cap = 4 * E
+    eng = RolloutEngine(E, N, f1=64, g=32, h=H, chunk=C, capacity=cap, seed=seed, env="switch", device="cuda")
+    assert eng.D == 3
+    P = {k: v.detach().cpu().clone() for k, v in eng.behavior.params().items()}
+    Pt = {k: v.detach().cpu().clone() for k, v in eng.target.params().items()}
+    ora = SwitchOracle(SwitchSpec(N, 100, -0.01, False, True), E)
+    tree = SumTreeOracle(cap, "qmix", 0.4, 0.4)
+    slot_row = eng.per.slot_rows().cpu().numpy().copy()
+    h = torch.zeros(E, N, H)
+    ht = torch.zeros(E, N, H)
+    keep = torch.ones(E, 1, 1)
+    near = 0
+    n_done = 0
+    for k in range(cap // E + 2):
+        rows = eng.staging.cpu().numpy().copy()
+        eng.run_graph(eps)
+        torch.cuda.synchronize()
+        O = eng.store.obs[rows].cpu().numpy()
+        A = eng.store.act[rows].cpu().numpy().astype(np.int64)
+        R = eng.store.rew[rows].cpu().numpy()
+        Dn = eng.store.done[rows].cpu().numpy().astype(bool)
+        td_dev = eng.chunk_td.cpu().numpy().copy()
+        np.testing.assert_array_equal(O[:, 0], ora.obs())
+        td = np.zeros(E)
+        with torch.no_grad():
+            for c in range(C):
+                t = k * C + c
+                s_t = torch.tensor(ora.obs())
+                q, h = nets.agent_forward(P, s_t, h * keep)
+                u, ra = eps_greedy_draws(seed, _counter_of_step(t), E, N, 5)
+                expl = u <= np.float32(eps)
+                np.testing.assert_array_equal(A[expl, c], ra[expl])
+                qn = q.numpy()
+                qa = np.take_along_axis(qn, A[:, c][..., None], 2)[..., 0]
+                gap = qn.max(2) - qa
+                assert (gap[~expl] <= 2e-5).all(), f"step {t}: greedy action off by {gap[~expl].max()}"
+                near += int((gap[~expl] > 0).sum())
+                o, r, ad, dn = ora.step(A[:, c])
+                np.testing.assert_array_equal(O[:, c + 1], o, err_msg=f"obs t={t}")
+                np.testing.assert_array_equal(R[:, c], r, err_msg=f"rew t={t}")
+                np.testing.assert_array_equal(Dn[:, c], dn, err_msg=f"done t={t}")
+                tq, ht = nets.agent_forward(Pt, torch.tensor(o), ht * keep)
+                td += np.abs(r.sum(1) + (1 - dn) * np.float32(0.99) * tq.max(2)[0].numpy().sum(1)
+                             - qa.sum(1)).astype(np.float64)
+                keep = torch.tensor(~dn, dtype=torch.float32).view(E, 1, 1)
+                n_done += int(dn.sum())
+                ora.reset_envs(dn)
+        np.testing.assert_allclose(td_dev, td, rtol=1e-4, atol=5e-4)
+        slots = np.asarray(tree.add_batch([float(x) for x in td_dev]), np.int64)
+        np.testing.assert_allclose(eng.per.tree().cpu().numpy(), tree.tree, rtol=1e-6, atol=1e-9)
+        new_staging = slot_row[slots].copy()
+        slot_row[slots] = rows
+        np.testing.assert_array_equal(eng.per.slot_rows().cpu().numpy(), slot_row)
+        np.testing.assert_array_equal(eng.staging.cpu().numpy(), new_staging)
+    assert tree.n_data == cap and n_done > 0          # episodes ended (time limit at t = 100) inside the run
+    assert near <= E // 8, near
+
+
+def test_switch_state_roundtrip():
+    from minimarl.env import SwitchVecEnv
+    E, N = 100, 3
+    a = SwitchVecEnv(E, N, max_steps=30)
+    a.reset()
+    rng = np.random.default_rng(2)
+    for _ in range(12):
+        a.step(torch.as_tensor(rng.integers(0, 5, (E, N)).astype(np.int32)).cuda(), autoreset=True)
+    ts, _ = a.checkpoint_tensors()
+    b = SwitchVecEnv(E, N, max_steps=30)
+    b.restore_tensors(ts)
+    act = torch.as_tensor(rng.integers(0, 5, (E, N)).astype(np.int32)).cuda()
+    for x, y in zip(a.step(act, autoreset=True), b.step(act, autoreset=True)):
+        assert torch.equal(x, y)
+
+
+def _switch_random_score(E=512, seed=0):
+    ora = SwitchOracle(SwitchSpec(2, 100, -0.01, False, True), E)
+    rng = np.random.default_rng(seed)
+    score, active = np.zeros(E), np.ones(E, bool)
+    for _ in range(100):
+        _, r, _, dn = ora.step(rng.integers(0, 5, (E, 2)))
+        score += active * r.sum(1)
+        active &= ~dn
+    return float(score.mean())
+
+
+def test_qmix_learns_switch2():
+    """QMIX exactly as the reference's qmix/main.py trains it — Train_dqn + Mix_Net (mode "qmix") on its
+    default env Switch2 (2 agents, partial obs D = 3 with the step clock), PER alpha 0.8 / beta 0.2 —
+    on 64 lockstep envs, with the textbook TD target sum r + gamma (1 - d) Q'_tot (reference_compat=
+    False: the reference's N * gamma = 1.98 bootstrap makes the Bellman operator an expansion).
+    The greedy test score rises far above the random policy's (both agents must cross the one-cell
+    corridor in turn for the +5 each)."""
+    from minimarl.config import QTrainConfig
+    from minimarl.train import QTrainer
+    cfg = QTrainConfig(algo="qmix", env="switch", n_envs=64, n_agents=2, full_observable=False, buffer_limit=4096,
+                       alpha=0.8, beta=0.2, use_step_weight=False, max_epsilon=1.0, min_epsilon=0.05,
+                       epsilon_anneal_episode=300, max_episodes=1200, update_target_interval=10, update_iter=10,
+                       batch_size=64, test_interval=50, test_envs=128, reference_compat=False, seed=5)
+    tr = QTrainer(cfg, device="cuda")
+    rand = _switch_random_score()
+    best = -1e9
+    for rec in tr.train(1200):
+        best = max(best, rec["test_score"])
+    hist = [(r["episode"], round(r["test_score"], 2)) for r in tr.history]
+    print("random", rand, "history", hist)
+    assert best > rand + 4.0, (rand, hist)

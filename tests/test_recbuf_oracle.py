@@ -39,7 +39,7 @@ def replay(z, check):
     return ora
 
 
-@pytest.mark.parametrize("name", ["per", "uni"])
+@pytest.mark.parametrize("name", ["per", "uni", "per_edge"])
 def test_recbuf_oracle_matches_reference(name):
     z = np.load(os.path.join(GOLD, f"recbuf_{name}.npz"))
 
