@@ -227,6 +227,10 @@ def main():
                     help="timed offpolicy episode-QMix updates on one GPU (0 = skip; single-GPU runs only)")
     ap.add_argument("--train-episodes", type=int, default=3,
                     help="timed episodes of the integrated QMIX train loop (0 = skip)")
+    ap.add_argument("--repeats", type=int, default=10,
+                    help="timed regions of exactly --steps steps each; ms_per_step is their median (min / max beside)")
+    ap.add_argument("--cfg1-episodes", type=int, default=20,
+                    help="timed training episodes of the cfg1 VDN trainer lines (0 = skip; single-GPU runs only)")
     ap.add_argument("--probe-ranks", action="store_true", help="launcher check: gloo rendezvous only, no GPU")
     args = ap.parse_args()
 
@@ -278,23 +282,28 @@ def main():
         eng.run_graph(args.epsilon)
     eng.capture_steps()
     assert len(eng.per) == cap
-    # warm-up and timed region: exactly W and K lockstep steps (chunk graphs + single-step graphs)
+    # warm-up, then R timed regions of exactly K lockstep steps each (chunk graphs + single-step graphs),
+    # each bracketed by barrier + synchronize and maxed over ranks; the median region is the result
     eng.run_steps(args.warmup, args.epsilon)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.run_steps(args.steps, args.epsilon)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    reps = []
+    for _ in range(max(1, args.repeats)):
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.run_steps(args.steps, args.epsilon)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        reps.append(el)
+    elapsed = float(np.median(reps))
     steps = args.steps
     value = steps * E * N * world / elapsed
 
@@ -389,6 +398,52 @@ def main():
                    "train_score": tr.train_score(), "grad_allreduce": (("gloo" if shared else "rccl") if dist else None)}
         del tr
         torch.cuda.empty_cache()
+
+    # cfg1 (BASELINE configs[0]): VDN, 2 agents, full obs (D = 94), GRU-32, the vdn/_config.py learner (B = 32
+    # chunks of 10, 10 updates per episode, PER 10000 chunks, alpha = beta = 0.4) and the logged run's test cadence
+    # (test_interval 10, test_episodes 20; vdn/logs/vdn-1710766189.log:30-31). Two shapes: 32 lockstep envs (the
+    # BASELINE config; one training iteration = 100 steps of all 32 envs + 10 updates) and ONE env, the
+    # reference's own runner shape (an iteration = one episode + 10 updates), whose episodes/s sits beside the
+    # reference's logged 2.43 episodes/s (vdn/logs/vdn-1710766189.log:41,16539: 15000 episodes in 6160 s on a
+    # desktop CPU) and warm-up 2968 agent-env-steps/s (wandb run tw6w4mqv output.log:36)
+    cfg1 = None
+    if args.cfg1_episodes > 0 and world == 1:
+        from minimarl.config import presets
+        from minimarl.train import QTrainer
+        cfg1 = {"workload": "VDN 2-agent gridworld (full obs D = 94), GRU-32, B = 32 x C = 10, 10 updates/episode, "
+                            "PER 10000 chunks, 20 greedy test episodes every 10 episodes",
+                "reference_cpu": {"episodes_per_s": 2.43, "warmup_agent_env_steps_per_s": 2968.0,
+                                  "source": "reference's own logged run on a desktop CPU (12 cores / 24 threads): "
+                                            "vdn/logs/vdn-1710766189.log:41,16539 (15000 episodes in 6160 s); "
+                                            "warm-up 148.4 chunks/s, vdn/wandb/run-20240318_214947-tw6w4mqv/files/"
+                                            "output.log:36"}}
+        for envs in (32, 1):
+            c1 = presets()["cfg1"].q
+            c1.n_envs, c1.test_interval, c1.test_envs, c1.seed = envs, 10, 20, 23
+            tr1 = QTrainer(c1, device=dev, track_score=True)
+            torch.cuda.synchronize()
+            tw = time.perf_counter()
+            tr1.warmup()                          # epsilon = 1 rollout until the replay holds 10000 chunks
+            torch.cuda.synchronize()
+            el_w = time.perf_counter() - tw
+            tr1.train(10)                         # captures the learner graphs, runs the first test
+            torch.cuda.synchronize()
+            t7 = time.perf_counter()
+            tr1.train(args.cfg1_episodes)
+            torch.cuda.synchronize()
+            el7 = time.perf_counter() - t7
+            k7 = args.cfg1_episodes
+            cfg1[f"envs_{envs}"] = {
+                "training_iterations_per_s": round(k7 / el7, 2), "env_episodes_per_s": round(k7 * envs / el7, 1),
+                "agent_env_steps_per_s_incl_learning": round(envs * 2 * c1.max_step * k7 / el7, 1),
+                "learner_updates_per_s": round(c1.update_iter * k7 / el7, 1), "ms_per_iteration": round(el7 / k7 * 1e3, 3),
+                "warmup_agent_env_steps_per_s": round(c1.buffer_limit * c1.chunk_size * 2 / el_w, 1),
+                "timed_iterations": k7, "test_score": tr1.history[-1]["test_score"] if tr1.history else None}
+            del tr1
+            torch.cuda.empty_cache()
+        r1 = cfg1["envs_1"]
+        cfg1["vs_reference_cpu"] = {"episodes_per_s (1 env)": round(r1["env_episodes_per_s"] / 2.43, 1),
+                                    "warmup agent-env-steps/s (1 env)": round(r1["warmup_agent_env_steps_per_s"] / 2968.0, 1)}
 
     # MAPPO (BASELINE configs[2]): 4096 envs x 8 agents per GPU, T=100 rollout steps with the fused
     # actor/critic kernel, device GAE, then 15 PPO epochs of chunked (L=5) BPTT on the whole buffer
@@ -566,6 +621,7 @@ def main():
         t5 = time_kernel(dual5)
         f5 = 2 * qnet_flops_per_agent_step(D5, 64, 32, H5, A5) * E5 * N5
         cfg5 = {"workload": "cfg5 dual agent forward (target + behavior), synthetic obs", "envs": E5, "agents": N5,
+                "parity_test": "tests/test_gpu_headline.py::test_cfg5_dual_forward_vs_oracle",
                 "obs_dim": D5, "n_actions": A5, "gru": H5, "dual_us": round(t5 * 1e6, 2),
                 "agent_steps_per_s": round(2 * E5 * N5 / t5, 1), "tflops_fp32_equiv": round(f5 / t5 / 1e12, 2)}
         # cfg5 QMIX update at the throughput batch: agent nets GRU-32, Hm = 32 mixer over the 8100-wide
@@ -592,6 +648,8 @@ def main():
         torch.cuda.synchronize()
         el5 = (time.perf_counter() - t6) / k5
         cfg5["learner"] = {"batch_chunks": B5, "chunk": C5, "mixer_state_projection": "fp16 MFMA (rtol 2e-3 on Q_tot)",
+                           "parity_test": "tests/test_gpu_learner.py::test_learner_cfg5_benched_path_vs_oracle (same "
+                                          "graphs at B = 512: Q_tot / loss / TD, every gradient, post-Adam params)",
                            "ms_per_update": round(el5 * 1e3, 3), "chunk_samples_per_s": round(B5 / el5, 1),
                            "loss_finite": bool(torch.isfinite(l5.loss).all().item())}
         del n5, o5, h5, hq, l5, m5
@@ -635,6 +693,8 @@ def main():
             "metric": "agent-env-steps/sec (4096 envs x 8 agents per GPU, QMIX GRU-64 rollout step)",
             "value": round(value, 1), "unit": "agent-env-steps/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
+            "repeats": len(reps), "ms_per_step_min": round(min(reps) / steps * 1e3, 4),
+            "ms_per_step_max": round(max(reps) / steps * 1e3, 4),
             "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 (agent forward: fp16x3-split MFMA emulating f32 products, f32 accumulate)",
             "data": "synthetic (build's gridworld, random init)",
@@ -652,6 +712,7 @@ def main():
                                               "the build container (BASELINE.md)",
                         "cpu_baseline": cpu_l, "throughput_batch": big},
             "train_loop": trainer,
+            "cfg1_vdn": cfg1,
             "mappo": mappo,
             "offpolicy_qmix": offq,
             "cfg5_forward": cfg5,

@@ -200,6 +200,12 @@ double mm_per_beta(const mm_per* per);
 int mm_env_step_rows(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
                      float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s);
 const float* mm_env_reset_obs(const mm_env* env); /* device [N, D]: the (deterministic) reset obs */
+/* The rollout engine's chunk-start step: mm_chunk_begin_rows + mm_env_step_rows in ONE launch. Store rows
+ * are row_stride floats, chunk_len + 1 obs slots of N*D floats. Slot 0 of row staging[e] <- slot chunk_len
+ * of row cur_row[e] (the previous chunk's last next obs), or the reset obs where cur_row[e] < 0; then the
+ * step: next obs into slot 1 of row staging[e], cur_row[e] <- staging[e] (or -1 where the env finished). */
+int mm_env_step_rows_begin(mm_env* env, const int32_t* act, float* store_obs, int64_t row_stride, int32_t chunk_len,
+                           const int64_t* staging, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s);
 /* mm_env_step_rows (auto-reset via cur_row, no obs_cur) fused with mm_td_chunk_step_rows of the
  * PREVIOUS step (td_* inputs, slot step_in_chunk of store rows td_rows): one launch instead of two
  * for every in-chunk step of the rollout engine (cal_td_error + chunk lists, vdn/_utils.py:44-52,
@@ -224,6 +230,14 @@ int mm_chunk_begin_rows(int64_t n_envs, int32_t nd, float* store_obs, int64_t ro
 /* PER insert with store-row indirection: slot_row[slot] <-> rows_inout[j] (the evicted row is handed
  * back as the next staging row; chunk data is never copied). */
 int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s);
+/* The chunk's last rollout step: mm_td_chunk_step_rows of the k envs (slot step_in_chunk of store rows
+ * rows_inout, before the swap) followed by mm_per_insert(per, chunk_td, k, rows_inout, slots_out). For the
+ * multi-block insert (power-of-two capacity >= 16384) the TD / store runs inside the insert's first launch
+ * (one launch fewer); results identical to the two separate calls. */
+int mm_per_insert_td(mm_per* per, int64_t k, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                     const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
+                     int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
+                     uint8_t* store_done, uint64_t* counter, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s);
 int64_t* mm_per_slot_rows(mm_per* per);             /* device int64 [cap] */
 int64_t mm_per_capacity(const mm_per* per);
 void mm_per_set_size(mm_per* per, int64_t n);      /* host + device fill count (synchronous) */
@@ -304,6 +318,19 @@ int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, 
 int mm_mixer_bwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                  const float* qa, const float* dq, const float* done, float* dhm, float* dqa, float* delta,
                  mm_stream_t s);
+/* Mixer weight gradients of R rows from the backward's delta [R][mm_mixer_delta_dim] and the forward's save
+ * [R][mm_mixer_save_dim]: every Mix_Net parameter's gradient written into dP (the mixer's flat gradient, MIX_KEYS
+ * order) by one batched outer-reduce launch + a fixed-order partial sum. States: rows gathered through s_off
+ * (reset_obs for -1), or contiguous [R][S] when s_off is NULL. partial: mm_mixer_wgrad_partial_count floats. */
+int64_t mm_mixer_wgrad_partial_count(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1);
+int mm_mixer_wgrad(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* state, const int64_t* s_off,
+                   const float* reset_obs, const float* save, const float* delta, float* dP, float* partial,
+                   int64_t partial_count, mm_stream_t s);
+/* VDN mixing (vdn/_train.py:23-47, 68-71): out[b] = sum_i q[b,i,act[b,i]], or sum_i max_a q[b,i,a] when act is
+ * NULL; q rows at b*q_se + i*q_sa (unit action stride). An action outside [0, A) adds 0 and sets bit 0 of *err
+ * (err may be NULL). */
+int mm_vdn_sum(int64_t B, int32_t N, int32_t A, const float* q, int64_t q_se, int64_t q_sa, const int32_t* act,
+               float* out, int32_t* err, mm_stream_t s);
 /* All C steps of the agent BPTT chain in one launch (small batches): step t's arrays at the step-0 pointers
  * + t x (B x N x width) (save, acts, dqa, dgi, dgh, dq); done of step t < C-1 at done + t*B, step C-1
  * uses ones; dh carries the hidden gradient (in: zero, out: grad wrt the chunk-start hidden).
@@ -433,6 +460,14 @@ int mm_mappo_bwd(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, mm_stream_t
 int64_t mm_mappo_grad_scratch_count(const mm_mappo_dims* d, int32_t L);
 int mm_mappo_grad(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, const float* h_actor, const float* h_critic,
                   float* grad_actor, float* grad_critic, float* scratch, mm_stream_t s);
+/* R_MAPPOPolicy.evaluate_actions (rmappo_policy.py:101-136; RNNLayer's masked segments, rnn.py:24-80; the
+ * Categorical head, distributions.py:55-68): a TRAIN-mode forward of both nets (a: T = L steps of EN chunks, rows
+ * t*EN + en, chunk-start hiddens at h_in slot 0, masks [T, EN], save buffers), then per row the value, the log-prob
+ * of act[row] and the entropy (ent_rows [T*EN]), and *entropy = the mean of ent_rows weighted by active [T*EN]
+ * (NULL: plain mean). H 32, A 5. An action outside [0, A) sets bit 0 of *err (may be NULL). */
+int mm_mappo_evaluate_actions(const mm_mappo_dims* d, const mm_mappo_fwd_args* a, const int32_t* act,
+                              const float* active, float* values, float* logp, float* ent_rows, float* entropy,
+                              int32_t* err, mm_stream_t s);
 int64_t mm_mappo_wgrad_partial_count(const mm_mappo_dims* d, int64_t rs);
 int mm_mappo_wgrad(const mm_mappo_dims* d, int32_t net, const float* gsoa, int64_t rs, float* grad, float* partial,
                    mm_stream_t s);
@@ -526,6 +561,9 @@ const float* mm_switch_reset_obs(const mm_switch* w); /* device [N, D]: the (det
  * chunk-store engine as the Checkers env. */
 int mm_switch_step_rows(mm_switch* w, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
                         float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s);
+int mm_switch_step_rows_begin(mm_switch* w, const int32_t* act, float* store_obs, int64_t row_stride,
+                              int32_t chunk_len, const int64_t* staging, int64_t* cur_row, float* rew, uint8_t* done,
+                              mm_stream_t s);
 int mm_switch_step_rows_td(mm_switch* w, const int32_t* act, float* next_obs, int64_t next_se,
                            const int64_t* next_row, int64_t* cur_row, float* rew, uint8_t* done, float gamma,
                            const float* td_rew, const uint8_t* td_done, const float* q_taken, const float* max_q_next,

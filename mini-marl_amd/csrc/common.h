@@ -148,6 +148,16 @@ struct TdFuse {
   int slot, C, on;
 };
 
+// Chunk start folded into the env kernels (mm_chunk_begin_rows, rollout.hip): slot 0 of the env's new
+// staging row <- slot src_off of its previous row (cur_row before this step), or the reset obs.
+struct BeginCopy {
+  float* store;           // chunk-store obs base
+  int64_t row_stride;     // floats per store row
+  int64_t src_off;        // C * N * D: the previous chunk's last next obs
+  const float* reset_obs; // [N * D]
+  int on;
+};
+
 }  // namespace mm
 
 #define MM_HIP_CHECK(expr)                                                     \

@@ -25,7 +25,6 @@ static constexpr int OBS_LOCAL = 47;
 struct EnvDev {
   int E, N, R, C, D, max_steps, full_obs, init_apples;
   int eb;  // envs per block of the step kernel
-  int dbg;  // debug: stop the step kernel after phase dbg (0 = full run)
   float step_cost, inv_r, inv_c;
   int32_t* pos;     // [E][N] r*256 + c
   int8_t* grid;     // [E][R*C] 0 empty, 1 lemon, 2 apple
@@ -113,12 +112,33 @@ static constexpr int WT = 64;     // lanes of the (env, agent) work: one wave
 #endif
 static constexpr int TB = MM_ENV_TB;  // threads per block: the extra waves only help stream the obs / state out
 
+// LDS layout of the step kernel (byte offsets, 16-byte aligned pieces), shared by the kernel and the host
+struct EnvSmem {
+  int sloc, srow, sbsrc, std3, spos, sact, sdm, sgrid, socc, total;
+};
+__host__ __device__ __forceinline__ int al16(int x) { return (x + 15) & ~15; }
+__host__ __device__ __forceinline__ EnvSmem env_smem(int EPW, int N, int RC) {
+  EnvSmem m;
+  int o = 0;
+  m.sloc = o;  o = al16(o + EPW * N * OBS_LOCAL * 4);   // [EPW][N][47] f32 obs tile
+  m.srow = o;  o = al16(o + EPW * 8);                   // [EPW] i64 destination rows
+  m.sbsrc = o; o = al16(o + EPW * 8);                   // [EPW] i64 chunk-begin source rows
+  m.std3 = o;  o = al16(o + 3 * EPW * N * 4);           // [3][EPW*N] fused TD inputs
+  m.spos = o;  o = al16(o + EPW * N * 4);               // [EPW*N] positions
+  m.sact = o;  o = al16(o + EPW * N * 4);               // [EPW*N] actions
+  m.sdm = o;   o = al16(o + 8);                         // termination mask (wave ballot)
+  m.sgrid = o; o = al16(o + EPW * RC);                  // [EPW][RC] grids
+  m.socc = o;  o = al16(o + EPW * RC);                  // [EPW][RC] occupancy
+  m.total = o;
+  return m;
+}
+
 __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32_t* __restrict__ act,
                                                            float* __restrict__ next_obs, int64_t next_se,
                                                            const int64_t* __restrict__ next_row,
                                                            float* __restrict__ obs_cur,
                                                            int64_t* __restrict__ cur_row, float* rew,  // rew may alias tdf.rew
-                                                           uint8_t* __restrict__ done_out, TdFuse tdf) {
+                                                           uint8_t* __restrict__ done_out, TdFuse tdf, BeginCopy bc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int RC = d.R * d.C;
   const int N = d.N;
@@ -127,14 +147,16 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
   const bool autoreset = obs_cur || cur_row;
   const int ND = N * d.D;
   const int LD = N * OBS_LOCAL;                                              // local tile per env
-  float* sloc = reinterpret_cast<float*>(smem);                              // [EPW][N][47]
-  int64_t* srow = reinterpret_cast<int64_t*>(sloc + EPW * LD);               // [EPW]
-  float* std3 = reinterpret_cast<float*>(srow + EPW);                        // [3][EPW*N] td inputs
-  int32_t* spos = reinterpret_cast<int32_t*>(std3 + 3 * EPW * N);            // [EPW*N]
-  int32_t* sact = spos + EPW * N;                                            // [EPW*N]
-  uint8_t* sdone = reinterpret_cast<uint8_t*>(sact + EPW * N);               // [EPW]
-  int8_t* sgrid = reinterpret_cast<int8_t*>(sdone + ((EPW + 15) & ~15));     // [EPW][RC]
-  uint8_t* socc = reinterpret_cast<uint8_t*>(sgrid + ((EPW * RC + 15) & ~15));  // [EPW][RC]
+  const EnvSmem lay = env_smem(EPW, N, RC);
+  float* sloc = reinterpret_cast<float*>(smem + lay.sloc);
+  int64_t* srow = reinterpret_cast<int64_t*>(smem + lay.srow);
+  int64_t* sbsrc = reinterpret_cast<int64_t*>(smem + lay.sbsrc);
+  float* std3 = reinterpret_cast<float*>(smem + lay.std3);
+  int32_t* spos = reinterpret_cast<int32_t*>(smem + lay.spos);
+  int32_t* sact = reinterpret_cast<int32_t*>(smem + lay.sact);
+  uint64_t* sdm = reinterpret_cast<uint64_t*>(smem + lay.sdm);
+  int8_t* sgrid = reinterpret_cast<int8_t*>(smem + lay.sgrid);
+  uint8_t* socc = reinterpret_cast<uint8_t*>(smem + lay.socc);
   const int e0 = blockIdx.x * EPW;
   const int ne = min(EPW, d.E - e0);
   const int nl = ne * N;                   // active (env, agent) lanes
@@ -166,13 +188,14 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
     }
   }
   int apples0 = 0, steps0 = 0;
-  int64_t srow_r = 0;
+  int64_t srow_r = 0, bsrc_r = -1;
   uint8_t tdone = 0;
   if (lane < ne) {
     srow_r = next_row ? next_row[e0 + lane] : (int64_t)(e0 + lane);
     apples0 = d.apples[e0 + lane];
     steps0 = d.steps[e0 + lane];
     if (tdf.on) tdone = tdf.done[e0 + lane];
+    if (bc.on) bsrc_r = cur_row[e0 + lane];     // read before this step overwrites it
   }
   for (int i = lane; i < ne * RC; i += TB) socc[i] = 0;
 #pragma unroll
@@ -192,9 +215,11 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
       tdf.s_rew[(trow * tdf.C + tdf.slot) * N + k_l] = trew;
     }
   }
-  if (lane < ne) srow[lane] = srow_r;
+  if (lane < ne) {
+    srow[lane] = srow_r;
+    sbsrc[lane] = bsrc_r;
+  }
   __syncthreads();
-  if (d.dbg == 1) return;
   // occupancy map of the starting positions (agent id + 1)
   if (lane < nl) socc[le_l * RC + (pos_r >> 8) * d.C + (pos_r & 255)] = (uint8_t)(k_l + 1);
   __syncthreads();
@@ -216,7 +241,6 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
     if (tdf.counter && blockIdx.x == 0 && lane == 0) *tdf.counter += 1;
   }
 
-  if (d.dbg == 2) return;
   // ---- phase 1: dynamics, one lane per env, agents in id order (oracle/env.py VecEnvOracle.step).
   // A move is blocked by the border or by the occupancy map (positions as updated so far this step),
   // so each agent costs two dependent LDS round trips (occupancy, then the fruit of its cell).
@@ -254,7 +278,9 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
       rew[(int64_t)e * N + k] = rk;
     }
     const bool dn = steps >= d.max_steps || apples == 0;
-    sdone[le] = dn ? 1 : 0;
+    // termination mask of the block's envs: one wave ballot (lanes < ne are wave 0's first lanes)
+    const uint64_t dm = __ballot(dn);
+    if (lane == 0) *sdm = dm;
     done_out[e] = dn ? 1 : 0;
     if (cur_row) cur_row[e] = dn ? -1 : srow_r;
     d.steps[e] = dn && autoreset ? 0 : steps;
@@ -266,7 +292,6 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
   const int ea = lane & (WT - 1), part = lane / WT;
   int mypos = 0;
   if (ea < nl) mypos = spos[ea];
-  if (d.dbg == 3) return;
   if (ea < nl) {
     const int le2 = ea / N, k2 = ea % N;
     float* o = sloc + le2 * LD + k2 * OBS_LOCAL;
@@ -302,8 +327,9 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
   }
   __syncthreads();
 
-  if (d.dbg == 4) return;
   // ---- phase 3: stream the obs out (env le's N*D run from its local tile) and write state back
+  const uint64_t dmask = *sdm;
+  auto env_done = [&](int le) { return ((dmask >> le) & 1ull) != 0; };
   const bool full = d.full_obs != 0;
   const float* robs = d.reset_obs;
   const bool vec = (ND & 3) == 0 && (next_se & 3) == 0 && ((uintptr_t)next_obs & 15) == 0 &&
@@ -331,7 +357,7 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
       }
       if (next_obs) *reinterpret_cast<float4*>(next_obs + srow[le] * next_se + r) = v;
       if (obs_cur) {
-        if (sdone[le]) v = *reinterpret_cast<const float4*>(robs + r);
+        if (env_done(le)) v = *reinterpret_cast<const float4*>(robs + r);
         *reinterpret_cast<float4*>(obs_cur + (int64_t)(e0 + le) * ND + r) = v;
       }
       r4 += TB;
@@ -345,32 +371,48 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
       const int le = i / ND, r = i - le * ND;
       const float v = sloc[le * LD + (full ? r % LD : r)];
       if (next_obs) next_obs[srow[le] * next_se + r] = v;
-      if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = sdone[le] ? robs[r] : v;
+      if (obs_cur) obs_cur[(int64_t)(e0 + le) * ND + r] = env_done(le) ? robs[r] : v;
     }
   }
-  if (d.dbg == 5) return;
+  if (bc.on) {
+    // chunk start (mm_chunk_begin_rows folded in): slot 0 of the new staging row <- slot C of the env's
+    // previous row (its last next obs), or the reset obs where the env had just reset
+    const bool bvec = (ND & 3) == 0 && (bc.row_stride & 3) == 0 && (bc.src_off & 3) == 0 &&
+                      ((uintptr_t)bc.store & 15) == 0 && ((uintptr_t)robs & 15) == 0;
+    if (bvec) {
+      const int ND4 = ND >> 2;
+      for (int i = lane; i < ne * ND4; i += TB) {
+        const int le = i / ND4, r = (i - le * ND4) * 4;
+        const int64_t src = sbsrc[le];
+        const float* sp = src >= 0 ? bc.store + src * bc.row_stride + bc.src_off : robs;
+        *reinterpret_cast<float4*>(bc.store + srow[le] * bc.row_stride + r) = *reinterpret_cast<const float4*>(sp + r);
+      }
+    } else {
+      for (int i = lane; i < ne * ND; i += TB) {
+        const int le = i / ND, r = i - le * ND;
+        const int64_t src = sbsrc[le];
+        bc.store[srow[le] * bc.row_stride + r] = src >= 0 ? bc.store[src * bc.row_stride + bc.src_off + r] : robs[r];
+      }
+    }
+  }
   if ((RC & 3) == 0) {
     uint32_t* g32 = reinterpret_cast<uint32_t*>(d.grid + (int64_t)e0 * RC);
     const uint32_t* ig32 = reinterpret_cast<const uint32_t*>(d.init_grid);
     const int RC4 = RC >> 2;
     for (int i = lane; i < ne * RC4; i += TB) {
       const int le = i / RC4;
-      g32[i] = (autoreset && sdone[le]) ? ig32[i - le * RC4] : reinterpret_cast<const uint32_t*>(sgrid)[i];
+      g32[i] = (autoreset && env_done(le)) ? ig32[i - le * RC4] : reinterpret_cast<const uint32_t*>(sgrid)[i];
     }
   } else {
     for (int i = lane; i < ne * RC; i += TB) {
       const int le = i / RC;
-      d.grid[(int64_t)e0 * RC + i] = (autoreset && sdone[le]) ? d.init_grid[i % RC] : sgrid[i];
+      d.grid[(int64_t)e0 * RC + i] = (autoreset && env_done(le)) ? d.init_grid[i % RC] : sgrid[i];
     }
   }
-  if (lane < nl) d.pos[(int64_t)e0 * N + lane] = (autoreset && sdone[le_l]) ? d.init_pos[k_l] : mypos;
+  if (lane < nl) d.pos[(int64_t)e0 * N + lane] = (autoreset && env_done(le_l)) ? d.init_pos[k_l] : mypos;
 }
 
-static size_t step_smem(const EnvDev& d) {
-  const size_t EPW = d.eb, RC = (size_t)d.R * d.C;
-  return EPW * d.N * OBS_LOCAL * 4 + EPW * 8 + 3 * EPW * d.N * 4 + 2 * EPW * d.N * 4 + ((EPW + 15) & ~15ull) +
-         ((EPW * RC + 15) & ~15ull) + EPW * RC;
-}
+static size_t step_smem(const EnvDev& d) { return (size_t)env_smem(d.eb, d.N, d.R * d.C).total; }
 
 int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out) {
   (void)seed;  // the layout is deterministic (ma_gym Checkers resets to a fixed layout)
@@ -382,8 +424,7 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   EnvDev d;
   d.E = (int)n_envs;
   d.N = cfg->n_agents;
-  d.dbg = getenv("MM_ENV_DBG") ? atoi(getenv("MM_ENV_DBG")) : 0;
-  d.eb = getenv("MM_ENV_EB") ? atoi(getenv("MM_ENV_EB")) : WT / d.N;
+  d.eb = WT / d.N;
   MM_REQUIRE(d.eb >= 1 && d.eb * d.N <= WT, "env_create: bad envs-per-block");
   d.R = 3 * ((d.N + 1) / 2);
   d.C = cols;
@@ -456,15 +497,19 @@ int env_reset(mm_env* env, float* obs, hipStream_t s) {
 }
 
 int env_step(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
-             float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, const TdFuse* tdf, hipStream_t s) {
+             float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, const TdFuse* tdf, hipStream_t s,
+             const BeginCopy* bcp = nullptr) {
   MM_REQUIRE(env && act && rew && done, "env_step: null argument");
   MM_REQUIRE(next_obs || obs_cur, "env_step: no obs output");
   const EnvDev& d = env->d;
   const int blocks = (d.E + d.eb - 1) / d.eb;
   TdFuse t{};
   if (tdf) t = *tdf;
+  BeginCopy bc{};
+  if (bcp) bc = *bcp;
+  MM_REQUIRE(!bc.on || (cur_row && next_row), "env_step: the chunk-begin copy needs cur_row and the staging rows");
   hipLaunchKernelGGL(env_step_wave_kernel, dim3(blocks), dim3(TB), step_smem(d), s, d, act, next_obs,
-                     next_se > 0 ? next_se : (int64_t)d.N * d.D, next_row, obs_cur, cur_row, rew, done, t);
+                     next_se > 0 ? next_se : (int64_t)d.N * d.D, next_row, obs_cur, cur_row, rew, done, t, bc);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -512,6 +557,15 @@ int mm_env_step_rows_td(mm_env* env, const int32_t* act, float* next_obs, int64_
   return mm::env_step(env, act, next_obs, next_se, next_row, nullptr, cur_row, rew, done, &t, (hipStream_t)s);
 }
 const float* mm_env_reset_obs(const mm_env* env) { return env ? env->d.reset_obs : nullptr; }
+int mm_env_step_rows_begin(mm_env* env, const int32_t* act, float* store_obs, int64_t row_stride, int32_t chunk_len,
+                           const int64_t* staging, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s) {
+  MM_REQUIRE(env && store_obs && staging && cur_row && chunk_len >= 1, "env_step_rows_begin: bad arguments");
+  const int64_t nd = (int64_t)env->d.N * env->d.D;
+  MM_REQUIRE(row_stride >= (chunk_len + 1) * nd, "env_step_rows_begin: row_stride < (chunk_len + 1) * N * D");
+  const mm::BeginCopy bc{store_obs, row_stride, chunk_len * nd, env->d.reset_obs, 1};
+  return mm::env_step(env, act, store_obs + nd, row_stride, staging, nullptr, cur_row, rew, done, nullptr,
+                      (hipStream_t)s, &bc);
+}
 int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples) {
   if (!env) return MM_EINVAL;
   const mm::EnvDev& d = env->d;

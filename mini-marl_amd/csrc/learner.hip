@@ -21,6 +21,12 @@
 
 namespace mm {
 
+// Element offset of state row i in the obs array: the gathered chunk-store offsets (-1: the env's reset
+// obs), or, without offsets (the torch ops' contiguous [rows, S] state), row i itself.
+__device__ __forceinline__ int64_t state_off(const int64_t* s_off, int64_t i, int S) {
+  return s_off ? s_off[i] : i * (int64_t)S;
+}
+
 // ------------------------------------------------------------------ gather
 // For sample b (PER slot -> chunk-store row) and step t:
 //   s_off[t][b]  = element offset of s_t in store.obs  (-1 => the env's reset obs)
@@ -169,7 +175,7 @@ __global__ __launch_bounds__(256) void mixer_gi_kernel(MixGiArgs a) {
   const int rb = blockIdx.y, col = blockIdx.x * 32 + i;
   const int row = rb * 32 + i;
   const float* W = nt.P + o.gWih + (int64_t)(row < M3 ? row : 0) * S;
-  const int64_t off = col < a.R ? nt.s_off[col] : -1;
+  const int64_t off = col < a.R ? state_off(nt.s_off, col, a.S) : -1;
   const float* x = off >= 0 ? a.obs + off : a.reset_obs;
   const int KD = (S + 31) / 32;
   f32x16 acc = {0};
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(256) void mixer_gi_tiled_kernel(MixGiArgs a) {
   for (int p = 0; p < 8; ++p) {
     const int rr = (threadIdx.x >> 5) + 8 * p;
     const int c = c0 + rr;
-    const int64_t off = c < a.R ? nt.s_off[c] : -1;
+    const int64_t off = c < a.R ? state_off(nt.s_off, c, a.S) : -1;
     xr[p] = c < a.R ? (off >= 0 ? a.obs + off : a.reset_obs) : nullptr;
     wr[p] = m0 + rr < M3 ? Wih + (int64_t)(m0 + rr) * S : nullptr;
   }
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(64 * 2 * RBK) void mixer_gi_f16_kernel(MixGiArgs a)
     const int idx = tid + j * NT;
     if (idx < 64 * KC) {
       const int p = idx / KC, x = idx % KC, c = min(c0 + p, a.R - 1);
-      const int64_t off = nt.s_off[c];
+      const int64_t off = state_off(nt.s_off, c, a.S);
       src[j] = (off >= 0 ? a.obs + off : a.reset_obs);
       dst[j] = p * PITCH + x;
       kk[j] = x;
@@ -360,7 +366,7 @@ __device__ __forceinline__ void mixer_fwd_body(const MixFwdArgs& a, const MixFwd
     for (int i = threadIdx.x; i < 3 * Hm; i += blockDim.x) gi[i] = nt.gi[(int64_t)b * 3 * Hm + i];
     __syncthreads();
   } else {
-    const int64_t off = nt.s_off[b];
+    const int64_t off = state_off(nt.s_off, b, a.S);
     const float* src = off >= 0 ? a.obs + off : a.reset_obs;
     for (int i = threadIdx.x; i < S; i += blockDim.x) xs[i] = src[i];
     __syncthreads();
@@ -2510,7 +2516,7 @@ int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const 
 int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
                 const float* P0, const int64_t* s_off0, float* gi0, const float* P1, const int64_t* s_off1, float* gi1,
                 mm_stream_t s) {
-  MM_REQUIRE(R > 0 && P0 && s_off0 && gi0 && obs && reset_obs, "mixer_gi: bad args");
+  MM_REQUIRE(R > 0 && P0 && gi0 && obs && (s_off0 || !P1), "mixer_gi: bad args");
   mm::MixGiArgs a;
   a.net[0] = {P0, s_off0, gi0};
   a.net[1] = {P1 ? P1 : P0, P1 ? s_off1 : s_off0, P1 ? gi1 : gi0};
@@ -2538,7 +2544,7 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
 int mm_mixer_gi_f16(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* obs, const float* reset_obs,
                     const float* P0, const int64_t* s_off0, float* gi0, const float* P1, const int64_t* s_off1,
                     float* gi1, mm_stream_t s) {
-  MM_REQUIRE(R > 0 && P0 && s_off0 && gi0 && obs && reset_obs, "mixer_gi_f16: bad args");
+  MM_REQUIRE(R > 0 && P0 && gi0 && obs && (s_off0 || !P1), "mixer_gi_f16: bad args");
   MM_REQUIRE(Hm == 32 || Hm == 64, "mixer_gi_f16: Hm must be 32 or 64");
   mm::MixGiArgs a;
   a.net[0] = {P0, s_off0, gi0};
@@ -2879,6 +2885,68 @@ int mm_outer_reduce_batch(const mm_outer_args* x, int32_t n_jobs, float* partial
   hipLaunchKernelGGL(mm::outer_sum_kernel, dim3(gx, n_jobs), dim3(256), 0, (hipStream_t)s, ob);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
+}
+
+// Mixer weight gradients of R = rows samples from the backward's per-row operands (mm_mixer_bwd /
+// mm_mixer_bwd_seq delta [R][mm_mixer_delta_dim], the forward's save [R][mm_mixer_save_dim]) and the
+// states (state rows through s_off with reset_obs for -1 offsets, or contiguous [R][S] rows when s_off
+// is NULL), as ONE batched outer-reduce launch + its fixed-order partial sum (deterministic):
+//   gWih/gbih <- d_gi x s,  gWhh/gbhh <- d_gh x h_in,  hypernets <- their deltas x h_out,
+//   b2 output layer <- dQ_tot x relu(b2 hidden)          (Mix_Net, qmix/_network.py:172-217)
+// dP: the mixer's flat gradient (overwritten).
+static int mixer_wgrad_jobs(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* state,
+                            const int64_t* s_off, const float* reset_obs, const float* save, const float* delta,
+                            float* dP, mm_outer_args* j) {
+  const mm::MixOff o = mm::mix_offsets(S, Hm, K1, N);
+  const int64_t MSD = mm::mix_save_dim(Hm, K1, N), MDD = mm::mix_delta_dim(Hm, K1, N);
+  const float* hm1 = save + 5 * Hm;
+  auto job = [&](int i, const float* U, const float* V, int64_t v_m, const int64_t* voff, int64_t w, int64_t b,
+                 int32_t rows, int32_t cols) {
+    mm_outer_args& a = j[i];
+    a.U = U;
+    a.u_g = 0;
+    a.u_m = MDD;
+    a.V = V;
+    a.v_g = 0;
+    a.v_m = v_m;
+    a.v_off = voff;
+    a.v_reset = voff ? reset_obs : nullptr;
+    a.dW = dP + w;
+    a.w_g = 0;
+    a.db = dP + b;
+    a.b_g = 0;
+    a.M = R;
+    a.R = rows;
+    a.Cc = cols;
+    a.accumulate = 0;
+    a.groups = 1;
+  };
+  job(0, delta, state, s_off ? 0 : S, s_off, o.gWih, o.gbih, 3 * Hm, S);
+  job(1, delta + 3 * Hm, save, MSD, nullptr, o.gWhh, o.gbhh, 3 * Hm, Hm);
+  job(2, delta + 6 * Hm, hm1, MSD, nullptr, o.w1W, o.w1b, N * K1, Hm);
+  job(3, delta + 6 * Hm + N * K1, hm1, MSD, nullptr, o.b1W, o.b1b, K1, Hm);
+  job(4, delta + 6 * Hm + N * K1 + K1, hm1, MSD, nullptr, o.w2W, o.w2b, K1, Hm);
+  job(5, delta + 6 * Hm + N * K1 + 2 * K1, hm1, MSD, nullptr, o.b2aW, o.b2ab, K1, Hm);
+  job(6, delta + 6 * Hm + N * K1 + 3 * K1, save + 6 * Hm + N * K1 + 2 * K1, MSD, nullptr, o.b2bW, o.b2bb, 1, K1);
+  return 7;
+}
+
+int64_t mm_mixer_wgrad_partial_count(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1) {
+  if (R < 1 || N < 1 || S < 1 || Hm < 1 || K1 < 1) return -1;
+  mm_outer_args j[7];
+  const float* f = reinterpret_cast<const float*>(16);
+  const int n = mixer_wgrad_jobs(R, N, S, Hm, K1, f, nullptr, nullptr, f, f, const_cast<float*>(f), j);
+  return mm_outer_reduce_batch_partial(j, n);
+}
+
+int mm_mixer_wgrad(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* state, const int64_t* s_off,
+                   const float* reset_obs, const float* save, const float* delta, float* dP, float* partial,
+                   int64_t partial_count, mm_stream_t s) {
+  MM_REQUIRE(R > 0 && state && save && delta && dP && partial, "mixer_wgrad: bad args");
+  MM_REQUIRE(!s_off || reset_obs, "mixer_wgrad: s_off needs reset_obs");
+  mm_outer_args j[7];
+  const int n = mixer_wgrad_jobs(R, N, S, Hm, K1, state, s_off, reset_obs, save, delta, dP, j);
+  return mm_outer_reduce_batch(j, n, partial, partial_count, s);
 }
 
 int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {

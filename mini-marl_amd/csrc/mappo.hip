@@ -675,6 +675,71 @@ struct MappoShape {
   }
 };
 
+// evaluate_actions epilogue (r_actor_critic.py:95-140, act.py:40-82, distributions.py:55-68) after a
+// TRAIN-mode forward: per row the critic value, the log-prob of the given action from the actor's
+// log-softmax save fields, and the Categorical entropy -sum_a p_a log p_a; then the masked mean of the
+// entropies over active_masks (or the plain mean) in one workgroup, fixed order (deterministic).
+template <int H, int A>
+__global__ __launch_bounds__(256) void mappo_eval_rows_kernel(const float* __restrict__ save0,
+                                                              const float* __restrict__ save1, int64_t rows,
+                                                              const int32_t* __restrict__ act,
+                                                              float* __restrict__ values, float* __restrict__ logp,
+                                                              float* __restrict__ ent_rows, int32_t* __restrict__ err) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  using S0 = SF<H, A>;
+  using S1 = SF<H, 1>;
+  const float* c0 = soa_col(save0, r, S0::NS);
+  float lp[A];
+  soa_ld<A>(c0, S0::OUT, lp);
+  float ent = 0.0f;
+#pragma unroll
+  for (int q = 0; q < A; ++q) ent -= expf(lp[q]) * lp[q];
+  const int a = act[r];
+  if ((a < 0 || a >= A) && err) atomicOr(err, 1);
+  float lpa = 0.0f;
+#pragma unroll
+  for (int q = 0; q < A; ++q)
+    if (q == a) lpa = lp[q];
+  values[r] = soa_ld1(soa_col(save1, r, S1::NS), S1::OUT);
+  logp[r] = lpa;
+  ent_rows[r] = ent;
+}
+
+__global__ __launch_bounds__(1024) void masked_mean_kernel(const float* __restrict__ x, const float* __restrict__ m,
+                                                           int64_t rows, float* __restrict__ out) {
+  __shared__ float sx[1024], sm[1024];
+  float ax = 0.f, am = 0.f;
+  for (int64_t r = threadIdx.x; r < rows; r += 1024) {
+    const float w = m ? m[r] : 1.0f;
+    ax += x[r] * w;
+    am += w;
+  }
+  sx[threadIdx.x] = ax;
+  sm[threadIdx.x] = am;
+  __syncthreads();
+  for (int st = 512; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) {
+      sx[threadIdx.x] += sx[threadIdx.x + st];
+      sm[threadIdx.x] += sm[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = sx[0] / sm[0];
+}
+
+template <int H, int A>
+static int mappo_eval_launch(const mm_mappo_fwd_args* a, const int32_t* act, const float* active, float* values,
+                             float* logp, float* ent_rows, float* entropy, int32_t* err, hipStream_t s) {
+  const int64_t rows = (int64_t)a->T * a->en;
+  hipLaunchKernelGGL((mappo_eval_rows_kernel<H, A>), dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s,
+                     a->net[0].save, a->net[1].save, rows, act, values, logp, ent_rows, err);
+  MM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(masked_mean_kernel, dim3(1), dim3(1024), 0, s, ent_rows, active, rows, entropy);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 #define MM_MAPPO_DISPATCH(d, CALL)                                                  \
   do {                                                                              \
     if ((d)->hidden == 32 && (d)->n_actions == 5 && (d)->obs_dim == 47) {           \
@@ -753,6 +818,17 @@ int mm_mappo_bwd(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, mm_stream_t
                  a->active && a->act && a->adv && a->old_logp && a->old_value && a->returns && a->stats,
              "mappo_bwd: null pointer");
   MM_MAPPO_DISPATCH(d, SH::bwd(a, (hipStream_t)s));
+}
+
+int mm_mappo_evaluate_actions(const mm_mappo_dims* d, const mm_mappo_fwd_args* a, const int32_t* act,
+                              const float* active, float* values, float* logp, float* ent_rows, float* entropy,
+                              int32_t* err, mm_stream_t s) {
+  MM_REQUIRE(d && a && act && values && logp && ent_rows && entropy, "mappo_evaluate_actions: null argument");
+  MM_REQUIRE(a->mode == MM_MAPPO_TRAIN, "mappo_evaluate_actions: TRAIN-mode forward arguments required");
+  MM_REQUIRE(d->hidden == 32 && d->n_actions == 5, "mappo_evaluate_actions: H 32, A 5");
+  const int rc = mm_mappo_fwd(d, a, s);
+  if (rc) return rc;
+  return mm::mappo_eval_launch<32, 5>(a, act, active, values, logp, ent_rows, entropy, err, (hipStream_t)s);
 }
 
 int64_t mm_mappo_wgrad_partial_count(const mm_mappo_dims* d, int64_t rs) {

@@ -209,7 +209,7 @@ constexpr int FAST_MAX_CAND = 4096;   // keys sharing the threshold's 16-bit top
 template <int VPT>
 __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
                                                           const float* td, int64_t K, double eps,
-                                                          int64_t* rows_inout, int64_t* slots_out, int dbg) {
+                                                          int64_t* rows_inout, int64_t* slots_out) {
   __shared__ uint32_t binsum[256];
   __shared__ uint32_t wsum[PT / 64];
   __shared__ int32_t victims[FAST_MAX_VICTIMS];
@@ -238,10 +238,6 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
       if ((i & 15) == 14) asm volatile("" ::: "memory");  // bound the loads in flight (VGPRs)
     }
     auto top16 = [&](int i) -> uint32_t { return (kp[i >> 1] >> ((i & 1) * 16)) & 0xffffu; };
-    if (dbg == 1) {
-      if (top16(0) == 0x1234 && top16(VPT - 1) == 0x4321) st->n_samples = 7;
-      return;
-    }
     const double* lv = leaves + s0;
     auto full = [&](int i) -> uint64_t { return (uint64_t)__double_as_longlong(lv[i]); };
     auto valid = [&](int i) -> bool { return s0 + i < n_data; };
@@ -352,7 +348,6 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
       s_need = need;
     }
     __syncthreads();
-    if (dbg == 2) return;
     const uint64_t T = s_prefix;
     const uint32_t T16 = (uint32_t)(T >> 48);
     asm volatile("" : "+v"(lv));
@@ -390,7 +385,6 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
     }
     __syncthreads();
   }
-  if (dbg == 3) return;
   // priorities, slot assignment, row swap
   for (int64_t j = t; j < K; j += PT) {
     const int64_t slot = j < free_n ? n_data + j : (int64_t)victims[j - free_n];
@@ -403,7 +397,6 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
     }
   }
   __syncthreads();
-  if (dbg == 4) return;
   // rebuild: register subtree of the thread's VPT leaves, then the PT-leaf top tree in LDS
   double v[VPT / 2];
   int64_t lvl_nodes = cap >> 1;  // nodes on the current level (first: the leaves' parents)
@@ -599,31 +592,33 @@ __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t ca
 
 // ---------------------------------------------------------------- multi-block batched insert
 // For large power-of-two capacities the single-workgroup insert is bound by one CU's memory
-// bandwidth over the whole tree. This path spreads every pass over cap/1024 workgroups
-// (seven stream-ordered launches, graph-capturable, same results as per_add_fast_kernel):
-//   1 hist1     12-bit histogram (sign + exponent) of the candidate keys, LDS then global
-//   2 hist2     every block finds the threshold's bin b1 from hist1, then histograms bits 51..40
-//               of the keys in b1
-//   3 cand      every block finds b2; keys with the 24-bit prefix (b1, b2) are appended to a list
-//   4 count     every block radix-selects the exact key T among the listed keys (LDS, 8-bit digits
-//               over bits 39..0) and counts its slots' keys < T and == T
-//   5 victims   slot-ordered compaction: block prefix of the counts + in-block scans
-//   6 write     priorities (td+eps)^alpha into free slots / victims, row swaps
-//   7 rebuild   1024-leaf subtrees in LDS per block; the last block (arrival ticket) builds the
-//               top levels, updates n_data and clears the histograms for the next insert
+// bandwidth over the whole tree. This path spreads every pass over G = cap/1024 workgroups in FOUR
+// stream-ordered launches (graph-capturable, same results as per_add_fast_kernel); each pass's grid-wide
+// reduction is finished by its last-arriving workgroup (arrival ticket, no spinning):
+//   A sel1    [the chunk's last rollout TD / store, folded in: td_chunk_kernel's arithmetic]
+//             12-bit histogram (sign + exponent) of the candidate keys; the last block picks the
+//             threshold's bin b1
+//   B sel2    histogram of bits 51..40 of the keys in b1; the last block picks b2
+//   C sel3    keys with the 24-bit prefix (b1, b2) listed with their slots, per-block counts of the
+//             keys below the prefix; the last block radix-selects the exact key T among the listed
+//             keys (8-bit digits over bits 39..0) and turns the counts into per-block victim offsets
+//   D apply   every block writes its own victims / free slots ((td + eps)^alpha, row swaps), rebuilds
+//             its 1024-leaf subtree from LDS; the last block builds the top levels, updates n_data and
+//             clears the scratch for the next insert
 constexpr int MB_T = 256, MB_VPT = 4, MB_SLOTS = MB_T * MB_VPT;   // 1024 slots per block
 constexpr int64_t MB_MIN_CAP = 16384;
 constexpr int MB_CAND_LDS = 4096;
+constexpr int MB_MAX_BLOCKS = 1024;
 struct MbScratch {
   uint32_t hist1[4096];
   uint32_t hist2[4096];
-  uint32_t blk[2 * 1024];    // per block: (#key < T, #key == T)
+  uint32_t blk[2 * MB_MAX_BLOCKS];   // C: per block #keys below the 24-bit prefix; then victim offsets
   uint32_t cand_n;
   uint32_t ticket;
-  uint64_t tsel[2];          // (T, number of slots equal to T that are taken)
-  uint64_t cand[1];          // [cap] (reused as int64 victims after the select)
+  uint64_t sel[4];                    // b1 | (b1, b2) prefix, remaining rank, T, take_eq
+  uint64_t cand[1];                   // [2 cap] the listed (key, slot) pairs: keys at cand, slots at cand + cap
 };
-static size_t mb_bytes(int64_t cap) { return sizeof(MbScratch) + (size_t)cap * 8; }
+static size_t mb_bytes(int64_t cap) { return sizeof(MbScratch) + (size_t)cap * 16; }
 
 __device__ __forceinline__ uint64_t leaf_key(const double* leaves, int64_t s) {
   return (uint64_t)__double_as_longlong(leaves[s]);
@@ -652,13 +647,14 @@ __device__ __forceinline__ uint32_t mb_scan(uint32_t v, uint32_t* wsum, uint32_t
   return before + incl - v;
 }
 
-// Find the bin holding the need-th key of a 4096-bin histogram: returns bin, updates need to the
-// rank inside it. Every thread gets the result.
-__device__ __forceinline__ int mb_pick(const uint32_t* __restrict__ h, int64_t& need, uint32_t* wsum, int64_t* sh) {
+// Find the bin holding the need-th key of a 4096-bin global histogram written by other workgroups'
+// atomics (read through L2 with device-scope atomic loads): returns bin, updates need to the rank inside
+// it. Every thread gets the result.
+__device__ __forceinline__ int mb_pick(uint32_t* h, int64_t& need, uint32_t* wsum, int64_t* sh) {
   uint32_t loc[16], sum = 0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    loc[i] = h[threadIdx.x * 16 + i];
+    loc[i] = __hip_atomic_load(&h[threadIdx.x * 16 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sum += loc[i];
   }
   uint32_t tot;
@@ -682,11 +678,68 @@ __device__ __forceinline__ int mb_pick(const uint32_t* __restrict__ h, int64_t& 
   return bin;
 }
 
-__global__ __launch_bounds__(MB_T) void per_mb_hist1(const double* __restrict__ tree, int64_t cap, const PerDev* st,
-                                                     int64_t K, MbScratch* mb) {
+// arrival ticket of a pass: true in the workgroup that finishes last (its earlier writes and every other
+// workgroup's are then visible to it at device scope)
+__device__ __forceinline__ bool mb_last(uint32_t* ticket, uint32_t* s_last) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) *s_last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  const bool last = *s_last != 0;
+  if (last) __threadfence();
+  return last;
+}
+
+// The chunk's last TD / store step (td_chunk_kernel, rollout.hip; cal_td_error + the chunk lists,
+// vdn/_utils.py:44-52, vdn/main.py:140-167): thread per (env, agent), agent-order sums per env.
+__device__ void mb_td_fold(const TdFuse& t, int64_t E, int N, float (*sh)[MB_T]) {
+  const int epb = MB_T / N;
+  const int le = threadIdx.x / N, k = threadIdx.x % N;
+  if (t.counter && blockIdx.x == 0 && threadIdx.x == 0) *t.counter += 1;   // RNG stream of the next step
+  for (int64_t g0 = blockIdx.x; g0 * epb < E; g0 += gridDim.x) {
+    const int64_t e = g0 * epb + le;
+    const bool on = le < epb && e < E;
+    float r = 0.f, q = 0.f, m = 0.f;
+    if (on) {
+      const int64_t o = e * N + k;
+      const int64_t row = t.rows[e];
+      r = t.rew[o];
+      q = t.q_taken[o];
+      m = t.maxq[o];
+      t.s_act[(row * t.C + t.slot) * N + k] = (uint8_t)t.act[o];
+      t.s_rew[(row * t.C + t.slot) * N + k] = r;
+      if (k == 0) t.s_done[row * t.C + t.slot] = t.done[e];
+    }
+    sh[0][threadIdx.x] = r;
+    sh[1][threadIdx.x] = q;
+    sh[2][threadIdx.x] = m;
+    __syncthreads();
+    if (on && k == 0) {
+      float sr = 0.f, sq = 0.f, sm = 0.f;
+      for (int j = 0; j < N; ++j) {
+        sr += sh[0][threadIdx.x + j];
+        sq += sh[1][threadIdx.x + j];
+        sm += sh[2][threadIdx.x + j];
+      }
+      const float d = t.done[e] ? 1.0f : 0.0f;
+      const float td = fabsf(sr + (1.0f - d) * t.gamma * sm - sq);
+      t.chunk_td[e] = (t.slot == 0 ? 0.0f : t.chunk_td[e]) + td;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_sel1(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+                                                    int64_t K, MbScratch* mb, TdFuse tdf, int32_t td_n) {
   __shared__ uint32_t h[4096];
+  __shared__ uint32_t wsum[MB_T / 64];
+  __shared__ int64_t sh[2];
+  __shared__ uint32_t s_last;
+  __shared__ float shtd[3][MB_T];
+  if (tdf.on) mb_td_fold(tdf, K, td_n, shtd);
   const int64_t n_data = st->n_data;
-  if (K - min(K, cap - n_data) <= 0) return;
+  int64_t need = K - min(K, cap - n_data);
+  if (need <= 0) return;
   const double* leaves = tree + (cap - 1);
   for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
   __syncthreads();
@@ -699,17 +752,25 @@ __global__ __launch_bounds__(MB_T) void per_mb_hist1(const double* __restrict__ 
   __syncthreads();
   for (int i = threadIdx.x; i < 4096; i += MB_T)
     if (h[i]) atomicAdd(&mb->hist1[i], h[i]);
+  if (!mb_last(&mb->ticket, &s_last)) return;
+  const int b1 = mb_pick(mb->hist1, need, wsum, sh);
+  if (threadIdx.x == 0) {
+    mb->sel[0] = (uint64_t)b1;
+    mb->sel[1] = (uint64_t)need;
+    mb->ticket = 0;
+  }
 }
 
-__global__ __launch_bounds__(MB_T) void per_mb_hist2(const double* __restrict__ tree, int64_t cap, const PerDev* st,
-                                                     int64_t K, MbScratch* mb) {
+__global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+                                                    int64_t K, MbScratch* mb) {
   __shared__ uint32_t h[4096];
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
+  __shared__ uint32_t s_last;
   const int64_t n_data = st->n_data;
-  int64_t need = K - min(K, cap - n_data);
-  if (need <= 0) return;
-  const int b1 = mb_pick(mb->hist1, need, wsum, sh);
+  if (K - min(K, cap - n_data) <= 0) return;
+  const uint64_t b1 = mb->sel[0];
+  int64_t need = (int64_t)mb->sel[1];
   const double* leaves = tree + (cap - 1);
   for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
   __syncthreads();
@@ -719,60 +780,70 @@ __global__ __launch_bounds__(MB_T) void per_mb_hist2(const double* __restrict__ 
     const int64_t sl = base + threadIdx.x + i * MB_T;
     if (sl < n_data) {
       const uint64_t k = leaf_key(leaves, sl);
-      if ((int)(k >> 52) == b1) atomicAdd(&h[(k >> 40) & 4095], 1u);
+      if ((k >> 52) == b1) atomicAdd(&h[(k >> 40) & 4095], 1u);
     }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 4096; i += MB_T)
     if (h[i]) atomicAdd(&mb->hist2[i], h[i]);
+  if (!mb_last(&mb->ticket, &s_last)) return;
+  const int b2 = mb_pick(mb->hist2, need, wsum, sh);
+  if (threadIdx.x == 0) {
+    mb->sel[0] = (b1 << 12) | (uint64_t)b2;   // the 24-bit prefix
+    mb->sel[1] = (uint64_t)need;
+    mb->ticket = 0;
+  }
 }
 
-__global__ __launch_bounds__(MB_T) void per_mb_cand(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+__global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ tree, int64_t cap, const PerDev* st,
                                                     int64_t K, MbScratch* mb) {
+  __shared__ uint64_t cl[MB_CAND_LDS];
+  __shared__ uint32_t bins[256];
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
+  __shared__ uint32_t s_last;
+  __shared__ uint32_t cnt[2 * MB_MAX_BLOCKS];
   const int64_t n_data = st->n_data;
-  int64_t need = K - min(K, cap - n_data);
-  if (need <= 0) return;
-  const uint64_t b1 = (uint64_t)mb_pick(mb->hist1, need, wsum, sh);
-  const uint64_t b2 = (uint64_t)mb_pick(mb->hist2, need, wsum, sh);
-  const uint64_t pre = (b1 << 12) | b2;
+  if (K - min(K, cap - n_data) <= 0) return;
+  const uint64_t pre = mb->sel[0];
   const double* leaves = tree + (cap - 1);
+  uint64_t* ckey = mb->cand;
+  uint64_t* cslot = mb->cand + cap;
   const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+  uint32_t below = 0;
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = base + threadIdx.x + i * MB_T;
     if (sl < n_data) {
       const uint64_t k = leaf_key(leaves, sl);
-      if ((k >> 40) == pre) mb->cand[atomicAdd(&mb->cand_n, 1u)] = k;
+      const uint64_t kp = k >> 40;
+      below += kp < pre ? 1u : 0u;
+      if (kp == pre) {
+        const uint32_t at = atomicAdd(&mb->cand_n, 1u);
+        ckey[at] = k;
+        cslot[at] = (uint64_t)sl;
+      }
     }
   }
-}
-
-__global__ __launch_bounds__(MB_T) void per_mb_count(const double* __restrict__ tree, int64_t cap, const PerDev* st,
-                                                     int64_t K, MbScratch* mb, uint64_t* Tout) {
-  __shared__ uint64_t cl[MB_CAND_LDS];
-  __shared__ uint32_t bins[256];
-  __shared__ uint32_t wsum[MB_T / 64];
-  __shared__ int64_t sh[2];
-  const int64_t n_data = st->n_data;
-  int64_t need = K - min(K, cap - n_data);
-  if (need <= 0) return;
-  const uint64_t b1 = (uint64_t)mb_pick(mb->hist1, need, wsum, sh);
-  const uint64_t b2 = (uint64_t)mb_pick(mb->hist2, need, wsum, sh);
-  uint64_t prefix = ((b1 << 12) | b2) << 40;
-  const uint32_t m = mb->cand_n;
+  uint32_t tb;
+  (void)mb_scan(below, wsum, &tb);
+  if (threadIdx.x == 0) mb->blk[blockIdx.x] = tb;
+  if (!mb_last(&mb->ticket, &s_last)) return;
+  // ---- last block: exact key T among the listed keys (radix select over bits 39..0)
+  int64_t need = (int64_t)mb->sel[1];
+  const uint32_t m = __hip_atomic_load(&mb->cand_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool in_lds = m <= (uint32_t)MB_CAND_LDS;
   if (in_lds)
-    for (uint32_t i = threadIdx.x; i < m; i += MB_T) cl[i] = mb->cand[i];
+    for (uint32_t i = threadIdx.x; i < m; i += MB_T)
+      cl[i] = __hip_atomic_load(&ckey[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  const uint64_t* cs = in_lds ? cl : mb->cand;
+  uint64_t prefix = pre << 40;
   for (int shift = 32; shift >= 0; shift -= 8) {
     for (int i = threadIdx.x; i < 256; i += MB_T) bins[i] = 0;
     __syncthreads();
     const uint64_t hmask = ~0ull << (shift + 8);
     for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
-      const uint64_t k = cs[i];
+      const uint64_t k = in_lds ? cl[i] : __hip_atomic_load(&ckey[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((k & hmask) == prefix) atomicAdd(&bins[(k >> shift) & 255], 1u);
     }
     __syncthreads();
@@ -788,102 +859,129 @@ __global__ __launch_bounds__(MB_T) void per_mb_count(const double* __restrict__ 
     need = sh[1];
     __syncthreads();
   }
-  const uint64_t T = prefix;   // the rest-th smallest key; take the first `need` slots equal to it
-  const double* leaves = tree + (cap - 1);
-  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS + threadIdx.x * MB_VPT;
-  uint32_t lt = 0, eq = 0;
+  const uint64_t T = prefix;   // the rest-th smallest key; the first `need` slots equal to it are taken
+  // per block: lt = keys below the prefix + listed keys < T, eq = listed keys == T
+  const int G = (int)gridDim.x;
+  for (int b = threadIdx.x; b < G; b += MB_T) {
+    cnt[2 * b] = __hip_atomic_load(&mb->blk[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cnt[2 * b + 1] = 0;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
+    const uint64_t k = in_lds ? cl[i] : __hip_atomic_load(&ckey[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int b = (int)(__hip_atomic_load(&cslot[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / MB_SLOTS);
+    if (k < T) atomicAdd(&cnt[2 * b], 1u);
+    else if (k == T) atomicAdd(&cnt[2 * b + 1], 1u);
+  }
+  __syncthreads();
+  // exclusive prefix over blocks (G <= 1024: four entries per thread)
+  uint32_t lt4[4], eq4[4], slt = 0, seq = 0;
 #pragma unroll
-  for (int i = 0; i < MB_VPT; ++i) {
-    const int64_t sl = base + i;
-    if (sl < n_data) {
-      const uint64_t k = leaf_key(leaves, sl);
+  for (int q = 0; q < 4; ++q) {
+    const int b = threadIdx.x * 4 + q;
+    lt4[q] = b < G ? cnt[2 * b] : 0u;
+    eq4[q] = b < G ? cnt[2 * b + 1] : 0u;
+    slt += lt4[q];
+    seq += eq4[q];
+  }
+  uint32_t tot;
+  uint32_t blt = mb_scan(slt, wsum, &tot);
+  uint32_t beq = mb_scan(seq, wsum, &tot);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int b = threadIdx.x * 4 + q;
+    if (b < G) {
+      mb->blk[b] = blt;
+      mb->blk[MB_MAX_BLOCKS + b] = beq;
+    }
+    blt += lt4[q];
+    beq += eq4[q];
+  }
+  if (threadIdx.x == 0) {
+    mb->sel[2] = T;
+    mb->sel[3] = (uint64_t)need;
+    mb->ticket = 0;
+  }
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
+                                                     const float* td, int64_t K, double eps, int64_t* rows_inout,
+                                                     int64_t* slots_out, MbScratch* mb) {
+  __shared__ double lv[MB_SLOTS];
+  __shared__ double v[2][MB_SLOTS / 2];
+  __shared__ uint32_t wsum[MB_T / 64];
+  __shared__ uint32_t s_last;
+  const int L = 63 - __clzll((unsigned long long)cap);      // leaves at level L
+  const int64_t n_data = st->n_data;
+  const double alpha = st->alpha;
+  const int64_t free_n = min(K, cap - n_data);
+  const bool evict = K - free_n > 0;
+  double* leaves = tree + (cap - 1);
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+  // this block's 1024 leaves: 4 contiguous per thread (keys for the victim test, LDS copy for the rebuild)
+  const int64_t s0 = base + threadIdx.x * MB_VPT;
+  double x[MB_VPT];
+  {
+    const double2 a = *reinterpret_cast<const double2*>(leaves + s0);
+    const double2 b = *reinterpret_cast<const double2*>(leaves + s0 + 2);
+    x[0] = a.x;
+    x[1] = a.y;
+    x[2] = b.x;
+    x[3] = b.y;
+  }
+  uint32_t lt = 0, eq = 0;
+  uint64_t T = 0;
+  if (evict) {
+    T = mb->sel[2];
+#pragma unroll
+    for (int i = 0; i < MB_VPT; ++i) {
+      const uint64_t k = s0 + i < n_data ? (uint64_t)__double_as_longlong(x[i]) : ~0ull;
       lt += k < T ? 1u : 0u;
       eq += k == T ? 1u : 0u;
     }
   }
-  uint32_t tlt, teq;
-  (void)mb_scan(lt, wsum, &tlt);
-  (void)mb_scan(eq, wsum, &teq);
-  if (threadIdx.x == 0) {
-    mb->blk[2 * blockIdx.x] = tlt;
-    mb->blk[2 * blockIdx.x + 1] = teq;
-    if (blockIdx.x == 0) {
-      Tout[0] = T;
-      Tout[1] = (uint64_t)need;
-    }
-  }
-}
-
-__global__ __launch_bounds__(MB_T) void per_mb_victims(const double* __restrict__ tree, int64_t cap, const PerDev* st,
-                                                       int64_t K, MbScratch* mb, const uint64_t* Tin) {
-  __shared__ uint32_t wsum[MB_T / 64];
-  const int64_t n_data = st->n_data;
-  if (K - min(K, cap - n_data) <= 0) return;
-  const uint64_t T = Tin[0];
-  const int64_t take_eq = (int64_t)Tin[1];
-  int64_t lt_before = 0, eq_before = 0;
-  for (unsigned b = 0; b < blockIdx.x; ++b) {
-    lt_before += mb->blk[2 * b];
-    eq_before += mb->blk[2 * b + 1];
-  }
-  const double* leaves = tree + (cap - 1);
-  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS + threadIdx.x * MB_VPT;
-  uint64_t k[MB_VPT];
-  uint32_t lt = 0, eq = 0;
-#pragma unroll
-  for (int i = 0; i < MB_VPT; ++i) {
-    k[i] = base + i < n_data ? leaf_key(leaves, base + i) : ~0ull;
-    lt += k[i] < T ? 1u : 0u;
-    eq += k[i] == T ? 1u : 0u;
-  }
   uint32_t tot;
-  int64_t lt_rank = lt_before + mb_scan(lt, wsum, &tot);
-  int64_t eq_rank = eq_before + mb_scan(eq, wsum, &tot);
-  int64_t* victims = reinterpret_cast<int64_t*>(mb->cand);
+  int64_t lt_rank = mb_scan(lt, wsum, &tot);
+  int64_t eq_rank = mb_scan(eq, wsum, &tot);
+  if (evict) {
+    lt_rank += mb->blk[blockIdx.x];
+    eq_rank += mb->blk[MB_MAX_BLOCKS + blockIdx.x];
+  }
+  const int64_t take_eq = evict ? (int64_t)mb->sel[3] : 0;
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
-    if (k[i] < T) {
-      victims[lt_rank + min(eq_rank, take_eq)] = base + i;
-      ++lt_rank;
-    } else if (k[i] == T) {
-      if (eq_rank < take_eq) victims[lt_rank + eq_rank] = base + i;
-      ++eq_rank;
+    const int64_t sl = s0 + i;
+    int64_t j = -1;
+    if (sl >= n_data && sl < n_data + free_n) {
+      j = sl - n_data;                                   // a free slot, filled in order
+    } else if (evict && sl < n_data) {
+      const uint64_t k = (uint64_t)__double_as_longlong(x[i]);
+      if (k < T) {
+        j = free_n + lt_rank + min(eq_rank, take_eq);    // victims in ascending slot order
+        ++lt_rank;
+      } else if (k == T) {
+        if (eq_rank < take_eq) j = free_n + lt_rank + eq_rank;
+        ++eq_rank;
+      }
     }
+    if (j >= 0) {
+      x[i] = pow((double)td[j] + eps, alpha);
+      leaves[sl] = x[i];
+      if (slots_out) slots_out[j] = sl;
+      if (rows_inout) {
+        const int64_t old = slot_row[sl];
+        slot_row[sl] = rows_inout[j];
+        rows_inout[j] = old;
+      }
+    }
+    lv[threadIdx.x * MB_VPT + i] = x[i];
   }
-}
-
-__global__ __launch_bounds__(MB_T) void per_mb_write(double* tree, int64_t* slot_row, int64_t cap, const PerDev* st,
-                                                     const float* td, int64_t K, double eps, int64_t* rows_inout,
-                                                     int64_t* slots_out, const MbScratch* mb) {
-  const int64_t j = (int64_t)blockIdx.x * MB_T + threadIdx.x;
-  if (j >= K) return;
-  const int64_t n_data = st->n_data;
-  const int64_t free_n = min(K, cap - n_data);
-  const int64_t* victims = reinterpret_cast<const int64_t*>(mb->cand);
-  const int64_t slot = j < free_n ? n_data + j : victims[j - free_n];
-  tree[cap - 1 + slot] = pow((double)td[j] + eps, st->alpha);
-  if (slots_out) slots_out[j] = slot;
-  if (rows_inout) {
-    const int64_t old = slot_row[slot];
-    slot_row[slot] = rows_inout[j];
-    rows_inout[j] = old;
-  }
-}
-
-__global__ __launch_bounds__(MB_T) void per_mb_rebuild(double* tree, int64_t cap, PerDev* st, int64_t K,
-                                                       MbScratch* mb) {
-  __shared__ double v[2][MB_SLOTS / 2];
-  __shared__ uint32_t s_last;
-  const int L = 63 - __clzll((unsigned long long)cap);      // leaves at level L
-  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
-  const double* leaves = tree + (cap - 1);
-  // levels L-1 .. L-10: node i of level l at heap index 2^l - 1 + i; this block owns i in
-  // [blockIdx * n, (blockIdx + 1) * n) with n = 2^(l - (L - 10)); LDS ping-pong between levels
+  __syncthreads();
+  // levels L-1 .. L-10 of this block's subtree from the LDS leaves (pairwise f64 sums = rebuild_tree)
   {
     const int64_t o = ((int64_t)1 << (L - 1)) - 1 + (int64_t)blockIdx.x * (MB_SLOTS / 2);
     for (int i = threadIdx.x; i < MB_SLOTS / 2; i += MB_T) {
-      const double2 x = *reinterpret_cast<const double2*>(leaves + base + 2 * i);
-      v[0][i] = x.x + x.y;
+      v[0][i] = lv[2 * i] + lv[2 * i + 1];
       tree[o + i] = v[0][i];
     }
   }
@@ -892,43 +990,39 @@ __global__ __launch_bounds__(MB_T) void per_mb_rebuild(double* tree, int64_t cap
   for (int n = MB_SLOTS / 4, l = L - 2; n >= 1; n >>= 1, --l) {
     const int64_t o = ((int64_t)1 << l) - 1 + (int64_t)blockIdx.x * n;
     for (int i = threadIdx.x; i < n; i += MB_T) {
-      const double x = v[cur][2 * i] + v[cur][2 * i + 1];
-      v[cur ^ 1][i] = x;
-      tree[o + i] = x;
+      const double y = v[cur][2 * i] + v[cur][2 * i + 1];
+      v[cur ^ 1][i] = y;
+      tree[o + i] = y;
     }
     cur ^= 1;
     __syncthreads();
   }
-  // arrival ticket: the last block builds the levels above the per-block roots
-  __threadfence();
-  if (threadIdx.x == 0) s_last = atomicAdd(&mb->ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
+  if (!mb_last(&mb->ticket, &s_last)) return;
+  // the last block: the levels above the per-block roots
   const int G = gridDim.x, lg = L - 10;                     // G = 2^lg roots at level lg (G <= 1024)
-  double* w = &v[0][0];
+  double* w = &lv[0];
   for (int i = threadIdx.x; i < G; i += MB_T)
     w[i] = __hip_atomic_load(&tree[((int64_t)1 << lg) - 1 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   for (int n = G / 2, l = lg - 1; n >= 1; n >>= 1, --l) {
-    double x[4];
+    double y[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = threadIdx.x + q * MB_T;
-      x[q] = i < n ? w[2 * i] + w[2 * i + 1] : 0.0;
+      y[q] = i < n ? w[2 * i] + w[2 * i + 1] : 0.0;
     }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = threadIdx.x + q * MB_T;
       if (i < n) {
-        w[i] = x[q];
-        tree[((int64_t)1 << l) - 1 + i] = x[q];
+        w[i] = y[q];
+        tree[((int64_t)1 << l) - 1 + i] = y[q];
       }
     }
     __syncthreads();
   }
-  // next insert starts from clear histograms / list / ticket
+  // the next insert starts from clear histograms / list / ticket
   for (int i = threadIdx.x; i < 4096; i += MB_T) {
     mb->hist1[i] = 0;
     mb->hist2[i] = 0;
@@ -936,24 +1030,22 @@ __global__ __launch_bounds__(MB_T) void per_mb_rebuild(double* tree, int64_t cap
   if (threadIdx.x == 0) {
     mb->cand_n = 0;
     mb->ticket = 0;
-    st->n_data = min(cap, st->n_data + K);
+    st->n_data = min(cap, n_data + K);
   }
 }
 
 static int per_insert_mb(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out,
-                         hipStream_t s) {
+                         const TdFuse* tdf, int32_t td_n, hipStream_t s) {
   const int64_t cap = per->cap;
   const int G = (int)(cap / MB_SLOTS);
   MbScratch* mb = static_cast<MbScratch*>(per->mb);
-  uint64_t* tsel = mb->tsel;
-  hipLaunchKernelGGL(per_mb_hist1, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
-  hipLaunchKernelGGL(per_mb_hist2, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
-  hipLaunchKernelGGL(per_mb_cand, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
-  hipLaunchKernelGGL(per_mb_count, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, tsel);
-  hipLaunchKernelGGL(per_mb_victims, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, tsel);
-  hipLaunchKernelGGL(per_mb_write, dim3((int)((k + MB_T - 1) / MB_T)), dim3(MB_T), 0, s, per->tree, per->slot_row,
-                     cap, per->st, td, k, per->eps, rows_inout, slots_out, mb);
-  hipLaunchKernelGGL(per_mb_rebuild, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
+  TdFuse t{};
+  if (tdf) t = *tdf;
+  hipLaunchKernelGGL(per_mb_sel1, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, t, td_n);
+  hipLaunchKernelGGL(per_mb_sel2, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
+  hipLaunchKernelGGL(per_mb_sel3, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
+  hipLaunchKernelGGL(per_mb_apply, dim3(G), dim3(MB_T), 0, s, per->tree, per->slot_row, cap, per->st, td, k,
+                     per->eps, rows_inout, slots_out, mb);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -1027,23 +1119,31 @@ static int64_t* per_scratch(mm_per* p) {
   return reinterpret_cast<int64_t*>(static_cast<char*>(p->alloc) + tree_b + row_b);
 }
 
-int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s) {
+static int per_insert_impl(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out,
+                           const mm::TdFuse* tdf, int32_t td_n, hipStream_t s) {
   MM_REQUIRE(per && (td || k == 0), "per_add: null argument");
   MM_REQUIRE(k >= 0 && k <= per->cap, "per_add: batch %lld larger than capacity", (long long)k);
   if (k == 0) return MM_OK;
   const int64_t cap = per->cap;
   const bool pow2 = (cap & (cap - 1)) == 0;
   const int64_t vpt = cap / mm::PT;
-  static const int dbg = getenv("MM_PER_DBG") ? atoi(getenv("MM_PER_DBG")) : 0;  // debug timing
-  static const bool single_wg = getenv("MM_PER_SINGLE") && atoi(getenv("MM_PER_SINGLE"));  // A/B
-  if (per->mb && !single_wg) {
-    const int rc = mm::per_insert_mb(per, td, k, rows_inout, slots_out, (hipStream_t)s);
+  if (per->mb) {
+    const int rc = mm::per_insert_mb(per, td, k, rows_inout, slots_out, tdf, td_n, s);
     if (rc) return rc;
-  } else if (pow2 && cap >= 2 * mm::PT && vpt <= 64 && k <= mm::FAST_MAX_VICTIMS) {
+    per->n_data = std::min(per->cap, per->n_data + k);
+    return MM_OK;
+  }
+  if (tdf) {   // the other insert paths run the chunk's last TD / store as its own launch first
+    const int rc = mm_td_chunk_step_rows(k, td_n, tdf->gamma, tdf->rew, tdf->done, tdf->q_taken, tdf->maxq, tdf->act,
+                                         tdf->chunk_td, tdf->slot, tdf->C, tdf->s_act, tdf->s_rew, tdf->s_done,
+                                         tdf->rows, tdf->counter, (mm_stream_t)s);
+    if (rc) return rc;
+  }
+  if (pow2 && cap >= 2 * mm::PT && vpt <= 64 && k <= mm::FAST_MAX_VICTIMS) {
 #define MM_PER_FAST(V)                                                                                        \
   case V:                                                                                                     \
-    hipLaunchKernelGGL(mm::per_add_fast_kernel<V>, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree,      \
-                       per->slot_row, cap, per->st, td, k, per->eps, rows_inout, slots_out, dbg);            \
+    hipLaunchKernelGGL(mm::per_add_fast_kernel<V>, dim3(1), dim3(mm::PT), 0, s, per->tree, per->slot_row, cap, \
+                       per->st, td, k, per->eps, rows_inout, slots_out);                                      \
     break;
     switch (vpt) {
       MM_PER_FAST(2)
@@ -1055,12 +1155,29 @@ int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, 
     }
 #undef MM_PER_FAST
   } else {
-    hipLaunchKernelGGL(mm::per_add_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->slot_row, cap,
-                       per->st, td, k, per->eps, rows_inout, slots_out, per_scratch(per));
+    hipLaunchKernelGGL(mm::per_add_kernel, dim3(1), dim3(mm::PT), 0, s, per->tree, per->slot_row, cap, per->st, td, k,
+                       per->eps, rows_inout, slots_out, per_scratch(per));
   }
   MM_HIP_CHECK(hipGetLastError());
   per->n_data = std::min(per->cap, per->n_data + k);
   return MM_OK;
+}
+
+int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s) {
+  return per_insert_impl(per, td, k, rows_inout, slots_out, nullptr, 0, (hipStream_t)s);
+}
+
+int mm_per_insert_td(mm_per* per, int64_t k, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                     const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,
+                     int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act, float* store_rew,
+                     uint8_t* store_done, uint64_t* counter, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s) {
+  MM_REQUIRE(rew && done && q_taken && max_q_next && act && chunk_td && store_act && store_rew && store_done &&
+                 rows_inout, "per_insert_td: null argument");
+  MM_REQUIRE(step_in_chunk >= 0 && step_in_chunk < chunk_len, "per_insert_td: bad step");
+  MM_REQUIRE(n_agents >= 1 && n_agents <= 256, "per_insert_td: n_agents must be in [1,256]");
+  const mm::TdFuse t{rew, done, q_taken, max_q_next, act, chunk_td, store_act, store_rew, store_done, rows_inout,
+                     counter, gamma, step_in_chunk, chunk_len, 1};
+  return per_insert_impl(per, chunk_td, k, rows_inout, slots_out, &t, n_agents, (hipStream_t)s);
 }
 
 int mm_per_add_batch(mm_per* per, const float* td, int64_t k, int64_t* slots_out, mm_stream_t s) {

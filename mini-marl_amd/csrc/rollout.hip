@@ -141,6 +141,32 @@ __global__ __launch_bounds__(256) void chunk_score_kernel(int E, int C, int N, c
   }
 }
 
+// VDN mixing of one step (vdn/_train.py:23-47: q.gather(2, action).squeeze().sum(1); the target side
+// max(2)[0].sum(1), vdn/_train.py:68-71): out[b] = sum_i q[b, i, act[b, i]] (or max_a q[b, i, a] when act
+// is NULL), agents summed in id order. One thread per row; q rows at b * q_se + i * q_sa.
+__global__ __launch_bounds__(256) void vdn_sum_kernel(int64_t B, int N, int A, const float* __restrict__ q, int64_t q_se,
+                                                      int64_t q_sa, const int32_t* __restrict__ act,
+                                                      float* __restrict__ out, int32_t* __restrict__ err) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  float acc = 0.f;
+  for (int i = 0; i < N; ++i) {
+    const float* qr = q + b * q_se + (int64_t)i * q_sa;
+    float v;
+    if (act) {
+      const int a = act[b * N + i];
+      const bool ok = a >= 0 && a < A;
+      if (!ok && err) atomicOr(err, 1);
+      v = ok ? qr[a] : 0.f;
+    } else {
+      v = qr[0];
+      for (int a = 1; a < A; ++a) v = fmaxf(v, qr[a]);
+    }
+    acc += v;
+  }
+  out[b] = acc;
+}
+
 }  // namespace mm
 
 extern "C" {
@@ -215,6 +241,16 @@ int mm_chunk_begin(int64_t n_envs, int32_t nd, const float* obs_cur, float* stor
   const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 8192);
   hipLaunchKernelGGL(mm::chunk_begin_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)s, (int)n_envs, nd,
                      obs_cur, store_obs, row_stride, rows);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_vdn_sum(int64_t B, int32_t N, int32_t A, const float* q, int64_t q_se, int64_t q_sa, const int32_t* act,
+               float* out, int32_t* err, mm_stream_t s) {
+  MM_REQUIRE(q && out && N >= 1 && A >= 1 && B >= 0, "vdn_sum: bad args");
+  if (B == 0) return MM_OK;
+  hipLaunchKernelGGL(mm::vdn_sum_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)s, B, N, A, q,
+                     q_se, q_sa, act, out, err);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void switch_step_kernel(SwitchTab tab, SwitchS
                                                           int64_t next_se, const int64_t* __restrict__ next_row,
                                                           float* __restrict__ obs_cur, int64_t* __restrict__ cur_row,
                                                           float* rew, uint8_t* __restrict__ agent_done,
-                                                          uint8_t* __restrict__ done_out, TdFuse tdf) {
+                                                          uint8_t* __restrict__ done_out, TdFuse tdf, BeginCopy bc) {
   const int64_t gl = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t e = gl / NP;
   const int k = (int)(gl % NP);
@@ -128,6 +128,7 @@ __global__ __launch_bounds__(256) void switch_step_kernel(SwitchTab tab, SwitchS
     }
   }
   const int64_t srow = env_ok ? (next_row ? next_row[e] : e) : 0;
+  const int64_t bsrc = (bc.on && env_ok) ? cur_row[e] : -1;   // read before lane 0 overwrites it below
   int a[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) a[j] = __shfl(a_own, base + (j < NP ? j : 0));
@@ -203,6 +204,11 @@ __global__ __launch_bounds__(256) void switch_step_kernel(SwitchTab tab, SwitchS
   // ---- outputs
   const int ld = 2 + clock;
   const int D = full ? ld * N : ld;
+  if (bc.on && ag) {   // chunk start (mm_chunk_begin_rows folded in): this agent's D floats of slot 0
+    const float* sp = bsrc >= 0 ? bc.store + bsrc * bc.row_stride + bc.src_off : bc.reset_obs;
+    float* dp = bc.store + srow * bc.row_stride;
+    for (int f = 0; f < D; ++f) dp[k * D + f] = sp[k * D + f];
+  }
   if (ag) {
     rew[e * N + k] = reached ? 5.0f : step_cost;
     if (agent_done) agent_done[e * N + k] = my_done ? 1 : 0;
@@ -253,22 +259,25 @@ struct mm_switch {
 namespace mm {
 static int switch_step(mm_switch* w, const int32_t* act, float* next_obs, int64_t next_se, const int64_t* next_row,
                        float* obs_cur, int64_t* cur_row, float* rew, uint8_t* agent_done, uint8_t* done,
-                       const TdFuse* tdf, hipStream_t s) {
+                       const TdFuse* tdf, hipStream_t s, const BeginCopy* bcp = nullptr) {
   MM_REQUIRE(w && act && rew && done, "switch_step: bad arguments");
   MM_REQUIRE(next_obs || obs_cur, "switch_step: no obs output");
   const mm_switch_cfg& c = w->cfg;
   const int D = (2 + c.clock) * (c.full_observable ? c.n_agents : 1);
   TdFuse t{};
   if (tdf) t = *tdf;
+  BeginCopy bc{};
+  if (bcp) bc = *bcp;
+  MM_REQUIRE(!bc.on || (cur_row && next_row), "switch_step: the chunk-begin copy needs cur_row and the staging rows");
   const int64_t se = next_se > 0 ? next_se : (int64_t)c.n_agents * D;
   if (c.n_agents == 2) {
     hipLaunchKernelGGL(switch_step_kernel<2>, dim3((w->E * 2 + 255) / 256), dim3(256), 0, s, w->tab, w->st, w->E,
                        c.n_agents, c.max_steps, c.full_observable, c.clock, c.step_cost, act, next_obs, se, next_row,
-                       obs_cur, cur_row, rew, agent_done, done, t);
+                       obs_cur, cur_row, rew, agent_done, done, t, bc);
   } else {
     hipLaunchKernelGGL(switch_step_kernel<4>, dim3((w->E * 4 + 255) / 256), dim3(256), 0, s, w->tab, w->st, w->E,
                        c.n_agents, c.max_steps, c.full_observable, c.clock, c.step_cost, act, next_obs, se, next_row,
-                       obs_cur, cur_row, rew, agent_done, done, t);
+                       obs_cur, cur_row, rew, agent_done, done, t, bc);
   }
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
@@ -341,6 +350,17 @@ int mm_switch_step_rows(mm_switch* w, const int32_t* act, float* next_obs, int64
                         float* obs_cur, int64_t* cur_row, float* rew, uint8_t* done, mm_stream_t s) {
   return mm::switch_step(w, act, next_obs, next_se, next_row, obs_cur, cur_row, rew, nullptr, done, nullptr,
                          (hipStream_t)s);
+}
+
+int mm_switch_step_rows_begin(mm_switch* w, const int32_t* act, float* store_obs, int64_t row_stride,
+                              int32_t chunk_len, const int64_t* staging, int64_t* cur_row, float* rew, uint8_t* done,
+                              mm_stream_t s) {
+  MM_REQUIRE(w && store_obs && staging && cur_row && chunk_len >= 1, "switch_step_rows_begin: bad arguments");
+  const int64_t nd = (int64_t)w->cfg.n_agents * mm_switch_obs_dim(w);
+  MM_REQUIRE(row_stride >= (chunk_len + 1) * nd, "switch_step_rows_begin: row_stride < (chunk_len + 1) * N * D");
+  const mm::BeginCopy bc{store_obs, row_stride, chunk_len * nd, w->reset_obs, 1};
+  return mm::switch_step(w, act, store_obs + nd, row_stride, staging, nullptr, cur_row, rew, nullptr, done, nullptr,
+                         (hipStream_t)s, &bc);
 }
 
 int mm_switch_step_rows_td(mm_switch* w, const int32_t* act, float* next_obs, int64_t next_se,

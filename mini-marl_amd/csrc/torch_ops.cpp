@@ -13,6 +13,17 @@
 //   agent_q_max                  target_network(next_state) -> max     qmix/main.py:191-193
 //   td_error                     cal_td_error                         vdn/_utils.py:44-52, qmix/_utils.py:86-97
 //   gae_scan                     SharedReplayBuffer.compute_returns   mappo/runner/shared/shared_buffer.py:131-157
+//   qmix_mixer_fwd               Mix_Net.forward (one step)           qmix/_network.py:199-217
+//   qmix_mixer_bwd               its backward: dQ_i, dh, every Mix_Net parameter gradient
+//   td_target_loss               Train_dqn / Target_Dqn TD target + MSE (or Huber), dQ_tot seeds, priorities
+//                                                                     qmix/_train.py:75-84,118-121; vdn/_train.py:73-79
+//   vdn_sum                      VDN mixing sum_i Q_i(a_i) / sum_i max_a Q_i   vdn/_train.py:23-47,68-71
+//   mappo_get_actions            R_MAPPOPolicy.get_actions / act: MLPBase -> masked GRU step -> LayerNorm ->
+//                                Categorical sample + log-prob, critic value   rmappo_policy.py:57-99,
+//                                rnn.py:26-29, distributions.py:55-68
+//   mappo_evaluate_actions       R_MAPPOPolicy.evaluate_actions: masked GRU scan over L-step chunks (RNNLayer's
+//                                segments, rnn.py:30-80) + Categorical log-prob / entropy + values
+//                                rmappo_policy.py:101-136
 //   Env.reset / Env.step         gym.make("ma_gym:Checkers-v0")       vdn/main.py:61-64,143
 //   PER.insert / sample / update Prioritized_Experience_Replay        vdn/replay_buffer/buffer.py:34-90
 #include <ATen/ATen.h>
@@ -219,6 +230,258 @@ void gae_scan(const at::Tensor& rewards, const at::Tensor& value_preds, const at
      "gae_scan");
 }
 
+// ------------------------------------------------------------------ QMIX mixer, TD loss, VDN sum
+struct MixDims {
+  int32_t N, S, Hm, K1;
+  int64_t n_params, save_dim, delta_dim;
+};
+MixDims mix_dims(const std::vector<int64_t>& d) {
+  TORCH_CHECK(d.size() == 4, "mixer dims must be [n_agents, state_dim, mixer_hidden, hypernet_k1]");
+  MixDims m{(int32_t)d[0], (int32_t)d[1], (int32_t)d[2], (int32_t)d[3], 0, 0, 0};
+  ok(mm_mixer_param_count(m.S, m.Hm, m.K1, m.N, &m.n_params), "mixer dims");
+  m.save_dim = mm_mixer_save_dim(m.Hm, m.K1, m.N);
+  m.delta_dim = mm_mixer_delta_dim(m.Hm, m.K1, m.N);
+  return m;
+}
+
+void rows_of(const at::Tensor& t, int64_t B, int64_t width, at::ScalarType dt, const at::Tensor& like, const char* name) {
+  need(t, dt, name);
+  same_device(like, t, name);
+  TORCH_CHECK(t.numel() == B * width, name, " must hold [", B, ", ", width, "] elements, got ", t.sizes());
+}
+
+// Mix_Net.forward of one step: Q_tot[b] = mix(q[b], state[b]) with the GRU hidden h -> h_out (rows where
+// reset[b] != 0 start from zeros); save [B, mixer_save_dim] keeps what qmix_mixer_bwd needs.
+void qmix_mixer_fwd(const at::Tensor& P, std::vector<int64_t> dims, const at::Tensor& q, const at::Tensor& state,
+                    const at::Tensor& h, const c10::optional<at::Tensor>& reset, at::Tensor qtot, at::Tensor h_out,
+                    const c10::optional<at::Tensor>& save) {
+  const MixDims m = mix_dims(dims);
+  need(P, at::kFloat, "P");
+  TORCH_CHECK(P.numel() == m.n_params, "P has ", P.numel(), " elements, the mixer needs ", m.n_params);
+  need(state, at::kFloat, "state");
+  TORCH_CHECK(state.dim() >= 1 && state.numel() % m.S == 0, "state must be [B, state_dim]");
+  const int64_t B = state.numel() / m.S;
+  TORCH_CHECK(B >= 1, "empty batch");
+  rows_of(q, B, m.N, at::kFloat, state, "q");
+  rows_of(h, B, m.Hm, at::kFloat, state, "h");
+  rows_of(h_out, B, m.Hm, at::kFloat, state, "h_out");
+  rows_of(qtot, B, 1, at::kFloat, state, "qtot");
+  same_device(state, P, "P");
+  if (reset.has_value()) rows_of(*reset, B, 1, at::kByte, state, "reset");
+  if (save.has_value()) rows_of(*save, B, m.save_dim, at::kFloat, state, "save");
+  mm_mix_net n{};
+  n.P = P.data_ptr<float>();
+  n.gi = nullptr;
+  n.q = q.data_ptr<float>();
+  n.s_off = nullptr;                         // contiguous state rows
+  n.h_in = h.data_ptr<float>();
+  n.reset = reset.has_value() ? reset->data_ptr<uint8_t>() : nullptr;
+  n.h_out = h_out.data_ptr<float>();
+  n.qtot = qtot.data_ptr<float>();
+  n.save = save.has_value() ? save->data_ptr<float>() : nullptr;
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(state.device());
+  ok(mm_mixer_fwd((int32_t)B, m.N, m.S, m.Hm, m.K1, state.data_ptr<float>(), state.data_ptr<float>(), &n, 1,
+                  stream_of(state)),
+     "qmix_mixer_fwd");
+}
+
+int64_t qmix_mixer_workspace(std::vector<int64_t> dims, int64_t B) {
+  const MixDims m = mix_dims(dims);
+  TORCH_CHECK(B >= 1, "B must be >= 1");
+  const int64_t part = mm_mixer_wgrad_partial_count((int32_t)B, m.N, m.S, m.Hm, m.K1);
+  TORCH_CHECK(part >= 0, "mixer workspace: bad dims");
+  return ((B * m.delta_dim + 3) & ~int64_t(3)) + part;
+}
+
+// Backward of one qmix_mixer_fwd step: dqtot [B] -> dq [B, N] (dQ_tot/dq_i), dh (in: the gradient w.r.t. h_out,
+// dropped where drop[b] > 0.5 — the next step restarted from zeros; out: the gradient w.r.t. h), dP [n_params]
+// (every Mix_Net parameter gradient, MIX_KEYS order, overwritten). workspace: qmix_mixer_workspace(dims, B) floats.
+void qmix_mixer_bwd(const at::Tensor& P, std::vector<int64_t> dims, const at::Tensor& state, const at::Tensor& save,
+                    const at::Tensor& q, const at::Tensor& dqtot, const at::Tensor& drop, at::Tensor dh, at::Tensor dq,
+                    at::Tensor dP, at::Tensor workspace) {
+  const MixDims m = mix_dims(dims);
+  need(P, at::kFloat, "P");
+  TORCH_CHECK(P.numel() == m.n_params, "P has ", P.numel(), " elements, the mixer needs ", m.n_params);
+  need(state, at::kFloat, "state");
+  const int64_t B = state.numel() / m.S;
+  TORCH_CHECK(B >= 1 && B * m.S == state.numel(), "state must be [B, state_dim]");
+  rows_of(save, B, m.save_dim, at::kFloat, state, "save");
+  rows_of(q, B, m.N, at::kFloat, state, "q");
+  rows_of(dqtot, B, 1, at::kFloat, state, "dqtot");
+  rows_of(drop, B, 1, at::kFloat, state, "drop");
+  rows_of(dh, B, m.Hm, at::kFloat, state, "dh");
+  rows_of(dq, B, m.N, at::kFloat, state, "dq");
+  need(dP, at::kFloat, "dP");
+  TORCH_CHECK(dP.numel() == m.n_params, "dP must hold the mixer's ", m.n_params, " parameters");
+  need(workspace, at::kFloat, "workspace");
+  const int64_t need_ws = qmix_mixer_workspace(dims, B);
+  TORCH_CHECK(workspace.numel() >= need_ws, "workspace has ", workspace.numel(), " floats, needs ", need_ws,
+              " (qmix_mixer_workspace)");
+  same_device(state, P, "P");
+  same_device(state, dP, "dP");
+  same_device(state, workspace, "workspace");
+  float* delta = workspace.data_ptr<float>();
+  const int64_t doff = (B * m.delta_dim + 3) & ~int64_t(3);
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(state.device());
+  const mm_stream_t st = stream_of(state);
+  ok(mm_mixer_bwd((int32_t)B, m.N, m.S, m.Hm, m.K1, P.data_ptr<float>(), save.data_ptr<float>(), q.data_ptr<float>(),
+                  dqtot.data_ptr<float>(), drop.data_ptr<float>(), dh.data_ptr<float>(), dq.data_ptr<float>(), delta,
+                  st),
+     "qmix_mixer_bwd");
+  ok(mm_mixer_wgrad((int32_t)B, m.N, m.S, m.Hm, m.K1, state.data_ptr<float>(), nullptr, nullptr,
+                    save.data_ptr<float>(), delta, dP.data_ptr<float>(), delta + doff, workspace.numel() - doff, st),
+     "qmix_mixer_bwd (weight gradients)");
+}
+
+// TD targets + loss over a chunk (rows t*B + b): y = w_b * sum_i (r_i + gamma (1-d) Q'_tot) (the reference,
+// flags 0) or sum_i r_i + gamma (1-d) Q'_tot (flag 4 = MM_LOSS_TARGET_SUM, no IS weight); MSE (or smooth-L1,
+// flag 2) mean over B summed over C; dqtot = dLoss/dQ_tot; td_last = |y - Q_tot| of the last step (priorities).
+void td_target_loss(const at::Tensor& rew, const at::Tensor& done, const c10::optional<at::Tensor>& is_weight,
+                    const at::Tensor& qtot, const at::Tensor& qtot_target, double gamma, int64_t flags,
+                    at::Tensor dqtot, at::Tensor td_last, at::Tensor loss, at::Tensor loss_parts) {
+  TORCH_CHECK((flags & ~(int64_t)(MM_LOSS_HUBER | MM_LOSS_TARGET_SUM)) == 0,
+              "flags: MM_LOSS_HUBER (2) | MM_LOSS_TARGET_SUM (4); VDN sums Q with vdn_sum first");
+  need(rew, at::kFloat, "rew");
+  TORCH_CHECK(rew.dim() == 3, "rew must be [C, B, N]");
+  const int64_t C = rew.size(0), B = rew.size(1), N = rew.size(2);
+  rows_of(done, C * B, 1, at::kFloat, rew, "done");
+  rows_of(qtot, C * B, 1, at::kFloat, rew, "qtot");
+  rows_of(qtot_target, C * B, 1, at::kFloat, rew, "qtot_target");
+  rows_of(dqtot, C * B, 1, at::kFloat, rew, "dqtot");
+  rows_of(loss_parts, C * B, 1, at::kFloat, rew, "loss_parts");
+  rows_of(td_last, B, 1, at::kFloat, rew, "td_last");
+  rows_of(loss, 1, 1, at::kFloat, rew, "loss");
+  TORCH_CHECK((flags & MM_LOSS_TARGET_SUM) || is_weight.has_value(), "is_weight required (reference target)");
+  if (is_weight.has_value()) rows_of(*is_weight, B, 1, at::kFloat, rew, "is_weight");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(rew.device());
+  ok(mm_lrn_loss_ex((int32_t)B, (int32_t)C, (int32_t)N, (float)gamma, rew.data_ptr<float>(), done.data_ptr<float>(),
+                    is_weight.has_value() ? is_weight->data_ptr<float>() : nullptr, qtot.data_ptr<float>(),
+                    qtot_target.data_ptr<float>(), (int32_t)flags, nullptr, nullptr, dqtot.data_ptr<float>(), nullptr,
+                    loss_parts.data_ptr<float>(), td_last.data_ptr<float>(), loss.data_ptr<float>(), stream_of(rew)),
+     "td_target_loss");
+}
+
+void vdn_sum(const at::Tensor& q, const c10::optional<at::Tensor>& act, at::Tensor out) {
+  TORCH_CHECK(q.is_cuda() && q.scalar_type() == at::kFloat && q.dim() == 3 && q.stride(2) == 1,
+              "q must be a float GPU tensor [B, N, A] with unit action stride");
+  const int64_t B = q.size(0), N = q.size(1), A = q.size(2);
+  rows_of(out, B, 1, at::kFloat, q, "out");
+  if (act.has_value()) rows_of(*act, B, N, at::kInt, q, "act");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  ok(mm_vdn_sum(B, (int32_t)N, (int32_t)A, q.data_ptr<float>(), q.stride(0), q.stride(1),
+                act.has_value() ? act->data_ptr<int32_t>() : nullptr, out.data_ptr<float>(), nullptr, stream_of(q)),
+     "vdn_sum");
+}
+
+// ------------------------------------------------------------------ MAPPO actor / critic
+mm_mappo_dims mappo_dims(const std::vector<int64_t>& d, const at::Tensor& actor_P, const at::Tensor& critic_P) {
+  TORCH_CHECK(d.size() == 3, "MAPPO dims must be [obs_dim, hidden, n_actions]");
+  mm_mappo_dims m{(int32_t)d[0], (int32_t)d[1], (int32_t)d[2]};
+  need(actor_P, at::kFloat, "actor_P");
+  need(critic_P, at::kFloat, "critic_P");
+  same_device(actor_P, critic_P, "critic_P");
+  TORCH_CHECK(actor_P.numel() == mm_mappo_param_count(&m, 0), "actor_P has ", actor_P.numel(),
+              " elements, the actor needs ", mm_mappo_param_count(&m, 0));
+  TORCH_CHECK(critic_P.numel() == mm_mappo_param_count(&m, 1), "critic_P has ", critic_P.numel(),
+              " elements, the critic needs ", mm_mappo_param_count(&m, 1));
+  return m;
+}
+
+// get_actions: rows R = E*N, one recurrent step (h <- h * mask), sample (device counter RNG or injected
+// uniforms u [R]) or, deterministic, the mode; writes both nets' new hiddens, actions, log-probs, values.
+void mappo_get_actions(const at::Tensor& actor_P, const at::Tensor& critic_P, std::vector<int64_t> dims,
+                       const at::Tensor& obs, const at::Tensor& h_actor, const at::Tensor& h_critic,
+                       const c10::optional<at::Tensor>& masks, const c10::optional<at::Tensor>& u, int64_t seed,
+                       int64_t counter, bool deterministic, at::Tensor h_actor_out, at::Tensor h_critic_out,
+                       at::Tensor actions, at::Tensor logp, at::Tensor values) {
+  const mm_mappo_dims m = mappo_dims(dims, actor_P, critic_P);
+  need(obs, at::kFloat, "obs");
+  TORCH_CHECK(obs.numel() % m.obs_dim == 0, "obs must be [R, obs_dim]");
+  const int64_t R = obs.numel() / m.obs_dim;
+  TORCH_CHECK(R >= 1, "empty batch");
+  same_device(obs, actor_P, "actor_P");
+  rows_of(h_actor, R, m.hidden, at::kFloat, obs, "h_actor");
+  rows_of(h_critic, R, m.hidden, at::kFloat, obs, "h_critic");
+  rows_of(h_actor_out, R, m.hidden, at::kFloat, obs, "h_actor_out");
+  rows_of(h_critic_out, R, m.hidden, at::kFloat, obs, "h_critic_out");
+  rows_of(actions, R, 1, at::kInt, obs, "actions");
+  rows_of(logp, R, 1, at::kFloat, obs, "logp");
+  rows_of(values, R, 1, at::kFloat, obs, "values");
+  if (masks.has_value()) rows_of(*masks, R, 1, at::kFloat, obs, "masks");
+  if (u.has_value()) rows_of(*u, R, 1, at::kFloat, obs, "u");
+  mm_mappo_fwd_args a{};
+  a.net[0] = {actor_P.data_ptr<float>(), h_actor.data_ptr<float>(), h_actor_out.data_ptr<float>(),
+              logp.data_ptr<float>(), nullptr};
+  a.net[1] = {critic_P.data_ptr<float>(), h_critic.data_ptr<float>(), h_critic_out.data_ptr<float>(),
+              values.data_ptr<float>(), nullptr};
+  a.obs = obs.data_ptr<float>();
+  a.mask = masks.has_value() ? masks->data_ptr<float>() : nullptr;
+  a.act_out = actions.data_ptr<int32_t>();
+  a.u = u.has_value() ? u->data_ptr<float>() : nullptr;
+  a.seed = (uint64_t)seed;
+  a.counter = (uint64_t)counter;
+  a.rows = R;
+  a.mode = MM_MAPPO_ROLLOUT;
+  a.deterministic = deterministic ? 1 : 0;
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(obs.device());
+  ok(mm_mappo_fwd(&m, &a, stream_of(obs)), "mappo_get_actions");
+}
+
+int64_t mappo_eval_rs(int64_t rows) { return (rows + 63) / 64 * 64; }
+
+int64_t mappo_evaluate_workspace(std::vector<int64_t> dims, int64_t rows) {
+  TORCH_CHECK(dims.size() == 3 && rows >= 1, "dims [obs_dim, hidden, n_actions], rows >= 1");
+  mm_mappo_dims m{(int32_t)dims[0], (int32_t)dims[1], (int32_t)dims[2]};
+  const int64_t rs = mappo_eval_rs(rows);
+  return (int64_t)(mm_mappo_save_fields(&m, 0) + mm_mappo_save_fields(&m, 1)) * rs + rs;
+}
+
+// evaluate_actions over n recurrent chunks of L steps (rows l*n + j, shared_buffer.py:318-427 order):
+// chunk-start hiddens h_actor0 / h_critic0 [n, H], masks [L*n] (h <- h * mask every step) -> values, log-probs of
+// actions [L*n], entropy [1] = the active-masked mean of the Categorical entropies.
+void mappo_evaluate_actions(const at::Tensor& actor_P, const at::Tensor& critic_P, std::vector<int64_t> dims,
+                            const at::Tensor& obs, const at::Tensor& h_actor0, const at::Tensor& h_critic0,
+                            const at::Tensor& actions, const at::Tensor& masks,
+                            const c10::optional<at::Tensor>& active_masks, int64_t L, at::Tensor values,
+                            at::Tensor logp, at::Tensor entropy, at::Tensor workspace) {
+  const mm_mappo_dims m = mappo_dims(dims, actor_P, critic_P);
+  need(obs, at::kFloat, "obs");
+  TORCH_CHECK(L >= 1 && obs.numel() % (m.obs_dim * L) == 0, "obs must be [L * n, obs_dim]");
+  const int64_t rows = obs.numel() / m.obs_dim, n = rows / L;
+  same_device(obs, actor_P, "actor_P");
+  rows_of(h_actor0, n, m.hidden, at::kFloat, obs, "h_actor0");
+  rows_of(h_critic0, n, m.hidden, at::kFloat, obs, "h_critic0");
+  rows_of(actions, rows, 1, at::kInt, obs, "actions");
+  rows_of(masks, rows, 1, at::kFloat, obs, "masks");
+  if (active_masks.has_value()) rows_of(*active_masks, rows, 1, at::kFloat, obs, "active_masks");
+  rows_of(values, rows, 1, at::kFloat, obs, "values");
+  rows_of(logp, rows, 1, at::kFloat, obs, "logp");
+  rows_of(entropy, 1, 1, at::kFloat, obs, "entropy");
+  need(workspace, at::kFloat, "workspace");
+  same_device(obs, workspace, "workspace");
+  TORCH_CHECK(workspace.numel() >= mappo_evaluate_workspace(dims, rows), "workspace too small (mappo_evaluate_workspace)");
+  const int64_t rs = mappo_eval_rs(rows);
+  float* ws = workspace.data_ptr<float>();
+  mm_mappo_fwd_args a{};
+  a.net[0] = {actor_P.data_ptr<float>(), h_actor0.data_ptr<float>(), nullptr, nullptr, ws};
+  a.net[1] = {critic_P.data_ptr<float>(), h_critic0.data_ptr<float>(), nullptr, nullptr,
+              ws + (int64_t)mm_mappo_save_fields(&m, 0) * rs};
+  a.obs = obs.data_ptr<float>();
+  a.mask = masks.data_ptr<float>();
+  a.en = n;
+  a.T = (int32_t)L;
+  a.L = (int32_t)L;
+  a.rs = rs;
+  a.mode = MM_MAPPO_TRAIN;
+  float* ent_rows = ws + (int64_t)(mm_mappo_save_fields(&m, 0) + mm_mappo_save_fields(&m, 1)) * rs;
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(obs.device());
+  ok(mm_mappo_evaluate_actions(&m, &a, actions.data_ptr<int32_t>(),
+                               active_masks.has_value() ? active_masks->data_ptr<float>() : nullptr,
+                               values.data_ptr<float>(), logp.data_ptr<float>(), ent_rows, entropy.data_ptr<float>(),
+                               nullptr, stream_of(obs)),
+     "mappo_evaluate_actions");
+}
+
 // ------------------------------------------------------------------ env (custom class)
 struct Env : torch::CustomClassHolder {
   mm_env* h = nullptr;
@@ -345,6 +608,21 @@ TORCH_LIBRARY(minimarl, m) {
   m.def("td_error(Tensor rew, Tensor done, Tensor q_taken, Tensor max_q_next, float gamma, Tensor(a!) td) -> ()");
   m.def("gae_scan(Tensor rewards, Tensor value_preds, Tensor masks, Tensor value_norm, float gamma, "
         "float gae_lambda, Tensor(a!) returns) -> ()");
+  m.def("qmix_mixer_fwd(Tensor P, int[] dims, Tensor q, Tensor state, Tensor h, Tensor? reset, Tensor(a!) qtot, "
+        "Tensor(b!) h_out, Tensor(c!)? save=None) -> ()");
+  m.def("qmix_mixer_workspace(int[] dims, int B) -> int");
+  m.def("qmix_mixer_bwd(Tensor P, int[] dims, Tensor state, Tensor save, Tensor q, Tensor dqtot, Tensor drop, "
+        "Tensor(a!) dh, Tensor(b!) dq, Tensor(c!) dP, Tensor(d!) workspace) -> ()");
+  m.def("td_target_loss(Tensor rew, Tensor done, Tensor? is_weight, Tensor qtot, Tensor qtot_target, float gamma, "
+        "int flags, Tensor(a!) dqtot, Tensor(b!) td_last, Tensor(c!) loss, Tensor(d!) loss_parts) -> ()");
+  m.def("vdn_sum(Tensor q, Tensor? act, Tensor(a!) out) -> ()");
+  m.def("mappo_get_actions(Tensor actor_P, Tensor critic_P, int[] dims, Tensor obs, Tensor h_actor, Tensor h_critic, "
+        "Tensor? masks, Tensor? u, int seed, int counter, bool deterministic, Tensor(a!) h_actor_out, "
+        "Tensor(b!) h_critic_out, Tensor(c!) actions, Tensor(d!) logp, Tensor(e!) values) -> ()");
+  m.def("mappo_evaluate_workspace(int[] dims, int rows) -> int");
+  m.def("mappo_evaluate_actions(Tensor actor_P, Tensor critic_P, int[] dims, Tensor obs, Tensor h_actor0, "
+        "Tensor h_critic0, Tensor actions, Tensor masks, Tensor? active_masks, int L, Tensor(a!) values, "
+        "Tensor(b!) logp, Tensor(c!) entropy, Tensor(d!) workspace) -> ()");
   m.class_<Env>("Env")
       .def(torch::init<int64_t, int64_t, int64_t, double, bool, int64_t>())
       .def("obs_dim", &Env::obs_dim)
@@ -369,4 +647,16 @@ TORCH_LIBRARY_IMPL(minimarl, CUDA, m) {
   m.impl("agent_q_max", agent_q_max);
   m.impl("td_error", td_error);
   m.impl("gae_scan", gae_scan);
+  m.impl("qmix_mixer_fwd", qmix_mixer_fwd);
+  m.impl("qmix_mixer_bwd", qmix_mixer_bwd);
+  m.impl("td_target_loss", td_target_loss);
+  m.impl("vdn_sum", vdn_sum);
+  m.impl("mappo_get_actions", mappo_get_actions);
+  m.impl("mappo_evaluate_actions", mappo_evaluate_actions);
+}
+
+// size queries: no tensor arguments, so they dispatch on the catch-all kernel
+TORCH_LIBRARY_IMPL(minimarl, CompositeExplicitAutograd, m) {
+  m.impl("qmix_mixer_workspace", qmix_mixer_workspace);
+  m.impl("mappo_evaluate_workspace", mappo_evaluate_workspace);
 }

@@ -70,6 +70,7 @@ _SIGS = [
     ("mm_env_step_rows_td", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp,
                                     c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_reset_obs", c_vp, [c_vp]),
+    ("mm_env_step_rows_begin", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_grid_shape", c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     ("mm_td_chunk_step", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
@@ -83,6 +84,8 @@ _SIGS = [
     ("mm_per_destroy", None, [c_vp]),
     ("mm_per_add_batch", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     ("mm_per_insert", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ("mm_per_insert_td", c_i32, [c_vp, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
+                                 c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_per_sample", c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_per_sample_rng", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
     ("mm_per_update", c_i32, [c_vp, c_vp, c_vp, c_i32, c_vp]),
@@ -188,6 +191,10 @@ _SIGS += [
                                c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_mixer_bwd", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp]),
+    ("mm_mixer_wgrad_partial_count", c_i64, [c_i32, c_i32, c_i32, c_i32, c_i32]),
+    ("mm_mixer_wgrad", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                               c_vp]),
+    ("mm_vdn_sum", c_i32, [c_i64, c_i32, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     ("mm_agent_bwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp, c_vp, c_vp, c_vp]),
     ("mm_agent_bwd_seq", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -259,6 +266,8 @@ _SIGS += [
     ("mm_mappo_grad_fields", c_i32, [_MD, c_i32]),
     ("mm_mappo_fwd", c_i32, [_MD, ctypes.POINTER(MappoFwdArgs), c_vp]),
     ("mm_mappo_bwd", c_i32, [_MD, ctypes.POINTER(MappoBwdArgs), c_vp]),
+    ("mm_mappo_evaluate_actions", c_i32, [_MD, ctypes.POINTER(MappoFwdArgs), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                          c_vp, c_vp]),
     ("mm_mappo_wgrad_partial_count", c_i64, [_MD, c_i64]),
     ("mm_mappo_wgrad", c_i32, [_MD, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp]),
     ("mm_mappo_grad_scratch_count", c_i64, [_MD, c_i32]),
@@ -345,6 +354,7 @@ _SIGS += [
     ("mm_switch_set_state", c_i32, [c_vp, c_vp, c_vp, c_vp]),
     ("mm_switch_reset_obs", c_vp, [c_vp]),
     ("mm_switch_step_rows", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_switch_step_rows_begin", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_switch_step_rows_td", c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp,
                                        c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 ]

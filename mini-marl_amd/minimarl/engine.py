@@ -10,11 +10,13 @@ qmix/main.py:100-237): for every env at every step
      (cal_td_error + chunk lists, qmix/_utils.py:86-97, qmix/main.py:204-233)
   5. every C steps: the E finished chunks go into the prioritized replay at once
 
-Two launches per in-chunk step: env(t) fused with the TD/store of step t-1, and the
-target fwd of step t fused with the behavior fwd of step t+1; the chunk's last step adds
-a standalone TD/store and the PER insert. All stream-ordered on one HIP stream, no host
-sync; a chunk of steps is captured once as a HIP graph and replayed. The store/TD of the
-last executed step therefore lands with the next step (``flush_td()`` writes it now).
+Two launches per step: env(t) — fused with the TD/store of step t-1 inside a chunk, with the
+chunk-start copy of the current obs into the new staging rows at a chunk's first step — and the
+target fwd of step t fused with the behavior fwd of step t+1; the chunk's last step adds the PER
+insert (four launches, its first one also running that step's TD/store). All stream-ordered on
+one HIP stream, no host sync; a chunk of steps is captured once as a HIP graph and replayed. The
+store/TD of the last executed step therefore lands with the next step (``flush_td()`` writes it
+now).
 Hidden states reset at episode ends (the reference re-inits them per episode,
 vdn/main.py:137-138); chunks span episode boundaries like the reference's
 global ``count_step`` (vdn/main.py:151-167).
@@ -180,11 +182,14 @@ class RolloutEngine:
         ND = self.N * self.D
         if not self._primed:
             self._prologue(s)
-        if c == 0:
-            check(L.mm_chunk_begin_rows(self.E, ND, ptr(self.store.obs), self.store.row_stride, ptr(self.cur_row),
-                                        self.C * ND, self.env.reset_obs_ptr(), ptr(self.staging), s), "chunk_begin")
         nxt = ctypes.c_void_p(self.store.obs.data_ptr() + 4 * (c + 1) * ND)
-        if c > 0 and not self._td_flushed:
+        if c == 0:
+            # chunk start folded into the env launch: slot 0 of the new staging rows <- the current obs
+            # (slot C of the previous rows, or the reset obs), then the step into slot 1
+            check(self.env.step_rows_begin(ptr(self.act_buf[k]), ptr(self.store.obs), self.store.row_stride, self.C,
+                                           ptr(self.staging), ptr(self.cur_row), ptr(self.rew), ptr(self.done_buf[k]),
+                                           s), "env_step_begin")
+        elif not self._td_flushed:
             # env(t) fused with the TD/store of step t-1 (same staging rows inside a chunk)
             kp = 1 - k
             check(self.env.step_rows_td(ptr(self.act_buf[k]), nxt, self.store.row_stride,
@@ -205,9 +210,12 @@ class RolloutEngine:
         check(L.mm_agent_q_fwd2(ctypes.byref(self.target.dims), ptr(self.target.packed), ctypes.byref(iot), self.E,
                                 ptr(self.behavior.packed), ctypes.byref(iob), self.E, s), "agent_q_fwd2")
         if c == self.C - 1:
-            # the chunk's last TD/store runs on its own (the insert needs it before the next env step)
-            self._td_standalone(s, k, c)
-            check(L.mm_per_insert(self.per._h, ptr(self.chunk_td), self.E, ptr(self.staging), None, s), "per_insert")
+            # the chunk's last TD / store folded into the PER insert's first launch (the insert needs the chunk
+            # priorities before the next env step)
+            check(L.mm_per_insert_td(self.per._h, self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done_buf[k]),
+                                     ptr(self.qsel_buf[k]), ptr(self.maxq), ptr(self.act_buf[k]), ptr(self.chunk_td),
+                                     c, self.C, ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
+                                     ptr(self.counter_dev), ptr(self.staging), None, s), "per_insert_td")
             self.chunks_inserted += self.E
             self._td_pending = False
         else:

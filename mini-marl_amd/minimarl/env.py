@@ -51,6 +51,9 @@ class VecEnv:
     def step_rows_td(self, *args):
         return lib().mm_env_step_rows_td(self._h, *args)
 
+    def step_rows_begin(self, *args):
+        return lib().mm_env_step_rows_begin(self._h, *args)
+
     def reset(self, out=None):
         out = out if out is not None else torch.empty(self.E, self.N, self.obs_dim, device=self.device)
         check(lib().mm_env_reset(self._h, ptr(out), stream_handle(self.device)), "env_reset")
@@ -138,6 +141,9 @@ class SwitchVecEnv:
 
     def step_rows_td(self, *args):
         return lib().mm_switch_step_rows_td(self._h, *args)
+
+    def step_rows_begin(self, *args):
+        return lib().mm_switch_step_rows_begin(self._h, *args)
 
     def reset(self, out=None):
         out = out if out is not None else torch.empty(self.E, self.N, self.obs_dim, device=self.device)

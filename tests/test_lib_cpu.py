@@ -64,8 +64,14 @@ def test_torch_op_library_registers_every_op():
     if not os.path.exists(TORCH_LIB_PATH):
         pytest.skip("torch op library not built")
     ops = load()
-    for name in ("qnet_pack", "agent_q_fwd", "agent_q_act", "agent_q_max", "td_error", "gae_scan"):
+    for name in ("qnet_pack", "agent_q_fwd", "agent_q_act", "agent_q_max", "td_error", "gae_scan", "qmix_mixer_fwd",
+                 "qmix_mixer_bwd", "td_target_loss", "vdn_sum", "mappo_get_actions", "mappo_evaluate_actions"):
         schema = str(getattr(ops, name).default._schema)
         assert schema.startswith(f"minimarl::{name}("), schema
         assert "(a!)" in schema          # outputs are caller-allocated mutable arguments
     assert torch.classes.minimarl.Env is not None and torch.classes.minimarl.PER is not None
+    # workspace size queries run on the host (no tensors): Mix_Net of qmix/_network.py at the golden shapes
+    # (N 8, state 8 x 47, Hm 32, k1 32) and evaluate_actions of 7 chunks x 5 steps
+    ws = ops.qmix_mixer_workspace([8, 376, 32, 32], 32)
+    assert ws >= 32 * (6 * 32 + 8 * 32 + 3 * 32 + 1)
+    assert ops.mappo_evaluate_workspace([47, 32, 5], 35) >= 2 * 64 * (8 + 8 * 32 + 1)
