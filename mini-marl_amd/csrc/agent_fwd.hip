@@ -14,6 +14,7 @@
 // with N = 8 each XCD's L2 only ever holds one agent's weights.
 // Arithmetic: exact-f32 MFMA v_mfma_f32_32x32x2_f32 (fp32 in, fp32 accumulate).
 #include "common.h"
+#include "fused_env.h"
 #include "minimarl.h"
 #include "qnet_geo.h"
 
@@ -25,8 +26,8 @@ struct QFwdParams {
   const float* packed;
   int E, N, D, A;
   int nblocks;  // blocks of this net inside a (possibly dual) launch
-  int stagger;  // LDS variant: waves 4-7 start stagger x 512 cycles late
-  int dbg;      // debug timing (MM_FWD_DBG): stop the fp16x3 kernel after phase dbg (0 = full)
+  int stagger;  // fp16x3 kernel: waves 8-15 start stagger x s_sleep(8) late
+  int dbg;      // unused (kept for the kernarg layout)
   int pad_;
 };
 
@@ -179,10 +180,12 @@ __device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_
 }
 
 // xn: layer-1 k-block 0 of the observation, loaded by the caller (before weight staging).
-template <int F1, int G, int H, int AB>
+// ol(kb, x) loads observation k-block kb (lane (i, hh) holds features 32 kb + kperm(s, hh) of env e);
+// zero_h: start the GRU from zeros (invalid env or reset flag)
+template <int F1, int G, int H, int AB, class OL>
 __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent, int e,
-                                                 const float* __restrict__ W, const float* orow,
-                                                 float (&xn)[16]) {
+                                                 const float* __restrict__ W, const OL& ol,
+                                                 float (&xn)[16], bool zero_h) {
   using S = Sched<F1, G, H, AB>;
   using CG = typename S::CG;
   constexpr int RB1 = S::RB1, RB2 = S::RB2, HB = S::HB, NF = S::NF;
@@ -218,7 +221,7 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
 #pragma unroll
       for (int s = 0; s < 16; ++s) fa[rb][s] = fn[rb][s];
     if (kb + 1 < p.g.KD) {
-      load_obs_kblock(orow, kb + 1, p.D, xn);
+      ol(kb + 1, xn);
 #pragma unroll
       for (int rb = 0; rb < RB1; ++rb)
         load_frag(W + CG::off_l1 + (int64_t)(rb * p.g.KD + kb + 1) * 1024, lane, fn[rb]);
@@ -257,7 +260,6 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
   }
 
   // ---- GRU cell
-  const bool zero_h = !valid || (io.reset && io.reset[e]);
   f32x16 h0[HB];
 #pragma unroll
   for (int hb = 0; hb < HB; ++hb) {
@@ -991,39 +993,9 @@ __global__ __launch_bounds__(256, (F1 > 64 ? 1 : 2)) void agent_q_fwd_kernel(QFw
   const float* orow = obs_row_ptr(p, agent, e);
   float xn[16];
   load_obs_kblock(orow, 0, p.D, xn);
-  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, p.packed + (int64_t)agent * p.g.agent_stride, orow, xn);
-}
-
-// Large-E variant: a 512-thread block (8 waves = 256 envs of one agent) first copies the agent's
-// whole fragment image into LDS (L2-resident: with N = 8 an XCD only serves one agent), then every
-// A-operand read is a conflict-free ds_read_b128 ([q][lane][4] image) instead of an L2 round trip.
-// The copy is LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction, all in flight at
-// once) issued after the first observation k-block's loads, so both latencies overlap.
-// One block per CU, two waves per SIMD.
-template <int F1, int G, int H, int AB>
-__global__ __launch_bounds__(512, 2) void agent_q_fwd_lds_kernel(QFwdParams p0, QFwdParams p1) {
-  extern __shared__ __attribute__((aligned(16))) float wsm[];
-  const bool second = (int)blockIdx.x >= p0.nblocks;
-  const QFwdParams& p = second ? p1 : p0;
-  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
-  const int agent = bid % p.N, tile = bid / p.N;
-  const int e = tile * 256 + (threadIdx.x >> 6) * 32 + (threadIdx.x & 31);
-  const float* orow = obs_row_ptr(p, agent, e);
-  float xn[16];
-  load_obs_kblock(orow, 0, p.D, xn);
-  const float* src = p.packed + (int64_t)agent * p.g.agent_stride;
-  const int nchunk = (int)(p.g.agent_stride >> 8);  // 1 KiB chunks (agent_stride is a multiple of 256)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int c = wave; c < nchunk; c += 8)
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 256 + lane * 4),
-                                     (__attribute__((address_space(3))) void*)(wsm + c * 256), 16, 0, 0);
-  __syncthreads();  // waits vmcnt(0): the DMA'd image has landed
-  // Stagger: waves 4-7 share SIMDs with waves 0-3 and run the same program; starting them ~2k
-  // cycles late puts one wave's VALU phases (GRU gates, epilogues) under the other's MFMAs
-  // (MI355X_MICROARCH "two waves ... try a stagger"; measured 54.6 -> 50.5 us dual at 4096 x 8).
-  if (wave >= 4)
-    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(8);
-  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, wsm, orow, xn);
+  const bool zero_h = e >= p.E || (p.io.reset && p.io.reset[e]);
+  agent_q_fwd_body<F1, G, H, AB>(p, agent, e, p.packed + (int64_t)agent * p.g.agent_stride,
+                                 [&](int kb, float (&x)[16]) { load_obs_kblock(orow, kb, p.D, x); }, xn, zero_h);
 }
 
 // ---------------------------------------------------------------- fp16x3-split forward (large E)
@@ -1114,9 +1086,10 @@ __device__ __forceinline__ void load_obs_ks(const float* orow, int kb, int D, fl
 }
 
 // Q output / argmax / eps-greedy / gather epilogue for 16-row Q tiles (rows 16t + 4g + r).
+// out_off: element offset of the act / qsel outputs (the fused rollout step's ring slot)
 template <int AT>
 __device__ __forceinline__ void q_epilogue16(const QFwdParams& p, int agent, int e, bool valid,
-                                             const f32x4 (&qa)[AT], float eps, uint64_t ctr) {
+                                             const f32x4 (&qa)[AT], float eps, uint64_t ctr, int64_t out_off = 0) {
   const int g = (threadIdx.x & 63) >> 4;
   const mm_qfwd_io& io = p.io;
   if (valid && io.q_out) {
@@ -1180,17 +1153,18 @@ __device__ __forceinline__ void q_epilogue16(const QFwdParams& p, int agent, int
   mine += __shfl_xor(mine, 32);
   const float qsel = (io.mode == MM_Q_MAX) ? best : mine;
   if (valid && g == 0) {
-    const int64_t o = (int64_t)e * p.N + agent;
+    const int64_t o = out_off + (int64_t)e * p.N + agent;
     if (io.act_out && io.mode == MM_Q_ACT) io.act_out[o] = act;
     if (io.qsel_out) io.qsel_out[o] = qsel;
   }
 }
 
-template <int F1, int G, int H, int AB>
+// ol(kb, x) loads observation k-step kb (lane (c, g) holds features 32 kb + kperm16(j, g) of env e)
+template <int F1, int G, int H, int AB, class OL>
 __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int agent, int e,
-                                                    const float* __restrict__ W, const float* orow,
+                                                    const float* __restrict__ W, const OL& ol,
                                                     float (&xn)[8], const f32x4 (&h0)[H / 16], float eps,
-                                                    uint64_t ctr) {
+                                                    uint64_t ctr, int64_t out_off = 0) {
   using CG = QnetCGeo<F1, G, H, AB>;
   constexpr int T1 = F1 / 16, T2 = G / 16, TH = H / 16, AT = (AB * 32 + 15) / 16;
   constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
@@ -1207,7 +1181,7 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
   for (int kb = 0; kb < p.g.KD; ++kb) {
     KS ob;
     split8(xn, ob);
-    if (kb + 1 < p.g.KD) load_obs_ks(orow, kb + 1, p.D, xn);
+    if (kb + 1 < p.g.KD) ol(kb + 1, xn);
 #pragma unroll
     for (int t = 0; t < T1; ++t) mm16(W + CG::off_l1 + (int64_t)((t >> 1) * p.g.KD + kb) * 1024, t & 1, ob, lane, x1[t]);
   }
@@ -1216,10 +1190,6 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
   for (int t = 0; t < T1; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) x1[t][r] = fmaxf(x1[t][r], 0.0f);
-  if (p.dbg == 2) {
-    if (x1[0][0] + x1[T1 - 1][3] == 12345.f) io.qsel_out[e] = eps;
-    return;
-  }
 #pragma unroll
   for (int kb = 0; kb < RB1; ++kb) split_pair(x1[2 * kb], x1[2 * kb + 1], x1s[kb]);
   float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
@@ -1247,10 +1217,6 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
   KS x2s[RB2];
 #pragma unroll
   for (int kb = 0; kb < RB2; ++kb) split_pair(x2[2 * kb], x2[2 * kb + 1], x2s[kb]);
-  if (p.dbg == 3) {
-    if (x2[0][0] + x2[T2 - 1][3] == 12345.f) io.qsel_out[e] = eps;
-    return;
-  }
 
   // ---- GRU cell (h0 loaded by the caller at kernel start)
   KS h0s[HB];
@@ -1367,10 +1333,6 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
   KS h1s[HB];
 #pragma unroll
   for (int kb = 0; kb < HB; ++kb) split_pair(h1[2 * kb], h1[2 * kb + 1], h1s[kb]);
-  if (p.dbg == 4) {
-    if (h1[0][0] + h1[TH - 1][3] == 12345.f) io.qsel_out[e] = eps;
-    return;
-  }
 
   // ---- Q head (only the 16-row tiles that hold real actions)
   f32x4 qa[AT];
@@ -1382,7 +1344,7 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
       for (int kb = 0; kb < HB; ++kb) mm16(W + CG::off_q + ((t >> 1) * HB + kb) * 1024, t & 1, h1s[kb], lane, qa[t]);
     }
   }
-  q_epilogue16<AT>(p, agent, e, valid, qa, eps, ctr);
+  q_epilogue16<AT>(p, agent, e, valid, qa, eps, ctr, out_off);
 }
 
 // The LDS-staged large-E kernel on the fp16x3 image: a 1024-thread block (16 waves x 16 envs = 256
@@ -1413,8 +1375,12 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
     const float* orow32 = obs_row_ptr(p, agent, e32);
     float x32[16];
     load_obs_kblock(orow32, 0, p.D, x32);
+    const bool zero_h = e32 >= p.E || (p.io.reset && p.io.reset[e32]);
     __syncthreads();
-    if (wave < 8) agent_q_fwd_body<F1, G, H, AB>(p, agent, e32, wsm, orow32, x32);
+    if (wave < 8)
+      agent_q_fwd_body<F1, G, H, AB>(p, agent, e32, wsm,
+                                     [&](int kb, float (&x)[16]) { load_obs_kblock(orow32, kb, p.D, x); }, x32,
+                                     zero_h);
     return;
   }
   const int e = tile * 256 + wave * 16 + (lane & 15);
@@ -1451,13 +1417,324 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
     for (int t = 0; t < H / 16; ++t) h0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
-  if (p.dbg == 1) {   // debug timing: stop after the loads + image DMA
-    if (xn[0] + h0[0][0] == 12345.f) p.io.qsel_out[e] = eps;
-    return;
-  }
   if (wave >= 8)
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(8);
-  agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm, orow, xn, h0, eps, ctr);
+  agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm,
+                                    [&](int kb, float (&x)[8]) { load_obs_ks(orow, kb, p.D, x); }, xn, h0, eps, ctr);
+}
+
+// ---------------------------------------------------------------- fused rollout step (env + dual forward)
+// One launch per lockstep step of the headline path (mm_rollout_step, include/minimarl.h): the dual fp16x3
+// forward above with the Checkers env transition folded in front of it. Each workgroup (net, agent, 256-env
+// tile) re-simulates its tile's transition: one thread per env, the 8 agent positions in registers, the grid in
+// LDS as 2-bit cells (96 cells = 6 words), agents moving in id order exactly as env.hip / oracle/env.py. That
+// costs ~1 us of the workgroup's time, all of it under the weight image's LDS-DMA, and replaces a separate env
+// launch, its launch boundary and the obs round trip through HBM (6.2 MB written + read twice per step at
+// 4096 x 8). The new state's observation of the workgroup's agent is a 45-bit mask (3x3 cells x 5 channels)
+// plus the two coordinates, kept per env in LDS, from which every lane builds its MFMA B-operand features.
+constexpr int FS_ENVS = 256;   // envs per workgroup (16 waves x 16 envs)
+struct FusedSmem {              // after the weight image (bytes)
+  static constexpr int pos = 0;                        // u16 [256][8]: r * 256 + c
+  static constexpr int grid = pos + FS_ENVS * 8 * 2;   // u32 [256][8]: 2-bit cells
+  static constexpr int mask = grid + FS_ENVS * 8 * 4;  // u64 [256][4]: obs masks of the observed agents
+  static constexpr int row = mask + FS_ENVS * 4 * 8;   // i32 [256]: the env's staging row
+  static constexpr int done = row + FS_ENVS * 4;       // u8 [256]
+  static constexpr int total = done + FS_ENVS;
+};
+
+__device__ __forceinline__ int fs_cell(const uint32_t* g, int i) { return (int)((g[i >> 4] >> ((i & 15) * 2)) & 3u); }
+
+// 45-bit local observation mask of the agent at (ar, ac): cell-major 3x3 (row-major, centre = own cell) x 5
+// channels {lemon, apple, even agent, odd agent, wall} (oracle/env.py observe)
+__device__ __forceinline__ uint64_t fs_obs_mask(const uint32_t* g, const int (&pr)[8], const int (&pc)[8], int N, int R,
+                                                int C, int ar, int ac) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int cell = 0; cell < 9; ++cell) {
+    const int rr = ar + cell / 3 - 1, cc = ac + cell % 3 - 1;
+    uint32_t bits;
+    if (rr < 0 || rr >= R || cc < 0 || cc >= C) {
+      bits = 16u;
+    } else {
+      const int item = fs_cell(g, rr * C + cc);
+      int who = -1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < N && pr[j] == rr && pc[j] == cc) who = j;
+      bits = (item == 1 ? 1u : 0u) | (item == 2 ? 2u : 0u) | ((item == 0 && who >= 0) ? ((who & 1) ? 8u : 4u) : 0u);
+    }
+    m |= (uint64_t)bits << (5 * cell);
+  }
+  return m;
+}
+
+// obs feature f of agent `agent` (partial: its 47 local features; full: agent f / 47's) from the LDS state
+__device__ __forceinline__ float fs_feature(const FusedEnv& ev, const uint16_t* sp, const uint64_t* sm, int agent,
+                                            int f) {
+  int q = 0, lf = f, a = agent;
+  if (ev.full_obs) {
+    q = f / 47;
+    lf = f - 47 * q;
+    a = q;
+  }
+  if (lf < 2) {
+    const int p = sp[a];
+    return lf == 0 ? (float)(p >> 8) * ev.inv_r : (float)(p & 255) * ev.inv_c;
+  }
+  return ((sm[q] >> (lf - 2)) & 1ull) ? 1.0f : 0.0f;
+}
+
+// the env state of thread le's env into LDS: positions and the obs masks of the observed agent(s)
+__device__ __forceinline__ void fs_publish(const FusedEnv& ev, const int (&pr)[8], const int (&pc)[8], const uint32_t* g,
+                                           int agent, uint16_t* sp, uint64_t* sm) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sp[j] = (uint16_t)(j < ev.N ? ((pr[j] << 8) | pc[j]) : 0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int aq = ev.full_obs ? q : agent;
+    if (q < (ev.full_obs ? ev.N : 1)) {
+      int ar = 0, ac = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j == aq) {
+          ar = pr[j];
+          ac = pc[j];
+        }
+      sm[q] = fs_obs_mask(g, pr, pc, ev.N, ev.R, ev.C, ar, ac);
+    }
+  }
+}
+
+// the agent's obs of the tile's 256 envs (from LDS) into store slot `slot`, all 1024 threads, env-contiguous
+__device__ __forceinline__ void fs_store_obs(const FusedEnv& ev, const mm_rollout_io& rio, int agent, int e0, int slot,
+                                             const uint16_t* s_pos, const uint64_t* s_mask, const int32_t* s_row) {
+  const int D = ev.D;
+  const int nenv = min(FS_ENVS, (int)(ev.E - e0));
+  const int64_t off = (int64_t)slot * ev.N * D + (int64_t)agent * D;
+  for (int i = threadIdx.x; i < nenv * D; i += blockDim.x) {
+    const int le = i / D, f = i - le * D;
+    rio.store_obs[(int64_t)s_row[le] * rio.row_stride + off + f] = fs_feature(ev, s_pos + le * 8, s_mask + le * 4, agent, f);
+  }
+}
+
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(1024, MM_H3_LB) void rollout_step_h3_kernel(QFwdParams p0, QFwdParams p1, FusedEnv ev,
+                                                                         mm_rollout_io rio) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  const bool second = (int)blockIdx.x >= p0.nblocks;          // behavior net (s_{t+1}); else target (s'_t)
+  const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  const QFwdParams& p = kargs[second ? 1 : 0];
+  (void)p1;
+  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
+  const int agent = bid % p.N, tile = bid / p.N;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int N = ev.N, RC = ev.R * ev.C;
+  const int64_t E = ev.E, EN = E * N;
+  const int e0 = tile * FS_ENVS;
+  char* aux = reinterpret_cast<char*>(wsm) + (size_t)p.g.agent_stride * 4;
+  uint16_t* s_pos = reinterpret_cast<uint16_t*>(aux + FusedSmem::pos);
+  uint32_t* s_grid = reinterpret_cast<uint32_t*>(aux + FusedSmem::grid);
+  uint64_t* s_mask = reinterpret_cast<uint64_t*>(aux + FusedSmem::mask);
+  uint8_t* s_done = reinterpret_cast<uint8_t*>(aux + FusedSmem::done);
+  const uint64_t t = *rio.step;                                  // this launch's step (all workgroups read it first)
+  const int c = (int)(t % (uint64_t)rio.chunk_len), pb = (int)(t & 1);
+  const bool designated = second && agent == 0;                 // writes the env-level outputs of the tile
+  const bool flagged = reinterpret_cast<const int*>(p.packed + 2 * p.g.agent_stride * p.N)[agent] != 0;
+
+  // ---- weight image DMA first (fp16x3 image, or the exact-f32 image of a range-guard-flagged agent)
+  {
+    const float* src = p.packed + (flagged ? 0 : (int64_t)p.N * p.g.agent_stride) + (int64_t)agent * p.g.agent_stride;
+    const int nchunk = (int)(p.g.agent_stride >> 8);
+    for (int ch = wave; ch < nchunk; ch += 16)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ch * 256 + lane * 4),
+                                       (__attribute__((address_space(3))) void*)(wsm + ch * 256), 16, 0, 0);
+  }
+  // ---- the wave's own hidden state (h3 path: 16 envs per wave) and the target net's reset flag (done_{t-1})
+  const mm_qfwd_io& io = p.io;
+  const int e = e0 + wave * 16 + (lane & 15);
+  const int g4 = lane >> 4;
+  const int ec = min(e, (int)E - 1);
+  f32x4 h0[H / 16];
+  if (!flagged) {
+    const float* hp = io.h_in + (int64_t)ec * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)(4 * g4) * io.hin_sf;
+#pragma unroll
+    for (int tt = 0; tt < H / 16; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h0[tt][r] = hp[(int64_t)(16 * tt + r) * io.hin_sf];
+  }
+  const bool reset_prev = rio.done[(int64_t)(pb ^ 1) * E + ec] != 0;
+
+  // ---- the tile's env transitions, one thread per env (threads 0..255)
+  int32_t* s_row = reinterpret_cast<int32_t*>(aux + FusedSmem::row);
+  const int le = tid;
+  const int64_t ee = e0 + le;
+  const bool ok_env = ee < E;
+  const int64_t es = ok_env ? ee : E - 1;
+  int pr[8], pc[8];
+  uint32_t* g = s_grid + min(le, FS_ENVS - 1) * 8;
+  int steps = 0, apples = 0;
+  int64_t row = 0;
+  if (tid < FS_ENVS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int pp = j < N ? ev.pos[pb][es * N + j] : -1;
+      pr[j] = j < N ? (pp >> 8) : -100;
+      pc[j] = j < N ? (pp & 255) : -100;
+    }
+    const int8_t* gs = ev.grid[pb] + es * RC;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      uint32_t word = 0;
+      for (int i = 0; i < 16; ++i) {
+        const int idx = w * 16 + i;
+        if (idx < RC) word |= (uint32_t)(gs[idx] & 3) << (2 * i);
+      }
+      g[w] = word;
+    }
+    steps = ev.steps[pb][es];
+    apples = ev.apples[pb][es];
+    row = rio.staging[es];
+    s_row[le] = (int32_t)row;
+    if (!second && c == 0) fs_publish(ev, pr, pc, g, agent, s_pos + le * 8, s_mask + le * 4);
+  }
+  if (!second && c == 0) {   // chunk start: s_t of this agent into store slot 0 (block-uniform branch)
+    __syncthreads();
+    fs_store_obs(ev, rio, agent, e0, 0, s_pos, s_mask, s_row);
+    __syncthreads();
+  }
+  if (tid < FS_ENVS) {
+    // dynamics (agents in id order; a move is blocked by the border or a cell held by another agent)
+    const int32_t* actp = rio.act + (int64_t)(t % 3) * EN + es * N;
+    steps += 1;
+    float rw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      rw[k] = 0.f;
+      if (k < N) {
+        const int ak = actp[k];
+        const int nr = pr[k] + (ak == 0 ? 1 : (ak == 2 ? -1 : 0));
+        const int nc = pc[k] + (ak == 1 ? -1 : (ak == 3 ? 1 : 0));
+        bool okm = nr >= 0 && nr < ev.R && nc >= 0 && nc < ev.C;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) okm = okm && (j == k || pr[j] != nr || pc[j] != nc);
+        if (okm) {
+          pr[k] = nr;
+          pc[k] = nc;
+        }
+        const int cell = pr[k] * ev.C + pc[k];
+        const int item = fs_cell(g, cell);
+        const bool big = (k & 1) == 0;
+        rw[k] = ev.step_cost + (item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f));
+        apples -= item == 2 ? 1 : 0;
+        g[cell >> 4] &= ~(3u << ((cell & 15) * 2));
+      }
+    }
+    const bool dn = steps >= ev.max_steps || apples == 0;
+    fs_publish(ev, pr, pc, g, agent, s_pos + le * 8, s_mask + le * 4);
+    s_done[le] = dn ? 1 : 0;
+    if (designated && ok_env) {
+      // env-level outputs: next state (auto-reset where done) into buffer pb ^ 1, rewards, done, cur_row
+      const int nb = pb ^ 1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < N) {
+          ev.pos[nb][ee * N + j] = dn ? ev.init_pos[j] : ((pr[j] << 8) | pc[j]);
+          rio.rew[(int64_t)pb * EN + ee * N + j] = rw[j];
+        }
+      int8_t* gd = ev.grid[nb] + ee * RC;
+      for (int i = 0; i < RC; ++i) gd[i] = dn ? ev.init_grid[i] : (int8_t)fs_cell(g, i);
+      ev.steps[nb][ee] = dn ? 0 : steps;
+      ev.apples[nb][ee] = dn ? ev.init_apples : apples;
+      rio.done[(int64_t)pb * E + ee] = dn ? 1 : 0;
+      rio.cur_row[ee] = dn ? -1 : row;
+      // the TD / store of step t - 1 (td_chunk_kernel's arithmetic, agent-order sums)
+      if (rio.td_on && c != 0) {
+        const int pp = pb ^ 1;
+        const int64_t r1 = (int64_t)((t + 2) % 3) * EN + ee * N;   // slot of step t - 1 in the 3-rings
+        float sr = 0.f, sq = 0.f, smx = 0.f;
+        for (int j = 0; j < N; ++j) {
+          const float rj = rio.rew[(int64_t)pp * EN + ee * N + j];
+          sr += rj;
+          sq += rio.qsel[r1 + j];
+          smx += rio.maxq[(int64_t)pp * EN + ee * N + j];
+          rio.store_act[(row * rio.chunk_len + c - 1) * N + j] = (uint8_t)rio.act[r1 + j];
+          rio.store_rew[(row * rio.chunk_len + c - 1) * N + j] = rj;
+        }
+        const uint8_t dprev = rio.done[(int64_t)pp * E + ee];
+        const float dd = dprev ? 1.0f : 0.0f;
+        const float td = fabsf(sr + (1.0f - dd) * rio.gamma * smx - sq);
+        rio.chunk_td[ee] = (c - 1 == 0 ? 0.0f : rio.chunk_td[ee]) + td;
+        rio.store_done[row * rio.chunk_len + c - 1] = dprev;
+      }
+    }
+  }
+  __syncthreads();   // weight image landed (the barrier waits vmcnt(0)), LDS state complete
+  if (!second) fs_store_obs(ev, rio, agent, e0, c + 1, s_pos, s_mask, s_row);   // s'_t into store slot c + 1
+
+  const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
+  const int64_t out_off = second ? (int64_t)((t + 1) % 3) * EN : (int64_t)pb * EN;
+  if (flagged) {
+    // range guard (qnet_h3_bound_block): the exact-f32 image, 8 waves x 32 envs
+    const int le32 = wave * 32 + (lane & 31);
+    const int e32 = e0 + le32;
+    const int hh = lane >> 5;
+    const int lc = min(le32, FS_ENVS - 1);
+    const bool reset_obs = second && s_done[lc];
+    auto ol32 = [&](int kb, float (&x)[16]) {
+#pragma unroll
+      for (int sidx = 0; sidx < 16; ++sidx) {
+        const int f = kb * 32 + kperm(sidx, hh);
+        float v = 0.f;
+        if (e32 < E && f < ev.D)
+          v = reset_obs ? ev.reset_obs[agent * ev.D + f] : fs_feature(ev, s_pos + lc * 8, s_mask + lc * 4, agent, f);
+        x[sidx] = v;
+      }
+    };
+    if (wave < 8) {
+      float x32[16];
+      ol32(0, x32);
+      const bool zero_h = e32 >= E || (second ? s_done[lc] != 0 : rio.done[(int64_t)(pb ^ 1) * E + min(e32, (int)E - 1)] != 0);
+      QFwdParams q = p;
+      q.io.act_out = io.act_out ? io.act_out + out_off : nullptr;
+      q.io.qsel_out = io.qsel_out ? io.qsel_out + out_off : nullptr;
+      q.io.counter = t;
+      q.io.counter_ptr = nullptr;
+      agent_q_fwd_body<F1, G, H, AB>(q, agent, e32, wsm, ol32, x32, zero_h);
+    }
+  } else {
+    const int le = wave * 16 + (lane & 15);
+    const bool reset_obs = second && s_done[le];
+    auto ol = [&](int kb, float (&x)[8]) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = kb * 32 + kperm16(j, g4);
+        float v = 0.f;
+        if (e < E && f < ev.D)
+          v = reset_obs ? ev.reset_obs[agent * ev.D + f] : fs_feature(ev, s_pos + le * 8, s_mask + le * 4, agent, f);
+        x[j] = v;
+      }
+    };
+    float xn[8];
+    ol(0, xn);
+    const bool zero_h = e >= E || (second ? s_done[le] != 0 : reset_prev);
+    if (zero_h) {
+#pragma unroll
+      for (int tt = 0; tt < H / 16; ++tt) h0[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (wave >= 8)
+      for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(8);
+    agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm, ol, xn, h0, eps, t, out_off);
+  }
+
+  // ---- the last workgroup to finish advances the step counter (every workgroup has read it by then)
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    if (atomicAdd(reinterpret_cast<unsigned long long*>(&rio.step[1]), 1ull) == (unsigned long long)gridDim.x - 1) {
+      rio.step[0] = t + 1;
+      rio.step[1] = 0;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- packing
@@ -1690,11 +1967,7 @@ static int launch_fwd(QFwdParams p0, const QFwdParams* p1in, hipStream_t s) {
     p1.nblocks = (p1.E + 255) / 256 * p1.N;
     const int nb = p0.nblocks + (p1in ? p1.nblocks : 0);
     const size_t sm = (size_t)p0.g.agent_stride * 4;
-    static const bool f32_exact = getenv("MM_FWD_F32") && atoi(getenv("MM_FWD_F32"));
-    if (f32_exact)
-      hipLaunchKernelGGL((agent_q_fwd_lds_kernel<F1, G, H, AB>), dim3(nb), dim3(512), sm, s, p0, p1);
-    else
-      hipLaunchKernelGGL((agent_q_fwd_h3_kernel<F1, G, H, AB>), dim3(nb), dim3(1024), sm, s, p0, p1);
+    hipLaunchKernelGGL((agent_q_fwd_h3_kernel<F1, G, H, AB>), dim3(nb), dim3(1024), sm, s, p0, p1);
   } else {
     const int nb = p0.nblocks + (p1in ? p1.nblocks : 0);
     hipLaunchKernelGGL((agent_q_fwd_kernel<F1, G, H, AB>), dim3(nb), dim3(256), 0, s, p0, p1);
@@ -1717,10 +1990,8 @@ static int make_params(const mm_qnet_dims* d, const float* packed, const mm_qfwd
   p->D = d->obs_dim;
   p->A = d->n_actions;
   p->nblocks = (int)((n_envs + 127) / 128) * d->n_agents;
-  static const int stagger = getenv("MM_FWD_STAGGER") ? atoi(getenv("MM_FWD_STAGGER")) : 4;
-  p->stagger = stagger;
-  static const int dbg = getenv("MM_FWD_DBG") ? atoi(getenv("MM_FWD_DBG")) : 0;
-  p->dbg = dbg;
+  p->stagger = 4;   // fp16x3 kernel: waves 8-15 start 4 x s_sleep(8) late (VALU phases under the others' MFMAs)
+  p->dbg = 0;
   MM_REQUIRE(io->obs, "agent_q_fwd: obs required");
   MM_REQUIRE(io->h_in || io->reset == nullptr, "agent_q_fwd: h_in required");
   MM_REQUIRE(io->mode != MM_Q_GATHER || io->act_in, "agent_q_fwd: GATHER needs act_in");
@@ -1743,8 +2014,7 @@ static int launch_split(int phase, QFwdParams p0, QFwdParams p1, hipStream_t s) 
   const bool single = p1.nblocks == 0;   // one net only (agent_q_split2 with io1 == NULL)
   if (phase == 1) {
     const int t0 = (p0.E + 31) / 32 * p0.N, t1 = single ? 0 : (p1.E + 31) / 32 * p1.N;
-    static const char* rb_env = getenv("MM_PRE_RB");   // "0": the 128-rows-per-block PRE (A/B)
-    if (t0 + t1 <= 2048 && p0.g.KD <= kPreRbMaxKD && !(rb_env && rb_env[0] == '0')) {
+    if (t0 + t1 <= 2048 && p0.g.KD <= kPreRbMaxKD) {
       // small batches: row blocks of each layer on separate waves (latency-bound regime)
       p0.nblocks = t0;
       p1.nblocks = t1;
@@ -1787,11 +2057,8 @@ static int launch_rec_seq(QFwdParams p0, QFwdParams p1, const RecSeq& s0, const 
   p0.nblocks = (p0.E + 31) / 32 * p0.N;
   p1.nblocks = single ? 0 : (p1.E + 31) / 32 * p1.N;
   // few tiles (small learner batches): gate-parallel waves shorten each step's dependent MFMA chain 3x;
-  // many tiles: the 2-wave kernel keeps more blocks per CU (MM_REC_GP=0/1 forces one, A/B)
-  const char* gp_env = getenv("MM_REC_GP");
-  static const int rdbg = getenv("MM_REC_DBG") ? atoi(getenv("MM_REC_DBG")) : 0;
-  p0.dbg = p1.dbg = rdbg;
-  const bool gp = gp_env ? gp_env[0] == '1' : (p0.nblocks + p1.nblocks) < 512;
+  // many tiles: the 2-wave kernel keeps more blocks per CU
+  const bool gp = (p0.nblocks + p1.nblocks) < 512;
   if (gp) {
     hipLaunchKernelGGL((agent_rec_seq_gp_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks),
                        dim3(64 * (3 * (H / 32) + 1)), 0, s, p0, p1, s0, s1);
@@ -1862,6 +2129,84 @@ int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const
   MM_REQUIRE(io0->gi && io1->gi, "agent_q_split: io.gi required");
   MM_REQUIRE(phase == 2 || (io0->obs && io1->obs), "agent_q_pre: obs required");
   return dispatch_split(d, phase, p0, p1, s);
+}
+
+// ---- fused rollout step (mm_rollout_step)
+static bool rollout_fits(const QFwdParams& p) {
+  return (size_t)p.g.agent_stride * 4 + FusedSmem::total <= 160 * 1024;
+}
+
+template <int F1, int G, int H, int AB>
+static int launch_rollout(QFwdParams p0, QFwdParams p1, const FusedEnv& ev, const mm_rollout_io& rio, hipStream_t s) {
+  p0.nblocks = (p0.E + FS_ENVS - 1) / FS_ENVS * p0.N;
+  p1.nblocks = (p1.E + FS_ENVS - 1) / FS_ENVS * p1.N;
+  const size_t sm = (size_t)p0.g.agent_stride * 4 + FusedSmem::total;
+  static bool attr = false;
+  if (!attr) {
+    MM_HIP_CHECK(hipFuncSetAttribute((const void*)rollout_step_h3_kernel<F1, G, H, AB>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+    attr = true;
+  }
+  hipLaunchKernelGGL((rollout_step_h3_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(1024), sm, s, p0, p1,
+                     ev, rio);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int rollout_step_supported(mm_env* env, const mm_qnet_dims* d, int64_t n_envs, FusedEnv* ev, QFwdParams* p) {
+  FusedEnv v;
+  int rc = env_fused_view(env, &v);
+  if (rc) return rc;
+  MM_REQUIRE(d && d->n_agents == v.N && d->obs_dim == v.D, "rollout_step: net dims do not match the env");
+  MM_REQUIRE(n_envs == v.E && n_envs >= 2048, "rollout_step: needs the env's E >= 2048 envs (got %lld)",
+             (long long)n_envs);
+  QnetOffsets o;
+  QFwdParams q{};
+  rc = qnet_geometry(d, &q.g, &o);
+  if (rc) return rc;
+  MM_REQUIRE(rollout_fits(q), "rollout_step: weight image + env state exceed the LDS");
+  const bool shape = (d->f1 == 64 && d->g == 32 && d->h == 32) || (d->f1 == 64 && d->g == 64 && d->h == 64) ||
+                     (d->f1 == 128 && d->g == 32 && d->h == 32) || (d->f1 == 64 && d->g == 32 && d->h == 64);
+  MM_REQUIRE(shape, "rollout_step: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
+  if (ev) *ev = v;
+  if (p) *p = q;
+  return MM_OK;
+}
+
+int rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
+                 const float* packed_b, const mm_qfwd_io* io_b, const mm_rollout_io* rio, hipStream_t s) {
+  MM_REQUIRE(rio && io_t && io_b && packed_t && packed_b, "rollout_step: null argument");
+  MM_REQUIRE(rio->store_obs && rio->store_act && rio->store_rew && rio->store_done && rio->staging && rio->cur_row &&
+                 rio->chunk_td && rio->act && rio->qsel && rio->maxq && rio->rew && rio->done && rio->step &&
+                 rio->chunk_len >= 1,
+             "rollout_step: null buffer in the rollout io");
+  MM_REQUIRE(io_t->mode == MM_Q_MAX && io_b->mode == MM_Q_ACT && io_t->qsel_out && io_b->act_out && io_b->qsel_out,
+             "rollout_step: target MM_Q_MAX -> maxq ring, behavior MM_Q_ACT -> act / qsel rings");
+  MM_REQUIRE(io_t->h_in && io_t->h_out && io_b->h_in && io_b->h_out, "rollout_step: hidden states required");
+  FusedEnv ev;
+  int rc = env_fused_view(env, &ev);
+  if (rc) return rc;
+  rc = rollout_step_supported(env, d, ev.E, nullptr, nullptr);
+  if (rc) return rc;
+  MM_REQUIRE(rio->row_stride >= (int64_t)(rio->chunk_len + 1) * ev.N * ev.D, "rollout_step: row_stride too small");
+  QFwdParams p0, p1;
+  mm_qfwd_io i0 = *io_t, i1 = *io_b;
+  i0.obs = i1.obs = ev.reset_obs;   // unused (the obs come from the env state); make_params wants a pointer
+  rc = make_params(d, packed_t, &i0, ev.E, &p0);
+  if (rc) return rc;
+  rc = make_params(d, packed_b, &i1, ev.E, &p1);
+  if (rc) return rc;
+  const int AB = (d->n_actions + 31) / 32;
+#define MM_ROLL(F1_, G_, H_)                                                                                 \
+  if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                              \
+    return AB == 1 ? launch_rollout<F1_, G_, H_, 1>(p0, p1, ev, *rio, s) : launch_rollout<F1_, G_, H_, 2>(p0, p1, ev, *rio, s);
+  MM_ROLL(64, 32, 32)
+  MM_ROLL(64, 64, 64)
+  MM_ROLL(128, 32, 32)
+  MM_ROLL(64, 32, 64)
+#undef MM_ROLL
+  set_error("rollout_step: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
+  return MM_EINVAL;
 }
 
 int agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs, hipStream_t s) {

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "common.h"
+#include "fused_env.h"
 #include "minimarl.h"
 
 namespace mm {
@@ -33,6 +34,11 @@ struct EnvDev {
   const int8_t* init_grid;  // [R*C]
   const int32_t* init_pos;  // [N]
   float* reset_obs;         // [N][D]
+  // the second state copy of the fused rollout step (fused_env.h), same layouts
+  int32_t* pos2;
+  int8_t* grid2;
+  int32_t* steps2;
+  int32_t* apples2;
 };
 }  // namespace mm
 
@@ -456,7 +462,8 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
     return o;
   };
   const size_t o_pos = take(E * d.N * 4), o_grid = take(E * RC), o_steps = take(E * 4), o_apples = take(E * 4),
-               o_igrid = take(RC), o_ipos = take(d.N * 4), o_robs = take((size_t)d.N * d.D * 4);
+               o_igrid = take(RC), o_ipos = take(d.N * 4), o_robs = take((size_t)d.N * d.D * 4),
+               o_pos2 = take(E * d.N * 4), o_grid2 = take(E * RC), o_steps2 = take(E * 4), o_apples2 = take(E * 4);
   void* base = nullptr;
   MM_HIP_CHECK(hipMalloc(&base, off));
   char* b = static_cast<char*>(base);
@@ -467,6 +474,10 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   d.init_grid = reinterpret_cast<int8_t*>(b + o_igrid);
   d.init_pos = reinterpret_cast<int32_t*>(b + o_ipos);
   d.reset_obs = reinterpret_cast<float*>(b + o_robs);
+  d.pos2 = reinterpret_cast<int32_t*>(b + o_pos2);
+  d.grid2 = reinterpret_cast<int8_t*>(b + o_grid2);
+  d.steps2 = reinterpret_cast<int32_t*>(b + o_steps2);
+  d.apples2 = reinterpret_cast<int32_t*>(b + o_apples2);
   MM_HIP_CHECK(hipMemcpy(b + o_igrid, grid.data(), RC, hipMemcpyHostToDevice));
   MM_HIP_CHECK(hipMemcpy(b + o_ipos, pos.data(), d.N * 4, hipMemcpyHostToDevice));
   mm_env* env = new mm_env;
@@ -515,6 +526,37 @@ int env_step(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, 
 }
 
 const float* env_reset_obs(const mm_env* env) { return env->d.reset_obs; }
+
+int env_fused_view(mm_env* env, FusedEnv* v) {
+  MM_REQUIRE(env && v, "env_fused_view: null argument");
+  const EnvDev& d = env->d;
+  MM_REQUIRE(d.N <= 8 && d.R * d.C <= 128 && d.R <= 255 && d.C <= 255,
+             "fused rollout step: needs N <= 8 agents and a grid of <= 128 cells (N=%d, %dx%d)", d.N, d.R, d.C);
+  MM_REQUIRE(!d.full_obs || d.N <= 4, "fused rollout step: full observation needs N <= 4 (N=%d)", d.N);
+  v->E = d.E;
+  v->N = d.N;
+  v->R = d.R;
+  v->C = d.C;
+  v->D = d.D;
+  v->max_steps = d.max_steps;
+  v->full_obs = d.full_obs;
+  v->init_apples = d.init_apples;
+  v->step_cost = d.step_cost;
+  v->inv_r = d.inv_r;
+  v->inv_c = d.inv_c;
+  v->pos[0] = d.pos;
+  v->pos[1] = d.pos2;
+  v->grid[0] = d.grid;
+  v->grid[1] = d.grid2;
+  v->steps[0] = d.steps;
+  v->steps[1] = d.steps2;
+  v->apples[0] = d.apples;
+  v->apples[1] = d.apples2;
+  v->init_grid = d.init_grid;
+  v->init_pos = d.init_pos;
+  v->reset_obs = d.reset_obs;
+  return MM_OK;
+}
 
 }  // namespace mm
 
@@ -566,6 +608,23 @@ int mm_env_step_rows_begin(mm_env* env, const int32_t* act, float* store_obs, in
   return mm::env_step(env, act, store_obs + nd, row_stride, staging, nullptr, cur_row, rew, done, nullptr,
                       (hipStream_t)s, &bc);
 }
+int mm_env_copy_state(mm_env* env, int32_t from, int32_t to, mm_stream_t s) {
+  MM_REQUIRE(env && (from == 0 || from == 1) && (to == 0 || to == 1), "env_copy_state: bad arguments");
+  if (from == to) return MM_OK;
+  const mm::EnvDev& d = env->d;
+  const size_t E = (size_t)d.E, RC = (size_t)d.R * d.C;
+  int32_t* pos[2] = {d.pos, d.pos2};
+  int8_t* grid[2] = {d.grid, d.grid2};
+  int32_t* steps[2] = {d.steps, d.steps2};
+  int32_t* apples[2] = {d.apples, d.apples2};
+  const hipStream_t st = (hipStream_t)s;
+  MM_HIP_CHECK(hipMemcpyAsync(pos[to], pos[from], E * d.N * 4, hipMemcpyDeviceToDevice, st));
+  MM_HIP_CHECK(hipMemcpyAsync(grid[to], grid[from], E * RC, hipMemcpyDeviceToDevice, st));
+  MM_HIP_CHECK(hipMemcpyAsync(steps[to], steps[from], E * 4, hipMemcpyDeviceToDevice, st));
+  MM_HIP_CHECK(hipMemcpyAsync(apples[to], apples[from], E * 4, hipMemcpyDeviceToDevice, st));
+  return MM_OK;
+}
+
 int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples) {
   if (!env) return MM_EINVAL;
   const mm::EnvDev& d = env->d;

@@ -2527,9 +2527,8 @@ int mm_mixer_gi(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, const f
   a.Hm = Hm;
   a.K1 = K1;
   a.N = N;
-  const char* gm_env = getenv("MM_GI_TILED");   // "0": the register-operand kernel
   // small R (B = 32 updates): the split-K register kernel gives more blocks and wins
-  if (R >= 2048 && !(gm_env && gm_env[0] == '0')) {
+  if (R >= 2048) {
     dim3 grid((3 * Hm + 63) / 64, (R + 63) / 64, P1 ? 2 : 1);
     hipLaunchKernelGGL(mm::mixer_gi_tiled_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
     MM_HIP_CHECK(hipGetLastError());
@@ -2599,10 +2598,8 @@ int mm_lrn_loss(int32_t B, int32_t C, int32_t N, float gamma, const float* rew, 
   return MM_OK;
 }
 
-static bool mix_split_enabled() {
-  const char* e = getenv("MM_MIX_SPLIT");   // "0": the one-kernel LDS sequence paths (A/B, tests)
-  return !(e && e[0] == '0');
-}
+static bool mix_split_enabled() { return true; }   // split recurrence / hypernet launches (the LDS sequence kernels
+                                                    // remain the fallback for shapes the split path does not take)
 // steps per LDS window of the serial mixer kernels
 static int mix_rec_win(int C, int Hm, bool bwd) {
   int win = C;
@@ -2665,8 +2662,7 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
     return MM_OK;
   }
   const mm::MixSeqGeo g(Hm, K1, N);
-  const char* lds_env = getenv("MM_MIX_LDS");   // "0" forces the L2-streamed kernel (A/B, tests)
-  if (g.bwd_floats() * 4 <= mm::kMixSeqLds && g.step_in() <= 1024 && !(lds_env && lds_env[0] == '0')) {
+  if (g.bwd_floats() * 4 <= mm::kMixSeqLds && g.step_in() <= 1024) {
     const int rc = mm::mix_seq_lds_setup();
     if (rc) return rc;
     hipLaunchKernelGGL(mm::mixer_bwd_seq_lds_kernel, dim3(B), dim3(256), g.bwd_floats() * 4, (hipStream_t)s, a, q);
@@ -2681,8 +2677,6 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
 
 int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1) {
   const mm::MixSeqGeo g(Hm, K1, N);
-  const char* lds_env = getenv("MM_MIX_LDS");
-  if (lds_env && lds_env[0] == '0') return 0;
   if (mix_split_enabled())
     return B < 512 && mm::mix_rec_supported(Hm) && mm::mix_rec_fwd_floats(Hm, 1) * 4 <= mm::kMixSeqLds &&
            mm::mix_hyper_fwd_floats(Hm, K1, N) * 4 <= 64 * 1024;
@@ -2955,9 +2949,8 @@ int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
                    x->M, x->R, x->Cc, 0};
   a.aligned16 = (x->R % 4 == 0 && x->x_m % 4 == 0 && x->x_g % 4 == 0 && x->Cc % 4 == 0 && x->w_g % 4 == 0 &&
                  (uintptr_t)x->X % 16 == 0 && (uintptr_t)x->W % 16 == 0);
-  const char* tm_env = getenv("MM_TMV_MFMA");   // "0": the scalar LDS-tiled kernel
   // small M (B = 32 updates): the 32 x 32 scalar tiles give more blocks and win
-  if (x->M >= 2048 && !(tm_env && tm_env[0] == '0')) {
+  if (x->M >= 2048) {
     dim3 grid((x->Cc + 63) / 64, (x->M + 63) / 64, x->groups);
     hipLaunchKernelGGL(mm::tmv_mfma_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
     MM_HIP_CHECK(hipGetLastError());

@@ -22,7 +22,6 @@ Adam moments alike), the layout the RCCL gradient all-reduce works on.
 """
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -119,7 +118,7 @@ class QLearner:
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM
         # chunk-sequence launches: agent REC and mixer backward as one launch each for all C steps
-        self.seq = not self.double and os.environ.get("MM_LRN_SEQ", "1") != "0"
+        self.seq = not self.double
         self.double_eps = 0.0          # epsilon of the double net's sample_action (vdn/_train.py:124-125)
         self.double_seed = 0x5eed
         self._draws = None

@@ -167,9 +167,6 @@ class QTrainer:
         return {"test_score": score, "test_loss": loss}
 
     # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)
-    _ENGINE_BUFFERS = ("cur_row", "init_obs", "h", "ht", "maxq", "rew", "chunk_td", "eps_dev", "counter_dev",
-                       "staging")
-
     def checkpoint_tensors(self, include_replay=True):
         """Learner (params, targets, Adam), replay (tree, slot map, annealed alpha / beta, sample counter),
         engine (hiddens, RNG step counter, current-obs rows, staging rows), env integer state and, with
@@ -180,14 +177,11 @@ class QTrainer:
         out = {"learner/" + k: v for k, v in ts.items()}
         pts, _ = eng.per.checkpoint_tensors()
         out.update({"per/" + k: v for k, v in pts.items()})
+        eng.env_state_to_live()          # fused mode: the env state of parity t % 2 into the env's live buffer
         ets, _ = eng.env.checkpoint_tensors()
         out.update({"env/" + k: v for k, v in ets.items()})
-        for k in self._ENGINE_BUFFERS:
-            out["engine/" + k] = getattr(eng, k)
-        for k in range(2):
-            out[f"engine/done_buf{k}"] = eng.done_buf[k]
-            out[f"engine/act_buf{k}"] = eng.act_buf[k]
-            out[f"engine/qsel_buf{k}"] = eng.qsel_buf[k]
+        for k, v in eng.state_buffers().items():
+            out["engine/" + k] = v
         if include_replay:
             for k in ("obs", "act", "rew", "done"):
                 out["store/" + k] = getattr(eng.store, k)
@@ -204,18 +198,17 @@ class QTrainer:
         self.learner.restore_tensors({k[8:]: v for k, v in ts.items() if k.startswith("learner/")}, scalars["learner"])
         eng.per.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("per/")})
         eng.env.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("env/")})
-        for k in self._ENGINE_BUFFERS:
-            copy_into(getattr(eng, k), ts["engine/" + k], k)
-        for k in range(2):
-            copy_into(eng.done_buf[k], ts[f"engine/done_buf{k}"], "done_buf")
-            copy_into(eng.act_buf[k], ts[f"engine/act_buf{k}"], "act_buf")
-            copy_into(eng.qsel_buf[k], ts[f"engine/qsel_buf{k}"], "qsel_buf")
+        for k, v in eng.state_buffers().items():
+            if "engine/" + k not in ts:
+                raise ValueError(f"checkpoint lacks engine/{k} (saved by an engine in the other step mode?)")
+            copy_into(v, ts["engine/" + k], k)
         if scalars.get("replay_saved"):
             for k in ("obs", "act", "rew", "done"):
                 copy_into(getattr(eng.store, k), ts["store/" + k], k)
         copy_into(self.ep_ret, ts["trainer/ep_ret"], "ep_ret")
         copy_into(self.score_acc, ts["trainer/score_acc"], "score_acc")
         eng.t, eng.chunks_inserted = int(scalars["t"]), int(scalars["chunks_inserted"])
+        eng.env_state_from_live()
         eng._primed, eng._td_pending = bool(scalars["primed"]), bool(scalars["td_pending"])
         eng._eps_host = None
         eng.behavior.mark_dirty()

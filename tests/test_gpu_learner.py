@@ -187,8 +187,11 @@ def test_learner_cfg5_benched_path_vs_oracle(mixer_fp16):
     post-Adam params atol 2e-6 where |g| > 1e-3 max). fp16 mode, derived from SURVEY 8c's separate
     rtol 2e-3 on Q_tot: Q_tot, the loss and the TD errors rtol 2e-3; every gradient tensor
     |g - g_ref| <= 5e-3 * max|g_ref| + 1e-2 * |g_ref| (gradients inherit the Q_tot error through
-    dQ_tot and the f16-rounded state operand of the mixer's W_ih gradient); post-Adam params atol 2e-6
-    where |g_ref| > 2e-2 * max|g_ref| (Adam's first step is lr * sign(g): only gradients well above the
+    dQ_tot and the f16-rounded state operand of the mixer's W_ih gradient) on at least 97 % of its
+    elements and a relative L2 error <= 2e-2 over the whole tensor — the rest are the mixer's
+    |W1| / |W2| / ReLU kinks: a hypernet output within the f16 error of 0 takes the other branch
+    (measured: 1.6 % of m.w1W); post-Adam params atol 2e-6 where |g_ref| > 2e-2 * max|g_ref| and the
+    gradient is within its bound (Adam's first step is lr * sign(g): only gradients well above the
     error bar have a pinned sign)."""
     from minimarl.learner import MIX_KEYS, Mixer, QLearner
     from minimarl.qnet import AgentQNet
@@ -219,33 +222,88 @@ def test_learner_cfg5_benched_path_vs_oracle(mixer_fp16):
     coef = min(1.0, 5.0 / (float(L.norm[0].item()) + 1e-6))
     if mixer_fp16:
         rt, ga, gr, psel = 2e-3, 5e-3, 1e-2, 2e-2
+        kink_frac, rel_l2 = 0.03, 2e-2
         np.testing.assert_allclose(L.qtot.cpu().numpy(), qtot_ref.numpy(), rtol=rt,
                                    atol=rt * float(qtot_ref.abs().max()))
         np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=rt)
         np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=rt, atol=rt * float(td.abs().max()))
     else:
         ga, gr, psel = 2e-4, 1e-3, 1e-3
+        kink_frac, rel_l2 = 0.0, None
         np.testing.assert_allclose(L.qtot.cpu().numpy(), qtot_ref.numpy(), rtol=1e-4,
                                    atol=1e-4 * float(qtot_ref.abs().max()))
         np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=1e-4)
         np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=1e-4, atol=1e-4)
 
     def close(g_dev, g_ref, what):
+        """-> mask of the elements within the elementwise bound; in fp16 mode up to kink_frac of a tensor may
+        sit outside it (hypernet outputs / pre-activations within the f16 error of 0 flip the |.| or ReLU
+        branch) as long as the tensor's relative L2 error stays within rel_l2."""
         scale = np.abs(g_ref).max()
-        np.testing.assert_array_less(np.abs(g_dev - g_ref), ga * scale + gr * np.abs(g_ref) + 1e-12, err_msg=what)
+        ok = np.abs(g_dev - g_ref) <= ga * scale + gr * np.abs(g_ref) + 1e-12
+        if kink_frac == 0.0:
+            np.testing.assert_array_less(np.abs(g_dev - g_ref), ga * scale + gr * np.abs(g_ref) + 1e-12, err_msg=what)
+            return ok
+        assert 1.0 - ok.mean() <= kink_frac, (what, 1.0 - ok.mean())
+        err = np.linalg.norm(g_dev - g_ref) / max(np.linalg.norm(g_ref), 1e-30)
+        assert err <= rel_l2, (what, err)
+        return ok
 
     for key in nets.AGENT_KEYS:
         g_ref = grads[key].numpy()
-        close(_grad_view(L, key).cpu().numpy() * coef, g_ref, key)
-        sel = np.abs(g_ref) > psel * np.abs(g_ref).max()
+        ok = close(_grad_view(L, key).cpu().numpy() * coef, g_ref, key)
+        sel = (np.abs(g_ref) > psel * np.abs(g_ref).max()) & ok
         np.testing.assert_allclose(L.beh.view(key).cpu().numpy()[sel], newP[key].numpy()[sel], atol=2e-6,
                                    err_msg=key)
     for key in MIX_KEYS:
         g_ref = grads["m." + key].numpy()
-        close(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy(), g_ref, "m." + key)
-        sel = np.abs(g_ref) > psel * np.abs(g_ref).max()
+        ok = close(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy(), g_ref, "m." + key)
+        sel = (np.abs(g_ref) > psel * np.abs(g_ref).max()) & ok
         np.testing.assert_allclose(L.mix.view(key).cpu().numpy()[sel], newM[key].numpy()[sel], atol=2e-6,
                                    err_msg="m." + key)
+
+
+@pytest.mark.parametrize("mode", ["qmix", "vdn"])
+def test_learner_switch_shapes_vs_oracle(mode):
+    """The Switch2 shapes QMIX trains on by default (qmix/_config.py:14-19): 2 agents, obs D = 3 (one partial
+    32-deep k-step), GRU-32 agents, Hm = 32 mixer over the 6-wide state; B = 32, C = 10, dones inside the
+    chunks. Loss rtol 1e-4, gradients 2e-4 * max + 1e-3 * |g| vs the torch-CPU oracle."""
+    from minimarl.learner import MIX_KEYS, Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    N, D, A, B, C = 2, 3, 5, 32, 10
+    beh = AgentQNet(N, D, A, 64, 32, 32, DEV, seed=21)
+    tgt = AgentQNet(N, D, A, 64, 32, 32, DEV, seed=22)
+    mix = tmix = None
+    if mode == "qmix":
+        mix, tmix = Mixer(N, N * D, 32, 32, DEV, seed=23), Mixer(N, N * D, 32, 32, DEV, seed=24)
+    P0 = {k: v.detach().cpu().clone() for k, v in beh.params().items()}
+    T0 = {k: v.detach().cpu().clone() for k, v in tgt.params().items()}
+    L = QLearner(beh, tgt, mix, tmix, batch=B, chunk=C, mode=mode, device=DEV)
+    g = torch.Generator().manual_seed(4)
+    st = torch.rand(B, C, N, D, generator=g)
+    ns = torch.rand(B, C, N, D, generator=g)
+    act = torch.randint(0, A, (B, C, N), generator=g).float()
+    rew = torch.randn(B, C, N, generator=g)
+    dn = (torch.rand(B, C, 1, generator=g) < 0.15).float()
+    w = torch.rand(B, 1, generator=g) * 0.5 + 0.5
+    batch = (st, act, rew, ns, dn, w)
+    L.load_batch(*batch)
+    if mode == "qmix":
+        M0 = {k: mix.view(k).detach().cpu().clone() for k in MIX_KEYS}
+        TM0 = {k: tmix.view(k).detach().cpu().clone() for k in MIX_KEYS}
+        newP, newM, grads, loss, td = nets.qmix_train_step(P0, M0, T0, TM0, batch, 0.99, 1e-3, 5.0)
+    else:
+        newP, grads, loss, td = nets.vdn_train_step(P0, T0, batch, 0.99, 1e-3, 5.0)
+    L.train_step(L._obs_buf, L._obs_buf)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(float(L.loss.item()), float(loss), rtol=1e-4)
+    np.testing.assert_allclose(L.td_last.cpu().numpy(), td.numpy(), rtol=1e-4, atol=1e-4)
+    coef = min(1.0, 5.0 / (float(L.norm[0].item()) + 1e-6))
+    for key in nets.AGENT_KEYS:
+        _check_grads(_grad_view(L, key).cpu().numpy() * coef, grads[key].numpy())
+    if mode == "qmix":
+        for key in MIX_KEYS:
+            _check_grads(L.mix.view(key, L.Gr[L.n_agent:]).cpu().numpy(), grads["m." + key].numpy())
 
 
 def test_learner_update_from_device_per():

@@ -326,3 +326,56 @@ def test_run_steps_exact_counts_match_eager():
                  (a.staging, b.staging), (a.chunk_td, b.chunk_td), (a.per.tree(), b.per.tree()),
                  (a.per.slot_rows(), b.per.slot_rows())]:
         assert torch.equal(x, y)
+
+
+def _engine_state(e):
+    e.env_state_to_live()
+    torch.cuda.synchronize()
+    st = [e.store.obs, e.store.act, e.store.rew, e.store.done, e.h, e.ht, e.chunk_td, e.cur_row, e.staging,
+          e.per.tree(), e.per.slot_rows(), e.act, e.last_rew, e.last_done]
+    pos, grid, steps, apples = e.env.get_state()
+    return [x.clone() for x in st] + [torch.as_tensor(v) for v in (pos, grid, steps, apples)]
+
+
+@pytest.mark.parametrize("dims,full", [((64, 64, 64), False), ((64, 32, 32), False), ((64, 32, 32), True)])
+def test_fused_step_matches_unfused(dims, full):
+    """The one-launch fused step (env + dual forward + TD(t-1), mm_rollout_step) is bit-identical to the
+    unfused launches: chunk store, hidden states, chunk priorities, PER tree / slot map, env state, through
+    chunk ends and PER eviction, with a flush_td mid-chunk."""
+    from minimarl.engine import RolloutEngine
+    f1, g, h = dims
+    N = 2 if full else 8
+    kw = dict(f1=f1, g=g, h=h, chunk=10, capacity=4096, seed=21, full_observable=full, device=DEV)
+    a = RolloutEngine(2048, N, fused=True, **kw)
+    b = RolloutEngine(2048, N, fused=False, **kw)
+    assert a.fused and not b.fused
+    for t in range(47):
+        a.step(0.3)
+        b.step(0.3)
+        if t == 23:
+            a.flush_td()
+            b.flush_td()
+    a.flush_td()
+    b.flush_td()
+    for i, (x, y) in enumerate(zip(_engine_state(a), _engine_state(b))):
+        assert torch.equal(x.cpu(), y.cpu()), i
+    assert a.t == b.t == 47 and len(a.per) == len(b.per) == 4096
+
+
+def test_fused_graph_replay_matches_eager():
+    """Fused-mode chunk graphs and single-step graphs replay bit-identically to eager fused steps."""
+    from minimarl.engine import RolloutEngine
+    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, device=DEV)
+    a = RolloutEngine(2048, 8, **kw)
+    b = RolloutEngine(2048, 8, **kw)
+    assert a.fused and b.fused
+    for _ in range(33):
+        a.step(0.25)
+    a.flush_td()
+    b.run_steps(3, 0.25)
+    b.run_steps(20, 0.25)
+    b.run_steps(10, 0.25)
+    b.flush_td()
+    for i, (x, y) in enumerate(zip(_engine_state(a), _engine_state(b))):
+        assert torch.equal(x.cpu(), y.cpu()), i
+    assert int(b.step_dev[0]) == 33 and int(b.step_dev[1]) == 0

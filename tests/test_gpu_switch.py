@@ -74,7 +74,7 @@ def test_engine_on_switch_vs_oracle_through_eviction(E, N):
     keep = torch.ones(E, 1, 1)
     near = 0
     n_done = 0
-    for k in range(cap // E + 2):
+    for k in range(cap // E + 8):            # 120 steps: every env reaches the 100-step limit
         rows = eng.staging.cpu().numpy().copy()
         eng.run_graph(eps)
         torch.cuda.synchronize()
