@@ -664,19 +664,32 @@ def main():
     achieved = flops / t_fwd / 1e12
     h3 = E >= 2048 and not os.environ.get("MM_FWD_F32")
     peak = PEAK_F16_TFLOPS / 3 if h3 else PEAK_FP32_TFLOPS
-    # algorithmic HBM bytes per launch: per agent-step obs 4D + hidden in/out 8H + outputs (act/q 8 or max 4)
-    alg_bytes = E * N * ((4 * D + 8 * Hh + 8) + (4 * D + 8 * Hh + 4))
+    if eng.fused:
+        # fused step (rollout_step_h3_kernel: env + both forwards + TD(t-1)). Algorithmic bytes per launch,
+        # per agent-step: hidden in/out of both nets 2 x 8H, the target's s'_t into the chunk store 4D,
+        # act read 4, act / Q(a) / max Q' out 12; per env: state read + write 2 x (4N + RC + 8), rew 4N,
+        # done 1, cur_row 8, and TD(t-1): ring reads 16N + 1, chunk_td 8, store act / rew / done 5N + 1
+        RC = eng.env.rows * eng.env.cols
+        alg_bytes = E * N * (16 * Hh + 4 * D + 16) + E * (2 * (4 * N + RC + 8) + 4 * N + 9 + 21 * N + 10)
+        kname = "rollout_step_h3_kernel"
+        pmc_glob = "r*_pmc_rollout_step.json"
+    else:
+        # algorithmic HBM bytes per launch: per agent-step obs 4D + hidden in/out 8H + outputs (act/q 8 or max 4)
+        alg_bytes = E * N * ((4 * D + 8 * Hh + 8) + (4 * D + 8 * Hh + 4))
+        kname = "agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"
+        pmc_glob = "r*_pmc_agent_fwd.json"
     traffic = None
-    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_agent_fwd.json")))
+    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", pmc_glob)))
     if prof and E == 4096 and N == 8 and Hh == 64:
         pm = json.load(open(prof[-1]))
-        if pm.get("kernel", "").startswith("agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"):
+        if pm.get("kernel", "").startswith(kname):
             traffic = int(pm["traffic_bytes_corrected"])
-    kname = "agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_source": os.path.basename(prof[-1]) if traffic else None,
-                "kernel": f"{kname}<64,64,64,1> (dual: target+behavior)", "kernel_us": round(t_fwd * 1e6, 2),
+                "kernel": f"{kname}<64,64,64,1> (" + ("fused step: env + target fwd + behavior fwd + TD(t-1)"
+                                                      if eng.fused else "dual: target+behavior") + ")",
+                "kernel_us": round(t_fwd * 1e6, 2),
                 "arith": "fp32 network FLOPs as fp16x3-split MFMA (v_mfma_f32_16x16x32_f16 x3, fp32 accumulate)"
                          if h3 else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
                 "fp32_native_peak": PEAK_FP32_TFLOPS, "frac_of_fp32_native_peak": round(achieved / PEAK_FP32_TFLOPS, 4),
@@ -701,6 +714,8 @@ def main():
             "config": {"workload": "QMIX 8-agent gridworld rollout, 4096 envs/GPU, GRU-64 agents, chunk 10, PER",
                        "envs_per_gpu": E, "agents": N, "obs_dim": D, "f1": F1, "gru": Hh, "chunk": 10,
                        "per_capacity_chunks": cap, "per_prefilled_chunks": fill_chunks * E,
+                       "step_launches": "1 fused (env + dual forward + TD) + PER insert every chunk" if eng.fused
+                       else "env + dual forward + PER insert every chunk",
                        "parallelism": f"env-shard x{world}"},
             "rccl_world_size": world,
             "learner_updates_per_s": round(upd_per_s, 1),

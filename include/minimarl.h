@@ -240,6 +240,8 @@ typedef struct mm_rollout_io {
   uint8_t* done;     /* [2][E] */
   uint64_t* step;    /* [2]: t, arrival ticket */
   float gamma;
+  int64_t n_rows;    /* chunk-store rows: a staging row outside [0, n_rows) is never written (error word bit 0) */
+  uint32_t* err;     /* [1] error word (may be NULL) */
 } mm_rollout_io;
 int mm_rollout_step_supported(mm_env* env, const mm_qnet_dims* d, int64_t n_envs);
 int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_target, const mm_qfwd_io* io_target,

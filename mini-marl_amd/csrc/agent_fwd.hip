@@ -1513,7 +1513,9 @@ __device__ __forceinline__ void fs_store_obs(const FusedEnv& ev, const mm_rollou
   const int64_t off = (int64_t)slot * ev.N * D + (int64_t)agent * D;
   for (int i = threadIdx.x; i < nenv * D; i += blockDim.x) {
     const int le = i / D, f = i - le * D;
-    rio.store_obs[(int64_t)s_row[le] * rio.row_stride + off + f] = fs_feature(ev, s_pos + le * 8, s_mask + le * 4, agent, f);
+    const int row = s_row[le];
+    if (row >= 0)
+      rio.store_obs[(int64_t)row * rio.row_stride + off + f] = fs_feature(ev, s_pos + le * 8, s_mask + le * 4, agent, f);
   }
 }
 
@@ -1594,6 +1596,10 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void rollout_step_h3_kernel(QFwdPar
     steps = ev.steps[pb][es];
     apples = ev.apples[pb][es];
     row = rio.staging[es];
+    if (row < 0 || row >= rio.n_rows) {   // a corrupt staging row: nothing of this env is stored
+      if (rio.err && ok_env) atomicOr(rio.err, 1u);
+      row = -1;
+    }
     s_row[le] = (int32_t)row;
     if (!second && c == 0) fs_publish(ev, pr, pc, g, agent, s_pos + le * 8, s_mask + le * 4);
   }
@@ -1648,7 +1654,7 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void rollout_step_h3_kernel(QFwdPar
       rio.done[(int64_t)pb * E + ee] = dn ? 1 : 0;
       rio.cur_row[ee] = dn ? -1 : row;
       // the TD / store of step t - 1 (td_chunk_kernel's arithmetic, agent-order sums)
-      if (rio.td_on && c != 0) {
+      if (rio.td_on && c != 0 && row >= 0) {
         const int pp = pb ^ 1;
         const int64_t r1 = (int64_t)((t + 2) % 3) * EN + ee * N;   // slot of step t - 1 in the 3-rings
         float sr = 0.f, sq = 0.f, smx = 0.f;
@@ -2189,6 +2195,7 @@ int rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, cons
   rc = rollout_step_supported(env, d, ev.E, nullptr, nullptr);
   if (rc) return rc;
   MM_REQUIRE(rio->row_stride >= (int64_t)(rio->chunk_len + 1) * ev.N * ev.D, "rollout_step: row_stride too small");
+  MM_REQUIRE(rio->n_rows >= 1 && rio->n_rows < (1ll << 31), "rollout_step: n_rows must be in [1, 2^31)");
   QFwdParams p0, p1;
   mm_qfwd_io i0 = *io_t, i1 = *io_b;
   i0.obs = i1.obs = ev.reset_obs;   // unused (the obs come from the env state); make_params wants a pointer

@@ -487,6 +487,7 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   const size_t sm = ((d.N * 4 + 15) & ~15) + RC;
   hipLaunchKernelGGL(env_reset_kernel, dim3(blocks), dim3(256), sm, 0, d, (float*)nullptr, 1);
   hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(b + o_pos2, b + o_pos, o_igrid - o_pos, hipMemcpyDeviceToDevice);   // buffer 2 = 1
   if (e != hipSuccess) {
     set_error("env_create: reset failed: %s", hipGetErrorString(e));
     (void)hipFree(base);

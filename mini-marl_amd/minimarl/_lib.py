@@ -56,7 +56,7 @@ class RolloutIO(ctypes.Structure):
                 ("row_stride", c_i64), ("chunk_len", c_i32), ("td_on", c_i32),
                 ("staging", c_vp), ("cur_row", c_vp), ("chunk_td", c_vp),
                 ("act", c_vp), ("qsel", c_vp), ("maxq", c_vp), ("rew", c_vp), ("done", c_vp), ("step", c_vp),
-                ("gamma", c_f32)]
+                ("gamma", c_f32), ("n_rows", c_i64), ("err", c_vp)]
 
 
 # (name, restype, argtypes) for every entry point of include/minimarl.h (+ extended ones)

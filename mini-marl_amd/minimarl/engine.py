@@ -235,6 +235,9 @@ class RolloutEngine:
             r.act, r.qsel, r.maxq = self.act_ring.data_ptr(), self.qsel_ring.data_ptr(), self.maxq_ring.data_ptr()
             r.rew, r.done, r.step = self.rew_ring.data_ptr(), self.done_ring.data_ptr(), self.step_dev.data_ptr()
             r.gamma = self.gamma
+            r.n_rows = self.store.rows
+            self.rollout_err = torch.zeros(1, dtype=torch.int32, device=dev)
+            r.err = self.rollout_err.data_ptr()
             self.rio = r
 
     def sync_target(self):

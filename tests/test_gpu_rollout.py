@@ -360,6 +360,27 @@ def test_fused_step_matches_unfused(dims, full):
     for i, (x, y) in enumerate(zip(_engine_state(a), _engine_state(b))):
         assert torch.equal(x.cpu(), y.cpu()), i
     assert a.t == b.t == 47 and len(a.per) == len(b.per) == 4096
+    assert int(a.rollout_err.item()) == 0
+
+
+def test_fused_step_skips_corrupt_staging_row():
+    """A staging row outside the chunk store is never written through (error word bit 0 instead)."""
+    from minimarl.engine import RolloutEngine
+    e = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=2, device=DEV)
+    assert e.fused
+    e.step(0.1)
+    e.step(0.1)
+    torch.cuda.synchronize()
+    before = e.store.obs.clone()
+    good = e.staging[5].item()
+    e.staging[5] = e.store.rows + 12345
+    e.step(0.1)
+    torch.cuda.synchronize()
+    assert int(e.rollout_err.item()) & 1
+    after = e.store.obs
+    assert torch.equal(after[good], before[good])              # env 5's real row untouched this step
+    e.staging[5] = good
+    e.rollout_err.zero_()
 
 
 def test_fused_graph_replay_matches_eager():
@@ -379,3 +400,4 @@ def test_fused_graph_replay_matches_eager():
     for i, (x, y) in enumerate(zip(_engine_state(a), _engine_state(b))):
         assert torch.equal(x.cpu(), y.cpu()), i
     assert int(b.step_dev[0]) == 33 and int(b.step_dev[1]) == 0
+    assert int(a.rollout_err.item()) == 0 and int(b.rollout_err.item()) == 0
