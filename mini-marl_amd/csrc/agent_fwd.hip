@@ -1426,86 +1426,15 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
 // ---------------------------------------------------------------- fused rollout step (env + dual forward)
 // One launch per lockstep step of the headline path (mm_rollout_step, include/minimarl.h): the dual fp16x3
 // forward above with the Checkers env transition folded in front of it. Each workgroup (net, agent, 256-env
-// tile) re-simulates its tile's transition: one thread per env, the 8 agent positions in registers, the grid in
-// LDS as 2-bit cells (96 cells = 6 words), agents moving in id order exactly as env.hip / oracle/env.py. That
-// costs ~1 us of the workgroup's time, all of it under the weight image's LDS-DMA, and replaces a separate env
-// launch, its launch boundary and the obs round trip through HBM (6.2 MB written + read twice per step at
-// 4096 x 8). The new state's observation of the workgroup's agent is a 45-bit mask (3x3 cells x 5 channels)
-// plus the two coordinates, kept per env in LDS, from which every lane builds its MFMA B-operand features.
-constexpr int FS_ENVS = 256;   // envs per workgroup (16 waves x 16 envs)
-struct FusedSmem {              // after the weight image (bytes)
-  static constexpr int pos = 0;                        // u16 [256][8]: r * 256 + c
-  static constexpr int grid = pos + FS_ENVS * 8 * 2;   // u32 [256][8]: 2-bit cells
-  static constexpr int mask = grid + FS_ENVS * 8 * 4;  // u64 [256][4]: obs masks of the observed agents
-  static constexpr int row = mask + FS_ENVS * 4 * 8;   // i32 [256]: the env's staging row
-  static constexpr int done = row + FS_ENVS * 4;       // u8 [256]
-  static constexpr int total = done + FS_ENVS;
-};
-
-__device__ __forceinline__ int fs_cell(const uint32_t* g, int i) { return (int)((g[i >> 4] >> ((i & 15) * 2)) & 3u); }
-
-// 45-bit local observation mask of the agent at (ar, ac): cell-major 3x3 (row-major, centre = own cell) x 5
-// channels {lemon, apple, even agent, odd agent, wall} (oracle/env.py observe)
-__device__ __forceinline__ uint64_t fs_obs_mask(const uint32_t* g, const int (&pr)[8], const int (&pc)[8], int N, int R,
-                                                int C, int ar, int ac) {
-  uint64_t m = 0;
-#pragma unroll
-  for (int cell = 0; cell < 9; ++cell) {
-    const int rr = ar + cell / 3 - 1, cc = ac + cell % 3 - 1;
-    uint32_t bits;
-    if (rr < 0 || rr >= R || cc < 0 || cc >= C) {
-      bits = 16u;
-    } else {
-      const int item = fs_cell(g, rr * C + cc);
-      int who = -1;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < N && pr[j] == rr && pc[j] == cc) who = j;
-      bits = (item == 1 ? 1u : 0u) | (item == 2 ? 2u : 0u) | ((item == 0 && who >= 0) ? ((who & 1) ? 8u : 4u) : 0u);
-    }
-    m |= (uint64_t)bits << (5 * cell);
-  }
-  return m;
-}
-
-// obs feature f of agent `agent` (partial: its 47 local features; full: agent f / 47's) from the LDS state
-__device__ __forceinline__ float fs_feature(const FusedEnv& ev, const uint16_t* sp, const uint64_t* sm, int agent,
-                                            int f) {
-  int q = 0, lf = f, a = agent;
-  if (ev.full_obs) {
-    q = f / 47;
-    lf = f - 47 * q;
-    a = q;
-  }
-  if (lf < 2) {
-    const int p = sp[a];
-    return lf == 0 ? (float)(p >> 8) * ev.inv_r : (float)(p & 255) * ev.inv_c;
-  }
-  return ((sm[q] >> (lf - 2)) & 1ull) ? 1.0f : 0.0f;
-}
-
-// the env state of thread le's env into LDS: positions and the obs masks of the observed agent(s)
-__device__ __forceinline__ void fs_publish(const FusedEnv& ev, const int (&pr)[8], const int (&pc)[8], const uint32_t* g,
-                                           int agent, uint16_t* sp, uint64_t* sm) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) sp[j] = (uint16_t)(j < ev.N ? ((pr[j] << 8) | pc[j]) : 0);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int aq = ev.full_obs ? q : agent;
-    if (q < (ev.full_obs ? ev.N : 1)) {
-      int ar = 0, ac = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j == aq) {
-          ar = pr[j];
-          ac = pc[j];
-        }
-      sm[q] = fs_obs_mask(g, pr, pc, ev.N, ev.R, ev.C, ar, ac);
-    }
-  }
-}
-
-// the agent's obs of the tile's 256 envs (from LDS) into store slot `slot`, all 1024 threads, env-contiguous
+// tile) re-simulates its tile's transition: one thread per env, the agent positions in registers, the grid in
+// LDS as 2-bit cells, agents moving in id order exactly as env.hip / oracle/env.py. The state comes in with
+// coalesced 16-byte loads issued together (no load sits behind another's latency), all of it under the weight
+// image's LDS-DMA; this replaces a separate env launch, its launch boundary and the obs round trip through HBM
+// (6.2 MB written + read twice per step at 4096 x 8). The new state's observation of the workgroup's agent is
+// a 45-bit mask (3x3 cells x 5 channels) plus the two coordinates, kept per env in LDS, from which every lane
+// builds its MFMA B-operand features; a finished env's reset obs comes from the same masks of the initial state.
+// LDS arrays are [item][env] (env fastest): thread-per-env and lane-per-env accesses are conflict-free.
+// the agent's obs of the tile's envs (from LDS) into store slot `slot`, all 1024 threads, env-contiguous runs
 __device__ __forceinline__ void fs_store_obs(const FusedEnv& ev, const mm_rollout_io& rio, int agent, int e0, int slot,
                                              const uint16_t* s_pos, const uint64_t* s_mask, const int32_t* s_row) {
   const int D = ev.D;
@@ -1515,7 +1444,46 @@ __device__ __forceinline__ void fs_store_obs(const FusedEnv& ev, const mm_rollou
     const int le = i / D, f = i - le * D;
     const int row = s_row[le];
     if (row >= 0)
-      rio.store_obs[(int64_t)row * rio.row_stride + off + f] = fs_feature(ev, s_pos + le * 8, s_mask + le * 4, agent, f);
+      rio.store_obs[(int64_t)row * rio.row_stride + off + f] =
+          fs_feature(ev, s_pos, s_mask, nullptr, nullptr, le, false, agent, f);
+  }
+}
+
+// range guard of the fused step (qnet_h3_bound_block): the exact-f32 image, 8 waves x 32 envs
+template <int F1, int G, int H, int AB>
+__device__ __forceinline__ void rollout_f32_fallback(const QFwdParams& p, int agent, int e0, const FusedEnv& ev,
+                                                  const uint8_t* done_ring, float* wsm, char* aux, uint64_t t, int pb,
+                                                  int64_t out_off, bool second) {
+  const uint16_t* s_pos = reinterpret_cast<const uint16_t*>(aux + FusedSmem::pos);
+  const uint64_t* s_mask = reinterpret_cast<const uint64_t*>(aux + FusedSmem::mask);
+  const uint64_t* s_imask = reinterpret_cast<const uint64_t*>(aux + FusedSmem::imask);
+  const uint16_t* s_ipos = reinterpret_cast<const uint16_t*>(aux + FusedSmem::ipos);
+  const uint8_t* s_done = reinterpret_cast<const uint8_t*>(aux + FusedSmem::done);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t E = ev.E;
+  const mm_qfwd_io& io = p.io;
+  const int le32 = wave * 32 + (lane & 31);
+  const int e32 = e0 + le32;
+  const int hh = lane >> 5;
+  const int lc = min(le32, FS_ENVS - 1);
+  const bool init = second && s_done[lc];
+  auto ol32 = [&](int kb, float (&x)[16]) {
+#pragma unroll
+    for (int sidx = 0; sidx < 16; ++sidx) {
+      const int f = kb * 32 + kperm(sidx, hh);
+      x[sidx] = (e32 < E && f < ev.D) ? fs_feature(ev, s_pos, s_mask, s_ipos, s_imask, lc, init, agent, f) : 0.f;
+    }
+  };
+  if (wave < 8) {
+    float x32[16];
+    ol32(0, x32);
+    const bool zero_h = e32 >= E || (second ? s_done[lc] != 0 : done_ring[(int64_t)(pb ^ 1) * E + min(e32, (int)E - 1)] != 0);
+    QFwdParams q = p;
+    q.io.act_out = io.act_out ? io.act_out + out_off : nullptr;
+    q.io.qsel_out = io.qsel_out ? io.qsel_out + out_off : nullptr;
+    q.io.counter = t;
+    q.io.counter_ptr = nullptr;
+    agent_q_fwd_body<F1, G, H, AB>(q, agent, e32, wsm, ol32, x32, zero_h);
   }
 }
 
@@ -1530,17 +1498,22 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void rollout_step_h3_kernel(QFwdPar
   const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
   const int agent = bid % p.N, tile = bid / p.N;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int N = ev.N, RC = ev.R * ev.C;
+  const int N = ev.N, RC = ev.R * ev.C, NPW = (RC + 15) >> 4;
   const int64_t E = ev.E, EN = E * N;
   const int e0 = tile * FS_ENVS;
   char* aux = reinterpret_cast<char*>(wsm) + (size_t)p.g.agent_stride * 4;
   uint16_t* s_pos = reinterpret_cast<uint16_t*>(aux + FusedSmem::pos);
   uint32_t* s_grid = reinterpret_cast<uint32_t*>(aux + FusedSmem::grid);
   uint64_t* s_mask = reinterpret_cast<uint64_t*>(aux + FusedSmem::mask);
+  int32_t* s_row = reinterpret_cast<int32_t*>(aux + FusedSmem::row);
+  uint64_t* s_imask = reinterpret_cast<uint64_t*>(aux + FusedSmem::imask);
+  uint32_t* s_igrid = reinterpret_cast<uint32_t*>(aux + FusedSmem::igrid);
+  uint16_t* s_ipos = reinterpret_cast<uint16_t*>(aux + FusedSmem::ipos);
   uint8_t* s_done = reinterpret_cast<uint8_t*>(aux + FusedSmem::done);
   const uint64_t t = *rio.step;                                  // this launch's step (all workgroups read it first)
   const int c = (int)(t % (uint64_t)rio.chunk_len), pb = (int)(t & 1);
   const bool designated = second && agent == 0;                 // writes the env-level outputs of the tile
+  const bool td = designated && rio.td_on && c != 0;            // ... and the TD / store of step t - 1
   const bool flagged = reinterpret_cast<const int*>(p.packed + 2 * p.g.agent_stride * p.N)[agent] != 0;
 
   // ---- weight image DMA first (fp16x3 image, or the exact-f32 image of a range-guard-flagged agent)
@@ -1566,80 +1539,115 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void rollout_step_h3_kernel(QFwdPar
   }
   const bool reset_prev = rio.done[(int64_t)(pb ^ 1) * E + ec] != 0;
 
-  // ---- the tile's env transitions, one thread per env (threads 0..255)
-  int32_t* s_row = reinterpret_cast<int32_t*>(aux + FusedSmem::row);
+  // ---- every global read of the env phase issued at once
+  // (a) the tile's grids: items (env, packed word), 2 per thread, rows read as whole dwords
+  uint32_t gw[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int it = tid + k * 1024, le = it / NPW, pw = it - le * NPW;
+    const int64_t es = min((int64_t)e0 + min(le, FS_ENVS - 1), E - 1);
+    gw[k] = fs_load_word(ev.grid[pb] + es * RC, RC, pw);
+  }
+  uint32_t igw = 0;
+  if (tid < NPW) igw = fs_load_word(ev.init_grid, RC, tid);
+  // (b) thread-per-env state: positions, actions a_t, counters, staging row (and the TD inputs of step t - 1)
   const int le = tid;
   const int64_t ee = e0 + le;
   const bool ok_env = ee < E;
   const int64_t es = ok_env ? ee : E - 1;
-  int pr[8], pc[8];
-  uint32_t* g = s_grid + min(le, FS_ENVS - 1) * 8;
+  int pr[8], pc[8], ak[8];
   int steps = 0, apples = 0;
   int64_t row = 0;
+  float td_r[8], td_q[8], td_m[8];
+  int td_a[8];
+  uint8_t dprev = 0;
+  float ctd = 0.f;
   if (tid < FS_ENVS) {
+    const int32_t* actp = rio.act + (int64_t)(t % 3) * EN + es * N;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int pp = j < N ? ev.pos[pb][es * N + j] : -1;
+      const int jj = j < N ? j : N - 1;
+      const int pp = ev.pos[pb][es * N + jj];
       pr[j] = j < N ? (pp >> 8) : -100;
       pc[j] = j < N ? (pp & 255) : -100;
-    }
-    const int8_t* gs = ev.grid[pb] + es * RC;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      uint32_t word = 0;
-      for (int i = 0; i < 16; ++i) {
-        const int idx = w * 16 + i;
-        if (idx < RC) word |= (uint32_t)(gs[idx] & 3) << (2 * i);
-      }
-      g[w] = word;
+      ak[j] = actp[jj];
     }
     steps = ev.steps[pb][es];
     apples = ev.apples[pb][es];
     row = rio.staging[es];
+    if (td) {
+      const int pp = pb ^ 1;
+      const int64_t r1 = (int64_t)((t + 2) % 3) * EN + es * N;   // slot of step t - 1 in the 3-rings
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int jj = j < N ? j : N - 1;
+        td_r[j] = rio.rew[(int64_t)pp * EN + es * N + jj];
+        td_m[j] = rio.maxq[(int64_t)pp * EN + es * N + jj];
+        td_q[j] = rio.qsel[r1 + jj];
+        td_a[j] = rio.act[r1 + jj];
+      }
+      dprev = rio.done[(int64_t)pp * E + es];
+      ctd = rio.chunk_td[es];
+    }
+  }
+  if (tid >= FS_ENVS && tid < FS_ENVS + 8) {   // initial positions (for the reset obs masks)
+    const int j = tid - FS_ENVS;
+    s_ipos[j] = (uint16_t)(j < N ? ev.init_pos[j] : 0);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int it = tid + k * 1024, lw = it / NPW, pw = it - lw * NPW;
+    if (lw < FS_ENVS) s_grid[pw * FS_ENVS + lw] = gw[k];
+  }
+  if (tid < NPW) s_igrid[tid] = igw;
+  if (tid < FS_ENVS) {
     if (row < 0 || row >= rio.n_rows) {   // a corrupt staging row: nothing of this env is stored
       if (rio.err && ok_env) atomicOr(rio.err, 1u);
       row = -1;
     }
     s_row[le] = (int32_t)row;
-    if (!second && c == 0) fs_publish(ev, pr, pc, g, agent, s_pos + le * 8, s_mask + le * 4);
   }
+  __syncthreads();   // grids, initial grid / positions in LDS
+
+  uint32_t* g = s_grid + min(le, FS_ENVS - 1);   // this thread's env grid, words FS_ENVS apart
   if (!second && c == 0) {   // chunk start: s_t of this agent into store slot 0 (block-uniform branch)
+    if (tid < FS_ENVS) fs_publish(ev, pr, pc, g, FS_ENVS, agent, s_pos + le, s_mask + le, FS_ENVS);
     __syncthreads();
     fs_store_obs(ev, rio, agent, e0, 0, s_pos, s_mask, s_row);
     __syncthreads();
   }
-  if (tid < FS_ENVS) {
-    // dynamics (agents in id order; a move is blocked by the border or a cell held by another agent)
-    const int32_t* actp = rio.act + (int64_t)(t % 3) * EN + es * N;
-    steps += 1;
-    float rw[8];
+  if (tid == FS_ENVS) {
+    // the initial state's obs masks (a finished env's behavior obs = the reset obs), one thread of wave 4
+    int ipr[8], ipc[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      rw[k] = 0.f;
-      if (k < N) {
-        const int ak = actp[k];
-        const int nr = pr[k] + (ak == 0 ? 1 : (ak == 2 ? -1 : 0));
-        const int nc = pc[k] + (ak == 1 ? -1 : (ak == 3 ? 1 : 0));
-        bool okm = nr >= 0 && nr < ev.R && nc >= 0 && nc < ev.C;
+    for (int j = 0; j < 8; ++j) {
+      const int pp = s_ipos[j];
+      ipr[j] = j < N ? (pp >> 8) : -100;
+      ipc[j] = j < N ? (pp & 255) : -100;
+    }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) okm = okm && (j == k || pr[j] != nr || pc[j] != nc);
-        if (okm) {
-          pr[k] = nr;
-          pc[k] = nc;
-        }
-        const int cell = pr[k] * ev.C + pc[k];
-        const int item = fs_cell(g, cell);
-        const bool big = (k & 1) == 0;
-        rw[k] = ev.step_cost + (item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f));
-        apples -= item == 2 ? 1 : 0;
-        g[cell >> 4] &= ~(3u << ((cell & 15) * 2));
+    for (int q = 0; q < 4; ++q) {
+      const int aq = ev.full_obs ? q : agent;
+      if (q < (ev.full_obs ? N : 1)) {
+        int ar = 0, ac = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j == aq) {
+            ar = ipr[j];
+            ac = ipc[j];
+          }
+        s_imask[q] = fs_obs_mask(s_igrid, 1, ipr, ipc, N, ev.R, ev.C, ar, ac);
       }
     }
-    const bool dn = steps >= ev.max_steps || apples == 0;
-    fs_publish(ev, pr, pc, g, agent, s_pos + le * 8, s_mask + le * 4);
+  }
+  if (tid < FS_ENVS) {
+    float rw[8];
+    const bool dn = fs_dynamics(ev, pr, pc, ak, g, FS_ENVS, steps, apples, rw);
+    fs_publish(ev, pr, pc, g, FS_ENVS, agent, s_pos + le, s_mask + le, FS_ENVS);
     s_done[le] = dn ? 1 : 0;
     if (designated && ok_env) {
-      // env-level outputs: next state (auto-reset where done) into buffer pb ^ 1, rewards, done, cur_row
+      // env-level outputs: next state (auto-reset where done) into buffer pb ^ 1 (the grid below), rewards,
+      // done, cur_row
       const int nb = pb ^ 1;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -1647,82 +1655,70 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void rollout_step_h3_kernel(QFwdPar
           ev.pos[nb][ee * N + j] = dn ? ev.init_pos[j] : ((pr[j] << 8) | pc[j]);
           rio.rew[(int64_t)pb * EN + ee * N + j] = rw[j];
         }
-      int8_t* gd = ev.grid[nb] + ee * RC;
-      for (int i = 0; i < RC; ++i) gd[i] = dn ? ev.init_grid[i] : (int8_t)fs_cell(g, i);
       ev.steps[nb][ee] = dn ? 0 : steps;
       ev.apples[nb][ee] = dn ? ev.init_apples : apples;
       rio.done[(int64_t)pb * E + ee] = dn ? 1 : 0;
       rio.cur_row[ee] = dn ? -1 : row;
       // the TD / store of step t - 1 (td_chunk_kernel's arithmetic, agent-order sums)
-      if (rio.td_on && c != 0 && row >= 0) {
-        const int pp = pb ^ 1;
-        const int64_t r1 = (int64_t)((t + 2) % 3) * EN + ee * N;   // slot of step t - 1 in the 3-rings
+      if (td && row >= 0) {
         float sr = 0.f, sq = 0.f, smx = 0.f;
-        for (int j = 0; j < N; ++j) {
-          const float rj = rio.rew[(int64_t)pp * EN + ee * N + j];
-          sr += rj;
-          sq += rio.qsel[r1 + j];
-          smx += rio.maxq[(int64_t)pp * EN + ee * N + j];
-          rio.store_act[(row * rio.chunk_len + c - 1) * N + j] = (uint8_t)rio.act[r1 + j];
-          rio.store_rew[(row * rio.chunk_len + c - 1) * N + j] = rj;
-        }
-        const uint8_t dprev = rio.done[(int64_t)pp * E + ee];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < N) {
+            sr += td_r[j];
+            sq += td_q[j];
+            smx += td_m[j];
+            rio.store_act[(row * rio.chunk_len + c - 1) * N + j] = (uint8_t)td_a[j];
+            rio.store_rew[(row * rio.chunk_len + c - 1) * N + j] = td_r[j];
+          }
         const float dd = dprev ? 1.0f : 0.0f;
-        const float td = fabsf(sr + (1.0f - dd) * rio.gamma * smx - sq);
-        rio.chunk_td[ee] = (c - 1 == 0 ? 0.0f : rio.chunk_td[ee]) + td;
+        const float tdv = fabsf(sr + (1.0f - dd) * rio.gamma * smx - sq);
+        rio.chunk_td[ee] = (c - 1 == 0 ? 0.0f : ctd) + tdv;
         rio.store_done[row * rio.chunk_len + c - 1] = dprev;
       }
     }
   }
   __syncthreads();   // weight image landed (the barrier waits vmcnt(0)), LDS state complete
   if (!second) fs_store_obs(ev, rio, agent, e0, c + 1, s_pos, s_mask, s_row);   // s'_t into store slot c + 1
+  if (designated) {
+    // the tile's next grids (the initial grid where the env finished) into buffer pb ^ 1: items (env, packed
+    // word), whole dwords where the row allows it
+    int8_t* gdst = ev.grid[pb ^ 1];
+    for (int it = tid; it < FS_ENVS * NPW; it += 1024) {
+      const int lw = it / NPW, pw = it - lw * NPW;
+      const int64_t ew = e0 + lw;
+      if (ew < E) {
+        const uint32_t w = s_done[lw] ? s_igrid[pw] : s_grid[pw * FS_ENVS + lw];
+        int8_t* rowp = gdst + ew * RC;
+        if ((RC & 3) == 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (16 * pw + 4 * q < RC)
+              *reinterpret_cast<uint32_t*>(rowp + 16 * pw + 4 * q) = fs_unpack4((w >> (8 * q)) & 0xFFu);
+        } else {
+          for (int i = 0; i < 16 && 16 * pw + i < RC; ++i) rowp[16 * pw + i] = (int8_t)((w >> (2 * i)) & 3u);
+        }
+      }
+    }
+  }
 
   const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
   const int64_t out_off = second ? (int64_t)((t + 1) % 3) * EN : (int64_t)pb * EN;
   if (flagged) {
-    // range guard (qnet_h3_bound_block): the exact-f32 image, 8 waves x 32 envs
-    const int le32 = wave * 32 + (lane & 31);
-    const int e32 = e0 + le32;
-    const int hh = lane >> 5;
-    const int lc = min(le32, FS_ENVS - 1);
-    const bool reset_obs = second && s_done[lc];
-    auto ol32 = [&](int kb, float (&x)[16]) {
-#pragma unroll
-      for (int sidx = 0; sidx < 16; ++sidx) {
-        const int f = kb * 32 + kperm(sidx, hh);
-        float v = 0.f;
-        if (e32 < E && f < ev.D)
-          v = reset_obs ? ev.reset_obs[agent * ev.D + f] : fs_feature(ev, s_pos + lc * 8, s_mask + lc * 4, agent, f);
-        x[sidx] = v;
-      }
-    };
-    if (wave < 8) {
-      float x32[16];
-      ol32(0, x32);
-      const bool zero_h = e32 >= E || (second ? s_done[lc] != 0 : rio.done[(int64_t)(pb ^ 1) * E + min(e32, (int)E - 1)] != 0);
-      QFwdParams q = p;
-      q.io.act_out = io.act_out ? io.act_out + out_off : nullptr;
-      q.io.qsel_out = io.qsel_out ? io.qsel_out + out_off : nullptr;
-      q.io.counter = t;
-      q.io.counter_ptr = nullptr;
-      agent_q_fwd_body<F1, G, H, AB>(q, agent, e32, wsm, ol32, x32, zero_h);
-    }
+    rollout_f32_fallback<F1, G, H, AB>(p, agent, e0, ev, rio.done, wsm, aux, t, pb, out_off, second);
   } else {
-    const int le = wave * 16 + (lane & 15);
-    const bool reset_obs = second && s_done[le];
+    const int lf = wave * 16 + (lane & 15);
+    const bool init = second && s_done[lf];
     auto ol = [&](int kb, float (&x)[8]) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int f = kb * 32 + kperm16(j, g4);
-        float v = 0.f;
-        if (e < E && f < ev.D)
-          v = reset_obs ? ev.reset_obs[agent * ev.D + f] : fs_feature(ev, s_pos + le * 8, s_mask + le * 4, agent, f);
-        x[j] = v;
+        x[j] = (e < E && f < ev.D) ? fs_feature(ev, s_pos, s_mask, s_ipos, s_imask, lf, init, agent, f) : 0.f;
       }
     };
     float xn[8];
     ol(0, xn);
-    const bool zero_h = e >= E || (second ? s_done[le] != 0 : reset_prev);
+    const bool zero_h = e >= E || (second ? s_done[lf] != 0 : reset_prev);
     if (zero_h) {
 #pragma unroll
       for (int tt = 0; tt < H / 16; ++tt) h0[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
