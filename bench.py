@@ -231,6 +231,9 @@ def main():
                     help="timed regions of exactly --steps steps each; ms_per_step is their median (min / max beside)")
     ap.add_argument("--cfg1-episodes", type=int, default=20,
                     help="timed training episodes of the cfg1 VDN trainer lines (0 = skip; single-GPU runs only)")
+    ap.add_argument("--fused-step", action="store_true",
+                    help="one-launch fused step (env + dual forward + TD; slower at 4096 x 8, DESIGN.md) instead of the "
+                         "two-launch default")
     ap.add_argument("--probe-ranks", action="store_true", help="launcher check: gloo rendezvous only, no GPU")
     args = ap.parse_args()
 
@@ -264,7 +267,8 @@ def main():
     E, N, Hh = args.envs, args.agents, args.hidden
     F1, G = 64, Hh
     cap = 16 * E
-    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=cap, seed=1234 + rank, device=dev)
+    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=cap, seed=1234 + rank, fused=args.fused_step,
+                        device=dev)
     D = eng.D
     from minimarl.learner import Mixer, QLearner
     mix = Mixer(N, N * D, 64, 32, dev, seed=7)

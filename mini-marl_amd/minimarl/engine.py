@@ -17,13 +17,15 @@ insert (four launches, its first one also running that step's TD/store). All str
 one HIP stream, no host sync; a chunk of steps is captured once as a HIP graph and replayed. The
 store/TD of the last executed step therefore lands with the next step (``flush_td()`` writes it
 now).
-Fused mode (``fused=None``: on wherever it applies — the Checkers env, E >= 2048 lockstep envs and a
-forward shape the fused kernel is built for): ONE launch per step (mm_rollout_step, agent_fwd.hip
+Fused mode (opt-in: ``fused=True``, or ``fused=None`` = on wherever it applies — the Checkers env, E >= 2048
+lockstep envs and a forward shape the fused kernel is built for): ONE launch per step (mm_rollout_step, agent_fwd.hip
 rollout_step_h3_kernel) runs the env transition, the target forward of step t and the behavior forward
 of step t+1, and the TD / store of step t-1; the chunk's last step adds the PER insert. Its per-step
 buffers are rings indexed by the device step counter (act / qsel by t % 3, rew / done / maxq by t % 2,
 the env state double-buffered by t % 2), so one captured step replays for any t. Bit-identical to the
-unfused launches (test_gpu_rollout.py test_fused_step_matches_unfused).
+unfused launches (test_gpu_rollout.py test_fused_step_matches_unfused), but slower at 4096 x 8 (51.5 us
+vs 9.8 + 27 us: every (net, agent) workgroup re-simulates its 256-env tile's transition, a serial
+agent-ordered chain that no other workgroup on the CU hides), so the default is the two-launch step.
 Hidden states reset at episode ends (the reference re-inits them per episode,
 vdn/main.py:137-138); chunks span episode boundaries like the reference's
 global ``count_step`` (vdn/main.py:151-167).
@@ -61,7 +63,7 @@ class ChunkStore:
 class RolloutEngine:
     def __init__(self, n_envs, n_agents, obs_dim=None, n_actions=5, f1=64, g=32, h=32, chunk=10,
                  capacity=None, gamma=0.99, max_steps=100, step_cost=-0.01, full_observable=False,
-                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", fused=None, device="cuda"):
+                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", fused=False, device="cuda"):
         self.device = torch.device(device)
         self.E, self.N, self.C = int(n_envs), int(n_agents), int(chunk)
         self.gamma = float(gamma)
@@ -236,7 +238,7 @@ class RolloutEngine:
             r.rew, r.done, r.step = self.rew_ring.data_ptr(), self.done_ring.data_ptr(), self.step_dev.data_ptr()
             r.gamma = self.gamma
             r.n_rows = self.store.rows
-            self.rollout_err = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.rollout_err = torch.zeros(1, dtype=torch.int32, device=self.device)
             r.err = self.rollout_err.data_ptr()
             self.rio = r
 

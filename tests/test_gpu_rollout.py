@@ -366,7 +366,7 @@ def test_fused_step_matches_unfused(dims, full):
 def test_fused_step_skips_corrupt_staging_row():
     """A staging row outside the chunk store is never written through (error word bit 0 instead)."""
     from minimarl.engine import RolloutEngine
-    e = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=2, device=DEV)
+    e = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=2, fused=True, device=DEV)
     assert e.fused
     e.step(0.1)
     e.step(0.1)
@@ -386,7 +386,7 @@ def test_fused_step_skips_corrupt_staging_row():
 def test_fused_graph_replay_matches_eager():
     """Fused-mode chunk graphs and single-step graphs replay bit-identically to eager fused steps."""
     from minimarl.engine import RolloutEngine
-    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, device=DEV)
+    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, fused=True, device=DEV)
     a = RolloutEngine(2048, 8, **kw)
     b = RolloutEngine(2048, 8, **kw)
     assert a.fused and b.fused

@@ -14,6 +14,6 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv 
   python3 bench.py --steps 40 --warmup 10 --learner-steps 5 --no-cpu-baseline --mappo-episodes 0 > $OUT/write.log 2>&1
 python3 profiles/summarize.py $OUT/stats > $OUT/kernel_stats.txt
 cp $(find $OUT/stats -name '*kernel_stats.csv' | head -1) $OUT/kernel_stats.csv
-python3 tools/pmc_traffic.py $OUT/fetch $OUT/write rollout_step_h3_kernel 262144 42250240 $OUT/pmc_rollout_step.json \
+python3 tools/pmc_traffic.py $OUT/fetch $OUT/write agent_q_fwd_h3_kernel 262144 46268416 $OUT/pmc_agent_fwd.json \
   "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace --output-format csv -- python3 bench.py --steps 40 --warmup 10 --learner-steps 5 --no-cpu-baseline --mappo-episodes 0 (two separate passes)"
 tail -1 $OUT/stats.log
