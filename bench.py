@@ -161,15 +161,24 @@ def cpu_offq_baseline(otr, batch_np, budget_s=6.0):
 
 
 def time_kernel(fn, iters=50):
-    """Average device time of fn() via events on torch's current stream (our launch stream)."""
+    """Average device time of fn(): `iters` back-to-back launches captured in one HIP graph and replayed
+    between events on torch's current stream (our launch stream), so host launch latency does not pad
+    the kernel time (rocprofv3's per-dispatch durations are the cross-check, profiles/)."""
+    from minimarl.qnet import graph_capture
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with graph_capture(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     start.record()
-    for _ in range(iters):
-        fn()
+    g.replay()
     end.record()
     torch.cuda.synchronize()
+    del g
     return start.elapsed_time(end) / iters / 1e3
 
 
@@ -621,7 +630,7 @@ def main():
 
         def dual5():
             L5.mm_agent_q_fwd2(ctypes.byref(n5[0].dims), ptr(n5[0].packed), ctypes.byref(io5[0]), E5,
-                               ptr(n5[1].packed), ctypes.byref(io5[1]), E5, st5)
+                               ptr(n5[1].packed), ctypes.byref(io5[1]), E5, stream_handle(dev))
         t5 = time_kernel(dual5)
         f5 = 2 * qnet_flops_per_agent_step(D5, 64, 32, H5, A5) * E5 * N5
         cfg5 = {"workload": "cfg5 dual agent forward (target + behavior), synthetic obs", "envs": E5, "agents": N5,
