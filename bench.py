@@ -672,7 +672,14 @@ def main():
     # behavior net on s_{t+1}: 2 nets x E x N agent-steps). At E >= 2048 it runs the fp16x3-split
     # kernel: every fp32 product as 3 f16 MFMAs, so its MFMA ceiling for the network's fp32 FLOPs
     # is the dense f16 peak / 3; the native f32-MFMA peak is reported beside it.
-    t_fwd = time_kernel(eng.fused_forward)
+    t_iso = time_kernel(eng.fused_forward)
+    if eng.fused:
+        t_fwd = t_iso
+    else:
+        # in its rollout context: graphs of K x (env + dual forward) and K x env, the difference per step (the
+        # forward then reads the obs the env launch just wrote, as in the timed rollout; back-to-back forwards
+        # alone re-read cold obs and take longer, reported as kernel_us_isolated)
+        t_fwd = time_kernel(lambda: (eng.env_only(), eng.fused_forward())) - time_kernel(eng.env_only)
     flops = 2 * qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
     achieved = flops / t_fwd / 1e12
     h3 = E >= 2048 and not os.environ.get("MM_FWD_F32")
@@ -702,7 +709,7 @@ def main():
                 "traffic_source": os.path.basename(prof[-1]) if traffic else None,
                 "kernel": f"{kname}<64,64,64,1> (" + ("fused step: env + target fwd + behavior fwd + TD(t-1)"
                                                       if eng.fused else "dual: target+behavior") + ")",
-                "kernel_us": round(t_fwd * 1e6, 2),
+                "kernel_us": round(t_fwd * 1e6, 2), "kernel_us_isolated": round(t_iso * 1e6, 2),
                 "arith": "fp32 network FLOPs as fp16x3-split MFMA (v_mfma_f32_16x16x32_f16 x3, fp32 accumulate)"
                          if h3 else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
                 "fp32_native_peak": PEAK_FP32_TFLOPS, "frac_of_fp32_native_peak": round(achieved / PEAK_FP32_TFLOPS, 4),

@@ -465,6 +465,20 @@ class RolloutEngine:
         for _ in range(n_steps):
             self.step(epsilon)
 
+    def env_only(self, k=0):
+        """The step's env launch on its own (two-launch mode, mid-chunk form with the TD folded in); for
+        timing the dual forward in its rollout context (bench.py: (env + forward) - env)."""
+        assert not self.fused
+        s = stream_handle(self.device)
+        nxt = ctypes.c_void_p(self.store.obs.data_ptr() + 4 * 2 * self.N * self.D)
+        kp = 1 - k
+        check(self.env.step_rows_td(ptr(self.act_buf[k]), nxt, self.store.row_stride, ptr(self.staging),
+                                    ptr(self.cur_row), ptr(self.rew), ptr(self.done_buf[k]), self.gamma, ptr(self.rew),
+                                    ptr(self.done_buf[kp]), ptr(self.qsel_buf[kp]), ptr(self.maxq),
+                                    ptr(self.act_buf[kp]), ptr(self.chunk_td), 1, self.C, ptr(self.store.act),
+                                    ptr(self.store.rew), ptr(self.store.done), ptr(self.staging), ptr(self.counter_dev),
+                                    s), "env_step_td")
+
     def fused_forward(self, k=0):
         """The step's dominant launch on its own (target fwd + behavior fwd); for timing. Fused mode: the
         whole step launch (env + both forwards + TD) with the TD off; it advances the device step counter."""
