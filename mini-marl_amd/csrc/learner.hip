@@ -2138,84 +2138,116 @@ __global__ __launch_bounds__(256) void outer_reduce_kernel(OuterArgs a) {
 }
 
 // Batched split-M outer reduce: many independent OuterArgs jobs in ONE launch, each job's M rows
-// split into 32-row slices; block (job, tile, group, slice) reduces one 32x32 tile over one slice
+// split into slices of 32-row chunks; block (job, tile, group, slice) reduces one tile over one slice
 // into a partial, outer_sum_kernel adds the slices in fixed order (deterministic).
 constexpr int OB_MAX = 16;
 struct OuterBatch {
   OuterArgs job[OB_MAX];
   int tiles_c[OB_MAX], tiles_r[OB_MAX], groups[OB_MAX], slices[OB_MAX], rps[OB_MAX];
+  int tr_shift[OB_MAX];  // block tile TR x TC = (32 << s) x (128 >> s): 32x128, 64x64 or 128x32 (least padding)
   int blk0[OB_MAX + 1];
   int64_t part[OB_MAX];  // partial offset: [slice][group][R*Cc + R]
   int njobs;
   float* partial;
 };
 
-// Block = 4 waves = one 64 x 64 tile of (R, Cc); per 32-row chunk the U / V slabs are staged in LDS
-// and every wave accumulates its 32 x 32 sub-tile with 16 exact-f32 MFMAs (v_mfma_f32_32x32x2_f32,
-// the reduction index m on the MFMA k dimension). Bias sums (U^T 1) by VALU in the c-tile-0 blocks.
-__global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
-  __shared__ float su[32][65];
-  __shared__ float svv[32][65];
-  int j = 0;
-  while (j + 1 < ob.njobs && (int)blockIdx.x >= ob.blk0[j + 1]) ++j;
+// Block = 4 waves = one TR x TC tile of (R, Cc), each wave a 32 x 32 sub-tile accumulated with 16
+// exact-f32 MFMAs per 32-row chunk (v_mfma_f32_32x32x2_f32, the reduction index m on the MFMA k
+// dimension). Per chunk the U [32][TR] and V [32][TC] slabs (NL = (TR + TC) / 8 floats per thread,
+// coalesced rows) are staged in LDS while the next chunk's slabs are already in flight; gathered V rows
+// (v_off) take their row offsets from LDS, loaded one chunk further ahead, so no load waits behind
+// another. Bias sums (U^T 1) come from the U values each thread loads (its column is fixed:
+// 256 % TR == 0), combined over the 256 / TR threads of a column in fixed order at the end.
+struct ObSmem {
+  float su[32][132];
+  float svv[32][132];
+  int64_t soff[2][32];
+  float sbias[256];
+};
+
+template <int TS>
+__device__ __forceinline__ void outer_tile(const OuterBatch& ob, int j, int t, ObSmem& sm) {
+  constexpr int TR = 32 << TS, TC = 128 >> TS, NU = TR / 8, NL = NU + TC / 8;
+  constexpr int MU = 256 / TR, MV = 256 / TC;   // rows between a thread's consecutive U / V elements
   const OuterArgs& a = ob.job[j];
-  int t = blockIdx.x - ob.blk0[j];
   const int tc_ = t % ob.tiles_c[j];
   t /= ob.tiles_c[j];
   const int tr_ = t % ob.tiles_r[j];
   t /= ob.tiles_r[j];
   const int g = t % ob.groups[j];
   const int sl = t / ob.groups[j];
-  const int r0 = tr_ * 64, c0 = tc_ * 64;
+  const int r0 = tr_ * TR, c0 = tc_ * TC;
   const int m_begin = sl * ob.rps[j], m_end = min(a.M, m_begin + ob.rps[j]);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
-  const int rw = wave >> 1, cw = wave & 1;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
+  constexpr int NRW = TR / 32;
+  const int rw = wave % NRW, cw = wave / NRW;
+  const bool gather = a.v_off != nullptr;
+  // this thread's U column xu / first row mu0, V column xv / first row mv0
+  const int xu = tid % TR, mu0 = tid / TR, xv = tid % TC, mv0 = tid / TC;
+  const bool uok = r0 + xu < a.R, vok = c0 + xv < a.Cc;
+  const float* Ub = a.U + g * a.u_g + r0 + xu;
+  const float* Vb = a.V + g * a.v_g + c0 + xv;
+  const float* Vr = gather ? a.v_reset + g * a.v_g + c0 + xv : nullptr;
+  const int64_t u_m = a.u_m, v_m = a.v_m;
   f32x16 acc;
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
   float sb = 0.f;
-  const bool do_b = a.db && tc_ == 0 && threadIdx.x < 64;
-  // register prefetch: chunk m0 + 32 is loaded while chunk m0 is reduced
-  float pu[8], pv[8];
-  auto load = [&](int m0) {
+  float pv[NL];
+  auto load = [&](int m0, int buf) {
+    const float* up = Ub + (int64_t)(m0 + mu0) * u_m;
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int k = threadIdx.x + 256 * p;
-      const int mm = k >> 6, x = k & 63;
-      const int m = m0 + mm;
-      float u = 0.f, v = 0.f;
-      if (m < m_end) {
-        if (r0 + x < a.R) u = a.U[g * a.u_g + (int64_t)m * a.u_m + r0 + x];
-        if (c0 + x < a.Cc) {
-          if (a.v_off) {
-            const int64_t off = a.v_off[m];
-            const float* base = off >= 0 ? a.V + off : a.v_reset;
-            v = base[g * a.v_g + c0 + x];
-          } else {
-            v = a.V[g * a.v_g + (int64_t)m * a.v_m + c0 + x];
-          }
-        }
+    for (int p = 0; p < NU; ++p) {
+      const int m = m0 + mu0 + MU * p;
+      pv[p] = (uok && m < m_end) ? up[0] : 0.f;
+      up += MU * u_m;
+    }
+    if (gather) {
+#pragma unroll
+      for (int p = 0; p < NL - NU; ++p) {
+        const int mm = mv0 + MV * p, m = m0 + mm;
+        const int64_t off = sm.soff[buf][mm];
+        pv[NU + p] = (vok && m < m_end) ? (off >= 0 ? Vb + off : Vr)[0] : 0.f;
       }
-      pu[p] = u;
-      pv[p] = v;
+    } else {
+      const float* vp = Vb + (int64_t)(m0 + mv0) * v_m;
+#pragma unroll
+      for (int p = 0; p < NL - NU; ++p) {
+        const int m = m0 + mv0 + MV * p;
+        pv[NU + p] = (vok && m < m_end) ? vp[0] : 0.f;
+        vp += MV * v_m;
+      }
     }
   };
-  if (m_begin < m_end) load(m_begin);
+  int64_t off_next = -1;
+  if (gather && tid < 32) {
+    const int m = m_begin + tid;
+    sm.soff[0][tid] = m < m_end ? a.v_off[m] : -1;
+    off_next = m + 32 < m_end ? a.v_off[m + 32] : -1;
+  }
+  __syncthreads();
+  if (m_begin < m_end) load(m_begin, 0);
+  int buf = 0;
   for (int m0 = m_begin; m0 < m_end; m0 += 32) {
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int k = threadIdx.x + 256 * p;
-      su[k >> 6][k & 63] = pu[p];
-      svv[k >> 6][k & 63] = pv[p];
+    for (int p = 0; p < NU; ++p) {
+      sm.su[mu0 + MU * p][xu] = pv[p];
+      sb += pv[p];
+    }
+#pragma unroll
+    for (int p = 0; p < NL - NU; ++p) sm.svv[mv0 + MV * p][xv] = pv[NU + p];
+    if (gather && tid < 32) {   // offsets of chunk m0 + 32 for the loads below; the next ones in flight
+      sm.soff[buf ^ 1][tid] = off_next;
+      const int m = m0 + 64 + tid;
+      off_next = m < m_end ? a.v_off[m] : -1;
     }
     __syncthreads();
-    if (m0 + 32 < m_end) load(m0 + 32);
+    if (m0 + 32 < m_end) load(m0 + 32, buf ^ 1);
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2)
-      acc = mfma32(su[2 * s2 + lh][rw * 32 + li], svv[2 * s2 + lh][cw * 32 + li], acc);
-    if (do_b)
-      for (int mm = 0; mm < 32; ++mm) sb += su[mm][threadIdx.x];
+      acc = mfma32(sm.su[2 * s2 + lh][rw * 32 + li], sm.svv[2 * s2 + lh][cw * 32 + li], acc);
     __syncthreads();
+    buf ^= 1;
   }
   const int64_t per = (int64_t)a.R * a.Cc + a.R;
   float* out = ob.partial + ob.part[j] + ((int64_t)sl * ob.groups[j] + g) * per;
@@ -2225,7 +2257,27 @@ __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
     const int r = r0 + rw * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
     if (r < a.R && c < a.Cc) out[(int64_t)r * a.Cc + c] = acc[q];
   }
-  if (do_b && r0 + threadIdx.x < a.R) out[(int64_t)a.R * a.Cc + r0 + threadIdx.x] = sb;
+  if (a.db && tc_ == 0) {
+    sm.sbias[tid] = sb;
+    __syncthreads();
+    if (tid < TR && r0 + tid < a.R) {
+      float s = 0.f;
+      for (int k = tid; k < 256; k += TR) s += sm.sbias[k];
+      out[(int64_t)a.R * a.Cc + r0 + tid] = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
+  __shared__ ObSmem sm;
+  int j = 0;
+  while (j + 1 < ob.njobs && (int)blockIdx.x >= ob.blk0[j + 1]) ++j;
+  const int t = blockIdx.x - ob.blk0[j];
+  switch (ob.tr_shift[j]) {
+    case 0: outer_tile<0>(ob, j, t, sm); break;
+    case 1: outer_tile<1>(ob, j, t, sm); break;
+    default: outer_tile<2>(ob, j, t, sm); break;
+  }
 }
 
 __global__ __launch_bounds__(256) void outer_sum_kernel(OuterBatch ob) {
@@ -2837,16 +2889,31 @@ static int64_t outer_batch_layout(const mm_outer_args* x, int n, mm::OuterBatch*
     const mm_outer_args& q = x[j];
     ob->job[j] = {q.U, q.u_g, q.u_m, q.V, q.v_g, q.v_m, q.v_off, q.v_reset, q.dW, q.w_g, q.db, q.b_g, q.M, q.R,
                   q.Cc, q.accumulate};
-    ob->tiles_c[j] = (q.Cc + 63) / 64;
-    ob->tiles_r[j] = (q.R + 63) / 64;
+    // tile shape with the least padded area (ties: fewer row tiles)
+    int best = 0;
+    int64_t best_area = -1;
+    for (int sh = 2; sh >= 0; --sh) {
+      const int TR = 32 << sh, TC = 128 >> sh;
+      const int64_t area = (int64_t)((q.R + TR - 1) / TR) * TR * ((q.Cc + TC - 1) / TC) * TC;
+      if (best_area < 0 || area < best_area) {
+        best_area = area;
+        best = sh;
+      }
+    }
+    ob->tr_shift[j] = best;
+    ob->tiles_r[j] = (q.R + (32 << best) - 1) / (32 << best);
+    ob->tiles_c[j] = (q.Cc + (128 >> best) - 1) / (128 >> best);
     ob->groups[j] = q.groups;
-    // rows per slice: 32-row chunks, at most ~64 slices per job (bounded partials at large batches)
+    // slices of 32-row chunks: about 4096 blocks per job (long-lived blocks, bounded partials), at most 64
     const int chunks = (q.M + 31) / 32;
-    ob->rps[j] = 32 * ((chunks + 63) / 64);
+    const int64_t tiles = (int64_t)ob->tiles_r[j] * ob->tiles_c[j] * q.groups;
+    int want = (int)std::min<int64_t>(64, std::max<int64_t>(1, (4096 + tiles - 1) / tiles));
+    want = std::min(want, chunks);
+    ob->rps[j] = 32 * ((chunks + want - 1) / want);
     ob->slices[j] = (q.M + ob->rps[j] - 1) / ob->rps[j];
     ob->blk0[j] = blk;
     ob->part[j] = part;
-    blk += ob->tiles_c[j] * ob->tiles_r[j] * q.groups * ob->slices[j];
+    blk += (int)(tiles * ob->slices[j]);
     part += (int64_t)ob->slices[j] * q.groups * ((int64_t)q.R * q.Cc + q.R);
   }
   ob->blk0[n] = blk;
