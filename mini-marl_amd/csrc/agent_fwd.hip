@@ -341,12 +341,15 @@ __device__ __forceinline__ void agent_pre_body(const QFwdParams& p, int agent, i
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const bool valid = e < p.E;
   const mm_qfwd_io& io = p.io;
-  float fr[16], xk[16];
+  float fr[16], xk[16], xn[16];
   f32x16 x1[RB1];
 #pragma unroll
   for (int rb = 0; rb < RB1; ++rb) x1[rb] = load_bias(W + CG::off_b1 + rb * 32, hh);
+  load_obs_kblock(orow, 0, p.D, xn);
   for (int kb = 0; kb < p.g.KD; ++kb) {
-    load_obs_kblock(orow, kb, p.D, xk);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) xk[s] = xn[s];
+    if (kb + 1 < p.g.KD) load_obs_kblock(orow, kb + 1, p.D, xn);   // next k-block in flight
 #pragma unroll
     for (int rb = 0; rb < RB1; ++rb) {
       load_frag(W + CG::off_l1 + (int64_t)(rb * p.g.KD + kb) * 1024, lane, fr);
@@ -1423,6 +1426,32 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
                                     [&](int kb, float (&x)[8]) { load_obs_ks(orow, kb, p.D, x); }, xn, h0, eps, ctr);
 }
 
+// ---------------------------------------------------------------- learner PRE, weights in LDS
+// Layers 1-2 and the GRU input projection of large learner batches: agent_pre_body (exact f32, one wave
+// = 32 rows) with the agent's f32 fragment image staged ONCE per 1024-thread block by LDS-DMA and shared
+// by its 16 waves (512 rows), instead of every wave streaming the ~100 KB of fragments (cfg5) from L2 per
+// 32 rows. Same arithmetic as agent_split_kernel<.., 1>: bit-identical results.
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(1024, 1) void agent_pre_lds_kernel(QFwdParams p0, QFwdParams p1) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  const bool second = (int)blockIdx.x >= p0.nblocks;
+  const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  const QFwdParams& p = kargs[second ? 1 : 0];
+  (void)p1;
+  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
+  const int agent = bid % p.N, tile = bid / p.N;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float* src = p.packed + (int64_t)agent * p.g.agent_stride;
+  const int nchunk = (int)(p.g.agent_stride >> 8);
+  for (int c = wave; c < nchunk; c += 16)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 256 + lane * 4),
+                                     (__attribute__((address_space(3))) void*)(wsm + c * 256), 16, 0, 0);
+  const int e = tile * 512 + wave * 32 + (lane & 31);
+  const float* orow = obs_row_ptr(p, agent, e);
+  __syncthreads();
+  agent_pre_body<F1, G, H, AB>(p, agent, e, wsm, orow);
+}
+
 // ---------------------------------------------------------------- fused rollout step (env + dual forward)
 // One launch per lockstep step of the headline path (mm_rollout_step, include/minimarl.h): the dual fp16x3
 // forward above with the Checkers env transition folded in front of it. Each workgroup (net, agent, 256-env
@@ -2023,6 +2052,16 @@ static int launch_split(int phase, QFwdParams p0, QFwdParams p1, hipStream_t s) 
       constexpr int NW = 3 * (H / 32) > F1 / 32 ? 3 * (H / 32) : F1 / 32;
       static_assert(NW >= G / 32, "layer-2 row blocks need a wave each");
       hipLaunchKernelGGL((agent_pre_rb_kernel<F1, G, H, AB>), dim3(t0 + t1), dim3(64 * NW), 0, s, p0, p1);
+      MM_HIP_CHECK(hipGetLastError());
+      return MM_OK;
+    }
+    const size_t sm = (size_t)p0.g.agent_stride * 4;
+    if (sm <= 160 * 1024) {
+      // many row tiles: the f32 image staged once per 512 rows
+      p0.nblocks = (p0.E + 511) / 512 * p0.N;
+      p1.nblocks = single ? 0 : (p1.E + 511) / 512 * p1.N;
+      hipLaunchKernelGGL((agent_pre_lds_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(1024), sm, s, p0,
+                         p1);
       MM_HIP_CHECK(hipGetLastError());
       return MM_OK;
     }

@@ -260,56 +260,60 @@ __global__ __launch_bounds__(256) void mixer_gi_tiled_kernel(MixGiArgs a) {
 // accumulate). Block = 64 samples x all 3Hm gate rows (RBK = 3Hm / 32 row blocks; 2 RBK waves, each one
 // 32 x 32 tile), the K = S state width in 64-deep chunks staged as f16 in LDS (row pitch 72 halves:
 // conflict-free 16-byte fragment reads), the next chunk's global loads in flight during the MFMAs.
+// Loads are 16-byte (4 consecutive k of one state / weight row per item; a row whose start is not
+// 16-byte aligned takes 4 scalar loads), the 64 samples' state offsets read once into LDS.
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
 template <int RBK>
 __global__ __launch_bounds__(64 * 2 * RBK) void mixer_gi_f16_kernel(MixGiArgs a) {
   constexpr int NT = 64 * 2 * RBK, ROWS = 32 * RBK, PITCH = 72, KC = 64;
-  constexpr int NLD = (64 * KC + ROWS * KC + NT - 1) / NT;   // staged elements per thread per chunk
+  constexpr int NX4 = 64 * KC / 4, NW4 = ROWS * KC / 4;    // 4-float items per chunk: state, weights
+  constexpr int NI = (NX4 + NW4 + NT - 1) / NT;            // items per thread per chunk
   __shared__ __attribute__((aligned(16))) _Float16 sx[2][64 * PITCH];
   __shared__ __attribute__((aligned(16))) _Float16 sw[2][ROWS * PITCH];
+  __shared__ const float* srow[64];
   const MixGiNet& nt = a.net[blockIdx.y];
   const int S = a.S, M3 = 3 * a.Hm;
   const MixOff o = mix_offsets(S, a.Hm, a.K1, a.N);
   const int c0 = blockIdx.x * 64;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
   const int cw = wave & 1, rw = wave >> 1;   // this wave's 32 samples / 32 gate rows
-  // source row pointers of the elements this thread stages (fixed across chunks)
-  const float* src[NLD];
-  int dst[NLD], kk[NLD];
-#pragma unroll
-  for (int j = 0; j < NLD; ++j) {
-    const int idx = tid + j * NT;
-    if (idx < 64 * KC) {
-      const int p = idx / KC, x = idx % KC, c = min(c0 + p, a.R - 1);
-      const int64_t off = state_off(nt.s_off, c, a.S);
-      src[j] = (off >= 0 ? a.obs + off : a.reset_obs);
-      dst[j] = p * PITCH + x;
-      kk[j] = x;
-    } else {
-      const int i2 = min(idx - 64 * KC, ROWS * KC - 1);
-      const int m = i2 / KC, x = i2 % KC;
-      src[j] = nt.P + o.gWih + (int64_t)min(m, M3 - 1) * S;
-      dst[j] = -1 - (m * PITCH + x);   // negative: the W image
-      kk[j] = x;
-    }
+  if (tid < 64) {
+    const int c = min(c0 + tid, a.R - 1);
+    const int64_t off = state_off(nt.s_off, c, a.S);
+    srow[tid] = off >= 0 ? a.obs + off : a.reset_obs;
   }
-  float v[NLD];
+  const float* Wih = nt.P + o.gWih;
+  __syncthreads();
+  float4 v[NI];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int j = 0; j < NLD; ++j) {
-      const int k = k0 + kk[j];
-      v[j] = src[j][min(k, S - 1)];
-      if (k >= S) v[j] = 0.f;
+    for (int j = 0; j < NI; ++j) {
+      const int idx = tid + j * NT;
+      if (idx >= NX4 + NW4) break;
+      const int i2 = idx < NX4 ? idx : idx - NX4;
+      const int r = i2 >> 4, k = k0 + 4 * (i2 & 15);
+      const float* row = idx < NX4 ? srow[r] : Wih + (int64_t)min(r, M3 - 1) * S;
+      if (k + 3 < S && ((reinterpret_cast<uintptr_t>(row) & 15) == 0)) {
+        v[j] = *reinterpret_cast<const float4*>(row + k);
+      } else {
+        v[j].x = k < S ? row[k] : 0.f;
+        v[j].y = k + 1 < S ? row[k + 1] : 0.f;
+        v[j].z = k + 2 < S ? row[k + 2] : 0.f;
+        v[j].w = k + 3 < S ? row[k + 3] : 0.f;
+      }
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < NLD; ++j) {
-      if (tid + j * NT >= 64 * KC + ROWS * KC) continue;
-      if (dst[j] >= 0)
-        sx[buf][dst[j]] = (_Float16)v[j];
-      else
-        sw[buf][-1 - dst[j]] = (_Float16)v[j];
+    for (int j = 0; j < NI; ++j) {
+      const int idx = tid + j * NT;
+      if (idx >= NX4 + NW4) break;
+      const int i2 = idx < NX4 ? idx : idx - NX4;
+      const int r = i2 >> 4, x = 4 * (i2 & 15);
+      const h16x4 hv = {(_Float16)v[j].x, (_Float16)v[j].y, (_Float16)v[j].z, (_Float16)v[j].w};
+      _Float16* dst = idx < NX4 ? &sx[buf][r * PITCH + x] : &sw[buf][r * PITCH + x];
+      *reinterpret_cast<h16x4*>(dst) = hv;
     }
   };
   f32x16 acc;
