@@ -285,6 +285,10 @@ void mm_per_set_size(mm_per* per, int64_t n);      /* host + device fill count (
 void mm_per_set_size_host(mm_per* per, int64_t n); /* host mirror only (graph-replayed inserts) */
 int mm_per_copy_tree(mm_per* per, double* dst, mm_stream_t s);
 int mm_per_copy_slot_rows(mm_per* per, int64_t* dst, mm_stream_t s);
+/* Sticky device error bits of the PER (1 = an mm_per_update node outside the leaf range was skipped);
+ * synchronous; clear != 0 resets them. Replaces the IndexError / silent internal-node write of the
+ * reference's `self.tree[idx] = p` (vdn/replay_buffer/sumtree.py update) for bad indices. */
+int mm_per_error_word(mm_per* per, int32_t* host_out, int32_t clear, mm_stream_t s);
 /* Checkpoint state of the replay: tree (device f64 [2cap-1]) and slot -> row map (device i64 [cap])
  * copied stream-ordered; scalars[6] (host) = fill count, alpha, beta, alpha_inc, beta_inc, sample-call
  * counter (the device RNG stream index). Both calls synchronise the stream (the scalars cross PCIe). */

@@ -32,6 +32,8 @@ struct PerDev {
   int64_t n_data;
   double alpha, beta, alpha_inc, beta_inc;
   uint64_t n_samples;
+  int32_t err;   // sticky error bits: 1 = a priority update named a node outside the leaves (skipped)
+  int32_t pad;
 };
 }  // namespace mm
 
@@ -532,16 +534,86 @@ __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t ca
   }
 }
 
+// Small batches (B <= PU_B, power-of-two capacity: every leaf at depth L): one round trip for the sample
+// nodes / TDs, one for every sibling along the changed root paths, then the paths re-summed bottom-up in
+// LDS — each changed node = left child + right child, the changed child from LDS, the unchanged one as
+// loaded — the same f64 pairwise sums as rebuild_tree, so identical trees; duplicate nodes: the LAST
+// sample index wins. (The general kernel below pays a global round trip per 4 levels plus the duplicate
+// scratch passes: 13.8 us at B = 32 on a 65536-leaf tree.)
+constexpr int PU_B = 64, PU_L = 30;
+__global__ __launch_bounds__(1024) void per_update_small_kernel(double* tree, int64_t cap, const int64_t* nodes,
+                                                                const float* td, int B, PerDev* st, float eps) {
+  __shared__ int64_t snd[PU_B];
+  __shared__ float stv[PU_B];
+  __shared__ double sval[PU_L + 1][PU_B];   // [depth][sample]: new value of the sample's ancestor
+  __shared__ double ssib[PU_L + 1][PU_B];   // [depth][sample]: stored value of that ancestor's sibling
+  const int L = 63 - __clzll((unsigned long long)cap);
+  const int t = threadIdx.x;
+  const float alpha = (float)st->alpha;
+  if (t < B) {
+    const int64_t nd = nodes[t];
+    const bool ok = nd >= cap - 1 && nd < 2 * cap - 1;
+    snd[t] = ok ? nd : -1;
+    stv[t] = td[t];
+    if (!ok) atomicOr(&st->err, 1);
+  }
+  __syncthreads();
+  for (int i = t; i < B * L; i += blockDim.x) {
+    const int k = i / L, d = 1 + i % L;
+    const int64_t nd = snd[k];
+    if (nd >= 0) {
+      const int64_t a = ((nd + 1) >> (L - d)) - 1;   // ancestor at depth d
+      ssib[d][k] = tree[((a + 1) ^ 1) - 1];
+    }
+  }
+  if (t < B && snd[t] >= 0) {
+    int w = t;   // the last sample naming the same leaf
+    for (int k2 = t + 1; k2 < B; ++k2)
+      if (snd[k2] == snd[t]) w = k2;
+    // the reference computes (td + eps) ** alpha on a float32 tensor (vdn/_train.py:230-233)
+    const double v = (double)powf(stv[w] + eps, alpha);
+    sval[L][t] = v;
+    if (w == t) tree[snd[t]] = v;
+  }
+  __syncthreads();
+  for (int d = L - 1; d >= 0; --d) {
+    if (t < B && snd[t] >= 0) {
+      const int64_t nd = snd[t];
+      const int64_t c = ((nd + 1) >> (L - d - 1)) - 1, s = ((c + 1) ^ 1) - 1;   // path child, its sibling
+      double sv = ssib[d + 1][t];
+      for (int k2 = 0; k2 < B; ++k2) {
+        const int64_t n2 = snd[k2];
+        if (n2 >= 0 && ((n2 + 1) >> (L - d - 1)) - 1 == s) {
+          sv = sval[d + 1][k2];   // the sibling is on another changed path
+          break;
+        }
+      }
+      const double cv = sval[d + 1][t];
+      const double v = (c & 1) ? cv + sv : sv + cv;   // odd index = left child
+      sval[d][t] = v;
+      tree[((nd + 1) >> (L - d)) - 1] = v;
+    }
+    __syncthreads();
+  }
+}
+
 // Duplicate nodes: the LAST sample index wins (sequential tree[idx] = p semantics). One workgroup;
 // the per-leaf winner is found with atomicMax into the leaf scratch `last` (all -1 between calls,
 // restored before the rebuild), O(B) instead of comparing every pair.
 __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t cap, const int64_t* nodes, const float* td,
                                                         int B, const PerDev* st, float eps, int32_t* last) {
   const float alpha = (float)st->alpha;
+  bool bad = false;
   for (int k = threadIdx.x; k < B; k += PT) {
     const int64_t nd = nodes[k];
-    if (nd >= cap - 1 && nd < 2 * cap - 1) atomicMax(&last[nd - (cap - 1)], k);
+    if (nd >= cap - 1 && nd < 2 * cap - 1)
+      atomicMax(&last[nd - (cap - 1)], k);
+    else
+      bad = true;
   }
+  // out-of-range nodes are skipped (the reference's tree[idx] = p would raise or write an internal node)
+  // and flagged in the sticky error word, read by mm_per_error_word
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&const_cast<PerDev*>(st)->err, 1);
   __syncthreads();
   for (int k = threadIdx.x; k < B; k += PT) {
     const int64_t nd = nodes[k];
@@ -593,18 +665,18 @@ __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t ca
 // ---------------------------------------------------------------- multi-block batched insert
 // For large power-of-two capacities the single-workgroup insert is bound by one CU's memory
 // bandwidth over the whole tree. This path spreads every pass over G = cap/1024 workgroups in FOUR
-// stream-ordered launches (graph-capturable, same results as per_add_fast_kernel); each pass's grid-wide
-// reduction is finished by its last-arriving workgroup (arrival ticket, no spinning):
+// stream-ordered launches (graph-capturable, same results as per_add_fast_kernel). A pass's decision is
+// re-derived by EVERY workgroup of the next launch from the finished global counts (the launch boundary
+// orders it after the previous pass's atomics), so only the last pass needs an arrival ticket:
 //   A sel1    [the chunk's last rollout TD / store, folded in: td_chunk_kernel's arithmetic]
-//             12-bit histogram (sign + exponent) of the candidate keys; the last block picks the
-//             threshold's bin b1
-//   B sel2    histogram of bits 51..40 of the keys in b1; the last block picks b2
-//   C sel3    keys with the 24-bit prefix (b1, b2) listed with their slots, per-block counts of the
-//             keys below the prefix; the last block radix-selects the exact key T among the listed
-//             keys (8-bit digits over bits 39..0) and turns the counts into per-block victim offsets
-//   D apply   every block writes its own victims / free slots ((td + eps)^alpha, row swaps), rebuilds
-//             its 1024-leaf subtree from LDS; the last block builds the top levels, updates n_data and
-//             clears the scratch for the next insert
+//             12-bit histogram (sign + exponent) of the candidate keys
+//   B sel2    each block picks the threshold's bin b1; histogram of bits 51..40 of the keys in b1
+//   C sel3    each block picks b2; keys with the 24-bit prefix (b1, b2) listed with their slots,
+//             per-block counts of the keys below the prefix
+//   D apply   each block radix-selects the exact key T among the listed keys (8-bit digits over bits
+//             39..0) and its own victim offsets, writes its victims / free slots ((td + eps)^alpha, row
+//             swaps) and rebuilds its 1024-leaf subtree from LDS; the last block (ticket) builds the top
+//             levels and updates n_data
 constexpr int MB_T = 256, MB_VPT = 4, MB_SLOTS = MB_T * MB_VPT;   // 1024 slots per block
 constexpr int64_t MB_MIN_CAP = 16384;
 constexpr int MB_CAND_LDS = 4096;
@@ -733,14 +805,12 @@ __device__ void mb_td_fold(TdFuse t, int64_t E, int N, float (*sh)[MB_T]) {
 __global__ __launch_bounds__(MB_T) void per_mb_sel1(const double* __restrict__ tree, int64_t cap, const PerDev* st,
                                                     int64_t K, MbScratch* mb, TdFuse tdf, int32_t td_n) {
   __shared__ uint32_t h[4096];
-  __shared__ uint32_t wsum[MB_T / 64];
-  __shared__ int64_t sh[2];
-  __shared__ uint32_t s_last;
   __shared__ float shtd[3][MB_T];
   if (tdf.on) mb_td_fold(tdf, K, td_n, shtd);
+  // the candidate list of the previous insert was last read by its apply launch, which has finished
+  if (blockIdx.x == 0 && threadIdx.x == 0) mb->cand_n = 0;
   const int64_t n_data = st->n_data;
-  int64_t need = K - min(K, cap - n_data);
-  if (need <= 0) return;
+  if (K - min(K, cap - n_data) <= 0) return;
   const double* leaves = tree + (cap - 1);
   for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
   __syncthreads();
@@ -753,25 +823,25 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel1(const double* __restrict__ t
   __syncthreads();
   for (int i = threadIdx.x; i < 4096; i += MB_T)
     if (h[i]) atomicAdd(&mb->hist1[i], h[i]);
-  if (!mb_last(&mb->ticket, &s_last)) return;
-  const int b1 = mb_pick(mb->hist1, need, wsum, sh);
-  if (threadIdx.x == 0) {
-    mb->sel[0] = (uint64_t)b1;
-    mb->sel[1] = (uint64_t)need;
-    mb->ticket = 0;
-  }
 }
 
+// Every workgroup of sel2 / sel3 / apply re-derives the previous pass's decision itself from the finished
+// global histogram / candidate list (the launch boundary orders it after every atomic of the previous
+// pass), so no pass needs an arrival ticket and its device-scope fences; block 0 records the decision for
+// the launch after next (sel[0..1] by sel2, sel[2..3] by sel3: never a slot the same launch reads).
 __global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ tree, int64_t cap, const PerDev* st,
                                                     int64_t K, MbScratch* mb) {
   __shared__ uint32_t h[4096];
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
-  __shared__ uint32_t s_last;
   const int64_t n_data = st->n_data;
-  if (K - min(K, cap - n_data) <= 0) return;
-  const uint64_t b1 = mb->sel[0];
-  int64_t need = (int64_t)mb->sel[1];
+  int64_t need = K - min(K, cap - n_data);
+  if (need <= 0) return;
+  const uint64_t b1 = (uint64_t)mb_pick(mb->hist1, need, wsum, sh);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    mb->sel[0] = b1;
+    mb->sel[1] = (uint64_t)need;
+  }
   const double* leaves = tree + (cap - 1);
   for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
   __syncthreads();
@@ -787,26 +857,23 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ t
   __syncthreads();
   for (int i = threadIdx.x; i < 4096; i += MB_T)
     if (h[i]) atomicAdd(&mb->hist2[i], h[i]);
-  if (!mb_last(&mb->ticket, &s_last)) return;
-  const int b2 = mb_pick(mb->hist2, need, wsum, sh);
-  if (threadIdx.x == 0) {
-    mb->sel[0] = (b1 << 12) | (uint64_t)b2;   // the 24-bit prefix
-    mb->sel[1] = (uint64_t)need;
-    mb->ticket = 0;
-  }
 }
 
 __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ tree, int64_t cap, const PerDev* st,
                                                     int64_t K, MbScratch* mb) {
-  __shared__ uint64_t cl[MB_CAND_LDS];
-  __shared__ uint32_t bins[256];
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
-  __shared__ uint32_t s_last;
-  __shared__ uint32_t cnt[2 * MB_MAX_BLOCKS];
   const int64_t n_data = st->n_data;
   if (K - min(K, cap - n_data) <= 0) return;
-  const uint64_t pre = mb->sel[0];
+  const uint64_t b1 = mb->sel[0];
+  int64_t need = (int64_t)mb->sel[1];
+  const uint64_t pre = (b1 << 12) | (uint64_t)mb_pick(mb->hist2, need, wsum, sh);   // the 24-bit prefix
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    mb->sel[2] = pre;
+    mb->sel[3] = (uint64_t)need;
+  }
+  // hist1 was last read by sel2 (finished): cleared here for the next insert
+  for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist1[i] = 0;
   const double* leaves = tree + (cap - 1);
   uint64_t* ckey = mb->cand;
   uint64_t* cslot = mb->cand + cap;
@@ -829,14 +896,21 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
   uint32_t tb;
   (void)mb_scan(below, wsum, &tb);
   if (threadIdx.x == 0) mb->blk[blockIdx.x] = tb;
-  if (!mb_last(&mb->ticket, &s_last)) return;
-  // ---- last block: exact key T among the listed keys (radix select over bits 39..0)
-  int64_t need = (int64_t)mb->sel[1];
-  const uint32_t m = __hip_atomic_load(&mb->cand_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The exact threshold key T among the listed candidates (radix select over bits 39..0 below the 24-bit
+// prefix) and this workgroup's victim offsets: lt_off = keys < T in the workgroups before it (their keys
+// below the prefix + their listed keys < T), eq_off = listed keys == T in them. Run by every workgroup.
+__device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uint32_t* bins, uint32_t* wsum,
+                             int64_t* sh, uint64_t& T, int64_t& take_eq, int64_t& lt_off, int64_t& eq_off) {
+  const uint64_t pre = mb->sel[2];
+  int64_t need = (int64_t)mb->sel[3];
+  const uint64_t* ckey = mb->cand;
+  const uint64_t* cslot = mb->cand + cap;
+  const uint32_t m = mb->cand_n;
   const bool in_lds = m <= (uint32_t)MB_CAND_LDS;
   if (in_lds)
-    for (uint32_t i = threadIdx.x; i < m; i += MB_T)
-      cl[i] = __hip_atomic_load(&ckey[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = threadIdx.x; i < m; i += MB_T) cl[i] = ckey[i];
   __syncthreads();
   uint64_t prefix = pre << 40;
   for (int shift = 32; shift >= 0; shift -= 8) {
@@ -844,7 +918,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
     __syncthreads();
     const uint64_t hmask = ~0ull << (shift + 8);
     for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
-      const uint64_t k = in_lds ? cl[i] : __hip_atomic_load(&ckey[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t k = in_lds ? cl[i] : ckey[i];
       if ((k & hmask) == prefix) atomicAdd(&bins[(k >> shift) & 255], 1u);
     }
     __syncthreads();
@@ -860,49 +934,22 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
     need = sh[1];
     __syncthreads();
   }
-  const uint64_t T = prefix;   // the rest-th smallest key; the first `need` slots equal to it are taken
-  // per block: lt = keys below the prefix + listed keys < T, eq = listed keys == T
-  const int G = (int)gridDim.x;
-  for (int b = threadIdx.x; b < G; b += MB_T) {
-    cnt[2 * b] = __hip_atomic_load(&mb->blk[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    cnt[2 * b + 1] = 0;
-  }
-  __syncthreads();
+  T = prefix;        // the rest-th smallest key; the first `need` slots equal to it are taken
+  take_eq = need;
+  const uint32_t me = blockIdx.x;
+  uint32_t lt = 0, eq = 0;
+  for (uint32_t b = threadIdx.x; b < me; b += MB_T) lt += mb->blk[b];
   for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
-    const uint64_t k = in_lds ? cl[i] : __hip_atomic_load(&ckey[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int b = (int)(__hip_atomic_load(&cslot[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / MB_SLOTS);
-    if (k < T) atomicAdd(&cnt[2 * b], 1u);
-    else if (k == T) atomicAdd(&cnt[2 * b + 1], 1u);
+    if ((uint32_t)(cslot[i] / MB_SLOTS) >= me) continue;
+    const uint64_t k = in_lds ? cl[i] : ckey[i];
+    lt += k < T ? 1u : 0u;
+    eq += k == T ? 1u : 0u;
   }
-  __syncthreads();
-  // exclusive prefix over blocks (G <= 1024: four entries per thread)
-  uint32_t lt4[4], eq4[4], slt = 0, seq = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int b = threadIdx.x * 4 + q;
-    lt4[q] = b < G ? cnt[2 * b] : 0u;
-    eq4[q] = b < G ? cnt[2 * b + 1] : 0u;
-    slt += lt4[q];
-    seq += eq4[q];
-  }
-  uint32_t tot;
-  uint32_t blt = mb_scan(slt, wsum, &tot);
-  uint32_t beq = mb_scan(seq, wsum, &tot);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int b = threadIdx.x * 4 + q;
-    if (b < G) {
-      mb->blk[b] = blt;
-      mb->blk[MB_MAX_BLOCKS + b] = beq;
-    }
-    blt += lt4[q];
-    beq += eq4[q];
-  }
-  if (threadIdx.x == 0) {
-    mb->sel[2] = T;
-    mb->sel[3] = (uint64_t)need;
-    mb->ticket = 0;
-  }
+  uint32_t tl, te;
+  (void)mb_scan(lt, wsum, &tl);
+  (void)mb_scan(eq, wsum, &te);
+  lt_off = tl;
+  eq_off = te;
 }
 
 __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
@@ -910,7 +957,10 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
                                                      int64_t* slots_out, MbScratch* mb) {
   __shared__ double lv[MB_SLOTS];
   __shared__ double v[2][MB_SLOTS / 2];
+  __shared__ uint64_t cl[MB_CAND_LDS];
+  __shared__ uint32_t bins[256];
   __shared__ uint32_t wsum[MB_T / 64];
+  __shared__ int64_t sh[2];
   __shared__ uint32_t s_last;
   const int L = 63 - __clzll((unsigned long long)cap);      // leaves at level L
   const int64_t n_data = st->n_data;
@@ -919,7 +969,8 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   const bool evict = K - free_n > 0;
   double* leaves = tree + (cap - 1);
   const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
-  // this block's 1024 leaves: 4 contiguous per thread (keys for the victim test, LDS copy for the rebuild)
+  // this block's 1024 leaves: 4 contiguous per thread (keys for the victim test, LDS copy for the
+  // rebuild), loaded first so the latency overlaps the threshold selection
   const int64_t s0 = base + threadIdx.x * MB_VPT;
   double x[MB_VPT];
   {
@@ -930,10 +981,15 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
     x[2] = b.x;
     x[3] = b.y;
   }
-  uint32_t lt = 0, eq = 0;
   uint64_t T = 0;
+  int64_t take_eq = 0, lt_off = 0, eq_off = 0;
   if (evict) {
-    T = mb->sel[2];
+    mb_threshold(mb, cap, cl, bins, wsum, sh, T, take_eq, lt_off, eq_off);
+    // hist2 was last read by sel3 (finished): cleared here for the next insert
+    for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist2[i] = 0;
+  }
+  uint32_t lt = 0, eq = 0;
+  if (evict) {
 #pragma unroll
     for (int i = 0; i < MB_VPT; ++i) {
       const uint64_t k = s0 + i < n_data ? (uint64_t)__double_as_longlong(x[i]) : ~0ull;
@@ -944,11 +1000,8 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   uint32_t tot;
   int64_t lt_rank = mb_scan(lt, wsum, &tot);
   int64_t eq_rank = mb_scan(eq, wsum, &tot);
-  if (evict) {
-    lt_rank += mb->blk[blockIdx.x];
-    eq_rank += mb->blk[MB_MAX_BLOCKS + blockIdx.x];
-  }
-  const int64_t take_eq = evict ? (int64_t)mb->sel[3] : 0;
+  lt_rank += lt_off;
+  eq_rank += eq_off;
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = s0 + i;
@@ -1023,13 +1076,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
     }
     __syncthreads();
   }
-  // the next insert starts from clear histograms / list / ticket
-  for (int i = threadIdx.x; i < 4096; i += MB_T) {
-    mb->hist1[i] = 0;
-    mb->hist2[i] = 0;
-  }
   if (threadIdx.x == 0) {
-    mb->cand_n = 0;
     mb->ticket = 0;
     st->n_data = min(cap, n_data + K);
   }
@@ -1248,8 +1295,12 @@ int mm_per_sample_rng(mm_per* per, int32_t batch, uint64_t seed, uint64_t counte
 int mm_per_update(mm_per* per, const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s) {
   MM_REQUIRE(per && nodes && td, "per_update: null argument");
   MM_REQUIRE(batch >= 1 && batch <= 65536, "per_update: bad batch");
-  hipLaunchKernelGGL(mm::per_update_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->cap, nodes, td,
-                     batch, per->st, (float)per->eps, per->last);
+  if ((per->cap & (per->cap - 1)) == 0 && batch <= mm::PU_B)
+    hipLaunchKernelGGL(mm::per_update_small_kernel, dim3(1), dim3(1024), 0, (hipStream_t)s, per->tree, per->cap, nodes,
+                       td, batch, per->st, (float)per->eps);
+  else
+    hipLaunchKernelGGL(mm::per_update_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->cap, nodes, td,
+                       batch, per->st, (float)per->eps, per->last);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -1267,6 +1318,13 @@ void mm_per_set_size(mm_per* per, int64_t n) {
   if (!per) return;
   per->n_data = n;
   (void)hipMemcpy(&per->st->n_data, &n, sizeof(n), hipMemcpyHostToDevice);
+}
+int mm_per_error_word(mm_per* per, int32_t* host_out, int32_t clear, mm_stream_t s) {
+  MM_REQUIRE(per && host_out, "per_error_word: null argument");
+  MM_HIP_CHECK(hipMemcpyAsync(host_out, &per->st->err, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)s));
+  if (clear) MM_HIP_CHECK(hipMemsetAsync(&per->st->err, 0, sizeof(int32_t), (hipStream_t)s));
+  MM_HIP_CHECK(hipStreamSynchronize((hipStream_t)s));
+  return MM_OK;
 }
 int mm_per_copy_tree(mm_per* per, double* dst, mm_stream_t s) {
   MM_REQUIRE(per && dst, "per_copy_tree: null argument");
@@ -1310,6 +1368,8 @@ int mm_per_load_state(mm_per* per, const double* tree_src, const int64_t* rows_s
   h.alpha_inc = scalars[3];
   h.beta_inc = scalars[4];
   h.n_samples = (uint64_t)scalars[5];
+  h.err = 0;
+  h.pad = 0;
   MM_HIP_CHECK(hipMemcpyAsync(per->st, &h, sizeof(h), hipMemcpyHostToDevice, (hipStream_t)s));
   MM_HIP_CHECK(hipStreamSynchronize((hipStream_t)s));
   per->n_data = h.n_data;

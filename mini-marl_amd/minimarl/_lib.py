@@ -114,6 +114,7 @@ _SIGS = [
     ("mm_per_set_size_host", None, [c_vp, c_i64]),
     ("mm_per_copy_tree", c_i32, [c_vp, c_vp, c_vp]),
     ("mm_per_copy_slot_rows", c_i32, [c_vp, c_vp, c_vp]),
+    ("mm_per_error_word", c_i32, [c_vp, c_vp, c_i32, c_vp]),
 ]
 
 _lib = None

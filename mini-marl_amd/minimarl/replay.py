@@ -96,6 +96,20 @@ class DevicePER:
         check(lib().mm_per_copy_slot_rows(self._h, ptr(out), stream_handle(self.device)), "per_copy_rows")
         return out
 
+    def error_word(self, clear=False):
+        """Sticky device error bits (synchronous): 1 = a priority update named a node outside the
+        leaves; the kernel skipped it (the reference's tree write would raise / corrupt a node)."""
+        out = ctypes.c_int32(0)
+        check(lib().mm_per_error_word(self._h, ctypes.byref(out), int(bool(clear)), stream_handle(self.device)),
+              "per_error_word")
+        return int(out.value)
+
+    def check_errors(self):
+        """Raise IndexError if a device-side priority update was given an out-of-range node."""
+        e = self.error_word(clear=True)
+        if e & 1:
+            raise IndexError("PER update: tree node outside the leaf range [cap-1, 2cap-1) (skipped on device)")
+
     def slot_rows_ptr(self):
         return lib().mm_per_slot_rows(self._h)
 

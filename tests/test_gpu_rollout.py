@@ -212,6 +212,56 @@ def test_per_batched_vs_oracle(flavor, cap, kb, rounds):
         np.testing.assert_allclose(dev.tree().cpu().numpy(), ora.tree, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("cap,B", [(65536, 32), (65536, 64), (1024, 1), (1024, 64), (4, 8)])
+def test_per_small_batch_update_vs_oracle(cap, B):
+    """Small-batch priority update (LDS path re-sum, B <= 64 on power-of-two trees) vs the oracle's full
+    rebuild: sampled nodes with duplicates and shared ancestors, several rounds."""
+    dev, ora = _per_pair("qmix", cap)
+    rng = np.random.default_rng(7)
+    td = (rng.random(cap) * 2).astype(np.float32)
+    dev.add(torch.tensor(td))
+    ora.add_batch([float(x) for x in td])
+    for rnd in range(4):
+        fr = rng.random(B)
+        nodes, _, _ = dev.sample(B, fracs=fr)
+        on, _, _, _ = ora.sample(B, fr)               # keeps the oracle's alpha / beta schedule in step
+        nd = nodes.cpu().numpy().copy()
+        np.testing.assert_array_equal(nd, on)
+        if B > 2:
+            nd[1] = nd[0]                              # a duplicate: the later sample wins
+            nd[2] = ((nd[0] + 1) ^ 1) - 1              # the sibling leaf of a changed leaf
+        newtd = rng.random(B).astype(np.float32)
+        dev.update(torch.tensor(nd, device=DEV), torch.tensor(newtd))
+        for k in range(B):
+            ora.tree[nd[k]] = float(np.float32((np.float32(newtd[k]) + np.float32(1e-6)) ** np.float32(ora.alpha)))
+        ora.rebuild()
+        np.testing.assert_allclose(dev.tree().cpu().numpy(), ora.tree, rtol=1e-6, atol=1e-9)
+    assert dev.error_word() == 0
+
+
+@pytest.mark.parametrize("cap", [64, 100])
+def test_per_update_flags_out_of_range_nodes(cap):
+    """Nodes outside the leaf range are skipped (tree unchanged there) and set the sticky error bit;
+    in-range nodes of the same update are applied as usual."""
+    dev, ora = _per_pair("vdn", cap)
+    td = np.linspace(0.1, 2.0, 40).astype(np.float32)
+    dev.add(torch.tensor(td))
+    ora.add_batch([float(x) for x in td])
+    assert dev.error_word() == 0
+    good = cap - 1 + 3
+    nodes = torch.tensor([good, 0, cap - 2, 2 * cap - 1, -5], dtype=torch.int64, device=DEV)
+    dev.update(nodes, torch.tensor([0.7, 9.0, 9.0, 9.0, 9.0]))
+    ora.tree[good] = float(np.float32((np.float32(0.7) + np.float32(1e-6)) ** np.float32(ora.alpha)))
+    ora.rebuild()
+    np.testing.assert_allclose(dev.tree().cpu().numpy(), ora.tree, rtol=1e-6, atol=1e-9)
+    assert dev.error_word() == 1
+    with pytest.raises(IndexError):
+        dev.check_errors()                       # raises and clears
+    assert dev.error_word() == 0
+    dev.update(nodes[:1], torch.tensor([0.3]))
+    dev.check_errors()                           # in-range only: no error
+
+
 def test_rollout_engine_end_to_end_vs_oracle():
     """Engine transitions (store contents), TD chunk priorities and actions vs an oracle replay.
     In-chunk steps run the env kernel fused with the previous step's TD/store, so the store rows
