@@ -346,129 +346,6 @@ __global__ __launch_bounds__(64 * 2 * RBK) void mixer_gi_f16_kernel(MixGiArgs a)
   }
 }
 
-// The same fp16 projection shaped for HBM bandwidth (the cfg5 update reads 2 x R rows of S = 8100
-// floats): the kernel above stages every 64-sample tile's state AND the whole W_ih (3Hm x S f32) through
-// LDS per block, so W_ih crosses L2 -> LDS once per 64 samples (4 GB per cfg5 update, more than the
-// 2.65 GB of state). Here a block is WPB waves x 32 samples (WPB picked so the grid is one round of <= 256
-// blocks): each wave streams its own 32 state rows straight into registers (lane (sample, half) loads the 8
-// consecutive k its B fragment needs, two 64-deep chunks in flight), and only W_ih goes through LDS (f16,
-// double-buffered, shared by the WPB waves). Same fragments, same MFMA order over k, same zero padding
-// beyond S as mixer_gi_f16_kernel: bit-identical results.
-template <int RBK, int WPB>
-__global__ __launch_bounds__(64 * WPB) void mixer_gi_f16s_kernel(MixGiArgs a, int passes) {
-  constexpr int NT = 64 * WPB, ROWS = 32 * RBK, PITCH = 72, KC = 64;
-  constexpr int NW4 = ROWS * KC / 4, NI = (NW4 + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) _Float16 sw[2][ROWS * PITCH];
-  const MixGiNet& nt = a.net[blockIdx.y];
-  const int S = a.S, M3 = 3 * a.Hm;
-  const MixOff o = mix_offsets(S, a.Hm, a.K1, a.N);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, lh = lane >> 5;
-  const float* Wih = nt.P + o.gWih;
-  const bool wal = (reinterpret_cast<uintptr_t>(Wih) & 15) == 0 && (S & 3) == 0;
-  for (int pass = 0; pass < passes; ++pass) {
-  const int c = (blockIdx.x * passes + pass) * (32 * WPB) + wave * 32 + li;
-  if (__builtin_amdgcn_readfirstlane((blockIdx.x * passes + pass) * (32 * WPB)) >= a.R) break;
-  const int64_t off = state_off(nt.s_off, min(c, a.R - 1), S);
-  const float* srow = off >= 0 ? a.obs + off : a.reset_obs;
-  const bool sal = (reinterpret_cast<uintptr_t>(srow) & 15) == 0;
-  float4 wv[NI];
-  auto wload = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int idx = tid + j * NT;
-      if (idx >= NW4) break;
-      const int r = idx >> 4, k = k0 + 4 * (idx & 15);
-      const float* row = Wih + (int64_t)min(r, M3 - 1) * S;
-      if (wal && k + 3 < S) {
-        wv[j] = *reinterpret_cast<const float4*>(row + k);
-      } else {
-        wv[j].x = k < S ? row[k] : 0.f;
-        wv[j].y = k + 1 < S ? row[k + 1] : 0.f;
-        wv[j].z = k + 2 < S ? row[k + 2] : 0.f;
-        wv[j].w = k + 3 < S ? row[k + 3] : 0.f;
-      }
-    }
-  };
-  auto wstore = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int idx = tid + j * NT;
-      if (idx >= NW4) break;
-      const int r = idx >> 4, x = 4 * (idx & 15);
-      const h16x4 hv = {(_Float16)wv[j].x, (_Float16)wv[j].y, (_Float16)wv[j].z, (_Float16)wv[j].w};
-      *reinterpret_cast<h16x4*>(&sw[buf][r * PITCH + x]) = hv;
-    }
-  };
-  // state chunk at k0: d[2 ks], d[2 ks + 1] = s[k0 + 16 ks + 8 lh + 0..7] (zero beyond S)
-  auto sload = [&](int k0, float4 (&d)[8]) {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int k = k0 + 16 * ks + 8 * lh;
-      if (sal && k + 7 < S) {
-        d[2 * ks] = *reinterpret_cast<const float4*>(srow + k);
-        d[2 * ks + 1] = *reinterpret_cast<const float4*>(srow + k + 4);
-      } else {
-        float t[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) t[i] = k + i < S ? srow[k + i] : 0.f;
-        d[2 * ks] = make_float4(t[0], t[1], t[2], t[3]);
-        d[2 * ks + 1] = make_float4(t[4], t[5], t[6], t[7]);
-      }
-    }
-  };
-  f32x16 acc[RBK];
-#pragma unroll
-  for (int r = 0; r < RBK; ++r)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[r][q] = 0.f;
-  auto compute = [&](const float4 (&d)[8], int buf) {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const float4 u = d[2 * ks], v = d[2 * ks + 1];
-      const h16x8 bv = {(_Float16)u.x, (_Float16)u.y, (_Float16)u.z, (_Float16)u.w,
-                        (_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-#pragma unroll
-      for (int r = 0; r < RBK; ++r) {
-        const h16x8 av = *reinterpret_cast<const h16x8*>(&sw[buf][(r * 32 + li) * PITCH + ks * 16 + 8 * lh]);
-        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc[r], 0, 0, 0);
-      }
-    }
-  };
-  const int nch = (S + KC - 1) / KC;
-  float4 sa[8], sb[8];
-  sload(0, sa);
-  if (nch > 1) sload(KC, sb);
-  wload(0);
-  wstore(0);
-  __syncthreads();
-  for (int ch = 0; ch < nch; ch += 2) {
-    // even chunk: state in sa, weights in buffer 0
-    if (ch + 1 < nch) wload((ch + 1) * KC);
-    compute(sa, 0);
-    if (ch + 2 < nch) sload((ch + 2) * KC, sa);
-    if (ch + 1 < nch) wstore(1);
-    __syncthreads();
-    if (ch + 1 >= nch) break;
-    // odd chunk: state in sb, weights in buffer 1
-    if (ch + 2 < nch) wload((ch + 2) * KC);
-    compute(sb, 1);
-    if (ch + 3 < nch) sload((ch + 3) * KC, sb);
-    if (ch + 2 < nch) wstore(0);
-    __syncthreads();
-  }
-  if (c < a.R) {
-#pragma unroll
-    for (int r = 0; r < RBK; ++r)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int m = r * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-        if (m < M3) nt.gi[(int64_t)c * M3 + m] = nt.P[o.gbih + m] + acc[r][q];
-      }
-  }
-  __syncthreads();   // the next pass restages both weight buffers
-  }
-}
-
 // One block per (sample, net): blockIdx.y selects behavior / target.
 __device__ __forceinline__ void mixer_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, int b);
 
@@ -2734,16 +2611,11 @@ int mm_mixer_gi_f16(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, con
   a.Hm = Hm;
   a.K1 = K1;
   a.N = N;
-  // 4 waves (one per SIMD, no spills at either Hm) x 32 samples per pass; a block makes enough passes
-  // that the grid fits two blocks per CU (every byte of state in flight from the first round)
-  const int nets = P1 ? 2 : 1;
-  const int tiles = (R + 31) / 32;
-  const int passes = std::max(1, (tiles * nets + 4 * 512 - 1) / (4 * 512));
-  const dim3 grid((tiles + 4 * passes - 1) / (4 * passes), nets);
+  dim3 grid((R + 63) / 64, P1 ? 2 : 1);
   if (Hm == 32)
-    hipLaunchKernelGGL((mm::mixer_gi_f16s_kernel<3, 4>), grid, dim3(256), 0, (hipStream_t)s, a, passes);
+    hipLaunchKernelGGL(mm::mixer_gi_f16_kernel<3>, grid, dim3(384), 0, (hipStream_t)s, a);
   else
-    hipLaunchKernelGGL((mm::mixer_gi_f16s_kernel<6, 4>), grid, dim3(256), 0, (hipStream_t)s, a, passes);
+    hipLaunchKernelGGL(mm::mixer_gi_f16_kernel<6>, grid, dim3(768), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

@@ -547,6 +547,7 @@ __global__ __launch_bounds__(1024) void per_update_small_kernel(double* tree, in
   __shared__ float stv[PU_B];
   __shared__ double sval[PU_L + 1][PU_B];   // [depth][sample]: new value of the sample's ancestor
   __shared__ double ssib[PU_L + 1][PU_B];   // [depth][sample]: stored value of that ancestor's sibling
+  __shared__ int8_t spart[PU_L + 1][PU_B];  // [depth][sample]: a sample whose path holds that sibling, or -1
   const int L = 63 - __clzll((unsigned long long)cap);
   const int t = threadIdx.x;
   const float alpha = (float)st->alpha;
@@ -558,42 +559,48 @@ __global__ __launch_bounds__(1024) void per_update_small_kernel(double* tree, in
     if (!ok) atomicOr(&st->err, 1);
   }
   __syncthreads();
+  // per (sample, depth): the sibling's stored value (one round trip for all) and whether the sibling lies on
+  // another changed path (then its new value is taken instead); scans without early exit, so the LDS reads
+  // of a scan are all in flight together
   for (int i = t; i < B * L; i += blockDim.x) {
     const int k = i / L, d = 1 + i % L;
     const int64_t nd = snd[k];
     if (nd >= 0) {
       const int64_t a = ((nd + 1) >> (L - d)) - 1;   // ancestor at depth d
-      ssib[d][k] = tree[((a + 1) ^ 1) - 1];
+      const int64_t sib = ((a + 1) ^ 1) - 1;
+      ssib[d][k] = tree[sib];
+      int part = -1;
+#pragma unroll 8
+      for (int k2 = B - 1; k2 >= 0; --k2) {
+        const int64_t n2 = snd[k2];
+        part = (n2 >= 0 && ((n2 + 1) >> (L - d)) - 1 == sib) ? k2 : part;
+      }
+      spart[d][k] = (int8_t)part;
     }
   }
   if (t < B && snd[t] >= 0) {
     int w = t;   // the last sample naming the same leaf
-    for (int k2 = t + 1; k2 < B; ++k2)
-      if (snd[k2] == snd[t]) w = k2;
+#pragma unroll 8
+    for (int k2 = 0; k2 < B; ++k2) w = (k2 > t && snd[k2] == snd[t]) ? k2 : w;
     // the reference computes (td + eps) ** alpha on a float32 tensor (vdn/_train.py:230-233)
-    const double v = (double)powf(stv[w] + eps, alpha);
-    sval[L][t] = v;
-    if (w == t) tree[snd[t]] = v;
+    sval[L][t] = (double)powf(stv[w] + eps, alpha);
   }
   __syncthreads();
   for (int d = L - 1; d >= 0; --d) {
     if (t < B && snd[t] >= 0) {
-      const int64_t nd = snd[t];
-      const int64_t c = ((nd + 1) >> (L - d - 1)) - 1, s = ((c + 1) ^ 1) - 1;   // path child, its sibling
-      double sv = ssib[d + 1][t];
-      for (int k2 = 0; k2 < B; ++k2) {
-        const int64_t n2 = snd[k2];
-        if (n2 >= 0 && ((n2 + 1) >> (L - d - 1)) - 1 == s) {
-          sv = sval[d + 1][k2];   // the sibling is on another changed path
-          break;
-        }
-      }
+      const int64_t c = ((snd[t] + 1) >> (L - d - 1)) - 1;   // the path's child at depth d + 1
+      const int part = spart[d + 1][t];
+      const double sv = part >= 0 ? sval[d + 1][part] : ssib[d + 1][t];
       const double cv = sval[d + 1][t];
-      const double v = (c & 1) ? cv + sv : sv + cv;   // odd index = left child
-      sval[d][t] = v;
-      tree[((nd + 1) >> (L - d)) - 1] = v;
+      sval[d][t] = (c & 1) ? cv + sv : sv + cv;   // odd index = left child
     }
     __syncthreads();
+  }
+  // every changed node written once the paths are done; nodes shared by several paths get identical values
+  for (int i = t; i < B * (L + 1); i += blockDim.x) {
+    const int k = i / (L + 1), d = i % (L + 1);
+    const int64_t nd = snd[k];
+    if (nd >= 0) tree[((nd + 1) >> (L - d)) - 1] = sval[d][k];
   }
 }
 
