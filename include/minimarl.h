@@ -101,6 +101,11 @@ int mm_agent_q_pre2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_i
                     const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
 int mm_agent_q_rec2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
                     const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
+/* PRE on the fp16x3-split fragment image (the fast mode of large learner batches, QLearner(mixer_fp16=True)):
+ * same outputs as mm_agent_q_pre2 within the fp16x3 forward's rtol 1e-5 (not bit-identical); agents flagged by
+ * the pack-time range guard run on the exact-f32 image. Reference: qmix/_network.py:44-64 (Q_Net.forward). */
+int mm_agent_q_pre2_h3(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
+                       const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s);
 /* REC for all `steps` chunk steps in one launch (the W_hh fragments stay in registers, the hidden
  * state in LDS): step t reads io.gi / writes io.save, io.qsel_out and reads io.act_in at the step-0
  * pointers + t * (E*N*3H / E*N*SD / E*N / E*act_se); h_in/h_out are not used (zero start, resets

@@ -1426,6 +1426,121 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
                                     [&](int kb, float (&x)[8]) { load_obs_ks(orow, kb, p.D, x); }, xn, h0, eps, ctr);
 }
 
+// ---------------------------------------------------------------- learner PRE on the fp16x3 image
+// The learner's non-recurrent part (layers 1-2 with their training saves, and gi = W_ih x2 + b_ih) of large
+// batches in the fast (cfg5) mode, QLearner(mixer_fp16=True): agent_q_fwd_body_h3's layers 1-2 and its
+// W_ih gate products (fp16x3 split, fp32 accumulate: ~2^-22 relative per product, the forward's rtol 1e-5
+// parity) instead of agent_pre_body's exact-f32 MFMAs, at ~5x less MFMA time per product. Same outputs /
+// layouts as agent_pre_body: saves [x1 | x2] by feature, gi [r | z | n] by feature.
+template <int F1, int G, int H, int AB>
+__device__ __forceinline__ void agent_pre_body_h3(const QFwdParams& p, int agent, int e, const float* __restrict__ W,
+                                                  const float* orow) {
+  using CG = QnetCGeo<F1, G, H, AB>;
+  constexpr int T1 = F1 / 16, T2 = G / 16, TH = H / 16;
+  constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const bool valid = e < p.E;
+  const mm_qfwd_io& io = p.io;
+  float xn[8];
+  load_obs_ks(orow, 0, p.D, xn);
+  // ---- layer 1 (next obs k-step prefetched)
+  f32x4 x1[T1];
+#pragma unroll
+  for (int t = 0; t < T1; ++t) x1[t] = bias4(W + CG::off_b1, t, g);
+  for (int kb = 0; kb < p.g.KD; ++kb) {
+    KS ob;
+    split8(xn, ob);
+    if (kb + 1 < p.g.KD) load_obs_ks(orow, kb + 1, p.D, xn);
+#pragma unroll
+    for (int t = 0; t < T1; ++t) mm16(W + CG::off_l1 + (int64_t)((t >> 1) * p.g.KD + kb) * 1024, t & 1, ob, lane, x1[t]);
+  }
+  float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
+  KS x1s[RB1];
+#pragma unroll
+  for (int t = 0; t < T1; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x1[t][r] = fmaxf(x1[t][r], 0.0f);
+      if (sv) sv[16 * t + 4 * g + r] = x1[t][r];
+    }
+  }
+#pragma unroll
+  for (int kb = 0; kb < RB1; ++kb) split_pair(x1[2 * kb], x1[2 * kb + 1], x1s[kb]);
+  // ---- layer 2
+  f32x4 x2[T2];
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    x2[t] = bias4(W + CG::off_b2, t, g);
+#pragma unroll
+    for (int kb = 0; kb < RB1; ++kb) mm16(W + CG::off_l2 + ((t >> 1) * RB1 + kb) * 1024, t & 1, x1s[kb], lane, x2[t]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      x2[t][r] = fmaxf(x2[t][r], 0.0f);
+      if (sv) sv[F1 + 16 * t + 4 * g + r] = x2[t][r];
+    }
+  }
+  KS x2s[RB2];
+#pragma unroll
+  for (int kb = 0; kb < RB2; ++kb) split_pair(x2[2 * kb], x2[2 * kb + 1], x2s[kb]);
+  // ---- gi = W_ih x2 + b_ih (gates r, z, n), three gates' fragments per k-step interleaved
+  float* gi = valid ? io.gi + ((int64_t)e * p.N + agent) * 3 * H : nullptr;
+#pragma unroll
+  for (int t = 0; t < TH; ++t) {
+    const int rb = t >> 1, q = t & 1;
+    f32x4 ar = bias4(W + CG::off_brz, t, g);
+    f32x4 az = bias4(W + CG::off_brz + H, t, g);
+    f32x4 an = bias4(W + CG::off_bin, t, g);
+#pragma unroll
+    for (int kb = 0; kb < RB2; ++kb) {
+      const int base = CG::off_ih + (rb * RB2 + kb) * 1024, gs = HB * RB2 * 1024;
+      const Frag f0 = ldfrag(W + base, q, lane);
+      const Frag f1 = ldfrag(W + base + gs, q, lane);
+      const Frag f2 = ldfrag(W + base + 2 * gs, q, lane);
+      mmf(f0, x2s[kb], ar);
+      mmf(f1, x2s[kb], az);
+      mmf(f2, x2s[kb], an);
+    }
+    if (gi) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 16 * t + 4 * g + r;
+        gi[f] = ar[r];
+        gi[H + f] = az[r];
+        gi[2 * H + f] = an[r];
+      }
+    }
+  }
+}
+
+// 1024-thread block = 16 waves x 16 rows of one agent (the dual forward's geometry); an agent flagged by
+// the pack-time range guard runs its 256 rows on the exact-f32 image (agent_pre_body, 8 waves x 32 rows).
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(1024, 1) void agent_pre_h3_kernel(QFwdParams p0, QFwdParams p1) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  const bool second = (int)blockIdx.x >= p0.nblocks;
+  const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  const QFwdParams& p = kargs[second ? 1 : 0];
+  (void)p1;
+  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
+  const int agent = bid % p.N, tile = bid / p.N;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool exact = reinterpret_cast<const int*>(p.packed + 2 * p.g.agent_stride * p.N)[agent] != 0;
+  const float* src = p.packed + (exact ? 0 : (int64_t)p.N * p.g.agent_stride) + (int64_t)agent * p.g.agent_stride;
+  const int nchunk = (int)(p.g.agent_stride >> 8);
+  for (int c = wave; c < nchunk; c += 16)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 256 + lane * 4),
+                                     (__attribute__((address_space(3))) void*)(wsm + c * 256), 16, 0, 0);
+  __syncthreads();
+  if (exact) {
+    const int e32 = tile * 256 + wave * 32 + (lane & 31);
+    if (wave < 8) agent_pre_body<F1, G, H, AB>(p, agent, e32, wsm, obs_row_ptr(p, agent, e32));
+    return;
+  }
+  const int e = tile * 256 + wave * 16 + (lane & 15);
+  agent_pre_body_h3<F1, G, H, AB>(p, agent, e, wsm, obs_row_ptr(p, agent, e));
+}
+
 // ---------------------------------------------------------------- learner PRE, weights in LDS
 // Layers 1-2 and the GRU input projection of large learner batches: agent_pre_body (exact f32, one wave
 // = 32 rows) with the agent's f32 fragment image staged ONCE per 1024-thread block by LDS-DMA and shared
@@ -2077,12 +2192,27 @@ static int launch_split(int phase, QFwdParams p0, QFwdParams p1, hipStream_t s) 
   return MM_OK;
 }
 
+template <int F1, int G, int H, int AB>
+static int launch_pre_h3(QFwdParams p0, QFwdParams p1, hipStream_t s) {
+  const bool single = p1.nblocks == 0;
+  p0.nblocks = (p0.E + 255) / 256 * p0.N;
+  p1.nblocks = single ? 0 : (p1.E + 255) / 256 * p1.N;
+  const size_t sm = (size_t)p0.g.agent_stride * 4;
+  MM_REQUIRE(sm <= 160 * 1024, "agent_q_pre_h3: fragment image (%zu B) exceeds LDS", sm);
+  hipLaunchKernelGGL((agent_pre_h3_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(1024), sm, s, p0, p1);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 static int dispatch_split(const mm_qnet_dims* d, int phase, const QFwdParams& p0, const QFwdParams& p1,
                           hipStream_t s) {
   const int AB = (d->n_actions + 31) / 32;
 #define MM_SPLIT(F1_, G_, H_)                                                                               \
-  if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                             \
-    return AB == 1 ? launch_split<F1_, G_, H_, 1>(phase, p0, p1, s) : launch_split<F1_, G_, H_, 2>(phase, p0, p1, s);
+  if (d->f1 == F1_ && d->g == G_ && d->h == H_) {                                                           \
+    if (phase == 3)                                                                                         \
+      return AB == 1 ? launch_pre_h3<F1_, G_, H_, 1>(p0, p1, s) : launch_pre_h3<F1_, G_, H_, 2>(p0, p1, s); \
+    return AB == 1 ? launch_split<F1_, G_, H_, 1>(phase, p0, p1, s) : launch_split<F1_, G_, H_, 2>(phase, p0, p1, s); \
+  }
   MM_SPLIT(64, 32, 32)
   MM_SPLIT(64, 64, 64)
   MM_SPLIT(128, 32, 32)
@@ -2168,7 +2298,7 @@ int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const
   rc = make_params(d, packed1, io1, e1, &p1);
   if (rc) return rc;
   MM_REQUIRE(io0->gi && io1->gi, "agent_q_split: io.gi required");
-  MM_REQUIRE(phase == 2 || (io0->obs && io1->obs), "agent_q_pre: obs required");
+  MM_REQUIRE(phase == 2 || (io0->obs && io1->obs), "agent_q_pre: obs required");   // phase 3: PRE on fp16x3
   return dispatch_split(d, phase, p0, p1, s);
 }
 

@@ -85,6 +85,11 @@ int mm_agent_q_pre2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_i
   return mm::agent_q_split2(1, d, packed0, io0, n_envs0, packed1, io1, n_envs1, (hipStream_t)s);
 }
 
+int mm_agent_q_pre2_h3(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
+                       const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, mm_stream_t s) {
+  return mm::agent_q_split2(3, d, packed0, io0, n_envs0, packed1, io1, n_envs1, (hipStream_t)s);
+}
+
 int mm_agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,
                         const float* packed1, const mm_qfwd_io* io1, int64_t n_envs1, int32_t steps,
                         const uint8_t* reset, mm_stream_t s) {

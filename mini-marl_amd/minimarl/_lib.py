@@ -218,6 +218,8 @@ _SIGS += [
     ("mm_outer_reduce", c_i32, [ctypes.POINTER(OuterArgs), c_vp]),
     ("mm_agent_q_pre2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
                                 ctypes.POINTER(QFwdIO), c_i64, c_vp]),
+    ("mm_agent_q_pre2_h3", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
+                                ctypes.POINTER(QFwdIO), c_i64, c_vp]),
     ("mm_agent_q_rec_seq2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
                                     ctypes.POINTER(QFwdIO), c_i64, c_i32, c_vp, c_vp]),
     ("mm_mixer_bwd_seq", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -113,7 +113,8 @@ class QLearner:
         # of qmix/qmix.py:215-217 (no IS weight)
         self.reference_compat = bool(reference_compat)
         # cfg5 mode: the mixer state projection [B*C, N*D] x [N*D, 3Hm] on fp16 MFMA (rtol 2e-3
-        # on Q_tot, a tolerance stated apart from the fp32 parity)
+        # on Q_tot, a tolerance stated apart from the fp32 parity); at B*C >= 2048 also the agents'
+        # non-recurrent layers on the fp16x3-split image (mm_agent_q_pre2_h3, rtol 1e-5 of exact f32)
         self.mixer_fp16 = bool(mixer_fp16)
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM
@@ -305,8 +306,10 @@ class QLearner:
             io.h_in = self.hb.data_ptr()       # unused by PRE
             io.gi = gi.data_ptr()
         pb.save = self.asave.data_ptr()
-        check(L.mm_agent_q_pre2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pb), CB,
-                                ptr(self.tgt.packed), ctypes.byref(pt), CB, s), "learner fwd pre")
+        # fast mode (mixer_fp16) at large batches: the PRE on the fp16x3 image (rtol 1e-5 of exact f32)
+        pre_fn = L.mm_agent_q_pre2_h3 if (self.mixer_fp16 and CB >= 2048) else L.mm_agent_q_pre2
+        check(pre_fn(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pb), CB,
+                     ptr(self.tgt.packed), ctypes.byref(pt), CB, s), "learner fwd pre")
         if self.double:   # the double net (behavior weights) on s'
             pd = QFwdIO()
             pd.obs, pd.obs_se, pd.obs_sa, pd.obs_off = obs_p.value, 1, D, 0

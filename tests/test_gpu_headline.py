@@ -347,3 +347,53 @@ def test_headline_learner_b4096_vs_oracle():
 def RolloutEngine_(E, N):
     from minimarl.engine import RolloutEngine
     return RolloutEngine(E, N, f1=64, g=64, h=64, chunk=10, capacity=16 * E, seed=1234, device=DEV)
+
+
+@pytest.mark.parametrize("dims,flag", [((27, 300, 36, 64, 32, 32), None), ((8, 47, 5, 64, 64, 64), None),
+                                       ((27, 300, 36, 64, 32, 32), 5)])
+def test_pre_h3_matches_exact_pre(dims, flag):
+    """``mm_agent_q_pre2_h3`` (the cfg5 fast-mode learner PRE on the fp16x3 image) vs the exact-f32
+    ``mm_agent_q_pre2`` on the same rows of two nets: gi and the x1 | x2 training saves within the fp16x3
+    forward's rtol 1e-5; with ``flag`` an agent pushed out of the f16 range takes the exact-f32 image
+    (then bit-identical to the exact PRE for that agent)."""
+    from minimarl._lib import QFwdIO, check, lib
+    from minimarl.qnet import AgentQNet, ptr, stream_handle
+    N, D, A, F1, G, H = dims
+    nets_ = [AgentQNet(N, D, A, F1, G, H, DEV, seed=s) for s in (31, 32)]
+    if flag is not None:
+        with torch.no_grad():
+            nets_[0].view("W1")[flag, 0, :] = 3.0e3
+        nets_[0].mark_dirty()
+    E, rows = 5000, 3000
+    g = torch.Generator().manual_seed(8)
+    store = torch.rand(rows, N, D, generator=g).to(DEV)
+    reset_obs = torch.rand(N, D, generator=g).to(DEV)
+    offs = [torch.randint(0, rows, (E,), generator=g) * (N * D) for _ in range(2)]
+    for o in offs:
+        o[torch.rand(E, generator=g) < 0.1] = -1
+    offs = [o.to(DEV) for o in offs]
+    SD = F1 + G + 6 * H
+    out = {}
+    for fn in ("mm_agent_q_pre2", "mm_agent_q_pre2_h3"):
+        gis = [torch.zeros(E, N, 3 * H, device=DEV) for _ in range(2)]
+        save = torch.zeros(E, N, SD, device=DEV)
+        ios = []
+        for k in range(2):
+            io = QFwdIO()
+            io.obs, io.obs_se, io.obs_sa, io.obs_off = store.data_ptr(), 1, D, 0
+            io.obs_row, io.reset_obs = offs[k].data_ptr(), reset_obs.data_ptr()
+            io.h_in = store.data_ptr()      # unused by PRE
+            io.gi = gis[k].data_ptr()
+            ios.append(io)
+        ios[0].save = save.data_ptr()
+        check(getattr(lib(), fn)(ctypes.byref(nets_[0].dims), ptr(_pack_q(nets_[0])), ctypes.byref(ios[0]), E,
+                                 ptr(_pack_q(nets_[1])), ctypes.byref(ios[1]), E, stream_handle(DEV)), fn)
+        torch.cuda.synchronize()
+        out[fn] = (gis[0].cpu().numpy(), gis[1].cpu().numpy(), save[..., :F1 + G].cpu().numpy())
+    ex, h3 = out["mm_agent_q_pre2"], out["mm_agent_q_pre2_h3"]
+    for a, b in zip(h3, ex):
+        scale = max(1.0, float(np.abs(b).max()))
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=2e-5 * scale)
+    if flag is not None:   # net 0's flagged agent: gi and saves from the exact-f32 image
+        for i in (0, 2):
+            np.testing.assert_array_equal(h3[i][:, flag], ex[i][:, flag])
