@@ -702,25 +702,33 @@ __global__ __launch_bounds__(256, 2) void agent_rec_seq_kernel(QFwdParams p0, QF
       for (int s = 0; s < 16; ++s) anh = mfma32(fz[2][kb][s], h0[kb][s], anh);
     float* sv = (io.save && valid) ? io.save + t * sq.save_st + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H)
                                    : nullptr;
-    float h1v[16];
+    float h1v[16], h0v[16], rv[16], zv[16], nv[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      float h0v = h0[0][s];
+      h0v[s] = h0[0][s];
 #pragma unroll
       for (int kb = 1; kb < HB; ++kb)
-        if (kb == hb) h0v = h0[kb][s];
-      const float r = sigmoidf_(ar[s]);
-      const float z = sigmoidf_(az[s]);
-      const float n = tanhf_(anx[s] + r * anh[s]);
-      h1v[s] = n + z * (h0v - n);
-      if (sv) {
-        float* o = sv + F1 + G + hb * 32 + kperm(s, hh);
-        o[0] = h0v;
-        o[H] = r;
-        o[2 * H] = z;
-        o[3 * H] = n;
-        o[4 * H] = anh[s];
-        o[5 * H] = h1v[s];
+        if (kb == hb) h0v[s] = h0[kb][s];
+      rv[s] = sigmoidf_(ar[s]);
+      zv[s] = sigmoidf_(az[s]);
+      nv[s] = tanhf_(anx[s] + rv[s] * anh[s]);
+      h1v[s] = nv[s] + zv[s] * (h0v[s] - nv[s]);
+    }
+    if (sv) {
+      // the save row's 6 fields: lane (e, hh) holds features 8j + 4hh + 0..3 of each, so every field goes
+      // out as 4 16-byte stores (sv + F1 + G and the field strides are multiples of 4 floats; the host
+      // requires a 16-byte aligned save base) instead of 16 scattered 4-byte stores
+      float* o = sv + F1 + G + hb * 32 + 4 * hh;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = 4 * j;
+        float* oj = o + 8 * j;
+        *reinterpret_cast<float4*>(oj) = make_float4(h0v[q], h0v[q + 1], h0v[q + 2], h0v[q + 3]);
+        *reinterpret_cast<float4*>(oj + H) = make_float4(rv[q], rv[q + 1], rv[q + 2], rv[q + 3]);
+        *reinterpret_cast<float4*>(oj + 2 * H) = make_float4(zv[q], zv[q + 1], zv[q + 2], zv[q + 3]);
+        *reinterpret_cast<float4*>(oj + 3 * H) = make_float4(nv[q], nv[q + 1], nv[q + 2], nv[q + 3]);
+        *reinterpret_cast<float4*>(oj + 4 * H) = make_float4(anh[q], anh[q + 1], anh[q + 2], anh[q + 3]);
+        *reinterpret_cast<float4*>(oj + 5 * H) = make_float4(h1v[q], h1v[q + 1], h1v[q + 2], h1v[q + 3]);
       }
     }
     __syncthreads();   // every wave has read hx (its h0) before it is overwritten
@@ -2256,6 +2264,8 @@ int agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_
   }
   MM_REQUIRE(steps >= 1 && (steps == 1 || reset), "agent_q_rec_seq: steps >= 1 and reset flags required");
   MM_REQUIRE(io0->gi && (single || io1->gi), "agent_q_rec_seq: io.gi required");
+  MM_REQUIRE(((uintptr_t)io0->save & 15) == 0 && (single || ((uintptr_t)io1->save & 15) == 0),
+             "agent_q_rec_seq: the training save base must be 16-byte aligned");
   auto mk = [&](const QFwdParams& p) {
     RecSeq q;
     q.C = steps;
