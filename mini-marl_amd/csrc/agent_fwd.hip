@@ -332,6 +332,15 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
 // PRE: layers 1-2 and the GRU input projection for every (row, agent) of a chunk batch; REC: one
 // recurrent step from those projections. Same MFMA accumulation order as the fused body (biases,
 // then W_ih x2, then W_hh h), so PRE + REC reproduce agent_q_fwd_body bit for bit.
+// a 32-wide act-frag vector (lane half hh holds features kperm(s, hh)) stored as 4 runs of 4 floats:
+// features 8j + 4hh + 0..3 are v[4j..4j+3]. dst must be 16-byte aligned (row strides of saves / gi are
+// multiples of 4 floats; the bases are torch allocations).
+__device__ __forceinline__ void store_kperm16(float* dst, int hh, const f32x16& v) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    *reinterpret_cast<float4*>(dst + 8 * j + 4 * hh) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+}
+
 template <int F1, int G, int H, int AB>
 __device__ __forceinline__ void agent_pre_body(const QFwdParams& p, int agent, int e, const float* __restrict__ W,
                                                const float* orow) {
@@ -359,12 +368,11 @@ __device__ __forceinline__ void agent_pre_body(const QFwdParams& p, int agent, i
   }
   float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
 #pragma unroll
-  for (int rb = 0; rb < RB1; ++rb)
+  for (int rb = 0; rb < RB1; ++rb) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      x1[rb][s] = fmaxf(x1[rb][s], 0.0f);
-      if (sv) sv[rb * 32 + kperm(s, hh)] = x1[rb][s];
-    }
+    for (int s = 0; s < 16; ++s) x1[rb][s] = fmaxf(x1[rb][s], 0.0f);
+    if (sv) store_kperm16(sv + rb * 32, hh, x1[rb]);
+  }
   f32x16 x2[RB2];
 #pragma unroll
   for (int rb = 0; rb < RB2; ++rb) {
@@ -376,10 +384,8 @@ __device__ __forceinline__ void agent_pre_body(const QFwdParams& p, int agent, i
       for (int s = 0; s < 16; ++s) x2[rb] = mfma32(fr[s], x1[kb][s], x2[rb]);
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      x2[rb][s] = fmaxf(x2[rb][s], 0.0f);
-      if (sv) sv[F1 + rb * 32 + kperm(s, hh)] = x2[rb][s];
-    }
+    for (int s = 0; s < 16; ++s) x2[rb][s] = fmaxf(x2[rb][s], 0.0f);
+    if (sv) store_kperm16(sv + F1 + rb * 32, hh, x2[rb]);
   }
   float* gi = valid ? io.gi + ((int64_t)e * p.N + agent) * 3 * H : nullptr;
 #pragma unroll
@@ -394,10 +400,7 @@ __device__ __forceinline__ void agent_pre_body(const QFwdParams& p, int agent, i
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = mfma32(fr[s], x2[kb][s], acc);
       }
-      if (gi) {
-#pragma unroll
-        for (int s = 0; s < 16; ++s) gi[gte * H + hb * 32 + kperm(s, hh)] = acc[s];
-      }
+      if (gi) store_kperm16(gi + gte * H + hb * 32, hh, acc);
     }
   }
 }
@@ -458,10 +461,10 @@ __device__ __forceinline__ void agent_pre_rb_body(const QFwdParams& p, int agent
       }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const float v = fmaxf(acc[s], 0.0f);
-      x1s[wv][s][lane] = v;
-      if (sv) sv[wv * 32 + kperm(s, hh)] = v;
+      acc[s] = fmaxf(acc[s], 0.0f);
+      x1s[wv][s][lane] = acc[s];
     }
+    if (sv) store_kperm16(sv + wv * 32, hh, acc);
   }
   __syncthreads();
   // ---- layer 2 (row block wv)
@@ -473,10 +476,10 @@ __device__ __forceinline__ void agent_pre_rb_body(const QFwdParams& p, int agent
       for (int s = 0; s < 16; ++s) acc = mfma32(f2[kb][s], x1s[kb][s][lane], acc);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const float v = fmaxf(acc[s], 0.0f);
-      x2s[wv][s][lane] = v;
-      if (sv) sv[F1 + wv * 32 + kperm(s, hh)] = v;
+      acc[s] = fmaxf(acc[s], 0.0f);
+      x2s[wv][s][lane] = acc[s];
     }
+    if (sv) store_kperm16(sv + F1 + wv * 32, hh, acc);
   }
   __syncthreads();
   // ---- GRU input projection (gate gte, hidden block hb3)
@@ -488,8 +491,7 @@ __device__ __forceinline__ void agent_pre_rb_body(const QFwdParams& p, int agent
       for (int s = 0; s < 16; ++s) acc = mfma32(f3[kb][s], x2s[kb][s][lane], acc);
     if (valid) {
       float* gi = io.gi + ((int64_t)e * p.N + agent) * 3 * H;
-#pragma unroll
-      for (int s = 0; s < 16; ++s) gi[gte * H + hb3 * 32 + kperm(s, hh)] = acc[s];
+      store_kperm16(gi + gte * H + hb3 * 32, hh, acc);
     }
   }
 }
@@ -1468,10 +1470,8 @@ __device__ __forceinline__ void agent_pre_body_h3(const QFwdParams& p, int agent
 #pragma unroll
   for (int t = 0; t < T1; ++t) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      x1[t][r] = fmaxf(x1[t][r], 0.0f);
-      if (sv) sv[16 * t + 4 * g + r] = x1[t][r];
-    }
+    for (int r = 0; r < 4; ++r) x1[t][r] = fmaxf(x1[t][r], 0.0f);
+    if (sv) *reinterpret_cast<f32x4*>(sv + 16 * t + 4 * g) = x1[t];
   }
 #pragma unroll
   for (int kb = 0; kb < RB1; ++kb) split_pair(x1[2 * kb], x1[2 * kb + 1], x1s[kb]);
@@ -1483,10 +1483,8 @@ __device__ __forceinline__ void agent_pre_body_h3(const QFwdParams& p, int agent
 #pragma unroll
     for (int kb = 0; kb < RB1; ++kb) mm16(W + CG::off_l2 + ((t >> 1) * RB1 + kb) * 1024, t & 1, x1s[kb], lane, x2[t]);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      x2[t][r] = fmaxf(x2[t][r], 0.0f);
-      if (sv) sv[F1 + 16 * t + 4 * g + r] = x2[t][r];
-    }
+    for (int r = 0; r < 4; ++r) x2[t][r] = fmaxf(x2[t][r], 0.0f);
+    if (sv) *reinterpret_cast<f32x4*>(sv + F1 + 16 * t + 4 * g) = x2[t];
   }
   KS x2s[RB2];
 #pragma unroll
@@ -1510,13 +1508,10 @@ __device__ __forceinline__ void agent_pre_body_h3(const QFwdParams& p, int agent
       mmf(f2, x2s[kb], an);
     }
     if (gi) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int f = 16 * t + 4 * g + r;
-        gi[f] = ar[r];
-        gi[H + f] = az[r];
-        gi[2 * H + f] = an[r];
-      }
+      float* o = gi + 16 * t + 4 * g;
+      *reinterpret_cast<f32x4*>(o) = ar;
+      *reinterpret_cast<f32x4*>(o + H) = az;
+      *reinterpret_cast<f32x4*>(o + 2 * H) = an;
     }
   }
 }
@@ -2301,6 +2296,8 @@ int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const
   if (rc) return rc;
   if (!io1 || e1 <= 0) {   // single net
     MM_REQUIRE(io0->gi, "agent_q_split: io.gi required");
+    MM_REQUIRE(phase == 2 || (((uintptr_t)io0->gi | (uintptr_t)io0->save) & 15) == 0,
+               "agent_q_pre: gi / save bases must be 16-byte aligned");
     p1 = p0;
     p1.nblocks = 0;
     return dispatch_split(d, phase, p0, p1, s);
@@ -2308,6 +2305,8 @@ int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const
   rc = make_params(d, packed1, io1, e1, &p1);
   if (rc) return rc;
   MM_REQUIRE(io0->gi && io1->gi, "agent_q_split: io.gi required");
+  MM_REQUIRE(phase == 2 || (((uintptr_t)io0->gi | (uintptr_t)io1->gi | (uintptr_t)io0->save | (uintptr_t)io1->save) & 15) == 0,
+             "agent_q_pre: gi / save bases must be 16-byte aligned");
   MM_REQUIRE(phase == 2 || (io0->obs && io1->obs), "agent_q_pre: obs required");   // phase 3: PRE on fp16x3
   return dispatch_split(d, phase, p0, p1, s);
 }

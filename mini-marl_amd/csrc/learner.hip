@@ -336,12 +336,16 @@ __global__ __launch_bounds__(64 * 2 * RBK) void mixer_gi_f16_kernel(MixGiArgs a)
     __syncthreads();
   }
   // D: col = sample li, row = (q & 3) + 8 (q >> 2) + 4 lh
+  // gate rows rw*32 + 8j + 4lh + 0..3 of sample c are acc[4j..4j+3]: 16-byte stores (M3 = 96 / 192 and the
+  // gi base keep every run 16-byte aligned), not 16 scattered dword stores per lane
   const int c = c0 + cw * 32 + li;
   if (c < a.R) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int m = rw * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
-      if (m < M3) nt.gi[(int64_t)c * M3 + m] = nt.P[o.gbih + m] + acc[q];
+    for (int j = 0; j < 4; ++j) {
+      const int m = rw * 32 + 8 * j + 4 * lh;
+      const float* bb = nt.P + o.gbih + m;
+      *reinterpret_cast<float4*>(nt.gi + (int64_t)c * M3 + m) =
+          make_float4(bb[0] + acc[4 * j], bb[1] + acc[4 * j + 1], bb[2] + acc[4 * j + 2], bb[3] + acc[4 * j + 3]);
     }
   }
 }
@@ -2601,6 +2605,7 @@ int mm_mixer_gi_f16(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, con
                     float* gi1, mm_stream_t s) {
   MM_REQUIRE(R > 0 && P0 && gi0 && obs && (s_off0 || !P1), "mixer_gi_f16: bad args");
   MM_REQUIRE(Hm == 32 || Hm == 64, "mixer_gi_f16: Hm must be 32 or 64");
+  MM_REQUIRE((((uintptr_t)gi0 | (uintptr_t)gi1) & 15) == 0, "mixer_gi_f16: gi must be 16-byte aligned");
   mm::MixGiArgs a;
   a.net[0] = {P0, s_off0, gi0};
   a.net[1] = {P1 ? P1 : P0, P1 ? s_off1 : s_off0, P1 ? gi1 : gi0};
