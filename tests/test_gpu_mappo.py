@@ -390,3 +390,41 @@ def test_data_parallel_hooks_match_single_replica():
     assert all(np.isfinite(v) for v in i2.values()), i2
     np.testing.assert_allclose(p2.actor.flat.cpu().numpy(), p1.actor.flat.cpu().numpy(), rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(p2.critic.flat.cpu().numpy(), p1.critic.flat.cpu().numpy(), rtol=1e-4, atol=1e-6)
+
+
+def test_full_train_15_epochs_vs_oracle_at_scale():
+    """R_MAPPO.train as benched (15 PPO epochs, one full-batch minibatch each, ValueNorm updated per epoch,
+    advantages normalised once, clip 0.5 + Adam per net; ramppo_network.py:211-287) at 128 envs x 8 agents x
+    T = 40 (the golden covers E = 4, N = 2, T = 10 only): post-train parameters vs ``om.ppo_train`` on the same
+    rollout. Coordinates whose epoch-0 gradient is significant (> 1e-3 of the tensor's max) within 5e-5;
+    every coordinate within 15 epochs x 2 lr (Adam steps of near-zero gradients follow rounding noise)."""
+    from minimarl.env import VecEnv
+    from minimarl.mappo import MappoPolicy, MappoRunner
+    E, N, T, L, EP = 128, 8, 40, 5, 15
+    env = VecEnv(E, N, max_steps=100, device=DEV)
+    p = MappoPolicy(env.obs_dim, 5, 32, DEV, seed=5)
+    r = MappoRunner(env, p, T=T, L=L, ppo_epoch=EP, seed=13)
+    r.warmup()
+    r.rollout()
+    r.compute()
+    torch.cuda.synchronize()
+    PA = {k: p.actor.view(k).detach().cpu().clone() for k in om.NET_KEYS}
+    PC = {k: p.critic.view(k).detach().cpu().clone() for k in om.NET_KEYS}
+    vn0 = [float(x) for x in r.trainer.vn.cpu().numpy()]
+    data = _ref_layout(r.buf, E, N)
+    r.train()
+    torch.cuda.synchronize()
+    rec = []
+    PA2, PC2, vn2 = om.ppo_train(PA, PC, data, om.ValueNorm(*vn0), EP, L, record=rec)
+    lr = 1e-4
+    for n, (net, ref, tag) in enumerate(((p.actor, PA2, "ga"), (p.critic, PC2, "gc"))):
+        for k in om.NET_KEYS:
+            got = net.view(k).detach().cpu().numpy()
+            want = ref[k].detach().numpy()
+            g = np.abs(rec[0][tag][k].numpy())
+            sel = g > 1e-3 * g.max()
+            np.testing.assert_allclose(got[sel], want[sel], atol=5e-5, err_msg=f"net {n} {k}")
+            np.testing.assert_allclose(got, want, atol=2 * EP * lr, err_msg=f"net {n} {k} (all)")
+    vn = r.trainer.value_normalizer_state()
+    np.testing.assert_allclose(vn["running_mean"], vn2.m.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(vn["running_mean_sq"], vn2.msq.numpy(), rtol=1e-5, atol=1e-6)
