@@ -406,6 +406,10 @@ int mm_outer_reduce(const mm_outer_args* x, mm_stream_t s);
 int64_t mm_outer_reduce_batch_partial(const mm_outer_args* x, int32_t n_jobs);
 int mm_outer_reduce_batch(const mm_outer_args* x, int32_t n_jobs, float* partial, int64_t partial_count,
                           mm_stream_t s);
+/* The same reduction with every product as a bf16x3 split on v_mfma_f32_32x32x16_bf16 (~2^-16 relative per
+ * product, fp32 exponent range): the learner's fast mode (QLearner(mixer_fp16=True) at C*B >= 2048). */
+int mm_outer_reduce_batch_bf3(const mm_outer_args* x, int32_t n_jobs, float* partial, int64_t partial_count,
+                              mm_stream_t s);
 /* Batched (gated) transposed mat-vec Y[g] = (W[g]^T X[g]) * Z[g]. */
 typedef struct mm_tmv_args {
   const float* W; int64_t w_g;

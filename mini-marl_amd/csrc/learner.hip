@@ -2156,6 +2156,7 @@ struct OuterBatch {
   int blk0[OB_MAX + 1];
   int64_t part[OB_MAX];  // partial offset: [slice][group][R*Cc + R]
   int njobs;
+  int bf3;   // fast mode: the MFMA products as bf16x3 splits (outer_tile_bf3)
   float* partial;
 };
 
@@ -2173,7 +2174,29 @@ struct ObSmem {
   float sbias[256];
 };
 
-template <int TS>
+// bf16x3 split (the learner's fast mode): x = hi + lo + O(2^-16 x) with hi = bf16(x), lo = bf16(x - hi), both
+// round-to-nearest-even; hi_a hi_b + hi_a lo_b + lo_a hi_b in fp32 accumulation carries ~2^-16 relative error
+// per product at fp32's exponent range (no f16 underflow of small gradients), on v_mfma_f32_32x32x16_bf16:
+// 3 x 32 cycles per 32 x 32 x 16 block instead of 8 x 64 cycles of the exact-f32 MFMA.
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t bf16_rne_bits(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ void bf3_split(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+  s16x8 h, l;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t hb = bf16_rne_bits(x[i]);
+    h[i] = (short)hb;
+    l[i] = (short)bf16_rne_bits(x[i] - __uint_as_float(hb << 16));
+  }
+  hi = __builtin_bit_cast(bf16x8, h);
+  lo = __builtin_bit_cast(bf16x8, l);
+}
+
+template <int TS, bool BF3 = false>
 __device__ __forceinline__ void outer_tile(const OuterBatch& ob, int j, int t, ObSmem& sm) {
   constexpr int TR = 32 << TS, TC = 128 >> TS, NU = TR / 8, NL = NU + TC / 8;
   constexpr int MU = 256 / TR, MV = 256 / TC;   // rows between a thread's consecutive U / V elements
@@ -2251,9 +2274,28 @@ __device__ __forceinline__ void outer_tile(const OuterBatch& ob, int j, int t, O
     }
     __syncthreads();
     if (m0 + 32 < m_end) load(m0 + 32, buf ^ 1);
+    if constexpr (BF3) {
+      // two 16-deep k-steps over the chunk's 32 rows m: lane (li, lh) holds rows m = 16 ks + 8 lh + 0..7
 #pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2)
-      acc = mfma32(sm.su[2 * s2 + lh][rw * 32 + li], sm.svv[2 * s2 + lh][cw * 32 + li], acc);
+      for (int ks = 0; ks < 2; ++ks) {
+        float av[8], bv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          av[i] = sm.su[16 * ks + 8 * lh + i][rw * 32 + li];
+          bv[i] = sm.svv[16 * ks + 8 * lh + i][cw * 32 + li];
+        }
+        bf16x8 ah, al, bh, bl;
+        bf3_split(av, ah, al);
+        bf3_split(bv, bh, bl);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2)
+        acc = mfma32(sm.su[2 * s2 + lh][rw * 32 + li], sm.svv[2 * s2 + lh][cw * 32 + li], acc);
+    }
     __syncthreads();
     buf ^= 1;
   }
@@ -2281,6 +2323,14 @@ __global__ __launch_bounds__(256) void outer_batch_kernel(OuterBatch ob) {
   int j = 0;
   while (j + 1 < ob.njobs && (int)blockIdx.x >= ob.blk0[j + 1]) ++j;
   const int t = blockIdx.x - ob.blk0[j];
+  if (ob.bf3) {
+    switch (ob.tr_shift[j]) {
+      case 0: outer_tile<0, true>(ob, j, t, sm); break;
+      case 1: outer_tile<1, true>(ob, j, t, sm); break;
+      default: outer_tile<2, true>(ob, j, t, sm); break;
+    }
+    return;
+  }
   switch (ob.tr_shift[j]) {
     case 0: outer_tile<0>(ob, j, t, sm); break;
     case 1: outer_tile<1>(ob, j, t, sm); break;
@@ -2936,8 +2986,18 @@ int64_t mm_outer_reduce_batch_partial(const mm_outer_args* x, int32_t n_jobs) {
   return outer_batch_layout(x, n_jobs, &ob);
 }
 
+static int outer_reduce_batch_impl(const mm_outer_args* x, int32_t n_jobs, float* partial, int64_t partial_count,
+                                   int bf3, mm_stream_t s);
 int mm_outer_reduce_batch(const mm_outer_args* x, int32_t n_jobs, float* partial, int64_t partial_count,
                           mm_stream_t s) {
+  return outer_reduce_batch_impl(x, n_jobs, partial, partial_count, 0, s);
+}
+int mm_outer_reduce_batch_bf3(const mm_outer_args* x, int32_t n_jobs, float* partial, int64_t partial_count,
+                              mm_stream_t s) {
+  return outer_reduce_batch_impl(x, n_jobs, partial, partial_count, 1, s);
+}
+static int outer_reduce_batch_impl(const mm_outer_args* x, int32_t n_jobs, float* partial, int64_t partial_count,
+                                   int bf3, mm_stream_t s) {
   MM_REQUIRE(x && partial && n_jobs >= 1 && n_jobs <= mm::OB_MAX, "outer_reduce_batch: bad args");
   mm::OuterBatch ob;
   int64_t maxper = 0;
@@ -2949,6 +3009,7 @@ int mm_outer_reduce_batch(const mm_outer_args* x, int32_t n_jobs, float* partial
   MM_REQUIRE(need <= partial_count, "outer_reduce_batch: partial buffer too small (%lld < %lld)",
              (long long)partial_count, (long long)need);
   ob.partial = partial;
+  ob.bf3 = bf3;
   hipLaunchKernelGGL(mm::outer_batch_kernel, dim3(ob.blk0[n_jobs]), dim3(256), 0, (hipStream_t)s, ob);
   MM_HIP_CHECK(hipGetLastError());
   const int gx = (int)std::min<int64_t>((maxper + 255) / 256, 1024);

@@ -228,6 +228,7 @@ _SIGS += [
                                 ctypes.POINTER(QFwdIO), c_i64, c_vp]),
     ("mm_outer_reduce_batch_partial", c_i64, [ctypes.POINTER(OuterArgs), c_i32]),
     ("mm_outer_reduce_batch", c_i32, [ctypes.POINTER(OuterArgs), c_i32, c_vp, c_i64, c_vp]),
+    ("mm_outer_reduce_batch_bf3", c_i32, [ctypes.POINTER(OuterArgs), c_i32, c_vp, c_i64, c_vp]),
     ("mm_tmv", c_i32, [ctypes.POINTER(TmvArgs), c_vp]),
     ("mm_clip_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
                              c_vp, c_f32, c_vp]),

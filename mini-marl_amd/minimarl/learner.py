@@ -114,7 +114,8 @@ class QLearner:
         self.reference_compat = bool(reference_compat)
         # cfg5 mode: the mixer state projection [B*C, N*D] x [N*D, 3Hm] on fp16 MFMA (rtol 2e-3
         # on Q_tot, a tolerance stated apart from the fp32 parity); at B*C >= 2048 also the agents'
-        # non-recurrent layers on the fp16x3-split image (mm_agent_q_pre2_h3, rtol 1e-5 of exact f32)
+        # non-recurrent layers on the fp16x3-split image (mm_agent_q_pre2_h3, rtol 1e-5 of exact f32) and the
+        # batched weight-gradient products as bf16x3 splits (mm_outer_reduce_batch_bf3, ~2^-16 relative)
         self.mixer_fp16 = bool(mixer_fp16)
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM
@@ -424,7 +425,9 @@ class QLearner:
         if self.has_mixer:
             self._mixer_wgrad(L, s, obs_p, reset_p, CB, jobs)
         arr = (OuterArgs * len(jobs))(*jobs)
-        check(L.mm_outer_reduce_batch(arr, len(jobs), ptr(self._opart), self._opart.numel(), s), "outer batch")
+        # fast mode at large batches: the weight-gradient products as bf16x3 splits (~2^-16 relative)
+        ob_fn = L.mm_outer_reduce_batch_bf3 if (self.mixer_fp16 and self.C * self.B >= 2048) else L.mm_outer_reduce_batch
+        check(ob_fn(arr, len(jobs), ptr(self._opart), self._opart.numel(), s), "outer batch")
 
     def _forward_seq(self, L, s, obs_p, reset_p):
         """REC of both nets over all C steps in one chunk-sequence launch, then the mixers per step."""
