@@ -1452,8 +1452,27 @@ __device__ __forceinline__ void agent_pre_body_h3(const QFwdParams& p, int agent
   const int g = lane >> 4;
   const bool valid = e < p.E;
   const mm_qfwd_io& io = p.io;
+  // obs k-steps as 16-byte loads where the row is 16-byte aligned (the cfg5 store rows of D = 300 are): lane
+  // (c, g) reads features 32 kb + 16 q + 4 g + 0..3 for q = 0, 1 — 2 loads instead of 8 guarded dword loads
+  const bool o16 = orow && (reinterpret_cast<uintptr_t>(orow) & 15) == 0;
+  auto ld_obs = [&](int kb, float (&x)[8]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int k0 = kb * 32 + 16 * q + 4 * g;
+      if (o16 && k0 + 3 < p.D) {
+        const float4 v = *reinterpret_cast<const float4*>(orow + k0);
+        x[4 * q] = v.x;
+        x[4 * q + 1] = v.y;
+        x[4 * q + 2] = v.z;
+        x[4 * q + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[4 * q + r] = (orow && k0 + r < p.D) ? orow[k0 + r] : 0.0f;
+      }
+    }
+  };
   float xn[8];
-  load_obs_ks(orow, 0, p.D, xn);
+  ld_obs(0, xn);
   // ---- layer 1 (next obs k-step prefetched)
   f32x4 x1[T1];
 #pragma unroll
@@ -1461,7 +1480,7 @@ __device__ __forceinline__ void agent_pre_body_h3(const QFwdParams& p, int agent
   for (int kb = 0; kb < p.g.KD; ++kb) {
     KS ob;
     split8(xn, ob);
-    if (kb + 1 < p.g.KD) load_obs_ks(orow, kb + 1, p.D, xn);
+    if (kb + 1 < p.g.KD) ld_obs(kb + 1, xn);
 #pragma unroll
     for (int t = 0; t < T1; ++t) mm16(W + CG::off_l1 + (int64_t)((t >> 1) * p.g.KD + kb) * 1024, t & 1, ob, lane, x1[t]);
   }
