@@ -298,6 +298,12 @@ def main():
     # warm-up, then R timed regions of exactly K lockstep steps each (chunk graphs + single-step graphs),
     # each bracketed by barrier + synchronize and maxed over ranks; the median region is the result
     eng.run_steps(args.warmup, args.epsilon)
+    # each timed region of K steps replays ONE captured K-step graph (captured here, untimed, for every graph
+    # phase a region starts at): consecutive graph launches leave the GPU idle ~9 us each (region
+    # fixed cost), which a run of chunk + single-step graph replays per region would pay ~10 times
+    G = eng.graph_steps()
+    for i in range(min(G, max(1, args.repeats))):
+        eng.capture_region(args.steps, start=eng.t + i * args.steps)
     reps = []
     for _ in range(max(1, args.repeats)):
         torch.cuda.synchronize()
@@ -661,6 +667,10 @@ def main():
         torch.cuda.synchronize()
         el5 = (time.perf_counter() - t6) / k5
         cfg5["learner"] = {"batch_chunks": B5, "chunk": C5, "mixer_state_projection": "fp16 MFMA (rtol 2e-3 on Q_tot)",
+                           "agent_path": "exact f32 (agent PRE as fp16x3-split MFMA, rtol 1e-5 of f32; agent weight "
+                                         "gradients exact f32 MFMA)",
+                           "mixer_weight_gradients": "bf16x3-split MFMA products (~2^-16 relative per product)"
+                           if l5.mixer_bf3 else "exact f32 MFMA",
                            "parity_test": "tests/test_gpu_learner.py::test_learner_cfg5_benched_path_vs_oracle (same "
                                           "graphs at B = 512: Q_tot / loss / TD, every gradient, post-Adam params)",
                            "ms_per_update": round(el5 * 1e3, 3), "chunk_samples_per_s": round(B5 / el5, 1),

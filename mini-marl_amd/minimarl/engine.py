@@ -104,6 +104,7 @@ class RolloutEngine:
         self._td_pending = False     # last step's TD/store not yet written (fused into the next env step)
         self._td_flushed = False
         self.graph = None
+        self._region_graphs = {}
         self.t = 0
         self.seed = int(seed)
         self.chunks_inserted = 0
@@ -440,6 +441,8 @@ class RolloutEngine:
             self.set_epsilon(epsilon)
         assert not self._td_flushed, "run_steps after flush_td(): continue with step() to the chunk end"
         G = self.graph_steps()
+        if (self.t % G, int(n_steps)) in self._region_graphs:
+            return self.run_region(n_steps)
         left = int(n_steps)
         while left > 0:
             if self.t % G == 0 and left >= G:
@@ -460,6 +463,53 @@ class RolloutEngine:
             else:
                 self._td_pending = True
             left -= 1
+
+    def capture_region(self, n_steps, start=None):
+        """Capture ONE HIP graph of exactly ``n_steps`` lockstep steps starting at step ``start`` (default: the
+        current step; only its graph phase ``start % graph_steps()`` matters), so a timed region of n steps is
+        one graph launch instead of a run of chunk / single-step graph replays: on MI355X each graph launch
+        after the first leaves the GPU idle for ~9 us (rocprofv3 kernel trace of tools/region_probe.py), i.e.
+        ~90 us per 20-step region entered mid-chunk. Same launches as ``capture`` in the same order; graphs are
+        cached per (phase, n_steps) and ``run_steps`` replays them."""
+        G = self.graph_steps()
+        start = self.t if start is None else int(start)
+        key = (start % G, int(n_steps))
+        if key in self._region_graphs:
+            return self._region_graphs[key]
+        assert not self._td_flushed, "capture_region after flush_td(): continue with step() to the chunk end"
+        self.behavior.pack()
+        self.target.pack()
+        if not self._primed:
+            self._prologue(stream_handle(self.device))
+        torch.cuda.synchronize(self.device)
+        saved = (self.t, self.chunks_inserted, self._td_pending, self._td_flushed)
+        n0 = len(self.per)
+        self.t = start
+        g = torch.cuda.CUDAGraph()
+        with graph_capture(g):
+            for _ in range(int(n_steps)):
+                self._step_launch()
+        inserts = self.chunks_inserted - saved[1]
+        self.t, self.chunks_inserted, self._td_pending, self._td_flushed = saved
+        lib().mm_per_set_size(self.per._h, n0)
+        self._region_graphs[key] = (g, inserts)
+        return self._region_graphs[key]
+
+    def run_region(self, n_steps, epsilon=None):
+        """Replay the captured ``n_steps`` region graph of the current phase (``capture_region``)."""
+        if epsilon is not None:
+            self.set_epsilon(epsilon)
+        G = self.graph_steps()
+        g, inserts = self._region_graphs.get((self.t % G, int(n_steps))) or self.capture_region(n_steps)
+        self.behavior.pack()
+        self.target.pack()
+        g.replay()
+        self.t += int(n_steps)
+        self.chunks_inserted += inserts
+        self.per.n_mirror_add(inserts)
+        self._td_pending = self.t % self.C != 0
+
+    _region_graphs = None
 
     def run(self, n_steps, epsilon):
         for _ in range(n_steps):

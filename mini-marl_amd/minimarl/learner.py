@@ -422,12 +422,26 @@ class QLearner:
         # outer product of the update (agent + mixer) in ONE split-M launch (+ its partial sum)
         jobs = []
         self._agent_wgrad(L, s, obs_p, reset_p, CB, jobs)
+        mjobs = []
         if self.has_mixer:
-            self._mixer_wgrad(L, s, obs_p, reset_p, CB, jobs)
+            self._mixer_wgrad(L, s, obs_p, reset_p, CB, mjobs)
+        if self.mixer_bf3:
+            # fast mode at large batches: the agent weight gradients stay exact f32 (the fp32 parity bar); only
+            # the MIXER's products run as bf16x3 splits (~2^-16 relative), a second launch over the same partials
+            arr = (OuterArgs * len(jobs))(*jobs)
+            check(L.mm_outer_reduce_batch(arr, len(jobs), ptr(self._opart), self._opart.numel(), s), "outer batch")
+            marr = (OuterArgs * len(mjobs))(*mjobs)
+            check(L.mm_outer_reduce_batch_bf3(marr, len(mjobs), ptr(self._opart), self._opart.numel(), s),
+                  "outer batch (mixer, bf16x3)")
+            return
+        jobs += mjobs
         arr = (OuterArgs * len(jobs))(*jobs)
-        # fast mode at large batches: the weight-gradient products as bf16x3 splits (~2^-16 relative)
-        ob_fn = L.mm_outer_reduce_batch_bf3 if (self.mixer_fp16 and self.C * self.B >= 2048) else L.mm_outer_reduce_batch
-        check(ob_fn(arr, len(jobs), ptr(self._opart), self._opart.numel(), s), "outer batch")
+        check(L.mm_outer_reduce_batch(arr, len(jobs), ptr(self._opart), self._opart.numel(), s), "outer batch")
+
+    @property
+    def mixer_bf3(self):
+        """cfg5 fast mode at large batches: the mixer's weight-gradient products as bf16x3 splits."""
+        return self.mixer_fp16 and self.has_mixer and self.C * self.B >= 2048
 
     def _forward_seq(self, L, s, obs_p, reset_p):
         """REC of both nets over all C steps in one chunk-sequence launch, then the mixers per step."""
