@@ -4,8 +4,8 @@ Workload (BASELINE.json configs[1]): QMIX 8-agent gridworld, 4096 envs per GPU, 
 Q-net GRU-64 (F1 = G = H = 64), chunk 10, device PER. One "step" = one lockstep
 rollout step of every env on every rank: behavior Q forward + eps-greedy, env step,
 target Q forward on the next obs, TD error + transition store, and every 10th step
-the chunk insert into the prioritized replay. Synthetic data = the build's own
-gridworld (the reference's ma_gym env is absent); random-init weights.
+the chunk insert into the prioritized replay. Env = ma_gym Checkers-v0 restated (oracle/env.py; ma-gym
+itself is absent), 8 agents as 4 stacked 3x8 boards; random-init weights.
 
 The JSON line also carries the QMIX learner (updates/s, configs[1]) and the MAPPO episode
 (configs[2]: rollout + GAE + 15 PPO epochs; agent-env-steps/s including training).
@@ -201,6 +201,22 @@ def spawn_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
+def replica_checksums(dist, tensors):
+    """{name: [exact int64 checksum of the tensor's bytes on every rank]} (data-parallel replicas must stay
+    bit-identical after every update); an all-gather over the process group."""
+    out = {}
+    for name, t in tensors.items():
+        ck = t.detach().contiguous().view(torch.int32).to(torch.int64).sum().reshape(1)
+        if dist is None:
+            out[name] = [int(ck.item())]
+            continue
+        ck = ck.to(t.device) if dist.get_backend() == "nccl" else ck.cpu()
+        parts = [torch.zeros_like(ck) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, ck)
+        out[name] = [int(x.item()) for x in parts]
+    return out
+
+
 def probe_ranks(world, rank):
     """``--probe-ranks``: rendezvous over gloo (no GPU), gather every rank id, rank 0 prints one JSON line."""
     import torch.distributed as dist
@@ -240,9 +256,6 @@ def main():
                     help="timed regions of exactly --steps steps each; ms_per_step is their median (min / max beside)")
     ap.add_argument("--cfg1-episodes", type=int, default=20,
                     help="timed training episodes of the cfg1 VDN trainer lines (0 = skip; single-GPU runs only)")
-    ap.add_argument("--fused-step", action="store_true",
-                    help="one-launch fused step (env + dual forward + TD; slower at 4096 x 8, DESIGN.md) instead of the "
-                         "two-launch default")
     ap.add_argument("--probe-ranks", action="store_true", help="launcher check: gloo rendezvous only, no GPU")
     args = ap.parse_args()
 
@@ -276,8 +289,7 @@ def main():
     E, N, Hh = args.envs, args.agents, args.hidden
     F1, G = 64, Hh
     cap = 16 * E
-    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=cap, seed=1234 + rank, fused=args.fused_step,
-                        device=dev)
+    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=cap, seed=1234 + rank, device=dev)
     D = eng.D
     from minimarl.learner import Mixer, QLearner
     mix = Mixer(N, N * D, 64, 32, dev, seed=7)
@@ -301,8 +313,8 @@ def main():
     # each timed region of K steps replays ONE captured K-step graph (captured here, untimed, for every graph
     # phase a region starts at): consecutive graph launches leave the GPU idle ~9 us each (region
     # fixed cost), which a run of chunk + single-step graph replays per region would pay ~10 times
-    G = eng.graph_steps()
-    for i in range(min(G, max(1, args.repeats))):
+    n_phase = eng.graph_steps()
+    for i in range(min(n_phase, max(1, args.repeats))):
         eng.capture_region(args.steps, start=eng.t + i * args.steps)
     reps = []
     for _ in range(max(1, args.repeats)):
@@ -354,6 +366,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el_l = float(t.item())
     upd_per_s = args.learner_steps / el_l
+    replicas = replica_checksums(dist, {"qmix_learner_params": learner.P}) if dist else None
 
     # the same QMIX update at SURVEY 8(d)'s throughput batch (B = 4096 chunks of C = 10), single GPU
     big = None
@@ -408,6 +421,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el_t = float(t.item())
         k = args.train_episodes
+        if dist:
+            replicas.update(replica_checksums(dist, {"train_loop_learner_params": tr.learner.P}))
         trainer = {"algo": "QMIX train loop (rollout + 10 Train_dqn updates per episode + target sync)",
                    "envs_per_gpu": E, "agents": N, "episode_steps": tcfg.max_step, "updates_per_episode":
                    tcfg.update_iter, "batch_chunks": tcfg.batch_size, "episodes": k,
@@ -504,6 +519,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el_m = float(t.item())
         k = args.mappo_episodes
+        if dist:
+            replicas.update(replica_checksums(dist, {"mappo_actor": mpol.actor.flat, "mappo_critic": mpol.critic.flat}))
         Dm, Hm_ = menv.obs_dim, 32
         macs = sum(Hm_ * Dm + Hm_ * Hm_ + 6 * Hm_ * Hm_ + o * Hm_ for o in (5, 1))
         mflop = 6.0 * macs * E * N * 100
@@ -667,8 +684,7 @@ def main():
         torch.cuda.synchronize()
         el5 = (time.perf_counter() - t6) / k5
         cfg5["learner"] = {"batch_chunks": B5, "chunk": C5, "mixer_state_projection": "fp16 MFMA (rtol 2e-3 on Q_tot)",
-                           "agent_path": "exact f32 (agent PRE as fp16x3-split MFMA, rtol 1e-5 of f32; agent weight "
-                                         "gradients exact f32 MFMA)",
+                           "agent_path": "exact f32 MFMA (forward, BPTT and weight gradients)",
                            "mixer_weight_gradients": "bf16x3-split MFMA products (~2^-16 relative per product)"
                            if l5.mixer_bf3 else "exact f32 MFMA",
                            "parity_test": "tests/test_gpu_learner.py::test_learner_cfg5_benched_path_vs_oracle (same "
@@ -683,31 +699,18 @@ def main():
     # kernel: every fp32 product as 3 f16 MFMAs, so its MFMA ceiling for the network's fp32 FLOPs
     # is the dense f16 peak / 3; the native f32-MFMA peak is reported beside it.
     t_iso = time_kernel(eng.fused_forward)
-    if eng.fused:
-        t_fwd = t_iso
-    else:
-        # in its rollout context: graphs of K x (env + dual forward) and K x env, the difference per step (the
-        # forward then reads the obs the env launch just wrote, as in the timed rollout; back-to-back forwards
-        # alone re-read cold obs and take longer, reported as kernel_us_isolated)
-        t_fwd = time_kernel(lambda: (eng.env_only(), eng.fused_forward())) - time_kernel(eng.env_only)
+    # in its rollout context: graphs of K x (env + dual forward) and K x env, the difference per step (the
+    # forward then reads the obs the env launch just wrote, as in the timed rollout; back-to-back forwards
+    # alone re-read cold obs and take longer, reported as kernel_us_isolated)
+    t_fwd = time_kernel(lambda: (eng.env_only(), eng.fused_forward())) - time_kernel(eng.env_only)
     flops = 2 * qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
     achieved = flops / t_fwd / 1e12
     h3 = E >= 2048 and not os.environ.get("MM_FWD_F32")
     peak = PEAK_F16_TFLOPS / 3 if h3 else PEAK_FP32_TFLOPS
-    if eng.fused:
-        # fused step (rollout_step_h3_kernel: env + both forwards + TD(t-1)). Algorithmic bytes per launch,
-        # per agent-step: hidden in/out of both nets 2 x 8H, the target's s'_t into the chunk store 4D,
-        # act read 4, act / Q(a) / max Q' out 12; per env: state read + write 2 x (4N + RC + 8), rew 4N,
-        # done 1, cur_row 8, and TD(t-1): ring reads 16N + 1, chunk_td 8, store act / rew / done 5N + 1
-        RC = eng.env.rows * eng.env.cols
-        alg_bytes = E * N * (16 * Hh + 4 * D + 16) + E * (2 * (4 * N + RC + 8) + 4 * N + 9 + 21 * N + 10)
-        kname = "rollout_step_h3_kernel"
-        pmc_glob = "r*_pmc_rollout_step.json"
-    else:
-        # algorithmic HBM bytes per launch: per agent-step obs 4D + hidden in/out 8H + outputs (act/q 8 or max 4)
-        alg_bytes = E * N * ((4 * D + 8 * Hh + 8) + (4 * D + 8 * Hh + 4))
-        kname = "agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"
-        pmc_glob = "r*_pmc_agent_fwd.json"
+    # algorithmic HBM bytes per launch: per agent-step obs 4D + hidden in/out 8H + outputs (act/q 8 or max 4)
+    alg_bytes = E * N * ((4 * D + 8 * Hh + 8) + (4 * D + 8 * Hh + 4))
+    kname = "agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"
+    pmc_glob = "r*_pmc_agent_fwd.json"
     traffic = None
     prof = sorted(glob.glob(os.path.join(ROOT, "profiles", pmc_glob)))
     if prof and E == 4096 and N == 8 and Hh == 64:
@@ -717,8 +720,7 @@ def main():
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_source": os.path.basename(prof[-1]) if traffic else None,
-                "kernel": f"{kname}<64,64,64,1> (" + ("fused step: env + target fwd + behavior fwd + TD(t-1)"
-                                                      if eng.fused else "dual: target+behavior") + ")",
+                "kernel": f"{kname}<64,64,64,1> (dual: target+behavior)",
                 "kernel_us": round(t_fwd * 1e6, 2), "kernel_us_isolated": round(t_iso * 1e6, 2),
                 "arith": "fp32 network FLOPs as fp16x3-split MFMA (v_mfma_f32_16x16x32_f16 x3, fp32 accumulate)"
                          if h3 else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
@@ -740,14 +742,15 @@ def main():
             "ms_per_step_max": round(max(reps) / steps * 1e3, 4),
             "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 (agent forward: fp16x3-split MFMA emulating f32 products, f32 accumulate)",
-            "data": "synthetic (build's gridworld, random init)",
+            "data": "synthetic (restated ma_gym Checkers, 4 bands for 8 agents; random init)",
             "config": {"workload": "QMIX 8-agent gridworld rollout, 4096 envs/GPU, GRU-64 agents, chunk 10, PER",
                        "envs_per_gpu": E, "agents": N, "obs_dim": D, "f1": F1, "gru": Hh, "chunk": 10,
                        "per_capacity_chunks": cap, "per_prefilled_chunks": fill_chunks * E,
-                       "step_launches": "1 fused (env + dual forward + TD) + PER insert every chunk" if eng.fused
-                       else "env + dual forward + PER insert every chunk",
+                       "step_launches": "env + dual forward + PER insert every chunk; one captured graph per "
+                                        "timed region",
                        "parallelism": f"env-shard x{world}"},
             "rccl_world_size": world,
+            "replica_checksums": replicas,
             "learner_updates_per_s": round(upd_per_s, 1),
             "learner": {"algo": "QMIX Train_dqn update", "batch_chunks": args.batch, "chunk": 10,
                         "mixer_hidden": 64, "ms_per_update": round(el_l / args.learner_steps * 1e3, 4),

@@ -10,6 +10,7 @@
  *
  * Which reference interface each entry point replaces (reference @ /root/reference):
  *   mm_env_*             gym.make("ma_gym:Checkers-v0") reset/step   vdn/main.py:61-64,83,93,143; qmix/main.py:66-71,189
+ *                        (ma_gym checkers.py restated in oracle/env.py)
  *   mm_switch_*          gym.make("ma_gym:Switch2-v0") reset/step    qmix/_config.py:14-19; qmix/main.py:66-71,103-115
  *   mm_agent_q_fwd       Q_Net.forward / sample_action               qmix/_network.py:44-74; vdn/_network.py:52-58,71-88
  *   mm_qnet_*            Q_Net parameters (per-agent Linear/GRUCell)  qmix/_network.py:15-42; vdn/_network.py:32-42,61-69
@@ -135,11 +136,12 @@ int mm_env_reset(mm_env* env, float* obs, mm_stream_t s);
  * the next CURRENT obs (reset obs where done) into obs_cur; otherwise done envs stay terminal. */
 int mm_env_step(mm_env* env, const int32_t* act, float* next_obs, float* obs_cur, float* rew,
                 uint8_t* done, mm_stream_t s);
-/* Copy out the integer state (for parity tests): pos [E,N,2] int32, grid [E,R,C] int8, steps [E],
- * apples [E]; host pointers, synchronous. */
-int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples);
+/* Copy out the integer state (for parity tests): pos / prev [E,N,2] int32 (ma_gym's agent_pos /
+ * agent_prev_pos), grid [E,R,C] int8 (_full_obs: 0 empty, 1 lemon, 2 apple, 3 + k agent k's marker),
+ * steps [E], apples [E]; host pointers, synchronous. */
+int mm_env_get_state(mm_env* env, int32_t* pos, int32_t* prev, int8_t* grid, int32_t* steps, int32_t* apples);
 /* Restore the integer state written by mm_env_get_state (checkpoint resume; host pointers, synchronous). */
-int mm_env_set_state(mm_env* env, const int32_t* pos, const int8_t* grid, const int32_t* steps,
+int mm_env_set_state(mm_env* env, const int32_t* pos, const int32_t* prev, const int8_t* grid, const int32_t* steps,
                      const int32_t* apples);
 int mm_env_grid_shape(const mm_env* env, int32_t* rows, int32_t* cols);
 
@@ -221,47 +223,6 @@ int mm_env_step_rows_td(mm_env* env, const int32_t* act, float* next_obs, int64_
                         float* chunk_td, int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act,
                         float* store_rew, uint8_t* store_done, const int64_t* td_rows, uint64_t* counter,
                         mm_stream_t s);
-/* ---- fused rollout step (the headline path, E >= 2048 envs): env step + target forward + behavior forward in
- * ONE launch (agent_fwd.hip rollout_step_h3_kernel). Every (net, agent, 256-env tile) workgroup re-simulates its
- * tile's env transition from the env state in registers / LDS while its weight image streams in, builds its
- * agent's observation straight from the new state (no obs round trip through HBM), and runs the fp16x3 forward:
- * target net on s'_t (-> max_a Q' into maxq[t % 2]), behavior net on s_{t+1} (the reset obs where the env
- * finished; -> epsilon-greedy act_{t+1} into act[(t + 1) % 3], Q(s_{t+1}, a_{t+1}) into qsel[(t + 1) % 3]).
- * One workgroup per env tile (behavior net, agent 0) writes the env state (double-buffered by t % 2 inside
- * the env), rew[t % 2], done[t % 2], cur_row, and the TD / store of step t - 1 (cal_td_error + the chunk
- * lists, when t % chunk_len != 0 and td_on); target workgroups write their agent's s'_t into store slot
- * t % chunk_len + 1 (and s_t into slot 0 at a chunk start). t is the device step counter step[0] (also the
- * exploration RNG counter); the last workgroup to finish advances it (step[1] is its arrival ticket, 0 between
- * launches). io_target / io_behavior give the hidden states, modes (MM_Q_MAX / MM_Q_ACT), seed, eps_ptr and the
- * ring bases (qsel_out = maxq ring for the target, act_out / qsel_out = act / qsel rings for the behavior). */
-typedef struct mm_rollout_io {
-  float* store_obs; uint8_t* store_act; float* store_rew; uint8_t* store_done;
-  int64_t row_stride; int32_t chunk_len; int32_t td_on;
-  const int64_t* staging; int64_t* cur_row; float* chunk_td;
-  int32_t* act;      /* [3][E][N] */
-  float* qsel;       /* [3][E][N] */
-  float* maxq;       /* [2][E][N] */
-  float* rew;        /* [2][E][N] */
-  uint8_t* done;     /* [2][E] */
-  uint64_t* step;    /* [2]: t, arrival ticket */
-  float gamma;
-  int64_t n_rows;    /* chunk-store rows: a staging row outside [0, n_rows) is never written (error word bit 0) */
-  uint32_t* err;     /* [1] error word (may be NULL) */
-} mm_rollout_io;
-int mm_rollout_step_supported(mm_env* env, const mm_qnet_dims* d, int64_t n_envs);
-int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_target, const mm_qfwd_io* io_target,
-                    const float* packed_behavior, const mm_qfwd_io* io_behavior, const mm_rollout_io* rio,
-                    mm_stream_t s);
-/* the env's state buffers: copy buffer `from` into buffer `to` (0 = the live state get/set_state and the
- * unfused steps use; the fused step alternates by t % 2) */
-int mm_env_copy_state(mm_env* env, int32_t from, int32_t to, mm_stream_t s);
-/* mm_per_insert_td with the TD inputs in the fused step's rings: t = *step - 1 selects rew / done / maxq
- * slot t % 2 and qsel / act slot t % 3 (graph-replayable: nothing about t is baked into the launch). */
-int mm_per_insert_td_ring(mm_per* per, int64_t k, int32_t n_agents, float gamma, const float* rew_ring,
-                          const uint8_t* done_ring, const float* qsel_ring, const float* maxq_ring,
-                          const int32_t* act_ring, const uint64_t* step, float* chunk_td, int32_t step_in_chunk,
-                          int32_t chunk_len, uint8_t* store_act, float* store_rew, uint8_t* store_done,
-                          int64_t* rows_inout, int64_t* slots_out, mm_stream_t s);
 /* TD step writing into store rows rows[e]; increments the device RNG step counter (may be NULL). */
 int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                           const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,

@@ -14,7 +14,6 @@
 // with N = 8 each XCD's L2 only ever holds one agent's weights.
 // Arithmetic: exact-f32 MFMA v_mfma_f32_32x32x2_f32 (fp32 in, fp32 accumulate).
 #include "common.h"
-#include "fused_env.h"
 #include "minimarl.h"
 #include "qnet_geo.h"
 
@@ -1589,322 +1588,6 @@ __global__ __launch_bounds__(1024, 1) void agent_pre_lds_kernel(QFwdParams p0, Q
   agent_pre_body<F1, G, H, AB>(p, agent, e, wsm, orow);
 }
 
-// ---------------------------------------------------------------- fused rollout step (env + dual forward)
-// One launch per lockstep step of the headline path (mm_rollout_step, include/minimarl.h): the dual fp16x3
-// forward above with the Checkers env transition folded in front of it. Each workgroup (net, agent, 256-env
-// tile) re-simulates its tile's transition: one thread per env, the agent positions in registers, the grid in
-// LDS as 2-bit cells, agents moving in id order exactly as env.hip / oracle/env.py. The state comes in with
-// coalesced 16-byte loads issued together (no load sits behind another's latency), all of it under the weight
-// image's LDS-DMA; this replaces a separate env launch, its launch boundary and the obs round trip through HBM
-// (6.2 MB written + read twice per step at 4096 x 8). The new state's observation of the workgroup's agent is
-// a 45-bit mask (3x3 cells x 5 channels) plus the two coordinates, kept per env in LDS, from which every lane
-// builds its MFMA B-operand features; a finished env's reset obs comes from the same masks of the initial state.
-// LDS arrays are [item][env] (env fastest): thread-per-env and lane-per-env accesses are conflict-free.
-// the agent's obs of the tile's envs (from LDS) into store slot `slot`, all 1024 threads, env-contiguous runs
-__device__ __forceinline__ void fs_store_obs(const FusedEnv& ev, const mm_rollout_io& rio, int agent, int e0, int slot,
-                                             const uint16_t* s_pos, const uint64_t* s_mask, const int32_t* s_row) {
-  const int D = ev.D;
-  const int nenv = min(FS_ENVS, (int)(ev.E - e0));
-  const int64_t off = (int64_t)slot * ev.N * D + (int64_t)agent * D;
-  for (int i = threadIdx.x; i < nenv * D; i += blockDim.x) {
-    const int le = i / D, f = i - le * D;
-    const int row = s_row[le];
-    if (row >= 0)
-      rio.store_obs[(int64_t)row * rio.row_stride + off + f] =
-          fs_feature(ev, s_pos, s_mask, nullptr, nullptr, le, false, agent, f);
-  }
-}
-
-// range guard of the fused step (qnet_h3_bound_block): the exact-f32 image, 8 waves x 32 envs
-template <int F1, int G, int H, int AB>
-__device__ __forceinline__ void rollout_f32_fallback(const QFwdParams& p, int agent, int e0, const FusedEnv& ev,
-                                                  const uint8_t* done_ring, float* wsm, char* aux, uint64_t t, int pb,
-                                                  int64_t out_off, bool second) {
-  const uint16_t* s_pos = reinterpret_cast<const uint16_t*>(aux + FusedSmem::pos);
-  const uint64_t* s_mask = reinterpret_cast<const uint64_t*>(aux + FusedSmem::mask);
-  const uint64_t* s_imask = reinterpret_cast<const uint64_t*>(aux + FusedSmem::imask);
-  const uint16_t* s_ipos = reinterpret_cast<const uint16_t*>(aux + FusedSmem::ipos);
-  const uint8_t* s_done = reinterpret_cast<const uint8_t*>(aux + FusedSmem::done);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t E = ev.E;
-  const mm_qfwd_io& io = p.io;
-  const int le32 = wave * 32 + (lane & 31);
-  const int e32 = e0 + le32;
-  const int hh = lane >> 5;
-  const int lc = min(le32, FS_ENVS - 1);
-  const bool init = second && s_done[lc];
-  auto ol32 = [&](int kb, float (&x)[16]) {
-#pragma unroll
-    for (int sidx = 0; sidx < 16; ++sidx) {
-      const int f = kb * 32 + kperm(sidx, hh);
-      x[sidx] = (e32 < E && f < ev.D) ? fs_feature(ev, s_pos, s_mask, s_ipos, s_imask, lc, init, agent, f) : 0.f;
-    }
-  };
-  if (wave < 8) {
-    float x32[16];
-    ol32(0, x32);
-    const bool zero_h = e32 >= E || (second ? s_done[lc] != 0 : done_ring[(int64_t)(pb ^ 1) * E + min(e32, (int)E - 1)] != 0);
-    QFwdParams q = p;
-    q.io.act_out = io.act_out ? io.act_out + out_off : nullptr;
-    q.io.qsel_out = io.qsel_out ? io.qsel_out + out_off : nullptr;
-    q.io.counter = t;
-    q.io.counter_ptr = nullptr;
-    agent_q_fwd_body<F1, G, H, AB>(q, agent, e32, wsm, ol32, x32, zero_h);
-  }
-}
-
-template <int F1, int G, int H, int AB>
-__global__ __launch_bounds__(1024, MM_H3_LB) void rollout_step_h3_kernel(QFwdParams p0, QFwdParams p1, FusedEnv ev,
-                                                                         mm_rollout_io rio) {
-  extern __shared__ __attribute__((aligned(16))) float wsm[];
-  const bool second = (int)blockIdx.x >= p0.nblocks;          // behavior net (s_{t+1}); else target (s'_t)
-  const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
-  const QFwdParams& p = kargs[second ? 1 : 0];
-  (void)p1;
-  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
-  const int agent = bid % p.N, tile = bid / p.N;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int N = ev.N, RC = ev.R * ev.C, NPW = (RC + 15) >> 4;
-  const int64_t E = ev.E, EN = E * N;
-  const int e0 = tile * FS_ENVS;
-  char* aux = reinterpret_cast<char*>(wsm) + (size_t)p.g.agent_stride * 4;
-  uint16_t* s_pos = reinterpret_cast<uint16_t*>(aux + FusedSmem::pos);
-  uint32_t* s_grid = reinterpret_cast<uint32_t*>(aux + FusedSmem::grid);
-  uint64_t* s_mask = reinterpret_cast<uint64_t*>(aux + FusedSmem::mask);
-  int32_t* s_row = reinterpret_cast<int32_t*>(aux + FusedSmem::row);
-  uint64_t* s_imask = reinterpret_cast<uint64_t*>(aux + FusedSmem::imask);
-  uint32_t* s_igrid = reinterpret_cast<uint32_t*>(aux + FusedSmem::igrid);
-  uint16_t* s_ipos = reinterpret_cast<uint16_t*>(aux + FusedSmem::ipos);
-  uint8_t* s_done = reinterpret_cast<uint8_t*>(aux + FusedSmem::done);
-  const uint64_t t = *rio.step;                                  // this launch's step (all workgroups read it first)
-  const int c = (int)(t % (uint64_t)rio.chunk_len), pb = (int)(t & 1);
-  const bool designated = second && agent == 0;                 // writes the env-level outputs of the tile
-  const bool td = designated && rio.td_on && c != 0;            // ... and the TD / store of step t - 1
-  const bool flagged = reinterpret_cast<const int*>(p.packed + 2 * p.g.agent_stride * p.N)[agent] != 0;
-
-  // ---- weight image DMA first (fp16x3 image, or the exact-f32 image of a range-guard-flagged agent)
-  {
-    const float* src = p.packed + (flagged ? 0 : (int64_t)p.N * p.g.agent_stride) + (int64_t)agent * p.g.agent_stride;
-    const int nchunk = (int)(p.g.agent_stride >> 8);
-    for (int ch = wave; ch < nchunk; ch += 16)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + ch * 256 + lane * 4),
-                                       (__attribute__((address_space(3))) void*)(wsm + ch * 256), 16, 0, 0);
-  }
-  // ---- the wave's own hidden state (h3 path: 16 envs per wave) and the target net's reset flag (done_{t-1})
-  const mm_qfwd_io& io = p.io;
-  const int e = e0 + wave * 16 + (lane & 15);
-  const int g4 = lane >> 4;
-  const int ec = min(e, (int)E - 1);
-  f32x4 h0[H / 16];
-  if (!flagged) {
-    const float* hp = io.h_in + (int64_t)ec * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)(4 * g4) * io.hin_sf;
-#pragma unroll
-    for (int tt = 0; tt < H / 16; ++tt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) h0[tt][r] = hp[(int64_t)(16 * tt + r) * io.hin_sf];
-  }
-  const bool reset_prev = rio.done[(int64_t)(pb ^ 1) * E + ec] != 0;
-
-  // ---- every global read of the env phase issued at once
-  // (a) the tile's grids: items (env, packed word), 2 per thread, rows read as whole dwords
-  uint32_t gw[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int it = tid + k * 1024, le = it / NPW, pw = it - le * NPW;
-    const int64_t es = min((int64_t)e0 + min(le, FS_ENVS - 1), E - 1);
-    gw[k] = fs_load_word(ev.grid[pb] + es * RC, RC, pw);
-  }
-  uint32_t igw = 0;
-  if (tid < NPW) igw = fs_load_word(ev.init_grid, RC, tid);
-  // (b) thread-per-env state: positions, actions a_t, counters, staging row (and the TD inputs of step t - 1)
-  const int le = tid;
-  const int64_t ee = e0 + le;
-  const bool ok_env = ee < E;
-  const int64_t es = ok_env ? ee : E - 1;
-  int pr[8], pc[8], ak[8];
-  int steps = 0, apples = 0;
-  int64_t row = 0;
-  float td_r[8], td_q[8], td_m[8];
-  int td_a[8];
-  uint8_t dprev = 0;
-  float ctd = 0.f;
-  if (tid < FS_ENVS) {
-    const int32_t* actp = rio.act + (int64_t)(t % 3) * EN + es * N;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int jj = j < N ? j : N - 1;
-      const int pp = ev.pos[pb][es * N + jj];
-      pr[j] = j < N ? (pp >> 8) : -100;
-      pc[j] = j < N ? (pp & 255) : -100;
-      ak[j] = actp[jj];
-    }
-    steps = ev.steps[pb][es];
-    apples = ev.apples[pb][es];
-    row = rio.staging[es];
-    if (td) {
-      const int pp = pb ^ 1;
-      const int64_t r1 = (int64_t)((t + 2) % 3) * EN + es * N;   // slot of step t - 1 in the 3-rings
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int jj = j < N ? j : N - 1;
-        td_r[j] = rio.rew[(int64_t)pp * EN + es * N + jj];
-        td_m[j] = rio.maxq[(int64_t)pp * EN + es * N + jj];
-        td_q[j] = rio.qsel[r1 + jj];
-        td_a[j] = rio.act[r1 + jj];
-      }
-      dprev = rio.done[(int64_t)pp * E + es];
-      ctd = rio.chunk_td[es];
-    }
-  }
-  if (tid >= FS_ENVS && tid < FS_ENVS + 8) {   // initial positions (for the reset obs masks)
-    const int j = tid - FS_ENVS;
-    s_ipos[j] = (uint16_t)(j < N ? ev.init_pos[j] : 0);
-  }
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int it = tid + k * 1024, lw = it / NPW, pw = it - lw * NPW;
-    if (lw < FS_ENVS) s_grid[pw * FS_ENVS + lw] = gw[k];
-  }
-  if (tid < NPW) s_igrid[tid] = igw;
-  if (tid < FS_ENVS) {
-    if (row < 0 || row >= rio.n_rows) {   // a corrupt staging row: nothing of this env is stored
-      if (rio.err && ok_env) atomicOr(rio.err, 1u);
-      row = -1;
-    }
-    s_row[le] = (int32_t)row;
-  }
-  __syncthreads();   // grids, initial grid / positions in LDS
-
-  uint32_t* g = s_grid + min(le, FS_ENVS - 1);   // this thread's env grid, words FS_ENVS apart
-  if (!second && c == 0) {   // chunk start: s_t of this agent into store slot 0 (block-uniform branch)
-    if (tid < FS_ENVS) fs_publish(ev, pr, pc, g, FS_ENVS, agent, s_pos + le, s_mask + le, FS_ENVS);
-    __syncthreads();
-    fs_store_obs(ev, rio, agent, e0, 0, s_pos, s_mask, s_row);
-    __syncthreads();
-  }
-  if (tid == FS_ENVS) {
-    // the initial state's obs masks (a finished env's behavior obs = the reset obs), one thread of wave 4
-    int ipr[8], ipc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int pp = s_ipos[j];
-      ipr[j] = j < N ? (pp >> 8) : -100;
-      ipc[j] = j < N ? (pp & 255) : -100;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int aq = ev.full_obs ? q : agent;
-      if (q < (ev.full_obs ? N : 1)) {
-        int ar = 0, ac = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j == aq) {
-            ar = ipr[j];
-            ac = ipc[j];
-          }
-        s_imask[q] = fs_obs_mask(s_igrid, 1, ipr, ipc, N, ev.R, ev.C, ar, ac);
-      }
-    }
-  }
-  if (tid < FS_ENVS) {
-    float rw[8];
-    const bool dn = fs_dynamics(ev, pr, pc, ak, g, FS_ENVS, steps, apples, rw);
-    fs_publish(ev, pr, pc, g, FS_ENVS, agent, s_pos + le, s_mask + le, FS_ENVS);
-    s_done[le] = dn ? 1 : 0;
-    if (designated && ok_env) {
-      // env-level outputs: next state (auto-reset where done) into buffer pb ^ 1 (the grid below), rewards,
-      // done, cur_row
-      const int nb = pb ^ 1;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < N) {
-          ev.pos[nb][ee * N + j] = dn ? ev.init_pos[j] : ((pr[j] << 8) | pc[j]);
-          rio.rew[(int64_t)pb * EN + ee * N + j] = rw[j];
-        }
-      ev.steps[nb][ee] = dn ? 0 : steps;
-      ev.apples[nb][ee] = dn ? ev.init_apples : apples;
-      rio.done[(int64_t)pb * E + ee] = dn ? 1 : 0;
-      rio.cur_row[ee] = dn ? -1 : row;
-      // the TD / store of step t - 1 (td_chunk_kernel's arithmetic, agent-order sums)
-      if (td && row >= 0) {
-        float sr = 0.f, sq = 0.f, smx = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < N) {
-            sr += td_r[j];
-            sq += td_q[j];
-            smx += td_m[j];
-            rio.store_act[(row * rio.chunk_len + c - 1) * N + j] = (uint8_t)td_a[j];
-            rio.store_rew[(row * rio.chunk_len + c - 1) * N + j] = td_r[j];
-          }
-        const float dd = dprev ? 1.0f : 0.0f;
-        const float tdv = fabsf(sr + (1.0f - dd) * rio.gamma * smx - sq);
-        rio.chunk_td[ee] = (c - 1 == 0 ? 0.0f : ctd) + tdv;
-        rio.store_done[row * rio.chunk_len + c - 1] = dprev;
-      }
-    }
-  }
-  __syncthreads();   // weight image landed (the barrier waits vmcnt(0)), LDS state complete
-  if (!second) fs_store_obs(ev, rio, agent, e0, c + 1, s_pos, s_mask, s_row);   // s'_t into store slot c + 1
-  if (designated) {
-    // the tile's next grids (the initial grid where the env finished) into buffer pb ^ 1: items (env, packed
-    // word), whole dwords where the row allows it
-    int8_t* gdst = ev.grid[pb ^ 1];
-    for (int it = tid; it < FS_ENVS * NPW; it += 1024) {
-      const int lw = it / NPW, pw = it - lw * NPW;
-      const int64_t ew = e0 + lw;
-      if (ew < E) {
-        const uint32_t w = s_done[lw] ? s_igrid[pw] : s_grid[pw * FS_ENVS + lw];
-        int8_t* rowp = gdst + ew * RC;
-        if ((RC & 3) == 0) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (16 * pw + 4 * q < RC)
-              *reinterpret_cast<uint32_t*>(rowp + 16 * pw + 4 * q) = fs_unpack4((w >> (8 * q)) & 0xFFu);
-        } else {
-          for (int i = 0; i < 16 && 16 * pw + i < RC; ++i) rowp[16 * pw + i] = (int8_t)((w >> (2 * i)) & 3u);
-        }
-      }
-    }
-  }
-
-  const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
-  const int64_t out_off = second ? (int64_t)((t + 1) % 3) * EN : (int64_t)pb * EN;
-  if (flagged) {
-    rollout_f32_fallback<F1, G, H, AB>(p, agent, e0, ev, rio.done, wsm, aux, t, pb, out_off, second);
-  } else {
-    const int lf = wave * 16 + (lane & 15);
-    const bool init = second && s_done[lf];
-    auto ol = [&](int kb, float (&x)[8]) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int f = kb * 32 + kperm16(j, g4);
-        x[j] = (e < E && f < ev.D) ? fs_feature(ev, s_pos, s_mask, s_ipos, s_imask, lf, init, agent, f) : 0.f;
-      }
-    };
-    float xn[8];
-    ol(0, xn);
-    const bool zero_h = e >= E || (second ? s_done[lf] != 0 : reset_prev);
-    if (zero_h) {
-#pragma unroll
-      for (int tt = 0; tt < H / 16; ++tt) h0[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (wave >= 8)
-      for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(8);
-    agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm, ol, xn, h0, eps, t, out_off);
-  }
-
-  // ---- the last workgroup to finish advances the step counter (every workgroup has read it by then)
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    if (atomicAdd(reinterpret_cast<unsigned long long*>(&rio.step[1]), 1ull) == (unsigned long long)gridDim.x - 1) {
-      rio.step[0] = t + 1;
-      rio.step[1] = 0;
-    }
-  }
-}
-
 // ---------------------------------------------------------------- packing
 // One thread per packed element: gathers the canonical flat parameters into
 // the per-lane MFMA fragment image (zero padding outside the real shape).
@@ -2328,85 +2011,6 @@ int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const
              "agent_q_pre: gi / save bases must be 16-byte aligned");
   MM_REQUIRE(phase == 2 || (io0->obs && io1->obs), "agent_q_pre: obs required");   // phase 3: PRE on fp16x3
   return dispatch_split(d, phase, p0, p1, s);
-}
-
-// ---- fused rollout step (mm_rollout_step)
-static bool rollout_fits(const QFwdParams& p) {
-  return (size_t)p.g.agent_stride * 4 + FusedSmem::total <= 160 * 1024;
-}
-
-template <int F1, int G, int H, int AB>
-static int launch_rollout(QFwdParams p0, QFwdParams p1, const FusedEnv& ev, const mm_rollout_io& rio, hipStream_t s) {
-  p0.nblocks = (p0.E + FS_ENVS - 1) / FS_ENVS * p0.N;
-  p1.nblocks = (p1.E + FS_ENVS - 1) / FS_ENVS * p1.N;
-  const size_t sm = (size_t)p0.g.agent_stride * 4 + FusedSmem::total;
-  static bool attr = false;
-  if (!attr) {
-    MM_HIP_CHECK(hipFuncSetAttribute((const void*)rollout_step_h3_kernel<F1, G, H, AB>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-    attr = true;
-  }
-  hipLaunchKernelGGL((rollout_step_h3_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(1024), sm, s, p0, p1,
-                     ev, rio);
-  MM_HIP_CHECK(hipGetLastError());
-  return MM_OK;
-}
-
-int rollout_step_supported(mm_env* env, const mm_qnet_dims* d, int64_t n_envs, FusedEnv* ev, QFwdParams* p) {
-  FusedEnv v;
-  int rc = env_fused_view(env, &v);
-  if (rc) return rc;
-  MM_REQUIRE(d && d->n_agents == v.N && d->obs_dim == v.D, "rollout_step: net dims do not match the env");
-  MM_REQUIRE(n_envs == v.E && n_envs >= 2048, "rollout_step: needs the env's E >= 2048 envs (got %lld)",
-             (long long)n_envs);
-  QnetOffsets o;
-  QFwdParams q{};
-  rc = qnet_geometry(d, &q.g, &o);
-  if (rc) return rc;
-  MM_REQUIRE(rollout_fits(q), "rollout_step: weight image + env state exceed the LDS");
-  const bool shape = (d->f1 == 64 && d->g == 32 && d->h == 32) || (d->f1 == 64 && d->g == 64 && d->h == 64) ||
-                     (d->f1 == 128 && d->g == 32 && d->h == 32) || (d->f1 == 64 && d->g == 32 && d->h == 64);
-  MM_REQUIRE(shape, "rollout_step: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
-  if (ev) *ev = v;
-  if (p) *p = q;
-  return MM_OK;
-}
-
-int rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
-                 const float* packed_b, const mm_qfwd_io* io_b, const mm_rollout_io* rio, hipStream_t s) {
-  MM_REQUIRE(rio && io_t && io_b && packed_t && packed_b, "rollout_step: null argument");
-  MM_REQUIRE(rio->store_obs && rio->store_act && rio->store_rew && rio->store_done && rio->staging && rio->cur_row &&
-                 rio->chunk_td && rio->act && rio->qsel && rio->maxq && rio->rew && rio->done && rio->step &&
-                 rio->chunk_len >= 1,
-             "rollout_step: null buffer in the rollout io");
-  MM_REQUIRE(io_t->mode == MM_Q_MAX && io_b->mode == MM_Q_ACT && io_t->qsel_out && io_b->act_out && io_b->qsel_out,
-             "rollout_step: target MM_Q_MAX -> maxq ring, behavior MM_Q_ACT -> act / qsel rings");
-  MM_REQUIRE(io_t->h_in && io_t->h_out && io_b->h_in && io_b->h_out, "rollout_step: hidden states required");
-  FusedEnv ev;
-  int rc = env_fused_view(env, &ev);
-  if (rc) return rc;
-  rc = rollout_step_supported(env, d, ev.E, nullptr, nullptr);
-  if (rc) return rc;
-  MM_REQUIRE(rio->row_stride >= (int64_t)(rio->chunk_len + 1) * ev.N * ev.D, "rollout_step: row_stride too small");
-  MM_REQUIRE(rio->n_rows >= 1 && rio->n_rows < (1ll << 31), "rollout_step: n_rows must be in [1, 2^31)");
-  QFwdParams p0, p1;
-  mm_qfwd_io i0 = *io_t, i1 = *io_b;
-  i0.obs = i1.obs = ev.reset_obs;   // unused (the obs come from the env state); make_params wants a pointer
-  rc = make_params(d, packed_t, &i0, ev.E, &p0);
-  if (rc) return rc;
-  rc = make_params(d, packed_b, &i1, ev.E, &p1);
-  if (rc) return rc;
-  const int AB = (d->n_actions + 31) / 32;
-#define MM_ROLL(F1_, G_, H_)                                                                                 \
-  if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                              \
-    return AB == 1 ? launch_rollout<F1_, G_, H_, 1>(p0, p1, ev, *rio, s) : launch_rollout<F1_, G_, H_, 2>(p0, p1, ev, *rio, s);
-  MM_ROLL(64, 32, 32)
-  MM_ROLL(64, 64, 64)
-  MM_ROLL(128, 32, 32)
-  MM_ROLL(64, 32, 64)
-#undef MM_ROLL
-  set_error("rollout_step: unsupported (F1,G,H)=(%d,%d,%d)", d->f1, d->g, d->h);
-  return MM_EINVAL;
 }
 
 int agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs, hipStream_t s) {

@@ -26,11 +26,6 @@ int agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* 
                  const float* packed1, const mm_qfwd_io* io1, int64_t e1, hipStream_t s);
 int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
                    const float* packed1, const mm_qfwd_io* io1, int64_t e1, hipStream_t s);
-int rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
-                 const float* packed_b, const mm_qfwd_io* io_b, const mm_rollout_io* rio, hipStream_t s);
-struct FusedEnv;
-struct QFwdParams;
-int rollout_step_supported(mm_env* env, const mm_qnet_dims* d, int64_t n_envs, FusedEnv* ev, QFwdParams* p);
 }  // namespace mm
 
 extern "C" {
@@ -63,16 +58,6 @@ int mm_qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, mm_s
 int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,
                    mm_stream_t s) {
   return mm::agent_q_fwd(d, packed, io, n_envs, (hipStream_t)s);
-}
-
-int mm_rollout_step_supported(mm_env* env, const mm_qnet_dims* d, int64_t n_envs) {
-  return mm::rollout_step_supported(env, d, n_envs, nullptr, nullptr);
-}
-
-int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_target, const mm_qfwd_io* io_target,
-                    const float* packed_behavior, const mm_qfwd_io* io_behavior, const mm_rollout_io* rio,
-                    mm_stream_t s) {
-  return mm::rollout_step(env, d, packed_target, io_target, packed_behavior, io_behavior, rio, (hipStream_t)s);
 }
 
 int mm_agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t n_envs0,

@@ -146,23 +146,8 @@ struct TdFuse {
   uint64_t* counter;      // RNG step counter (may be null)
   float gamma;
   int slot, C, on;
-  // ring mode (the fused rollout step's buffers): t = *ring_step - 1 picks rew / done / maxq slot t % 2 and
-  // q_taken / act slot t % 3 (slot strides ring_en = E * N, ring_e = E); null: the plain pointers above
-  const uint64_t* ring_step;
-  int64_t ring_en, ring_e;
 };
 
-// rebase a ring-mode TdFuse onto step t's slots (device side; every thread reads the same *ring_step)
-__device__ __forceinline__ void td_resolve_ring(TdFuse& t) {
-  if (!t.ring_step) return;
-  const uint64_t st = *t.ring_step - 1;
-  const int64_t p2 = (int64_t)(st & 1), p3 = (int64_t)(st % 3);
-  t.rew += p2 * t.ring_en;
-  t.maxq += p2 * t.ring_en;
-  t.done += p2 * t.ring_e;
-  t.q_taken += p3 * t.ring_en;
-  t.act += p3 * t.ring_en;
-}
 
 // Chunk start folded into the env kernels (mm_chunk_begin_rows, rollout.hip): slot 0 of the env's new
 // staging row <- slot src_off of its previous row (cur_row before this step), or the reset obs.

@@ -1,23 +1,24 @@
-// Lockstep "checkers" gridworld: E envs x N agents stepped by one kernel (gfx950).
+// ma_gym Checkers-v0, restated (oracle/env.py): E envs x N agents stepped by one kernel (gfx950).
 //
 // Replaces the per-step gym env call (vdn/main.py:93,143; qmix/main.py:115,189;
-// mappo/runner/shared/magym_runner.py:53-57). ma_gym itself is absent, so the
-// dynamics are the build's own spec, defined in oracle/env.py (parity with
-// ma_gym: UNPINNED; parity with oracle/env.py: bit-exact, integer state).
+// mappo/runner/shared/magym_runner.py:53-57). ma-gym 0.0.14 itself is absent, so the dynamics follow the
+// rule-by-rule restatement of ma_gym's published envs/checkers/checkers.py in oracle/env.py (parity with
+// ma_gym: UNPINNED; parity with oracle/env.py: bit-exact, integer state). The state mirrors ma_gym's:
+// _full_obs as one byte per cell (0 empty, 1 lemon, 2 apple, 3 + k agent k's marker), agent_pos and
+// agent_prev_pos packed in one word per agent (prev_r << 24 | prev_c << 16 | r << 8 | c), _step_count and
+// _food_count['apple'] per env.
 //
-// Block = 256 threads, EB = 4 envs (E/4 blocks: 1024 for 4096 envs, 4 resident per CU). Phase 0 stages
-// every global input of the step (grids as bytes [E][R*C] so the copy is one contiguous coalesced run,
-// positions, actions, counters, reset tables) in LDS in ONE round trip;
-// phase 1 runs the sequential-in-agent-order dynamics one thread per env;
-// phase 2 generates obs [env, agent, feat]: each thread decodes its feature
-// positions once, then walks the block's envs, so consecutive lanes store
-// consecutive floats (coalesced) with O(1) LDS lookups (grid + occupancy
-// map) per element; phase 3 writes state back (or the
-// initial state for envs that auto-reset).
+// One wave per env tile (256-thread blocks, the extra waves stream the obs out): phase 0 stages every global
+// input of the step (grids as bytes [E][R*C], one contiguous coalesced run; positions, actions, counters,
+// coordinate tables) in LDS in ONE round trip; phase 1 runs the sequential-in-agent-order dynamics one lane
+// per env on the LDS grid; phase 2 builds each (env, agent)'s 47 local features into an LDS tile from the
+// grid; phase 3 streams the tile out as 16-byte stores and writes the state back (or the initial state for
+// envs that auto-reset).
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
-#include "fused_env.h"
 #include "minimarl.h"
 
 namespace mm {
@@ -26,19 +27,16 @@ static constexpr int OBS_LOCAL = 47;
 struct EnvDev {
   int E, N, R, C, D, max_steps, full_obs, init_apples;
   int eb;  // envs per block of the step kernel
-  float step_cost, inv_r, inv_c;
-  int32_t* pos;     // [E][N] r*256 + c
-  int8_t* grid;     // [E][R*C] 0 empty, 1 lemon, 2 apple
+  float step_cost;
+  int32_t* pos;     // [E][N] prev_r << 24 | prev_c << 16 | r << 8 | c
+  int8_t* grid;     // [E][R*C] _full_obs codes
   int32_t* steps;   // [E]
   int32_t* apples;  // [E]
-  const int8_t* init_grid;  // [R*C]
-  const int32_t* init_pos;  // [N]
+  const int8_t* init_grid;  // [R*C] (agent markers at their start cells, then the fruit)
+  const int32_t* init_pos;  // [N] (prev = pos)
+  const float* rtab;        // [R] round(r / (R - 1), 2) as f32
+  const float* ctab;        // [C] round(c / (C - 1), 2) as f32
   float* reset_obs;         // [N][D]
-  // the second state copy of the fused rollout step (fused_env.h), same layouts
-  int32_t* pos2;
-  int8_t* grid2;
-  int32_t* steps2;
-  int32_t* apples2;
 };
 }  // namespace mm
 
@@ -49,25 +47,21 @@ struct mm_env {
 
 namespace mm {
 
+__device__ __forceinline__ int pos_r(int32_t w) { return (w >> 8) & 255; }
+__device__ __forceinline__ int pos_c(int32_t w) { return w & 255; }
+
+// feature f in [0, 47) of agent k's local obs (get_agent_obs): coords from the tables, then the 3x3 cells x
+// {lemon, apple, even agent, odd agent, wall} read from the grid; off-grid cells stay all zero
 __device__ __forceinline__ float obs_value(const EnvDev& d, const int32_t* pos, const int8_t* grid, int k, int f) {
-  // f in [0, 47): local obs feature of agent k
-  const int p = pos[k];
-  const int r = p >> 8, c = p & 255;
-  if (f == 0) return (float)r * d.inv_r;
-  if (f == 1) return (float)c * d.inv_c;
+  const int r = pos_r(pos[k]), c = pos_c(pos[k]);
+  if (f == 0) return d.rtab[r];
+  if (f == 1) return d.ctab[c];
   const int cell = (f - 2) / 5, ch = (f - 2) % 5;
   const int rr = r + cell / 3 - 1, cc = c + cell % 3 - 1;
-  const bool inside = rr >= 0 && rr < d.R && cc >= 0 && cc < d.C;
-  if (!inside) return ch == 4 ? 1.0f : 0.0f;
-  if (ch == 4) return 0.0f;
+  if (rr < 0 || rr >= d.R || cc < 0 || cc >= d.C || ch == 4) return 0.0f;
   const int item = grid[rr * d.C + cc];
-  if (ch == 0) return item == 1 ? 1.0f : 0.0f;
-  if (ch == 1) return item == 2 ? 1.0f : 0.0f;
-  if (item != 0) return 0.0f;
-  const int key = (rr << 8) | cc;
-  for (int j = 0; j < d.N; ++j)
-    if (pos[j] == key) return ((j & 1) == (ch - 2)) ? 1.0f : 0.0f;
-  return 0.0f;
+  if (ch < 2) return item == ch + 1 ? 1.0f : 0.0f;
+  return (item >= 3 && ((item - 3) & 1) == ch - 2) ? 1.0f : 0.0f;
 }
 
 // Writes obs of one env (N x D) from the given state into out (+ optional 2nd copy).
@@ -106,35 +100,32 @@ __global__ __launch_bounds__(256) void env_reset_kernel(EnvDev d, float* obs, in
   }
 }
 
-// One wave per block, EPW = 64 / N envs per wave (lane = env-slot * N + agent). Phase 0 issues
-// every global read of the step at once (positions, actions, grid words, counters, destination
-// rows, the fused TD inputs); phase 1 runs the sequential-in-agent-order dynamics, one lane per
-// env with positions in registers; phase 2 builds the occupancy map, then every (env, agent)
-// lane writes its 47 local features into an LDS tile; phase 3 streams the tile out as 16-byte
-// stores (one contiguous N*D run per env, coalesced across the wave) and writes the state back.
+// One wave of (env, agent) lanes per block, EPW = 64 / N envs (lane = env-slot * N + agent). Phase 0 issues
+// every global read of the step at once (positions, actions, grid words, counters, destination rows, the fused
+// TD inputs, the coordinate tables); phase 1 runs ma_gym's sequential-in-agent-order dynamics, one lane per env
+// on the env's LDS grid; phase 2 every (env, agent) lane writes its 47 local features into an LDS tile; phase 3
+// streams the tile out as 16-byte stores (one contiguous N*D run per env, coalesced across the wave) and writes
+// the state back.
 static constexpr int WT = 64;     // lanes of the (env, agent) work: one wave
-#ifndef MM_ENV_TB
-#define MM_ENV_TB 256
-#endif
-static constexpr int TB = MM_ENV_TB;  // threads per block: the extra waves only help stream the obs / state out
+static constexpr int TB = 256;    // threads per block: the extra waves only help stream the obs / state out
 
 // LDS layout of the step kernel (byte offsets, 16-byte aligned pieces), shared by the kernel and the host
 struct EnvSmem {
-  int sloc, srow, sbsrc, std3, spos, sact, sdm, sgrid, socc, total;
+  int sloc, srow, sbsrc, std3, spos, sact, sdm, stab, sgrid, total;
 };
 __host__ __device__ __forceinline__ int al16(int x) { return (x + 15) & ~15; }
-__host__ __device__ __forceinline__ EnvSmem env_smem(int EPW, int N, int RC) {
+__host__ __device__ __forceinline__ EnvSmem env_smem(int EPW, int N, int R, int C) {
   EnvSmem m;
   int o = 0;
   m.sloc = o;  o = al16(o + EPW * N * OBS_LOCAL * 4);   // [EPW][N][47] f32 obs tile
   m.srow = o;  o = al16(o + EPW * 8);                   // [EPW] i64 destination rows
   m.sbsrc = o; o = al16(o + EPW * 8);                   // [EPW] i64 chunk-begin source rows
   m.std3 = o;  o = al16(o + 3 * EPW * N * 4);           // [3][EPW*N] fused TD inputs
-  m.spos = o;  o = al16(o + EPW * N * 4);               // [EPW*N] positions
+  m.spos = o;  o = al16(o + EPW * N * 4);               // [EPW*N] position words
   m.sact = o;  o = al16(o + EPW * N * 4);               // [EPW*N] actions
   m.sdm = o;   o = al16(o + 8);                         // termination mask (wave ballot)
-  m.sgrid = o; o = al16(o + EPW * RC);                  // [EPW][RC] grids
-  m.socc = o;  o = al16(o + EPW * RC);                  // [EPW][RC] occupancy
+  m.stab = o;  o = al16(o + (R + C) * 4);               // [R] row + [C] column coordinate features
+  m.sgrid = o; o = al16(o + EPW * R * C);               // [EPW][RC] grids (_full_obs)
   m.total = o;
   return m;
 }
@@ -153,7 +144,7 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
   const bool autoreset = obs_cur || cur_row;
   const int ND = N * d.D;
   const int LD = N * OBS_LOCAL;                                              // local tile per env
-  const EnvSmem lay = env_smem(EPW, N, RC);
+  const EnvSmem lay = env_smem(EPW, N, d.R, d.C);
   float* sloc = reinterpret_cast<float*>(smem + lay.sloc);
   int64_t* srow = reinterpret_cast<int64_t*>(smem + lay.srow);
   int64_t* sbsrc = reinterpret_cast<int64_t*>(smem + lay.sbsrc);
@@ -161,8 +152,8 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
   int32_t* spos = reinterpret_cast<int32_t*>(smem + lay.spos);
   int32_t* sact = reinterpret_cast<int32_t*>(smem + lay.sact);
   uint64_t* sdm = reinterpret_cast<uint64_t*>(smem + lay.sdm);
+  float* stab = reinterpret_cast<float*>(smem + lay.stab);
   int8_t* sgrid = reinterpret_cast<int8_t*>(smem + lay.sgrid);
-  uint8_t* socc = reinterpret_cast<uint8_t*>(smem + lay.socc);
   const int e0 = blockIdx.x * EPW;
   const int ne = min(EPW, d.E - e0);
   const int nl = ne * N;                   // active (env, agent) lanes
@@ -178,12 +169,12 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
   uint32_t gr[GWR];
 #pragma unroll
   for (int w = 0; w < GWR; ++w) gr[w] = (lane + w * TB < nw) ? g32[lane + w * TB] : 0u;
-  int32_t pos_r = 0, act_r = 0, tact_r = 0;
-  float trew = 0.f, tq = 0.f, tm = 0.f;
+  int32_t pos_w = 0, act_r = 0, tact_r = 0;
+  float trew = 0.f, tq = 0.f, tm = 0.f, tab = 0.f;
   int64_t trow = 0;
   if (lane < nl) {
     const int64_t o = (int64_t)e0 * N + lane;
-    pos_r = d.pos[o];
+    pos_w = d.pos[o];
     act_r = act[o];
     if (tdf.on) {
       trew = tdf.rew[o];
@@ -193,6 +184,7 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
       trow = tdf.rows[e_l];
     }
   }
+  if (lane < d.R + d.C) tab = lane < d.R ? d.rtab[lane] : d.ctab[lane - d.R];
   int apples0 = 0, steps0 = 0;
   int64_t srow_r = 0, bsrc_r = -1;
   uint8_t tdone = 0;
@@ -203,15 +195,16 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
     if (tdf.on) tdone = tdf.done[e0 + lane];
     if (bc.on) bsrc_r = cur_row[e0 + lane];     // read before this step overwrites it
   }
-  for (int i = lane; i < ne * RC; i += TB) socc[i] = 0;
 #pragma unroll
   for (int w = 0; w < GWR; ++w)
     if (lane + w * TB < nw) reinterpret_cast<uint32_t*>(sgrid)[lane + w * TB] = gr[w];
   for (int i = lane + GWR * TB; i < nw; i += TB) reinterpret_cast<uint32_t*>(sgrid)[i] = g32[i];
   if (!g32ok)
     for (int i = lane; i < ne * RC; i += TB) sgrid[i] = d.grid[(int64_t)e0 * RC + i];
+  for (int i = lane + TB; i < d.R + d.C; i += TB) stab[i] = i < d.R ? d.rtab[i] : d.ctab[i - d.R];
+  if (lane < d.R + d.C) stab[lane] = tab;
   if (lane < nl) {
-    spos[lane] = pos_r;
+    spos[lane] = pos_w;
     sact[lane] = act_r;
     if (tdf.on) {
       std3[lane] = trew;
@@ -225,9 +218,6 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
     srow[lane] = srow_r;
     sbsrc[lane] = bsrc_r;
   }
-  __syncthreads();
-  // occupancy map of the starting positions (agent id + 1)
-  if (lane < nl) socc[le_l * RC + (pos_r >> 8) * d.C + (pos_r & 255)] = (uint8_t)(k_l + 1);
   __syncthreads();
 
   // fused TD of the previous step: agent-order sums per env (one lane per env)
@@ -247,40 +237,45 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
     if (tdf.counter && blockIdx.x == 0 && lane == 0) *tdf.counter += 1;
   }
 
-  // ---- phase 1: dynamics, one lane per env, agents in id order (oracle/env.py VecEnvOracle.step).
-  // A move is blocked by the border or by the occupancy map (positions as updated so far this step),
-  // so each agent costs two dependent LDS round trips (occupancy, then the fruit of its cell).
+  // ---- phase 1: ma_gym Checkers.step, one lane per env, agents in id order (oracle/env.py
+  // VecEnvOracle.step): move when the next cell is on the grid and holds no agent marker (agent_prev_pos <-
+  // old position only then); if agent_pos != agent_prev_pos (possibly stale) the fruit at the agent's cell is
+  // eaten (lemon / apple reward, apple count) and the view update writes empty at agent_prev_pos and the
+  // marker at agent_pos. Two dependent LDS round trips per agent (the target cell, then the agent's cell).
   if (lane < ne) {
     const int le = lane, e = e0 + lane;
     int8_t* g = sgrid + le * RC;
-    uint8_t* oc = socc + le * RC;
     int32_t* p = spos + le * N;
     int apples = apples0;
     const int steps = steps0 + 1;
 #pragma unroll 1
     for (int k = 0; k < N; ++k) {
       const int a = sact[le * N + k];
-      const int pk = p[k];
-      const int r = pk >> 8, c = pk & 255;
+      const int32_t w = p[k];
+      int r = pos_r(w), c = pos_c(w), pr = (w >> 24) & 255, pc = (w >> 16) & 255;
       const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
       const int nc = c + (a == 1 ? -1 : (a == 3 ? 1 : 0));
-      const bool inside = nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
-      const int tcell = inside ? nr * d.C + nc : 0;
-      const int occ = inside ? oc[tcell] : 0;
-      const bool ok = inside && (occ == 0 || occ == k + 1);
-      const int ocell = r * d.C + c;
-      const int cell = ok ? tcell : ocell;
-      if (ok) {
-        oc[ocell] = 0;
-        oc[tcell] = (uint8_t)(k + 1);
+      const bool inside = a != 4 && nr >= 0 && nr < d.R && nc >= 0 && nc < d.C;
+      if (inside && g[nr * d.C + nc] < 3) {
+        pr = r;
+        pc = c;
+        r = nr;
+        c = nc;
       }
-      p[k] = ok ? ((nr << 8) | nc) : pk;
-      const int item = g[cell];
-      const bool big = (k & 1) == 0;
-      const float rk =
-          d.step_cost + (item == 2 ? (big ? 10.0f : 1.0f) : (item == 1 ? (big ? -10.0f : -1.0f) : 0.0f));
-      apples -= item == 2 ? 1 : 0;
-      g[cell] = 0;
+      float rk = d.step_cost;
+      if (r != pr || c != pc) {
+        const int cell = r * d.C + c;
+        const int item = g[cell];
+        const bool big = (k & 1) == 0;
+        if (item == 1) rk += big ? -10.0f : -1.0f;
+        if (item == 2) {
+          rk += big ? 10.0f : 1.0f;
+          apples -= 1;
+        }
+        g[pr * d.C + pc] = 0;
+        g[cell] = (int8_t)(3 + k);
+      }
+      p[k] = (pr << 24) | (pc << 16) | (r << 8) | c;
       rew[(int64_t)e * N + k] = rk;
     }
     const bool dn = steps >= d.max_steps || apples == 0;
@@ -301,34 +296,22 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
   if (ea < nl) {
     const int le2 = ea / N, k2 = ea % N;
     float* o = sloc + le2 * LD + k2 * OBS_LOCAL;
-    const int pr = mypos >> 8, pc = mypos & 255;
+    const int pr = pos_r(mypos), pc = pos_c(mypos);
     if (part == 0) {
-      o[0] = (float)pr * d.inv_r;
-      o[1] = (float)pc * d.inv_c;
+      o[0] = stab[pr];
+      o[1] = stab[d.R + pc];
     }
     const int8_t* g = sgrid + le2 * RC;
-    const uint8_t* oc = socc + le2 * RC;
     for (int cell = part; cell < 9; cell += TB / WT) {
       const int rr = pr + cell / 3 - 1, cc = pc + cell % 3 - 1;
       const bool inside = rr >= 0 && rr < d.R && cc >= 0 && cc < d.C;
-      float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f, v4 = 1.f;
-      if (inside) {
-        const int ci = rr * d.C + cc;
-        const int item = g[ci];
-        const int occ = oc[ci];
-        v0 = item == 1 ? 1.f : 0.f;
-        v1 = item == 2 ? 1.f : 0.f;
-        const bool ag = item == 0 && occ != 0;
-        v2 = (ag && ((occ - 1) & 1) == 0) ? 1.f : 0.f;
-        v3 = (ag && ((occ - 1) & 1) == 1) ? 1.f : 0.f;
-        v4 = 0.f;
-      }
+      const int item = inside ? g[rr * d.C + cc] : 0;
       float* q = o + 2 + 5 * cell;
-      q[0] = v0;
-      q[1] = v1;
-      q[2] = v2;
-      q[3] = v3;
-      q[4] = v4;
+      q[0] = item == 1 ? 1.f : 0.f;
+      q[1] = item == 2 ? 1.f : 0.f;
+      q[2] = (item >= 3 && ((item - 3) & 1) == 0) ? 1.f : 0.f;
+      q[3] = (item >= 3 && ((item - 3) & 1) == 1) ? 1.f : 0.f;
+      q[4] = 0.f;
     }
   }
   __syncthreads();
@@ -402,12 +385,12 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
     }
   }
   if ((RC & 3) == 0) {
-    uint32_t* g32 = reinterpret_cast<uint32_t*>(d.grid + (int64_t)e0 * RC);
+    uint32_t* g32w = reinterpret_cast<uint32_t*>(d.grid + (int64_t)e0 * RC);
     const uint32_t* ig32 = reinterpret_cast<const uint32_t*>(d.init_grid);
     const int RC4 = RC >> 2;
     for (int i = lane; i < ne * RC4; i += TB) {
       const int le = i / RC4;
-      g32[i] = (autoreset && env_done(le)) ? ig32[i - le * RC4] : reinterpret_cast<const uint32_t*>(sgrid)[i];
+      g32w[i] = (autoreset && env_done(le)) ? ig32[i - le * RC4] : reinterpret_cast<const uint32_t*>(sgrid)[i];
     }
   } else {
     for (int i = lane; i < ne * RC; i += TB) {
@@ -418,7 +401,16 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
   if (lane < nl) d.pos[(int64_t)e0 * N + lane] = (autoreset && env_done(le_l)) ? d.init_pos[k_l] : mypos;
 }
 
-static size_t step_smem(const EnvDev& d) { return (size_t)env_smem(d.eb, d.N, d.R * d.C).total; }
+static size_t step_smem(const EnvDev& d) { return (size_t)env_smem(d.eb, d.N, d.R, d.C).total; }
+
+// round(i / (n - 1), 2) as Python computes it (the correctly rounded 2-decimal value of the double quotient,
+// ties to even), then float32: printf's %.2f rounds the exact binary value the same way
+static float coord_feature(int i, int n) {
+  if (n <= 1) return 0.0f;
+  char buf[32];
+  snprintf(buf, sizeof(buf), "%.2f", (double)i / (double)(n - 1));
+  return (float)strtod(buf, nullptr);
+}
 
 int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** out) {
   (void)seed;  // the layout is deterministic (ma_gym Checkers resets to a fixed layout)
@@ -439,19 +431,30 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   d.D = OBS_LOCAL * (d.full_obs ? d.N : 1);
   d.max_steps = cfg->max_steps;
   d.step_cost = cfg->step_cost;
-  d.inv_r = 1.0f / (float)(d.R > 1 ? d.R - 1 : 1);
-  d.inv_c = 1.0f / (float)(d.C > 1 ? d.C - 1 : 1);
   const int RC = d.R * d.C;
+  // __init_full_obs: agent markers first, then the fruit of every 3-row band (lemon flag first, flipped
+  // after every cell of the column-major walk over columns 0..C-3)
   std::vector<int8_t> grid(RC, 0);
-  int apples = 0;
-  for (int r = 0; r < d.R; ++r)
-    for (int c = 0; c < d.C - 2; ++c) {
-      grid[r * d.C + c] = ((r + c) % 2 == 0) ? 2 : 1;
-      apples += ((r + c) % 2 == 0);
-    }
-  d.init_apples = apples;
   std::vector<int32_t> pos(d.N);
-  for (int k = 0; k < d.N; ++k) pos[k] = ((3 * (k / 2) + 2 * (k % 2)) << 8) | (d.C - 2);
+  for (int k = 0; k < d.N; ++k) {
+    const int r = 3 * (k / 2) + 2 * (k % 2), c = d.C - 2;
+    pos[k] = (r << 24) | (c << 16) | (r << 8) | c;
+    grid[r * d.C + c] = (int8_t)(3 + k);
+  }
+  int apples = 0;
+  for (int b = 0; b < d.R / 3; ++b) {
+    bool lemon = true;
+    for (int c = 0; c < d.C - 2; ++c)
+      for (int lr = 0; lr < 3; ++lr) {
+        grid[(3 * b + lr) * d.C + c] = lemon ? 1 : 2;
+        apples += lemon ? 0 : 1;
+        lemon = !lemon;
+      }
+  }
+  d.init_apples = apples;
+  std::vector<float> tab(d.R + d.C);
+  for (int r = 0; r < d.R; ++r) tab[r] = coord_feature(r, d.R);
+  for (int c = 0; c < d.C; ++c) tab[d.R + c] = coord_feature(c, d.C);
   MM_REQUIRE(step_smem(d) <= 64 * 1024, "env_create: grid too large for LDS staging");
 
   const size_t E = (size_t)d.E;
@@ -462,8 +465,8 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
     return o;
   };
   const size_t o_pos = take(E * d.N * 4), o_grid = take(E * RC), o_steps = take(E * 4), o_apples = take(E * 4),
-               o_igrid = take(RC), o_ipos = take(d.N * 4), o_robs = take((size_t)d.N * d.D * 4),
-               o_pos2 = take(E * d.N * 4), o_grid2 = take(E * RC), o_steps2 = take(E * 4), o_apples2 = take(E * 4);
+               o_igrid = take(RC), o_ipos = take(d.N * 4), o_tab = take((d.R + d.C) * 4),
+               o_robs = take((size_t)d.N * d.D * 4);
   void* base = nullptr;
   MM_HIP_CHECK(hipMalloc(&base, off));
   char* b = static_cast<char*>(base);
@@ -473,21 +476,21 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   d.apples = reinterpret_cast<int32_t*>(b + o_apples);
   d.init_grid = reinterpret_cast<int8_t*>(b + o_igrid);
   d.init_pos = reinterpret_cast<int32_t*>(b + o_ipos);
+  d.rtab = reinterpret_cast<float*>(b + o_tab);
+  d.ctab = d.rtab + d.R;
   d.reset_obs = reinterpret_cast<float*>(b + o_robs);
-  d.pos2 = reinterpret_cast<int32_t*>(b + o_pos2);
-  d.grid2 = reinterpret_cast<int8_t*>(b + o_grid2);
-  d.steps2 = reinterpret_cast<int32_t*>(b + o_steps2);
-  d.apples2 = reinterpret_cast<int32_t*>(b + o_apples2);
-  MM_HIP_CHECK(hipMemcpy(b + o_igrid, grid.data(), RC, hipMemcpyHostToDevice));
-  MM_HIP_CHECK(hipMemcpy(b + o_ipos, pos.data(), d.N * 4, hipMemcpyHostToDevice));
+  hipError_t e = hipMemcpy(b + o_igrid, grid.data(), RC, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b + o_ipos, pos.data(), d.N * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b + o_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
   mm_env* env = new mm_env;
   env->d = d;
   env->alloc = base;
   const int blocks = (d.E + d.eb - 1) / d.eb;
   const size_t sm = ((d.N * 4 + 15) & ~15) + RC;
-  hipLaunchKernelGGL(env_reset_kernel, dim3(blocks), dim3(256), sm, 0, d, (float*)nullptr, 1);
-  hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpy(b + o_pos2, b + o_pos, o_igrid - o_pos, hipMemcpyDeviceToDevice);   // buffer 2 = 1
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(env_reset_kernel, dim3(blocks), dim3(256), sm, 0, d, (float*)nullptr, 1);
+    e = hipDeviceSynchronize();
+  }
   if (e != hipSuccess) {
     set_error("env_create: reset failed: %s", hipGetErrorString(e));
     (void)hipFree(base);
@@ -527,37 +530,6 @@ int env_step(mm_env* env, const int32_t* act, float* next_obs, int64_t next_se, 
 }
 
 const float* env_reset_obs(const mm_env* env) { return env->d.reset_obs; }
-
-int env_fused_view(mm_env* env, FusedEnv* v) {
-  MM_REQUIRE(env && v, "env_fused_view: null argument");
-  const EnvDev& d = env->d;
-  MM_REQUIRE(d.N <= 8 && d.R * d.C <= 128 && d.R <= 255 && d.C <= 255,
-             "fused rollout step: needs N <= 8 agents and a grid of <= 128 cells (N=%d, %dx%d)", d.N, d.R, d.C);
-  MM_REQUIRE(!d.full_obs || d.N <= 4, "fused rollout step: full observation needs N <= 4 (N=%d)", d.N);
-  v->E = d.E;
-  v->N = d.N;
-  v->R = d.R;
-  v->C = d.C;
-  v->D = d.D;
-  v->max_steps = d.max_steps;
-  v->full_obs = d.full_obs;
-  v->init_apples = d.init_apples;
-  v->step_cost = d.step_cost;
-  v->inv_r = d.inv_r;
-  v->inv_c = d.inv_c;
-  v->pos[0] = d.pos;
-  v->pos[1] = d.pos2;
-  v->grid[0] = d.grid;
-  v->grid[1] = d.grid2;
-  v->steps[0] = d.steps;
-  v->steps[1] = d.steps2;
-  v->apples[0] = d.apples;
-  v->apples[1] = d.apples2;
-  v->init_grid = d.init_grid;
-  v->init_pos = d.init_pos;
-  v->reset_obs = d.reset_obs;
-  return MM_OK;
-}
 
 }  // namespace mm
 
@@ -609,32 +581,21 @@ int mm_env_step_rows_begin(mm_env* env, const int32_t* act, float* store_obs, in
   return mm::env_step(env, act, store_obs + nd, row_stride, staging, nullptr, cur_row, rew, done, nullptr,
                       (hipStream_t)s, &bc);
 }
-int mm_env_copy_state(mm_env* env, int32_t from, int32_t to, mm_stream_t s) {
-  MM_REQUIRE(env && (from == 0 || from == 1) && (to == 0 || to == 1), "env_copy_state: bad arguments");
-  if (from == to) return MM_OK;
-  const mm::EnvDev& d = env->d;
-  const size_t E = (size_t)d.E, RC = (size_t)d.R * d.C;
-  int32_t* pos[2] = {d.pos, d.pos2};
-  int8_t* grid[2] = {d.grid, d.grid2};
-  int32_t* steps[2] = {d.steps, d.steps2};
-  int32_t* apples[2] = {d.apples, d.apples2};
-  const hipStream_t st = (hipStream_t)s;
-  MM_HIP_CHECK(hipMemcpyAsync(pos[to], pos[from], E * d.N * 4, hipMemcpyDeviceToDevice, st));
-  MM_HIP_CHECK(hipMemcpyAsync(grid[to], grid[from], E * RC, hipMemcpyDeviceToDevice, st));
-  MM_HIP_CHECK(hipMemcpyAsync(steps[to], steps[from], E * 4, hipMemcpyDeviceToDevice, st));
-  MM_HIP_CHECK(hipMemcpyAsync(apples[to], apples[from], E * 4, hipMemcpyDeviceToDevice, st));
-  return MM_OK;
-}
-
-int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, int32_t* apples) {
+int mm_env_get_state(mm_env* env, int32_t* pos, int32_t* prev, int8_t* grid, int32_t* steps, int32_t* apples) {
   if (!env) return MM_EINVAL;
   const mm::EnvDev& d = env->d;
   if (hipDeviceSynchronize() != hipSuccess) return MM_EHIP;
   std::vector<int32_t> p((size_t)d.E * d.N);
   if (hipMemcpy(p.data(), d.pos, p.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
   for (size_t i = 0; i < p.size(); ++i) {
-    pos[2 * i] = p[i] >> 8;
-    pos[2 * i + 1] = p[i] & 255;
+    if (pos) {
+      pos[2 * i] = (p[i] >> 8) & 255;
+      pos[2 * i + 1] = p[i] & 255;
+    }
+    if (prev) {
+      prev[2 * i] = (p[i] >> 24) & 255;
+      prev[2 * i + 1] = (p[i] >> 16) & 255;
+    }
   }
   if (grid && hipMemcpy(grid, d.grid, (size_t)d.E * d.R * d.C, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
   if (steps && hipMemcpy(steps, d.steps, (size_t)d.E * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
@@ -642,19 +603,23 @@ int mm_env_get_state(mm_env* env, int32_t* pos, int8_t* grid, int32_t* steps, in
   return MM_OK;
 }
 
-int mm_env_set_state(mm_env* env, const int32_t* pos, const int8_t* grid, const int32_t* steps,
+int mm_env_set_state(mm_env* env, const int32_t* pos, const int32_t* prev, const int8_t* grid, const int32_t* steps,
                      const int32_t* apples) {
-  MM_REQUIRE(env && pos && grid && steps && apples, "env_set_state: null argument");
+  MM_REQUIRE(env && pos && prev && grid && steps && apples, "env_set_state: null argument");
   const mm::EnvDev& d = env->d;
   std::vector<int32_t> p((size_t)d.E * d.N);
   for (size_t i = 0; i < p.size(); ++i) {
-    MM_REQUIRE(pos[2 * i] >= 0 && pos[2 * i] < d.R && pos[2 * i + 1] >= 0 && pos[2 * i + 1] < d.C,
+    MM_REQUIRE(pos[2 * i] >= 0 && pos[2 * i] < d.R && pos[2 * i + 1] >= 0 && pos[2 * i + 1] < d.C &&
+                   prev[2 * i] >= 0 && prev[2 * i] < d.R && prev[2 * i + 1] >= 0 && prev[2 * i + 1] < d.C,
                "env_set_state: position out of the grid");
-    p[i] = (pos[2 * i] << 8) | pos[2 * i + 1];
+    p[i] = (prev[2 * i] << 24) | (prev[2 * i + 1] << 16) | (pos[2 * i] << 8) | pos[2 * i + 1];
   }
+  const size_t RC = (size_t)d.R * d.C;
+  for (size_t i = 0; i < (size_t)d.E * RC; ++i)
+    MM_REQUIRE(grid[i] >= 0 && grid[i] < 3 + d.N, "env_set_state: grid code out of range");
   MM_HIP_CHECK(hipDeviceSynchronize());
   MM_HIP_CHECK(hipMemcpy(d.pos, p.data(), p.size() * 4, hipMemcpyHostToDevice));
-  MM_HIP_CHECK(hipMemcpy(d.grid, grid, (size_t)d.E * d.R * d.C, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(d.grid, grid, (size_t)d.E * RC, hipMemcpyHostToDevice));
   MM_HIP_CHECK(hipMemcpy(d.steps, steps, (size_t)d.E * 4, hipMemcpyHostToDevice));
   MM_HIP_CHECK(hipMemcpy(d.apples, apples, (size_t)d.E * 4, hipMemcpyHostToDevice));
   return MM_OK;

@@ -778,7 +778,6 @@ __device__ __forceinline__ bool mb_last(uint32_t* ticket, uint32_t* s_last) {
 // The chunk's last TD / store step (td_chunk_kernel, rollout.hip; cal_td_error + the chunk lists,
 // vdn/_utils.py:44-52, vdn/main.py:140-167): thread per (env, agent), agent-order sums per env.
 __device__ void mb_td_fold(TdFuse t, int64_t E, int N, float (*sh)[MB_T]) {
-  td_resolve_ring(t);
   const int epb = MB_T / N;
   const int le = threadIdx.x / N, k = threadIdx.x % N;
   if (t.counter && blockIdx.x == 0 && threadIdx.x == 0) *t.counter += 1;   // RNG stream of the next step
@@ -1232,23 +1231,6 @@ static int per_insert_impl(mm_per* per, const float* td, int64_t k, int64_t* row
 
 int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s) {
   return per_insert_impl(per, td, k, rows_inout, slots_out, nullptr, 0, (hipStream_t)s);
-}
-
-int mm_per_insert_td_ring(mm_per* per, int64_t k, int32_t n_agents, float gamma, const float* rew_ring,
-                          const uint8_t* done_ring, const float* qsel_ring, const float* maxq_ring,
-                          const int32_t* act_ring, const uint64_t* step, float* chunk_td, int32_t step_in_chunk,
-                          int32_t chunk_len, uint8_t* store_act, float* store_rew, uint8_t* store_done,
-                          int64_t* rows_inout, int64_t* slots_out, mm_stream_t s) {
-  MM_REQUIRE(rew_ring && done_ring && qsel_ring && maxq_ring && act_ring && step && chunk_td && store_act &&
-                 store_rew && store_done && rows_inout, "per_insert_td_ring: null argument");
-  MM_REQUIRE(step_in_chunk >= 0 && step_in_chunk < chunk_len, "per_insert_td_ring: bad step");
-  MM_REQUIRE(n_agents >= 1 && n_agents <= 256, "per_insert_td_ring: n_agents must be in [1,256]");
-  mm::TdFuse t{rew_ring, done_ring, qsel_ring, maxq_ring, act_ring, chunk_td, store_act, store_rew, store_done,
-               rows_inout, nullptr, gamma, step_in_chunk, chunk_len, 1};
-  t.ring_step = step;
-  t.ring_en = k * n_agents;
-  t.ring_e = k;
-  return per_insert_impl(per, chunk_td, k, rows_inout, slots_out, &t, n_agents, (hipStream_t)s);
 }
 
 int mm_per_insert_td(mm_per* per, int64_t k, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,

@@ -50,15 +50,6 @@ class EnvCfg(ctypes.Structure):
                 ("step_cost", c_f32)]
 
 
-class RolloutIO(ctypes.Structure):
-    """mm_rollout_io (include/minimarl.h): buffers of the fused rollout step."""
-    _fields_ = [("store_obs", c_vp), ("store_act", c_vp), ("store_rew", c_vp), ("store_done", c_vp),
-                ("row_stride", c_i64), ("chunk_len", c_i32), ("td_on", c_i32),
-                ("staging", c_vp), ("cur_row", c_vp), ("chunk_td", c_vp),
-                ("act", c_vp), ("qsel", c_vp), ("maxq", c_vp), ("rew", c_vp), ("done", c_vp), ("step", c_vp),
-                ("gamma", c_f32), ("n_rows", c_i64), ("err", c_vp)]
-
-
 # (name, restype, argtypes) for every entry point of include/minimarl.h (+ extended ones)
 _SIGS = [
     ("mm_last_error", ctypes.c_char_p, []),
@@ -80,7 +71,7 @@ _SIGS = [
                                     c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_reset_obs", c_vp, [c_vp]),
     ("mm_env_step_rows_begin", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    ("mm_env_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_grid_shape", c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     ("mm_td_chunk_step", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                                  c_vp, c_vp, c_i64, c_vp]),
@@ -95,12 +86,6 @@ _SIGS = [
     ("mm_per_insert", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     ("mm_per_insert_td", c_i32, [c_vp, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
                                  c_vp, c_vp, c_vp, c_vp, c_vp]),
-    ("mm_per_insert_td_ring", c_i32, [c_vp, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32,
-                                      c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    ("mm_rollout_step_supported", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_i64]),
-    ("mm_rollout_step", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_vp,
-                                ctypes.POINTER(QFwdIO), ctypes.POINTER(RolloutIO), c_vp]),
-    ("mm_env_copy_state", c_i32, [c_vp, c_i32, c_i32, c_vp]),
     ("mm_per_sample", c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_per_sample_rng", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
     ("mm_per_update", c_i32, [c_vp, c_vp, c_vp, c_i32, c_vp]),
@@ -236,7 +221,7 @@ _SIGS += [
                               c_vp, c_f32, c_vp]),
     ("mm_per_sample_uniform", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
     ("mm_eval_accum", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    ("mm_env_set_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_set_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_per_save_state", c_i32, [c_vp, c_vp, c_vp, ctypes.POINTER(c_f64), c_vp]),
     ("mm_per_load_state", c_i32, [c_vp, c_vp, c_vp, ctypes.POINTER(c_f64), c_vp]),
     ("mm_debug_trace", c_i32, [c_vp, c_i32]),

@@ -17,15 +17,6 @@ insert (four launches, its first one also running that step's TD/store). All str
 one HIP stream, no host sync; a chunk of steps is captured once as a HIP graph and replayed. The
 store/TD of the last executed step therefore lands with the next step (``flush_td()`` writes it
 now).
-Fused mode (opt-in: ``fused=True``, or ``fused=None`` = on wherever it applies — the Checkers env, E >= 2048
-lockstep envs and a forward shape the fused kernel is built for): ONE launch per step (mm_rollout_step, agent_fwd.hip
-rollout_step_h3_kernel) runs the env transition, the target forward of step t and the behavior forward
-of step t+1, and the TD / store of step t-1; the chunk's last step adds the PER insert. Its per-step
-buffers are rings indexed by the device step counter (act / qsel by t % 3, rew / done / maxq by t % 2,
-the env state double-buffered by t % 2), so one captured step replays for any t. Bit-identical to the
-unfused launches (test_gpu_rollout.py test_fused_step_matches_unfused), but slower at 4096 x 8 (51.5 us
-vs 9.8 + 27 us: every (net, agent) workgroup re-simulates its 256-env tile's transition, a serial
-agent-ordered chain that no other workgroup on the CU hides), so the default is the two-launch step.
 Hidden states reset at episode ends (the reference re-inits them per episode,
 vdn/main.py:137-138); chunks span episode boundaries like the reference's
 global ``count_step`` (vdn/main.py:151-167).
@@ -41,7 +32,7 @@ import ctypes
 
 import torch
 
-from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, RolloutIO, check, lib
+from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, check, lib
 from .env import make_env
 from .qnet import AgentQNet, graph_capture, ptr, stream_handle
 from .replay import DevicePER
@@ -63,7 +54,7 @@ class ChunkStore:
 class RolloutEngine:
     def __init__(self, n_envs, n_agents, obs_dim=None, n_actions=5, f1=64, g=32, h=32, chunk=10,
                  capacity=None, gamma=0.99, max_steps=100, step_cost=-0.01, full_observable=False,
-                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", fused=False, device="cuda"):
+                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", device="cuda"):
         self.device = torch.device(device)
         self.E, self.N, self.C = int(n_envs), int(n_agents), int(chunk)
         self.gamma = float(gamma)
@@ -108,60 +99,28 @@ class RolloutEngine:
         self.t = 0
         self.seed = int(seed)
         self.chunks_inserted = 0
-        self.fused = self._fused_ok() if fused is None else bool(fused)
-        if self.fused:
-            if not self._fused_ok():
-                raise ValueError("RolloutEngine(fused=True): " + lib().mm_last_error().decode(errors="replace"))
-            assert self.store.rows < 2 ** 31, "fused step: store rows are 32-bit in LDS"
-            # rings of the fused step (see the module docstring); step_dev = [t, arrival ticket]
-            self.act_ring = torch.zeros(3, E, N, dtype=torch.int32, device=dev)
-            self.qsel_ring = torch.zeros(3, E, N, device=dev)
-            self.maxq_ring = torch.zeros(2, E, N, device=dev)
-            self.rew_ring = torch.zeros(2, E, N, device=dev)
-            self.done_ring = torch.zeros(2, E, dtype=torch.uint8, device=dev)
-            self.step_dev = torch.zeros(2, dtype=torch.int64, device=dev)
         self._build_io()
         self.env.reset(self.init_obs)
 
-    def _fused_ok(self):
-        if self.env_kind != "checkers":
-            return False
-        return lib().mm_rollout_step_supported(self.env.handle(), ctypes.byref(self.behavior.dims), self.E) == 0
-
     def state_buffers(self):
-        """The per-step device buffers a checkpoint must carry (name -> tensor) in this engine's mode."""
+        """The per-step device buffers a checkpoint must carry (name -> tensor)."""
         out = {k: getattr(self, k) for k in ("cur_row", "init_obs", "h", "ht", "chunk_td", "eps_dev", "staging")}
-        if self.fused:
-            for k in ("act_ring", "qsel_ring", "maxq_ring", "rew_ring", "done_ring", "step_dev"):
-                out[k] = getattr(self, k)
-        else:
-            out.update(maxq=self.maxq, rew=self.rew, counter_dev=self.counter_dev)
-            for k in range(2):
-                out[f"done_buf{k}"] = self.done_buf[k]
-                out[f"act_buf{k}"] = self.act_buf[k]
-                out[f"qsel_buf{k}"] = self.qsel_buf[k]
+        out.update(maxq=self.maxq, rew=self.rew, counter_dev=self.counter_dev)
+        for k in range(2):
+            out[f"done_buf{k}"] = self.done_buf[k]
+            out[f"act_buf{k}"] = self.act_buf[k]
+            out[f"qsel_buf{k}"] = self.qsel_buf[k]
         return out
-
-    def env_state_to_live(self):
-        """Fused mode keeps the env state in buffer t % 2: copy it into buffer 0, the one the env's state
-        accessors (checkpoint_tensors / get_state) read."""
-        if self.fused and self.t % 2:
-            check(lib().mm_env_copy_state(self.env.handle(), 1, 0, stream_handle(self.device)), "env_copy_state")
-
-    def env_state_from_live(self):
-        """After the env state was restored into buffer 0: make it the fused step's buffer t % 2."""
-        if self.fused and self.t % 2:
-            check(lib().mm_env_copy_state(self.env.handle(), 0, 1, stream_handle(self.device)), "env_copy_state")
 
     @property
     def last_rew(self):
         """rewards [E, N] of the last executed step"""
-        return self.rew_ring[(self.t - 1) % 2] if self.fused else self.rew
+        return self.rew
 
     @property
     def last_done(self):
         """done flags [E] of the last executed step"""
-        return self.done_ring[(self.t - 1) % 2] if self.fused else self.done_buf[(self.t - 1) % 2]
+        return self.done_buf[(self.t - 1) % 2]
 
     def current_obs(self):
         """s_{t+1} [E,N,D] as the next behavior forward reads it (materialised for tests only)."""
@@ -174,8 +133,6 @@ class RolloutEngine:
     @property
     def act(self):
         """actions [E, N] of the last executed step"""
-        if self.fused:
-            return self.act_ring[(self.t - 1) % 3] if self.t > 0 else self.act_ring[0]
         return self.act_buf[(self.t - 1) % 2] if self.t > 0 else self.act_buf[0]
 
     def _io_behavior(self, k):
@@ -219,30 +176,6 @@ class RolloutEngine:
         self.io_b0 = self._io_behavior(0)
         self.io_b0.counter_ptr = None
         self.io_b0.counter = 0x7FFFFFFFFFFFFFFF
-        if self.fused:
-            # prologue: a_0 / Q(s_0, a_0) into ring slot 0
-            self.io_b0.act_out, self.io_b0.qsel_out = self.act_ring[0].data_ptr(), self.qsel_ring[0].data_ptr()
-            # fused step: ring bases (the kernel offsets them by t); obs come from the env state
-            self.io_fb = self._io_behavior(0)
-            self.io_fb.act_out, self.io_fb.qsel_out = self.act_ring.data_ptr(), self.qsel_ring.data_ptr()
-            self.io_fb.reset = self.io_fb.obs_row = None
-            self.io_fb.counter_ptr = None
-            self.io_ft = self._io_target(0)
-            self.io_ft.qsel_out = self.maxq_ring.data_ptr()
-            self.io_ft.reset = self.io_ft.obs_row = None
-            r = RolloutIO()
-            r.store_obs, r.store_act = self.store.obs.data_ptr(), self.store.act.data_ptr()
-            r.store_rew, r.store_done = self.store.rew.data_ptr(), self.store.done.data_ptr()
-            r.row_stride, r.chunk_len, r.td_on = self.store.row_stride, self.C, 1
-            r.staging, r.cur_row, r.chunk_td = self.staging.data_ptr(), self.cur_row.data_ptr(), self.chunk_td.data_ptr()
-            r.act, r.qsel, r.maxq = self.act_ring.data_ptr(), self.qsel_ring.data_ptr(), self.maxq_ring.data_ptr()
-            r.rew, r.done, r.step = self.rew_ring.data_ptr(), self.done_ring.data_ptr(), self.step_dev.data_ptr()
-            r.gamma = self.gamma
-            r.n_rows = self.store.rows
-            self.rollout_err = torch.zeros(1, dtype=torch.int32, device=self.device)
-            r.err = self.rollout_err.data_ptr()
-            self.rio = r
-
     def sync_target(self):
         self.target.copy_from(self.behavior)
 
@@ -261,40 +194,8 @@ class RolloutEngine:
         self.behavior.forward_io(self.E, self.io_b0, s)
         self._primed = True
 
-    def _step_launch_fused(self):
-        """Step t in ONE launch: env(t) + target fwd(t) + behavior fwd(t+1) + TD/store(t-1); PER insert at the
-        chunk end. Nothing about t is baked into the launches (the kernel reads the device step counter)."""
-        s = stream_handle(self.device)
-        L = lib()
-        c = self.t % self.C
-        if not self._primed:
-            self._prologue(s)
-        self.behavior.pack(s)
-        self.target.pack(s)
-        r = self.rio
-        if self._td_flushed:      # TD(t-1) already written by flush_td: this one launch skips it
-            r = RolloutIO.from_buffer_copy(self.rio)
-            r.td_on = 0
-        check(L.mm_rollout_step(self.env.handle(), ctypes.byref(self.behavior.dims), ptr(self.target.packed),
-                                ctypes.byref(self.io_ft), ptr(self.behavior.packed), ctypes.byref(self.io_fb),
-                                ctypes.byref(r), s), "rollout_step")
-        self._td_flushed = False
-        if c == self.C - 1:
-            check(L.mm_per_insert_td_ring(self.per._h, self.E, self.N, self.gamma, ptr(self.rew_ring),
-                                          ptr(self.done_ring), ptr(self.qsel_ring), ptr(self.maxq_ring),
-                                          ptr(self.act_ring), ptr(self.step_dev), ptr(self.chunk_td), c, self.C,
-                                          ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done),
-                                          ptr(self.staging), None, s), "per_insert_td_ring")
-            self.chunks_inserted += self.E
-            self._td_pending = False
-        else:
-            self._td_pending = True
-        self.t += 1
-
     def _step_launch(self):
         """Step t: env(t) -> [target fwd(t) + behavior fwd(t+1)] in ONE launch -> TD/store(t)."""
-        if self.fused:
-            return self._step_launch_fused()
         s = stream_handle(self.device)
         L = lib()
         t = self.t
@@ -352,15 +253,6 @@ class RolloutEngine:
             self._td_flushed = True
 
     def _td_standalone(self, s, k, c):
-        if self.fused:
-            t = self.t - 1
-            p2, p3 = t % 2, t % 3
-            check(lib().mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew_ring[p2]),
-                                              ptr(self.done_ring[p2]), ptr(self.qsel_ring[p3]),
-                                              ptr(self.maxq_ring[p2]), ptr(self.act_ring[p3]), ptr(self.chunk_td),
-                                              c, self.C, ptr(self.store.act), ptr(self.store.rew),
-                                              ptr(self.store.done), ptr(self.staging), None, s), "td_chunk")
-            return
         check(lib().mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done_buf[k]),
                                           ptr(self.qsel_buf[k]), ptr(self.maxq), ptr(self.act_buf[k]),
                                           ptr(self.chunk_td), c, self.C, ptr(self.store.act), ptr(self.store.rew),
@@ -369,8 +261,6 @@ class RolloutEngine:
 
     # ------------------------------------------------------------------ HIP graph replay
     def graph_steps(self):
-        if self.fused:
-            return self.C
         return self.C if self.C % 2 == 0 else 2 * self.C
 
     def capture(self):
@@ -516,9 +406,8 @@ class RolloutEngine:
             self.step(epsilon)
 
     def env_only(self, k=0):
-        """The step's env launch on its own (two-launch mode, mid-chunk form with the TD folded in); for
-        timing the dual forward in its rollout context (bench.py: (env + forward) - env)."""
-        assert not self.fused
+        """The step's env launch on its own (mid-chunk form with the TD folded in); for timing the dual
+        forward in its rollout context (bench.py: (env + forward) - env)."""
         s = stream_handle(self.device)
         nxt = ctypes.c_void_p(self.store.obs.data_ptr() + 4 * 2 * self.N * self.D)
         kp = 1 - k
@@ -530,16 +419,8 @@ class RolloutEngine:
                                     s), "env_step_td")
 
     def fused_forward(self, k=0):
-        """The step's dominant launch on its own (target fwd + behavior fwd); for timing. Fused mode: the
-        whole step launch (env + both forwards + TD) with the TD off; it advances the device step counter."""
+        """The step's dominant launch on its own (target fwd + behavior fwd); for timing."""
         s = stream_handle(self.device)
-        if self.fused:
-            r = RolloutIO.from_buffer_copy(self.rio)
-            r.td_on = 0
-            check(lib().mm_rollout_step(self.env.handle(), ctypes.byref(self.behavior.dims), ptr(self.target.packed),
-                                        ctypes.byref(self.io_ft), ptr(self.behavior.packed), ctypes.byref(self.io_fb),
-                                        ctypes.byref(r), s), "rollout_step")
-            return
         check(lib().mm_agent_q_fwd2(ctypes.byref(self.target.dims), ptr(self.target.packed),
                                     ctypes.byref(self.io_t[k]), self.E, ptr(self.behavior.packed),
                                     ctypes.byref(self.io_b[1 - k]), self.E, s), "agent_q_fwd2")

@@ -1,9 +1,10 @@
-"""Lockstep checkers gridworld stepped on the GPU (csrc/env.hip).
+"""ma_gym Checkers-v0 stepped on the GPU (csrc/env.hip), E envs in lockstep.
 
 Stands in for ``gym.make("ma_gym:Checkers-v0", full_observable, max_steps,
 step_cost)`` (vdn/main.py:61-64, qmix/main.py:66-71): E independent envs x N
-agents, obs laid out [env, agent, feat] in HBM. Dynamics spec: oracle/env.py
-(ma_gym itself is absent: parity with it is unpinned).
+agents, obs laid out [env, agent, feat] in HBM. Dynamics: the rule-by-rule restatement of
+ma_gym's published checkers.py in oracle/env.py (ma-gym 0.0.14 itself is absent: parity with it
+is unpinned; N > 2 is the documented band extension).
 """
 import ctypes
 
@@ -74,32 +75,37 @@ class VecEnv:
         return nxt, rew, done
 
     def get_state(self):
+        """(pos, prev, grid, steps, apples): agent_pos / agent_prev_pos [E,N,2], _full_obs codes [E,R,C]
+        (0 empty, 1 lemon, 2 apple, 3 + k agent k), _step_count [E], apples left [E]."""
         pos = np.empty((self.E, self.N, 2), np.int32)
+        prev = np.empty((self.E, self.N, 2), np.int32)
         grid = np.empty((self.E, self.rows, self.cols), np.int8)
         steps = np.empty(self.E, np.int32)
         apples = np.empty(self.E, np.int32)
-        check(lib().mm_env_get_state(self._h, pos.ctypes.data, grid.ctypes.data, steps.ctypes.data,
-                                     apples.ctypes.data), "env_get_state")
-        return pos, grid, steps, apples
+        check(lib().mm_env_get_state(self._h, pos.ctypes.data, prev.ctypes.data, grid.ctypes.data,
+                                     steps.ctypes.data, apples.ctypes.data), "env_get_state")
+        return pos, prev, grid, steps, apples
 
-    def set_state(self, pos, grid, steps, apples):
+    def set_state(self, pos, prev, grid, steps, apples):
         """Restore the state returned by get_state (checkpoint resume)."""
         pos = np.ascontiguousarray(pos, np.int32)
+        prev = np.ascontiguousarray(prev, np.int32)
         grid = np.ascontiguousarray(grid, np.int8)
         steps = np.ascontiguousarray(steps, np.int32)
         apples = np.ascontiguousarray(apples, np.int32)
-        assert pos.shape == (self.E, self.N, 2) and grid.shape == (self.E, self.rows, self.cols)
-        check(lib().mm_env_set_state(self._h, pos.ctypes.data, grid.ctypes.data, steps.ctypes.data,
-                                     apples.ctypes.data), "env_set_state")
+        assert pos.shape == prev.shape == (self.E, self.N, 2) and grid.shape == (self.E, self.rows, self.cols)
+        check(lib().mm_env_set_state(self._h, pos.ctypes.data, prev.ctypes.data, grid.ctypes.data,
+                                     steps.ctypes.data, apples.ctypes.data), "env_set_state")
 
     # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)
     def checkpoint_tensors(self):
-        pos, grid, steps, apples = self.get_state()
-        return {"pos": torch.from_numpy(pos), "grid": torch.from_numpy(grid), "steps": torch.from_numpy(steps),
-                "apples": torch.from_numpy(apples)}, {}
+        pos, prev, grid, steps, apples = self.get_state()
+        return {"pos": torch.from_numpy(pos), "prev": torch.from_numpy(prev), "grid": torch.from_numpy(grid),
+                "steps": torch.from_numpy(steps), "apples": torch.from_numpy(apples)}, {}
 
     def restore_tensors(self, ts, scalars=None):
-        self.set_state(ts["pos"].numpy(), ts["grid"].numpy(), ts["steps"].numpy(), ts["apples"].numpy())
+        self.set_state(ts["pos"].numpy(), ts["prev"].numpy(), ts["grid"].numpy(), ts["steps"].numpy(),
+                       ts["apples"].numpy())
 
 
 class SwitchVecEnv:

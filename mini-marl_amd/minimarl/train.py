@@ -177,7 +177,6 @@ class QTrainer:
         out = {"learner/" + k: v for k, v in ts.items()}
         pts, _ = eng.per.checkpoint_tensors()
         out.update({"per/" + k: v for k, v in pts.items()})
-        eng.env_state_to_live()          # fused mode: the env state of parity t % 2 into the env's live buffer
         ets, _ = eng.env.checkpoint_tensors()
         out.update({"env/" + k: v for k, v in ets.items()})
         for k, v in eng.state_buffers().items():
@@ -200,7 +199,7 @@ class QTrainer:
         eng.env.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("env/")})
         for k, v in eng.state_buffers().items():
             if "engine/" + k not in ts:
-                raise ValueError(f"checkpoint lacks engine/{k} (saved by an engine in the other step mode?)")
+                raise ValueError(f"checkpoint lacks engine/{k}")
             copy_into(v, ts["engine/" + k], k)
         if scalars.get("replay_saved"):
             for k in ("obs", "act", "rew", "done"):
@@ -208,7 +207,6 @@ class QTrainer:
         copy_into(self.ep_ret, ts["trainer/ep_ret"], "ep_ret")
         copy_into(self.score_acc, ts["trainer/score_acc"], "score_acc")
         eng.t, eng.chunks_inserted = int(scalars["t"]), int(scalars["chunks_inserted"])
-        eng.env_state_from_live()
         eng._primed, eng._td_pending = bool(scalars["primed"]), bool(scalars["td_pending"])
         eng._eps_host = None
         eng.behavior.mark_dirty()

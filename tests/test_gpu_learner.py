@@ -22,9 +22,9 @@ def _grad_view(learner, key):
     return learner.beh.view(key, learner.Gr[:learner.n_agent])
 
 
-def _check_grads(g_dev, g_ref):
+def _check_grads(g_dev, g_ref, what=""):
     scale = np.abs(g_ref).max()
-    np.testing.assert_array_less(np.abs(g_dev - g_ref), 2e-4 * scale + 1e-3 * np.abs(g_ref) + 1e-12)
+    np.testing.assert_array_less(np.abs(g_dev - g_ref), 2e-4 * scale + 1e-3 * np.abs(g_ref) + 1e-12, err_msg=what)
 
 
 def _make(fx, style, mode):
@@ -181,8 +181,9 @@ def test_learner_cfg5_benched_path_vs_oracle(mixer_fp16):
     replayed): 27 agents, obs 300, 36 actions, GRU-32 agents, Hm = 32 mixer over the 8100-wide state,
     C = 10 and B = 512 chunk samples, so the large-batch kernels run: agent_split (row tiles of 32
     samples), the chunk-sequence REC, the 8-samples-per-block mixer forward / backward (B >= 512) and,
-    with mixer_fp16, mixer_gi_f16 over 5120 rows per net, the fp16x3 agent PRE and the mixer's bf16x3
-    weight-gradient products.
+    with mixer_fp16, mixer_gi_f16 over 5120 rows per net and the mixer's bf16x3 weight-gradient products (the
+    agent path stays exact f32: the opt-in fp16x3 PRE, QLearner.fast_pre, flips ~0.3 % of dW1 / dW2 elements past
+    this bar through ReLU masks of near-zero pre-activations).
 
     Tolerances. fp32 mode: the file's fp32 bar (loss rtol 1e-4; gradients 2e-4 * max + 1e-3 * |g|;
     post-Adam params atol 2e-6 where |g| > 1e-3 max).
@@ -249,7 +250,7 @@ def test_learner_cfg5_benched_path_vs_oracle(mixer_fp16):
     for key in nets.AGENT_KEYS:      # the fp32 bar in both modes, no outliers
         g_ref = grads[key].numpy()
         g_dev = _grad_view(L, key).cpu().numpy() * coef
-        _check_grads(g_dev, g_ref)
+        _check_grads(g_dev, g_ref, key)
         sel = np.abs(g_ref) > 1e-3 * np.abs(g_ref).max()
         np.testing.assert_allclose(L.beh.view(key).cpu().numpy()[sel], newP[key].numpy()[sel], atol=2e-6,
                                    err_msg=key)

@@ -2,9 +2,16 @@
 golden vectors (tests/golden/mappo_*.npz) and the oracle (oracle/mappo.py).
 
 Tolerances (fp32; the device uses hardware exp/rcp for the GRU gates, ~1e-6 relative):
-values / log-probs / hiddens rtol 1e-5 atol 2e-6; returns rtol 1e-6; gradients
-|g - g_ref| <= 1e-3 * max|g_ref| + 1e-3 * |g_ref|; post-Adam params atol 3e-5 (a tenth of the
-three Adam steps' ~3e-4 travel) where |g_ref| is not negligible.
+values / log-probs / hiddens rtol 1e-5 atol 2e-6; returns rtol 1e-6.
+
+Training (gradients, post-Adam parameters, loss logs) is held to a bar DERIVED per test from the oracle on
+the same data (``_fp32_spread``): the oracle is run three times, in fp32 in the device's chunk order, in fp32
+in a random chunk order (the reference's randperm) and in float64; per tensor, the fp32 spread is
+max(|fp32 chunk - fp32 permuted|, |fp32 - f64|, 2^-23 max|f64|) (inf-norm), i.e. how far two legitimate fp32
+evaluations of the same sums land from each other and from the exact value. The device (different summation
+trees: MFMA k-accumulation, 128 block partials; hardware exp / rcp) must land within K_FP32 = 16 spreads of
+the f64 value. Measured spreads are ~1e-7 .. 8e-7 of a tensor's max at the golden size and at 512 x 8 x 100
+(tools/mappo_tol.py), so the bars are ~1e-5 of max|g| instead of the round-3 fixed 1e-3 .. 2e-3.
 """
 import numpy as np
 import pytest
@@ -15,6 +22,50 @@ from oracle import mappo as om
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 TOL = dict(rtol=1e-5, atol=2e-6)
+K_FP32 = 16
+
+
+def _ppo_oracle(PA, PC, data, vn0, epochs, L, dtype=torch.float32, perms=None):
+    """om.ppo_train in the given float dtype (params, buffer and ValueNorm cast); -> (record, PA2, PC2, vn2)."""
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        npd = np.float64 if dtype == torch.float64 else np.float32
+        d = {k: (v.astype(npd) if v.dtype in (np.float32, np.float64) else v) for k, v in data.items()}
+        pa = {k: torch.as_tensor(v).to(dtype) for k, v in PA.items()}
+        pc = {k: torch.as_tensor(v).to(dtype) for k, v in PC.items()}
+        rec = []
+        PA2, PC2, vn2 = om.ppo_train(pa, pc, d, om.ValueNorm(*vn0), epochs, L, perms=perms, record=rec)
+    finally:
+        torch.set_default_dtype(old)
+    return rec, PA2, PC2, vn2
+
+
+def _fp32_spread(f, n_chunks):
+    """f(dtype, perms) -> {name: array}; -> (f64 values, {name: fp32 spread}) (module docstring)."""
+    a = f(torch.float32, None)
+    b = f(torch.float32, np.random.default_rng(123).permutation(n_chunks)[None].repeat(64, 0))
+    c = f(torch.float64, None)
+    sp = {}
+    for k in c:
+        x, y, z = (np.asarray(v[k], np.float64) for v in (a, b, c))
+        sp[k] = max(np.abs(x - y).max(), np.abs(x - z).max(), 2.0 ** -23 * np.abs(z).max(), 1e-30)
+    return c, sp
+
+
+def _unclipped_grads(rec, ep=0):
+    """{(net, key): gradient before clip_grad_norm_} of epoch ep of an om.ppo_train record."""
+    out = {}
+    for n, tag, nk in ((0, "ga", "na"), (1, "gc", "nc")):
+        coef = min(1.0, 0.5 / (rec[ep][nk] + 1e-6))
+        for k in om.NET_KEYS:
+            out[(n, k)] = rec[ep][tag][k].double().numpy() / coef
+    return out
+
+
+def _assert_within(got, want, spread, what):
+    err = float(np.abs(np.asarray(got, np.float64) - want).max())
+    assert err <= K_FP32 * spread, f"{what}: |dev - f64| = {err:.3e} > {K_FP32} x spread {spread:.3e}"
 
 
 def _policy(fx, prefix=""):
@@ -150,13 +201,27 @@ def _trainer_from_fixture(fx, fused=True):
     return p, buf, tr
 
 
+def _golden_oracle_inputs(fx):
+    sd = {k[len("before."):]: fx[k] for k in fx if k.startswith("before.")}
+    PA, PC = om.net_from_state(sd, "actor.", "actor"), om.net_from_state(sd, "critic.", "critic")
+    data = {k[5:]: fx[k] for k in fx if k.startswith("data.")}
+    vn0 = (float(fx["vn0.running_mean"][0]), float(fx["vn0.running_mean_sq"][0]), float(fx["vn0.debiasing_term"]))
+    n_chunks = int(fx["T"]) * int(fx["E"]) * int(fx["N"]) // int(fx["L"])
+    return PA, PC, data, vn0, n_chunks
+
+
 @pytest.mark.parametrize("fused", [True, False], ids=["fused_mfma", "saves_wgrad"])
 def test_first_epoch_gradients_match_reference(golden, fused):
-    """Unclipped gradients of PPO epoch 0 vs the reference's (clipped) ones / its clip coefficient:
-    the fused MFMA pass (mm_mappo_grad, a partial tile of chunks) and the saves + wgrad path."""
+    """Unclipped gradients of PPO epoch 0: the fused MFMA pass (mm_mappo_grad, a partial tile of chunks) and
+    the saves + wgrad path, each tensor within K_FP32 fp32 spreads (module docstring) of the f64 oracle, and the
+    reference's own fp32 gradients (golden, clipped -> divided by its clip coefficient) within the same bar
+    plus their own distance to f64."""
     from minimarl._lib import lib
     fx = golden("mappo_train")
     p, buf, tr = _trainer_from_fixture(fx, fused)
+    PA, PC, data, vn0, nch = _golden_oracle_inputs(fx)
+    L = int(fx["L"])
+    g64, spread = _fp32_spread(lambda dt, pm: _unclipped_grads(_ppo_oracle(PA, PC, data, vn0, 1, L, dt, pm)[0]), nch)
     tr.prepare(buf)
     assert lib().mm_mappo_vn_update(tr.vn.data_ptr(), tr.stats.data_ptr(), 0.99999, None) == 0
     if fused:
@@ -170,38 +235,58 @@ def test_first_epoch_gradients_match_reference(golden, fused):
         for k in om.NET_KEYS:
             g = net.view(k, tr.grad[n]).cpu().numpy()
             ref = fx[f"grad{tag}0.{om.ref_name(k, kind)}"] / coef
-            scale = np.abs(ref).max()
-            np.testing.assert_array_less(np.abs(g - ref), 1e-3 * scale + 1e-3 * np.abs(ref) + 1e-9,
-                                         err_msg=f"{kind} {k}")
+            _assert_within(g, g64[(n, k)], spread[(n, k)], f"{kind} {k} vs f64")
+            ref_err = float(np.abs(ref - g64[(n, k)]).max())
+            assert np.abs(g - ref).max() <= K_FP32 * spread[(n, k)] + ref_err, f"{kind} {k} vs golden"
         # pads of the flat layout carry zero gradient
         assert float(tr.grad[n].abs().sum()) == pytest.approx(
             sum(float(net.view(k, tr.grad[n]).abs().sum()) for k in om.NET_KEYS), rel=1e-6)
 
 
+def _train_outputs(rec, PA2, PC2, vn2):
+    """post-train parameters and the train() log of an om.ppo_train run (R_MAPPO.train averages the per-epoch
+    losses / norms, ramppo_network.py:245-287)"""
+    out = {("actor", k): PA2[k].double().numpy() for k in om.NET_KEYS}
+    out.update({("critic", k): PC2[k].double().numpy() for k in om.NET_KEYS})
+    E = len(rec)
+    out["value_loss"] = np.array(sum(r["vloss"] for r in rec) / E)
+    out["policy_loss"] = np.array(sum(r["pol"] for r in rec) / E)
+    out["dist_entropy"] = np.array(sum(r["ent"] for r in rec) / E)
+    out["actor_grad_norm"] = np.array(sum(r["na"] for r in rec) / E)
+    out["critic_grad_norm"] = np.array(sum(r["nc"] for r in rec) / E)
+    out["vn_mean"] = vn2.m.double().numpy()
+    out["vn_mean_sq"] = vn2.msq.double().numpy()
+    return out
+
+
 @pytest.mark.parametrize("fused", [True, False], ids=["fused_mfma", "saves_wgrad"])
 def test_ppo_train_matches_reference(golden, fused):
+    """The golden train() (3 epochs): post-Adam parameters, ValueNorm state and the train_info log within K_FP32
+    fp32 spreads of the f64 oracle (a parameter's spread includes Adam's sign sensitivity: a near-zero gradient
+    whose sign differs between two fp32 orders moves the coordinate by ~lr either way, and the permuted fp32
+    run shows exactly that); and within the same bar plus the reference's own fp32 distance of its golden
+    values. The mean ratio is identically 1 at epoch 0 and tested at rtol 1e-5."""
     fx = golden("mappo_train")
     p, buf, tr = _trainer_from_fixture(fx, fused)
+    PA, PC, data, vn0, nch = _golden_oracle_inputs(fx)
+    EP, L = int(fx["epochs"]), int(fx["L"])
+    o64, spread = _fp32_spread(lambda dt, pm: _train_outputs(*_ppo_oracle(PA, PC, data, vn0, EP, L, dt, pm)), nch)
     info = tr.train(buf)
     torch.cuda.synchronize()
-    for n, (net, kind) in enumerate(((p.actor, "actor"), (p.critic, "critic"))):
-        tag = "a" if n == 0 else "c"
+    for net, kind in ((p.actor, "actor"), (p.critic, "critic")):
         for k in om.NET_KEYS:
-            name = om.ref_name(k, kind)
-            after = fx[f"after.{kind}.{name}"]
-            g = np.abs(fx[f"grad{tag}0.{name}"])
-            sel = g > 1e-3 * g.max()
             got = net.view(k).cpu().numpy()
-            np.testing.assert_allclose(got[sel], after[sel], atol=3e-5, err_msg=f"{kind} {k}")
-            np.testing.assert_allclose(got, after, atol=4e-4, err_msg=f"{kind} {k} (all)")
+            after = fx[f"after.{kind}.{om.ref_name(k, kind)}"]
+            _assert_within(got, o64[(kind, k)], spread[(kind, k)], f"{kind} {k} vs f64")
+            ref_err = float(np.abs(after - o64[(kind, k)]).max())
+            assert np.abs(got - after).max() <= K_FP32 * spread[(kind, k)] + ref_err, f"{kind} {k} vs golden"
     vn = tr.value_normalizer_state()
-    np.testing.assert_allclose(vn["running_mean"], fx["vn1.running_mean"], rtol=1e-5)
-    np.testing.assert_allclose(vn["running_mean_sq"], fx["vn1.running_mean_sq"], rtol=1e-5)
-    np.testing.assert_allclose(info["value_loss"], float(fx["info.value_loss"]), rtol=1e-3)
-    np.testing.assert_allclose(info["policy_loss"], float(fx["info.policy_loss"]), rtol=1e-2, atol=1e-5)
-    np.testing.assert_allclose(info["dist_entropy"], float(fx["info.dist_entropy"]), rtol=1e-5)
-    np.testing.assert_allclose(info["actor_grad_norm"], float(fx["info.actor_grad_norm"]), rtol=1e-3)
-    np.testing.assert_allclose(info["critic_grad_norm"], float(fx["info.critic_grad_norm"]), rtol=1e-3)
+    _assert_within(vn["running_mean"], o64["vn_mean"], spread["vn_mean"], "vn mean")
+    _assert_within(vn["running_mean_sq"], o64["vn_mean_sq"], spread["vn_mean_sq"], "vn mean_sq")
+    for key in ("value_loss", "policy_loss", "dist_entropy", "actor_grad_norm", "critic_grad_norm"):
+        _assert_within(info[key], o64[key], spread[key], key)
+        ref_err = abs(float(fx["info." + key]) - float(o64[key]))
+        assert abs(info[key] - float(fx["info." + key])) <= K_FP32 * spread[key] + ref_err, key
     np.testing.assert_allclose(info["ratio"], float(fx["info.ratio"]), rtol=1e-5)
 
 
@@ -260,8 +345,8 @@ def test_cfg3_scale_rollout_and_epoch_gradients_vs_oracle():
       driven with the stored actions; log-probs, values and next hiddens vs ``om.get_actions`` from the
       device's stored input hiddens (rtol 1e-5 atol 2e-6); hiddens zeroed where the env finished;
     * GAE + ValueNorm (shared_buffer.py:131-157) vs ``om.compute_returns`` (rtol 1e-5 atol 1e-5);
-    * PPO epoch 0 (ramppo_network.py:103-209): every gradient of actor and critic vs the oracle's
-      autograd on the full recurrent minibatch, |g - g_ref| <= 2e-3 max|g_ref| + 2e-3 |g_ref|."""
+    * PPO epoch 0 (ramppo_network.py:103-209): every gradient of actor and critic within K_FP32 fp32 spreads
+      (module docstring) of the f64 oracle's autograd on the full recurrent minibatch."""
     import ctypes
     from minimarl._lib import lib
     from minimarl.env import VecEnv
@@ -313,16 +398,11 @@ def test_cfg3_scale_rollout_and_epoch_gradients_vs_oracle():
     assert lib().mm_mappo_vn_update(tr.vn.data_ptr(), tr.stats.data_ptr(), 0.99999, None) == 0
     tr.gradients(b)
     torch.cuda.synchronize()
-    rec = []
-    om.ppo_train(PA, PC, data, om.ValueNorm(*vn0), 1, L, record=rec)
-    for n, (net, tag) in enumerate(((p.actor, "ga"), (p.critic, "gc"))):
-        nrm = rec[0]["na" if n == 0 else "nc"]
-        coef = min(1.0, 0.5 / (nrm + 1e-6))
+    g64, spread = _fp32_spread(lambda dt, pm: _unclipped_grads(_ppo_oracle(PA, PC, data, vn0, 1, L, dt, pm)[0]),
+                               T * EN // L)
+    for n, net in enumerate((p.actor, p.critic)):
         for k in om.NET_KEYS:
-            g = net.view(k, tr.grad[n]).cpu().numpy()
-            ref = rec[0][tag][k].numpy() / coef
-            np.testing.assert_array_less(np.abs(g - ref), 2e-3 * np.abs(ref).max() + 2e-3 * np.abs(ref) + 1e-9,
-                                         err_msg=f"net {n} {k}")
+            _assert_within(net.view(k, tr.grad[n]).cpu().numpy(), g64[(n, k)], spread[(n, k)], f"net {n} {k}")
 
 
 @pytest.mark.parametrize("L", [5, 10, 1])
@@ -395,9 +475,9 @@ def test_data_parallel_hooks_match_single_replica():
 def test_full_train_15_epochs_vs_oracle_at_scale():
     """R_MAPPO.train as benched (15 PPO epochs, one full-batch minibatch each, ValueNorm updated per epoch,
     advantages normalised once, clip 0.5 + Adam per net; ramppo_network.py:211-287) at 128 envs x 8 agents x
-    T = 40 (the golden covers E = 4, N = 2, T = 10 only): post-train parameters vs ``om.ppo_train`` on the same
-    rollout. Coordinates whose epoch-0 gradient is significant (> 1e-3 of the tensor's max) within 5e-5;
-    every coordinate within 15 epochs x 2 lr (Adam steps of near-zero gradients follow rounding noise)."""
+    T = 40 (the golden covers E = 4, N = 2, T = 10 only): post-train parameters and ValueNorm state within K_FP32
+    fp32 spreads (module docstring; over 15 epochs the spread carries Adam's sign-flip steps of near-zero
+    gradients) of the f64 oracle on the same rollout."""
     from minimarl.env import VecEnv
     from minimarl.mappo import MappoPolicy, MappoRunner
     E, N, T, L, EP = 128, 8, 40, 5, 15
@@ -414,17 +494,11 @@ def test_full_train_15_epochs_vs_oracle_at_scale():
     data = _ref_layout(r.buf, E, N)
     r.train()
     torch.cuda.synchronize()
-    rec = []
-    PA2, PC2, vn2 = om.ppo_train(PA, PC, data, om.ValueNorm(*vn0), EP, L, record=rec)
-    lr = 1e-4
-    for n, (net, ref, tag) in enumerate(((p.actor, PA2, "ga"), (p.critic, PC2, "gc"))):
+    o64, spread = _fp32_spread(lambda dt, pm: _train_outputs(*_ppo_oracle(PA, PC, data, vn0, EP, L, dt, pm)),
+                               T * E * N // L)
+    for net, kind in ((p.actor, "actor"), (p.critic, "critic")):
         for k in om.NET_KEYS:
-            got = net.view(k).detach().cpu().numpy()
-            want = ref[k].detach().numpy()
-            g = np.abs(rec[0][tag][k].numpy())
-            sel = g > 1e-3 * g.max()
-            np.testing.assert_allclose(got[sel], want[sel], atol=5e-5, err_msg=f"net {n} {k}")
-            np.testing.assert_allclose(got, want, atol=2 * EP * lr, err_msg=f"net {n} {k} (all)")
+            _assert_within(net.view(k).detach().cpu().numpy(), o64[(kind, k)], spread[(kind, k)], f"{kind} {k}")
     vn = r.trainer.value_normalizer_state()
-    np.testing.assert_allclose(vn["running_mean"], vn2.m.numpy(), rtol=1e-5, atol=1e-6)
-    np.testing.assert_allclose(vn["running_mean_sq"], vn2.msq.numpy(), rtol=1e-5, atol=1e-6)
+    _assert_within(vn["running_mean"], o64["vn_mean"], spread["vn_mean"], "vn mean")
+    _assert_within(vn["running_mean_sq"], o64["vn_mean_sq"], spread["vn_mean_sq"], "vn mean_sq")

@@ -119,6 +119,9 @@ def test_eps_greedy_device_rng_rate():
 
 @pytest.mark.parametrize("n_agents,full_obs", [(2, False), (2, True), (8, False), (3, False), (17, False), (5, True)])
 def test_env_bit_exact_vs_oracle(n_agents, full_obs):
+    """The restated ma_gym Checkers dynamics (oracle/env.py) bit for bit: obs, rewards, done, auto-reset obs and
+    the integer state (agent_pos, the stale agent_prev_pos, _full_obs codes, counters) over 230 steps of a
+    left-biased walk (fruit eaten, apples run out, agents block and erase each other)."""
     from minimarl.env import VecEnv
     E, steps = 300, 230
     spec = EnvSpec(n_agents, max_steps=100, full_observable=full_obs)
@@ -137,8 +140,9 @@ def test_env_bit_exact_vs_oracle(n_agents, full_obs):
         np.testing.assert_array_equal(done.cpu().numpy().astype(bool), odone)
         ora.reset_envs(odone)
         np.testing.assert_array_equal(cur.cpu().numpy(), ora.observe())
-    pos, grid, st, ap = env.get_state()
+    pos, prev, grid, st, ap = env.get_state()
     np.testing.assert_array_equal(pos, ora.pos)
+    np.testing.assert_array_equal(prev, ora.prev)
     np.testing.assert_array_equal(grid, ora.grid)
     np.testing.assert_array_equal(st, ora.steps)
     np.testing.assert_array_equal(ap, ora.apples)
@@ -262,6 +266,36 @@ def test_per_update_flags_out_of_range_nodes(cap):
     dev.check_errors()                           # in-range only: no error
 
 
+def test_env_stale_prev_erase_scenario():
+    """ma_gym's stale agent_prev_pos (oracle/env.py): agent 1 leaves (1,6) for (1,7), agent 0 moves into (1,6);
+    in the same step agent 1's view update (its stale prev is (1,6)) writes empty there, so agent 0 vanishes
+    from _full_obs and from every observation (its own centre cell included) while both stay put. Scripted in
+    env 0 on the device env and the oracle, random actions in the other envs."""
+    from minimarl.env import VecEnv
+    E = 64
+    spec = EnvSpec(2, max_steps=100, full_observable=True)
+    ora = VecEnvOracle(spec, E)
+    env = VecEnv(E, 2, 100, -0.01, True, device=DEV)
+    env.reset()
+    rng = np.random.default_rng(8)
+    script = [(4, 2), (4, 3), (0, 4), (4, 4), (4, 4)]
+    for a_env0 in script:
+        a = rng.integers(0, 5, (E, 2)).astype(np.int32)
+        a[0] = a_env0
+        nxt, rew, done, cur = env.step(torch.tensor(a), autoreset=True)
+        onxt, orew, odone = ora.step(a)
+        np.testing.assert_array_equal(nxt.cpu().numpy(), onxt)
+        np.testing.assert_array_equal(rew.cpu().numpy(), orew)
+        ora.reset_envs(odone)
+    assert tuple(ora.pos[0, 0]) == (1, 6) and tuple(ora.pos[0, 1]) == (1, 7) and ora.grid[0, 1, 6] == 0
+    centre = 2 + 4 * 5                                    # agent 0's own cell, channel "A1"
+    assert onxt[0, 0, centre + 2] == 0.0
+    pos, prev, grid, _, _ = env.get_state()
+    np.testing.assert_array_equal(pos, ora.pos)
+    np.testing.assert_array_equal(prev, ora.prev)
+    np.testing.assert_array_equal(grid, ora.grid)
+
+
 def test_rollout_engine_end_to_end_vs_oracle():
     """Engine transitions (store contents), TD chunk priorities and actions vs an oracle replay.
     In-chunk steps run the env kernel fused with the previous step's TD/store, so the store rows
@@ -379,75 +413,29 @@ def test_run_steps_exact_counts_match_eager():
 
 
 def _engine_state(e):
-    e.env_state_to_live()
     torch.cuda.synchronize()
     st = [e.store.obs, e.store.act, e.store.rew, e.store.done, e.h, e.ht, e.chunk_td, e.cur_row, e.staging,
-          e.per.tree(), e.per.slot_rows(), e.act, e.last_rew, e.last_done]
-    pos, grid, steps, apples = e.env.get_state()
-    return [x.clone() for x in st] + [torch.as_tensor(v) for v in (pos, grid, steps, apples)]
+          e.per.tree(), e.per.slot_rows(), e.act, e.last_rew, e.last_done, e.counter_dev]
+    return [x.clone() for x in st] + [torch.as_tensor(v) for v in e.env.get_state()]
 
 
-@pytest.mark.parametrize("dims,full", [((64, 64, 64), False), ((64, 32, 32), False), ((64, 32, 32), True)])
-def test_fused_step_matches_unfused(dims, full):
-    """The one-launch fused step (env + dual forward + TD(t-1), mm_rollout_step) is bit-identical to the
-    unfused launches: chunk store, hidden states, chunk priorities, PER tree / slot map, env state, through
-    chunk ends and PER eviction, with a flush_td mid-chunk."""
+def test_region_graphs_match_eager():
+    """bench.py's timed regions: ONE captured graph of exactly K steps from any graph phase (capture_region /
+    run_steps) is bit-identical to eager steps, through chunk ends, PER eviction and the env's auto-resets."""
     from minimarl.engine import RolloutEngine
-    f1, g, h = dims
-    N = 2 if full else 8
-    kw = dict(f1=f1, g=g, h=h, chunk=10, capacity=4096, seed=21, full_observable=full, device=DEV)
-    a = RolloutEngine(2048, N, fused=True, **kw)
-    b = RolloutEngine(2048, N, fused=False, **kw)
-    assert a.fused and not b.fused
-    for t in range(47):
+    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=256, seed=17, device=DEV)
+    a = RolloutEngine(64, 8, **kw)
+    b = RolloutEngine(64, 8, **kw)
+    for _ in range(57):
         a.step(0.3)
-        b.step(0.3)
-        if t == 23:
-            a.flush_td()
-            b.flush_td()
     a.flush_td()
+    b.run_steps(3, 0.3)
+    b.capture_region(20)
+    b.run_steps(20, 0.3)                      # the region graph (phase 3)
+    b.capture_region(14, start=b.t + 20)      # captured ahead for the phase two regions later
+    b.run_steps(20, 0.3)
+    b.run_steps(14, 0.3)
     b.flush_td()
+    assert a.t == b.t == 57 and len(a.per) == len(b.per) == 256
     for i, (x, y) in enumerate(zip(_engine_state(a), _engine_state(b))):
         assert torch.equal(x.cpu(), y.cpu()), i
-    assert a.t == b.t == 47 and len(a.per) == len(b.per) == 4096
-    assert int(a.rollout_err.item()) == 0
-
-
-def test_fused_step_skips_corrupt_staging_row():
-    """A staging row outside the chunk store is never written through (error word bit 0 instead)."""
-    from minimarl.engine import RolloutEngine
-    e = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=2, fused=True, device=DEV)
-    assert e.fused
-    e.step(0.1)
-    e.step(0.1)
-    torch.cuda.synchronize()
-    before = e.store.obs.clone()
-    good = e.staging[5].item()
-    e.staging[5] = e.store.rows + 12345
-    e.step(0.1)
-    torch.cuda.synchronize()
-    assert int(e.rollout_err.item()) & 1
-    after = e.store.obs
-    assert torch.equal(after[good], before[good])              # env 5's real row untouched this step
-    e.staging[5] = good
-    e.rollout_err.zero_()
-
-
-def test_fused_graph_replay_matches_eager():
-    """Fused-mode chunk graphs and single-step graphs replay bit-identically to eager fused steps."""
-    from minimarl.engine import RolloutEngine
-    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, fused=True, device=DEV)
-    a = RolloutEngine(2048, 8, **kw)
-    b = RolloutEngine(2048, 8, **kw)
-    assert a.fused and b.fused
-    for _ in range(33):
-        a.step(0.25)
-    a.flush_td()
-    b.run_steps(3, 0.25)
-    b.run_steps(20, 0.25)
-    b.run_steps(10, 0.25)
-    b.flush_td()
-    for i, (x, y) in enumerate(zip(_engine_state(a), _engine_state(b))):
-        assert torch.equal(x.cpu(), y.cpu()), i
-    assert int(b.step_dev[0]) == 33 and int(b.step_dev[1]) == 0
-    assert int(a.rollout_err.item()) == 0 and int(b.rollout_err.item()) == 0

@@ -12,6 +12,11 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mini-marl_amd"))
+if os.environ.get("MB_SPIN") == "1":
+    # hipDeviceScheduleSpin before the runtime creates its context: synchronize spin-waits for completion
+    import ctypes
+    _hip = ctypes.CDLL("libamdhip64.so")
+    assert _hip.hipSetDeviceFlags(ctypes.c_uint(1)) == 0
 import torch  # noqa: E402
 from minimarl.engine import RolloutEngine  # noqa: E402
 
