@@ -464,15 +464,16 @@ int mm_mappo_fwd(const mm_mappo_dims* d, const mm_mappo_fwd_args* a, mm_stream_t
 /* Loss seeds + chunked BPTT of both nets (after a TRAIN forward of the same data). */
 int mm_mappo_bwd(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, mm_stream_t s);
 /* Weight gradients of one net from mm_mappo_bwd's SoA operands into its flat gradient vector. */
-/* One PPO epoch's gradients of both nets in one pass (mappo_grad.hip; replaces mm_mappo_fwd TRAIN +
- * mm_mappo_bwd + mm_mappo_wgrad, ramppo_network.py:56-209): per tile of 32 L-step chunks the forward
- * is run from the stored chunk-start hiddens (h_actor / h_critic = rnn_states / rnn_states_critic
- * [T+1, EN, H], 16-byte aligned), recomputed step by step in reverse for the BPTT, and the weight
- * gradients are reduced on MFMA inside the kernel. Uses a's P, obs, mask, active, act, adv, old_logp,
- * old_value, returns, stats, loss_acc, coefficients, en, T, L (save / gsoa / rs ignored). Writes the
- * full flat gradient vectors. scratch: mm_mappo_grad_scratch_count(d, L) floats, 16-byte aligned.
- * H 32, A 5, D 47 | 94. */
-int64_t mm_mappo_grad_scratch_count(const mm_mappo_dims* d, int32_t L);
+/* One PPO epoch's gradients of both nets (mappo_grad.hip; replaces mm_mappo_fwd TRAIN + mm_mappo_bwd +
+ * mm_mappo_wgrad, ramppo_network.py:56-209) in two passes: the recurrent pass runs, per tile of 32 L-step
+ * chunks, the forward from the stored chunk-start hiddens (h_actor / h_critic = rnn_states /
+ * rnn_states_critic [T+1, EN, H], 16-byte aligned), recomputes it step by step in reverse for the BPTT and
+ * writes d loss / d x2 (the GRU input) of every row-step; the row-parallel MLP pass backpropagates those
+ * through the LN-MLP. Weight gradients are reduced on MFMA inside both. Uses a's P, obs, mask, active, act,
+ * adv, old_logp, old_value, returns, stats, loss_acc, coefficients, en, T, L (save / gsoa / rs ignored).
+ * Writes the full flat gradient vectors. scratch: mm_mappo_grad_scratch_count(d, L, T, en) floats, 16-byte
+ * aligned. H 32, A 5, D 47 | 94. */
+int64_t mm_mappo_grad_scratch_count(const mm_mappo_dims* d, int32_t L, int32_t T, int64_t en);
 int mm_mappo_grad(const mm_mappo_dims* d, const mm_mappo_bwd_args* a, const float* h_actor, const float* h_critic,
                   float* grad_actor, float* grad_critic, float* scratch, mm_stream_t s);
 /* R_MAPPOPolicy.evaluate_actions (rmappo_policy.py:101-136; RNNLayer's masked segments, rnn.py:24-80; the

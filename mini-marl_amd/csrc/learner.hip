@@ -2879,14 +2879,15 @@ int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t
   const size_t smem = sizeof(float) * mm::agent_bwd_seq_floats(d->h, d->n_actions, win);
   MM_REQUIRE(smem <= mm::kMixSeqLds, "agent_bwd_seq: W_hh too large for LDS");
   {
-    static bool attr = false;
-    if (!attr) {
+    // thread-safe one-time setup (a function-local static's initialiser runs once); the sizes are compile-time
+    static const int attr_rc = [&]() -> int {
       MM_HIP_CHECK(hipFuncSetAttribute((const void*)mm::agent_bwd_seq_kernel<32>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)mm::kMixSeqLds));
       MM_HIP_CHECK(hipFuncSetAttribute((const void*)mm::agent_bwd_seq_kernel<64>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)mm::kMixSeqLds));
-      attr = true;
-    }
+      return MM_OK;
+    }();
+    if (attr_rc != MM_OK) return attr_rc;
   }
   mm::AgentBwdArgs a = {P, oWq, oWhh, save, acts, dqa, done, dh, dgi, dgh, dq, B, d->n_agents, d->f1, d->g, d->h,
                         d->n_actions};

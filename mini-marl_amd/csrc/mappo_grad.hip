@@ -1,6 +1,5 @@
-// MAPPO training gradients on MFMA, one pass over the buffer per PPO epoch (replaces the per-thread
-// TRAIN forward + saves, the BPTT backward writing per-row gradient operands and the separate
-// weight-gradient reduction: no per-row arrays leave the chip except one hidden state per step).
+// MAPPO training gradients on MFMA, one PPO epoch in two row passes (replaces the per-thread TRAIN forward
+// + saves, the BPTT backward writing per-row gradient operands and the separate weight-gradient reduction).
 //
 // Reference (restated in oracle/mappo.py, pinned by tests/golden/mappo_*.npz):
 //   trunk  mappo/utils/algorithm_utils/mlp.py:31-55, rnn.py:24-29,79, act.py / distributions.py,
@@ -8,22 +7,28 @@
 //   loss   mappo/algorithms/ramppo_network.py:56-209 (ppo_update, cal_value_loss)
 //   chunks mappo/runner/shared/shared_buffer.py:318-427 (L steps, start hidden = stored hidden)
 //
-// Layout: one wave = one tile of 32 chunks. Activations live in the MFMA "act-frag" layout: lane
-// (c, h) = (lane & 31, lane >> 5) holds, for chunk c, the 16 features kperm(q, h) of a 32-wide
-// vector (q = 0..15), which is exactly the D layout of v_mfma_f32_32x32x2_f32 with features on M and
-// chunks on N and, with the same k permutation, the B operand of the next layer — forward and
-// backward layer chains need no data movement. Weight gradients dW[m][n] = sum_c delta[m][c] x[n][c]
-// put the chunk index on the MFMA k dimension: delta and x tiles are transposed through a per-wave
-// LDS tile (4 x ds_write_b128 + 16 x ds_read_b32 per lane), and the same transposed reads give the
-// bias and LayerNorm column sums. Each wave keeps its weight-gradient accumulators in registers
-// across all its tiles; a block reduces its 4 waves in LDS and writes one partial; a second kernel
-// sums the partials in a fixed order (deterministic).
+// Layout: one wave = one tile of 32 rows (chunks in the recurrent pass, row-steps in the MLP pass).
+// Activations live in the MFMA "act-frag" layout: lane (c, h) = (lane & 31, lane >> 5) holds, for row c,
+// the 16 features kperm(q, h) of a 32-wide vector (q = 0..15), which is exactly the D layout of
+// v_mfma_f32_32x32x2_f32 with features on M and rows on N and, with the same k permutation, the B operand of
+// the next layer — forward and backward layer chains need no data movement. Weight gradients
+// dW[m][n] = sum_c delta[m][c] x[n][c] put the row index on the MFMA k dimension: delta and x tiles are
+// transposed through a per-wave LDS tile (4 x ds_write_b128 + 16 x ds_read_b32 per lane), and the same
+// transposed reads give the bias and LayerNorm column sums. Each wave keeps its weight-gradient
+// accumulators in registers across all its tiles; a block reduces its waves in LDS in a fixed order and
+// writes one partial; a third kernel sums every partial of both passes in a fixed order (deterministic).
 //
-// Per tile: pass 1 runs the trunk forward over the L steps from the stored chunk-start hidden and
-// keeps the L input hiddens in a per-wave global scratch (L2-resident, reused across tiles); pass 2
-// walks the steps backwards, recomputes each step's forward from its input hidden and runs the
-// backward. Weights: the net's matrices are staged once per block into LDS with padded row pitches
-// (16-byte A-fragment reads) plus transposed copies of W_ih / W_hh for the backward data chain.
+// Pass G (mappo_grad_gru_kernel, per tile of 32 L-step chunks): step 1 runs the trunk forward over the L
+// steps from the stored chunk-start hidden and parks the L input hiddens and GRU inputs x2 in a per-wave
+// global scratch (reused across the wave's tiles); step 2 walks the steps backwards, recomputes each step's
+// GRU gates from its parked input hidden and x2, seeds the PPO / Huber loss, runs the head, LN_r and GRU
+// backward, accumulates dW_ih, dW_hh, dWo and their biases / LN_r parameters, and writes the step's
+// gradient w.r.t. the GRU input x2 (dx2 = W_ih^T dgates, 32 floats per row-step) to HBM.
+// Pass M (mappo_grad_mlp_kernel, row-parallel, no recurrence): per tile of 32 row-steps it recomputes the
+// LN-MLP forward from the obs and backpropagates dx2 through LN2, L2, LN1, L1 and LN0, accumulating dW2,
+// dW1, b1, b2 and the three LayerNorms' parameters. Splitting the MLP backward out of the recurrent pass
+// keeps pass G's registers to its 7 accumulator tiles + the step's GRU state (no spills, 2 waves per SIMD)
+// and drops the parking of the MLP activations the single-pass kernel needed.
 #include "common.h"
 #include "minimarl.h"
 #include "trunk.h"
@@ -34,10 +39,14 @@ namespace mgr {
 constexpr int H = 32;          // hidden width this kernel is written for
 constexpr int TP = 36;         // pitch of a transpose tile row (one chunk)
 constexpr int TILE = 32 * TP;  // floats per transpose tile
-constexpr int NTW = 4;         // transpose tiles per wave
-constexpr int NWAVE = 4;       // waves per block (one block per CU: ~140 KB of LDS)
-constexpr int NB = 128;        // blocks per net
+constexpr int GW = 4;          // pass G: waves per block (1 per SIMD), one block per CU
+constexpr int GT = 2;          // pass G: transpose tiles per wave
+constexpr int MT = 4;          // pass M: transpose tiles per wave
+constexpr int NB = 128;        // blocks per net and pass
 
+// LDS image of a net (padded rows; transposed W_ih / W_hh for the backward data chain). Pass G stages all
+// of it (the recomputed forward needs the MLP too); pass M stages the leading MLP part only (up to W2) plus
+// the LayerNorm / bias vectors it reads, relocated right after W2 (MLP layout Geo::M*).
 template <int D, int O>
 struct Geo {
   static constexpr int DT = (D + 31) / 32, DPT = 32 * DT, P1 = DPT + 4, PW = 36, PT = 100;
@@ -45,7 +54,13 @@ struct Geo {
                        WhhT = WihT + 32 * PT, ln0w = WhhT + 32 * PT, ln0b = ln0w + DPT, b1 = ln0b + DPT,
                        ln1w = b1 + 32, ln1b = ln1w + 32, b2 = ln1b + 32, ln2w = b2 + 32, ln2b = ln2w + 32,
                        bih = ln2b + 32, bhh = bih + 96, lnrw = bhh + 96, lnrb = lnrw + 32, Wo = lnrb + 32,
-                       bo = Wo + 8 * 32, scr = bo + 8, total = scr + NWAVE * NTW * TILE;
+                       bo = Wo + 8 * 32, scr = bo + 8, total = scr + GW * GT * TILE;
+    // pass M image: W1, W2, then ln0w .. ln2b at MLN + (the same offsets relative to ln0w)
+  static constexpr int MLN = Wih, mscr = MLN + (bih - ln0w);
+  // pass M waves per block: 8 (2 per SIMD, no spills at D <= 64) where the image + 8 waves' transpose tiles fit
+  // the 160 KB of LDS; wider obs (DT = 3) run 4 waves with the full register file (no spills)
+  static constexpr int MW = (DT <= 2 && (mscr + 8 * MT * TILE) * 4 <= 160 * 1024) ? 8 : 4;
+  static constexpr int mtotal = mscr + MW * MT * TILE;
   static_assert(O <= 8, "head wider than 8 outputs");
 };
 
@@ -172,56 +187,67 @@ __device__ __forceinline__ void ln32_bwd(const float (&dy)[16], const float (&xh
   for (int q = 0; q < 16; ++q) dx[q] = rs * (dy[q] * w[kperm(q, h)] - sg - xh[q] * sgx);
 }
 
-// stage the net's flat MGeo parameters into the padded LDS image
+// value of LDS image offset e (< Geo::scr) from the net's flat MGeo parameters
 template <int D, int O>
-__device__ void stage(float* sm, const float* __restrict__ P) {
+__device__ __forceinline__ float stage_value(const float* __restrict__ P, int e) {
   using G = Geo<D, O>;
   using F = MGeo<D, H, O>;
-  for (int e = threadIdx.x; e < G::scr; e += blockDim.x) {
-    float v = 0.f;
-    if (e < G::W2) {
-      const int m = e / G::P1, k = e - m * G::P1;
-      if (k < D) v = P[F::W1 + m * F::Dp + k];
-    } else if (e < G::Wih) {
-      const int r = e - G::W2, m = r / G::PW, k = r - m * G::PW;
-      if (k < H) v = P[F::W2 + m * H + k];
-    } else if (e < G::Whh) {
-      const int r = e - G::Wih, m = r / G::PW, k = r - m * G::PW;
-      if (k < H) v = P[F::Wih + m * H + k];
-    } else if (e < G::WihT) {
-      const int r = e - G::Whh, m = r / G::PW, k = r - m * G::PW;
-      if (k < H) v = P[F::Whh + m * H + k];
-    } else if (e < G::WhhT) {
-      const int r = e - G::WihT, i = r / G::PT, j = r - i * G::PT;
-      if (j < 3 * H) v = P[F::Wih + j * H + i];
-    } else if (e < G::ln0w) {
-      const int r = e - G::WhhT, i = r / G::PT, j = r - i * G::PT;
-      if (j < 3 * H) v = P[F::Whh + j * H + i];
-    } else if (e < G::ln0b) {
-      const int k = e - G::ln0w;
-      if (k < D) v = P[F::ln0_w + k];
-    } else if (e < G::b1) {
-      const int k = e - G::ln0b;
-      if (k < D) v = P[F::ln0_b + k];
-    } else if (e < G::bih) {
-      const int r = e - G::b1, seg = r >> 5, i = r & 31;
-      const int src[6] = {F::b1, F::ln1_w, F::ln1_b, F::b2, F::ln2_w, F::ln2_b};
-      v = P[src[seg] + i];
-    } else if (e < G::lnrw) {
-      const int r = e - G::bih;
-      v = r < 96 ? P[F::bih + r] : P[F::bhh + r - 96];
-    } else if (e < G::Wo) {
-      const int r = e - G::lnrw;
-      v = r < 32 ? P[F::lnr_w + r] : P[F::lnr_b + r - 32];
-    } else if (e < G::bo) {
-      const int r = e - G::Wo, o = r >> 5, i = r & 31;
-      if (o < O) v = P[F::Wo + o * H + i];
-    } else {
-      const int o = e - G::bo;
-      if (o < O) v = P[F::bo + o];
-    }
-    sm[e] = v;
+  float v = 0.f;
+  if (e < G::W2) {
+    const int m = e / G::P1, k = e - m * G::P1;
+    if (k < D) v = P[F::W1 + m * F::Dp + k];
+  } else if (e < G::Wih) {
+    const int r = e - G::W2, m = r / G::PW, k = r - m * G::PW;
+    if (k < H) v = P[F::W2 + m * H + k];
+  } else if (e < G::Whh) {
+    const int r = e - G::Wih, m = r / G::PW, k = r - m * G::PW;
+    if (k < H) v = P[F::Wih + m * H + k];
+  } else if (e < G::WihT) {
+    const int r = e - G::Whh, m = r / G::PW, k = r - m * G::PW;
+    if (k < H) v = P[F::Whh + m * H + k];
+  } else if (e < G::WhhT) {
+    const int r = e - G::WihT, i = r / G::PT, j = r - i * G::PT;
+    if (j < 3 * H) v = P[F::Wih + j * H + i];
+  } else if (e < G::ln0w) {
+    const int r = e - G::WhhT, i = r / G::PT, j = r - i * G::PT;
+    if (j < 3 * H) v = P[F::Whh + j * H + i];
+  } else if (e < G::ln0b) {
+    const int k = e - G::ln0w;
+    if (k < D) v = P[F::ln0_w + k];
+  } else if (e < G::b1) {
+    const int k = e - G::ln0b;
+    if (k < D) v = P[F::ln0_b + k];
+  } else if (e < G::bih) {
+    const int r = e - G::b1, seg = r >> 5, i = r & 31;
+    const int src[6] = {F::b1, F::ln1_w, F::ln1_b, F::b2, F::ln2_w, F::ln2_b};
+    v = P[src[seg] + i];
+  } else if (e < G::lnrw) {
+    const int r = e - G::bih;
+    v = r < 96 ? P[F::bih + r] : P[F::bhh + r - 96];
+  } else if (e < G::Wo) {
+    const int r = e - G::lnrw;
+    v = r < 32 ? P[F::lnr_w + r] : P[F::lnr_b + r - 32];
+  } else if (e < G::bo) {
+    const int r = e - G::Wo, o = r >> 5, i = r & 31;
+    if (o < O) v = P[F::Wo + o * H + i];
+  } else {
+    const int o = e - G::bo;
+    if (o < O) v = P[F::bo + o];
   }
+  return v;
+}
+// pass G: the whole image
+template <int D, int O>
+__device__ void stage(float* sm, const float* __restrict__ P) {
+  for (int e = threadIdx.x; e < Geo<D, O>::scr; e += blockDim.x) sm[e] = stage_value<D, O>(P, e);
+  __syncthreads();
+}
+// pass M: W1, W2 and the MLP's LayerNorm / bias vectors (relocated to Geo::MLN)
+template <int D, int O>
+__device__ void stage_mlp(float* sm, const float* __restrict__ P) {
+  using G = Geo<D, O>;
+  for (int e = threadIdx.x; e < G::mscr; e += blockDim.x)
+    sm[e] = stage_value<D, O>(P, e < G::MLN ? e : e - G::MLN + G::ln0w);
   __syncthreads();
 }
 
@@ -259,14 +285,24 @@ __device__ __forceinline__ void ln0_stats(const float (&x)[DT][16], float& mu, f
   rs = 1.0f / sqrtf(xsum(d2) / (float)D + kLnEps);
 }
 
-// The trunk forward of one step up to the new hidden (LN0, L1, LN1, L2, LN2, GRU) in act-frag.
-template <int D, int O>
-struct Step {
-  using G = Geo<D, O>;
-  static constexpr int DT = G::DT;
-  float mu0, rs0, a1[16], mu1, rs1, a2[16], mu2, rs2, r[16], z[16], n[16], ghn[16], h2[16];
+// Offsets of the MLP's LayerNorm / bias vectors relative to ln0w (the same in both LDS images)
+template <int D>
+struct LnOff {
+  static constexpr int DPT = 32 * ((D + 31) / 32);
+  static constexpr int ln0w = 0, ln0b = DPT, b1 = 2 * DPT, ln1w = b1 + 32, ln1b = ln1w + 32, b2 = ln1b + 32,
+                       ln2w = b2 + 32, ln2b = ln2w + 32;
+};
 
-  __device__ __forceinline__ void run(const float* sm, const float* __restrict__ orow, const float (&hin)[16]) {
+// LN0 -> L1 -> ReLU -> LN1 -> L2 -> ReLU (-> LN2 statistics) of one row tile in act-frag. W1 / W2: the padded
+// LDS rows (pitches P1 / PW); lv: the LayerNorm / bias vectors (LnOff).
+template <int D, int O>
+struct Mlp {
+  using G = Geo<D, O>;
+  using LO = LnOff<D>;
+  static constexpr int DT = G::DT;
+  float mu0, rs0, a1[16], mu1, rs1, a2[16], mu2, rs2;
+
+  __device__ __forceinline__ void run(const float* W1, const float* W2, const float* lv, const float* __restrict__ orow) {
     const int h = lane_h();
     float x[DT][16];
     load_obs<D, DT>(orow, x);
@@ -279,30 +315,44 @@ struct Step {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int f = 32 * t + kperm(q, h);
-        f0[q] = (x[t][q] - mu0) * rs0 * sm[G::ln0w + f] + sm[G::ln0b + f];
+        f0[q] = (x[t][q] - mu0) * rs0 * lv[LO::ln0w + f] + lv[LO::ln0b + f];
       }
-      mm_rows<G::P1>(sm + G::W1 + 32 * t, f0, acc, kgroups(D - 32 * t));
+      mm_rows<G::P1>(W1 + 32 * t, f0, acc, kgroups(D - 32 * t));
     }
     float f[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) a1[q] = fmaxf(acc[q] + sm[G::b1 + kperm(q, h)], 0.f);
+    for (int q = 0; q < 16; ++q) a1[q] = fmaxf(acc[q] + lv[LO::b1 + kperm(q, h)], 0.f);
     ln32(a1, mu1, rs1);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) f[q] = (a1[q] - mu1) * rs1 * sm[G::ln1w + kperm(q, h)] + sm[G::ln1b + kperm(q, h)];
+    for (int q = 0; q < 16; ++q) f[q] = (a1[q] - mu1) * rs1 * lv[LO::ln1w + kperm(q, h)] + lv[LO::ln1b + kperm(q, h)];
     zero16(acc);
-    mm_rows<G::PW>(sm + G::W2, f, acc);
+    mm_rows<G::PW>(W2, f, acc);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) a2[q] = fmaxf(acc[q] + sm[G::b2 + kperm(q, h)], 0.f);
+    for (int q = 0; q < 16; ++q) a2[q] = fmaxf(acc[q] + lv[LO::b2 + kperm(q, h)], 0.f);
     ln32(a2, mu2, rs2);
+  }
+  // x2 = LN2(a2)
+  __device__ __forceinline__ void x2(const float* lv, float (&o)[16]) const {
+    const int h = lane_h();
 #pragma unroll
-    for (int q = 0; q < 16; ++q) f[q] = (a2[q] - mu2) * rs2 * sm[G::ln2w + kperm(q, h)] + sm[G::ln2b + kperm(q, h)];
-    // GRU, torch gate order r, z, n; h' = n + z (h - n)
+    for (int q = 0; q < 16; ++q) o[q] = (a2[q] - mu2) * rs2 * lv[LO::ln2w + kperm(q, h)] + lv[LO::ln2b + kperm(q, h)];
+  }
+};
+
+// GRU cell (torch gate order r, z, n; h' = n + z (h - n)) of one row tile from x2 and the input hidden
+template <int D, int O>
+struct Gru {
+  using G = Geo<D, O>;
+  float r[16], z[16], n[16], ghn[16], h2[16];
+
+  __device__ __forceinline__ void run(const float* sm, const float (&x2)[16], const float (&hin)[16]) {
+    const int h = lane_h();
     f32x16 ai, ah;
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
       zero16(ai);
       zero16(ah);
-      mm_rows<G::PW>(sm + G::Wih + 32 * g * G::PW, f, ai);
+      mm_rows<G::PW>(sm + G::Wih + 32 * g * G::PW, x2, ai);
       mm_rows<G::PW>(sm + G::Whh + 32 * g * G::PW, hin, ah);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -324,52 +374,66 @@ struct Step {
 struct GradArgs {
   mm_mappo_bwd_args a;
   const float* h_in[2];
-  float* hseq;      // [2][NB * NWAVE][L + 2][64 * 16]: input hidden per step, then a1 / a2 of the step
-  float* partial;   // [2][NB][pstride]
+  float* hseq;      // [2][NB * GW][2][L][64 * 16]: input hidden and GRU input x2 of every step of the wave's tile
+  float* dx2;       // [2][T * EN][32]: d loss / d x2 of every row-step (pass G -> pass M)
+  float* partial;   // [2][2 NB][pstride]: pass G blocks, then pass M blocks
   int64_t pstride;
 };
 
+// store an act-frag vector as row `row` of a [rows][32] array: features 8 j + 4 h + 0..3 are 4 consecutive floats
+__device__ __forceinline__ void st_row32(float* base, int64_t row, const float (&v)[16]) {
+  float* p = base + row * 32 + 4 * lane_h();
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    *reinterpret_cast<float4*>(p + 8 * j) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+}
+__device__ __forceinline__ void ld_row32(const float* base, int64_t row, float (&v)[16]) {
+  const float* p = base + row * 32 + 4 * lane_h();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float4 t = *reinterpret_cast<const float4*>(p + 8 * j);
+    v[4 * j] = t.x;
+    v[4 * j + 1] = t.y;
+    v[4 * j + 2] = t.z;
+    v[4 * j + 3] = t.w;
+  }
+}
+
+// ---------------------------------------------------------------- pass G: recurrent part
 template <int D, int A, int O>
-__device__ void grad_body(const GradArgs& k, int net, float* sm) {
+__device__ void gru_body(const GradArgs& k, int net, float* sm) {
   using G = Geo<D, O>;
   using F = MGeo<D, H, O>;
-  constexpr int DT = G::DT;
   const mm_mappo_bwd_args& a = k.a;
   stage<D, O>(sm, a.P[net]);
   const int lane = (int)(threadIdx.x & 63), ci = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform: scalar loop control
-  float* S0 = sm + G::scr + w * NTW * TILE;
+  float* S0 = sm + G::scr + w * GT * TILE;
   float* S1 = S0 + TILE;
-  float* S2 = S1 + TILE;
-  float* S3 = S2 + TILE;
   const int L = a.L;
   const int64_t EN = a.en, nch = (int64_t)(a.T / L) * EN, ntile = (nch + 31) / 32;
-  const int wg = blockIdx.x * NWAVE + w, nwg = gridDim.x * NWAVE;
-  float* hs = k.hseq + ((int64_t)net * nwg + wg) * (L + 2) * 1024 + lane * 16;
+  const int wg = blockIdx.x * GW + w, nwg = gridDim.x * GW;
+  float* hs = k.hseq + ((int64_t)net * nwg + wg) * 2 * L * 1024 + lane * 16;   // input hiddens, then x2
+  float* xs = hs + L * 1024;
+  float* dx2o = k.dx2 + (int64_t)net * a.T * EN * 32;
   const float* __restrict__ hin0 = k.h_in[net];
   const float inv_m = 1.0f / a.stats[MM_MST_ACTIVE_SUM];
 
-  f32x16 aWih[3], aWhh[3], aW2, aW1[DT], aWo;
+  f32x16 aWih[3], aWhh[3], aWo;
 #pragma unroll
   for (int g = 0; g < 3; ++g) {
     zero16(aWih[g]);
     zero16(aWhh[g]);
   }
-  zero16(aW2);
   zero16(aWo);
-#pragma unroll
-  for (int t = 0; t < DT; ++t) zero16(aW1[t]);
-  float sbr = 0.f, sbz = 0.f, sbn = 0.f, sbhn = 0.f, sb2 = 0.f, sb1 = 0.f, sbo = 0.f;
-  float slrw = 0.f, slrb = 0.f, sl2w = 0.f, sl2b = 0.f, sl1w = 0.f, sl1b = 0.f, sl0w[DT], sl0b[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t) sl0w[t] = sl0b[t] = 0.f;
+  float sbr = 0.f, sbz = 0.f, sbn = 0.f, sbhn = 0.f, sbo = 0.f, slrw = 0.f, slrb = 0.f;
   float lsum0 = 0.f, lsum1 = 0.f, lsum2 = 0.f;
 
   for (int64_t tile = wg; tile < ntile; tile += nwg) {
     const int64_t c = tile * 32 + ci;
     const bool valid = c < nch;
     const int64_t cc = valid ? c : 0, kc = cc / EN, en = cc - kc * EN;
-    // ---- pass 1: forward over the chunk, input hidden of every step kept in the wave scratch
+    // ---- step 1: forward over the chunk, input hidden of every step kept in the wave scratch
     float hc[16];
     {
       const float* hp = hin0 + ((kc * L) * EN + en) * H + 4 * h;
@@ -387,40 +451,35 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
       const float m = a.mask[row];
 #pragma unroll
       for (int q = 0; q < 16; ++q) hc[q] *= m;
-      float4* hsl = reinterpret_cast<float4*>(hs + l * 1024);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) hsl[g] = make_float4(hc[4 * g], hc[4 * g + 1], hc[4 * g + 2], hc[4 * g + 3]);
+      st16(hs + l * 1024, hc);
+      const float* smo = sm + opaque0();
+      float x2[16];
+      {
+        Mlp<D, O> mp;
+        mp.run(smo + G::W1, smo + G::W2, smo + G::ln0w, a.obs + row * D);
+        mp.x2(smo + G::ln0w, x2);
+      }
+      st16(xs + l * 1024, x2);         // the GRU input of every step, for step 2 (no MLP recompute there)
       if (l + 1 < L) {
-        Step<D, O> st;
-        st.run(sm + opaque0(), a.obs + row * D, hc);
+        Gru<D, O> gr;
+        gr.run(smo, x2, hc);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) hc[q] = st.h2[q];
+        for (int q = 0; q < 16; ++q) hc[q] = gr.h2[q];
       }
     }
-    // ---- pass 2: backward over the steps, each step's forward recomputed from its input hidden
+    // ---- step 2: backward over the steps, each step's forward recomputed from its input hidden
     float dhn[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) dhn[q] = 0.f;
     for (int l = L - 1; l >= 0; --l) {
       const int64_t row = (kc * L + l) * EN + en;
-      float hin[16];
-      ld16(hs + l * 1024, hin);
-      Step<D, O> st;
-      st.run(sm + opaque0(), a.obs + row * D, hin);
       const float* smb = sm + opaque0();
-      const float mu0 = st.mu0, rs0 = st.rs0, mu1 = st.mu1, rs1 = st.rs1, mu2 = st.mu2, rs2 = st.rs2;
-      // a1 / a2 are needed again only by the LN2 / LN1 backward: parked in the wave scratch (L2) so
-      // the GRU backward has the registers; the GRU weight-gradient inputs x2 / hin go to tiles S0 / S1
-      st16(hs + L * 1024, st.a1);
-      st16(hs + (L + 1) * 1024, st.a2);
-      {
-        float x2[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-          x2[q] = (st.a2[q] - mu2) * rs2 * smb[G::ln2w + kperm(q, h)] + smb[G::ln2b + kperm(q, h)];
-        tput(S0, x2);
-        tput(S1, hin);
-      }
+      float hin[16], x2[16];
+      ld16(opaque_ptr(hs + l * 1024), hin);
+      ld16(opaque_ptr(xs + l * 1024), x2);
+      __builtin_amdgcn_sched_barrier(0);
+      Gru<D, O> st;
+      st.run(smb, x2, hin);
       // head: y = LN_r(h2); out = Wo y + bo
       float mur, rsr, xr[16], y[16];
       ln32(st.h2, mur, rsr);
@@ -512,12 +571,12 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
           v[q] = d;
           dy[q] = s;
         }
-        tput(S2, v);
-        tput(S3, y);
+        tput(S0, v);
+        tput(S1, y);
         wave_fence();
         float At[16], Bt[16];
-        tget(S2, At);
-        tget(S3, Bt);
+        tget(S0, At);
+        tget(S1, Bt);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
           acc_mfma(aWo, At[s], Bt[s]);
@@ -526,11 +585,11 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
         wave_fence();
 #pragma unroll
         for (int q = 0; q < 16; ++q) v[q] = dy[q] * xr[q];
-        tput(S2, v);
-        tput(S3, dy);
+        tput(S0, v);
+        tput(S1, dy);
         wave_fence();
-        slrw += tsum(S2);
-        slrb += tsum(S3);
+        slrw += tsum(S0);
+        slrb += tsum(S1);
         wave_fence();
       }
       // LN_r backward -> d h2 (+ the gradient carried from the next step)
@@ -550,11 +609,20 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
         dghn[q] = dpn[q] * r;
         dhn[q] = d * z;
       }
-      f32x16 dx2;
-      zero16(dx2);
-      mm_rows<G::PT>(smb + G::WihT, dgr, dx2);
-      mm_rows<G::PT>(smb + G::WihT + 32, dgz, dx2);
-      mm_rows<G::PT>(smb + G::WihT + 64, dpn, dx2);
+      {
+        // d x2 = W_ih^T dgates -> the MLP pass
+        f32x16 dx2;
+        zero16(dx2);
+        mm_rows<G::PT>(smb + G::WihT, dgr, dx2);
+        mm_rows<G::PT>(smb + G::WihT + 32, dgz, dx2);
+        mm_rows<G::PT>(smb + G::WihT + 64, dpn, dx2);
+        if (valid) {
+          float v[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] = dx2[q];
+          st_row32(dx2o, row, v);
+        }
+      }
       {
         f32x16 dhh;
         zero16(dhh);
@@ -565,158 +633,49 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) dhn[q] = (dhn[q] + dhh[q]) * mk;
       }
-      // GRU weight gradients: dW_ih += dg x2^T, dW_hh += dgh hin^T (x2 in S0, hin in S1), biases
-      tput(S2, dgr);
-      tput(S3, dgz);
-      wave_fence();
-#pragma unroll
-      for (int s0 = 0; s0 < 16; s0 += 4) {
-        float X[4], Hh[4], R[4], Z[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int off = h * TP + ci + 2 * (s0 + j) * TP;
-          X[j] = S0[off];
-          Hh[j] = S1[off];
-          R[j] = S2[off];
-          Z[j] = S3[off];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc_mfma(aWih[0], R[j], X[j]);
-          acc_mfma(aWhh[0], R[j], Hh[j]);
-          acc_mfma(aWih[1], Z[j], X[j]);
-          acc_mfma(aWhh[1], Z[j], Hh[j]);
-          sbr += R[j];
-          sbz += Z[j];
-        }
-      }
-      wave_fence();
-      tput(S2, dpn);
-      tput(S3, dghn);
-      wave_fence();
-#pragma unroll
-      for (int s0 = 0; s0 < 16; s0 += 4) {
-        float X[4], Hh[4], Nn[4], Nh[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int off = h * TP + ci + 2 * (s0 + j) * TP;
-          X[j] = S0[off];
-          Hh[j] = S1[off];
-          Nn[j] = S2[off];
-          Nh[j] = S3[off];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc_mfma(aWih[2], Nn[j], X[j]);
-          acc_mfma(aWhh[2], Nh[j], Hh[j]);
-          sbn += Nn[j];
-          sbhn += Nh[j];
-        }
-      }
-      wave_fence();
-      // ---- LN2 backward (x2 = LN2(a2), a2 = relu(W2 f1 + b2))
-      float da[16], xh[16], tt[16];
+      // GRU weight gradients: dW_ih += dg x2^T, dW_hh += dgh hin^T, gate biases (two transpose tiles)
       {
-        float av[16], dxv[16];
-        ld16(opaque_ptr(hs + (L + 1) * 1024), av);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          xh[q] = (av[q] - mu2) * rs2;
-          dxv[q] = dx2[q];
-        }
-        ln32_bwd(dxv, xh, rs2, smb + G::ln2w, da);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          tt[q] = dxv[q] * xh[q];
-          da[q] = av[q] > 0.f ? da[q] : 0.f;
-        }
-        tput(S2, tt);
-        tput(S3, dxv);
-      }
-      // dW2 += da2 f1^T, db2 (f1 = LN1(a1))
-      float a1v[16];
-      ld16(opaque_ptr(hs + L * 1024), a1v);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        xh[q] = (a1v[q] - mu1) * rs1;
-        tt[q] = xh[q] * smb[G::ln1w + kperm(q, h)] + smb[G::ln1b + kperm(q, h)];
-      }
-      tput(S0, da);
-      tput(S1, tt);
-      wave_fence();
-      sl2w += tsum(S2);
-      sl2b += tsum(S3);
-      {
-        float At[16], Bt[16];
-        tget(S0, At);
-        tget(S1, Bt);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          acc_mfma(aW2, At[s], Bt[s]);
-          sb2 += At[s];
-        }
-      }
-      wave_fence();
-      // ---- LN1 backward: dx1 = W2^T da2
-      {
-        f32x16 acc;
-        zero16(acc);
-        mm_cols<G::PW>(smb + G::W2, da, acc);
-        float dxv[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) dxv[q] = acc[q];
-        ln32_bwd(dxv, xh, rs1, smb + G::ln1w, da);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          tt[q] = dxv[q] * xh[q];
-          da[q] = a1v[q] > 0.f ? da[q] : 0.f;
-        }
-        tput(S2, tt);
-        tput(S3, dxv);
-        tput(S0, da);
+        float XT[16], HT[16];
+        tput(S0, x2);
+        tput(S1, hin);
         wave_fence();
-        sl1w += tsum(S2);
-        sl1b += tsum(S3);
+        tget(S0, XT);
+        tget(S1, HT);
         wave_fence();
-      }
-      // ---- L1 / LN0: dW1 += da1 f0^T, db1, df0 = W1^T da1 -> LN0 parameter gradients
-      {
-        float x[DT][16];
-        load_obs<D, DT>(a.obs + row * D, x);
-        float At[16];
-        tget(S0, At);
+        tput(S0, dgr);
+        tput(S1, dgz);
+        wave_fence();
+        {
+          float R[16], Z[16];
+          tget(S0, R);
+          tget(S1, Z);
 #pragma unroll
-        for (int s = 0; s < 16; ++s) sb1 += At[s];
-#pragma unroll
-        for (int t = 0; t < DT; ++t) {
-          float x0[16], f0[16];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int f = 32 * t + kperm(q, h);
-            x0[q] = (x[t][q] - mu0) * rs0;
-            f0[q] = x0[q] * smb[G::ln0w + f] + smb[G::ln0b + f];
+          for (int s = 0; s < 16; ++s) {
+            acc_mfma(aWih[0], R[s], XT[s]);
+            acc_mfma(aWhh[0], R[s], HT[s]);
+            acc_mfma(aWih[1], Z[s], XT[s]);
+            acc_mfma(aWhh[1], Z[s], HT[s]);
+            sbr += R[s];
+            sbz += Z[s];
           }
-          tput(S1, f0);
-          f32x16 acc;
-          zero16(acc);
-          mm_cols<G::P1>(smb + G::W1 + 32 * t, da, acc);
-          float dfv[16];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            dfv[q] = acc[q];
-            tt[q] = acc[q] * x0[q];
-          }
-          tput(S2, tt);
-          tput(S3, dfv);
-          wave_fence();
-          float Bt[16];
-          tget(S1, Bt);
-#pragma unroll
-          for (int s = 0; s < 16; ++s) acc_mfma(aW1[t], At[s], Bt[s]);
-          sl0w[t] += tsum(S2);
-          sl0b[t] += tsum(S3);
-          wave_fence();
         }
+        wave_fence();
+        tput(S0, dpn);
+        tput(S1, dghn);
+        wave_fence();
+        {
+          float Nn[16], Nh[16];
+          tget(S0, Nn);
+          tget(S1, Nh);
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            acc_mfma(aWih[2], Nn[s], XT[s]);
+            acc_mfma(aWhh[2], Nh[s], HT[s]);
+            sbn += Nn[s];
+            sbhn += Nh[s];
+          }
+        }
+        wave_fence();
       }
     }
   }
@@ -740,7 +699,7 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
     }
   }
 
-  // ---- block reduction of the 4 waves (fixed order) into the flat gradient layout, one partial
+  // ---- block reduction of the waves (fixed order) into the flat gradient layout, one partial
   __syncthreads();
   float* red = sm;
   for (int e = threadIdx.x; e < F::total; e += blockDim.x) red[e] = 0.f;
@@ -748,11 +707,184 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
   sbz = xsum(sbz);
   sbn = xsum(sbn);
   sbhn = xsum(sbhn);
-  sb2 = xsum(sb2);
-  sb1 = xsum(sb1);
   sbo = xsum(sbo);
   slrw = xsum(slrw);
   slrb = xsum(slrb);
+  __syncthreads();
+  for (int ww = 0; ww < GW; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int mm = kperm(q, h);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          red[F::Wih + (32 * g + mm) * H + ci] += aWih[g][q];
+          red[F::Whh + (32 * g + mm) * H + ci] += aWhh[g][q];
+        }
+        if (mm < O) red[F::Wo + mm * H + ci] += aWo[q];
+      }
+      if (h == 0) {
+        red[F::bih + ci] += sbr;
+        red[F::bih + 32 + ci] += sbz;
+        red[F::bih + 64 + ci] += sbn;
+        red[F::bhh + ci] += sbr;
+        red[F::bhh + 32 + ci] += sbz;
+        red[F::bhh + 64 + ci] += sbhn;
+        red[F::lnr_w + ci] += slrw;
+        red[F::lnr_b + ci] += slrb;
+        if (ci < O) red[F::bo + ci] += sbo;
+      }
+    }
+    __syncthreads();
+  }
+  float* outp = k.partial + ((int64_t)net * 2 * NB + blockIdx.x) * k.pstride;
+  for (int e = threadIdx.x; e < F::total; e += blockDim.x) outp[e] = red[e];
+}
+
+// ---------------------------------------------------------------- pass M: LN-MLP backward, row-parallel
+template <int D, int O>
+__device__ void mlp_body(const GradArgs& k, int net, float* sm) {
+  using G = Geo<D, O>;
+  using F = MGeo<D, H, O>;
+  using LO = LnOff<D>;
+  constexpr int DT = G::DT;
+  const mm_mappo_bwd_args& a = k.a;
+  stage_mlp<D, O>(sm, a.P[net]);
+  const int lane = (int)(threadIdx.x & 63), ci = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  float* S0 = sm + G::mscr + w * MT * TILE;
+  float* S1 = S0 + TILE;
+  float* S2 = S1 + TILE;
+  float* S3 = S2 + TILE;
+  const int64_t R = (int64_t)a.T * a.en, ntile = (R + 31) / 32;
+  constexpr int MWV = G::MW;
+  const int wg = blockIdx.x * MWV + w, nwg = gridDim.x * MWV;
+  const float* dx2i = k.dx2 + (int64_t)net * R * 32;
+
+  f32x16 aW2, aW1[DT];
+  zero16(aW2);
+#pragma unroll
+  for (int t = 0; t < DT; ++t) zero16(aW1[t]);
+  float sb2 = 0.f, sb1 = 0.f, sl2w = 0.f, sl2b = 0.f, sl1w = 0.f, sl1b = 0.f, sl0w[DT], sl0b[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) sl0w[t] = sl0b[t] = 0.f;
+
+  for (int64_t tile = wg; tile < ntile; tile += nwg) {
+    const int64_t r = tile * 32 + ci;
+    const bool valid = r < R;
+    const int64_t row = valid ? r : R - 1;
+    const float* smb = sm + opaque0();
+    const float* lv = smb + G::MLN;
+    float dxv[16];
+    ld_row32(dx2i, row, dxv);
+    if (!valid) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dxv[q] = 0.f;
+    }
+    Mlp<D, O> mp;
+    mp.run(smb + G::W1, smb + G::W2, lv, a.obs + row * D);
+    // ---- LN2 backward (x2 = LN2(a2), a2 = relu(W2 f1 + b2))
+    float da[16], xh[16], tt[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) xh[q] = (mp.a2[q] - mp.mu2) * mp.rs2;
+    ln32_bwd(dxv, xh, mp.rs2, lv + LO::ln2w, da);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      tt[q] = dxv[q] * xh[q];
+      da[q] = mp.a2[q] > 0.f ? da[q] : 0.f;
+    }
+    tput(S2, tt);
+    tput(S3, dxv);
+    // dW2 += da2 f1^T, db2 (f1 = LN1(a1))
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      xh[q] = (mp.a1[q] - mp.mu1) * mp.rs1;
+      tt[q] = xh[q] * lv[LO::ln1w + kperm(q, h)] + lv[LO::ln1b + kperm(q, h)];
+    }
+    tput(S0, da);
+    tput(S1, tt);
+    wave_fence();
+    sl2w += tsum(S2);
+    sl2b += tsum(S3);
+    {
+      float At[16], Bt[16];
+      tget(S0, At);
+      tget(S1, Bt);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        acc_mfma(aW2, At[s], Bt[s]);
+        sb2 += At[s];
+      }
+    }
+    wave_fence();
+    // ---- LN1 backward: dx1 = W2^T da2
+    {
+      f32x16 acc;
+      zero16(acc);
+      mm_cols<G::PW>(smb + G::W2, da, acc);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dxv[q] = acc[q];
+      ln32_bwd(dxv, xh, mp.rs1, lv + LO::ln1w, da);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        tt[q] = dxv[q] * xh[q];
+        da[q] = mp.a1[q] > 0.f ? da[q] : 0.f;
+      }
+      tput(S2, tt);
+      tput(S3, dxv);
+      tput(S0, da);
+      wave_fence();
+      sl1w += tsum(S2);
+      sl1b += tsum(S3);
+      wave_fence();
+    }
+    // ---- L1 / LN0: dW1 += da1 f0^T, db1, df0 = W1^T da1 -> LN0 parameter gradients
+    {
+      float x[DT][16];
+      load_obs<D, DT>(a.obs + row * D, x);
+      float At[16];
+      tget(S0, At);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) sb1 += At[s];
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        float x0[16], f0[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int f = 32 * t + kperm(q, h);
+          x0[q] = (x[t][q] - mp.mu0) * mp.rs0;
+          f0[q] = x0[q] * lv[LO::ln0w + f] + lv[LO::ln0b + f];
+        }
+        tput(S1, f0);
+        f32x16 acc;
+        zero16(acc);
+        mm_cols<G::P1>(smb + G::W1 + 32 * t, da, acc);
+        float dfv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          dfv[q] = acc[q];
+          tt[q] = acc[q] * x0[q];
+        }
+        tput(S2, tt);
+        tput(S3, dfv);
+        wave_fence();
+        float Bt[16];
+        tget(S1, Bt);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc_mfma(aW1[t], At[s], Bt[s]);
+        sl0w[t] += tsum(S2);
+        sl0b[t] += tsum(S3);
+        wave_fence();
+      }
+    }
+  }
+
+  // ---- block reduction (fixed order), one partial per block
+  __syncthreads();
+  float* red = sm;
+  for (int e = threadIdx.x; e < F::total; e += blockDim.x) red[e] = 0.f;
+  sb2 = xsum(sb2);
+  sb1 = xsum(sb1);
   sl2w = xsum(sl2w);
   sl2b = xsum(sl2b);
   sl1w = xsum(sl1w);
@@ -763,33 +895,19 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
     sl0b[t] = xsum(sl0b[t]);
   }
   __syncthreads();
-  for (int ww = 0; ww < NWAVE; ++ww) {
+  for (int ww = 0; ww < MWV; ++ww) {
     if (w == ww) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int m = kperm(q, h);
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          red[F::Wih + (32 * g + m) * H + ci] += aWih[g][q];
-          red[F::Whh + (32 * g + m) * H + ci] += aWhh[g][q];
-        }
-        red[F::W2 + m * H + ci] += aW2[q];
+        const int mm = kperm(q, h);
+        red[F::W2 + mm * H + ci] += aW2[q];
 #pragma unroll
         for (int t = 0; t < DT; ++t)
-          if (32 * t + ci < D) red[F::W1 + m * F::Dp + 32 * t + ci] += aW1[t][q];
-        if (m < O) red[F::Wo + m * H + ci] += aWo[q];
+          if (32 * t + ci < D) red[F::W1 + mm * F::Dp + 32 * t + ci] += aW1[t][q];
       }
       if (h == 0) {
-        red[F::bih + ci] += sbr;
-        red[F::bih + 32 + ci] += sbz;
-        red[F::bih + 64 + ci] += sbn;
-        red[F::bhh + ci] += sbr;
-        red[F::bhh + 32 + ci] += sbz;
-        red[F::bhh + 64 + ci] += sbhn;
         red[F::b2 + ci] += sb2;
         red[F::b1 + ci] += sb1;
-        red[F::lnr_w + ci] += slrw;
-        red[F::lnr_b + ci] += slrb;
         red[F::ln2_w + ci] += sl2w;
         red[F::ln2_b + ci] += sl2b;
         red[F::ln1_w + ci] += sl1w;
@@ -800,25 +918,33 @@ __device__ void grad_body(const GradArgs& k, int net, float* sm) {
             red[F::ln0_w + 32 * t + ci] += sl0w[t];
             red[F::ln0_b + 32 * t + ci] += sl0b[t];
           }
-        if (ci < O) red[F::bo + ci] += sbo;
       }
     }
     __syncthreads();
   }
-  float* outp = k.partial + ((int64_t)net * gridDim.x + blockIdx.x) * k.pstride;
+  float* outp = k.partial + ((int64_t)net * 2 * NB + NB + blockIdx.x) * k.pstride;
   for (int e = threadIdx.x; e < F::total; e += blockDim.x) outp[e] = red[e];
 }
 
 template <int D, int A>
-__global__ __launch_bounds__(256, 1) void mappo_grad_kernel(GradArgs k) {
+__global__ __launch_bounds__(64 * GW, 1) void mappo_grad_gru_kernel(GradArgs k) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if (blockIdx.y == 0)
-    grad_body<D, A, A>(k, 0, sm);
+    gru_body<D, A, A>(k, 0, sm);
   else
-    grad_body<D, A, 1>(k, 1, sm);
+    gru_body<D, A, 1>(k, 1, sm);
 }
 
-// grad[p] = sum over blocks of partial[b][p], fixed order
+template <int D, int A>
+__global__ __launch_bounds__((64 * Geo<D, A>::MW), 1) void mappo_grad_mlp_kernel(GradArgs k) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (blockIdx.y == 0)
+    mlp_body<D, A>(k, 0, sm);
+  else
+    mlp_body<D, 1>(k, 1, sm);
+}
+
+// grad[p] = sum over the partials of both passes [b][p], fixed order
 __global__ __launch_bounds__(256) void mappo_grad_sum_kernel(const float* __restrict__ partial, int nb,
                                                              int64_t pstride, int n0, int n1, float* g0, float* g1) {
   const int net = blockIdx.y;
@@ -834,29 +960,40 @@ __global__ __launch_bounds__(256) void mappo_grad_sum_kernel(const float* __rest
 template <int D, int A>
 struct GradShape {
   static int64_t pstride() { return ((int64_t)MGeo<D, H, A>::total + 3) & ~3ll; }
-  static int64_t scratch(int L) { return 2ll * NB * NWAVE * (L + 2) * 1024 + 2ll * NB * pstride(); }
+  static int64_t hseq_count(int L) { return 2ll * NB * GW * 2 * L * 1024; }
+  static int64_t scratch(int L, int T, int64_t en) {
+    return hseq_count(L) + 2ll * T * en * 32 + 2ll * 2 * NB * pstride();
+  }
   static int run(const mm_mappo_bwd_args* a, const float* ha, const float* hc, float* ga, float* gc, float* scratch,
                  hipStream_t s) {
-    static bool attr = false;
-    constexpr size_t lds = (size_t)Geo<D, A>::total * 4;
-    static_assert(Geo<D, A>::total == Geo<D, 1>::total, "actor / critic LDS images differ");
-    if (!attr) {
-      MM_HIP_CHECK(hipFuncSetAttribute((const void*)mappo_grad_kernel<D, A>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds));
-      attr = true;
-    }
+    constexpr size_t lds_g = (size_t)Geo<D, A>::total * 4, lds_m = (size_t)Geo<D, A>::mtotal * 4;
+    static_assert(Geo<D, A>::total == Geo<D, 1>::total && Geo<D, A>::mtotal == Geo<D, 1>::mtotal,
+                  "actor / critic LDS images differ");
+    static_assert(Geo<D, A>::total * 4 <= 160 * 1024 && Geo<D, A>::mtotal * 4 <= 160 * 1024, "LDS budget");
+    // thread-safe one-time setup (a function-local static's initialiser runs once); the sizes are compile-time
+    static const int attr_rc = [&]() -> int {
+      MM_HIP_CHECK(hipFuncSetAttribute((const void*)mappo_grad_gru_kernel<D, A>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_g));
+      MM_HIP_CHECK(hipFuncSetAttribute((const void*)mappo_grad_mlp_kernel<D, A>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m));
+      return MM_OK;
+    }();
+    if (attr_rc != MM_OK) return attr_rc;
     GradArgs k = {};
     k.a = *a;
     k.h_in[0] = ha;
     k.h_in[1] = hc;
     k.hseq = scratch;
-    k.partial = scratch + 2ll * NB * NWAVE * (a->L + 2) * 1024;
+    k.dx2 = scratch + hseq_count(a->L);
+    k.partial = k.dx2 + 2ll * a->T * a->en * 32;
     k.pstride = pstride();
-    hipLaunchKernelGGL((mappo_grad_kernel<D, A>), dim3(NB, 2), dim3(64 * NWAVE), lds, s, k);
+    hipLaunchKernelGGL((mappo_grad_gru_kernel<D, A>), dim3(NB, 2), dim3(64 * GW), lds_g, s, k);
+    MM_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((mappo_grad_mlp_kernel<D, A>), dim3(NB, 2), dim3(64 * Geo<D, A>::MW), lds_m, s, k);
     MM_HIP_CHECK(hipGetLastError());
     const int n0 = MGeo<D, H, A>::total, n1 = MGeo<D, H, 1>::total;
-    hipLaunchKernelGGL(mappo_grad_sum_kernel, dim3((n0 + 255) / 256, 2), dim3(256), 0, s, k.partial, NB, k.pstride, n0,
-                       n1, ga, gc);
+    hipLaunchKernelGGL(mappo_grad_sum_kernel, dim3((n0 + 255) / 256, 2), dim3(256), 0, s, k.partial, 2 * NB,
+                       k.pstride, n0, n1, ga, gc);
     MM_HIP_CHECK(hipGetLastError());
     return MM_OK;
   }
@@ -867,10 +1004,10 @@ struct GradShape {
 
 extern "C" {
 
-int64_t mm_mappo_grad_scratch_count(const mm_mappo_dims* d, int32_t L) {
-  if (!d || L <= 0 || d->hidden != 32 || d->n_actions != 5) return -1;
-  if (d->obs_dim == 47) return mm::mgr::GradShape<47, 5>::scratch(L);
-  if (d->obs_dim == 94) return mm::mgr::GradShape<94, 5>::scratch(L);
+int64_t mm_mappo_grad_scratch_count(const mm_mappo_dims* d, int32_t L, int32_t T, int64_t en) {
+  if (!d || L <= 0 || T <= 0 || en <= 0 || d->hidden != 32 || d->n_actions != 5) return -1;
+  if (d->obs_dim == 47) return mm::mgr::GradShape<47, 5>::scratch(L, T, en);
+  if (d->obs_dim == 94) return mm::mgr::GradShape<94, 5>::scratch(L, T, en);
   return -1;
 }
 

@@ -26,6 +26,15 @@
 #include "minimarl.h"
 
 namespace mm {
+
+// two consecutive doubles of the sum tree's leaf row: leaves = tree + (cap - 1) is only 8-byte aligned for a
+// power-of-two capacity, so the pair is copied (well-defined at 8-byte alignment; still one 16-byte load)
+__device__ __forceinline__ double2 ld_double2(const double* p) {
+  double2 v;
+  __builtin_memcpy(&v, p, sizeof(v));
+  return v;
+}
+
 // Mutable PER scalars live in HBM so that inserts / samples / updates are graph-replayable
 // (the host keeps an identical mirror for queries).
 struct PerDev {
@@ -233,7 +242,7 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
     uint32_t kp[VPT / 2];
 #pragma unroll
     for (int i = 0; i < VPT; i += 2) {
-      const double2 v = *reinterpret_cast<const double2*>(leaves + s0 + i);
+      const double2 v = ld_double2(leaves + s0 + i);
       const uint32_t a = (s0 + i < n_data) ? (uint32_t)((uint64_t)__double_as_longlong(v.x) >> 48) : 0xffffu;
       const uint32_t b = (s0 + i + 1 < n_data) ? (uint32_t)((uint64_t)__double_as_longlong(v.y) >> 48) : 0xffffu;
       kp[i / 2] = a | (b << 16);
@@ -406,7 +415,7 @@ __global__ __launch_bounds__(PT) void per_add_fast_kernel(double* tree, int64_t*
     const int64_t base = lvl_nodes - 1 + (int64_t)t * (VPT / 2);
 #pragma unroll
     for (int i = 0; i < VPT / 2; ++i) {
-      const double2 x = *reinterpret_cast<const double2*>(leaves + s0 + 2 * i);
+      const double2 x = ld_double2(leaves + s0 + 2 * i);
       v[i] = x.x + x.y;
       tree[base + i] = v[i];
       if ((i & 7) == 7) asm volatile("" ::: "memory");  // bound the loads in flight (VGPRs)
@@ -986,8 +995,8 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   const int64_t s0 = base + threadIdx.x * MB_VPT;
   double x[MB_VPT];
   {
-    const double2 a = *reinterpret_cast<const double2*>(leaves + s0);
-    const double2 b = *reinterpret_cast<const double2*>(leaves + s0 + 2);
+    const double2 a = ld_double2(leaves + s0);
+    const double2 b = ld_double2(leaves + s0 + 2);
     x[0] = a.x;
     x[1] = a.y;
     x[2] = b.x;

@@ -274,7 +274,7 @@ _SIGS += [
                                           c_vp, c_vp]),
     ("mm_mappo_wgrad_partial_count", c_i64, [_MD, c_i64]),
     ("mm_mappo_wgrad", c_i32, [_MD, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp]),
-    ("mm_mappo_grad_scratch_count", c_i64, [_MD, c_i32]),
+    ("mm_mappo_grad_scratch_count", c_i64, [_MD, c_i32, c_i32, c_i64]),
     ("mm_mappo_grad", c_i32, [_MD, ctypes.POINTER(MappoBwdArgs), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_mappo_gae", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i64, c_f32, c_f32, c_vp]),
     ("mm_mappo_adv_stats", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),

@@ -177,16 +177,17 @@ class _LearnerAdapter:
         self._learner, self._key = None, None
 
     def _bind(self, beh, tgt, mix, tmix, optimizer):
-        """The QLearner for these nets and optimizer hyper-parameters. A change of any net or of lr / betas /
-        eps rebuilds it: the old learner releases its nets first, and when the trained nets are the same
-        objects the Adam moments carry over (the reference's optimizer keeps its state across calls)."""
+        """The QLearner for these nets and this optimizer. A change of any net, of the optimizer object or of its
+        lr / betas / eps rebuilds it: the old learner releases its nets first. The Adam moments carry over only
+        when the SAME optimizer object trains the same nets with changed hyper-parameters (the reference's
+        torch optimizer keeps its state across calls; a new optimizer object starts empty)."""
         lr, betas, eps = _hyper(optimizer)
-        key = tuple(id(x) for x in (beh, tgt, mix, tmix)) + (lr, tuple(betas), eps)
+        key = tuple(id(x) for x in (beh, tgt, mix, tmix, optimizer)) + (lr, tuple(betas), eps)
         if self._learner is None or key != self._key:
             adam = None
             if self._learner is not None:
                 state = self._learner.release()
-                if self._key[0] == key[0] and self._key[2] == key[2]:
+                if self._key[0] == key[0] and self._key[2] == key[2] and self._key[4] == key[4]:
                     adam = state
             self._learner = QLearner(beh.net, tgt.net, mix.mixer if mix is not None else None,
                                      tmix.mixer if tmix is not None else None, batch=self.batch_size,

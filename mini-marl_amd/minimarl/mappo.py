@@ -230,7 +230,7 @@ class MappoTrainer:
         self.rows = self.T * self.EN
         self.rs = _rs(self.rows)
         if self.fused:
-            n_scr = int(L_.mm_mappo_grad_scratch_count(d, self.L))
+            n_scr = int(L_.mm_mappo_grad_scratch_count(d, self.L, self.T, self.EN))
             if n_scr <= 0:
                 raise RuntimeError("mappo_grad: unsupported dims for the fused gradient pass")
             self.gscr = torch.zeros(n_scr, device=dev)

@@ -138,18 +138,26 @@ class QTrainer:
         self.episode += 1
         return eps
 
+    def check_device_errors(self):
+        """Raise if a device-side sticky error bit is set (the PER's out-of-range priority-update nodes, skipped on
+        the device where the reference's tree write would raise); polled at the host syncs train() already has."""
+        self.eng.per.check_errors()
+
     def train(self, n_episodes, log=None):
-        """Run n_episodes training episodes; greedy tests every test_interval episodes (host sync)."""
+        """Run n_episodes training episodes; greedy tests every test_interval episodes (host sync); the device
+        error words are polled at every test and at the end."""
         for _ in range(int(n_episodes)):
             eps = self.train_episode()
             ep = self.episode - 1
             if self.evaluator is not None and (ep + 1) % self.cfg.test_interval == 0:
+                self.check_device_errors()
                 rec = self.test()
                 rec.update(episode=ep + 1, epsilon=eps, train_score=self.train_score(reset=True),
                            loss=float(self.learner.loss.item()), alpha=self.eng.per.alpha, beta=self.eng.per.beta)
                 self.history.append(rec)
                 if log is not None:
                     log(rec)
+        self.check_device_errors()
         return self.history
 
     # ------------------------------------------------------------------ scores
