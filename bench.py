@@ -694,25 +694,37 @@ def main():
         del n5, o5, h5, hq, l5, m5
         torch.cuda.empty_cache()
 
-    # roofline of the dominant kernel: the fused agent Q forward (one launch = target net on s'_t +
-    # behavior net on s_{t+1}: 2 nets x E x N agent-steps). At E >= 2048 it runs the fp16x3-split
-    # kernel: every fp32 product as 3 f16 MFMAs, so its MFMA ceiling for the network's fp32 FLOPs
-    # is the dense f16 peak / 3; the native f32-MFMA peak is reported beside it.
-    t_iso = time_kernel(eng.fused_forward)
-    # in its rollout context: graphs of K x (env + dual forward) and K x env, the difference per step (the
-    # forward then reads the obs the env launch just wrote, as in the timed rollout; back-to-back forwards
-    # alone re-read cold obs and take longer, reported as kernel_us_isolated)
-    t_fwd = time_kernel(lambda: (eng.env_only(), eng.fused_forward())) - time_kernel(eng.env_only)
+    # roofline of the dominant kernel. Fused mode (E >= 2048, the default here): the ONE launch of a rollout step,
+    # mm_rollout_step = env step + target net on s'_t + behavior net on s_{t+1} (2 nets x E x N agent-steps of
+    # network FLOPs; the env step is integer work on top). Otherwise the dual forward launch of the two-launch
+    # step. At E >= 2048 the network runs as fp16x3-split MFMAs (every fp32 product as 3 f16 MFMAs), so the
+    # MFMA ceiling for the network's fp32 FLOPs is the dense f16 peak / 3; the native f32-MFMA peak beside it.
     flops = 2 * qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
-    achieved = flops / t_fwd / 1e12
     h3 = E >= 2048 and not os.environ.get("MM_FWD_F32")
     peak = PEAK_F16_TFLOPS / 3 if h3 else PEAK_FP32_TFLOPS
-    # algorithmic HBM bytes per launch: per agent-step obs 4D + hidden in/out 8H + outputs (act/q 8 or max 4)
-    alg_bytes = E * N * ((4 * D + 8 * Hh + 8) + (4 * D + 8 * Hh + 4))
-    kname = "agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"
-    pmc_glob = "r*_pmc_agent_fwd.json"
+    if eng.fused:
+        t_fwd = t_iso = time_kernel(eng.fused_step_only)
+        kname = "rollout_step_kernel"
+        RC = eng.env.rows * eng.env.cols
+        # algorithmic HBM bytes per launch: per agent-step the stored s'_t 4D, hidden in/out of both nets 16H,
+        # action in 4, behavior act / Q(a) out 8, max Q' out 4, reward out 4, position word in / out 8; per env
+        # the grid in / out 2RC, step / apple counters in / out 16, done 1, store row in 8, cur_row out 8
+        alg_bytes = E * N * (4 * D + 16 * Hh + 28) + E * (2 * RC + 33)
+        kdesc = f"{kname}<64,64,64,1> (env step + dual forward: target+behavior, one launch per rollout step)"
+    else:
+        t_iso = time_kernel(eng.fused_forward)
+        # in its rollout context: graphs of K x (env + dual forward) and K x env, the difference per step (the
+        # forward then reads the obs the env launch just wrote, as in the timed rollout; back-to-back forwards
+        # alone re-read cold obs and take longer, reported as kernel_us_isolated)
+        t_fwd = time_kernel(lambda: (eng.env_only(), eng.fused_forward())) - time_kernel(eng.env_only)
+        kname = "agent_q_fwd_h3_kernel" if h3 else "agent_q_fwd_lds_kernel"
+        # algorithmic HBM bytes per launch: per agent-step obs 4D + hidden in/out 8H + outputs (act/q 8 or max 4)
+        alg_bytes = E * N * ((4 * D + 8 * Hh + 8) + (4 * D + 8 * Hh + 4))
+        kdesc = f"{kname}<64,64,64,1> (dual: target+behavior)"
+    achieved = flops / t_fwd / 1e12
     traffic = None
-    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", pmc_glob)))
+    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_rollout_step.json" if eng.fused
+                                         else "r*_pmc_agent_fwd.json")))
     if prof and E == 4096 and N == 8 and Hh == 64:
         pm = json.load(open(prof[-1]))
         if pm.get("kernel", "").startswith(kname):
@@ -720,7 +732,7 @@ def main():
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_source": os.path.basename(prof[-1]) if traffic else None,
-                "kernel": f"{kname}<64,64,64,1> (dual: target+behavior)",
+                "kernel": kdesc,
                 "kernel_us": round(t_fwd * 1e6, 2), "kernel_us_isolated": round(t_iso * 1e6, 2),
                 "arith": "fp32 network FLOPs as fp16x3-split MFMA (v_mfma_f32_16x16x32_f16 x3, fp32 accumulate)"
                          if h3 else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
@@ -746,8 +758,9 @@ def main():
             "config": {"workload": "QMIX 8-agent gridworld rollout, 4096 envs/GPU, GRU-64 agents, chunk 10, PER",
                        "envs_per_gpu": E, "agents": N, "obs_dim": D, "f1": F1, "gru": Hh, "chunk": 10,
                        "per_capacity_chunks": cap, "per_prefilled_chunks": fill_chunks * E,
-                       "step_launches": "env + dual forward + PER insert every chunk; one captured graph per "
-                                        "timed region",
+                       "step_launches": ("ONE fused launch (env step + dual forward) per step" if eng.fused else
+                                         "env + dual forward per step") + " + PER insert every chunk; one captured "
+                                                                            "graph per timed region",
                        "parallelism": f"env-shard x{world}"},
             "rccl_world_size": world,
             "replica_checksums": replicas,

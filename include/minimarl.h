@@ -144,6 +144,12 @@ int mm_env_get_state(mm_env* env, int32_t* pos, int32_t* prev, int8_t* grid, int
 int mm_env_set_state(mm_env* env, const int32_t* pos, const int32_t* prev, const int8_t* grid, const int32_t* steps,
                      const int32_t* apples);
 int mm_env_grid_shape(const mm_env* env, int32_t* rows, int32_t* cols);
+/* The same for one of the two state buffers of the fused rollout step (mm_rollout_step reads buffer
+ * state_in = t % 2 and writes the other): which = 0 is the buffer the env kernels use. */
+int mm_env_get_state_buf(mm_env* env, int32_t which, int32_t* pos, int32_t* prev, int8_t* grid, int32_t* steps,
+                         int32_t* apples);
+int mm_env_set_state_buf(mm_env* env, int32_t which, const int32_t* pos, const int32_t* prev, const int8_t* grid,
+                         const int32_t* steps, const int32_t* apples);
 
 /* ------------------------------------------------------------------ TD error + chunk store */
 /* One rollout step for E envs: td = |sum_i r_i + (1-done)*gamma*sum_i maxq'_i - sum_i q_taken_i|
@@ -223,6 +229,35 @@ int mm_env_step_rows_td(mm_env* env, const int32_t* act, float* next_obs, int64_
                         float* chunk_td, int32_t step_in_chunk, int32_t chunk_len, uint8_t* store_act,
                         float* store_rew, uint8_t* store_done, const int64_t* td_rows, uint64_t* counter,
                         mm_stream_t s);
+/* ONE launch per rollout step (replaces the per-step loop body of vdn/main.py:93-167 / qmix/main.py:186-233:
+ * env.step, the chunk-list append, the target max_a Q' of the next obs and sample_action of the next step):
+ * the env step of step t (mm_env_step_rows_td / _begin semantics) fused into the dual forward of
+ * mm_agent_q_fwd2 (target net io_t on s'_t, mode MAX; behavior net io_b on s_{t+1}, mode ACT). Results are
+ * bit-identical to the two-launch step. The observations never touch HBM on the way in: every block steps
+ * its env tile itself and builds its agent's obs from the grid in LDS. Double-buffered state: the env state
+ * buffer state_in (= t % 2, see mm_env_get_state_buf) is read and the other written; counter[state_in] is
+ * the behavior net's RNG step counter and counter[1 - state_in] = counter[state_in] + 1 is written; rew /
+ * done / io_t.qsel_out must not alias the td_* inputs of the previous step, nor io_b.act_out / qsel_out
+ * the act of this step or td_act / td_qsel (a ring of 3). io_b.reset must be NULL (the behavior hidden
+ * state resets where this step's env finished). Supported when mm_rollout_step_supported() != 0. */
+typedef struct mm_rollout_step_io {
+  const int32_t* act;                 /* [E,N] actions of step t */
+  float* store_obs; int64_t row_stride; int32_t slot, chunk_len;   /* s'_t -> slot (= step_in_chunk + 1) of row staging[e] */
+  int32_t begin;                      /* chunk start: also s_t -> slot 0 of row staging[e] */
+  const int64_t* staging; int64_t* cur_row;
+  float* rew; uint8_t* done;          /* [E,N] rewards, [E] done of step t */
+  int32_t state_in;                   /* env state buffer read (0 / 1) */
+  uint64_t* counter;                  /* [2] device RNG step counter */
+  /* TD / store of the previous step (mm_td_chunk_step_rows semantics, slot td_slot of rows staging[e]; the
+   * RNG counter is not touched) when td_on */
+  int32_t td_on, td_slot; float gamma;
+  const float* td_rew; const uint8_t* td_done; const float* td_qsel; const float* td_maxq; const int32_t* td_act;
+  float* chunk_td; uint8_t* store_act; float* store_rew; uint8_t* store_done;
+} mm_rollout_step_io;
+int mm_rollout_step_supported(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs);
+int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
+                    const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_step_io* x,
+                    mm_stream_t s);
 /* TD step writing into store rows rows[e]; increments the device RNG step counter (may be NULL). */
 int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                           const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,

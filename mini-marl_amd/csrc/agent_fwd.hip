@@ -13,7 +13,11 @@
 // 1 KiB each per 16 MFMAs), L2/L1-resident: block b serves agent b % N, so
 // with N = 8 each XCD's L2 only ever holds one agent's weights.
 // Arithmetic: exact-f32 MFMA v_mfma_f32_32x32x2_f32 (fp32 in, fp32 accumulate).
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
+#include "env_dev.h"
 #include "minimarl.h"
 #include "qnet_geo.h"
 
@@ -1435,6 +1439,459 @@ __global__ __launch_bounds__(1024, MM_H3_LB) void agent_q_fwd_h3_kernel(QFwdPara
                                     [&](int kb, float (&x)[8]) { load_obs_ks(orow, kb, p.D, x); }, xn, h0, eps, ctr);
 }
 
+// ---------------------------------------------------------------- fused rollout step
+// ONE launch per rollout step for the LDS-staged geometry (E >= 2048, the image in LDS): the env step of
+// step t (the restated Checkers dynamics of env.hip, oracle/env.py) inside the dual forward of
+// agent_q_fwd_h3_kernel (target net on s'_t, behavior net on s_{t+1}). It replaces the env launch + the
+// forward launch of the two-launch engine step (vdn/main.py:93-143: sample_action -> env.step -> store ->
+// target max_a Q'), with identical results.
+//
+// Every block (256 envs x one agent x one net) runs the env dynamics of its 256 envs itself: the 16 blocks of
+// an env tile compute the same transitions redundantly and each builds its own agent's observation k-steps
+// straight from the grid in LDS, so no observation is read from HBM and no block waits for another. Block
+// timeline (tools/roll_trace.py): (1) all 16 waves stage the tile's env inputs (grids, positions, actions,
+// counters; the writer block also step t-1's TD inputs) as contiguous 1 KiB LDS-DMA pieces into the region the
+// weight image later occupies; (2) waves 0-3 unpack them (one lane per env: nibble rows, packed positions /
+// actions) while the writer's waves 4-15 fold the TD / chunk-store write of step t-1; (3) waves 4-15 issue the
+// image DMA while waves 0-3 run the dynamics (env_step_wave_kernel's phase 1, one LDS round trip per agent);
+// (4) after the barrier every wave runs agent_q_fwd_body_h3 with its obs k-steps built from the LDS grid
+// (target blocks store s'_t into the chunk store on the way). Cross-block hazards are avoided by buffering
+// instead of synchronisation: the env state is double-buffered (read buffer par = t % 2, the tile's writer
+// block — target net, agent 0 — writes buffer 1 - par), the RNG step counter too (counter[1 - par] =
+// counter[par] + 1), rewards / max Q' by step parity and the actions / Q(a) of the behavior net in a ring of
+// 3, so the writer can fold in step t - 1's TD while other blocks of the same launch already write step
+// t + 1's actions. At a chunk start target blocks also store s_t into slot 0.
+struct RollStep {   // kernarg right after the two QFwdParams (read through the kernarg pointer)
+  EnvDev env;
+  const int32_t* act;      // [E][N] actions of step t
+  float* store_obs;        // chunk-store obs; s'_t of (e, agent) at staging[e] * row_stride + next_off + agent * D
+  int64_t row_stride, next_off;
+  const int64_t* staging;  // [E] store rows of this chunk
+  int64_t* cur_row;        // [E] staging[e], or -1 where the env finished (written by the writer blocks)
+  float* rew;              // [E][N] rewards of step t
+  uint8_t* done;           // [E]
+  uint64_t* counter;       // [2] RNG step counter, double-buffered
+  TdFuse td;               // step t - 1's TD / store (td.on), td.counter unused
+  uint64_t* trace;         // timing trace (MM_ROLL_TRACE; tools/roll_trace.py), nullptr normally
+  int par, begin, lds_env, pad_;   // state buffer read; chunk start (also write s_t to slot 0); env LDS offset
+};
+// timing stamps (s_memrealtime, 100 MHz) of block b at trace[8 b + i] when tracing
+#define MM_RSTAMP(i, cond)                                                                             \
+  do {                                                                                                 \
+    if (rs.trace && (cond) && blockIdx.x < 512) rs.trace[8 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
+static_assert(sizeof(QFwdParams) % 8 == 0 && alignof(RollStep) == 8, "rollout_step kernarg layout");
+#ifndef MM_ROLL_PROBE
+#define MM_ROLL_PROBE 0   // timing probes only (tools/roll_probe.py): 1 skip the env step, 2 skip the obs build, 4 skip obs stores
+#endif
+static constexpr int kRollMaxN = 10;    // 3 ceil(N / 2) <= 16 rows and agent markers 3 + k in a nibble
+static constexpr int kRollMaxR = 16;    // rows of 8 cells: one 32-bit nibble word per row
+
+// LDS staging of the env step (after the weight image): coordinate features, the tile's grids as nibble rows
+// (row r of env l = cells (r, 0..7) at bits 4c of word l * roll_gbw(R) + r), agent cells r << 4 | c, done flags
+struct RollLds {
+  int stab, sgrid, spos, sdone, total;
+};
+__host__ __device__ __forceinline__ int roll_gbw(int R) { return R | 1; }   // odd word stride: fewer bank conflicts
+__host__ __device__ __forceinline__ RollLds roll_lds(int R, int C, int N) {
+  auto a16 = [](int x) { return (x + 15) & ~15; };
+  RollLds m;
+  int o = 0;
+  m.stab = o;  o = a16(o + (R + C) * 4);
+  m.sgrid = o; o = a16(o + 256 * roll_gbw(R) * 4);
+  m.spos = o;  o = a16(o + 256 * N);
+  m.sdone = o; o = a16(o + 256);
+  m.total = o;
+  return m;
+}
+// 4 grid bytes (codes < 16) -> 4 nibbles, and back
+__device__ __forceinline__ uint32_t nib_pack4(uint32_t x) {
+  return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u);
+}
+__device__ __forceinline__ uint32_t nib_unpack4(uint32_t x) {
+  return (x & 0xFu) | ((x & 0xF0u) << 4) | ((x & 0xF00u) << 8) | ((x & 0xF000u) << 12);
+}
+// position word of the global state (prev_r << 24 | prev_c << 16 | r << 8 | c) -> 16 bits (4 per field)
+__device__ __forceinline__ uint32_t pos16(int32_t w) {
+  return (uint32_t)((((w >> 24) & 15) << 12) | (((w >> 16) & 15) << 8) | (((w >> 8) & 15) << 4) | (w & 15));
+}
+
+// The local observation of an agent at (r, c) as a bit word: bit f = feature f (>= 2) of get_agent_obs, i.e. bit
+// 2 + 5 cell + ch for the 3 x 3 cells (row-major) x {lemon, apple, even agent, odd agent, wall}; off-grid cells
+// are 0 (env.hip obs_value). Item code -> channel bits by a nibble table: 1 lemon, 2 apple, 3 + k agent k.
+__device__ __forceinline__ uint64_t roll_obs_word(const uint32_t* rows, int R, int r, int c) {
+  const uint32_t wm = r > 0 ? rows[r - 1] : 0u, w0 = rows[r], wp = r + 1 < R ? rows[r + 1] : 0u;
+  auto nb3 = [c](uint32_t w) { return (c > 0 ? (w >> (4 * c - 4)) : (w << 4)) & 0xFFFu; };   // cells c-1, c, c+1
+  const uint64_t items = (uint64_t)nb3(wm) | ((uint64_t)nb3(w0) << 12) | ((uint64_t)nb3(wp) << 24);
+  constexpr uint64_t kLut = 0x4848484848484210ull;   // item -> {lemon 1, apple 2, even agent 4, odd agent 8}
+  uint64_t word = 0;
+#pragma unroll
+  for (int cell = 0; cell < 9; ++cell) {
+    const uint32_t it = (uint32_t)(items >> (4 * cell)) & 15u;
+    word |= ((kLut >> (4 * it)) & 15ull) << (2 + 5 * cell);
+  }
+  return word;
+}
+// features f0 .. f0 + 3 of the word into x[0..3] (the coordinates for f < 2)
+__device__ __forceinline__ void roll_feat4(uint64_t word, int f0, float cr, float cc, float* x) {
+  const uint32_t fld = f0 < 64 ? (uint32_t)(word >> f0) : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = (float)((fld >> i) & 1u);
+  if (f0 == 0) {
+    x[0] = cr;
+    x[1] = cc;
+  }
+}
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+// store features f0 .. f0 + 3 (< D) of one (env, agent) row
+__device__ __forceinline__ void roll_store4(float* dst, int f0, int D, const float* x) {
+  if (f0 + 3 < D) {
+    *reinterpret_cast<f32x4u*>(dst + f0) = f32x4u{x[0], x[1], x[2], x[3]};
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (f0 + i < D) dst[f0 + i] = x[i];
+  }
+}
+
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QFwdParams p1, RollStep rs_) {
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  const bool second = (int)blockIdx.x >= p0.nblocks;     // p0: target net on s'_t, p1: behavior net on s_{t+1}
+  // parameters read from the kernarg segment on demand (uniform scalar loads) instead of held in SGPRs
+  const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  const QFwdParams& p = kargs[second ? 1 : 0];
+  const RollStep& rs = *reinterpret_cast<const RollStep*>(kargs + 2);
+  (void)p1;
+  (void)rs_;
+  const int bid = second ? (int)blockIdx.x - p0.nblocks : (int)blockIdx.x;
+  const int agent = bid % p.N, tile = bid / p.N;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const EnvDev& ev = rs.env;
+  const int N = p.N, D = p.D, R = ev.R, C = ev.C, RC = R * C, E = p.E;
+  const RollLds lay = roll_lds(R, C, N);
+  char* envl = reinterpret_cast<char*>(wsm) + rs.lds_env;
+  float* stab = reinterpret_cast<float*>(envl + lay.stab);
+  uint8_t* sgrid = reinterpret_cast<uint8_t*>(envl + lay.sgrid);
+  uint8_t* spos = reinterpret_cast<uint8_t*>(envl + lay.spos);
+  uint8_t* sdone = reinterpret_cast<uint8_t*>(envl + lay.sdone);
+  const bool writer = !second && agent == 0;
+  const int e0 = tile * 256;
+  const int par = rs.par;
+  const mm_qfwd_io& io = p.io;
+  const bool exact = reinterpret_cast<const int*>(p.packed + 2 * p.g.agent_stride * p.N)[agent] != 0;
+  MM_RSTAMP(0, threadIdx.x == 0);
+
+  if (threadIdx.x >= 256 && threadIdx.x < 256 + R + C) {
+    const int i = threadIdx.x - 256;
+    stab[i] = i < R ? ev.rtab[i] : ev.ctab[i - R];
+  }
+
+  // ---- waves 0-3: the env step of the tile, one lane per env (env_step_wave_kernel's phase 1 on nibble rows:
+  // one LDS round trip per agent, the agents in a rolled loop over packed position / action registers)
+  const int le_d = threadIdx.x;
+  const int de = e0 + le_d;
+  const bool dvalid = threadIdx.x < 256 && de < E && !(MM_ROLL_PROBE & 1);
+  uint32_t pq[kRollMaxN / 2];   // 16-bit position words, agent k in half k & 1 of pq[k >> 1]
+  uint32_t aq[2];               // 4-bit actions, agent k at bits 4 (k & 7) of aq[k >> 3]
+  int steps0 = 0, apples0 = 0;
+  int64_t myrow = 0;   // writer: this env's store row (cur_row after the step)
+  uint32_t* rows = reinterpret_cast<uint32_t*>(sgrid) + le_d * roll_gbw(R);
+  // the tile's env inputs are contiguous in HBM (grids [E][RC], positions / actions [E][N], counters [E]): staged
+  // by all 16 waves as 1 KiB LDS-DMA pieces into the image region (free until the image DMA below), so a
+  // dynamics lane then reads its env with a few ds_read_b128 instead of ~24 strided global loads
+  const int ne = min(256, E - e0);
+  const int st_grid = 0, st_pos = (256 * RC + 15) & ~15, st_act = st_pos + 256 * N * 4, st_steps = st_act + 256 * N * 4,
+            st_apples = st_steps + 1024;
+  // the writer block also stages the TD / store inputs of step t - 1 (same contiguous layout)
+  const bool tdw = writer && rs.td.on;
+  const int st_srow = st_apples + 1024 + 4 * 256 * N * 4 + 2048 + 1024 + 256;   // the tile's staging rows (writer)
+  const int st_trew = st_apples + 1024, st_tq = st_trew + 256 * N * 4, st_tm = st_tq + 256 * N * 4,
+            st_tact = st_tm + 256 * N * 4, st_trow = st_tact + 256 * N * 4, st_ctd = st_trow + 2048,
+            st_tdone = st_ctd + 1024;
+  {
+    char* stg = reinterpret_cast<char*>(wsm);
+    auto piece16 = [&](const void* src, int off, int bytes) {   // bytes of src -> stg + off, 16 B per lane
+      for (int c = wave; c * 1024 < bytes; c += 16)
+        if (c * 1024 + lane * 16 < bytes)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(static_cast<const char*>(src) + c * 1024 + lane * 16),
+              (__attribute__((address_space(3))) void*)(stg + off + c * 1024), 16, 0, 0);
+    };
+    if (!(MM_ROLL_PROBE & 1)) {
+      piece16((par ? ev.grid_alt : ev.grid) + (int64_t)e0 * RC, st_grid, ne * RC);
+      piece16((par ? ev.pos_alt : ev.pos) + (int64_t)e0 * N, st_pos, ne * N * 4);
+      piece16(rs.act + (int64_t)e0 * N, st_act, ne * N * 4);
+      piece16((par ? ev.steps_alt : ev.steps) + e0, st_steps, (ne * 4 + 15) & ~15);
+      piece16((par ? ev.apples_alt : ev.apples) + e0, st_apples, (ne * 4 + 15) & ~15);
+    }
+    if (writer) piece16(rs.staging + e0, st_srow, (ne * 8 + 15) & ~15);
+    if (tdw) {
+      const TdFuse& td = rs.td;
+      piece16(td.rew + (int64_t)e0 * N, st_trew, ne * N * 4);
+      piece16(td.q_taken + (int64_t)e0 * N, st_tq, ne * N * 4);
+      piece16(td.maxq + (int64_t)e0 * N, st_tm, ne * N * 4);
+      piece16(td.act + (int64_t)e0 * N, st_tact, ne * N * 4);
+      piece16(td.rows + e0, st_trow, (ne * 8 + 15) & ~15);
+      piece16(td.chunk_td + e0, st_ctd, (ne * 4 + 15) & ~15);
+      if (threadIdx.x < ne) reinterpret_cast<uint8_t*>(wsm)[st_tdone + threadIdx.x] = td.done[e0 + threadIdx.x];
+    }
+  }
+  __syncthreads();
+  if (tdw && wave >= 4) {
+    // the TD / store of step t - 1 (td_chunk_kernel's arithmetic: agent-order sums per env), from the staging
+    const TdFuse& td = rs.td;
+    const char* stg = reinterpret_cast<const char*>(wsm);
+    const float* trew = reinterpret_cast<const float*>(stg + st_trew);
+    const float* tq = reinterpret_cast<const float*>(stg + st_tq);
+    const float* tm = reinterpret_cast<const float*>(stg + st_tm);
+    const int32_t* tact = reinterpret_cast<const int32_t*>(stg + st_tact);
+    const int64_t* trow = reinterpret_cast<const int64_t*>(stg + st_trow);
+    const float* ctd = reinterpret_cast<const float*>(stg + st_ctd);
+    const uint8_t* tdone = reinterpret_cast<const uint8_t*>(stg + st_tdone);
+    const int i = threadIdx.x - 256;   // 768 threads
+    if (i < ne) {
+      float sr = 0.f, sq = 0.f, st = 0.f;
+      for (int j = 0; j < N; ++j) {
+        sr += trew[i * N + j];
+        sq += tq[i * N + j];
+        st += tm[i * N + j];
+      }
+      const uint8_t dd = tdone[i];
+      const float dn = dd ? 1.0f : 0.0f;
+      const float v = fabsf(sr + (1.0f - dn) * td.gamma * st - sq);
+      td.chunk_td[e0 + i] = (td.slot == 0 ? 0.0f : ctd[i]) + v;
+      td.s_done[trow[i] * td.C + td.slot] = dd;
+    }
+    for (int q = i; q < ne * N; q += 768) {
+      const int l = q / N, k = q - l * N;
+      const int64_t o = (trow[l] * td.C + td.slot) * N + k;
+      td.s_act[o] = (uint8_t)tact[q];
+      td.s_rew[o] = trew[q];
+    }
+  }
+  if (dvalid) {
+    const char* stg = reinterpret_cast<const char*>(wsm);
+    const int32_t* pw = reinterpret_cast<const int32_t*>(stg + st_pos) + le_d * N;
+    const int32_t* ac = reinterpret_cast<const int32_t*>(stg + st_act) + le_d * N;
+    const uint4* gin = reinterpret_cast<const uint4*>(stg + st_grid + le_d * RC);
+    if (writer) myrow = reinterpret_cast<const int64_t*>(stg + st_srow)[le_d];
+    steps0 = reinterpret_cast<const int32_t*>(stg + st_steps)[le_d];
+    apples0 = reinterpret_cast<const int32_t*>(stg + st_apples)[le_d];
+#pragma unroll
+    for (int j = 0; j < kRollMaxN / 2; ++j) pq[j] = 0u;
+    aq[0] = aq[1] = 0u;
+#pragma unroll
+    for (int k = 0; k < kRollMaxN; ++k)
+      if (k < N) {
+        const int32_t w = pw[k];
+        pq[k >> 1] |= pos16(w) << (16 * (k & 1));
+        aq[k >> 3] |= (uint32_t)(ac[k] & 15) << (4 * (k & 7));
+        spos[le_d * N + k] = (uint8_t)((pos_r(w) << 4) | pos_c(w));
+      }
+#pragma unroll
+    for (int j = 0; j < kRollMaxR / 2; ++j)
+      if (2 * j < R) {   // 16 bytes = 2 rows of 8 cells (RC = 8 R)
+        const uint4 g = gin[j];
+        rows[2 * j] = nib_pack4(g.x) | (nib_pack4(g.y) << 16);
+        if (2 * j + 1 < R) rows[2 * j + 1] = nib_pack4(g.z) | (nib_pack4(g.w) << 16);
+      }
+  }
+  MM_RSTAMP(1, threadIdx.x == 0);
+  __syncthreads();
+  MM_RSTAMP(2, threadIdx.x == 0);
+  // ---- waves 4-15, once the env inputs have been consumed: the weight image DMA into the staging region
+  // (range-guarded agents: the exact-f32 image) while waves 0-3 run the env step
+  if (wave >= 4) {
+    const float* src = p.packed + (exact ? 0 : (int64_t)p.N * p.g.agent_stride) + (int64_t)agent * p.g.agent_stride;
+    const int nchunk = (int)(p.g.agent_stride >> 8);
+    for (int c = wave - 4; c < nchunk; c += 12)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 256 + lane * 4),
+                                       (__attribute__((address_space(3))) void*)(wsm + c * 256), 16, 0, 0);
+  }
+  const int le = wave * 16 + (lane & 15), e = e0 + le;
+  if (rs.begin) {
+    // chunk start: slot 0 of the staging rows <- s_t, the observation of the state before this step; lane
+    // (env, g) writes features 16 q + 4 g .. + 3 of its env
+    __syncthreads();
+    if (!second && e < E) {
+      const int rc = spos[le * N + agent];
+      const uint64_t wd =
+          roll_obs_word(reinterpret_cast<const uint32_t*>(sgrid) + le * roll_gbw(R), R, rc >> 4, rc & 15);
+      const float cr = stab[rc >> 4], cc = stab[R + (rc & 15)];
+      float* d0 = rs.store_obs + rs.staging[e] * rs.row_stride + (int64_t)agent * D;
+      for (int f0 = 4 * (lane >> 4); f0 < D; f0 += 16) {
+        float x[4];
+        roll_feat4(wd, f0, cr, cc, x);
+        roll_store4(d0, f0, D, x);
+      }
+    }
+    __syncthreads();
+  }
+  if (dvalid) {
+    int apples = apples0;
+    const int steps = steps0 + 1;
+    int32_t* pout = (par ? ev.pos : ev.pos_alt) + (int64_t)de * N;
+    float* rout = rs.rew + (int64_t)de * N;
+#pragma unroll 1
+    for (int k = 0; k < N; ++k) {
+      const uint32_t w = pq[0] & 0xFFFFu;
+      const int a = (int)(aq[0] & 15u);
+#pragma unroll
+      for (int j = 0; j < kRollMaxN / 2 - 1; ++j) pq[j] = __builtin_amdgcn_alignbit(pq[j + 1], pq[j], 16);
+      pq[kRollMaxN / 2 - 1] >>= 16;
+      aq[0] = __builtin_amdgcn_alignbit(aq[1], aq[0], 4);
+      aq[1] >>= 4;
+      int r = (w >> 4) & 15, c = w & 15, pr = (w >> 12) & 15, pc = (w >> 8) & 15;
+      const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
+      const int nc = c + (a == 1 ? -1 : (a == 3 ? 1 : 0));
+      const bool inside = a != 4 && nr >= 0 && nr < R && nc >= 0 && nc < C;
+      // every row this agent may read or write, in one round trip: the target row, its own row, its stale prev row
+      const uint32_t w_n = rows[inside ? nr : r], w_r = rows[r], w_p = rows[pr];
+      const bool moved = inside && ((w_n >> (4 * nc)) & 15u) < 3u;
+      if (moved) {
+        pr = r;
+        pc = c;
+        r = nr;
+        c = nc;
+      }
+      // view update (ma_gym __update_agent_view) when agent_pos != agent_prev_pos: empty at agent_prev_pos, the
+      // marker at agent_pos; the fruit under a moving agent is eaten. Branch-free: both rows are written back
+      // every agent (unchanged when there is no update; the (r, c) row last, so a shared row gets both edits).
+      const bool upd = r != pr || c != pc;
+      const uint32_t A = moved ? w_n : w_r;   // row of (r, c)
+      const uint32_t B = moved ? w_r : w_p;   // row of (pr, pc)
+      const uint32_t item = upd ? (A >> (4 * c)) & 15u : 0u;
+      const bool big = (k & 1) == 0;
+      const float rk = ev.step_cost + (item == 1u ? (big ? -10.0f : -1.0f) : (item == 2u ? (big ? 10.0f : 1.0f) : 0.0f));
+      apples -= item == 2u ? 1 : 0;
+      const uint32_t clr = upd ? ~(15u << (4 * pc)) : ~0u;
+      const uint32_t A1 = pr == r ? (A & clr) : A;
+      rows[pr] = B & clr;
+      rows[r] = upd ? ((A1 & ~(15u << (4 * c))) | ((uint32_t)(3 + k) << (4 * c))) : A1;
+      spos[le_d * N + k] = (uint8_t)((r << 4) | c);
+      if (writer) {
+        pout[k] = (pr << 24) | (pc << 16) | (r << 8) | c;
+        rout[k] = rk;
+      }
+    }
+    const bool dn = steps >= ev.max_steps || apples == 0;
+    sdone[le_d] = dn ? 1 : 0;
+    if (writer) {
+      // the step's outputs and the next state (auto-reset where the episode ended)
+      rs.done[de] = dn ? 1 : 0;
+      rs.cur_row[de] = dn ? -1 : myrow;
+      (par ? ev.steps : ev.steps_alt)[de] = dn ? 0 : steps;
+      (par ? ev.apples : ev.apples_alt)[de] = dn ? ev.init_apples : apples;
+      uint4* gout = reinterpret_cast<uint4*>((par ? ev.grid : ev.grid_alt) + (int64_t)de * RC);
+      const uint4* ig = reinterpret_cast<const uint4*>(ev.init_grid);
+#pragma unroll
+      for (int j = 0; j < kRollMaxR / 2; ++j)
+        if (2 * j < R) {
+          uint4 v;
+          if (dn) {
+            v = ig[j];
+          } else {
+            const uint32_t a0 = rows[2 * j], a1 = 2 * j + 1 < R ? rows[2 * j + 1] : 0u;
+            v = make_uint4(nib_unpack4(a0 & 0xFFFFu), nib_unpack4(a0 >> 16), nib_unpack4(a1 & 0xFFFFu),
+                           nib_unpack4(a1 >> 16));
+          }
+          gout[j] = v;
+        }
+      if (dn)
+        for (int k = 0; k < N; ++k) pout[k] = ev.init_pos[k];
+    }
+  }
+  if (writer && tile == 0 && threadIdx.x == 0) rs.counter[1 - par] = rs.counter[par] + 1;
+  MM_RSTAMP(3, threadIdx.x == 0);
+
+  if (exact) {
+    // range-guarded agent: the exact-f32 body, 8 waves x 32 envs (agent_q_fwd_h3_kernel's fallback)
+    const int l32 = wave * 32 + (lane & 31), e32 = e0 + l32, hh = (lane & 63) >> 5;
+    const int64_t srow32 = (!second && e32 < E) ? rs.staging[e32] : 0;
+    const bool r32 = !second && io.reset && e32 < E && io.reset[e32];
+    __syncthreads();
+    const bool bd = second && e32 < E && sdone[l32];
+    float* dst = (!second && e32 < E) ? rs.store_obs + srow32 * rs.row_stride + rs.next_off + (int64_t)agent * D : nullptr;
+    const int rc32 = spos[l32 * N + agent];
+    const uint64_t wd32 =
+        roll_obs_word(reinterpret_cast<const uint32_t*>(sgrid) + l32 * roll_gbw(R), R, rc32 >> 4, rc32 & 15);
+    const float cr32 = stab[rc32 >> 4], cc32 = stab[R + (rc32 & 15)];
+    // k-block kb: element s = 4 i + j holds feature 32 kb + 8 i + 4 hh + j (kperm)
+    auto ol32 = [&](int kb, float (&x)[16]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int f0 = kb * 32 + 8 * i + 4 * hh;
+        roll_feat4(wd32, f0, cr32, cc32, x + 4 * i);
+        if (bd || e32 >= E)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[4 * i + j] = (e32 < E && f0 + j < D) ? ev.reset_obs[agent * D + f0 + j] : 0.0f;
+        if (dst) roll_store4(dst, f0, D, x + 4 * i);
+      }
+    };
+    float x32[16];
+    if (wave < 8) {
+      ol32(0, x32);
+      agent_q_fwd_body<F1, G, H, AB>(p, agent, e32, wsm, ol32, x32, e32 >= E || r32 || bd);
+    }
+    return;
+  }
+  // hidden state of this wave's 16 envs (target: reset where step t - 1 ended; behavior: where step t ended)
+  const int ec = min(e, E - 1);
+  const int g = lane >> 4;
+  f32x4 h0[H / 16];
+  {
+    const float* hp = io.h_in + (int64_t)ec * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)(4 * g) * io.hin_sf;
+#pragma unroll
+    for (int t = 0; t < H / 16; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h0[t][r] = hp[(int64_t)(16 * t + r) * io.hin_sf];
+  }
+  const bool rt = !second && io.reset && io.reset[ec];
+  const float eps = (io.mode == MM_Q_ACT && io.eps_ptr) ? *io.eps_ptr : io.epsilon;
+  const uint64_t ctr = (io.mode == MM_Q_ACT && io.counter_ptr) ? *io.counter_ptr : io.counter;
+  __syncthreads();
+  MM_RSTAMP(4, threadIdx.x == 0);
+  const bool bd = second && e < E && sdone[le];
+  if (e >= E || rt || bd) {
+#pragma unroll
+    for (int t = 0; t < H / 16; ++t) h0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // the store destination of s'_t (target blocks), loaded after the env step (a global load before it would be
+  // waited on inside the dynamics loop by the spill reloads' vmcnt)
+  const int64_t srow = (!second && e < E) ? rs.staging[e] : 0;
+  float* dst = (!second && e < E) ? rs.store_obs + srow * rs.row_stride + rs.next_off + (int64_t)agent * D : nullptr;
+  const int rc = spos[le * N + agent];
+  const uint64_t wd = roll_obs_word(reinterpret_cast<const uint32_t*>(sgrid) + le * roll_gbw(R), R, rc >> 4, rc & 15);
+  const float cr = stab[rc >> 4], cc = stab[R + (rc & 15)];
+  // k-step kb: element 4 q + j holds feature 32 kb + 16 q + 4 g + j (kperm16)
+  auto ol = [&](int kb, float (&x)[8]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int f0 = kb * 32 + 16 * q + 4 * g;
+      if (MM_ROLL_PROBE & 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[4 * q + j] = 0.25f;
+      } else {
+        roll_feat4(wd, f0, cr, cc, x + 4 * q);
+      }
+      if (bd || e >= E)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[4 * q + j] = (e < E && f0 + j < D) ? ev.reset_obs[agent * D + f0 + j] : 0.0f;
+      if (dst && !(MM_ROLL_PROBE & 4)) roll_store4(dst, f0, D, x + 4 * q);
+    }
+  };
+  float xn[8];
+  ol(0, xn);
+  MM_RSTAMP(5, threadIdx.x == 0);
+  if (wave >= 8)
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(8);
+  agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm, ol, xn, h0, eps, ctr);
+  MM_RSTAMP(6, threadIdx.x == 0);
+  MM_RSTAMP(7, threadIdx.x == 64 * 15);
+}
+
 // ---------------------------------------------------------------- learner PRE on the fp16x3 image
 // The learner's non-recurrent part (layers 1-2 with their training saves, and gi = W_ih x2 + b_ih) of large
 // batches in the fast (cfg5) mode, QLearner(mixer_fp16=True): agent_q_fwd_body_h3's layers 1-2 and its
@@ -1827,6 +2284,16 @@ static int launch_fwd(QFwdParams p0, const QFwdParams* p1in, hipStream_t s) {
   return MM_OK;
 }
 
+template <int F1, int G, int H, int AB>
+static int launch_roll(QFwdParams p0, QFwdParams p1, const RollStep& rs, size_t sm, hipStream_t s) {
+  p0.nblocks = (p0.E + 255) / 256 * p0.N;
+  p1.nblocks = (p1.E + 255) / 256 * p1.N;
+  hipLaunchKernelGGL((rollout_step_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(1024), sm, s, p0, p1,
+                     rs);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 static int make_params(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,
                        QFwdParams* p) {
   MM_REQUIRE(d && packed && io, "agent_q_fwd: null argument");
@@ -2031,6 +2498,88 @@ int agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* 
   rc = make_params(d, packed1, io1, e1, &p1);
   if (rc) return rc;
   return dispatch(d, p0, &p1, s);
+}
+
+// LDS bytes of the fused rollout step for this env / net, or 0 when the fused step does not apply (the
+// two-launch path is used instead): local obs (D = 47), agent markers in a nibble, a grid of <= 128 cells
+// in 16-byte rows, E >= 2048 and image + env staging within the CU's 160 KiB.
+// bytes of the region that first stages the env (and TD) inputs and then holds the weight image
+static size_t roll_region(const EnvDev& ev, const QnetGeo& g) {
+  // grids | positions | actions | steps | apples | TD: rew, Q(a), max Q', act | TD rows | chunk_td | dones | rows
+  const size_t staging = ((256 * (size_t)ev.R * ev.C + 15) & ~size_t(15)) + 6 * 256 * (size_t)ev.N * 4 + 7424;
+  return (std::max((size_t)g.agent_stride * 4, staging) + 15) & ~size_t(15);
+}
+
+size_t rollout_step_lds(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs) {
+  if (!env || !d) return 0;
+  const EnvDev& ev = env->d;
+  QnetGeo g;
+  QnetOffsets o;
+  if (qnet_geometry(d, &g, &o)) return 0;
+  if (ev.full_obs || ev.D != OBS_LOCAL || d->obs_dim != ev.D || d->n_agents != ev.N) return 0;
+  if (ev.N > kRollMaxN || ev.R > kRollMaxR || ev.C != 8) return 0;   // 8 columns: one nibble word per row
+  if (n_envs < 2048 || n_envs != ev.E) return 0;
+  const bool known = (d->f1 == 64 && d->g == 32 && d->h == 32) || (d->f1 == 64 && d->g == 64 && d->h == 64) ||
+                     (d->f1 == 128 && d->g == 32 && d->h == 32) || (d->f1 == 64 && d->g == 32 && d->h == 64);
+  if (!known) return 0;
+  const size_t sm = roll_region(ev, g) + (size_t)roll_lds(ev.R, ev.C, ev.N).total;
+  return sm <= 160 * 1024 ? sm : 0;
+}
+
+int rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
+                 const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_step_io* x,
+                 hipStream_t s) {
+  MM_REQUIRE(env && d && x, "rollout_step: null argument");
+  const size_t sm = rollout_step_lds(env, d, n_envs);
+  MM_REQUIRE(sm > 0, "rollout_step: configuration not supported by the fused step (mm_rollout_step_supported)");
+  MM_REQUIRE(x->act && x->store_obs && x->staging && x->cur_row && x->rew && x->done && x->counter,
+             "rollout_step: null step buffer");
+  MM_REQUIRE(x->state_in == 0 || x->state_in == 1, "rollout_step: state_in must be 0 or 1");
+  MM_REQUIRE(io_t->mode == MM_Q_MAX && io_b->mode == MM_Q_ACT, "rollout_step: target io must be MAX, behavior io ACT");
+  MM_REQUIRE(io_t->h_in && io_b->h_in && io_t->h_out && io_b->h_out, "rollout_step: hidden states required");
+  MM_REQUIRE(io_b->reset == nullptr, "rollout_step: the behavior reset flags are the step's own dones (pass NULL)");
+  const int64_t nd = (int64_t)d->n_agents * d->obs_dim;
+  MM_REQUIRE(x->slot >= 1 && x->chunk_len >= x->slot && x->row_stride >= (x->chunk_len + 1) * nd,
+             "rollout_step: bad store slot / row stride");
+  QFwdParams p0, p1;
+  int rc = make_params(d, packed_t, io_t, n_envs, &p0);
+  if (rc) return rc;
+  rc = make_params(d, packed_b, io_b, n_envs, &p1);
+  if (rc) return rc;
+  RollStep rs;
+  rs.env = env->d;
+  rs.act = x->act;
+  rs.store_obs = x->store_obs;
+  rs.row_stride = x->row_stride;
+  rs.next_off = (int64_t)x->slot * nd;
+  rs.staging = x->staging;
+  rs.cur_row = x->cur_row;
+  rs.rew = x->rew;
+  rs.done = x->done;
+  rs.counter = x->counter;
+  rs.td = TdFuse{};
+  if (x->td_on) {
+    MM_REQUIRE(x->td_rew && x->td_done && x->td_qsel && x->td_maxq && x->td_act && x->chunk_td && x->store_act &&
+                   x->store_rew && x->store_done, "rollout_step: null TD argument");
+    MM_REQUIRE(x->td_slot >= 0 && x->td_slot < x->chunk_len, "rollout_step: bad TD slot");
+    rs.td = TdFuse{x->td_rew, x->td_done, x->td_qsel, x->td_maxq, x->td_act, x->chunk_td, x->store_act,
+                   x->store_rew, x->store_done, x->staging, nullptr, x->gamma, x->td_slot, x->chunk_len, 1};
+  }
+  rs.par = x->state_in;
+  rs.trace = debug_trace_buffer("MM_ROLL_TRACE");
+  rs.begin = x->begin ? 1 : 0;
+  rs.lds_env = (int)roll_region(env->d, p0.g);
+  const int AB = (d->n_actions + 31) / 32;
+#define MM_ROLL(F1_, G_, H_)                                                                             \
+  if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                          \
+    return AB == 1 ? launch_roll<F1_, G_, H_, 1>(p0, p1, rs, sm, s) : launch_roll<F1_, G_, H_, 2>(p0, p1, rs, sm, s);
+  MM_ROLL(64, 32, 32)
+  MM_ROLL(64, 64, 64)
+  MM_ROLL(128, 32, 32)
+  MM_ROLL(64, 32, 64)
+#undef MM_ROLL
+  set_error("rollout_step: unsupported (F1,G,H)");
+  return MM_EINVAL;
 }
 
 }  // namespace mm

@@ -19,36 +19,10 @@
 #include <vector>
 
 #include "common.h"
+#include "env_dev.h"
 #include "minimarl.h"
 
 namespace mm {
-static constexpr int OBS_LOCAL = 47;
-
-struct EnvDev {
-  int E, N, R, C, D, max_steps, full_obs, init_apples;
-  int eb;  // envs per block of the step kernel
-  float step_cost;
-  int32_t* pos;     // [E][N] prev_r << 24 | prev_c << 16 | r << 8 | c
-  int8_t* grid;     // [E][R*C] _full_obs codes
-  int32_t* steps;   // [E]
-  int32_t* apples;  // [E]
-  const int8_t* init_grid;  // [R*C] (agent markers at their start cells, then the fruit)
-  const int32_t* init_pos;  // [N] (prev = pos)
-  const float* rtab;        // [R] round(r / (R - 1), 2) as f32
-  const float* ctab;        // [C] round(c / (C - 1), 2) as f32
-  float* reset_obs;         // [N][D]
-};
-}  // namespace mm
-
-struct mm_env {
-  mm::EnvDev d;
-  void* alloc;
-};
-
-namespace mm {
-
-__device__ __forceinline__ int pos_r(int32_t w) { return (w >> 8) & 255; }
-__device__ __forceinline__ int pos_c(int32_t w) { return w & 255; }
 
 // feature f in [0, 47) of agent k's local obs (get_agent_obs): coords from the tables, then the 3x3 cells x
 // {lemon, apple, even agent, odd agent, wall} read from the grid; off-grid cells stay all zero
@@ -465,6 +439,7 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
     return o;
   };
   const size_t o_pos = take(E * d.N * 4), o_grid = take(E * RC), o_steps = take(E * 4), o_apples = take(E * 4),
+               o_pos2 = take(E * d.N * 4), o_grid2 = take(E * RC), o_steps2 = take(E * 4), o_apples2 = take(E * 4),
                o_igrid = take(RC), o_ipos = take(d.N * 4), o_tab = take((d.R + d.C) * 4),
                o_robs = take((size_t)d.N * d.D * 4);
   void* base = nullptr;
@@ -474,6 +449,10 @@ int env_create(const mm_env_cfg* cfg, int64_t n_envs, uint64_t seed, mm_env** ou
   d.grid = reinterpret_cast<int8_t*>(b + o_grid);
   d.steps = reinterpret_cast<int32_t*>(b + o_steps);
   d.apples = reinterpret_cast<int32_t*>(b + o_apples);
+  d.pos_alt = reinterpret_cast<int32_t*>(b + o_pos2);
+  d.grid_alt = reinterpret_cast<int8_t*>(b + o_grid2);
+  d.steps_alt = reinterpret_cast<int32_t*>(b + o_steps2);
+  d.apples_alt = reinterpret_cast<int32_t*>(b + o_apples2);
   d.init_grid = reinterpret_cast<int8_t*>(b + o_igrid);
   d.init_pos = reinterpret_cast<int32_t*>(b + o_ipos);
   d.rtab = reinterpret_cast<float*>(b + o_tab);
@@ -581,12 +560,15 @@ int mm_env_step_rows_begin(mm_env* env, const int32_t* act, float* store_obs, in
   return mm::env_step(env, act, store_obs + nd, row_stride, staging, nullptr, cur_row, rew, done, nullptr,
                       (hipStream_t)s, &bc);
 }
-int mm_env_get_state(mm_env* env, int32_t* pos, int32_t* prev, int8_t* grid, int32_t* steps, int32_t* apples) {
-  if (!env) return MM_EINVAL;
+int mm_env_get_state_buf(mm_env* env, int32_t which, int32_t* pos, int32_t* prev, int8_t* grid, int32_t* steps,
+                         int32_t* apples) {
+  if (!env || which < 0 || which > 1) return MM_EINVAL;
   const mm::EnvDev& d = env->d;
+  const int32_t* dpos = which ? d.pos_alt : d.pos;
+  const int8_t* dgrid = which ? d.grid_alt : d.grid;
   if (hipDeviceSynchronize() != hipSuccess) return MM_EHIP;
   std::vector<int32_t> p((size_t)d.E * d.N);
-  if (hipMemcpy(p.data(), d.pos, p.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
+  if (hipMemcpy(p.data(), dpos, p.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
   for (size_t i = 0; i < p.size(); ++i) {
     if (pos) {
       pos[2 * i] = (p[i] >> 8) & 255;
@@ -597,15 +579,21 @@ int mm_env_get_state(mm_env* env, int32_t* pos, int32_t* prev, int8_t* grid, int
       prev[2 * i + 1] = (p[i] >> 16) & 255;
     }
   }
-  if (grid && hipMemcpy(grid, d.grid, (size_t)d.E * d.R * d.C, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
-  if (steps && hipMemcpy(steps, d.steps, (size_t)d.E * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
-  if (apples && hipMemcpy(apples, d.apples, (size_t)d.E * 4, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
+  if (grid && hipMemcpy(grid, dgrid, (size_t)d.E * d.R * d.C, hipMemcpyDeviceToHost) != hipSuccess) return MM_EHIP;
+  if (steps && hipMemcpy(steps, which ? d.steps_alt : d.steps, (size_t)d.E * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return MM_EHIP;
+  if (apples && hipMemcpy(apples, which ? d.apples_alt : d.apples, (size_t)d.E * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return MM_EHIP;
   return MM_OK;
 }
+int mm_env_get_state(mm_env* env, int32_t* pos, int32_t* prev, int8_t* grid, int32_t* steps, int32_t* apples) {
+  return mm_env_get_state_buf(env, 0, pos, prev, grid, steps, apples);
+}
 
-int mm_env_set_state(mm_env* env, const int32_t* pos, const int32_t* prev, const int8_t* grid, const int32_t* steps,
-                     const int32_t* apples) {
+int mm_env_set_state_buf(mm_env* env, int32_t which, const int32_t* pos, const int32_t* prev, const int8_t* grid,
+                         const int32_t* steps, const int32_t* apples) {
   MM_REQUIRE(env && pos && prev && grid && steps && apples, "env_set_state: null argument");
+  MM_REQUIRE(which == 0 || which == 1, "env_set_state: state buffer must be 0 or 1");
   const mm::EnvDev& d = env->d;
   std::vector<int32_t> p((size_t)d.E * d.N);
   for (size_t i = 0; i < p.size(); ++i) {
@@ -618,10 +606,14 @@ int mm_env_set_state(mm_env* env, const int32_t* pos, const int32_t* prev, const
   for (size_t i = 0; i < (size_t)d.E * RC; ++i)
     MM_REQUIRE(grid[i] >= 0 && grid[i] < 3 + d.N, "env_set_state: grid code out of range");
   MM_HIP_CHECK(hipDeviceSynchronize());
-  MM_HIP_CHECK(hipMemcpy(d.pos, p.data(), p.size() * 4, hipMemcpyHostToDevice));
-  MM_HIP_CHECK(hipMemcpy(d.grid, grid, (size_t)d.E * RC, hipMemcpyHostToDevice));
-  MM_HIP_CHECK(hipMemcpy(d.steps, steps, (size_t)d.E * 4, hipMemcpyHostToDevice));
-  MM_HIP_CHECK(hipMemcpy(d.apples, apples, (size_t)d.E * 4, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(which ? d.pos_alt : d.pos, p.data(), p.size() * 4, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(which ? d.grid_alt : d.grid, grid, (size_t)d.E * RC, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(which ? d.steps_alt : d.steps, steps, (size_t)d.E * 4, hipMemcpyHostToDevice));
+  MM_HIP_CHECK(hipMemcpy(which ? d.apples_alt : d.apples, apples, (size_t)d.E * 4, hipMemcpyHostToDevice));
   return MM_OK;
+}
+int mm_env_set_state(mm_env* env, const int32_t* pos, const int32_t* prev, const int8_t* grid, const int32_t* steps,
+                     const int32_t* apples) {
+  return mm_env_set_state_buf(env, 0, pos, prev, grid, steps, apples);
 }
 }

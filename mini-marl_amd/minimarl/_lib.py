@@ -45,6 +45,18 @@ class QFwdIO(ctypes.Structure):
     ]
 
 
+class RollStepIO(ctypes.Structure):
+    """mm_rollout_step_io (include/minimarl.h)"""
+    _fields_ = [
+        ("act", c_vp), ("store_obs", c_vp), ("row_stride", c_i64), ("slot", c_i32), ("chunk_len", c_i32),
+        ("begin", c_i32), ("staging", c_vp), ("cur_row", c_vp), ("rew", c_vp), ("done", c_vp),
+        ("state_in", c_i32), ("counter", c_vp),
+        ("td_on", c_i32), ("td_slot", c_i32), ("gamma", c_f32),
+        ("td_rew", c_vp), ("td_done", c_vp), ("td_qsel", c_vp), ("td_maxq", c_vp), ("td_act", c_vp),
+        ("chunk_td", c_vp), ("store_act", c_vp), ("store_rew", c_vp), ("store_done", c_vp),
+    ]
+
+
 class EnvCfg(ctypes.Structure):
     _fields_ = [("n_agents", c_i32), ("max_steps", c_i32), ("full_observable", c_i32), ("cols", c_i32),
                 ("step_cost", c_f32)]
@@ -72,6 +84,11 @@ _SIGS = [
     ("mm_env_reset_obs", c_vp, [c_vp]),
     ("mm_env_step_rows_begin", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_env_get_state", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_get_state_buf", c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_env_set_state_buf", c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_rollout_step_supported", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_i64]),
+    ("mm_rollout_step", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_vp,
+                                ctypes.POINTER(QFwdIO), c_i64, ctypes.POINTER(RollStepIO), c_vp]),
     ("mm_env_grid_shape", c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     ("mm_td_chunk_step", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                                  c_vp, c_vp, c_i64, c_vp]),

@@ -10,13 +10,16 @@ qmix/main.py:100-237): for every env at every step
      (cal_td_error + chunk lists, qmix/_utils.py:86-97, qmix/main.py:204-233)
   5. every C steps: the E finished chunks go into the prioritized replay at once
 
-Two launches per step: env(t) — fused with the TD/store of step t-1 inside a chunk, with the
-chunk-start copy of the current obs into the new staging rows at a chunk's first step — and the
-target fwd of step t fused with the behavior fwd of step t+1; the chunk's last step adds the PER
-insert (four launches, its first one also running that step's TD/store). All stream-ordered on
-one HIP stream, no host sync; a chunk of steps is captured once as a HIP graph and replayed. The
-store/TD of the last executed step therefore lands with the next step (``flush_td()`` writes it
-now).
+ONE launch per step where the fused rollout step applies (``fused``: the restated Checkers env, local obs,
+E >= 2048; mm_rollout_step): the env step of step t, the target fwd of step t and the behavior fwd of
+step t+1 in one kernel, the TD/store of step t-1 folded into it; the env state, RNG counter, rewards and
+max Q' alternate by step parity and the behavior outputs rotate through 3 buffers (so the graph cycle is
+lcm(C, 6) steps). Otherwise two launches per step: env(t) — fused with the TD/store of step t-1 inside
+a chunk, with the chunk-start copy of the current obs into the new staging rows at a chunk's first
+step — and the target fwd of step t fused with the behavior fwd of step t+1. The chunk's last step adds
+the PER insert (its first launch also running that step's TD/store). All stream-ordered on one HIP
+stream, no host sync; a chunk of steps is captured once as a HIP graph and replayed. The store/TD of
+the last executed step therefore lands with the next step (``flush_td()`` writes it now).
 Hidden states reset at episode ends (the reference re-inits them per episode,
 vdn/main.py:137-138); chunks span episode boundaries like the reference's
 global ``count_step`` (vdn/main.py:151-167).
@@ -29,10 +32,12 @@ slot -> row; inserts swap the finished staging rows in and take the evicted
 rows back as the next staging rows (no chunk copy).
 """
 import ctypes
+import math
+import os
 
 import torch
 
-from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, check, lib
+from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, RollStepIO, check, lib
 from .env import make_env
 from .qnet import AgentQNet, graph_capture, ptr, stream_handle
 from .replay import DevicePER
@@ -54,7 +59,7 @@ class ChunkStore:
 class RolloutEngine:
     def __init__(self, n_envs, n_agents, obs_dim=None, n_actions=5, f1=64, g=32, h=32, chunk=10,
                  capacity=None, gamma=0.99, max_steps=100, step_cost=-0.01, full_observable=False,
-                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", device="cuda"):
+                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", fused=None, device="cuda"):
         self.device = torch.device(device)
         self.E, self.N, self.C = int(n_envs), int(n_agents), int(chunk)
         self.gamma = float(gamma)
@@ -73,6 +78,16 @@ class RolloutEngine:
         self.staging = torch.arange(self.capacity, self.capacity + self.E, dtype=torch.int64, device=self.device)
         E, N, D, H = self.E, self.N, self.D, self.H
         dev = self.device
+        ok = env == "checkers" and lib().mm_rollout_step_supported(self.env.handle(), ctypes.byref(self.behavior.dims),
+                                                                    E) != 0
+        if fused and not ok:
+            raise ValueError("RolloutEngine(fused=True): the fused rollout step does not support this configuration")
+        if fused is None and os.environ.get("MM_FUSED_STEP", "1") == "0":   # A/B runs: force the two-launch step
+            fused = False
+        self.fused = ok if fused is None else bool(fused)
+        nb = 3 if self.fused else 2
+        if self.fused:
+            self.env.state_buffer = lambda: self.t % 2
         # current obs s_{t+1} is never materialised: it is slot c+1 of row cur_row[e] of the chunk
         # store (the env's terminal next obs), or the env's reset obs where cur_row[e] = -1
         self.cur_row = torch.full((E,), -1, dtype=torch.int64, device=dev)
@@ -81,15 +96,19 @@ class RolloutEngine:
         # hidden load / store of a wave is one coalesced 128-byte run per feature row
         self.h = torch.zeros(N, H, E, device=dev)
         self.ht = torch.zeros(N, H, E, device=dev)
-        # ping-pong buffers indexed by step parity: done_t, act_t, q_taken_t live in slot t % 2
+        # ping-pong buffers indexed by step parity: done_t in slot t % 2; act_t, q_taken_t in slot t % nb (nb = 3
+        # in the fused mode, whose launch writes step t+1's actions while it reads step t-1's); the fused mode
+        # also alternates rew_t / max Q'_t (slot t % 2), the other mode uses slot 0 only
         self.done_buf = [torch.zeros(E, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.act_buf = [torch.zeros(E, N, dtype=torch.int32, device=dev) for _ in range(2)]
-        self.qsel_buf = [torch.zeros(E, N, device=dev) for _ in range(2)]
-        self.maxq = torch.zeros(E, N, device=dev)
-        self.rew = torch.zeros(E, N, device=dev)
+        self.act_buf = [torch.zeros(E, N, dtype=torch.int32, device=dev) for _ in range(nb)]
+        self.qsel_buf = [torch.zeros(E, N, device=dev) for _ in range(nb)]
+        self.maxq_buf = [torch.zeros(E, N, device=dev) for _ in range(2)]
+        self.rew_buf = [torch.zeros(E, N, device=dev) for _ in range(2)]
+        self.maxq, self.rew = self.maxq_buf[0], self.rew_buf[0]
         self.chunk_td = torch.zeros(E, device=dev)
         self.eps_dev = torch.zeros(1, device=dev)
-        self.counter_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # rollout step (RNG stream)
+        # rollout step counter (RNG stream); the fused mode double-buffers it (slot t % 2 is read at step t)
+        self.counter_dev = torch.zeros(2, dtype=torch.int64, device=dev)
         self._eps_host = None
         self._primed = False
         self._td_pending = False     # last step's TD/store not yet written (fused into the next env step)
@@ -105,9 +124,12 @@ class RolloutEngine:
     def state_buffers(self):
         """The per-step device buffers a checkpoint must carry (name -> tensor)."""
         out = {k: getattr(self, k) for k in ("cur_row", "init_obs", "h", "ht", "chunk_td", "eps_dev", "staging")}
-        out.update(maxq=self.maxq, rew=self.rew, counter_dev=self.counter_dev)
+        out.update(counter_dev=self.counter_dev)
         for k in range(2):
             out[f"done_buf{k}"] = self.done_buf[k]
+            out[f"maxq_buf{k}"] = self.maxq_buf[k]
+            out[f"rew_buf{k}"] = self.rew_buf[k]
+        for k in range(len(self.act_buf)):
             out[f"act_buf{k}"] = self.act_buf[k]
             out[f"qsel_buf{k}"] = self.qsel_buf[k]
         return out
@@ -115,7 +137,7 @@ class RolloutEngine:
     @property
     def last_rew(self):
         """rewards [E, N] of the last executed step"""
-        return self.rew
+        return self.rew_buf[(self.t - 1) % 2] if self.fused else self.rew
 
     @property
     def last_done(self):
@@ -133,7 +155,7 @@ class RolloutEngine:
     @property
     def act(self):
         """actions [E, N] of the last executed step"""
-        return self.act_buf[(self.t - 1) % 2] if self.t > 0 else self.act_buf[0]
+        return self.act_buf[(self.t - 1) % len(self.act_buf)] if self.t > 0 else self.act_buf[0]
 
     def _io_behavior(self, k):
         """behavior fwd writing slot k (acts for step t with t % 2 == k); reset = done_{t-1}."""
@@ -172,6 +194,21 @@ class RolloutEngine:
     def _build_io(self):
         self.io_b = [self._io_behavior(0), self._io_behavior(1)]
         self.io_t = [self._io_target(0), self._io_target(1)]
+        if self.fused:
+            # step t (k2 = t % 2, k3 = t % 3): target -> max Q'_t in maxq_buf[k2], reset = done_{t-1}; behavior ->
+            # act / Q(a) of step t+1 in slot (k3 + 1) % 3, RNG counter slot k2, reset = this step's dones (in-kernel)
+            self.fio_t, self.fio_b = [], {}
+            for k2 in range(2):
+                it = self._io_target(k2)
+                it.qsel_out = self.maxq_buf[k2].data_ptr()
+                self.fio_t.append(it)
+                for k3 in range(3):
+                    ib = self._io_behavior(0)
+                    ib.reset = None
+                    ib.act_out = self.act_buf[(k3 + 1) % 3].data_ptr()
+                    ib.qsel_out = self.qsel_buf[(k3 + 1) % 3].data_ptr()
+                    ib.counter_ptr = self.counter_dev.data_ptr() + 8 * k2
+                    self.fio_b[(k2, k3)] = ib
         # the prologue behavior fwd (step 0) uses its own RNG counter so it never repeats step 1's draws
         self.io_b0 = self._io_behavior(0)
         self.io_b0.counter_ptr = None
@@ -196,6 +233,8 @@ class RolloutEngine:
 
     def _step_launch(self):
         """Step t: env(t) -> [target fwd(t) + behavior fwd(t+1)] in ONE launch -> TD/store(t)."""
+        if self.fused:
+            return self._step_launch_fused()
         s = stream_handle(self.device)
         L = lib()
         t = self.t
@@ -243,6 +282,45 @@ class RolloutEngine:
             self._td_pending = True
         self.t += 1
 
+    def _step_launch_fused(self):
+        """Step t in ONE launch (mm_rollout_step): env(t) + target fwd(t) + behavior fwd(t+1), the TD/store of
+        step t-1 folded in; the chunk's last step adds the PER insert with its own TD/store."""
+        s = stream_handle(self.device)
+        L = lib()
+        t = self.t
+        c, k2, k3 = t % self.C, t % 2, t % 3
+        if not self._primed:
+            self._prologue(s)
+        x = RollStepIO()
+        x.act, x.store_obs, x.row_stride = ptr(self.act_buf[k3]), ptr(self.store.obs), self.store.row_stride
+        x.slot, x.chunk_len, x.begin = c + 1, self.C, int(c == 0)
+        x.staging, x.cur_row = ptr(self.staging), ptr(self.cur_row)
+        x.rew, x.done, x.state_in, x.counter = ptr(self.rew_buf[k2]), ptr(self.done_buf[k2]), k2, ptr(self.counter_dev)
+        if c >= 1 and not self._td_flushed:
+            kp, kp3 = 1 - k2, (t - 1) % 3
+            x.td_on, x.td_slot, x.gamma = 1, c - 1, self.gamma
+            x.td_rew, x.td_done = ptr(self.rew_buf[kp]), ptr(self.done_buf[kp])
+            x.td_qsel, x.td_maxq, x.td_act = ptr(self.qsel_buf[kp3]), ptr(self.maxq_buf[kp]), ptr(self.act_buf[kp3])
+            x.chunk_td = ptr(self.chunk_td)
+            x.store_act, x.store_rew, x.store_done = ptr(self.store.act), ptr(self.store.rew), ptr(self.store.done)
+        self._td_flushed = False
+        self.behavior.pack(s)
+        self.target.pack(s)
+        check(L.mm_rollout_step(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
+                                ctypes.byref(self.fio_t[k2]), ptr(self.behavior.packed),
+                                ctypes.byref(self.fio_b[(k2, k3)]), self.E, ctypes.byref(x), s), "rollout_step")
+        if c == self.C - 1:
+            check(L.mm_per_insert_td(self.per._h, self.E, self.N, self.gamma, ptr(self.rew_buf[k2]),
+                                     ptr(self.done_buf[k2]), ptr(self.qsel_buf[k3]), ptr(self.maxq_buf[k2]),
+                                     ptr(self.act_buf[k3]), ptr(self.chunk_td), c, self.C, ptr(self.store.act),
+                                     ptr(self.store.rew), ptr(self.store.done), None, ptr(self.staging), None, s),
+                  "per_insert_td")
+            self.chunks_inserted += self.E
+            self._td_pending = False
+        else:
+            self._td_pending = True
+        self.t += 1
+
     def flush_td(self):
         """Write the last step's TD / transition store now (eager use: it is otherwise fused into the
         next step's env launch); the next step then runs the unfused env kernel."""
@@ -253,14 +331,23 @@ class RolloutEngine:
             self._td_flushed = True
 
     def _td_standalone(self, s, k, c):
-        check(lib().mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(self.rew), ptr(self.done_buf[k]),
-                                          ptr(self.qsel_buf[k]), ptr(self.maxq), ptr(self.act_buf[k]),
+        if self.fused:   # step t = self.t - 1: its buffers by parity / ring slot; the RNG counter is per launch
+            t = self.t - 1
+            rew, qsel, maxq, act, ctr = (self.rew_buf[t % 2], self.qsel_buf[t % 3], self.maxq_buf[t % 2],
+                                         self.act_buf[t % 3], None)
+        else:
+            rew, qsel, maxq, act, ctr = self.rew, self.qsel_buf[k], self.maxq, self.act_buf[k], ptr(self.counter_dev)
+        check(lib().mm_td_chunk_step_rows(self.E, self.N, self.gamma, ptr(rew), ptr(self.done_buf[k]),
+                                          ptr(qsel), ptr(maxq), ptr(act),
                                           ptr(self.chunk_td), c, self.C, ptr(self.store.act), ptr(self.store.rew),
-                                          ptr(self.store.done), ptr(self.staging), ptr(self.counter_dev), s),
+                                          ptr(self.store.done), ptr(self.staging), ctr, s),
               "td_chunk")
 
     # ------------------------------------------------------------------ HIP graph replay
     def graph_steps(self):
+        """Steps after which every parity-indexed buffer is back at its start (the graph cycle)."""
+        if self.fused:
+            return self.C * 6 // math.gcd(self.C, 6)
         return self.C if self.C % 2 == 0 else 2 * self.C
 
     def capture(self):
@@ -417,6 +504,20 @@ class RolloutEngine:
                                     ptr(self.act_buf[kp]), ptr(self.chunk_td), 1, self.C, ptr(self.store.act),
                                     ptr(self.store.rew), ptr(self.store.done), ptr(self.staging), ptr(self.counter_dev),
                                     s), "env_step_td")
+
+    def fused_step_only(self, t=1):
+        """The fused mode's one launch on its own (mid-chunk phase t, no TD fold); for timing. Reads env state
+        buffer t % 2 and writes the other, so repeated launches recompute the same transition."""
+        s = stream_handle(self.device)
+        c, k2, k3 = t % self.C, t % 2, t % 3
+        x = RollStepIO()
+        x.act, x.store_obs, x.row_stride = ptr(self.act_buf[k3]), ptr(self.store.obs), self.store.row_stride
+        x.slot, x.chunk_len, x.begin = c + 1, self.C, 0
+        x.staging, x.cur_row = ptr(self.staging), ptr(self.cur_row)
+        x.rew, x.done, x.state_in, x.counter = ptr(self.rew_buf[k2]), ptr(self.done_buf[k2]), k2, ptr(self.counter_dev)
+        check(lib().mm_rollout_step(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
+                                    ctypes.byref(self.fio_t[k2]), ptr(self.behavior.packed),
+                                    ctypes.byref(self.fio_b[(k2, k3)]), self.E, ctypes.byref(x), s), "rollout_step")
 
     def fused_forward(self, k=0):
         """The step's dominant launch on its own (target fwd + behavior fwd); for timing."""

@@ -29,6 +29,9 @@ class VecEnv:
         r, c = c_i32(), c_i32()
         lib().mm_env_grid_shape(h, ctypes.byref(r), ctypes.byref(c))
         self.rows, self.cols = r.value, c.value
+        # which of the two state buffers holds the live state (the fused rollout step alternates them;
+        # RolloutEngine installs its step parity here)
+        self.state_buffer = lambda: 0
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -82,8 +85,8 @@ class VecEnv:
         grid = np.empty((self.E, self.rows, self.cols), np.int8)
         steps = np.empty(self.E, np.int32)
         apples = np.empty(self.E, np.int32)
-        check(lib().mm_env_get_state(self._h, pos.ctypes.data, prev.ctypes.data, grid.ctypes.data,
-                                     steps.ctypes.data, apples.ctypes.data), "env_get_state")
+        check(lib().mm_env_get_state_buf(self._h, self.state_buffer(), pos.ctypes.data, prev.ctypes.data,
+                                         grid.ctypes.data, steps.ctypes.data, apples.ctypes.data), "env_get_state")
         return pos, prev, grid, steps, apples
 
     def set_state(self, pos, prev, grid, steps, apples):
@@ -94,8 +97,8 @@ class VecEnv:
         steps = np.ascontiguousarray(steps, np.int32)
         apples = np.ascontiguousarray(apples, np.int32)
         assert pos.shape == prev.shape == (self.E, self.N, 2) and grid.shape == (self.E, self.rows, self.cols)
-        check(lib().mm_env_set_state(self._h, pos.ctypes.data, prev.ctypes.data, grid.ctypes.data,
-                                     steps.ctypes.data, apples.ctypes.data), "env_set_state")
+        check(lib().mm_env_set_state_buf(self._h, self.state_buffer(), pos.ctypes.data, prev.ctypes.data,
+                                         grid.ctypes.data, steps.ctypes.data, apples.ctypes.data), "env_set_state")
 
     # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)
     def checkpoint_tensors(self):

@@ -90,13 +90,16 @@ class QTrainer:
         G = eng.graph_steps()
         left = int(n_steps)
         while left > 0:
-            if eng.t % G == 0 and left >= G and self.track_score and G == C:
+            if eng.t % C == 0 and left >= C and self.track_score:
                 self._rows.copy_(eng.staging)            # rows this chunk is written into
-                eng.run_graph()
+                if G == C:
+                    eng.run_graph()
+                else:                                    # graph cycle of several chunks: one region graph per chunk
+                    eng.run_region(C)
                 check(lib().mm_chunk_score(eng.E, C, eng.N, ptr(eng.store.rew), ptr(eng.store.done),
                                            ptr(self._rows), ptr(self.ep_ret), ptr(self.score_acc),
                                            stream_handle(self.device)), "chunk_score")
-                left -= G
+                left -= C
             else:
                 k = G if (eng.t % G == 0 and left >= G) else 1
                 eng.run_steps(k)

@@ -1,0 +1,98 @@
+"""GPU: the fused one-launch rollout step (mm_rollout_step, RolloutEngine(fused=True)) against the two-launch
+step (env kernel + dual forward) and against the oracle env.
+
+The fused kernel runs the same restated Checkers dynamics and the same fp16x3 / exact-f32 forward bodies, so
+every stored transition, hidden state, chunk priority, PER tree and env state must be BIT-identical to the
+two-launch engine with the same seed, through chunk starts (slot-0 writes), chunk ends (PER insert with the
+TD fold), auto-resets, flush_td and graph replay; the env side is also checked bit-exact against
+oracle/env.py step by step."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.env import EnvSpec, VecEnvOracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _state(e):
+    torch.cuda.synchronize()
+    st = [e.store.obs, e.store.act, e.store.rew, e.store.done, e.h, e.ht, e.chunk_td, e.cur_row, e.staging,
+          e.per.tree(), e.per.slot_rows(), e.act, e.last_rew, e.last_done, e.counter_dev[e.t % 2 if e.fused else 0]]
+    return [x.detach().clone().cpu() for x in st] + [torch.as_tensor(v) for v in e.env.get_state()]
+
+
+def _pair(E, f1, g, h, seed, guard=False):
+    from minimarl.engine import RolloutEngine
+    kw = dict(f1=f1, g=g, h=h, chunk=10, capacity=4 * E, seed=seed, device=DEV)
+    a = RolloutEngine(E, 8, fused=False, **kw)
+    b = RolloutEngine(E, 8, fused=True, **kw)
+    assert b.fused and not a.fused and b.graph_steps() == 30
+    if guard:   # agent 3 beyond the fp16 range: both engines run it on the exact-f32 image
+        for eng in (a, b):
+            with torch.no_grad():
+                eng.behavior.view("W1")[3, 0, :] = 3.0e3
+            eng.behavior.mark_dirty()
+            eng.sync_target()
+    return a, b
+
+
+@pytest.mark.parametrize("E,f1,g,h,guard", [(2048, 64, 64, 64, False), (2200, 64, 32, 32, False),
+                                            (2048, 64, 64, 64, True)])
+def test_fused_step_bit_identical_to_two_launch(E, f1, g, h, guard):
+    a, b = _pair(E, f1, g, h, seed=21, guard=guard)
+    spec = EnvSpec(8, 100)
+    ora = VecEnvOracle(spec, E)
+    for t in range(34):
+        rows = b.staging.cpu().numpy()
+        a.step(0.3)
+        b.step(0.3)
+        if t == 14:
+            a.flush_td()
+            b.flush_td()
+        c = t % 10
+        act = b.act.cpu().numpy().astype(np.int64)
+        nxt, rew, done = ora.step(act)
+        np.testing.assert_array_equal(b.store.obs[rows, c + 1].cpu().numpy(), nxt)
+        if c == 0:
+            np.testing.assert_array_equal(b.store.obs[rows, 0].cpu().numpy(), a.store.obs[rows, 0].cpu().numpy())
+        np.testing.assert_array_equal(b.last_rew.cpu().numpy(), rew)
+        np.testing.assert_array_equal(b.last_done.cpu().numpy().astype(bool), done)
+        ora.reset_envs(done)
+        if c == 9 or t == 14:
+            for i, (x, y) in enumerate(zip(_state(a), _state(b))):
+                assert torch.equal(x, y), (t, i)
+    a.flush_td()
+    b.flush_td()
+    for i, (x, y) in enumerate(zip(_state(a), _state(b))):
+        assert torch.equal(x, y), ("end", i)
+    pos, prev, grid, steps, apples = b.env.get_state()
+    np.testing.assert_array_equal(pos, ora.pos)
+    np.testing.assert_array_equal(prev, ora.prev)
+    np.testing.assert_array_equal(grid, ora.grid)
+    np.testing.assert_array_equal(steps, ora.steps)
+    np.testing.assert_array_equal(apples, ora.apples)
+
+
+def test_fused_region_graphs_match_eager():
+    """bench.py's timed regions on the fused engine (30-step graph cycle): region graphs from several phases,
+    chunk graphs and single-step graphs replay bit-identically to eager fused steps."""
+    from minimarl.engine import RolloutEngine
+    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=2 * 2048, seed=23, device=DEV)
+    a = RolloutEngine(2048, 8, fused=True, **kw)
+    b = RolloutEngine(2048, 8, fused=True, **kw)
+    for _ in range(77):
+        a.step(0.3)
+    a.flush_td()
+    b.run_steps(3, 0.3)
+    b.capture_region(20)
+    b.run_steps(20, 0.3)                      # region graph, phase 3
+    b.capture_region(20, start=b.t + 20)
+    b.run_steps(20, 0.3)                      # phase 23
+    b.run_steps(20, 0.3)                      # phase 13: chunk / single-step graphs
+    b.run_steps(14, 0.3)
+    b.flush_td()
+    assert a.t == b.t == 77
+    for i, (x, y) in enumerate(zip(_state(a), _state(b))):
+        assert torch.equal(x, y), i
