@@ -695,13 +695,15 @@ __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t ca
 //   B sel2    each block picks the threshold's bin b1; histogram of bits 51..40 of the keys in b1
 //   C sel3    each block picks b2; keys with the 24-bit prefix (b1, b2) listed with their slots,
 //             per-block counts of the keys below the prefix
-//   D apply   each block radix-selects the exact key T among the listed keys (8-bit digits over bits
-//             39..0) and its own victim offsets, writes its victims / free slots ((td + eps)^alpha, row
+//   D apply   each block radix-selects the exact key T among the listed keys (8-bit digits over the bits
+//             below the candidates' common prefix; ties — equal priorities are common: envs that stayed
+//             greedy since an episode start repeat each other's chunks — cost no passes) and its own victim
+//             offsets, writes its victims / free slots ((td + eps)^alpha, row
 //             swaps) and rebuilds its 1024-leaf subtree from LDS; the last block (ticket) builds the top
 //             levels and updates n_data
 constexpr int MB_T = 256, MB_VPT = 4, MB_SLOTS = MB_T * MB_VPT;   // 1024 slots per block
 constexpr int64_t MB_MIN_CAP = 16384;
-constexpr int MB_CAND_LDS = 4096;
+constexpr int MB_CAND_LDS = 14336;   // listed keys cached in the apply block's LDS (112 KiB)
 constexpr int MB_MAX_BLOCKS = 1024;
 struct MbScratch {
   uint32_t hist1[4096];
@@ -903,12 +905,19 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = base + threadIdx.x + i * MB_T;
-    if (sl < n_data) {
-      const uint64_t k = leaf_key(leaves, sl);
-      const uint64_t kp = k >> 40;
-      below += kp < pre ? 1u : 0u;
-      if (kp == pre) {
-        const uint32_t at = atomicAdd(&mb->cand_n, 1u);
+    const uint64_t k = sl < n_data ? leaf_key(leaves, sl) : ~0ull;
+    below += (sl < n_data && (k >> 40) < pre) ? 1u : 0u;
+    // list the keys with the prefix: one cand_n reservation per wave (a tie-heavy threshold bin can hold
+    // tens of thousands of keys, and per-key atomics on one counter serialize)
+    const bool is_c = sl < n_data && (k >> 40) == pre;
+    const uint64_t m = __ballot(is_c);
+    if (m) {
+      const int lane = threadIdx.x & 63;
+      uint32_t at0 = 0;
+      if (lane == __builtin_ctzll(m)) at0 = atomicAdd(&mb->cand_n, (uint32_t)__popcll(m));
+      at0 = __shfl(at0, __builtin_ctzll(m));
+      if (is_c) {
+        const uint32_t at = at0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         ckey[at] = k;
         cslot[at] = (uint64_t)sl;
       }
@@ -922,6 +931,46 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
 // The exact threshold key T among the listed candidates (radix select over bits 39..0 below the 24-bit
 // prefix) and this workgroup's victim offsets: lt_off = keys < T in the workgroups before it (their keys
 // below the prefix + their listed keys < T), eq_off = listed keys == T in them. Run by every workgroup.
+// Block-wide min / max of a u64 (MB_T threads); every thread gets both.
+__device__ __forceinline__ void mb_minmax(uint64_t& lo, uint64_t& hi, uint64_t* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * wave] = lo;
+    red[2 * wave + 1] = hi;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < MB_T / 64; ++w) {
+    lo = red[2 * w] < lo ? red[2 * w] : lo;
+    hi = red[2 * w + 1] > hi ? red[2 * w + 1] : hi;
+  }
+  __syncthreads();
+}
+
+// bins[bin] += 1 for this lane when on: one LDS atomic per wave when every active lane has the same bin (the
+// common case inside a tie-heavy candidate list), per-lane atomics otherwise
+__device__ __forceinline__ void mb_bin_add(uint32_t* bins, bool on, uint32_t bin) {
+  const uint64_t act = __ballot(on);
+  if (!act) return;
+  const int first = __builtin_ctzll(act);
+  const uint32_t b0 = __shfl(bin, first);
+  if (__ballot(on && bin == b0) == act) {
+    if ((threadIdx.x & 63) == first) atomicAdd(&bins[b0], (uint32_t)__popcll(act));
+  } else if (on) {
+    atomicAdd(&bins[bin], 1u);
+  }
+}
+
+// The exact threshold key T among the listed candidates (radix select below the 24-bit prefix, over the bits
+// where the listed keys differ at all: a list of equal keys needs no pass) and this workgroup's victim offsets:
+// lt_off = keys < T in the workgroups before it (their keys below the prefix + their listed keys < T), eq_off =
+// listed keys == T in them. Run by every workgroup.
 __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uint32_t* bins, uint32_t* wsum,
                              int64_t* sh, uint64_t& T, int64_t& take_eq, int64_t& lt_off, int64_t& eq_off) {
   const uint64_t pre = mb->sel[2];
@@ -930,17 +979,29 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
   const uint64_t* cslot = mb->cand + cap;
   const uint32_t m = mb->cand_n;
   const bool in_lds = m <= (uint32_t)MB_CAND_LDS;
-  if (in_lds)
-    for (uint32_t i = threadIdx.x; i < m; i += MB_T) cl[i] = ckey[i];
-  __syncthreads();
-  uint64_t prefix = pre << 40;
-  for (int shift = 32; shift >= 0; shift -= 8) {
+  uint64_t lo = ~0ull, hi = 0;
+  for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
+    const uint64_t k = ckey[i];
+    if (in_lds) cl[i] = k;
+    lo = k < lo ? k : lo;
+    hi = k > hi ? k : hi;
+  }
+  mb_minmax(lo, hi, reinterpret_cast<uint64_t*>(bins));   // (also the barrier after the LDS fill)
+  // bits of the listed keys above the highest differing one are common: start the 8-bit digits below them
+  uint64_t prefix = m ? lo & (lo == hi ? ~0ull : (~0ull << (64 - __clzll(lo ^ hi)))) : (pre << 40);
+  int top = (lo == hi || !m) ? -1 : 63 - __clzll(lo ^ hi);   // highest differing bit
+  for (int shift = top - 7; top >= 0; shift -= 8) {
+    const int sft = shift < 0 ? 0 : shift;
+    const int width = shift < 0 ? shift + 8 : 8;           // the last digit may be narrower
     for (int i = threadIdx.x; i < 256; i += MB_T) bins[i] = 0;
     __syncthreads();
-    const uint64_t hmask = ~0ull << (shift + 8);
-    for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
-      const uint64_t k = in_lds ? cl[i] : ckey[i];
-      if ((k & hmask) == prefix) atomicAdd(&bins[(k >> shift) & 255], 1u);
+    const uint64_t hmask = ~0ull << (sft + width);
+    const uint32_t dmask = (1u << width) - 1u;
+    for (uint32_t i0 = 0; i0 < m; i0 += MB_T) {
+      const uint32_t i = i0 + threadIdx.x;
+      const uint64_t k = i < m ? (in_lds ? cl[i] : ckey[i]) : 0;
+      const bool on = i < m && (k & hmask) == prefix;
+      mb_bin_add(bins, on, (uint32_t)(k >> sft) & dmask);
     }
     __syncthreads();
     const uint32_t v = bins[threadIdx.x];
@@ -951,9 +1012,10 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
       sh[1] = need - before;
     }
     __syncthreads();
-    prefix |= (uint64_t)sh[0] << shift;
+    prefix |= (uint64_t)sh[0] << sft;
     need = sh[1];
     __syncthreads();
+    if (shift <= 0) break;
   }
   T = prefix;        // the rest-th smallest key; the first `need` slots equal to it are taken
   take_eq = need;

@@ -186,7 +186,9 @@ def test_per_golden_sequence_single_inserts(golden, flavor):
                                                   ("vdn", 2048, 700, 7), ("qmix", 8192, 3000, 6),
                                                   # >= 16384: the multi-block insert
                                                   ("qmix", 65536, 8192, 10), ("vdn", 16384, 5000, 8),
-                                                  ("qmix", 32768, 4096, 12)])
+                                                  ("qmix", 32768, 4096, 12),
+                                                  # clustered priorities: threshold bins of ~all leaves
+                                                  ("qmix", 65536, 16384, 8)])
 def test_per_batched_vs_oracle(flavor, cap, kb, rounds):
     dev, ora = _per_pair(flavor, cap)
     rng = np.random.default_rng(1)
@@ -196,6 +198,8 @@ def test_per_batched_vs_oracle(flavor, cap, kb, rounds):
             td[:50] = td[50]                       # ties
         if cap == 32768 and rnd in (3, 4, 5, 6, 7, 8, 9):
             td[:] = 0.5                            # whole rounds of equal priorities (huge tie sets)
+        if kb == 16384 and rnd >= 3:               # one 24-bit key prefix, ties mixed with distinct keys
+            td = (0.5 + np.floor(rng.random(kb) * 300) * 1e-7).astype(np.float32)
         slots = dev.add(torch.tensor(td))
         oslots = ora.add_batch([float(x) for x in td])
         np.testing.assert_array_equal(slots.cpu().numpy(), oslots)
