@@ -57,6 +57,10 @@ int mm_qnet_param_offsets(const mm_qnet_dims* d, int64_t offs[11]);
 int64_t mm_qnet_packed_count(const mm_qnet_dims* d);
 /* Repack flat params into the fragment image (call after every optimizer step). */
 int mm_qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s);
+/* Repack only the exact-f32 fragment image (the learner's own forward after an Adam step; ~1/4 of the
+ * full pack's time). The fp16x3 image and its safety flags are left stale: call mm_qnet_pack before the
+ * next large-E (fp16x3) forward. */
+int mm_qnet_pack_f32(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s);
 
 enum { MM_Q_NONE = 0, MM_Q_ACT = 1, MM_Q_MAX = 2, MM_Q_GATHER = 3 };
 

@@ -2234,19 +2234,21 @@ __device__ void qnet_h3_bound_block(const float* __restrict__ params, int* flags
 
 // both images (f32 fragments, fp16x3 split) from the canonical parameters in ONE launch; the last N
 // blocks compute the per-agent fp16x3 safety flags
+// f32_only: the exact-f32 image alone (no fp16x3 image, no flag blocks) — what the learner's own exact forward
+// reads after each Adam step; the rollout's fp16x3 image is refreshed lazily by a full pack before its next use
 __global__ __launch_bounds__(1024) void qnet_pack_kernel(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g, int N,
-                                 int D, int F1, int G, int H, int A, QnetOffsets o) {
-  const int nb = (int)gridDim.x - N;
+                                 int D, int F1, int G, int H, int A, QnetOffsets o, int f32_only) {
+  const int nb = (int)gridDim.x - (f32_only ? 0 : N);
   if ((int)blockIdx.x >= nb) {
     qnet_h3_bound_block(params, reinterpret_cast<int*>(packed + 2 * g.agent_stride * N), (int)blockIdx.x - nb, D,
                         F1, G, H, A, o);
     return;
   }
   qnet_pack_body(params, packed, g, N, D, F1, G, H, A, o, nb);
-  qnet_pack_h3_body(params, packed, g, N, D, F1, G, H, A, o, nb);
+  if (!f32_only) qnet_pack_h3_body(params, packed, g, N, D, F1, G, H, A, o, nb);
 }
 
-int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s) {
+int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s, int f32_only) {
   QnetGeo g;
   QnetOffsets o;
   int rc = qnet_geometry(d, &g, &o);
@@ -2254,9 +2256,9 @@ int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStre
   const int64_t total = g.agent_stride * d->n_agents;
   // 1024-thread blocks: the N flag blocks' scans and row bounds are latency chains, 16 waves each
   const int threads = 1024;
-  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 1024) + d->n_agents;
+  const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 1024) + (f32_only ? 0 : d->n_agents);
   hipLaunchKernelGGL(qnet_pack_kernel, dim3(blocks), dim3(threads), 0, s, params, packed, g, d->n_agents,
-                     d->obs_dim, d->f1, d->g, d->h, d->n_actions, o);
+                     d->obs_dim, d->f1, d->g, d->h, d->n_actions, o, f32_only);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

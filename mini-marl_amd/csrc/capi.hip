@@ -17,7 +17,7 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s);
+int qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, hipStream_t s, int f32_only);
 int agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
                      const float* packed1, const mm_qfwd_io* io1, int64_t e1, int32_t steps, const uint8_t* reset,
                      hipStream_t s);
@@ -56,7 +56,12 @@ int64_t mm_qnet_packed_count(const mm_qnet_dims* d) {
 
 int mm_qnet_pack(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s) {
   MM_REQUIRE(params && packed, "qnet_pack: null pointer");
-  return mm::qnet_pack(d, params, packed, (hipStream_t)s);
+  return mm::qnet_pack(d, params, packed, (hipStream_t)s, 0);
+}
+
+int mm_qnet_pack_f32(const mm_qnet_dims* d, const float* params, float* packed, mm_stream_t s) {
+  MM_REQUIRE(params && packed, "qnet_pack_f32: null pointer");
+  return mm::qnet_pack(d, params, packed, (hipStream_t)s, 1);
 }
 
 int mm_agent_q_fwd(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,

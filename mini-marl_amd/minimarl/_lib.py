@@ -69,6 +69,7 @@ _SIGS = [
     ("mm_qnet_param_offsets", c_i32, [ctypes.POINTER(QnetDims), ctypes.POINTER(c_i64)]),
     ("mm_qnet_packed_count", c_i64, [ctypes.POINTER(QnetDims)]),
     ("mm_qnet_pack", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_vp, c_vp]),
+    ("mm_qnet_pack_f32", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_vp, c_vp]),
     ("mm_agent_q_fwd", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp]),
     ("mm_agent_q_fwd2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
                                 ctypes.POINTER(QFwdIO), c_i64, c_vp]),

@@ -287,8 +287,8 @@ class QLearner:
             self._push_double_eps()
         B, C, N, H, D = self.B, self.C, self.N, self.H, self.D
         CB = C * B
-        self.beh.pack(s)
-        self.tgt.pack(s)
+        self._pack(self.beh, s)
+        self._pack(self.tgt, s)
         obs_p = ctypes.c_void_p(obs_base) if isinstance(obs_base, int) else ptr(obs_base)
         reset_p = ctypes.c_void_p(reset_obs_ptr) if isinstance(reset_obs_ptr, int) else ptr(reset_obs_ptr)
         ND = N * D
@@ -506,8 +506,20 @@ class QLearner:
                                      self.clip, self.lr, self.b1, self.b2, self.aeps, ptr(self.step_dev),
                                      ptr(self.partials), ptr(self.norm), float(grad_scale), s), "clip_adam")
         self.beh.mark_dirty()
-        self.beh.pack(s)
+        self._pack(self.beh, s)
         self.updates += 1
+
+    def _uses_h3(self):
+        """Whether this learner's own forward reads the fp16x3 image (the opt-in fast PRE)."""
+        return self.mixer_fp16 and self.C * self.B >= 2048 and self.fast_pre
+
+    def _pack(self, net, s=None):
+        """Repack what the learner's forward reads: the exact-f32 image only, unless the fast PRE runs (the
+        rollout's fp16x3 image is then refreshed lazily by its own full pack before the next rollout step)."""
+        if self._uses_h3():
+            net.pack(s)
+        else:
+            net.pack_f32(s)
 
     def train_step(self, obs_base, reset_obs_ptr):
         self.compute_grads(obs_base, reset_obs_ptr)
@@ -638,8 +650,8 @@ class QLearner:
         graphs (the RCCL all-reduce, when used, runs between them eagerly; its 1/world scale is baked
         into the second graph from ``_graph_scale``). ``per=None`` captures the update of the batch
         placed by ``load_batch`` instead (no sampling, no priority update)."""
-        self.beh.pack()
-        self.tgt.pack()
+        self._pack(self.beh)
+        self._pack(self.tgt)
         self._push_double_eps()
         torch.cuda.synchronize(self.dev)
         n0 = self.updates
@@ -673,8 +685,8 @@ class QLearner:
 
     def replay_update(self, allreduce=None):
         g1, g2 = self.graphs
-        self.tgt.pack()                 # target synced since capture: repack eagerly (no-op otherwise)
-        self.beh.pack()
+        self._pack(self.tgt)            # target synced since capture: repack eagerly (no-op otherwise)
+        self._pack(self.beh)
         self._push_double_eps()
         if allreduce is None and getattr(self, "graph_fused", None) is not None:
             self.graph_fused.replay()
@@ -683,6 +695,8 @@ class QLearner:
             if allreduce is not None:
                 allreduce(self.Gr)      # the 1/world scale was baked at capture (set _graph_scale first)
             g2.replay()
+        if not self._uses_h3():
+            self.beh.mark_h3_stale()    # the graph refreshed the f32 image only
         self.updates += 1
 
     # ------------------------------------------------------------------ checkpoint (minimarl.checkpoint)

@@ -87,6 +87,7 @@ class AgentQNet:
             check(-22, "qnet_packed_count")
         self.packed = torch.zeros(n_packed, dtype=torch.float32, device=self.device)
         self._dirty = True
+        self._h3_stale = False      # exact-f32 image current, fp16x3 image + flags not (pack_f32)
         if seed is not None:
             self.init_default(seed)
 
@@ -148,10 +149,23 @@ class AgentQNet:
         self.mark_dirty()
 
     def pack(self, stream=None):
-        if self._dirty:
+        """Both fragment images (exact f32 and fp16x3) + the fp16x3 range flags, when the params changed."""
+        if self._dirty or self._h3_stale:
             check(lib().mm_qnet_pack(ctypes.byref(self.dims), ptr(self.flat), ptr(self.packed),
                                      stream or stream_handle(self.device)), "qnet_pack")
-            self._dirty = False
+            self._dirty = self._h3_stale = False
+
+    def pack_f32(self, stream=None):
+        """Only the exact-f32 image (the learner's own forward after an Adam step); the fp16x3 image is then
+        repacked by the next ``pack`` (the rollout's, before its next large-E forward)."""
+        if self._dirty:
+            check(lib().mm_qnet_pack_f32(ctypes.byref(self.dims), ptr(self.flat), ptr(self.packed),
+                                         stream or stream_handle(self.device)), "qnet_pack_f32")
+            self._dirty, self._h3_stale = False, True
+
+    def mark_h3_stale(self):
+        """The exact-f32 image was refreshed by a replayed graph (pack_f32 captured): only the fp16x3 image is old."""
+        self._dirty, self._h3_stale = False, True
 
     # ------------------------------------------------------------------ forward
     def forward_io(self, n_envs, io, stream=None):

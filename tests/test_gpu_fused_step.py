@@ -96,3 +96,35 @@ def test_fused_region_graphs_match_eager():
     assert a.t == b.t == 77
     for i, (x, y) in enumerate(zip(_state(a), _state(b))):
         assert torch.equal(x, y), i
+
+
+def test_learner_repacks_f32_image_and_rollout_refreshes_fp16x3_image():
+    """After an Adam step the learner's graph repacks only the exact-f32 image (mm_qnet_pack_f32, what its own
+    forward reads); the rollout's next full pack then refreshes the fp16x3 image and flags, so the packed buffer
+    is bit-identical to a fresh full pack of the updated parameters."""
+    from minimarl.engine import RolloutEngine
+    from minimarl.learner import Mixer, QLearner
+    from minimarl.qnet import AgentQNet
+    eng = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, device=DEV)
+    for _ in range(2):
+        eng.run_graph(0.5)
+    N, D = eng.N, eng.D
+    mix, tmix = Mixer(N, N * D, 64, 32, DEV, seed=7), Mixer(N, N * D, 64, 32, DEV, seed=7)
+    lrn = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device=DEV)
+    lrn.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=1)
+    before = eng.behavior.packed.clone()
+    lrn.replay_update()
+    lrn.replay_update()
+    assert eng.behavior._h3_stale and not eng.behavior._dirty
+    torch.cuda.synchronize()
+    ref = AgentQNet(N, D, 5, 64, 64, 64, DEV)
+    ref.flat.copy_(eng.behavior.flat)
+    ref.mark_dirty()
+    ref.pack()
+    f32_len = (ref.packed.numel() - 64) // 2   # [f32 image | fp16x3 image | flags (padded to 64)]
+    assert torch.equal(ref.packed[:f32_len], eng.behavior.packed[:f32_len])        # f32 image current
+    assert not torch.equal(before[:f32_len], eng.behavior.packed[:f32_len])        # ... and it did change
+    eng.step(0.1)                                                                   # the rollout's full pack
+    torch.cuda.synchronize()
+    assert not eng.behavior._h3_stale
+    assert torch.equal(ref.packed, eng.behavior.packed)
