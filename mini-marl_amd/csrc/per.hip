@@ -694,7 +694,7 @@ __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t ca
 //             12-bit histogram (sign + exponent) of the candidate keys
 //   B sel2    each block picks the threshold's bin b1; histogram of bits 51..40 of the keys in b1
 //   C sel3    each block picks b2; keys with the 24-bit prefix (b1, b2) listed with their slots,
-//             per-block counts of the keys below the prefix
+//             histogram of their bits 39..28, per-block counts of the keys below the prefix
 //   D apply   each block radix-selects the exact key T among the listed keys (8-bit digits over the bits
 //             below the candidates' common prefix; ties — equal priorities are common: envs that stayed
 //             greedy since an episode start repeat each other's chunks — cost no passes) and its own victim
@@ -703,11 +703,12 @@ __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t ca
 //             levels and updates n_data
 constexpr int MB_T = 256, MB_VPT = 4, MB_SLOTS = MB_T * MB_VPT;   // 1024 slots per block
 constexpr int64_t MB_MIN_CAP = 16384;
-constexpr int MB_CAND_LDS = 14336;   // listed keys cached in the apply block's LDS (112 KiB)
+constexpr int MB_CAND_LDS = 12288;   // keys with the 36-bit prefix compacted into the apply block's LDS
 constexpr int MB_MAX_BLOCKS = 1024;
 struct MbScratch {
   uint32_t hist1[4096];
   uint32_t hist2[4096];
+  uint32_t hist3[4096];              // bits 39..28 of the keys with the 24-bit prefix (sel3), read by apply
   uint32_t blk[2 * MB_MAX_BLOCKS];   // C: per block #keys below the 24-bit prefix; then victim offsets
   uint32_t cand_n;
   uint32_t ticket;
@@ -832,6 +833,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel1(const double* __restrict__ t
   if (tdf.on) mb_td_fold(tdf, K, td_n, shtd);
   // the candidate list of the previous insert was last read by its apply launch, which has finished
   if (blockIdx.x == 0 && threadIdx.x == 0) mb->cand_n = 0;
+  for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist3[i] = 0;
   const int64_t n_data = st->n_data;
   if (K - min(K, cap - n_data) <= 0) return;
   const double* leaves = tree + (cap - 1);
@@ -882,10 +884,25 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ t
     if (h[i]) atomicAdd(&mb->hist2[i], h[i]);
 }
 
+// bins[bin] += 1 for this lane when on: one LDS atomic per wave when every active lane has the same bin (the
+// common case inside a tie-heavy candidate list), per-lane atomics otherwise
+__device__ __forceinline__ void mb_bin_add(uint32_t* bins, bool on, uint32_t bin) {
+  const uint64_t act = __ballot(on);
+  if (!act) return;
+  const int first = __builtin_ctzll(act);
+  const uint32_t b0 = __shfl(bin, first);
+  if (__ballot(on && bin == b0) == act) {
+    if ((threadIdx.x & 63) == first) atomicAdd(&bins[b0], (uint32_t)__popcll(act));
+  } else if (on) {
+    atomicAdd(&bins[bin], 1u);
+  }
+}
+
 __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ tree, int64_t cap, const PerDev* st,
                                                     int64_t K, MbScratch* mb) {
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
+  __shared__ uint32_t h3[4096];
   const int64_t n_data = st->n_data;
   if (K - min(K, cap - n_data) <= 0) return;
   const uint64_t b1 = mb->sel[0];
@@ -897,6 +914,8 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
   }
   // hist1 was last read by sel2 (finished): cleared here for the next insert
   for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist1[i] = 0;
+  for (int i = threadIdx.x; i < 4096; i += MB_T) h3[i] = 0;
+  __syncthreads();
   const double* leaves = tree + (cap - 1);
   uint64_t* ckey = mb->cand;
   uint64_t* cslot = mb->cand + cap;
@@ -910,6 +929,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
     // list the keys with the prefix: one cand_n reservation per wave (a tie-heavy threshold bin can hold
     // tens of thousands of keys, and per-key atomics on one counter serialize)
     const bool is_c = sl < n_data && (k >> 40) == pre;
+    mb_bin_add(h3, is_c, (uint32_t)(k >> 28) & 4095u);   // wave-aggregated: a tie bin is one atomic per wave
     const uint64_t m = __ballot(is_c);
     if (m) {
       const int lane = threadIdx.x & 63;
@@ -924,8 +944,10 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
     }
   }
   uint32_t tb;
-  (void)mb_scan(below, wsum, &tb);
+  (void)mb_scan(below, wsum, &tb);   // (its barriers also order the h3 atomics before the flush)
   if (threadIdx.x == 0) mb->blk[blockIdx.x] = tb;
+  for (int i = threadIdx.x; i < 4096; i += MB_T)
+    if (h3[i]) atomicAdd(&mb->hist3[i], h3[i]);
 }
 
 // The exact threshold key T among the listed candidates (radix select over bits 39..0 below the 24-bit
@@ -953,54 +975,73 @@ __device__ __forceinline__ void mb_minmax(uint64_t& lo, uint64_t& hi, uint64_t* 
   __syncthreads();
 }
 
-// bins[bin] += 1 for this lane when on: one LDS atomic per wave when every active lane has the same bin (the
-// common case inside a tie-heavy candidate list), per-lane atomics otherwise
-__device__ __forceinline__ void mb_bin_add(uint32_t* bins, bool on, uint32_t bin) {
-  const uint64_t act = __ballot(on);
-  if (!act) return;
-  const int first = __builtin_ctzll(act);
-  const uint32_t b0 = __shfl(bin, first);
-  if (__ballot(on && bin == b0) == act) {
-    if ((threadIdx.x & 63) == first) atomicAdd(&bins[b0], (uint32_t)__popcll(act));
-  } else if (on) {
-    atomicAdd(&bins[bin], 1u);
-  }
-}
 
-// The exact threshold key T among the listed candidates (radix select below the 24-bit prefix, over the bits
-// where the listed keys differ at all: a list of equal keys needs no pass) and this workgroup's victim offsets:
-// lt_off = keys < T in the workgroups before it (their keys below the prefix + their listed keys < T), eq_off =
-// listed keys == T in them. Run by every workgroup.
-__device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uint32_t* bins, uint32_t* wsum,
-                             int64_t* sh, uint64_t& T, int64_t& take_eq, int64_t& lt_off, int64_t& eq_off) {
-  const uint64_t pre = mb->sel[2];
+// The exact threshold key T (radix select) and this workgroup's victim offsets: lt_off = keys < T in the
+// workgroups before it, eq_off = keys == T in them. Run by every workgroup. The third histogram (sel3) narrows
+// the 24-bit prefix to 36 bits first, so ONE pass over the listed keys (coalesced, no atomics) counts the
+// earlier workgroups' keys below the 36-bit prefix and compacts those with it into LDS (key, workgroup); the
+// radix digits then run over that short list, from its highest differing bit (a list of equal keys — ties are
+// common: envs that stay greedy from an episode start repeat each other's chunks — needs no pass at all).
+__device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uint16_t* cb, uint32_t* bins,
+                             uint32_t* wsum, int64_t* sh, uint32_t* s_n, uint64_t& T, int64_t& take_eq,
+                             int64_t& lt_off, int64_t& eq_off) {
+  const uint64_t pre24 = mb->sel[2];
   int64_t need = (int64_t)mb->sel[3];
+  const uint64_t pre = (pre24 << 12) | (uint64_t)mb_pick(const_cast<uint32_t*>(mb->hist3), need, wsum, sh);
   const uint64_t* ckey = mb->cand;
   const uint64_t* cslot = mb->cand + cap;
   const uint32_t m = mb->cand_n;
-  const bool in_lds = m <= (uint32_t)MB_CAND_LDS;
+  const uint32_t me = blockIdx.x;
+  if (threadIdx.x == 0) *s_n = 0;
+  __syncthreads();
+  uint32_t lt = 0;
   uint64_t lo = ~0ull, hi = 0;
-  for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
-    const uint64_t k = ckey[i];
-    if (in_lds) cl[i] = k;
-    lo = k < lo ? k : lo;
-    hi = k > hi ? k : hi;
+  for (uint32_t i0 = 0; i0 < m; i0 += MB_T) {
+    const uint32_t i = i0 + threadIdx.x;
+    uint64_t k = 0, blk = 0;
+    if (i < m) {
+      k = ckey[i];
+      blk = cslot[i] / MB_SLOTS;
+    }
+    const uint64_t kp = k >> 28;
+    lt += (i < m && kp < pre && blk < me) ? 1u : 0u;
+    const bool in = i < m && kp == pre;
+    if (in) {
+      lo = k < lo ? k : lo;
+      hi = k > hi ? k : hi;
+    }
+    const uint64_t w = __ballot(in);
+    if (w) {
+      const int lane = threadIdx.x & 63, first = __builtin_ctzll(w);
+      uint32_t at0 = 0;
+      if (lane == first) at0 = atomicAdd(s_n, (uint32_t)__popcll(w));
+      at0 = __shfl(at0, first);
+      const uint32_t at = at0 + (uint32_t)__popcll(w & ((1ull << lane) - 1ull));
+      if (in && at < (uint32_t)MB_CAND_LDS) {
+        cl[at] = k;
+        cb[at] = (uint16_t)blk;
+      }
+    }
   }
-  mb_minmax(lo, hi, reinterpret_cast<uint64_t*>(bins));   // (also the barrier after the LDS fill)
-  // bits of the listed keys above the highest differing one are common: start the 8-bit digits below them
-  uint64_t prefix = m ? lo & (lo == hi ? ~0ull : (~0ull << (64 - __clzll(lo ^ hi)))) : (pre << 40);
-  int top = (lo == hi || !m) ? -1 : 63 - __clzll(lo ^ hi);   // highest differing bit
+  mb_minmax(lo, hi, reinterpret_cast<uint64_t*>(bins));   // (its barriers publish the compacted list)
+  const uint32_t n = *s_n;
+  const bool in_lds = n <= (uint32_t)MB_CAND_LDS;
+  // candidate j of the 36-bit bin: from LDS, or (overflow: tens of thousands of exactly equal keys are the only
+  // way there) filtered from the global list on every pass
+  uint64_t prefix = lo & (lo == hi ? ~0ull : (~0ull << (64 - __clzll(lo ^ hi))));
+  const int top = (n == 0 || lo == hi) ? -1 : 63 - __clzll(lo ^ hi);
   for (int shift = top - 7; top >= 0; shift -= 8) {
     const int sft = shift < 0 ? 0 : shift;
-    const int width = shift < 0 ? shift + 8 : 8;           // the last digit may be narrower
+    const int width = shift < 0 ? shift + 8 : 8;
     for (int i = threadIdx.x; i < 256; i += MB_T) bins[i] = 0;
     __syncthreads();
     const uint64_t hmask = ~0ull << (sft + width);
     const uint32_t dmask = (1u << width) - 1u;
-    for (uint32_t i0 = 0; i0 < m; i0 += MB_T) {
+    const uint32_t cnt = in_lds ? n : m;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += MB_T) {
       const uint32_t i = i0 + threadIdx.x;
-      const uint64_t k = i < m ? (in_lds ? cl[i] : ckey[i]) : 0;
-      const bool on = i < m && (k & hmask) == prefix;
+      const uint64_t k = i < cnt ? (in_lds ? cl[i] : ckey[i]) : 0;
+      const bool on = i < cnt && (k >> 28) == pre && (k & hmask) == prefix;
       mb_bin_add(bins, on, (uint32_t)(k >> sft) & dmask);
     }
     __syncthreads();
@@ -1019,14 +1060,21 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
   }
   T = prefix;        // the rest-th smallest key; the first `need` slots equal to it are taken
   take_eq = need;
-  const uint32_t me = blockIdx.x;
-  uint32_t lt = 0, eq = 0;
+  uint32_t eq = 0;
   for (uint32_t b = threadIdx.x; b < me; b += MB_T) lt += mb->blk[b];
-  for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
-    if ((uint32_t)(cslot[i] / MB_SLOTS) >= me) continue;
-    const uint64_t k = in_lds ? cl[i] : ckey[i];
-    lt += k < T ? 1u : 0u;
-    eq += k == T ? 1u : 0u;
+  if (in_lds) {
+    for (uint32_t i = threadIdx.x; i < n; i += MB_T)
+      if (cb[i] < me) {
+        lt += cl[i] < T ? 1u : 0u;
+        eq += cl[i] == T ? 1u : 0u;
+      }
+  } else {
+    for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
+      const uint64_t k = ckey[i];
+      if ((k >> 28) != pre || (uint32_t)(cslot[i] / MB_SLOTS) >= me) continue;
+      lt += k < T ? 1u : 0u;
+      eq += k == T ? 1u : 0u;
+    }
   }
   uint32_t tl, te;
   (void)mb_scan(lt, wsum, &tl);
@@ -1041,6 +1089,8 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   __shared__ double lv[MB_SLOTS];
   __shared__ double v[2][MB_SLOTS / 2];
   __shared__ uint64_t cl[MB_CAND_LDS];
+  __shared__ uint16_t cb[MB_CAND_LDS];
+  __shared__ uint32_t s_n;
   __shared__ uint32_t bins[256];
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
@@ -1067,7 +1117,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   uint64_t T = 0;
   int64_t take_eq = 0, lt_off = 0, eq_off = 0;
   if (evict) {
-    mb_threshold(mb, cap, cl, bins, wsum, sh, T, take_eq, lt_off, eq_off);
+    mb_threshold(mb, cap, cl, cb, bins, wsum, sh, &s_n, T, take_eq, lt_off, eq_off);
     // hist2 was last read by sel3 (finished): cleared here for the next insert
     for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist2[i] = 0;
   }

@@ -60,7 +60,7 @@ def test_headline_engine_vs_oracle_through_eviction():
     eps = 0.1
     seed = 1234
     eng = RolloutEngine(E, N, f1=64, g=H, h=H, chunk=C, capacity=cap, seed=seed, device=DEV)
-    assert eng.graph_steps() == C
+    assert eng.fused and eng.graph_steps() == 3 * C   # the benched one-launch step (graph cycle lcm(C, 6))
     P = {k: v.detach().cpu().clone() for k, v in eng.behavior.params().items()}
     Pt = {k: v.detach().cpu().clone() for k, v in eng.target.params().items()}
     spec = EnvSpec(N, 100)
@@ -77,7 +77,7 @@ def test_headline_engine_vs_oracle_through_eviction():
         if k + 1 in windows:                # window start: hidden states before chunk k
             snap = dict(h=eng.h.permute(2, 0, 1).cpu().clone(), ht=eng.ht.permute(2, 0, 1).cpu().clone(),
                         done_prev=last_done.copy(), steps=[])
-        eng.run_graph(eps)
+        eng.run_region(C, eps)              # one chunk: a captured C-step region graph per graph phase
         torch.cuda.synchronize()
         O = eng.store.obs[rows].cpu().numpy()
         A = eng.store.act[rows].cpu().numpy().astype(np.int64)
