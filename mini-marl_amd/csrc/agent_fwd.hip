@@ -1074,6 +1074,14 @@ __device__ __forceinline__ void mm16(const float* __restrict__ blk, int q, const
   acc = mfma16x16(ah, x.l, acc);
   acc = mfma16x16(ah, x.h, acc);
 }
+// the same for a k-step whose X is exactly f16 (x.l == 0: {0, 1} observation bits): Wl·xh + Wh·xh, same sum
+// (the skipped Wh·xl term is exactly 0; the accumulation order of the other two is unchanged)
+__device__ __forceinline__ void mm16_x16(const float* __restrict__ blk, int q, const KS& x, int lane, f32x4& acc) {
+  const f16x8 ah = *reinterpret_cast<const f16x8*>(blk + (q * 2) * 256 + lane * 4);
+  const f16x8 al = *reinterpret_cast<const f16x8*>(blk + (q * 2 + 1) * 256 + lane * 4);
+  acc = mfma16x16(al, x.h, acc);
+  acc = mfma16x16(ah, x.h, acc);
+}
 struct Frag {
   f16x8 h, l;
 };
@@ -1180,7 +1188,7 @@ template <int F1, int G, int H, int AB, class OL>
 __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int agent, int e,
                                                     const float* __restrict__ W, const OL& ol,
                                                     float (&xn)[8], const f32x4 (&h0)[H / 16], float eps,
-                                                    uint64_t ctr, int64_t out_off = 0) {
+                                                    uint64_t ctr, int64_t out_off = 0, int x16_from_kb = 1 << 30) {
   using CG = QnetCGeo<F1, G, H, AB>;
   constexpr int T1 = F1 / 16, T2 = G / 16, TH = H / 16, AT = (AB * 32 + 15) / 16;
   constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
@@ -1198,8 +1206,15 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
     KS ob;
     split8(xn, ob);
     if (kb + 1 < p.g.KD) ol(kb + 1, xn);
+    if (kb >= x16_from_kb) {   // observation k-steps known to be exact in f16 (the fused rollout step's bits)
 #pragma unroll
-    for (int t = 0; t < T1; ++t) mm16(W + CG::off_l1 + (int64_t)((t >> 1) * p.g.KD + kb) * 1024, t & 1, ob, lane, x1[t]);
+      for (int t = 0; t < T1; ++t)
+        mm16_x16(W + CG::off_l1 + (int64_t)((t >> 1) * p.g.KD + kb) * 1024, t & 1, ob, lane, x1[t]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < T1; ++t)
+        mm16(W + CG::off_l1 + (int64_t)((t >> 1) * p.g.KD + kb) * 1024, t & 1, ob, lane, x1[t]);
+    }
   }
   KS x1s[RB1];
 #pragma unroll
@@ -1887,7 +1902,10 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
   MM_RSTAMP(5, threadIdx.x == 0);
   if (wave >= 8)
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(8);
-  agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm, ol, xn, h0, eps, ctr);
+  // observation features 32.. are {0, 1} bits of the grid (only features 0, 1, the coordinates, are not
+  // exact in f16): layer-1 k-steps from 1 on skip the Wh·xl MFMA (exactly 0); behavior blocks of envs that
+  // reset read the reset obs, which are the same kind of values
+  agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm, ol, xn, h0, eps, ctr, 0, 1);
   MM_RSTAMP(6, threadIdx.x == 0);
   MM_RSTAMP(7, threadIdx.x == 64 * 15);
 }
