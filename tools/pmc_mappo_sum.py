@@ -39,8 +39,9 @@ def main():
         res["kernels"][k] = {"fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w,
                              "dispatches": fe.get(k, {}).get("dispatches", 0)}
     for k, cs in sq.items():
-        if "mappo_grad_kernel" in k:
-            res["sq_mappo_grad_kernel"] = cs
+        for name in ("mappo_grad_kernel", "mappo_grad_gru_kernel", "mappo_grad_mlp_kernel"):
+            if name in k:   # round 4: the pass is split in a recurrent and a row-parallel MLP kernel
+                res["sq_" + name] = cs
     json.dump(res, open(os.path.join(o, "pmc_mappo.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
