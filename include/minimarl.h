@@ -346,6 +346,23 @@ int mm_mixer_gi_f16(int32_t R, int32_t N, int32_t S, int32_t Hm, int32_t K1, con
 int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1);
 int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
                      int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s);
+/* The split halves of mm_mixer_fwd_seq / mm_mixer_bwd_seq (same arguments), so the mixer's own recurrence can
+ * run on a second stream beside the agent chain (Train_dqn.train, qmix/_train.py:55-116: the Mix_Net GRU over
+ * the state needs no agent Q; its backward needs only the hypernet pass's dhm): fwd_seq_rec -> [join with the
+ * agent forward] -> fwd_seq_hyper; bwd_seq_hyper -> {bwd_seq_rec || agent BPTT}. Only where
+ * mm_mixer_seq_split(B, N, S, Hm, K1, P, ws, steps) != 0 (else MM_EINVAL). */
+int mm_mixer_fwd_seq_rec(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
+                         int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s);
+int mm_mixer_fwd_seq_hyper(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
+                           int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s);
+int mm_mixer_bwd_seq_hyper(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                           const float* qa, const float* dq, const float* done, const float* ones, float* dhm,
+                           float* dqa, float* delta, float* ws, int32_t steps, mm_stream_t s);
+int mm_mixer_bwd_seq_rec(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                         const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
+                         float* delta, float* ws, int32_t steps, mm_stream_t s);
+int mm_mixer_seq_split(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* ws,
+                       int32_t steps);
 int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                      const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
                      float* delta, float* ws, int32_t steps, mm_stream_t s);

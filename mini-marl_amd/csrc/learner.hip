@@ -2719,10 +2719,24 @@ static int mix_rec_win(int C, int Hm, bool bwd) {
   return win;
 }
 
-int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
-                     const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
-                     float* delta, float* ws, int32_t steps, mm_stream_t s) {
+// the split (hypernet + recurrence) mixer backward applies: one launch each, so a caller may run the recurrence
+// beside the agent BPTT (it reads only the mixer's own saves and the hypernet pass's dhm / delta)
+static bool mix_bwd_split_ok(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* ws,
+                             int32_t steps) {
+  const int win = mix_rec_win(steps, Hm, true);
+  return B < 512 && ws && mix_split_enabled() && mm::mix_rec_supported(Hm) &&
+         mm::mix_rec_bwd_floats(Hm, win) * 4 <= mm::kMixSeqLds && mm::mix_hyper_bwd_floats(Hm, K1, N) * 4 <= mm::kMixSeqLds &&
+         Hm % 4 == 0 && K1 % 4 == 0 && mm::mix_offsets(S, Hm, K1, N).w1W % 4 == 0 && (uintptr_t)P % 16 == 0 &&
+         (uintptr_t)ws % 16 == 0;
+}
+
+// part 0: the whole backward; 1: the hypernet pass only (dq -> dqa, dhm, delta); 2: the recurrence only
+static int mixer_bwd_seq_part(int part, int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P,
+                              const float* save, const float* qa, const float* dq, const float* done, const float* ones,
+                              float* dhm, float* dqa, float* delta, float* ws, int32_t steps, mm_stream_t s) {
   MM_REQUIRE(P && save && qa && dq && done && ones && dhm && dqa && delta && steps >= 1, "mixer_bwd_seq: bad args");
+  MM_REQUIRE(part == 0 || mix_bwd_split_ok(B, N, S, Hm, K1, P, ws, steps),
+             "mixer_bwd_seq: the hypernet / recurrence parts need the split path (mm_mixer_seq_split)");
   mm::MixBwdArgs a = {P, save, qa, dq, done, dhm, dqa, delta, B, N, S, Hm, K1};
   mm::MixBwdSeq q;
   q.C = steps;
@@ -2749,10 +2763,13 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
     const int rc = mm::mix_seq_lds_setup();
     if (rc) return rc;
     const int R = B * steps;
-    hipLaunchKernelGGL(mm::mixer_hyper_bwd_kernel, dim3((R + mm::MIX_SPB - 1) / mm::MIX_SPB), dim3(256),
-                       mm::mix_hyper_bwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R, ws,
-                       mm::debug_trace_buffer("MM_HYB_TRACE"));
-    MM_HIP_CHECK(hipGetLastError());
+    if (part != 2) {
+      hipLaunchKernelGGL(mm::mixer_hyper_bwd_kernel, dim3((R + mm::MIX_SPB - 1) / mm::MIX_SPB), dim3(256),
+                         mm::mix_hyper_bwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R, ws,
+                         mm::debug_trace_buffer("MM_HYB_TRACE"));
+      MM_HIP_CHECK(hipGetLastError());
+    }
+    if (part == 1) return MM_OK;
     mm::MixRecBwd rq;
     rq.C = steps;
     rq.win = win;
@@ -2772,6 +2789,7 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
     MM_HIP_CHECK(hipGetLastError());
     return MM_OK;
   }
+  MM_REQUIRE(part == 0, "mixer_bwd_seq: split path not taken");
   const mm::MixSeqGeo g(Hm, K1, N);
   if (g.bwd_floats() * 4 <= mm::kMixSeqLds && g.step_in() <= 1024) {
     const int rc = mm::mix_seq_lds_setup();
@@ -2786,6 +2804,22 @@ int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
   return MM_OK;
 }
 
+int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                     const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
+                     float* delta, float* ws, int32_t steps, mm_stream_t s) {
+  return mixer_bwd_seq_part(0, B, N, S, Hm, K1, P, save, qa, dq, done, ones, dhm, dqa, delta, ws, steps, s);
+}
+int mm_mixer_bwd_seq_hyper(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                           const float* qa, const float* dq, const float* done, const float* ones, float* dhm,
+                           float* dqa, float* delta, float* ws, int32_t steps, mm_stream_t s) {
+  return mixer_bwd_seq_part(1, B, N, S, Hm, K1, P, save, qa, dq, done, ones, dhm, dqa, delta, ws, steps, s);
+}
+int mm_mixer_bwd_seq_rec(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
+                         const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
+                         float* delta, float* ws, int32_t steps, mm_stream_t s) {
+  return mixer_bwd_seq_part(2, B, N, S, Hm, K1, P, save, qa, dq, done, ones, dhm, dqa, delta, ws, steps, s);
+}
+
 int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1) {
   const mm::MixSeqGeo g(Hm, K1, N);
   if (mix_split_enabled())
@@ -2794,9 +2828,12 @@ int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1) {
   return B < 512 && g.fwd_floats() * 4 <= mm::kMixSeqLds && 3 * Hm <= 256 && N <= 256;
 }
 
-int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
-                     int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s) {
+// part 0: the whole forward; 1: the mixer recurrence only (reads gi, not the agents' Q: a caller may run it
+// beside the agent forward); 2: the hypernet pass only (after both)
+static int mixer_fwd_seq_part(int part, int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
+                              int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s) {
   MM_REQUIRE(nets && n_nets >= 1 && n_nets <= 2 && B > 0 && steps >= 1, "mixer_fwd_seq: bad args");
+  MM_REQUIRE(part == 0 || mix_split_enabled(), "mixer_fwd_seq: the parts need the split path");
   MM_REQUIRE(steps == 1 || reset_steps, "mixer_fwd_seq: reset_steps required for steps > 1");
   MM_REQUIRE(mm_mixer_fwd_seq_fits(B, N, Hm, K1), "mixer_fwd_seq: B >= 512 or the weights exceed the LDS");
   for (int i = 0; i < n_nets; ++i)
@@ -2836,13 +2873,16 @@ int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
     rq.save_st = q.save_st;
     rq.reset_steps = reset_steps;
     rq.trace = mm::debug_trace_buffer("MM_MIX_TRACE_FWD");
-    if (Hm == 32)
-      hipLaunchKernelGGL(mm::mixer_rec_fwd_kernel<32>, dim3(B, n_nets), dim3(256),
-                         mm::mix_rec_fwd_floats(Hm, rq.win) * 4, (hipStream_t)s, a, rq);
-    else
-      hipLaunchKernelGGL(mm::mixer_rec_fwd_kernel<64>, dim3(B, n_nets), dim3(256),
-                         mm::mix_rec_fwd_floats(Hm, rq.win) * 4, (hipStream_t)s, a, rq);
-    MM_HIP_CHECK(hipGetLastError());
+    if (part != 2) {
+      if (Hm == 32)
+        hipLaunchKernelGGL(mm::mixer_rec_fwd_kernel<32>, dim3(B, n_nets), dim3(256),
+                           mm::mix_rec_fwd_floats(Hm, rq.win) * 4, (hipStream_t)s, a, rq);
+      else
+        hipLaunchKernelGGL(mm::mixer_rec_fwd_kernel<64>, dim3(B, n_nets), dim3(256),
+                           mm::mix_rec_fwd_floats(Hm, rq.win) * 4, (hipStream_t)s, a, rq);
+      MM_HIP_CHECK(hipGetLastError());
+    }
+    if (part == 1) return MM_OK;
     const int R = B * steps;
     hipLaunchKernelGGL(mm::mixer_hyper_fwd_kernel, dim3((R + mm::MIX_SPB - 1) / mm::MIX_SPB, n_nets), dim3(256),
                        mm::mix_hyper_fwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R);
@@ -2854,6 +2894,25 @@ int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, co
                      q);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
+}
+
+int mm_mixer_fwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
+                     int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s) {
+  return mixer_fwd_seq_part(0, B, N, S, Hm, K1, nets, n_nets, steps, reset_steps, s);
+}
+int mm_mixer_fwd_seq_rec(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
+                         int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s) {
+  return mixer_fwd_seq_part(1, B, N, S, Hm, K1, nets, n_nets, steps, reset_steps, s);
+}
+int mm_mixer_fwd_seq_hyper(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
+                           int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s) {
+  return mixer_fwd_seq_part(2, B, N, S, Hm, K1, nets, n_nets, steps, reset_steps, s);
+}
+
+int mm_mixer_seq_split(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* ws,
+                       int32_t steps) {
+  return (mm_mixer_fwd_seq_fits(B, N, Hm, K1) && mix_split_enabled() &&
+          mix_bwd_split_ok(B, N, S, Hm, K1, P, ws, steps)) ? 1 : 0;
 }
 
 int mm_mixer_bwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,

@@ -247,6 +247,15 @@ _SIGS += [
     ("mm_mixer_fwd_seq_fits", c_i32, [c_i32, c_i32, c_i32, c_i32]),
     ("mm_mixer_fwd_seq", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(MixNetIO), c_i32, c_i32, c_vp,
                                  c_vp]),
+    ("mm_mixer_fwd_seq_rec", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(MixNetIO), c_i32, c_i32, c_vp,
+                                     c_vp]),
+    ("mm_mixer_fwd_seq_hyper", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(MixNetIO), c_i32, c_i32,
+                                       c_vp, c_vp]),
+    ("mm_mixer_bwd_seq_hyper", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                       c_vp, c_vp, c_vp, c_i32, c_vp]),
+    ("mm_mixer_bwd_seq_rec", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_vp, c_vp, c_i32, c_vp]),
+    ("mm_mixer_seq_split", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32]),
 ]
 
 

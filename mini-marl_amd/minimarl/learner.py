@@ -292,12 +292,23 @@ class QLearner:
         obs_p = ctypes.c_void_p(obs_base) if isinstance(obs_base, int) else ptr(obs_base)
         reset_p = ctypes.c_void_p(reset_obs_ptr) if isinstance(reset_obs_ptr, int) else ptr(reset_obs_ptr)
         ND = N * D
+        split = self._mixer_split()
+        if split:
+            # two streams (captured as a fork / join in the update graph): the mixer's state projection and its
+            # GRU recurrence need no agent Q, so they run beside the agent PRE / REC chain
+            side = self._side_stream()
+            side.wait_stream(torch.cuda.current_stream(self.dev))
+            s_m = ctypes.c_void_p(side.cuda_stream)
+        else:
+            s_m = s
         if self.has_mixer:
             # mixer GRU input projections of every (t, b) for both mixers: one MFMA launch
             mx = self.mix
             gi_fn = L.mm_mixer_gi_f16 if self.mixer_fp16 else L.mm_mixer_gi
             check(gi_fn(CB, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, ptr(mx.flat), ptr(self.s_off),
-                        ptr(self.gi_b), ptr(self.tmix.flat), ptr(self.s2_off), ptr(self.gi_t), s), "mixer gi")
+                        ptr(self.gi_b), ptr(self.tmix.flat), ptr(self.s2_off), ptr(self.gi_t), s_m), "mixer gi")
+            if split:
+                self._mixer_seq_call(L, L.mm_mixer_fwd_seq_rec, s_m, "mixer fwd seq (recurrence)")
         # ---- forward over the chunk: the non-recurrent part (layers 1-2, W_ih x2) of every (t, b) of
         # both nets in ONE launch, then one recurrent step (W_hh h, gates, Q head) per t
         pb, pt = QFwdIO(), QFwdIO()
@@ -327,7 +338,7 @@ class QLearner:
         if self.double and self._draws is None:
             self.dctr.add_(C)             # stream-ordered: captured into the update graph
         if self.seq:
-            self._forward_seq(L, s, obs_p, reset_p)
+            self._forward_seq(L, s, obs_p, reset_p, split)
         for t in range(0 if not self.seq else C, C):
             ib, it = QFwdIO(), QFwdIO()
             for io, h, gi in ((ib, self.hb, self.gi_ab), (it, self.ht, self.gi_at)):
@@ -400,9 +411,17 @@ class QLearner:
         if self.seq:
             if self.has_mixer:
                 mx = self.mix
-                check(L.mm_mixer_bwd_seq(B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.msave), ptr(self.qa),
-                                         ptr(self.dq), ptr(self.done), ptr(self.ones_f), ptr(self.dhm), ptr(self.dqa),
-                                         ptr(self.mdelta), ptr(self.mxws), C, s), "mixer bwd seq")
+                margs = (B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.msave), ptr(self.qa), ptr(self.dq),
+                         ptr(self.done), ptr(self.ones_f), ptr(self.dhm), ptr(self.dqa), ptr(self.mdelta),
+                         ptr(self.mxws), C)
+                if split:
+                    # the hypernet pass (-> dqa for the agents), then the mixer recurrence's backward beside the
+                    # agent BPTT; joined before the weight gradients
+                    check(L.mm_mixer_bwd_seq_hyper(*margs, s), "mixer bwd seq (hypernets)")
+                    side.wait_stream(torch.cuda.current_stream(self.dev))
+                    check(L.mm_mixer_bwd_seq_rec(*margs, s_m), "mixer bwd seq (recurrence)")
+                else:
+                    check(L.mm_mixer_bwd_seq(*margs, s), "mixer bwd seq")
         agent_seq = self.seq and B < 512 and self.H in (32, 64)
         if agent_seq:
             # the agent BPTT chain over all C steps in one launch (W_hh in LDS, dh carried in registers)
@@ -421,6 +440,8 @@ class QLearner:
             check(L.mm_agent_bwd(ctypes.byref(self.beh.dims), ptr(P), o[8], o[5], B, ptr(self.asave[t]),
                                  ctypes.c_void_p(self.acts.data_ptr() + 4 * t * B * N), ptr(self.dqa[t]), ptr(dn),
                                  ptr(self.dh), ptr(self.dgi[t]), ptr(self.dgh[t]), ptr(self.dqv[t]), s), "agent bwd")
+        if split:
+            torch.cuda.current_stream(self.dev).wait_stream(side)   # join: the mixer deltas are complete
         # ---- deferred weight gradients: batched over all C*B rows, grouped by agent; every
         # outer product of the update (agent + mixer) in ONE split-M launch (+ its partial sum)
         jobs = []
@@ -446,7 +467,37 @@ class QLearner:
         """cfg5 fast mode at large batches: the mixer's weight-gradient products as bf16x3 splits."""
         return self.mixer_fp16 and self.has_mixer and self.C * self.B >= 2048
 
-    def _forward_seq(self, L, s, obs_p, reset_p):
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.dev)
+        return self._side
+
+    def _mixer_split(self):
+        """The mixer's state projection + GRU recurrence run on a second stream beside the agent chain (and its
+        recurrence backward beside the agent BPTT): sequence path, both split mixer kernels available."""
+        if not (self.has_mixer and self.seq and self.B < 512):
+            return False
+        mx = self.mix
+        return bool(lib().mm_mixer_seq_split(self.B, self.N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(self.mxws),
+                                             self.C))
+
+    def _mixer_nets(self):
+        nets = (MixNetIO * 2)()
+        for k, (Pm, q, qt, sv, gi) in enumerate(((self.mix.flat, self.qa, self.qtot, self.msave, self.gi_b),
+                                                  (self.tmix.flat, self.maxq, self.qtot_t, None, self.gi_t))):
+            n = nets[k]
+            n.P, n.q, n.gi, n.qtot = Pm.data_ptr(), q.data_ptr(), gi.data_ptr(), qt.data_ptr()
+            n.s_off = self.s_off.data_ptr()
+            n.h_in, n.h_out = self.hm[0].data_ptr(), self.mhseq[k].data_ptr()
+            n.reset = self.ones8.data_ptr()
+            n.save = sv.data_ptr() if sv is not None else None
+        return nets
+
+    def _mixer_seq_call(self, L, fn, s, what):
+        mx = self.mix
+        check(fn(self.B, self.N, mx.S, mx.Hm, mx.K1, self._mixer_nets(), 2, self.C, ptr(self.done8), s), what)
+
+    def _forward_seq(self, L, s, obs_p, reset_p, split=False):
         """REC of both nets over all C steps in one chunk-sequence launch, then the mixers per step."""
         B, C, N, H = self.B, self.C, self.N, self.H
         ib, it = QFwdIO(), QFwdIO()
@@ -463,19 +514,15 @@ class QLearner:
                                     ptr(self.tgt.packed), ctypes.byref(it), B, C, ptr(self.done8), s), "rec seq")
         if self.has_mixer:
             mx = self.mix
+            if split:
+                # join the mixer recurrence (side stream), then the hypernet pass over the agents' Q
+                torch.cuda.current_stream(self.dev).wait_stream(self._side_stream())
+                self._mixer_seq_call(L, L.mm_mixer_fwd_seq_hyper, s, "mixer fwd seq (hypernets)")
+                return
             if L.mm_mixer_fwd_seq_fits(B, N, mx.Hm, mx.K1):
                 # all C steps of both mixers in ONE launch: weights staged once into LDS, the mixer
                 # hidden carried in LDS (bit-identical to the per-step launches below)
-                nets = (MixNetIO * 2)()
-                for k, (Pm, q, qt, sv, gi) in enumerate(((self.mix.flat, self.qa, self.qtot, self.msave, self.gi_b),
-                                                          (self.tmix.flat, self.maxq, self.qtot_t, None, self.gi_t))):
-                    n = nets[k]
-                    n.P, n.q, n.gi, n.qtot = Pm.data_ptr(), q.data_ptr(), gi.data_ptr(), qt.data_ptr()
-                    n.s_off = self.s_off.data_ptr()
-                    n.h_in, n.h_out = self.hm[0].data_ptr(), self.mhseq[k].data_ptr()
-                    n.reset = self.ones8.data_ptr()
-                    n.save = sv.data_ptr() if sv is not None else None
-                check(L.mm_mixer_fwd_seq(B, N, mx.S, mx.Hm, mx.K1, nets, 2, C, ptr(self.done8), s), "mixer fwd seq")
+                self._mixer_seq_call(L, L.mm_mixer_fwd_seq, s, "mixer fwd seq")
                 return
             # per-step mixer launches (B >= 512: 8 samples per block share the weight reads), reading
             # the REC outputs of every step
