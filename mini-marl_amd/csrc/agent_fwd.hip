@@ -1573,6 +1573,7 @@ __device__ __forceinline__ void roll_store4(float* dst, int f0, int D, const flo
 template <int F1, int G, int H, int AB>
 __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QFwdParams p1, RollStep rs_) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];
+  const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();   // (timing trace only)
   const bool second = (int)blockIdx.x >= p0.nblocks;     // p0: target net on s'_t, p1: behavior net on s_{t+1}
   // parameters read from the kernarg segment on demand (uniform scalar loads) instead of held in SGPRs
   const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1715,7 +1716,7 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
   }
   MM_RSTAMP(1, threadIdx.x == 0);
   __syncthreads();
-  MM_RSTAMP(2, threadIdx.x == 0);
+  if (rs.trace && threadIdx.x == 0 && blockIdx.x < 512) rs.trace[8 * blockIdx.x + 2] = t_entry;
   // ---- waves 4-15, once the env inputs have been consumed: the weight image DMA into the staging region
   // (range-guarded agents: the exact-f32 image) while waves 0-3 run the env step
   if (wave >= 4) {

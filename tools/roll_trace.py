@@ -1,5 +1,5 @@
 """Per-block timeline of ONE fused rollout-step launch (MM_ROLL_TRACE stamps, csrc/agent_fwd.hip MM_RSTAMP):
-0 start, 1 env inputs staged (wave 0), 2 after the first barrier, 3 env step done (wave 0), 4 after the second
+0 start (after the first kernarg-dependent load), 1 env inputs staged (wave 0), 2 kernel entry (first instruction), 3 env step done (wave 0), 4 after the second
 barrier, 5 obs k-step 0 built, 6 / 7 body end of waves 0 / 15. Prints, per stamp, min / median / max over blocks in us from the earliest start. GPU only."""
 import ctypes
 import os
@@ -30,7 +30,7 @@ for rep in range(3):
     t0 = tr[:, 0].min()
     rel = (tr - t0) * 0.01
     print(f"rep {rep}: blocks {nb}")
-    for i, name in enumerate(["start", "env staged", "barrier A", "env done", "barrier B", "obs ks0", "end w0", "end w15"]):
+    for i, name in enumerate(["start", "env staged", "entry", "env done", "barrier B", "obs ks0", "end w0", "end w15"]):
         col = rel[:, i]
         print(f"  {i} {name:11s} min {col.min():6.2f} med {np.median(col):6.2f} max {col.max():6.2f}  "
               f"(target med {np.median(col[: nb // 2]):6.2f}, behavior med {np.median(col[nb // 2:]):6.2f})")
