@@ -1642,7 +1642,7 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
       piece16((par ? ev.steps_alt : ev.steps) + e0, st_steps, (ne * 4 + 15) & ~15);
       piece16((par ? ev.apples_alt : ev.apples) + e0, st_apples, (ne * 4 + 15) & ~15);
     }
-    if (writer) piece16(rs.staging + e0, st_srow, (ne * 8 + 15) & ~15);
+    if (!second) piece16(rs.staging + e0, st_srow, (ne * 8 + 15) & ~15);   // target blocks: the store rows
     if (tdw) {
       const TdFuse& td = rs.td;
       piece16(td.rew + (int64_t)e0 * N, st_trew, ne * N * 4);
@@ -1714,6 +1714,15 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
         if (2 * j + 1 < R) rows[2 * j + 1] = nib_pack4(g.z) | (nib_pack4(g.w) << 16);
       }
   }
+  // the store rows of this wave's envs (h3 lane mapping, and the exact path's 32-env mapping), read from the
+  // staging before the image DMA overwrites it: no global round trip in front of the first obs store
+  int64_t srow_h3 = 0, srow_ex = 0;
+  if (!second) {
+    const int64_t* st_rows = reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(wsm) + st_srow);
+    const int l16 = wave * 16 + (lane & 15), l32 = wave * 32 + (lane & 31);
+    if (e0 + l16 < E) srow_h3 = st_rows[l16];
+    if (l32 < 256 && e0 + l32 < E) srow_ex = st_rows[l32];
+  }
   MM_RSTAMP(1, threadIdx.x == 0);
   __syncthreads();
   if (rs.trace && threadIdx.x == 0 && blockIdx.x < 512) rs.trace[8 * blockIdx.x + 2] = t_entry;
@@ -1765,6 +1774,7 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
       const bool inside = a != 4 && nr >= 0 && nr < R && nc >= 0 && nc < C;
       // every row this agent may read or write, in one round trip: the target row, its own row, its stale prev row
       const uint32_t w_n = rows[inside ? nr : r], w_r = rows[r], w_p = rows[pr];
+      asm volatile("" ::"v"(w_n), "v"(w_r), "v"(w_p));   // all three reads in flight together (not sunk into branches)
       const bool moved = inside && ((w_n >> (4 * nc)) & 15u) < 3u;
       if (moved) {
         pr = r;
@@ -1825,7 +1835,7 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
   if (exact) {
     // range-guarded agent: the exact-f32 body, 8 waves x 32 envs (agent_q_fwd_h3_kernel's fallback)
     const int l32 = wave * 32 + (lane & 31), e32 = e0 + l32, hh = (lane & 63) >> 5;
-    const int64_t srow32 = (!second && e32 < E) ? rs.staging[e32] : 0;
+    const int64_t srow32 = srow_ex;
     const bool r32 = !second && io.reset && e32 < E && io.reset[e32];
     __syncthreads();
     const bool bd = second && e32 < E && sdone[l32];
@@ -1876,7 +1886,7 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
   }
   // the store destination of s'_t (target blocks), loaded after the env step (a global load before it would be
   // waited on inside the dynamics loop by the spill reloads' vmcnt)
-  const int64_t srow = (!second && e < E) ? rs.staging[e] : 0;
+  const int64_t srow = srow_h3;
   float* dst = (!second && e < E) ? rs.store_obs + srow * rs.row_stride + rs.next_off + (int64_t)agent * D : nullptr;
   const int rc = spos[le * N + agent];
   const uint64_t wd = roll_obs_word(reinterpret_cast<const uint32_t*>(sgrid) + le * roll_gbw(R), R, rc >> 4, rc & 15);
