@@ -2548,7 +2548,9 @@ size_t rollout_step_lds(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs
   QnetOffsets o;
   if (qnet_geometry(d, &g, &o)) return 0;
   if (ev.full_obs || ev.D != OBS_LOCAL || d->obs_dim != ev.D || d->n_agents != ev.N) return 0;
-  if (ev.N > kRollMaxN || ev.R > kRollMaxR || ev.C != 8) return 0;   // 8 columns: one nibble word per row
+  // 8 columns: one nibble word per row; an even row count: whole 16-byte grid pieces per env (staging reads and the
+  // writer's grid stores)
+  if (ev.N > kRollMaxN || ev.R > kRollMaxR || ev.C != 8 || (ev.R & 1)) return 0;
   if (n_envs < 2048 || n_envs != ev.E) return 0;
   const bool known = (d->f1 == 64 && d->g == 32 && d->h == 32) || (d->f1 == 64 && d->g == 64 && d->h == 64) ||
                      (d->f1 == 128 && d->g == 32 && d->h == 32) || (d->f1 == 64 && d->g == 32 && d->h == 64);

@@ -23,11 +23,11 @@ def _state(e):
     return [x.detach().clone().cpu() for x in st] + [torch.as_tensor(v) for v in e.env.get_state()]
 
 
-def _pair(E, f1, g, h, seed, guard=False):
+def _pair(E, f1, g, h, seed, guard=False, n=8):
     from minimarl.engine import RolloutEngine
     kw = dict(f1=f1, g=g, h=h, chunk=10, capacity=4 * E, seed=seed, device=DEV)
-    a = RolloutEngine(E, 8, fused=False, **kw)
-    b = RolloutEngine(E, 8, fused=True, **kw)
+    a = RolloutEngine(E, n, fused=False, **kw)
+    b = RolloutEngine(E, n, fused=True, **kw)
     assert b.fused and not a.fused and b.graph_steps() == 30
     if guard:   # agent 3 beyond the fp16 range: both engines run it on the exact-f32 image
         for eng in (a, b):
@@ -38,11 +38,11 @@ def _pair(E, f1, g, h, seed, guard=False):
     return a, b
 
 
-@pytest.mark.parametrize("E,f1,g,h,guard", [(2048, 64, 64, 64, False), (2200, 64, 32, 32, False),
-                                            (2048, 64, 64, 64, True)])
-def test_fused_step_bit_identical_to_two_launch(E, f1, g, h, guard):
-    a, b = _pair(E, f1, g, h, seed=21, guard=guard)
-    spec = EnvSpec(8, 100)
+@pytest.mark.parametrize("E,f1,g,h,guard,n", [(2048, 64, 64, 64, False, 8), (2200, 64, 32, 32, False, 8),
+                                              (2048, 64, 64, 64, True, 8), (2304, 64, 32, 32, False, 4)])
+def test_fused_step_bit_identical_to_two_launch(E, f1, g, h, guard, n):
+    a, b = _pair(E, f1, g, h, seed=21, guard=guard, n=n)
+    spec = EnvSpec(n, 100)
     ora = VecEnvOracle(spec, E)
     for t in range(34):
         rows = b.staging.cpu().numpy()
@@ -128,3 +128,14 @@ def test_learner_repacks_f32_image_and_rollout_refreshes_fp16x3_image():
     torch.cuda.synchronize()
     assert not eng.behavior._h3_stale
     assert torch.equal(ref.packed, eng.behavior.packed)
+
+
+def test_fused_step_not_taken_for_odd_band_counts():
+    """2 or 6 agents give an odd row count (3 rows per band): no whole 16-byte grid pieces per env, so the engine
+    keeps the two-launch step there (and refuses fused=True)."""
+    from minimarl.engine import RolloutEngine
+    for n in (2, 6):
+        eng = RolloutEngine(2048, n, f1=64, g=32, h=32, chunk=10, capacity=4096, device=DEV)
+        assert not eng.fused
+        with pytest.raises(ValueError):
+            RolloutEngine(2048, n, f1=64, g=32, h=32, chunk=10, capacity=4096, fused=True, device=DEV)
