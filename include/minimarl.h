@@ -258,6 +258,8 @@ typedef struct mm_rollout_step_io {
   const float* td_rew; const uint8_t* td_done; const float* td_qsel; const float* td_maxq; const int32_t* td_act;
   float* chunk_td; uint8_t* store_act; float* store_rew; uint8_t* store_done;
 } mm_rollout_step_io;
+/* 1 when the fused step fits: local obs, 8 grid columns and an even row count (4 or 8 agents), E >= 2048, one of
+ * the compiled layer widths, LDS budget; 0 otherwise (use the two-launch step). */
 int mm_rollout_step_supported(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs);
 int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
                     const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_step_io* x,
