@@ -40,7 +40,8 @@ def _pair(E, f1, g, h, seed, guard=False, n=8):
 
 @pytest.mark.parametrize("E,f1,g,h,guard,n", [(2048, 64, 64, 64, False, 8), (2200, 64, 32, 32, False, 8),
                                               (2048, 64, 64, 64, True, 8), (2304, 64, 32, 32, False, 4),
-                                              (2048, 128, 32, 32, False, 8), (2048, 64, 32, 64, False, 8)])
+                                              (2048, 128, 32, 32, False, 8), (2048, 64, 32, 64, False, 8),
+                                              (2100, 64, 64, 64, True, 4)])
 def test_fused_step_bit_identical_to_two_launch(E, f1, g, h, guard, n):
     a, b = _pair(E, f1, g, h, seed=21, guard=guard, n=n)
     spec = EnvSpec(n, 100)
