@@ -1,5 +1,6 @@
 """Summarise tools/pmc_fwd_sq.sh: per-dispatch means of every counter over the dual-forward dispatches
-(agent_q_fwd_h3_kernel, grid 262144), plus derived fractions. Usage: python tools/pmc_fwd_sum.py <dir>"""
+(agent_q_fwd_h3_kernel, grid 262144), plus derived fractions. Usage: python tools/pmc_fwd_sum.py <dir>
+[<kernel-name substring> <label>] (tools/pmc_roll_sq.sh: rollout_step_kernel)"""
 import csv
 import glob
 import json
@@ -7,12 +8,14 @@ import os
 import sys
 
 d = sys.argv[1]
+KN = sys.argv[2] if len(sys.argv) > 2 else "agent_q_fwd_h3_kernel"
+LABEL = sys.argv[3] if len(sys.argv) > 3 else "agent_q_fwd_h3_kernel<64,64,64,1> dual (grid 262144 = 256 blocks x 1024)"
 acc = {}
 dur = []
 for path in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
     per = {}                                # (counter, dispatch) -> sum over the counter's instances
     for r in csv.DictReader(open(path)):
-        if "agent_q_fwd_h3_kernel" not in r["Kernel_Name"] or int(r["Grid_Size"]) != 262144:
+        if KN not in r["Kernel_Name"] or int(r["Grid_Size"]) != 262144:
             continue
         key = (r["Counter_Name"], path, r["Dispatch_Id"])
         per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
@@ -20,10 +23,10 @@ for path in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), re
         acc.setdefault(name, []).append(v)
 for path in glob.glob(os.path.join(d, "p*", "**", "*kernel_trace.csv"), recursive=True):
     for r in csv.DictReader(open(path)):
-        if "agent_q_fwd_h3_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == 262144:
+        if KN in r["Kernel_Name"] and int(r["Grid_Size_X"]) == 262144:
             dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
 mean = {k: sum(v) / len(v) for k, v in acc.items()}
-out = {"kernel": "agent_q_fwd_h3_kernel<64,64,64,1> dual (grid 262144 = 256 blocks x 1024)",
+out = {"kernel": LABEL,
        "dispatches": {k: len(v) for k, v in acc.items()}, "mean_per_dispatch": mean}
 if dur:
     out["mean_us_traced"] = sum(dur) / len(dur)
