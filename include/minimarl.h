@@ -404,6 +404,14 @@ int mm_vdn_sum(int64_t B, int32_t N, int32_t A, const float* q, int64_t q_se, in
  * + t x (B x N x width) (save, acts, dqa, dgi, dgh, dq); done of step t < C-1 at done + t*B, step C-1
  * uses ones; dh carries the hidden gradient (in: zero, out: grad wrt the chunk-start hidden).
  * Bit-identical to C per-step mm_agent_bwd launches. */
+/* mm_agent_bwd_seq and the mixer recurrence's backward (mm_mixer_bwd_seq_rec with the same B, done, ones, dqa and
+ * steps; S, Hm, K1, mP .. ws its mixer arguments) in ONE launch: the two chains are independent and share the grid
+ * (agent blocks first); results identical to the two calls. Needs the split mixer path (mm_mixer_seq_split). */
+int mm_agent_mixer_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B,
+                           const float* save, const int32_t* acts, const float* dqa, const float* done,
+                           const float* ones, float* dh, float* dgi, float* dgh, float* dq, int32_t steps, int32_t S,
+                           int32_t Hm, int32_t K1, const float* mP, const float* msave, const float* qa,
+                           const float* mdq, float* dhm, float* mdelta, float* ws, mm_stream_t s);
 int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B, const float* save,
                      const int32_t* acts, const float* dqa, const float* done, const float* ones, float* dh,
                      float* dgi, float* dgh, float* dq, int32_t steps, mm_stream_t s);

@@ -1651,13 +1651,13 @@ __host__ __device__ inline size_t mix_hyper_bwd_floats(int Hm, int K1, int N) {
   return (size_t)(N * K1 + 3 * K1) * Hm + (size_t)MIX_SPB * (N * K1 + 3 * K1 + 4 * Hm + 4 * Hm);
 }
 
+// bid: the sample (block) index; sm: the block's dynamic LDS (mixer_rec_bwd_kernel, agent_mixer_bwd_kernel)
 template <int HM>
-__global__ __launch_bounds__(256) void mixer_rec_bwd_kernel(MixBwdArgs a, MixRecBwd sq) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+__device__ __forceinline__ void mixer_rec_bwd_body(const MixBwdArgs& a, const MixRecBwd& sq, int bid, float* sm) {
   using Geo = MixRecGeo<HM>;
   constexpr int M3 = Geo::M3, LD = Geo::LDB, NW = 4;   // 256 threads = 4 waves
   static_assert(M3 % (4 * NW) == 0, "W_hh^T partial loop assumes 16 | 3 Hm");
-  const int b = blockIdx.x, ti = (int)threadIdx.x;
+  const int b = bid, ti = (int)threadIdx.x;
   const MixOff o = mix_offsets(a.S, HM, a.K1, a.N);
   const int svd = mix_save_dim(HM, a.K1, a.N), dld = mix_delta_dim(HM, a.K1, a.N);
   constexpr int SI = 9 * HM;       // per-step inputs: hm0 r z n anh (5Hm) | X_0..X_3 (4Hm); done apart
@@ -1752,6 +1752,12 @@ __global__ __launch_bounds__(256) void mixer_rec_bwd_kernel(MixBwdArgs a, MixRec
   }
   if (tr) tr[2] = clock64();
   if (ti < HM) a.dhm[(int64_t)b * HM + ti] = dhm_c;
+}
+
+template <int HM>
+__global__ __launch_bounds__(256) void mixer_rec_bwd_kernel(MixBwdArgs a, MixRecBwd sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  mixer_rec_bwd_body<HM>(a, sq, (int)blockIdx.x, sm);
 }
 
 // dynamic-LDS limit of the sequence kernels (MI355X: 160 KB per CU, one block per CU)
@@ -1856,9 +1862,11 @@ __host__ __device__ inline size_t agent_bwd_seq_floats(int H, int A, int win) {
   return (size_t)H * (3 * H + 4) + 3 * (size_t)H * H + 4 * 3 * (size_t)H + (size_t)A * H + 4 +
          4 * (size_t)win * (5 * H + 3);
 }
+// (bx, by) = (batch group of 4 samples, agent); sm: the block's dynamic LDS (agent_bwd_seq_kernel,
+// agent_mixer_bwd_kernel)
 template <int H>
-__global__ __launch_bounds__(256) void agent_bwd_seq_kernel(AgentBwdArgs a, AgentBwdSeq sq) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+__device__ __forceinline__ void agent_bwd_seq_body(const AgentBwdArgs& a, const AgentBwdSeq& sq, int bx, int by,
+                                                   float* sm) {
   constexpr int H3 = 3 * H, LDT = H3 + 4, SI = 5 * H;   // input rows: 16-byte aligned (H % 4 == 0)
   const int A = a.A;
   float* whT = sm;                 // [H][LDT]: whT[f * LDT + r] = W_hh[r][f]
@@ -1868,23 +1876,23 @@ __global__ __launch_bounds__(256) void agent_bwd_seq_kernel(AgentBwdArgs a, Agen
   float* inw = wq + ((A * H + 3) & ~3);   // [win][4][5H]: h0 r z n anh of (step, wave)
   float* scw = inw + sq.win * 4 * SI;      // [win][4][3]: act (int bits) | dQ(a) | done
   const int w = threadIdx.x >> 6, f = threadIdx.x & 63;
-  const int i = blockIdx.y;
-  const int b = blockIdx.x * 4 + w;
+  const int i = by;
+  const int b = bx * 4 + w;
   const bool on = b < a.B && f < H;
   const int64_t pair = (int64_t)(b < a.B ? b : 0) * a.N + i;
   const int SD = a.F1 + a.G + 6 * H;
-  uint64_t* tr = (sq.trace && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) ? sq.trace : nullptr;
+  uint64_t* tr = (sq.trace && bx == 0 && by == 0 && threadIdx.x == 0) ? sq.trace : nullptr;
   if (tr) tr[0] = clock64();
   const float* Wq_g = a.P + a.oWq + (int64_t)i * A * H;
   const float* Whh = a.P + a.oWhh + (int64_t)i * H3 * H;
   // input row (step w0 + row / 4, wave row % 4): the 5H saved GRU values (16-byte pieces), then the
   // action (raw int bits), dQ(a) and the done flag (one word each)
   auto save_row = [&](int w0, int row) -> const float* {
-    const int t = w0 + (row >> 2), bb = min((int)blockIdx.x * 4 + (row & 3), a.B - 1);
+    const int t = w0 + (row >> 2), bb = min(bx * 4 + (row & 3), a.B - 1);
     return a.save + t * sq.save_st + ((int64_t)bb * a.N + i) * SD + a.F1 + a.G;
   };
   auto scalar_in = [&](int w0, int row, int j) -> const float* {   // j = 0 act, 1 dQ(a), 2 done
-    const int t = w0 + (row >> 2), bb = min((int)blockIdx.x * 4 + (row & 3), a.B - 1);
+    const int t = w0 + (row >> 2), bb = min(bx * 4 + (row & 3), a.B - 1);
     const int64_t pr = (int64_t)bb * a.N + i;
     if (j == 0) return reinterpret_cast<const float*>(a.acts + t * sq.acts_st + pr);
     if (j == 1) return a.dqa + t * sq.dqa_st + pr;
@@ -1986,6 +1994,27 @@ __global__ __launch_bounds__(256) void agent_bwd_seq_kernel(AgentBwdArgs a, Agen
   }
   if (tr) tr[2] = clock64();
   if (on) a.dh[pair * H + f] = dh;
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void agent_bwd_seq_kernel(AgentBwdArgs a, AgentBwdSeq sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  agent_bwd_seq_body<H>(a, sq, (int)blockIdx.x, (int)blockIdx.y, sm);
+}
+
+// The agent BPTT (blocks [0, n_agent_blocks), (batch group, agent) = (bid % gx, bid / gx)) and the mixer
+// recurrence's backward (the remaining B blocks, one per sample) in ONE launch: the two chains are independent
+// (both read the hypernet pass's outputs), so they share the grid instead of a stream fork / join in the update
+// graph. Same bodies as the two kernels, so the same results.
+template <int H, int HM>
+__global__ __launch_bounds__(256) void agent_mixer_bwd_kernel(AgentBwdArgs a, AgentBwdSeq q, MixBwdArgs ma,
+                                                              MixRecBwd mq, int gx, int n_agent_blocks) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bid = (int)blockIdx.x;
+  if (bid < n_agent_blocks)
+    agent_bwd_seq_body<H>(a, q, bid % gx, bid / gx, sm);
+  else
+    mixer_rec_bwd_body<HM>(ma, mq, bid - n_agent_blocks, sm);
 }
 
 // Large-batch variant (H <= 64): one block = one agent x 32 samples, one wave = 8 samples of that
@@ -2925,9 +2954,11 @@ int mm_mixer_bwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const 
   return MM_OK;
 }
 
-int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B, const float* save,
-                     const int32_t* acts, const float* dqa, const float* done, const float* ones, float* dh,
-                     float* dgi, float* dgh, float* dq, int32_t steps, mm_stream_t s) {
+// The agent BPTT's kernel arguments and dynamic LDS size (mm_agent_bwd_seq, mm_agent_mixer_bwd_seq)
+static int agent_bwd_seq_prep(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B,
+                              const float* save, const int32_t* acts, const float* dqa, const float* done,
+                              const float* ones, float* dh, float* dgi, float* dgh, float* dq, int32_t steps,
+                              mm::AgentBwdArgs* a, mm::AgentBwdSeq* q, size_t* smem) {
   MM_REQUIRE(d && P && save && acts && dqa && done && ones && dh && dgi && dgh && dq && steps >= 1 && B > 0,
              "agent_bwd_seq: bad args");
   MM_REQUIRE((d->h == 32 || d->h == 64) && d->n_actions <= 64, "agent_bwd_seq: needs H in {32, 64} and A <= 64");
@@ -2935,39 +2966,91 @@ int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t
              "agent_bwd_seq: W_hh / save rows must be 16-byte aligned (16-byte LDS-DMA)");
   int win = steps;
   while (win > 1 && mm::agent_bwd_seq_floats(d->h, d->n_actions, win) * 4 > mm::kMixSeqLds) win = (win + 1) / 2;
-  const size_t smem = sizeof(float) * mm::agent_bwd_seq_floats(d->h, d->n_actions, win);
-  MM_REQUIRE(smem <= mm::kMixSeqLds, "agent_bwd_seq: W_hh too large for LDS");
+  *smem = sizeof(float) * mm::agent_bwd_seq_floats(d->h, d->n_actions, win);
+  MM_REQUIRE(*smem <= mm::kMixSeqLds, "agent_bwd_seq: W_hh too large for LDS");
   {
     // thread-safe one-time setup (a function-local static's initialiser runs once); the sizes are compile-time
     static const int attr_rc = [&]() -> int {
-      MM_HIP_CHECK(hipFuncSetAttribute((const void*)mm::agent_bwd_seq_kernel<32>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)mm::kMixSeqLds));
-      MM_HIP_CHECK(hipFuncSetAttribute((const void*)mm::agent_bwd_seq_kernel<64>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)mm::kMixSeqLds));
+      const void* k[] = {(const void*)mm::agent_bwd_seq_kernel<32>, (const void*)mm::agent_bwd_seq_kernel<64>,
+                         (const void*)mm::agent_mixer_bwd_kernel<32, 32>, (const void*)mm::agent_mixer_bwd_kernel<32, 64>,
+                         (const void*)mm::agent_mixer_bwd_kernel<64, 32>, (const void*)mm::agent_mixer_bwd_kernel<64, 64>};
+      for (const void* f : k)
+        MM_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mm::kMixSeqLds));
       return MM_OK;
     }();
     if (attr_rc != MM_OK) return attr_rc;
   }
-  mm::AgentBwdArgs a = {P, oWq, oWhh, save, acts, dqa, done, dh, dgi, dgh, dq, B, d->n_agents, d->f1, d->g, d->h,
-                        d->n_actions};
+  *a = {P, oWq, oWhh, save, acts, dqa, done, dh, dgi, dgh, dq, B, d->n_agents, d->f1, d->g, d->h, d->n_actions};
   const int64_t BN = (int64_t)B * d->n_agents;
+  q->C = steps;
+  q->save_st = BN * (d->f1 + d->g + 6 * d->h);
+  q->acts_st = BN;
+  q->dqa_st = BN;
+  q->dgi_st = BN * 3 * d->h;
+  q->dq_st = BN * d->n_actions;
+  q->done_st = B;
+  q->ones = ones;
+  q->win = win;
+  q->trace = mm::debug_trace_buffer("MM_ABWD_TRACE");
+  return MM_OK;
+}
+
+int mm_agent_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B, const float* save,
+                     const int32_t* acts, const float* dqa, const float* done, const float* ones, float* dh,
+                     float* dgi, float* dgh, float* dq, int32_t steps, mm_stream_t s) {
+  mm::AgentBwdArgs a;
   mm::AgentBwdSeq q;
-  q.C = steps;
-  q.save_st = BN * (d->f1 + d->g + 6 * d->h);
-  q.acts_st = BN;
-  q.dqa_st = BN;
-  q.dgi_st = BN * 3 * d->h;
-  q.dq_st = BN * d->n_actions;
-  q.done_st = B;
-  q.ones = ones;
-  q.win = win;
-  q.trace = mm::debug_trace_buffer("MM_ABWD_TRACE");
+  size_t smem = 0;
+  const int rc = agent_bwd_seq_prep(d, P, oWq, oWhh, B, save, acts, dqa, done, ones, dh, dgi, dgh, dq, steps, &a, &q,
+                                    &smem);
+  if (rc) return rc;
   if (d->h == 32)
     hipLaunchKernelGGL(mm::agent_bwd_seq_kernel<32>, dim3((B + 3) / 4, d->n_agents), dim3(256), smem, (hipStream_t)s,
                        a, q);
   else
     hipLaunchKernelGGL(mm::agent_bwd_seq_kernel<64>, dim3((B + 3) / 4, d->n_agents), dim3(256), smem, (hipStream_t)s,
                        a, q);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_agent_mixer_bwd_seq(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWhh, int32_t B,
+                           const float* save, const int32_t* acts, const float* dqa, const float* done,
+                           const float* ones, float* dh, float* dgi, float* dgh, float* dq, int32_t steps, int32_t S,
+                           int32_t Hm, int32_t K1, const float* mP, const float* msave, const float* qa,
+                           const float* mdq, float* dhm, float* mdelta, float* ws, mm_stream_t s) {
+  mm::AgentBwdArgs a;
+  mm::AgentBwdSeq q;
+  size_t smem = 0;
+  int rc = agent_bwd_seq_prep(d, P, oWq, oWhh, B, save, acts, dqa, done, ones, dh, dgi, dgh, dq, steps, &a, &q, &smem);
+  if (rc) return rc;
+  MM_REQUIRE(mP && msave && qa && mdq && dhm && mdelta && (Hm == 32 || Hm == 64) &&
+                 mix_bwd_split_ok(B, d->n_agents, S, Hm, K1, mP, ws, steps),
+             "agent_mixer_bwd_seq: the mixer recurrence needs the split path (mm_mixer_seq_split)");
+  rc = mm::mix_seq_lds_setup();
+  if (rc) return rc;
+  const int N = d->n_agents;
+  const mm::MixBwdArgs ma = {mP, msave, qa, mdq, done, dhm, const_cast<float*>(dqa), mdelta, B, N, S, Hm, K1};
+  mm::MixRecBwd mq;
+  mq.C = steps;
+  mq.win = mix_rec_win(steps, Hm, true);
+  mq.save_st = (int64_t)B * mm::mix_save_dim(Hm, K1, N);
+  mq.delta_st = (int64_t)B * mm::mix_delta_dim(Hm, K1, N);
+  mq.done_st = B;
+  mq.done = done;
+  mq.xws = ws;
+  mq.ones = ones;
+  mq.trace = mm::debug_trace_buffer("MM_MIX_TRACE_BWD");
+  const size_t sm = std::max(smem, mm::mix_rec_bwd_floats(Hm, mq.win) * 4);
+  const int gx = (B + 3) / 4, na = gx * N;
+#define MM_PAIR(HA, HMX)                                                                                          \
+  hipLaunchKernelGGL((mm::agent_mixer_bwd_kernel<HA, HMX>), dim3(na + B), dim3(256), sm, (hipStream_t)s, a, q, ma, \
+                     mq, gx, na)
+  if (d->h == 32 && Hm == 32) MM_PAIR(32, 32);
+  else if (d->h == 32) MM_PAIR(32, 64);
+  else if (Hm == 32) MM_PAIR(64, 32);
+  else MM_PAIR(64, 64);
+#undef MM_PAIR
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

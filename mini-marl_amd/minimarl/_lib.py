@@ -218,6 +218,9 @@ _SIGS += [
                              c_vp, c_vp, c_vp, c_vp]),
     ("mm_agent_bwd_seq", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    ("mm_agent_mixer_bwd_seq", c_i32, [ctypes.POINTER(QnetDims), c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp,
+                                       c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_outer_reduce", c_i32, [ctypes.POINTER(OuterArgs), c_vp]),
     ("mm_agent_q_pre2", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_i64, c_vp,
                                 ctypes.POINTER(QFwdIO), c_i64, c_vp]),

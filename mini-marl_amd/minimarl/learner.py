@@ -22,6 +22,7 @@ Adam moments alike), the layout the RCCL gradient all-reduce works on.
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -117,6 +118,8 @@ class QLearner:
         # weight-gradient products as bf16x3 splits (mm_outer_reduce_batch_bf3, ~2^-16 relative); the agent path
         # stays exact f32
         self.mixer_fp16 = bool(mixer_fp16)
+        # the agent BPTT and the mixer recurrence's backward in one launch (MM_LRN_PAIR_BWD=0: side stream)
+        self._pair_bwd = os.environ.get("MM_LRN_PAIR_BWD", "1") != "0"
         self.fast_pre = False           # opt-in: the fp16x3 agent PRE (not at the fp32 gradient bar, see compute_grads)
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM
@@ -406,6 +409,8 @@ class QLearner:
                                ptr(self.qtot_t), self.loss_flags, ptr(self.qa), ptr(self.maxq), ptr(self.dq),
                                ptr(self.dqa), ptr(self.loss_parts), ptr(self.td_last), ptr(self.loss), s), "loss")
         # ---- backward through time (data-gradient chains only)
+        agent_seq = self.seq and B < 512 and self.H in (32, 64)
+        pair_bwd = bool(split) and agent_seq and self.has_mixer and self._pair_bwd
         o = self.beh.offs
         P = self.P
         if self.seq:
@@ -416,14 +421,23 @@ class QLearner:
                          ptr(self.mxws), C)
                 if split:
                     # the hypernet pass (-> dqa for the agents), then the mixer recurrence's backward beside the
-                    # agent BPTT; joined before the weight gradients
+                    # agent BPTT: one shared launch below (mm_agent_mixer_bwd_seq), or the side stream joined
+                    # before the weight gradients
                     check(L.mm_mixer_bwd_seq_hyper(*margs, s), "mixer bwd seq (hypernets)")
-                    side.wait_stream(torch.cuda.current_stream(self.dev))
-                    check(L.mm_mixer_bwd_seq_rec(*margs, s_m), "mixer bwd seq (recurrence)")
+                    if not pair_bwd:
+                        side.wait_stream(torch.cuda.current_stream(self.dev))
+                        check(L.mm_mixer_bwd_seq_rec(*margs, s_m), "mixer bwd seq (recurrence)")
                 else:
                     check(L.mm_mixer_bwd_seq(*margs, s), "mixer bwd seq")
-        agent_seq = self.seq and B < 512 and self.H in (32, 64)
-        if agent_seq:
+        if pair_bwd:
+            # the agent BPTT chain and the mixer recurrence's backward sharing one grid
+            mx = self.mix
+            check(L.mm_agent_mixer_bwd_seq(ctypes.byref(self.beh.dims), ptr(P), o[8], o[5], B, ptr(self.asave),
+                                           ptr(self.acts), ptr(self.dqa), ptr(self.done), ptr(self.ones_f),
+                                           ptr(self.dh), ptr(self.dgi), ptr(self.dgh), ptr(self.dqv), C, mx.S, mx.Hm,
+                                           mx.K1, ptr(mx.flat), ptr(self.msave), ptr(self.qa), ptr(self.dq),
+                                           ptr(self.dhm), ptr(self.mdelta), ptr(self.mxws), s), "agent+mixer bwd seq")
+        elif agent_seq:
             # the agent BPTT chain over all C steps in one launch (W_hh in LDS, dh carried in registers)
             check(L.mm_agent_bwd_seq(ctypes.byref(self.beh.dims), ptr(P), o[8], o[5], B, ptr(self.asave),
                                      ptr(self.acts), ptr(self.dqa), ptr(self.done), ptr(self.ones_f), ptr(self.dh),
@@ -440,7 +454,7 @@ class QLearner:
             check(L.mm_agent_bwd(ctypes.byref(self.beh.dims), ptr(P), o[8], o[5], B, ptr(self.asave[t]),
                                  ctypes.c_void_p(self.acts.data_ptr() + 4 * t * B * N), ptr(self.dqa[t]), ptr(dn),
                                  ptr(self.dh), ptr(self.dgi[t]), ptr(self.dgh[t]), ptr(self.dqv[t]), s), "agent bwd")
-        if split:
+        if split and not pair_bwd:
             torch.cuda.current_stream(self.dev).wait_stream(side)   # join: the mixer deltas are complete
         # ---- deferred weight gradients: batched over all C*B rows, grouped by agent; every
         # outer product of the update (agent + mixer) in ONE split-M launch (+ its partial sum)
