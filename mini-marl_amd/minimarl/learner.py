@@ -120,6 +120,8 @@ class QLearner:
         self.mixer_fp16 = bool(mixer_fp16)
         # the agent BPTT and the mixer recurrence's backward in one launch (MM_LRN_PAIR_BWD=0: side stream)
         self._pair_bwd = os.environ.get("MM_LRN_PAIR_BWD", "1") != "0"
+        # the mixer's forward state projection + recurrence on a side stream (MM_LRN_FWD_SIDE=0: in line)
+        self._fwd_side = os.environ.get("MM_LRN_FWD_SIDE", "1") != "0"
         self.fast_pre = False           # opt-in: the fp16x3 agent PRE (not at the fp32 gradient bar, see compute_grads)
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM
@@ -296,10 +298,11 @@ class QLearner:
         reset_p = ctypes.c_void_p(reset_obs_ptr) if isinstance(reset_obs_ptr, int) else ptr(reset_obs_ptr)
         ND = N * D
         split = self._mixer_split()
-        if split:
+        side = self._side_stream() if split else None
+        fwd_side = split and self._fwd_side
+        if fwd_side:
             # two streams (captured as a fork / join in the update graph): the mixer's state projection and its
             # GRU recurrence need no agent Q, so they run beside the agent PRE / REC chain
-            side = self._side_stream()
             side.wait_stream(torch.cuda.current_stream(self.dev))
             s_m = ctypes.c_void_p(side.cuda_stream)
         else:
@@ -341,7 +344,7 @@ class QLearner:
         if self.double and self._draws is None:
             self.dctr.add_(C)             # stream-ordered: captured into the update graph
         if self.seq:
-            self._forward_seq(L, s, obs_p, reset_p, split)
+            self._forward_seq(L, s, obs_p, reset_p, split, join=fwd_side)
         for t in range(0 if not self.seq else C, C):
             ib, it = QFwdIO(), QFwdIO()
             for io, h, gi in ((ib, self.hb, self.gi_ab), (it, self.ht, self.gi_at)):
@@ -511,7 +514,7 @@ class QLearner:
         mx = self.mix
         check(fn(self.B, self.N, mx.S, mx.Hm, mx.K1, self._mixer_nets(), 2, self.C, ptr(self.done8), s), what)
 
-    def _forward_seq(self, L, s, obs_p, reset_p, split=False):
+    def _forward_seq(self, L, s, obs_p, reset_p, split=False, join=False):
         """REC of both nets over all C steps in one chunk-sequence launch, then the mixers per step."""
         B, C, N, H = self.B, self.C, self.N, self.H
         ib, it = QFwdIO(), QFwdIO()
@@ -530,7 +533,8 @@ class QLearner:
             mx = self.mix
             if split:
                 # join the mixer recurrence (side stream), then the hypernet pass over the agents' Q
-                torch.cuda.current_stream(self.dev).wait_stream(self._side_stream())
+                if join:
+                    torch.cuda.current_stream(self.dev).wait_stream(self._side_stream())
                 self._mixer_seq_call(L, L.mm_mixer_fwd_seq_hyper, s, "mixer fwd seq (hypernets)")
                 return
             if L.mm_mixer_fwd_seq_fits(B, N, mx.Hm, mx.K1):
