@@ -257,6 +257,9 @@ typedef struct mm_rollout_step_io {
   int32_t td_on, td_slot; float gamma;
   const float* td_rew; const uint8_t* td_done; const float* td_qsel; const float* td_maxq; const int32_t* td_act;
   float* chunk_td; uint8_t* store_act; float* store_rew; uint8_t* store_done;
+  /* guard rail: rows of the chunk store; a staging row outside [0, n_rows) is never written through (its env's
+   * stores are skipped) and sets bit 0 of *err (device int32, sticky; may be NULL) */
+  int64_t n_rows; int32_t* err;
 } mm_rollout_step_io;
 /* 1 when the fused step fits: local obs, 8 grid columns and an even row count (4 or 8 agents), E >= 2048, one of
  * the compiled layer widths, LDS budget; 0 otherwise (use the two-launch step). */

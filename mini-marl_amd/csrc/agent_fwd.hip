@@ -105,8 +105,9 @@ __device__ __forceinline__ void load_obs_kblock(const float* orow, int kb, int D
 
 // Q output / argmax / eps-greedy / gather epilogue shared by the fused and the split forward.
 template <int AB>
-__device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_io& io, int agent, int e, bool valid,
-                                             const f32x16 (&qa)[AB], float eps, uint64_t ctr, int act_pre = -1);
+__device__ __forceinline__ int q_epilogue_v(const QFwdParams& p, const mm_qfwd_io& io, int agent, int e, bool valid,
+                                            const f32x16 (&qa)[AB], float eps, uint64_t ctr, int act_pre = -1,
+                                            int64_t out_off = 0);
 template <int AB>
 __device__ __forceinline__ void q_epilogue(const QFwdParams& p, int agent, int e, bool valid, const f32x16 (&qa)[AB]) {
   const mm_qfwd_io& io = p.io;
@@ -114,9 +115,11 @@ __device__ __forceinline__ void q_epilogue(const QFwdParams& p, int agent, int e
   const uint64_t ctr = (io.mode == MM_Q_ACT && io.counter_ptr) ? *io.counter_ptr : io.counter;
   q_epilogue_v<AB>(p, io, agent, e, valid, qa, eps, ctr);
 }
+// returns the selected action (every lane); out_off: element offset of the act / qsel outputs (a ring slot)
 template <int AB>
-__device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_io& io, int agent, int e, bool valid,
-                                             const f32x16 (&qa)[AB], float eps, uint64_t ctr, int act_pre) {
+__device__ __forceinline__ int q_epilogue_v(const QFwdParams& p, const mm_qfwd_io& io, int agent, int e, bool valid,
+                                            const f32x16 (&qa)[AB], float eps, uint64_t ctr, int act_pre,
+                                            int64_t out_off) {
   const int hh = (threadIdx.x & 63) >> 5;
   if (valid && io.q_out) {
     float* qrow = io.q_out + (int64_t)e * io.q_se + (int64_t)agent * io.q_sa;
@@ -128,7 +131,7 @@ __device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_
         if (row < p.A) qrow[row] = qa[ab][s];
       }
   }
-  if (io.mode == MM_Q_NONE) return;
+  if (io.mode == MM_Q_NONE) return 0;
 
   // ---- epilogue: first-index argmax over A rows spread across the two lane halves
   float best = -INFINITY;
@@ -176,19 +179,23 @@ __device__ __forceinline__ void q_epilogue_v(const QFwdParams& p, const mm_qfwd_
       if (ab * 32 + kperm(s, hh) == act) mine = qa[ab][s];
   const float qsel = (io.mode == MM_Q_MAX) ? best : mine + __shfl_xor(mine, 32);
   if (valid && hh == 0) {
-    const int64_t o = (int64_t)e * p.N + agent;
+    const int64_t o = out_off + (int64_t)e * p.N + agent;
     if (io.act_out && io.mode == MM_Q_ACT) io.act_out[o] = act;
     if (io.qsel_out) io.qsel_out[o] = qsel;
   }
+  return act;
 }
 
 // xn: layer-1 k-block 0 of the observation, loaded by the caller (before weight staging).
 // ol(kb, x) loads observation k-block kb (lane (i, hh) holds features 32 kb + kperm(s, hh) of env e);
 // zero_h: start the GRU from zeros (invalid env or reset flag)
+// ovr: the epilogue's epsilon / RNG step counter / output offset are eps_o / ctr_o / off_o instead of read from
+// p.io (the chunk-persistent rollout); returns the selected action (ACT mode)
 template <int F1, int G, int H, int AB, class OL>
-__device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent, int e,
-                                                 const float* __restrict__ W, const OL& ol,
-                                                 float (&xn)[16], bool zero_h) {
+__device__ __forceinline__ int agent_q_fwd_body(const QFwdParams& p, int agent, int e,
+                                                const float* __restrict__ W, const OL& ol,
+                                                float (&xn)[16], bool zero_h, bool ovr = false, float eps_o = 0.f,
+                                                uint64_t ctr_o = 0, int64_t off_o = 0) {
   using S = Sched<F1, G, H, AB>;
   using CG = typename S::CG;
   constexpr int RB1 = S::RB1, RB2 = S::RB2, HB = S::HB, NF = S::NF;
@@ -328,7 +335,9 @@ __device__ __forceinline__ void agent_q_fwd_body(const QFwdParams& p, int agent,
 #pragma unroll
     for (int kb = 0; kb < HB; ++kb) consume(S::NF2 + S::NFG + ab * HB + kb, h1[kb], qa[ab]);
   }
+  if (ovr) return q_epilogue_v<AB>(p, io, agent, e, valid, qa, eps_o, ctr_o, -1, off_o);
   q_epilogue<AB>(p, agent, e, valid, qa);
+  return 0;
 }
 
 // ---------------------------------------------------------------- split forward (training)
@@ -1112,8 +1121,8 @@ __device__ __forceinline__ void load_obs_ks(const float* orow, int kb, int D, fl
 // Q output / argmax / eps-greedy / gather epilogue for 16-row Q tiles (rows 16t + 4g + r).
 // out_off: element offset of the act / qsel outputs (the fused rollout step's ring slot)
 template <int AT>
-__device__ __forceinline__ void q_epilogue16(const QFwdParams& p, int agent, int e, bool valid,
-                                             const f32x4 (&qa)[AT], float eps, uint64_t ctr, int64_t out_off = 0) {
+__device__ __forceinline__ int q_epilogue16(const QFwdParams& p, int agent, int e, bool valid,
+                                            const f32x4 (&qa)[AT], float eps, uint64_t ctr, int64_t out_off = 0) {
   const int g = (threadIdx.x & 63) >> 4;
   const mm_qfwd_io& io = p.io;
   if (valid && io.q_out) {
@@ -1126,7 +1135,7 @@ __device__ __forceinline__ void q_epilogue16(const QFwdParams& p, int agent, int
         if (row < p.A) qrow[row] = qa[t][r];
       }
   }
-  if (io.mode == MM_Q_NONE) return;
+  if (io.mode == MM_Q_NONE) return 0;
   float best = -INFINITY;
   int bi = 0x7fffffff;
 #pragma unroll
@@ -1181,11 +1190,12 @@ __device__ __forceinline__ void q_epilogue16(const QFwdParams& p, int agent, int
     if (io.act_out && io.mode == MM_Q_ACT) io.act_out[o] = act;
     if (io.qsel_out) io.qsel_out[o] = qsel;
   }
+  return act;
 }
 
 // ol(kb, x) loads observation k-step kb (lane (c, g) holds features 32 kb + kperm16(j, g) of env e)
 template <int F1, int G, int H, int AB, class OL>
-__device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int agent, int e,
+__device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agent, int e,
                                                     const float* __restrict__ W, const OL& ol,
                                                     float (&xn)[8], const f32x4 (&h0)[H / 16], float eps,
                                                     uint64_t ctr, int64_t out_off = 0, int x16_from_kb = 1 << 30) {
@@ -1375,7 +1385,7 @@ __device__ __forceinline__ void agent_q_fwd_body_h3(const QFwdParams& p, int age
       for (int kb = 0; kb < HB; ++kb) mm16(W + CG::off_q + ((t >> 1) * HB + kb) * 1024, t & 1, h1s[kb], lane, qa[t]);
     }
   }
-  q_epilogue16<AT>(p, agent, e, valid, qa, eps, ctr, out_off);
+  return q_epilogue16<AT>(p, agent, e, valid, qa, eps, ctr, out_off);
 }
 
 // The LDS-staged large-E kernel on the fp16x3 image: a 1024-thread block (16 waves x 16 envs = 256
@@ -1487,18 +1497,38 @@ struct RollStep {   // kernarg right after the two QFwdParams (read through the 
   uint8_t* done;           // [E]
   uint64_t* counter;       // [2] RNG step counter, double-buffered
   TdFuse td;               // step t - 1's TD / store (td.on), td.counter unused
-  uint64_t* trace;         // timing trace (MM_ROLL_TRACE; tools/roll_trace.py), nullptr normally
+  uint64_t* trace;         // timing trace (MM_ROLL_TRACE builds only; tools/roll_trace.py), nullptr normally
+  int64_t n_rows;          // chunk-store rows: a staging row outside [0, n_rows) is never written through
+  uint32_t* err;           // sticky error bits (bit 0: a corrupt staging row was skipped)
   int par, begin, lds_env, pad_;   // state buffer read; chunk start (also write s_t to slot 0); env LDS offset
 };
-// timing stamps (s_memrealtime, 100 MHz) of block b at trace[8 b + i] when tracing
+// a store row the kernel may write through; otherwise the sticky error bit 0 is set and the row's stores skipped
+__device__ __forceinline__ bool roll_row_ok(int64_t row, int64_t n_rows, uint32_t* err) {
+  const bool ok = row >= 0 && row < n_rows;
+  if (!ok && err) atomicOr(err, 1u);
+  return ok;
+}
+// timing stamps (s_memrealtime, 100 MHz) of block b at trace[8 b + i] when tracing (builds with -DMM_ROLL_DEBUG=1
+// only: tools/roll_trace.py, tools/roll_probe.py); compiled out of the product kernel
+#ifndef MM_ROLL_DEBUG
+#define MM_ROLL_DEBUG 0
+#endif
+#if MM_ROLL_DEBUG
 #define MM_RSTAMP(i, cond)                                                                             \
   do {                                                                                                 \
     if (rs.trace && (cond) && blockIdx.x < 512) rs.trace[8 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+#else
+#define MM_RSTAMP(i, cond) \
+  do {                     \
+  } while (0)
+#endif
 
 static_assert(sizeof(QFwdParams) % 8 == 0 && alignof(RollStep) == 8, "rollout_step kernarg layout");
-#ifndef MM_ROLL_PROBE
-#define MM_ROLL_PROBE 0   // timing probes only (tools/roll_probe.py): 1 skip the env step, 2 skip the obs build, 4 skip obs stores
+#if MM_ROLL_DEBUG && defined(MM_ROLL_PROBE_BITS)
+#define MM_ROLL_PROBE MM_ROLL_PROBE_BITS   // timing probes only (tools/roll_probe.py): 1 skip the env step, 2 skip the obs build, 4 skip obs stores
+#else
+#define MM_ROLL_PROBE 0
 #endif
 static constexpr int kRollMaxN = 10;    // 3 ceil(N / 2) <= 16 rows and agent markers 3 + k in a nibble
 static constexpr int kRollMaxR = 16;    // rows of 8 cells: one 32-bit nibble word per row
@@ -1573,7 +1603,9 @@ __device__ __forceinline__ void roll_store4(float* dst, int f0, int D, const flo
 template <int F1, int G, int H, int AB>
 __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QFwdParams p1, RollStep rs_) {
   extern __shared__ __attribute__((aligned(16))) float wsm[];
+#if MM_ROLL_DEBUG
   const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();   // (timing trace only)
+#endif
   const bool second = (int)blockIdx.x >= p0.nblocks;     // p0: target net on s'_t, p1: behavior net on s_{t+1}
   // parameters read from the kernarg segment on demand (uniform scalar loads) instead of held in SGPRs
   const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1678,10 +1710,11 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
       const float dn = dd ? 1.0f : 0.0f;
       const float v = fabsf(sr + (1.0f - dn) * td.gamma * st - sq);
       td.chunk_td[e0 + i] = (td.slot == 0 ? 0.0f : ctd[i]) + v;
-      td.s_done[trow[i] * td.C + td.slot] = dd;
+      if (roll_row_ok(trow[i], rs.n_rows, rs.err)) td.s_done[trow[i] * td.C + td.slot] = dd;
     }
     for (int q = i; q < ne * N; q += 768) {
       const int l = q / N, k = q - l * N;
+      if (trow[l] < 0 || trow[l] >= rs.n_rows) continue;   // (flagged above)
       const int64_t o = (trow[l] * td.C + td.slot) * N + k;
       td.s_act[o] = (uint8_t)tact[q];
       td.s_rew[o] = trew[q];
@@ -1692,7 +1725,10 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
     const int32_t* pw = reinterpret_cast<const int32_t*>(stg + st_pos) + le_d * N;
     const int32_t* ac = reinterpret_cast<const int32_t*>(stg + st_act) + le_d * N;
     const uint4* gin = reinterpret_cast<const uint4*>(stg + st_grid + le_d * RC);
-    if (writer) myrow = reinterpret_cast<const int64_t*>(stg + st_srow)[le_d];
+    if (writer) {
+      myrow = reinterpret_cast<const int64_t*>(stg + st_srow)[le_d];
+      if (!roll_row_ok(myrow, rs.n_rows, rs.err)) myrow = -1;   // a corrupt row is never handed on as cur_row
+    }
     steps0 = reinterpret_cast<const int32_t*>(stg + st_steps)[le_d];
     apples0 = reinterpret_cast<const int32_t*>(stg + st_apples)[le_d];
 #pragma unroll
@@ -1720,12 +1756,17 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
   if (!second) {
     const int64_t* st_rows = reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(wsm) + st_srow);
     const int l16 = wave * 16 + (lane & 15), l32 = wave * 32 + (lane & 31);
+    // out-of-range rows -> -1 (sticky error bit 0): no store of this env goes through them
     if (e0 + l16 < E) srow_h3 = st_rows[l16];
     if (l32 < 256 && e0 + l32 < E) srow_ex = st_rows[l32];
+    if (e0 + l16 < E && !roll_row_ok(srow_h3, rs.n_rows, rs.err)) srow_h3 = -1;
+    if (l32 < 256 && e0 + l32 < E && !roll_row_ok(srow_ex, rs.n_rows, rs.err)) srow_ex = -1;
   }
   MM_RSTAMP(1, threadIdx.x == 0);
   __syncthreads();
+#if MM_ROLL_DEBUG
   if (rs.trace && threadIdx.x == 0 && blockIdx.x < 512) rs.trace[8 * blockIdx.x + 2] = t_entry;
+#endif
   // ---- waves 4-15, once the env inputs have been consumed: the weight image DMA into the staging region
   // (range-guarded agents: the exact-f32 image) while waves 0-3 run the env step
   if (wave >= 4) {
@@ -1740,12 +1781,12 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
     // chunk start: slot 0 of the staging rows <- s_t, the observation of the state before this step; lane
     // (env, g) writes features 16 q + 4 g .. + 3 of its env
     __syncthreads();
-    if (!second && e < E) {
+    if (!second && e < E && srow_h3 >= 0) {
       const int rc = spos[le * N + agent];
       const uint64_t wd =
           roll_obs_word(reinterpret_cast<const uint32_t*>(sgrid) + le * roll_gbw(R), R, rc >> 4, rc & 15);
       const float cr = stab[rc >> 4], cc = stab[R + (rc & 15)];
-      float* d0 = rs.store_obs + rs.staging[e] * rs.row_stride + (int64_t)agent * D;
+      float* d0 = rs.store_obs + srow_h3 * rs.row_stride + (int64_t)agent * D;
       for (int f0 = 4 * (lane >> 4); f0 < D; f0 += 16) {
         float x[4];
         roll_feat4(wd, f0, cr, cc, x);
@@ -1839,7 +1880,8 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
     const bool r32 = !second && io.reset && e32 < E && io.reset[e32];
     __syncthreads();
     const bool bd = second && e32 < E && sdone[l32];
-    float* dst = (!second && e32 < E) ? rs.store_obs + srow32 * rs.row_stride + rs.next_off + (int64_t)agent * D : nullptr;
+    float* dst = (!second && e32 < E && srow32 >= 0) ? rs.store_obs + srow32 * rs.row_stride + rs.next_off + (int64_t)agent * D
+                                                      : nullptr;
     const int rc32 = spos[l32 * N + agent];
     const uint64_t wd32 =
         roll_obs_word(reinterpret_cast<const uint32_t*>(sgrid) + l32 * roll_gbw(R), R, rc32 >> 4, rc32 & 15);
@@ -1887,7 +1929,8 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
   // the store destination of s'_t (target blocks), loaded after the env step (a global load before it would be
   // waited on inside the dynamics loop by the spill reloads' vmcnt)
   const int64_t srow = srow_h3;
-  float* dst = (!second && e < E) ? rs.store_obs + srow * rs.row_stride + rs.next_off + (int64_t)agent * D : nullptr;
+  float* dst = (!second && e < E && srow >= 0) ? rs.store_obs + srow * rs.row_stride + rs.next_off + (int64_t)agent * D
+                                               : nullptr;
   const int rc = spos[le * N + agent];
   const uint64_t wd = roll_obs_word(reinterpret_cast<const uint32_t*>(sgrid) + le * roll_gbw(R), R, rc >> 4, rc & 15);
   const float cr = stab[rc >> 4], cc = stab[R + (rc & 15)];
@@ -2599,7 +2642,14 @@ int rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, cons
                    x->store_rew, x->store_done, x->staging, nullptr, x->gamma, x->td_slot, x->chunk_len, 1};
   }
   rs.par = x->state_in;
+#if MM_ROLL_DEBUG
   rs.trace = debug_trace_buffer("MM_ROLL_TRACE");
+#else
+  rs.trace = nullptr;
+#endif
+  MM_REQUIRE(x->n_rows >= 1 && x->n_rows < (1ll << 40), "rollout_step: n_rows must be the chunk store's row count");
+  rs.n_rows = x->n_rows;
+  rs.err = reinterpret_cast<uint32_t*>(x->err);
   rs.begin = x->begin ? 1 : 0;
   rs.lds_env = (int)roll_region(env->d, p0.g);
   const int AB = (d->n_actions + 31) / 32;

@@ -1091,7 +1091,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   __shared__ uint64_t cl[MB_CAND_LDS];
   __shared__ uint16_t cb[MB_CAND_LDS];
   __shared__ uint32_t s_n;
-  __shared__ uint32_t bins[256];
+  __shared__ __attribute__((aligned(16))) uint32_t bins[256];   // mb_minmax reuses it as uint64_t
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
   __shared__ uint32_t s_last;

@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MM_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libminimarl.so")  # A/B runs
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libminimarl.so")
+# (A/B tools that load another build of the library assign LIB_PATH before the first lib() call)
 
 c_i32 = ctypes.c_int32
 c_i64 = ctypes.c_int64
@@ -54,6 +55,7 @@ class RollStepIO(ctypes.Structure):
         ("td_on", c_i32), ("td_slot", c_i32), ("gamma", c_f32),
         ("td_rew", c_vp), ("td_done", c_vp), ("td_qsel", c_vp), ("td_maxq", c_vp), ("td_act", c_vp),
         ("chunk_td", c_vp), ("store_act", c_vp), ("store_rew", c_vp), ("store_done", c_vp),
+        ("n_rows", c_i64), ("err", c_vp),
     ]
 
 

@@ -33,7 +33,6 @@ rows back as the next staging rows (no chunk copy).
 """
 import ctypes
 import math
-import os
 
 import torch
 
@@ -82,8 +81,6 @@ class RolloutEngine:
                                                                     E) != 0
         if fused and not ok:
             raise ValueError("RolloutEngine(fused=True): the fused rollout step does not support this configuration")
-        if fused is None and os.environ.get("MM_FUSED_STEP", "1") == "0":   # A/B runs: force the two-launch step
-            fused = False
         self.fused = ok if fused is None else bool(fused)
         nb = 3 if self.fused else 2
         if self.fused:
@@ -106,6 +103,9 @@ class RolloutEngine:
         self.rew_buf = [torch.zeros(E, N, device=dev) for _ in range(2)]
         self.maxq, self.rew = self.maxq_buf[0], self.rew_buf[0]
         self.chunk_td = torch.zeros(E, device=dev)
+        # sticky device error bits of the rollout kernels (bit 0: a staging row outside the chunk store was skipped;
+        # bit 1: a chunk-persistent launch timed out waiting for a hand-off); polled by check_errors()
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.eps_dev = torch.zeros(1, device=dev)
         # rollout step counter (RNG stream); the fused mode double-buffers it (slot t % 2 is read at step t)
         self.counter_dev = torch.zeros(2, dtype=torch.int64, device=dev)
@@ -213,6 +213,18 @@ class RolloutEngine:
         self.io_b0 = self._io_behavior(0)
         self.io_b0.counter_ptr = None
         self.io_b0.counter = 0x7FFFFFFFFFFFFFFF
+    def check_errors(self, clear=True):
+        """Raise if a rollout kernel set a sticky error bit (synchronous): bit 0 = a staging row outside the chunk
+        store was met and that env's stores were skipped (a corrupt PER slot map), bit 1 = a chunk-persistent launch
+        gave up waiting for a tile's action hand-off (its blocks were not co-resident)."""
+        w = int(self.err.item())
+        if clear:
+            self.err.zero_()
+        if w:
+            raise RuntimeError(f"rollout engine device error bits {w:#x}: "
+                               + ("corrupt staging row skipped; " if w & 1 else "")
+                               + ("chunk-persistent hand-off timed out; " if w & 2 else ""))
+
     def sync_target(self):
         self.target.copy_from(self.behavior)
 
@@ -296,6 +308,7 @@ class RolloutEngine:
         x.slot, x.chunk_len, x.begin = c + 1, self.C, int(c == 0)
         x.staging, x.cur_row = ptr(self.staging), ptr(self.cur_row)
         x.rew, x.done, x.state_in, x.counter = ptr(self.rew_buf[k2]), ptr(self.done_buf[k2]), k2, ptr(self.counter_dev)
+        x.n_rows, x.err = self.store.rows, ptr(self.err)
         if c >= 1 and not self._td_flushed:
             kp, kp3 = 1 - k2, (t - 1) % 3
             x.td_on, x.td_slot, x.gamma = 1, c - 1, self.gamma
@@ -515,6 +528,7 @@ class RolloutEngine:
         x.slot, x.chunk_len, x.begin = c + 1, self.C, 0
         x.staging, x.cur_row = ptr(self.staging), ptr(self.cur_row)
         x.rew, x.done, x.state_in, x.counter = ptr(self.rew_buf[k2]), ptr(self.done_buf[k2]), k2, ptr(self.counter_dev)
+        x.n_rows, x.err = self.store.rows, ptr(self.err)
         check(lib().mm_rollout_step(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
                                     ctypes.byref(self.fio_t[k2]), ptr(self.behavior.packed),
                                     ctypes.byref(self.fio_b[(k2, k3)]), self.E, ctypes.byref(x), s), "rollout_step")

@@ -22,7 +22,6 @@ Adam moments alike), the layout the RCCL gradient all-reduce works on.
 """
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -101,7 +100,7 @@ class QLearner:
 
     def __init__(self, behavior, target, mixer=None, target_mixer=None, batch=32, chunk=10, gamma=0.99, lr=1e-3,
                  grad_clip=5.0, betas=(0.9, 0.999), adam_eps=1e-8, mode="qmix", clip_mixer=False, device="cuda",
-                 reference_compat=True, mixer_fp16=False):
+                 reference_compat=True, mixer_fp16=False, pair_bwd=True, fwd_side=True):
         assert mode in ("qmix", "vdn", "qmix_min", "vdn_double")
         self.mode = mode
         self.has_mixer = mode in ("qmix", "qmix_min")
@@ -118,10 +117,10 @@ class QLearner:
         # weight-gradient products as bf16x3 splits (mm_outer_reduce_batch_bf3, ~2^-16 relative); the agent path
         # stays exact f32
         self.mixer_fp16 = bool(mixer_fp16)
-        # the agent BPTT and the mixer recurrence's backward in one launch (MM_LRN_PAIR_BWD=0: side stream)
-        self._pair_bwd = os.environ.get("MM_LRN_PAIR_BWD", "1") != "0"
-        # the mixer's forward state projection + recurrence on a side stream (MM_LRN_FWD_SIDE=0: in line)
-        self._fwd_side = os.environ.get("MM_LRN_FWD_SIDE", "1") != "0"
+        # the agent BPTT and the mixer recurrence's backward in one launch (pair_bwd=False: side stream)
+        self._pair_bwd = bool(pair_bwd)
+        # the mixer's forward state projection + recurrence on a side stream (fwd_side=False: in line)
+        self._fwd_side = bool(fwd_side)
         self.fast_pre = False           # opt-in: the fp16x3 agent PRE (not at the fp32 gradient bar, see compute_grads)
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM

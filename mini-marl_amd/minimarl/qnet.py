@@ -285,11 +285,13 @@ class Q_Net:
         return self.forward(obs, hidden)
 
     def _packed(self):
-        """The fragment image, repacked by the ``minimarl::qnet_pack`` op when the params changed."""
+        """The fragment image, repacked by the ``minimarl::qnet_pack`` op when the params changed — or when only
+        the exact-f32 image is current (``_h3_stale``: a learner update ran ``pack_f32``), since a large-batch
+        forward reads the fp16x3 image and its range flags (qnet_pack writes all three)."""
         from .ops import dims, load
-        if self.net._dirty:
+        if self.net._dirty or self.net._h3_stale:
             load().qnet_pack(self.net.flat, dims(self.net), self.net.packed)
-            self.net._dirty = False
+            self.net._dirty = self.net._h3_stale = False
         return self.net.packed
 
     def forward(self, obs, hidden):

@@ -145,6 +145,7 @@ class QTrainer:
         """Raise if a device-side sticky error bit is set (the PER's out-of-range priority-update nodes, skipped on
         the device where the reference's tree write would raise); polled at the host syncs train() already has."""
         self.eng.per.check_errors()
+        self.eng.check_errors()
 
     def train(self, n_episodes, log=None):
         """Run n_episodes training episodes; greedy tests every test_interval episodes (host sync); the device
@@ -207,6 +208,9 @@ class QTrainer:
         eng = self.eng
         self.learner.restore_tensors({k[8:]: v for k, v in ts.items() if k.startswith("learner/")}, scalars["learner"])
         eng.per.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("per/")})
+        # the step count first: the fused step double-buffers the env state by step parity (env.state_buffer()
+        # = t % 2), so the restored state must land in the buffer the next step reads
+        eng.t, eng.chunks_inserted = int(scalars["t"]), int(scalars["chunks_inserted"])
         eng.env.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("env/")})
         for k, v in eng.state_buffers().items():
             if "engine/" + k not in ts:
@@ -217,7 +221,6 @@ class QTrainer:
                 copy_into(getattr(eng.store, k), ts["store/" + k], k)
         copy_into(self.ep_ret, ts["trainer/ep_ret"], "ep_ret")
         copy_into(self.score_acc, ts["trainer/score_acc"], "score_acc")
-        eng.t, eng.chunks_inserted = int(scalars["t"]), int(scalars["chunks_inserted"])
         eng._primed, eng._td_pending = bool(scalars["primed"]), bool(scalars["td_pending"])
         eng._eps_host = None
         eng.behavior.mark_dirty()

@@ -135,6 +135,39 @@ def test_learner_adapter_rebinds(golden):
     assert torch.isfinite(q).all()
 
 
+def test_adapter_large_batch_forward_after_update_uses_new_weights(golden):
+    """After an adapter train step (the learner repacks only the exact-f32 image, pack_f32), a large-batch
+    forward (B >= 2048: the fp16x3 LDS kernel and its range flags) must see the updated weights: equal to a
+    fresh Q_Net loaded with the same state_dict (full pack). ADVICE r4: _packed() ignored _h3_stale."""
+    from minimarl.adapters import Mix_Net, Q_Net, Train_dqn
+    fx = golden("qmix_train")
+    N, D = fx["states"].shape[2:]
+    obs_sp, act_sp = [_Space((D,))] * N, [_Space(n=5)] * N
+    args = _args(fx)
+    bq, tq = Q_Net(obs_sp, act_sp, args), Q_Net(obs_sp, act_sp, args)
+    bm, tm = Mix_Net(obs_sp, args), Mix_Net(obs_sp, args)
+    sd = lambda p: {k[len(p):]: fx[k] for k in fx if k.startswith(p)}  # noqa: E731
+    bq.load_state_dict(sd("before_q."))
+    tq.load_state_dict(sd("target_q."))
+    bm.load_state_dict(sd("before_m."))
+    tm.load_state_dict(sd("target_m."))
+    B = 4096
+    g = torch.Generator().manual_seed(5)
+    obs = (torch.rand(B, N, D, generator=g) < 0.2).float()
+    obs[..., :2] = torch.rand(B, N, 2, generator=g)
+    h = torch.randn(B, N, bq.net.H, generator=g) * 0.3
+    q_before, _ = bq(obs, h)                      # packs both images at the initial weights
+    Train_dqn(args, DEV).train(FixtureReplay(fx), bq, bm, tq, tm,
+                               torch.optim.Adam(params=[torch.zeros(1)], lr=float(fx["lr"])), 0.1)
+    q_after, h_after = bq(obs, h)
+    fresh = Q_Net(obs_sp, act_sp, args)
+    fresh.load_state_dict(bq.state_dict())
+    q_ref, h_ref = fresh(obs, h)
+    torch.cuda.synchronize()
+    assert not torch.equal(q_after, q_before)
+    assert torch.equal(q_after, q_ref) and torch.equal(h_after, h_ref)
+
+
 def test_mix_net_adapter_golden(golden):
     from minimarl.adapters import Mix_Net
     fx = golden("mixnet")

@@ -139,3 +139,36 @@ def test_trainer_resume_bit_identical(tmp_path):
                  (a.score_acc, b.score_acc)]:
         assert torch.equal(x, y)
     assert a.eng.per.alpha == b.eng.per.alpha and a.eng.per.alpha > cfg.alpha
+
+
+def test_trainer_resume_bit_identical_fused_odd_step(tmp_path):
+    """The same at the fused one-launch step's geometry (E = 2048, 4 agents, local obs), checkpointed at an ODD
+    step count: the fused step double-buffers the env state by step parity, so the restore must write the state
+    into the buffer the next step reads (the restore used to run before the step count was set)."""
+    from minimarl.checkpoint import load_checkpoint, save_checkpoint
+    from minimarl.config import QTrainConfig
+    from minimarl.train import QTrainer
+    cfg = QTrainConfig(algo="qmix", n_envs=2048, n_agents=4, full_observable=False, buffer_limit=4096, max_step=13,
+                       update_iter=2, update_target_interval=2, test_interval=0, test_envs=0,
+                       epsilon_anneal_episode=10, seed=11)
+    a = QTrainer(cfg, device=DEV)
+    assert a.eng.fused
+    a.train_episode()
+    assert a.eng.t % 2 == 1
+    path = str(tmp_path / "trainer_fused.safetensors")
+    save_checkpoint(path, trainer=a)
+    for _ in range(2):
+        a.train_episode()
+    b = QTrainer(cfg, device=DEV)
+    load_checkpoint(path, trainer=b)
+    assert b.eng.t == a.eng.t - 26 and b.eng.t % 2 == 1
+    for _ in range(2):
+        b.train_episode()
+    torch.cuda.synchronize()
+    for x, y in [(a.learner.P, b.learner.P), (a.eng.per.tree(), b.eng.per.tree()),
+                 (a.eng.per.slot_rows(), b.eng.per.slot_rows()), (a.eng.store.obs, b.eng.store.obs),
+                 (a.eng.store.act, b.eng.store.act), (a.eng.h, b.eng.h), (a.eng.ht, b.eng.ht),
+                 (a.score_acc, b.score_acc)]:
+        assert torch.equal(x, y)
+    for x, y in zip(a.eng.env.get_state(), b.eng.env.get_state()):
+        assert np.array_equal(x, y)

@@ -141,3 +141,39 @@ def test_fused_step_not_taken_for_odd_band_counts():
         assert not eng.fused
         with pytest.raises(ValueError):
             RolloutEngine(2048, n, f1=64, g=32, h=32, chunk=10, capacity=4096, fused=True, device=DEV)
+
+
+def test_fused_step_skips_corrupt_staging_row():
+    """Guard rail: a staging row outside the chunk store (a corrupt PER slot map) is never written through by the
+    fused step (obs store, chunk-start slot 0, the folded TD / act / rew / done store) and sets the engine's sticky
+    error bit 0, which check_errors() raises; every other env's stores match an uncorrupted twin bit for bit."""
+    from minimarl.engine import RolloutEngine
+    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=2 * 2048, seed=31, device=DEV)
+    a = RolloutEngine(2048, 8, fused=True, **kw)
+    b = RolloutEngine(2048, 8, fused=True, **kw)
+    for _ in range(3):
+        a.step(0.3)
+        b.step(0.3)
+    a.check_errors()
+    bad = [5, 700, 2047]
+    good_rows = b.staging.clone()
+    with torch.no_grad():
+        b.staging[5] = b.store.rows + 100
+        b.staging[700] = -3
+        b.staging[2047] = b.store.rows
+    for _ in range(4):
+        a.step(0.3)
+        b.step(0.3)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="corrupt staging row"):
+        b.check_errors()
+    b.check_errors()                                    # cleared
+    keep = torch.ones(2048, dtype=torch.bool)
+    keep[bad] = False
+    rows = good_rows.cpu()[keep]
+    for x, y in ((a.store.obs, b.store.obs), (a.store.act, b.store.act), (a.store.rew, b.store.rew),
+                 (a.store.done, b.store.done)):
+        assert torch.equal(x.cpu()[rows], y.cpu()[rows])
+    assert torch.equal(a.chunk_td.cpu()[keep], b.chunk_td.cpu()[keep])
+    # corrupt rows are never handed on as cur_row
+    assert not (b.cur_row.cpu()[bad] >= b.store.rows).any() and not (b.cur_row.cpu()[bad] < -1).any()

@@ -565,21 +565,23 @@ def test_multi_sample_blocks_bit_identical(knob):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
 
 
-def test_paired_bwd_launch_matches_side_stream(monkeypatch):
+@pytest.mark.parametrize("fwd_side", [True, False])
+def test_paired_bwd_launch_matches_side_stream(fwd_side):
     """The agent BPTT and the mixer recurrence's backward sharing one launch (mm_agent_mixer_bwd_seq, the default
-    on the split mixer path) against the side-stream version (MM_LRN_PAIR_BWD=0): bit-identical parameters and
-    loss after three captured updates at the bench's B = 32 shape."""
+    on the split mixer path) against the side-stream version (QLearner(pair_bwd=False)), with the mixer's forward
+    on its side stream or in line (fwd_side): bit-identical parameters and loss after three captured updates at
+    the bench's B = 32 shape."""
     from minimarl.engine import RolloutEngine
     from minimarl.learner import Mixer, QLearner
     res = []
     for v in ("1", "0"):
-        monkeypatch.setenv("MM_LRN_PAIR_BWD", v)
         eng = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, device="cuda")
         for _ in range(2):
             eng.run_graph(0.5)
         N, D = eng.N, eng.D
         mix, tmix = Mixer(N, N * D, 64, 32, "cuda", seed=7), Mixer(N, N * D, 64, 32, "cuda", seed=7)
-        lrn = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda")
+        lrn = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda",
+                       pair_bwd=v == "1", fwd_side=fwd_side)
         assert lrn._pair_bwd == (v == "1") and lrn._mixer_split()
         lrn.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=1)
         for _ in range(3):
