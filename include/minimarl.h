@@ -267,6 +267,46 @@ int mm_rollout_step_supported(const mm_env* env, const mm_qnet_dims* d, int64_t 
 int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
                     const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_step_io* x,
                     mm_stream_t s);
+/* The rollout steps [c0, c0 + n_steps) of ONE chunk in ONE launch (chunk-persistent; replaces n_steps iterations
+ * of the reference's per-step loop body, vdn/main.py:93-167 / qmix/main.py:186-233, like n_steps mm_rollout_step
+ * calls, with bit-identical results): every (net, agent, 256-env tile) block stays resident for all the steps, keeps
+ * its weight image and its copy of the tile's env state in LDS, and waits only for the tile's behavior actions of
+ * each step (a tile-local hand-off through handoff / flags), never for a launch boundary. Per step t = c0 + i:
+ * rewards into rew + i E N, dones into done + i E, cur_row; the target's max Q'_t into io_t->qsel_out + t_off0 +
+ * i E N; the behavior's act / Q(a) of step t + 1 into io_b->act_out / qsel_out + b_off0 + i E N (+ b_offn for the
+ * next chunk's step 0 when t + 1 = chunk_len); s'_t into slot t + 1 (and at t = 0 s_0 into slot 0) of row
+ * staging[e]. act0 holds the actions of step c0, done_prev the dones of step c0 - 1. Hidden states are updated in
+ * place (h_in == h_out, io.reset NULL). The TD / chunk-store fold of the steps is mm_td_fold_range. ctl = device
+ * int64 [3]: launch sequence, env state buffer (low int32 of ctl[1], read; flipped by each launch: see
+ * mm_env_get_state_buf), arrival ticket — zero-initialised once, then owned by these launches.
+ * flags [T][N] (8 B) and handoff [T][chunk_len][N][256] (bytes), T = ceil(E / 256), zero-initialised. Supported
+ * when mm_rollout_chunk_supported() != 0 (the fused step's geometry and 2 N T blocks <= the device's CUs: all
+ * blocks must be co-resident; a hand-off wait longer than 20 ms sets bit 1 of *err and proceeds). */
+typedef struct mm_rollout_chunk_io {
+  float* store_obs; int64_t row_stride; int64_t n_rows;
+  const int64_t* staging; int64_t* cur_row;
+  int32_t c0, n_steps, chunk_len, pad_;
+  const int32_t* act0; const uint8_t* done_prev;
+  float* rew; uint8_t* done;
+  int64_t b_off0, b_offn, t_off0;
+  int64_t* counter;      /* device RNG step counter: step c0 + i draws with *counter + i; += n_steps */
+  int64_t* ctl;          /* device int64 [3]: launch sequence, env state buffer (low int32), arrival ticket */
+  int64_t* flags; uint8_t* handoff;
+  int32_t* err;
+} mm_rollout_chunk_io;
+int mm_rollout_chunk_supported(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs);
+int mm_rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
+                     const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_chunk_io* x,
+                     mm_stream_t s);
+/* The TD / chunk-store fold of n_slots consecutive rollout steps slot0 .. slot0 + n_slots - 1 of a chunk (what
+ * n_slots mm_td_chunk_step_rows calls do, identical results; cal_td_error + the chunk lists, vdn/_utils.py:44-52,
+ * vdn/main.py:140-167): step j's rew / q_taken / max_q_next / act at + j ring_se elements, done at + j n_envs; rows
+ * outside [0, n_rows) are skipped and set bit 0 of *err (may be NULL). At most 16 slots per call. */
+int mm_td_fold_range(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                     const float* q_taken, const float* max_q_next, const int32_t* act, int64_t ring_se,
+                     int32_t slot0, int32_t n_slots, int32_t chunk_len, float* chunk_td, uint8_t* store_act,
+                     float* store_rew, uint8_t* store_done, const int64_t* rows, int64_t n_rows, int32_t* err,
+                     mm_stream_t s);
 /* TD step writing into store rows rows[e]; increments the device RNG step counter (may be NULL). */
 int mm_td_chunk_step_rows(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                           const float* q_taken, const float* max_q_next, const int32_t* act, float* chunk_td,

@@ -1964,6 +1964,477 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
   MM_RSTAMP(7, threadIdx.x == 64 * 15);
 }
 
+// ---------------------------------------------------------------- chunk-persistent rollout
+// The rollout steps of (part of) one chunk in ONE launch (mm_rollout_chunk): each (net, agent, 256-env tile) block
+// of rollout_step_kernel stays resident for all n steps, so its weight image is DMA'd into LDS once per launch
+// instead of once per step, its copy of the tile's env state (grids, positions, dones) lives in LDS across the
+// steps, and the only cross-block dependency of a step — the N behavior blocks' actions of the tile, which every
+// block of the tile needs for its (redundant) env dynamics — is a tile-local hand-off through HBM (per-step
+// slots, written write-through `sc1` + `s_waitcnt vmcnt(0)` + an `sc1` flag store, polled with `sc1` loads:
+// MI355X_MICROARCH.md's inter-workgroup hand-off, row 1), not a launch boundary. Per step t = c0 + i (same
+// arithmetic as rollout_step_kernel, results bit-identical):
+//   (1) i > 0: wave 0 polls the N behavior flags of the tile; the dynamics lanes load the actions of step t;
+//   (2) envs that ended at step t - 1 are reset in LDS (the launch's initial state is already post-reset);
+//   (3) chunk start (c == 0): target blocks store s_t into slot 0 of their rows;
+//   (4) waves 0-3: the env dynamics of step t (one lane per env, one LDS round trip per agent); the tile's
+//       writer block (target net, agent 0) writes rew / done of step t into their ring positions and cur_row;
+//   (5) every wave: the forward (target on s'_t -> max Q'_t, storing s'_t into slot c + 1; behavior on s_{t+1}
+//       -> act / Q(a) of step t + 1 into their ring positions); behavior blocks then publish their actions.
+// The TD / chunk-store fold of the launch's steps runs afterwards (mm_td_fold_range). Blocks are mapped so that a
+// tile's 2N blocks share an XCD (blocks b, b + 8, ... share one: MI355X_MICROARCH.md "Workgroup dispatch"), which
+// keeps the hand-off in one L2 — a speed choice only, correctness never depends on placement. All blocks must be
+// co-resident (one per CU, the host checks the grid against the CU count); every wait has a time limit (sticky
+// error bit 1 on expiry, the block then proceeds) so the grid always drains. The last block to finish advances
+// the launch state (RNG step counter += n, env state buffer flipped, launch sequence + 1).
+// the dynamic LDS of the rollout kernels (one extern array per kernel; helper for device functions)
+__device__ __forceinline__ float* wsm_ptr() {
+  extern __shared__ __attribute__((aligned(16))) float wsm_dyn[];
+  return wsm_dyn;
+}
+struct RollChunk {   // kernarg right after the two QFwdParams
+  EnvDev env;
+  float* store_obs;
+  int64_t row_stride;
+  const int64_t* staging;
+  int64_t* cur_row;
+  int64_t n_rows;
+  const int32_t* act0;       // [E][N] actions of the launch's first step
+  const uint8_t* done_prev;  // [E] dones of the step before the launch (the target's hidden reset of step c0)
+  float* rew;                // [E][N] rewards of step c0 (step c0 + i at + i E N)
+  uint8_t* done;             // [E] dones of step c0 (+ i E)
+  int64_t b_off0, b_offn;    // io_b.act_out / qsel_out element offsets: step c0 + 1 (+ i E N); the next chunk's step 0
+  int64_t t_off0;            // io_t.qsel_out (max Q') element offset of step c0 (+ i E N)
+  uint64_t* counter;         // RNG step counter (step c0 + i draws with *counter + i)
+  uint64_t* seq;             // launch sequence number (hand-off flag epoch)
+  int32_t* envpar;           // env state buffer read (0 / 1)
+  uint32_t* ticket;          // blocks finished
+  uint64_t* flags;           // [T][N] behavior hand-off flags: (seq << 16) + step index published
+  uint8_t* hx;               // [T][C][N][256] hand-off actions, one slot per step
+  uint32_t* err;             // sticky error bits: 1 staging row outside the store, 2 hand-off wait expired
+  int c0, n, C, lds_env;
+};
+static_assert(alignof(RollChunk) == 8, "rollout_chunk kernarg layout");
+static constexpr uint64_t kHandoffTimeout = 2000000;   // s_memrealtime ticks (100 MHz): 20 ms
+
+// LDS after the weight image: coordinate features, nibble-row grids, 16-bit position words (prev_r, prev_c, r, c),
+// dones by step parity, the behavior block's outgoing actions
+struct RollChunkLds {
+  int stab, sgrid, spq, ssa, sdone, shx, total;
+};
+__host__ __device__ __forceinline__ RollChunkLds roll_chunk_lds(int R, int C, int N) {
+  auto a16 = [](int x) { return (x + 15) & ~15; };
+  RollChunkLds m;
+  int o = 0;
+  m.stab = o;  o = a16(o + (R + C) * 4);
+  m.sgrid = o; o = a16(o + 256 * roll_gbw(R) * 4);
+  m.spq = o;   o = a16(o + 256 * N * 2);
+  m.ssa = o;   o = a16(o + 2 * 256 * 2);
+  m.sdone = o; o = a16(o + 2 * 256);
+  m.shx = o;   o = a16(o + 256);
+  m.total = o;
+  return m;
+}
+
+// per-launch constants of a chunk-kernel block (computed once, read by the step loop)
+struct ChunkCtx {
+  float* stab;
+  uint32_t* sgrid;
+  uint16_t* spq;      // [256][N] position words prev_r << 12 | prev_c << 8 | r << 4 | c
+  uint16_t* ssa;      // [2][256] steps, apples of the env
+  uint8_t* sdone;     // [2][256] dones by step parity
+  uint8_t* shx;       // [256] the behavior block's outgoing actions
+  uint64_t ctr0, seq;
+  float eps;
+  int tile, agent, e0;
+  bool second, writer;
+};
+
+// The n steps of a chunk-kernel block; EXACT: the range-guarded agent's exact-f32 body (8 waves x 32 envs), else the
+// fp16x3 body (16 waves x 16 envs). One instantiation per body keeps each loop's live registers those of one body.
+template <int F1, int G, int H, int AB>
+__device__ __forceinline__ ChunkCtx chunk_ctx(const QFwdParams* kargs) {
+  const RollChunk& rc = *reinterpret_cast<const RollChunk*>(kargs + 2);
+  const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;   // a tile's 2N blocks: b, b + 8, ... (one XCD)
+  const int N = kargs[0].N;
+  ChunkCtx cx;
+  cx.tile = lb / (2 * N);
+  const int role = lb % (2 * N);
+  cx.second = role >= N;                          // false: target net on s'_t, true: behavior on s_{t+1}
+  cx.agent = cx.second ? role - N : role;
+  cx.writer = !cx.second && cx.agent == 0;
+  cx.e0 = cx.tile * 256;
+  const RollChunkLds lay = roll_chunk_lds(rc.env.R, rc.env.C, N);
+  char* envl = reinterpret_cast<char*>(wsm_ptr()) + rc.lds_env;
+  cx.stab = reinterpret_cast<float*>(envl + lay.stab);
+  cx.sgrid = reinterpret_cast<uint32_t*>(envl + lay.sgrid);
+  cx.spq = reinterpret_cast<uint16_t*>(envl + lay.spq);
+  cx.ssa = reinterpret_cast<uint16_t*>(envl + lay.ssa);
+  cx.sdone = reinterpret_cast<uint8_t*>(envl + lay.sdone);
+  cx.shx = reinterpret_cast<uint8_t*>(envl + lay.shx);
+  // (the last block rewrites these only after every block has finished: constant for the launch)
+  cx.ctr0 = *rc.counter;
+  cx.seq = *rc.seq;
+  cx.eps = cx.second ? *kargs[1].io.eps_ptr : 0.0f;
+  return cx;
+}
+
+template <int F1, int G, int H, int AB, bool EXACT>
+__device__ __forceinline__ void roll_chunk_steps() {
+  const QFwdParams* kargs0 = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nsteps = reinterpret_cast<const RollChunk*>(kargs0 + 2)->n;
+  for (int i = 0; i < nsteps; ++i) {
+  // every per-launch constant is re-derived from the kernarg segment in each step (scalar loads, K$ hits) through
+  // a pointer the compiler cannot prove invariant: nothing uniform stays live across the step's forward body
+  const QFwdParams* kargs = kargs0;
+  asm volatile("" : "+s"(kargs));
+  const ChunkCtx cx = chunk_ctx<F1, G, H, AB>(kargs);
+  const QFwdParams& p = kargs[cx.second ? 1 : 0];
+  const RollChunk& rc = *reinterpret_cast<const RollChunk*>(kargs + 2);
+  const EnvDev& ev = rc.env;
+  const int N = p.N, D = p.D, R = ev.R, C = ev.C, E = p.E;
+  const int64_t EN = (int64_t)E * N, nd = (int64_t)N * D;
+  const mm_qfwd_io& io = p.io;
+  const int tile = cx.tile, agent = cx.agent, e0 = cx.e0;
+  const bool second = cx.second, writer = cx.writer;
+  const int le_d = threadIdx.x, de = e0 + le_d;
+  const bool dvalid = threadIdx.x < 256 && de < E;
+  uint32_t* rows = cx.sgrid + le_d * roll_gbw(R);
+  const int le = wave * 16 + (lane & 15), e = e0 + le;           // fp16x3 body / begin-store lane mapping
+  const int l32 = wave * 32 + (lane & 31), e32 = e0 + l32;       // exact body lane mapping (waves 0-7)
+    const int c = rc.c0 + i;
+    const uint64_t ctr = cx.ctr0 + (uint64_t)i;
+    const int cur = i & 1, prv = cur ^ 1;
+    // (1) the actions of step t (i > 0: published by the tile's N behavior blocks at the end of their step t - 1)
+    uint32_t aq[2] = {0u, 0u};   // 4-bit actions, agent k at bits 4 (k & 7) of aq[k >> 3]
+    if (i > 0) {
+      if (wave == 0 && lane < N) {
+        const uint64_t want = (cx.seq << 16) + (uint64_t)i;
+        uint64_t* f = rc.flags + (int64_t)tile * N + lane;
+        const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - tw > kHandoffTimeout) {
+            atomicOr(rc.err, 2u);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      if (dvalid) {
+        uint8_t* hs = rc.hx + ((int64_t)tile * C + i) * N * 256;
+        uint32_t w[kRollMaxN];
+#pragma unroll
+        for (int k = 0; k < kRollMaxN; ++k)
+          if (k < N)
+            w[k] = __hip_atomic_load(reinterpret_cast<uint32_t*>(hs + k * 256 + (le_d & ~3)), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < kRollMaxN; ++k)
+          if (k < N) aq[k >> 3] |= ((w[k] >> (8 * (le_d & 3))) & 15u) << (4 * (k & 7));
+        // (2) auto-reset of an env that ended at step t - 1 (the initial grid / positions / counters)
+        if (cx.sdone[prv * 256 + le_d]) {
+          const uint4* ig = reinterpret_cast<const uint4*>(ev.init_grid);
+#pragma unroll
+          for (int j = 0; j < kRollMaxR / 2; ++j)
+            if (2 * j < R) {
+              const uint4 g = ig[j];
+              rows[2 * j] = nib_pack4(g.x) | (nib_pack4(g.y) << 16);
+              if (2 * j + 1 < R) rows[2 * j + 1] = nib_pack4(g.z) | (nib_pack4(g.w) << 16);
+            }
+          for (int k = 0; k < N; ++k) cx.spq[le_d * N + k] = (uint16_t)pos16(ev.init_pos[k]);
+          cx.ssa[le_d] = 0;
+          cx.ssa[256 + le_d] = (uint16_t)ev.init_apples;
+        }
+      }
+    } else if (dvalid) {
+      for (int k = 0; k < N; ++k) aq[k >> 3] |= (uint32_t)(rc.act0[(int64_t)de * N + k] & 15) << (4 * (k & 7));
+    }
+    // the store rows of the target's obs stores (re-read per step: not live across the body); out of range -> -1
+    int64_t srow = -1;
+    if (!second) {
+      const int el = EXACT ? e32 : e;
+      if ((EXACT ? (wave < 8) : true) && el < E) {
+        srow = rc.staging[el];
+        if (srow < 0 || srow >= rc.n_rows) srow = -1;   // (flagged once per launch by the prologue)
+      }
+    }
+    // (3) chunk start: slot 0 of the staging rows <- s_t (lane (env, g) writes features 16 q + 4 g .. + 3)
+    if (c == 0) {
+      __syncthreads();
+      if (!second && e < E) {
+        const int64_t srb = rc.staging[e];
+        if (srb >= 0 && srb < rc.n_rows) {
+          const int rcw = cx.spq[le * N + agent] & 0xFF;
+          const uint64_t wd = roll_obs_word(cx.sgrid + le * roll_gbw(R), R, rcw >> 4, rcw & 15);
+          const float cr = cx.stab[rcw >> 4], cc = cx.stab[R + (rcw & 15)];
+          float* d0 = rc.store_obs + srb * rc.row_stride + (int64_t)agent * D;
+          for (int f0 = 4 * (lane >> 4); f0 < D; f0 += 16) {
+            float x[4];
+            roll_feat4(wd, f0, cr, cc, x);
+            roll_store4(d0, f0, D, x);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // (4) the env dynamics of step t (rollout_step_kernel's loop; positions / counters from LDS)
+    if (dvalid) {
+      int64_t myrow = -1;
+      if (writer) {
+        myrow = rc.staging[de];
+        if (myrow < 0 || myrow >= rc.n_rows) myrow = -1;   // never handed on as cur_row
+      }
+      uint32_t pq[kRollMaxN / 2];
+#pragma unroll
+      for (int j = 0; j < kRollMaxN / 2; ++j) pq[j] = 0u;
+#pragma unroll
+      for (int k = 0; k < kRollMaxN; ++k)
+        if (k < N) pq[k >> 1] |= (uint32_t)cx.spq[le_d * N + k] << (16 * (k & 1));
+      const int st = (int)cx.ssa[le_d] + 1;
+      int apples = cx.ssa[256 + le_d];
+      float* rout = rc.rew + (int64_t)i * EN + (int64_t)de * N;
+#pragma unroll 1
+      for (int k = 0; k < N; ++k) {
+        const uint32_t w = pq[0] & 0xFFFFu;
+        const int a = (int)(aq[0] & 15u);
+#pragma unroll
+        for (int j = 0; j < kRollMaxN / 2 - 1; ++j) pq[j] = __builtin_amdgcn_alignbit(pq[j + 1], pq[j], 16);
+        pq[kRollMaxN / 2 - 1] >>= 16;
+        aq[0] = __builtin_amdgcn_alignbit(aq[1], aq[0], 4);
+        aq[1] >>= 4;
+        int r = (w >> 4) & 15, cc = w & 15, pr = (w >> 12) & 15, pc = (w >> 8) & 15;
+        const int nr = r + (a == 0 ? 1 : (a == 2 ? -1 : 0));
+        const int nc = cc + (a == 1 ? -1 : (a == 3 ? 1 : 0));
+        const bool inside = a != 4 && nr >= 0 && nr < R && nc >= 0 && nc < C;
+        const uint32_t w_n = rows[inside ? nr : r], w_r = rows[r], w_p = rows[pr];
+        asm volatile("" ::"v"(w_n), "v"(w_r), "v"(w_p));
+        const bool moved = inside && ((w_n >> (4 * nc)) & 15u) < 3u;
+        if (moved) {
+          pr = r;
+          pc = cc;
+          r = nr;
+          cc = nc;
+        }
+        const bool upd = r != pr || cc != pc;
+        const uint32_t A = moved ? w_n : w_r;
+        const uint32_t B = moved ? w_r : w_p;
+        const uint32_t item = upd ? (A >> (4 * cc)) & 15u : 0u;
+        const bool big = (k & 1) == 0;
+        const float rk = ev.step_cost + (item == 1u ? (big ? -10.0f : -1.0f) : (item == 2u ? (big ? 10.0f : 1.0f) : 0.0f));
+        apples -= item == 2u ? 1 : 0;
+        const uint32_t clr = upd ? ~(15u << (4 * pc)) : ~0u;
+        const uint32_t A1 = pr == r ? (A & clr) : A;
+        rows[pr] = B & clr;
+        rows[r] = upd ? ((A1 & ~(15u << (4 * cc))) | ((uint32_t)(3 + k) << (4 * cc))) : A1;
+        cx.spq[le_d * N + k] = (uint16_t)((pr << 12) | (pc << 8) | (r << 4) | cc);
+        if (writer) rout[k] = rk;
+      }
+      const bool dn = st >= ev.max_steps || apples == 0;
+      cx.ssa[le_d] = (uint16_t)st;
+      cx.ssa[256 + le_d] = (uint16_t)apples;
+      cx.sdone[cur * 256 + le_d] = dn ? 1 : 0;
+      if (writer) {
+        rc.done[(int64_t)i * E + de] = dn ? 1 : 0;
+        rc.cur_row[de] = dn ? -1 : myrow;
+      }
+    }
+    __syncthreads();
+    // (5) the forward: target on s'_t (max Q'_t, s'_t stored into slot c + 1), behavior on s_{t+1} (act / Q(a))
+    const int64_t off = second ? ((c + 1 < C) ? rc.b_off0 + (int64_t)i * EN : rc.b_offn) : rc.t_off0 + (int64_t)i * EN;
+    const int64_t nxt_off = (int64_t)(c + 1) * nd;
+    if constexpr (EXACT) {
+      const int hh = lane >> 5;
+      if (wave < 8) {
+        const bool ok32 = e32 < E;
+        const bool r32 = !second && ok32 && cx.sdone[prv * 256 + l32];
+        const bool bd = second && ok32 && cx.sdone[cur * 256 + l32];
+        float* dst = (!second && srow >= 0) ? rc.store_obs + srow * rc.row_stride + nxt_off + (int64_t)agent * D : nullptr;
+        const int ls = ok32 ? l32 : 0;
+        const int rc32 = cx.spq[ls * N + agent] & 0xFF;
+        const uint64_t wd32 = roll_obs_word(cx.sgrid + ls * roll_gbw(R), R, rc32 >> 4, rc32 & 15);
+        const float cr32 = cx.stab[rc32 >> 4], cc32 = cx.stab[R + (rc32 & 15)];
+        auto ol32 = [&](int kb, float (&x)[16]) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int f0 = kb * 32 + 8 * q + 4 * hh;
+            roll_feat4(wd32, f0, cr32, cc32, x + 4 * q);
+            if (bd || !ok32)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) x[4 * q + j] = (ok32 && f0 + j < D) ? ev.reset_obs[agent * D + f0 + j] : 0.0f;
+            if (dst) roll_store4(dst, f0, D, x + 4 * q);
+          }
+        };
+        float x32[16];
+        ol32(0, x32);
+        const int a = agent_q_fwd_body<F1, G, H, AB>(p, agent, ok32 ? e32 : E, wsm_ptr(), ol32, x32,
+                                                     !ok32 || r32 || bd, true, cx.eps, ctr, off);
+        if (second && hh == 0 && ok32) cx.shx[l32] = (uint8_t)a;
+      }
+    } else {
+      const int ec = min(e, E - 1);
+      const int g = lane >> 4;
+      f32x4 h0[H / 16];
+      {
+        const float* hp = io.h_in + (int64_t)ec * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)(4 * g) * io.hin_sf;
+#pragma unroll
+        for (int t = 0; t < H / 16; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h0[t][r] = hp[(int64_t)(16 * t + r) * io.hin_sf];
+      }
+      const bool rt = !second && e < E && cx.sdone[prv * 256 + le];
+      const bool bd = second && e < E && cx.sdone[cur * 256 + le];
+      if (e >= E || rt || bd) {
+#pragma unroll
+        for (int t = 0; t < H / 16; ++t) h0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      float* dst = (!second && srow >= 0) ? rc.store_obs + srow * rc.row_stride + nxt_off + (int64_t)agent * D : nullptr;
+      const int ls = e < E ? le : 0;
+      const int rcw = cx.spq[ls * N + agent] & 0xFF;
+      const uint64_t wd = roll_obs_word(cx.sgrid + ls * roll_gbw(R), R, rcw >> 4, rcw & 15);
+      const float cr = cx.stab[rcw >> 4], cc = cx.stab[R + (rcw & 15)];
+      auto ol = [&](int kb, float (&x)[8]) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int f0 = kb * 32 + 16 * q + 4 * g;
+          roll_feat4(wd, f0, cr, cc, x + 4 * q);
+          if (bd || e >= E)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[4 * q + j] = (e < E && f0 + j < D) ? ev.reset_obs[agent * D + f0 + j] : 0.0f;
+          if (dst) roll_store4(dst, f0, D, x + 4 * q);
+        }
+      };
+      float xn[8];
+      ol(0, xn);
+      if (wave >= 8)
+        for (int s = 0; s < p.stagger; ++s) __builtin_amdgcn_s_sleep(8);
+      const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr(), ol, xn, h0, cx.eps, ctr, off, 1);
+      if (second && g == 0 && e < E) cx.shx[le] = (uint8_t)a;
+    }
+    // behavior blocks: publish the actions of step t + 1 for the tile (not after the launch's last step)
+    if (second && i + 1 < rc.n) {
+      __syncthreads();
+      if (wave == 0) {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(cx.shx)[lane];   // envs 4 lane .. 4 lane + 3
+        uint32_t* hd = reinterpret_cast<uint32_t*>(rc.hx + (((int64_t)tile * C + i + 1) * N + agent) * 256);
+        __hip_atomic_store(hd + lane, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(rc.flags + (int64_t)tile * N + agent, (cx.seq << 16) + (uint64_t)(i + 1), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// the range-guarded (rare) path as a call: its fp32 body's register allocation stays out of the fp16x3 loop's
+template <int F1, int G, int H, int AB>
+__device__ __attribute__((noinline)) void roll_chunk_steps_exact() {
+  roll_chunk_steps<F1, G, H, AB, true>();
+}
+
+template <int F1, int G, int H, int AB>
+__global__ __launch_bounds__(1024, 1) void rollout_chunk_kernel(QFwdParams p0, QFwdParams p1, RollChunk rc_) {
+  float* wsm = wsm_ptr();
+  const QFwdParams* kargs = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  const RollChunk& rc = *reinterpret_cast<const RollChunk*>(kargs + 2);
+  (void)p0;
+  (void)p1;
+  (void)rc_;
+  const int N = kargs[0].N;
+  const ChunkCtx cx = chunk_ctx<F1, G, H, AB>(kargs);
+  const int nb = (int)gridDim.x;
+  const QFwdParams& p = kargs[cx.second ? 1 : 0];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const EnvDev& ev = rc.env;
+  const int R = ev.R, C = ev.C, RC = R * C, E = p.E;
+  const int agent = cx.agent, e0 = cx.e0;
+  const bool exact = reinterpret_cast<const int*>(p.packed + 2 * p.g.agent_stride * N)[agent] != 0;
+  const int par = *rc.envpar;
+
+  // ---- once per launch: the weight image (the exact-f32 one for a range-guarded agent) into LDS
+  {
+    const float* src = p.packed + (exact ? 0 : (int64_t)N * p.g.agent_stride) + (int64_t)agent * p.g.agent_stride;
+    const int nchunk = (int)(p.g.agent_stride >> 8);
+    for (int c = wave; c < nchunk; c += 16)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 256 + lane * 4),
+                                       (__attribute__((address_space(3))) void*)(wsm + c * 256), 16, 0, 0);
+  }
+  if (threadIdx.x >= 256 && threadIdx.x < 256 + R + C) {
+    const int i = threadIdx.x - 256;
+    cx.stab[i] = i < R ? ev.rtab[i] : ev.ctab[i - R];
+  }
+  // ---- the tile's env state into LDS (one lane per env); staging rows checked once (sticky bit 0)
+  const int le_d = threadIdx.x, de = e0 + le_d;
+  const bool dvalid = threadIdx.x < 256 && de < E;
+  if (dvalid) {
+    const int32_t* pw = (par ? ev.pos_alt : ev.pos) + (int64_t)de * N;
+    const uint4* gin = reinterpret_cast<const uint4*>((par ? ev.grid_alt : ev.grid) + (int64_t)de * RC);
+    uint32_t* rows = cx.sgrid + le_d * roll_gbw(R);
+    cx.ssa[le_d] = (uint16_t)(par ? ev.steps_alt : ev.steps)[de];
+    cx.ssa[256 + le_d] = (uint16_t)(par ? ev.apples_alt : ev.apples)[de];
+    for (int k = 0; k < N; ++k) cx.spq[le_d * N + k] = (uint16_t)pos16(pw[k]);
+#pragma unroll
+    for (int j = 0; j < kRollMaxR / 2; ++j)
+      if (2 * j < R) {
+        const uint4 g = gin[j];
+        rows[2 * j] = nib_pack4(g.x) | (nib_pack4(g.y) << 16);
+        if (2 * j + 1 < R) rows[2 * j + 1] = nib_pack4(g.z) | (nib_pack4(g.w) << 16);
+      }
+    cx.sdone[256 + le_d] = rc.done_prev[de];   // "previous step" slot of step 0 (parity 1)
+    if (cx.writer) roll_row_ok(rc.staging[de], rc.n_rows, rc.err);
+  } else if (threadIdx.x < 256) {
+    cx.sdone[256 + le_d] = 0;
+  }
+  __syncthreads();
+
+  if (exact)
+    roll_chunk_steps_exact<F1, G, H, AB>();
+  else
+    roll_chunk_steps<F1, G, H, AB, false>();
+
+  // ---- the tile's final env state into buffer 1 - par (reset where the last step ended), by the writer block
+  const int lastp = (rc.n - 1) & 1;
+  if (cx.writer && dvalid) {
+    const bool dn = cx.sdone[lastp * 256 + le_d] != 0;
+    int32_t* pout = (par ? ev.pos : ev.pos_alt) + (int64_t)de * N;
+    for (int k = 0; k < N; ++k) {
+      const uint32_t w = cx.spq[le_d * N + k];
+      pout[k] = dn ? ev.init_pos[k]
+                   : (int32_t)((((w >> 12) & 15) << 24) | (((w >> 8) & 15) << 16) | (((w >> 4) & 15) << 8) | (w & 15));
+    }
+    (par ? ev.steps : ev.steps_alt)[de] = dn ? 0 : (int32_t)cx.ssa[le_d];
+    (par ? ev.apples : ev.apples_alt)[de] = dn ? ev.init_apples : (int32_t)cx.ssa[256 + le_d];
+    uint4* gout = reinterpret_cast<uint4*>((par ? ev.grid : ev.grid_alt) + (int64_t)de * RC);
+    const uint4* ig = reinterpret_cast<const uint4*>(ev.init_grid);
+    const uint32_t* rows = cx.sgrid + le_d * roll_gbw(R);
+#pragma unroll
+    for (int j = 0; j < kRollMaxR / 2; ++j)
+      if (2 * j < R) {
+        uint4 v;
+        if (dn) {
+          v = ig[j];
+        } else {
+          const uint32_t a0 = rows[2 * j], a1 = 2 * j + 1 < R ? rows[2 * j + 1] : 0u;
+          v = make_uint4(nib_unpack4(a0 & 0xFFFFu), nib_unpack4(a0 >> 16), nib_unpack4(a1 & 0xFFFFu),
+                         nib_unpack4(a1 >> 16));
+        }
+        gout[j] = v;
+      }
+  }
+  // ---- the last block to finish advances the launch state (every block has read it by then)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (atomicAdd(rc.ticket, 1u) == (uint32_t)nb - 1) {
+      *rc.counter = cx.ctr0 + (uint64_t)rc.n;
+      *rc.envpar = 1 - par;
+      *rc.seq = cx.seq + 1;
+      *rc.ticket = 0u;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- learner PRE on the fp16x3 image
 // The learner's non-recurrent part (layers 1-2 with their training saves, and gi = W_ih x2 + b_ih) of large
 // batches in the fast (cfg5) mode, QLearner(mixer_fp16=True): agent_q_fwd_body_h3's layers 1-2 and its
@@ -2368,6 +2839,13 @@ static int launch_roll(QFwdParams p0, QFwdParams p1, const RollStep& rs, size_t 
   return MM_OK;
 }
 
+template <int F1, int G, int H, int AB>
+static int launch_chunk(QFwdParams p0, QFwdParams p1, const RollChunk& rc, int nb, size_t sm, hipStream_t s) {
+  hipLaunchKernelGGL((rollout_chunk_kernel<F1, G, H, AB>), dim3(nb), dim3(1024), sm, s, p0, p1, rc);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 static int make_params(const mm_qnet_dims* d, const float* packed, const mm_qfwd_io* io, int64_t n_envs,
                        QFwdParams* p) {
   MM_REQUIRE(d && packed && io, "agent_q_fwd: null argument");
@@ -2662,6 +3140,100 @@ int rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, cons
   MM_ROLL(64, 32, 64)
 #undef MM_ROLL
   set_error("rollout_step: unsupported (F1,G,H)");
+  return MM_EINVAL;
+}
+
+// LDS bytes of the chunk-persistent rollout (image + the env state it keeps across steps), or 0 when it does not
+// apply: the fused step's geometry, and a grid of 2 N ceil(E / 256) blocks that fits the device's CUs one block per
+// CU (every block must be co-resident: the hand-off waits need all of a tile's blocks running).
+size_t rollout_chunk_lds(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs) {
+  if (rollout_step_lds(env, d, n_envs) == 0) return 0;
+  const EnvDev& ev = env->d;
+  QnetGeo g;
+  QnetOffsets o;
+  if (qnet_geometry(d, &g, &o)) return 0;
+  const size_t img = ((size_t)g.agent_stride * 4 + 15) & ~size_t(15);
+  const size_t sm = img + (size_t)roll_chunk_lds(ev.R, ev.C, ev.N).total;
+  if (sm > 160 * 1024) return 0;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  const int64_t nb = 2 * (int64_t)ev.N * ((n_envs + 255) / 256);
+  return nb <= cus ? sm : 0;
+}
+
+int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
+                  const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_chunk_io* x,
+                  hipStream_t s) {
+  MM_REQUIRE(env && d && x && io_t && io_b, "rollout_chunk: null argument");
+  const size_t sm = rollout_chunk_lds(env, d, n_envs);
+  MM_REQUIRE(sm > 0, "rollout_chunk: configuration not supported (mm_rollout_chunk_supported)");
+  const EnvDev& ev = env->d;
+  MM_REQUIRE(x->store_obs && x->staging && x->cur_row && x->act0 && x->done_prev && x->rew && x->done && x->counter &&
+                 x->ctl && x->flags && x->handoff, "rollout_chunk: null buffer");
+  MM_REQUIRE(x->chunk_len >= 1 && x->chunk_len <= 4096 && x->c0 >= 0 && x->n_steps >= 1 &&
+                 x->c0 + x->n_steps <= x->chunk_len, "rollout_chunk: steps [c0, c0 + n) must lie in one chunk");
+  MM_REQUIRE(x->n_rows >= 1 && x->n_rows < (1ll << 40), "rollout_chunk: n_rows must be the chunk store's row count");
+  MM_REQUIRE(io_t->mode == MM_Q_MAX && io_b->mode == MM_Q_ACT, "rollout_chunk: target io must be MAX, behavior io ACT");
+  MM_REQUIRE(io_t->h_in && io_b->h_in && io_t->h_in == io_t->h_out && io_b->h_in == io_b->h_out,
+             "rollout_chunk: hidden states required, updated in place");
+  MM_REQUIRE(io_b->eps_ptr && io_b->act_out && io_b->qsel_out && io_t->qsel_out,
+             "rollout_chunk: behavior eps_ptr / act_out / qsel_out and target qsel_out required");
+  MM_REQUIRE(io_b->reset == nullptr && io_t->reset == nullptr, "rollout_chunk: reset flags come from the env (pass NULL)");
+  const int64_t nd = (int64_t)d->n_agents * d->obs_dim;
+  MM_REQUIRE(x->row_stride >= (x->chunk_len + 1) * nd, "rollout_chunk: row stride too small");
+  QFwdParams p0, p1;
+  mm_qfwd_io i0 = *io_t, i1 = *io_b;
+  i0.obs = i1.obs = ev.reset_obs;   // unused (the obs come from the env state); make_params wants a pointer
+  int rc = make_params(d, packed_t, &i0, n_envs, &p0);
+  if (rc) return rc;
+  rc = make_params(d, packed_b, &i1, n_envs, &p1);
+  if (rc) return rc;
+  const int tiles = (int)((n_envs + 255) / 256);
+  p0.nblocks = p1.nblocks = tiles * d->n_agents;
+  RollChunk r;
+  r.env = ev;
+  r.store_obs = x->store_obs;
+  r.row_stride = x->row_stride;
+  r.staging = x->staging;
+  r.cur_row = x->cur_row;
+  r.n_rows = x->n_rows;
+  r.act0 = x->act0;
+  r.done_prev = x->done_prev;
+  r.rew = x->rew;
+  r.done = x->done;
+  r.b_off0 = x->b_off0;
+  r.b_offn = x->b_offn;
+  r.t_off0 = x->t_off0;
+  r.counter = reinterpret_cast<uint64_t*>(x->counter);
+  r.seq = reinterpret_cast<uint64_t*>(x->ctl);
+  r.envpar = reinterpret_cast<int32_t*>(x->ctl + 1);
+  r.ticket = reinterpret_cast<uint32_t*>(x->ctl + 2);
+  r.flags = reinterpret_cast<uint64_t*>(x->flags);
+  r.hx = x->handoff;
+  r.err = reinterpret_cast<uint32_t*>(x->err);
+  r.c0 = x->c0;
+  r.n = x->n_steps;
+  r.C = x->chunk_len;
+  QnetGeo g;
+  QnetOffsets o;
+  qnet_geometry(d, &g, &o);
+  r.lds_env = (int)(((size_t)g.agent_stride * 4 + 15) & ~size_t(15));
+  const int nb = 2 * tiles * d->n_agents;
+  const int AB = (d->n_actions + 31) / 32;
+#define MM_ROLLC(F1_, G_, H_)                                                                       \
+  if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                     \
+    return AB == 1 ? launch_chunk<F1_, G_, H_, 1>(p0, p1, r, nb, sm, s)                             \
+                   : launch_chunk<F1_, G_, H_, 2>(p0, p1, r, nb, sm, s);
+  MM_ROLLC(64, 32, 32)
+  MM_ROLLC(64, 64, 64)
+  MM_ROLLC(128, 32, 32)
+  MM_ROLLC(64, 32, 64)
+#undef MM_ROLLC
+  set_error("rollout_chunk: unsupported (F1,G,H)");
   return MM_EINVAL;
 }
 

@@ -27,6 +27,10 @@ int agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* 
 int agent_q_split2(int phase, const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
                    const float* packed1, const mm_qfwd_io* io1, int64_t e1, hipStream_t s);
 size_t rollout_step_lds(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs);
+size_t rollout_chunk_lds(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs);
+int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
+                  const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_chunk_io* x,
+                  hipStream_t s);
 int rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
                  const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_step_io* x,
                  hipStream_t s);
@@ -76,6 +80,16 @@ int mm_agent_q_fwd2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_i
 
 int mm_rollout_step_supported(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs) {
   return mm::rollout_step_lds(env, d, n_envs) > 0 ? 1 : 0;
+}
+
+int mm_rollout_chunk_supported(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs) {
+  return mm::rollout_chunk_lds(env, d, n_envs) > 0 ? 1 : 0;
+}
+
+int mm_rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
+                     const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_chunk_io* x,
+                     mm_stream_t s) {
+  return mm::rollout_chunk(env, d, packed_t, io_t, packed_b, io_b, n_envs, x, (hipStream_t)s);
 }
 
 int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,

@@ -56,6 +56,58 @@ __global__ __launch_bounds__(256) void td_chunk_kernel(int E, int N, float gamma
   }
 }
 
+// The TD / store of n consecutive steps of a chunk (the chunk-persistent rollout's fold, mm_td_fold_range):
+// thread (slot j, env) computes td_chunk_kernel's per-step value (agent-order sums) and stores the step's act / rew /
+// done; then one thread per env accumulates the chunk priority over the slots in order (the same float additions as
+// n consecutive td_chunk_kernel launches). Block = 64 envs x n slots.
+__global__ __launch_bounds__(1024) void td_fold_range_kernel(int E, int N, float gamma, const float* __restrict__ rew,
+                                                             const uint8_t* __restrict__ done,
+                                                             const float* __restrict__ q_taken,
+                                                             const float* __restrict__ maxq_next,
+                                                             const int32_t* __restrict__ act, int64_t ring_se,
+                                                             int slot0, int n, int C, float* __restrict__ chunk_td,
+                                                             uint8_t* __restrict__ s_act, float* __restrict__ s_rew,
+                                                             uint8_t* __restrict__ s_done,
+                                                             const int64_t* __restrict__ rows, int64_t n_rows,
+                                                             uint32_t* err) {
+  __shared__ float tdv[16][64];
+  const int j = threadIdx.x >> 6, le = threadIdx.x & 63;
+  const int e = blockIdx.x * 64 + le;
+  const bool on = e < E && j < n;
+  if (on) {
+    const int t = slot0 + j;
+    const int64_t o = (int64_t)j * ring_se + (int64_t)e * N;
+    const float* r = rew + o;
+    const float* q = q_taken + o;
+    const float* m = maxq_next + o;
+    const uint8_t d8 = done[(int64_t)j * E + e];
+    float sr = 0.f, sq = 0.f, st = 0.f;   // agent order, like the reference's sum over dim 1
+    for (int k = 0; k < N; ++k) {
+      sr += r[k];
+      sq += q[k];
+      st += m[k];
+    }
+    const float d = d8 ? 1.0f : 0.0f;
+    tdv[j][le] = fabsf(sr + (1.0f - d) * gamma * st - sq);
+    const int64_t row = rows[e];
+    if (row >= 0 && row < n_rows) {
+      for (int k = 0; k < N; ++k) {
+        s_act[(row * C + t) * N + k] = (uint8_t)act[o + k];
+        s_rew[(row * C + t) * N + k] = r[k];
+      }
+      s_done[row * C + t] = d8;
+    } else if (err) {
+      atomicOr(err, 1u);
+    }
+  }
+  __syncthreads();
+  if (j == 0 && e < E) {
+    float ctd = slot0 == 0 ? 0.0f : chunk_td[e];
+    for (int jj = 0; jj < n; ++jj) ctd = (slot0 + jj == 0 ? 0.0f : ctd) + tdv[jj][le];
+    chunk_td[e] = ctd;
+  }
+}
+
 // chunk begin: obs_cur [E][ND] -> store slot 0 of each env's staging row
 __global__ __launch_bounds__(256) void chunk_begin_kernel(int E, int ND, const float* __restrict__ obs_cur,
                                                           float* __restrict__ s_obs, int64_t row_stride,
@@ -201,6 +253,25 @@ int mm_chunk_begin_rows(int64_t n_envs, int32_t nd, float* store_obs, int64_t ro
   const int blocks = (int)std::min<int64_t>((total + threads - 1) / threads, 8192);
   hipLaunchKernelGGL(mm::chunk_begin_rows_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)s, (int)n_envs, nd,
                      store_obs, row_stride, src_rows, src_off, reset_obs, dst_rows);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_td_fold_range(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                     const float* q_taken, const float* max_q_next, const int32_t* act, int64_t ring_se,
+                     int32_t slot0, int32_t n_slots, int32_t chunk_len, float* chunk_td, uint8_t* store_act,
+                     float* store_rew, uint8_t* store_done, const int64_t* rows, int64_t n_rows, int32_t* err,
+                     mm_stream_t s) {
+  MM_REQUIRE(rew && done && q_taken && max_q_next && act && chunk_td && store_act && store_rew && store_done && rows,
+             "td_fold_range: null argument");
+  MM_REQUIRE(n_slots >= 1 && n_slots <= 16 && slot0 >= 0 && slot0 + n_slots <= chunk_len,
+             "td_fold_range: slots [slot0, slot0 + n) must lie in one chunk, n <= 16");
+  MM_REQUIRE(n_agents >= 1 && n_agents <= 256 && ring_se >= n_envs * n_agents, "td_fold_range: bad agents / ring");
+  if (n_envs <= 0) return MM_OK;
+  const int blocks = (int)((n_envs + 63) / 64);
+  hipLaunchKernelGGL(mm::td_fold_range_kernel, dim3(blocks), dim3(64 * n_slots), 0, (hipStream_t)s, (int)n_envs,
+                     n_agents, gamma, rew, done, q_taken, max_q_next, act, ring_se, slot0, n_slots, chunk_len,
+                     chunk_td, store_act, store_rew, store_done, rows, n_rows, reinterpret_cast<uint32_t*>(err));
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

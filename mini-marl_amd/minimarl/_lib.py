@@ -59,6 +59,17 @@ class RollStepIO(ctypes.Structure):
     ]
 
 
+class RollChunkIO(ctypes.Structure):
+    """mm_rollout_chunk_io (include/minimarl.h)"""
+    _fields_ = [
+        ("store_obs", c_vp), ("row_stride", c_i64), ("n_rows", c_i64), ("staging", c_vp), ("cur_row", c_vp),
+        ("c0", c_i32), ("n_steps", c_i32), ("chunk_len", c_i32), ("pad_", c_i32),
+        ("act0", c_vp), ("done_prev", c_vp), ("rew", c_vp), ("done", c_vp),
+        ("b_off0", c_i64), ("b_offn", c_i64), ("t_off0", c_i64),
+        ("counter", c_vp), ("ctl", c_vp), ("flags", c_vp), ("handoff", c_vp), ("err", c_vp),
+    ]
+
+
 class EnvCfg(ctypes.Structure):
     _fields_ = [("n_agents", c_i32), ("max_steps", c_i32), ("full_observable", c_i32), ("cols", c_i32),
                 ("step_cost", c_f32)]
@@ -92,6 +103,11 @@ _SIGS = [
     ("mm_rollout_step_supported", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_i64]),
     ("mm_rollout_step", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_vp,
                                 ctypes.POINTER(QFwdIO), c_i64, ctypes.POINTER(RollStepIO), c_vp]),
+    ("mm_rollout_chunk_supported", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_i64]),
+    ("mm_rollout_chunk", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_vp,
+                                 ctypes.POINTER(QFwdIO), c_i64, ctypes.POINTER(RollChunkIO), c_vp]),
+    ("mm_td_fold_range", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32,
+                                 c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     ("mm_env_grid_shape", c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),
     ("mm_td_chunk_step", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                                  c_vp, c_vp, c_i64, c_vp]),

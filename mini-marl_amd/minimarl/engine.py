@@ -36,7 +36,7 @@ import math
 
 import torch
 
-from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, RollStepIO, check, lib
+from ._lib import MM_Q_ACT, MM_Q_MAX, QFwdIO, RollChunkIO, RollStepIO, check, lib
 from .env import make_env
 from .qnet import AgentQNet, graph_capture, ptr, stream_handle
 from .replay import DevicePER
@@ -58,7 +58,8 @@ class ChunkStore:
 class RolloutEngine:
     def __init__(self, n_envs, n_agents, obs_dim=None, n_actions=5, f1=64, g=32, h=32, chunk=10,
                  capacity=None, gamma=0.99, max_steps=100, step_cost=-0.01, full_observable=False,
-                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", fused=None, device="cuda"):
+                 per_flavor="qmix", per_kwargs=None, seed=0, env="checkers", fused=None, persistent=None,
+                 device="cuda"):
         self.device = torch.device(device)
         self.E, self.N, self.C = int(n_envs), int(n_agents), int(chunk)
         self.gamma = float(gamma)
@@ -79,9 +80,17 @@ class RolloutEngine:
         dev = self.device
         ok = env == "checkers" and lib().mm_rollout_step_supported(self.env.handle(), ctypes.byref(self.behavior.dims),
                                                                     E) != 0
+        okc = env == "checkers" and lib().mm_rollout_chunk_supported(self.env.handle(),
+                                                                      ctypes.byref(self.behavior.dims), E) != 0
         if fused and not ok:
             raise ValueError("RolloutEngine(fused=True): the fused rollout step does not support this configuration")
-        self.fused = ok if fused is None else bool(fused)
+        if persistent and not okc:
+            raise ValueError("RolloutEngine(persistent=True): the chunk-persistent rollout does not support this "
+                             "configuration (or the grid does not fit the device's CUs)")
+        # step modes: "chunk" (chunk-persistent launches, mm_rollout_chunk: the default where it fits), "fused" (one
+        # launch per step, mm_rollout_step; fused=True asks for it explicitly), "two-launch" (fused=False)
+        self.chunked = bool(persistent) if persistent is not None else (okc and fused is None)
+        self.fused = False if self.chunked else (ok if fused is None else bool(fused))
         nb = 3 if self.fused else 2
         if self.fused:
             self.env.state_buffer = lambda: self.t % 2
@@ -118,6 +127,20 @@ class RolloutEngine:
         self.t = 0
         self.seed = int(seed)
         self.chunks_inserted = 0
+        if self.chunked:
+            C, T = self.C, (E + 255) // 256
+            # per-chunk rings: act / Q(a) of step t at [(t // C) % 2][t % C] (written one step ahead, so a chunk's
+            # last step writes the next chunk's position 0 into the other half); max Q', rewards, dones at [t % C]
+            self.act_r = torch.zeros(2 * C, E, N, dtype=torch.int32, device=dev)
+            self.qsel_r = torch.zeros(2 * C, E, N, device=dev)
+            self.maxq_r = torch.zeros(C, E, N, device=dev)
+            self.rew_r = torch.zeros(C, E, N, device=dev)
+            self.done_r = torch.zeros(C, E, dtype=torch.uint8, device=dev)
+            # launch state owned by the chunk kernel: launch sequence, env state buffer, arrival ticket
+            self.ctl = torch.zeros(3, dtype=torch.int64, device=dev)
+            self.hflags = torch.zeros(T * N, dtype=torch.int64, device=dev)
+            self.hx = torch.zeros(T * C * N * 256, dtype=torch.uint8, device=dev)
+            self.env.state_buffer = lambda: int(self.ctl[1].item()) & 1
         self._build_io()
         self.env.reset(self.init_obs)
 
@@ -125,6 +148,9 @@ class RolloutEngine:
         """The per-step device buffers a checkpoint must carry (name -> tensor)."""
         out = {k: getattr(self, k) for k in ("cur_row", "init_obs", "h", "ht", "chunk_td", "eps_dev", "staging")}
         out.update(counter_dev=self.counter_dev)
+        if self.chunked:   # (the launch sequence / hand-off flags are the engine's own, never restored)
+            out.update({k: getattr(self, k) for k in ("act_r", "qsel_r", "maxq_r", "rew_r", "done_r")})
+            return out
         for k in range(2):
             out[f"done_buf{k}"] = self.done_buf[k]
             out[f"maxq_buf{k}"] = self.maxq_buf[k]
@@ -137,12 +163,20 @@ class RolloutEngine:
     @property
     def last_rew(self):
         """rewards [E, N] of the last executed step"""
+        if self.chunked:
+            return self.rew_r[(self.t - 1) % self.C]
         return self.rew_buf[(self.t - 1) % 2] if self.fused else self.rew
 
     @property
     def last_done(self):
         """done flags [E] of the last executed step"""
+        if self.chunked:
+            return self.done_r[(self.t - 1) % self.C]
         return self.done_buf[(self.t - 1) % 2]
+
+    def _act_idx(self, t):
+        """chunk mode: ring index of the actions / Q(a) of step t"""
+        return ((t // self.C) % 2) * self.C + t % self.C
 
     def current_obs(self):
         """s_{t+1} [E,N,D] as the next behavior forward reads it (materialised for tests only)."""
@@ -155,6 +189,8 @@ class RolloutEngine:
     @property
     def act(self):
         """actions [E, N] of the last executed step"""
+        if self.chunked:
+            return self.act_r[self._act_idx(max(self.t - 1, 0))]
         return self.act_buf[(self.t - 1) % len(self.act_buf)] if self.t > 0 else self.act_buf[0]
 
     def _io_behavior(self, k):
@@ -209,6 +245,16 @@ class RolloutEngine:
                     ib.qsel_out = self.qsel_buf[(k3 + 1) % 3].data_ptr()
                     ib.counter_ptr = self.counter_dev.data_ptr() + 8 * k2
                     self.fio_b[(k2, k3)] = ib
+        if self.chunked:
+            # the chunk launch's target (max Q' into the ring) and behavior (act / Q(a) into the rings) io; the
+            # reset flags come from the env inside the kernel
+            self.cio_t = self._io_target(0)
+            self.cio_t.reset = None
+            self.cio_t.qsel_out = self.maxq_r.data_ptr()
+            self.cio_b = self._io_behavior(0)
+            self.cio_b.reset = None
+            self.cio_b.act_out, self.cio_b.qsel_out = self.act_r.data_ptr(), self.qsel_r.data_ptr()
+            self.cio_b.counter_ptr = None
         # the prologue behavior fwd (step 0) uses its own RNG counter so it never repeats step 1's draws
         self.io_b0 = self._io_behavior(0)
         self.io_b0.counter_ptr = None
@@ -240,11 +286,65 @@ class RolloutEngine:
         self._step_launch()
 
     def _prologue(self, s):
+        if self.chunked:   # the first step's actions / Q(a) into their ring position; fresh hiddens
+            ia, EN = self._act_idx(self.t), self.E * self.N
+            self.io_b0.act_out = self.act_r.data_ptr() + 4 * ia * EN
+            self.io_b0.qsel_out = self.qsel_r.data_ptr() + 4 * ia * EN
+            self.io_b0.reset = None
         self.behavior.forward_io(self.E, self.io_b0, s)
         self._primed = True
 
+    def _advance(self, n):
+        """Launch the next n steps: chunk mode as one chunk-persistent launch per chunk span (split at chunk
+        boundaries), the other modes one step at a time."""
+        n = int(n)
+        while n > 0:
+            m = min(n, self.C - self.t % self.C) if self.chunked else 1
+            self._launch_chunk(m) if self.chunked else self._step_launch()
+            n -= m
+
+    def _launch_chunk(self, n):
+        """Steps t .. t + n - 1 (one chunk span) in ONE chunk-persistent launch (mm_rollout_chunk), then their TD /
+        chunk-store fold (mm_td_fold_range) and, at the chunk's end, the PER insert."""
+        s = stream_handle(self.device)
+        L = lib()
+        t, C, E, N = self.t, self.C, self.E, self.N
+        c0, EN = t % C, E * N
+        assert 1 <= n <= C - c0
+        if not self._primed:
+            self._prologue(s)
+        k, ia = (t // C) % 2, self._act_idx(t)
+        x = RollChunkIO()
+        x.store_obs, x.row_stride, x.n_rows = ptr(self.store.obs), self.store.row_stride, self.store.rows
+        x.staging, x.cur_row = ptr(self.staging), ptr(self.cur_row)
+        x.c0, x.n_steps, x.chunk_len = c0, n, C
+        x.act0 = self.act_r.data_ptr() + 4 * ia * EN
+        x.done_prev = self.done_r.data_ptr() + ((c0 - 1) % C) * E
+        x.rew, x.done = self.rew_r.data_ptr() + 4 * c0 * EN, self.done_r.data_ptr() + c0 * E
+        x.b_off0, x.b_offn, x.t_off0 = (k * C + c0 + 1) * EN, (1 - k) * C * EN, c0 * EN
+        x.counter, x.ctl, x.flags, x.handoff, x.err = (ptr(self.counter_dev), ptr(self.ctl), ptr(self.hflags),
+                                                       ptr(self.hx), ptr(self.err))
+        self.behavior.pack(s)
+        self.target.pack(s)
+        check(L.mm_rollout_chunk(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
+                                 ctypes.byref(self.cio_t), ptr(self.behavior.packed), ctypes.byref(self.cio_b), E,
+                                 ctypes.byref(x), s), "rollout_chunk")
+        check(L.mm_td_fold_range(E, N, self.gamma, self.rew_r.data_ptr() + 4 * c0 * EN,
+                                 self.done_r.data_ptr() + c0 * E, self.qsel_r.data_ptr() + 4 * ia * EN,
+                                 self.maxq_r.data_ptr() + 4 * c0 * EN, self.act_r.data_ptr() + 4 * ia * EN, EN, c0, n,
+                                 C, ptr(self.chunk_td), ptr(self.store.act), ptr(self.store.rew),
+                                 ptr(self.store.done), ptr(self.staging), self.store.rows, ptr(self.err), s),
+              "td_fold_range")
+        if c0 + n == C:
+            check(L.mm_per_insert(self.per._h, ptr(self.chunk_td), E, ptr(self.staging), None, s), "per_insert")
+            self.chunks_inserted += E
+        self._td_pending = False
+        self.t += n
+
     def _step_launch(self):
         """Step t: env(t) -> [target fwd(t) + behavior fwd(t+1)] in ONE launch -> TD/store(t)."""
+        if self.chunked:
+            return self._launch_chunk(1)
         if self.fused:
             return self._step_launch_fused()
         s = stream_handle(self.device)
@@ -359,6 +459,8 @@ class RolloutEngine:
     # ------------------------------------------------------------------ HIP graph replay
     def graph_steps(self):
         """Steps after which every parity-indexed buffer is back at its start (the graph cycle)."""
+        if self.chunked:
+            return 2 * self.C
         if self.fused:
             return self.C * 6 // math.gcd(self.C, 6)
         return self.C if self.C % 2 == 0 else 2 * self.C
@@ -375,8 +477,7 @@ class RolloutEngine:
         g = torch.cuda.CUDAGraph()
         t0, ins0, n0 = self.t, self.chunks_inserted, len(self.per)
         with graph_capture(g):
-            for _ in range(self.graph_steps()):
-                self._step_launch()
+            self._advance(self.graph_steps())
         # capture does not execute: rewind the host bookkeeping (PER fill-count mirror too)
         self.t, self.chunks_inserted = t0, ins0
         lib().mm_per_set_size(self.per._h, n0)
@@ -451,7 +552,7 @@ class RolloutEngine:
                 self.per.n_mirror_add(self.E)
                 self._td_pending = False
             else:
-                self._td_pending = True
+                self._td_pending = not self.chunked
             left -= 1
 
     def capture_region(self, n_steps, start=None):
@@ -477,8 +578,7 @@ class RolloutEngine:
         self.t = start
         g = torch.cuda.CUDAGraph()
         with graph_capture(g):
-            for _ in range(int(n_steps)):
-                self._step_launch()
+            self._advance(int(n_steps))
         inserts = self.chunks_inserted - saved[1]
         self.t, self.chunks_inserted, self._td_pending, self._td_flushed = saved
         lib().mm_per_set_size(self.per._h, n0)
@@ -497,7 +597,7 @@ class RolloutEngine:
         self.t += int(n_steps)
         self.chunks_inserted += inserts
         self.per.n_mirror_add(inserts)
-        self._td_pending = self.t % self.C != 0
+        self._td_pending = self.t % self.C != 0 and not self.chunked
 
     _region_graphs = None
 
@@ -532,6 +632,29 @@ class RolloutEngine:
         check(lib().mm_rollout_step(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
                                     ctypes.byref(self.fio_t[k2]), ptr(self.behavior.packed),
                                     ctypes.byref(self.fio_b[(k2, k3)]), self.E, ctypes.byref(x), s), "rollout_step")
+
+    def chunk_only(self, n=None):
+        """The chunk mode's one launch on its own (steps 0 .. n - 1 of a chunk, no TD fold / insert); for timing.
+        Advances the env / hidden state like the real launch (the host step count is left alone)."""
+        n = self.C if n is None else int(n)
+        t0 = self.t
+        self.t = (t0 // (2 * self.C)) * 2 * self.C
+        s = stream_handle(self.device)
+        C, E, N = self.C, self.E, self.N
+        EN = E * N
+        x = RollChunkIO()
+        x.store_obs, x.row_stride, x.n_rows = ptr(self.store.obs), self.store.row_stride, self.store.rows
+        x.staging, x.cur_row = ptr(self.staging), ptr(self.cur_row)
+        x.c0, x.n_steps, x.chunk_len = 0, n, C
+        x.act0, x.done_prev = self.act_r.data_ptr(), self.done_r.data_ptr() + (C - 1) * E
+        x.rew, x.done = self.rew_r.data_ptr(), self.done_r.data_ptr()
+        x.b_off0, x.b_offn, x.t_off0 = EN, C * EN, 0
+        x.counter, x.ctl, x.flags, x.handoff, x.err = (ptr(self.counter_dev), ptr(self.ctl), ptr(self.hflags),
+                                                       ptr(self.hx), ptr(self.err))
+        self.t = t0
+        check(lib().mm_rollout_chunk(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
+                                     ctypes.byref(self.cio_t), ptr(self.behavior.packed), ctypes.byref(self.cio_b), E,
+                                     ctypes.byref(x), s), "rollout_chunk")
 
     def fused_forward(self, k=0):
         """The step's dominant launch on its own (target fwd + behavior fwd); for timing."""

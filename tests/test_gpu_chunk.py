@@ -1,0 +1,165 @@
+"""GPU: the chunk-persistent rollout (mm_rollout_chunk + mm_td_fold_range, RolloutEngine(persistent=True)) against the
+fused one-launch-per-step engine (mm_rollout_step) and the oracle env.
+
+The chunk kernel runs the same restated Checkers dynamics and the same fp16x3 / exact-f32 forward bodies as the fused
+step, with the weight image and the env state kept on chip across the steps of a launch and the tile's actions handed
+between its blocks through HBM flags; so every stored transition, hidden state, chunk priority, PER tree, env state
+and RNG counter must be BIT-identical to the fused engine with the same seed — through chunk starts (slot 0),
+chunk ends (TD fold + PER insert), auto-resets, launches of 1 .. C steps (eager steps, chunk graphs, region graphs
+from several phases) and the range-guarded exact-f32 agent path."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.env import EnvSpec, VecEnvOracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _state(e):
+    torch.cuda.synchronize()
+    st = [e.store.obs, e.store.act, e.store.rew, e.store.done, e.h, e.ht, e.chunk_td, e.cur_row, e.staging,
+          e.per.tree(), e.per.slot_rows(), e.act, e.last_rew, e.last_done, e.counter_dev[e.t % 2 if e.fused else 0]]
+    return [x.detach().clone().cpu() for x in st] + [torch.as_tensor(v) for v in e.env.get_state()]
+
+
+def _pair(E, f1, g, h, seed, guard=False, n=8, cap_mult=4):
+    from minimarl.engine import RolloutEngine
+    kw = dict(f1=f1, g=g, h=h, chunk=10, capacity=cap_mult * E, seed=seed, device=DEV)
+    a = RolloutEngine(E, n, fused=True, **kw)
+    b = RolloutEngine(E, n, persistent=True, **kw)
+    assert a.fused and not a.chunked and b.chunked and not b.fused and b.graph_steps() == 20
+    if guard:   # agent 3 beyond the fp16 range: both engines run it on the exact-f32 image
+        for eng in (a, b):
+            with torch.no_grad():
+                eng.behavior.view("W1")[3, 0, :] = 3.0e3
+            eng.behavior.mark_dirty()
+            eng.sync_target()
+    return a, b
+
+
+def _same(a, b, tag):
+    for i, (x, y) in enumerate(zip(_state(a), _state(b))):
+        assert torch.equal(x, y), (tag, i)
+
+
+@pytest.mark.parametrize("E,f1,g,h,guard,n", [(2048, 64, 64, 64, False, 8), (2200, 64, 32, 32, False, 8),
+                                              (2048, 64, 64, 64, True, 8), (2304, 64, 32, 32, False, 4),
+                                              (2048, 128, 32, 32, False, 8), (2048, 64, 32, 64, False, 8),
+                                              (2100, 64, 64, 64, True, 4)])
+def test_chunk_eager_steps_bit_identical_to_fused(E, f1, g, h, guard, n):
+    """One-step chunk launches (eager step()) vs fused steps, and the env vs the oracle step by step."""
+    a, b = _pair(E, f1, g, h, seed=21, guard=guard, n=n)
+    ora = VecEnvOracle(EnvSpec(n, 100), E)
+    for t in range(34):
+        rows = b.staging.cpu().numpy()
+        a.step(0.3)
+        b.step(0.3)
+        c = t % 10
+        act = b.act.cpu().numpy().astype(np.int64)
+        nxt, rew, done = ora.step(act)
+        np.testing.assert_array_equal(b.store.obs[rows, c + 1].cpu().numpy(), nxt)
+        np.testing.assert_array_equal(b.last_rew.cpu().numpy(), rew)
+        np.testing.assert_array_equal(b.last_done.cpu().numpy().astype(bool), done)
+        ora.reset_envs(done)
+        if c == 9:
+            _same(a, b, t)
+    a.flush_td()
+    _same(a, b, "end")
+    b.check_errors()
+    pos, prev, grid, steps, apples = b.env.get_state()
+    np.testing.assert_array_equal(pos, ora.pos)
+    np.testing.assert_array_equal(prev, ora.prev)
+    np.testing.assert_array_equal(grid, ora.grid)
+    np.testing.assert_array_equal(steps, ora.steps)
+    np.testing.assert_array_equal(apples, ora.apples)
+
+
+@pytest.mark.parametrize("guard", [False, True])
+def test_chunk_launch_spans_and_graphs_bit_identical_to_fused(guard):
+    """Multi-step chunk launches inside graphs — region graphs entered mid-chunk (spans 7 + 10 + 3), whole-cycle
+    chunk graphs (10 + 10), single-step graphs, a region from a chunk boundary (10 + 3) — through PER eviction
+    (2 x E capacity), against eager fused steps."""
+    a, b = _pair(2048, 64, 64, 64, seed=23, guard=guard, cap_mult=2)
+    for _ in range(93):
+        a.step(0.3)
+    a.flush_td()
+    b.run_steps(3, 0.3)                        # single-step graphs (phase 0..2)
+    b.capture_region(20)
+    b.run_steps(20, 0.3)                       # region graph at phase 3: launches of 7, 10, 3 steps
+    b.run_steps(7, 0.3)                        # phase 3 .. 9: single steps
+    b.run_steps(20, 0.3)                       # phase 10 .. : single steps to the cycle start, then ...
+    b.run_graph(0.3)                           # ... t = 50 -> 70: whole-cycle graph (10 + 10)
+    b.capture_region(13)
+    b.run_steps(13, 0.3)                       # phase 10 (a chunk boundary): 10 + 3
+    b.run_steps(10, 0.3)
+    assert a.t == b.t == 93
+    _same(a, b, "end")
+    b.check_errors()
+
+
+def test_chunk_skips_corrupt_staging_row():
+    """Guard rail of the chunk launch (and its TD fold): a staging row outside the chunk store is never written
+    through and sets the sticky error bit 0; every other env matches an uncorrupted twin bit for bit."""
+    from minimarl.engine import RolloutEngine
+    kw = dict(f1=64, g=64, h=64, chunk=10, capacity=2 * 2048, seed=31, persistent=True, device=DEV)
+    a = RolloutEngine(2048, 8, **kw)
+    b = RolloutEngine(2048, 8, **kw)
+    for _ in range(3):
+        a.step(0.3)
+        b.step(0.3)
+    bad = [5, 700, 2047]
+    good_rows = b.staging.clone()
+    with torch.no_grad():
+        b.staging[5] = b.store.rows + 100
+        b.staging[700] = -3
+        b.staging[2047] = b.store.rows
+    a.run_steps(4, 0.3)
+    b.run_steps(4, 0.3)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="corrupt staging row"):
+        b.check_errors()
+    b.check_errors()
+    keep = torch.ones(2048, dtype=torch.bool)
+    keep[bad] = False
+    rows = good_rows.cpu()[keep]
+    for x, y in ((a.store.obs, b.store.obs), (a.store.act, b.store.act), (a.store.rew, b.store.rew),
+                 (a.store.done, b.store.done)):
+        assert torch.equal(x.cpu()[rows], y.cpu()[rows])
+    assert torch.equal(a.chunk_td.cpu()[keep], b.chunk_td.cpu()[keep])
+    assert not (b.cur_row.cpu()[bad] >= b.store.rows).any() and not (b.cur_row.cpu()[bad] < -1).any()
+
+
+def test_chunk_trainer_resume_bit_identical(tmp_path):
+    """QTrainer in chunk mode checkpointed mid-chunk at an odd step: the env state buffer is device-side (flipped
+    per launch), the rings and the RNG counter are in the checkpoint; the resumed trainer is bit-identical."""
+    from minimarl.checkpoint import load_checkpoint, save_checkpoint
+    from minimarl.config import QTrainConfig
+    from minimarl.train import QTrainer
+    cfg = QTrainConfig(algo="qmix", n_envs=2048, n_agents=4, full_observable=False, buffer_limit=4096, max_step=13,
+                       update_iter=2, update_target_interval=2, test_interval=0, test_envs=0,
+                       epsilon_anneal_episode=10, seed=11)
+    a = QTrainer(cfg, device=DEV)
+    assert a.eng.chunked
+    a.train_episode()
+    assert a.eng.t % 2 == 1 and a.eng.t % 10 != 0
+    path = str(tmp_path / "trainer_chunk.safetensors")
+    save_checkpoint(path, trainer=a)
+    for _ in range(2):
+        a.train_episode()
+    b = QTrainer(cfg, device=DEV)
+    b.train_episode()   # a different history (launch count / env buffer parity) before the restore
+    b.train_episode()
+    load_checkpoint(path, trainer=b)
+    assert b.eng.t == a.eng.t - 26
+    for _ in range(2):
+        b.train_episode()
+    torch.cuda.synchronize()
+    for x, y in [(a.learner.P, b.learner.P), (a.eng.per.tree(), b.eng.per.tree()),
+                 (a.eng.per.slot_rows(), b.eng.per.slot_rows()), (a.eng.store.obs, b.eng.store.obs),
+                 (a.eng.store.act, b.eng.store.act), (a.eng.h, b.eng.h), (a.eng.ht, b.eng.ht),
+                 (a.score_acc, b.score_acc)]:
+        assert torch.equal(x, y)
+    for x, y in zip(a.eng.env.get_state(), b.eng.env.get_state()):
+        assert np.array_equal(x, y)

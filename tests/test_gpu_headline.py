@@ -53,14 +53,21 @@ def _check_actions_rng(act, t, seed, eps, N):
     return expl
 
 
-def test_headline_engine_vs_oracle_through_eviction():
+@pytest.mark.parametrize("mode", ["chunk", "fused"])
+def test_headline_engine_vs_oracle_through_eviction(mode):
+    """mode "chunk": the benched chunk-persistent launches (graph cycle 2C); "fused": one launch per step (lcm(C, 6))."""
     from minimarl.engine import RolloutEngine
     E, N, H, C = 4096, 8, 64, 10
     cap = 16 * E
     eps = 0.1
     seed = 1234
-    eng = RolloutEngine(E, N, f1=64, g=H, h=H, chunk=C, capacity=cap, seed=seed, device=DEV)
-    assert eng.fused and eng.graph_steps() == 3 * C   # the benched one-launch step (graph cycle lcm(C, 6))
+    kw = dict(persistent=True) if mode == "chunk" else dict(fused=True)
+    eng = RolloutEngine(E, N, f1=64, g=H, h=H, chunk=C, capacity=cap, seed=seed, device=DEV, **kw)
+    if mode == "chunk":
+        assert eng.chunked and eng.graph_steps() == 2 * C
+        assert RolloutEngine(E, N, f1=64, g=H, h=H, chunk=C, capacity=E, device=DEV).chunked   # the default mode
+    else:
+        assert eng.fused and eng.graph_steps() == 3 * C
     P = {k: v.detach().cpu().clone() for k, v in eng.behavior.params().items()}
     Pt = {k: v.detach().cpu().clone() for k, v in eng.target.params().items()}
     spec = EnvSpec(N, 100)
