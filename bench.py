@@ -289,7 +289,9 @@ def main():
     E, N, Hh = args.envs, args.agents, args.hidden
     F1, G = 64, Hh
     cap = 16 * E
-    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=cap, seed=1234 + rank, device=dev)
+    # (ranks sharing one GPU: one launch per step, the chunk-persistent kernel needs every CU for its own blocks)
+    eng = RolloutEngine(E, N, f1=F1, g=G, h=Hh, chunk=10, capacity=cap, seed=1234 + rank, device=dev,
+                        persistent=False if shared else None)
     D = eng.D
     from minimarl.learner import Mixer, QLearner
     mix = Mixer(N, N * D, 64, 32, dev, seed=7)
@@ -402,6 +404,7 @@ def main():
         from minimarl.train import QTrainer
         tcfg = presets()["cfg2"].q
         tcfg.n_envs, tcfg.n_agents, tcfg.buffer_limit, tcfg.test_interval = E, N, cap, 0
+        tcfg.persistent = False if shared else None
         tcfg.seed = 17
         tr = QTrainer(tcfg, device=dev, rank=rank, grad_allreduce=allreduce, world=world, track_score=True)
         if dist:
@@ -700,9 +703,26 @@ def main():
     # step. At E >= 2048 the network runs as fp16x3-split MFMAs (every fp32 product as 3 f16 MFMAs), so the
     # MFMA ceiling for the network's fp32 FLOPs is the dense f16 peak / 3; the native f32-MFMA peak beside it.
     flops = 2 * qnet_flops_per_agent_step(D, F1, G, Hh, 5) * E * N
-    h3 = E >= 2048 and not os.environ.get("MM_FWD_F32")
+    h3 = E >= 2048
     peak = PEAK_F16_TFLOPS / 3 if h3 else PEAK_FP32_TFLOPS
-    if eng.fused:
+    per_launch_steps = 1
+    if eng.chunked:
+        # chunk mode (the default at the headline shape): ONE launch runs the C steps of a chunk, mm_rollout_chunk =
+        # per step the env step + target net on s'_t + behavior net on s_{t+1}; its FLOPs per launch = C steps' worth
+        per_launch_steps = eng.C
+        t_fwd = t_iso = time_kernel(lambda: eng.chunk_only(eng.C))
+        flops *= eng.C
+        kname = "rollout_chunk_kernel"
+        RC = eng.env.rows * eng.env.cols
+        # algorithmic HBM bytes per launch: per step and agent-step the stored s'_t 4D, hidden in / out of both
+        # nets 16H, behavior act / Q(a) out 8, max Q' out 4, reward out 4; per step and env done 1 + cur_row 8;
+        # per launch and agent-step the first actions in 4 and the position word in / out 8; per launch and env
+        # the grid in / out 2RC, step / apple counters in / out 16, store row in 8 (the weight images, LDS-resident
+        # for the launch, and the tile-local action hand-off, <= 2N bytes per agent-step, are not counted)
+        alg_bytes = eng.C * (E * N * (4 * D + 16 * Hh + 16) + E * 9) + E * N * 12 + E * (2 * RC + 24)
+        kdesc = (f"{kname}<64,64,64,1> (C = {eng.C} rollout steps per launch: env step + dual forward, "
+                 "chunk-persistent)")
+    elif eng.fused:
         t_fwd = t_iso = time_kernel(eng.fused_step_only)
         kname = "rollout_step_kernel"
         RC = eng.env.rows * eng.env.cols
@@ -723,8 +743,8 @@ def main():
         kdesc = f"{kname}<64,64,64,1> (dual: target+behavior)"
     achieved = flops / t_fwd / 1e12
     traffic = None
-    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_rollout_step.json" if eng.fused
-                                         else "r*_pmc_agent_fwd.json")))
+    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_rollout_chunk.json" if eng.chunked else
+                                         "r*_pmc_rollout_step.json" if eng.fused else "r*_pmc_agent_fwd.json")))
     if prof and E == 4096 and N == 8 and Hh == 64:
         pm = json.load(open(prof[-1]))
         if pm.get("kernel", "").startswith(kname):
@@ -734,6 +754,8 @@ def main():
                 "traffic_source": os.path.basename(prof[-1]) if traffic else None,
                 "kernel": kdesc,
                 "kernel_us": round(t_fwd * 1e6, 2), "kernel_us_isolated": round(t_iso * 1e6, 2),
+                "rollout_steps_per_launch": per_launch_steps,
+                "kernel_us_per_step": round(t_fwd * 1e6 / per_launch_steps, 2),
                 "arith": "fp32 network FLOPs as fp16x3-split MFMA (v_mfma_f32_16x16x32_f16 x3, fp32 accumulate)"
                          if h3 else "exact f32 MFMA (v_mfma_f32_32x32x2_f32)",
                 "fp32_native_peak": PEAK_FP32_TFLOPS, "frac_of_fp32_native_peak": round(achieved / PEAK_FP32_TFLOPS, 4),
@@ -758,7 +780,9 @@ def main():
             "config": {"workload": "QMIX 8-agent gridworld rollout, 4096 envs/GPU, GRU-64 agents, chunk 10, PER",
                        "envs_per_gpu": E, "agents": N, "obs_dim": D, "f1": F1, "gru": Hh, "chunk": 10,
                        "per_capacity_chunks": cap, "per_prefilled_chunks": fill_chunks * E,
-                       "step_launches": ("ONE fused launch (env step + dual forward) per step" if eng.fused else
+                       "step_launches": ("ONE chunk-persistent launch per chunk span (env step + dual forward of "
+                                         "each step) + the TD fold" if eng.chunked else
+                                         "ONE fused launch (env step + dual forward) per step" if eng.fused else
                                          "env + dual forward per step") + " + PER insert every chunk; one captured "
                                                                             "graph per timed region",
                        "parallelism": f"env-shard x{world}"},

@@ -1708,7 +1708,7 @@ __global__ __launch_bounds__(1024, 1) void rollout_step_kernel(QFwdParams p0, QF
       }
       const uint8_t dd = tdone[i];
       const float dn = dd ? 1.0f : 0.0f;
-      const float v = fabsf(sr + (1.0f - dn) * td.gamma * st - sq);
+      const float v = rollout_td(sr, sq, st, dn, td.gamma);
       td.chunk_td[e0 + i] = (td.slot == 0 ? 0.0f : ctd[i]) + v;
       if (roll_row_ok(trow[i], rs.n_rows, rs.err)) td.s_done[trow[i] * td.C + td.slot] = dd;
     }
@@ -2011,7 +2011,7 @@ struct RollChunk {   // kernarg right after the two QFwdParams
   uint64_t* flags;           // [T][N] behavior hand-off flags: (seq << 16) + step index published
   uint8_t* hx;               // [T][C][N][256] hand-off actions, one slot per step
   uint32_t* err;             // sticky error bits: 1 staging row outside the store, 2 hand-off wait expired
-  int c0, n, C, lds_env;
+  int c0, n, CL, lds_env;   // first step's chunk position, steps, chunk length, LDS offset of the env state
 };
 static_assert(alignof(RollChunk) == 8, "rollout_chunk kernarg layout");
 static constexpr uint64_t kHandoffTimeout = 2000000;   // s_memrealtime ticks (100 MHz): 20 ms
@@ -2082,24 +2082,29 @@ __device__ __forceinline__ ChunkCtx chunk_ctx(const QFwdParams* kargs) {
 template <int F1, int G, int H, int AB, bool EXACT>
 __device__ __forceinline__ void roll_chunk_steps() {
   const QFwdParams* kargs0 = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nsteps = reinterpret_cast<const RollChunk*>(kargs0 + 2)->n;
   for (int i = 0; i < nsteps; ++i) {
   // every per-launch constant is re-derived from the kernarg segment in each step (scalar loads, K$ hits) through
-  // a pointer the compiler cannot prove invariant: nothing uniform stays live across the step's forward body
+  // a pointer the compiler cannot prove invariant, and every lane index from a thread id it cannot hoist: nothing
+  // stays live across the step's forward body (the body's registers are those of rollout_step_kernel's)
   const QFwdParams* kargs = kargs0;
   asm volatile("" : "+s"(kargs));
+  int tz = 0;
+  asm volatile("" : "+s"(tz));
+  const int tx = (int)threadIdx.x + tz;
+  const int wave = tx >> 6, lane = tx & 63;
   const ChunkCtx cx = chunk_ctx<F1, G, H, AB>(kargs);
   const QFwdParams& p = kargs[cx.second ? 1 : 0];
   const RollChunk& rc = *reinterpret_cast<const RollChunk*>(kargs + 2);
+  const int CL = rc.CL;   // chunk length (C below is the env grid's column count)
   const EnvDev& ev = rc.env;
   const int N = p.N, D = p.D, R = ev.R, C = ev.C, E = p.E;
   const int64_t EN = (int64_t)E * N, nd = (int64_t)N * D;
   const mm_qfwd_io& io = p.io;
   const int tile = cx.tile, agent = cx.agent, e0 = cx.e0;
   const bool second = cx.second, writer = cx.writer;
-  const int le_d = threadIdx.x, de = e0 + le_d;
-  const bool dvalid = threadIdx.x < 256 && de < E;
+  const int le_d = tx, de = e0 + le_d;
+  const bool dvalid = tx < 256 && de < E;
   uint32_t* rows = cx.sgrid + le_d * roll_gbw(R);
   const int le = wave * 16 + (lane & 15), e = e0 + le;           // fp16x3 body / begin-store lane mapping
   const int l32 = wave * 32 + (lane & 31), e32 = e0 + l32;       // exact body lane mapping (waves 0-7)
@@ -2123,7 +2128,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       }
       __syncthreads();
       if (dvalid) {
-        uint8_t* hs = rc.hx + ((int64_t)tile * C + i) * N * 256;
+        uint8_t* hs = rc.hx + ((int64_t)tile * CL + i) * N * 256;
         uint32_t w[kRollMaxN];
 #pragma unroll
         for (int k = 0; k < kRollMaxN; ++k)
@@ -2242,7 +2247,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
     }
     __syncthreads();
     // (5) the forward: target on s'_t (max Q'_t, s'_t stored into slot c + 1), behavior on s_{t+1} (act / Q(a))
-    const int64_t off = second ? ((c + 1 < C) ? rc.b_off0 + (int64_t)i * EN : rc.b_offn) : rc.t_off0 + (int64_t)i * EN;
+    const int64_t off = second ? ((c + 1 < CL) ? rc.b_off0 + (int64_t)i * EN : rc.b_offn) : rc.t_off0 + (int64_t)i * EN;
     const int64_t nxt_off = (int64_t)(c + 1) * nd;
     if constexpr (EXACT) {
       const int hh = lane >> 5;
@@ -2268,7 +2273,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
         };
         float x32[16];
         ol32(0, x32);
-        const int a = agent_q_fwd_body<F1, G, H, AB>(p, agent, ok32 ? e32 : E, wsm_ptr(), ol32, x32,
+        const int a = agent_q_fwd_body<F1, G, H, AB>(p, agent, ok32 ? e32 : E, wsm_ptr() + tz, ol32, x32,
                                                      !ok32 || r32 || bd, true, cx.eps, ctr, off);
         if (second && hh == 0 && ok32) cx.shx[l32] = (uint8_t)a;
       }
@@ -2309,7 +2314,9 @@ __device__ __forceinline__ void roll_chunk_steps() {
       ol(0, xn);
       if (wave >= 8)
         for (int s = 0; s < p.stagger; ++s) __builtin_amdgcn_s_sleep(8);
-      const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr(), ol, xn, h0, cx.eps, ctr, off, 1);
+      // (the image base offset by the per-step opaque zero: the fragment addresses are formed inside the step,
+      // not hoisted out of the loop into registers that then spill)
+      const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr() + tz, ol, xn, h0, cx.eps, ctr, off, 1);
       if (second && g == 0 && e < E) cx.shx[le] = (uint8_t)a;
     }
     // behavior blocks: publish the actions of step t + 1 for the tile (not after the launch's last step)
@@ -2317,7 +2324,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       __syncthreads();
       if (wave == 0) {
         const uint32_t w = reinterpret_cast<const uint32_t*>(cx.shx)[lane];   // envs 4 lane .. 4 lane + 3
-        uint32_t* hd = reinterpret_cast<uint32_t*>(rc.hx + (((int64_t)tile * C + i + 1) * N + agent) * 256);
+        uint32_t* hd = reinterpret_cast<uint32_t*>(rc.hx + (((int64_t)tile * CL + i + 1) * N + agent) * 256);
         __hip_atomic_store(hd + lane, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
@@ -2326,12 +2333,6 @@ __device__ __forceinline__ void roll_chunk_steps() {
       }
     }
   }
-}
-
-// the range-guarded (rare) path as a call: its fp32 body's register allocation stays out of the fp16x3 loop's
-template <int F1, int G, int H, int AB>
-__device__ __attribute__((noinline)) void roll_chunk_steps_exact() {
-  roll_chunk_steps<F1, G, H, AB, true>();
 }
 
 template <int F1, int G, int H, int AB>
@@ -2389,8 +2390,10 @@ __global__ __launch_bounds__(1024, 1) void rollout_chunk_kernel(QFwdParams p0, Q
   }
   __syncthreads();
 
+  // (two loops, one per body: the exact-f32 loop's spills stay in that rare path — the fp16x3 loop's spill code is
+  // the same as with no exact path at all, checked in the ISA)
   if (exact)
-    roll_chunk_steps_exact<F1, G, H, AB>();
+    roll_chunk_steps<F1, G, H, AB, true>();
   else
     roll_chunk_steps<F1, G, H, AB, false>();
 
@@ -3217,7 +3220,7 @@ int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, con
   r.err = reinterpret_cast<uint32_t*>(x->err);
   r.c0 = x->c0;
   r.n = x->n_steps;
-  r.C = x->chunk_len;
+  r.CL = x->chunk_len;
   QnetGeo g;
   QnetOffsets o;
   qnet_geometry(d, &g, &o);

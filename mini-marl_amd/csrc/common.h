@@ -48,6 +48,13 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 __device__ __forceinline__ uint64_t rng_draw(uint64_t seed, uint64_t counter, uint64_t a, uint64_t b) {
   return mix64(seed ^ mix64(counter * 0xD1B54A32D192ED03ull ^ mix64(a * 0x8CB92BA72F3D8DD7ull + b)));
 }
+// the rollout priority term |sum_i r_i + (1 - d) gamma sum_i max Q'_i - sum_i Q_i(a_i)| (cal_td_error,
+// vdn/_utils.py:44-52) with ONE fixed rounding sequence (no FMA contraction): every kernel that folds a rollout TD
+// (two-launch, fused, chunk-persistent, PER insert) produces the same bits
+__device__ __forceinline__ float rollout_td(float sr, float sq, float st, float d, float gamma) {
+  const float boot = __fmul_rn(__fmul_rn(1.0f - d, gamma), st);
+  return fabsf(__fsub_rn(__fadd_rn(sr, boot), sq));
+}
 __device__ __forceinline__ float rng_uniform(uint64_t r) { return (float)(r >> 40) * (1.0f / 16777216.0f); }
 
 // Debug timing traces: a static device buffer of 4096 u64 slots, allocated when the named

@@ -204,7 +204,7 @@ __global__ __launch_bounds__(TB) void env_step_wave_kernel(EnvDev d, const int32
       st += std3[2 * EPW * N + lane * N + j];
     }
     const float dn = tdone ? 1.0f : 0.0f;
-    const float td = fabsf(sr + (1.0f - dn) * tdf.gamma * st - sq);
+    const float td = rollout_td(sr, sq, st, dn, tdf.gamma);
     tdf.chunk_td[e] = (tdf.slot == 0 ? 0.0f : tdf.chunk_td[e]) + td;
     const int64_t row = tdf.rows[e];
     tdf.s_done[row * tdf.C + tdf.slot] = tdone;

@@ -638,11 +638,17 @@ __global__ __launch_bounds__(256) void mappo_insert_kernel(const uint8_t* __rest
 }
 
 // ------------------------------------------------------------------ host dispatch
+int mappo_roll_fwd(const mm_mappo_dims* d, const mm_mappo_fwd_args* a, hipStream_t s);   // mappo_grad.hip
+
 template <int D, int H, int A>
 struct MappoShape {
   using GA = MGeo<D, H, A>;
   using GC = MGeo<D, H, 1>;
   static int fwd(const mm_mappo_fwd_args* a, hipStream_t s) {
+    if (a->mode != MM_MAPPO_TRAIN && H == 32) {   // rollout / get_values: the MFMA forward (mappo_grad.hip)
+      const mm_mappo_dims d{D, H, A};
+      return mappo_roll_fwd(&d, a, s);
+    }
     const int64_t n = a->mode == MM_MAPPO_TRAIN ? (int64_t)(a->T / a->L) * a->en : a->rows;
     if (n <= 0) return MM_OK;
     const int nets = a->mode == MM_MAPPO_VALUES ? 1 : 2;

@@ -29,6 +29,8 @@
 // dW1, b1, b2 and the three LayerNorms' parameters. Splitting the MLP backward out of the recurrent pass
 // keeps pass G's registers to its 7 accumulator tiles + the step's GRU state (no spills, 2 waves per SIMD)
 // and drops the parking of the MLP activations the single-pass kernel needed.
+#include <algorithm>
+
 #include "common.h"
 #include "minimarl.h"
 #include "trunk.h"
@@ -926,6 +928,141 @@ __device__ void mlp_body(const GradArgs& k, int net, float* sm) {
   for (int e = threadIdx.x; e < F::total; e += blockDim.x) outp[e] = red[e];
 }
 
+// ---------------------------------------------------------------- rollout forward on MFMA
+// get_actions / get_values (rmappo_policy.py:57-99; r_actor_critic.py:60-93, 189-208) for one step of every row: the
+// actor and critic trunks (LN0 -> L1 -> LN1 -> L2 -> LN2 -> GRU on h * mask -> LN_r -> head) with the same act-frag
+// MFMA building blocks as the training passes (Mlp / Gru above: one wave = 32 rows, features on M, rows on N,
+// v_mfma_f32_32x32x2_f32 exact-f32 products), then per row (lane half h = 0) the Categorical sample / log-prob
+// (inverse CDF of the softmax with the injected or counter-RNG uniform, mappo.hip fwd_body's arithmetic) or the
+// value, and the new hidden state as 16-byte stores. Block = 4 waves, 2 blocks per CU (the forward part of the
+// LDS image only); blockIdx.y = net (0 actor, 1 critic; VALUES mode: critic only).
+template <int D, int O>
+__device__ void stage_fwd(float* sm, const float* __restrict__ P) {
+  using G = Geo<D, O>;
+  constexpr int gap = G::ln0w - G::WihT;   // the transposed W_ih / W_hh of the backward: not staged
+  for (int e = threadIdx.x; e < G::scr - gap; e += blockDim.x) {
+    const int src = e < G::WihT ? e : e + gap;
+    sm[src] = stage_value<D, O>(P, src);
+  }
+  __syncthreads();
+}
+
+template <int D, int A, int O>
+__device__ void roll_body(const mm_mappo_fwd_args& a, int net, float* sm) {
+  using G = Geo<D, O>;
+  stage_fwd<D, O>(sm, a.net[net].P);
+  const mm_mappo_net_io& io = a.net[net];
+  const int lane = (int)(threadIdx.x & 63), ci = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t R = a.rows, ntile = (R + 31) / 32;
+  const uint64_t ctr = a.counter_ptr ? *a.counter_ptr : a.counter;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + w; tile < ntile; tile += (int64_t)gridDim.x * 4) {
+    const int64_t r0 = tile * 32 + ci;
+    const bool valid = r0 < R;
+    const int64_t row = valid ? r0 : R - 1;
+    const float* smo = sm + opaque0();
+    float x2[16], hc[16];
+    {
+      Mlp<D, O> mp;
+      mp.run(smo + G::W1, smo + G::W2, smo + G::ln0w, a.obs + row * D);
+      mp.x2(smo + G::ln0w, x2);
+    }
+    ld_row32(io.h_in, row, hc);
+    const float m = a.mask ? a.mask[row] : 1.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) hc[q] *= m;
+    Gru<D, O> gr;
+    gr.run(smo, x2, hc);
+    if (valid && io.h_out) st_row32(io.h_out, row, gr.h2);
+    // head: LN_r(h2) -> Wo y + bo
+    float mur, rsr, y[16];
+    ln32(gr.h2, mur, rsr);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) y[q] = (gr.h2[q] - mur) * rsr * smo[G::lnrw + kperm(q, h)] + smo[G::lnrb + kperm(q, h)];
+    float l[O];
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sacc = fmaf(smo[G::Wo + o * 32 + kperm(q, h)], y[q], sacc);
+      l[o] = smo[G::bo + o] + xsum(sacc);
+    }
+    if (!valid || h != 0) continue;
+    if constexpr (O == 1) {
+      if (io.out) io.out[row] = l[0];
+    } else {
+      // log-softmax (mappo.hip log_softmax)
+      float mx = l[0];
+#pragma unroll
+      for (int q = 1; q < O; ++q) mx = fmaxf(mx, l[q]);
+      float se = 0.0f;
+#pragma unroll
+      for (int q = 0; q < O; ++q) se += expf(l[q] - mx);
+      const float lse = mx + logf(se);
+#pragma unroll
+      for (int q = 0; q < O; ++q) l[q] -= lse;
+      int act;
+      if (a.act_in) {
+        act = a.act_in[row];
+      } else if (a.deterministic) {
+        act = 0;   // Categorical.mode() = first argmax (distributions.py:61-62)
+#pragma unroll
+        for (int q = 1; q < O; ++q)
+          if (l[q] > l[act]) act = q;
+        if (a.act_out) a.act_out[row] = act;
+      } else {
+        const float u = a.u ? a.u[row] : rng_uniform(rng_draw(a.seed, ctr, (uint64_t)row, 0x9E37ull));
+        act = O - 1;   // inverse CDF: first k with u < cumsum(p)[k], the last action if rounding leaves none
+        bool found = false;
+        float cs = 0.0f;
+#pragma unroll
+        for (int q = 0; q < O; ++q) {
+          cs += expf(l[q]);
+          if (!found && u < cs) {
+            act = q;
+            found = true;
+          }
+        }
+        if (a.act_out) a.act_out[row] = act;
+      }
+      float lp = l[0];
+#pragma unroll
+      for (int q = 1; q < O; ++q)
+        if (q == act) lp = l[q];
+      if (io.out) io.out[row] = lp;
+    }
+  }
+}
+
+template <int D, int A>
+__global__ __launch_bounds__(256, 2) void mappo_roll_kernel(mm_mappo_fwd_args a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int net = (int)blockIdx.y + (a.mode == MM_MAPPO_VALUES ? 1 : 0);
+  if (net == 0)
+    roll_body<D, A, A>(a, 0, sm);
+  else
+    roll_body<D, A, 1>(a, 1, sm);
+}
+
+template <int D, int A>
+static int roll_fwd(const mm_mappo_fwd_args* a, hipStream_t s) {
+  constexpr size_t lds = (size_t)Geo<D, A>::scr * 4;
+  static_assert(Geo<D, A>::scr == Geo<D, 1>::scr, "actor / critic LDS images differ");
+  static const int attr_rc = [&]() -> int {
+    MM_HIP_CHECK(hipFuncSetAttribute((const void*)mappo_roll_kernel<D, A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+    return MM_OK;
+  }();
+  if (attr_rc != MM_OK) return attr_rc;
+  if (a->rows <= 0) return MM_OK;
+  const int64_t ntile = (a->rows + 31) / 32;
+  const int nets = a->mode == MM_MAPPO_VALUES ? 1 : 2;
+  const unsigned nb = (unsigned)std::min<int64_t>((ntile + 3) / 4, 1024);
+  hipLaunchKernelGGL((mappo_roll_kernel<D, A>), dim3(nb, nets), dim3(256), lds, s, *a);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
 template <int D, int A>
 __global__ __launch_bounds__(64 * GW, 1) void mappo_grad_gru_kernel(GradArgs k) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -1000,6 +1137,12 @@ struct GradShape {
 };
 
 }  // namespace mgr
+
+// the rollout / get_values forward on MFMA (mappo.hip routes MM_MAPPO_ROLLOUT / VALUES here for H 32, D 47 | 94, A 5)
+int mappo_roll_fwd(const mm_mappo_dims* d, const mm_mappo_fwd_args* a, hipStream_t s) {
+  if (d->obs_dim == 47) return mgr::roll_fwd<47, 5>(a, s);
+  return mgr::roll_fwd<94, 5>(a, s);
+}
 }  // namespace mm
 
 extern "C" {

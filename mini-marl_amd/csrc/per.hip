@@ -819,7 +819,7 @@ __device__ void mb_td_fold(TdFuse t, int64_t E, int N, float (*sh)[MB_T]) {
         sm += sh[2][threadIdx.x + j];
       }
       const float d = t.done[e] ? 1.0f : 0.0f;
-      const float td = fabsf(sr + (1.0f - d) * t.gamma * sm - sq);
+      const float td = rollout_td(sr, sq, sm, d, t.gamma);
       t.chunk_td[e] = (t.slot == 0 ? 0.0f : t.chunk_td[e]) + td;
     }
     __syncthreads();

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void td_chunk_kernel(int E, int N, float gamma
       st += sh[2][threadIdx.x + j];
     }
     const float d = done[e] ? 1.0f : 0.0f;
-    const float td = fabsf(sr + (1.0f - d) * gamma * st - sq);
+    const float td = rollout_td(sr, sq, st, d, gamma);
     chunk_td[e] = (t == 0 ? 0.0f : chunk_td[e]) + td;
   }
 }
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(1024) void td_fold_range_kernel(int E, int N, float
       st += m[k];
     }
     const float d = d8 ? 1.0f : 0.0f;
-    tdv[j][le] = fabsf(sr + (1.0f - d) * gamma * st - sq);
+    tdv[j][le] = rollout_td(sr, sq, st, d, gamma);
     const int64_t row = rows[e];
     if (row >= 0 && row < n_rows) {
       for (int k = 0; k < N; ++k) {
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void eval_accum_kernel(int E, int N, float gam
   score[e] += sr;
   const bool dn = done[e] != 0;
   if (q_taken && maxq_next && loss) {
-    const float td = fabsf(sr + (dn ? 0.0f : 1.0f) * gamma * st - sq);
+    const float td = rollout_td(sr, sq, st, dn ? 1.0f : 0.0f, gamma);
     loss[e] += td * td;
   }
   if (dn) active[e] = 0;

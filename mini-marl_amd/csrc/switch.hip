@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void switch_step_kernel(SwitchTab tab, SwitchS
     }
     if (env_ok && k == 0) {
       const float dn = tdone ? 1.0f : 0.0f;
-      const float td = fabsf(sr + (1.0f - dn) * tdf.gamma * sm - sq);
+      const float td = rollout_td(sr, sq, sm, dn, tdf.gamma);
       tdf.chunk_td[e] = (tdf.slot == 0 ? 0.0f : tdf.chunk_td[e]) + td;
       tdf.s_done[trow * tdf.C + tdf.slot] = tdone;
     }

@@ -8,6 +8,7 @@ iteration = ``max_step`` lockstep steps of all of them) and ``test_envs`` (greed
 in parallel, the reference's ``test_episodes``).
 """
 from dataclasses import dataclass, field, replace
+from typing import Optional
 
 
 @dataclass
@@ -22,6 +23,9 @@ class QTrainConfig:
     max_step: int = 100                 # --max_step
     step_cost: float = -0.01            # --step_cost
     n_actions: int = 5
+    # rollout step mode (RolloutEngine persistent=): None = the chunk-persistent launches where they fit, False = one
+    # launch per step (e.g. several processes sharing one GPU: the chunk kernel needs every CU for its own blocks)
+    persistent: Optional[bool] = None
     # agent Q_Net (vdn/_network.py:14-19): D -> f1 -> g (ReLU) -> GRUCell(g, h) -> A
     f1: int = 64
     g: int = 32

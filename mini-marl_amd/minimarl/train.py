@@ -50,7 +50,7 @@ class QTrainer:
                                  chunk=c.chunk_size, capacity=c.buffer_limit, gamma=c.gamma, max_steps=c.max_step,
                                  step_cost=c.step_cost, full_observable=c.full_observable,
                                  per_flavor=c.per_flavor, per_kwargs=per_kwargs, seed=c.seed + 7919 * rank,
-                                 env=c.env, device=self.device)
+                                 env=c.env, persistent=c.persistent, device=self.device)
         eng = self.eng
         # the behavior net's init does not depend on the rank (same seed): replicas start identical
         eng.behavior.init_default(c.seed)

@@ -6,7 +6,8 @@ the driver's). This exercises, with real inter-process all-reduces: the rank-0 p
 QMIX learner's flat-gradient all-reduce inside replay_update (QLearner.replay_update(allreduce)), the
 integrated train loop's learner, and MAPPO's per-epoch gradient all-reduce plus the all-reduced advantage /
 return statistics (MappoRunner(grad_allreduce=...)). After the updates every replica's parameters must be
-bit-identical (exact int64 checksums of the parameter bytes, all-gathered by bench.py)."""
+bit-identical (exact int64 checksums of the parameter bytes, all-gathered by bench.py). Each rank runs cfg4's shard:
+4096 envs x 8 agents (the rollout in one-launch-per-step mode: two processes share the GPU)."""
 import json
 import os
 import subprocess
@@ -23,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_two_ranks_replicas_stay_identical():
     env = dict(os.environ, MM_BENCH_SHARED_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
-           "--repeats", "1", "--envs", "512", "--learner-steps", "5", "--learner-big-steps", "0",
+           "--repeats", "1", "--envs", "4096", "--learner-steps", "5", "--learner-big-steps", "0",
            "--train-episodes", "1", "--cfg1-episodes", "0", "--mappo-episodes", "1", "--offq-updates", "0",
            "--no-cfg5", "--no-cpu-baseline"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)

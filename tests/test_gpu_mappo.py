@@ -53,6 +53,26 @@ def _fp32_spread(f, n_chunks):
     return c, sp
 
 
+def _fp32_rollout_outputs(PA, PC, data, E, N, T):
+    """data with the rollout's stored old log-probs / values replaced by the fp32 oracle's own forward from the
+    stored hiddens (an fp32 variant of which forward produced them: the device's rollout and training forwards are
+    the same MFMA code, so its epoch-0 ratio is exactly 1; the oracle's, against the device's old log-probs, is
+    1 + O(2^-24) — a fp32-rounding effect the spread must include)."""
+    d2 = dict(data)
+    lp_all, v_all = data["action_log_probs"].copy(), data["value_preds"].copy()
+    EN = E * N
+    for t in range(T):
+        v, _, lp, _, _ = om.get_actions(PA, PC, torch.from_numpy(data["obs"][t].reshape(EN, -1)),
+                                        torch.from_numpy(data["rnn_states"][t].reshape(EN, -1)),
+                                        torch.from_numpy(data["rnn_states_critic"][t].reshape(EN, -1)),
+                                        torch.from_numpy(data["masks"][t].reshape(EN, 1)),
+                                        actions=torch.from_numpy(data["actions"][t].reshape(EN, 1).astype(np.int64)))
+        lp_all[t] = lp.numpy().reshape(E, N, 1)
+        v_all[t] = v.numpy().reshape(E, N, 1)
+    d2["action_log_probs"], d2["value_preds"] = lp_all, v_all
+    return d2
+
+
 def _unclipped_grads(rec, ep=0):
     """{(net, key): gradient before clip_grad_norm_} of epoch ep of an om.ppo_train record."""
     out = {}
@@ -477,7 +497,8 @@ def test_full_train_15_epochs_vs_oracle_at_scale():
     advantages normalised once, clip 0.5 + Adam per net; ramppo_network.py:211-287) at 128 envs x 8 agents x
     T = 40 (the golden covers E = 4, N = 2, T = 10 only): post-train parameters and ValueNorm state within K_FP32
     fp32 spreads (module docstring; over 15 epochs the spread carries Adam's sign-flip steps of near-zero
-    gradients) of the f64 oracle on the same rollout."""
+    gradients; and the fp32 variant of the rollout's old log-probs / values, _fp32_rollout_outputs) of the f64
+    oracle on the same rollout."""
     from minimarl.env import VecEnv
     from minimarl.mappo import MappoPolicy, MappoRunner
     E, N, T, L, EP = 128, 8, 40, 5, 15
@@ -496,9 +517,65 @@ def test_full_train_15_epochs_vs_oracle_at_scale():
     torch.cuda.synchronize()
     o64, spread = _fp32_spread(lambda dt, pm: _train_outputs(*_ppo_oracle(PA, PC, data, vn0, EP, L, dt, pm)),
                                T * E * N // L)
+    # + the fp32 variant whose old log-probs / values come from the oracle's own fp32 forward
+    o_rl = _train_outputs(*_ppo_oracle(PA, PC, _fp32_rollout_outputs(PA, PC, data, E, N, T), vn0, EP, L,
+                                       torch.float32, None))
+    for k in o64:
+        spread[k] = max(spread[k], float(np.abs(np.asarray(o_rl[k], np.float64) - np.asarray(o64[k], np.float64)).max()))
     for net, kind in ((p.actor, "actor"), (p.critic, "critic")):
         for k in om.NET_KEYS:
             _assert_within(net.view(k).detach().cpu().numpy(), o64[(kind, k)], spread[(kind, k)], f"{kind} {k}")
     vn = r.trainer.value_normalizer_state()
     _assert_within(vn["running_mean"], o64["vn_mean"], spread["vn_mean"], "vn mean")
     _assert_within(vn["running_mean_sq"], o64["vn_mean_sq"], spread["vn_mean_sq"], "vn mean_sq")
+
+
+def test_cfg3_full_size_rollout_returns_and_epoch():
+    """cfg3 at its own size (4096 envs x 8 agents x T = 100, the shape bench.py times), checked through properties
+    the oracle can afford at that size (magym_runner.py:30-105):
+    * the env: obs / rewards / masks bit-exact vs the env oracle for the first 5 steps, driven with the stored actions;
+      every later step's masks are exactly 0 / 1 per env and all agents of an env share them;
+    * GAE + ValueNorm returns (shared_buffer.py:131-157) vs ``om.compute_returns`` on the device's own rewards,
+      values and masks (rtol 1e-5 atol 1e-5);
+    * one full PPO epoch (ramppo_network.py:211-287): finite losses and gradient norms, ratio 1 at epoch 0 (the
+      policy has not moved: every active row's exp(logp - logp_old) = 1 up to fp32 rounding), parameters changed
+      and finite."""
+    from minimarl.env import VecEnv
+    from minimarl.mappo import MappoPolicy, MappoRunner
+    from oracle.env import EnvSpec, VecEnvOracle
+    E, N, T, L = 4096, 8, 100, 5
+    env = VecEnv(E, N, max_steps=100, device=DEV)
+    p = MappoPolicy(env.obs_dim, 5, 32, DEV, seed=3)
+    r = MappoRunner(env, p, T=T, L=L, ppo_epoch=1, seed=11)
+    r.warmup()
+    r.rollout()
+    r.compute()
+    torch.cuda.synchronize()
+    b = r.buf
+    obs, acts = b.obs.cpu().numpy(), b.actions.cpu().numpy().astype(np.int64)
+    masks, rew = b.masks.cpu().numpy(), b.rewards.cpu().numpy()
+    ora = VecEnvOracle(EnvSpec(N, 100), E)
+    np.testing.assert_array_equal(obs[0].reshape(E, N, -1), ora.observe())
+    for t in range(5):
+        _, rw, dn = ora.step(acts[t].reshape(E, N))
+        ora.reset_envs(dn)
+        np.testing.assert_array_equal(obs[t + 1].reshape(E, N, -1), ora.observe())
+        np.testing.assert_array_equal(rew[t].reshape(E, N), rw)
+        np.testing.assert_array_equal(masks[t + 1].reshape(E, N), np.repeat((~dn)[:, None], N, 1).astype(np.float32))
+    m = masks.reshape(T + 1, E, N)
+    assert set(np.unique(m)) <= {0.0, 1.0} and (m == m[:, :, :1]).all()
+    assert m[1:].min() == 0.0                       # envs finished inside the episode
+    tr = r.trainer
+    vn0 = [float(x) for x in tr.vn.cpu().numpy()]
+    data = _ref_layout(b, E, N)
+    ret_ref, _ = om.compute_returns(data["rewards"], data["value_preds"], data["masks"], data["value_preds"][T],
+                                    om.ValueNorm(*vn0), 0.99, 0.95)
+    np.testing.assert_allclose(data["returns"][:T], ret_ref[:T], rtol=1e-5, atol=1e-5)
+    a0, c0 = p.actor.flat.clone(), p.critic.flat.clone()
+    info = r.train()
+    torch.cuda.synchronize()
+    for k in ("value_loss", "policy_loss", "dist_entropy", "actor_grad_norm", "critic_grad_norm", "ratio"):
+        assert np.isfinite(info[k]), k
+    assert abs(info["ratio"] - 1.0) < 1e-3          # (an f32 atomic sum over 3.3M rows)
+    assert torch.isfinite(p.actor.flat).all() and torch.isfinite(p.critic.flat).all()
+    assert not torch.equal(p.actor.flat, a0) and not torch.equal(p.critic.flat, c0)
