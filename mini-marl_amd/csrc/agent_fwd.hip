@@ -2011,6 +2011,7 @@ struct RollChunk {   // kernarg right after the two QFwdParams
   uint64_t* flags;           // [T][N] behavior hand-off flags: (seq << 16) + step index published
   uint8_t* hx;               // [T][C][N][256] hand-off actions, one slot per step
   uint32_t* err;             // sticky error bits: 1 staging row outside the store, 2 hand-off wait expired
+  uint64_t* trace;           // per-step timing stamps (MM_ROLL_DEBUG builds, tools/chunk_trace.py), else nullptr
   int c0, n, CL, lds_env;   // first step's chunk position, steps, chunk length, LDS offset of the env state
 };
 static_assert(alignof(RollChunk) == 8, "rollout_chunk kernarg layout");
@@ -2079,6 +2080,21 @@ __device__ __forceinline__ ChunkCtx chunk_ctx(const QFwdParams* kargs) {
   return cx;
 }
 
+// timing stamp k of step i of waves 0 and 15 (lane 0; MM_ROLL_DEBUG builds only)
+#if MM_ROLL_DEBUG
+#define MM_CSTAMP(k)                                                                                          \
+  do {                                                                                                        \
+    if (rc.trace && lane == 0 && i < 16 && (wave == 0 || wave == 15)) {                                       \
+      const int lbk = cx.tile * 2 * N + (second ? N : 0) + agent;                                             \
+      rc.trace[(((int64_t)lbk * 2 + (wave ? 1 : 0)) * 16 + i) * 4 + (k)] = __builtin_amdgcn_s_memrealtime();  \
+    }                                                                                                         \
+  } while (0)
+#else
+#define MM_CSTAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 template <int F1, int G, int H, int AB, bool EXACT>
 __device__ __forceinline__ void roll_chunk_steps() {
   const QFwdParams* kargs0 = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -2111,6 +2127,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
     const int c = rc.c0 + i;
     const uint64_t ctr = cx.ctr0 + (uint64_t)i;
     const int cur = i & 1, prv = cur ^ 1;
+    MM_CSTAMP(0);
     // (1) the actions of step t (i > 0: published by the tile's N behavior blocks at the end of their step t - 1)
     uint32_t aq[2] = {0u, 0u};   // 4-bit actions, agent k at bits 4 (k & 7) of aq[k >> 3]
     if (i > 0) {
@@ -2127,6 +2144,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
         }
       }
       __syncthreads();
+      MM_CSTAMP(1);
       if (dvalid) {
         uint8_t* hs = rc.hx + ((int64_t)tile * CL + i) * N * 256;
         uint32_t w[kRollMaxN];
@@ -2246,6 +2264,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       }
     }
     __syncthreads();
+    MM_CSTAMP(2);
     // (5) the forward: target on s'_t (max Q'_t, s'_t stored into slot c + 1), behavior on s_{t+1} (act / Q(a))
     const int64_t off = second ? ((c + 1 < CL) ? rc.b_off0 + (int64_t)i * EN : rc.b_offn) : rc.t_off0 + (int64_t)i * EN;
     const int64_t nxt_off = (int64_t)(c + 1) * nd;
@@ -2319,6 +2338,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr() + tz, ol, xn, h0, cx.eps, ctr, off, 1);
       if (second && g == 0 && e < E) cx.shx[le] = (uint8_t)a;
     }
+    MM_CSTAMP(3);
     // behavior blocks: publish the actions of step t + 1 for the tile (not after the launch's last step)
     if (second && i + 1 < rc.n) {
       __syncthreads();
@@ -3218,6 +3238,11 @@ int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, con
   r.flags = reinterpret_cast<uint64_t*>(x->flags);
   r.hx = x->handoff;
   r.err = reinterpret_cast<uint32_t*>(x->err);
+#if MM_ROLL_DEBUG
+  r.trace = debug_trace_buffer("MM_ROLL_TRACE");
+#else
+  r.trace = nullptr;
+#endif
   r.c0 = x->c0;
   r.n = x->n_steps;
   r.CL = x->chunk_len;

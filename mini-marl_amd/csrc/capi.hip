@@ -147,8 +147,8 @@ namespace mm {
 static uint64_t* g_trace = nullptr;
 int debug_trace_alloc() {
   if (g_trace) return 0;
-  if (hipMalloc(&g_trace, 4096 * sizeof(uint64_t)) != hipSuccess) return -1;
-  return hipMemset(g_trace, 0, 4096 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+  if (hipMalloc(&g_trace, 65536 * sizeof(uint64_t)) != hipSuccess) return -1;
+  return hipMemset(g_trace, 0, 65536 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
 }
 uint64_t* debug_trace_buffer(const char* env_name) {
   const char* v = getenv(env_name);
@@ -159,7 +159,7 @@ uint64_t* debug_trace_buffer(const char* env_name) {
 
 extern "C" int mm_debug_trace(uint64_t* host_out, int32_t n) {
   if (!host_out && n == 0) return mm::debug_trace_alloc();  // allocate up front (not legal inside graph capture)
-  if (!mm::g_trace || n <= 0 || n > 4096) { mm::set_error("mm_debug_trace: no trace buffer (set the trace env var) or bad n"); return -1; }
+  if (!mm::g_trace || n <= 0 || n > 65536) { mm::set_error("mm_debug_trace: no trace buffer (set the trace env var) or bad n"); return -1; }
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   return hipMemcpy(host_out, mm::g_trace, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost) == hipSuccess ? 0
                                                                                                           : -1;

@@ -150,7 +150,7 @@ def test_trainer_resume_bit_identical_fused_odd_step(tmp_path):
     from minimarl.train import QTrainer
     cfg = QTrainConfig(algo="qmix", n_envs=2048, n_agents=4, full_observable=False, buffer_limit=4096, max_step=13,
                        update_iter=2, update_target_interval=2, test_interval=0, test_envs=0,
-                       epsilon_anneal_episode=10, seed=11)
+                       epsilon_anneal_episode=10, seed=11, persistent=False)
     a = QTrainer(cfg, device=DEV)
     assert a.eng.fused
     a.train_episode()

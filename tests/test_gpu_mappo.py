@@ -53,24 +53,43 @@ def _fp32_spread(f, n_chunks):
     return c, sp
 
 
-def _fp32_rollout_outputs(PA, PC, data, E, N, T):
-    """data with the rollout's stored old log-probs / values replaced by the fp32 oracle's own forward from the
-    stored hiddens (an fp32 variant of which forward produced them: the device's rollout and training forwards are
-    the same MFMA code, so its epoch-0 ratio is exactly 1; the oracle's, against the device's old log-probs, is
-    1 + O(2^-24) — a fp32-rounding effect the spread must include)."""
-    d2 = dict(data)
-    lp_all, v_all = data["action_log_probs"].copy(), data["value_preds"].copy()
-    EN = E * N
-    for t in range(T):
-        v, _, lp, _, _ = om.get_actions(PA, PC, torch.from_numpy(data["obs"][t].reshape(EN, -1)),
-                                        torch.from_numpy(data["rnn_states"][t].reshape(EN, -1)),
-                                        torch.from_numpy(data["rnn_states_critic"][t].reshape(EN, -1)),
-                                        torch.from_numpy(data["masks"][t].reshape(EN, 1)),
-                                        actions=torch.from_numpy(data["actions"][t].reshape(EN, 1).astype(np.int64)))
-        lp_all[t] = lp.numpy().reshape(E, N, 1)
-        v_all[t] = v.numpy().reshape(E, N, 1)
-    d2["action_log_probs"], d2["value_preds"] = lp_all, v_all
-    return d2
+def _ppo_oracle_self_old(PA, PC, data, vn0, epochs, L, dtype=torch.float32):
+    """The oracle with the rollout's old log-probs / values replaced by its OWN epoch-0 training forward
+    (evaluate_chunks on the same chunk batch): its epoch-0 ratio is then exactly 1, as on the device, whose rollout
+    and training forwards are the same MFMA code (so the device's old log-probs carry no rounding the training
+    forward does not share). -> _train_outputs of that run."""
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        npd = np.float64 if dtype == torch.float64 else np.float32
+        d = {k: (v.astype(npd) if v.dtype in (np.float32, np.float64) else v) for k, v in data.items()}
+        PA2 = {k: torch.as_tensor(v).to(dtype) for k, v in PA.items()}
+        PC2 = {k: torch.as_tensor(v).to(dtype) for k, v in PC.items()}
+        vn = om.ValueNorm(*vn0)
+        adv = om.normalized_advantages(d, vn)
+        b = om.chunk_batch(d, adv, L, None)
+        with torch.no_grad():
+            lp, _ = om.evaluate_chunks(PA2, b["obs"], b["ha0"], b["masks"], L, "actor", b["actions"],
+                                       b["active_masks"])
+            v = om.evaluate_chunks(PC2, b["obs"], b["hc0"], b["masks"], L, "critic")
+        b["action_log_probs"], b["value_preds"] = lp.detach(), v.detach()
+        sa, sc, rec = {}, {}, []
+        for _ in range(epochs):
+            pa = {k: t.detach().clone().requires_grad_(True) for k, t in PA2.items()}
+            pc = {k: t.detach().clone().requires_grad_(True) for k, t in PC2.items()}
+            vn.update(b["returns"])
+            pol, ent, vloss, _ = om.ppo_losses(pa, pc, b, L, vn, entropy_coef=0.01)
+            ga = torch.autograd.grad(pol - ent * 0.01, [pa[k] for k in om.NET_KEYS])
+            gc = torch.autograd.grad(vloss * 0.5, [pc[k] for k in om.NET_KEYS])
+            ga, na = om.clip_grads(list(ga), 0.5)
+            gc, nc = om.clip_grads(list(gc), 0.5)
+            rec.append(dict(ga=dict(zip(om.NET_KEYS, ga)), gc=dict(zip(om.NET_KEYS, gc)), na=float(na), nc=float(nc),
+                            pol=float(pol.detach()), ent=float(ent.detach()), vloss=float(vloss.detach())))
+            PA2 = om.adam(PA2, dict(zip(om.NET_KEYS, ga)), sa, 1e-4, 1e-5)
+            PC2 = om.adam(PC2, dict(zip(om.NET_KEYS, gc)), sc, 1e-4, 1e-5)
+    finally:
+        torch.set_default_dtype(old)
+    return _train_outputs(rec, PA2, PC2, vn)
 
 
 def _unclipped_grads(rec, ep=0):
@@ -497,8 +516,9 @@ def test_full_train_15_epochs_vs_oracle_at_scale():
     advantages normalised once, clip 0.5 + Adam per net; ramppo_network.py:211-287) at 128 envs x 8 agents x
     T = 40 (the golden covers E = 4, N = 2, T = 10 only): post-train parameters and ValueNorm state within K_FP32
     fp32 spreads (module docstring; over 15 epochs the spread carries Adam's sign-flip steps of near-zero
-    gradients; and the fp32 variant of the rollout's old log-probs / values, _fp32_rollout_outputs) of the f64
-    oracle on the same rollout."""
+    gradients) of the f64 oracle on the same rollout whose old log-probs / values are its own epoch-0 forward
+    (_ppo_oracle_self_old: the device's rollout and training forwards are the same MFMA code, so its epoch-0 ratio
+    is exactly 1)."""
     from minimarl.env import VecEnv
     from minimarl.mappo import MappoPolicy, MappoRunner
     E, N, T, L, EP = 128, 8, 40, 5, 15
@@ -515,13 +535,15 @@ def test_full_train_15_epochs_vs_oracle_at_scale():
     data = _ref_layout(r.buf, E, N)
     r.train()
     torch.cuda.synchronize()
-    o64, spread = _fp32_spread(lambda dt, pm: _train_outputs(*_ppo_oracle(PA, PC, data, vn0, EP, L, dt, pm)),
-                               T * E * N // L)
-    # + the fp32 variant whose old log-probs / values come from the oracle's own fp32 forward
-    o_rl = _train_outputs(*_ppo_oracle(PA, PC, _fp32_rollout_outputs(PA, PC, data, E, N, T), vn0, EP, L,
-                                       torch.float32, None))
+    _, spread = _fp32_spread(lambda dt, pm: _train_outputs(*_ppo_oracle(PA, PC, data, vn0, EP, L, dt, pm)),
+                             T * E * N // L)
+    # the reference: the f64 oracle whose old log-probs / values are its own epoch-0 training forward (ratio exactly 1
+    # at epoch 0, as on the device, whose rollout and training forwards are one MFMA code path); the spread also
+    # covers the fp32 run of that variant
+    o64 = _ppo_oracle_self_old(PA, PC, data, vn0, EP, L, torch.float64)
+    o_32 = _ppo_oracle_self_old(PA, PC, data, vn0, EP, L, torch.float32)
     for k in o64:
-        spread[k] = max(spread[k], float(np.abs(np.asarray(o_rl[k], np.float64) - np.asarray(o64[k], np.float64)).max()))
+        spread[k] = max(spread[k], float(np.abs(np.asarray(o_32[k], np.float64) - np.asarray(o64[k], np.float64)).max()))
     for net, kind in ((p.actor, "actor"), (p.critic, "critic")):
         for k in om.NET_KEYS:
             _assert_within(net.view(k).detach().cpu().numpy(), o64[(kind, k)], spread[(kind, k)], f"{kind} {k}")
