@@ -408,6 +408,23 @@ int mm_mixer_bwd_seq_rec(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1
                          float* delta, float* ws, int32_t steps, mm_stream_t s);
 int mm_mixer_seq_split(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* ws,
                        int32_t steps);
+/* The learner forward's two independent chains in shared grids (no stream fork / join in the update graph), each
+ * block running the separate kernel's body, so results are identical to the separate calls:
+ *   mm_agent_mixer_pre     = mm_mixer_gi(R = rows, both mixers) + mm_agent_q_pre2(both nets, rows rows each)
+ *   mm_agent_mixer_rec_seq = mm_mixer_fwd_seq_rec(B, nets[2], steps, reset_steps)
+ *                            + mm_agent_q_rec_seq2(both nets, B envs each, steps, reset)
+ * (Train_dqn.train's forward, qmix/_train.py:55-77). mm_agent_mixer_pair_supported returns bit 0 when the pre pair
+ * applies to (dims, B x steps rows), bit 1 when the recurrence pair does; outside them both return MM_EINVAL. */
+int mm_agent_mixer_pair_supported(const mm_qnet_dims* d, int32_t B, int32_t steps, int32_t N, int32_t S, int32_t Hm,
+                                  int32_t K1);
+int mm_agent_mixer_pre(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, const float* packed1,
+                       const mm_qfwd_io* io1, int64_t rows, int32_t N, int32_t S, int32_t Hm, int32_t K1,
+                       const float* obs, const float* reset_obs, const float* mP0, const int64_t* s_off0, float* gi0,
+                       const float* mP1, const int64_t* s_off1, float* gi1, mm_stream_t s);
+int mm_agent_mixer_rec_seq(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, const float* packed1,
+                           const mm_qfwd_io* io1, int32_t B, int32_t steps, const uint8_t* reset, int32_t N,
+                           int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets, int32_t n_nets,
+                           const uint8_t* reset_steps, mm_stream_t s);
 int mm_mixer_bwd_seq(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                      const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
                      float* delta, float* ws, int32_t steps, mm_stream_t s);

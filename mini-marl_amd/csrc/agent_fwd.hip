@@ -787,19 +787,33 @@ __global__ __launch_bounds__(256, 2) void agent_rec_seq_kernel(QFwdParams p0, QF
 // n-wave only STORES (the training save rows of step t - 1, staged in LDS by the r-wave and written
 // out while the r-wave computes step t's gates), and the Q wave loads its gathered action before
 // issuing its stores. No wave on the recurrence's critical path ever waits for a store.
+// LDS of one gate-parallel REC block (dynamic, so a paired launch can carve the same space for another body)
+template <int H>
+struct RecGpLds {
+  static constexpr int HB = H / 32;
+  static constexpr size_t hx = 0;                                  // float [2][HB][16][64]
+  static constexpr size_t gx = hx + 2 * HB * 16 * 64 * 4;          // float [2][HB][16][64]
+  static constexpr size_t svs = gx + 2 * HB * 16 * 64 * 4;         // float [2][HB][6][32][33]
+  static constexpr size_t zreset = svs + 2 * HB * 6 * 32 * 33 * 4; // int [64]
+  static constexpr size_t bytes = zreset + 64 * 4;
+};
+
 template <int F1, int G, int H, int AB>
-__device__ __forceinline__ void rec_seq_gp_body(const QFwdParams& p, const RecSeq& sq, int bid) {
+__device__ __forceinline__ void rec_seq_gp_body(const QFwdParams& p, const RecSeq& sq, int bid, char* lds) {
   const uint64_t t_entry = clock64();
   using S = Sched<F1, G, H, AB>;
   using CG = typename S::CG;
+  using LY = RecGpLds<H>;
   constexpr int RB2 = S::RB2, HB = S::HB;
   constexpr int SROW = F1 + G + 6 * H;   // training save row of one (env, agent)
-  __shared__ float hx[2][HB][16][64];   // new hidden blocks, double-buffered by step parity
-  __shared__ float gx[2][HB][16][64];   // z / n-hidden gate accumulators handed to the r-wave
+  // new hidden blocks, double-buffered by step parity
+  float(*hx)[HB][16][64] = reinterpret_cast<float(*)[HB][16][64]>(lds + LY::hx);
+  // z / n-hidden gate accumulators handed to the r-wave
+  float(*gx)[HB][16][64] = reinterpret_cast<float(*)[HB][16][64]>(lds + LY::gx);
   // save-row staging [step parity][hb][field][feature][env] (env stride 33: conflict-free both ways), so
   // the save rows go out as 128-byte runs (one env's 32 features of one field)
-  __shared__ float svs[2][HB][6][32][33];
-  __shared__ int zreset[64];   // reset flag of the next step, written by the r-wave of hb 0 in the gate phase
+  float(*svs)[HB][6][32][33] = reinterpret_cast<float(*)[HB][6][32][33]>(lds + LY::svs);
+  int* zreset = reinterpret_cast<int*>(lds + LY::zreset);   // reset flag of the next step (r-wave of hb 0)
   const int agent = bid % p.N, tile = bid / p.N;
   const float* W = p.packed + (int64_t)agent * p.g.agent_stride;
   const int lane = threadIdx.x & 63, hh = lane >> 5, wv = threadIdx.x >> 6;
@@ -998,10 +1012,11 @@ __device__ __forceinline__ void rec_seq_gp_body(const QFwdParams& p, const RecSe
 template <int F1, int G, int H, int AB>
 __global__ __launch_bounds__(64 * (3 * (H / 32) + 1)) void agent_rec_seq_gp_kernel(QFwdParams p0, QFwdParams p1,
                                                                                    RecSeq s0, RecSeq s1) {
+  extern __shared__ __attribute__((aligned(16))) char rlds[];
   if ((int)blockIdx.x >= p0.nblocks)
-    rec_seq_gp_body<F1, G, H, AB>(p1, s1, (int)blockIdx.x - p0.nblocks);
+    rec_seq_gp_body<F1, G, H, AB>(p1, s1, (int)blockIdx.x - p0.nblocks, rlds);
   else
-    rec_seq_gp_body<F1, G, H, AB>(p0, s0, (int)blockIdx.x);
+    rec_seq_gp_body<F1, G, H, AB>(p0, s0, (int)blockIdx.x, rlds);
 }
 
 // One launch serves one or two nets (e.g. the target net on s'_t and the behavior net on
@@ -2980,8 +2995,12 @@ static int launch_rec_seq(QFwdParams p0, QFwdParams p1, const RecSeq& s0, const 
   // many tiles: the 2-wave kernel keeps more blocks per CU
   const bool gp = (p0.nblocks + p1.nblocks) < 512;
   if (gp) {
+    static const hipError_t attr = hipFuncSetAttribute((const void*)agent_rec_seq_gp_kernel<F1, G, H, AB>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)RecGpLds<H>::bytes);
+    MM_HIP_CHECK(attr);
     hipLaunchKernelGGL((agent_rec_seq_gp_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks),
-                       dim3(64 * (3 * (H / 32) + 1)), 0, s, p0, p1, s0, s1);
+                       dim3(64 * (3 * (H / 32) + 1)), RecGpLds<H>::bytes, s, p0, p1, s0, s1);
   } else {
     hipLaunchKernelGGL((agent_rec_seq_kernel<F1, G, H, AB>), dim3(p0.nblocks + p1.nblocks), dim3(64 * (H / 32)), 0,
                        s, p0, p1, s0, s1);
@@ -2990,13 +3009,13 @@ static int launch_rec_seq(QFwdParams p0, QFwdParams p1, const RecSeq& s0, const 
   return MM_OK;
 }
 
-int agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
-                     const float* packed1, const mm_qfwd_io* io1, int64_t e1, int32_t steps, const uint8_t* reset,
-                     hipStream_t s) {
-  QFwdParams p0, p1;
+// the two nets' launch parameters and sequence arguments of agent_q_rec_seq2 (also the paired launch's)
+static int rec_seq_args(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
+                        const float* packed1, const mm_qfwd_io* io1, int64_t e1, int32_t steps, const uint8_t* reset,
+                        QFwdParams& p0, QFwdParams& p1, RecSeq& s0, RecSeq& s1, bool& single) {
   int rc = make_params(d, packed0, io0, e0, &p0);
   if (rc) return rc;
-  const bool single = !io1 || e1 <= 0;
+  single = !io1 || e1 <= 0;
   if (single) {
     p1 = p0;
   } else {
@@ -3019,8 +3038,20 @@ int agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_
     q.trace = nullptr;
     return q;
   };
-  RecSeq s0 = mk(p0), s1 = mk(p1);
+  s0 = mk(p0);
+  s1 = mk(p1);
   s0.trace = debug_trace_buffer("MM_REC_TRACE");
+  return MM_OK;
+}
+
+int agent_q_rec_seq2(const mm_qnet_dims* d, const float* packed0, const mm_qfwd_io* io0, int64_t e0,
+                     const float* packed1, const mm_qfwd_io* io1, int64_t e1, int32_t steps, const uint8_t* reset,
+                     hipStream_t s) {
+  QFwdParams p0, p1;
+  RecSeq s0, s1;
+  bool single;
+  const int rc = rec_seq_args(d, packed0, io0, e0, packed1, io1, e1, steps, reset, p0, p1, s0, s1, single);
+  if (rc) return rc;
   const int AB = (d->n_actions + 31) / 32;
 #define MM_RSEQ(F1_, G_, H_)                                                                                    \
   if (d->f1 == F1_ && d->g == G_ && d->h == H_)                                                                 \

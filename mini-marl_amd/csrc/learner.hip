@@ -166,39 +166,46 @@ struct MixGiArgs {
   int R, S, Hm, K1, N;
 };
 
-__global__ __launch_bounds__(256) void mixer_gi_kernel(MixGiArgs a) {
+// one 32-sample x 32-row tile (bx, by) of net bz, by the block's first 4 waves (a paired launch's wider block
+// lets its other waves pass: every thread reaches the barrier)
+__device__ __forceinline__ void mixer_gi_body(const MixGiArgs& a, int bx, int by, int bz) {
   __shared__ float red[4][1024];
-  const MixGiNet& nt = a.net[blockIdx.z];
+  const MixGiNet& nt = a.net[bz];
   const int S = a.S, M3 = 3 * a.Hm;
   const MixOff o = mix_offsets(S, a.Hm, a.K1, a.N);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, hh = lane >> 5;
-  const int rb = blockIdx.y, col = blockIdx.x * 32 + i;
+  const int rb = by, col = bx * 32 + i;
   const int row = rb * 32 + i;
-  const float* W = nt.P + o.gWih + (int64_t)(row < M3 ? row : 0) * S;
-  const int64_t off = col < a.R ? state_off(nt.s_off, col, a.S) : -1;
-  const float* x = off >= 0 ? a.obs + off : a.reset_obs;
-  const int KD = (S + 31) / 32;
-  f32x16 acc = {0};
-  for (int kb = wave; kb < KD; kb += 4) {
-    float av[16], bv[16];
+  if (wave < 4) {
+    const float* W = nt.P + o.gWih + (int64_t)(row < M3 ? row : 0) * S;
+    const int64_t off = col < a.R ? state_off(nt.s_off, col, a.S) : -1;
+    const float* x = off >= 0 ? a.obs + off : a.reset_obs;
+    const int KD = (S + 31) / 32;
+    f32x16 acc = {0};
+    for (int kb = wave; kb < KD; kb += 4) {
+      float av[16], bv[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int k = kb * 32 + kperm(s, hh);
-      const bool ok = k < S;
-      av[s] = (ok && row < M3) ? W[k] : 0.0f;
-      bv[s] = (ok && col < a.R) ? x[k] : 0.0f;
+      for (int s = 0; s < 16; ++s) {
+        const int k = kb * 32 + kperm(s, hh);
+        const bool ok = k < S;
+        av[s] = (ok && row < M3) ? W[k] : 0.0f;
+        bv[s] = (ok && col < a.R) ? x[k] : 0.0f;
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = mfma32(av[s], bv[s], acc);
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc = mfma32(av[s], bv[s], acc);
+    for (int s = 0; s < 16; ++s) red[wave][kperm(s, hh) * 32 + i] = acc[s];
   }
-#pragma unroll
-  for (int s = 0; s < 16; ++s) red[wave][kperm(s, hh) * 32 + i] = acc[s];
   __syncthreads();
-  for (int e = threadIdx.x; e < 1024; e += 256) {
-    const int m = rb * 32 + (e >> 5), c = blockIdx.x * 32 + (e & 31);
+  for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
+    const int m = rb * 32 + (e >> 5), c = bx * 32 + (e & 31);
     if (m < M3 && c < a.R)
       nt.gi[(int64_t)c * M3 + m] = nt.P[o.gbih + m] + ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e]));
   }
+}
+__global__ __launch_bounds__(256) void mixer_gi_kernel(MixGiArgs a) {
+  mixer_gi_body(a, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
 }
 
 // LDS-tiled form of the same projection: block = 4 waves = 64 samples x 64 gate rows, per 32-deep
@@ -1438,12 +1445,13 @@ __host__ __device__ inline size_t mix_rec_bwd_floats(int Hm, int win) {
 }
 inline bool mix_rec_supported(int Hm) { return Hm == 32 || Hm == 64; }
 
+// sample b of net `net` (block (b, net) of mixer_rec_fwd_kernel); sm: the block's dynamic LDS
 template <int HM>
-__device__ __forceinline__ void mixer_rec_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, const MixRecFwd& sq) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+__device__ __forceinline__ void mixer_rec_fwd_body(const MixFwdArgs& a, const MixFwdNet& nt, const MixRecFwd& sq, int b,
+                                                   int net, float* sm) {
   using Geo = MixRecGeo<HM>;
   constexpr int M3 = Geo::M3, LD = Geo::LDF;
-  const int b = blockIdx.x, ti = (int)threadIdx.x;
+  const int ti = (int)threadIdx.x;
   const MixOff o = mix_offsets(a.S, HM, a.K1, a.N);
   float* img = sm;                 // W_hh [M3][LD]
   float* hb = img + M3 * LD;       // [2][HM] hidden by step parity (already zero where the step resets)
@@ -1451,7 +1459,7 @@ __device__ __forceinline__ void mixer_rec_fwd_body(const MixFwdArgs& a, const Mi
   float* bhh = gh + M3;            // [M3]
   float* gin = bhh + M3;           // [win][M3] input projections of the window's steps
   float* rs = gin + sq.win * M3;   // [win + 1] 1: step w0 + tt starts from zero hidden
-  uint64_t* tr = (sq.trace && b == 0 && blockIdx.y == 0 && ti == 0) ? sq.trace : nullptr;
+  uint64_t* tr = (sq.trace && b == 0 && net == 0 && ti == 0) ? sq.trace : nullptr;
   if (tr) tr[0] = clock64();
   // prologue: W_hh image, b_hh, h_in and the first window's input projections by LDS-DMA (one round
   // trip, compact code); the reset flags by a plain load issued first
@@ -1537,10 +1545,11 @@ __device__ __forceinline__ void mixer_rec_fwd_body(const MixFwdArgs& a, const Mi
 // one inlined body per net: each reads its own kernel-argument fields with scalar loads
 template <int HM>
 __global__ __launch_bounds__(256) void mixer_rec_fwd_kernel(MixFwdArgs a, MixRecFwd sq) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   if (blockIdx.y == 0)
-    mixer_rec_fwd_body<HM>(a, a.net[0], sq);
+    mixer_rec_fwd_body<HM>(a, a.net[0], sq, (int)blockIdx.x, 0, sm);
   else
-    mixer_rec_fwd_body<HM>(a, a.net[1], sq);
+    mixer_rec_fwd_body<HM>(a, a.net[1], sq, (int)blockIdx.x, 1, sm);
 }
 
 // all R = C*B rows of one net: the hidden sequence (h_out) -> hypernets, Q_tot, save-row tail
@@ -2859,8 +2868,10 @@ int mm_mixer_fwd_seq_fits(int32_t B, int32_t N, int32_t Hm, int32_t K1) {
 
 // part 0: the whole forward; 1: the mixer recurrence only (reads gi, not the agents' Q: a caller may run it
 // beside the agent forward); 2: the hypernet pass only (after both)
+// part 3: no launch, the recurrence's arguments into *a_out / *rq_out (a paired launch, mm_agent_mixer_rec_seq)
 static int mixer_fwd_seq_part(int part, int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const mm_mix_net* nets,
-                              int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s) {
+                              int32_t n_nets, int32_t steps, const uint8_t* reset_steps, mm_stream_t s,
+                              mm::MixFwdArgs* a_out = nullptr, mm::MixRecFwd* rq_out = nullptr) {
   MM_REQUIRE(nets && n_nets >= 1 && n_nets <= 2 && B > 0 && steps >= 1, "mixer_fwd_seq: bad args");
   MM_REQUIRE(part == 0 || mix_split_enabled(), "mixer_fwd_seq: the parts need the split path");
   MM_REQUIRE(steps == 1 || reset_steps, "mixer_fwd_seq: reset_steps required for steps > 1");
@@ -2902,6 +2913,11 @@ static int mixer_fwd_seq_part(int part, int32_t B, int32_t N, int32_t S, int32_t
     rq.save_st = q.save_st;
     rq.reset_steps = reset_steps;
     rq.trace = mm::debug_trace_buffer("MM_MIX_TRACE_FWD");
+    if (part == 3) {
+      *a_out = a;
+      *rq_out = rq;
+      return MM_OK;
+    }
     if (part != 2) {
       if (Hm == 32)
         hipLaunchKernelGGL(mm::mixer_rec_fwd_kernel<32>, dim3(B, n_nets), dim3(256),

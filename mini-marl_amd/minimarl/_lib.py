@@ -277,6 +277,13 @@ _SIGS += [
     ("mm_mixer_bwd_seq_rec", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      c_vp, c_vp, c_vp, c_i32, c_vp]),
     ("mm_mixer_seq_split", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32]),
+    ("mm_agent_mixer_pair_supported", c_i32, [ctypes.POINTER(QnetDims), c_i32, c_i32, c_i32, c_i32, c_i32, c_i32]),
+    ("mm_agent_mixer_pre", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_vp,
+                                   ctypes.POINTER(QFwdIO), c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                   c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("mm_agent_mixer_rec_seq", c_i32, [ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_vp,
+                                       ctypes.POINTER(QFwdIO), c_i32, c_i32, c_vp, c_i32, c_i32, c_i32, c_i32,
+                                       ctypes.POINTER(MixNetIO), c_i32, c_vp, c_vp]),
 ]
 
 

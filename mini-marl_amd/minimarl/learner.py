@@ -100,7 +100,7 @@ class QLearner:
 
     def __init__(self, behavior, target, mixer=None, target_mixer=None, batch=32, chunk=10, gamma=0.99, lr=1e-3,
                  grad_clip=5.0, betas=(0.9, 0.999), adam_eps=1e-8, mode="qmix", clip_mixer=False, device="cuda",
-                 reference_compat=True, mixer_fp16=False, pair_bwd=True, fwd_side=True):
+                 reference_compat=True, mixer_fp16=False, pair_bwd=True, fwd_side=True, pair_fwd=True):
         assert mode in ("qmix", "vdn", "qmix_min", "vdn_double")
         self.mode = mode
         self.has_mixer = mode in ("qmix", "qmix_min")
@@ -121,6 +121,10 @@ class QLearner:
         self._pair_bwd = bool(pair_bwd)
         # the mixer's forward state projection + recurrence on a side stream (fwd_side=False: in line)
         self._fwd_side = bool(fwd_side)
+        # the forward's agent and mixer chains in shared grids (mm_agent_mixer_pre / mm_agent_mixer_rec_seq) where
+        # the shapes allow: no fork / join at all (pair_fwd=False: the side stream above)
+        self._pair_fwd = bool(pair_fwd)
+        self._pair_ok = None
         self.fast_pre = False           # opt-in: the fp16x3 agent PRE (not at the fp32 gradient bar, see compute_grads)
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM
@@ -297,8 +301,9 @@ class QLearner:
         reset_p = ctypes.c_void_p(reset_obs_ptr) if isinstance(reset_obs_ptr, int) else ptr(reset_obs_ptr)
         ND = N * D
         split = self._mixer_split()
+        pair = bool(split) and self._fwd_pair()
         side = self._side_stream() if split else None
-        fwd_side = split and self._fwd_side
+        fwd_side = split and self._fwd_side and not pair
         if fwd_side:
             # two streams (captured as a fork / join in the update graph): the mixer's state projection and its
             # GRU recurrence need no agent Q, so they run beside the agent PRE / REC chain
@@ -306,7 +311,7 @@ class QLearner:
             s_m = ctypes.c_void_p(side.cuda_stream)
         else:
             s_m = s
-        if self.has_mixer:
+        if self.has_mixer and not pair:
             # mixer GRU input projections of every (t, b) for both mixers: one MFMA launch
             mx = self.mix
             gi_fn = L.mm_mixer_gi_f16 if self.mixer_fp16 else L.mm_mixer_gi
@@ -328,8 +333,16 @@ class QLearner:
         # lo parts of a wide layer 1 (D = 300, |W| ~ 0.06) fall into f16's subnormal range, and the few ReLU masks that
         # flip against f32 put ~0.3 % of dW1 / dW2 outside the fp32 bar (test_learner_cfg5_benched_path_vs_oracle)
         pre_fn = L.mm_agent_q_pre2_h3 if (self.mixer_fp16 and CB >= 2048 and self.fast_pre) else L.mm_agent_q_pre2
-        check(pre_fn(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pb), CB,
-                     ptr(self.tgt.packed), ctypes.byref(pt), CB, s), "learner fwd pre")
+        if pair:
+            # + the mixers' state projection (mm_mixer_gi) in the same grid
+            mx = self.mix
+            check(L.mm_agent_mixer_pre(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pb),
+                                       ptr(self.tgt.packed), ctypes.byref(pt), CB, N, mx.S, mx.Hm, mx.K1, obs_p,
+                                       reset_p, ptr(mx.flat), ptr(self.s_off), ptr(self.gi_b), ptr(self.tmix.flat),
+                                       ptr(self.s2_off), ptr(self.gi_t), s), "learner fwd pre + mixer gi")
+        else:
+            check(pre_fn(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(pb), CB,
+                         ptr(self.tgt.packed), ctypes.byref(pt), CB, s), "learner fwd pre")
         if self.double:   # the double net (behavior weights) on s'
             pd = QFwdIO()
             pd.obs, pd.obs_se, pd.obs_sa, pd.obs_off = obs_p.value, 1, D, 0
@@ -343,7 +356,7 @@ class QLearner:
         if self.double and self._draws is None:
             self.dctr.add_(C)             # stream-ordered: captured into the update graph
         if self.seq:
-            self._forward_seq(L, s, obs_p, reset_p, split, join=fwd_side)
+            self._forward_seq(L, s, obs_p, reset_p, split, join=fwd_side, pair=pair)
         for t in range(0 if not self.seq else C, C):
             ib, it = QFwdIO(), QFwdIO()
             for io, h, gi in ((ib, self.hb, self.gi_ab), (it, self.ht, self.gi_at)):
@@ -488,6 +501,15 @@ class QLearner:
             self._side = torch.cuda.Stream(self.dev)
         return self._side
 
+    def _fwd_pair(self):
+        """Both paired forward launches apply (QMIX, exact-f32 state projection, the B = 32 shapes)."""
+        if self._pair_ok is None:
+            mx = self.mix
+            self._pair_ok = bool(self._pair_fwd and self.has_mixer and not self.double and not self.mixer_fp16 and
+                                 lib().mm_agent_mixer_pair_supported(ctypes.byref(self.beh.dims), self.B, self.C,
+                                                                     self.N, mx.S, mx.Hm, mx.K1) == 3)
+        return self._pair_ok
+
     def _mixer_split(self):
         """The mixer's state projection + GRU recurrence run on a second stream beside the agent chain (and its
         recurrence backward beside the agent BPTT): sequence path, both split mixer kernels available."""
@@ -513,7 +535,7 @@ class QLearner:
         mx = self.mix
         check(fn(self.B, self.N, mx.S, mx.Hm, mx.K1, self._mixer_nets(), 2, self.C, ptr(self.done8), s), what)
 
-    def _forward_seq(self, L, s, obs_p, reset_p, split=False, join=False):
+    def _forward_seq(self, L, s, obs_p, reset_p, split=False, join=False, pair=False):
         """REC of both nets over all C steps in one chunk-sequence launch, then the mixers per step."""
         B, C, N, H = self.B, self.C, self.N, self.H
         ib, it = QFwdIO(), QFwdIO()
@@ -526,6 +548,15 @@ class QLearner:
         ib.save = self.asave.data_ptr()
         it.mode = MM_Q_MAX
         it.qsel_out = self.maxq.data_ptr()
+        if pair:
+            # + the mixers' GRU over the state (mm_mixer_fwd_seq_rec) in the same grid, then the hypernet pass
+            mx = self.mix
+            check(L.mm_agent_mixer_rec_seq(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib),
+                                           ptr(self.tgt.packed), ctypes.byref(it), B, C, ptr(self.done8), N, mx.S,
+                                           mx.Hm, mx.K1, self._mixer_nets(), 2, ptr(self.done8), s),
+                  "rec seq + mixer recurrence")
+            self._mixer_seq_call(L, L.mm_mixer_fwd_seq_hyper, s, "mixer fwd seq (hypernets)")
+            return
         check(L.mm_agent_q_rec_seq2(ctypes.byref(self.beh.dims), ptr(self.beh.packed), ctypes.byref(ib), B,
                                     ptr(self.tgt.packed), ctypes.byref(it), B, C, ptr(self.done8), s), "rec seq")
         if self.has_mixer:

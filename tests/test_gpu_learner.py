@@ -6,6 +6,7 @@ gradients |g - g_ref| <= 2e-4 * max|g_ref| + 1e-3 * |g_ref|; new priorities rtol
 post-Adam params atol 2e-6 where |g_ref| > 1e-4 * max|g_ref| (Adam's first step is
 lr * sign(g), so near-zero gradients are compared through the gradient check instead).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -590,3 +591,33 @@ def test_paired_bwd_launch_matches_side_stream(fwd_side):
         res.append((eng.behavior.flat.clone(), mix.flat.clone(), lrn.loss.clone()))
     for x, y in zip(*res):
         assert torch.equal(x, y)
+
+
+def test_paired_fwd_launches_bit_identical():
+    """The forward's agent and mixer chains in shared grids (mm_agent_mixer_pre: agent PRE + mixer state projection,
+    mm_agent_mixer_rec_seq: agent recurrence + mixer recurrence; the default at the bench's B = 32 shape) against the
+    separate launches on a side stream (QLearner(pair_fwd=False)) and in line (fwd_side=False): bit-identical
+    parameters, Adam moments and loss after three captured updates."""
+    from minimarl._lib import lib
+    from minimarl.engine import RolloutEngine
+    from minimarl.learner import Mixer, QLearner
+    res = []
+    for pair, side in ((True, True), (False, True), (False, False)):
+        eng = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, device="cuda")
+        for _ in range(2):
+            eng.run_graph(0.5)
+        N, D = eng.N, eng.D
+        mix, tmix = Mixer(N, N * D, 64, 32, "cuda", seed=7), Mixer(N, N * D, 64, 32, "cuda", seed=7)
+        lrn = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda",
+                       pair_fwd=pair, fwd_side=side)
+        assert lrn._fwd_pair() == pair
+        if pair:
+            assert lib().mm_agent_mixer_pair_supported(ctypes.byref(eng.behavior.dims), 32, 10, N, N * D, 64, 32) == 3
+        lrn.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=1)
+        for _ in range(3):
+            lrn.replay_update()
+        torch.cuda.synchronize()
+        res.append((eng.behavior.flat.clone(), mix.flat.clone(), lrn.m.clone(), lrn.v.clone(), lrn.loss.clone()))
+    for other in res[1:]:
+        for x, y in zip(res[0], other):
+            assert torch.equal(x, y)

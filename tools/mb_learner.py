@@ -14,7 +14,8 @@ eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=10, capacity=CAP, seed=1, dev
 for _ in range(max(4, CAP // E + 1)):
     eng.run_graph(0.1)
 mix, tmix = Mixer(N, N * eng.D, 64, 32, "cuda", seed=7), Mixer(N, N * eng.D, 64, 32, "cuda", seed=7)
-L = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda")
+kw = {k: os.environ[v] == "1" for k, v in (("fwd_side", "MB_FWD_SIDE"),) if v in os.environ}
+L = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda", **kw)
 L.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=3)
 if os.environ.get("MB_FUSED", "1") == "0":     # A/B: the two-graph replay path
     L.graph_fused = None
@@ -27,5 +28,5 @@ for _ in range(50):
     L.replay_update()
 b.record()
 torch.cuda.synchronize()
-print(json.dumps({"dbg": os.environ.get("MM_MIX_DBG", "0"), "fused": L.graph_fused is not None,
+print(json.dumps({"kw": kw, "fused": L.graph_fused is not None,
                   "ms_per_update": a.elapsed_time(b) / 50}))
