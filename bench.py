@@ -348,16 +348,16 @@ def main():
             dist.all_reduce(g)
             return world
         learner._graph_scale = 1.0 / world
-    learner.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=99 + rank)
-    for _ in range(5):
-        learner.replay_update(allreduce)
+    # single-replica: the trainer's update_iter = 10 consecutive updates per graph launch (QTrainer.learn)
+    per_replay = 10 if allreduce is None else 1
+    learner.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=99 + rank, per_replay=per_replay)
+    learner.replay_updates(10, allreduce)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(args.learner_steps):
-        learner.replay_update(allreduce)
+    learner.replay_updates(args.learner_steps, allreduce)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -791,7 +791,7 @@ def main():
             "learner_updates_per_s": round(upd_per_s, 1),
             "learner": {"algo": "QMIX Train_dqn update", "batch_chunks": args.batch, "chunk": 10,
                         "mixer_hidden": 64, "ms_per_update": round(el_l / args.learner_steps * 1e3, 4),
-                        "updates": args.learner_steps, "grad_allreduce": (("gloo" if shared else "rccl") if dist else None),
+                        "updates": args.learner_steps, "updates_per_graph_launch": per_replay, "grad_allreduce": (("gloo" if shared else "rccl") if dist else None),
                         "reference_cpu_updates_per_s": 12.0,
                         "reference_cpu_note": "reference Train_dqn.train at its own shapes (GRU-32), 8 threads of "
                                               "the build container (BASELINE.md)",

@@ -403,6 +403,13 @@ int mm_mixer_fwd_seq_hyper(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t 
 int mm_mixer_bwd_seq_hyper(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                            const float* qa, const float* dq, const float* done, const float* ones, float* dhm,
                            float* dqa, float* delta, float* ws, int32_t steps, mm_stream_t s);
+/* mm_mixer_bwd_seq_hyper, then mm_per_update(per, nodes, td, batch): the small priority update rides as one more
+ * block of the hypernet launch (its TDs come from the loss before it; Train_dqn's priority update,
+ * qmix/main.py:240-244). Results identical to the two calls. */
+int mm_mixer_bwd_seq_hyper_per(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P,
+                               const float* save, const float* qa, const float* dq, const float* done,
+                               const float* ones, float* dhm, float* dqa, float* delta, float* ws, int32_t steps,
+                               mm_per* per, const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s);
 int mm_mixer_bwd_seq_rec(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P, const float* save,
                          const float* qa, const float* dq, const float* done, const float* ones, float* dhm, float* dqa,
                          float* delta, float* ws, int32_t steps, mm_stream_t s);
@@ -508,6 +515,16 @@ typedef struct mm_tmv_args {
 int mm_tmv(const mm_tmv_args* x, mm_stream_t s);
 /* Global-norm clip (torch clip_grad_norm_ over G[0:n_clip]) scaled by grad_scale (1/world after an
  * all-reduce), then Adam on P[0:n]; step is a device counter, norm_out receives the pre-clip norm. */
+/* mm_clip_adam (two_groups = 0, clip group G[0:n_clip]) or mm_clip2_adam (two_groups != 0, split = n_clip), then the
+ * behavior net's exact-f32 image written from the new parameters (what mm_qnet_pack_f32(d, P, packed) writes after
+ * the step; the agent net's d->n_agents nets lead P), and, when per != NULL, mm_per_update(per, nodes, td, batch):
+ * two launches instead of four (the Adam step and the image in one grid, the priority update one more block of it).
+ * Results identical to the separate calls (Train_dqn.train's step + priority update, qmix/_train.py:86-96,
+ * qmix/main.py:240-244). */
+int mm_clip_adam_pack(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip, int32_t two_groups,
+                      float max_norm, float lr, float beta1, float beta2, float eps, float* step, float* partials,
+                      float* norm_out, float grad_scale, const mm_qnet_dims* d, float* packed, mm_per* per,
+                      const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s);
 /* clip_grad_norm_ on G[0:split] and on G[split:n] separately (qmix/qmix.py:235-238), then Adam. */
 int mm_clip2_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t split, float max_norm, float lr,
                   float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, float grad_scale,

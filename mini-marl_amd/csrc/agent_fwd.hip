@@ -2627,6 +2627,64 @@ __global__ __launch_bounds__(1024, 1) void agent_pre_lds_kernel(QFwdParams p0, Q
 }
 
 // ---------------------------------------------------------------- packing
+// The canonical flat parameters behind f32 image element r of one agent (r < agent_stride): j0 (and, for the
+// combined b_ih + b_hh rows of the r / z gates, j1) as indices into the flat parameters, bias = a bias image
+// element (value j0 + j1, or j0 + 0.0f). j0 = -1: zero padding. Every parameter of the agent net appears in
+// exactly one image element.
+struct PackSrc {
+  int64_t j0, j1;
+  bool bias;
+};
+__device__ __forceinline__ PackSrc qnet_pack_src(const QnetGeo& g, int agent, int64_t r, int D, int F1, int G, int H,
+                                                 int A, const QnetOffsets& o) {
+  PackSrc ps{-1, -1, false};
+  bool hit = false;
+  // weight images: [rb][kb][q][lane][s & 3] (see load_frag)
+  auto wimg = [&](int64_t off, int KB, int rows, int cols, int64_t src) {
+    const int64_t sz = (int64_t)((rows + 31) / 32) * KB * 1024;
+    if (r >= off && r < off + sz) {
+      const int64_t t = r - off;
+      const int lane = (int)((t >> 2) & 63), s = (int)(((t >> 8) & 3) * 4 + (t & 3));
+      const int64_t blk = t >> 10;
+      const int kb = (int)(blk % KB), rb = (int)(blk / KB);
+      const int row = rb * 32 + (lane & 31), col = kb * 32 + kperm(s, lane >> 5);
+      if (row < rows && col < cols) ps.j0 = src + (int64_t)row * cols + col;
+      hit = true;
+    }
+  };
+  // bias images: [rb][h][s] -> b[32 rb + kperm(s, h)]
+  auto bimg = [&](int64_t off, int rows, int64_t src, int64_t src2) {
+    const int64_t sz = (int64_t)((rows + 31) / 32) * 32;
+    if (r >= off && r < off + sz) {
+      const int64_t t = r - off;
+      const int s = (int)(t & 15), h = (int)((t >> 4) & 1), rb = (int)(t >> 5);
+      const int row = rb * 32 + kperm(s, h);
+      if (row < rows) {
+        ps.j0 = src + row;
+        ps.j1 = src2 >= 0 ? src2 + row : -1;
+        ps.bias = true;
+      }
+      hit = true;
+    }
+  };
+  wimg(g.off_l1, g.KD, F1, D, o.W1 + (int64_t)agent * F1 * D);
+  if (!hit) wimg(g.off_l2, F1 / 32, G, F1, o.W2 + (int64_t)agent * G * F1);
+  if (!hit) wimg(g.off_ih, G / 32, 3 * H, G, o.Wih + (int64_t)agent * 3 * H * G);
+  if (!hit) wimg(g.off_hh, H / 32, 3 * H, H, o.Whh + (int64_t)agent * 3 * H * H);
+  if (!hit) wimg(g.off_q, H / 32, A, H, o.Wq + (int64_t)agent * A * H);
+  if (!hit) bimg(g.off_b1, F1, o.b1 + (int64_t)agent * F1, -1);
+  if (!hit) bimg(g.off_b2, G, o.b2 + (int64_t)agent * G, -1);
+  if (!hit) bimg(g.off_brz, 2 * H, o.bih + (int64_t)agent * 3 * H, o.bhh + (int64_t)agent * 3 * H);
+  if (!hit) bimg(g.off_bin, H, o.bih + (int64_t)agent * 3 * H + 2 * H, -1);
+  if (!hit) bimg(g.off_bhn, H, o.bhh + (int64_t)agent * 3 * H + 2 * H, -1);
+  if (!hit) bimg(g.off_bq, A, o.bq + (int64_t)agent * A, -1);
+  return ps;
+}
+__device__ __forceinline__ float qnet_pack_value(const PackSrc& ps, float v0, float v1) {
+  if (ps.j0 < 0) return 0.0f;
+  return ps.bias ? v0 + (ps.j1 >= 0 ? v1 : 0.0f) : v0;
+}
+
 // One thread per packed element: gathers the canonical flat parameters into
 // the per-lane MFMA fragment image (zero padding outside the real shape).
 __device__ __forceinline__ void qnet_pack_body(const float* __restrict__ params, float* __restrict__ packed, QnetGeo g,
@@ -2636,46 +2694,10 @@ __device__ __forceinline__ void qnet_pack_body(const float* __restrict__ params,
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)nblk * blockDim.x) {
     const int agent = (int)(idx / per_agent);
-    int64_t r = idx % per_agent;
-    float v = 0.0f;
-    // weight images: [rb][kb][q][lane][s & 3] (see load_frag)
-    auto wimg = [&](int64_t off, int KB, int rows, int cols, int64_t src, int64_t& rr, bool& hit) {
-      const int64_t sz = (int64_t)((rows + 31) / 32) * KB * 1024;
-      if (rr >= off && rr < off + sz) {
-        const int64_t t = rr - off;
-        // [rb][kb][q][lane][s&3]
-        const int lane = (int)((t >> 2) & 63), s = (int)(((t >> 8) & 3) * 4 + (t & 3));
-        const int64_t blk = t >> 10;
-        const int kb = (int)(blk % KB), rb = (int)(blk / KB);
-        const int row = rb * 32 + (lane & 31), col = kb * 32 + kperm(s, lane >> 5);
-        if (row < rows && col < cols) v = params[src + (int64_t)row * cols + col];
-        hit = true;
-      }
-    };
-    // bias images: [rb][h][s] -> b[32 rb + kperm(s, h)]
-    auto bimg = [&](int64_t off, int rows, int64_t src, int64_t src2, int64_t& rr, bool& hit) {
-      const int64_t sz = (int64_t)((rows + 31) / 32) * 32;
-      if (rr >= off && rr < off + sz) {
-        const int64_t t = rr - off;
-        const int s = (int)(t & 15), h = (int)((t >> 4) & 1), rb = (int)(t >> 5);
-        const int row = rb * 32 + kperm(s, h);
-        if (row < rows) v = params[src + row] + (src2 >= 0 ? params[src2 + row] : 0.0f);
-        hit = true;
-      }
-    };
-    bool hit = false;
-    wimg(g.off_l1, g.KD, F1, D, o.W1 + (int64_t)agent * F1 * D, r, hit);
-    if (!hit) wimg(g.off_l2, F1 / 32, G, F1, o.W2 + (int64_t)agent * G * F1, r, hit);
-    if (!hit) wimg(g.off_ih, G / 32, 3 * H, G, o.Wih + (int64_t)agent * 3 * H * G, r, hit);
-    if (!hit) wimg(g.off_hh, H / 32, 3 * H, H, o.Whh + (int64_t)agent * 3 * H * H, r, hit);
-    if (!hit) wimg(g.off_q, H / 32, A, H, o.Wq + (int64_t)agent * A * H, r, hit);
-    if (!hit) bimg(g.off_b1, F1, o.b1 + (int64_t)agent * F1, -1, r, hit);
-    if (!hit) bimg(g.off_b2, G, o.b2 + (int64_t)agent * G, -1, r, hit);
-    if (!hit) bimg(g.off_brz, 2 * H, o.bih + (int64_t)agent * 3 * H, o.bhh + (int64_t)agent * 3 * H, r, hit);
-    if (!hit) bimg(g.off_bin, H, o.bih + (int64_t)agent * 3 * H + 2 * H, -1, r, hit);
-    if (!hit) bimg(g.off_bhn, H, o.bhh + (int64_t)agent * 3 * H + 2 * H, -1, r, hit);
-    if (!hit) bimg(g.off_bq, A, o.bq + (int64_t)agent * A, -1, r, hit);
-    packed[idx] = v;
+    const PackSrc ps = qnet_pack_src(g, agent, idx % per_agent, D, F1, G, H, A, o);
+    const float v0 = ps.j0 >= 0 ? params[ps.j0] : 0.0f;
+    const float v1 = ps.j1 >= 0 ? params[ps.j1] : 0.0f;
+    packed[idx] = qnet_pack_value(ps, v0, v1);
   }
 }
 

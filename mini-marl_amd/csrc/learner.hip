@@ -18,6 +18,7 @@
 #pragma clang fp contract(off)
 #include "common.h"
 #include "minimarl.h"
+#include "per_small.h"
 
 namespace mm {
 
@@ -32,24 +33,41 @@ __device__ __forceinline__ int64_t state_off(const int64_t* s_off, int64_t i, in
 //   s_off[t][b]  = element offset of s_t in store.obs  (-1 => the env's reset obs)
 //   s2_off[t][b] = element offset of s'_t
 //   acts[t][b][i] (int32), rew[t][b][i] (f32), done[t][b] (f32), done8[t][b] (u8)
-__global__ void lrn_gather_kernel(int B, int C, int N, int64_t row_stride, int64_t nd, const int64_t* slots,
-                                  const int64_t* slot_row, const uint8_t* s_done, const uint8_t* s_act,
-                                  const float* s_rew, int64_t* s_off, int64_t* s2_off, int32_t* acts, float* rew,
-                                  float* done, uint8_t* done8) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * C) return;
-  const int b = i % B, t = i / B;
-  const int64_t row = slot_row[slots[b]];
-  const uint8_t dprev = t > 0 ? s_done[row * C + t - 1] : 0;
-  s_off[i] = (t > 0 && dprev) ? -1 : row * row_stride + (int64_t)t * nd;
-  s2_off[i] = row * row_stride + (int64_t)(t + 1) * nd;
-  const uint8_t dn = s_done[row * C + t];
-  done[i] = dn ? 1.0f : 0.0f;
-  done8[i] = dn;
+// The learner's chunk-store gather of the sampled slots (lrn_gather_kernel): row i = (t, b) of the [C][B] batch from chunk-store row
+// slot_row[slots[b]] — state offsets (s_t: -1 after an earlier done in the chunk, i.e. the reset obs; s'_t), the
+// agents' actions and rewards, the done flag (f32 and u8). qmix/replay_buffer/per.py:61-81 (Replay_buffer.sample
+// over chunk lists), vdn/replay_buffer/buffer.py:58-70.
+struct SampleGather {
+  int C, N;
+  int64_t row_stride, nd;
+  const int64_t* slot_row;
+  const uint8_t* s_done;
+  const uint8_t* s_act;
+  const float* s_rew;
+  int64_t *s_off, *s2_off;
+  int32_t* acts;
+  float *rew, *done;
+  uint8_t* done8;
+};
+// row: the chunk-store row of sample b = i % B
+__device__ __forceinline__ void sample_gather_row(const SampleGather& g, int B, int64_t row, int i) {
+  const int C = g.C, N = g.N;
+  const int t = i / B;
+  const uint8_t dprev = t > 0 ? g.s_done[row * C + t - 1] : 0;
+  g.s_off[i] = (t > 0 && dprev) ? -1 : row * g.row_stride + (int64_t)t * g.nd;
+  g.s2_off[i] = row * g.row_stride + (int64_t)(t + 1) * g.nd;
+  const uint8_t dn = g.s_done[row * C + t];
+  g.done[i] = dn ? 1.0f : 0.0f;
+  g.done8[i] = dn;
   for (int k = 0; k < N; ++k) {
-    acts[(int64_t)i * N + k] = s_act[(row * C + t) * N + k];
-    rew[(int64_t)i * N + k] = s_rew[(row * C + t) * N + k];
+    g.acts[(int64_t)i * N + k] = g.s_act[(row * C + t) * N + k];
+    g.rew[(int64_t)i * N + k] = g.s_rew[(row * C + t) * N + k];
   }
+}
+
+__global__ void lrn_gather_kernel(SampleGather g, int B, const int64_t* slots) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B * g.C) sample_gather_row(g, B, g.slot_row[slots[i % B]], i);
 }
 
 // ------------------------------------------------------------------ block helpers
@@ -863,27 +881,34 @@ __global__ __launch_bounds__(256) void lrn_loss_reduce_kernel(int B, int C, cons
 // Small batches (B * C <= 1024, B <= 256): the loss terms and the per-step in-order reduction in ONE
 // workgroup (the parts go through global memory inside the block: same values, same summation order as
 // lrn_loss_kernel + lrn_loss_reduce_kernel, one launch fewer per update).
-__global__ __launch_bounds__(1024) void lrn_loss_small_kernel(int B, int C, int N, float gamma, const float* rew,
-                                                              const float* done, const float* isw, const float* qtot,
-                                                              const float* qtot_t, int flags, const float* qa,
-                                                              const float* maxq, float* dq, float* dqa,
-                                                              float* loss_parts, float* td_last, float* loss) {
+struct LossArgs {
+  int B, C, N;
+  float gamma;
+  const float *rew, *done, *isw, *qtot, *qtot_t;
+  int flags;
+  const float *qa, *maxq;
+  float *dq, *dqa, *loss_parts, *td_last, *loss;
+};
+// one block, any size (B <= 256, C <= 256, B * C rows grid-strided over the block)
+__device__ __forceinline__ void lrn_loss_small_body(const LossArgs& a) {
   __shared__ float sh[256];
-  const int i = threadIdx.x;
-  if (i < B * C) lrn_loss_elem(i, B, C, N, gamma, rew, done, isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts, td_last);
+  for (int i = threadIdx.x; i < a.B * a.C; i += blockDim.x)
+    lrn_loss_elem(i, a.B, a.C, a.N, a.gamma, a.rew, a.done, a.isw, a.qtot, a.qtot_t, a.flags, a.qa, a.maxq, a.dq,
+                  a.dqa, a.loss_parts, a.td_last);
   __syncthreads();
-  for (int t = threadIdx.x; t < C; t += blockDim.x) {
+  for (int t = threadIdx.x; t < a.C; t += blockDim.x) {
     float sacc = 0.f;
-    for (int b = 0; b < B; ++b) sacc += loss_parts[(int64_t)t * B + b];
+    for (int b = 0; b < a.B; ++b) sacc += a.loss_parts[(int64_t)t * a.B + b];
     sh[t] = sacc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     float tot = 0.f;
-    for (int t = 0; t < C; ++t) tot += sh[t] / (float)B;
-    *loss = tot;
+    for (int t = 0; t < a.C; ++t) tot += sh[t] / (float)a.B;
+    *a.loss = tot;
   }
 }
+__global__ __launch_bounds__(1024) void lrn_loss_small_kernel(LossArgs a) { lrn_loss_small_body(a); }
 
 // ------------------------------------------------------------------ mixer backward (one step)
 struct MixBwdArgs {
@@ -1579,7 +1604,16 @@ __host__ __device__ inline size_t mix_hyper_fwd_floats(int Hm, int K1, int N) {
 // all R = C*B rows at once (flat row arrays: save [R][MSD], qa [R][N], dq [R], dqa [R][N],
 // delta [R][MDD]): mixer_bwd_body's hypernet deltas + dqa, and X_j = W_j^T d_j (j = w1, b1, w2, b2a)
 // stored apart in xws [R][4][Hm] (the serial kernel adds them to the future gradient in order).
-__global__ __launch_bounds__(256) void mixer_hyper_bwd_kernel(MixBwdArgs a, int R, float* xws, uint64_t* trace) {
+// PER: one more block (the last) runs the small priority update (its inputs, the loss's TDs, are final here)
+template <bool PER>
+__global__ __launch_bounds__(256) void mixer_hyper_bwd_kernel(MixBwdArgs a, int R, float* xws, uint64_t* trace,
+                                                              PerUpd pu) {
+  if constexpr (PER) {
+    if ((int)blockIdx.x == (int)gridDim.x - 1) {
+      per_update_small_block(pu);
+      return;
+    }
+  }
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int Q = MIX_SPB;
   const int Hm = a.Hm, K1 = a.K1, N = a.N, NK = N * K1, SH = NK + 3 * K1;
@@ -1780,9 +1814,12 @@ static int mix_seq_lds_setup() {
                                    (int)kMixSeqLds));
   const void* serial[] = {(const void*)mixer_rec_fwd_kernel<32>, (const void*)mixer_rec_fwd_kernel<64>,
                           (const void*)mixer_rec_bwd_kernel<32>, (const void*)mixer_rec_bwd_kernel<64>,
-                          (const void*)mixer_hyper_bwd_kernel};
+                          (const void*)mixer_hyper_bwd_kernel<false>};
   for (const void* k : serial)
     MM_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMixSeqLds));
+  // (the PER block's static LDS comes off the dynamic limit)
+  MM_HIP_CHECK(hipFuncSetAttribute((const void*)mixer_hyper_bwd_kernel<true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMixSeqLds - kPerSmallLds)));
   done = true;
   return MM_OK;
 }
@@ -2548,59 +2585,82 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* G, int64_t n, f
 // torch.optim.Adam (no amsgrad / weight decay) with clip_grad_norm_ applied to G[0:n_clip]
 // With partials2 != null a second clip group [n_clip, n) uses its own norm (partials2) and coefficient
 // (qmix/qmix.py:235-238 clips the agent net and the mixer separately).
-__global__ __launch_bounds__(256) void adam_kernel(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip,
-                                                   const float* partials, int n_part, float max_norm, float lr,
-                                                   float b1, float b2, float eps, const float* step, float* norm_out,
-                                                   float grad_scale, const float* partials2) {
-  __shared__ float s_coef, s_coef2;
+struct AdamArgs {
+  float *P, *G, *m, *v;
+  int64_t n, n_clip;
+  const float* partials;   // [n_part] sumsq partials of G[0:n_clip] (sumsq_kernel)
+  int n_part;              // <= 256
+  float max_norm, lr, b1, b2, eps;
+  const float* step;
+  float* norm_out;
+  float grad_scale;
+  const float* partials2;  // second clip group [n_clip, n) or nullptr
+};
+// per-launch Adam constants of the block: clip coefficients of both groups from the sumsq partials (threads 0-255:
+// one partial each, a fixed-order tree — the same sums whatever the block size) and the bias corrections
+struct AdamConst {
+  float coef, coef2, step_size, bc2s;
+};
+__device__ __forceinline__ AdamConst adam_const(const AdamArgs& a) {
+  __shared__ float s_coef[2];
   __shared__ float red[2][256];
-  // sum the sumsq partials with the whole block (one load per thread, fixed-order tree), not one
-  // thread's sequential loop (one memory round trip per few partials)
-  {
+  const int tid = (int)threadIdx.x;
+  if (tid < 256) {
     float p1 = 0.f, p2 = 0.f;
-    for (int i = threadIdx.x; i < n_part; i += blockDim.x) {
-      p1 += partials[i];
-      if (partials2) p2 += partials2[i];
+    for (int i = tid; i < a.n_part; i += 256) {
+      p1 += a.partials[i];
+      if (a.partials2) p2 += a.partials2[i];
     }
-    red[0][threadIdx.x] = p1;
-    red[1][threadIdx.x] = p2;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-      if ((int)threadIdx.x < st) {
-        red[0][threadIdx.x] += red[0][threadIdx.x + st];
-        red[1][threadIdx.x] += red[1][threadIdx.x + st];
-      }
-      __syncthreads();
-    }
+    red[0][tid] = p1;
+    red[1][tid] = p2;
   }
-  if (threadIdx.x == 0) {
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) {
+      red[0][tid] += red[0][tid + st];
+      red[1][tid] += red[1][tid + st];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
     const float tot = red[0][0], tot2 = red[1][0];
-    const float norm = sqrtf(tot) * grad_scale;
-    const float norm2 = sqrtf(tot2) * grad_scale;
-    s_coef = max_norm > 0.f ? fminf(1.0f, max_norm / (norm + 1e-6f)) : 1.0f;
-    s_coef2 = (partials2 && max_norm > 0.f) ? fminf(1.0f, max_norm / (norm2 + 1e-6f)) : 1.0f;
-    if (norm_out && blockIdx.x == 0) {
-      norm_out[0] = norm;
-      if (partials2) norm_out[1] = norm2;
+    const float norm = sqrtf(tot) * a.grad_scale;
+    const float norm2 = sqrtf(tot2) * a.grad_scale;
+    s_coef[0] = a.max_norm > 0.f ? fminf(1.0f, a.max_norm / (norm + 1e-6f)) : 1.0f;
+    s_coef[1] = (a.partials2 && a.max_norm > 0.f) ? fminf(1.0f, a.max_norm / (norm2 + 1e-6f)) : 1.0f;
+    if (a.norm_out && blockIdx.x == 0) {
+      a.norm_out[0] = norm;
+      if (a.partials2) a.norm_out[1] = norm2;
     }
   }
   __syncthreads();
-  const float coef = s_coef, coef2 = s_coef2;
-  const float t = *step;
-  const float bc1 = 1.0f - powf(b1, t);
-  const float bc2 = 1.0f - powf(b2, t);
-  const float step_size = lr / bc1;
-  const float bc2s = sqrtf(bc2);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float g = G[i] * grad_scale;
-    g *= i < n_clip ? coef : coef2;
-    const float mi = m[i] + (g - m[i]) * (1.0f - b1);
-    const float vi = v[i] * b2 + g * g * (1.0f - b2);
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    P[i] = P[i] - step_size * (mi / denom);
-  }
+  AdamConst c;
+  c.coef = s_coef[0];
+  c.coef2 = s_coef[1];
+  const float t = *a.step;
+  const float bc1 = 1.0f - powf(a.b1, t);
+  const float bc2 = 1.0f - powf(a.b2, t);
+  c.step_size = a.lr / bc1;
+  c.bc2s = sqrtf(bc2);
+  return c;
+}
+// one parameter's Adam step; returns the new value
+__device__ __forceinline__ float adam_elem(const AdamArgs& a, const AdamConst& c, int64_t i) {
+  float g = a.G[i] * a.grad_scale;
+  g *= i < a.n_clip ? c.coef : c.coef2;
+  const float mi = a.m[i] + (g - a.m[i]) * (1.0f - a.b1);
+  const float vi = a.v[i] * a.b2 + g * g * (1.0f - a.b2);
+  a.m[i] = mi;
+  a.v[i] = vi;
+  const float denom = sqrtf(vi) / c.bc2s + a.eps;
+  const float p = a.P[i] - c.step_size * (mi / denom);
+  a.P[i] = p;
+  return p;
+}
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  const AdamConst c = adam_const(a);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x)
+    adam_elem(a, c, i);
 }
 
 }  // namespace mm
@@ -2622,8 +2682,9 @@ int mm_lrn_gather(int32_t B, int32_t C, int32_t N, int64_t row_stride, int64_t n
                   mm_stream_t s) {
   MM_REQUIRE(B > 0 && C > 0 && N > 0, "lrn_gather: bad dims");
   const int n = B * C;
-  hipLaunchKernelGGL(mm::lrn_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, B, C, N,
-                     row_stride, nd, slots, slot_row, s_done, s_act, s_rew, s_off, s2_off, acts, rew, done, done8);
+  const mm::SampleGather g = {C, N, row_stride, nd, slot_row, s_done, s_act, s_rew, s_off, s2_off, acts, rew, done,
+                              done8};
+  hipLaunchKernelGGL(mm::lrn_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)s, g, B, slots);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -2722,8 +2783,9 @@ int mm_lrn_loss_ex(int32_t B, int32_t C, int32_t N, float gamma, const float* re
   MM_REQUIRE((flags & MM_LOSS_TARGET_SUM) || isw, "lrn_loss: isw required");
   const int n = B * C;
   if (n <= 1024 && B <= 256 && C <= 256) {
-    hipLaunchKernelGGL(mm::lrn_loss_small_kernel, dim3(1), dim3(1024), 0, (hipStream_t)s, B, C, N, gamma, rew, done,
-                       isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts, td_last, loss);
+    const mm::LossArgs a = {B, C, N, gamma, rew, done, isw, qtot, qtot_t, flags, qa, maxq, dq, dqa, loss_parts,
+                            td_last, loss};
+    hipLaunchKernelGGL(mm::lrn_loss_small_kernel, dim3(1), dim3(1024), 0, (hipStream_t)s, a);
     MM_HIP_CHECK(hipGetLastError());
     return MM_OK;
   }
@@ -2769,9 +2831,11 @@ static bool mix_bwd_split_ok(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_
 }
 
 // part 0: the whole backward; 1: the hypernet pass only (dq -> dqa, dhm, delta); 2: the recurrence only
+// pu (part 1, may be null): the PER priority update as one more block of the hypernet launch
 static int mixer_bwd_seq_part(int part, int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P,
                               const float* save, const float* qa, const float* dq, const float* done, const float* ones,
-                              float* dhm, float* dqa, float* delta, float* ws, int32_t steps, mm_stream_t s) {
+                              float* dhm, float* dqa, float* delta, float* ws, int32_t steps, mm_stream_t s,
+                              const mm::PerUpd* pu = nullptr) {
   MM_REQUIRE(P && save && qa && dq && done && ones && dhm && dqa && delta && steps >= 1, "mixer_bwd_seq: bad args");
   MM_REQUIRE(part == 0 || mix_bwd_split_ok(B, N, S, Hm, K1, P, ws, steps),
              "mixer_bwd_seq: the hypernet / recurrence parts need the split path (mm_mixer_seq_split)");
@@ -2802,9 +2866,15 @@ static int mixer_bwd_seq_part(int part, int32_t B, int32_t N, int32_t S, int32_t
     if (rc) return rc;
     const int R = B * steps;
     if (part != 2) {
-      hipLaunchKernelGGL(mm::mixer_hyper_bwd_kernel, dim3((R + mm::MIX_SPB - 1) / mm::MIX_SPB), dim3(256),
-                         mm::mix_hyper_bwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R, ws,
-                         mm::debug_trace_buffer("MM_HYB_TRACE"));
+      const int nbh = (R + mm::MIX_SPB - 1) / mm::MIX_SPB;
+      if (pu)
+        hipLaunchKernelGGL(mm::mixer_hyper_bwd_kernel<true>, dim3(nbh + 1), dim3(256),
+                           mm::mix_hyper_bwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R, ws,
+                           mm::debug_trace_buffer("MM_HYB_TRACE"), *pu);
+      else
+        hipLaunchKernelGGL(mm::mixer_hyper_bwd_kernel<false>, dim3(nbh), dim3(256),
+                           mm::mix_hyper_bwd_floats(Hm, K1, N) * 4, (hipStream_t)s, a, R, ws,
+                           mm::debug_trace_buffer("MM_HYB_TRACE"), mm::PerUpd{});
       MM_HIP_CHECK(hipGetLastError());
     }
     if (part == 1) return MM_OK;
@@ -3274,8 +3344,9 @@ int mm_clip_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t n_cl
   hipLaunchKernelGGL(mm::sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, G, n_clip, partials, step);
   MM_HIP_CHECK(hipGetLastError());
   const int nb2 = (int)std::min<int64_t>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(mm::adam_kernel, dim3(nb2), dim3(256), 0, (hipStream_t)s, P, G, m, v, n, n_clip, partials, nb,
-                     max_norm, lr, beta1, beta2, eps, step, norm_out, grad_scale, (const float*)nullptr);
+  const mm::AdamArgs a = {P, G, m, v, n, n_clip, partials, nb, max_norm, lr, beta1, beta2, eps, step, norm_out,
+                          grad_scale, nullptr};
+  hipLaunchKernelGGL(mm::adam_kernel, dim3(nb2), dim3(256), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -3294,8 +3365,9 @@ int mm_clip2_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t spl
                      (float*)nullptr);
   MM_HIP_CHECK(hipGetLastError());
   const int nb2 = (int)std::min<int64_t>((n + 255) / 256, 2048);
-  hipLaunchKernelGGL(mm::adam_kernel, dim3(nb2), dim3(256), 0, (hipStream_t)s, P, G, m, v, n, split, partials, nb,
-                     max_norm, lr, beta1, beta2, eps, step, norm_out, grad_scale, (const float*)(partials + nb));
+  const mm::AdamArgs a = {P, G, m, v, n, split, partials, nb, max_norm, lr, beta1, beta2, eps, step, norm_out,
+                          grad_scale, partials + nb};
+  hipLaunchKernelGGL(mm::adam_kernel, dim3(nb2), dim3(256), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

@@ -6,11 +6,16 @@
 //                            W_ih x2 of every (t, b) row, both nets)
 //   mm_agent_mixer_rec_seq = mm_mixer_fwd_seq_rec (the Mix_Net GRU over the state) || mm_agent_q_rec_seq2 (the
 //                            agent GRU + Q head over the C steps, both nets)
+//   mm_clip_adam_pack      = mm_clip_adam + mm_qnet_pack_f32 of the behavior net (+ mm_per_update): the Adam step
+//                            writes the exact-f32 image from the new values (one more block: the priorities)
+//   mm_mixer_bwd_seq_hyper_per = mm_mixer_bwd_seq_hyper + mm_per_update (one more block of the hypernet pass)
 // (Train_dqn.train's forward over the chunk, qmix/_train.py:55-77: Q_Net per step, then Mix_Net per step; the
-// Mix_Net's GRU depends on the state only, so it runs beside the agent chain.) Each block runs the same body as the
-// separate kernel, so the results are bit-identical to the two launches (test_paired_fwd_launches_bit_identical).
+// Mix_Net's GRU depends on the state only, so it runs beside the agent chain; the step / priority update,
+// qmix/_train.py:86-96 and main.py:240-244.) Each block runs the same body as the separate kernel, so the results
+// are bit-identical to the separate launches (test_paired_fwd_launches_bit_identical, test_clip_adam_pack_*).
 #include "agent_fwd.hip"
 #include "learner.hip"
+#include "per.hip"
 
 namespace mm {
 
@@ -83,9 +88,88 @@ static bool rec_pair_ok(const mm_qnet_dims* d, int32_t B, int32_t N, int32_t Hm,
          rec_pair_lds(Hm, steps) <= 160 * 1024;
 }
 
+// Blocks [0, nA): image elements (grid-stride): the Adam step of the element's parameter(s), the image element
+// from the new values (qnet_pack_value: what qnet_pack_kernel writes after adam_kernel); blocks [nA, nA + nB): the
+// Adam step of the parameters outside the agent image ([n_agent, n): the mixer's); block nA + nB (when pu.tree):
+// per_update_small_block. Every parameter's step runs exactly once (qnet_pack_src: each agent parameter lies in one
+// image element). (A parameter-centric order — coalesced Adam, each image element written through the inverse
+// mapping — measured 16.0 vs 13.2 us at the B = 32 shapes.)
+__global__ __launch_bounds__(1024) void adam_pack_kernel(AdamArgs a, float* packed, QnetGeo g, int N, int D, int F1,
+                                                         int G, int H, int A, QnetOffsets o, int nA, int nB, PerUpd pu) {
+  const int bid = (int)blockIdx.x;
+  if (bid >= nA + nB) {
+    per_update_small_block(pu);
+    return;
+  }
+  const AdamConst c = adam_const(a);
+  if (bid < nA) {
+    const int64_t per_agent = g.agent_stride, total = per_agent * N;
+    for (int64_t idx = bid * 1024ll + threadIdx.x; idx < total; idx += (int64_t)nA * 1024) {
+      const PackSrc ps = qnet_pack_src(g, (int)(idx / per_agent), idx % per_agent, D, F1, G, H, A, o);
+      const float v0 = ps.j0 >= 0 ? adam_elem(a, c, ps.j0) : 0.0f;
+      const float v1 = ps.j1 >= 0 ? adam_elem(a, c, ps.j1) : 0.0f;
+      packed[idx] = qnet_pack_value(ps, v0, v1);
+    }
+  } else {
+    for (int64_t i = o.total + (int64_t)(bid - nA) * 1024 + threadIdx.x; i < a.n; i += (int64_t)nB * 1024)
+      adam_elem(a, c, i);
+  }
+}
+
 }  // namespace mm
 
 extern "C" {
+
+int mm_mixer_bwd_seq_hyper_per(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const float* P,
+                               const float* save, const float* qa, const float* dq, const float* done,
+                               const float* ones, float* dhm, float* dqa, float* delta, float* ws, int32_t steps,
+                               mm_per* per, const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s) {
+  MM_REQUIRE(per && nodes && td, "mixer_bwd_seq_hyper_per: null PER argument");
+  const bool small = (per->cap & (per->cap - 1)) == 0 && batch >= 1 && batch <= mm::PU_B &&
+                     mm::mix_hyper_bwd_floats(Hm, K1, N) * 4 + mm::kPerSmallLds <= mm::kMixSeqLds;
+  if (small) {
+    const mm::PerUpd pu = {per->tree, per->cap, nodes, td, per->st, batch, (float)per->eps};
+    return mixer_bwd_seq_part(1, B, N, S, Hm, K1, P, save, qa, dq, done, ones, dhm, dqa, delta, ws, steps, s, &pu);
+  }
+  const int rc = mixer_bwd_seq_part(1, B, N, S, Hm, K1, P, save, qa, dq, done, ones, dhm, dqa, delta, ws, steps, s);
+  if (rc) return rc;
+  return mm_per_update(per, nodes, td, batch, s);
+}
+
+int mm_clip_adam_pack(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip, int32_t two_groups,
+                      float max_norm, float lr, float beta1, float beta2, float eps, float* step, float* partials,
+                      float* norm_out, float grad_scale, const mm_qnet_dims* d, float* packed, mm_per* per,
+                      const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s) {
+  MM_REQUIRE(P && G && m && v && step && partials && packed && d && n > 0 && n_clip >= 0 && n_clip <= n,
+             "clip_adam_pack: bad args");
+  mm::QnetGeo g;
+  mm::QnetOffsets o;
+  int rc = mm::qnet_geometry(d, &g, &o);
+  if (rc) return rc;
+  MM_REQUIRE(o.total <= n, "clip_adam_pack: the agent net (%lld params) must lead P (%lld)", (long long)o.total,
+             (long long)n);
+  const int nb = 256;
+  hipLaunchKernelGGL(mm::sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, G, n_clip, partials, step);
+  MM_HIP_CHECK(hipGetLastError());
+  if (two_groups) {
+    hipLaunchKernelGGL(mm::sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)s, G + n_clip, n - n_clip,
+                       partials + nb, (float*)nullptr);
+    MM_HIP_CHECK(hipGetLastError());
+  }
+  const mm::AdamArgs a = {P, G, m, v, n, n_clip, partials, nb, max_norm, lr, beta1, beta2, eps, step, norm_out,
+                          grad_scale, two_groups ? partials + nb : nullptr};
+  const int64_t total = g.agent_stride * d->n_agents;
+  const int nA = (int)std::min<int64_t>((total + 1023) / 1024, 1024);
+  const int nB = (int)std::min<int64_t>((n - o.total + 1023) / 1024, 512);
+  mm::PerUpd pu = {};
+  const bool per_block = per && nodes && td && (per->cap & (per->cap - 1)) == 0 && batch >= 1 && batch <= mm::PU_B;
+  if (per_block) pu = {per->tree, per->cap, nodes, td, per->st, batch, (float)per->eps};
+  hipLaunchKernelGGL(mm::adam_pack_kernel, dim3(nA + nB + (per_block ? 1 : 0)), dim3(1024), 0, (hipStream_t)s, a,
+                     packed, g, d->n_agents, d->obs_dim, d->f1, d->g, d->h, d->n_actions, o, nA, nB, pu);
+  MM_HIP_CHECK(hipGetLastError());
+  if (per && !per_block) return mm_per_update(per, nodes, td, batch, s);
+  return MM_OK;
+}
 
 int mm_agent_mixer_pair_supported(const mm_qnet_dims* d, int32_t B, int32_t steps, int32_t N, int32_t S, int32_t Hm,
                                   int32_t K1) {

@@ -256,6 +256,9 @@ _SIGS += [
     ("mm_tmv", c_i32, [ctypes.POINTER(TmvArgs), c_vp]),
     ("mm_clip_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
                              c_vp, c_f32, c_vp]),
+    ("mm_clip_adam_pack", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32, c_f32,
+                                  c_vp, c_vp, c_vp, c_f32, ctypes.POINTER(QnetDims), c_vp, c_vp, c_vp, c_vp, c_i32,
+                                  c_vp]),
     ("mm_clip2_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
                               c_vp, c_f32, c_vp]),
     ("mm_per_sample_uniform", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),
@@ -274,6 +277,8 @@ _SIGS += [
                                        c_vp, c_vp]),
     ("mm_mixer_bwd_seq_hyper", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                        c_vp, c_vp, c_vp, c_i32, c_vp]),
+    ("mm_mixer_bwd_seq_hyper_per", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp]),
     ("mm_mixer_bwd_seq_rec", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                      c_vp, c_vp, c_vp, c_i32, c_vp]),
     ("mm_mixer_seq_split", c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32]),

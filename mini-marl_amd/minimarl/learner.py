@@ -125,6 +125,8 @@ class QLearner:
         # the shapes allow: no fork / join at all (pair_fwd=False: the side stream above)
         self._pair_fwd = bool(pair_fwd)
         self._pair_ok = None
+        self._per_next = None          # the PER of the update being recorded (sample_and_grads -> compute_grads)
+        self._per_done = False         # its priority update already issued (with the hypernet backward)
         self.fast_pre = False           # opt-in: the fp16x3 agent PRE (not at the fp32 gradient bar, see compute_grads)
         if not self.reference_compat:
             self.loss_flags |= MM_LOSS_TARGET_SUM
@@ -437,13 +439,21 @@ class QLearner:
                 if split:
                     # the hypernet pass (-> dqa for the agents), then the mixer recurrence's backward beside the
                     # agent BPTT: one shared launch below (mm_agent_mixer_bwd_seq), or the side stream joined
-                    # before the weight gradients
-                    check(L.mm_mixer_bwd_seq_hyper(*margs, s), "mixer bwd seq (hypernets)")
+                    # before the weight gradients. A sampled update's priority update rides along (the loss's TDs
+                    # are final): one more block of the hypernet launch
+                    if self._per_next is not None:
+                        check(L.mm_mixer_bwd_seq_hyper_per(*margs, self._per_next._h, ptr(self.nodes),
+                                                           ptr(self.td_last), self.B, s),
+                              "mixer bwd seq (hypernets) + priority update")
+                        self._per_done = True
+                    else:
+                        check(L.mm_mixer_bwd_seq_hyper(*margs, s), "mixer bwd seq (hypernets)")
                     if not pair_bwd:
                         side.wait_stream(torch.cuda.current_stream(self.dev))
                         check(L.mm_mixer_bwd_seq_rec(*margs, s_m), "mixer bwd seq (recurrence)")
                 else:
                     check(L.mm_mixer_bwd_seq(*margs, s), "mixer bwd seq")
+        self._per_next = None
         if pair_bwd:
             # the agent BPTT chain and the mixer recurrence's backward sharing one grid
             mx = self.mix
@@ -588,10 +598,25 @@ class QLearner:
                     n.save = sv.data_ptr() if sv is not None else None
                 check(L.mm_mixer_fwd(B, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, nets, 2, s), "mixer fwd")
 
-    def apply_grads(self, grad_scale=1.0):
+    def apply_grads(self, grad_scale=1.0, per=None):
         """clip_grad_norm_ + Adam (grads scaled first, e.g. 1/world after an all-reduce), then repack
-        the behavior fragments for the next forward."""
+        the behavior fragments for the next forward; with ``per`` also the priority update of the sampled
+        chunks. Returns True when that update was issued here."""
         s = stream_handle(self.dev)
+        if not self._uses_h3():
+            # one launch after the norm's partial sums: the Adam step writes the exact-f32 image from the new values
+            # (no pack launch) and one more block updates the priorities (mm_clip_adam_pack)
+            two = self.mode == "qmix_min"   # clip agent net and mixer separately (qmix/qmix.py:235-238)
+            check(lib().mm_clip_adam_pack(ptr(self.P), ptr(self.Gr), ptr(self.m), ptr(self.v), self.n,
+                                          self.n_agent if two else self.n_clip, int(two), self.clip, self.lr, self.b1,
+                                          self.b2, self.aeps, ptr(self.step_dev), ptr(self.partials), ptr(self.norm),
+                                          float(grad_scale), ctypes.byref(self.beh.dims), ptr(self.beh.packed),
+                                          per._h if per is not None else None,
+                                          ptr(self.nodes) if per is not None else None,
+                                          ptr(self.td_last) if per is not None else None, self.B, s), "clip_adam_pack")
+            self.beh.mark_h3_stale()       # the exact-f32 image is current, the fp16x3 image is not
+            self.updates += 1
+            return per is not None
         if self.mode == "qmix_min":   # clip agent net and mixer separately (qmix/qmix.py:235-238)
             check(lib().mm_clip2_adam(ptr(self.P), ptr(self.Gr), ptr(self.m), ptr(self.v), self.n, self.n_agent,
                                       self.clip, self.lr, self.b1, self.b2, self.aeps, ptr(self.step_dev),
@@ -603,6 +628,7 @@ class QLearner:
         self.beh.mark_dirty()
         self._pack(self.beh, s)
         self.updates += 1
+        return False
 
     def _uses_h3(self):
         """Whether this learner's own forward reads the fp16x3 image (the opt-in fast PRE)."""
@@ -707,6 +733,7 @@ class QLearner:
             check(L.mm_per_sample_rng(per._h, self.B, seed, counter, ptr(self.nodes), ptr(self.slots),
                                       ptr(self.isw), s), "per_sample_rng")
         self.gather(per, store)
+        self._per_next, self._per_done = per, False
         self.compute_grads(store.obs, reset_obs_ptr)
 
     def sample_uniform_and_grads(self, per, store, reset_obs_ptr, seed=0, counter=0):
@@ -725,7 +752,12 @@ class QLearner:
         self.apply_grads(scale)
 
     def apply_and_reprioritize(self, per, grad_scale=1.0):
-        self.apply_grads(grad_scale)
+        if self._per_done:              # issued with the hypernet backward (compute_grads)
+            self._per_done = False
+            self.apply_grads(grad_scale)
+            return
+        if self.apply_grads(grad_scale, per=per):
+            return
         check(lib().mm_per_update(per._h, ptr(self.nodes), ptr(self.td_last), self.B, stream_handle(self.dev)),
               "per_update")
 
@@ -740,11 +772,13 @@ class QLearner:
         self.apply_and_reprioritize(per, scale)
 
     # ------------------------------------------------------------------ HIP graph of an update
-    def capture_update(self, per, store, reset_obs_ptr, seed=0):
+    def capture_update(self, per, store, reset_obs_ptr, seed=0, per_replay=1):
         """Capture [sample -> gather -> fwd/bwd] and [clip/Adam -> repack -> reprioritize] as two HIP
         graphs (the RCCL all-reduce, when used, runs between them eagerly; its 1/world scale is baked
         into the second graph from ``_graph_scale``). ``per=None`` captures the update of the batch
-        placed by ``load_batch`` instead (no sampling, no priority update)."""
+        placed by ``load_batch`` instead (no sampling, no priority update). ``per_replay`` > 1 also captures that
+        many consecutive single-replica updates as one graph (``replay_updates``: the trainer's update_iter
+        updates after an episode, Train_dqn.train called update_iter times, qmix/main.py:240-250)."""
         self._pack(self.beh)
         self._pack(self.tgt)
         self._push_double_eps()
@@ -771,12 +805,43 @@ class QLearner:
             else:
                 self.sample_and_grads(per, store, reset_obs_ptr, seed=seed)
                 self.apply_and_reprioritize(per, self._graph_scale)
+        self.graph_multi, self._per_replay = None, int(per_replay)
+        if self._per_replay > 1:
+            gk = torch.cuda.CUDAGraph()
+            with graph_capture(gk):
+                for _ in range(self._per_replay):
+                    if per is None:
+                        self.compute_grads(self._obs_ptr, self._reset_obs)
+                        self.apply_grads(self._graph_scale)
+                    else:
+                        self.sample_and_grads(per, store, reset_obs_ptr, seed=seed)
+                        self.apply_and_reprioritize(per, self._graph_scale)
+            self.graph_multi = gk
         self.updates = n0
         self.graphs = (g1, g2)
         self.graph_fused = g12
         return self.graphs
 
     _graph_scale = 1.0
+    graph_multi, _per_replay = None, 1
+
+    def replay_updates(self, n, allreduce=None):
+        """``n`` consecutive updates: single-replica ones as replays of the captured ``per_replay``-update graph
+        (one graph launch per ``per_replay`` updates: the B = 32 update is launch-latency bound), the rest (and every
+        update with an all-reduce between its halves) one by one."""
+        k = self._per_replay
+        if allreduce is None and self.graph_multi is not None and n >= k:
+            self._pack(self.tgt)
+            self._pack(self.beh)
+            self._push_double_eps()
+            while n >= k:
+                self.graph_multi.replay()
+                self.updates += k
+                n -= k
+            if not self._uses_h3():
+                self.beh.mark_h3_stale()
+        for _ in range(n):
+            self.replay_update(allreduce)
 
     def replay_update(self, allreduce=None):
         g1, g2 = self.graphs

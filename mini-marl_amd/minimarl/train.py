@@ -116,7 +116,8 @@ class QTrainer:
     # ------------------------------------------------------------------ learning
     def _capture(self):
         eng = self.eng
-        self.learner.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=self.cfg.seed + 104729 * self.rank)
+        self.learner.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=self.cfg.seed + 104729 * self.rank,
+                                    per_replay=self.cfg.update_iter if self.allreduce is None else 1)
         self.updates_captured = True
 
     def learn(self, epsilon):
@@ -125,8 +126,7 @@ class QTrainer:
             self._capture()
         if self.cfg.algo == "vdn_double":
             self.learner.double_eps = epsilon if self.cfg.double_epsilon else 0.0
-        for _ in range(self.cfg.update_iter):
-            self.learner.replay_update(self.allreduce)
+        self.learner.replay_updates(self.cfg.update_iter, self.allreduce)
 
     def train_episode(self):
         """One training episode (vdn/main.py:127-196), no host sync."""

@@ -621,3 +621,122 @@ def test_paired_fwd_launches_bit_identical():
     for other in res[1:]:
         for x, y in zip(res[0], other):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("two_groups", [0, 1])
+def test_clip_adam_pack_matches_separate_calls(two_groups):
+    """mm_clip_adam_pack (the Adam step writing the behavior net's exact-f32 image, the priority update one more
+    block of the same launch) against mm_clip_adam / mm_clip2_adam + mm_qnet_pack_f32 + mm_per_update: bit-identical
+    parameters, moments, step, norms, image and sum tree (random gradients large enough that the clip engages)."""
+    from minimarl._lib import check, lib
+    from minimarl.qnet import AgentQNet, ptr, stream_handle
+    from minimarl.replay import DevicePER
+    L = lib()
+    N, D, A = 8, 47, 5
+    net = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=5)
+    n_agent, n_mix = net.n_params, 9000
+    n = n_agent + n_mix
+    g = torch.Generator().manual_seed(11)
+    P0 = torch.randn(n, generator=g) * 0.1
+    G0 = torch.randn(n, generator=g) * 0.05
+    m0 = torch.randn(n, generator=g) * 1e-3
+    v0 = torch.rand(n, generator=g) * 1e-4
+    B, cap = 32, 4096
+    nodes = torch.randint(cap - 1, 2 * cap - 1, (B,), generator=g).to(DEV)
+    td = torch.rand(B, generator=g).to(DEV)
+    outs = []
+    for fused in (False, True):
+        P, G, m, v = (x.clone().to(DEV) for x in (P0, G0, m0, v0))
+        step = torch.full((1,), 2.0, device=DEV)
+        partials = torch.zeros(512, device=DEV)
+        norm = torch.zeros(2, device=DEV)
+        packed = torch.zeros_like(net.packed)
+        per = DevicePER(cap, "qmix", device=DEV)
+        per.add(torch.rand(cap, generator=torch.Generator().manual_seed(3)).to(DEV))
+        s = stream_handle(torch.device(DEV))
+        args = (ptr(P), ptr(G), ptr(m), ptr(v), n, n_agent)   # clip group(s): the agent net [, the rest]
+        hyp = (5.0, 1e-3, 0.9, 0.999, 1e-8, ptr(step), ptr(partials), ptr(norm), 1.0)
+        if fused:
+            check(L.mm_clip_adam_pack(*args, two_groups, *hyp, ctypes.byref(net.dims), ptr(packed), per._h,
+                                      ptr(nodes), ptr(td), B, s), "clip_adam_pack")
+        else:
+            fn = L.mm_clip2_adam if two_groups else L.mm_clip_adam
+            check(fn(*args, *hyp, s), "clip_adam")
+            check(L.mm_qnet_pack_f32(ctypes.byref(net.dims), ptr(P), ptr(packed), s), "pack_f32")
+            check(L.mm_per_update(per._h, ptr(nodes), ptr(td), B, s), "per_update")
+        torch.cuda.synchronize()
+        img = (net.packed.numel() - ((N + 63) & ~63)) // 2   # the f32 image: the first N agent strides
+        outs.append((P, m, v, step, norm, packed[:img], per.tree()))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    assert outs[1][4][0] > 5.0           # the clip engaged (norm above max_norm)
+
+
+def test_hyper_bwd_per_block_matches_separate_update():
+    """mm_mixer_bwd_seq_hyper_per (the small priority update as one more block of the hypernet backward, what a
+    sampled B = 32 QMIX update issues) against mm_mixer_bwd_seq_hyper + mm_per_update on the same inputs:
+    bit-identical hypernet outputs and sum trees."""
+    from minimarl._lib import check, lib
+    from minimarl.engine import RolloutEngine
+    from minimarl.learner import Mixer, QLearner
+    from minimarl.qnet import ptr, stream_handle
+    from minimarl.replay import DevicePER
+    L = lib()
+    eng = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, device="cuda")
+    for _ in range(2):
+        eng.run_graph(0.5)
+    N, D = eng.N, eng.D
+    mix, tmix = Mixer(N, N * D, 64, 32, "cuda", seed=7), Mixer(N, N * D, 64, 32, "cuda", seed=7)
+    lrn = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda")
+    assert lrn._mixer_split()
+    lrn.sample_and_grads(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=1)
+    torch.cuda.synchronize()
+    ts, _ = eng.per.checkpoint_tensors()
+    outs = (lrn.dhm, lrn.dqa, lrn.mdelta, lrn.mxws)
+    snap = [t.clone() for t in outs]
+    s = stream_handle(torch.device(DEV))
+    mx = lrn.mix
+    margs = (lrn.B, N, mx.S, mx.Hm, mx.K1, ptr(mx.flat), ptr(lrn.msave), ptr(lrn.qa), ptr(lrn.dq), ptr(lrn.done),
+             ptr(lrn.ones_f), ptr(lrn.dhm), ptr(lrn.dqa), ptr(lrn.mdelta), ptr(lrn.mxws), lrn.C)
+    td = lrn.td_last * 1.5 + 0.25      # other priorities than the ones sample_and_grads already wrote
+    res = []
+    for fused in (False, True):
+        for t, v in zip(outs, snap):
+            t.copy_(v)
+        per = DevicePER(4096, "qmix", device=DEV)
+        per.restore_tensors(ts)
+        if fused:
+            check(L.mm_mixer_bwd_seq_hyper_per(*margs, per._h, ptr(lrn.nodes), ptr(td), lrn.B, s), "hyp+per")
+        else:
+            check(L.mm_mixer_bwd_seq_hyper(*margs, s), "hyper")
+            check(L.mm_per_update(per._h, ptr(lrn.nodes), ptr(td), lrn.B, s), "per_update")
+        torch.cuda.synchronize()
+        res.append([t.clone() for t in outs] + [per.tree()])
+    for x, y in zip(*res):
+        assert torch.equal(x, y)
+    assert not torch.equal(res[0][-1], ts["tree"])       # the update changed the tree
+
+
+
+
+def test_multi_update_graph_matches_single_replays():
+    """capture_update(per_replay=5) + replay_updates(10) (two launches of a 5-update graph) against ten replays of
+    the one-update graph from the same state: bit-identical parameters, Adam moments, PER tree and loss."""
+    from minimarl.engine import RolloutEngine
+    from minimarl.learner import Mixer, QLearner
+    res = []
+    for k in (1, 5):
+        eng = RolloutEngine(2048, 8, f1=64, g=64, h=64, chunk=10, capacity=4096, seed=3, device="cuda")
+        for _ in range(2):
+            eng.run_graph(0.5)
+        N, D = eng.N, eng.D
+        mix, tmix = Mixer(N, N * D, 64, 32, "cuda", seed=7), Mixer(N, N * D, 64, 32, "cuda", seed=7)
+        lrn = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda")
+        lrn.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=1, per_replay=k)
+        lrn.replay_updates(10)
+        torch.cuda.synchronize()
+        assert lrn.updates == 10
+        res.append((lrn.P.clone(), lrn.m.clone(), lrn.v.clone(), eng.per.tree(), lrn.loss.clone(),
+                    eng.behavior.packed.clone()))
+    for x, y in zip(*res):
+        assert torch.equal(x, y)

@@ -16,17 +16,16 @@ for _ in range(max(4, CAP // E + 1)):
 mix, tmix = Mixer(N, N * eng.D, 64, 32, "cuda", seed=7), Mixer(N, N * eng.D, 64, 32, "cuda", seed=7)
 kw = {k: os.environ[v] == "1" for k, v in (("fwd_side", "MB_FWD_SIDE"),) if v in os.environ}
 L = QLearner(eng.behavior, eng.target, mix, tmix, batch=32, chunk=10, mode="qmix", device="cuda", **kw)
-L.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=3)
+K = int(os.environ.get("MB_K", 10))              # updates per graph launch (the trainer's update_iter)
+L.capture_update(eng.per, eng.store, eng.env.reset_obs_ptr(), seed=3, per_replay=K)
 if os.environ.get("MB_FUSED", "1") == "0":     # A/B: the two-graph replay path
     L.graph_fused = None
-for _ in range(5):
-    L.replay_update()
+L.replay_updates(10)
 torch.cuda.synchronize()
 a, b = torch.cuda.Event(True), torch.cuda.Event(True)
 a.record()
-for _ in range(50):
-    L.replay_update()
+L.replay_updates(50)
 b.record()
 torch.cuda.synchronize()
-print(json.dumps({"kw": kw, "fused": L.graph_fused is not None,
+print(json.dumps({"kw": kw, "per_replay": K, "fused": L.graph_fused is not None,
                   "ms_per_update": a.elapsed_time(b) / 50}))
