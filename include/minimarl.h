@@ -519,12 +519,16 @@ int mm_tmv(const mm_tmv_args* x, mm_stream_t s);
  * behavior net's exact-f32 image written from the new parameters (what mm_qnet_pack_f32(d, P, packed) writes after
  * the step; the agent net's d->n_agents nets lead P), and, when per != NULL, mm_per_update(per, nodes, td, batch):
  * two launches instead of four (the Adam step and the image in one grid, the priority update one more block of it).
+ * next_per != NULL (per == NULL: the priorities already updated): that block runs mm_per_sample_rng(next_per, batch,
+ * next_seed, next_counter, next_nodes, next_slots, next_isw) instead — the NEXT update's draws, one launch fewer.
  * Results identical to the separate calls (Train_dqn.train's step + priority update, qmix/_train.py:86-96,
  * qmix/main.py:240-244). */
 int mm_clip_adam_pack(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip, int32_t two_groups,
                       float max_norm, float lr, float beta1, float beta2, float eps, float* step, float* partials,
                       float* norm_out, float grad_scale, const mm_qnet_dims* d, float* packed, mm_per* per,
-                      const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s);
+                      const int64_t* nodes, const float* td, int32_t batch, mm_per* next_per, uint64_t next_seed,
+                      uint64_t next_counter, int64_t* next_nodes, int64_t* next_slots, float* next_isw,
+                      mm_stream_t s);
 /* clip_grad_norm_ on G[0:split] and on G[split:n] separately (qmix/qmix.py:235-238), then Adam. */
 int mm_clip2_adam(float* P, float* G, float* m, float* v, int64_t n, int64_t split, float max_norm, float lr,
                   float beta1, float beta2, float eps, float* step, float* partials, float* norm_out, float grad_scale,

@@ -459,86 +459,10 @@ __global__ __launch_bounds__(1024) void per_uniform_kernel(int64_t cap, int B, u
   }
 }
 
-constexpr int PER_SAMPLE_MAXJ = 8;   // per_sample_kernel: batch <= PT * 8
 __global__ __launch_bounds__(PT) void per_sample_kernel(double* tree, int64_t cap, int B, const double* fracs,
                                                         uint64_t seed, uint64_t counter, PerDev* st, double decay,
                                                         int64_t* nodes_out, int64_t* slots_out, float* is_w) {
-  // anneal alpha / beta before the draws (buffer.py:53-56)
-  const double alpha = fmin(1.0, st->alpha + st->alpha_inc);
-  const double beta = fmin(1.0, st->beta + st->beta_inc);
-  // device-side draw counter: every (graph-replayed) sample call gets a fresh RNG stream
-  const uint64_t ctr = counter + st->n_samples;
-  // the tree's top 11 levels (2047 nodes) staged in LDS in one round trip: a draw's descent then pays a
-  // global round trip only below depth 10 (6 instead of 16 dependent loads at 65536 leaves); same nodes,
-  // same comparisons
-  __shared__ double top[2047];
-  const int64_t n_nodes = 2 * cap - 1;
-  const int64_t ntop = n_nodes < 2047 ? n_nodes : 2047;
-  for (int64_t i = threadIdx.x; i < ntop; i += PT) top[i] = tree[i];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    st->alpha = alpha;
-    st->beta = beta;
-    st->n_samples += 1;
-  }
-  // each thread owns samples k = threadIdx.x + j * PT (B <= PT * PER_SAMPLE_MAXJ), leaf priorities and
-  // IS weights kept in registers
-  double pk[PER_SAMPLE_MAXJ], wk[PER_SAMPLE_MAXJ];
-  const double total = top[0];
-  const double seg = total / (double)B;
-#pragma unroll
-  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
-    const int k = threadIdx.x + j * PT;
-    pk[j] = 0.0;
-    if (k >= B) continue;
-    double f = fracs ? fracs[k] : (double)(rng_draw(seed, ctr, (uint64_t)k, 77) >> 11) * (1.0 / 9007199254740992.0);
-    const double a = seg * (double)k;
-    const double b = seg * (double)(k + 1);
-    double s = a + (b - a) * f;
-    int64_t idx = 0;
-    while (true) {
-      const int64_t left = 2 * idx + 1;
-      if (left >= n_nodes) break;
-      const double lv = left < ntop ? top[left] : tree[left];
-      if (s <= lv) {
-        idx = left;
-      } else {
-        s = s - lv;
-        idx = left + 1;
-      }
-    }
-    nodes_out[k] = idx;
-    if (slots_out) slots_out[k] = idx - (cap - 1);
-    pk[j] = tree[idx];
-  }
-  __syncthreads();
-  // VDN: whole tree x step_weight after sampling (buffer.py:72-73)
-  if (decay != 1.0) {
-    for (int64_t i = threadIdx.x; i < n_nodes; i += PT) tree[i] = decay * tree[i];
-    __syncthreads();
-  }
-  const double total2 = tree[0];
-  double mx = 0.0;
-#pragma unroll
-  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
-    const int k = threadIdx.x + j * PT;
-    wk[j] = 0.0;
-    if (k >= B) continue;
-    wk[j] = pow((double)cap * (pk[j] / total2), -beta);
-    mx = fmax(mx, wk[j]);
-  }
-  // block max (exact in any order)
-  __shared__ double s_mx[PT / 64];
-  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-  if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  mx = s_mx[0];
-  for (int w = 1; w < PT / 64; ++w) mx = fmax(mx, s_mx[w]);
-#pragma unroll
-  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
-    const int k = threadIdx.x + j * PT;
-    if (k < B) is_w[k] = (float)(wk[j] / mx);
-  }
+  per_sample_body(tree, cap, B, fracs, seed, counter, st, decay, nodes_out, slots_out, is_w);
 }
 
 __global__ __launch_bounds__(1024) void per_update_small_kernel(double* tree, int64_t cap, const int64_t* nodes,
@@ -1308,16 +1232,20 @@ int mm_per_sample_uniform(mm_per* per, int32_t batch, uint64_t seed, uint64_t co
   return MM_OK;
 }
 
+// the host mirror of a sample call's annealing (buffer.py:53-56); returns the tree decay of the call
+static double per_sample_prep(mm_per* per) {
+  per->alpha = std::min(1.0, per->alpha + per->alpha_inc);
+  per->beta = std::min(1.0, per->beta + per->beta_inc);
+  return per->use_step_weight ? per->step_weight : 1.0;
+}
+
 static int per_sample_impl(mm_per* per, int32_t batch, const double* fracs, uint64_t seed, uint64_t counter,
                            int64_t* nodes_out, int64_t* slots_out, float* is_w, mm_stream_t s) {
   MM_REQUIRE(per && nodes_out && is_w, "per_sample: null argument");
   MM_REQUIRE(batch >= 1 && batch <= mm::PT * mm::PER_SAMPLE_MAXJ, "per_sample: batch must be in [1, %d]",
              mm::PT * mm::PER_SAMPLE_MAXJ);
   MM_REQUIRE(per->n_data > 0, "per_sample: empty buffer");
-  // anneal before the draws (buffer.py:53-56)
-  per->alpha = std::min(1.0, per->alpha + per->alpha_inc);
-  per->beta = std::min(1.0, per->beta + per->beta_inc);
-  const double decay = per->use_step_weight ? per->step_weight : 1.0;
+  const double decay = per_sample_prep(per);
   hipLaunchKernelGGL(mm::per_sample_kernel, dim3(1), dim3(mm::PT), 0, (hipStream_t)s, per->tree, per->cap, batch,
                      fracs, seed, counter, per->st, decay, nodes_out, slots_out, is_w);
   MM_HIP_CHECK(hipGetLastError());

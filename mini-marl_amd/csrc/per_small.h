@@ -90,6 +90,92 @@ __device__ __forceinline__ void per_update_small_body(double* tree, int64_t cap,
   }
 }
 
+// Stratified PER sampling (one 1024-thread block; per_sample_kernel's, or one extra block of the learner's Adam
+// launch sampling the NEXT update's batch): B draws, the sampled nodes / slots, IS weights, alpha / beta annealing
+// and the VDN step-weight decay (vdn/replay_buffer/buffer.py:50-81, qmix/replay_buffer/per.py:36-59).
+constexpr int PS_T = 1024;            // the block size
+constexpr int PER_SAMPLE_MAXJ = 8;    // batch <= PS_T * 8
+__device__ __forceinline__ void per_sample_body(double* tree, int64_t cap, int B, const double* fracs, uint64_t seed,
+                                                uint64_t counter, PerDev* st, double decay, int64_t* nodes_out,
+                                                int64_t* slots_out, float* is_w) {
+  // anneal alpha / beta before the draws (buffer.py:53-56)
+  const double alpha = fmin(1.0, st->alpha + st->alpha_inc);
+  const double beta = fmin(1.0, st->beta + st->beta_inc);
+  // device-side draw counter: every (graph-replayed) sample call gets a fresh RNG stream
+  const uint64_t ctr = counter + st->n_samples;
+  // the tree's top 11 levels (2047 nodes) staged in LDS in one round trip: a draw's descent then pays a
+  // global round trip only below depth 10 (6 instead of 16 dependent loads at 65536 leaves); same nodes,
+  // same comparisons
+  __shared__ double top[2047];
+  const int64_t n_nodes = 2 * cap - 1;
+  const int64_t ntop = n_nodes < 2047 ? n_nodes : 2047;
+  for (int64_t i = threadIdx.x; i < ntop; i += PS_T) top[i] = tree[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st->alpha = alpha;
+    st->beta = beta;
+    st->n_samples += 1;
+  }
+  // each thread owns samples k = threadIdx.x + j * PS_T (B <= PS_T * PER_SAMPLE_MAXJ), leaf priorities and
+  // IS weights kept in registers
+  double pk[PER_SAMPLE_MAXJ], wk[PER_SAMPLE_MAXJ];
+  const double total = top[0];
+  const double seg = total / (double)B;
+#pragma unroll
+  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
+    const int k = threadIdx.x + j * PS_T;
+    pk[j] = 0.0;
+    if (k >= B) continue;
+    double f = fracs ? fracs[k] : (double)(rng_draw(seed, ctr, (uint64_t)k, 77) >> 11) * (1.0 / 9007199254740992.0);
+    const double a = seg * (double)k;
+    const double b = seg * (double)(k + 1);
+    double s = a + (b - a) * f;
+    int64_t idx = 0;
+    while (true) {
+      const int64_t left = 2 * idx + 1;
+      if (left >= n_nodes) break;
+      const double lv = left < ntop ? top[left] : tree[left];
+      if (s <= lv) {
+        idx = left;
+      } else {
+        s = s - lv;
+        idx = left + 1;
+      }
+    }
+    nodes_out[k] = idx;
+    if (slots_out) slots_out[k] = idx - (cap - 1);
+    pk[j] = tree[idx];
+  }
+  __syncthreads();
+  // VDN: whole tree x step_weight after sampling (buffer.py:72-73)
+  if (decay != 1.0) {
+    for (int64_t i = threadIdx.x; i < n_nodes; i += PS_T) tree[i] = decay * tree[i];
+    __syncthreads();
+  }
+  const double total2 = tree[0];
+  double mx = 0.0;
+#pragma unroll
+  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
+    const int k = threadIdx.x + j * PS_T;
+    wk[j] = 0.0;
+    if (k >= B) continue;
+    wk[j] = pow((double)cap * (pk[j] / total2), -beta);
+    mx = fmax(mx, wk[j]);
+  }
+  // block max (exact in any order)
+  __shared__ double s_mx[PS_T / 64];
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) s_mx[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = s_mx[0];
+  for (int w = 1; w < PS_T / 64; ++w) mx = fmax(mx, s_mx[w]);
+#pragma unroll
+  for (int j = 0; j < PER_SAMPLE_MAXJ; ++j) {
+    const int k = threadIdx.x + j * PS_T;
+    if (k < B) is_w[k] = (float)(wk[j] / mx);
+  }
+}
+
 // the small update's arguments as one extra block of another launch (tree == nullptr: none)
 struct PerUpd {
   double* tree;
@@ -102,6 +188,20 @@ struct PerUpd {
 };
 __device__ __forceinline__ void per_update_small_block(const PerUpd& pu) {
   per_update_small_body(pu.tree, pu.cap, pu.nodes, pu.td, pu.B, pu.st, pu.eps);
+}
+// a sample's arguments as one extra block of another launch (tree == nullptr: none)
+struct PerSmp {
+  double* tree;
+  int64_t cap;
+  PerDev* st;
+  uint64_t seed, counter;
+  double decay;
+  int64_t *nodes, *slots;
+  float* isw;
+  int B;
+};
+__device__ __forceinline__ void per_sample_block(const PerSmp& ps) {
+  per_sample_body(ps.tree, ps.cap, ps.B, nullptr, ps.seed, ps.counter, ps.st, ps.decay, ps.nodes, ps.slots, ps.isw);
 }
 
 }  // namespace mm

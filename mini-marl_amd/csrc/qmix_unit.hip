@@ -6,8 +6,9 @@
 //                            W_ih x2 of every (t, b) row, both nets)
 //   mm_agent_mixer_rec_seq = mm_mixer_fwd_seq_rec (the Mix_Net GRU over the state) || mm_agent_q_rec_seq2 (the
 //                            agent GRU + Q head over the C steps, both nets)
-//   mm_clip_adam_pack      = mm_clip_adam + mm_qnet_pack_f32 of the behavior net (+ mm_per_update): the Adam step
-//                            writes the exact-f32 image from the new values (one more block: the priorities)
+//   mm_clip_adam_pack      = mm_clip_adam + mm_qnet_pack_f32 of the behavior net (+ mm_per_update, or + the next
+//                            update's mm_per_sample_rng): the Adam step writes the exact-f32 image from the new
+//                            values (one more block: the priorities, or the next batch's draws)
 //   mm_mixer_bwd_seq_hyper_per = mm_mixer_bwd_seq_hyper + mm_per_update (one more block of the hypernet pass)
 // (Train_dqn.train's forward over the chunk, qmix/_train.py:55-77: Q_Net per step, then Mix_Net per step; the
 // Mix_Net's GRU depends on the state only, so it runs beside the agent chain; the step / priority update,
@@ -94,11 +95,16 @@ static bool rec_pair_ok(const mm_qnet_dims* d, int32_t B, int32_t N, int32_t Hm,
 // per_update_small_block. Every parameter's step runs exactly once (qnet_pack_src: each agent parameter lies in one
 // image element). (A parameter-centric order — coalesced Adam, each image element written through the inverse
 // mapping — measured 16.0 vs 13.2 us at the B = 32 shapes.)
+// (ps.tree: the extra block samples the NEXT update's batch instead, once this update's priorities are in)
 __global__ __launch_bounds__(1024) void adam_pack_kernel(AdamArgs a, float* packed, QnetGeo g, int N, int D, int F1,
-                                                         int G, int H, int A, QnetOffsets o, int nA, int nB, PerUpd pu) {
+                                                         int G, int H, int A, QnetOffsets o, int nA, int nB, PerUpd pu,
+                                                         PerSmp ps) {
   const int bid = (int)blockIdx.x;
   if (bid >= nA + nB) {
-    per_update_small_block(pu);
+    if (ps.tree)
+      per_sample_block(ps);
+    else
+      per_update_small_block(pu);
     return;
   }
   const AdamConst c = adam_const(a);
@@ -139,7 +145,9 @@ int mm_mixer_bwd_seq_hyper_per(int32_t B, int32_t N, int32_t S, int32_t Hm, int3
 int mm_clip_adam_pack(float* P, float* G, float* m, float* v, int64_t n, int64_t n_clip, int32_t two_groups,
                       float max_norm, float lr, float beta1, float beta2, float eps, float* step, float* partials,
                       float* norm_out, float grad_scale, const mm_qnet_dims* d, float* packed, mm_per* per,
-                      const int64_t* nodes, const float* td, int32_t batch, mm_stream_t s) {
+                      const int64_t* nodes, const float* td, int32_t batch, mm_per* next_per, uint64_t next_seed,
+                      uint64_t next_counter, int64_t* next_nodes, int64_t* next_slots, float* next_isw,
+                      mm_stream_t s) {
   MM_REQUIRE(P && G && m && v && step && partials && packed && d && n > 0 && n_clip >= 0 && n_clip <= n,
              "clip_adam_pack: bad args");
   mm::QnetGeo g;
@@ -162,10 +170,21 @@ int mm_clip_adam_pack(float* P, float* G, float* m, float* v, int64_t n, int64_t
   const int nA = (int)std::min<int64_t>((total + 1023) / 1024, 1024);
   const int nB = (int)std::min<int64_t>((n - o.total + 1023) / 1024, 512);
   mm::PerUpd pu = {};
+  mm::PerSmp ps = {};
   const bool per_block = per && nodes && td && (per->cap & (per->cap - 1)) == 0 && batch >= 1 && batch <= mm::PU_B;
-  if (per_block) pu = {per->tree, per->cap, nodes, td, per->st, batch, (float)per->eps};
-  hipLaunchKernelGGL(mm::adam_pack_kernel, dim3(nA + nB + (per_block ? 1 : 0)), dim3(1024), 0, (hipStream_t)s, a,
-                     packed, g, d->n_agents, d->obs_dim, d->f1, d->g, d->h, d->n_actions, o, nA, nB, pu);
+  if (next_per) {   // sample the next update's batch (this update's priorities must be in already)
+    MM_REQUIRE(!per && next_nodes && next_slots && next_isw && batch >= 1 && batch <= mm::PS_T * mm::PER_SAMPLE_MAXJ,
+               "clip_adam_pack: the next sample needs its outputs and no priority update in the same launch");
+    MM_REQUIRE(next_per->n_data > 0, "per_sample: empty buffer");
+    const double decay = per_sample_prep(next_per);
+    ps = {next_per->tree, next_per->cap, next_per->st, next_seed, next_counter, decay, next_nodes, next_slots,
+          next_isw, batch};
+  } else if (per_block) {
+    pu = {per->tree, per->cap, nodes, td, per->st, batch, (float)per->eps};
+  }
+  const int extra = (next_per || per_block) ? 1 : 0;
+  hipLaunchKernelGGL(mm::adam_pack_kernel, dim3(nA + nB + extra), dim3(1024), 0, (hipStream_t)s, a, packed, g,
+                     d->n_agents, d->obs_dim, d->f1, d->g, d->h, d->n_actions, o, nA, nB, pu, ps);
   MM_HIP_CHECK(hipGetLastError());
   if (per && !per_block) return mm_per_update(per, nodes, td, batch, s);
   return MM_OK;

@@ -258,7 +258,7 @@ _SIGS += [
                              c_vp, c_f32, c_vp]),
     ("mm_clip_adam_pack", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32, c_f32,
                                   c_vp, c_vp, c_vp, c_f32, ctypes.POINTER(QnetDims), c_vp, c_vp, c_vp, c_vp, c_i32,
-                                  c_vp]),
+                                  c_vp, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
     ("mm_clip2_adam", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_vp,
                               c_vp, c_f32, c_vp]),
     ("mm_per_sample_uniform", c_i32, [c_vp, c_i32, c_u64, c_u64, c_vp, c_vp, c_vp]),

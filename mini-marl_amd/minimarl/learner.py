@@ -598,10 +598,11 @@ class QLearner:
                     n.save = sv.data_ptr() if sv is not None else None
                 check(L.mm_mixer_fwd(B, N, mx.S, mx.Hm, mx.K1, obs_p, reset_p, nets, 2, s), "mixer fwd")
 
-    def apply_grads(self, grad_scale=1.0, per=None):
+    def apply_grads(self, grad_scale=1.0, per=None, sample_next=None):
         """clip_grad_norm_ + Adam (grads scaled first, e.g. 1/world after an all-reduce), then repack
         the behavior fragments for the next forward; with ``per`` also the priority update of the sampled
-        chunks. Returns True when that update was issued here."""
+        chunks (returns True when that update was issued here); with ``sample_next`` = (per, seed, counter) and no
+        ``per``, the next update's PER draws in the same launch (its sample_and_grads then runs presampled)."""
         s = stream_handle(self.dev)
         if not self._uses_h3():
             # one launch after the norm's partial sums: the Adam step writes the exact-f32 image from the new values
@@ -613,7 +614,12 @@ class QLearner:
                                           float(grad_scale), ctypes.byref(self.beh.dims), ptr(self.beh.packed),
                                           per._h if per is not None else None,
                                           ptr(self.nodes) if per is not None else None,
-                                          ptr(self.td_last) if per is not None else None, self.B, s), "clip_adam_pack")
+                                          ptr(self.td_last) if per is not None else None, self.B,
+                                          sample_next[0]._h if sample_next else None,
+                                          sample_next[1] if sample_next else 0, sample_next[2] if sample_next else 0,
+                                          ptr(self.nodes) if sample_next else None,
+                                          ptr(self.slots) if sample_next else None,
+                                          ptr(self.isw) if sample_next else None, s), "clip_adam_pack")
             self.beh.mark_h3_stale()       # the exact-f32 image is current, the fp16x3 image is not
             self.updates += 1
             return per is not None
@@ -722,10 +728,13 @@ class QLearner:
                     mo["b2bW"], 0, mo["b2bb"], 0, M, 1, K1, 1, jobs=jobs)
 
     # ------------------------------------------------------------------ full update from the PER
-    def sample_and_grads(self, per, store, reset_obs_ptr, fracs=None, seed=0, counter=0):
-        """PER sample (injected fractions or the device counter RNG) -> gather -> forward/backward."""
+    def sample_and_grads(self, per, store, reset_obs_ptr, fracs=None, seed=0, counter=0, presampled=False):
+        """PER sample (injected fractions or the device counter RNG) -> gather -> forward/backward (presampled: the
+        draws already issued by the previous update's step launch)."""
         L, s = lib(), stream_handle(self.dev)
-        if fracs is not None:
+        if presampled:
+            pass
+        elif fracs is not None:
             fr = torch.as_tensor(fracs, dtype=torch.float64).to(self.dev).contiguous()
             check(L.mm_per_sample(per._h, self.B, ptr(fr), ptr(self.nodes), ptr(self.slots), ptr(self.isw), s),
                   "per_sample")
@@ -751,15 +760,18 @@ class QLearner:
             scale = 1.0 / allreduce(self.Gr)
         self.apply_grads(scale)
 
-    def apply_and_reprioritize(self, per, grad_scale=1.0):
+    def apply_and_reprioritize(self, per, grad_scale=1.0, sample_next=None):
+        """Returns True when the next update's draws (``sample_next`` = (seed, counter)) were issued with the step."""
         if self._per_done:              # issued with the hypernet backward (compute_grads)
             self._per_done = False
-            self.apply_grads(grad_scale)
-            return
+            ahead = sample_next is not None and not self._uses_h3()
+            self.apply_grads(grad_scale, sample_next=(per,) + tuple(sample_next) if ahead else None)
+            return ahead
         if self.apply_grads(grad_scale, per=per):
-            return
+            return False
         check(lib().mm_per_update(per._h, ptr(self.nodes), ptr(self.td_last), self.B, stream_handle(self.dev)),
               "per_update")
+        return False
 
     def update(self, per, store, reset_obs_ptr, fracs=None, seed=0, counter=0, allreduce=None):
         """One reference update iteration: sample -> gather -> grads [-> all-reduce] -> clip/Adam ->
@@ -809,13 +821,15 @@ class QLearner:
         if self._per_replay > 1:
             gk = torch.cuda.CUDAGraph()
             with graph_capture(gk):
-                for _ in range(self._per_replay):
+                ahead = False   # each update's step launch also draws the next update's batch
+                for i in range(self._per_replay):
                     if per is None:
                         self.compute_grads(self._obs_ptr, self._reset_obs)
                         self.apply_grads(self._graph_scale)
                     else:
-                        self.sample_and_grads(per, store, reset_obs_ptr, seed=seed)
-                        self.apply_and_reprioritize(per, self._graph_scale)
+                        self.sample_and_grads(per, store, reset_obs_ptr, seed=seed, presampled=ahead)
+                        ahead = self.apply_and_reprioritize(per, self._graph_scale,
+                                                            sample_next=(seed, 0) if i + 1 < self._per_replay else None)
             self.graph_multi = gk
         self.updates = n0
         self.graphs = (g1, g2)

@@ -658,7 +658,7 @@ def test_clip_adam_pack_matches_separate_calls(two_groups):
         hyp = (5.0, 1e-3, 0.9, 0.999, 1e-8, ptr(step), ptr(partials), ptr(norm), 1.0)
         if fused:
             check(L.mm_clip_adam_pack(*args, two_groups, *hyp, ctypes.byref(net.dims), ptr(packed), per._h,
-                                      ptr(nodes), ptr(td), B, s), "clip_adam_pack")
+                                      ptr(nodes), ptr(td), B, None, 0, 0, None, None, None, s), "clip_adam_pack")
         else:
             fn = L.mm_clip2_adam if two_groups else L.mm_clip_adam
             check(fn(*args, *hyp, s), "clip_adam")
