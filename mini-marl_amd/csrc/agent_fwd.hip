@@ -2427,10 +2427,25 @@ __global__ __launch_bounds__(1024, 1) void rollout_chunk_kernel(QFwdParams p0, Q
 
   // (two loops, one per body: the exact-f32 loop's spills stay in that rare path — the fp16x3 loop's spill code is
   // the same as with no exact path at all, checked in the ISA)
+#if MM_ROLL_DEBUG
+  // in-kernel clock (MI355X_MICROARCH.md DVFS check 6): shader-clock and 100 MHz stamps around the step loop of
+  // every block, trace[60000 + 4 b ..] (tools/chunk_trace.py: delta memtime / delta memrealtime x 100 MHz)
+  uint64_t* clk = (rc.trace && threadIdx.x == 0) ? rc.trace + 60000 + 4 * (int)blockIdx.x : nullptr;
+  if (clk) {
+    clk[0] = __builtin_amdgcn_s_memtime();
+    clk[1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   if (exact)
     roll_chunk_steps<F1, G, H, AB, true>();
   else
     roll_chunk_steps<F1, G, H, AB, false>();
+#if MM_ROLL_DEBUG
+  if (clk) {
+    clk[2] = __builtin_amdgcn_s_memtime();
+    clk[3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 
   // ---- the tile's final env state into buffer 1 - par (reset where the last step ended), by the writer block
   const int lastp = (rc.n - 1) & 1;

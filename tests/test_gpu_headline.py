@@ -11,7 +11,10 @@ that configuration past the point where the PER is full and evicting, and checks
   ``oracle/env.py`` driven with the stored actions;
 * every exploratory action bit-exact vs the restated device RNG (``oracle/rng.py``);
 * the PER: the device's own chunk priorities fed to ``SumTreeOracle.add_batch`` give the same
-  slots, the same tree (rtol 1e-6) and the same slot -> row map and staging rows;
+  slots, the same tree (rtol 1e-6) and the same slot -> row map and staging rows; and the slots' CONTENTS:
+  the store row each slot points at holds the chunk the oracle put in that slot (a digest of its obs /
+  actions / rewards / dones), for every slot filled by the chunk and a sample of 256 older slots (rows
+  swapped in by the insert are never written again while their slot lives);
 
 and on two two-chunk windows (one before, one after eviction starts), from the device's hidden
 states at the window start, with the torch-CPU oracle nets (``oracle/nets.py``, fp32):
@@ -25,6 +28,7 @@ Reference call sites restated: qmix/main.py:180-233 (rollout step + chunking), q
 sumtree.py:37-55 (collect_sample / add with min eviction).
 """
 import ctypes
+import hashlib
 
 import numpy as np
 import pytest
@@ -79,6 +83,13 @@ def test_headline_engine_vs_oracle_through_eviction(mode):
     snap = None
     last_done = np.zeros(E, bool)
     n_near_tie = 0
+    slot_digest = {}                        # slot -> digest of the chunk the oracle put there
+    pick = np.random.default_rng(0)
+
+    def digests(o, a, r, d):
+        return [hashlib.blake2b(o[i].tobytes() + a[i].tobytes() + r[i].tobytes() + d[i].tobytes(),
+                                digest_size=16).digest() for i in range(o.shape[0])]
+
     for k in range(n_chunks):
         rows = eng.staging.cpu().numpy().copy()
         if k + 1 in windows:                # window start: hidden states before chunk k
@@ -113,6 +124,16 @@ def test_headline_engine_vs_oracle_through_eviction(mode):
         np.testing.assert_array_equal(eng.per.slot_rows().cpu().numpy(), slot_row)
         np.testing.assert_array_equal(eng.staging.cpu().numpy(), new_staging)
         assert len(eng.per) == min(cap, (k + 1) * E)
+        # ---- PER slot contents: the rows the device's slot map names hold the oracle's chunks
+        for sl, dg in zip(slots, digests(O, eng.store.act[rows].cpu().numpy(), R, eng.store.done[rows].cpu().numpy())):
+            slot_digest[int(sl)] = dg
+        older = np.setdiff1d(np.fromiter(slot_digest.keys(), np.int64), slots)
+        check = np.concatenate([slots, pick.choice(older, min(256, older.size), replace=False) if older.size else
+                                np.zeros(0, np.int64)])
+        dev_rows = torch.as_tensor(eng.per.slot_rows().cpu().numpy()[check], device=DEV)
+        got = digests(eng.store.obs[dev_rows].cpu().numpy(), eng.store.act[dev_rows].cpu().numpy(),
+                      eng.store.rew[dev_rows].cpu().numpy(), eng.store.done[dev_rows].cpu().numpy())
+        assert got == [slot_digest[int(sl)] for sl in check]
         # ---- oracle nets over the window (chunks k-1, k), from the device hidden states
         if k in windows:
             n_near_tie += _check_window(snap, P, Pt, td_dev, eng, E, N, C, seed, eps)

@@ -1,7 +1,9 @@
 """Per-step timeline of ONE chunk-persistent launch (10 steps, 4096 envs x 8 agents), from the MM_ROLL_DEBUG build's
 s_memrealtime stamps (csrc/agent_fwd.hip MM_CSTAMP, 100 MHz) of waves 0 and 15 of every block: per step 0 loop top,
 1 hand-off flags seen, 2 dynamics done, 3 forward done. Prints the medians over behavior blocks of each phase per
-step and the per-step period, in us. GPU only; needs `make -C mini-marl_amd debug`."""
+step and the per-step period, in us, and the in-kernel shader clock (s_memtime / s_memrealtime around each block's
+step loop, after ~0.5 s of back-to-back launches: MI355X_MICROARCH.md DVFS check). GPU only; needs
+`make -C mini-marl_amd debug`."""
 import ctypes
 import json
 import os
@@ -24,6 +26,8 @@ eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=C, capacity=4 * E, seed=1, de
 for _ in range(3):
     eng.run_steps(20, 0.1)
 out = {}
+for _ in range(2000):                               # ~0.5 s of back-to-back launches before the stamped ones (DVFS)
+    eng.chunk_only(C)
 for rep in range(2):
     torch.cuda.synchronize()
     eng.chunk_only(C)
@@ -46,5 +50,10 @@ for rep in range(2):
               f"  dyn {np.round(dyn, 2).tolist()}\n  fwd {np.round(fwd, 2).tolist()}  last end {end:.2f}")
         out[f"rep{rep}_{wname}"] = {"period": per.tolist(), "wait": wait.tolist(), "dyn": dyn.tolist(),
                                      "fwd": fwd.tolist()}
+    # in-kernel clock: delta s_memtime / delta s_memrealtime x 100 MHz around every block's step loop
+    ck = buf[60000:60000 + 4 * nb].reshape(nb, 4).astype(np.float64)
+    ghz = (ck[:, 2] - ck[:, 0]) / np.maximum(ck[:, 3] - ck[:, 1], 1) * 0.1
+    print(f"rep {rep} in-kernel clock GHz: median {np.median(ghz):.3f} min {ghz.min():.3f} max {ghz.max():.3f}")
+    out[f"rep{rep}_clock_ghz_median"] = float(np.median(ghz))
 print(json.dumps(out))
 eng.check_errors()
