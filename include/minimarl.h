@@ -271,7 +271,7 @@ int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, c
  * of the reference's per-step loop body, vdn/main.py:93-167 / qmix/main.py:186-233, like n_steps mm_rollout_step
  * calls, with bit-identical results): every (net, agent, 256-env tile) block stays resident for all the steps, keeps
  * its weight image and its copy of the tile's env state in LDS, and waits only for the tile's behavior actions of
- * each step (a tile-local hand-off through handoff / flags), never for a launch boundary. Per step t = c0 + i:
+ * each step (a tile-local hand-off through tagged handoff words), never for a launch boundary. Per step t = c0 + i:
  * rewards into rew + i E N, dones into done + i E, cur_row; the target's max Q'_t into io_t->qsel_out + t_off0 +
  * i E N; the behavior's act / Q(a) of step t + 1 into io_b->act_out / qsel_out + b_off0 + i E N (+ b_offn for the
  * next chunk's step 0 when t + 1 = chunk_len); s'_t into slot t + 1 (and at t = 0 s_0 into slot 0) of row
@@ -279,7 +279,8 @@ int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, c
  * place (h_in == h_out, io.reset NULL). The TD / chunk-store fold of the steps is mm_td_fold_range. ctl = device
  * int64 [3]: launch sequence, env state buffer (low int32 of ctl[1], read; flipped by each launch: see
  * mm_env_get_state_buf), arrival ticket — zero-initialised once, then owned by these launches.
- * flags [T][N] (8 B) and handoff [T][chunk_len][N][256] (bytes), T = ceil(E / 256), zero-initialised. Supported
+ * handoff = int64 [T][chunk_len][N][32], T = ceil(E / 256), zero-initialised: word w of (tile, step, agent) =
+ * (low 32 bits of the launch sequence + 1) << 32 | the 4-bit actions of the tile's envs 8 w .. 8 w + 7. Supported
  * when mm_rollout_chunk_supported() != 0 (the fused step's geometry and 2 N T blocks <= the device's CUs: all
  * blocks must be co-resident; a hand-off wait longer than 20 ms sets bit 1 of *err and proceeds). */
 typedef struct mm_rollout_chunk_io {
@@ -291,7 +292,7 @@ typedef struct mm_rollout_chunk_io {
   int64_t b_off0, b_offn, t_off0;
   int64_t* counter;      /* device RNG step counter: step c0 + i draws with *counter + i; += n_steps */
   int64_t* ctl;          /* device int64 [3]: launch sequence, env state buffer (low int32), arrival ticket */
-  int64_t* flags; uint8_t* handoff;
+  int64_t* handoff;
   int32_t* err;
 } mm_rollout_chunk_io;
 int mm_rollout_chunk_supported(const mm_env* env, const mm_qnet_dims* d, int64_t n_envs);

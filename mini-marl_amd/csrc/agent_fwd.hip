@@ -2023,8 +2023,7 @@ struct RollChunk {   // kernarg right after the two QFwdParams
   uint64_t* seq;             // launch sequence number (hand-off flag epoch)
   int32_t* envpar;           // env state buffer read (0 / 1)
   uint32_t* ticket;          // blocks finished
-  uint64_t* flags;           // [T][N] behavior hand-off flags: (seq << 16) + step index published
-  uint8_t* hx;               // [T][C][N][256] hand-off actions, one slot per step
+  uint64_t* hx;              // [T][C][N][32] hand-off words, one slot per step: (seq + 1) << 32 | 8 envs' 4-bit actions
   uint32_t* err;             // sticky error bits: 1 staging row outside the store, 2 hand-off wait expired
   uint64_t* trace;           // per-step timing stamps (MM_ROLL_DEBUG builds, tools/chunk_trace.py), else nullptr
   int c0, n, CL, lds_env;   // first step's chunk position, steps, chunk length, LDS offset of the env state
@@ -2046,7 +2045,7 @@ __host__ __device__ __forceinline__ RollChunkLds roll_chunk_lds(int R, int C, in
   m.spq = o;   o = a16(o + 256 * N * 2);
   m.ssa = o;   o = a16(o + 2 * 256 * 2);
   m.sdone = o; o = a16(o + 2 * 256);
-  m.shx = o;   o = a16(o + 256);
+  m.shx = o;   o = a16(o + N * 32 * 4);   // (exact body: the outgoing actions, 256 B; every block: the step's hand-off words)
   m.total = o;
   return m;
 }
@@ -2058,7 +2057,7 @@ struct ChunkCtx {
   uint16_t* spq;      // [256][N] position words prev_r << 12 | prev_c << 8 | r << 4 | c
   uint16_t* ssa;      // [2][256] steps, apples of the env
   uint8_t* sdone;     // [2][256] dones by step parity
-  uint8_t* shx;       // [256] the behavior block's outgoing actions
+  uint8_t* shx;       // [256] the exact-body behavior block's outgoing actions; at the loop top [N][32] u32 hand-off words
   uint64_t ctr0, seq;
   float eps;
   int tile, agent, e0;
@@ -2146,14 +2145,36 @@ __device__ __forceinline__ void roll_chunk_steps() {
     // (1) the actions of step t (i > 0: published by the tile's N behavior blocks at the end of their step t - 1)
     uint32_t aq[2] = {0u, 0u};   // 4-bit actions, agent k at bits 4 (k & 7) of aq[k >> 3]
     if (i > 0) {
-      if (wave == 0 && lane < N) {
-        const uint64_t want = (cx.seq << 16) + (uint64_t)i;
-        uint64_t* f = rc.flags + (int64_t)tile * N + lane;
+      __syncthreads();   // every wave is past its reads of the LDS env state of step i - 1
+      if (wave == 0) {
+        // the tile's N x 32 hand-off words of step i, polled by wave 0 until each carries this launch's tag (tag and
+        // actions are one 64-bit word: a word that matches holds this step's actions, no flag / fence needed), their
+        // action halves into LDS
+        const uint64_t* hs = rc.hx + ((int64_t)tile * CL + i) * N * 32;
+        uint32_t* hl = reinterpret_cast<uint32_t*>(cx.shx);
+        const uint32_t tag = (uint32_t)cx.seq + 1u;
+        const int nw = N * 32;
+        uint32_t got = 0u;   // bit q: word q * 64 + lane received (or outside the N x 32 words)
+#pragma unroll
+        for (int q = 0; q < (kRollMaxN * 32 + 63) / 64; ++q)
+          if (q * 64 + lane >= nw) got |= 1u << q;
+        const uint32_t need = (1u << ((kRollMaxN * 32 + 63) / 64)) - 1u;
         const uint64_t tw = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        while (true) {
+          uint64_t w[(kRollMaxN * 32 + 63) / 64];
+#pragma unroll
+          for (int q = 0; q < (kRollMaxN * 32 + 63) / 64; ++q)
+            if (!((got >> q) & 1u)) w[q] = __hip_atomic_load(hs + q * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int q = 0; q < (kRollMaxN * 32 + 63) / 64; ++q)
+            if (!((got >> q) & 1u) && (uint32_t)(w[q] >> 32) == tag) {
+              hl[q * 64 + lane] = (uint32_t)w[q];
+              got |= 1u << q;
+            }
+          if (__all(got == need)) break;
           __builtin_amdgcn_s_sleep(1);
           if (__builtin_amdgcn_s_memrealtime() - tw > kHandoffTimeout) {
-            atomicOr(rc.err, 2u);
+            if (lane == 0) atomicOr(rc.err, 2u);
             break;
           }
         }
@@ -2161,16 +2182,11 @@ __device__ __forceinline__ void roll_chunk_steps() {
       __syncthreads();
       MM_CSTAMP(1);
       if (dvalid) {
-        uint8_t* hs = rc.hx + ((int64_t)tile * CL + i) * N * 256;
-        uint32_t w[kRollMaxN];
+        const uint32_t* hl = reinterpret_cast<const uint32_t*>(cx.shx) + (le_d >> 3);
+        const uint32_t sh = 4u * (uint32_t)(le_d & 7);
 #pragma unroll
         for (int k = 0; k < kRollMaxN; ++k)
-          if (k < N)
-            w[k] = __hip_atomic_load(reinterpret_cast<uint32_t*>(hs + k * 256 + (le_d & ~3)), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int k = 0; k < kRollMaxN; ++k)
-          if (k < N) aq[k >> 3] |= ((w[k] >> (8 * (le_d & 3))) & 15u) << (4 * (k & 7));
+          if (k < N) aq[k >> 3] |= ((hl[k * 32] >> sh) & 15u) << (4 * (k & 7));
         // (2) auto-reset of an env that ended at step t - 1 (the initial grid / positions / counters)
         if (cx.sdone[prv * 256 + le_d]) {
           const uint4* ig = reinterpret_cast<const uint4*>(ev.init_grid);
@@ -2351,20 +2367,29 @@ __device__ __forceinline__ void roll_chunk_steps() {
       // (the image base offset by the per-step opaque zero: the fragment addresses are formed inside the step,
       // not hoisted out of the loop into registers that then spill)
       const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr() + tz, ol, xn, h0, cx.eps, ctr, off, 1);
-      if (second && g == 0 && e < E) cx.shx[le] = (uint8_t)a;
+      // behavior blocks: each wave publishes its 16 envs' actions of step t + 1 as soon as its forward is done (every
+      // lane (c, g) holds env c's action): lanes 0-7 / 8-15 OR their nibbles into the two hand-off words of the wave
+      if (second && i + 1 < rc.n) {
+        uint32_t v = ((uint32_t)a & 15u) << (4 * (lane & 7));
+        v |= __shfl_xor(v, 1);
+        v |= __shfl_xor(v, 2);
+        v |= __shfl_xor(v, 4);
+        if (lane == 0 || lane == 8) {
+          uint64_t* hd = rc.hx + (((int64_t)tile * CL + i + 1) * N + agent) * 32 + wave * 2 + (lane >> 3);
+          __hip_atomic_store(hd, ((uint64_t)((uint32_t)cx.seq + 1u) << 32) | v, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     }
     MM_CSTAMP(3);
-    // behavior blocks: publish the actions of step t + 1 for the tile (not after the launch's last step)
-    if (second && i + 1 < rc.n) {
+    // exact-f32 body (8 waves x 32 envs): the actions gathered in LDS, then wave 0 publishes the 32 words
+    if (EXACT && second && i + 1 < rc.n) {
       __syncthreads();
-      if (wave == 0) {
-        const uint32_t w = reinterpret_cast<const uint32_t*>(cx.shx)[lane];   // envs 4 lane .. 4 lane + 3
-        uint32_t* hd = reinterpret_cast<uint32_t*>(rc.hx + (((int64_t)tile * CL + i + 1) * N + agent) * 256);
-        __hip_atomic_store(hd + lane, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store(rc.flags + (int64_t)tile * N + agent, (cx.seq << 16) + (uint64_t)(i + 1), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+      if (wave == 0 && lane < 32) {
+        const uint2 b = reinterpret_cast<const uint2*>(cx.shx)[lane];   // envs 8 lane .. 8 lane + 7
+        uint64_t* hd = rc.hx + (((int64_t)tile * CL + i + 1) * N + agent) * 32 + lane;
+        __hip_atomic_store(hd, ((uint64_t)((uint32_t)cx.seq + 1u) << 32) | nib_pack4(b.x) | (nib_pack4(b.y) << 16),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -3264,7 +3289,7 @@ int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, con
   MM_REQUIRE(sm > 0, "rollout_chunk: configuration not supported (mm_rollout_chunk_supported)");
   const EnvDev& ev = env->d;
   MM_REQUIRE(x->store_obs && x->staging && x->cur_row && x->act0 && x->done_prev && x->rew && x->done && x->counter &&
-                 x->ctl && x->flags && x->handoff, "rollout_chunk: null buffer");
+                 x->ctl && x->handoff, "rollout_chunk: null buffer");
   MM_REQUIRE(x->chunk_len >= 1 && x->chunk_len <= 4096 && x->c0 >= 0 && x->n_steps >= 1 &&
                  x->c0 + x->n_steps <= x->chunk_len, "rollout_chunk: steps [c0, c0 + n) must lie in one chunk");
   MM_REQUIRE(x->n_rows >= 1 && x->n_rows < (1ll << 40), "rollout_chunk: n_rows must be the chunk store's row count");
@@ -3303,8 +3328,7 @@ int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, con
   r.seq = reinterpret_cast<uint64_t*>(x->ctl);
   r.envpar = reinterpret_cast<int32_t*>(x->ctl + 1);
   r.ticket = reinterpret_cast<uint32_t*>(x->ctl + 2);
-  r.flags = reinterpret_cast<uint64_t*>(x->flags);
-  r.hx = x->handoff;
+  r.hx = reinterpret_cast<uint64_t*>(x->handoff);
   r.err = reinterpret_cast<uint32_t*>(x->err);
 #if MM_ROLL_DEBUG
   r.trace = debug_trace_buffer("MM_ROLL_TRACE");

@@ -66,7 +66,7 @@ class RollChunkIO(ctypes.Structure):
         ("c0", c_i32), ("n_steps", c_i32), ("chunk_len", c_i32), ("pad_", c_i32),
         ("act0", c_vp), ("done_prev", c_vp), ("rew", c_vp), ("done", c_vp),
         ("b_off0", c_i64), ("b_offn", c_i64), ("t_off0", c_i64),
-        ("counter", c_vp), ("ctl", c_vp), ("flags", c_vp), ("handoff", c_vp), ("err", c_vp),
+        ("counter", c_vp), ("ctl", c_vp), ("handoff", c_vp), ("err", c_vp),
     ]
 
 

@@ -138,8 +138,8 @@ class RolloutEngine:
             self.done_r = torch.zeros(C, E, dtype=torch.uint8, device=dev)
             # launch state owned by the chunk kernel: launch sequence, env state buffer, arrival ticket
             self.ctl = torch.zeros(3, dtype=torch.int64, device=dev)
-            self.hflags = torch.zeros(T * N, dtype=torch.int64, device=dev)
-            self.hx = torch.zeros(T * C * N * 256, dtype=torch.uint8, device=dev)
+            # tagged hand-off words [T][C][N][32]: (launch sequence + 1) << 32 | 8 envs' 4-bit actions
+            self.hx = torch.zeros(T * C * N * 32, dtype=torch.int64, device=dev)
             self.env.state_buffer = lambda: int(self.ctl[1].item()) & 1
         self._build_io()
         self.env.reset(self.init_obs)
@@ -322,8 +322,7 @@ class RolloutEngine:
         x.done_prev = self.done_r.data_ptr() + ((c0 - 1) % C) * E
         x.rew, x.done = self.rew_r.data_ptr() + 4 * c0 * EN, self.done_r.data_ptr() + c0 * E
         x.b_off0, x.b_offn, x.t_off0 = (k * C + c0 + 1) * EN, (1 - k) * C * EN, c0 * EN
-        x.counter, x.ctl, x.flags, x.handoff, x.err = (ptr(self.counter_dev), ptr(self.ctl), ptr(self.hflags),
-                                                       ptr(self.hx), ptr(self.err))
+        x.counter, x.ctl, x.handoff, x.err = ptr(self.counter_dev), ptr(self.ctl), ptr(self.hx), ptr(self.err)
         self.behavior.pack(s)
         self.target.pack(s)
         check(L.mm_rollout_chunk(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
@@ -649,8 +648,7 @@ class RolloutEngine:
         x.act0, x.done_prev = self.act_r.data_ptr(), self.done_r.data_ptr() + (C - 1) * E
         x.rew, x.done = self.rew_r.data_ptr(), self.done_r.data_ptr()
         x.b_off0, x.b_offn, x.t_off0 = EN, C * EN, 0
-        x.counter, x.ctl, x.flags, x.handoff, x.err = (ptr(self.counter_dev), ptr(self.ctl), ptr(self.hflags),
-                                                       ptr(self.hx), ptr(self.err))
+        x.counter, x.ctl, x.handoff, x.err = ptr(self.counter_dev), ptr(self.ctl), ptr(self.hx), ptr(self.err)
         self.t = t0
         check(lib().mm_rollout_chunk(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
                                      ctypes.byref(self.cio_t), ptr(self.behavior.packed), ctypes.byref(self.cio_b), E,
