@@ -1072,13 +1072,36 @@ __device__ __forceinline__ f32x4 mfma16x16(const f16x8& a, const f16x8& b, f32x4
 struct KS {
   f16x8 h, l;
 };
+#ifndef MM_SPLIT_MIX
+#define MM_SPLIT_MIX 1
+#endif
+typedef _Float16 f16x2_ __attribute__((ext_vector_type(2)));
+typedef float f32x2_ __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split8(const float (&x)[8], KS& t) {
+#if MM_SPLIT_MIX
+  // per pair: hi = v_cvt_pk_f16_f32 (round to nearest even, as (_Float16)x), lo = f16(x - hi) by v_fma_mixlo / mixhi
+  // (fma(hi, -1, x) with hi read as f16 and x as f32: the residual x - hi is exact in f32, rounded once to f16 — the
+  // same bits as (_Float16)(x - (float)hi)); 3 VALU per pair instead of ~5.5
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x2_ v = {x[2 * j], x[2 * j + 1]};
+    hw[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_));
+    uint32_t lo;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hw[j]), "v"(v.x));
+    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hw[j]), "v"(v.y));
+    lw[j] = lo;
+  }
+  t.h = __builtin_bit_cast(f16x8, hw);
+  t.l = __builtin_bit_cast(f16x8, lw);
+#else
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const _Float16 hv = (_Float16)x[j];
     t.h[j] = hv;
     t.l[j] = (_Float16)(x[j] - (float)hv);
   }
+#endif
 }
 // two consecutive 16-row D tiles -> one k-step
 __device__ __forceinline__ void split_pair(const f32x4& a, const f32x4& b, KS& t) {
@@ -1175,17 +1198,33 @@ __device__ __forceinline__ int q_epilogue16(const QFwdParams& p, int agent, int 
   }
   int act = bi;
   if (io.mode == MM_Q_ACT) {
-    float u;
-    if (io.u) {
-      u = valid ? io.u[e] : 1.0f;
+#ifndef MM_RNG_SPLIT
+#define MM_RNG_SPLIT 1
+#endif
+    if (MM_RNG_SPLIT && !io.u && !io.rand_act) {
+      // both device draws of env c in ONE rng_draw sequence: lanes of even g draw the uniform, odd g the random
+      // action (the same (seed, counter, e, b) streams as two calls), exchanged across g by an xor-16 shuffle
+      const bool ra_lane = (g & 1) != 0;
+      const uint64_t r = rng_draw(ra_lane ? io.seed ^ 0x5bd1e995ull : io.seed, ctr, (uint64_t)e,
+                                  ra_lane ? (uint64_t)agent : 0xFFFFFFFFull);
+      const float uu = rng_uniform(r);
+      const int ra = (int)rng_mod_small(r, (uint32_t)p.A);
+      const float uo = __shfl_xor(uu, 16);
+      const int rao = __shfl_xor(ra, 16);
+      if ((ra_lane ? uo : uu) <= eps) act = ra_lane ? ra : rao;
     } else {
-      u = rng_uniform(rng_draw(io.seed, ctr, (uint64_t)e, 0xFFFFFFFFull));
-    }
-    if (u <= eps) {
-      if (io.rand_act) {
-        act = valid ? io.rand_act[(int64_t)e * p.N + agent] : 0;
+      float u;
+      if (io.u) {
+        u = valid ? io.u[e] : 1.0f;
       } else {
-        act = (int)(rng_draw(io.seed ^ 0x5bd1e995ull, ctr, (uint64_t)e, (uint64_t)agent) % (uint64_t)p.A);
+        u = rng_uniform(rng_draw(io.seed, ctr, (uint64_t)e, 0xFFFFFFFFull));
+      }
+      if (u <= eps) {
+        if (io.rand_act) {
+          act = valid ? io.rand_act[(int64_t)e * p.N + agent] : 0;
+        } else {
+          act = (int)(rng_draw(io.seed ^ 0x5bd1e995ull, ctr, (uint64_t)e, (uint64_t)agent) % (uint64_t)p.A);
+        }
       }
     }
   } else if (io.mode == MM_Q_GATHER) {
@@ -1245,7 +1284,7 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
 #pragma unroll
   for (int t = 0; t < T1; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x1[t][r] = fmaxf(x1[t][r], 0.0f);
+    for (int r = 0; r < 4; ++r) x1[t][r] = relu_bits(x1[t][r]);
 #pragma unroll
   for (int kb = 0; kb < RB1; ++kb) split_pair(x1[2 * kb], x1[2 * kb + 1], x1s[kb]);
   float* sv = (io.save && valid) ? io.save + ((int64_t)e * p.N + agent) * (F1 + G + 6 * H) : nullptr;
@@ -1264,7 +1303,7 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
 #pragma unroll
     for (int kb = 0; kb < RB1; ++kb) mm16(W + CG::off_l2 + ((t >> 1) * RB1 + kb) * 1024, t & 1, x1s[kb], lane, x2[t]);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x2[t][r] = fmaxf(x2[t][r], 0.0f);
+    for (int r = 0; r < 4; ++r) x2[t][r] = relu_bits(x2[t][r]);
     if (sv) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) sv[F1 + 16 * t + 4 * g + r] = x2[t][r];
@@ -2566,7 +2605,7 @@ __device__ __forceinline__ void agent_pre_body_h3(const QFwdParams& p, int agent
 #pragma unroll
   for (int t = 0; t < T1; ++t) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x1[t][r] = fmaxf(x1[t][r], 0.0f);
+    for (int r = 0; r < 4; ++r) x1[t][r] = relu_bits(x1[t][r]);
     if (sv) *reinterpret_cast<f32x4*>(sv + 16 * t + 4 * g) = x1[t];
   }
 #pragma unroll
@@ -2579,7 +2618,7 @@ __device__ __forceinline__ void agent_pre_body_h3(const QFwdParams& p, int agent
 #pragma unroll
     for (int kb = 0; kb < RB1; ++kb) mm16(W + CG::off_l2 + ((t >> 1) * RB1 + kb) * 1024, t & 1, x1s[kb], lane, x2[t]);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x2[t][r] = fmaxf(x2[t][r], 0.0f);
+    for (int r = 0; r < 4; ++r) x2[t][r] = relu_bits(x2[t][r]);
     if (sv) *reinterpret_cast<f32x4*>(sv + F1 + 16 * t + 4 * g) = x2[t];
   }
   KS x2s[RB2];

@@ -56,6 +56,19 @@ __device__ __forceinline__ float rollout_td(float sr, float sq, float st, float 
   return fabsf(__fsub_rn(__fadd_rn(sr, boot), sq));
 }
 __device__ __forceinline__ float rng_uniform(uint64_t r) { return (float)(r >> 40) * (1.0f / 16777216.0f); }
+// r % m for 1 <= m <= 65536 in 32-bit arithmetic (exact: r = hi 2^32 + lo, (hi % m)(2^32 % m) + lo % m < 2^32)
+__device__ __forceinline__ uint32_t rng_mod_small(uint64_t r, uint32_t m) {
+  const uint32_t p32 = (0xFFFFFFFFu % m + 1u) % m;   // 2^32 mod m
+  return ((uint32_t)(r >> 32) % m * p32 + (uint32_t)r % m) % m;
+}
+// max(x, 0) on the bit pattern: one v_max_i32 (negative floats are negative integers; no canonicalising v_max_f32
+// pair), equal to fmaxf(x, 0) for every non-NaN x but -0 -> +0
+#ifndef MM_RELU_BITS
+#define MM_RELU_BITS 1
+#endif
+__device__ __forceinline__ float relu_bits(float x) {
+  return MM_RELU_BITS ? __int_as_float(max(__float_as_int(x), 0)) : fmaxf(x, 0.0f);
+}
 
 // Debug timing traces: a static device buffer of 4096 u64 slots, allocated when the named
 // environment variable is set (kernels record clock64() into it); mm_debug_trace copies it out.

@@ -100,6 +100,8 @@ class RolloutEngine:
         self.init_obs = torch.empty(E, N, D, device=dev)
         # hidden states feature-major [N, H, E] (env fastest): the forward's lane = env, so every
         # hidden load / store of a wave is one coalesced 128-byte run per feature row
+        # hidden states [N][H][E] (env-contiguous: a wave's 16 envs of one feature are 64 contiguous bytes; the chunk
+        # kernel reads / writes them with buffer ops at SGPR feature offsets)
         self.h = torch.zeros(N, H, E, device=dev)
         self.ht = torch.zeros(N, H, E, device=dev)
         # ping-pong buffers indexed by step parity: done_t in slot t % 2; act_t, q_taken_t in slot t % nb (nb = 3
@@ -201,9 +203,8 @@ class RolloutEngine:
         b.obs_row = self.cur_row.data_ptr()
         b.reset_obs = self.env.reset_obs_ptr()
         b.h_in = b.h_out = self.h.data_ptr()
-        b.hin_se = b.hout_se = 1
-        b.hin_sa = b.hout_sa = H * self.E
-        b.hin_sf = b.hout_sf = self.E
+        b.hin_sa, b.hin_sf, b.hin_se = self.h.stride()   # (self.h is [N][H][E])
+        b.hout_sa, b.hout_se, b.hout_sf = b.hin_sa, b.hin_se, b.hin_sf
         b.reset = self.done_buf[1 - k].data_ptr()
         b.mode = MM_Q_ACT
         b.act_out, b.qsel_out = self.act_buf[k].data_ptr(), self.qsel_buf[k].data_ptr()
@@ -219,9 +220,8 @@ class RolloutEngine:
         t.obs_row = self.staging.data_ptr()
         t.reset_obs = self.env.reset_obs_ptr()
         t.h_in = t.h_out = self.ht.data_ptr()
-        t.hin_se = t.hout_se = 1
-        t.hin_sa = t.hout_sa = H * self.E
-        t.hin_sf = t.hout_sf = self.E
+        t.hin_sa, t.hin_sf, t.hin_se = self.ht.stride()   # (self.ht is [N][H][E])
+        t.hout_sa, t.hout_se, t.hout_sf = t.hin_sa, t.hin_se, t.hin_sf
         t.reset = self.done_buf[1 - k].data_ptr()
         t.mode = MM_Q_MAX
         t.qsel_out = self.maxq.data_ptr()

@@ -1,7 +1,7 @@
 # chunk kernel hand-off / TD fold change: parity tests, microbenchmark, 20- and 200-step quick benches, kernel stats
 mkdir -p gpurun_out/ho
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_chunk.py tests/test_gpu_fused_step.py tests/test_gpu_headline.py -x -q --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/ho/t.log 2>&1
+timeout -k 10 600 python -u -m pytest tests ${TESTS:--m gpu} -x -q --timeout 150 --timeout-method thread -p no:cacheprovider > gpurun_out/ho/t.log 2>&1
 rc=$?; tail -3 gpurun_out/ho/t.log; grep "^E  \|FAILED" gpurun_out/ho/t.log | head -8; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/mb_chunk.py chunk > gpurun_out/ho/mb_chunk.json 2> gpurun_out/ho/mb_chunk.err || { tail -5 gpurun_out/ho/mb_chunk.err; exit 1; }
 cat gpurun_out/ho/mb_chunk.json

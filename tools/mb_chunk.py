@@ -8,7 +8,12 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mini-marl_amd"))
 import torch  # noqa: E402
+import minimarl._lib as _L  # noqa: E402
 from minimarl.engine import RolloutEngine  # noqa: E402
+
+# A/B: MB_LIB = another build of libminimarl.so; MB_HOLD=neh = hidden states stored [N][E][H] (feature-contiguous)
+if os.environ.get("MB_LIB"):
+    _L.LIB_PATH = os.path.abspath(os.environ["MB_LIB"])
 
 E, N, C, CAP = 4096, 8, 10, 65536
 modes = sys.argv[1:] or ["chunk", "fused"]
@@ -29,6 +34,10 @@ out = {}
 for mode in modes:
     kw = dict(persistent=True) if mode == "chunk" else dict(fused=True)
     eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=C, capacity=CAP, seed=1, device="cuda", **kw)
+    if os.environ.get("MB_HOLD") == "neh":   # feature-contiguous hidden-state storage
+        eng.h = torch.zeros(N, E, 64, device="cuda").permute(0, 2, 1)
+        eng.ht = torch.zeros(N, E, 64, device="cuda").permute(0, 2, 1)
+        eng._build_io()
     while len(eng.per) < CAP:
         eng.run_steps(eng.graph_steps(), 0.5)
     res = {}
@@ -49,7 +58,15 @@ for mode in modes:
         eng.check_errors()
     else:
         res["fused_step_kernel_us"] = 1000 * timed(lambda: eng.fused_step_only(1), 20)
+    # digest of the final state (A/B builds that claim identical arithmetic must agree on it)
+    import hashlib
+    hs = hashlib.sha1()
+    for tsr in (eng.h, eng.ht, eng.store.obs, eng.store.act, eng.chunk_td, eng.per.tree()):
+        hs.update(tsr.contiguous().cpu().numpy().tobytes())
+    res["state_sha1"] = hs.hexdigest()[:16]
     out[mode] = res
     del eng
     torch.cuda.empty_cache()
+out["lib"] = _L.LIB_PATH
+out["hold"] = os.environ.get("MB_HOLD", "0")
 print(json.dumps(out))
