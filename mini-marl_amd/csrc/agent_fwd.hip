@@ -2156,10 +2156,13 @@ __device__ __forceinline__ void roll_chunk_steps() {
   // every per-launch constant is re-derived from the kernarg segment in each step (scalar loads, K$ hits) through
   // a pointer the compiler cannot prove invariant, and every lane index from a thread id it cannot hoist: nothing
   // stays live across the step's forward body (the body's registers are those of rollout_step_kernel's)
-  const QFwdParams* kargs = kargs0;
-  asm volatile("" : "+s"(kargs));
+  // (the opaque offset is added in the kernarg address space, so the parameter reads stay scalar loads: a laundered
+  // generic pointer would turn every one of them into a vector flat load)
   int tz = 0;
   asm volatile("" : "+s"(tz));
+  const QFwdParams* kargs =
+      (const QFwdParams*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() + tz);
+  (void)kargs0;
   const int tx = (int)threadIdx.x + tz;
   const int wave = tx >> 6, lane = tx & 63;
   const ChunkCtx cx = chunk_ctx<F1, G, H, AB>(kargs);

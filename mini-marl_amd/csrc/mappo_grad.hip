@@ -150,10 +150,13 @@ __device__ __forceinline__ void st16(float* p, const float (&v)[16]) {
   for (int g = 0; g < 4; ++g)
     reinterpret_cast<float4*>(p)[g] = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
 }
-// a pointer the compiler cannot see through (no store-to-load forwarding of parked registers)
+// a pointer the compiler cannot see through (no store-to-load forwarding of parked registers), laundered in the global
+// address space: the loads through it stay global_load (a laundered generic pointer makes them flat loads, which
+// also count on lgkmcnt, so every LDS wait after them would wait for their HBM round trip)
 __device__ __forceinline__ const float* opaque_ptr(const float* p) {
-  asm volatile("" : "+v"(p));
-  return p;
+  auto g = (const __attribute__((address_space(1))) float*)p;
+  asm volatile("" : "+v"(g));
+  return (const float*)g;
 }
 
 __device__ __forceinline__ void zero16(f32x16& a) {

@@ -10,7 +10,10 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mini-marl_amd"))
 import torch  # noqa: E402
+import minimarl._lib as _L  # noqa: E402
 
+if os.environ.get("MB_LIB"):   # A/B: another build of libminimarl.so
+    _L.LIB_PATH = os.path.abspath(os.environ["MB_LIB"])
 from minimarl.env import VecEnv  # noqa: E402
 from minimarl.mappo import MappoPolicy, MappoRunner  # noqa: E402
 
