@@ -1261,11 +1261,43 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
   const bool valid = e < p.E;
   const mm_qfwd_io& io = p.io;
   const int ATr = (p.A + 15) / 16;   // Q tiles that hold real actions
+#ifndef MM_LDS_REBASE
+#define MM_LDS_REBASE 1
+#endif
+  // LDS image addressing of the post-layer-1 fragments and the biases: per-lane base pointers every 15360 floats (each
+  // 4 KiB block then lies within the 64 KiB immediate offset of its base) and one for the biases (+ 4 g), made opaque in
+  // the LDS address space, so each ds_read_b128 is base + immediate (no v_add per fragment beyond the first 64 KiB)
+  constexpr int NWB = (CG::off_b1 + 15359) / 15360;
+  auto lds_opaque = [](const float* q) {
+    auto l = (const __attribute__((address_space(3))) float*)q;
+    if (MM_LDS_REBASE) asm volatile("" : "+v"(l));
+    return (const float*)l;
+  };
+  const float* WL[NWB];
+#pragma unroll
+  for (int k = 0; k < NWB; ++k) WL[k] = lds_opaque(W + 15360 * k + lane * 4);
+  const float* WBias = lds_opaque(W + CG::off_b1 + 4 * g);
+  // fragment block at image offset off (compile-time), lane part included / bias tile t of the vector at offset off
+  auto wblk = [&](int off) { return WL[off / 15360] + (off % 15360); };
+  auto wbias = [&](int off, int t) { return *reinterpret_cast<const f32x4*>(WBias + (off - CG::off_b1) + 16 * t); };
+  auto mmb = [&](int off, int q, const KS& x, f32x4& acc) {
+    const f16x8 ah = *reinterpret_cast<const f16x8*>(wblk(off) + (q * 2) * 256);
+    const f16x8 al = *reinterpret_cast<const f16x8*>(wblk(off) + (q * 2 + 1) * 256);
+    acc = mfma16x16(al, x.h, acc);
+    acc = mfma16x16(ah, x.l, acc);
+    acc = mfma16x16(ah, x.h, acc);
+  };
+  auto frag = [&](int off, int q) {
+    Frag f;
+    f.h = *reinterpret_cast<const f16x8*>(wblk(off) + (q * 2) * 256);
+    f.l = *reinterpret_cast<const f16x8*>(wblk(off) + (q * 2 + 1) * 256);
+    return f;
+  };
 
   // ---- layer 1 (K = D in 32-deep k-steps, next obs k-step prefetched)
   f32x4 x1[T1];
 #pragma unroll
-  for (int t = 0; t < T1; ++t) x1[t] = bias4(W + CG::off_b1, t, g);
+  for (int t = 0; t < T1; ++t) x1[t] = wbias(CG::off_b1, t);
   for (int kb = 0; kb < p.g.KD; ++kb) {
     KS ob;
     split8(xn, ob);
@@ -1299,9 +1331,9 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
   f32x4 x2[T2];
 #pragma unroll
   for (int t = 0; t < T2; ++t) {
-    x2[t] = bias4(W + CG::off_b2, t, g);
+    x2[t] = wbias(CG::off_b2, t);
 #pragma unroll
-    for (int kb = 0; kb < RB1; ++kb) mm16(W + CG::off_l2 + ((t >> 1) * RB1 + kb) * 1024, t & 1, x1s[kb], lane, x2[t]);
+    for (int kb = 0; kb < RB1; ++kb) mmb(CG::off_l2 + ((t >> 1) * RB1 + kb) * 1024, t & 1, x1s[kb], x2[t]);
 #pragma unroll
     for (int r = 0; r < 4; ++r) x2[t][r] = relu_bits(x2[t][r]);
     if (sv) {
@@ -1327,14 +1359,14 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
 #pragma unroll
   for (int t = 0; t < TH; ++t) {
     const int rb = t >> 1, q = t & 1;
-    f32x4 ar = bias4(W + CG::off_brz, t, g);
-    f32x4 az = bias4(W + CG::off_brz + H, t, g);
-    f32x4 anx = bias4(W + CG::off_bin, t, g);
-    f32x4 anh = bias4(W + CG::off_bhn, t, g);
+    f32x4 ar = wbias(CG::off_brz, t);
+    f32x4 az = wbias(CG::off_brz + H, t);
+    f32x4 anx = wbias(CG::off_bin, t);
+    f32x4 anh = wbias(CG::off_bhn, t);
     auto tri = [&](int base, int gstride, const KS& x, f32x4& a0, f32x4& a1, f32x4& a2) {
-      const Frag f0 = ldfrag(W + base, q, lane);
-      const Frag f1 = ldfrag(W + base + gstride, q, lane);
-      const Frag f2 = ldfrag(W + base + 2 * gstride, q, lane);
+      const Frag f0 = frag(base, q);
+      const Frag f1 = frag(base + gstride, q);
+      const Frag f2 = frag(base + 2 * gstride, q);
       a0 = mfma16x16(f0.l, x.h, a0);
       a1 = mfma16x16(f1.l, x.h, a1);
       a2 = mfma16x16(f2.l, x.h, a2);
@@ -1433,10 +1465,10 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
   f32x4 qa[AT];
 #pragma unroll
   for (int t = 0; t < AT; ++t) {
-    qa[t] = bias4(W + CG::off_bq, t, g);
+    qa[t] = wbias(CG::off_bq, t);
     if (t < ATr) {
 #pragma unroll
-      for (int kb = 0; kb < HB; ++kb) mm16(W + CG::off_q + ((t >> 1) * HB + kb) * 1024, t & 1, h1s[kb], lane, qa[t]);
+      for (int kb = 0; kb < HB; ++kb) mmb(CG::off_q + ((t >> 1) * HB + kb) * 1024, t & 1, h1s[kb], qa[t]);
     }
   }
   return q_epilogue16<AT>(p, agent, e, valid, qa, eps, ctr, out_off);
@@ -2291,8 +2323,20 @@ __device__ __forceinline__ void roll_chunk_steps() {
       const int st = (int)cx.ssa[le_d] + 1;
       int apples = cx.ssa[256 + le_d];
       float* rout = rc.rew + (int64_t)i * EN + (int64_t)de * N;
+#ifndef MM_DYN_UNROLL
+#define MM_DYN_UNROLL 1
+#endif
+      // (unrolled over the compile-time agent bound: each agent's own target cell is independent of the others, so
+      // the compiler can compute it ahead of the previous agent's LDS round trip; only the grid rows chain them)
+#if MM_DYN_UNROLL
+#pragma unroll
+      for (int k = 0; k < kRollMaxN; ++k) {
+        if (k < N) {
+#else
 #pragma unroll 1
       for (int k = 0; k < N; ++k) {
+        {
+#endif
         const uint32_t w = pq[0] & 0xFFFFu;
         const int a = (int)(aq[0] & 15u);
 #pragma unroll
@@ -2318,7 +2362,8 @@ __device__ __forceinline__ void roll_chunk_steps() {
         const uint32_t B = moved ? w_r : w_p;
         const uint32_t item = upd ? (A >> (4 * cc)) & 15u : 0u;
         const bool big = (k & 1) == 0;
-        const float rk = ev.step_cost + (item == 1u ? (big ? -10.0f : -1.0f) : (item == 2u ? (big ? 10.0f : 1.0f) : 0.0f));
+        const float mag = big ? 10.0f : 1.0f;   // (selects, no branch: item 1 lemon -mag, 2 apple +mag)
+        const float rk = ev.step_cost + (item == 2u ? mag : (item == 1u ? -mag : 0.0f));
         apples -= item == 2u ? 1 : 0;
         const uint32_t clr = upd ? ~(15u << (4 * pc)) : ~0u;
         const uint32_t A1 = pr == r ? (A & clr) : A;
@@ -2326,6 +2371,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
         rows[r] = upd ? ((A1 & ~(15u << (4 * cc))) | ((uint32_t)(3 + k) << (4 * cc))) : A1;
         cx.spq[le_d * N + k] = (uint16_t)((pr << 12) | (pc << 8) | (r << 4) | cc);
         if (writer) rout[k] = rk;
+        }
       }
       const bool dn = st >= ev.max_steps || apples == 0;
       cx.ssa[le_d] = (uint16_t)st;
