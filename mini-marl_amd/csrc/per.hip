@@ -627,8 +627,26 @@ __device__ __forceinline__ int mb_pick(uint32_t* h, int64_t& need, uint32_t* wsu
 }
 
 // arrival ticket of a pass: true in the workgroup that finishes last (its earlier writes and every other
-// workgroup's are then visible to it at device scope)
+// workgroup's are then visible to it at device scope). One lane fences: the workgroup barrier orders every wave's
+// stores before thread 0's agent-scope release (an L2 write-back, not per-lane state), and thread 0's acquire before
+// the barrier that releases the other waves of the last workgroup (MI355X_MICROARCH.md: a fence by every lane of a
+// 1024-thread workgroup costs several times one lane's)
+#ifndef MM_PER_ONE_FENCE
+#define MM_PER_ONE_FENCE 1
+#endif
 __device__ __forceinline__ bool mb_last(uint32_t* ticket, uint32_t* s_last) {
+#if MM_PER_ONE_FENCE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in L2 before the barrier
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const bool l = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    if (l) __threadfence();
+    *s_last = l ? 1u : 0u;
+  }
+  __syncthreads();
+  return *s_last != 0;
+#else
   __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) *s_last = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
@@ -636,6 +654,7 @@ __device__ __forceinline__ bool mb_last(uint32_t* ticket, uint32_t* s_last) {
   const bool last = *s_last != 0;
   if (last) __threadfence();
   return last;
+#endif
 }
 
 // The chunk's last TD / store step (td_chunk_kernel, rollout.hip; cal_td_error + the chunk lists,
