@@ -278,7 +278,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    # MM_BENCH_DIST1=1 (with a launcher's RANK / WORLD_SIZE / MASTER_*): the collective path at world size 1 — on a
+    # one-GPU box this runs the RCCL branch (init with device_id, barriers, the max-over-ranks timing, the gradient
+    # all-reduce, the replica checksums) on the hardware; the numbers equal the N = 1 line's
+    if world > 1 or (os.environ.get("MM_BENCH_DIST1", "0") == "1" and "WORLD_SIZE" in os.environ):
         import torch.distributed as dist
         if shared:
             dist.init_process_group("gloo")

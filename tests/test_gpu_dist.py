@@ -39,3 +39,25 @@ def test_bench_two_ranks_replicas_stay_identical():
     assert line["mappo"]["grad_allreduce"] == "gloo"
     assert all(np.isfinite(v) for v in line["mappo"]["train_info"].values()), line["mappo"]["train_info"]
     assert line["value"] > 0 and np.isfinite(line["train_loop"]["ms_per_episode"])
+
+
+@pytest.mark.timeout(300)
+def test_bench_rccl_branch_world_size_one():
+    """The RCCL branch itself on the box's one GPU: bench.py under torch.distributed.run with one rank and
+    MM_BENCH_DIST1=1 initialises the "nccl" (= RCCL) process group with device_id and runs every collective of the
+    N > 1 path (parameter broadcast, barriers, max-over-ranks timing, the learner / train-loop / MAPPO gradient
+    all-reduces, the all-gathered replica checksums) through RCCL."""
+    env = dict(os.environ, MM_BENCH_DIST1="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", "29531", os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "10",
+           "--warmup", "2", "--repeats", "1", "--learner-steps", "3", "--learner-big-steps", "0", "--train-episodes",
+           "1", "--cfg1-episodes", "0", "--mappo-episodes", "1", "--offq-updates", "0", "--no-cfg5", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["rccl_world_size"] == 1 and line["n_gpus"] == 1
+    assert set(line["replica_checksums"]) == {"qmix_learner_params", "train_loop_learner_params", "mappo_actor",
+                                              "mappo_critic"}
+    assert line["learner"]["grad_allreduce"] == "rccl" and line["mappo"]["grad_allreduce"] == "rccl"
+    assert line["train_loop"]["grad_allreduce"] == "rccl"
+    assert all(np.isfinite(v) for v in line["mappo"]["train_info"].values()), line["mappo"]["train_info"]
