@@ -1252,7 +1252,8 @@ template <int F1, int G, int H, int AB, class OL>
 __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agent, int e,
                                                     const float* __restrict__ W, const OL& ol,
                                                     float (&xn)[8], const f32x4 (&h0)[H / 16], float eps,
-                                                    uint64_t ctr, int64_t out_off = 0, int x16_from_kb = 1 << 30) {
+                                                    uint64_t ctr, int64_t out_off = 0, int x16_from_kb = 1 << 30,
+                                                    f32x4 (*h1_keep)[H / 16] = nullptr, bool store_h = true) {
   using CG = QnetCGeo<F1, G, H, AB>;
   constexpr int T1 = F1 / 16, T2 = G / 16, TH = H / 16, AT = (AB * 32 + 15) / 16;
   constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
@@ -1349,7 +1350,7 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
   KS h0s[HB];
 #pragma unroll
   for (int kb = 0; kb < HB; ++kb) split_pair(h0[2 * kb], h0[2 * kb + 1], h0s[kb]);
-  float* hop = (valid && io.h_out) ? io.h_out + (int64_t)e * io.hout_se + (int64_t)agent * io.hout_sa +
+  float* hop = (valid && io.h_out && store_h) ? io.h_out + (int64_t)e * io.hout_se + (int64_t)agent * io.hout_sa +
                                          (int64_t)(4 * g) * io.hout_sf
                                    : nullptr;
   // GRU: per hidden tile t and k-step, the three gates' fragments are read together and their
@@ -1456,6 +1457,10 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
 #pragma unroll
       for (int r = 0; r < 4; ++r) hop[(int64_t)(16 * t + r) * io.hout_sf] = h1[t][r];
     }
+  }
+  if (h1_keep) {
+#pragma unroll
+    for (int t = 0; t < TH; ++t) (*h1_keep)[t] = h1[t];
   }
   KS h1s[HB];
 #pragma unroll
@@ -2184,6 +2189,14 @@ template <int F1, int G, int H, int AB, bool EXACT>
 __device__ __forceinline__ void roll_chunk_steps() {
   const QFwdParams* kargs0 = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
   const int nsteps = reinterpret_cast<const RollChunk*>(kargs0 + 2)->n;
+#ifndef MM_HREG
+#define MM_HREG 1
+#endif
+  // fp16x3 body: each lane's hidden state stays in registers from one step to the next (the same lane owns the same
+  // (env, agent, features) every step); read from h_in at the launch's first step, written to h_out at its last
+  f32x4 hkeep[H / 16];
+#pragma unroll
+  for (int t = 0; t < H / 16; ++t) hkeep[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int i = 0; i < nsteps; ++i) {
   // every per-launch constant is re-derived from the kernarg segment in each step (scalar loads, K$ hits) through
   // a pointer the compiler cannot prove invariant, and every lane index from a thread id it cannot hoist: nothing
@@ -2419,12 +2432,15 @@ __device__ __forceinline__ void roll_chunk_steps() {
       const int ec = min(e, E - 1);
       const int g = lane >> 4;
       f32x4 h0[H / 16];
-      {
+      if (!MM_HREG || i == 0) {
         const float* hp = io.h_in + (int64_t)ec * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)(4 * g) * io.hin_sf;
 #pragma unroll
         for (int t = 0; t < H / 16; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) h0[t][r] = hp[(int64_t)(16 * t + r) * io.hin_sf];
+      } else {
+#pragma unroll
+        for (int t = 0; t < H / 16; ++t) h0[t] = hkeep[t];
       }
       const bool rt = !second && e < E && cx.sdone[prv * 256 + le];
       const bool bd = second && e < E && cx.sdone[cur * 256 + le];
@@ -2454,7 +2470,8 @@ __device__ __forceinline__ void roll_chunk_steps() {
         for (int s = 0; s < p.stagger; ++s) __builtin_amdgcn_s_sleep(8);
       // (the image base offset by the per-step opaque zero: the fragment addresses are formed inside the step,
       // not hoisted out of the loop into registers that then spill)
-      const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr() + tz, ol, xn, h0, cx.eps, ctr, off, 1);
+      const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr() + tz, ol, xn, h0, cx.eps, ctr, off, 1,
+                                                      MM_HREG ? &hkeep : nullptr, !MM_HREG || i + 1 == nsteps);
       // behavior blocks: each wave publishes its 16 envs' actions of step t + 1 as soon as its forward is done (every
       // lane (c, g) holds env c's action): lanes 0-7 / 8-15 OR their nibbles into the two hand-off words of the wave
       if (second && i + 1 < rc.n) {
