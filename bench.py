@@ -717,12 +717,13 @@ def main():
         flops *= eng.C
         kname = "rollout_chunk_kernel"
         RC = eng.env.rows * eng.env.cols
-        # algorithmic HBM bytes per launch: per step and agent-step the stored s'_t 4D, hidden in / out of both
-        # nets 16H, behavior act / Q(a) out 8, max Q' out 4, reward out 4; per step and env done 1 + cur_row 8;
-        # per launch and agent-step the first actions in 4 and the position word in / out 8; per launch and env
-        # the grid in / out 2RC, step / apple counters in / out 16, store row in 8 (the weight images, LDS-resident
-        # for the launch, and the tile-local action hand-off, <= 2N bytes per agent-step, are not counted)
-        alg_bytes = eng.C * (E * N * (4 * D + 16 * Hh + 16) + E * 9) + E * N * 12 + E * (2 * RC + 24)
+        # algorithmic HBM bytes per launch: per step and agent-step the stored s'_t 4D, behavior act / Q(a) out 8,
+        # max Q' out 4, reward out 4; per step and env done 1 + cur_row 8; per launch and agent-step the hidden
+        # states of both nets in / out 16H (register-resident across the launch's steps), the first actions in 4 and
+        # the position word in / out 8; per launch and env the grid in / out 2RC, step / apple counters in / out 16,
+        # store row in 8 (the weight images, LDS-resident for the launch, and the tile-local action hand-off,
+        # <= 2N bytes per agent-step, are not counted)
+        alg_bytes = eng.C * (E * N * (4 * D + 16) + E * 9) + E * N * (16 * Hh + 12) + E * (2 * RC + 24)
         kdesc = (f"{kname}<64,64,64,1> (C = {eng.C} rollout steps per launch: env step + dual forward, "
                  "chunk-persistent)")
     elif eng.fused:

@@ -16,7 +16,7 @@ done
 python3 tools/pmc_fwd_sum.py $O rollout_chunk_kernel "rollout_chunk_kernel<64,64,64,1> (10 rollout steps per launch; grid 262144 = 256 blocks x 1024)" > $O/summary_sq.json || exit 1
 timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/fetch -- python3 tools/mb_chunk_pmc.py > $O/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
 timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $O/write -- python3 tools/mb_chunk_pmc.py > $O/write.log 2>&1 || { echo "write pass failed"; exit 1; }
-# algorithmic bytes of one C = 10 launch at 4096 x 8 (D 47, H 64, 12 x 8 grid), bench.py's formula:
-# 10 (32768 (188 + 1024 + 16) + 4096 x 9) + 32768 x 12 + 4096 (192 + 24)
-python3 tools/pmc_traffic.py $O/fetch $O/write rollout_chunk_kernel 262144 404037632 $O/pmc_rollout_chunk.json \
+# algorithmic bytes of one C = 10 launch at 4096 x 8 (D 47, H 64, 12 x 8 grid), bench.py's formula (hidden states
+# in / out once per launch): 10 (32768 (188 + 16) + 4096 x 9) + 32768 (1024 + 12) + 4096 (192 + 24)
+python3 tools/pmc_traffic.py $O/fetch $O/write rollout_chunk_kernel 262144 102047744 $O/pmc_rollout_chunk.json \
   "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace --output-format csv -- python3 tools/mb_chunk_pmc.py (two separate passes)"
