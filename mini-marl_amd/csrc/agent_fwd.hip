@@ -1669,6 +1669,34 @@ __device__ __forceinline__ uint64_t roll_obs_word(const uint32_t* rows, int R, i
   }
   return word;
 }
+// roll_obs_word shared by the 4 lanes (c, g = 0..3) of one env in the fp16x3 layout: lane group g < 3 builds the 3 cells
+// of grid row r - 1 + g (bits 2 + 15 g .. 16 + 15 g of the word), and two v_permlane16/32_swap ORs per dword combine
+// the groups (the 4 lanes of an env differ in lane bits 4 and 5) — the same word, one row read and ~1/3 of the ALU
+// per lane. Every lane of the wave must be active.
+__device__ __forceinline__ uint64_t roll_obs_word_g(const uint32_t* rows, int R, int r, int c, int g) {
+  const int rr = r - 1 + g;
+  const uint32_t w = (g < 3 && rr >= 0 && rr < R) ? rows[rr] : 0u;
+  const uint32_t f12 = (c > 0 ? (w >> (4 * c - 4)) : (w << 4)) & 0xFFFu;   // cells c-1, c, c+1
+  constexpr uint64_t kLut = 0x4848484848484210ull;   // item -> {lemon 1, apple 2, even agent 4, odd agent 8}
+  uint32_t f15 = 0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const uint32_t it = (f12 >> (4 * j)) & 15u;
+    f15 |= (uint32_t)((kLut >> (4 * it)) & 15ull) << (5 * j);
+  }
+  uint32_t lo = g < 2 ? f15 << (2 + 15 * g) : 0u, hi = g == 2 ? f15 : 0u;
+  auto or16 = [](uint32_t v) {
+    const auto x = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return x[0] | x[1];
+  };
+  auto or32 = [](uint32_t v) {
+    const auto x = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return x[0] | x[1];
+  };
+  lo = or32(or16(lo));
+  hi = or32(or16(hi));
+  return ((uint64_t)hi << 32) | lo;
+}
 // features f0 .. f0 + 3 of the word into x[0..3] (the coordinates for f < 2)
 __device__ __forceinline__ void roll_feat4(uint64_t word, int f0, float cr, float cc, float* x) {
   const uint32_t fld = f0 < 64 ? (uint32_t)(word >> f0) : 0u;
@@ -2451,7 +2479,11 @@ __device__ __forceinline__ void roll_chunk_steps() {
       float* dst = (!second && srow >= 0) ? rc.store_obs + srow * rc.row_stride + nxt_off + (int64_t)agent * D : nullptr;
       const int ls = e < E ? le : 0;
       const int rcw = cx.spq[ls * N + agent] & 0xFF;
-      const uint64_t wd = roll_obs_word(cx.sgrid + ls * roll_gbw(R), R, rcw >> 4, rcw & 15);
+#ifndef MM_OBS_SPLIT
+#define MM_OBS_SPLIT 1
+#endif
+      const uint64_t wd = MM_OBS_SPLIT ? roll_obs_word_g(cx.sgrid + ls * roll_gbw(R), R, rcw >> 4, rcw & 15, g)
+                                       : roll_obs_word(cx.sgrid + ls * roll_gbw(R), R, rcw >> 4, rcw & 15);
       const float cr = cx.stab[rcw >> 4], cc = cx.stab[R + (rcw & 15)];
       auto ol = [&](int kb, float (&x)[8]) {
 #pragma unroll
