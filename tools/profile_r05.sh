@@ -2,7 +2,7 @@
 # Round-5 profile on the GPU box (via gpurun from the repo root). Each step bounded, chained with &&.
 # Outputs under gpurun_out/prof5/; the summaries are copied into profiles/r05_*.
 export TMPDIR=/tmp
-O=gpurun_out/prof5
+O=${O:-gpurun_out/prof5}
 mkdir -p $O
 Q="--steps 40 --warmup 10 --repeats 1 --learner-steps 10 --learner-big-steps 0 --train-episodes 0 --cfg1-episodes 0 --mappo-episodes 0 --offq-updates 0 --no-cfg5 --no-cpu-baseline"
 timeout -k 10 600 python -u bench.py > $O/bench_default.log 2> $O/bench_default.err && \
