@@ -322,6 +322,14 @@ int mm_chunk_begin_rows(int64_t n_envs, int32_t nd, float* store_obs, int64_t ro
 /* PER insert with store-row indirection: slot_row[slot] <-> rows_inout[j] (the evicted row is handed
  * back as the next staging row; chunk data is never copied). */
 int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s);
+/* mm_td_fold_range of the chunk's last span (slot0 + n_slots == chunk_len) followed by mm_per_insert(per, chunk_td, k,
+ * rows_inout = the staging rows, slots_out), with the fold's workgroups beside the insert's first histogram pass in ONE
+ * launch (the chunk-persistent rollout's chunk end; same results as the two calls). */
+int mm_per_insert_fold(mm_per* per, int64_t k, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                       const float* q_taken, const float* max_q_next, const int32_t* act, int64_t ring_se,
+                       int32_t slot0, int32_t n_slots, int32_t chunk_len, float* chunk_td, uint8_t* store_act,
+                       float* store_rew, uint8_t* store_done, int64_t* rows_inout, int64_t n_rows, int32_t* err,
+                       int64_t* slots_out, mm_stream_t s);
 /* The chunk's last rollout step: mm_td_chunk_step_rows of the k envs (slot step_in_chunk of store rows
  * rows_inout, before the swap) followed by mm_per_insert(per, chunk_td, k, rows_inout, slots_out). For the
  * multi-block insert (power-of-two capacity >= 16384) the TD / store runs inside the insert's first launch

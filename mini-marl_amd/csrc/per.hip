@@ -25,6 +25,7 @@
 #include "common.h"
 #include "minimarl.h"
 #include "per_small.h"
+#include "rollout_fold.h"
 
 namespace mm {
 
@@ -696,20 +697,19 @@ __device__ void mb_td_fold(TdFuse t, int64_t E, int N, float (*sh)[MB_T]) {
   }
 }
 
-__global__ __launch_bounds__(MB_T) void per_mb_sel1(const double* __restrict__ tree, int64_t cap, const PerDev* st,
-                                                    int64_t K, MbScratch* mb, TdFuse tdf, int32_t td_n) {
+// pass A's histogram part, run by workgroup b of the nb histogram workgroups
+__device__ __forceinline__ void mb_sel1_hist(const double* __restrict__ tree, int64_t cap, const PerDev* st, int64_t K,
+                                             MbScratch* mb, int b, int nb) {
   __shared__ uint32_t h[4096];
-  __shared__ float shtd[3][MB_T];
-  if (tdf.on) mb_td_fold(tdf, K, td_n, shtd);
   // the candidate list of the previous insert was last read by its apply launch, which has finished
-  if (blockIdx.x == 0 && threadIdx.x == 0) mb->cand_n = 0;
-  for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist3[i] = 0;
+  if (b == 0 && threadIdx.x == 0) mb->cand_n = 0;
+  for (int i = b * MB_T + threadIdx.x; i < 4096; i += nb * MB_T) mb->hist3[i] = 0;
   const int64_t n_data = st->n_data;
   if (K - min(K, cap - n_data) <= 0) return;
   const double* leaves = tree + (cap - 1);
   for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+  const int64_t base = (int64_t)b * MB_SLOTS;
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = base + threadIdx.x + i * MB_T;
@@ -718,6 +718,27 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel1(const double* __restrict__ t
   __syncthreads();
   for (int i = threadIdx.x; i < 4096; i += MB_T)
     if (h[i]) atomicAdd(&mb->hist1[i], h[i]);
+}
+
+__global__ __launch_bounds__(MB_T) void per_mb_sel1(const double* __restrict__ tree, int64_t cap, const PerDev* st,
+                                                    int64_t K, MbScratch* mb, TdFuse tdf, int32_t td_n) {
+  __shared__ float shtd[3][MB_T];
+  if (tdf.on) mb_td_fold(tdf, K, td_n, shtd);
+  mb_sel1_hist(tree, cap, st, K, mb, blockIdx.x, gridDim.x);
+}
+
+// pass A with the chunk-persistent rollout's TD / store fold of the chunk's last span (rollout_fold.h) in the same
+// grid: workgroups [0, nh) build the histogram of the existing leaves, the rest fold 16 envs each. Independent work
+// (the histogram reads only leaves, the fold writes chunk_td and the store rows that only apply reads), one launch
+// instead of two.
+template <bool VEC>
+__global__ __launch_bounds__(MB_T) void per_mb_sel1_fold(const double* __restrict__ tree, int64_t cap,
+                                                         const PerDev* st, int64_t K, MbScratch* mb, int nh,
+                                                         FoldArgs fa) {
+  if ((int)blockIdx.x < nh)
+    mb_sel1_hist(tree, cap, st, K, mb, blockIdx.x, nh);
+  else
+    td_fold_group<VEC>(fa, (int)blockIdx.x - nh);
 }
 
 // Every workgroup of sel2 / sel3 / apply re-derives the previous pass's decision itself from the finished
@@ -1092,13 +1113,19 @@ __global__ __launch_bounds__(MB_T) void per_td_fold_kernel(TdFuse tdf, int64_t E
 }
 
 static int per_insert_mb(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out,
-                         const TdFuse* tdf, int32_t td_n, hipStream_t s) {
+                         const TdFuse* tdf, int32_t td_n, hipStream_t s, const FoldArgs* fold = nullptr) {
   const int64_t cap = per->cap;
   const int G = (int)(cap / MB_SLOTS);
   MbScratch* mb = static_cast<MbScratch*>(per->mb);
   TdFuse t{};
   if (tdf) t = *tdf;
-  hipLaunchKernelGGL(per_mb_sel1, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, t, td_n);
+  if (fold) {
+    const int fb = (fold->E + 15) / 16;
+    auto kern = fold_vec_ok(*fold) ? per_mb_sel1_fold<true> : per_mb_sel1_fold<false>;
+    hipLaunchKernelGGL(kern, dim3(G + fb), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, G, *fold);
+  } else {
+    hipLaunchKernelGGL(per_mb_sel1, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, t, td_n);
+  }
   hipLaunchKernelGGL(per_mb_sel2, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
   hipLaunchKernelGGL(per_mb_sel3, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
   hipLaunchKernelGGL(per_mb_apply, dim3(G), dim3(MB_T), 0, s, per->tree, per->slot_row, cap, per->st, td, k,
@@ -1222,6 +1249,32 @@ static int per_insert_impl(mm_per* per, const float* td, int64_t k, int64_t* row
 
 int mm_per_insert(mm_per* per, const float* td, int64_t k, int64_t* rows_inout, int64_t* slots_out, mm_stream_t s) {
   return per_insert_impl(per, td, k, rows_inout, slots_out, nullptr, 0, (hipStream_t)s);
+}
+
+int mm_per_insert_fold(mm_per* per, int64_t k, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
+                       const float* q_taken, const float* max_q_next, const int32_t* act, int64_t ring_se,
+                       int32_t slot0, int32_t n_slots, int32_t chunk_len, float* chunk_td, uint8_t* store_act,
+                       float* store_rew, uint8_t* store_done, int64_t* rows_inout, int64_t n_rows, int32_t* err,
+                       int64_t* slots_out, mm_stream_t s) {
+  MM_REQUIRE(per && rew && done && q_taken && max_q_next && act && chunk_td && store_act && store_rew && store_done &&
+                 rows_inout, "per_insert_fold: null argument");
+  MM_REQUIRE(n_slots >= 1 && n_slots <= 16 && slot0 >= 0 && slot0 + n_slots == chunk_len,
+             "per_insert_fold: the slots [slot0, slot0 + n) must end the chunk, n <= 16");
+  MM_REQUIRE(n_agents >= 1 && n_agents <= 256 && ring_se >= k * n_agents, "per_insert_fold: bad agents / ring");
+  MM_REQUIRE(k >= 1 && k <= per->cap, "per_insert_fold: batch %lld outside [1, capacity]", (long long)k);
+  if (!per->mb) {   // (the single-workgroup insert paths: the fold as its own launch, then the insert)
+    const int rc = mm_td_fold_range(k, n_agents, gamma, rew, done, q_taken, max_q_next, act, ring_se, slot0, n_slots,
+                                    chunk_len, chunk_td, store_act, store_rew, store_done, rows_inout, n_rows, err, s);
+    if (rc) return rc;
+    return per_insert_impl(per, chunk_td, k, rows_inout, slots_out, nullptr, 0, (hipStream_t)s);
+  }
+  const mm::FoldArgs fa{rew, done, q_taken, max_q_next, act, chunk_td, store_act, store_rew, store_done, rows_inout,
+                        reinterpret_cast<uint32_t*>(err), ring_se, n_rows, (int)k, n_agents, slot0, n_slots,
+                        chunk_len, gamma};
+  const int rc = mm::per_insert_mb(per, chunk_td, k, rows_inout, slots_out, nullptr, 0, (hipStream_t)s, &fa);
+  if (rc) return rc;
+  per->n_data = std::min(per->cap, per->n_data + k);
+  return MM_OK;
 }
 
 int mm_per_insert_td(mm_per* per, int64_t k, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,

@@ -9,6 +9,7 @@
 // HBM-bound, one thread per env; sums over agents in registers.
 #include "common.h"
 #include "minimarl.h"
+#include "rollout_fold.h"
 
 namespace mm {
 
@@ -56,76 +57,11 @@ __global__ __launch_bounds__(256) void td_chunk_kernel(int E, int N, float gamma
   }
 }
 
-// The TD / store of n consecutive steps of a chunk (the chunk-persistent rollout's fold, mm_td_fold_range):
-// thread (slot j, env) computes td_chunk_kernel's per-step value (agent-order sums) and stores the step's act / rew /
-// done; then one thread per env accumulates the chunk priority over the slots in order (the same float additions as
-// n consecutive td_chunk_kernel launches). Block = 16 envs x n slots (E / 16 blocks: every CU takes a share of the
-// scattered store-row writes, which bound this kernel); VEC (N % 4 == 0, 16-byte aligned rings / store rows): the
-// agent values as float4 / int4 loads and the store rows written as float4 / packed-byte words, same values.
+// The TD / store of n consecutive steps of a chunk (the chunk-persistent rollout's fold, mm_td_fold_range): one
+// 16-env group per block (rollout_fold.h), E / 16 blocks
 template <bool VEC>
-__global__ __launch_bounds__(256) void td_fold_range_kernel(int E, int N, float gamma, const float* __restrict__ rew,
-                                                            const uint8_t* __restrict__ done,
-                                                            const float* __restrict__ q_taken,
-                                                            const float* __restrict__ maxq_next,
-                                                            const int32_t* __restrict__ act, int64_t ring_se,
-                                                            int slot0, int n, int C, float* __restrict__ chunk_td,
-                                                            uint8_t* __restrict__ s_act, float* __restrict__ s_rew,
-                                                            uint8_t* __restrict__ s_done,
-                                                            const int64_t* __restrict__ rows, int64_t n_rows,
-                                                            uint32_t* err) {
-  __shared__ float tdv[16][16];
-  const int j = threadIdx.x >> 4, le = threadIdx.x & 15;
-  const int e = blockIdx.x * 16 + le;
-  const bool on = e < E && j < n;
-  if (on) {
-    const int t = slot0 + j;
-    const int64_t o = (int64_t)j * ring_se + (int64_t)e * N;
-    const int64_t row = rows[e];
-    const uint8_t d8 = done[(int64_t)j * E + e];
-    const bool rok = row >= 0 && row < n_rows;
-    const int64_t so = (row * C + t) * N;
-    float sr = 0.f, sq = 0.f, st = 0.f;   // agent order, like the reference's sum over dim 1
-    if constexpr (VEC) {
-      for (int k = 0; k < N; k += 4) {
-        const float4 r4 = *reinterpret_cast<const float4*>(rew + o + k);
-        const float4 q4 = *reinterpret_cast<const float4*>(q_taken + o + k);
-        const float4 m4 = *reinterpret_cast<const float4*>(maxq_next + o + k);
-        const int4 a4 = *reinterpret_cast<const int4*>(act + o + k);
-        sr += r4.x; sr += r4.y; sr += r4.z; sr += r4.w;
-        sq += q4.x; sq += q4.y; sq += q4.z; sq += q4.w;
-        st += m4.x; st += m4.y; st += m4.z; st += m4.w;
-        if (rok) {
-          *reinterpret_cast<float4*>(s_rew + so + k) = r4;
-          *reinterpret_cast<uint32_t*>(s_act + so + k) = (uint32_t)(a4.x & 255) | ((uint32_t)(a4.y & 255) << 8) |
-                                                          ((uint32_t)(a4.z & 255) << 16) | ((uint32_t)a4.w << 24);
-        }
-      }
-    } else {
-      for (int k = 0; k < N; ++k) {
-        const float r = rew[o + k];
-        sr += r;
-        sq += q_taken[o + k];
-        st += maxq_next[o + k];
-        if (rok) {
-          s_act[so + k] = (uint8_t)act[o + k];
-          s_rew[so + k] = r;
-        }
-      }
-    }
-    const float d = d8 ? 1.0f : 0.0f;
-    tdv[j][le] = rollout_td(sr, sq, st, d, gamma);
-    if (rok) {
-      s_done[row * C + t] = d8;
-    } else if (err) {
-      atomicOr(err, 1u);
-    }
-  }
-  __syncthreads();
-  if (j == 0 && e < E) {
-    float ctd = slot0 == 0 ? 0.0f : chunk_td[e];
-    for (int jj = 0; jj < n; ++jj) ctd = (slot0 + jj == 0 ? 0.0f : ctd) + tdv[jj][le];
-    chunk_td[e] = ctd;
-  }
+__global__ __launch_bounds__(256) void td_fold_range_kernel(FoldArgs a) {
+  td_fold_group<VEC>(a, blockIdx.x);
 }
 
 // chunk begin: obs_cur [E][ND] -> store slot 0 of each env's staging row
@@ -288,14 +224,12 @@ int mm_td_fold_range(int64_t n_envs, int32_t n_agents, float gamma, const float*
              "td_fold_range: slots [slot0, slot0 + n) must lie in one chunk, n <= 16");
   MM_REQUIRE(n_agents >= 1 && n_agents <= 256 && ring_se >= n_envs * n_agents, "td_fold_range: bad agents / ring");
   if (n_envs <= 0) return MM_OK;
+  mm::FoldArgs a{rew, done, q_taken, max_q_next, act, chunk_td, store_act, store_rew, store_done, rows,
+                 reinterpret_cast<uint32_t*>(err), ring_se, n_rows, (int)n_envs, n_agents, slot0, n_slots, chunk_len,
+                 gamma};
   const int blocks = (int)((n_envs + 15) / 16);
-  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  const bool vec = n_agents % 4 == 0 && ring_se % 4 == 0 && a16(rew) && a16(q_taken) && a16(max_q_next) &&
-                   a16(act) && a16(store_rew) && ((uintptr_t)store_act & 3) == 0;
-  auto kern = vec ? mm::td_fold_range_kernel<true> : mm::td_fold_range_kernel<false>;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(16 * n_slots), 0, (hipStream_t)s, (int)n_envs, n_agents, gamma, rew,
-                     done, q_taken, max_q_next, act, ring_se, slot0, n_slots, chunk_len, chunk_td, store_act,
-                     store_rew, store_done, rows, n_rows, reinterpret_cast<uint32_t*>(err));
+  auto kern = mm::fold_vec_ok(a) ? mm::td_fold_range_kernel<true> : mm::td_fold_range_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(16 * n_slots), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

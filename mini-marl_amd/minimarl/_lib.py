@@ -120,6 +120,8 @@ _SIGS = [
     ("mm_per_destroy", None, [c_vp]),
     ("mm_per_add_batch", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     ("mm_per_insert", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ("mm_per_insert_fold", c_i32, [c_vp, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32,
+                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     ("mm_per_insert_td", c_i32, [c_vp, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
                                  c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("mm_per_sample", c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -328,15 +328,15 @@ class RolloutEngine:
         check(L.mm_rollout_chunk(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
                                  ctypes.byref(self.cio_t), ptr(self.behavior.packed), ctypes.byref(self.cio_b), E,
                                  ctypes.byref(x), s), "rollout_chunk")
-        check(L.mm_td_fold_range(E, N, self.gamma, self.rew_r.data_ptr() + 4 * c0 * EN,
-                                 self.done_r.data_ptr() + c0 * E, self.qsel_r.data_ptr() + 4 * ia * EN,
-                                 self.maxq_r.data_ptr() + 4 * c0 * EN, self.act_r.data_ptr() + 4 * ia * EN, EN, c0, n,
-                                 C, ptr(self.chunk_td), ptr(self.store.act), ptr(self.store.rew),
-                                 ptr(self.store.done), ptr(self.staging), self.store.rows, ptr(self.err), s),
-              "td_fold_range")
-        if c0 + n == C:
-            check(L.mm_per_insert(self.per._h, ptr(self.chunk_td), E, ptr(self.staging), None, s), "per_insert")
+        fold = (E, N, self.gamma, self.rew_r.data_ptr() + 4 * c0 * EN, self.done_r.data_ptr() + c0 * E,
+                self.qsel_r.data_ptr() + 4 * ia * EN, self.maxq_r.data_ptr() + 4 * c0 * EN,
+                self.act_r.data_ptr() + 4 * ia * EN, EN, c0, n, C, ptr(self.chunk_td), ptr(self.store.act),
+                ptr(self.store.rew), ptr(self.store.done), ptr(self.staging), self.store.rows, ptr(self.err))
+        if c0 + n == C:   # the chunk's end: its last span's TD / store fold rides in the PER insert's first launch
+            check(L.mm_per_insert_fold(self.per._h, *fold, None, s), "per_insert_fold")
             self.chunks_inserted += E
+        else:
+            check(L.mm_td_fold_range(*fold, s), "td_fold_range")
         self._td_pending = False
         self.t += n
 
