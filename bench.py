@@ -341,6 +341,12 @@ def main():
         reps.append(el)
     elapsed = float(np.median(reps))
     steps = args.steps
+    # the device error words of the timed rollout (untimed poll): bit 0 a staging row outside the chunk store, bit 1 a
+    # chunk-persistent hand-off wait that expired (its blocks were not co-resident), bit 8 a PER tree-node guard; any
+    # set bit means the timed regions did not run the path as specified, and the line is not printed
+    errors = int(eng.err.item()) | (eng.per.error_word(clear=False) << 8)
+    if errors:
+        raise SystemExit(f"bench.py: rollout device error bits {errors:#x} after the timed regions")
     value = steps * E * N * world / elapsed
 
     # learner: one QMIX update = PER sample (B chunks) -> C-step fwd/BPTT -> [RCCL all-reduce of the
@@ -771,6 +777,9 @@ def main():
         cpu = cpu_baseline(E, N, F1, G, Hh)
         cpu_l = cpu_learner_baseline(N, D, B=args.batch, C=10, H=Hh, Hm=64)
 
+    errors |= int(eng.err.item()) | (eng.per.error_word(clear=False) << 8)   # (the learner's PER updates too)
+    if errors:
+        raise SystemExit(f"bench.py: device error bits {errors:#x} after the learner / other lines")
     if rank == 0:
         line = {
             "metric": "agent-env-steps/sec (4096 envs x 8 agents per GPU, QMIX GRU-64 rollout step)",
@@ -791,6 +800,7 @@ def main():
                                                                             "graph per timed region",
                        "parallelism": f"env-shard x{world}"},
             "rccl_world_size": world,
+            "errors": errors,
             "replica_checksums": replicas,
             "learner_updates_per_s": round(upd_per_s, 1),
             "learner": {"algo": "QMIX Train_dqn update", "batch_chunks": args.batch, "chunk": 10,

@@ -299,10 +299,24 @@ int mm_rollout_chunk_supported(const mm_env* env, const mm_qnet_dims* d, int64_t
 int mm_rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
                      const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_chunk_io* x,
                      mm_stream_t s);
+/* Co-residency contract of mm_rollout_chunk: NOTHING else may run on the device while it runs (no kernel on another
+ * stream, no collective, no other process's work), because its blocks wait for each other's hand-off words. A launch
+ * that was not fully co-resident completes (every wait expires after 20 ms) with bit 1 of *err set: its rollout data
+ * is then invalid and the caller must stop (RolloutEngine.check_errors raises). Keep collectives stream-ordered on the
+ * rollout stream, or outside the rollout's graph launches.
+ * Diagnostic for that path: mm_hold_cus occupies n_blocks CUs (one 1024-thread workgroup with 64 KiB of LDS each) for
+ * `ticks` of the 100 MHz clock; *seen (device int32) |= 2 if one of the n_watch handoff words carries `tag` in its
+ * high 32 bits when a workgroup starts, |= 1 if one does when it ends (1 alone: a chunk launch ran beside it). */
+int mm_hold_cus(int32_t n_blocks, int64_t ticks, const int64_t* watch, int64_t n_watch, uint32_t tag, int32_t* seen,
+                mm_stream_t s);
+/* Large-batch learner kernel shapes (process-wide, default 1 / 1): at B >= 512 the mixer forward and its recurrence
+ * backward run 8 samples per block and the agent backward 8 samples per wave; 0 selects the one-sample kernels
+ * (identical results, slower). */
+int mm_learner_set_multi_sample(int32_t mixer, int32_t agent_bwd);
 /* The TD / chunk-store fold of n_slots consecutive rollout steps slot0 .. slot0 + n_slots - 1 of a chunk (what
  * n_slots mm_td_chunk_step_rows calls do, identical results; cal_td_error + the chunk lists, vdn/_utils.py:44-52,
  * vdn/main.py:140-167): step j's rew / q_taken / max_q_next / act at + j ring_se elements, done at + j n_envs; rows
- * outside [0, n_rows) are skipped and set bit 0 of *err (may be NULL). At most 16 slots per call. */
+ * outside [0, n_rows) are skipped and set bit 0 of *err (may be NULL). Any span length (groups of 16 slots). */
 int mm_td_fold_range(int64_t n_envs, int32_t n_agents, float gamma, const float* rew, const uint8_t* done,
                      const float* q_taken, const float* max_q_next, const int32_t* act, int64_t ring_se,
                      int32_t slot0, int32_t n_slots, int32_t chunk_len, float* chunk_td, uint8_t* store_act,

@@ -2217,9 +2217,6 @@ template <int F1, int G, int H, int AB, bool EXACT>
 __device__ __forceinline__ void roll_chunk_steps() {
   const QFwdParams* kargs0 = (const QFwdParams*)__builtin_amdgcn_kernarg_segment_ptr();
   const int nsteps = reinterpret_cast<const RollChunk*>(kargs0 + 2)->n;
-#ifndef MM_HREG
-#define MM_HREG 1
-#endif
   // fp16x3 body: each lane's hidden state stays in registers from one step to the next (the same lane owns the same
   // (env, agent, features) every step); read from h_in at the launch's first step, written to h_out at its last
   f32x4 hkeep[H / 16];
@@ -2364,20 +2361,11 @@ __device__ __forceinline__ void roll_chunk_steps() {
       const int st = (int)cx.ssa[le_d] + 1;
       int apples = cx.ssa[256 + le_d];
       float* rout = rc.rew + (int64_t)i * EN + (int64_t)de * N;
-#ifndef MM_DYN_UNROLL
-#define MM_DYN_UNROLL 1
-#endif
       // (unrolled over the compile-time agent bound: each agent's own target cell is independent of the others, so
       // the compiler can compute it ahead of the previous agent's LDS round trip; only the grid rows chain them)
-#if MM_DYN_UNROLL
 #pragma unroll
       for (int k = 0; k < kRollMaxN; ++k) {
         if (k < N) {
-#else
-#pragma unroll 1
-      for (int k = 0; k < N; ++k) {
-        {
-#endif
         const uint32_t w = pq[0] & 0xFFFFu;
         const int a = (int)(aq[0] & 15u);
 #pragma unroll
@@ -2460,7 +2448,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       const int ec = min(e, E - 1);
       const int g = lane >> 4;
       f32x4 h0[H / 16];
-      if (!MM_HREG || i == 0) {
+      if (i == 0) {
         const float* hp = io.h_in + (int64_t)ec * io.hin_se + (int64_t)agent * io.hin_sa + (int64_t)(4 * g) * io.hin_sf;
 #pragma unroll
         for (int t = 0; t < H / 16; ++t)
@@ -2479,11 +2467,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       float* dst = (!second && srow >= 0) ? rc.store_obs + srow * rc.row_stride + nxt_off + (int64_t)agent * D : nullptr;
       const int ls = e < E ? le : 0;
       const int rcw = cx.spq[ls * N + agent] & 0xFF;
-#ifndef MM_OBS_SPLIT
-#define MM_OBS_SPLIT 1
-#endif
-      const uint64_t wd = MM_OBS_SPLIT ? roll_obs_word_g(cx.sgrid + ls * roll_gbw(R), R, rcw >> 4, rcw & 15, g)
-                                       : roll_obs_word(cx.sgrid + ls * roll_gbw(R), R, rcw >> 4, rcw & 15);
+      const uint64_t wd = roll_obs_word_g(cx.sgrid + ls * roll_gbw(R), R, rcw >> 4, rcw & 15, g);
       const float cr = cx.stab[rcw >> 4], cc = cx.stab[R + (rcw & 15)];
       auto ol = [&](int kb, float (&x)[8]) {
 #pragma unroll
@@ -2503,7 +2487,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       // (the image base offset by the per-step opaque zero: the fragment addresses are formed inside the step,
       // not hoisted out of the loop into registers that then spill)
       const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr() + tz, ol, xn, h0, cx.eps, ctr, off, 1,
-                                                      MM_HREG ? &hkeep : nullptr, !MM_HREG || i + 1 == nsteps);
+                                                      &hkeep, i + 1 == nsteps);
       // behavior blocks: each wave publishes its 16 envs' actions of step t + 1 as soon as its forward is done (every
       // lane (c, g) holds env c's action): lanes 0-7 / 8-15 OR their nibbles into the two hand-off words of the wave
       if (second && i + 1 < rc.n) {

@@ -21,6 +21,10 @@
 #include "per_small.h"
 
 namespace mm {
+// large-batch kernel shape (mm_learner_set_multi_sample): B >= 512 runs the mixer forward / recurrence backward with
+// MIX_SPB samples per block and the agent backward with BWD_SPW samples per wave (shared weight reads); 0 selects the
+// one-sample kernels, whose results are identical (tests/test_gpu_learner.py pins the equality)
+static int g_mix_multi = 1, g_bwd_multi = 1;
 
 // Element offset of state row i in the obs array: the gathered chunk-store offsets (-1: the env's reset
 // obs), or, without offsets (the torch ops' contiguous [rows, S] state), row i itself.
@@ -2668,6 +2672,12 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 // ------------------------------------------------------------------ C ABI
 extern "C" {
 
+int mm_learner_set_multi_sample(int32_t mixer, int32_t agent_bwd) {
+  mm::g_mix_multi = mixer != 0;
+  mm::g_bwd_multi = agent_bwd != 0;
+  return MM_OK;
+}
+
 int mm_mixer_param_count(int32_t state_dim, int32_t hm, int32_t k1, int32_t n_agents, int64_t* count) {
   MM_REQUIRE(count && state_dim > 0 && hm > 0 && k1 > 0 && n_agents > 0, "mixer_param_count: bad dims");
   *count = mm::mix_offsets(state_dim, hm, k1, n_agents).total;
@@ -2710,8 +2720,7 @@ int mm_mixer_fwd(int32_t B, int32_t N, int32_t S, int32_t Hm, int32_t K1, const 
   bool all_gi = true;
   for (int i = 0; i < n_nets; ++i) all_gi = all_gi && nets[i].gi;
   const size_t smm = sizeof(float) * (size_t)mm::MIX_SPB * (9 * Hm + N * K1 + 4 * K1);
-  const char* mm_env = getenv("MM_MIX_MULTI");   // "0" forces the one-sample-per-block kernel (tests)
-  if (B >= 512 && all_gi && smm <= 64 * 1024 && !(mm_env && mm_env[0] == '0')) {
+  if (B >= 512 && all_gi && smm <= 64 * 1024 && mm::g_mix_multi) {
     hipLaunchKernelGGL(mm::mixer_fwd_multi_kernel, dim3((B + mm::MIX_SPB - 1) / mm::MIX_SPB, n_nets), dim3(256), smm,
                        (hipStream_t)s, a);
     MM_HIP_CHECK(hipGetLastError());
@@ -2850,8 +2859,7 @@ static int mixer_bwd_seq_part(int part, int32_t B, int32_t N, int32_t S, int32_t
   q.delta_st = (int64_t)B * mm::mix_delta_dim(Hm, K1, N);
   q.ones = ones;
   const size_t smm = sizeof(float) * (size_t)mm::MIX_SPB * (4 * Hm + N * K1 + 3 * K1 + 4 * Hm);
-  const char* mm_env = getenv("MM_MIX_MULTI");   // "0" forces the one-sample-per-block kernel (tests)
-  if (B >= 512 && smm <= 64 * 1024 && !(mm_env && mm_env[0] == '0')) {
+  if (B >= 512 && smm <= 64 * 1024 && mm::g_mix_multi) {
     hipLaunchKernelGGL(mm::mixer_bwd_seq_multi_kernel, dim3((B + mm::MIX_SPB - 1) / mm::MIX_SPB), dim3(256), smm,
                        (hipStream_t)s, a, q);
     MM_HIP_CHECK(hipGetLastError());
@@ -3148,8 +3156,7 @@ int mm_agent_bwd(const mm_qnet_dims* d, const float* P, int64_t oWq, int64_t oWh
   mm::AgentBwdArgs a = {P, oWq, oWhh, save, acts, dqa, done, dh, dgi, dgh, dq,
                         B, d->n_agents, d->f1, d->g, d->h, d->n_actions};
   const int pairs = B * d->n_agents;
-  const char* bm_env = getenv("MM_BWD_MULTI");   // "0" forces the one-pair-per-wave kernel (tests)
-  if (B >= 512 && d->h <= 64 && !(bm_env && bm_env[0] == '0')) {
+  if (B >= 512 && d->h <= 64 && mm::g_bwd_multi) {
     hipLaunchKernelGGL(mm::agent_bwd_multi_kernel, dim3((B + 4 * mm::BWD_SPW - 1) / (4 * mm::BWD_SPW), d->n_agents),
                        dim3(256), 0, (hipStream_t)s, a);
     MM_HIP_CHECK(hipGetLastError());

@@ -1258,8 +1258,8 @@ int mm_per_insert_fold(mm_per* per, int64_t k, int32_t n_agents, float gamma, co
                        int64_t* slots_out, mm_stream_t s) {
   MM_REQUIRE(per && rew && done && q_taken && max_q_next && act && chunk_td && store_act && store_rew && store_done &&
                  rows_inout, "per_insert_fold: null argument");
-  MM_REQUIRE(n_slots >= 1 && n_slots <= 16 && slot0 >= 0 && slot0 + n_slots == chunk_len,
-             "per_insert_fold: the slots [slot0, slot0 + n) must end the chunk, n <= 16");
+  MM_REQUIRE(n_slots >= 1 && slot0 >= 0 && slot0 + n_slots == chunk_len,
+             "per_insert_fold: the slots [slot0, slot0 + n) must end the chunk");
   MM_REQUIRE(n_agents >= 1 && n_agents <= 256 && ring_se >= k * n_agents, "per_insert_fold: bad agents / ring");
   MM_REQUIRE(k >= 1 && k <= per->cap, "per_insert_fold: batch %lld outside [1, capacity]", (long long)k);
   if (!per->mb) {   // (the single-workgroup insert paths: the fold as its own launch, then the insert)

@@ -64,6 +64,28 @@ __global__ __launch_bounds__(256) void td_fold_range_kernel(FoldArgs a) {
   td_fold_group<VEC>(a, blockIdx.x);
 }
 
+// Diagnostic (mm_hold_cus): one 1024-thread workgroup per CU (16 waves holding VGPRs + 64 KiB of dynamic LDS, so no
+// chunk-kernel block, which needs every VGPR of the CU's SIMDs, can share the CU) that spins on the 100 MHz clock for `ticks`; *seen |= 2 if a watched hand-off word already carries `tag` when
+// the block starts, |= 1 if one carries it when the block ends (1 alone: a chunk-persistent launch ran beside it).
+// tests/test_gpu_chunk.py uses it to break the chunk kernel's co-residency contract on purpose (bounded: the waits
+// expire, the grid drains).
+__device__ __forceinline__ int hold_scan(const uint64_t* watch, int64_t n_watch, uint32_t tag) {
+  int saw = 0;
+  for (int64_t i = threadIdx.x; i < n_watch; i += blockDim.x)
+    saw |= (uint32_t)(__hip_atomic_load(watch + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag ? 1 : 0;
+  return __syncthreads_or(saw) ? 1 : 0;
+}
+__global__ __launch_bounds__(1024) void hold_cus_kernel(int64_t ticks, const uint64_t* watch, int64_t n_watch,
+                                                      uint32_t tag, int32_t* seen) {
+  extern __shared__ float hold_lds[];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  hold_lds[threadIdx.x] = 0.0f;
+  const int pre = hold_scan(watch, n_watch, tag);
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(64);
+  const int post = hold_scan(watch, n_watch, tag);
+  if (threadIdx.x == 0 && (pre || post)) atomicOr(seen, (pre ? 2 : 0) | (post ? 1 : 0));
+}
+
 // chunk begin: obs_cur [E][ND] -> store slot 0 of each env's staging row
 __global__ __launch_bounds__(256) void chunk_begin_kernel(int E, int ND, const float* __restrict__ obs_cur,
                                                           float* __restrict__ s_obs, int64_t row_stride,
@@ -220,8 +242,8 @@ int mm_td_fold_range(int64_t n_envs, int32_t n_agents, float gamma, const float*
                      mm_stream_t s) {
   MM_REQUIRE(rew && done && q_taken && max_q_next && act && chunk_td && store_act && store_rew && store_done && rows,
              "td_fold_range: null argument");
-  MM_REQUIRE(n_slots >= 1 && n_slots <= 16 && slot0 >= 0 && slot0 + n_slots <= chunk_len,
-             "td_fold_range: slots [slot0, slot0 + n) must lie in one chunk, n <= 16");
+  MM_REQUIRE(n_slots >= 1 && slot0 >= 0 && slot0 + n_slots <= chunk_len,
+             "td_fold_range: slots [slot0, slot0 + n) must lie in one chunk");
   MM_REQUIRE(n_agents >= 1 && n_agents <= 256 && ring_se >= n_envs * n_agents, "td_fold_range: bad agents / ring");
   if (n_envs <= 0) return MM_OK;
   mm::FoldArgs a{rew, done, q_taken, max_q_next, act, chunk_td, store_act, store_rew, store_done, rows,
@@ -229,7 +251,7 @@ int mm_td_fold_range(int64_t n_envs, int32_t n_agents, float gamma, const float*
                  gamma};
   const int blocks = (int)((n_envs + 15) / 16);
   auto kern = mm::fold_vec_ok(a) ? mm::td_fold_range_kernel<true> : mm::td_fold_range_kernel<false>;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(16 * n_slots), 0, (hipStream_t)s, a);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(16 * std::min(n_slots, 16)), 0, (hipStream_t)s, a);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
@@ -280,6 +302,16 @@ int mm_vdn_sum(int64_t B, int32_t N, int32_t A, const float* q, int64_t q_se, in
   if (B == 0) return MM_OK;
   hipLaunchKernelGGL(mm::vdn_sum_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)s, B, N, A, q,
                      q_se, q_sa, act, out, err);
+  MM_HIP_CHECK(hipGetLastError());
+  return MM_OK;
+}
+
+int mm_hold_cus(int32_t n_blocks, int64_t ticks, const int64_t* watch, int64_t n_watch, uint32_t tag, int32_t* seen,
+                mm_stream_t s) {
+  MM_REQUIRE(n_blocks >= 1 && n_blocks <= 4096 && ticks >= 0 && ticks <= 200000000ll && seen && (watch || !n_watch),
+             "hold_cus: bad args (at most 2 s)");
+  hipLaunchKernelGGL(mm::hold_cus_kernel, dim3(n_blocks), dim3(1024), 64 * 1024, (hipStream_t)s, ticks,
+                     reinterpret_cast<const uint64_t*>(watch), n_watch, tag, seen);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

@@ -27,63 +27,71 @@ struct FoldArgs {
   float gamma;
 };
 
-// one 16-env group (block-local index blk) of the fold; blockDim.x >= 16 n
+// one 16-env group (block-local index blk) of the fold; blockDim.x >= 16 min(n, 16). Spans longer than 16 slots
+// (chunk lengths > 16) run in slot groups of 16: each group's per-step values go through tdv, then the env's thread
+// adds them to its running priority in slot order, so the float additions are those of n td_chunk_kernel launches.
 template <bool VEC>
 __device__ __forceinline__ void td_fold_group(const FoldArgs& a, int blk) {
   __shared__ float tdv[16][16];
-  const int j = threadIdx.x >> 4, le = threadIdx.x & 15;
+  const int jl = threadIdx.x >> 4, le = threadIdx.x & 15;
   const int e = blk * 16 + le;
   const int N = a.N;
-  const bool on = e < a.E && j < a.n;
-  if (on) {
-    const int t = a.slot0 + j;
-    const int64_t o = (int64_t)j * a.ring_se + (int64_t)e * N;
-    const int64_t row = a.rows[e];
-    const uint8_t d8 = a.done[(int64_t)j * a.E + e];
-    const bool rok = row >= 0 && row < a.n_rows;
-    const int64_t so = (row * a.C + t) * N;
-    float sr = 0.f, sq = 0.f, st = 0.f;   // agent order, like the reference's sum over dim 1
-    if constexpr (VEC) {
-      for (int k = 0; k < N; k += 4) {
-        const float4 r4 = *reinterpret_cast<const float4*>(a.rew + o + k);
-        const float4 q4 = *reinterpret_cast<const float4*>(a.q_taken + o + k);
-        const float4 m4 = *reinterpret_cast<const float4*>(a.maxq_next + o + k);
-        const int4 a4 = *reinterpret_cast<const int4*>(a.act + o + k);
-        sr += r4.x; sr += r4.y; sr += r4.z; sr += r4.w;
-        sq += q4.x; sq += q4.y; sq += q4.z; sq += q4.w;
-        st += m4.x; st += m4.y; st += m4.z; st += m4.w;
-        if (rok) {
-          *reinterpret_cast<float4*>(a.s_rew + so + k) = r4;
-          *reinterpret_cast<uint32_t*>(a.s_act + so + k) = (uint32_t)(a4.x & 255) | ((uint32_t)(a4.y & 255) << 8) |
-                                                            ((uint32_t)(a4.z & 255) << 16) | ((uint32_t)a4.w << 24);
+  float ctd = 0.0f;
+  if (jl == 0 && e < a.E && a.slot0 != 0) ctd = a.chunk_td[e];
+  for (int j0 = 0; j0 < a.n; j0 += 16) {
+    const int j = j0 + jl;
+    const bool on = e < a.E && jl < 16 && j < a.n;
+    if (on) {
+      const int t = a.slot0 + j;
+      const int64_t o = (int64_t)j * a.ring_se + (int64_t)e * N;
+      const int64_t row = a.rows[e];
+      const uint8_t d8 = a.done[(int64_t)j * a.E + e];
+      const bool rok = row >= 0 && row < a.n_rows;
+      const int64_t so = (row * a.C + t) * N;
+      float sr = 0.f, sq = 0.f, st = 0.f;   // agent order, like the reference's sum over dim 1
+      if constexpr (VEC) {
+        for (int k = 0; k < N; k += 4) {
+          const float4 r4 = *reinterpret_cast<const float4*>(a.rew + o + k);
+          const float4 q4 = *reinterpret_cast<const float4*>(a.q_taken + o + k);
+          const float4 m4 = *reinterpret_cast<const float4*>(a.maxq_next + o + k);
+          const int4 a4 = *reinterpret_cast<const int4*>(a.act + o + k);
+          sr += r4.x; sr += r4.y; sr += r4.z; sr += r4.w;
+          sq += q4.x; sq += q4.y; sq += q4.z; sq += q4.w;
+          st += m4.x; st += m4.y; st += m4.z; st += m4.w;
+          if (rok) {
+            *reinterpret_cast<float4*>(a.s_rew + so + k) = r4;
+            *reinterpret_cast<uint32_t*>(a.s_act + so + k) = (uint32_t)(a4.x & 255) | ((uint32_t)(a4.y & 255) << 8) |
+                                                              ((uint32_t)(a4.z & 255) << 16) | ((uint32_t)a4.w << 24);
+          }
+        }
+      } else {
+        for (int k = 0; k < N; ++k) {
+          const float r = a.rew[o + k];
+          sr += r;
+          sq += a.q_taken[o + k];
+          st += a.maxq_next[o + k];
+          if (rok) {
+            a.s_act[so + k] = (uint8_t)a.act[o + k];
+            a.s_rew[so + k] = r;
+          }
         }
       }
-    } else {
-      for (int k = 0; k < N; ++k) {
-        const float r = a.rew[o + k];
-        sr += r;
-        sq += a.q_taken[o + k];
-        st += a.maxq_next[o + k];
-        if (rok) {
-          a.s_act[so + k] = (uint8_t)a.act[o + k];
-          a.s_rew[so + k] = r;
-        }
+      const float d = d8 ? 1.0f : 0.0f;
+      tdv[jl][le] = rollout_td(sr, sq, st, d, a.gamma);
+      if (rok) {
+        a.s_done[row * a.C + t] = d8;
+      } else if (a.err) {
+        atomicOr(a.err, 1u);
       }
     }
-    const float d = d8 ? 1.0f : 0.0f;
-    tdv[j][le] = rollout_td(sr, sq, st, d, a.gamma);
-    if (rok) {
-      a.s_done[row * a.C + t] = d8;
-    } else if (a.err) {
-      atomicOr(a.err, 1u);
+    __syncthreads();
+    if (jl == 0 && e < a.E) {
+      const int m = a.n - j0 < 16 ? a.n - j0 : 16;
+      for (int jj = 0; jj < m; ++jj) ctd = (a.slot0 + j0 + jj == 0 ? 0.0f : ctd) + tdv[jj][le];
     }
+    __syncthreads();
   }
-  __syncthreads();
-  if (j == 0 && e < a.E) {
-    float ctd = a.slot0 == 0 ? 0.0f : a.chunk_td[e];
-    for (int jj = 0; jj < a.n; ++jj) ctd = (a.slot0 + jj == 0 ? 0.0f : ctd) + tdv[jj][le];
-    a.chunk_td[e] = ctd;
-  }
+  if (jl == 0 && e < a.E) a.chunk_td[e] = ctd;
 }
 
 // VEC applies: N % 4 == 0 and every ring / store base 16-byte aligned (4-byte for the act bytes)

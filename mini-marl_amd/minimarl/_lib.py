@@ -106,6 +106,8 @@ _SIGS = [
     ("mm_rollout_chunk_supported", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_i64]),
     ("mm_rollout_chunk", c_i32, [c_vp, ctypes.POINTER(QnetDims), c_vp, ctypes.POINTER(QFwdIO), c_vp,
                                  ctypes.POINTER(QFwdIO), c_i64, ctypes.POINTER(RollChunkIO), c_vp]),
+    ("mm_learner_set_multi_sample", c_i32, [c_i32, c_i32]),
+    ("mm_hold_cus", c_i32, [c_i32, c_i64, c_vp, c_i64, ctypes.c_uint32, c_vp, c_vp]),
     ("mm_td_fold_range", c_i32, [c_i64, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32,
                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     ("mm_env_grid_shape", c_i32, [c_vp, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)]),

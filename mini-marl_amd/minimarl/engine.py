@@ -146,9 +146,44 @@ class RolloutEngine:
         self._build_io()
         self.env.reset(self.init_obs)
 
+    @property
+    def step_mode(self):
+        """"chunk" (mm_rollout_chunk), "fused" (mm_rollout_step) or "two-launch" (env launch + dual forward)."""
+        return "chunk" if self.chunked else ("fused" if self.fused else "two-launch")
+
+    def _carry_views(self):
+        """The mode-specific buffers holding the step state every mode shares at a chunk boundary t (no TD pending):
+        act / Q(a) of step t (written one step ahead), done of step t - 1, the RNG step counter read at step t."""
+        t, C = self.t, self.C
+        if self.chunked:
+            i = self._act_idx(t)
+            return self.act_r[i], self.qsel_r[i], self.done_r[(t - 1) % C], self.counter_dev[0:1]
+        nb = len(self.act_buf)
+        ctr = self.counter_dev[t % 2:t % 2 + 1] if self.fused else self.counter_dev[0:1]
+        return self.act_buf[t % nb], self.qsel_buf[t % nb], self.done_buf[(t - 1) % 2], ctr
+
+    def carry_state(self):
+        """Mode-independent step state (name -> tensor) at a chunk boundary: with the common buffers of
+        state_buffers() it lets a checkpoint written in one step mode resume in another (the modes are bit-identical
+        step for step, tests/test_gpu_chunk.py). None mid-chunk, where each mode holds the chunk's steps in its own
+        rings / pending TD."""
+        if self.t % self.C != 0 or self._td_pending:
+            return None
+        act, qsel, done_prev, ctr = self._carry_views()
+        return {"act": act, "qsel": qsel, "done_prev": done_prev, "counter": ctr}
+
+    def load_carry(self, carry, copy):
+        """Inverse of carry_state() (``copy(dst, src, name)``); the engine's step count must already be restored."""
+        assert self.t % self.C == 0
+        for name, dst in zip(("act", "qsel", "done_prev", "counter"), self._carry_views()):
+            copy(dst, carry[name], "carry/" + name)
+        self._td_pending = self._td_flushed = False
+
+    COMMON_STATE = ("cur_row", "init_obs", "h", "ht", "chunk_td", "eps_dev", "staging")
+
     def state_buffers(self):
         """The per-step device buffers a checkpoint must carry (name -> tensor)."""
-        out = {k: getattr(self, k) for k in ("cur_row", "init_obs", "h", "ht", "chunk_td", "eps_dev", "staging")}
+        out = {k: getattr(self, k) for k in self.COMMON_STATE}
         out.update(counter_dev=self.counter_dev)
         if self.chunked:   # (the launch sequence / hand-off flags are the engine's own, never restored)
             out.update({k: getattr(self, k) for k in ("act_r", "qsel_r", "maxq_r", "rew_r", "done_r")})

@@ -193,12 +193,16 @@ class QTrainer:
         out.update({"env/" + k: v for k, v in ets.items()})
         for k, v in eng.state_buffers().items():
             out["engine/" + k] = v
+        carry = eng.carry_state()   # (at a chunk boundary: lets another step mode resume the file)
+        for k, v in (carry or {}).items():
+            out["carry/" + k] = v
         if include_replay:
             for k in ("obs", "act", "rew", "done"):
                 out["store/" + k] = getattr(eng.store, k)
         out["trainer/ep_ret"] = self.ep_ret
         out["trainer/score_acc"] = self.score_acc
         scalars = {"learner": sc, "t": eng.t, "chunks_inserted": eng.chunks_inserted, "primed": eng._primed,
+                   "step_mode": eng.step_mode,
                    "td_pending": eng._td_pending, "episode": self.episode, "warmed": self.warmed,
                    "replay_saved": bool(include_replay)}
         return out, scalars
@@ -206,22 +210,36 @@ class QTrainer:
     def restore_tensors(self, ts, scalars):
         from .checkpoint import copy_into
         eng = self.eng
+        # the step mode the file was written in (files before round 6 carry none: the chunk rings name chunk mode);
+        # another mode can resume it only from the mode-independent carry of a chunk boundary
+        saved_mode = scalars.get("step_mode") or ("chunk" if "engine/act_r" in ts else "fused or two-launch")
+        if saved_mode != eng.step_mode and "carry/act" not in ts:
+            raise ValueError(f"checkpoint was written by the {saved_mode!r} rollout step mode mid-chunk "
+                             f"(t = {scalars['t']}); this engine runs {eng.step_mode!r}. Resume it with the same mode "
+                             f"(QTrainConfig.persistent=True for 'chunk', False for the others) or save at a chunk "
+                             f"boundary, where any mode can resume it")
         self.learner.restore_tensors({k[8:]: v for k, v in ts.items() if k.startswith("learner/")}, scalars["learner"])
         eng.per.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("per/")})
         # the step count first: the fused step double-buffers the env state by step parity (env.state_buffer()
         # = t % 2), so the restored state must land in the buffer the next step reads
         eng.t, eng.chunks_inserted = int(scalars["t"]), int(scalars["chunks_inserted"])
         eng.env.restore_tensors({k[4:]: v for k, v in ts.items() if k.startswith("env/")})
-        for k, v in eng.state_buffers().items():
-            if "engine/" + k not in ts:
-                raise ValueError(f"checkpoint lacks engine/{k}")
-            copy_into(v, ts["engine/" + k], k)
+        if saved_mode == eng.step_mode:
+            for k, v in eng.state_buffers().items():
+                if "engine/" + k not in ts:
+                    raise ValueError(f"checkpoint lacks engine/{k}")
+                copy_into(v, ts["engine/" + k], k)
+        else:   # another step mode, saved at a chunk boundary: the shared buffers plus the mode-independent carry
+            for k in eng.COMMON_STATE:
+                copy_into(getattr(eng, k), ts["engine/" + k], k)
+            eng.load_carry({k[6:]: v for k, v in ts.items() if k.startswith("carry/")}, copy_into)
         if scalars.get("replay_saved"):
             for k in ("obs", "act", "rew", "done"):
                 copy_into(getattr(eng.store, k), ts["store/" + k], k)
         copy_into(self.ep_ret, ts["trainer/ep_ret"], "ep_ret")
         copy_into(self.score_acc, ts["trainer/score_acc"], "score_acc")
-        eng._primed, eng._td_pending = bool(scalars["primed"]), bool(scalars["td_pending"])
+        eng._primed = bool(scalars["primed"])
+        eng._td_pending = bool(scalars["td_pending"]) and saved_mode == eng.step_mode
         eng._eps_host = None
         eng.behavior.mark_dirty()
         eng.target.mark_dirty()

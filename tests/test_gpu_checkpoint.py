@@ -172,3 +172,45 @@ def test_trainer_resume_bit_identical_fused_odd_step(tmp_path):
         assert torch.equal(x, y)
     for x, y in zip(a.eng.env.get_state(), b.eng.env.get_state()):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("src_persistent", [True, False])
+def test_trainer_resume_across_step_modes(tmp_path, src_persistent):
+    """the engine state a checkpoint holds depends on the rollout step mode picked for the device (chunk
+    rings vs fused ping-pong buffers). A file saved at a chunk boundary also carries the mode-independent step state
+    (act / Q(a) of step t, done of step t - 1, RNG counter), so a trainer running the OTHER mode resumes it and
+    continues bit-identically to the uninterrupted run (the two modes are bit-identical step for step); a file saved
+    mid-chunk names both modes in its error."""
+    from minimarl.checkpoint import load_checkpoint, save_checkpoint
+    from minimarl.config import QTrainConfig
+    from minimarl.train import QTrainer
+    kw = dict(algo="qmix", n_envs=2048, n_agents=4, full_observable=False, buffer_limit=4096, max_step=20,
+              update_iter=2, update_target_interval=2, test_interval=0, test_envs=0, epsilon_anneal_episode=10, seed=13)
+    a = QTrainer(QTrainConfig(persistent=src_persistent, **kw), device=DEV)
+    assert a.eng.chunked == src_persistent
+    a.train_episode()
+    assert a.eng.t % 10 == 0
+    path = str(tmp_path / "trainer_mode.safetensors")
+    save_checkpoint(path, trainer=a)
+    for _ in range(2):
+        a.train_episode()
+    b = QTrainer(QTrainConfig(persistent=not src_persistent, **kw), device=DEV)
+    assert b.eng.step_mode != a.eng.step_mode
+    b.train_episode()   # a different history before the restore
+    load_checkpoint(path, trainer=b)
+    assert b.eng.t == a.eng.t - 40
+    for _ in range(2):
+        b.train_episode()
+    torch.cuda.synchronize()
+    for x, y in [(a.learner.P, b.learner.P), (a.eng.per.tree(), b.eng.per.tree()),
+                 (a.eng.per.slot_rows(), b.eng.per.slot_rows()), (a.eng.store.obs, b.eng.store.obs),
+                 (a.eng.store.act, b.eng.store.act), (a.eng.h, b.eng.h), (a.eng.ht, b.eng.ht),
+                 (a.eng.chunk_td, b.eng.chunk_td), (a.score_acc, b.score_acc)]:
+        assert torch.equal(x, y)
+    for x, y in zip(a.eng.env.get_state(), b.eng.env.get_state()):
+        assert np.array_equal(x, y)
+    # mid-chunk: the other mode refuses with both modes named
+    a.eng.run_steps(3, 0.1)
+    save_checkpoint(path, trainer=a)
+    with pytest.raises(ValueError, match="step mode"):
+        load_checkpoint(path, trainer=b)

@@ -533,17 +533,18 @@ def test_outer_reduce_batch_large_rows(M, fn):
                                    atol=1e-3 * float(U[k].abs().max()) * np.sqrt(M / 320))
 
 
-@pytest.mark.parametrize("knob", ["MM_MIX_MULTI", "MM_BWD_MULTI"])
+@pytest.mark.parametrize("knob", ["mixer", "agent_bwd"])
 def test_multi_sample_blocks_bit_identical(knob):
     """B >= 512 runs the mixer forward with 8 samples per block and the agent backward with 8
     samples per wave (shared weight reads); each must give exactly the one-sample kernel's results
-    (knob = 0)."""
+    (mm_learner_set_multi_sample with that kernel's flag 0)."""
+    from minimarl._lib import lib
     from minimarl.learner import Mixer, QLearner
     from minimarl.qnet import AgentQNet
     N, D, A, B, C = 4, 47, 5, 600, 4
     res = []
-    for multi in ("1", "0"):
-        os.environ[knob] = multi
+    for multi in (1, 0):
+        lib().mm_learner_set_multi_sample(multi if knob == "mixer" else 1, multi if knob == "agent_bwd" else 1)
         try:
             beh = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=1)
             tgt = AgentQNet(N, D, A, 64, 64, 64, DEV, seed=2)
@@ -562,7 +563,7 @@ def test_multi_sample_blocks_bit_identical(knob):
             torch.cuda.synchronize()
             res.append((L.loss.clone(), L.P.clone(), L.td_last.clone()))
         finally:
-            os.environ.pop(knob, None)
+            lib().mm_learner_set_multi_sample(1, 1)
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
 
 
