@@ -718,9 +718,11 @@ def main():
     if eng.chunked:
         # chunk mode (the default at the headline shape): ONE launch runs the C steps of a chunk, mm_rollout_chunk =
         # per step the env step + target net on s'_t + behavior net on s_{t+1}; its FLOPs per launch = C steps' worth
-        per_launch_steps = eng.C
-        t_fwd = t_iso = time_kernel(lambda: eng.chunk_only(eng.C))
-        flops *= eng.C
+        # (the timed regions run launches of up to (S - 1) C steps across chunk boundaries: the roofline times a launch
+        # of the region's length)
+        per_launch_steps = L = min(args.steps, (eng.S - 1) * eng.C)
+        t_fwd = t_iso = time_kernel(lambda: eng.chunk_only(L))
+        flops *= L
         kname = "rollout_chunk_kernel"
         RC = eng.env.rows * eng.env.cols
         # algorithmic HBM bytes per launch: per step and agent-step the stored s'_t 4D, behavior act / Q(a) out 8,
@@ -729,8 +731,8 @@ def main():
         # the position word in / out 8; per launch and env the grid in / out 2RC, step / apple counters in / out 16,
         # store row in 8 (the weight images, LDS-resident for the launch, and the tile-local action hand-off,
         # <= 2N bytes per agent-step, are not counted)
-        alg_bytes = eng.C * (E * N * (4 * D + 16) + E * 9) + E * N * (16 * Hh + 12) + E * (2 * RC + 24)
-        kdesc = (f"{kname}<64,64,64,1> (C = {eng.C} rollout steps per launch: env step + dual forward, "
+        alg_bytes = L * (E * N * (4 * D + 16) + E * 9) + E * N * (16 * Hh + 12) + E * (2 * RC + 24)
+        kdesc = (f"{kname}<64,64,64,1> ({L} rollout steps per launch, chunk {eng.C}: env step + dual forward, "
                  "chunk-persistent)")
     elif eng.fused:
         t_fwd = t_iso = time_kernel(eng.fused_step_only)
@@ -793,8 +795,9 @@ def main():
             "config": {"workload": "QMIX 8-agent gridworld rollout, 4096 envs/GPU, GRU-64 agents, chunk 10, PER",
                        "envs_per_gpu": E, "agents": N, "obs_dim": D, "f1": F1, "gru": Hh, "chunk": 10,
                        "per_capacity_chunks": cap, "per_prefilled_chunks": fill_chunks * E,
-                       "step_launches": ("ONE chunk-persistent launch per chunk span (env step + dual forward of "
-                                         "each step) + the TD fold" if eng.chunked else
+                       "step_launches": ("chunk-persistent launches of up to (S - 1) C = "
+                                         f"{(eng.S - 1) * eng.C} steps across chunk boundaries (env step + dual forward "
+                                         "of each step; S = 4 staging row sets), then per chunk the TD fold" if eng.chunked else
                                          "ONE fused launch (env step + dual forward) per step" if eng.fused else
                                          "env + dual forward per step") + " + PER insert every chunk; one captured "
                                                                             "graph per timed region",

@@ -267,30 +267,33 @@ int mm_rollout_step_supported(const mm_env* env, const mm_qnet_dims* d, int64_t 
 int mm_rollout_step(mm_env* env, const mm_qnet_dims* d, const float* packed_t, const mm_qfwd_io* io_t,
                     const float* packed_b, const mm_qfwd_io* io_b, int64_t n_envs, const mm_rollout_step_io* x,
                     mm_stream_t s);
-/* The rollout steps [c0, c0 + n_steps) of ONE chunk in ONE launch (chunk-persistent; replaces n_steps iterations
- * of the reference's per-step loop body, vdn/main.py:93-167 / qmix/main.py:186-233, like n_steps mm_rollout_step
- * calls, with bit-identical results): every (net, agent, 256-env tile) block stays resident for all the steps, keeps
- * its weight image and its copy of the tile's env state in LDS, and waits only for the tile's behavior actions of
- * each step (a tile-local hand-off through tagged handoff words), never for a launch boundary. Per step t = c0 + i:
- * rewards into rew + i E N, dones into done + i E, cur_row; the target's max Q'_t into io_t->qsel_out + t_off0 +
- * i E N; the behavior's act / Q(a) of step t + 1 into io_b->act_out / qsel_out + b_off0 + i E N (+ b_offn for the
- * next chunk's step 0 when t + 1 = chunk_len); s'_t into slot t + 1 (and at t = 0 s_0 into slot 0) of row
- * staging[e]. act0 holds the actions of step c0, done_prev the dones of step c0 - 1. Hidden states are updated in
- * place (h_in == h_out, io.reset NULL). The TD / chunk-store fold of the steps is mm_td_fold_range. ctl = device
- * int64 [3]: launch sequence, env state buffer (low int32 of ctl[1], read; flipped by each launch: see
+/* The rollout steps t0 .. t0 + n_steps - 1 (chunk position c0 = t0 % chunk_len) in ONE launch (chunk-persistent; replaces
+ * n_steps iterations of the reference's per-step loop body, vdn/main.py:93-167 / qmix/main.py:186-233, like n_steps
+ * mm_rollout_step calls, with bit-identical results): every (net, agent, 256-env tile) block stays resident for all
+ * the steps, keeps its weight image and its copy of the tile's env state in LDS, and waits only for the tile's
+ * behavior actions of each step (a tile-local hand-off through tagged handoff words), never for a launch boundary.
+ * A launch may cross chunk boundaries: its k-th chunk (k = 0 .. n_sets - 1) writes staging row set (set0 + k) %
+ * n_sets of staging [n_sets][E] (s'_t into slot c + 1 and, at a chunk start, s_t into slot 0 of row staging[set][e]),
+ * so the chunks' PER inserts can all run after the launch (each insert swaps its own set's rows). Per-step outputs
+ * live in rings of ring_len steps, launch step i at ring position p = (ring_pos + i) % ring_len: rewards at rew +
+ * p E N, dones at done + p E, the target's max Q' at io_t->qsel_out + p E N, the behavior's act / Q(a) of the NEXT
+ * step at io_b->act_out / qsel_out + ((p + 1) % ring_len) E N (so n_steps < ring_len); cur_row per env. act0 holds
+ * the actions of step t0, done_prev the dones of step t0 - 1. Hidden states are updated in place (h_in == h_out,
+ * io.reset NULL). The TD / chunk-store fold of the steps is mm_td_fold_range / mm_per_insert_fold per chunk. ctl =
+ * device int64 [3]: launch sequence, env state buffer (low int32 of ctl[1], read; flipped by each launch: see
  * mm_env_get_state_buf), arrival ticket — zero-initialised once, then owned by these launches.
- * handoff = int64 [T][chunk_len][N][32], T = ceil(E / 256), zero-initialised: word w of (tile, step, agent) =
- * (low 32 bits of the launch sequence + 1) << 32 | the 4-bit actions of the tile's envs 8 w .. 8 w + 7. Supported
- * when mm_rollout_chunk_supported() != 0 (the fused step's geometry and 2 N T blocks <= the device's CUs: all
- * blocks must be co-resident; a hand-off wait longer than 20 ms sets bit 1 of *err and proceeds). */
+ * handoff = int64 [T][handoff_len][N][32], T = ceil(E / 256), handoff_len >= n_steps, zero-initialised: word w of
+ * (tile, launch step, agent) = (low 32 bits of the launch sequence + 1) << 32 | the 4-bit actions of the tile's envs
+ * 8 w .. 8 w + 7. Supported when mm_rollout_chunk_supported() != 0 (the fused step's geometry and 2 N T blocks <= the
+ * device's CUs: all blocks must be co-resident; a hand-off wait longer than 20 ms sets bit 1 of *err and proceeds). */
 typedef struct mm_rollout_chunk_io {
   float* store_obs; int64_t row_stride; int64_t n_rows;
   const int64_t* staging; int64_t* cur_row;
-  int32_t c0, n_steps, chunk_len, pad_;
+  int32_t c0, n_steps, chunk_len, n_sets;
+  int32_t set0, ring_len, ring_pos, handoff_len;
   const int32_t* act0; const uint8_t* done_prev;
   float* rew; uint8_t* done;
-  int64_t b_off0, b_offn, t_off0;
-  int64_t* counter;      /* device RNG step counter: step c0 + i draws with *counter + i; += n_steps */
+  int64_t* counter;      /* device RNG step counter: step t0 + i draws with *counter + i; += n_steps */
   int64_t* ctl;          /* device int64 [3]: launch sequence, env state buffer (low int32), arrival ticket */
   int64_t* handoff;
   int32_t* err;

@@ -2114,15 +2114,13 @@ struct RollChunk {   // kernarg right after the two QFwdParams
   EnvDev env;
   float* store_obs;
   int64_t row_stride;
-  const int64_t* staging;
+  const int64_t* staging;    // [S][E] staging row sets: the launch's k-th chunk writes set (set0 + k) % S
   int64_t* cur_row;
   int64_t n_rows;
   const int32_t* act0;       // [E][N] actions of the launch's first step
   const uint8_t* done_prev;  // [E] dones of the step before the launch (the target's hidden reset of step c0)
-  float* rew;                // [E][N] rewards of step c0 (step c0 + i at + i E N)
-  uint8_t* done;             // [E] dones of step c0 (+ i E)
-  int64_t b_off0, b_offn;    // io_b.act_out / qsel_out element offsets: step c0 + 1 (+ i E N); the next chunk's step 0
-  int64_t t_off0;            // io_t.qsel_out (max Q') element offset of step c0 (+ i E N)
+  float* rew;                // ring [RL][E][N]: rewards of launch step i at ring position (pos0 + i) % RL
+  uint8_t* done;             // ring [RL][E]
   uint64_t* counter;         // RNG step counter (step c0 + i draws with *counter + i)
   uint64_t* seq;             // launch sequence number (hand-off flag epoch)
   int32_t* envpar;           // env state buffer read (0 / 1)
@@ -2131,6 +2129,8 @@ struct RollChunk {   // kernarg right after the two QFwdParams
   uint32_t* err;             // sticky error bits: 1 staging row outside the store, 2 hand-off wait expired
   uint64_t* trace;           // per-step timing stamps (MM_ROLL_DEBUG builds, tools/chunk_trace.py), else nullptr
   int c0, n, CL, lds_env;   // first step's chunk position, steps, chunk length, LDS offset of the env state
+  int S, set0, RL, pos0;     // staging sets, the first chunk's set, ring length (steps), the first step's ring position
+  int hxl;                   // hand-off word slots per tile (steps): launch step i's words at slot i
 };
 static_assert(alignof(RollChunk) == 8, "rollout_chunk kernarg layout");
 static constexpr uint64_t kHandoffTimeout = 2000000;   // s_memrealtime ticks (100 MHz): 20 ms
@@ -2250,7 +2250,17 @@ __device__ __forceinline__ void roll_chunk_steps() {
   uint32_t* rows = cx.sgrid + le_d * roll_gbw(R);
   const int le = wave * 16 + (lane & 15), e = e0 + le;           // fp16x3 body / begin-store lane mapping
   const int l32 = wave * 32 + (lane & 31), e32 = e0 + l32;       // exact body lane mapping (waves 0-7)
-    const int c = rc.c0 + i;
+    // chunk position c of launch step i, the chunk's staging set (a launch may cross chunk boundaries: its k-th chunk
+    // writes staging set (set0 + k) % S), ring position of the step (rings of RL steps hold rewards / dones / max Q' /
+    // actions / Q(a) by step)
+    int c = rc.c0 + i, kset = rc.set0;
+    while (c >= CL) {
+      c -= CL;
+      kset = kset + 1 == rc.S ? 0 : kset + 1;
+    }
+    const int64_t* stg = rc.staging + (int64_t)kset * E;
+    const int pos = rc.pos0 + i >= rc.RL ? rc.pos0 + i - rc.RL : rc.pos0 + i;
+    const int posn = pos + 1 == rc.RL ? 0 : pos + 1;
     const uint64_t ctr = cx.ctr0 + (uint64_t)i;
     const int cur = i & 1, prv = cur ^ 1;
     MM_CSTAMP(0);
@@ -2262,7 +2272,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
         // the tile's N x 32 hand-off words of step i, polled by wave 0 until each carries this launch's tag (tag and
         // actions are one 64-bit word: a word that matches holds this step's actions, no flag / fence needed), their
         // action halves into LDS
-        const uint64_t* hs = rc.hx + ((int64_t)tile * CL + i) * N * 32;
+        const uint64_t* hs = rc.hx + ((int64_t)tile * rc.hxl + i) * N * 32;
         uint32_t* hl = reinterpret_cast<uint32_t*>(cx.shx);
         const uint32_t tag = (uint32_t)cx.seq + 1u;
         const int nw = N * 32;
@@ -2322,7 +2332,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
     if (!second) {
       const int el = EXACT ? e32 : e;
       if ((EXACT ? (wave < 8) : true) && el < E) {
-        srow = rc.staging[el];
+        srow = stg[el];
         if (srow < 0 || srow >= rc.n_rows) srow = -1;   // (flagged once per launch by the prologue)
       }
     }
@@ -2330,7 +2340,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
     if (c == 0) {
       __syncthreads();
       if (!second && e < E) {
-        const int64_t srb = rc.staging[e];
+        const int64_t srb = stg[e];
         if (srb >= 0 && srb < rc.n_rows) {
           const int rcw = cx.spq[le * N + agent] & 0xFF;
           const uint64_t wd = roll_obs_word(cx.sgrid + le * roll_gbw(R), R, rcw >> 4, rcw & 15);
@@ -2349,7 +2359,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
     if (dvalid) {
       int64_t myrow = -1;
       if (writer) {
-        myrow = rc.staging[de];
+        myrow = stg[de];
         if (myrow < 0 || myrow >= rc.n_rows) myrow = -1;   // never handed on as cur_row
       }
       uint32_t pq[kRollMaxN / 2];
@@ -2360,7 +2370,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
         if (k < N) pq[k >> 1] |= (uint32_t)cx.spq[le_d * N + k] << (16 * (k & 1));
       const int st = (int)cx.ssa[le_d] + 1;
       int apples = cx.ssa[256 + le_d];
-      float* rout = rc.rew + (int64_t)i * EN + (int64_t)de * N;
+      float* rout = rc.rew + (int64_t)pos * EN + (int64_t)de * N;
       // (unrolled over the compile-time agent bound: each agent's own target cell is independent of the others, so
       // the compiler can compute it ahead of the previous agent's LDS round trip; only the grid rows chain them)
 #pragma unroll
@@ -2407,14 +2417,14 @@ __device__ __forceinline__ void roll_chunk_steps() {
       cx.ssa[256 + le_d] = (uint16_t)apples;
       cx.sdone[cur * 256 + le_d] = dn ? 1 : 0;
       if (writer) {
-        rc.done[(int64_t)i * E + de] = dn ? 1 : 0;
+        rc.done[(int64_t)pos * E + de] = dn ? 1 : 0;
         rc.cur_row[de] = dn ? -1 : myrow;
       }
     }
     __syncthreads();
     MM_CSTAMP(2);
     // (5) the forward: target on s'_t (max Q'_t, s'_t stored into slot c + 1), behavior on s_{t+1} (act / Q(a))
-    const int64_t off = second ? ((c + 1 < CL) ? rc.b_off0 + (int64_t)i * EN : rc.b_offn) : rc.t_off0 + (int64_t)i * EN;
+    const int64_t off = (int64_t)(second ? posn : pos) * EN;
     const int64_t nxt_off = (int64_t)(c + 1) * nd;
     if constexpr (EXACT) {
       const int hh = lane >> 5;
@@ -2496,7 +2506,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
         v |= __shfl_xor(v, 2);
         v |= __shfl_xor(v, 4);
         if (lane == 0 || lane == 8) {
-          uint64_t* hd = rc.hx + (((int64_t)tile * CL + i + 1) * N + agent) * 32 + wave * 2 + (lane >> 3);
+          uint64_t* hd = rc.hx + (((int64_t)tile * rc.hxl + i + 1) * N + agent) * 32 + wave * 2 + (lane >> 3);
           __hip_atomic_store(hd, ((uint64_t)((uint32_t)cx.seq + 1u) << 32) | v, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2508,7 +2518,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       __syncthreads();
       if (wave == 0 && lane < 32) {
         const uint2 b = reinterpret_cast<const uint2*>(cx.shx)[lane];   // envs 8 lane .. 8 lane + 7
-        uint64_t* hd = rc.hx + (((int64_t)tile * CL + i + 1) * N + agent) * 32 + lane;
+        uint64_t* hd = rc.hx + (((int64_t)tile * rc.hxl + i + 1) * N + agent) * 32 + lane;
         __hip_atomic_store(hd, ((uint64_t)((uint32_t)cx.seq + 1u) << 32) | nib_pack4(b.x) | (nib_pack4(b.y) << 16),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -2565,7 +2575,13 @@ __global__ __launch_bounds__(1024, 1) void rollout_chunk_kernel(QFwdParams p0, Q
         if (2 * j + 1 < R) rows[2 * j + 1] = nib_pack4(g.z) | (nib_pack4(g.w) << 16);
       }
     cx.sdone[256 + le_d] = rc.done_prev[de];   // "previous step" slot of step 0 (parity 1)
-    if (cx.writer) roll_row_ok(rc.staging[de], rc.n_rows, rc.err);
+    if (cx.writer) {   // every staging set the launch writes
+      int ks = rc.set0;
+      for (int k = 0; k < rc.S && k * rc.CL < rc.c0 + rc.n; ++k) {
+        roll_row_ok(rc.staging[(int64_t)ks * E + de], rc.n_rows, rc.err);
+        ks = ks + 1 == rc.S ? 0 : ks + 1;
+      }
+    }
   } else if (threadIdx.x < 256) {
     cx.sdone[256 + le_d] = 0;
   }
@@ -3411,8 +3427,14 @@ int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, con
   const EnvDev& ev = env->d;
   MM_REQUIRE(x->store_obs && x->staging && x->cur_row && x->act0 && x->done_prev && x->rew && x->done && x->counter &&
                  x->ctl && x->handoff, "rollout_chunk: null buffer");
-  MM_REQUIRE(x->chunk_len >= 1 && x->chunk_len <= 4096 && x->c0 >= 0 && x->n_steps >= 1 &&
-                 x->c0 + x->n_steps <= x->chunk_len, "rollout_chunk: steps [c0, c0 + n) must lie in one chunk");
+  MM_REQUIRE(x->chunk_len >= 1 && x->chunk_len <= 4096 && x->c0 >= 0 && x->c0 < x->chunk_len && x->n_steps >= 1,
+             "rollout_chunk: bad chunk position / step count");
+  MM_REQUIRE(x->n_sets >= 1 && x->n_sets <= 64 && x->set0 >= 0 && x->set0 < x->n_sets &&
+                 x->c0 + x->n_steps <= (int64_t)x->n_sets * x->chunk_len,
+             "rollout_chunk: the launch's steps span more chunks than staging sets (%d)", x->n_sets);
+  MM_REQUIRE(x->ring_len >= 2 && x->ring_pos >= 0 && x->ring_pos < x->ring_len && x->n_steps < x->ring_len,
+             "rollout_chunk: the rings must hold the launch's steps plus the next step's actions (n_steps < ring_len)");
+  MM_REQUIRE(x->handoff_len >= x->n_steps, "rollout_chunk: handoff_len < n_steps");
   MM_REQUIRE(x->n_rows >= 1 && x->n_rows < (1ll << 40), "rollout_chunk: n_rows must be the chunk store's row count");
   MM_REQUIRE(io_t->mode == MM_Q_MAX && io_b->mode == MM_Q_ACT, "rollout_chunk: target io must be MAX, behavior io ACT");
   MM_REQUIRE(io_t->h_in && io_b->h_in && io_t->h_in == io_t->h_out && io_b->h_in == io_b->h_out,
@@ -3442,9 +3464,6 @@ int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, con
   r.done_prev = x->done_prev;
   r.rew = x->rew;
   r.done = x->done;
-  r.b_off0 = x->b_off0;
-  r.b_offn = x->b_offn;
-  r.t_off0 = x->t_off0;
   r.counter = reinterpret_cast<uint64_t*>(x->counter);
   r.seq = reinterpret_cast<uint64_t*>(x->ctl);
   r.envpar = reinterpret_cast<int32_t*>(x->ctl + 1);
@@ -3459,6 +3478,11 @@ int rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, con
   r.c0 = x->c0;
   r.n = x->n_steps;
   r.CL = x->chunk_len;
+  r.S = x->n_sets;
+  r.set0 = x->set0;
+  r.RL = x->ring_len;
+  r.pos0 = x->ring_pos;
+  r.hxl = x->handoff_len;
   QnetGeo g;
   QnetOffsets o;
   qnet_geometry(d, &g, &o);

@@ -63,9 +63,9 @@ class RollChunkIO(ctypes.Structure):
     """mm_rollout_chunk_io (include/minimarl.h)"""
     _fields_ = [
         ("store_obs", c_vp), ("row_stride", c_i64), ("n_rows", c_i64), ("staging", c_vp), ("cur_row", c_vp),
-        ("c0", c_i32), ("n_steps", c_i32), ("chunk_len", c_i32), ("pad_", c_i32),
+        ("c0", c_i32), ("n_steps", c_i32), ("chunk_len", c_i32), ("n_sets", c_i32),
+        ("set0", c_i32), ("ring_len", c_i32), ("ring_pos", c_i32), ("handoff_len", c_i32),
         ("act0", c_vp), ("done_prev", c_vp), ("rew", c_vp), ("done", c_vp),
-        ("b_off0", c_i64), ("b_offn", c_i64), ("t_off0", c_i64),
         ("counter", c_vp), ("ctl", c_vp), ("handoff", c_vp), ("err", c_vp),
     ]
 

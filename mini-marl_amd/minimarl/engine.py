@@ -74,8 +74,14 @@ class RolloutEngine:
         self.H = h
         self.capacity = int(capacity or 4 * self.E)
         self.per = DevicePER(self.capacity, per_flavor, device=self.device, **(per_kwargs or {}))
-        self.store = ChunkStore(self.capacity + self.E, self.C, self.N, self.D, self.device)
-        self.staging = torch.arange(self.capacity, self.capacity + self.E, dtype=torch.int64, device=self.device)
+        # S staging row sets [S][E] (every mode allocates them, so the store has the same rows in every mode and a
+        # checkpoint moves between modes): the chunk-persistent launches write chunk k into set k % S, so ONE launch
+        # can run up to S - 1 whole chunks (plus the partial ones at its ends) with the chunks' PER inserts after it;
+        # the other modes use set 0
+        self.S = self.N_STAGING_SETS
+        self.store = ChunkStore(self.capacity + self.S * self.E, self.C, self.N, self.D, self.device)
+        self.staging_all = torch.arange(self.capacity, self.capacity + self.S * self.E, dtype=torch.int64,
+                                        device=self.device).view(self.S, self.E)
         E, N, D, H = self.E, self.N, self.D, self.H
         dev = self.device
         ok = env == "checkers" and lib().mm_rollout_step_supported(self.env.handle(), ctypes.byref(self.behavior.dims),
@@ -131,20 +137,34 @@ class RolloutEngine:
         self.chunks_inserted = 0
         if self.chunked:
             C, T = self.C, (E + 255) // 256
-            # per-chunk rings: act / Q(a) of step t at [(t // C) % 2][t % C] (written one step ahead, so a chunk's
-            # last step writes the next chunk's position 0 into the other half); max Q', rewards, dones at [t % C]
-            self.act_r = torch.zeros(2 * C, E, N, dtype=torch.int32, device=dev)
-            self.qsel_r = torch.zeros(2 * C, E, N, device=dev)
-            self.maxq_r = torch.zeros(C, E, N, device=dev)
-            self.rew_r = torch.zeros(C, E, N, device=dev)
-            self.done_r = torch.zeros(C, E, dtype=torch.uint8, device=dev)
+            # per-step rings of RL = S C steps: act / Q(a) of step t at [t % RL] (written one step ahead by the
+            # previous step's behavior forward), max Q', rewards, dones of step t at [t % RL]; a launch runs at most
+            # (S - 1) C steps, so its rings never overwrite a step its chunks' folds still read
+            self.RL = RL = self.S * C
+            self.act_r = torch.zeros(RL, E, N, dtype=torch.int32, device=dev)
+            self.qsel_r = torch.zeros(RL, E, N, device=dev)
+            self.maxq_r = torch.zeros(RL, E, N, device=dev)
+            self.rew_r = torch.zeros(RL, E, N, device=dev)
+            self.done_r = torch.zeros(RL, E, dtype=torch.uint8, device=dev)
             # launch state owned by the chunk kernel: launch sequence, env state buffer, arrival ticket
             self.ctl = torch.zeros(3, dtype=torch.int64, device=dev)
-            # tagged hand-off words [T][C][N][32]: (launch sequence + 1) << 32 | 8 envs' 4-bit actions
-            self.hx = torch.zeros(T * C * N * 32, dtype=torch.int64, device=dev)
+            # tagged hand-off words [T][RL][N][32] (slot = launch step): (launch sequence + 1) << 32 | 8 envs' actions
+            self.hx = torch.zeros(T * RL * N * 32, dtype=torch.int64, device=dev)
             self.env.state_buffer = lambda: int(self.ctl[1].item()) & 1
         self._build_io()
         self.env.reset(self.init_obs)
+
+    N_STAGING_SETS = 4
+
+    @property
+    def staging(self):
+        """[E] staging rows of the current chunk (chunk mode: set (t // C) % S; the other modes: set 0)."""
+        return self.staging_all[(self.t // self.C) % self.S] if self.chunked else self.staging_all[0]
+
+    def staging_set(self, t=None):
+        """index of the staging set chunk t // C writes"""
+        t = self.t if t is None else t
+        return (t // self.C) % self.S if self.chunked else 0
 
     @property
     def step_mode(self):
@@ -157,7 +177,7 @@ class RolloutEngine:
         t, C = self.t, self.C
         if self.chunked:
             i = self._act_idx(t)
-            return self.act_r[i], self.qsel_r[i], self.done_r[(t - 1) % C], self.counter_dev[0:1]
+            return self.act_r[i], self.qsel_r[i], self.done_r[(t - 1) % self.RL], self.counter_dev[0:1]
         nb = len(self.act_buf)
         ctr = self.counter_dev[t % 2:t % 2 + 1] if self.fused else self.counter_dev[0:1]
         return self.act_buf[t % nb], self.qsel_buf[t % nb], self.done_buf[(t - 1) % 2], ctr
@@ -172,14 +192,17 @@ class RolloutEngine:
         act, qsel, done_prev, ctr = self._carry_views()
         return {"act": act, "qsel": qsel, "done_prev": done_prev, "counter": ctr}
 
-    def load_carry(self, carry, copy):
-        """Inverse of carry_state() (``copy(dst, src, name)``); the engine's step count must already be restored."""
+    def load_carry(self, carry, copy, staging_all, src_set):
+        """Inverse of carry_state() (``copy(dst, src, name)``); the engine's step count must already be restored.
+        ``staging_all`` = the saved staging sets, whose set ``src_set`` is the current chunk's in the saved mode: the
+        sets are rotated so it lands where this mode reads it (every other set holds free rows in every mode)."""
         assert self.t % self.C == 0
         for name, dst in zip(("act", "qsel", "done_prev", "counter"), self._carry_views()):
             copy(dst, carry[name], "carry/" + name)
+        copy(self.staging_all, torch.roll(staging_all, self.staging_set() - src_set, 0), "staging_all")
         self._td_pending = self._td_flushed = False
 
-    COMMON_STATE = ("cur_row", "init_obs", "h", "ht", "chunk_td", "eps_dev", "staging")
+    COMMON_STATE = ("cur_row", "init_obs", "h", "ht", "chunk_td", "eps_dev", "staging_all")
 
     def state_buffers(self):
         """The per-step device buffers a checkpoint must carry (name -> tensor)."""
@@ -201,19 +224,19 @@ class RolloutEngine:
     def last_rew(self):
         """rewards [E, N] of the last executed step"""
         if self.chunked:
-            return self.rew_r[(self.t - 1) % self.C]
+            return self.rew_r[(self.t - 1) % self.RL]
         return self.rew_buf[(self.t - 1) % 2] if self.fused else self.rew
 
     @property
     def last_done(self):
         """done flags [E] of the last executed step"""
         if self.chunked:
-            return self.done_r[(self.t - 1) % self.C]
+            return self.done_r[(self.t - 1) % self.RL]
         return self.done_buf[(self.t - 1) % 2]
 
     def _act_idx(self, t):
-        """chunk mode: ring index of the actions / Q(a) of step t"""
-        return ((t // self.C) % 2) * self.C + t % self.C
+        """chunk mode: ring index of the actions / Q(a) (and rewards, dones, max Q') of step t"""
+        return t % self.RL
 
     def current_obs(self):
         """s_{t+1} [E,N,D] as the next behavior forward reads it (materialised for tests only)."""
@@ -330,48 +353,56 @@ class RolloutEngine:
         self._primed = True
 
     def _advance(self, n):
-        """Launch the next n steps: chunk mode as one chunk-persistent launch per chunk span (split at chunk
-        boundaries), the other modes one step at a time."""
+        """Launch the next n steps: chunk mode as chunk-persistent launches of up to (S - 1) C steps each (across chunk
+        boundaries; the folds and PER inserts of the launch's chunks follow it), the other modes one step at a time."""
         n = int(n)
         while n > 0:
-            m = min(n, self.C - self.t % self.C) if self.chunked else 1
+            m = min(n, (self.S - 1) * self.C) if self.chunked else 1
             self._launch_chunk(m) if self.chunked else self._step_launch()
             n -= m
 
     def _launch_chunk(self, n):
-        """Steps t .. t + n - 1 (one chunk span) in ONE chunk-persistent launch (mm_rollout_chunk), then their TD /
-        chunk-store fold (mm_td_fold_range) and, at the chunk's end, the PER insert."""
+        """Steps t .. t + n - 1 in ONE chunk-persistent launch (mm_rollout_chunk, across chunk boundaries), then per
+        chunk piece of the span its TD / chunk-store fold (mm_td_fold_range) or, where the piece ends its chunk, the
+        fold inside the PER insert (mm_per_insert_fold) — the chunks' inserts in chunk order, each swapping its own
+        staging set, with nothing sampling in between (the reference's insert-per-chunk semantics)."""
         s = stream_handle(self.device)
         L = lib()
-        t, C, E, N = self.t, self.C, self.E, self.N
-        c0, EN = t % C, E * N
-        assert 1 <= n <= C - c0
+        t, C, E, N, RL = self.t, self.C, self.E, self.N, self.RL
+        c0, EN, p = t % C, E * N, t % RL
+        assert 1 <= n <= (self.S - 1) * C
         if not self._primed:
             self._prologue(s)
-        k, ia = (t // C) % 2, self._act_idx(t)
         x = RollChunkIO()
         x.store_obs, x.row_stride, x.n_rows = ptr(self.store.obs), self.store.row_stride, self.store.rows
-        x.staging, x.cur_row = ptr(self.staging), ptr(self.cur_row)
-        x.c0, x.n_steps, x.chunk_len = c0, n, C
-        x.act0 = self.act_r.data_ptr() + 4 * ia * EN
-        x.done_prev = self.done_r.data_ptr() + ((c0 - 1) % C) * E
-        x.rew, x.done = self.rew_r.data_ptr() + 4 * c0 * EN, self.done_r.data_ptr() + c0 * E
-        x.b_off0, x.b_offn, x.t_off0 = (k * C + c0 + 1) * EN, (1 - k) * C * EN, c0 * EN
+        x.staging, x.cur_row = ptr(self.staging_all), ptr(self.cur_row)
+        x.c0, x.n_steps, x.chunk_len, x.n_sets = c0, n, C, self.S
+        x.set0, x.ring_len, x.ring_pos, x.handoff_len = self.staging_set(t), RL, p, RL
+        x.act0 = self.act_r.data_ptr() + 4 * p * EN
+        x.done_prev = self.done_r.data_ptr() + ((t - 1) % RL) * E
+        x.rew, x.done = self.rew_r.data_ptr(), self.done_r.data_ptr()
         x.counter, x.ctl, x.handoff, x.err = ptr(self.counter_dev), ptr(self.ctl), ptr(self.hx), ptr(self.err)
         self.behavior.pack(s)
         self.target.pack(s)
         check(L.mm_rollout_chunk(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
                                  ctypes.byref(self.cio_t), ptr(self.behavior.packed), ctypes.byref(self.cio_b), E,
                                  ctypes.byref(x), s), "rollout_chunk")
-        fold = (E, N, self.gamma, self.rew_r.data_ptr() + 4 * c0 * EN, self.done_r.data_ptr() + c0 * E,
-                self.qsel_r.data_ptr() + 4 * ia * EN, self.maxq_r.data_ptr() + 4 * c0 * EN,
-                self.act_r.data_ptr() + 4 * ia * EN, EN, c0, n, C, ptr(self.chunk_td), ptr(self.store.act),
-                ptr(self.store.rew), ptr(self.store.done), ptr(self.staging), self.store.rows, ptr(self.err))
-        if c0 + n == C:   # the chunk's end: its last span's TD / store fold rides in the PER insert's first launch
-            check(L.mm_per_insert_fold(self.per._h, *fold, None, s), "per_insert_fold")
-            self.chunks_inserted += E
-        else:
-            check(L.mm_td_fold_range(*fold, s), "td_fold_range")
+        tt = t
+        while tt < t + n:   # the span's chunk pieces in order
+            a = tt % C
+            m = min(C - a, t + n - tt)
+            q = tt % RL
+            fold = (E, N, self.gamma, self.rew_r.data_ptr() + 4 * q * EN, self.done_r.data_ptr() + q * E,
+                    self.qsel_r.data_ptr() + 4 * q * EN, self.maxq_r.data_ptr() + 4 * q * EN,
+                    self.act_r.data_ptr() + 4 * q * EN, EN, a, m, C, ptr(self.chunk_td), ptr(self.store.act),
+                    ptr(self.store.rew), ptr(self.store.done), ptr(self.staging_all[self.staging_set(tt)]),
+                    self.store.rows, ptr(self.err))
+            if a + m == C:   # the chunk's end: its last piece's fold rides in the PER insert's first launch
+                check(L.mm_per_insert_fold(self.per._h, *fold, None, s), "per_insert_fold")
+                self.chunks_inserted += E
+            else:
+                check(L.mm_td_fold_range(*fold, s), "td_fold_range")
+            tt += m
         self._td_pending = False
         self.t += n
 
@@ -494,7 +525,7 @@ class RolloutEngine:
     def graph_steps(self):
         """Steps after which every parity-indexed buffer is back at its start (the graph cycle)."""
         if self.chunked:
-            return 2 * self.C
+            return self.RL
         if self.fused:
             return self.C * 6 // math.gcd(self.C, 6)
         return self.C if self.C % 2 == 0 else 2 * self.C
@@ -516,7 +547,10 @@ class RolloutEngine:
         self.t, self.chunks_inserted = t0, ins0
         lib().mm_per_set_size(self.per._h, n0)
         self.graph = g
+        self._graph_phase = t0 % self.graph_steps()
         return g
+
+    _graph_phase = 0
 
     def run_graph(self, epsilon=None):
         """Replay one captured chunk (graph_steps() env steps)."""
@@ -524,6 +558,7 @@ class RolloutEngine:
             self.set_epsilon(epsilon)
         if self.graph is None:
             self.capture()
+        assert self.t % self.graph_steps() == self._graph_phase, "run_graph at another graph phase than captured"
         self.behavior.pack()          # weights changed since capture (learner / target sync): repack eagerly
         self.target.pack()
         self.graph.replay()
@@ -668,23 +703,20 @@ class RolloutEngine:
                                     ctypes.byref(self.fio_b[(k2, k3)]), self.E, ctypes.byref(x), s), "rollout_step")
 
     def chunk_only(self, n=None):
-        """The chunk mode's one launch on its own (steps 0 .. n - 1 of a chunk, no TD fold / insert); for timing.
-        Advances the env / hidden state like the real launch (the host step count is left alone)."""
+        """The chunk mode's one launch on its own (steps 0 .. n - 1 from a ring / staging-set cycle start, no TD fold /
+        insert); for timing. Advances the env / hidden state like the real launch (the host step count is left alone)."""
         n = self.C if n is None else int(n)
-        t0 = self.t
-        self.t = (t0 // (2 * self.C)) * 2 * self.C
+        assert 1 <= n <= (self.S - 1) * self.C
         s = stream_handle(self.device)
-        C, E, N = self.C, self.E, self.N
-        EN = E * N
+        C, E, N, RL = self.C, self.E, self.N, self.RL
         x = RollChunkIO()
         x.store_obs, x.row_stride, x.n_rows = ptr(self.store.obs), self.store.row_stride, self.store.rows
-        x.staging, x.cur_row = ptr(self.staging), ptr(self.cur_row)
-        x.c0, x.n_steps, x.chunk_len = 0, n, C
-        x.act0, x.done_prev = self.act_r.data_ptr(), self.done_r.data_ptr() + (C - 1) * E
+        x.staging, x.cur_row = ptr(self.staging_all), ptr(self.cur_row)
+        x.c0, x.n_steps, x.chunk_len, x.n_sets = 0, n, C, self.S
+        x.set0, x.ring_len, x.ring_pos, x.handoff_len = 0, RL, 0, RL
+        x.act0, x.done_prev = self.act_r.data_ptr(), self.done_r.data_ptr() + (RL - 1) * E
         x.rew, x.done = self.rew_r.data_ptr(), self.done_r.data_ptr()
-        x.b_off0, x.b_offn, x.t_off0 = EN, C * EN, 0
         x.counter, x.ctl, x.handoff, x.err = ptr(self.counter_dev), ptr(self.ctl), ptr(self.hx), ptr(self.err)
-        self.t = t0
         check(lib().mm_rollout_chunk(self.env.handle(), ctypes.byref(self.target.dims), ptr(self.target.packed),
                                      ctypes.byref(self.cio_t), ptr(self.behavior.packed), ctypes.byref(self.cio_b), E,
                                      ctypes.byref(x), s), "rollout_chunk")

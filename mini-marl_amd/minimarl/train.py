@@ -231,8 +231,11 @@ class QTrainer:
                 copy_into(v, ts["engine/" + k], k)
         else:   # another step mode, saved at a chunk boundary: the shared buffers plus the mode-independent carry
             for k in eng.COMMON_STATE:
-                copy_into(getattr(eng, k), ts["engine/" + k], k)
-            eng.load_carry({k[6:]: v for k, v in ts.items() if k.startswith("carry/")}, copy_into)
+                if k != "staging_all":
+                    copy_into(getattr(eng, k), ts["engine/" + k], k)
+            src_set = (eng.t // eng.C) % eng.S if saved_mode == "chunk" else 0
+            eng.load_carry({k[6:]: v for k, v in ts.items() if k.startswith("carry/")}, copy_into,
+                           ts["engine/staging_all"], src_set)
         if scalars.get("replay_saved"):
             for k in ("obs", "act", "rew", "done"):
                 copy_into(getattr(eng.store, k), ts["store/" + k], k)

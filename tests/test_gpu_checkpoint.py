@@ -202,9 +202,12 @@ def test_trainer_resume_across_step_modes(tmp_path, src_persistent):
     for _ in range(2):
         b.train_episode()
     torch.cuda.synchronize()
+    # (the modes place chunks in different physical store rows — chunk mode rotates its staging sets — so the PER's
+    # chunks are compared through the slot maps)
+    ra, rb = a.eng.per.slot_rows().long(), b.eng.per.slot_rows().long()
     for x, y in [(a.learner.P, b.learner.P), (a.eng.per.tree(), b.eng.per.tree()),
-                 (a.eng.per.slot_rows(), b.eng.per.slot_rows()), (a.eng.store.obs, b.eng.store.obs),
-                 (a.eng.store.act, b.eng.store.act), (a.eng.h, b.eng.h), (a.eng.ht, b.eng.ht),
+                 (a.eng.store.obs[ra], b.eng.store.obs[rb]), (a.eng.store.act[ra], b.eng.store.act[rb]),
+                 (a.eng.store.rew[ra], b.eng.store.rew[rb]), (a.eng.h, b.eng.h), (a.eng.ht, b.eng.ht),
                  (a.eng.chunk_td, b.eng.chunk_td), (a.score_acc, b.score_acc)]:
         assert torch.equal(x, y)
     for x, y in zip(a.eng.env.get_state(), b.eng.env.get_state()):

@@ -18,9 +18,18 @@ DEV = "cuda"
 
 
 def _state(e):
+    """The engine state as the algorithm sees it: the PER (tree, and the chunk each slot names: store rows gathered
+    through the slot map), the current chunk's staged slots, hiddens, priorities, rings, RNG counter, env state. The
+    physical store rows differ between the modes (the chunk launches rotate S staging sets, the fused step uses one),
+    so rows are compared through the maps, not by index."""
     torch.cuda.synchronize()
-    st = [e.store.obs, e.store.act, e.store.rew, e.store.done, e.h, e.ht, e.chunk_td, e.cur_row, e.staging,
-          e.per.tree(), e.per.slot_rows(), e.act, e.last_rew, e.last_done, e.counter_dev[e.t % 2 if e.fused else 0]]
+    rows = e.per.slot_rows().long()
+    c = e.t % e.C
+    stg = e.staging.long()
+    st = [e.store.obs[rows], e.store.act[rows], e.store.rew[rows], e.store.done[rows],
+          e.store.obs[stg, :c + 1] if c else e.store.obs[stg, :0], e.store.act[stg, :c], e.store.rew[stg, :c],
+          e.store.done[stg, :c], e.h, e.ht, e.chunk_td, e.cur_row >= 0,
+          e.per.tree(), e.act, e.last_rew, e.last_done, e.counter_dev[e.t % 2 if e.fused else 0]]
     return [x.detach().clone().cpu() for x in st] + [torch.as_tensor(v) for v in e.env.get_state()]
 
 
@@ -29,7 +38,7 @@ def _pair(E, f1, g, h, seed, guard=False, n=8, cap_mult=4, chunk=10, max_steps=1
     kw = dict(f1=f1, g=g, h=h, chunk=chunk, capacity=cap_mult * E, seed=seed, max_steps=max_steps, device=DEV)
     a = RolloutEngine(E, n, fused=True, **kw)
     b = RolloutEngine(E, n, persistent=True, **kw)
-    assert a.fused and not a.chunked and b.chunked and not b.fused and b.graph_steps() == 2 * chunk
+    assert a.fused and not a.chunked and b.chunked and not b.fused and b.graph_steps() == b.S * chunk
     if guard:   # agent 3 beyond the fp16 range: both engines run it on the exact-f32 image
         for eng in (a, b):
             with torch.no_grad():
@@ -78,23 +87,23 @@ def test_chunk_eager_steps_bit_identical_to_fused(E, f1, g, h, guard, n):
 
 @pytest.mark.parametrize("guard", [False, True])
 def test_chunk_launch_spans_and_graphs_bit_identical_to_fused(guard):
-    """Multi-step chunk launches inside graphs — region graphs entered mid-chunk (spans 7 + 10 + 3), whole-cycle
-    chunk graphs (10 + 10), single-step graphs, a region from a chunk boundary (10 + 3) — through PER eviction
-    (2 x E capacity), against eager fused steps."""
+    """Multi-step chunk launches inside graphs — region graphs entered mid-chunk (one 20-step launch across two chunk
+    ends, phase 3), whole-cycle chunk graphs (S C = 40 steps: launches of 30 + 10), single-step graphs, a region from a
+    chunk boundary (13 steps) — through PER eviction (2 x E capacity), against eager fused steps."""
     a, b = _pair(2048, 64, 64, 64, seed=23, guard=guard, cap_mult=2)
-    for _ in range(93):
-        a.step(0.3)
-    a.flush_td()
     b.run_steps(3, 0.3)                        # single-step graphs (phase 0..2)
     b.capture_region(20)
-    b.run_steps(20, 0.3)                       # region graph at phase 3: launches of 7, 10, 3 steps
-    b.run_steps(7, 0.3)                        # phase 3 .. 9: single steps
-    b.run_steps(20, 0.3)                       # phase 10 .. : single steps to the cycle start, then ...
-    b.run_graph(0.3)                           # ... t = 50 -> 70: whole-cycle graph (10 + 10)
+    b.run_steps(20, 0.3)                       # region graph at phase 3: ONE launch of 20 steps (3 chunks)
+    b.run_steps(7, 0.3)                        # phase 23 .. 29: single steps
+    b.run_steps(20, 0.3)                       # phase 30 .. : single steps to the cycle start, then 10 more
+    b.run_graph(0.3)                           # t = 50 -> 90: whole-cycle graph (30 + 10)
     b.capture_region(13)
-    b.run_steps(13, 0.3)                       # phase 10 (a chunk boundary): 10 + 3
+    b.run_steps(13, 0.3)                       # phase 10 (a chunk boundary): one launch of 13
     b.run_steps(10, 0.3)
-    assert a.t == b.t == 93
+    for _ in range(b.t):
+        a.step(0.3)
+    a.flush_td()
+    assert a.t == b.t == 113
     _same(a, b, "end")
     b.check_errors()
 
@@ -108,13 +117,13 @@ def test_chunk_long_chunks_and_inner_resets_bit_identical_to_fused(chunk, max_st
     C = chunk
     a, b = _pair(2048, 64, 64, 64, seed=29, cap_mult=2, chunk=C, max_steps=max_steps)
     ora = VecEnvOracle(EnvSpec(8, max_steps), 2048)
-    b.run_graph(0.3)                           # 2C steps: launches of C + C
+    b.run_graph(0.3)                           # S C steps: launches of 3C + C
     b.run_steps(3, 0.3)                        # single-step graphs
     b.capture_region(2 * C)
-    b.run_steps(2 * C, 0.3)                    # region graph at phase 3: C - 3, C, 3
+    b.run_steps(2 * C, 0.3)                    # region graph at phase 3: ONE launch over chunk pieces C - 3, C, 3
     b.run_steps(C - 3, 0.3)                    # to a chunk boundary
     b.capture_region(C + 4)
-    b.run_steps(C + 4, 0.3)                    # region from a chunk boundary: C, 4
+    b.run_steps(C + 4, 0.3)                    # region from a chunk boundary: one launch, pieces C, 4
     n_b = b.t
     for t in range(n_b):
         a.step(0.3)

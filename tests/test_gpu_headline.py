@@ -68,7 +68,7 @@ def test_headline_engine_vs_oracle_through_eviction(mode):
     kw = dict(persistent=True) if mode == "chunk" else dict(fused=True)
     eng = RolloutEngine(E, N, f1=64, g=H, h=H, chunk=C, capacity=cap, seed=seed, device=DEV, **kw)
     if mode == "chunk":
-        assert eng.chunked and eng.graph_steps() == 2 * C
+        assert eng.chunked and eng.graph_steps() == eng.S * C
         assert RolloutEngine(E, N, f1=64, g=H, h=H, chunk=C, capacity=E, device=DEV).chunked   # the default mode
     else:
         assert eng.fused and eng.graph_steps() == 3 * C
@@ -122,7 +122,8 @@ def test_headline_engine_vs_oracle_through_eviction(mode):
         new_staging = slot_row[slots].copy()
         slot_row[slots] = rows
         np.testing.assert_array_equal(eng.per.slot_rows().cpu().numpy(), slot_row)
-        np.testing.assert_array_equal(eng.staging.cpu().numpy(), new_staging)
+        # (the evicted rows go back into this chunk's staging set: chunk mode rotates S sets, the fused mode has one)
+        np.testing.assert_array_equal(eng.staging_all[eng.staging_set(k * C)].cpu().numpy(), new_staging)
         assert len(eng.per) == min(cap, (k + 1) * E)
         # ---- PER slot contents: the rows the device's slot map names hold the oracle's chunks
         for sl, dg in zip(slots, digests(O, eng.store.act[rows].cpu().numpy(), R, eng.store.done[rows].cpu().numpy())):
