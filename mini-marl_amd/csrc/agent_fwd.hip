@@ -1058,6 +1058,9 @@ __global__ __launch_bounds__(256, (F1 > 64 ? 1 : 2)) void agent_q_fwd_kernel(QFw
 #ifndef MM_H3_LB
 #define MM_H3_LB 1
 #endif
+#ifndef MM_ABL
+#define MM_ABL 0   // ABLATION (timing-only variant builds, wrong results): bit mask of removed work
+#endif
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -1077,7 +1080,7 @@ struct KS {
 #endif
 typedef _Float16 f16x2_ __attribute__((ext_vector_type(2)));
 typedef float f32x2_ __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void split8(const float (&x)[8], KS& t) {
+__device__ __forceinline__ void split8(const float (&x)[8], KS& t, int lo_pairs = 4) {
 #if MM_SPLIT_MIX
   // per pair: hi = v_cvt_pk_f16_f32 (round to nearest even, as (_Float16)x), lo = f16(x - hi) by v_fma_mixlo / mixhi
   // (fma(hi, -1, x) with hi read as f16 and x as f32: the residual x - hi is exact in f32, rounded once to f16 — the
@@ -1088,9 +1091,15 @@ __device__ __forceinline__ void split8(const float (&x)[8], KS& t) {
     const f32x2_ v = {x[2 * j], x[2 * j + 1]};
     hw[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_));
     uint32_t lo;
+    if (MM_ABL & 8) {
+      lw[j] = hw[j];
+    } else if (j >= lo_pairs) {
+      lw[j] = 0u;   // (pairs known to be exact in f16: lo = +0, what the fma_mix pair would give)
+    } else {
     asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hw[j]), "v"(v.x));
     asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hw[j]), "v"(v.y));
     lw[j] = lo;
+    }
   }
   t.h = __builtin_bit_cast(f16x8, hw);
   t.l = __builtin_bit_cast(f16x8, lw);
@@ -1160,7 +1169,8 @@ __device__ __forceinline__ void load_obs_ks(const float* orow, int kb, int D, fl
 // out_off: element offset of the act / qsel outputs (the fused rollout step's ring slot)
 template <int AT>
 __device__ __forceinline__ int q_epilogue16(const QFwdParams& p, int agent, int e, bool valid,
-                                            const f32x4 (&qa)[AT], float eps, uint64_t ctr, int64_t out_off = 0) {
+                                            const f32x4 (&qa)[AT], float eps, uint64_t ctr, int64_t out_off = 0,
+                                            const uint64_t* rng_in = nullptr) {
   const int g = (threadIdx.x & 63) >> 4;
   const mm_qfwd_io& io = p.io;
   if (valid && io.q_out) {
@@ -1201,14 +1211,18 @@ __device__ __forceinline__ int q_epilogue16(const QFwdParams& p, int agent, int 
 #ifndef MM_RNG_SPLIT
 #define MM_RNG_SPLIT 1
 #endif
-    if (MM_RNG_SPLIT && !io.u && !io.rand_act) {
+    if (MM_ABL & 1) {
+    } else if (MM_RNG_SPLIT && !io.u && !io.rand_act) {
       // both device draws of env c in ONE rng_draw sequence: lanes of even g draw the uniform, odd g the random
       // action (the same (seed, counter, e, b) streams as two calls), exchanged across g by an xor-16 shuffle
       const bool ra_lane = (g & 1) != 0;
-      const uint64_t r = rng_draw(ra_lane ? io.seed ^ 0x5bd1e995ull : io.seed, ctr, (uint64_t)e,
-                                  ra_lane ? (uint64_t)agent : 0xFFFFFFFFull);
+      // (rng_in: this lane's rng_inner(e, b), computed once per launch by the chunk-persistent rollout)
+      const uint64_t sd = ra_lane ? io.seed ^ 0x5bd1e995ull : io.seed;
+      const uint64_t r = rng_in ? rng_draw_inner(sd, ctr, *rng_in)
+                                : rng_draw(sd, ctr, (uint64_t)e, ra_lane ? (uint64_t)agent : 0xFFFFFFFFull);
       const float uu = rng_uniform(r);
-      const int ra = (int)rng_mod_small(r, (uint32_t)p.A);
+      const uint32_t Au = (uint32_t)p.A;
+      const int ra = (int)rng_mod_small_u(r, Au, 0xFFFFFFFFu / Au, (0xFFFFFFFFu % Au + 1u) % Au);
       const float uo = __shfl_xor(uu, 16);
       const int rao = __shfl_xor(ra, 16);
       if ((ra_lane ? uo : uu) <= eps) act = ra_lane ? ra : rao;
@@ -1253,7 +1267,8 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
                                                     const float* __restrict__ W, const OL& ol,
                                                     float (&xn)[8], const f32x4 (&h0)[H / 16], float eps,
                                                     uint64_t ctr, int64_t out_off = 0, int x16_from_kb = 1 << 30,
-                                                    f32x4 (*h1_keep)[H / 16] = nullptr, bool store_h = true) {
+                                                    f32x4 (*h1_keep)[H / 16] = nullptr, bool store_h = true,
+                                                    const uint64_t* rng_in = nullptr) {
   using CG = QnetCGeo<F1, G, H, AB>;
   constexpr int T1 = F1 / 16, T2 = G / 16, TH = H / 16, AT = (AB * 32 + 15) / 16;
   constexpr int RB1 = F1 / 32, RB2 = G / 32, HB = H / 32;
@@ -1301,7 +1316,9 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
   for (int t = 0; t < T1; ++t) x1[t] = wbias(CG::off_b1, t);
   for (int kb = 0; kb < p.g.KD; ++kb) {
     KS ob;
-    split8(xn, ob);
+    // observation k-steps from x16_from_kb on are exact in f16 (the rollout's 0/1 bits: no lo part at all); in the
+    // rollout's k-step 0 only pair 0 (features 0, 1 of lane group 0: the two coordinates) can have one
+    split8(xn, ob, kb >= x16_from_kb ? 0 : (x16_from_kb == 1 ? 1 : 4));
     if (kb + 1 < p.g.KD) ol(kb + 1, xn);
     if (kb >= x16_from_kb) {   // observation k-steps known to be exact in f16 (the fused rollout step's bits)
 #pragma unroll
@@ -1394,24 +1411,35 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
       const f32x2 vr = {ar[rp], ar[rp + 1]}, vz = {az[rp], az[rp + 1]};
       const f32x2 vx = {anx[rp], anx[rp + 1]}, vh = {anh[rp], anh[rp + 1]}, v0 = {h0[t][rp], h0[t][rp + 1]};
       f32x2 er = vr * -1.4426950408889634f, ez = vz * -1.4426950408889634f;
+      if (!(MM_ABL & 2)) {
       er.x = __builtin_amdgcn_exp2f(er.x);
       er.y = __builtin_amdgcn_exp2f(er.y);
       ez.x = __builtin_amdgcn_exp2f(ez.x);
       ez.y = __builtin_amdgcn_exp2f(ez.y);
+      }
       er = er + 1.0f;
       ez = ez + 1.0f;
       f32x2 rr, z;
+      if (MM_ABL & 2) {
+        rr = er;
+        z = ez;
+      } else {
       rr.x = __builtin_amdgcn_rcpf(er.x);
       rr.y = __builtin_amdgcn_rcpf(er.y);
       z.x = __builtin_amdgcn_rcpf(ez.x);
       z.y = __builtin_amdgcn_rcpf(ez.y);
+      }
       f32x2 en = (vx + rr * vh) * 2.8853900817779268f;
+      f32x2 n;
+      if (MM_ABL & 2) {
+        n = en;
+      } else {
       en.x = __builtin_amdgcn_exp2f(en.x);
       en.y = __builtin_amdgcn_exp2f(en.y);
       en = en + 1.0f;
-      f32x2 n;
       n.x = __builtin_amdgcn_rcpf(en.x);
       n.y = __builtin_amdgcn_rcpf(en.y);
+      }
       n = 1.0f - 2.0f * n;
       const f32x2 hn = n + z * (v0 - n);
       h1[t][rp] = hn.x;
@@ -1476,7 +1504,7 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
       for (int kb = 0; kb < HB; ++kb) mmb(CG::off_q + ((t >> 1) * HB + kb) * 1024, t & 1, h1s[kb], qa[t]);
     }
   }
-  return q_epilogue16<AT>(p, agent, e, valid, qa, eps, ctr, out_off);
+  return q_epilogue16<AT>(p, agent, e, valid, qa, eps, ctr, out_off, rng_in);
 }
 
 // The LDS-staged large-E kernel on the fp16x3 image: a 1024-thread block (16 waves x 16 envs = 256
@@ -2222,6 +2250,14 @@ __device__ __forceinline__ void roll_chunk_steps() {
   f32x4 hkeep[H / 16];
 #pragma unroll
   for (int t = 0; t < H / 16; ++t) hkeep[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // behavior lanes: the (env, agent) part of the eps-greedy draws (rng_inner) is the same every step
+  uint64_t rin = 0;
+  if (!EXACT) {
+    const ChunkCtx c0x = chunk_ctx<F1, G, H, AB>(kargs0);
+    const int l0 = (int)threadIdx.x & 63;
+    const int e_r = c0x.e0 + ((int)threadIdx.x >> 6) * 16 + (l0 & 15);
+    rin = rng_inner((uint64_t)e_r, ((l0 >> 4) & 1) ? (uint64_t)c0x.agent : 0xFFFFFFFFull);
+  }
   for (int i = 0; i < nsteps; ++i) {
   // every per-launch constant is re-derived from the kernarg segment in each step (scalar loads, K$ hits) through
   // a pointer the compiler cannot prove invariant, and every lane index from a thread id it cannot hoist: nothing
@@ -2483,11 +2519,15 @@ __device__ __forceinline__ void roll_chunk_steps() {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int f0 = kb * 32 + 16 * q + 4 * g;
+          if (MM_ABL & 4) {
+            for (int j = 0; j < 4; ++j) x[4 * q + j] = (float)((wd >> (f0 + j)) & 1);
+          } else {
           roll_feat4(wd, f0, cr, cc, x + 4 * q);
           if (bd || e >= E)
 #pragma unroll
             for (int j = 0; j < 4; ++j) x[4 * q + j] = (e < E && f0 + j < D) ? ev.reset_obs[agent * D + f0 + j] : 0.0f;
-          if (dst) roll_store4(dst, f0, D, x + 4 * q);
+          }
+          if (dst && !(MM_ABL & 16)) roll_store4(dst, f0, D, x + 4 * q);
         }
       };
       float xn[8];
@@ -2497,7 +2537,7 @@ __device__ __forceinline__ void roll_chunk_steps() {
       // (the image base offset by the per-step opaque zero: the fragment addresses are formed inside the step,
       // not hoisted out of the loop into registers that then spill)
       const int a = agent_q_fwd_body_h3<F1, G, H, AB>(p, agent, e, wsm_ptr() + tz, ol, xn, h0, cx.eps, ctr, off, 1,
-                                                      &hkeep, i + 1 == nsteps);
+                                                      &hkeep, i + 1 == nsteps, &rin);
       // behavior blocks: each wave publishes its 16 envs' actions of step t + 1 as soon as its forward is done (every
       // lane (c, g) holds env c's action): lanes 0-7 / 8-15 OR their nibbles into the two hand-off words of the wave
       if (second && i + 1 < rc.n) {

@@ -48,6 +48,19 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 __device__ __forceinline__ uint64_t rng_draw(uint64_t seed, uint64_t counter, uint64_t a, uint64_t b) {
   return mix64(seed ^ mix64(counter * 0xD1B54A32D192ED03ull ^ mix64(a * 0x8CB92BA72F3D8DD7ull + b)));
 }
+// rng_draw split at its (a, b) part: rng_draw(seed, counter, a, b) == rng_draw_inner(seed, counter, rng_inner(a, b)),
+// so a lane that draws with the same (a, b) every step computes rng_inner once
+__device__ __forceinline__ uint64_t rng_inner(uint64_t a, uint64_t b) { return mix64(a * 0x8CB92BA72F3D8DD7ull + b); }
+__device__ __forceinline__ uint64_t rng_draw_inner(uint64_t seed, uint64_t counter, uint64_t inner) {
+  return mix64(seed ^ mix64(counter * 0xD1B54A32D192ED03ull ^ inner));
+}
+// x % m for a wave-uniform 1 <= m <= 65536 without a division: q0 = umulhi(x, floor((2^32 - 1) / m)) is floor(x / m)
+// or up to 2 below it, so x - q0 m lies in [0, 3 m) and two conditional subtractions make it exact
+__device__ __forceinline__ uint32_t umod_small(uint32_t x, uint32_t m, uint32_t minv) {
+  uint32_t r = x - __umulhi(x, minv) * m;
+  r = r >= m ? r - m : r;
+  return r >= m ? r - m : r;
+}
 // the rollout priority term |sum_i r_i + (1 - d) gamma sum_i max Q'_i - sum_i Q_i(a_i)| (cal_td_error,
 // vdn/_utils.py:44-52) with ONE fixed rounding sequence (no FMA contraction): every kernel that folds a rollout TD
 // (two-launch, fused, chunk-persistent, PER insert) produces the same bits
@@ -60,6 +73,10 @@ __device__ __forceinline__ float rng_uniform(uint64_t r) { return (float)(r >> 4
 __device__ __forceinline__ uint32_t rng_mod_small(uint64_t r, uint32_t m) {
   const uint32_t p32 = (0xFFFFFFFFu % m + 1u) % m;   // 2^32 mod m
   return ((uint32_t)(r >> 32) % m * p32 + (uint32_t)r % m) % m;
+}
+// the same value with the wave-uniform constants hoisted: minv = 0xFFFFFFFF / m, p32 = 2^32 mod m
+__device__ __forceinline__ uint32_t rng_mod_small_u(uint64_t r, uint32_t m, uint32_t minv, uint32_t p32) {
+  return umod_small(umod_small((uint32_t)(r >> 32), m, minv) * p32 + umod_small((uint32_t)r, m, minv), m, minv);
 }
 // max(x, 0) on the bit pattern: one v_max_i32 (negative floats are negative integers; no canonicalising v_max_f32
 // pair), equal to fmaxf(x, 0) for every non-NaN x but -0 -> +0

@@ -1,5 +1,5 @@
 """Eager chunk-kernel launches for counter runs (tools/pmc_chunk.sh): the headline shape (4096 envs x 8 agents,
-GRU-64, chunk 10), 3 warm-up launches, then 10 launches of the C = 10 steps of a chunk. GPU only."""
+GRU-64, chunk 10), 3 warm-up launches, then 10 launches of 20 steps (the bench region's launch). GPU only."""
 import os
 import sys
 
@@ -10,7 +10,7 @@ from minimarl.engine import RolloutEngine  # noqa: E402
 E, N, C = 4096, 8, 10
 eng = RolloutEngine(E, N, f1=64, g=64, h=64, chunk=C, capacity=4 * E, seed=1, device="cuda", persistent=True)
 for _ in range(13):
-    eng.chunk_only(C)
+    eng.chunk_only(2 * C)
 torch.cuda.synchronize()
 eng.check_errors()
 print("ok")

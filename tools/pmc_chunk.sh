@@ -1,5 +1,5 @@
 #!/bin/bash
-# Counters of the chunk-persistent rollout kernel (tools/mb_chunk_pmc.py: 13 launches of 10 steps at 4096 x 8,
+# Counters of the chunk-persistent rollout kernel (tools/mb_chunk_pmc.py: 13 launches of 20 steps at 4096 x 8,
 # GRU-64): three SQ passes (8 SQ + GRBM each) -> tools/pmc_fwd_sum.py, and two HBM passes (FETCH_SIZE, WRITE_SIZE)
 # -> tools/pmc_traffic.py. Each pass its own rocprofv3 run. usage: bash tools/pmc_chunk.sh <outdir>
 export TMPDIR=/tmp
@@ -13,10 +13,10 @@ for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv --pmc $P -d $O/p$i -- python3 tools/mb_chunk_pmc.py > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
 done
-python3 tools/pmc_fwd_sum.py $O rollout_chunk_kernel "rollout_chunk_kernel<64,64,64,1> (10 rollout steps per launch; grid 262144 = 256 blocks x 1024)" > $O/summary_sq.json || exit 1
+python3 tools/pmc_fwd_sum.py $O rollout_chunk_kernel "rollout_chunk_kernel<64,64,64,1> (20 rollout steps per launch; grid 262144 = 256 blocks x 1024)" > $O/summary_sq.json || exit 1
 timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/fetch -- python3 tools/mb_chunk_pmc.py > $O/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
 timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $O/write -- python3 tools/mb_chunk_pmc.py > $O/write.log 2>&1 || { echo "write pass failed"; exit 1; }
-# algorithmic bytes of one C = 10 launch at 4096 x 8 (D 47, H 64, 12 x 8 grid), bench.py's formula (hidden states
-# in / out once per launch): 10 (32768 (188 + 16) + 4096 x 9) + 32768 (1024 + 12) + 4096 (192 + 24)
-python3 tools/pmc_traffic.py $O/fetch $O/write rollout_chunk_kernel 262144 102047744 $O/pmc_rollout_chunk.json \
+# algorithmic bytes of one 20-step launch at 4096 x 8 (D 47, H 64, 12 x 8 grid), bench.py's formula (hidden states
+# in / out once per launch): 20 (32768 (188 + 16) + 4096 x 9) + 32768 (1024 + 12) + 4096 (192 + 24)
+python3 tools/pmc_traffic.py $O/fetch $O/write rollout_chunk_kernel 262144 169263104 $O/pmc_rollout_chunk.json \
   "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace --output-format csv -- python3 tools/mb_chunk_pmc.py (two separate passes)"

@@ -1,15 +1,15 @@
-"""Summarise an SQ / GRBM counter run (tools/pmc_roll_sq.sh and friends): per-dispatch means of every counter over
+"""Summarise an SQ / GRBM counter run (tools/pmc_chunk.sh and friends): per-dispatch means of every counter over
 the dispatches of one kernel, plus derived fractions. Usage:
     python tools/pmc_fwd_sum.py <dir> [<kernel-name substring> <label> [<grid size>]]
 
-Normalisation (verdict r04 item 7): a counter run is several `rocprofv3 --pmc` passes, each with its own kernel
-trace; GRBM_GUI_ACTIVE and the kernel duration are matched PER DISPATCH WITHIN ONE PASS (same Dispatch_Id in that
-pass's counter_collection.csv and kernel_trace.csv), never a counter of one pass against a duration of another.
-From the matched pairs: effective clock = GRBM_GUI_ACTIVE / 8 XCDs / duration. MFMA busy is reported against
-SIMD-cycles = (duration x clock) x 1024 SIMDs with clock = min(effective clock, 2.4 GHz) — the GRBM window can
-include counter start / stop around the dispatch (an effective clock above the 2.4 GHz peak engine clock shows
-it), so the kernel's own duration at the peak clock is the cap (a lower bound on the busy fraction is the same
-ratio at 2.4 GHz, an upper bound at the effective clock if that is lower)."""
+Clock normalisation (verdict r05 item 5): a counter run is several `rocprofv3 --pmc` passes, each with its own kernel
+trace; counters and the kernel duration are matched PER DISPATCH WITHIN ONE PASS (same Dispatch_Id in that pass's
+counter_collection.csv and kernel_trace.csv). The clock of a dispatch is SQ_BUSY_CYCLES / 32 shader engines /
+duration (SQ_BUSY_CYCLES counts engine cycles per SE, summed over the 8 XCDs x 4 SEs): it agrees with the in-kernel
+s_memtime clock of the chunk kernel's debug build (tools/chunk_trace.py) and stays below the 2.4 GHz peak, where
+GRBM_GUI_ACTIVE / 8 / duration reads high on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md, DVFS) — that
+quotient is kept only as a diagnostic, never capped or used. MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (duration x
+SQ clock x 1024 SIMDs), both from the same dispatch of the same pass."""
 import csv
 import glob
 import json
@@ -20,9 +20,9 @@ d = sys.argv[1]
 KN = sys.argv[2] if len(sys.argv) > 2 else "agent_q_fwd_h3_kernel"
 LABEL = sys.argv[3] if len(sys.argv) > 3 else KN
 GRID = int(sys.argv[4]) if len(sys.argv) > 4 else 262144
-PEAK_GHZ, SIMDS, XCDS = 2.4, 1024, 8
+PEAK_GHZ, SIMDS, XCDS, SES = 2.4, 1024, 8, 32
 
-acc, clocks, durs = {}, [], []
+acc, clocks, grbm_clocks, durs = {}, [], [], []
 busy_cycles = {}      # counter -> list of (value, simd-cycles of the same dispatch)
 for pdir in sorted(glob.glob(os.path.join(d, "p*"))):
     if not os.path.isdir(pdir):
@@ -42,13 +42,17 @@ for pdir in sorted(glob.glob(os.path.join(d, "p*"))):
     for (name, did), v in per.items():
         acc.setdefault(name, []).append(v)
     for (name, did), v in per.items():
-        if name != "GRBM_GUI_ACTIVE" or did not in dur:
+        if did not in dur:
             continue
         t = dur[did]
-        clk = v / XCDS / t / 1e9
+        if name == "GRBM_GUI_ACTIVE":
+            grbm_clocks.append(v / XCDS / t / 1e9)
+        if name != "SQ_BUSY_CYCLES":
+            continue
+        clk = v / SES / t / 1e9
         clocks.append(clk)
         durs.append(t)
-        cyc = t * min(clk, PEAK_GHZ) * 1e9 * SIMDS
+        cyc = t * clk * 1e9 * SIMDS
         for (n2, d2), v2 in per.items():
             if d2 == did and n2 in ("SQ_VALU_MFMA_BUSY_CYCLES",):
                 busy_cycles.setdefault(n2, []).append((v2, cyc, t * PEAK_GHZ * 1e9 * SIMDS))
@@ -57,9 +61,14 @@ out = {"kernel": LABEL, "dispatches": {k: len(v) for k, v in acc.items()}, "mean
 if durs:
     out["mean_us_traced_matched"] = 1e6 * sum(durs) / len(durs)
     out["effective_clock_ghz"] = sum(clocks) / len(clocks)
+    out["effective_clock_ghz_min"] = min(clocks)
     out["effective_clock_ghz_max"] = max(clocks)
-    out["clock_normalisation"] = ("per dispatch within one pass: GRBM_GUI_ACTIVE / 8 / duration; SIMD-cycles = "
-                                  "duration x min(that clock, 2.4 GHz) x 1024")
+    out["clock_normalisation"] = ("per dispatch within one pass: SQ_BUSY_CYCLES / 32 SEs / duration; SIMD-cycles = "
+                                  "duration x that clock x 1024")
+if grbm_clocks:
+    out["grbm_gui_active_clock_ghz_diagnostic"] = {"mean": sum(grbm_clocks) / len(grbm_clocks), "max": max(grbm_clocks),
+                                                   "note": "GRBM_GUI_ACTIVE / 8 / duration: reads high on short "
+                                                           "dispatches; not used"}
 for k, v in busy_cycles.items():
     out["mfma_busy_frac_of_simd_cycles"] = sum(a for a, _, _ in v) / sum(c for _, c, _ in v)
     out["mfma_busy_frac_at_peak_clock"] = sum(a for a, _, _ in v) / sum(p for _, _, p in v)
