@@ -404,16 +404,303 @@ __device__ __forceinline__ void ld_row32(const float* base, int64_t row, float (
   }
 }
 
+// ---------------------------------------------------------------- fp16x3 products of pass G
+// Every fp32 product of pass G runs as three v_mfma_f32_32x32x16_f16 (Wl·xh + Wh·xl + Wh·xh, fp32 accumulate; Wh =
+// f16(W), Wl = f16(W - Wh), the same for x): 6 MFMAs of 32 cycles for a 32 x 32 x 32 block instead of 16
+// v_mfma_f32_32x32x2_f32 of 64 cycles (5.3x less matrix-pipe time). Both operands are scaled by powers of two
+// before the split so that their largest magnitude lies in [2^13, 2^14): the weight image by one factor per image (its
+// max |W|), the vector operand of a W x product by one factor per column (a column of the MFMA's result depends on
+// that column's operand only: the max over the row's two lanes, unscaled per lane), the operands of a weight gradient
+// (rows summed over the k dimension) by one factor per wave tile. Then every operand within 2^-16 of its scale's max
+// has normal f16 hi and lo parts, hi + lo represents it to 2^-24 relative, and the
+// dropped Wl·xl term is ~2^-24 relative: fp32-level products relative to the tile's largest terms (smaller operands
+// carry an absolute error below 2^-38 of the max). Results are unscaled by the exact inverse powers of two;
+// weight-gradient blocks, whose operand scales change from tile to tile, accumulate into a temporary tile that is
+// unscaled into the running accumulator (running scales that are only lowered measured both slower — the rescale
+// paths spill — and, where a late tile's values sit far below the running max, outside the fp32 bars).
+// The act-frag layout carries over: MFMA block j (k-steps s in [8 j, 8 j + 8)) takes lane (c, h)'s v[8 j .. 8 j + 7]
+// as its B operand (features kperm(s, h)), and the weight images hold, per 32 x 32 block, lane (i, h)'s A operand
+// W[i][kperm(8 j + e, h)] for e < 8 as f16 hi / lo pieces ([j][hi | lo][lane][8 halves], one ds_read_b128 each).
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef _Float16 h2v_ __attribute__((ext_vector_type(2)));
+typedef float f2v_ __attribute__((ext_vector_type(2)));
+struct S16 {
+  h8v h[2], l[2];
+};
+__device__ __forceinline__ void split16(const float (&v)[16], S16& o) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const f2v_ x = {v[8 * j + 2 * p], v[8 * j + 2 * p + 1]};
+      hw[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, h2v_));
+      uint32_t lo;   // lo = f16(x - hi): the residual is exact in f32, rounded once (v_fma_mixlo / mixhi)
+      asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hw[p]), "v"(x.x));
+      asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hw[p]), "v"(x.y));
+      lw[p] = lo;
+    }
+    o.h[j] = __builtin_bit_cast(h8v, hw);
+    o.l[j] = __builtin_bit_cast(h8v, lw);
+  }
+}
+__device__ __forceinline__ f32x16 mf16(const h8v& a, const h8v& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+constexpr int HBLK = 1024;   // floats per split 32 x 32 block
+// acc += W v over the first nj 16-deep k blocks (W: the split block at LDS float offset blk)
+__device__ __forceinline__ void mmh(const float* blk, const S16& v, f32x16& acc, int nj = 2) {
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (j >= nj) break;
+    const h8v ah = *reinterpret_cast<const h8v*>(blk + (2 * j * 64 + lane) * 4);
+    const h8v al = *reinterpret_cast<const h8v*>(blk + ((2 * j + 1) * 64 + lane) * 4);
+    acc = mf16(al, v.h[j], acc);
+    acc = mf16(ah, v.l[j], acc);
+    acc = mf16(ah, v.h[j], acc);
+  }
+}
+// weight-gradient accumulation, chunks on k: acc[i][n] += sum_k a[i][k] b[n][k] (a, b: transposed tiles, tget)
+__device__ __forceinline__ void accg(f32x16& acc, const S16& a, const S16& b) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    acc = mf16(a.l[j], b.h[j], acc);
+    acc = mf16(a.h[j], b.l[j], acc);
+    acc = mf16(a.h[j], b.h[j], acc);
+  }
+}
+// the power of two that brings a max magnitude m into [2^13, 2^14) (1 for m = 0)
+__device__ __forceinline__ float scale_for(float m) {
+  int e = 0;
+  (void)frexpf(m, &e);
+  return m > 0.f ? ldexpf(1.0f, 14 - e) : 1.0f;
+}
+__device__ __forceinline__ float absmax16(const float (&v)[16], float m = 0.f) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) m = fmaxf(m, fabsf(v[q]));
+  return m;
+}
+// the wave-wide max of per-lane values >= 0 (DPP within each row of 16, then v_permlane16 / 32 swaps; no LDS)
+template <int CTRL>
+__device__ __forceinline__ float dpp_max(float m) {
+  const int o = __builtin_amdgcn_update_dpp(0, __float_as_int(m), CTRL, 0xF, 0xF, false);
+  return fmaxf(m, __int_as_float(o));
+}
+__device__ __forceinline__ float wave_max(float m) {
+  m = dpp_max<0xB1>(m);    // quad_perm [1, 0, 3, 2]
+  m = dpp_max<0x4E>(m);    // quad_perm [2, 3, 0, 1]
+  m = dpp_max<0x141>(m);   // row_half_mirror
+  m = dpp_max<0x140>(m);   // row_mirror
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  m = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// the max over the two lanes of one act-frag column (chunk c: lanes c and c + 32)
+__device__ __forceinline__ float col_max(float m) {
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// split of x * s (s: a power of two)
+__device__ __forceinline__ void split16s(const float (&v)[16], float s, S16& o) {
+  float x[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) x[q] = v[q] * s;
+  split16(x, o);
+}
+// running += tmp * inv (a weight-gradient block unscaled into its accumulator)
+__device__ __forceinline__ void acc_unscale(f32x16& run, const f32x16& tmp, float inv) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) run[q] = fmaf(tmp[q], inv, run[q]);
+}
+
+// Pass G's LDS image: the split blocks of W1 (DT blocks), W2, W_ih (3 gate blocks), W_hh (3), W_ih^T (3: block g = the
+// gate-g columns), W_hh^T (3), then the f32 LayerNorm / bias / head vectors (Geo's ln0w .. bo block, same relative
+// offsets), then the wave transpose tiles (offsets in floats)
+template <int D, int O>
+struct GeoH {
+  using G = Geo<D, O>;
+  static constexpr int DT = G::DT;
+  static constexpr int W1 = 0, W2 = W1 + DT * HBLK, Wih = W2 + HBLK, Whh = Wih + 3 * HBLK, WihT = Whh + 3 * HBLK,
+                       WhhT = WihT + 3 * HBLK, vec = WhhT + 3 * HBLK, nblk = vec / HBLK;
+  static constexpr int v(int g_off) { return vec + (g_off - G::ln0w); }   // a Geo vector offset in this image
+  static constexpr int ln0w = vec, bih = vec + (G::bih - G::ln0w), bhh = vec + (G::bhh - G::ln0w),
+                       lnrw = vec + (G::lnrw - G::ln0w), lnrb = vec + (G::lnrb - G::ln0w),
+                       Wo = vec + (G::Wo - G::ln0w), bo = vec + (G::bo - G::ln0w);
+  // scales (f32): [0] the weight image's, then the static scales of the LayerNorm outputs the products read, from
+  // their bounds |LN(x) w + b| <= sqrt(n - 1) max|w| + max|b| (a normalised n-vector has no entry beyond
+  // sqrt(n - 1)): [1] f0 = LN0, [2] f1 = LN1, [3] x2 = LN2, [4] y = LN_r; the GRU hidden states (|h| < 1) use 2^14
+  static constexpr int wsc = vec + (G::scr - G::ln0w);
+  static constexpr int scr = wsc + 8, total = scr + GW * GT * TILE;
+};
+// W of split block b at (row i, column k) from the flat MGeo parameters
+template <int D, int O>
+__device__ __forceinline__ float hblk_value(const float* __restrict__ P, int b, int i, int k) {
+  using GH = GeoH<D, O>;
+  using F = MGeo<D, H, O>;
+  constexpr int DT = GH::DT;
+  if (b < DT) {
+    const int kk = 32 * b + k;
+    return kk < D ? P[F::W1 + i * F::Dp + kk] : 0.f;
+  }
+  b -= DT;
+  if (b == 0) return P[F::W2 + i * H + k];
+  b -= 1;
+  if (b < 3) return P[F::Wih + (32 * b + i) * H + k];
+  b -= 3;
+  if (b < 3) return P[F::Whh + (32 * b + i) * H + k];
+  b -= 3;
+  if (b < 3) return P[F::Wih + (32 * b + k) * H + i];   // W_ih^T, gate-b columns
+  b -= 3;
+  return P[F::Whh + (32 * b + k) * H + i];              // W_hh^T
+}
+template <int D, int O>
+__device__ void stage_h(float* sm, const float* __restrict__ P) {
+  using GH = GeoH<D, O>;
+  // the image's weight scale: max |W| over the staged matrices (every entry of a block is one (b, i, k))
+  float m = 0.f;
+  for (int x = threadIdx.x; x < GH::nblk * 1024; x += blockDim.x)
+    m = fmaxf(m, fabsf(hblk_value<D, O>(P, x >> 10, (x >> 5) & 31, x & 31)));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) sm[GH::wsc + (threadIdx.x >> 6)] = m;   // (GW = 4 waves)
+  __syncthreads();
+  const float sw = scale_for(fmaxf(fmaxf(sm[GH::wsc], sm[GH::wsc + 1]), fmaxf(sm[GH::wsc + 2], sm[GH::wsc + 3])));
+  __syncthreads();
+  if (threadIdx.x == 0) sm[GH::wsc] = sw;
+  if (threadIdx.x < 64) {   // the LayerNorm output bounds (wave 0)
+    using F = MGeo<D, H, O>;
+    const int l = threadIdx.x;
+    float w0 = 0.f, b0 = 0.f;
+    for (int k = l; k < D; k += 64) {
+      w0 = fmaxf(w0, fabsf(P[F::ln0_w + k]));
+      b0 = fmaxf(b0, fabsf(P[F::ln0_b + k]));
+    }
+    const float w1 = l < 32 ? fabsf(P[F::ln1_w + l]) : 0.f, b1 = l < 32 ? fabsf(P[F::ln1_b + l]) : 0.f;
+    const float w2 = l < 32 ? fabsf(P[F::ln2_w + l]) : 0.f, b2 = l < 32 ? fabsf(P[F::ln2_b + l]) : 0.f;
+    const float wr = l < 32 ? fabsf(P[F::lnr_w + l]) : 0.f, br = l < 32 ? fabsf(P[F::lnr_b + l]) : 0.f;
+    const float s31 = sqrtf(31.f);
+    const float B0 = sqrtf((float)(D - 1)) * wave_max(w0) + wave_max(b0), B1 = s31 * wave_max(w1) + wave_max(b1);
+    const float B2 = s31 * wave_max(w2) + wave_max(b2), Br = s31 * wave_max(wr) + wave_max(br);
+    if (l == 0) {
+      sm[GH::wsc + 1] = scale_for(B0 * 1.0001f);   // (headroom for the bound's own rounding)
+      sm[GH::wsc + 2] = scale_for(B1 * 1.0001f);
+      sm[GH::wsc + 3] = scale_for(B2 * 1.0001f);
+      sm[GH::wsc + 4] = scale_for(Br * 1.0001f);
+    }
+  }
+  _Float16* hs = reinterpret_cast<_Float16*>(sm);
+  for (int x = threadIdx.x; x < GH::nblk * 2 * HBLK; x += blockDim.x) {   // halves
+    const int b = x / (2 * HBLK), r = x % (2 * HBLK);
+    const int jp = r / 512, l = (r % 512) / 8, e8 = r % 8;
+    const int j = jp >> 1, part = jp & 1, i = l & 31, hh = l >> 5;
+    const float w = hblk_value<D, O>(P, b, i, kperm(8 * j + e8, hh)) * sw;
+    const _Float16 hi = (_Float16)w;
+    hs[x] = part ? (_Float16)(w - (float)hi) : hi;
+  }
+  for (int e = threadIdx.x; e < GH::wsc - GH::vec; e += blockDim.x)
+    sm[GH::vec + e] = stage_value<D, O>(P, Geo<D, O>::ln0w + e);
+  __syncthreads();
+}
+
+// LN0 -> L1 -> ReLU -> LN1 -> L2 -> ReLU -> LN2 of one row tile on the split image (pass G's step 1)
+template <int D, int O>
+__device__ __forceinline__ void mlp_x2_h(const float* sm, const float* __restrict__ orow, float (&x2)[16]) {
+  using GH = GeoH<D, O>;
+  using LO = LnOff<D>;
+  constexpr int DT = GH::DT;
+  const int h = lane_h();
+  const float* lv = sm + GH::ln0w;
+  const float sw = sm[GH::wsc];
+  float x[DT][16];
+  load_obs<D, DT>(orow, x);
+  float mu0, rs0;
+  ln0_stats<D, DT>(x, mu0, rs0);
+  f32x16 acc;
+  zero16(acc);
+  float f0[DT][16];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int f = 32 * t + kperm(q, h);
+      f0[t][q] = (x[t][q] - mu0) * rs0 * lv[LO::ln0w + f] + lv[LO::ln0b + f];
+    }
+  }
+  const float s0 = sm[GH::wsc + 1];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+    S16 sf;
+    split16s(f0[t], s0, sf);
+    mmh(sm + GH::W1 + t * HBLK, sf, acc, kgroups(D - 32 * t) > 2 ? 2 : 1);
+  }
+  float a1[16], f[16], mu1, rs1;
+  const float u0 = 1.0f / (sw * s0);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) a1[q] = fmaxf(acc[q] * u0 + lv[LO::b1 + kperm(q, h)], 0.f);
+  ln32(a1, mu1, rs1);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) f[q] = (a1[q] - mu1) * rs1 * lv[LO::ln1w + kperm(q, h)] + lv[LO::ln1b + kperm(q, h)];
+  zero16(acc);
+  const float s1 = sm[GH::wsc + 2];
+  {
+    S16 sf;
+    split16s(f, s1, sf);
+    mmh(sm + GH::W2, sf, acc);
+  }
+  float a2[16], mu2, rs2;
+  const float u1 = 1.0f / (sw * s1);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) a2[q] = fmaxf(acc[q] * u1 + lv[LO::b2 + kperm(q, h)], 0.f);
+  ln32(a2, mu2, rs2);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) x2[q] = (a2[q] - mu2) * rs2 * lv[LO::ln2w + kperm(q, h)] + lv[LO::ln2b + kperm(q, h)];
+}
+
+// GRU cell on the split image (Gru's arithmetic with fp16x3 products)
+template <int D, int O>
+struct GruH {
+  using GH = GeoH<D, O>;
+  float r[16], z[16], n[16], ghn[16], h2[16];
+
+  // sx2 / shin: x2 and hin split at their wave scales; ux / uh = 1 / (weight scale x that scale)
+  __device__ __forceinline__ void run(const float* sm, const S16& sx2, float ux, const S16& shin, float uh,
+                                      const float (&hin)[16]) {
+    const int h = lane_h();
+    f32x16 ai, ah;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      zero16(ai);
+      zero16(ah);
+      mmh(sm + GH::Wih + g * HBLK, sx2, ai);
+      mmh(sm + GH::Whh + g * HBLK, shin, ah);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = 32 * g + kperm(q, h);
+        const float gi = ai[q] * ux + sm[GH::bih + j], gh = ah[q] * uh + sm[GH::bhh + j];
+        if (g == 0) r[q] = sigmoidf_(gi + gh);
+        if (g == 1) z[q] = sigmoidf_(gi + gh);
+        if (g == 2) {
+          ghn[q] = gh;
+          n[q] = tanhf_(gi + r[q] * gh);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) h2[q] = n[q] + z[q] * (hin[q] - n[q]);
+  }
+};
+
 // ---------------------------------------------------------------- pass G: recurrent part
 template <int D, int A, int O>
 __device__ void gru_body(const GradArgs& k, int net, float* sm) {
-  using G = Geo<D, O>;
+  using GH = GeoH<D, O>;
   using F = MGeo<D, H, O>;
   const mm_mappo_bwd_args& a = k.a;
-  stage<D, O>(sm, a.P[net]);
+  stage_h<D, O>(sm, a.P[net]);
   const int lane = (int)(threadIdx.x & 63), ci = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform: scalar loop control
-  float* S0 = sm + G::scr + w * GT * TILE;
+  float* S0 = sm + GH::scr + w * GT * TILE;
   float* S1 = S0 + TILE;
   const int L = a.L;
   const int64_t EN = a.en, nch = (int64_t)(a.T / L) * EN, ntile = (nch + 31) / 32;
@@ -459,15 +746,15 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
       st16(hs + l * 1024, hc);
       const float* smo = sm + opaque0();
       float x2[16];
-      {
-        Mlp<D, O> mp;
-        mp.run(smo + G::W1, smo + G::W2, smo + G::ln0w, a.obs + row * D);
-        mp.x2(smo + G::ln0w, x2);
-      }
+      mlp_x2_h<D, O>(smo, a.obs + row * D, x2);
       st16(xs + l * 1024, x2);         // the GRU input of every step, for step 2 (no MLP recompute there)
       if (l + 1 < L) {
-        Gru<D, O> gr;
-        gr.run(smo, x2, hc);
+        GruH<D, O> gr;
+        S16 sx, sh;
+        const float sw = smo[GH::wsc], s_x = smo[GH::wsc + 3], s_h = 0x1p14f;
+        split16s(x2, s_x, sx);
+        split16s(hc, s_h, sh);
+        gr.run(smo, sx, 1.0f / (sw * s_x), sh, 1.0f / (sw * s_h), hc);
 #pragma unroll
         for (int q = 0; q < 16; ++q) hc[q] = gr.h2[q];
       }
@@ -483,23 +770,30 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
       ld16(opaque_ptr(hs + l * 1024), hin);
       ld16(opaque_ptr(xs + l * 1024), x2);
       __builtin_amdgcn_sched_barrier(0);
-      Gru<D, O> st;
-      st.run(smb, x2, hin);
+      GruH<D, O> st;
+      const float sw = smb[GH::wsc];
+      const float s_x = smb[GH::wsc + 3], s_h = 0x1p14f;   // (the static scales of x2 and the hidden state)
+      {
+        S16 sx, sh;
+        split16s(x2, s_x, sx);
+        split16s(hin, s_h, sh);
+        st.run(smb, sx, 1.0f / (sw * s_x), sh, 1.0f / (sw * s_h), hin);
+      }
       // head: y = LN_r(h2); out = Wo y + bo
       float mur, rsr, xr[16], y[16];
       ln32(st.h2, mur, rsr);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         xr[q] = (st.h2[q] - mur) * rsr;
-        y[q] = xr[q] * smb[G::lnrw + kperm(q, h)] + smb[G::lnrb + kperm(q, h)];
+        y[q] = xr[q] * smb[GH::lnrw + kperm(q, h)] + smb[GH::lnrb + kperm(q, h)];
       }
       float out[O];
 #pragma unroll
       for (int o = 0; o < O; ++o) {
         float s = 0.f;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) s = fmaf(smb[G::Wo + o * 32 + kperm(q, h)], y[q], s);
-        out[o] = smb[G::bo + o] + xsum(s);
+        for (int q = 0; q < 16; ++q) s = fmaf(smb[GH::Wo + o * 32 + kperm(q, h)], y[q], s);
+        out[o] = smb[GH::bo + o] + xsum(s);
       }
       // ---- loss seed d(out) (mappo.hip bwd_body; ramppo_network.py:56-209)
       const float m = valid ? a.active[row] : 0.f;
@@ -571,7 +865,7 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
 #pragma unroll
           for (int oo = 0; oo < O; ++oo) {
             if (oo == o) d = dout[oo];
-            s = fmaf(smb[G::Wo + oo * 32 + o], dout[oo], s);
+            s = fmaf(smb[GH::Wo + oo * 32 + o], dout[oo], s);
           }
           v[q] = d;
           dy[q] = s;
@@ -582,11 +876,18 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
         float At[16], Bt[16];
         tget(S0, At);
         tget(S1, Bt);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          acc_mfma(aWo, At[s], Bt[s]);
-          sbo += At[s];
+        {
+          const float s_a = scale_for(wave_max(absmax16(At))), s_b = smb[GH::wsc + 4];
+          S16 sa, sb;
+          split16s(At, s_a, sa);
+          split16s(Bt, s_b, sb);
+          f32x16 tmp;
+          zero16(tmp);
+          accg(tmp, sa, sb);
+          acc_unscale(aWo, tmp, 1.0f / (s_a * s_b));
         }
+#pragma unroll
+        for (int s = 0; s < 16; ++s) sbo += At[s];
         wave_fence();
 #pragma unroll
         for (int q = 0; q < 16; ++q) v[q] = dy[q] * xr[q];
@@ -599,7 +900,7 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
       }
       // LN_r backward -> d h2 (+ the gradient carried from the next step)
       float dh[16];
-      ln32_bwd(dy, xr, rsr, smb + G::lnrw, dh);
+      ln32_bwd(dy, xr, rsr, smb + GH::lnrw, dh);
       // ---- GRU backward (h2 = n + z (hin - n); gates r, z, n)
       float dgr[16], dgz[16], dpn[16], dghn[16];
 #pragma unroll
@@ -614,29 +915,40 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
         dghn[q] = dpn[q] * r;
         dhn[q] = d * z;
       }
+      // one column scale for the four gate deltas (the dx2 / dhh products), their wave scale for the weight gradients
+      const float md = absmax16(dghn, absmax16(dpn, absmax16(dgz, absmax16(dgr))));
+      const float c_d = scale_for(col_max(md)), s_d = scale_for(wave_max(md));
+      const float u_d = 1.0f / (sw * c_d);
+      S16 sgr, sgz;
+      split16s(dgr, c_d, sgr);
+      split16s(dgz, c_d, sgz);
       {
         // d x2 = W_ih^T dgates -> the MLP pass
         f32x16 dx2;
         zero16(dx2);
-        mm_rows<G::PT>(smb + G::WihT, dgr, dx2);
-        mm_rows<G::PT>(smb + G::WihT + 32, dgz, dx2);
-        mm_rows<G::PT>(smb + G::WihT + 64, dpn, dx2);
+        S16 spn;
+        split16s(dpn, c_d, spn);
+        mmh(smb + GH::WihT, sgr, dx2);
+        mmh(smb + GH::WihT + HBLK, sgz, dx2);
+        mmh(smb + GH::WihT + 2 * HBLK, spn, dx2);
         if (valid) {
           float v[16];
 #pragma unroll
-          for (int q = 0; q < 16; ++q) v[q] = dx2[q];
+          for (int q = 0; q < 16; ++q) v[q] = dx2[q] * u_d;
           st_row32(dx2o, row, v);
         }
       }
       {
         f32x16 dhh;
         zero16(dhh);
-        mm_rows<G::PT>(smb + G::WhhT, dgr, dhh);
-        mm_rows<G::PT>(smb + G::WhhT + 32, dgz, dhh);
-        mm_rows<G::PT>(smb + G::WhhT + 64, dghn, dhh);
+        S16 shn;
+        split16s(dghn, c_d, shn);
+        mmh(smb + GH::WhhT, sgr, dhh);
+        mmh(smb + GH::WhhT + HBLK, sgz, dhh);
+        mmh(smb + GH::WhhT + 2 * HBLK, shn, dhh);
         const float mk = a.mask[row];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) dhn[q] = (dhn[q] + dhh[q]) * mk;
+        for (int q = 0; q < 16; ++q) dhn[q] = (dhn[q] + dhh[q] * u_d) * mk;
       }
       // GRU weight gradients: dW_ih += dg x2^T, dW_hh += dgh hin^T, gate biases (two transpose tiles)
       {
@@ -647,6 +959,12 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
         tget(S0, XT);
         tget(S1, HT);
         wave_fence();
+        // (XT / HT hold x2 / hin transposed: the same values, the same wave scales)
+        S16 sXT, sHT;
+        split16s(XT, s_x, sXT);
+        split16s(HT, s_h, sHT);
+        const float u_dx = 1.0f / (s_d * s_x), u_dh = 1.0f / (s_d * s_h);
+        f32x16 tmp;
         tput(S0, dgr);
         tput(S1, dgz);
         wave_fence();
@@ -654,12 +972,23 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
           float R[16], Z[16];
           tget(S0, R);
           tget(S1, Z);
+          S16 sR, sZ;
+          split16s(R, s_d, sR);
+          split16s(Z, s_d, sZ);
+          zero16(tmp);
+          accg(tmp, sR, sXT);
+          acc_unscale(aWih[0], tmp, u_dx);
+          zero16(tmp);
+          accg(tmp, sR, sHT);
+          acc_unscale(aWhh[0], tmp, u_dh);
+          zero16(tmp);
+          accg(tmp, sZ, sXT);
+          acc_unscale(aWih[1], tmp, u_dx);
+          zero16(tmp);
+          accg(tmp, sZ, sHT);
+          acc_unscale(aWhh[1], tmp, u_dh);
 #pragma unroll
           for (int s = 0; s < 16; ++s) {
-            acc_mfma(aWih[0], R[s], XT[s]);
-            acc_mfma(aWhh[0], R[s], HT[s]);
-            acc_mfma(aWih[1], Z[s], XT[s]);
-            acc_mfma(aWhh[1], Z[s], HT[s]);
             sbr += R[s];
             sbz += Z[s];
           }
@@ -672,10 +1001,17 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
           float Nn[16], Nh[16];
           tget(S0, Nn);
           tget(S1, Nh);
+          S16 sN, sH2;
+          split16s(Nn, s_d, sN);
+          split16s(Nh, s_d, sH2);
+          zero16(tmp);
+          accg(tmp, sN, sXT);
+          acc_unscale(aWih[2], tmp, u_dx);
+          zero16(tmp);
+          accg(tmp, sH2, sHT);
+          acc_unscale(aWhh[2], tmp, u_dh);
 #pragma unroll
           for (int s = 0; s < 16; ++s) {
-            acc_mfma(aWih[2], Nn[s], XT[s]);
-            acc_mfma(aWhh[2], Nh[s], HT[s]);
             sbn += Nn[s];
             sbhn += Nh[s];
           }
@@ -1106,10 +1442,10 @@ struct GradShape {
   }
   static int run(const mm_mappo_bwd_args* a, const float* ha, const float* hc, float* ga, float* gc, float* scratch,
                  hipStream_t s) {
-    constexpr size_t lds_g = (size_t)Geo<D, A>::total * 4, lds_m = (size_t)Geo<D, A>::mtotal * 4;
-    static_assert(Geo<D, A>::total == Geo<D, 1>::total && Geo<D, A>::mtotal == Geo<D, 1>::mtotal,
+    constexpr size_t lds_g = (size_t)GeoH<D, A>::total * 4, lds_m = (size_t)Geo<D, A>::mtotal * 4;
+    static_assert(GeoH<D, A>::total == GeoH<D, 1>::total && Geo<D, A>::mtotal == Geo<D, 1>::mtotal,
                   "actor / critic LDS images differ");
-    static_assert(Geo<D, A>::total * 4 <= 160 * 1024 && Geo<D, A>::mtotal * 4 <= 160 * 1024, "LDS budget");
+    static_assert(GeoH<D, A>::total * 4 <= 160 * 1024 && Geo<D, A>::mtotal * 4 <= 160 * 1024, "LDS budget");
     // thread-safe one-time setup (a function-local static's initialiser runs once); the sizes are compile-time
     static const int attr_rc = [&]() -> int {
       MM_HIP_CHECK(hipFuncSetAttribute((const void*)mappo_grad_gru_kernel<D, A>,
