@@ -43,7 +43,7 @@ constexpr int TP = 36;         // pitch of a transpose tile row (one chunk)
 constexpr int TILE = 32 * TP;  // floats per transpose tile
 constexpr int GW = 4;          // pass G: waves per block (1 per SIMD), one block per CU
 constexpr int GT = 2;          // pass G: transpose tiles per wave
-constexpr int MT = 4;          // pass M: transpose tiles per wave
+constexpr int MT = 3;          // pass M: transpose tiles per wave
 constexpr int NB = 128;        // blocks per net and pass
 
 // LDS image of a net (padded rows; transposed W_ih / W_hh for the backward data chain). Pass G stages all
@@ -56,13 +56,7 @@ struct Geo {
                        WhhT = WihT + 32 * PT, ln0w = WhhT + 32 * PT, ln0b = ln0w + DPT, b1 = ln0b + DPT,
                        ln1w = b1 + 32, ln1b = ln1w + 32, b2 = ln1b + 32, ln2w = b2 + 32, ln2b = ln2w + 32,
                        bih = ln2b + 32, bhh = bih + 96, lnrw = bhh + 96, lnrb = lnrw + 32, Wo = lnrb + 32,
-                       bo = Wo + 8 * 32, scr = bo + 8, total = scr + GW * GT * TILE;
-    // pass M image: W1, W2, then ln0w .. ln2b at MLN + (the same offsets relative to ln0w)
-  static constexpr int MLN = Wih, mscr = MLN + (bih - ln0w);
-  // pass M waves per block: 8 (2 per SIMD, no spills at D <= 64) where the image + 8 waves' transpose tiles fit
-  // the 160 KB of LDS; wider obs (DT = 3) run 4 waves with the full register file (no spills)
-  static constexpr int MW = (DT <= 2 && (mscr + 8 * MT * TILE) * 4 <= 160 * 1024) ? 8 : 4;
-  static constexpr int mtotal = mscr + MW * MT * TILE;
+                       bo = Wo + 8 * 32, scr = bo + 8;
   static_assert(O <= 8, "head wider than 8 outputs");
 };
 
@@ -240,20 +234,6 @@ __device__ __forceinline__ float stage_value(const float* __restrict__ P, int e)
     if (o < O) v = P[F::bo + o];
   }
   return v;
-}
-// pass G: the whole image
-template <int D, int O>
-__device__ void stage(float* sm, const float* __restrict__ P) {
-  for (int e = threadIdx.x; e < Geo<D, O>::scr; e += blockDim.x) sm[e] = stage_value<D, O>(P, e);
-  __syncthreads();
-}
-// pass M: W1, W2 and the MLP's LayerNorm / bias vectors (relocated to Geo::MLN)
-template <int D, int O>
-__device__ void stage_mlp(float* sm, const float* __restrict__ P) {
-  using G = Geo<D, O>;
-  for (int e = threadIdx.x; e < G::mscr; e += blockDim.x)
-    sm[e] = stage_value<D, O>(P, e < G::MLN ? e : e - G::MLN + G::ln0w);
-  __syncthreads();
 }
 
 // obs row -> DT act-frag tiles (feature 32 t + kperm(q, h); zero beyond D)
@@ -534,8 +514,23 @@ struct GeoH {
   static constexpr int wsc = vec + (G::scr - G::ln0w);
   static constexpr int scr = wsc + 8, total = scr + GW * GT * TILE;
 };
-// W of split block b at (row i, column k) from the flat MGeo parameters
+// Pass M's LDS image: the split blocks of W1 (DT), W2, W2^T, W1^T (DT: block t = the columns 32 t .. 32 t + 31 of W1),
+// the f32 LayerNorm / bias vectors of the MLP (ln0w .. ln2b, LnOff offsets), the scales (GeoH's wsc slots), then the
+// wave transpose tiles. W1 / W2 / the vectors sit at GeoH's offsets, so the forward (MlpH) reads either image.
 template <int D, int O>
+struct GeoM {
+  using G = Geo<D, O>;
+  static constexpr int DT = G::DT;
+  static constexpr int W1 = 0, W2 = W1 + DT * HBLK, W2T = W2 + HBLK, W1T = W2T + HBLK, vec = W1T + DT * HBLK,
+                       nblk = vec / HBLK, ln0w = vec, wsc = vec + (G::bih - G::ln0w), scr = wsc + 8;
+  // waves per block: 8 (2 per SIMD) where the registers allow it (DT <= 2) and the tiles fit the 160 KB of LDS
+  static constexpr int MW = (DT <= 2 && (scr + 8 * MT * TILE) * 4 <= 160 * 1024) ? 8 : 4;
+  static constexpr int total = scr + MW * MT * TILE;
+};
+static_assert(GeoH<47, 5>::W2 == GeoM<47, 5>::W2 && GeoH<94, 5>::W2 == GeoM<94, 5>::W2, "W1 / W2 offsets");
+
+// W of split block b at (row i, column k) from the flat MGeo parameters (MI: pass M's image, else pass G's)
+template <int D, int O, bool MI>
 __device__ __forceinline__ float hblk_value(const float* __restrict__ P, int b, int i, int k) {
   using GH = GeoH<D, O>;
   using F = MGeo<D, H, O>;
@@ -547,6 +542,12 @@ __device__ __forceinline__ float hblk_value(const float* __restrict__ P, int b, 
   b -= DT;
   if (b == 0) return P[F::W2 + i * H + k];
   b -= 1;
+  if constexpr (MI) {
+    if (b == 0) return P[F::W2 + k * H + i];   // W2^T
+    b -= 1;
+    const int kk = 32 * b + i;                 // W1^T, columns 32 b ..
+    return kk < D ? P[F::W1 + k * F::Dp + kk] : 0.f;
+  }
   if (b < 3) return P[F::Wih + (32 * b + i) * H + k];
   b -= 3;
   if (b < 3) return P[F::Whh + (32 * b + i) * H + k];
@@ -555,17 +556,20 @@ __device__ __forceinline__ float hblk_value(const float* __restrict__ P, int b, 
   b -= 3;
   return P[F::Whh + (32 * b + k) * H + i];              // W_hh^T
 }
-template <int D, int O>
+// stage a split image (MI: pass M's GeoM, else pass G's GeoH) and its scales
+template <int D, int O, bool MI>
 __device__ void stage_h(float* sm, const float* __restrict__ P) {
-  using GH = GeoH<D, O>;
+  using GH = std::conditional_t<MI, GeoM<D, O>, GeoH<D, O>>;
   // the image's weight scale: max |W| over the staged matrices (every entry of a block is one (b, i, k))
   float m = 0.f;
   for (int x = threadIdx.x; x < GH::nblk * 1024; x += blockDim.x)
-    m = fmaxf(m, fabsf(hblk_value<D, O>(P, x >> 10, (x >> 5) & 31, x & 31)));
+    m = fmaxf(m, fabsf(hblk_value<D, O, MI>(P, x >> 10, (x >> 5) & 31, x & 31)));
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) sm[GH::wsc + (threadIdx.x >> 6)] = m;   // (GW = 4 waves)
+  if ((threadIdx.x & 63) == 0) sm[GH::wsc + (threadIdx.x >> 6)] = m;   // (<= 8 waves: the 8 scale slots)
   __syncthreads();
-  const float sw = scale_for(fmaxf(fmaxf(sm[GH::wsc], sm[GH::wsc + 1]), fmaxf(sm[GH::wsc + 2], sm[GH::wsc + 3])));
+  float mw = 0.f;
+  for (int ww = 0; ww < (int)(blockDim.x >> 6); ++ww) mw = fmaxf(mw, sm[GH::wsc + ww]);
+  const float sw = scale_for(mw);
   __syncthreads();
   if (threadIdx.x == 0) sm[GH::wsc] = sw;
   if (threadIdx.x < 64) {   // the LayerNorm output bounds (wave 0)
@@ -594,7 +598,7 @@ __device__ void stage_h(float* sm, const float* __restrict__ P) {
     const int b = x / (2 * HBLK), r = x % (2 * HBLK);
     const int jp = r / 512, l = (r % 512) / 8, e8 = r % 8;
     const int j = jp >> 1, part = jp & 1, i = l & 31, hh = l >> 5;
-    const float w = hblk_value<D, O>(P, b, i, kperm(8 * j + e8, hh)) * sw;
+    const float w = hblk_value<D, O, MI>(P, b, i, kperm(8 * j + e8, hh)) * sw;
     const _Float16 hi = (_Float16)w;
     hs[x] = part ? (_Float16)(w - (float)hi) : hi;
   }
@@ -603,58 +607,67 @@ __device__ void stage_h(float* sm, const float* __restrict__ P) {
   __syncthreads();
 }
 
-// LN0 -> L1 -> ReLU -> LN1 -> L2 -> ReLU -> LN2 of one row tile on the split image (pass G's step 1)
+// LN0 -> L1 -> ReLU -> LN1 -> L2 -> ReLU (-> LN2 statistics) of one row tile on a split image (GI: GeoH or GeoM; both
+// hold W1 / W2 / the MLP vectors / the scales at the same places): Mlp's arithmetic with fp16x3 products
+template <int D, class GI>
+struct MlpH {
+  using LO = LnOff<D>;
+  static constexpr int DT = GI::DT;
+  float mu0, rs0, a1[16], mu1, rs1, a2[16], mu2, rs2;
+
+  __device__ __forceinline__ void run(const float* sm, const float* __restrict__ orow) {
+    const int h = lane_h();
+    const float* lv = sm + GI::ln0w;
+    const float sw = sm[GI::wsc];
+    float x[DT][16];
+    load_obs<D, DT>(orow, x);
+    ln0_stats<D, DT>(x, mu0, rs0);
+    f32x16 acc;
+    zero16(acc);
+    const float s0 = sm[GI::wsc + 1];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      float f0[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int f = 32 * t + kperm(q, h);
+        f0[q] = (x[t][q] - mu0) * rs0 * lv[LO::ln0w + f] + lv[LO::ln0b + f];
+      }
+      S16 sf;
+      split16s(f0, s0, sf);
+      mmh(sm + GI::W1 + t * HBLK, sf, acc, kgroups(D - 32 * t) > 2 ? 2 : 1);
+    }
+    float f[16];
+    const float u0 = 1.0f / (sw * s0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a1[q] = fmaxf(acc[q] * u0 + lv[LO::b1 + kperm(q, h)], 0.f);
+    ln32(a1, mu1, rs1);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) f[q] = (a1[q] - mu1) * rs1 * lv[LO::ln1w + kperm(q, h)] + lv[LO::ln1b + kperm(q, h)];
+    zero16(acc);
+    const float s1 = sm[GI::wsc + 2];
+    {
+      S16 sf;
+      split16s(f, s1, sf);
+      mmh(sm + GI::W2, sf, acc);
+    }
+    const float u1 = 1.0f / (sw * s1);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a2[q] = fmaxf(acc[q] * u1 + lv[LO::b2 + kperm(q, h)], 0.f);
+    ln32(a2, mu2, rs2);
+  }
+};
+// x2 = LN2(a2) of one row tile on pass G's image (pass G's step 1)
 template <int D, int O>
 __device__ __forceinline__ void mlp_x2_h(const float* sm, const float* __restrict__ orow, float (&x2)[16]) {
-  using GH = GeoH<D, O>;
   using LO = LnOff<D>;
-  constexpr int DT = GH::DT;
   const int h = lane_h();
-  const float* lv = sm + GH::ln0w;
-  const float sw = sm[GH::wsc];
-  float x[DT][16];
-  load_obs<D, DT>(orow, x);
-  float mu0, rs0;
-  ln0_stats<D, DT>(x, mu0, rs0);
-  f32x16 acc;
-  zero16(acc);
-  float f0[DT][16];
+  const float* lv = sm + GeoH<D, O>::ln0w;
+  MlpH<D, GeoH<D, O>> mp;
+  mp.run(sm, orow);
 #pragma unroll
-  for (int t = 0; t < DT; ++t) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int f = 32 * t + kperm(q, h);
-      f0[t][q] = (x[t][q] - mu0) * rs0 * lv[LO::ln0w + f] + lv[LO::ln0b + f];
-    }
-  }
-  const float s0 = sm[GH::wsc + 1];
-#pragma unroll
-  for (int t = 0; t < DT; ++t) {
-    S16 sf;
-    split16s(f0[t], s0, sf);
-    mmh(sm + GH::W1 + t * HBLK, sf, acc, kgroups(D - 32 * t) > 2 ? 2 : 1);
-  }
-  float a1[16], f[16], mu1, rs1;
-  const float u0 = 1.0f / (sw * s0);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) a1[q] = fmaxf(acc[q] * u0 + lv[LO::b1 + kperm(q, h)], 0.f);
-  ln32(a1, mu1, rs1);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) f[q] = (a1[q] - mu1) * rs1 * lv[LO::ln1w + kperm(q, h)] + lv[LO::ln1b + kperm(q, h)];
-  zero16(acc);
-  const float s1 = sm[GH::wsc + 2];
-  {
-    S16 sf;
-    split16s(f, s1, sf);
-    mmh(sm + GH::W2, sf, acc);
-  }
-  float a2[16], mu2, rs2;
-  const float u1 = 1.0f / (sw * s1);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) a2[q] = fmaxf(acc[q] * u1 + lv[LO::b2 + kperm(q, h)], 0.f);
-  ln32(a2, mu2, rs2);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) x2[q] = (a2[q] - mu2) * rs2 * lv[LO::ln2w + kperm(q, h)] + lv[LO::ln2b + kperm(q, h)];
+  for (int q = 0; q < 16; ++q)
+    x2[q] = (mp.a2[q] - mp.mu2) * mp.rs2 * lv[LO::ln2w + kperm(q, h)] + lv[LO::ln2b + kperm(q, h)];
 }
 
 // GRU cell on the split image (Gru's arithmetic with fp16x3 products)
@@ -697,7 +710,7 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
   using GH = GeoH<D, O>;
   using F = MGeo<D, H, O>;
   const mm_mappo_bwd_args& a = k.a;
-  stage_h<D, O>(sm, a.P[net]);
+  stage_h<D, O, false>(sm, a.P[net]);
   const int lane = (int)(threadIdx.x & 63), ci = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform: scalar loop control
   float* S0 = sm + GH::scr + w * GT * TILE;
@@ -1083,22 +1096,25 @@ __device__ void gru_body(const GradArgs& k, int net, float* sm) {
 }
 
 // ---------------------------------------------------------------- pass M: LN-MLP backward, row-parallel
+// One wave = 32 row-steps (rows on the MFMA's N), fp16x3 products on pass M's split image: the forward (MlpH), then
+// dW2 / db2 / LN2 parameters from d x2 (pass G's output), dx1 = W2^T da2 -> LN1 backward, dW1 / db1, df0 = W1^T da1 ->
+// LN0 parameters. Weight-gradient operands are transposed through 3 LDS tiles per wave (chunks on k); the vector
+// operands of the W^T products take one scale per column (row), those of the weight gradients one per wave tile.
 template <int D, int O>
 __device__ void mlp_body(const GradArgs& k, int net, float* sm) {
-  using G = Geo<D, O>;
+  using GM = GeoM<D, O>;
   using F = MGeo<D, H, O>;
   using LO = LnOff<D>;
-  constexpr int DT = G::DT;
+  constexpr int DT = GM::DT;
   const mm_mappo_bwd_args& a = k.a;
-  stage_mlp<D, O>(sm, a.P[net]);
+  stage_h<D, O, true>(sm, a.P[net]);
   const int lane = (int)(threadIdx.x & 63), ci = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  float* S0 = sm + G::mscr + w * MT * TILE;
+  float* S0 = sm + GM::scr + w * MT * TILE;
   float* S1 = S0 + TILE;
   float* S2 = S1 + TILE;
-  float* S3 = S2 + TILE;
   const int64_t R = (int64_t)a.T * a.en, ntile = (R + 31) / 32;
-  constexpr int MWV = G::MW;
+  constexpr int MWV = GM::MW;
   const int wg = blockIdx.x * MWV + w, nwg = gridDim.x * MWV;
   const float* dx2i = k.dx2 + (int64_t)net * R * 32;
 
@@ -1115,17 +1131,18 @@ __device__ void mlp_body(const GradArgs& k, int net, float* sm) {
     const bool valid = r < R;
     const int64_t row = valid ? r : R - 1;
     const float* smb = sm + opaque0();
-    const float* lv = smb + G::MLN;
+    const float* lv = smb + GM::ln0w;
+    const float sw = smb[GM::wsc], s_f0 = smb[GM::wsc + 1], s_f1 = smb[GM::wsc + 2];
     float dxv[16];
     ld_row32(dx2i, row, dxv);
     if (!valid) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) dxv[q] = 0.f;
     }
-    Mlp<D, O> mp;
-    mp.run(smb + G::W1, smb + G::W2, lv, a.obs + row * D);
-    // ---- LN2 backward (x2 = LN2(a2), a2 = relu(W2 f1 + b2))
-    float da[16], xh[16], tt[16];
+    MlpH<D, GM> mp;
+    mp.run(smb, a.obs + row * D);
+    // ---- LN2 backward (x2 = LN2(a2), a2 = relu(W2 f1 + b2)); f1 = LN1(a1)
+    float da[16], xh[16], tt[16], f1[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) xh[q] = (mp.a2[q] - mp.mu2) * mp.rs2;
     ln32_bwd(dxv, xh, mp.rs2, lv + LO::ln2w, da);
@@ -1133,88 +1150,107 @@ __device__ void mlp_body(const GradArgs& k, int net, float* sm) {
     for (int q = 0; q < 16; ++q) {
       tt[q] = dxv[q] * xh[q];
       da[q] = mp.a2[q] > 0.f ? da[q] : 0.f;
-    }
-    tput(S2, tt);
-    tput(S3, dxv);
-    // dW2 += da2 f1^T, db2 (f1 = LN1(a1))
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
       xh[q] = (mp.a1[q] - mp.mu1) * mp.rs1;
-      tt[q] = xh[q] * lv[LO::ln1w + kperm(q, h)] + lv[LO::ln1b + kperm(q, h)];
+      f1[q] = xh[q] * lv[LO::ln1w + kperm(q, h)] + lv[LO::ln1b + kperm(q, h)];
     }
     tput(S0, da);
-    tput(S1, tt);
-    wave_fence();
-    sl2w += tsum(S2);
-    sl2b += tsum(S3);
+    tput(S1, f1);
+    tput(S2, tt);
+    const float s_a2 = scale_for(wave_max(absmax16(da)));
+    // ---- LN1 backward: dx1 = W2^T da2 (one scale per column), then da1
+    float dx1[16], da1[16];
     {
-      float At[16], Bt[16];
-      tget(S0, At);
-      tget(S1, Bt);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        acc_mfma(aW2, At[s], Bt[s]);
-        sb2 += At[s];
-      }
-    }
-    wave_fence();
-    // ---- LN1 backward: dx1 = W2^T da2
-    {
+      const float c_a = scale_for(col_max(absmax16(da)));
+      S16 sa;
+      split16s(da, c_a, sa);
       f32x16 acc;
       zero16(acc);
-      mm_cols<G::PW>(smb + G::W2, da, acc);
+      mmh(smb + GM::W2T, sa, acc);
+      const float u = 1.0f / (sw * c_a);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) dxv[q] = acc[q];
-      ln32_bwd(dxv, xh, mp.rs1, lv + LO::ln1w, da);
+      for (int q = 0; q < 16; ++q) dx1[q] = acc[q] * u;
+      ln32_bwd(dx1, xh, mp.rs1, lv + LO::ln1w, da1);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        tt[q] = dxv[q] * xh[q];
-        da[q] = mp.a1[q] > 0.f ? da[q] : 0.f;
+        tt[q] = dx1[q] * xh[q];
+        da1[q] = mp.a1[q] > 0.f ? da1[q] : 0.f;
       }
-      tput(S2, tt);
-      tput(S3, dxv);
-      tput(S0, da);
-      wave_fence();
-      sl1w += tsum(S2);
-      sl1b += tsum(S3);
-      wave_fence();
     }
+    wave_fence();
+    // dW2 += da2 f1^T, db2
+    float At[16];
+    {
+      float Bt[16];
+      tget(S0, At);
+      tget(S1, Bt);
+      sl2w += tsum(S2);
+      wave_fence();
+      tput(S0, da1);
+      tput(S1, dxv);
+      tput(S2, tt);
+      S16 sa, sb;
+      split16s(At, s_a2, sa);
+      split16s(Bt, s_f1, sb);
+      f32x16 tmp;
+      zero16(tmp);
+      accg(tmp, sa, sb);
+      acc_unscale(aW2, tmp, 1.0f / (s_a2 * s_f1));
+#pragma unroll
+      for (int s = 0; s < 16; ++s) sb2 += At[s];
+    }
+    const float s_a1 = scale_for(wave_max(absmax16(da1)));
+    wave_fence();
+    sl2b += tsum(S1);
+    sl1w += tsum(S2);
+    tget(S0, At);   // da1 transposed
+    wave_fence();
+    tput(S1, dx1);
+    wave_fence();
+    sl1b += tsum(S1);
+    wave_fence();
     // ---- L1 / LN0: dW1 += da1 f0^T, db1, df0 = W1^T da1 -> LN0 parameter gradients
     {
-      float x[DT][16];
-      load_obs<D, DT>(a.obs + row * D, x);
-      float At[16];
-      tget(S0, At);
+      S16 sa;
+      split16s(At, s_a1, sa);
 #pragma unroll
       for (int s = 0; s < 16; ++s) sb1 += At[s];
+      const float c_b = scale_for(col_max(absmax16(da1)));
+      S16 sd;
+      split16s(da1, c_b, sd);
+      const float u_b = 1.0f / (sw * c_b), u_w = 1.0f / (s_a1 * s_f0);
+      float x[DT][16];
+      load_obs<D, DT>(a.obs + row * D, x);
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
-        float x0[16], f0[16];
+        float x0[16], f0[16], dfv[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int f = 32 * t + kperm(q, h);
           x0[q] = (x[t][q] - mp.mu0) * mp.rs0;
           f0[q] = x0[q] * lv[LO::ln0w + f] + lv[LO::ln0b + f];
         }
-        tput(S1, f0);
+        tput(S0, f0);
         f32x16 acc;
         zero16(acc);
-        mm_cols<G::P1>(smb + G::W1 + 32 * t, da, acc);
-        float dfv[16];
+        mmh(smb + GM::W1T + t * HBLK, sd, acc);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          dfv[q] = acc[q];
-          tt[q] = acc[q] * x0[q];
+          dfv[q] = acc[q] * u_b;
+          tt[q] = dfv[q] * x0[q];
         }
-        tput(S2, tt);
-        tput(S3, dfv);
+        tput(S1, tt);
+        tput(S2, dfv);
         wave_fence();
         float Bt[16];
-        tget(S1, Bt);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) acc_mfma(aW1[t], At[s], Bt[s]);
-        sl0w[t] += tsum(S2);
-        sl0b[t] += tsum(S3);
+        tget(S0, Bt);
+        sl0w[t] += tsum(S1);
+        sl0b[t] += tsum(S2);
+        S16 sb;
+        split16s(Bt, s_f0, sb);
+        f32x16 tmp;
+        zero16(tmp);
+        accg(tmp, sa, sb);
+        acc_unscale(aW1[t], tmp, u_w);
         wave_fence();
       }
     }
@@ -1412,7 +1448,7 @@ __global__ __launch_bounds__(64 * GW, 1) void mappo_grad_gru_kernel(GradArgs k) 
 }
 
 template <int D, int A>
-__global__ __launch_bounds__((64 * Geo<D, A>::MW), 1) void mappo_grad_mlp_kernel(GradArgs k) {
+__global__ __launch_bounds__((64 * GeoM<D, A>::MW), 1) void mappo_grad_mlp_kernel(GradArgs k) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if (blockIdx.y == 0)
     mlp_body<D, A>(k, 0, sm);
@@ -1442,10 +1478,10 @@ struct GradShape {
   }
   static int run(const mm_mappo_bwd_args* a, const float* ha, const float* hc, float* ga, float* gc, float* scratch,
                  hipStream_t s) {
-    constexpr size_t lds_g = (size_t)GeoH<D, A>::total * 4, lds_m = (size_t)Geo<D, A>::mtotal * 4;
-    static_assert(GeoH<D, A>::total == GeoH<D, 1>::total && Geo<D, A>::mtotal == Geo<D, 1>::mtotal,
+    constexpr size_t lds_g = (size_t)GeoH<D, A>::total * 4, lds_m = (size_t)GeoM<D, A>::total * 4;
+    static_assert(GeoH<D, A>::total == GeoH<D, 1>::total && GeoM<D, A>::total == GeoM<D, 1>::total,
                   "actor / critic LDS images differ");
-    static_assert(GeoH<D, A>::total * 4 <= 160 * 1024 && Geo<D, A>::mtotal * 4 <= 160 * 1024, "LDS budget");
+    static_assert(GeoH<D, A>::total * 4 <= 160 * 1024 && GeoM<D, A>::total * 4 <= 160 * 1024, "LDS budget");
     // thread-safe one-time setup (a function-local static's initialiser runs once); the sizes are compile-time
     static const int attr_rc = [&]() -> int {
       MM_HIP_CHECK(hipFuncSetAttribute((const void*)mappo_grad_gru_kernel<D, A>,
@@ -1465,7 +1501,7 @@ struct GradShape {
     k.pstride = pstride();
     hipLaunchKernelGGL((mappo_grad_gru_kernel<D, A>), dim3(NB, 2), dim3(64 * GW), lds_g, s, k);
     MM_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL((mappo_grad_mlp_kernel<D, A>), dim3(NB, 2), dim3(64 * Geo<D, A>::MW), lds_m, s, k);
+    hipLaunchKernelGGL((mappo_grad_mlp_kernel<D, A>), dim3(NB, 2), dim3(64 * GeoM<D, A>::MW), lds_m, s, k);
     MM_HIP_CHECK(hipGetLastError());
     const int n0 = MGeo<D, H, A>::total, n1 = MGeo<D, H, 1>::total;
     hipLaunchKernelGGL(mappo_grad_sum_kernel, dim3((n0 + 255) / 256, 2), dim3(256), 0, s, k.partial, 2 * NB,
