@@ -1058,9 +1058,6 @@ __global__ __launch_bounds__(256, (F1 > 64 ? 1 : 2)) void agent_q_fwd_kernel(QFw
 #ifndef MM_H3_LB
 #define MM_H3_LB 1
 #endif
-#ifndef MM_ABL
-#define MM_ABL 0   // ABLATION (timing-only variant builds, wrong results): bit mask of removed work
-#endif
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -1091,14 +1088,12 @@ __device__ __forceinline__ void split8(const float (&x)[8], KS& t, int lo_pairs 
     const f32x2_ v = {x[2 * j], x[2 * j + 1]};
     hw[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_));
     uint32_t lo;
-    if (MM_ABL & 8) {
-      lw[j] = hw[j];
-    } else if (j >= lo_pairs) {
+    if (j >= lo_pairs) {
       lw[j] = 0u;   // (pairs known to be exact in f16: lo = +0, what the fma_mix pair would give)
     } else {
-    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hw[j]), "v"(v.x));
-    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hw[j]), "v"(v.y));
-    lw[j] = lo;
+      asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(hw[j]), "v"(v.x));
+      asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(hw[j]), "v"(v.y));
+      lw[j] = lo;
     }
   }
   t.h = __builtin_bit_cast(f16x8, hw);
@@ -1211,8 +1206,7 @@ __device__ __forceinline__ int q_epilogue16(const QFwdParams& p, int agent, int 
 #ifndef MM_RNG_SPLIT
 #define MM_RNG_SPLIT 1
 #endif
-    if (MM_ABL & 1) {
-    } else if (MM_RNG_SPLIT && !io.u && !io.rand_act) {
+    if (MM_RNG_SPLIT && !io.u && !io.rand_act) {
       // both device draws of env c in ONE rng_draw sequence: lanes of even g draw the uniform, odd g the random
       // action (the same (seed, counter, e, b) streams as two calls), exchanged across g by an xor-16 shuffle
       const bool ra_lane = (g & 1) != 0;
@@ -1411,35 +1405,24 @@ __device__ __forceinline__ int agent_q_fwd_body_h3(const QFwdParams& p, int agen
       const f32x2 vr = {ar[rp], ar[rp + 1]}, vz = {az[rp], az[rp + 1]};
       const f32x2 vx = {anx[rp], anx[rp + 1]}, vh = {anh[rp], anh[rp + 1]}, v0 = {h0[t][rp], h0[t][rp + 1]};
       f32x2 er = vr * -1.4426950408889634f, ez = vz * -1.4426950408889634f;
-      if (!(MM_ABL & 2)) {
       er.x = __builtin_amdgcn_exp2f(er.x);
       er.y = __builtin_amdgcn_exp2f(er.y);
       ez.x = __builtin_amdgcn_exp2f(ez.x);
       ez.y = __builtin_amdgcn_exp2f(ez.y);
-      }
       er = er + 1.0f;
       ez = ez + 1.0f;
       f32x2 rr, z;
-      if (MM_ABL & 2) {
-        rr = er;
-        z = ez;
-      } else {
       rr.x = __builtin_amdgcn_rcpf(er.x);
       rr.y = __builtin_amdgcn_rcpf(er.y);
       z.x = __builtin_amdgcn_rcpf(ez.x);
       z.y = __builtin_amdgcn_rcpf(ez.y);
-      }
       f32x2 en = (vx + rr * vh) * 2.8853900817779268f;
-      f32x2 n;
-      if (MM_ABL & 2) {
-        n = en;
-      } else {
       en.x = __builtin_amdgcn_exp2f(en.x);
       en.y = __builtin_amdgcn_exp2f(en.y);
       en = en + 1.0f;
+      f32x2 n;
       n.x = __builtin_amdgcn_rcpf(en.x);
       n.y = __builtin_amdgcn_rcpf(en.y);
-      }
       n = 1.0f - 2.0f * n;
       const f32x2 hn = n + z * (v0 - n);
       h1[t][rp] = hn.x;
@@ -2519,15 +2502,11 @@ __device__ __forceinline__ void roll_chunk_steps() {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int f0 = kb * 32 + 16 * q + 4 * g;
-          if (MM_ABL & 4) {
-            for (int j = 0; j < 4; ++j) x[4 * q + j] = (float)((wd >> (f0 + j)) & 1);
-          } else {
           roll_feat4(wd, f0, cr, cc, x + 4 * q);
           if (bd || e >= E)
 #pragma unroll
             for (int j = 0; j < 4; ++j) x[4 * q + j] = (e < E && f0 + j < D) ? ev.reset_obs[agent * D + f0 + j] : 0.0f;
-          }
-          if (dst && !(MM_ABL & 16)) roll_store4(dst, f0, D, x + 4 * q);
+          if (dst) roll_store4(dst, f0, D, x + 4 * q);
         }
       };
       float xn[8];

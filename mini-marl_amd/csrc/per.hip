@@ -565,9 +565,26 @@ struct MbScratch {
   uint32_t cand_n;
   uint32_t ticket;
   uint64_t sel[4];                    // b1 | (b1, b2) prefix, remaining rank, T, take_eq
-  uint64_t cand[1];                   // [2 cap] the listed (key, slot) pairs: keys at cand, slots at cand + cap
+  uint64_t cand[1];                   // [2 cap] the listed (key, slot) pairs: keys at cand, slots at cand + cap;
+                                      // then [cap] f64: the new chunks' priorities from the fold (mm_per_insert_fold)
 };
-static size_t mb_bytes(int64_t cap) { return sizeof(MbScratch) + (size_t)cap * 16; }
+static size_t mb_bytes(int64_t cap) { return sizeof(MbScratch) + (size_t)cap * 24; }
+__host__ __device__ inline double* mb_prio(MbScratch* mb, int64_t cap) {
+  return reinterpret_cast<double*>(mb->cand + 2 * cap);
+}
+
+// phase stamps of the multi-block insert (s_memrealtime, 100 MHz) per launch k and workgroup, tools/mb_per_trace.py;
+// trace builds only (-DMM_PER_TRACE=1), never the product
+#if MM_PER_TRACE
+__device__ uint64_t g_per_trace[4][64][16];
+#define PER_STAMP(k, i)                                   \
+  if (threadIdx.x == 0 && blockIdx.x < 64) g_per_trace[k][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();
+#define PER_NOTE(i, v) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_per_trace[0][0][i] = (uint64_t)(v);
+#else
+#define PER_STAMP(k, i)
+#define PER_NOTE(i, v)
+#endif
 
 __device__ __forceinline__ uint64_t leaf_key(const double* leaves, int64_t s) {
   return (uint64_t)__double_as_longlong(leaves[s]);
@@ -596,16 +613,22 @@ __device__ __forceinline__ uint32_t mb_scan(uint32_t v, uint32_t* wsum, uint32_t
   return before + incl - v;
 }
 
-// Find the bin holding the need-th key of a 4096-bin global histogram written by other workgroups'
-// atomics (read through L2 with device-scope atomic loads): returns bin, updates need to the rank inside
-// it. Every thread gets the result.
-__device__ __forceinline__ int mb_pick(uint32_t* h, int64_t& need, uint32_t* wsum, int64_t* sh) {
+// Find the bin holding the need-th key of a 4096-bin global histogram written by the previous launch's
+// atomics (complete at the launch boundary; this launch starts with invalidated vector caches, so plain
+// 16-byte loads read the L2 copies): returns bin, updates need to the rank inside it. Every thread gets the result.
+__device__ __forceinline__ int mb_pick(const uint32_t* h, int64_t& need, uint32_t* wsum, int64_t* sh) {
   uint32_t loc[16], sum = 0;
+  const uint4* h4 = reinterpret_cast<const uint4*>(h + threadIdx.x * 16);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    loc[i] = __hip_atomic_load(&h[threadIdx.x * 16 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sum += loc[i];
+  for (int i = 0; i < 4; ++i) {
+    const uint4 v = h4[i];
+    loc[4 * i] = v.x;
+    loc[4 * i + 1] = v.y;
+    loc[4 * i + 2] = v.z;
+    loc[4 * i + 3] = v.w;
   }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sum += loc[i];
   uint32_t tot;
   const uint32_t before = mb_scan(sum, wsum, &tot);
   if ((int64_t)before < need && (int64_t)(before + sum) >= need) {
@@ -735,10 +758,13 @@ template <bool VEC>
 __global__ __launch_bounds__(MB_T) void per_mb_sel1_fold(const double* __restrict__ tree, int64_t cap,
                                                          const PerDev* st, int64_t K, MbScratch* mb, int nh,
                                                          FoldArgs fa) {
-  if ((int)blockIdx.x < nh)
+  if ((int)blockIdx.x < nh) {
+    PER_STAMP(0, 0);
     mb_sel1_hist(tree, cap, st, K, mb, blockIdx.x, nh);
-  else
+    PER_STAMP(0, 1);
+  } else {
     td_fold_group<VEC>(fa, (int)blockIdx.x - nh);
+  }
 }
 
 // Every workgroup of sel2 / sel3 / apply re-derives the previous pass's decision itself from the finished
@@ -753,26 +779,33 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ t
   const int64_t n_data = st->n_data;
   int64_t need = K - min(K, cap - n_data);
   if (need <= 0) return;
+  PER_STAMP(1, 0);
+  // this block's keys first: their loads overlap the pick's round trip
+  const double* leaves = tree + (cap - 1);
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+  uint64_t kk[MB_VPT];
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    const int64_t sl = base + threadIdx.x + i * MB_T;
+    kk[i] = sl < n_data ? leaf_key(leaves, sl) : ~0ull;
+  }
   const uint64_t b1 = (uint64_t)mb_pick(mb->hist1, need, wsum, sh);
+  PER_STAMP(1, 1);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     mb->sel[0] = b1;
     mb->sel[1] = (uint64_t)need;
   }
-  const double* leaves = tree + (cap - 1);
   for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = base + threadIdx.x + i * MB_T;
-    if (sl < n_data) {
-      const uint64_t k = leaf_key(leaves, sl);
-      if ((k >> 52) == b1) atomicAdd(&h[(k >> 40) & 4095], 1u);
-    }
+    if (sl < n_data && (kk[i] >> 52) == b1) atomicAdd(&h[(kk[i] >> 40) & 4095], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 4096; i += MB_T)
     if (h[i]) atomicAdd(&mb->hist2[i], h[i]);
+  PER_STAMP(1, 2);
 }
 
 // bins[bin] += 1 for this lane when on: one LDS atomic per wave when every active lane has the same bin (the
@@ -796,9 +829,19 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
   __shared__ uint32_t h3[4096];
   const int64_t n_data = st->n_data;
   if (K - min(K, cap - n_data) <= 0) return;
+  PER_STAMP(2, 0);
+  const double* leaves = tree + (cap - 1);
+  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
+  uint64_t kk[MB_VPT];   // this block's keys first: their loads overlap the pick's round trip
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    const int64_t sl = base + threadIdx.x + i * MB_T;
+    kk[i] = sl < n_data ? leaf_key(leaves, sl) : ~0ull;
+  }
   const uint64_t b1 = mb->sel[0];
   int64_t need = (int64_t)mb->sel[1];
   const uint64_t pre = (b1 << 12) | (uint64_t)mb_pick(mb->hist2, need, wsum, sh);   // the 24-bit prefix
+  PER_STAMP(2, 1);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     mb->sel[2] = pre;
     mb->sel[3] = (uint64_t)need;
@@ -807,15 +850,13 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
   for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist1[i] = 0;
   for (int i = threadIdx.x; i < 4096; i += MB_T) h3[i] = 0;
   __syncthreads();
-  const double* leaves = tree + (cap - 1);
   uint64_t* ckey = mb->cand;
   uint64_t* cslot = mb->cand + cap;
-  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
   uint32_t below = 0;
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = base + threadIdx.x + i * MB_T;
-    const uint64_t k = sl < n_data ? leaf_key(leaves, sl) : ~0ull;
+    const uint64_t k = kk[i];
     below += (sl < n_data && (k >> 40) < pre) ? 1u : 0u;
     // list the keys with the prefix: one cand_n reservation per wave (a tie-heavy threshold bin can hold
     // tens of thousands of keys, and per-key atomics on one counter serialize)
@@ -839,6 +880,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ t
   if (threadIdx.x == 0) mb->blk[blockIdx.x] = tb;
   for (int i = threadIdx.x; i < 4096; i += MB_T)
     if (h3[i]) atomicAdd(&mb->hist3[i], h3[i]);
+  PER_STAMP(2, 2);
 }
 
 // The exact threshold key T among the listed candidates (radix select over bits 39..0 below the 24-bit
@@ -878,10 +920,17 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
                              int64_t& lt_off, int64_t& eq_off) {
   const uint64_t pre24 = mb->sel[2];
   int64_t need = (int64_t)mb->sel[3];
-  const uint64_t pre = (pre24 << 12) | (uint64_t)mb_pick(const_cast<uint32_t*>(mb->hist3), need, wsum, sh);
   const uint64_t* ckey = mb->cand;
   const uint64_t* cslot = mb->cand + cap;
+  // the listed candidates' first MB_T entries are loaded before the pick (their latency overlaps its round trip)
   const uint32_t m = mb->cand_n;
+  uint64_t k_first = 0, s_first = 0;
+  if (threadIdx.x < m) {
+    k_first = ckey[threadIdx.x];
+    s_first = cslot[threadIdx.x];
+  }
+  const uint64_t pre = (pre24 << 12) | (uint64_t)mb_pick(mb->hist3, need, wsum, sh);
+  PER_STAMP(3, 1);
   const uint32_t me = blockIdx.x;
   if (threadIdx.x == 0) *s_n = 0;
   __syncthreads();
@@ -891,8 +940,8 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
     const uint32_t i = i0 + threadIdx.x;
     uint64_t k = 0, blk = 0;
     if (i < m) {
-      k = ckey[i];
-      blk = cslot[i] / MB_SLOTS;
+      k = i0 == 0 ? k_first : ckey[i];
+      blk = (i0 == 0 ? s_first : cslot[i]) / MB_SLOTS;
     }
     const uint64_t kp = k >> 28;
     lt += (i < m && kp < pre && blk < me) ? 1u : 0u;
@@ -916,6 +965,9 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
   }
   mb_minmax(lo, hi, reinterpret_cast<uint64_t*>(bins));   // (its barriers publish the compacted list)
   const uint32_t n = *s_n;
+  PER_STAMP(3, 2);
+  PER_NOTE(6, m);
+  PER_NOTE(7, n);
   const bool in_lds = n <= (uint32_t)MB_CAND_LDS;
   // candidate j of the 36-bit bin: from LDS, or (overflow: tens of thousands of exactly equal keys are the only
   // way there) filtered from the global list on every pass
@@ -949,6 +1001,7 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
     __syncthreads();
     if (shift <= 0) break;
   }
+  PER_STAMP(3, 3);
   T = prefix;        // the rest-th smallest key; the first `need` slots equal to it are taken
   take_eq = need;
   uint32_t eq = 0;
@@ -971,12 +1024,13 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
   (void)mb_scan(lt, wsum, &tl);
   (void)mb_scan(eq, wsum, &te);
   lt_off = tl;
-  eq_off = te;
+  eq_off = te;  PER_STAMP(3, 4);
 }
 
+// prio (the fold path): the new chunks' priorities, computed by the fold; else (td + eps)^alpha here
 __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
-                                                     const float* td, int64_t K, double eps, int64_t* rows_inout,
-                                                     int64_t* slots_out, MbScratch* mb) {
+                                                     const float* td, const double* prio, int64_t K, double eps,
+                                                     int64_t* rows_inout, int64_t* slots_out, MbScratch* mb) {
   __shared__ double lv[MB_SLOTS];
   __shared__ double v[2][MB_SLOTS / 2];
   __shared__ uint64_t cl[MB_CAND_LDS];
@@ -992,11 +1046,13 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   const int64_t free_n = min(K, cap - n_data);
   const bool evict = K - free_n > 0;
   double* leaves = tree + (cap - 1);
+  PER_STAMP(3, 0);
   const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
   // this block's 1024 leaves: 4 contiguous per thread (keys for the victim test, LDS copy for the
-  // rebuild), loaded first so the latency overlaps the threshold selection
+  // rebuild) and their store rows, loaded first so the latency overlaps the threshold selection
   const int64_t s0 = base + threadIdx.x * MB_VPT;
   double x[MB_VPT];
+  int64_t srow[MB_VPT] = {0, 0, 0, 0};
   {
     const double2 a = ld_double2(leaves + s0);
     const double2 b = ld_double2(leaves + s0 + 2);
@@ -1004,6 +1060,14 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
     x[1] = a.y;
     x[2] = b.x;
     x[3] = b.y;
+    if (rows_inout) {
+      const longlong2 ra = *reinterpret_cast<const longlong2*>(slot_row + s0);
+      const longlong2 rb = *reinterpret_cast<const longlong2*>(slot_row + s0 + 2);
+      srow[0] = ra.x;
+      srow[1] = ra.y;
+      srow[2] = rb.x;
+      srow[3] = rb.y;
+    }
   }
   uint64_t T = 0;
   int64_t take_eq = 0, lt_off = 0, eq_off = 0;
@@ -1026,6 +1090,10 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   int64_t eq_rank = mb_scan(eq, wsum, &tot);
   lt_rank += lt_off;
   eq_rank += eq_off;
+  PER_STAMP(3, 8);
+  // the insert index j of each of the thread's slots (-1: kept), then every load of the new chunks' data at once,
+  // then the stores (one global round trip per thread, not one per slot behind the previous slot's stores)
+  int64_t jj[MB_VPT];
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = s0 + i;
@@ -1042,19 +1110,33 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
         ++eq_rank;
       }
     }
+    jj[i] = j;
+  }
+  double pv[MB_VPT];
+  int64_t rin[MB_VPT];
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    pv[i] = jj[i] < 0 ? 0.0 : (prio ? prio[jj[i]] : (double)td[jj[i]]);
+    rin[i] = (jj[i] >= 0 && rows_inout) ? rows_inout[jj[i]] : 0;
+  }
+  PER_STAMP(3, 9);
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i) {
+    const int64_t sl = s0 + i, j = jj[i];
     if (j >= 0) {
-      x[i] = pow((double)td[j] + eps, alpha);
+      x[i] = prio ? pv[i] : pow(pv[i] + eps, alpha);
       leaves[sl] = x[i];
       if (slots_out) slots_out[j] = sl;
       if (rows_inout) {
-        const int64_t old = slot_row[sl];
-        slot_row[sl] = rows_inout[j];
-        rows_inout[j] = old;
+        slot_row[sl] = rin[i];
+        rows_inout[j] = srow[i];
       }
     }
     lv[threadIdx.x * MB_VPT + i] = x[i];
   }
+  PER_STAMP(3, 10);
   __syncthreads();
+  PER_STAMP(3, 5);
   // levels L-1 .. L-10 of this block's subtree from the LDS leaves (pairwise f64 sums = rebuild_tree)
   {
     const int64_t o = ((int64_t)1 << (L - 1)) - 1 + (int64_t)blockIdx.x * (MB_SLOTS / 2);
@@ -1075,9 +1157,28 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
     cur ^= 1;
     __syncthreads();
   }
+  PER_STAMP(3, 6);
   if (!mb_last(&mb->ticket, &s_last)) return;
   // the last block: the levels above the per-block roots
   const int G = gridDim.x, lg = L - 10;                     // G = 2^lg roots at level lg (G <= 1024)
+  if (G <= 64) {   // one wave: root i in lane i, each level's pairwise sums by lane shuffles (no block barriers)
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    double y = lane < G ? __hip_atomic_load(&tree[((int64_t)1 << lg) - 1 + lane], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                        : 0.0;
+    for (int n = G / 2, l = lg - 1; n >= 1; n >>= 1, --l) {
+      const double a = __shfl(y, (2 * lane) & 63), b = __shfl(y, (2 * lane + 1) & 63);
+      y = a + b;
+      if (lane < n) tree[((int64_t)1 << l) - 1 + lane] = y;
+    }
+    if (lane == 0) {
+      mb->ticket = 0;
+      st->n_data = min(cap, n_data + K);
+    }
+    PER_STAMP(3, 7);
+    return;
+  }
   double* w = &lv[0];
   for (int i = threadIdx.x; i < G; i += MB_T)
     w[i] = __hip_atomic_load(&tree[((int64_t)1 << lg) - 1 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1103,7 +1204,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   if (threadIdx.x == 0) {
     mb->ticket = 0;
     st->n_data = min(cap, n_data + K);
-  }
+  }  PER_STAMP(3, 7);
 }
 
 // the chunk's last TD / store on its own (the single-workgroup insert paths)
@@ -1119,21 +1220,32 @@ static int per_insert_mb(mm_per* per, const float* td, int64_t k, int64_t* rows_
   MbScratch* mb = static_cast<MbScratch*>(per->mb);
   TdFuse t{};
   if (tdf) t = *tdf;
+  double* prio = nullptr;
   if (fold) {
+    FoldArgs fa = *fold;
+    fa.prio = prio = mb_prio(mb, cap);
+    fa.alpha = &per->st->alpha;
+    fa.eps = per->eps;
     const int fb = (fold->E + 15) / 16;
-    auto kern = fold_vec_ok(*fold) ? per_mb_sel1_fold<true> : per_mb_sel1_fold<false>;
-    hipLaunchKernelGGL(kern, dim3(G + fb), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, G, *fold);
+    auto kern = fold_vec_ok(fa) ? per_mb_sel1_fold<true> : per_mb_sel1_fold<false>;
+    hipLaunchKernelGGL(kern, dim3(G + fb), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, G, fa);
   } else {
     hipLaunchKernelGGL(per_mb_sel1, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, t, td_n);
   }
   hipLaunchKernelGGL(per_mb_sel2, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
   hipLaunchKernelGGL(per_mb_sel3, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
-  hipLaunchKernelGGL(per_mb_apply, dim3(G), dim3(MB_T), 0, s, per->tree, per->slot_row, cap, per->st, td, k,
+  hipLaunchKernelGGL(per_mb_apply, dim3(G), dim3(MB_T), 0, s, per->tree, per->slot_row, cap, per->st, td, prio, k,
                      per->eps, rows_inout, slots_out, mb);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }
 }  // namespace mm
+
+#if MM_PER_TRACE
+extern "C" int mm_per_trace_copy(uint64_t* out) {   // trace builds only: [4][64][8] stamps
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mm::g_per_trace), sizeof(mm::g_per_trace)) == hipSuccess ? 0 : -1;   // [4][64][16]
+}
+#endif
 
 extern "C" {
 

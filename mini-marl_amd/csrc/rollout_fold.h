@@ -25,6 +25,11 @@ struct FoldArgs {
   int64_t ring_se, n_rows;
   int E, N, slot0, n, C;
   float gamma;
+  // the PER insert's fold (per_mb_sel1_fold) only: the chunk priorities (td + eps)^alpha of the finished chunks,
+  // computed here beside the histogram instead of on the insert's critical path (per_mb_apply reads them)
+  double* prio = nullptr;        // [E]
+  const double* alpha = nullptr; // the PER's device alpha (PerDev::alpha)
+  double eps = 0.0;
 };
 
 // one 16-env group (block-local index blk) of the fold; blockDim.x >= 16 min(n, 16). Spans longer than 16 slots
@@ -91,7 +96,10 @@ __device__ __forceinline__ void td_fold_group(const FoldArgs& a, int blk) {
     }
     __syncthreads();
   }
-  if (jl == 0 && e < a.E) a.chunk_td[e] = ctd;
+  if (jl == 0 && e < a.E) {
+    a.chunk_td[e] = ctd;
+    if (a.prio) a.prio[e] = pow((double)ctd + a.eps, *a.alpha);   // = per_mb_apply's pow of chunk_td[e]
+  }
 }
 
 // VEC applies: N % 4 == 0 and every ring / store base 16-byte aligned (4-byte for the act bytes)
