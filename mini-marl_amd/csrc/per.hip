@@ -538,33 +538,36 @@ __global__ __launch_bounds__(PT) void per_update_kernel(double* tree, int64_t ca
 
 // ---------------------------------------------------------------- multi-block batched insert
 // For large power-of-two capacities the single-workgroup insert is bound by one CU's memory
-// bandwidth over the whole tree. This path spreads every pass over G = cap/1024 workgroups in FOUR
+// bandwidth over the whole tree. This path spreads every pass over G = cap/1024 workgroups in THREE
 // stream-ordered launches (graph-capturable, same results as per_add_fast_kernel). A pass's decision is
 // re-derived by EVERY workgroup of the next launch from the finished global counts (the launch boundary
 // orders it after the previous pass's atomics), so only the last pass needs an arrival ticket:
-//   A sel1    [the chunk's last rollout TD / store, folded in: td_chunk_kernel's arithmetic]
-//             12-bit histogram (sign + exponent) of the candidate keys
-//   B sel2    each block picks the threshold's bin b1; histogram of bits 51..40 of the keys in b1
-//   C sel3    each block picks b2; keys with the 24-bit prefix (b1, b2) listed with their slots,
-//             histogram of their bits 39..28, per-block counts of the keys below the prefix
-//   D apply   each block radix-selects the exact key T among the listed keys (8-bit digits over the bits
-//             below the candidates' common prefix; ties — equal priorities are common: envs that stayed
+//   A sel1    [the chunk's last rollout TD / store and the new chunks' priorities, folded in]
+//             first-level histogram of the keys: 7 binades around the previous insert's threshold x 512
+//             mantissa steps (mb_bin1), two edge bins for the keys outside the window (the priorities
+//             (td + eps)^alpha span a few binades and drift slowly: a fixed 12-bit sign + exponent histogram
+//             resolves ~2 bits of them)
+//   B sel2    each block picks the threshold's bin b1; the keys in b1 listed with their slots, histogram of
+//             their next 12 bits (31..42), per-block counts of the keys below b1
+//   C apply   each block picks b2 (an interior b1: the candidates share a 33-bit prefix; an edge b1: all
+//             listed keys are candidates), radix-selects the exact key T among the candidates (8-bit digits
+//             over the bits below their common prefix; ties — equal priorities are common: envs that stayed
 //             greedy since an episode start repeat each other's chunks — cost no passes) and its own victim
-//             offsets, writes its victims / free slots ((td + eps)^alpha, row
-//             swaps) and rebuilds its 1024-leaf subtree from LDS; the last block (ticket) builds the top
-//             levels and updates n_data
+//             offsets, writes its victims / free slots (the fold's priorities, row swaps) and rebuilds its
+//             1024-leaf subtree from LDS; the last block (ticket) builds the top levels and updates n_data
 constexpr int MB_T = 256, MB_VPT = 4, MB_SLOTS = MB_T * MB_VPT;   // 1024 slots per block
 constexpr int64_t MB_MIN_CAP = 16384;
-constexpr int MB_CAND_LDS = 12288;   // keys with the 36-bit prefix compacted into the apply block's LDS
+constexpr int MB_CAND_LDS = 12288;   // candidate keys compacted into the apply block's LDS
 constexpr int MB_MAX_BLOCKS = 1024;
 struct MbScratch {
-  uint32_t hist1[4096];
-  uint32_t hist2[4096];
-  uint32_t hist3[4096];              // bits 39..28 of the keys with the 24-bit prefix (sel3), read by apply
-  uint32_t blk[2 * MB_MAX_BLOCKS];   // C: per block #keys below the 24-bit prefix; then victim offsets
+  uint32_t hist1[4096];               // first level (mb_bin1), built by sel1, read by sel2
+  uint32_t hist2[4096];               // bits 44..33 of the keys in bin b1 (sel2), read by apply
+  uint32_t blk[2 * MB_MAX_BLOCKS];   // per block #keys below bin b1 (sel2)
   uint32_t cand_n;
   uint32_t ticket;
-  uint64_t sel[4];                    // b1 | (b1, b2) prefix, remaining rank, T, take_eq
+  int32_t ewin;                       // the first level's lowest biased exponent (apply's last block: T's - 3)
+  int32_t pad_;
+  uint64_t sel[4];                    // b1, the remaining rank inside it (sel2 block 0, for the record)
   uint64_t cand[1];                   // [2 cap] the listed (key, slot) pairs: keys at cand, slots at cand + cap;
                                       // then [cap] f64: the new chunks' priorities from the fold (mm_per_insert_fold)
 };
@@ -588,6 +591,17 @@ __device__ uint64_t g_per_trace[4][64][16];
 
 __device__ __forceinline__ uint64_t leaf_key(const double* leaves, int64_t s) {
   return (uint64_t)__double_as_longlong(leaves[s]);
+}
+// first-level bin of a key (monotone in the key) in the window of 7 binades from biased exponent e0: 0 below it (and
+// +0), 4095 above it, else 1 + (binade - e0) * 512 + the top 9 mantissa bits — an interior bin is the class of keys
+// sharing their top 21 bits (sign 0, exponent, 9 mantissa bits). The window follows the threshold from insert to
+// insert (MbScratch::ewin); one that misses it only costs speed (an edge bin lists all its keys).
+constexpr int MB_WIN = 7, MB_EWIN0 = 1023 - 3;
+__device__ __forceinline__ uint32_t mb_bin1(uint64_t k, int e0) {
+  const int e = (int)(k >> 52);
+  if (e < e0) return 0u;
+  if (e >= e0 + MB_WIN) return 4095u;
+  return 1u + (((uint32_t)(e - e0) << 9) | (uint32_t)((k >> 43) & 511u));
 }
 
 // block-wide exclusive scan of one u32 per thread (MB_T threads) + total
@@ -726,9 +740,10 @@ __device__ __forceinline__ void mb_sel1_hist(const double* __restrict__ tree, in
   __shared__ uint32_t h[4096];
   // the candidate list of the previous insert was last read by its apply launch, which has finished
   if (b == 0 && threadIdx.x == 0) mb->cand_n = 0;
-  for (int i = b * MB_T + threadIdx.x; i < 4096; i += nb * MB_T) mb->hist3[i] = 0;
+  for (int i = b * MB_T + threadIdx.x; i < 4096; i += nb * MB_T) mb->hist2[i] = 0;   // (last read by apply)
   const int64_t n_data = st->n_data;
   if (K - min(K, cap - n_data) <= 0) return;
+  const int e0 = mb->ewin;
   const double* leaves = tree + (cap - 1);
   for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
   __syncthreads();
@@ -736,7 +751,7 @@ __device__ __forceinline__ void mb_sel1_hist(const double* __restrict__ tree, in
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = base + threadIdx.x + i * MB_T;
-    if (sl < n_data) atomicAdd(&h[leaf_key(leaves, sl) >> 52], 1u);
+    if (sl < n_data) atomicAdd(&h[mb_bin1(leaf_key(leaves, sl), e0)], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 4096; i += MB_T)
@@ -767,10 +782,23 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel1_fold(const double* __restric
   }
 }
 
-// Every workgroup of sel2 / sel3 / apply re-derives the previous pass's decision itself from the finished
-// global histogram / candidate list (the launch boundary orders it after every atomic of the previous
-// pass), so no pass needs an arrival ticket and its device-scope fences; block 0 records the decision for
-// the launch after next (sel[0..1] by sel2, sel[2..3] by sel3: never a slot the same launch reads).
+// Every workgroup of sel2 / apply re-derives the previous pass's decision itself from the finished global
+// histogram (the launch boundary orders it after every atomic of the previous pass), so no pass needs an arrival
+// ticket and its device-scope fences.
+// bins[bin] += 1 for this lane when on: one LDS atomic per wave when every active lane has the same bin (the
+// common case inside a tie-heavy candidate list), per-lane atomics otherwise
+__device__ __forceinline__ void mb_bin_add(uint32_t* bins, bool on, uint32_t bin) {
+  const uint64_t act = __ballot(on);
+  if (!act) return;
+  const int first = __builtin_ctzll(act);
+  const uint32_t b0 = __shfl(bin, first);
+  if (__ballot(on && bin == b0) == act) {
+    if ((threadIdx.x & 63) == first) atomicAdd(&bins[b0], (uint32_t)__popcll(act));
+  } else if (on) {
+    atomicAdd(&bins[bin], 1u);
+  }
+}
+
 __global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ tree, int64_t cap, const PerDev* st,
                                                     int64_t K, MbScratch* mb) {
   __shared__ uint32_t h[4096];
@@ -789,7 +817,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ t
     const int64_t sl = base + threadIdx.x + i * MB_T;
     kk[i] = sl < n_data ? leaf_key(leaves, sl) : ~0ull;
   }
-  const uint64_t b1 = (uint64_t)mb_pick(mb->hist1, need, wsum, sh);
+  const uint32_t b1 = (uint32_t)mb_pick(mb->hist1, need, wsum, sh);
   PER_STAMP(1, 1);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     mb->sel[0] = b1;
@@ -797,95 +825,42 @@ __global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ t
   }
   for (int i = threadIdx.x; i < 4096; i += MB_T) h[i] = 0;
   __syncthreads();
+  uint64_t* ckey = mb->cand;
+  uint64_t* cslot = mb->cand + cap;
+  uint32_t below = 0, nc = 0;
+  bool isc[MB_VPT];
+  const int e0 = mb->ewin;
 #pragma unroll
   for (int i = 0; i < MB_VPT; ++i) {
     const int64_t sl = base + threadIdx.x + i * MB_T;
-    if (sl < n_data && (kk[i] >> 52) == b1) atomicAdd(&h[(kk[i] >> 40) & 4095], 1u);
+    const uint32_t bb = mb_bin1(kk[i], e0);
+    below += (sl < n_data && bb < b1) ? 1u : 0u;
+    isc[i] = sl < n_data && bb == b1;
+    nc += isc[i] ? 1u : 0u;
+    mb_bin_add(h, isc[i], (uint32_t)(kk[i] >> 31) & 4095u);   // wave-aggregated: a tie bin is one atomic per wave
+  }
+  // the keys in b1 listed with ONE cand_n reservation per block (per-wave atomics on one counter serialize): a block
+  // scan of (below, listed) packed in 16-bit halves (each <= 1024)
+  uint32_t tb;
+  const uint32_t ex = mb_scan((below << 16) | nc, wsum, &tb);   // (its barriers also order the h atomics)
+  if (threadIdx.x == 0) {
+    mb->blk[blockIdx.x] = tb >> 16;
+    sh[0] = (tb & 0xFFFFu) ? (int64_t)atomicAdd(&mb->cand_n, tb & 0xFFFFu) : 0;
   }
   __syncthreads();
+  uint32_t at = (uint32_t)sh[0] + (ex & 0xFFFFu);
+#pragma unroll
+  for (int i = 0; i < MB_VPT; ++i)
+    if (isc[i]) {
+      ckey[at] = kk[i];
+      cslot[at] = (uint64_t)(base + threadIdx.x + i * MB_T);
+      ++at;
+    }
   for (int i = threadIdx.x; i < 4096; i += MB_T)
     if (h[i]) atomicAdd(&mb->hist2[i], h[i]);
   PER_STAMP(1, 2);
 }
 
-// bins[bin] += 1 for this lane when on: one LDS atomic per wave when every active lane has the same bin (the
-// common case inside a tie-heavy candidate list), per-lane atomics otherwise
-__device__ __forceinline__ void mb_bin_add(uint32_t* bins, bool on, uint32_t bin) {
-  const uint64_t act = __ballot(on);
-  if (!act) return;
-  const int first = __builtin_ctzll(act);
-  const uint32_t b0 = __shfl(bin, first);
-  if (__ballot(on && bin == b0) == act) {
-    if ((threadIdx.x & 63) == first) atomicAdd(&bins[b0], (uint32_t)__popcll(act));
-  } else if (on) {
-    atomicAdd(&bins[bin], 1u);
-  }
-}
-
-__global__ __launch_bounds__(MB_T) void per_mb_sel3(const double* __restrict__ tree, int64_t cap, const PerDev* st,
-                                                    int64_t K, MbScratch* mb) {
-  __shared__ uint32_t wsum[MB_T / 64];
-  __shared__ int64_t sh[2];
-  __shared__ uint32_t h3[4096];
-  const int64_t n_data = st->n_data;
-  if (K - min(K, cap - n_data) <= 0) return;
-  PER_STAMP(2, 0);
-  const double* leaves = tree + (cap - 1);
-  const int64_t base = (int64_t)blockIdx.x * MB_SLOTS;
-  uint64_t kk[MB_VPT];   // this block's keys first: their loads overlap the pick's round trip
-#pragma unroll
-  for (int i = 0; i < MB_VPT; ++i) {
-    const int64_t sl = base + threadIdx.x + i * MB_T;
-    kk[i] = sl < n_data ? leaf_key(leaves, sl) : ~0ull;
-  }
-  const uint64_t b1 = mb->sel[0];
-  int64_t need = (int64_t)mb->sel[1];
-  const uint64_t pre = (b1 << 12) | (uint64_t)mb_pick(mb->hist2, need, wsum, sh);   // the 24-bit prefix
-  PER_STAMP(2, 1);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    mb->sel[2] = pre;
-    mb->sel[3] = (uint64_t)need;
-  }
-  // hist1 was last read by sel2 (finished): cleared here for the next insert
-  for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist1[i] = 0;
-  for (int i = threadIdx.x; i < 4096; i += MB_T) h3[i] = 0;
-  __syncthreads();
-  uint64_t* ckey = mb->cand;
-  uint64_t* cslot = mb->cand + cap;
-  uint32_t below = 0;
-#pragma unroll
-  for (int i = 0; i < MB_VPT; ++i) {
-    const int64_t sl = base + threadIdx.x + i * MB_T;
-    const uint64_t k = kk[i];
-    below += (sl < n_data && (k >> 40) < pre) ? 1u : 0u;
-    // list the keys with the prefix: one cand_n reservation per wave (a tie-heavy threshold bin can hold
-    // tens of thousands of keys, and per-key atomics on one counter serialize)
-    const bool is_c = sl < n_data && (k >> 40) == pre;
-    mb_bin_add(h3, is_c, (uint32_t)(k >> 28) & 4095u);   // wave-aggregated: a tie bin is one atomic per wave
-    const uint64_t m = __ballot(is_c);
-    if (m) {
-      const int lane = threadIdx.x & 63;
-      uint32_t at0 = 0;
-      if (lane == __builtin_ctzll(m)) at0 = atomicAdd(&mb->cand_n, (uint32_t)__popcll(m));
-      at0 = __shfl(at0, __builtin_ctzll(m));
-      if (is_c) {
-        const uint32_t at = at0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        ckey[at] = k;
-        cslot[at] = (uint64_t)sl;
-      }
-    }
-  }
-  uint32_t tb;
-  (void)mb_scan(below, wsum, &tb);   // (its barriers also order the h3 atomics before the flush)
-  if (threadIdx.x == 0) mb->blk[blockIdx.x] = tb;
-  for (int i = threadIdx.x; i < 4096; i += MB_T)
-    if (h3[i]) atomicAdd(&mb->hist3[i], h3[i]);
-  PER_STAMP(2, 2);
-}
-
-// The exact threshold key T among the listed candidates (radix select over bits 39..0 below the 24-bit
-// prefix) and this workgroup's victim offsets: lt_off = keys < T in the workgroups before it (their keys
-// below the prefix + their listed keys < T), eq_off = listed keys == T in them. Run by every workgroup.
 // Block-wide min / max of a u64 (MB_T threads); every thread gets both.
 __device__ __forceinline__ void mb_minmax(uint64_t& lo, uint64_t& hi, uint64_t* red) {
 #pragma unroll
@@ -910,56 +885,73 @@ __device__ __forceinline__ void mb_minmax(uint64_t& lo, uint64_t& hi, uint64_t* 
 
 
 // The exact threshold key T (radix select) and this workgroup's victim offsets: lt_off = keys < T in the
-// workgroups before it, eq_off = keys == T in them. Run by every workgroup. The third histogram (sel3) narrows
-// the 24-bit prefix to 36 bits first, so ONE pass over the listed keys (coalesced, no atomics) counts the
-// earlier workgroups' keys below the 36-bit prefix and compacts those with it into LDS (key, workgroup); the
-// radix digits then run over that short list, from its highest differing bit (a list of equal keys — ties are
-// common: envs that stay greedy from an episode start repeat each other's chunks — needs no pass at all).
+// workgroups before it, eq_off = keys == T in them. Run by every workgroup. The second histogram (sel2) narrows an
+// interior first-level bin (19-bit prefix) to a 31-bit prefix, so ONE pass over the listed keys (coalesced loads
+// issued ahead, no global atomics) counts the earlier workgroups' keys below the prefix and compacts those with it
+// into LDS (key, workgroup); the radix digits then run over that short list, from its highest differing bit (a list
+// of equal keys — ties are common: envs that stay greedy from an episode start repeat each other's chunks — needs no
+// pass at all). An edge bin (keys outside the first level's binades) takes every listed key as a candidate.
 __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uint16_t* cb, uint32_t* bins,
                              uint32_t* wsum, int64_t* sh, uint32_t* s_n, uint64_t& T, int64_t& take_eq,
                              int64_t& lt_off, int64_t& eq_off) {
-  const uint64_t pre24 = mb->sel[2];
-  int64_t need = (int64_t)mb->sel[3];
+  const uint32_t b1 = (uint32_t)mb->sel[0];
+  int64_t need = (int64_t)mb->sel[1];
+  const bool edge = b1 == 0u || b1 == 4095u;
   const uint64_t* ckey = mb->cand;
   const uint64_t* cslot = mb->cand + cap;
-  // the listed candidates' first MB_T entries are loaded before the pick (their latency overlaps its round trip)
+  // the listed keys' first PF * MB_T entries are loaded before the pick (their latency overlaps its round trip)
+  constexpr int PF = 4;
   const uint32_t m = mb->cand_n;
-  uint64_t k_first = 0, s_first = 0;
-  if (threadIdx.x < m) {
-    k_first = ckey[threadIdx.x];
-    s_first = cslot[threadIdx.x];
+  uint64_t kf[PF], sf[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) {
+    const uint32_t i = q * MB_T + threadIdx.x;
+    kf[q] = i < m ? ckey[i] : 0;
+    sf[q] = i < m ? cslot[i] : 0;
   }
-  const uint64_t pre = (pre24 << 12) | (uint64_t)mb_pick(mb->hist3, need, wsum, sh);
+  uint64_t pre = 0;   // interior b1: the candidates' 33-bit prefix (sign, exponent, 21 mantissa bits)
+  if (!edge) {
+    const uint64_t p21 = ((uint64_t)(((b1 - 1u) >> 9) + (uint32_t)mb->ewin) << 9) | ((b1 - 1u) & 511u);
+    pre = (p21 << 12) | (uint64_t)mb_pick(mb->hist2, need, wsum, sh);
+  }
   PER_STAMP(3, 1);
+  auto is_cand = [&](uint64_t k) { return edge || (k >> 31) == pre; };
   const uint32_t me = blockIdx.x;
   if (threadIdx.x == 0) *s_n = 0;
   __syncthreads();
   uint32_t lt = 0;
   uint64_t lo = ~0ull, hi = 0;
-  for (uint32_t i0 = 0; i0 < m; i0 += MB_T) {
-    const uint32_t i = i0 + threadIdx.x;
-    uint64_t k = 0, blk = 0;
-    if (i < m) {
-      k = i0 == 0 ? k_first : ckey[i];
-      blk = (i0 == 0 ? s_first : cslot[i]) / MB_SLOTS;
+  for (uint32_t i00 = 0; i00 < m; i00 += PF * MB_T) {
+    uint64_t kq[PF], sq[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {   // this round's keys (loaded last round), the next round's loads issued
+      const uint32_t i = i00 + (PF + q) * MB_T + threadIdx.x;
+      kq[q] = kf[q];
+      sq[q] = sf[q];
+      kf[q] = i < m ? ckey[i] : 0;
+      sf[q] = i < m ? cslot[i] : 0;
     }
-    const uint64_t kp = k >> 28;
-    lt += (i < m && kp < pre && blk < me) ? 1u : 0u;
-    const bool in = i < m && kp == pre;
-    if (in) {
-      lo = k < lo ? k : lo;
-      hi = k > hi ? k : hi;
-    }
-    const uint64_t w = __ballot(in);
-    if (w) {
-      const int lane = threadIdx.x & 63, first = __builtin_ctzll(w);
-      uint32_t at0 = 0;
-      if (lane == first) at0 = atomicAdd(s_n, (uint32_t)__popcll(w));
-      at0 = __shfl(at0, first);
-      const uint32_t at = at0 + (uint32_t)__popcll(w & ((1ull << lane) - 1ull));
-      if (in && at < (uint32_t)MB_CAND_LDS) {
-        cl[at] = k;
-        cb[at] = (uint16_t)blk;
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const uint32_t i = i00 + q * MB_T + threadIdx.x;
+      const uint64_t k = kq[q], blk = sq[q] / MB_SLOTS;
+      lt += (i < m && !edge && (k >> 31) < pre && blk < me) ? 1u : 0u;
+      const bool in = i < m && is_cand(k);
+      if (in) {
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+      }
+      const uint64_t w = __ballot(in);
+      if (w) {
+        const int lane = threadIdx.x & 63, first = __builtin_ctzll(w);
+        uint32_t at0 = 0;
+        if (lane == first) at0 = atomicAdd(s_n, (uint32_t)__popcll(w));
+        at0 = __shfl(at0, first);
+        const uint32_t at = at0 + (uint32_t)__popcll(w & ((1ull << lane) - 1ull));
+        if (in && at < (uint32_t)MB_CAND_LDS) {
+          cl[at] = k;
+          cb[at] = (uint16_t)blk;
+        }
       }
     }
   }
@@ -969,10 +961,30 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
   PER_NOTE(6, m);
   PER_NOTE(7, n);
   const bool in_lds = n <= (uint32_t)MB_CAND_LDS;
-  // candidate j of the 36-bit bin: from LDS, or (overflow: tens of thousands of exactly equal keys are the only
-  // way there) filtered from the global list on every pass
+  // candidate j: from LDS, or (overflow: tens of thousands of exactly equal keys, or an edge bin's list) filtered
+  // from the global list on every pass
   uint64_t prefix = lo & (lo == hi ? ~0ull : (~0ull << (64 - __clzll(lo ^ hi))));
-  const int top = (n == 0 || lo == hi) ? -1 : 63 - __clzll(lo ^ hi);
+  int top = (n == 0 || lo == hi) ? -1 : 63 - __clzll(lo ^ hi);
+  if (top >= 0 && in_lds && n <= (uint32_t)MB_T) {
+    // a short list of distinct keys: candidate i's rank among the n by direct comparison (no radix passes)
+    if (threadIdx.x < n) {
+      const uint64_t k = cl[threadIdx.x];
+      uint32_t less = 0, eq = 0;
+      for (uint32_t j = 0; j < n; ++j) {
+        less += cl[j] < k ? 1u : 0u;
+        eq += cl[j] == k ? 1u : 0u;
+      }
+      if ((int64_t)less < need && need <= (int64_t)(less + eq)) {   // (equal keys write the same values)
+        sh[0] = (int64_t)k;
+        sh[1] = need - less;
+      }
+    }
+    __syncthreads();
+    prefix = (uint64_t)sh[0];
+    need = sh[1];
+    top = -1;
+    __syncthreads();
+  }
   for (int shift = top - 7; top >= 0; shift -= 8) {
     const int sft = shift < 0 ? 0 : shift;
     const int width = shift < 0 ? shift + 8 : 8;
@@ -984,7 +996,7 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
     for (uint32_t i0 = 0; i0 < cnt; i0 += MB_T) {
       const uint32_t i = i0 + threadIdx.x;
       const uint64_t k = i < cnt ? (in_lds ? cl[i] : ckey[i]) : 0;
-      const bool on = i < cnt && (k >> 28) == pre && (k & hmask) == prefix;
+      const bool on = i < cnt && is_cand(k) && (k & hmask) == prefix;
       mb_bin_add(bins, on, (uint32_t)(k >> sft) & dmask);
     }
     __syncthreads();
@@ -1015,7 +1027,7 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
   } else {
     for (uint32_t i = threadIdx.x; i < m; i += MB_T) {
       const uint64_t k = ckey[i];
-      if ((k >> 28) != pre || (uint32_t)(cslot[i] / MB_SLOTS) >= me) continue;
+      if (!is_cand(k) || (uint32_t)(cslot[i] / MB_SLOTS) >= me) continue;
       lt += k < T ? 1u : 0u;
       eq += k == T ? 1u : 0u;
     }
@@ -1024,7 +1036,8 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
   (void)mb_scan(lt, wsum, &tl);
   (void)mb_scan(eq, wsum, &te);
   lt_off = tl;
-  eq_off = te;  PER_STAMP(3, 4);
+  eq_off = te;
+  PER_STAMP(3, 4);
 }
 
 // prio (the fold path): the new chunks' priorities, computed by the fold; else (td + eps)^alpha here
@@ -1073,8 +1086,8 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   int64_t take_eq = 0, lt_off = 0, eq_off = 0;
   if (evict) {
     mb_threshold(mb, cap, cl, cb, bins, wsum, sh, &s_n, T, take_eq, lt_off, eq_off);
-    // hist2 was last read by sel3 (finished): cleared here for the next insert
-    for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist2[i] = 0;
+    // hist1 was last read by sel2 (finished): cleared here for the next insert
+    for (int i = blockIdx.x * MB_T + threadIdx.x; i < 4096; i += gridDim.x * MB_T) mb->hist1[i] = 0;
   }
   uint32_t lt = 0, eq = 0;
   if (evict) {
@@ -1175,6 +1188,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
     if (lane == 0) {
       mb->ticket = 0;
       st->n_data = min(cap, n_data + K);
+      if (evict) mb->ewin = min(max((int)(T >> 52) - 3, 0), 2047 - MB_WIN);   // the next insert's window
     }
     PER_STAMP(3, 7);
     return;
@@ -1204,6 +1218,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   if (threadIdx.x == 0) {
     mb->ticket = 0;
     st->n_data = min(cap, n_data + K);
+    if (evict) mb->ewin = min(max((int)(T >> 52) - 3, 0), 2047 - MB_WIN);   // the next insert's window
   }  PER_STAMP(3, 7);
 }
 
@@ -1233,7 +1248,6 @@ static int per_insert_mb(mm_per* per, const float* td, int64_t k, int64_t* rows_
     hipLaunchKernelGGL(per_mb_sel1, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, t, td_n);
   }
   hipLaunchKernelGGL(per_mb_sel2, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
-  hipLaunchKernelGGL(per_mb_sel3, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
   hipLaunchKernelGGL(per_mb_apply, dim3(G), dim3(MB_T), 0, s, per->tree, per->slot_row, cap, per->st, td, prio, k,
                      per->eps, rows_inout, slots_out, mb);
   MM_HIP_CHECK(hipGetLastError());
@@ -1291,7 +1305,9 @@ int mm_per_create(int64_t capacity, int32_t flavor, double alpha, double beta, d
   }
   p->mb = nullptr;
   if ((capacity & (capacity - 1)) == 0 && capacity >= mm::MB_MIN_CAP && capacity <= (1ll << 20)) {
-    if (hipMalloc(&p->mb, mm::mb_bytes(capacity)) != hipSuccess || hipMemset(p->mb, 0, mm::mb_bytes(capacity)) != hipSuccess) {
+    const int32_t ewin0 = mm::MB_EWIN0;   // the first-level window of the first insert: 2^-3 .. 2^4
+    if (hipMalloc(&p->mb, mm::mb_bytes(capacity)) != hipSuccess || hipMemset(p->mb, 0, mm::mb_bytes(capacity)) != hipSuccess ||
+        hipMemcpy(&static_cast<mm::MbScratch*>(p->mb)->ewin, &ewin0, 4, hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipFree(base);
       delete p;
       mm::set_error("per_create: scratch allocation failed");

@@ -22,6 +22,7 @@ Data parallel (SURVEY 8e): one trainer per rank on its own env shard and replay;
 gradient is all-reduced (``grad_allreduce``) between the captured backward and the clip/Adam graph,
 so the replicas stay identical (rank 0's initial parameters are broadcast by the caller).
 """
+import os
 import time
 
 import torch
@@ -34,6 +35,12 @@ from .learner import Mixer, QLearner
 from .qnet import ptr, stream_handle
 
 
+def _ranks_share_device(world):
+    """True when this node runs more ranks than it has GPUs (LOCAL_WORLD_SIZE from the launcher, else WORLD_SIZE)."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    return local > max(1, torch.cuda.device_count())
+
+
 class QTrainer:
     def __init__(self, cfg: QTrainConfig, device="cuda", rank=0, grad_allreduce=None, world=1, track_score=True):
         self.cfg = c = cfg
@@ -42,6 +49,11 @@ class QTrainer:
         assert c.algo in ("vdn", "vdn_double", "qmix", "qmix_min")
         if c.buffer_limit < c.n_envs:
             raise ValueError(f"buffer_limit ({c.buffer_limit} chunks) must hold one chunk per env ({c.n_envs})")
+        persistent = c.persistent
+        if persistent is None and world > 1 and _ranks_share_device(world):
+            # several ranks on one GPU: their kernels run beside each other, and the chunk-persistent launch needs
+            # every CU for its own blocks (its hand-off waits would expire: include/minimarl.h, co-residency)
+            persistent = False
         per_kwargs = dict(alpha=c.alpha, beta=c.beta, eps=c.eps, step_weight=c.step_weight,
                           use_step_weight=c.use_step_weight and c.per_flavor == "vdn",
                           update_alpha_beta=c.update_alpha_beta, max_episodes=c.max_episodes,
@@ -50,7 +62,7 @@ class QTrainer:
                                  chunk=c.chunk_size, capacity=c.buffer_limit, gamma=c.gamma, max_steps=c.max_step,
                                  step_cost=c.step_cost, full_observable=c.full_observable,
                                  per_flavor=c.per_flavor, per_kwargs=per_kwargs, seed=c.seed + 7919 * rank,
-                                 env=c.env, persistent=c.persistent, device=self.device)
+                                 env=c.env, persistent=persistent, device=self.device)
         eng = self.eng
         # the behavior net's init does not depend on the rank (same seed): replicas start identical
         eng.behavior.init_default(c.seed)

@@ -220,6 +220,34 @@ def test_per_batched_vs_oracle(flavor, cap, kb, rounds):
         np.testing.assert_allclose(dev.tree().cpu().numpy(), ora.tree, rtol=1e-6, atol=1e-9)
 
 
+def test_per_batched_edge_bins_vs_oracle():
+    """Multi-block insert with priorities outside the first selection level's binades (2^-16 .. 2^15): tiny (eps
+    1e-12, td = 0: (1e-12)^0.8 ~ 2^-32) and huge (td up to 1e9) keys, so the threshold falls in either edge bin of the
+    first level in some rounds (every listed key a candidate), and in an interior bin in others."""
+    from minimarl.replay import DevicePER
+    cap, kb = 65536, 8192
+    kw = dict(alpha=0.8, beta=0.2, eps=1e-12, use_step_weight=False, update_alpha_beta=True, max_episodes=100000,
+              update_iter=10)
+    dev = DevicePER(cap, "qmix", device=DEV, **kw)
+    ora = SumTreeOracle(cap, "qmix", 0.8, 0.2, eps=1e-12, alpha_inc=0.2 / 1e6, beta_inc=0.8 / 1e6)
+    rng = np.random.default_rng(5)
+    for rnd in range(14):
+        if rnd % 3 == 0:
+            td = np.zeros(kb, np.float32)                                    # all in the low edge bin
+            td[: kb // 4] = (rng.random(kb // 4) * 1e-9).astype(np.float32)
+        elif rnd % 3 == 1:
+            td = (10.0 ** (rng.random(kb) * 9)).astype(np.float32)          # up to 1e9: the high edge bin
+        else:
+            td = (10.0 ** (rng.random(kb) * 20 - 12)).astype(np.float32)    # every bin kind at once
+        slots = dev.add(torch.tensor(td))
+        oslots = ora.add_batch([float(x) for x in td])
+        np.testing.assert_array_equal(slots.cpu().numpy(), oslots)
+        tree = dev.tree().cpu().numpy()
+        # leaves exact; the root within f64 summation-order noise (the oracle propagates deltas: huge - huge + tiny)
+        np.testing.assert_allclose(tree[cap - 1:], ora.tree[cap - 1:], rtol=1e-12, atol=0)
+        np.testing.assert_allclose(tree[0], ora.tree[cap - 1:].sum(), rtol=1e-9)
+
+
 @pytest.mark.parametrize("cap,B", [(65536, 32), (65536, 64), (1024, 1), (1024, 64), (4, 8)])
 def test_per_small_batch_update_vs_oracle(cap, B):
     """Small-batch priority update (LDS path re-sum, B <= 64 on power-of-two trees) vs the oracle's full

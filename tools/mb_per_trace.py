@@ -38,7 +38,6 @@ def main():
         t0 = b[0, :, 0].min()
         sel1_end = b[0, :, 1].max()
         s2 = b[1, :, :3]
-        s3 = b[2, :, :3]
         ap = b[3]
         last = int(np.argmax(ap[:, 7]))
         line = {
@@ -47,10 +46,7 @@ def main():
             "gap12": (s2[:, 0].min() - sel1_end) * tick,
             "sel2_pick": np.median(s2[:, 1] - s2[:, 0]) * tick, "sel2_rest": np.median(s2[:, 2] - s2[:, 1]) * tick,
             "sel2_us": (s2[:, 2].max() - s2[:, 0].min()) * tick,
-            "gap23": (s3[:, 0].min() - s2[:, 2].max()) * tick,
-            "sel3_pick": np.median(s3[:, 1] - s3[:, 0]) * tick, "sel3_rest": np.median(s3[:, 2] - s3[:, 1]) * tick,
-            "sel3_us": (s3[:, 2].max() - s3[:, 0].min()) * tick,
-            "gap3a": (ap[:, 0].min() - s3[:, 2].max()) * tick,
+            "gap2a": (ap[:, 0].min() - s2[:, 2].max()) * tick,
         }
         names = ["pick", "scan", "radix", "offs", "write", "subtree"]
         for i, nm in enumerate(names):
