@@ -546,7 +546,7 @@ def main():
                  # gradients = 3 x 2 x MACs per row-step of both nets; the fused pass also recomputes the forward)
                  "grad_gflop_per_epoch": round(mflop / 1e9, 1),
                  "grad_tflops_fp32": round(mflop / (t_tr / k / 15 * 1e-3) / 1e12, 2),
-                 "grad_path": "fused mm_mappo_grad (v_mfma_f32_32x32x2_f32, forward recomputed from chunk-start hiddens)",
+                 "grad_path": "mm_mappo_grad: recurrent + MLP passes on fp16x3-split v_mfma_f32_32x32x16_f16 with power-of-two operand scaling (fp32-level products, f32 accumulate), forward recomputed from chunk-start hiddens",
                  "ppo_updates_per_s": round(15 * k / el_m, 2),
                  "train_info": {kk: round(float(v), 6) for kk, v in info.items()},
                  "grad_allreduce": (("gloo" if shared else "rccl") if dist else None)}

@@ -1,6 +1,6 @@
 """Summarise an SQ / GRBM counter run (tools/pmc_chunk.sh and friends): per-dispatch means of every counter over
 the dispatches of one kernel, plus derived fractions. Usage:
-    python tools/pmc_fwd_sum.py <dir> [<kernel-name substring> <label> [<grid size>]]
+    python tools/pmc_fwd_sum.py <dir> [<kernel-name substring> <label> [<grid size>]]   (grid size 0: any grid)
 
 Clock normalisation (verdict r05 item 5): a counter run is several `rocprofv3 --pmc` passes, each with its own kernel
 trace; counters and the kernel duration are matched PER DISPATCH WITHIN ONE PASS (same Dispatch_Id in that pass's
@@ -30,12 +30,12 @@ for pdir in sorted(glob.glob(os.path.join(d, "p*"))):
     dur = {}
     for path in glob.glob(os.path.join(pdir, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
-            if KN in r["Kernel_Name"] and int(r["Grid_Size_X"]) == GRID:
+            if KN in r["Kernel_Name"] and (GRID == 0 or int(r["Grid_Size_X"]) == GRID):
                 dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     per = {}                                # (counter, dispatch) -> sum over the counter's instances
     for path in glob.glob(os.path.join(pdir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
-            if KN not in r["Kernel_Name"] or int(r["Grid_Size"]) != GRID:
+            if KN not in r["Kernel_Name"] or (GRID != 0 and int(r["Grid_Size"]) != GRID):
                 continue
             key = (r["Counter_Name"], r["Dispatch_Id"])
             per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
