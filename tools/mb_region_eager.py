@@ -40,6 +40,31 @@ def main():
         torch.cuda.synchronize()
         tg.append(time.perf_counter() - t0)
     eng.check_errors()
+    # the chunk launch alone (20 steps from a ring cycle start, no fold / insert), event-timed like bench.py's roofline
+    ev0, ev1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    tc = []
+    for _ in range(8):
+        ev0.record()
+        eng.chunk_only(20)
+        ev1.record()
+        torch.cuda.synchronize()
+        tc.append(ev0.elapsed_time(ev1))
+    # an empty graph region: launch + synchronize cost alone
+    g = torch.cuda.CUDAGraph()
+    s_ = torch.cuda.Stream()
+    x = torch.zeros(1, device=dev)
+    with torch.cuda.stream(s_):
+        g.capture_begin()
+        x.add_(1)
+        g.capture_end()
+    te = []
+    for _ in range(8):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize()
+        te.append(time.perf_counter() - t0)
+    print({"chunk_only20_ms_min": round(min(tc), 4), "tiny_graph_ms_min": round(min(te) * 1e3, 4)})
     print({"eager_region_ms_min": round(min(ts) * 1e3, 4), "graph_region_ms_min": round(min(tg) * 1e3, 4),
            "eager_ms": [round(x * 1e3, 3) for x in ts], "graph_ms": [round(x * 1e3, 3) for x in tg], "steps": 20})
 
