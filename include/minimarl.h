@@ -305,7 +305,9 @@ int mm_rollout_chunk(mm_env* env, const mm_qnet_dims* d, const float* packed_t, 
 /* Co-residency contract of mm_rollout_chunk: NOTHING else may run on the device while it runs (no kernel on another
  * stream, no collective, no other process's work), because its blocks wait for each other's hand-off words. A launch
  * that was not fully co-resident completes (every wait expires after 20 ms) with bit 1 of *err set: its rollout data
- * is then invalid and the caller must stop (RolloutEngine.check_errors raises). Keep collectives stream-ordered on the
+ * is then invalid and the caller must stop (RolloutEngine.check_errors raises); while the bit is set, mm_td_fold_range
+ * and mm_per_insert_fold (multi-block insert, power-of-two capacity >= 16384) fold and insert nothing, so no data of
+ * such a launch reaches the chunk store's act / rew / done rows or the PER. Keep collectives stream-ordered on the
  * rollout stream, or outside the rollout's graph launches.
  * Diagnostic for that path: mm_hold_cus occupies n_blocks CUs (one 1024-thread workgroup with 64 KiB of LDS each) for
  * `ticks` of the 100 MHz clock; *seen (device int32) |= 2 if one of the n_watch handoff words carries `tag` in its

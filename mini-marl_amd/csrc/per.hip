@@ -592,6 +592,11 @@ __device__ uint64_t g_per_trace[4][64][16];
 __device__ __forceinline__ uint64_t leaf_key(const double* leaves, int64_t s) {
   return (uint64_t)__double_as_longlong(leaves[s]);
 }
+// the insert of a chunk folded from a timed-out chunk-persistent launch (error bit 1 of the rollout's word, sticky
+// until the host reads it): every pass returns at once, block-uniformly, so nothing of it enters the tree
+__device__ __forceinline__ bool mb_skip(const uint32_t* err) {
+  return err && (*reinterpret_cast<const volatile uint32_t*>(err) & 2u);
+}
 // first-level bin of a key (monotone in the key) in the window of 7 binades from biased exponent e0: 0 below it (and
 // +0), 4095 above it, else 1 + (binade - e0) * 512 + the top 9 mantissa bits — an interior bin is the class of keys
 // sharing their top 21 bits (sign 0, exponent, 9 mantissa bits). The window follows the threshold from insert to
@@ -773,6 +778,7 @@ template <bool VEC>
 __global__ __launch_bounds__(MB_T) void per_mb_sel1_fold(const double* __restrict__ tree, int64_t cap,
                                                          const PerDev* st, int64_t K, MbScratch* mb, int nh,
                                                          FoldArgs fa) {
+  if (mb_skip(fa.err)) return;
   if ((int)blockIdx.x < nh) {
     PER_STAMP(0, 0);
     mb_sel1_hist(tree, cap, st, K, mb, blockIdx.x, nh);
@@ -800,10 +806,11 @@ __device__ __forceinline__ void mb_bin_add(uint32_t* bins, bool on, uint32_t bin
 }
 
 __global__ __launch_bounds__(MB_T) void per_mb_sel2(const double* __restrict__ tree, int64_t cap, const PerDev* st,
-                                                    int64_t K, MbScratch* mb) {
+                                                    int64_t K, MbScratch* mb, const uint32_t* skip_err) {
   __shared__ uint32_t h[4096];
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
+  if (mb_skip(skip_err)) return;
   const int64_t n_data = st->n_data;
   int64_t need = K - min(K, cap - n_data);
   if (need <= 0) return;
@@ -1043,7 +1050,8 @@ __device__ void mb_threshold(const MbScratch* mb, int64_t cap, uint64_t* cl, uin
 // prio (the fold path): the new chunks' priorities, computed by the fold; else (td + eps)^alpha here
 __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot_row, int64_t cap, PerDev* st,
                                                      const float* td, const double* prio, int64_t K, double eps,
-                                                     int64_t* rows_inout, int64_t* slots_out, MbScratch* mb) {
+                                                     int64_t* rows_inout, int64_t* slots_out, MbScratch* mb,
+                                                     const uint32_t* skip_err) {
   __shared__ double lv[MB_SLOTS];
   __shared__ double v[2][MB_SLOTS / 2];
   __shared__ uint64_t cl[MB_CAND_LDS];
@@ -1053,6 +1061,7 @@ __global__ __launch_bounds__(MB_T) void per_mb_apply(double* tree, int64_t* slot
   __shared__ uint32_t wsum[MB_T / 64];
   __shared__ int64_t sh[2];
   __shared__ uint32_t s_last;
+  if (mb_skip(skip_err)) return;
   const int L = 63 - __clzll((unsigned long long)cap);      // leaves at level L
   const int64_t n_data = st->n_data;
   const double alpha = st->alpha;
@@ -1247,9 +1256,10 @@ static int per_insert_mb(mm_per* per, const float* td, int64_t k, int64_t* rows_
   } else {
     hipLaunchKernelGGL(per_mb_sel1, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, t, td_n);
   }
-  hipLaunchKernelGGL(per_mb_sel2, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb);
+  const uint32_t* skip_err = fold ? fold->err : nullptr;
+  hipLaunchKernelGGL(per_mb_sel2, dim3(G), dim3(MB_T), 0, s, per->tree, cap, per->st, k, mb, skip_err);
   hipLaunchKernelGGL(per_mb_apply, dim3(G), dim3(MB_T), 0, s, per->tree, per->slot_row, cap, per->st, td, prio, k,
-                     per->eps, rows_inout, slots_out, mb);
+                     per->eps, rows_inout, slots_out, mb, skip_err);
   MM_HIP_CHECK(hipGetLastError());
   return MM_OK;
 }

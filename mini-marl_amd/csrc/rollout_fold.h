@@ -21,7 +21,8 @@ struct FoldArgs {
   float* s_rew;
   uint8_t* s_done;         // store [rows][C]
   const int64_t* rows;     // [E] staging rows
-  uint32_t* err;           // sticky bit 0: a staging row outside the store
+  uint32_t* err;           // sticky bit 0: a staging row outside the store; bit 1 set (a chunk-persistent launch whose
+                           // hand-off wait expired): nothing is folded — its steps' data never reach the chunk store
   int64_t ring_se, n_rows;
   int E, N, slot0, n, C;
   float gamma;
@@ -38,6 +39,7 @@ struct FoldArgs {
 template <bool VEC>
 __device__ __forceinline__ void td_fold_group(const FoldArgs& a, int blk) {
   __shared__ float tdv[16][16];
+  if (a.err && (*reinterpret_cast<const volatile uint32_t*>(a.err) & 2u)) return;   // (block-uniform)
   const int jl = threadIdx.x >> 4, le = threadIdx.x & 15;
   const int e = blk * 16 + le;
   const int N = a.N;

@@ -243,3 +243,26 @@ def test_chunk_handoff_timeout_is_reported_and_grid_drains():
     e.step(0.3)
     torch.cuda.synchronize()
     e.check_errors()
+
+
+def test_timed_out_launch_is_not_folded_or_inserted():
+    """A chunk launch whose hand-off wait expired (error bit 1, set here by hand as the timeout would) leaves the chunk
+    store's act / rew / done rows, the chunk priorities and the PER tree / slot map untouched: the TD fold and every
+    pass of the multi-block insert return at once while the bit is set, and check_errors() reports it."""
+    from minimarl.engine import RolloutEngine
+    E = 2048
+    e = RolloutEngine(E, 8, f1=64, g=64, h=64, chunk=10, capacity=8 * E, seed=5, persistent=True, device=DEV)
+    e.run(20, 0.3)                                   # two chunks inserted: the tree holds data
+    torch.cuda.synchronize()
+    e.check_errors()
+    tree0, rows0 = e.per.tree().clone(), e.per.slot_rows().clone()
+    act0, rew0, done0 = e.store.act.clone(), e.store.rew.clone(), e.store.done.clone()
+    td0 = e.chunk_td.clone()
+    e.err.fill_(2)
+    e.run(10, 0.3)                                   # one more chunk: its folds and insert must all be skipped
+    torch.cuda.synchronize()
+    assert torch.equal(e.per.tree(), tree0) and torch.equal(e.per.slot_rows(), rows0)
+    assert torch.equal(e.store.act, act0) and torch.equal(e.store.rew, rew0) and torch.equal(e.store.done, done0)
+    assert torch.equal(e.chunk_td, td0)
+    with pytest.raises(RuntimeError, match="hand-off timed out"):
+        e.check_errors()
