@@ -10,6 +10,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mini-marl_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+import minimarl._lib as _L  # noqa: E402
+
+if os.environ.get("MB_LIB"):   # A/B: another build of libminimarl.so
+    _L.LIB_PATH = os.path.abspath(os.environ["MB_LIB"])
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from minimarl.synth import offq_episode_batch as make_batch  # noqa: E402
