@@ -869,7 +869,8 @@ __global__ __launch_bounds__(256) void lrn_loss_reduce_kernel(int B, int C, cons
   float tot = 0.f;
   for (int t = 0; t < C; ++t) {
     float s = 0.f;
-    for (int b = threadIdx.x; b < B; b += 256) s += parts[(int64_t)t * B + b];
+#pragma unroll 16
+    for (int b = threadIdx.x; b < B; b += 256) s += parts[(int64_t)t * B + b];   // (loads issued ahead, adds in order)
     sh[threadIdx.x] = s;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
