@@ -2543,20 +2543,93 @@ __global__ __launch_bounds__(256) void tmv_mfma_kernel(TmvArgs a) {
   f32x16 acc;
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-  for (int rr = 0; rr < a.R; rr += 32) {
-    for (int k = threadIdx.x; k < 32 * 64; k += 256) {
+  // chunk rr + 32's slabs are loaded into registers while chunk rr is reduced (one memory latency per launch
+  // instead of one per 32-deep chunk; same values, same MFMA order)
+  float px[8], pw[8];
+  auto fetch = [&](int rr) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = threadIdx.x + 256 * q;
       const int mm = k >> 5, x = k & 31;          // X: 32 consecutive r of one row per 32 lanes
       const int m = m0 + mm, r = rr + x;
-      sx[x][mm] = (m < a.M && r < a.R) ? X[(int64_t)m * a.x_m + r] : 0.f;
+      px[q] = (m < a.M && r < a.R) ? X[(int64_t)m * a.x_m + r] : 0.f;
       const int kk = k >> 6, y = k & 63;          // W: 64 consecutive c of one r
       const int r2 = rr + kk, c = c0 + y;
-      sw[kk][y] = (r2 < a.R && c < a.Cc) ? W[(int64_t)r2 * a.Cc + c] : 0.f;
+      pw[q] = (r2 < a.R && c < a.Cc) ? W[(int64_t)r2 * a.Cc + c] : 0.f;
+    }
+  };
+  fetch(0);
+  for (int rr = 0; rr < a.R; rr += 32) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = threadIdx.x + 256 * q;
+      sx[k & 31][k >> 5] = px[q];
+      sw[k >> 6][k & 63] = pw[q];
     }
     __syncthreads();
+    if (rr + 32 < a.R) fetch(rr + 32);
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2)
       acc = mfma32(sx[2 * s2 + lh][mw * 32 + li], sw[2 * s2 + lh][cw * 32 + li], acc);
     __syncthreads();
+  }
+  const int c = c0 + cw * 32 + li;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int m = m0 + mw * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+    if (m < a.M && c < a.Cc) {
+      float v = acc[q];
+      if (a.Z && !(a.Z[g * a.z_g + (int64_t)m * a.z_m + c] > 0.f)) v = 0.f;
+      a.Y[g * a.y_g + (int64_t)m * a.y_m + c] = v;
+    }
+  }
+}
+
+// tmv_mfma_kernel's op and MFMA order for R <= TMV_FULL_RMAX with 16-byte aligned rows (aligned16): the block's whole r range of
+// X (64 rows) and W (64 columns) staged in ONE round of 16-byte loads (issued 4 deep) into dynamic LDS ([R][65] each,
+// X transposed) instead of a round of scalar loads per 32-deep chunk
+constexpr int TMV_FULL_RMAX = 64;   // (R = 192, 100 KB of LDS, one block per CU: slower than the chunked kernel)
+__global__ __launch_bounds__(256) void tmv_mfma_full_kernel(TmvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smt[];
+  const int R = a.R, R4 = R >> 2, Rp = (R + 31) & ~31;   // (the last 32-deep chunk's rows r >= R read zeros)
+  float (*sx)[65] = reinterpret_cast<float (*)[65]>(smt);             // [Rp][65]: [r][m]
+  float (*sw)[65] = reinterpret_cast<float (*)[65]>(smt + Rp * 65);   // [Rp][65]: [r][c]
+  const int g = blockIdx.z;
+  const int m0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
+  const int mw = wave >> 1, cw = wave & 1;
+  const float* X = a.X + g * a.x_g;
+  const float* W = a.W + g * a.w_g;
+#pragma unroll 4
+  for (int i = threadIdx.x; i < 64 * R4; i += 256) {   // X: 64 rows x R4 float4
+    const int mm = i / R4, r4 = i - mm * R4;
+    const float4 v = *reinterpret_cast<const float4*>(X + (int64_t)min(m0 + mm, a.M - 1) * a.x_m + 4 * r4);
+    sx[4 * r4][mm] = v.x;
+    sx[4 * r4 + 1][mm] = v.y;
+    sx[4 * r4 + 2][mm] = v.z;
+    sx[4 * r4 + 3][mm] = v.w;
+  }
+#pragma unroll 4
+  for (int i = threadIdx.x; i < 16 * R; i += 256) {    // W: R rows x 16 float4 (64 columns)
+    const int r = i >> 4, c4 = i & 15;
+    const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)r * a.Cc + min(c0 + 4 * c4, a.Cc - 4));
+    sw[r][4 * c4] = v.x;
+    sw[r][4 * c4 + 1] = v.y;
+    sw[r][4 * c4 + 2] = v.z;
+    sw[r][4 * c4 + 3] = v.w;
+  }
+  for (int i = R * 64 + threadIdx.x; i < Rp * 64; i += 256) {
+    sx[i >> 6][i & 63] = 0.f;
+    sw[i >> 6][i & 63] = 0.f;
+  }
+  __syncthreads();
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+  for (int rr = 0; rr < R; rr += 32) {
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2)
+      acc = mfma32(sx[rr + 2 * s2 + lh][mw * 32 + li], sw[rr + 2 * s2 + lh][cw * 32 + li], acc);
   }
   const int c = c0 + cw * 32 + li;
 #pragma unroll
@@ -3326,7 +3399,19 @@ int mm_tmv(const mm_tmv_args* x, mm_stream_t s) {
   // small M (B = 32 updates): the 32 x 32 scalar tiles give more blocks and win
   if (x->M >= 2048) {
     dim3 grid((x->Cc + 63) / 64, (x->M + 63) / 64, x->groups);
-    hipLaunchKernelGGL(mm::tmv_mfma_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
+    if (a.aligned16 && x->R <= mm::TMV_FULL_RMAX) {
+      const int Rp = (x->R + 31) & ~31;
+      const size_t lds = sizeof(float) * 2 * 65 * (size_t)Rp;
+      static const int attr_rc = [] {
+        MM_HIP_CHECK(hipFuncSetAttribute((const void*)mm::tmv_mfma_full_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(sizeof(float) * 2 * 65 * mm::TMV_FULL_RMAX)));
+        return MM_OK;
+      }();
+      if (attr_rc != MM_OK) return attr_rc;
+      hipLaunchKernelGGL(mm::tmv_mfma_full_kernel, grid, dim3(256), lds, (hipStream_t)s, a);
+    } else
+      hipLaunchKernelGGL(mm::tmv_mfma_kernel, grid, dim3(256), 0, (hipStream_t)s, a);
     MM_HIP_CHECK(hipGetLastError());
     return MM_OK;
   }
