@@ -259,15 +259,27 @@ __global__ __launch_bounds__(256) void mixer_gi_tiled_kernel(MixGiArgs a) {
   f32x16 acc;
 #pragma unroll
   for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-  for (int k0 = 0; k0 < S; k0 += 32) {
+  // chunk k0 + 32 is loaded into registers while chunk k0 is reduced (one memory latency per launch instead of one
+  // per 32-deep chunk; same values, same MFMA order)
+  float px[8], pw[8];
+  auto fetch = [&](int k0) {
     const bool ok = k0 + x < S;
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
+      px[p] = (ok && xr[p]) ? xr[p][k0 + x] : 0.f;
+      pw[p] = (ok && wr[p]) ? wr[p][k0 + x] : 0.f;
+    }
+  };
+  fetch(0);
+  for (int k0 = 0; k0 < S; k0 += 32) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
       const int rr = (threadIdx.x >> 5) + 8 * p;
-      sx[x][rr] = (ok && xr[p]) ? xr[p][k0 + x] : 0.f;
-      sw[x][rr] = (ok && wr[p]) ? wr[p][k0 + x] : 0.f;
+      sx[x][rr] = px[p];
+      sw[x][rr] = pw[p];
     }
     __syncthreads();
+    if (k0 + 32 < S) fetch(k0 + 32);
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2)
       acc = mfma32(sx[2 * s2 + lh][cw * 32 + li], sw[2 * s2 + lh][mw * 32 + li], acc);
