@@ -502,7 +502,8 @@ __device__ __forceinline__ void mixer_hyper_rows(const MixFwdArgs& a, const MixF
     float acc[MIX_SPB];
 #pragma unroll
     for (int q = 0; q < MIX_SPB; ++q) acc[q] = 0.f;
-    for (int k = 0; k < Hm; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < Hm; ++k) {   // (weight loads issued ahead; per-sample adds in k order)
       const float wk = w[k];
 #pragma unroll
       for (int q = 0; q < MIX_SPB; ++q) acc[q] += wk * h1[q * Hm + k];
@@ -582,7 +583,8 @@ __global__ __launch_bounds__(256) void mixer_fwd_multi_kernel(MixFwdArgs a) {
 #pragma unroll
     for (int q = 0; q < MIX_SPB; ++q) acc[q] = 0.f;
     const float* w = nt.P + o.gWhh + (int64_t)r * Hm;
-    for (int k = 0; k < Hm; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < Hm; ++k) {   // (weight loads issued ahead; per-sample adds in k order)
       const float wk = w[k];
 #pragma unroll
       for (int q = 0; q < MIX_SPB; ++q) acc[q] += wk * h0[q * Hm + k];
